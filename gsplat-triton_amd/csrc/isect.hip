@@ -1,0 +1,271 @@
+// Tile intersection: per-Gaussian tile counts, prefix offsets, (isect_id,
+// flatten_id) emission, radix sort and per-tile range offsets -- gfx950.
+//
+// Replaces the reference
+//   get_tile_per_gauss_kernel / get_isect_ids_kernel  gsplat/triton_impl/isect_tiles.py:134-252
+//   get_isec_tile                                    gsplat/triton_impl/isect_tiles.py:255-282
+//   torch.cumsum + .item()                           gsplat/triton_impl/isect_tiles.py:101-102
+//   radix_sort (CUB SortPairs, default stream)       gsplat/triton_impl/radix_sort/radix_sort.cu:9-62
+//   get_isect_offsets_kernel                         gsplat/triton_impl/isect_offset.py:39-63
+//
+// Bit-exactness: tile rectangles use the Triton float formulas (L2), ids use
+// the Triton tile-bit width (n_tiles-1).bit_length() (L1), depth bits are the
+// int32 bitcast sign-extended to int64 exactly as the reference, emission
+// order is Gaussian-major / tile-row-major, and the sort is a stable LSD
+// radix sort over the low 32+tile_bits+cam_bits bits (rocPRIM), so
+// isect_ids / flatten_ids equal the reference's element for element.
+//
+// Offsets: instead of materialising the int64 inclusive cumsum of
+// tiles_per_gauss (8 B x C*N written and re-read), the count kernel writes
+// one partial sum per 256-Gaussian block, a single-workgroup kernel scans
+// those, and the write kernel redoes the block-local scan in LDS.
+#include "common.h"
+#include "../../include/gsplat_hip.h"
+
+#include <rocprim/device/device_radix_sort.hpp>
+
+namespace gs {
+
+constexpr int kIsectBlock = 256;
+
+struct Rect {
+  int x0, x1, y0, y1;
+};
+
+// isect_tiles.py:255-282 -- float32 (p -/+ r) / ts with floor/ceil, clamped.
+GS_INLINE Rect tile_rect(float px, float py, int radius, int ts, int tw, int th) {
+  const float r = (float)radius, t = (float)ts;
+  Rect o;
+  o.x0 = min(max((int)floorf(__fdiv_rn(px - r, t)), 0), tw);
+  o.x1 = min(max((int)ceilf(__fdiv_rn(px + r, t)), 0), tw);
+  o.y0 = min(max((int)floorf(__fdiv_rn(py - r, t)), 0), th);
+  o.y1 = min(max((int)ceilf(__fdiv_rn(py + r, t)), 0), th);
+  return o;
+}
+
+GS_INLINE int tiles_of(const float *means2d, const int32_t *radii, int64_t i, int ts, int tw,
+                       int th, Rect *rect) {
+  const int r = radii[i];
+  if (r <= 0) return 0;
+  const float2 p = *reinterpret_cast<const float2 *>(means2d + 2 * i);
+  *rect = tile_rect(p.x, p.y, r, ts, tw, th);
+  return (rect->x1 - rect->x0) * (rect->y1 - rect->y0);
+}
+
+template <typename T>
+GS_INLINE T block_exclusive_scan(T v, T *lds /* [kIsectBlock/64 + 1] */, T *total) {
+  // wave-level inclusive scan with shuffles, then across the 4 waves via LDS
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  T x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    T y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) lds[wid] = x;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    T run = 0;
+    for (int w = 0; w < kIsectBlock / 64; ++w) {
+      T s = lds[w];
+      lds[w] = run;
+      run += s;
+    }
+    lds[kIsectBlock / 64] = run;
+  }
+  __syncthreads();
+  *total = lds[kIsectBlock / 64];
+  return lds[wid] + x - v;
+}
+
+__global__ void __launch_bounds__(kIsectBlock)
+isect_count_kernel(int64_t G, const float *__restrict__ means2d, const int32_t *__restrict__ radii,
+                   int ts, int tw, int th, int32_t *__restrict__ tiles_per_gauss,
+                   int64_t *__restrict__ block_sums) {
+  __shared__ int64_t lds[kIsectBlock / 64 + 1];
+  const int64_t i = (int64_t)blockIdx.x * kIsectBlock + threadIdx.x;
+  Rect rc;
+  int cnt = (i < G) ? tiles_of(means2d, radii, i, ts, tw, th, &rc) : 0;
+  if (i < G) tiles_per_gauss[i] = cnt;
+  int64_t tot;
+  block_exclusive_scan<int64_t>((int64_t)cnt, lds, &tot);
+  if (threadIdx.x == 0) block_sums[blockIdx.x] = tot;
+}
+
+// Exclusive scan of the per-block sums in place; total -> block_sums[nb].
+// One 1024-lane workgroup walks the (at most a few thousand) block sums.
+__global__ void __launch_bounds__(1024) isect_scan_blocks_kernel(int64_t nb, int64_t *block_sums) {
+  __shared__ int64_t wave_tot[16];
+  __shared__ int64_t chunk_tot;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  int64_t carry = 0;  // identical in every lane
+  for (int64_t base = 0; base < nb; base += 1024) {
+    const int64_t i = base + threadIdx.x;
+    const int64_t v = (i < nb) ? block_sums[i] : 0;
+    int64_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      int64_t y = __shfl_up(x, o, 64);
+      if (lane >= o) x += y;
+    }
+    if (lane == 63) wave_tot[wid] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int64_t run = 0;
+      for (int w = 0; w < 16; ++w) {
+        const int64_t s = wave_tot[w];
+        wave_tot[w] = run;
+        run += s;
+      }
+      chunk_tot = run;
+    }
+    __syncthreads();
+    if (i < nb) block_sums[i] = carry + wave_tot[wid] + x - v;
+    carry += chunk_tot;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) block_sums[nb] = carry;
+}
+
+__global__ void __launch_bounds__(kIsectBlock)
+isect_write_kernel(int64_t G, int N, const float *__restrict__ means2d,
+                   const int32_t *__restrict__ radii, const float *__restrict__ depths,
+                   const int32_t *__restrict__ camera_ids, int ts, int tw, int th, int tile_bits,
+                   const int64_t *__restrict__ block_prefix, int64_t *__restrict__ isect_ids,
+                   int32_t *__restrict__ flatten_ids) {
+  __shared__ int64_t lds[kIsectBlock / 64 + 1];
+  const int64_t i = (int64_t)blockIdx.x * kIsectBlock + threadIdx.x;
+  Rect rc{0, 0, 0, 0};
+  const int cnt = (i < G) ? tiles_of(means2d, radii, i, ts, tw, th, &rc) : 0;
+  int64_t tot;
+  const int64_t local = block_exclusive_scan<int64_t>((int64_t)cnt, lds, &tot);
+  if (cnt == 0) return;
+  int64_t cur = block_prefix[blockIdx.x] + local;
+  const int64_t cam = camera_ids ? (int64_t)camera_ids[i] : (i / N);
+  const int64_t hi = cam << (32 + tile_bits);
+  // sign-extended bitcast of the depth, as the reference (isect_tiles.py:223)
+  const int64_t dbits = (int64_t)__float_as_int(depths[i]);
+  const int32_t fid = (int32_t)i;
+  for (int y = rc.y0; y < rc.y1; ++y) {
+    for (int x = rc.x0; x < rc.x1; ++x) {
+      const int64_t tile = (int64_t)(y * tw + x);
+      isect_ids[cur] = hi | (tile << 32) | dbits;
+      flatten_ids[cur] = fid;
+      ++cur;
+    }
+  }
+}
+
+// One lane per sorted isect: fill offsets for the (cam, tile) keys between
+// the previous key and this one (CUDA-style fill; Triton tile-bit layout).
+__global__ void __launch_bounds__(256)
+isect_offsets_kernel(int64_t n, const int64_t *__restrict__ isect_ids, int n_tiles_total,
+                     int n_tiles, int tile_bits, int32_t *__restrict__ offsets) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t tmask = (tile_bits >= 63) ? -1 : ((int64_t)1 << tile_bits) - 1;
+  auto key_of = [&](int64_t id) -> int64_t {
+    const int64_t k = id >> 32;
+    return (k >> tile_bits) * n_tiles + (k & tmask);
+  };
+  const int64_t cur = key_of(isect_ids[i]);
+  if (i == 0) {
+    for (int64_t t = 0; t <= cur; ++t) offsets[t] = 0;
+  } else {
+    const int64_t prev = key_of(isect_ids[i - 1]);
+    if (prev != cur)
+      for (int64_t t = prev + 1; t <= cur; ++t) offsets[t] = (int32_t)i;
+  }
+  if (i == n - 1)
+    for (int64_t t = cur + 1; t < n_tiles_total; ++t) offsets[t] = (int32_t)n;
+}
+
+}  // namespace gs
+
+using namespace gs;
+
+extern "C" int64_t gsplat_hip_isect_workspace_bytes(int64_t n_gaussians) {
+  const int64_t nb = (n_gaussians + kIsectBlock - 1) / kIsectBlock;
+  return (nb + 2) * (int64_t)sizeof(int64_t);
+}
+
+extern "C" int gsplat_hip_isect_count(int64_t n_gaussians, const float *means2d,
+                                      const int32_t *radii, int tile_size, int tile_width,
+                                      int tile_height, int32_t *tiles_per_gauss,
+                                      void *workspace, int64_t *n_isects_device,
+                                      void *stream) {
+  GS_REQUIRE(n_gaussians >= 0 && tile_size > 0, "isect_count: bad sizes");
+  hipStream_t st = (hipStream_t)stream;
+  int64_t *ws = reinterpret_cast<int64_t *>(workspace);
+  const int64_t nb = (n_gaussians + kIsectBlock - 1) / kIsectBlock;
+  if (nb == 0) {
+    GS_HIP(hipMemsetAsync(n_isects_device, 0, sizeof(int64_t), st));
+    return 0;
+  }
+  hipLaunchKernelGGL(isect_count_kernel, dim3((unsigned)nb), dim3(kIsectBlock), 0, st,
+                     n_gaussians, means2d, radii, tile_size, tile_width, tile_height,
+                     tiles_per_gauss, ws);
+  hipLaunchKernelGGL(isect_scan_blocks_kernel, dim3(1), dim3(1024), 0, st, nb, ws);
+  GS_HIP(hipMemcpyAsync(n_isects_device, ws + nb, sizeof(int64_t), hipMemcpyDeviceToDevice, st));
+  GS_CHECK_LAUNCH("isect_count");
+  return 0;
+}
+
+extern "C" int gsplat_hip_isect_write(int64_t n_gaussians, int N, const float *means2d,
+                                      const int32_t *radii, const float *depths,
+                                      const int32_t *camera_ids, int tile_size, int tile_width,
+                                      int tile_height, int tile_bits, const void *workspace,
+                                      int64_t *isect_ids, int32_t *flatten_ids, void *stream) {
+  GS_REQUIRE(n_gaussians >= 0 && (camera_ids || N > 0 || n_gaussians == 0),
+             "isect_write: N must be > 0 when camera_ids is null");
+  const int64_t nb = (n_gaussians + kIsectBlock - 1) / kIsectBlock;
+  if (nb == 0) return 0;
+  hipLaunchKernelGGL(isect_write_kernel, dim3((unsigned)nb), dim3(kIsectBlock), 0,
+                     (hipStream_t)stream, n_gaussians, N, means2d, radii, depths, camera_ids,
+                     tile_size, tile_width, tile_height, tile_bits,
+                     reinterpret_cast<const int64_t *>(workspace), isect_ids, flatten_ids);
+  GS_CHECK_LAUNCH("isect_write");
+  return 0;
+}
+
+extern "C" int64_t gsplat_hip_sort_workspace_bytes(int64_t n) {
+  size_t bytes = 0;
+  (void)rocprim::radix_sort_pairs(nullptr, bytes, (const uint64_t *)nullptr, (uint64_t *)nullptr,
+                            (const int32_t *)nullptr, (int32_t *)nullptr, (size_t)n, 0u, 64u,
+                            (hipStream_t)0);
+  return (int64_t)bytes;
+}
+
+// Stable LSD radix sort of (isect_id, flatten_id) on bits [0, n_bits).
+extern "C" int gsplat_hip_radix_sort(int64_t n, int n_bits, const int64_t *keys_in,
+                                     const int32_t *vals_in, int64_t *keys_out,
+                                     int32_t *vals_out, void *workspace,
+                                     int64_t workspace_bytes, void *stream) {
+  GS_REQUIRE(n_bits > 0 && n_bits <= 64, "radix_sort: n_bits=%d out of range", n_bits);
+  if (n <= 0) return 0;
+  size_t bytes = (size_t)workspace_bytes;
+  hipError_t e = rocprim::radix_sort_pairs(
+      workspace, bytes, reinterpret_cast<const uint64_t *>(keys_in),
+      reinterpret_cast<uint64_t *>(keys_out), vals_in, vals_out, (size_t)n, 0u,
+      (unsigned)n_bits, (hipStream_t)stream);
+  GS_REQUIRE(e == hipSuccess, "radix_sort: %s", hipGetErrorString(e));
+  return 0;
+}
+
+extern "C" int gsplat_hip_isect_offsets(int64_t n_isects, const int64_t *isect_ids, int C,
+                                        int tile_width, int tile_height, int32_t *offsets,
+                                        void *stream) {
+  const int n_tiles = tile_width * tile_height;
+  hipStream_t st = (hipStream_t)stream;
+  if ((int64_t)C * n_tiles == 0) return 0;
+  if (n_isects <= 0) {
+    GS_HIP(hipMemsetAsync(offsets, 0, sizeof(int32_t) * (size_t)C * n_tiles, st));
+    return 0;
+  }
+  int tile_bits = 0;
+  while ((1 << tile_bits) < n_tiles) ++tile_bits;  // == (n_tiles - 1).bit_length()
+  hipLaunchKernelGGL(isect_offsets_kernel, dim3((unsigned)((n_isects + 255) / 256)), dim3(256), 0,
+                     st, n_isects, isect_ids, C * n_tiles, n_tiles, tile_bits, offsets);
+  GS_CHECK_LAUNCH("isect_offsets");
+  return 0;
+}

@@ -1,0 +1,242 @@
+// Real spherical harmonics (degree 0..4) -> RGB, forward and backward, gfx950.
+//
+// Replaces the reference Triton kernels
+//   _sh_to_color_kernel      gsplat/triton_impl/sh_fwd.py:69-191
+//   _sh_to_color_vjp_kernel  gsplat/triton_impl/sh_bwd.py:36-380
+// plus the torch glue `colors[~masks] = 0` / `v_coeffs[~masks] = 0`
+// (gsplat/triton_impl/_wrapper.py:567-568, 589-592), which is fused here:
+// masked rows are written as zeros without reading their coefficients.
+//
+// Mapping: one lane per row (Gaussian x camera) computing all three channels,
+// so v_dirs needs no atomics (the reference uses one lane per channel and
+// relaxed atomics).  The basis uses the reference's constants and the same
+// g/h recurrences; the VJP uses the analytic partials of each basis function.
+#include "common.h"
+#include "../../include/gsplat_hip.h"
+
+namespace gs {
+
+// Basis values B[k] and partials dB[k] = (dB/dx, dB/dy, dB/dz) w.r.t. the
+// normalised direction (sh_fwd.py:43-66 constants).
+template <int DEG, bool GRAD>
+GS_INLINE void sh_basis(float x, float y, float z, float *B, float (*dB)[3]) {
+  B[0] = 0.28209479177387814f;
+  if (GRAD) dB[0][0] = dB[0][1] = dB[0][2] = 0.f;
+  if (DEG < 1) return;
+  const float C1 = 0.4886025119029199f;
+  B[1] = -C1 * y;
+  B[2] = C1 * z;
+  B[3] = -C1 * x;
+  if (GRAD) {
+    dB[1][0] = 0.f; dB[1][1] = -C1; dB[1][2] = 0.f;
+    dB[2][0] = 0.f; dB[2][1] = 0.f; dB[2][2] = C1;
+    dB[3][0] = -C1; dB[3][1] = 0.f; dB[3][2] = 0.f;
+  }
+  if (DEG < 2) return;
+  const float zz = z * z;
+  const float g2 = 2.f * x * y, h2 = x * x - y * y;
+  const float C22 = 0.5462742152960396f;
+  const float c21 = -1.0925484305920792f * z;
+  B[4] = C22 * g2;
+  B[5] = c21 * y;
+  B[6] = 0.9461746957575601f * zz - 0.3153915652525201f;
+  B[7] = c21 * x;
+  B[8] = C22 * h2;
+  if (GRAD) {
+    dB[4][0] = 2.f * C22 * y; dB[4][1] = 2.f * C22 * x; dB[4][2] = 0.f;
+    dB[5][0] = 0.f; dB[5][1] = c21; dB[5][2] = -1.0925484305920792f * y;
+    dB[6][0] = 0.f; dB[6][1] = 0.f; dB[6][2] = 1.8923493915151202f * z;
+    dB[7][0] = c21; dB[7][1] = 0.f; dB[7][2] = -1.0925484305920792f * x;
+    dB[8][0] = 2.f * C22 * x; dB[8][1] = -2.f * C22 * y; dB[8][2] = 0.f;
+  }
+  if (DEG < 3) return;
+  const float g3 = x * g2 + y * h2, h3 = x * h2 - y * g2;
+  const float C33 = -0.5900435899266435f, C32 = 1.445305721320277f;
+  const float c31 = -2.285228997322329f * zz + 0.4570457994644658f;
+  B[9] = C33 * g3;
+  B[10] = C32 * g2 * z;
+  B[11] = c31 * y;
+  B[12] = z * (1.865881662950577f * zz - 1.119528997770346f);
+  B[13] = c31 * x;
+  B[14] = C32 * h2 * z;
+  B[15] = C33 * h3;
+  if (GRAD) {
+    const float dc31 = -4.570457994644658f * z;
+    dB[9][0] = 3.f * C33 * g2; dB[9][1] = 3.f * C33 * h2; dB[9][2] = 0.f;
+    dB[10][0] = 2.f * C32 * y * z; dB[10][1] = 2.f * C32 * x * z; dB[10][2] = C32 * g2;
+    dB[11][0] = 0.f; dB[11][1] = c31; dB[11][2] = dc31 * y;
+    dB[12][0] = 0.f; dB[12][1] = 0.f; dB[12][2] = 5.597644988851731f * zz - 1.119528997770346f;
+    dB[13][0] = c31; dB[13][1] = 0.f; dB[13][2] = dc31 * x;
+    dB[14][0] = 2.f * C32 * x * z; dB[14][1] = -2.f * C32 * y * z; dB[14][2] = C32 * h2;
+    dB[15][0] = 3.f * C33 * h2; dB[15][1] = -3.f * C33 * g2; dB[15][2] = 0.f;
+  }
+  if (DEG < 4) return;
+  const float g4 = x * g3 + y * h3, h4 = x * h3 - y * g3;
+  const float C44 = 0.6258357354491761f, C43 = -1.7701307697799304f;
+  const float c41 = z * (-4.683325804901024f * zz + 2.0071396306718676f);
+  const float c42 = 3.31161143515146f * zz - 0.47308734787878f;
+  B[16] = C44 * g4;
+  B[17] = C43 * g3 * z;
+  B[18] = c42 * g2;
+  B[19] = c41 * y;
+  B[20] = zz * (3.7024941420321507f * zz - 3.1735664074561294f) + 0.31735664074561293f;
+  B[21] = c41 * x;
+  B[22] = c42 * h2;
+  B[23] = C43 * h3 * z;
+  B[24] = C44 * h4;
+  if (GRAD) {
+    const float dc41 = -14.049977414703072f * zz + 2.0071396306718676f;
+    const float dc42 = 6.62322287030292f * z;
+    dB[16][0] = 4.f * C44 * g3; dB[16][1] = 4.f * C44 * h3; dB[16][2] = 0.f;
+    dB[17][0] = 3.f * C43 * g2 * z; dB[17][1] = 3.f * C43 * h2 * z; dB[17][2] = C43 * g3;
+    dB[18][0] = 2.f * c42 * y; dB[18][1] = 2.f * c42 * x; dB[18][2] = dc42 * g2;
+    dB[19][0] = 0.f; dB[19][1] = c41; dB[19][2] = dc41 * y;
+    dB[20][0] = 0.f; dB[20][1] = 0.f; dB[20][2] = z * (14.809976568128603f * zz - 6.347132814912259f);
+    dB[21][0] = c41; dB[21][1] = 0.f; dB[21][2] = dc41 * x;
+    dB[22][0] = 2.f * c42 * x; dB[22][1] = -2.f * c42 * y; dB[22][2] = dc42 * h2;
+    dB[23][0] = 3.f * C43 * h2 * z; dB[23][1] = -3.f * C43 * g2 * z; dB[23][2] = C43 * h3;
+    dB[24][0] = 4.f * C44 * h3; dB[24][1] = -4.f * C44 * g3; dB[24][2] = 0.f;
+  }
+}
+
+template <int DEG>
+__global__ void __launch_bounds__(256)
+sh_fwd_kernel(int64_t n, int K, int64_t n_coeff_rows,
+              const float *__restrict__ dirs, const float *__restrict__ coeffs,
+              const uint8_t *__restrict__ masks, float *__restrict__ colors) {
+  constexpr int NB = (DEG + 1) * (DEG + 1);
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float *o = colors + 3 * i;
+  if (masks && !masks[i]) {
+    o[0] = 0.f; o[1] = 0.f; o[2] = 0.f;
+    return;
+  }
+  float x = 0.f, y = 0.f, z = 0.f;
+  if (DEG > 0) {
+    const float *d = dirs + 3 * i;
+    x = d[0]; y = d[1]; z = d[2];
+    const float inorm = rsqrtf(x * x + y * y + z * z);
+    x *= inorm; y *= inorm; z *= inorm;
+  }
+  float B[NB];
+  sh_basis<DEG, false>(x, y, z, B, nullptr);
+  const float *cf = coeffs + (i % n_coeff_rows) * (int64_t)K * 3;
+  float r = 0.f, g = 0.f, b = 0.f;
+#pragma unroll
+  for (int k = 0; k < NB; ++k) {
+    r += B[k] * cf[3 * k];
+    g += B[k] * cf[3 * k + 1];
+    b += B[k] * cf[3 * k + 2];
+  }
+  o[0] = r; o[1] = g; o[2] = b;
+}
+
+template <int DEG>
+__global__ void __launch_bounds__(256)
+sh_bwd_kernel(int64_t n, int K, int64_t n_coeff_rows, const float *__restrict__ dirs, const float *__restrict__ coeffs,
+              const uint8_t *__restrict__ masks, const float *__restrict__ v_colors,
+              float *__restrict__ v_coeffs, float *__restrict__ v_dirs) {
+  constexpr int NB = (DEG + 1) * (DEG + 1);
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float *vc = v_coeffs + i * (int64_t)K * 3;
+  const bool on = !masks || masks[i];
+  if (!on) {
+    for (int k = 0; k < 3 * K; ++k) vc[k] = 0.f;
+    if (v_dirs) { v_dirs[3 * i] = 0.f; v_dirs[3 * i + 1] = 0.f; v_dirs[3 * i + 2] = 0.f; }
+    return;
+  }
+  const float vr = v_colors[3 * i], vg = v_colors[3 * i + 1], vb = v_colors[3 * i + 2];
+  float x = 0.f, y = 0.f, z = 0.f, inorm = 0.f;
+  if (DEG > 0) {
+    const float *d = dirs + 3 * i;
+    x = d[0]; y = d[1]; z = d[2];
+    inorm = rsqrtf(x * x + y * y + z * z);
+    x *= inorm; y *= inorm; z *= inorm;
+  }
+  float B[NB];
+  float dB[NB][3];
+  const bool want_dirs = (v_dirs != nullptr) && DEG > 0;
+  if (want_dirs) sh_basis<DEG, true>(x, y, z, B, dB);
+  else sh_basis<DEG, false>(x, y, z, B, nullptr);
+#pragma unroll
+  for (int k = 0; k < NB; ++k) {
+    vc[3 * k] = B[k] * vr;
+    vc[3 * k + 1] = B[k] * vg;
+    vc[3 * k + 2] = B[k] * vb;
+  }
+  for (int k = 3 * NB; k < 3 * K; ++k) vc[k] = 0.f;
+  if (v_dirs) {
+    if (DEG == 0) {
+      v_dirs[3 * i] = 0.f; v_dirs[3 * i + 1] = 0.f; v_dirs[3 * i + 2] = 0.f;
+      return;
+    }
+    const float *cf = coeffs + (i % n_coeff_rows) * (int64_t)K * 3;
+    float vx = 0.f, vy = 0.f, vz = 0.f;
+#pragma unroll
+    for (int k = 1; k < NB; ++k) {
+      const float w = cf[3 * k] * vr + cf[3 * k + 1] * vg + cf[3 * k + 2] * vb;
+      vx += dB[k][0] * w;
+      vy += dB[k][1] * w;
+      vz += dB[k][2] * w;
+    }
+    // VJP of the normalisation (sh_bwd.py:367-380)
+    const float dot = x * vx + y * vy + z * vz;
+    v_dirs[3 * i] = (vx - dot * x) * inorm;
+    v_dirs[3 * i + 1] = (vy - dot * y) * inorm;
+    v_dirs[3 * i + 2] = (vz - dot * z) * inorm;
+  }
+}
+
+}  // namespace gs
+
+using namespace gs;
+
+// coeffs: [n_coeff_rows, K, 3]; row i of dirs/colors uses coefficient row
+// i % n_coeff_rows, so a [N,K,3] tensor broadcast over C cameras is read in
+// place (n_coeff_rows = N) instead of being materialised as [C,N,K,3].
+extern "C" int gsplat_hip_sh_fwd(int degree, int64_t n, int64_t n_coeff_rows, int K, const float *dirs,
+                                 const float *coeffs, const uint8_t *masks, float *colors,
+                                 void *stream) {
+  GS_REQUIRE(degree >= 0 && degree <= 4, "sh_fwd: degree %d not in [0, 4]", degree);
+  GS_REQUIRE(K >= (degree + 1) * (degree + 1) && K <= 25, "sh_fwd: K=%d too small for degree %d",
+             K, degree);
+  if (n <= 0) return 0;
+  GS_REQUIRE(n_coeff_rows > 0 && n % n_coeff_rows == 0, "sh: n=%lld not a multiple of n_coeff_rows=%lld",
+             (long long)n, (long long)n_coeff_rows);
+  dim3 grid((unsigned)((n + 255) / 256));
+  hipStream_t st = (hipStream_t)stream;
+#define GS_SH_FWD(D)                                                                        \
+  case D:                                                                                   \
+    hipLaunchKernelGGL(sh_fwd_kernel<D>, grid, dim3(256), 0, st, n, K, n_coeff_rows, dirs, \
+                       coeffs, masks, colors);                                              \
+    break;
+  switch (degree) { GS_SH_FWD(0) GS_SH_FWD(1) GS_SH_FWD(2) GS_SH_FWD(3) GS_SH_FWD(4) }
+#undef GS_SH_FWD
+  GS_CHECK_LAUNCH("sh_fwd");
+  return 0;
+}
+
+extern "C" int gsplat_hip_sh_bwd(int degree, int64_t n, int64_t n_coeff_rows, int K, const float *dirs,
+                                 const float *coeffs, const uint8_t *masks,
+                                 const float *v_colors, float *v_coeffs, float *v_dirs,
+                                 void *stream) {
+  GS_REQUIRE(degree >= 0 && degree <= 4, "sh_bwd: degree %d not in [0, 4]", degree);
+  GS_REQUIRE(K >= (degree + 1) * (degree + 1) && K <= 25, "sh_bwd: K=%d too small for degree %d",
+             K, degree);
+  if (n <= 0) return 0;
+  GS_REQUIRE(n_coeff_rows > 0 && n % n_coeff_rows == 0, "sh: n=%lld not a multiple of n_coeff_rows=%lld",
+             (long long)n, (long long)n_coeff_rows);
+  dim3 grid((unsigned)((n + 255) / 256));
+  hipStream_t st = (hipStream_t)stream;
+#define GS_SH_BWD(D)                                                                     \
+  case D:                                                                                \
+    hipLaunchKernelGGL(sh_bwd_kernel<D>, grid, dim3(256), 0, st, n, K, n_coeff_rows, dirs, coeffs, \
+                       masks, v_colors, v_coeffs, v_dirs);                               \
+    break;
+  switch (degree) { GS_SH_BWD(0) GS_SH_BWD(1) GS_SH_BWD(2) GS_SH_BWD(3) GS_SH_BWD(4) }
+#undef GS_SH_BWD
+  GS_CHECK_LAUNCH("sh_bwd");
+  return 0;
+}

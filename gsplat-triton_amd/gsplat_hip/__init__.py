@@ -1,0 +1,26 @@
+"""gsplat_hip -- MI355X (gfx950) backend for the gsplat rasterization hot path.
+
+Exports the backend surface that gsplat/rendering.py imports from
+`gsplat.triton_impl._wrapper` (rendering.py:20-27), implemented with
+hand-written HIP kernels behind the C ABI in include/gsplat_hip.h, plus a
+`rasterization()` front-end mirroring gsplat/rendering.py:44-598.
+"""
+
+from ._wrapper import (
+    fully_fused_projection,
+    isect_offset_encode,
+    isect_tiles,
+    rasterize_to_pixels,
+    spherical_harmonics,
+)
+from .rendering import rasterization
+
+__all__ = [
+    "fully_fused_projection",
+    "isect_tiles",
+    "isect_offset_encode",
+    "spherical_harmonics",
+    "rasterize_to_pixels",
+    "rasterization",
+]
+__version__ = "0.1.0"

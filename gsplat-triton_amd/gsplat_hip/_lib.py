@@ -1,0 +1,88 @@
+"""ctypes binding of libgsplat_hip.so (the C ABI declared in include/gsplat_hip.h).
+
+This is the reference-side binding a maintainer would add next to
+gsplat/triton_impl: it replaces the Triton JIT launches and the nvcc-JIT
+`radix_sort` extension (gsplat/triton_impl/radix_sort/__init__.py:10-13).
+The library is prebuilt in-tree (`make -C gsplat-triton_amd/csrc`); if it is
+missing or cannot be loaded every op raises -- there is no fallback path.
+"""
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("GSPLAT_HIP_LIB", os.path.join(_HERE, "libgsplat_hip.so"))
+ABI_VERSION = 1
+
+_p = ctypes.c_void_p
+_i32 = ctypes.c_int
+_i64 = ctypes.c_int64
+_f = ctypes.c_float
+
+# name -> (restype, argtypes)
+_SIGS = {
+    "gsplat_hip_last_error": (ctypes.c_char_p, []),
+    "gsplat_hip_abi_version": (_i32, []),
+    "gsplat_hip_projection_fwd": (_i32, [_i32, _i32, _p, _p, _p, _p, _p, _i32, _i32, _f, _f, _f,
+                                         _f, _p, _p, _p, _p, _p, _p]),
+    "gsplat_hip_projection_bwd": (_i32, [_i32, _i32, _p, _p, _p, _p, _p, _i32, _i32, _f, _p, _p,
+                                         _p, _p, _p, _p, _p, _p, _p, _p, _p, _p]),
+    "gsplat_hip_sh_fwd": (_i32, [_i32, _i64, _i64, _i32, _p, _p, _p, _p, _p]),
+    "gsplat_hip_sh_bwd": (_i32, [_i32, _i64, _i64, _i32, _p, _p, _p, _p, _p, _p, _p]),
+    "gsplat_hip_isect_workspace_bytes": (_i64, [_i64]),
+    "gsplat_hip_isect_count": (_i32, [_i64, _p, _p, _i32, _i32, _i32, _p, _p, _p, _p]),
+    "gsplat_hip_isect_write": (_i32, [_i64, _i32, _p, _p, _p, _p, _i32, _i32, _i32, _i32, _p,
+                                      _p, _p, _p]),
+    "gsplat_hip_sort_workspace_bytes": (_i64, [_i64]),
+    "gsplat_hip_radix_sort": (_i32, [_i64, _i32, _p, _p, _p, _p, _p, _i64, _p]),
+    "gsplat_hip_isect_offsets": (_i32, [_i64, _p, _i32, _i32, _i32, _p, _p]),
+    "gsplat_hip_rasterize_supported_channels": (_i32, [_i32]),
+    "gsplat_hip_rasterize_fwd": (_i32, [_i32, _i32, _i32, _i32, _i32, _i32, _i32, _p, _p, _p, _p,
+                                        _p, _p, _p, _i64, _p, _p, _p, _p, _p]),
+    "gsplat_hip_rasterize_bwd": (_i32, [_i32, _i64, _i32, _i32, _i32, _i32, _i32, _i32, _p, _p,
+                                        _p, _p, _p, _p, _p, _i64, _p, _p, _p, _p, _p, _p, _p,
+                                        _p, _p, _p, _p]),
+}
+
+EXPORTED = tuple(_SIGS)
+
+_lib = None
+
+
+class GsplatHipError(RuntimeError):
+    pass
+
+
+def load():
+    """Load (once) and return the ctypes library, raising if unavailable."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise GsplatHipError(
+            f"libgsplat_hip.so not found at {LIB_PATH}; build it with "
+            "`make -C gsplat-triton_amd/csrc` (or __graft_entry__.build())")
+    lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    v = lib.gsplat_hip_abi_version()
+    if v != ABI_VERSION:
+        raise GsplatHipError(f"libgsplat_hip ABI {v} != expected {ABI_VERSION}; rebuild")
+    _lib = lib
+    return lib
+
+
+def call(name, *args):
+    """Invoke an int-returning entry point and raise on a non-zero status."""
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    if rc != 0:
+        msg = lib.gsplat_hip_last_error().decode(errors="replace")
+        raise GsplatHipError(f"{name} failed (status {rc}): {msg}")
+    return rc
+
+
+def query(name, *args):
+    return getattr(load(), name)(*args)

@@ -1,0 +1,438 @@
+"""The 5-function backend surface of gsplat, backed by libgsplat_hip.so.
+
+Drop-in for `gsplat/triton_impl/_wrapper.py` (the functions that
+`gsplat/rendering.py:11-29` imports from the selected backend):
+
+    fully_fused_projection   _wrapper.py:429-541  (autograd: _FullyFusedProjection :300)
+    isect_tiles              _wrapper.py:544 -> isect_tiles.py:13-131   (no grad)
+    isect_offset_encode      _wrapper.py:548 -> isect_offset.py:8-33    (no grad)
+    spherical_harmonics      _wrapper.py:596-620  (autograd: _SphericalHarmonics :552)
+    rasterize_to_pixels      _wrapper.py:185-297  (autograd: _RasterizeToPixels :42)
+
+Same signatures, defaults, assertions, error types and autograd contract
+(argument order, `None` gradients, `ctx.needs_input_grad[4]` gating,
+`means2d.absgrad`).  Every op runs through the HIP C ABI on torch's current
+stream; there is no CPU or Triton fallback.
+"""
+
+import math
+from typing import Optional, Tuple
+
+import torch
+from torch import Tensor
+
+from . import _lib
+
+_SUPPORTED_D = (1, 2, 3, 4, 8, 16, 32)
+
+
+def _ptr(t: Optional[Tensor]) -> int:
+    return 0 if t is None else t.data_ptr()
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _dev_check(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise _lib.GsplatHipError(
+                "gsplat_hip ops run on the GPU only; got a tensor on " + str(t.device))
+
+
+def _f32c(t: Optional[Tensor]) -> Optional[Tensor]:
+    if t is None:
+        return None
+    return t.contiguous() if t.dtype == torch.float32 else t.float().contiguous()
+
+
+def _aligned16(t: Tensor) -> Tensor:
+    return t if t.data_ptr() % 16 == 0 else t.clone()
+
+
+def _bit_length(x: int) -> int:
+    return int(x).bit_length()
+
+
+# ============================================================== projection ==
+class _FullyFusedProjection(torch.autograd.Function):
+    """Projects Gaussians to 2D (gsplat/triton_impl/_wrapper.py:300-426)."""
+
+    @staticmethod
+    def forward(ctx, means, covars, quats, scales, viewmats, Ks, width, height, eps2d,
+                near_plane, far_plane, radius_clip, calc_compensations,
+                camera_model="pinhole", block_size=256):
+        if camera_model != "pinhole":
+            raise NotImplementedError(f"Unsupported camera model: {camera_model}")
+        assert (covars is None) and (quats is not None) and (scales is not None)
+        means, quats, scales, viewmats, Ks = (_f32c(x) for x in (means, quats, scales, viewmats, Ks))
+        quats = _aligned16(quats)
+        _dev_check(means, quats, scales, viewmats, Ks)
+        C, N = viewmats.shape[0], means.shape[0]
+        dev = means.device
+        radii = torch.empty((C, N), dtype=torch.int32, device=dev)
+        means2d = torch.empty((C, N, 2), dtype=torch.float32, device=dev)
+        depths = torch.empty((C, N), dtype=torch.float32, device=dev)
+        conics = torch.empty((C, N, 3), dtype=torch.float32, device=dev)
+        comps = torch.empty((C, N), dtype=torch.float32, device=dev) if calc_compensations else None
+        _lib.call("gsplat_hip_projection_fwd", C, N, _ptr(means), _ptr(quats), _ptr(scales),
+                  _ptr(viewmats), _ptr(Ks), int(width), int(height), float(eps2d),
+                  float(near_plane), float(far_plane), float(radius_clip), _ptr(radii),
+                  _ptr(means2d), _ptr(depths), _ptr(conics), _ptr(comps), _stream())
+        ctx.save_for_backward(means, quats, scales, viewmats, Ks, radii, conics, comps)
+        ctx.width, ctx.height, ctx.eps2d = int(width), int(height), float(eps2d)
+        ctx.mark_non_differentiable(radii)
+        return radii, means2d, depths, conics, comps
+
+    @staticmethod
+    def backward(ctx, v_radii, v_means2d, v_depths, v_conics, v_compensations):
+        means, quats, scales, viewmats, Ks, radii, conics, comps = ctx.saved_tensors
+        C, N = viewmats.shape[0], means.shape[0]
+        dev = means.device
+
+        def g(t, shape):
+            return torch.zeros(shape, device=dev) if t is None else _f32c(t)
+
+        v_means2d = g(v_means2d, (C, N, 2))
+        v_depths = g(v_depths, (C, N))
+        v_conics = g(v_conics, (C, N, 3))
+        if comps is not None:
+            v_compensations = g(v_compensations, (C, N))
+        else:
+            v_compensations = None
+        want_vm = ctx.needs_input_grad[4]
+        v_means = torch.empty((N, 3), device=dev)
+        v_quats = torch.empty((N, 4), device=dev)
+        v_scales = torch.empty((N, 3), device=dev)
+        v_viewmats = torch.empty((C, 4, 4), device=dev) if want_vm else None
+        _lib.call("gsplat_hip_projection_bwd", C, N, _ptr(means), _ptr(quats), _ptr(scales),
+                  _ptr(viewmats), _ptr(Ks), ctx.width, ctx.height, ctx.eps2d, _ptr(radii),
+                  _ptr(conics), _ptr(comps), _ptr(v_means2d), _ptr(v_depths), _ptr(v_conics),
+                  _ptr(v_compensations), _ptr(v_means), _ptr(v_quats), _ptr(v_scales),
+                  _ptr(v_viewmats), _stream())
+        return (v_means if ctx.needs_input_grad[0] else None, None,
+                v_quats if ctx.needs_input_grad[2] else None,
+                v_scales if ctx.needs_input_grad[3] else None,
+                v_viewmats, None, None, None, None, None, None, None, None, None, None)
+
+
+def fully_fused_projection(
+    means: Tensor,  # [N, 3]
+    covars: Optional[Tensor],  # must be None (quats/scales path only, as the Triton backend)
+    quats: Optional[Tensor],  # [N, 4]
+    scales: Optional[Tensor],  # [N, 3]
+    viewmats: Tensor,  # [C, 4, 4]
+    Ks: Tensor,  # [C, 3, 3]
+    width: int,
+    height: int,
+    eps2d: float = 0.3,
+    near_plane: float = 0.01,
+    far_plane: float = 1e10,
+    radius_clip: float = 0.0,
+    packed: bool = False,
+    sparse_grad: bool = False,
+    calc_compensations: bool = False,
+    camera_model: str = "pinhole",
+    block_size: int = 256,
+) -> Tuple[Tensor, Tensor, Tensor, Tensor, Optional[Tensor]]:
+    """Projects Gaussians to 2D (gsplat/triton_impl/_wrapper.py:429-541).
+
+    Returns radii i32[C,N], means2d [C,N,2], depths [C,N], conics [C,N,3],
+    compensations [C,N] or None.  Entries with radii == 0 are invalid (written
+    as zeros here; the reference leaves them uninitialised)."""
+    C = viewmats.size(0)
+    N = means.size(0)
+    assert means.size() == (N, 3), means.size()
+    assert viewmats.size() == (C, 4, 4), viewmats.size()
+    assert Ks.size() == (C, 3, 3), Ks.size()
+    assert covars is None
+    assert quats is not None, "covars or quats is required"
+    assert scales is not None, "covars or scales is required"
+    assert quats.size() == (N, 4), quats.size()
+    assert scales.size() == (N, 3), scales.size()
+    if packed or sparse_grad:
+        # The Triton reference cannot run packed either.
+        raise NotImplementedError("packed / sparse_grad projection is not supported yet")
+    return _FullyFusedProjection.apply(means, covars, quats, scales, viewmats, Ks, width, height,
+                                       eps2d, near_plane, far_plane, radius_clip,
+                                       calc_compensations, camera_model, block_size)
+
+
+# =================================================================== isect ==
+@torch.no_grad()
+def isect_tiles(
+    means2d: Tensor,  # [C, N, 2] or [nnz, 2]
+    radii: Tensor,  # [C, N] or [nnz]
+    depths: Tensor,  # [C, N] or [nnz]
+    tile_size: int,
+    tile_width: int,
+    tile_height: int,
+    sort: bool = True,
+    packed: bool = False,
+    n_cameras: Optional[int] = None,
+    camera_ids: Optional[Tensor] = None,
+    gaussian_ids: Optional[Tensor] = None,
+    block_size: int = 256,
+) -> Tuple[Tensor, Tensor, Tensor]:
+    """Maps projected Gaussians to intersecting tiles (isect_tiles.py:13-131).
+
+    Returns tiles_per_gauss i32 [C,N] (or [nnz]), isect_ids i64 [n_isects]
+    (camera | tile | depth bits, Triton tile-bit width) and flatten_ids i32.
+    One device->host read of n_isects, as the reference."""
+    dev = means2d.device
+    if packed:
+        nnz = means2d.size(0)
+        assert means2d.shape == (nnz, 2), means2d.size()
+        assert radii.shape == (nnz,), radii.size()
+        assert depths.shape == (nnz,), depths.size()
+        assert camera_ids is not None, "camera_ids is required if packed is True"
+        assert gaussian_ids is not None, "gaussian_ids is required if packed is True"
+        assert n_cameras is not None, "n_cameras is required if packed is True"
+        C, N, G = n_cameras, 0, nnz
+        camera_ids = camera_ids.to(torch.int32).contiguous()
+    else:
+        C, N, _ = means2d.shape
+        G = C * N
+        assert means2d.shape == (C, N, 2), means2d.size()
+        assert radii.shape == (C, N), radii.size()
+        assert depths.shape == (C, N), depths.size()
+        camera_ids = None
+    means2d = _f32c(means2d)
+    radii = radii.to(torch.int32).contiguous()
+    depths = _f32c(depths)
+    _dev_check(means2d, radii, depths)
+    n_bit_tile = _bit_length(tile_height * tile_width - 1)
+    n_bit_cam = _bit_length(C - 1)
+    assert n_bit_tile + n_bit_cam <= 32, "tile_id and cam_id exceed 32 bits"
+
+    st = _stream()
+    tpg = torch.empty(G, dtype=torch.int32, device=dev)
+    ws = torch.empty(max(int(_lib.query("gsplat_hip_isect_workspace_bytes", G)), 8),
+                     dtype=torch.uint8, device=dev)
+    n_dev = torch.empty(1, dtype=torch.int64, device=dev)
+    _lib.call("gsplat_hip_isect_count", G, _ptr(means2d), _ptr(radii), tile_size, tile_width,
+              tile_height, _ptr(tpg), _ptr(ws), _ptr(n_dev), st)
+    n_isects = int(n_dev.item())  # the single host sync (isect_tiles.py:102)
+    isect_ids = torch.empty(n_isects, dtype=torch.int64, device=dev)
+    flatten_ids = torch.empty(n_isects, dtype=torch.int32, device=dev)
+    _lib.call("gsplat_hip_isect_write", G, N, _ptr(means2d), _ptr(radii), _ptr(depths),
+              _ptr(camera_ids), tile_size, tile_width, tile_height, n_bit_tile, _ptr(ws),
+              _ptr(isect_ids), _ptr(flatten_ids), st)
+    if sort and n_isects > 0:
+        sws = torch.empty(max(int(_lib.query("gsplat_hip_sort_workspace_bytes", n_isects)), 8),
+                          dtype=torch.uint8, device=dev)
+        keys = torch.empty_like(isect_ids)
+        vals = torch.empty_like(flatten_ids)
+        _lib.call("gsplat_hip_radix_sort", n_isects, 32 + n_bit_tile + n_bit_cam,
+                  _ptr(isect_ids), _ptr(flatten_ids), _ptr(keys), _ptr(vals), _ptr(sws),
+                  sws.numel(), st)
+        isect_ids, flatten_ids = keys, vals
+    if not packed:
+        tpg = tpg.view(C, N)
+    return tpg, isect_ids, flatten_ids
+
+
+@torch.no_grad()
+def isect_offset_encode(isect_ids: Tensor, C: int, tile_width: int, tile_height: int) -> Tensor:
+    """First sorted isect index of every tile, i32 [C, tile_height, tile_width]
+    (isect_offset.py:8-33)."""
+    _dev_check(isect_ids)
+    isect_ids = isect_ids.contiguous()
+    offsets = torch.empty((C, tile_height, tile_width), dtype=torch.int32, device=isect_ids.device)
+    _lib.call("gsplat_hip_isect_offsets", isect_ids.numel(), _ptr(isect_ids), C, tile_width,
+              tile_height, _ptr(offsets), _stream())
+    return offsets
+
+
+# ====================================================== spherical harmonics ==
+def _coeff_rows(coeffs: Tensor) -> Tuple[Tensor, int]:
+    """[..., K, 3] coefficients -> (contiguous storage, n_coeff_rows).  A
+    [N,K,3] tensor expanded to [C,N,K,3] (rendering.py:404) is read in place."""
+    if coeffs.dim() == 4 and coeffs.size(0) > 1 and coeffs.stride(0) == 0 \
+            and coeffs[0].is_contiguous() and coeffs.dtype == torch.float32:
+        return coeffs[0], coeffs.size(1)
+    c = _f32c(coeffs)
+    return c, c.numel() // (c.shape[-2] * c.shape[-1])
+
+
+class _SphericalHarmonics(torch.autograd.Function):
+    """Spherical harmonics (gsplat/triton_impl/_wrapper.py:552-593)."""
+
+    @staticmethod
+    def forward(ctx, sh_degree, dirs, coeffs, masks, block_size=None):
+        dirs = _f32c(dirs)
+        base, n_rows = _coeff_rows(coeffs)
+        _dev_check(dirs, base)
+        K = coeffs.shape[-2]
+        n = dirs.numel() // 3
+        m = None if masks is None else masks.to(torch.bool).contiguous()
+        colors = torch.empty(*dirs.shape[:-1], 3, device=dirs.device, dtype=torch.float32)
+        _lib.call("gsplat_hip_sh_fwd", int(sh_degree), n, n_rows, K, _ptr(dirs), _ptr(base),
+                  _ptr(m), _ptr(colors), _stream())
+        ctx.save_for_backward(dirs, base, m)
+        ctx.sh_degree, ctx.n_rows, ctx.coeff_shape = int(sh_degree), n_rows, coeffs.shape
+        return colors
+
+    @staticmethod
+    def backward(ctx, v_colors):
+        dirs, base, m = ctx.saved_tensors
+        K = ctx.coeff_shape[-2]
+        n = dirs.numel() // 3
+        v_colors = _f32c(v_colors)
+        v_coeffs = torch.empty(*dirs.shape[:-1], K, 3, device=dirs.device)
+        want_dirs = ctx.needs_input_grad[1]
+        v_dirs = torch.empty_like(dirs) if want_dirs else None
+        _lib.call("gsplat_hip_sh_bwd", ctx.sh_degree, n, ctx.n_rows, K, _ptr(dirs), _ptr(base),
+                  _ptr(m), _ptr(v_colors), _ptr(v_coeffs), _ptr(v_dirs), _stream())
+        return None, v_dirs, v_coeffs.view(ctx.coeff_shape), None, None
+
+
+def spherical_harmonics(
+    degrees_to_use: int,
+    dirs: Tensor,  # [..., 3]
+    coeffs: Tensor,  # [..., K, 3]
+    masks: Optional[Tensor] = None,
+    block_size: int = None,
+) -> Tensor:
+    """Computes spherical harmonics colours [..., 3] (_wrapper.py:596-620)."""
+    assert (degrees_to_use + 1) ** 2 <= coeffs.shape[-2], coeffs.shape
+    assert dirs.shape[:-1] == coeffs.shape[:-2], (dirs.shape, coeffs.shape)
+    assert dirs.shape[-1] == 3, dirs.shape
+    assert coeffs.shape[-1] == 3, coeffs.shape
+    if masks is not None:
+        assert masks.shape == dirs.shape[:-1], masks.shape
+    return _SphericalHarmonics.apply(degrees_to_use, dirs, coeffs, masks, block_size)
+
+
+# ============================================================ rasterization ==
+class _RasterizeToPixels(torch.autograd.Function):
+    """Rasterize Gaussians (gsplat/triton_impl/_wrapper.py:42-182)."""
+
+    @staticmethod
+    def forward(ctx, means2d, conics, colors, opacities, backgrounds, masks, width, height,
+                tile_size, isect_offsets, flatten_ids, absgrad, block_size=8):
+        ctx.means2d_in = means2d if absgrad else None  # receives .absgrad (_wrapper.py:156)
+        means2d, conics, colors, opacities, backgrounds = (
+            _f32c(x) for x in (means2d, conics, colors, opacities, backgrounds))
+        _dev_check(means2d, conics, colors, opacities, isect_offsets, flatten_ids)
+        isect_offsets = isect_offsets.to(torch.int32).contiguous()
+        flatten_ids = flatten_ids.to(torch.int32).contiguous()
+        m = None if masks is None else masks.to(torch.bool).contiguous()
+        C, th, tw = isect_offsets.shape
+        D = colors.shape[-1]
+        dev = means2d.device
+        render_colors = torch.empty((C, height, width, D), device=dev)
+        render_alphas = torch.empty((C, height, width, 1), device=dev)
+        last_ids = torch.empty((C, height, width), dtype=torch.int32, device=dev)
+        _lib.call("gsplat_hip_rasterize_fwd", C, D, width, height, tile_size, tw, th,
+                  _ptr(means2d), _ptr(conics), _ptr(colors), _ptr(opacities), _ptr(backgrounds),
+                  _ptr(m), _ptr(isect_offsets), flatten_ids.numel(), _ptr(flatten_ids),
+                  _ptr(render_colors), _ptr(render_alphas), _ptr(last_ids), _stream())
+        ctx.save_for_backward(means2d, conics, colors, opacities, backgrounds, m, isect_offsets,
+                              flatten_ids, render_alphas, last_ids)
+        ctx.width, ctx.height, ctx.tile_size, ctx.absgrad = width, height, tile_size, absgrad
+        return render_colors, render_alphas
+
+    @staticmethod
+    def backward(ctx, v_render_colors, v_render_alphas):
+        (means2d, conics, colors, opacities, backgrounds, m, isect_offsets, flatten_ids,
+         render_alphas, last_ids) = ctx.saved_tensors
+        C, th, tw = isect_offsets.shape
+        D = colors.shape[-1]
+        G = opacities.numel()
+        v_render_colors = _f32c(v_render_colors)
+        v_render_alphas = _f32c(v_render_alphas)
+        v_means2d = torch.empty_like(means2d)
+        v_conics = torch.empty_like(conics)
+        v_colors = torch.empty_like(colors)
+        v_opacities = torch.empty_like(opacities)
+        v_abs = torch.empty_like(means2d) if ctx.absgrad else None
+        _lib.call("gsplat_hip_rasterize_bwd", C, G, D, ctx.width, ctx.height, ctx.tile_size, tw,
+                  th, _ptr(means2d), _ptr(conics), _ptr(colors), _ptr(opacities),
+                  _ptr(backgrounds), _ptr(m), _ptr(isect_offsets), flatten_ids.numel(),
+                  _ptr(flatten_ids), _ptr(render_alphas), _ptr(last_ids), _ptr(v_render_colors),
+                  _ptr(v_render_alphas), _ptr(v_means2d), _ptr(v_conics), _ptr(v_colors),
+                  _ptr(v_opacities), _ptr(v_abs), _stream())
+        if ctx.absgrad:
+            ctx.means2d_in.absgrad = v_abs
+        v_backgrounds = None
+        if ctx.needs_input_grad[4]:
+            v_backgrounds = (v_render_colors * (1.0 - render_alphas)).sum(dim=(1, 2))
+        return (v_means2d, v_conics, v_colors, v_opacities, v_backgrounds,
+                None, None, None, None, None, None, None, None)
+
+
+def rasterize_to_pixels(
+    means2d: Tensor,  # [C, N, 2] or [nnz, 2]
+    conics: Tensor,  # [C, N, 3] or [nnz, 3]
+    colors: Tensor,  # [C, N, channels] or [nnz, channels]
+    opacities: Tensor,  # [C, N] or [nnz]
+    image_width: int,
+    image_height: int,
+    tile_size: int,
+    isect_offsets: Tensor,  # [C, tile_height, tile_width]
+    flatten_ids: Tensor,  # [n_isects]
+    backgrounds: Optional[Tensor] = None,  # [C, channels]
+    masks: Optional[Tensor] = None,  # [C, tile_height, tile_width]
+    packed: bool = False,
+    absgrad: bool = False,
+    block_size: int = 8,
+) -> Tuple[Tensor, Tensor]:
+    """Rasterizes Gaussians to pixels (_wrapper.py:185-297).
+
+    Returns render_colors [C,H,W,channels] and render_alphas [C,H,W,1].
+    Channel counts outside {1,2,3,4,8,16,32} are zero-padded to the next one;
+    above 32 they are rendered in chunks of 32."""
+    C = isect_offsets.size(0)
+    device = means2d.device
+    if packed:
+        nnz = means2d.size(0)
+        assert means2d.shape == (nnz, 2), means2d.shape
+        assert conics.shape == (nnz, 3), conics.shape
+        assert colors.shape[0] == nnz, colors.shape
+        assert opacities.shape == (nnz,), opacities.shape
+    else:
+        N = means2d.size(1)
+        assert means2d.shape == (C, N, 2), means2d.shape
+        assert conics.shape == (C, N, 3), conics.shape
+        assert colors.shape[:2] == (C, N), colors.shape
+        assert opacities.shape == (C, N), opacities.shape
+    if backgrounds is not None:
+        assert backgrounds.shape == (C, colors.shape[-1]), backgrounds.shape
+    if masks is not None:
+        assert masks.shape == isect_offsets.shape, masks.shape
+
+    channels = colors.shape[-1]
+    if channels > 512 or channels == 0:
+        raise ValueError(f"Unsupported number of color channels: {channels}")
+    tile_height, tile_width = isect_offsets.shape[1:3]
+    assert tile_height * tile_size >= image_height, \
+        f"Assert Failed: {tile_height} * {tile_size} >= {image_height}"
+    assert tile_width * tile_size >= image_width, \
+        f"Assert Failed: {tile_width} * {tile_size} >= {image_width}"
+
+    def run(cols, bgs):
+        D = cols.shape[-1]
+        Dp = next(d for d in _SUPPORTED_D if d >= D)
+        if Dp != D:
+            cols = torch.cat([cols, torch.zeros(*cols.shape[:-1], Dp - D, device=device)], -1)
+            if bgs is not None:
+                bgs = torch.cat([bgs, torch.zeros(*bgs.shape[:-1], Dp - D, device=device)], -1)
+        rc, ra = _RasterizeToPixels.apply(means2d, conics, cols, opacities, bgs, masks,
+                                          image_width, image_height, tile_size, isect_offsets,
+                                          flatten_ids, absgrad, block_size)
+        return (rc[..., :D] if Dp != D else rc), ra
+
+    if channels <= 32:
+        render_colors, render_alphas = run(colors, backgrounds)
+    else:
+        outs = []
+        render_alphas = None
+        for i in range(0, channels, 32):
+            rc, ra = run(colors[..., i:i + 32],
+                         None if backgrounds is None else backgrounds[..., i:i + 32])
+            outs.append(rc)
+            render_alphas = ra if render_alphas is None else render_alphas
+        render_colors = torch.cat(outs, dim=-1)
+    return render_colors, render_alphas

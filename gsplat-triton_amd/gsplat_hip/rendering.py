@@ -1,0 +1,150 @@
+"""`rasterization()` front-end over the HIP backend.
+
+Mirrors `gsplat.rendering.rasterization` (gsplat/rendering.py:44-598) for
+the backend-independent torch glue: SH view directions, opacity repeat,
+anti-aliasing compensation, RGB/D/ED channel assembly, channel chunking and
+the `meta` dict consumed by the densification strategies.  The upstream file
+is not modified in a drop-in deployment (it only needs the extra
+`GSPLAT_BACKEND == "hip"` import branch); this copy exists so
+the hot path can be exercised end to end without the rest of gsplat.
+"""
+
+import math
+from typing import Dict, Optional, Tuple
+
+import torch
+from torch import Tensor
+
+from ._wrapper import (
+    fully_fused_projection,
+    isect_offset_encode,
+    isect_tiles,
+    rasterize_to_pixels,
+    spherical_harmonics,
+)
+
+
+def rasterization(
+    means: Tensor,  # [N, 3]
+    quats: Tensor,  # [N, 4]
+    scales: Tensor,  # [N, 3]
+    opacities: Tensor,  # [N]
+    colors: Tensor,  # [(C,) N, D] or [(C,) N, K, 3]
+    viewmats: Tensor,  # [C, 4, 4]
+    Ks: Tensor,  # [C, 3, 3]
+    width: int,
+    height: int,
+    near_plane: float = 0.01,
+    far_plane: float = 1e10,
+    radius_clip: float = 0.0,
+    eps2d: float = 0.3,
+    sh_degree: Optional[int] = None,
+    packed: bool = True,
+    tile_size: int = 16,
+    backgrounds: Optional[Tensor] = None,
+    render_mode: str = "RGB",
+    sparse_grad: bool = False,
+    absgrad: bool = False,
+    rasterize_mode: str = "classic",
+    channel_chunk: int = 32,
+    distributed: bool = False,
+    camera_model: str = "pinhole",
+    covars: Optional[Tensor] = None,
+) -> Tuple[Tensor, Tensor, Dict]:
+    """Rasterize N 3D Gaussians to C images (gsplat/rendering.py:44-598)."""
+    meta = {}
+    N = means.shape[0]
+    C = viewmats.shape[0]
+    device = means.device
+    assert means.shape == (N, 3), means.shape
+    if covars is None:
+        assert quats.shape == (N, 4), quats.shape
+        assert scales.shape == (N, 3), scales.shape
+    else:
+        assert covars.shape == (N, 3, 3), covars.shape
+        raise NotImplementedError("covars input is not supported by this backend "
+                                  "(same as the Triton backend, _wrapper.py:517-523)")
+    assert opacities.shape == (N,), opacities.shape
+    assert viewmats.shape == (C, 4, 4), viewmats.shape
+    assert Ks.shape == (C, 3, 3), Ks.shape
+    assert render_mode in ["RGB", "D", "ED", "RGB+D", "RGB+ED"], render_mode
+    if sh_degree is None:
+        assert (colors.dim() == 2 and colors.shape[0] == N) or (
+            colors.dim() == 3 and colors.shape[:2] == (C, N)), colors.shape
+    else:
+        assert (colors.dim() == 3 and colors.shape[0] == N and colors.shape[2] == 3) or (
+            colors.dim() == 4 and colors.shape[:2] == (C, N) and colors.shape[3] == 3), colors.shape
+        assert (sh_degree + 1) ** 2 <= colors.shape[-2], colors.shape
+    if absgrad:
+        assert not distributed, "AbsGrad is not supported in distributed mode."
+    if packed:
+        raise NotImplementedError("packed=True is not supported yet (the Triton reference "
+                                  "backend cannot run it either, SURVEY L11); pass packed=False")
+    if distributed:
+        raise NotImplementedError("distributed=True (Gaussian-sharded rendering) is not wired "
+                                  "yet; per-camera data parallelism lives in gsplat_hip.distributed")
+
+    radii, means2d, depths, conics, compensations = fully_fused_projection(
+        means, None, quats, scales, viewmats, Ks, width, height, eps2d=eps2d, packed=False,
+        near_plane=near_plane, far_plane=far_plane, radius_clip=radius_clip,
+        sparse_grad=sparse_grad, calc_compensations=(rasterize_mode == "antialiased"),
+        camera_model=camera_model)
+    opacities = opacities.repeat(C, 1)  # [C, N]
+    if compensations is not None:
+        opacities = opacities * compensations
+    meta.update({"camera_ids": None, "gaussian_ids": None, "radii": radii, "means2d": means2d,
+                 "depths": depths, "conics": conics, "opacities": opacities})
+
+    if sh_degree is None:
+        if colors.dim() == 2:
+            colors = colors.expand(C, -1, -1)
+    else:
+        camtoworlds = torch.inverse(viewmats)  # [C, 4, 4]
+        dirs = means[None, :, :] - camtoworlds[:, None, :3, 3]  # [C, N, 3]
+        masks = radii > 0
+        shs = colors.expand(C, -1, -1, -1) if colors.dim() == 3 else colors
+        colors = spherical_harmonics(sh_degree, dirs, shs, masks=masks)  # [C, N, 3]
+        colors = torch.clamp_min(colors + 0.5, 0.0)
+
+    if render_mode in ["RGB+D", "RGB+ED"]:
+        colors = torch.cat((colors, depths[..., None]), dim=-1)
+        if backgrounds is not None:
+            backgrounds = torch.cat([backgrounds, torch.zeros(C, 1, device=backgrounds.device)], -1)
+    elif render_mode in ["D", "ED"]:
+        colors = depths[..., None]
+        if backgrounds is not None:
+            backgrounds = torch.zeros(C, 1, device=backgrounds.device)
+
+    tile_width = math.ceil(width / float(tile_size))
+    tile_height = math.ceil(height / float(tile_size))
+    tiles_per_gauss, isect_ids, flatten_ids = isect_tiles(
+        means2d, radii, depths, tile_size, tile_width, tile_height, packed=False, n_cameras=C)
+    isect_offsets = isect_offset_encode(isect_ids, C, tile_width, tile_height)
+    meta.update({"tile_width": tile_width, "tile_height": tile_height,
+                 "tiles_per_gauss": tiles_per_gauss, "isect_ids": isect_ids,
+                 "flatten_ids": flatten_ids, "isect_offsets": isect_offsets, "width": width,
+                 "height": height, "tile_size": tile_size, "n_cameras": C})
+
+    if colors.shape[-1] > channel_chunk:
+        n_chunks = (colors.shape[-1] + channel_chunk - 1) // channel_chunk
+        render_colors, render_alphas = [], []
+        for i in range(n_chunks):
+            sl = slice(i * channel_chunk, (i + 1) * channel_chunk)
+            rc, ra = rasterize_to_pixels(
+                means2d, conics, colors[..., sl], opacities, width, height, tile_size,
+                isect_offsets, flatten_ids,
+                backgrounds=None if backgrounds is None else backgrounds[..., sl],
+                packed=False, absgrad=absgrad)
+            render_colors.append(rc)
+            render_alphas.append(ra)
+        render_colors = torch.cat(render_colors, dim=-1)
+        render_alphas = render_alphas[0]
+    else:
+        render_colors, render_alphas = rasterize_to_pixels(
+            means2d, conics, colors, opacities, width, height, tile_size, isect_offsets,
+            flatten_ids, backgrounds=backgrounds, packed=False, absgrad=absgrad)
+    if render_mode in ["ED", "RGB+ED"]:
+        render_colors = torch.cat(
+            [render_colors[..., :-1],
+             render_colors[..., -1:] / render_alphas.clamp(min=1e-10)], dim=-1)
+    return render_colors, render_alphas, meta

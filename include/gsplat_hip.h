@@ -1,0 +1,153 @@
+/*
+ * gsplat_hip.h -- C ABI of libgsplat_hip.so, the MI355X (gfx950) backend for
+ * the gsplat rasterization hot path.
+ *
+ * Conventions
+ *   - Plain device pointers (HIP/torch allocations on the current device),
+ *     element counts and a `stream` (hipStream_t passed as void*).  Every
+ *     kernel is enqueued on `stream`; nothing touches the default stream,
+ *     nothing allocates, nothing synchronises.
+ *   - All float tensors are contiguous fp32, row-major, shapes as documented.
+ *   - Return value: 0 = ok, 1 = argument error, 2 = HIP error; the message is
+ *     available from gsplat_hip_last_error() (thread-local).
+ *   - Optional inputs/outputs are NULL when absent.
+ *   - Gradient outputs are fully written by the call (zeroed on `stream`
+ *     where accumulation is needed); callers may pass uninitialised memory.
+ *
+ * Each entry point names the reference interface it replaces
+ * (hieu1999210/gsplat-triton, paths relative to the repository root).
+ */
+#ifndef GSPLAT_HIP_H
+#define GSPLAT_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+const char *gsplat_hip_last_error(void);
+int gsplat_hip_abi_version(void);
+
+/* ---------------------------------------------------------------------------
+ * Fused EWA projection (pinhole).
+ * Replaces fused_projection_fwd() / fused_projection_fwd_kernel
+ *   gsplat/triton_impl/fused_projection_fwd.py:16-307, called from
+ *   _FullyFusedProjection.forward (gsplat/triton_impl/_wrapper.py:304-353).
+ * means[N,3] quats[N,4] (16-B aligned) scales[N,3] viewmats[C,4,4] Ks[C,3,3]
+ * -> radii i32[C,N], means2d[C,N,2], depths[C,N], conics[C,N,3],
+ *    compensations[C,N] (NULL unless calc_compensations).
+ * Entries with radii == 0 have means2d/conics/compensations written as 0.
+ */
+int gsplat_hip_projection_fwd(int C, int N, const float *means, const float *quats,
+                              const float *scales, const float *viewmats, const float *Ks,
+                              int width, int height, float eps2d, float near_plane,
+                              float far_plane, float radius_clip, int32_t *radii,
+                              float *means2d, float *depths, float *conics,
+                              float *compensations, void *stream);
+
+/* Replaces fused_projection_bwd() / fused_projection_bwd_kernel
+ *   gsplat/triton_impl/fused_projection_bwd.py:24-465, called from
+ *   _FullyFusedProjection.backward (gsplat/triton_impl/_wrapper.py:355-426).
+ * Only (c, n) with radii > 0 contribute.  v_viewmats[C,4,4] may be NULL
+ * (viewmats does not require grad, _wrapper.py:394). */
+int gsplat_hip_projection_bwd(int C, int N, const float *means, const float *quats,
+                              const float *scales, const float *viewmats, const float *Ks,
+                              int width, int height, float eps2d, const int32_t *radii,
+                              const float *conics, const float *compensations,
+                              const float *v_means2d, const float *v_depths,
+                              const float *v_conics, const float *v_compensations,
+                              float *v_means, float *v_quats, float *v_scales,
+                              float *v_viewmats, void *stream);
+
+/* ---------------------------------------------------------------------------
+ * Spherical harmonics, degree 0..4, RGB.
+ * Replaces sh_to_color_fwd() (gsplat/triton_impl/sh_fwd.py:194-233) and the
+ * mask zeroing of _SphericalHarmonics.forward (_wrapper.py:555-572).
+ * dirs[n,3], coeffs[n_coeff_rows,K,3] (row i uses coeff row i % n_coeff_rows,
+ * so [N,K,3] coefficients broadcast over C cameras need no copy),
+ * masks u8[n] or NULL -> colors[n,3] (0 where masks[i] == 0). */
+int gsplat_hip_sh_fwd(int degree, int64_t n, int64_t n_coeff_rows, int K, const float *dirs,
+                      const float *coeffs, const uint8_t *masks, float *colors, void *stream);
+
+/* Replaces sh_to_color_bwd() (gsplat/triton_impl/sh_bwd.py:383-436) and
+ * _SphericalHarmonics.backward (_wrapper.py:574-593).
+ * -> v_coeffs[n,K,3] (bases >= (degree+1)^2 and masked rows are 0),
+ *    v_dirs[n,3] or NULL. */
+int gsplat_hip_sh_bwd(int degree, int64_t n, int64_t n_coeff_rows, int K, const float *dirs,
+                      const float *coeffs, const uint8_t *masks, const float *v_colors,
+                      float *v_coeffs, float *v_dirs, void *stream);
+
+/* ---------------------------------------------------------------------------
+ * Tile intersection.  Replaces isect_tiles() (gsplat/triton_impl/isect_tiles.py:13-131)
+ * as three calls so that the caller can size the outputs after ONE device->host
+ * read of n_isects (the reference's cumsum(...)[-1].item(), isect_tiles.py:101-102):
+ *   1. gsplat_hip_isect_count: tiles_per_gauss i32[G] + per-block prefix in
+ *      `workspace` (gsplat_hip_isect_workspace_bytes(G) bytes) + total in
+ *      *n_isects_device (int64 on device).
+ *   2. gsplat_hip_isect_write: isect_ids i64[n_isects], flatten_ids i32[n_isects]
+ *      (unsorted; Gaussian-major, tile-row-major order).  tile_bits =
+ *      (tile_width*tile_height - 1).bit_length() (Triton convention, isect_tiles.py:105).
+ *      camera_ids i32[G] for packed inputs, else NULL and cam = i / N.
+ *   3. gsplat_hip_radix_sort: stable sort on bits [0, 32+tile_bits+cam_bits)
+ *      (replaces radix_sort, gsplat/triton_impl/radix_sort/radix_sort.cu:9-62).
+ * G = C*N Gaussians (non-packed) or nnz (packed). */
+int64_t gsplat_hip_isect_workspace_bytes(int64_t n_gaussians);
+int gsplat_hip_isect_count(int64_t n_gaussians, const float *means2d, const int32_t *radii,
+                           int tile_size, int tile_width, int tile_height,
+                           int32_t *tiles_per_gauss, void *workspace,
+                           int64_t *n_isects_device, void *stream);
+int gsplat_hip_isect_write(int64_t n_gaussians, int N, const float *means2d,
+                           const int32_t *radii, const float *depths, const int32_t *camera_ids,
+                           int tile_size, int tile_width, int tile_height, int tile_bits,
+                           const void *workspace, int64_t *isect_ids, int32_t *flatten_ids,
+                           void *stream);
+int64_t gsplat_hip_sort_workspace_bytes(int64_t n);
+int gsplat_hip_radix_sort(int64_t n, int n_bits, const int64_t *keys_in, const int32_t *vals_in,
+                          int64_t *keys_out, int32_t *vals_out, void *workspace,
+                          int64_t workspace_bytes, void *stream);
+
+/* Replaces get_isect_offsets() (gsplat/triton_impl/isect_offset.py:8-63).
+ * offsets i32[C,tile_height,tile_width]: index of the first sorted isect of
+ * each tile (= number of isects with a smaller (camera, tile) key). */
+int gsplat_hip_isect_offsets(int64_t n_isects, const int64_t *isect_ids, int C, int tile_width,
+                             int tile_height, int32_t *offsets, void *stream);
+
+/* ---------------------------------------------------------------------------
+ * Rasterization.  D in {1,2,3,4,8,16,32} (gsplat_hip_rasterize_supported_channels);
+ * tile_size <= 16.
+ * Replaces rasterize_to_pixels_fwd() (gsplat/triton_impl/rasterize_to_pixels_fwd.py:199-285)
+ * called from _RasterizeToPixels.forward (_wrapper.py:46-102).
+ * means2d[G,2] conics[G,3] colors[G,D] opacities[G] (G = C*N or nnz),
+ * backgrounds[C,D] or NULL, masks u8[C,th,tw] or NULL (true = skip tile),
+ * isect_offsets i32[C,th,tw], flatten_ids i32[n_isects]
+ * -> render_colors[C,H,W,D], render_alphas[C,H,W], last_ids i32[C,H,W]. */
+int gsplat_hip_rasterize_supported_channels(int D);
+int gsplat_hip_rasterize_fwd(int C, int D, int width, int height, int tile_size, int tile_width,
+                             int tile_height, const float *means2d, const float *conics,
+                             const float *colors, const float *opacities,
+                             const float *backgrounds, const uint8_t *masks,
+                             const int32_t *isect_offsets, int64_t n_isects,
+                             const int32_t *flatten_ids, float *render_colors,
+                             float *render_alphas, int32_t *last_ids, void *stream);
+
+/* Replaces rasterize_to_pixels_bwd() (gsplat/triton_impl/rasterize_to_pixels_bwd.py:340-457)
+ * called from _RasterizeToPixels.backward (_wrapper.py:104-182).
+ * -> v_means2d[G,2], v_conics[G,3], v_colors[G,D], v_opacities[G],
+ *    v_means2d_abs[G,2] or NULL (absgrad). */
+int gsplat_hip_rasterize_bwd(int C, int64_t n_gaussians, int D, int width, int height,
+                             int tile_size, int tile_width, int tile_height,
+                             const float *means2d, const float *conics, const float *colors,
+                             const float *opacities, const float *backgrounds,
+                             const uint8_t *masks, const int32_t *isect_offsets,
+                             int64_t n_isects, const int32_t *flatten_ids,
+                             const float *render_alphas, const int32_t *last_ids,
+                             const float *v_render_colors, const float *v_render_alphas,
+                             float *v_means2d, float *v_conics, float *v_colors,
+                             float *v_opacities, float *v_means2d_abs, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GSPLAT_HIP_H */

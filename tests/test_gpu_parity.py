@@ -1,0 +1,307 @@
+"""GPU parity: the HIP path (through the C ABI) against the reference goldens
+and the CPU oracle.  Tolerances follow the reference's own tests
+(triton_tests/test_fused_proj.py:116-162, test_sh.py:25-37,
+test_isect.py:86-89 [exact], test_ras2pix.py:132-161)."""
+
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import load_golden
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def T(x, dtype=None):
+    t = torch.from_numpy(np.ascontiguousarray(x)).to(DEV)
+    return t if dtype is None else t.to(dtype)
+
+
+def close(a, b, rtol, atol, what=""):
+    a = a.detach().cpu().numpy() if isinstance(a, torch.Tensor) else np.asarray(a)
+    b = b.detach().cpu().numpy() if isinstance(b, torch.Tensor) else np.asarray(b)
+    np.testing.assert_allclose(a, b, rtol=rtol, atol=atol, err_msg=what)
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import gsplat_hip  # noqa: F401  (fails loudly if the .so is missing)
+
+
+# -------------------------------------------------------------- projection
+PROJ = ["proj_garden", "proj_garden_comp", "proj_synth", "proj_synth_comp"]
+
+
+@pytest.mark.parametrize("name", PROJ)
+def test_projection_vs_reference(name):
+    import gsplat_hip
+    g = load_golden(name)
+    comp = "comps" in g
+    m, q, s, vm = (T(g[k]).requires_grad_(True) for k in ("means", "quats", "scales", "viewmats"))
+    radii, m2, d, cn, cp = gsplat_hip.fully_fused_projection(
+        m, None, q, s, vm, T(g["Ks"]), int(g["width"]), int(g["height"]), eps2d=float(g["eps2d"]),
+        near_plane=float(g["near"]), far_plane=float(g["far"]),
+        radius_clip=float(g["radius_clip"]), calc_compensations=comp)
+    assert torch.equal(radii.cpu(), torch.from_numpy(g["radii"]))
+    v = radii.cpu().numpy() > 0
+    close(m2.detach().cpu().numpy()[v], g["means2d"][v], 1e-4, 1e-4, "means2d")
+    close(d, g["depths"], 1e-5, 1e-5, "depths")
+    close(cn.detach().cpu().numpy()[v], g["conics"][v], 1e-4, 1e-5, "conics")
+    if comp:
+        close(cp.detach().cpu().numpy()[v], g["comps"][v], 5e-4, 1e-3, "comps")
+    loss = (m2 * T(g["v_means2d"])).sum() + (d * T(g["v_depths"])).sum() \
+        + (cn * T(g["v_conics"])).sum()
+    if comp:
+        loss = loss + (cp * T(g["v_comps"])).sum()
+    gm, gq, gs, gv = torch.autograd.grad(loss, (m, q, s, vm))
+    close(gm, g["v_means"], 1e-3, 1e-3, "v_means")
+    close(gq, g["v_quats"], 5e-3, 5e-3, "v_quats")
+    close(gs, g["v_scales"], 5e-2, 5e-2, "v_scales")
+    ref = g["v_viewmats"]
+    fin = np.isfinite(ref)  # the reference's v_viewmats can be NaN-poisoned (L22)
+    close(gv.cpu().numpy()[fin], ref[fin], 1e-4, 5e-3, "v_viewmats")
+
+
+# -------------------------------------------------------------------- SH
+@pytest.mark.parametrize("deg", range(5))
+def test_sh_vs_reference(deg):
+    import gsplat_hip
+    g = load_golden(f"sh_deg{deg}")
+    cf = T(g["coeffs"]).requires_grad_(True)
+    dr = T(g["dirs"]).requires_grad_(True)
+    col = gsplat_hip.spherical_harmonics(deg, dr, cf, masks=T(g["masks"]))
+    close(col, g["colors"], 1e-4, 1e-4, "colors")
+    gc, gd = torch.autograd.grad((col * T(g["v_colors"])).sum(), (cf, dr))
+    close(gc, g["v_coeffs"], 1e-4, 1e-4, "v_coeffs")
+    if deg > 0:
+        close(gd, g["v_dirs"], 1e-4, 1e-4, "v_dirs")
+
+
+def test_sh_broadcast_coeffs_match_materialised():
+    import gsplat_hip
+    torch.manual_seed(0)
+    C, N = 3, 777
+    sh = torch.randn(N, 16, 3, device=DEV, requires_grad=True)
+    dirs = torch.randn(C, N, 3, device=DEV)
+    masks = torch.rand(C, N, device=DEV) > 0.3
+    a = gsplat_hip.spherical_harmonics(3, dirs, sh.expand(C, -1, -1, -1), masks=masks)
+    b = gsplat_hip.spherical_harmonics(3, dirs, sh.expand(C, -1, -1, -1).contiguous(), masks=masks)
+    assert torch.equal(a, b)
+    ga, = torch.autograd.grad(a.sum(), sh)
+    gb, = torch.autograd.grad(b.sum(), sh)
+    close(ga, gb, 1e-6, 1e-6)
+
+
+# ----------------------------------------------------------------- isect
+@pytest.mark.parametrize("name", ["isect_garden_t16", "isect_garden_t4", "isect_pow2_c2"])
+def test_isect_bit_exact_vs_reference(name):
+    import gsplat_hip
+    g = load_golden(name)
+    ts, tw, th, C = (int(g[k]) for k in ("tile_size", "tile_width", "tile_height", "C"))
+    tpg, ids, fids = gsplat_hip.isect_tiles(T(g["means2d"]), T(g["radii"]), T(g["depths"]),
+                                            ts, tw, th)
+    assert np.array_equal(tpg.cpu().numpy(), g["tiles_per_gauss"])
+    assert np.array_equal(ids.cpu().numpy(), g["isect_ids"])
+    assert np.array_equal(fids.cpu().numpy(), g["flatten_ids"])
+    off = gsplat_hip.isect_offset_encode(ids, C, tw, th)
+    assert np.array_equal(off.cpu().numpy(), g["isect_offsets"])
+
+
+def test_isect_edge_cases():
+    import gsplat_hip
+    from oracle import gsplat_oracle as O
+    # empty input, all-invalid input, single isect
+    for C, N in ((1, 0), (2, 5)):
+        m2 = torch.zeros(C, N, 2, device=DEV)
+        r = torch.zeros(C, N, dtype=torch.int32, device=DEV)
+        d = torch.ones(C, N, device=DEV)
+        tpg, ids, fids = gsplat_hip.isect_tiles(m2, r, d, 16, 4, 3)
+        assert ids.numel() == 0 and fids.numel() == 0 and not tpg.any()
+        off = gsplat_hip.isect_offset_encode(ids, C, 4, 3)
+        assert off.shape == (C, 3, 4) and not off.any()
+    ids = torch.tensor([(2 << 32) | 7], dtype=torch.int64, device=DEV)
+    off = gsplat_hip.isect_offset_encode(ids, 1, 3, 2)
+    assert off.flatten().tolist() == O.isect_offset_encode(ids.cpu().numpy(), 1, 3, 2).reshape(-1).tolist()
+
+
+def test_isect_random_vs_oracle_large_radii():
+    """Ragged input: huge and tiny radii, off-screen means, C=3, exact."""
+    import gsplat_hip
+    from oracle import gsplat_oracle as O
+    rng = np.random.default_rng(1)
+    C, N, W, H, ts = 3, 3000, 333, 211, 16
+    tw, th = math.ceil(W / ts), math.ceil(H / ts)
+    m2 = rng.uniform(-60, 400, (C, N, 2)).astype(np.float32)
+    r = rng.choice([0, 1, 2, 5, 17, 90, 300], (C, N)).astype(np.int32)
+    d = rng.uniform(0.05, 50, (C, N)).astype(np.float32)
+    d[0, :50] = d[0, 50:100]  # depth ties -> stability matters
+    tpg, ids, fids = gsplat_hip.isect_tiles(T(m2), T(r), T(d), ts, tw, th)
+    otpg, oids, ofids = O.isect_tiles(m2, r, d, ts, tw, th)
+    assert np.array_equal(tpg.cpu().numpy(), otpg)
+    assert np.array_equal(ids.cpu().numpy(), oids)
+    assert np.array_equal(fids.cpu().numpy(), ofids)
+    off = gsplat_hip.isect_offset_encode(ids, C, tw, th)
+    assert np.array_equal(off.cpu().numpy(), O.isect_offset_encode(oids, C, tw, th))
+
+
+# ------------------------------------------------------------ rasterize
+RASTER = ["raster_garden_d3_bg", "raster_garden_d4", "raster_garden_d8_bg"]
+
+
+@pytest.mark.parametrize("name", RASTER)
+def test_raster_vs_reference(name):
+    import gsplat_hip
+    g = load_golden(name)
+    use_bg = "backgrounds" in g
+    m2, cn, cl, op = (T(g[k]).requires_grad_(True) for k in ("means2d", "conics", "colors",
+                                                             "opacities"))
+    bg = T(g["backgrounds"]).requires_grad_(True) if use_bg else None
+    rc, ra = gsplat_hip.rasterize_to_pixels(m2, cn, cl, op, int(g["width"]), int(g["height"]),
+                                            int(g["tile_size"]), T(g["isect_offsets"]),
+                                            T(g["flatten_ids"]), backgrounds=bg, absgrad=True)
+    close(ra, g["render_alphas"], 1.3e-6 * 10, 1e-5, "alphas")
+    close(rc, g["render_colors"], 1.3e-6 * 10, 1e-5, "colors")
+    ins = (m2, cn, cl, op) + ((bg,) if use_bg else ())
+    grads = torch.autograd.grad((rc * T(g["v_render_colors"])).sum()
+                                + (ra * T(g["v_render_alphas"])).sum(), ins)
+    close(grads[0], g["v_means2d"], 5e-3, 5e-3, "v_means2d")
+    close(grads[1], g["v_conics"], 1e-3, 1e-3, "v_conics")
+    close(grads[2], g["v_colors"], 1e-3, 1e-3, "v_colors")
+    close(grads[3], g["v_opacities"], 2e-3, 2e-3, "v_opacities")
+    if use_bg:
+        close(grads[4], g["v_backgrounds"], 5e-3, 5e-3, "v_backgrounds")
+    close(m2.absgrad, g["v_means2d_abs"], 5e-3, 5e-3, "absgrad")
+
+
+def _garden_scene(n, C, W, H, seed=0, scale=0.02):
+    """test_garden.npz is not available on the GPU box: a synthetic scene of the
+    same statistics (means in [-2,2]^3 in front of C cameras)."""
+    g = torch.Generator().manual_seed(seed)
+    means = (torch.rand(n, 3, generator=g) * 4 - 2)
+    quats = torch.nn.functional.normalize(torch.randn(n, 4, generator=g), dim=-1)
+    scales = torch.rand(n, 3, generator=g) * scale
+    opac = torch.rand(n, generator=g)
+    vm = torch.eye(4)[None].repeat(C, 1, 1)
+    for c in range(C):
+        a = 0.4 * c
+        vm[c, :3, :3] = torch.tensor([[math.cos(a), 0, math.sin(a)], [0, 1, 0],
+                                      [-math.sin(a), 0, math.cos(a)]])
+        vm[c, 2, 3] = 5.0
+    K = torch.tensor([[0.9 * W, 0, W / 2], [0, 0.9 * W, H / 2], [0, 0, 1]])[None].repeat(C, 1, 1)
+    return means, quats, scales, opac, vm, K
+
+
+@pytest.mark.parametrize("D,tile", [(3, 16), (4, 16), (16, 16), (32, 8), (5, 16)])
+def test_raster_vs_oracle_random(D, tile):
+    import gsplat_hip
+    from oracle import gsplat_oracle as O
+    C, N, W, H = 2, 4000, 173, 131
+    means, quats, scales, opac, vm, K = _garden_scene(N, C, W, H, seed=D, scale=0.05)
+    radii, m2, d, cn, _ = gsplat_hip.fully_fused_projection(
+        means.to(DEV), None, quats.to(DEV), scales.to(DEV), vm.to(DEV), K.to(DEV), W, H)
+    tw, th = math.ceil(W / tile), math.ceil(H / tile)
+    _, ids, fids = gsplat_hip.isect_tiles(m2, radii, d, tile, tw, th)
+    off = gsplat_hip.isect_offset_encode(ids, C, tw, th)
+    gcol = torch.Generator().manual_seed(3)
+    cols = torch.rand(C, N, D, generator=gcol).to(DEV)
+    ops = opac[None].repeat(C, 1).to(DEV)
+    bg = torch.rand(C, D, generator=gcol).to(DEV)
+    ins = [x.detach().clone().requires_grad_(True) for x in (m2, cn, cols, ops)]
+    rc, ra = gsplat_hip.rasterize_to_pixels(*ins, W, H, tile, off, fids, backgrounds=bg)
+    oc, oa, ol = O.raster_fwd(m2.cpu().numpy(), cn.cpu().numpy(), cols.cpu().numpy(),
+                              ops.cpu().numpy(), bg.cpu().numpy(), W, H, tile,
+                              off.cpu().numpy(), fids.cpu().numpy())
+    close(ra, oa, 1e-5, 2e-5, "alphas")
+    close(rc, oc, 1e-5, 2e-5, "colors")
+    vrc = torch.randn(rc.shape, generator=gcol).to(DEV)
+    vra = torch.randn(ra.shape, generator=gcol).to(DEV)
+    grads = torch.autograd.grad((rc * vrc).sum() + (ra * vra).sum(), ins)
+    Dp = next(x for x in (1, 2, 3, 4, 8, 16, 32) if x >= D)
+    pad = lambda x: np.concatenate([x, np.zeros(x.shape[:-1] + (Dp - D,), np.float32)], -1)
+    ref = O.raster_bwd(m2.cpu().numpy(), cn.cpu().numpy(), pad(cols.cpu().numpy()),
+                       ops.cpu().numpy(), pad(bg.cpu().numpy()), W, H, tile, off.cpu().numpy(),
+                       fids.cpu().numpy(), oa, ol, pad(vrc.cpu().numpy()), vra.cpu().numpy())
+    close(grads[0], ref[0], 5e-3, 5e-3, "v_means2d")
+    close(grads[1], ref[1], 1e-3, 1e-3, "v_conics")
+    close(grads[2], ref[2][..., :D], 1e-3, 1e-3, "v_colors")
+    close(grads[3], ref[3], 2e-3, 2e-3, "v_opacities")
+
+
+def test_raster_tile_masks_skip():
+    import gsplat_hip
+    C, N, W, H = 1, 500, 64, 48
+    means, quats, scales, opac, vm, K = _garden_scene(N, C, W, H, scale=0.1)
+    radii, m2, d, cn, _ = gsplat_hip.fully_fused_projection(
+        means.to(DEV), None, quats.to(DEV), scales.to(DEV), vm.to(DEV), K.to(DEV), W, H)
+    _, ids, fids = gsplat_hip.isect_tiles(m2, radii, d, 16, 4, 3)
+    off = gsplat_hip.isect_offset_encode(ids, C, 4, 3)
+    cols = torch.rand(C, N, 3, device=DEV)
+    bg = torch.tensor([[0.1, 0.2, 0.3]], device=DEV)
+    masks = torch.zeros(C, 3, 4, dtype=torch.bool, device=DEV)
+    masks[0, 1, 2] = True
+    rc, ra = gsplat_hip.rasterize_to_pixels(m2, cn, cols, opac[None].to(DEV), W, H, 16, off, fids,
+                                            backgrounds=bg, masks=masks)
+    rc0, ra0 = gsplat_hip.rasterize_to_pixels(m2, cn, cols, opac[None].to(DEV), W, H, 16, off,
+                                              fids, backgrounds=bg)
+    blk = (slice(None), slice(16, 32), slice(32, 48))
+    assert torch.all(ra[blk] == 0) and torch.allclose(rc[blk], bg.view(1, 1, 1, 3).expand_as(rc[blk]))
+    other = torch.ones_like(ra, dtype=torch.bool)
+    other[blk] = False
+    assert torch.equal(ra[other], ra0[other])
+
+
+# -------------------------------------------------------- end-to-end M1
+@pytest.mark.parametrize("name", ["e2e_m1_rgb", "e2e_m1c2_rgbed"])
+def test_rasterization_end_to_end_vs_reference(name):
+    import gsplat_hip
+    g = load_golden(name)
+    ins = [T(g[k]).requires_grad_(True) for k in ("means", "quats", "scales", "opacities", "sh")]
+    rc, ra, meta = gsplat_hip.rasterization(
+        *ins, T(g["viewmats"]), T(g["Ks"]), int(g["width"]), int(g["height"]), sh_degree=3,
+        packed=False, render_mode=str(g["render_mode"]), backgrounds=T(g["backgrounds"]))
+    assert np.array_equal(meta["radii"].cpu().numpy(), g["radii"])
+    assert np.array_equal(meta["isect_ids"].cpu().numpy(), g["isect_ids"])
+    assert np.array_equal(meta["flatten_ids"].cpu().numpy(), g["flatten_ids"])
+    assert np.array_equal(meta["isect_offsets"].cpu().numpy(), g["isect_offsets"])
+    close(ra, g["render_alphas"], 1e-4, 1e-4, "alphas")
+    close(rc, g["render_colors"], 1e-4, 1e-4, "colors")  # tests/test_rasterization.py:22-90
+    grads = torch.autograd.grad((rc * T(g["v_render_colors"])).sum()
+                                + (ra * T(g["v_render_alphas"])).sum(), ins)
+    for k, gr in zip(("v_means", "v_quats", "v_scales", "v_opacities", "v_sh"), grads):
+        ref = g[k]
+        scale = max(1.0, float(np.abs(ref).max()))
+        close(gr, ref, 2e-2, 2e-3 * scale, k)
+
+
+# ------------------------------------------- size-independent properties
+def test_full_size_invariants_m2():
+    """BASELINE config M2 scale (1M Gaussians, 1080p): properties that hold
+    at any size -- sorted keys, offsets = lower_bound, permutation of the
+    unsorted isects, alpha in [0, 1), colour = sum of vis*c + T*bg bounds."""
+    import gsplat_hip
+    C, N, W, H = 1, 1_000_000, 1920, 1080
+    means, quats, scales, opac, vm, K = _garden_scene(N, C, W, H, seed=7, scale=0.02)
+    radii, m2, d, cn, _ = gsplat_hip.fully_fused_projection(
+        means.to(DEV), None, quats.to(DEV), scales.to(DEV), vm.to(DEV), K.to(DEV), W, H)
+    tw, th = math.ceil(W / 16), math.ceil(H / 16)
+    tpg, ids, fids = gsplat_hip.isect_tiles(m2, radii, d, 16, tw, th)
+    _, ids_u, fids_u = gsplat_hip.isect_tiles(m2, radii, d, 16, tw, th, sort=False)
+    assert ids.numel() == int(tpg.sum()) > 1_000_000
+    assert torch.all(ids[1:] >= ids[:-1])
+    # stable sort <=> (key, unsorted position) pairs sorted
+    order = torch.sort(ids_u, stable=True).indices
+    assert torch.equal(ids_u[order], ids) and torch.equal(fids_u[order], fids)
+    off = gsplat_hip.isect_offset_encode(ids, C, tw, th)
+    tiles = torch.arange(C * tw * th, device=DEV, dtype=torch.int64)
+    tile_key = (ids >> 32) & ((1 << (tw * th - 1).bit_length()) - 1)
+    lb = torch.searchsorted(tile_key.contiguous(), tiles)
+    assert torch.equal(off.flatten().long(), lb)
+    cols = torch.rand(C, N, 3, device=DEV)
+    rc, ra = gsplat_hip.rasterize_to_pixels(m2, cn, cols, opac[None].to(DEV), W, H, 16, off, fids)
+    assert torch.isfinite(rc).all() and (ra >= 0).all() and (ra < 1).all()
+    assert (rc <= ra + 1e-5).all()  # colours in [0,1] => composite <= alpha
