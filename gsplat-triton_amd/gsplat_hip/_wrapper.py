@@ -55,6 +55,38 @@ def _bit_length(x: int) -> int:
     return int(x).bit_length()
 
 
+# Optional per-kernel timing (bench.py): when enabled, HIP events are recorded
+# on the launch stream immediately around the named C-ABI calls.
+_timers = None
+
+
+def enable_kernel_timers(enabled: bool = True):
+    global _timers
+    _timers = {} if enabled else None
+    return _timers
+
+
+class _Timed:
+    __slots__ = ("name", "ev")
+
+    def __init__(self, name):
+        self.name = name
+        self.ev = None
+
+    def __enter__(self):
+        if _timers is not None:
+            self.ev = torch.cuda.Event(enable_timing=True)
+            self.ev.record()
+        return self
+
+    def __exit__(self, *exc):
+        if self.ev is not None:
+            end = torch.cuda.Event(enable_timing=True)
+            end.record()
+            _timers.setdefault(self.name, []).append((self.ev, end))
+        return False
+
+
 # ============================================================== projection ==
 class _FullyFusedProjection(torch.autograd.Function):
     """Projects Gaussians to 2D (gsplat/triton_impl/_wrapper.py:300-426)."""
@@ -325,10 +357,12 @@ class _RasterizeToPixels(torch.autograd.Function):
         render_colors = torch.empty((C, height, width, D), device=dev)
         render_alphas = torch.empty((C, height, width, 1), device=dev)
         last_ids = torch.empty((C, height, width), dtype=torch.int32, device=dev)
-        _lib.call("gsplat_hip_rasterize_fwd", C, D, width, height, tile_size, tw, th,
-                  _ptr(means2d), _ptr(conics), _ptr(colors), _ptr(opacities), _ptr(backgrounds),
-                  _ptr(m), _ptr(isect_offsets), flatten_ids.numel(), _ptr(flatten_ids),
-                  _ptr(render_colors), _ptr(render_alphas), _ptr(last_ids), _stream())
+        with _Timed("rasterize_fwd"):
+            _lib.call("gsplat_hip_rasterize_fwd", C, D, width, height, tile_size, tw, th,
+                      _ptr(means2d), _ptr(conics), _ptr(colors), _ptr(opacities),
+                      _ptr(backgrounds), _ptr(m), _ptr(isect_offsets), flatten_ids.numel(),
+                      _ptr(flatten_ids), _ptr(render_colors), _ptr(render_alphas),
+                      _ptr(last_ids), _stream())
         ctx.save_for_backward(means2d, conics, colors, opacities, backgrounds, m, isect_offsets,
                               flatten_ids, render_alphas, last_ids)
         ctx.width, ctx.height, ctx.tile_size, ctx.absgrad = width, height, tile_size, absgrad
@@ -348,12 +382,13 @@ class _RasterizeToPixels(torch.autograd.Function):
         v_colors = torch.empty_like(colors)
         v_opacities = torch.empty_like(opacities)
         v_abs = torch.empty_like(means2d) if ctx.absgrad else None
-        _lib.call("gsplat_hip_rasterize_bwd", C, G, D, ctx.width, ctx.height, ctx.tile_size, tw,
-                  th, _ptr(means2d), _ptr(conics), _ptr(colors), _ptr(opacities),
-                  _ptr(backgrounds), _ptr(m), _ptr(isect_offsets), flatten_ids.numel(),
-                  _ptr(flatten_ids), _ptr(render_alphas), _ptr(last_ids), _ptr(v_render_colors),
-                  _ptr(v_render_alphas), _ptr(v_means2d), _ptr(v_conics), _ptr(v_colors),
-                  _ptr(v_opacities), _ptr(v_abs), _stream())
+        with _Timed("rasterize_bwd"):
+            _lib.call("gsplat_hip_rasterize_bwd", C, G, D, ctx.width, ctx.height, ctx.tile_size,
+                      tw, th, _ptr(means2d), _ptr(conics), _ptr(colors), _ptr(opacities),
+                      _ptr(backgrounds), _ptr(m), _ptr(isect_offsets), flatten_ids.numel(),
+                      _ptr(flatten_ids), _ptr(render_alphas), _ptr(last_ids),
+                      _ptr(v_render_colors), _ptr(v_render_alphas), _ptr(v_means2d),
+                      _ptr(v_conics), _ptr(v_colors), _ptr(v_opacities), _ptr(v_abs), _stream())
         if ctx.absgrad:
             ctx.means2d_in.absgrad = v_abs
         v_backgrounds = None

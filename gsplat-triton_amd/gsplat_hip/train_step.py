@@ -1,0 +1,191 @@
+"""One 3DGS training step over the HIP hot path (the unit bench.py measures).
+
+Mirrors the per-iteration work of examples/simple_trainer.py with its default
+config (sh_degree 3, packed=False, classic rasterize mode, batch 1):
+  render (simple_trainer.py:453-507, 603-615) -> loss 0.8*L1 + 0.2*(1-SSIM,
+  "valid" padding) (:642-646) -> backward (:683) -> DefaultStrategy running
+  statistics (gsplat/strategy/default.py:213-262) -> Adam on every parameter
+  group with the trainer's learning rates and batch scaling (:235-277).
+
+Multi-GPU is per-camera data parallelism: every rank holds the same
+Gaussians, renders its own camera, and the Gaussian gradients are summed with
+one RCCL all-reduce per parameter group over xGMI.
+"""
+
+import math
+import os
+from typing import Dict, Optional
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from .rendering import rasterization
+
+C0 = 0.28209479177387814
+
+
+def rgb_to_sh(rgb):
+    return (rgb - 0.5) / C0
+
+
+def load_garden_scene(path: str, scene_grid: int = 3):
+    """load_test_data(scene_grid) semantics (gsplat/_helper.py:9-55) on the
+    cropped garden fixture: tile the [-2,2]^3 crop into a scene_grid^2 grid."""
+    d = np.load(path)
+    means = torch.from_numpy(d["means3d"]).float()
+    colors = torch.from_numpy(d["colors"].astype(np.float32) / 255.0)
+    edges = torch.tensor([4.0, 4.0, 4.0])
+    r = scene_grid // 2
+    gx, gy = torch.meshgrid(torch.arange(-r, r + 1), torch.arange(-r, r + 1), indexing="ij")
+    grid = torch.stack([gx, gy, torch.zeros_like(gx)], -1).reshape(-1, 3).float()
+    means = (means[None] + grid[:, None] * edges).reshape(-1, 3)
+    colors = colors.repeat(scene_grid ** 2, 1)
+    return (means, colors, torch.from_numpy(d["viewmats"]), torch.from_numpy(d["Ks"]),
+            int(d["width"]), int(d["height"]))
+
+
+def camera_pool(viewmats, Ks, src_w, src_h, width, height, n, seed=0):
+    """`n` cameras: the scene's own cameras first, then small jitters of them;
+    intrinsics rescaled to width x height as profiling/main.py:85-87."""
+    g = torch.Generator().manual_seed(seed)
+    K = Ks.clone()
+    K[:, 0, :] *= width / src_w
+    K[:, 1, :] *= height / src_h
+    vms, ks = [], []
+    for i in range(n):
+        v = viewmats[i % len(viewmats)].clone()
+        if i >= len(viewmats):
+            v[:3, 3] += torch.randn(3, generator=g) * 0.05
+        vms.append(v)
+        ks.append(K[i % len(K)])
+    return torch.stack(vms), torch.stack(ks)
+
+
+def _gauss_window(size=11, sigma=1.5, device="cpu"):
+    x = torch.arange(size, dtype=torch.float32, device=device) - size // 2
+    w = torch.exp(-(x ** 2) / (2 * sigma ** 2))
+    return w / w.sum()
+
+
+def ssim(img1, img2, window=None):
+    """Mean SSIM with an 11x11 Gaussian window (sigma 1.5), "valid" padding --
+    the quantity fused_ssim(..., padding="valid") returns. img: [B,C,H,W]."""
+    Cc = img1.shape[1]
+    w = _gauss_window(device=img1.device) if window is None else window
+    wx = w.view(1, 1, 1, -1).repeat(Cc, 1, 1, 1)
+    wy = w.view(1, 1, -1, 1).repeat(Cc, 1, 1, 1)
+
+    def blur(x):
+        return F.conv2d(F.conv2d(x, wx, groups=Cc), wy, groups=Cc)
+
+    mu1, mu2 = blur(img1), blur(img2)
+    s11 = blur(img1 * img1) - mu1 * mu1
+    s22 = blur(img2 * img2) - mu2 * mu2
+    s12 = blur(img1 * img2) - mu1 * mu2
+    C1, C2 = 0.01 ** 2, 0.03 ** 2
+    m = ((2 * mu1 * mu2 + C1) * (2 * s12 + C2)) / ((mu1 * mu1 + mu2 * mu2 + C1) * (s11 + s22 + C2))
+    return m.mean()
+
+
+class Trainer:
+    """Holds the Gaussian parameters, Adam state and strategy statistics."""
+
+    LRS = {"means": 1.6e-4, "scales": 5e-3, "quats": 1e-3, "opacities": 5e-2,
+           "sh0": 2.5e-3, "shN": 2.5e-3 / 20}
+
+    def __init__(self, points, rgbs, viewmats, Ks, width, height, sh_degree=3, device="cuda",
+                 seed=42, world_size=1, rank=0, ssim_lambda=0.2, scene_scale=1.0):
+        g = torch.Generator().manual_seed(seed)  # identical on every rank (replicas)
+        N = points.shape[0]
+        self.device = device
+        self.width, self.height = width, height
+        self.sh_degree = sh_degree
+        self.ssim_lambda = ssim_lambda
+        self.world_size, self.rank = world_size, rank
+        # initial attributes as load_test_data(): scales U(0,0.02), unit quats,
+        # opacities U(0,1); colours from the SfM points as SH DC terms.
+        scales = torch.rand(N, 3, generator=g) * 0.02 + 1e-4
+        quats = F.normalize(torch.randn(N, 4, generator=g), dim=-1)
+        opac = torch.rand(N, generator=g).clamp(1e-3, 1 - 1e-3)
+        K = (sh_degree + 1) ** 2
+        sh = torch.zeros(N, K, 3)
+        sh[:, 0, :] = rgb_to_sh(rgbs)
+        sh[:, 1:, :] = torch.randn(N, K - 1, 3, generator=g) * 0.01
+        self.params = {
+            "means": points.clone(), "scales": torch.log(scales), "quats": quats,
+            "opacities": torch.logit(opac), "sh0": sh[:, :1].contiguous(),
+            "shN": sh[:, 1:].contiguous(),
+        }
+        self.params = {k: torch.nn.Parameter(v.to(device)) for k, v in self.params.items()}
+        BS = world_size  # batch 1 per rank (simple_trainer.py:261-277)
+        groups = [{"params": [p], "lr": self.LRS[k] * (scene_scale if k == "means" else 1.0)
+                   * math.sqrt(BS), "name": k} for k, p in self.params.items()]
+        kw = dict(eps=1e-15 / math.sqrt(BS), betas=(1 - BS * (1 - 0.9), 1 - BS * (1 - 0.999)))
+        try:
+            self.opt = torch.optim.Adam(groups, fused=True, **kw)
+        except (RuntimeError, TypeError):
+            self.opt = torch.optim.Adam(groups, foreach=True, **kw)
+        self.viewmats = viewmats.to(device)
+        self.Ks = Ks.to(device)
+        gt = torch.Generator().manual_seed(1234)
+        self.targets = torch.rand(len(viewmats), height, width, 3, generator=gt).to(device)
+        self.grad2d = torch.zeros(N, device=device)
+        self.count = torch.zeros(N, device=device)
+        self.window = _gauss_window(device=device)
+        self.last_meta = None
+
+    def camera_index(self, it: int) -> int:
+        return (it * self.world_size + self.rank) % len(self.viewmats)
+
+    def render(self, ci: int):
+        p = self.params
+        return rasterization(
+            p["means"], p["quats"], torch.exp(p["scales"]), torch.sigmoid(p["opacities"]),
+            torch.cat([p["sh0"], p["shN"]], 1), self.viewmats[ci:ci + 1], self.Ks[ci:ci + 1],
+            self.width, self.height, sh_degree=self.sh_degree, packed=False,
+            near_plane=0.01, far_plane=1e10, radius_clip=0.0, rasterize_mode="classic")
+
+    def step(self, it: int):
+        ci = self.camera_index(it)
+        colors, alphas, meta = self.render(ci)
+        meta["means2d"].retain_grad()  # DefaultStrategy.step_pre_backward
+        gt = self.targets[ci:ci + 1]
+        l1 = F.l1_loss(colors, gt)
+        ssim_loss = 1.0 - ssim(colors.permute(0, 3, 1, 2), gt.permute(0, 3, 1, 2), self.window)
+        loss = l1 * (1.0 - self.ssim_lambda) + ssim_loss * self.ssim_lambda
+        loss.backward()
+        if self.world_size > 1:
+            self.allreduce_grads()
+        self.update_state(meta)
+        self.opt.step()
+        self.opt.zero_grad(set_to_none=True)
+        self.last_meta = meta
+        return loss
+
+    def allreduce_grads(self):
+        """SUM the Gaussian gradients over ranks (RCCL over xGMI); issued
+        largest-first so the long shN transfer starts earliest."""
+        import torch.distributed as dist
+        works = []
+        for k in ("shN", "means", "quats", "scales", "sh0", "opacities"):
+            gr = self.params[k].grad
+            if gr is not None:
+                works.append(dist.all_reduce(gr, op=dist.ReduceOp.SUM, async_op=True))
+        for w in works:
+            w.wait()
+
+    @torch.no_grad()
+    def update_state(self, meta):
+        """DefaultStrategy._update_state for packed=False without the host
+        sync of torch.where (default.py:213-262): same sums, masked."""
+        g = meta["means2d"].grad
+        if g is None:
+            return
+        scale = torch.tensor([meta["width"] / 2.0 * meta["n_cameras"],
+                              meta["height"] / 2.0 * meta["n_cameras"]], device=g.device)
+        sel = (meta["radii"] > 0).float()  # [C, N]
+        self.grad2d += ((g * scale).norm(dim=-1) * sel).sum(0)
+        self.count += sel.sum(0)
+        # state["radii"] is only tracked when refine_scale2d_stop_iter > 0
+        # (default 0, default.py:90,255-262)

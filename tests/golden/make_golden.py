@@ -321,9 +321,23 @@ def gen_e2e():
         print(f"   {name} n_isects={len(meta['flatten_ids'])} {time.time()-t0:.1f}s")
 
 
+def gen_scene():
+    """Benchmark scene: assets/test_garden.npz cropped to [-2,2]^3 exactly as
+    load_test_data() does (gsplat/_helper.py:30-36) -- SfM points, colours and
+    the 3 cameras.  bench.py tiles it 3x3 (scene_grid=3) into M2."""
+    print("scene")
+    d = np.load(os.path.join(REF, "assets/test_garden.npz"))
+    means = d["means3d"].astype(np.float32)
+    sel = np.all((means >= -2) & (means <= 2), axis=-1)
+    np.savez_compressed(os.path.join(OUT, "garden_scene.npz"), means3d=means[sel],
+                        colors=d["colors"][sel], viewmats=d["viewmats"].astype(np.float32),
+                        Ks=d["Ks"].astype(np.float32), width=d["width"], height=d["height"])
+    print(f"  wrote garden_scene.npz ({int(sel.sum())} points)")
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["projection", "sh", "isect", "raster", "e2e"]
+    which = sys.argv[1:] or ["projection", "sh", "isect", "raster", "e2e", "scene"]
     torch.set_num_threads(8)
     for w in which:
         {"projection": gen_projection, "sh": gen_sh, "isect": gen_isect,
-         "raster": gen_raster, "e2e": gen_e2e}[w]()
+         "raster": gen_raster, "e2e": gen_e2e, "scene": gen_scene}[w]()
