@@ -293,9 +293,34 @@ inline bool supported_channels(int D) {
 
 }  // namespace gs
 
+namespace gs {
+int rasterize16_fwd(int C, int D, int W, int H, int tw, int th, const float *means2d,
+                    const float *conics, const float *colors, const float *opacities,
+                    const float *backgrounds, const uint8_t *masks, const int32_t *offsets,
+                    int64_t n_isects, const int32_t *flatten_ids, float *render_colors,
+                    float *render_alphas, int32_t *last_ids, hipStream_t st);
+int64_t rasterize16_bwd_workspace(int64_t G, int D, bool absgrad);
+int rasterize16_bwd(int C, int64_t G, int D, int W, int H, int tw, int th,
+                    const float *means2d, const float *conics, const float *colors,
+                    const float *opacities, const float *backgrounds, const uint8_t *masks,
+                    const int32_t *offsets, int64_t n_isects, const int32_t *flatten_ids,
+                    const float *render_alphas, const int32_t *last_ids,
+                    const float *v_render_colors, const float *v_render_alphas,
+                    float *v_means2d, float *v_conics, float *v_colors, float *v_opacities,
+                    float *v_abs, void *workspace, hipStream_t st);
+}  // namespace gs
+
 using namespace gs;
 
 extern "C" int gsplat_hip_rasterize_supported_channels(int D) { return supported_channels(D); }
+
+// 16x16 tiles (the gsplat default) run the wave-per-tile kernels of
+// rasterize16.hip; other tile sizes run the workgroup-per-tile kernels here.
+extern "C" int64_t gsplat_hip_rasterize_bwd_workspace_bytes(int64_t n_gaussians, int D,
+                                                            int tile_size, int absgrad) {
+  if (tile_size != 16 || !supported_channels(D)) return 0;
+  return rasterize16_bwd_workspace(n_gaussians, D, absgrad != 0);
+}
 
 static int check_common(int C, int D, int W, int H, int ts, int tw, int th) {
   GS_REQUIRE(supported_channels(D), "rasterize: unsupported channel count %d", D);
@@ -325,8 +350,12 @@ extern "C" int gsplat_hip_rasterize_fwd(int C, int D, int width, int height, int
   a.backgrounds = backgrounds; a.masks = masks; a.offsets = isect_offsets;
   a.flatten_ids = flatten_ids;
   a.render_colors = render_colors; a.render_alphas = render_alphas; a.last_ids = last_ids;
-  const int thr = block_threads(tile_size);
   hipStream_t st = (hipStream_t)stream;
+  if (tile_size == 16)
+    return rasterize16_fwd(C, D, width, height, tile_width, tile_height, means2d, conics, colors,
+                           opacities, backgrounds, masks, isect_offsets, n_isects, flatten_ids,
+                           render_colors, render_alphas, last_ids, st);
+  const int thr = block_threads(tile_size);
   switch (D) {
     case 1: return launch_fwd<1>(a, thr, st);
     case 2: return launch_fwd<2>(a, thr, st);
@@ -347,10 +376,22 @@ extern "C" int gsplat_hip_rasterize_bwd(
     const int32_t *isect_offsets, int64_t n_isects, const int32_t *flatten_ids,
     const float *render_alphas, const int32_t *last_ids, const float *v_render_colors,
     const float *v_render_alphas, float *v_means2d, float *v_conics, float *v_colors,
-    float *v_opacities, float *v_means2d_abs, void *stream) {
+    float *v_opacities, float *v_means2d_abs, void *workspace, int64_t workspace_bytes,
+    void *stream) {
   if (int e = check_common(C, D, width, height, tile_size, tile_width, tile_height)) return e;
   hipStream_t st = (hipStream_t)stream;
   const size_t G = (size_t)n_gaussians;
+  if (tile_size == 16) {
+    const int64_t need = rasterize16_bwd_workspace(n_gaussians, D, v_means2d_abs != nullptr);
+    GS_REQUIRE(workspace_bytes >= need && (need == 0 || workspace),
+               "rasterize_bwd: workspace of %lld bytes needed, %lld given", (long long)need,
+               (long long)workspace_bytes);
+    return rasterize16_bwd(C, n_gaussians, D, width, height, tile_width, tile_height, means2d,
+                           conics, colors, opacities, backgrounds, masks, isect_offsets,
+                           n_isects, flatten_ids, render_alphas, last_ids, v_render_colors,
+                           v_render_alphas, v_means2d, v_conics, v_colors, v_opacities,
+                           v_means2d_abs, workspace, st);
+  }
   GS_HIP(hipMemsetAsync(v_means2d, 0, sizeof(float) * 2 * G, st));
   GS_HIP(hipMemsetAsync(v_conics, 0, sizeof(float) * 3 * G, st));
   GS_HIP(hipMemsetAsync(v_colors, 0, sizeof(float) * D * G, st));

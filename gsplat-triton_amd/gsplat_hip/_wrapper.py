@@ -382,13 +382,17 @@ class _RasterizeToPixels(torch.autograd.Function):
         v_colors = torch.empty_like(colors)
         v_opacities = torch.empty_like(opacities)
         v_abs = torch.empty_like(means2d) if ctx.absgrad else None
+        wsb = int(_lib.query("gsplat_hip_rasterize_bwd_workspace_bytes", G, D, ctx.tile_size,
+                             int(bool(ctx.absgrad))))
+        ws = torch.empty(max(wsb, 4), dtype=torch.uint8, device=means2d.device)
         with _Timed("rasterize_bwd"):
             _lib.call("gsplat_hip_rasterize_bwd", C, G, D, ctx.width, ctx.height, ctx.tile_size,
                       tw, th, _ptr(means2d), _ptr(conics), _ptr(colors), _ptr(opacities),
                       _ptr(backgrounds), _ptr(m), _ptr(isect_offsets), flatten_ids.numel(),
                       _ptr(flatten_ids), _ptr(render_alphas), _ptr(last_ids),
                       _ptr(v_render_colors), _ptr(v_render_alphas), _ptr(v_means2d),
-                      _ptr(v_conics), _ptr(v_colors), _ptr(v_opacities), _ptr(v_abs), _stream())
+                      _ptr(v_conics), _ptr(v_colors), _ptr(v_opacities), _ptr(v_abs), _ptr(ws),
+                      wsb, _stream())
         if ctx.absgrad:
             ctx.means2d_in.absgrad = v_abs
         v_backgrounds = None

@@ -134,7 +134,12 @@ int gsplat_hip_rasterize_fwd(int C, int D, int width, int height, int tile_size,
 /* Replaces rasterize_to_pixels_bwd() (gsplat/triton_impl/rasterize_to_pixels_bwd.py:340-457)
  * called from _RasterizeToPixels.backward (_wrapper.py:104-182).
  * -> v_means2d[G,2], v_conics[G,3], v_colors[G,D], v_opacities[G],
- *    v_means2d_abs[G,2] or NULL (absgrad). */
+ *    v_means2d_abs[G,2] or NULL (absgrad).
+ * `workspace` must hold gsplat_hip_rasterize_bwd_workspace_bytes(G, D,
+ * tile_size, absgrad) bytes (the packed per-Gaussian gradient rows the 16x16
+ * kernel accumulates into; 0 bytes for other tile sizes). */
+int64_t gsplat_hip_rasterize_bwd_workspace_bytes(int64_t n_gaussians, int D, int tile_size,
+                                                 int absgrad);
 int gsplat_hip_rasterize_bwd(int C, int64_t n_gaussians, int D, int width, int height,
                              int tile_size, int tile_width, int tile_height,
                              const float *means2d, const float *conics, const float *colors,
@@ -144,7 +149,8 @@ int gsplat_hip_rasterize_bwd(int C, int64_t n_gaussians, int D, int width, int h
                              const float *render_alphas, const int32_t *last_ids,
                              const float *v_render_colors, const float *v_render_alphas,
                              float *v_means2d, float *v_conics, float *v_colors,
-                             float *v_opacities, float *v_means2d_abs, void *stream);
+                             float *v_opacities, float *v_means2d_abs, void *workspace,
+                             int64_t workspace_bytes, void *stream);
 
 #ifdef __cplusplus
 }
