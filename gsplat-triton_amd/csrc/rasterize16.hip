@@ -135,7 +135,7 @@ GS_INLINE bool stage_record(const Args &a, int64_t j, float x0, float x1, float 
   const float ms = rect_min_sigma(xy.x, xy.y, con.x, con.y, con.z, x0, x1, y0, y1);
   // keep iff some pixel can have opacity*exp(-sigma) >= 1/255 (margin 0.02
   // absorbs float rounding of the per-pixel sigma and __expf)
-  return ms <= __logf(255.f * con.w) + 0.02f;
+  return ms <= 0.69314718f * __builtin_amdgcn_logf(255.f * con.w) + 0.02f;
 }
 
 template <int D>
@@ -162,7 +162,7 @@ __global__ void __launch_bounds__(256) fwd_kernel(Args a) {
   const int64_t start = a.offsets[tile];
   const int64_t end = (tile == a.n_tiles - 1) ? a.n_isects : (int64_t)a.offsets[tile + 1];
 
-  float T[4] = {1.f, 1.f, 1.f, 1.f};
+  float T[4];
   float acc[4][D];
 #pragma unroll
   for (int p = 0; p < 4; ++p)
@@ -170,12 +170,13 @@ __global__ void __launch_bounds__(256) fwd_kernel(Args a) {
     for (int d = 0; d < D; ++d) acc[p][d] = 0.f;
   int32_t last[4] = {0, 0, 0, 0};
   const bool skip_tile = a.masks && a.masks[tile];
-  bool done[4];
+  // A terminated (or outside) pixel is encoded by a negative T: |T| is its
+  // final transmittance.  Keeps the per-pixel state in plain floats.
 #pragma unroll
-  for (int p = 0; p < 4; ++p) done[p] = !inside[p] || skip_tile;
+  for (int p = 0; p < 4; ++p) T[p] = (!inside[p] || skip_tile) ? -1.f : 1.f;
 
   for (int64_t b0 = start; b0 < end && !skip_tile; b0 += 64) {
-    const bool alive = !(done[0] && done[1] && done[2] && done[3]);
+    const bool alive = (T[0] > 0.f) | (T[1] > 0.f) | (T[2] > 0.f) | (T[3] > 0.f);
     if (__ballot(alive) == 0) break;
     const int64_t j = b0 + lane;
     float2 xy;
@@ -199,25 +200,34 @@ __global__ void __launch_bounds__(256) fwd_kernel(Args a) {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     for (int k = 0; k < cnt; ++k) {
+      // wave-uniform record (broadcast LDS reads)
       const float2 gxy = st.xy[k];
       const float4 cn = st.con[k];
+      const int32_t gidx = st.idx[k];
+      float gc[D];
+#pragma unroll
+      for (int d = 0; d < D; ++d) gc[d] = st.col[k][d];
+      // branch-free per pixel: every update is a select, so the four pixels
+      // of a lane cost straight-line VALU with no exec-mask juggling
 #pragma unroll
       for (int p = 0; p < 4; ++p) {
-        if (done[p]) continue;
         const float dx = gxy.x - fx[p], dy = gxy.y - fy[p];
         const float sigma = 0.5f * (cn.x * dx * dx + cn.z * dy * dy) + cn.y * dx * dy;
         const float alpha = fminf(kAlphaMax, cn.w * __expf(-sigma));
-        if (sigma < 0.f || alpha < kAlphaMin) continue;
-        const float nT = T[p] * (1.f - alpha);
-        if (nT <= kTMin) {
-          done[p] = true;
-          continue;
-        }
-        const float vis = alpha * T[p];
+        const float Tp = T[p];
+        const bool hit = (Tp > 0.f) & (sigma >= 0.f) & (alpha >= kAlphaMin);
+        const float nT = Tp * (1.f - alpha);
+        const bool term = hit & (nT <= kTMin);  // exclusive stop: not blended
+        const bool ok = hit & (nT > kTMin);
+        const float vis = ok ? alpha * Tp : 0.f;
 #pragma unroll
-        for (int d = 0; d < D; ++d) acc[p][d] += vis * st.col[k][d];
-        T[p] = nT;
-        last[p] = st.idx[k];
+        for (int d = 0; d < D; ++d) acc[p][d] += vis * gc[d];
+        T[p] = ok ? nT : (term ? -Tp : Tp);
+        last[p] = ok ? gidx : last[p];
+      }
+      if ((k & 15) == 15) {
+        const bool alive = (T[0] > 0.f) | (T[1] > 0.f) | (T[2] > 0.f) | (T[3] > 0.f);
+        if (__ballot(alive) == 0) break;
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -234,9 +244,9 @@ __global__ void __launch_bounds__(256) fwd_kernel(Args a) {
 #pragma unroll
     for (int d = 0; d < D; ++d) {
       const float bg = a.backgrounds ? a.backgrounds[c * D + d] : 0.f;
-      oc[d] = acc[p][d] + T[p] * bg;
+      oc[d] = acc[p][d] + fabsf(T[p]) * bg;
     }
-    a.render_alphas[pix] = 1.f - T[p];
+    a.render_alphas[pix] = 1.f - fabsf(T[p]);
     a.last_ids[pix] = last[p];
   }
 }
@@ -323,32 +333,37 @@ __global__ void __launch_bounds__(256) bwd_kernel(Args a) {
       float v[NV * 16];
 #pragma unroll
       for (int f = 0; f < NV * 16; ++f) v[f] = 0.f;
+      float gc[D];
+#pragma unroll
+      for (int d = 0; d < D; ++d) gc[d] = st.col[k][d];
       bool any = false;
+      // branch-free per pixel (selects instead of divergent `continue`s)
 #pragma unroll
       for (int p = 0; p < 4; ++p) {
         const float dx = gxy.x - fx[p], dy = gxy.y - fy[p];
         const float sigma = 0.5f * cn.x * dx * dx + 0.5f * cn.z * dy * dy + cn.y * dx * dy;
         const float ex = __expf(-sigma);
         const float alpha_raw = cn.w * ex;
-        if (!(idx <= mylast[p] && sigma >= 0.f && alpha_raw >= kAlphaMin)) continue;
-        any = true;
+        const bool valid = (idx <= mylast[p]) & (sigma >= 0.f) & (alpha_raw >= kAlphaMin);
+        any |= valid;
         const float alpha = fminf(kAlphaMax, alpha_raw);
-        const float ra = 1.f / (1.f - alpha);
-        T[p] *= ra;
-        const float w = alpha * T[p];
+        const float ra = __builtin_amdgcn_rcpf(1.f - alpha);
+        T[p] = valid ? T[p] * ra : T[p];
+        const float w = valid ? alpha * T[p] : 0.f;
         float gD = 0.f;
 #pragma unroll
         for (int d = 0; d < D; ++d) {
           v[d] += w * Drc[p][d];
-          gD += st.col[k][d] * Drc[p][d];
+          gD += gc[d] * Drc[p][d];
         }
         rD[p] += gD * w;
-        float Da = ra * (Tf[p] * Dra[p] + T[p] * gD - rD[p] - bgt[p]);
-        if (alpha_raw > kAlphaMax) Da = 0.f;
+        const float Da_raw = ra * (Tf[p] * Dra[p] + T[p] * gD - rD[p] - bgt[p]);
+        // clamped alpha (> 0.999) has no gradient (rasterize_to_pixels_bwd.py:184-187)
+        const float Da = (valid & (alpha_raw <= kAlphaMax)) ? Da_raw : 0.f;
         const float aD = alpha * Da;
         const float gmx = -aD * (cn.x * dx + cn.y * dy);
         const float gmy = -aD * (cn.y * dx + cn.z * dy);
-        v[D] += Da * ex;
+        v[D] += valid ? Da * ex : 0.f;
         v[D + 1] += gmx;
         v[D + 2] += gmy;
         v[D + 3] += -0.5f * aD * dx * dx;
