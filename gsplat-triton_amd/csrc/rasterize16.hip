@@ -22,6 +22,8 @@
 #include "common.h"
 #include "../../include/gsplat_hip.h"
 
+#include <stdlib.h>
+
 namespace gs {
 namespace r16 {
 
@@ -116,10 +118,34 @@ GS_INLINE float rect_min_sigma(float mx, float my, float a, float b, float c, fl
   return fmaxf(m, 0.f);
 }
 
-GS_INLINE int tile_of_wave(const Args &a) {
-  // 4 waves per workgroup handle 4 consecutive tiles
-  return blockIdx.x * 4 + (threadIdx.x >> 6);
-}
+// Geometry of one wave: PPL pixels per lane, WPT = 4 / PPL waves share a
+// tile, each owning a 16 x (4*PPL) strip; lane l owns column (l & 15) and
+// rows strip_y0 + PPL*(l >> 4) + p, p < PPL.
+template <int PPL>
+struct WaveGeom {
+  static constexpr int WPT = 4 / PPL;
+  static constexpr int SH = 4 * PPL;
+  int tile, c, tx, ty, strip;
+  int px, py0;  // this lane's column and first row
+  float x0, x1, y0, y1;  // strip rectangle of pixel centres
+
+  GS_INLINE WaveGeom(const Args &a, int lane) {
+    const int w = threadIdx.x >> 6;
+    tile = blockIdx.x * PPL + w / WPT;
+    strip = w % WPT;
+    const int ntile = a.tw * a.th;
+    c = tile / ntile;
+    const int rem = tile - c * ntile;
+    ty = rem / a.tw;
+    tx = rem - ty * a.tw;
+    px = tx * kTS + (lane & 15);
+    py0 = ty * kTS + SH * strip + PPL * (lane >> 4);
+    x0 = tx * kTS + 0.5f;
+    x1 = x0 + (kTS - 1);
+    y0 = ty * kTS + SH * strip + 0.5f;
+    y1 = y0 + (SH - 1);
+  }
+};
 
 template <int D>
 GS_INLINE bool stage_record(const Args &a, int64_t j, float x0, float x1, float y0, float y1,
@@ -138,46 +164,51 @@ GS_INLINE bool stage_record(const Args &a, int64_t j, float x0, float x1, float 
   return ms <= 0.69314718f * __builtin_amdgcn_logf(255.f * con.w) + 0.02f;
 }
 
-template <int D>
+template <int D, int PPL>
 __global__ void __launch_bounds__(256) fwd_kernel(Args a) {
   __shared__ WaveStage<D> stage_all[4];
   const int lane = threadIdx.x & 63;
   WaveStage<D> &st = stage_all[threadIdx.x >> 6];
-  const int tile = tile_of_wave(a);
-  if (tile >= a.n_tiles) return;
-  const int ntile = a.tw * a.th;
-  const int c = tile / ntile, rem = tile - c * ntile;
-  const int ty = rem / a.tw, tx = rem - ty * a.tw;
-  const int bx = tx * kTS + 2 * (lane & 7), by = ty * kTS + 2 * (lane >> 3);
-  float fx[4], fy[4];
-  bool inside[4];
+  const WaveGeom<PPL> geo(a, lane);
+  if (geo.tile >= a.n_tiles) return;
+  const int tile = geo.tile, c = geo.c;
+  const float x0 = geo.x0, x1 = geo.x1, y0 = geo.y0, y1 = geo.y1;
+  float fx[PPL], fy[PPL];
+  bool inside[PPL];
 #pragma unroll
-  for (int p = 0; p < 4; ++p) {
-    const int px = bx + (p & 1), py = by + (p >> 1);
+  for (int p = 0; p < PPL; ++p) {
+    const int px = geo.px, py = geo.py0 + p;
     inside[p] = px < a.W && py < a.H;
     fx[p] = (float)px + 0.5f;
     fy[p] = (float)py + 0.5f;
   }
-  const float x0 = tx * kTS + 0.5f, x1 = x0 + 15.f, y0 = ty * kTS + 0.5f, y1 = y0 + 15.f;
   const int64_t start = a.offsets[tile];
   const int64_t end = (tile == a.n_tiles - 1) ? a.n_isects : (int64_t)a.offsets[tile + 1];
 
-  float T[4];
-  float acc[4][D];
+  float T[PPL];
+  float acc[PPL][D];
 #pragma unroll
-  for (int p = 0; p < 4; ++p)
+  for (int p = 0; p < PPL; ++p)
 #pragma unroll
     for (int d = 0; d < D; ++d) acc[p][d] = 0.f;
-  int32_t last[4] = {0, 0, 0, 0};
+  int32_t last[PPL];
   const bool skip_tile = a.masks && a.masks[tile];
   // A terminated (or outside) pixel is encoded by a negative T: |T| is its
   // final transmittance.  Keeps the per-pixel state in plain floats.
 #pragma unroll
-  for (int p = 0; p < 4; ++p) T[p] = (!inside[p] || skip_tile) ? -1.f : 1.f;
+  for (int p = 0; p < PPL; ++p) {
+    T[p] = (!inside[p] || skip_tile) ? -1.f : 1.f;
+    last[p] = 0;
+  }
+  auto any_alive = [&]() {
+    bool al = false;
+#pragma unroll
+    for (int p = 0; p < PPL; ++p) al |= T[p] > 0.f;
+    return al;
+  };
 
   for (int64_t b0 = start; b0 < end && !skip_tile; b0 += 64) {
-    const bool alive = (T[0] > 0.f) | (T[1] > 0.f) | (T[2] > 0.f) | (T[3] > 0.f);
-    if (__ballot(alive) == 0) break;
+    if (__ballot(any_alive()) == 0) break;
     const int64_t j = b0 + lane;
     float2 xy;
     float4 con;
@@ -210,7 +241,7 @@ __global__ void __launch_bounds__(256) fwd_kernel(Args a) {
       // branch-free per pixel: every update is a select, so the four pixels
       // of a lane cost straight-line VALU with no exec-mask juggling
 #pragma unroll
-      for (int p = 0; p < 4; ++p) {
+      for (int p = 0; p < PPL; ++p) {
         const float dx = gxy.x - fx[p], dy = gxy.y - fy[p];
         const float sigma = 0.5f * (cn.x * dx * dx + cn.z * dy * dy) + cn.y * dx * dy;
         const float alpha = fminf(kAlphaMax, cn.w * __expf(-sigma));
@@ -225,10 +256,7 @@ __global__ void __launch_bounds__(256) fwd_kernel(Args a) {
         T[p] = ok ? nT : (term ? -Tp : Tp);
         last[p] = ok ? gidx : last[p];
       }
-      if ((k & 15) == 15) {
-        const bool alive = (T[0] > 0.f) | (T[1] > 0.f) | (T[2] > 0.f) | (T[3] > 0.f);
-        if (__ballot(alive) == 0) break;
-      }
+      if ((k & 15) == 15 && __ballot(any_alive()) == 0) break;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -236,10 +264,9 @@ __global__ void __launch_bounds__(256) fwd_kernel(Args a) {
   }
 
 #pragma unroll
-  for (int p = 0; p < 4; ++p) {
+  for (int p = 0; p < PPL; ++p) {
     if (!inside[p]) continue;
-    const int px = bx + (p & 1), py = by + (p >> 1);
-    const int64_t pix = ((int64_t)c * a.H + py) * a.W + px;
+    const int64_t pix = ((int64_t)c * a.H + geo.py0 + p) * a.W + geo.px;
     float *oc = a.render_colors + pix * D;
 #pragma unroll
     for (int d = 0; d < D; ++d) {
@@ -251,27 +278,24 @@ __global__ void __launch_bounds__(256) fwd_kernel(Args a) {
   }
 }
 
-template <int D, bool ABS>
+template <int D, bool ABS, int PPL>
 __global__ void __launch_bounds__(256) bwd_kernel(Args a) {
   constexpr int F = D + 6 + (ABS ? 2 : 0);
   constexpr int NV = (F + 15) / 16;
   __shared__ WaveStage<D> stage_all[4];
   const int lane = threadIdx.x & 63;
   WaveStage<D> &st = stage_all[threadIdx.x >> 6];
-  const int tile = tile_of_wave(a);
-  if (tile >= a.n_tiles) return;
+  const WaveGeom<PPL> geo(a, lane);
+  if (geo.tile >= a.n_tiles) return;
+  const int tile = geo.tile, c = geo.c;
   if (a.masks && a.masks[tile]) return;
-  const int ntile = a.tw * a.th;
-  const int c = tile / ntile, rem = tile - c * ntile;
-  const int ty = rem / a.tw, tx = rem - ty * a.tw;
-  const int bx = tx * kTS + 2 * (lane & 7), by = ty * kTS + 2 * (lane >> 3);
 
-  float fx[4], fy[4], T[4], Tf[4], Dra[4], rD[4], bgt[4], Drc[4][D];
-  int32_t mylast[4];
+  float fx[PPL], fy[PPL], T[PPL], Tf[PPL], Dra[PPL], rD[PPL], bgt[PPL], Drc[PPL][D];
+  int32_t mylast[PPL];
   int32_t lmax = -1;
 #pragma unroll
-  for (int p = 0; p < 4; ++p) {
-    const int px = bx + (p & 1), py = by + (p >> 1);
+  for (int p = 0; p < PPL; ++p) {
+    const int px = geo.px, py = geo.py0 + p;
     const bool in = px < a.W && py < a.H;
     fx[p] = (float)px + 0.5f;
     fy[p] = (float)py + 0.5f;
@@ -297,7 +321,7 @@ __global__ void __launch_bounds__(256) bwd_kernel(Args a) {
   }
 #pragma unroll
   for (int msk = 32; msk >= 1; msk >>= 1) lmax = max(lmax, __shfl_xor(lmax, msk, 64));
-  const float x0 = tx * kTS + 0.5f, x1 = x0 + 15.f, y0 = ty * kTS + 0.5f, y1 = y0 + 15.f;
+  const float x0 = geo.x0, x1 = geo.x1, y0 = geo.y0, y1 = geo.y1;
   const int64_t start = a.offsets[tile];
   const int64_t tend = (tile == a.n_tiles - 1) ? a.n_isects : (int64_t)a.offsets[tile + 1];
   const int64_t end = min(tend, (int64_t)lmax + 1);
@@ -339,7 +363,7 @@ __global__ void __launch_bounds__(256) bwd_kernel(Args a) {
       bool any = false;
       // branch-free per pixel (selects instead of divergent `continue`s)
 #pragma unroll
-      for (int p = 0; p < 4; ++p) {
+      for (int p = 0; p < PPL; ++p) {
         const float dx = gxy.x - fx[p], dy = gxy.y - fy[p];
         const float sigma = 0.5f * cn.x * dx * dx + 0.5f * cn.z * dy * dy + cn.y * dx * dy;
         const float ex = __expf(-sigma);
@@ -410,10 +434,23 @@ unpack_kernel(int64_t G, int S, const float *__restrict__ packed, float *__restr
 
 }  // namespace r16
 
+// pixels per lane (1: 4 waves per tile; 4: one wave per tile); GSPLAT_HIP_PPL
+// overrides it for experiments.
+static int ppl_choice(int dflt) {
+  static int v = [] {
+    const char *e = getenv("GSPLAT_HIP_PPL");
+    return e ? atoi(e) : 0;
+  }();
+  return (v == 1 || v == 2 || v == 4) ? v : dflt;
+}
+
 template <int D>
 int r16_fwd(const r16::Args &a, hipStream_t st) {
-  const int blocks = (a.n_tiles + 3) / 4;
-  hipLaunchKernelGGL(r16::fwd_kernel<D>, dim3(blocks), dim3(256), 0, st, a);
+  const int ppl = ppl_choice(1);
+  const int blocks = (a.n_tiles + ppl - 1) / ppl;
+  if (ppl == 1) hipLaunchKernelGGL((r16::fwd_kernel<D, 1>), dim3(blocks), dim3(256), 0, st, a);
+  else if (ppl == 2) hipLaunchKernelGGL((r16::fwd_kernel<D, 2>), dim3(blocks), dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((r16::fwd_kernel<D, 4>), dim3(blocks), dim3(256), 0, st, a);
   GS_CHECK_LAUNCH("rasterize_fwd16");
   return 0;
 }
@@ -426,8 +463,14 @@ int r16_bwd(r16::Args a, int64_t G, float *v_means2d, float *v_conics, float *v_
   a.packed = reinterpret_cast<float *>(workspace);
   GS_HIP(hipMemsetAsync(a.packed, 0, sizeof(float) * (size_t)a.S * G, st));
   if (a.n_isects > 0) {
-    const int blocks = (a.n_tiles + 3) / 4;
-    hipLaunchKernelGGL((r16::bwd_kernel<D, ABS>), dim3(blocks), dim3(256), 0, st, a);
+    const int ppl = ppl_choice(1);
+    const int blocks = (a.n_tiles + ppl - 1) / ppl;
+    if (ppl == 1)
+      hipLaunchKernelGGL((r16::bwd_kernel<D, ABS, 1>), dim3(blocks), dim3(256), 0, st, a);
+    else if (ppl == 2)
+      hipLaunchKernelGGL((r16::bwd_kernel<D, ABS, 2>), dim3(blocks), dim3(256), 0, st, a);
+    else
+      hipLaunchKernelGGL((r16::bwd_kernel<D, ABS, 4>), dim3(blocks), dim3(256), 0, st, a);
     GS_CHECK_LAUNCH("rasterize_bwd16");
   }
   if (G > 0) {
