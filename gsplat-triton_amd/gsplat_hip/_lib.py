@@ -43,6 +43,10 @@ _SIGS = {
     "gsplat_hip_rasterize_bwd": (_i32, [_i32, _i64, _i32, _i32, _i32, _i32, _i32, _i32, _p, _p,
                                         _p, _p, _p, _p, _p, _i64, _p, _p, _p, _p, _p, _p, _p,
                                         _p, _p, _p, _p, _i64, _p]),
+    "gsplat_hip_ssim_workspace_bytes": (_i64, [_i32, _i32, _i32, _i32]),
+    "gsplat_hip_ssim_l1_fwd": (_i32, [_i32, _i32, _i32, _i32, _p, _p, _p, _p, _p]),
+    "gsplat_hip_ssim_l1_bwd": (_i32, [_i32, _i32, _i32, _i32, _p, _p, _p, _p, _p, _p]),
+    "gsplat_hip_adam_step": (_i32, [_i32, _p, _p, _p, _p, _p, _p, _f, _f, _f, _i32, _p]),
 }
 
 EXPORTED = tuple(_SIGS)

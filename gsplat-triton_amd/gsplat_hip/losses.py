@@ -1,0 +1,90 @@
+"""Fused photometric loss and multi-tensor Adam for the training step.
+
+`l1_ssim_loss` = (1 - lam) * mean|render - gt| + lam * (1 - SSIM_valid),
+the loss of examples/simple_trainer.py:642-646 with fused_ssim
+(rahul-goel/fused-ssim, padding="valid") restated in HIP (csrc/ssim.hip).
+`FusedAdam` applies torch.optim.Adam's update to all Gaussian parameter
+groups in one kernel (csrc/adam.hip).
+"""
+
+import ctypes
+import math
+
+import torch
+
+from . import _lib
+from ._wrapper import _ptr, _stream
+
+
+class _L1SSIM(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, img, gt):
+        assert img.dim() == 4 and img.shape == gt.shape, (img.shape, gt.shape)
+        img = img.contiguous().float()
+        gt = gt.contiguous().float()
+        B, H, W, C = img.shape
+        ws = torch.empty(max(int(_lib.query("gsplat_hip_ssim_workspace_bytes", B, H, W, C)), 4),
+                         dtype=torch.uint8, device=img.device)
+        sums = torch.empty(2, device=img.device)
+        _lib.call("gsplat_hip_ssim_l1_fwd", B, H, W, C, _ptr(img), _ptr(gt), _ptr(sums),
+                  _ptr(ws), _stream())
+        ctx.save_for_backward(img, gt, ws)
+        n_map = B * C * (H - 10) * (W - 10)
+        n_img = B * C * H * W
+        return sums[0] / n_map, sums[1] / n_img  # mean SSIM, mean L1
+
+    @staticmethod
+    def backward(ctx, g_ssim, g_l1):
+        img, gt, ws = ctx.saved_tensors
+        B, H, W, C = img.shape
+        dloss = torch.stack([g_ssim.reshape(()), g_l1.reshape(())]).float().contiguous()
+        grad = torch.empty_like(img)
+        _lib.call("gsplat_hip_ssim_l1_bwd", B, H, W, C, _ptr(img), _ptr(gt), _ptr(ws),
+                  _ptr(dloss), _ptr(grad), _stream())
+        return grad, None
+
+
+def ssim_and_l1(img, gt):
+    """(mean SSIM over the valid region, mean L1) of [B,H,W,C] images."""
+    return _L1SSIM.apply(img, gt)
+
+
+def l1_ssim_loss(img, gt, ssim_lambda=0.2):
+    s, l1 = _L1SSIM.apply(img, gt)
+    return l1 * (1.0 - ssim_lambda) + (1.0 - s) * ssim_lambda
+
+
+class FusedAdam:
+    """torch.optim.Adam semantics (per-group lr, shared betas/eps) in one launch."""
+
+    def __init__(self, params, lrs, betas=(0.9, 0.999), eps=1e-8):
+        self.params = list(params)
+        self.lrs = [float(x) for x in lrs]
+        self.betas, self.eps = betas, eps
+        self.exp_avg = [torch.zeros_like(p) for p in self.params]
+        self.exp_avg_sq = [torch.zeros_like(p) for p in self.params]
+        self.step_count = 0
+        n = len(self.params)
+        self._numels = (ctypes.c_int64 * n)(*[p.numel() for p in self.params])
+        self._lrs = (ctypes.c_float * n)(*self.lrs)
+        for p in self.params:
+            assert p.is_contiguous() and p.dtype == torch.float32
+
+    @torch.no_grad()
+    def step(self):
+        self.step_count += 1
+        n = len(self.params)
+        P = ctypes.c_void_p * n
+        grads = [p.grad for p in self.params]
+        for gr in grads:
+            assert gr is None or gr.is_contiguous()
+        _lib.call("gsplat_hip_adam_step", n, P(*[p.data_ptr() for p in self.params]),
+                  P(*[0 if g is None else g.data_ptr() for g in grads]),
+                  P(*[m.data_ptr() for m in self.exp_avg]),
+                  P(*[v.data_ptr() for v in self.exp_avg_sq]), self._numels, self._lrs,
+                  float(self.betas[0]), float(self.betas[1]), float(self.eps), self.step_count,
+                  _stream())
+
+    def zero_grad(self, set_to_none=True):
+        for p in self.params:
+            p.grad = None

@@ -20,6 +20,7 @@ import numpy as np
 import torch
 import torch.nn.functional as F
 
+from .losses import FusedAdam, l1_ssim_loss
 from .rendering import rasterization
 
 C0 = 0.28209479177387814
@@ -95,7 +96,8 @@ class Trainer:
            "sh0": 2.5e-3, "shN": 2.5e-3 / 20}
 
     def __init__(self, points, rgbs, viewmats, Ks, width, height, sh_degree=3, device="cuda",
-                 seed=42, world_size=1, rank=0, ssim_lambda=0.2, scene_scale=1.0):
+                 seed=42, world_size=1, rank=0, ssim_lambda=0.2, scene_scale=1.0,
+                 fused=True):
         g = torch.Generator().manual_seed(seed)  # identical on every rank (replicas)
         N = points.shape[0]
         self.device = device
@@ -122,9 +124,10 @@ class Trainer:
         groups = [{"params": [p], "lr": self.LRS[k] * (scene_scale if k == "means" else 1.0)
                    * math.sqrt(BS), "name": k} for k, p in self.params.items()]
         kw = dict(eps=1e-15 / math.sqrt(BS), betas=(1 - BS * (1 - 0.9), 1 - BS * (1 - 0.999)))
-        try:
-            self.opt = torch.optim.Adam(groups, fused=True, **kw)
-        except (RuntimeError, TypeError):
+        self.fused = fused
+        if fused:  # HIP loss + one-launch Adam (csrc/ssim.hip, csrc/adam.hip)
+            self.opt = FusedAdam([g["params"][0] for g in groups], [g["lr"] for g in groups], **kw)
+        else:  # torch reference path (conv SSIM, torch.optim.Adam)
             self.opt = torch.optim.Adam(groups, foreach=True, **kw)
         self.viewmats = viewmats.to(device)
         self.Ks = Ks.to(device)
@@ -151,9 +154,13 @@ class Trainer:
         colors, alphas, meta = self.render(ci)
         meta["means2d"].retain_grad()  # DefaultStrategy.step_pre_backward
         gt = self.targets[ci:ci + 1]
-        l1 = F.l1_loss(colors, gt)
-        ssim_loss = 1.0 - ssim(colors.permute(0, 3, 1, 2), gt.permute(0, 3, 1, 2), self.window)
-        loss = l1 * (1.0 - self.ssim_lambda) + ssim_loss * self.ssim_lambda
+        if self.fused:
+            loss = l1_ssim_loss(colors, gt, self.ssim_lambda)
+        else:
+            l1 = F.l1_loss(colors, gt)
+            ssim_loss = 1.0 - ssim(colors.permute(0, 3, 1, 2), gt.permute(0, 3, 1, 2),
+                                   self.window)
+            loss = l1 * (1.0 - self.ssim_lambda) + ssim_loss * self.ssim_lambda
         loss.backward()
         if self.world_size > 1:
             self.allreduce_grads()

@@ -152,6 +152,32 @@ int gsplat_hip_rasterize_bwd(int C, int64_t n_gaussians, int D, int width, int h
                              float *v_opacities, float *v_means2d_abs, void *workspace,
                              int64_t workspace_bytes, void *stream);
 
+/* ---------------------------------------------------------------------------
+ * Trainer-side kernels of the training step (not part of the 5-function
+ * backend surface; used by gsplat_hip.train_step).
+ *
+ * Photometric loss terms of examples/simple_trainer.py:642-646:
+ * fused_ssim(render, gt, padding="valid") (rahul-goel/fused-ssim@1272e21a,
+ * examples/requirements.txt:22) and the L1 term.  Images [B,H,W,C] fp32.
+ * fwd: sums[0] = sum of the SSIM map over the valid region, sums[1] = sum |img1-img2|
+ *      (device floats, zeroed by the call); workspace = per-pixel partials.
+ * bwd: grad_img1 = dloss[0]/n_map * dSSIMsum + dloss[1]/n_img * sign(img1-img2)
+ *      where dloss (device, [2]) = dL/d(mean SSIM), dL/d(mean L1). */
+int64_t gsplat_hip_ssim_workspace_bytes(int B, int H, int W, int C);
+int gsplat_hip_ssim_l1_fwd(int B, int H, int W, int C, const float *img1, const float *img2,
+                           float *sums, void *workspace, void *stream);
+int gsplat_hip_ssim_l1_bwd(int B, int H, int W, int C, const float *img1, const float *img2,
+                           const void *workspace, const float *dloss, float *grad_img1,
+                           void *stream);
+
+/* One torch.optim.Adam step (amsgrad=False, no weight decay) over up to 8
+ * parameter groups in a single launch (replaces the per-group optimizers of
+ * examples/simple_trainer.py:265-276).  Host arrays of length n_groups. */
+int gsplat_hip_adam_step(int n_groups, float *const *params, const float *const *grads,
+                         float *const *exp_avgs, float *const *exp_avg_sqs,
+                         const int64_t *numels, const float *lrs, float beta1, float beta2,
+                         float eps, int step, void *stream);
+
 #ifdef __cplusplus
 }
 #endif
