@@ -3,8 +3,9 @@
 // The reference trainer steps six torch.optim.Adam instances, one per
 // parameter group (examples/simple_trainer.py:235-277).  This kernel applies
 // the identical update (torch.optim.Adam, amsgrad=False, weight_decay=0,
-// bias-corrected, exp_avg via lerp) to every group in one grid-stride launch:
-// HBM-bound, 28 B per element (p, g, m, v read; p, m, v written).
+// bias-corrected, exp_avg via lerp) to every group in one grid-stride launch.
+// HBM-bound: 28 B per element (p, g, m, v read; p, m, v written), moved as
+// 16-B vectors (4 elements per lane-iteration, scalar tail per group).
 #include "common.h"
 #include "../../include/gsplat_hip.h"
 
@@ -18,28 +19,53 @@ struct Groups {
   const float *grad[kMaxGroups];
   float *m[kMaxGroups];
   float *v[kMaxGroups];
-  int64_t begin[kMaxGroups + 1];  // prefix offsets over the flattened groups
+  int64_t numel[kMaxGroups];
+  int64_t begin[kMaxGroups + 1];  // prefix offsets in 4-element slots
   float step_size[kMaxGroups];    // lr / (1 - beta1^t)
   float inv_bc2_sqrt[kMaxGroups]; // 1 / sqrt(1 - beta2^t)
   int n;
 };
+
+GS_INLINE void upd(float &p, float gr, float &m, float &v, float b1, float b2, float eps,
+                   float ss, float ib) {
+  m = m + (1.f - b1) * (gr - m);  // lerp(m, g, 1 - beta1)
+  v = b2 * v + (1.f - b2) * gr * gr;
+  p -= ss * m / (sqrtf(v) * ib + eps);
+}
 
 __global__ void __launch_bounds__(256)
 step_kernel(Groups g, float beta1, float beta2, float eps) {
   const int64_t total = g.begin[g.n];
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   int grp = 0;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
-    while (i >= g.begin[grp + 1]) ++grp;
-    const int64_t k = i - g.begin[grp];
-    const float gr = g.grad[grp] ? g.grad[grp][k] : 0.f;
-    float m = g.m[grp][k], v = g.v[grp][k];
-    m = m + (1.f - beta1) * (gr - m);  // lerp(m, g, 1 - beta1)
-    v = beta2 * v + (1.f - beta2) * gr * gr;
-    const float denom = sqrtf(v) * g.inv_bc2_sqrt[grp] + eps;
-    g.param[grp][k] -= g.step_size[grp] * m / denom;
-    g.m[grp][k] = m;
-    g.v[grp][k] = v;
+  for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < total; s += stride) {
+    while (s >= g.begin[grp + 1]) ++grp;
+    const int64_t k0 = 4 * (s - g.begin[grp]);
+    const float ss = g.step_size[grp], ib = g.inv_bc2_sqrt[grp];
+    float *P = g.param[grp];
+    const float *G = g.grad[grp];
+    float *M = g.m[grp], *V = g.v[grp];
+    if (k0 + 4 <= g.numel[grp]) {
+      float4 p = *reinterpret_cast<float4 *>(P + k0);
+      const float4 gr = G ? *reinterpret_cast<const float4 *>(G + k0) : make_float4(0, 0, 0, 0);
+      float4 m = *reinterpret_cast<float4 *>(M + k0);
+      float4 v = *reinterpret_cast<float4 *>(V + k0);
+      upd(p.x, gr.x, m.x, v.x, beta1, beta2, eps, ss, ib);
+      upd(p.y, gr.y, m.y, v.y, beta1, beta2, eps, ss, ib);
+      upd(p.z, gr.z, m.z, v.z, beta1, beta2, eps, ss, ib);
+      upd(p.w, gr.w, m.w, v.w, beta1, beta2, eps, ss, ib);
+      *reinterpret_cast<float4 *>(P + k0) = p;
+      *reinterpret_cast<float4 *>(M + k0) = m;
+      *reinterpret_cast<float4 *>(V + k0) = v;
+    } else {
+      for (int64_t k = k0; k < g.numel[grp]; ++k) {
+        float p = P[k], m = M[k], v = V[k];
+        upd(p, G ? G[k] : 0.f, m, v, beta1, beta2, eps, ss, ib);
+        P[k] = p;
+        M[k] = m;
+        V[k] = v;
+      }
+    }
   }
 }
 
@@ -49,8 +75,8 @@ step_kernel(Groups g, float beta1, float beta2, float eps) {
 using namespace gs;
 
 // One Adam step over n_groups parameter groups.  Arrays are host arrays of
-// length n_groups; grads[i] may be NULL (treated as zero, as for a parameter
-// that received no gradient but is still stepped).  `step` is the 1-based step.
+// length n_groups; grads[i] may be NULL (treated as zero).  Every pointer must
+// be 16-B aligned.  `step` is the 1-based step count.
 extern "C" int gsplat_hip_adam_step(int n_groups, float *const *params, const float *const *grads,
                                     float *const *exp_avgs, float *const *exp_avg_sqs,
                                     const int64_t *numels, const float *lrs, float beta1,
@@ -63,11 +89,15 @@ extern "C" int gsplat_hip_adam_step(int n_groups, float *const *params, const fl
   g.begin[0] = 0;
   const double bc1 = 1.0 - pow((double)beta1, step), bc2 = 1.0 - pow((double)beta2, step);
   for (int i = 0; i < n_groups; ++i) {
+    const uintptr_t al = (uintptr_t)params[i] | (uintptr_t)grads[i] | (uintptr_t)exp_avgs[i] |
+                         (uintptr_t)exp_avg_sqs[i];
+    GS_REQUIRE((al & 15) == 0, "adam: group %d pointers must be 16-B aligned", i);
     g.param[i] = params[i];
     g.grad[i] = grads[i];
     g.m[i] = exp_avgs[i];
     g.v[i] = exp_avg_sqs[i];
-    g.begin[i + 1] = g.begin[i] + numels[i];
+    g.numel[i] = numels[i];
+    g.begin[i + 1] = g.begin[i] + (numels[i] + 3) / 4;
     g.step_size[i] = (float)(lrs[i] / bc1);
     g.inv_bc2_sqrt[i] = (float)(1.0 / sqrt(bc2));
   }

@@ -99,10 +99,22 @@ GS_INLINE void sh_basis(float x, float y, float z, float *B, float (*dB)[3]) {
   }
 }
 
+// Coefficient addressing: basis 0 (the DC term) lives at c0 + row*s0, bases
+// k >= 1 at cr + row*sr + 3*(k-1).  One [rows,K,3] tensor is c0 = coeffs,
+// cr = coeffs + 3, s0 = sr = 3K; the trainer's separate sh0 [N,1,3] / shN
+// [N,K-1,3] parameters are read in place (no torch.cat copy per step).
+struct Coeffs {
+  const float *c0, *cr;
+  int64_t s0, sr;
+};
+struct VCoeffs {
+  float *c0, *cr;
+  int64_t s0, sr;
+};
+
 template <int DEG>
 __global__ void __launch_bounds__(256)
-sh_fwd_kernel(int64_t n, int K, int64_t n_coeff_rows,
-              const float *__restrict__ dirs, const float *__restrict__ coeffs,
+sh_fwd_kernel(int64_t n, int64_t n_coeff_rows, Coeffs cf, const float *__restrict__ dirs,
               const uint8_t *__restrict__ masks, float *__restrict__ colors) {
   constexpr int NB = (DEG + 1) * (DEG + 1);
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -121,29 +133,33 @@ sh_fwd_kernel(int64_t n, int K, int64_t n_coeff_rows,
   }
   float B[NB];
   sh_basis<DEG, false>(x, y, z, B, nullptr);
-  const float *cf = coeffs + (i % n_coeff_rows) * (int64_t)K * 3;
-  float r = 0.f, g = 0.f, b = 0.f;
+  const int64_t row = i % n_coeff_rows;
+  const float *p0 = cf.c0 + row * cf.s0;
+  const float *pr = cf.cr + row * cf.sr;
+  float r = B[0] * p0[0], g = B[0] * p0[1], b = B[0] * p0[2];
 #pragma unroll
-  for (int k = 0; k < NB; ++k) {
-    r += B[k] * cf[3 * k];
-    g += B[k] * cf[3 * k + 1];
-    b += B[k] * cf[3 * k + 2];
+  for (int k = 1; k < NB; ++k) {
+    r += B[k] * pr[3 * (k - 1)];
+    g += B[k] * pr[3 * (k - 1) + 1];
+    b += B[k] * pr[3 * (k - 1) + 2];
   }
   o[0] = r; o[1] = g; o[2] = b;
 }
 
 template <int DEG>
 __global__ void __launch_bounds__(256)
-sh_bwd_kernel(int64_t n, int K, int64_t n_coeff_rows, const float *__restrict__ dirs, const float *__restrict__ coeffs,
-              const uint8_t *__restrict__ masks, const float *__restrict__ v_colors,
-              float *__restrict__ v_coeffs, float *__restrict__ v_dirs) {
+sh_bwd_kernel(int64_t n, int K, int64_t n_coeff_rows, Coeffs cf, const float *__restrict__ dirs,
+              const uint8_t *__restrict__ masks, const float *__restrict__ v_colors, VCoeffs vc,
+              float *__restrict__ v_dirs) {
   constexpr int NB = (DEG + 1) * (DEG + 1);
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  float *vc = v_coeffs + i * (int64_t)K * 3;
+  float *v0 = vc.c0 + i * vc.s0;
+  float *vr_ = vc.cr + i * vc.sr;
   const bool on = !masks || masks[i];
   if (!on) {
-    for (int k = 0; k < 3 * K; ++k) vc[k] = 0.f;
+    v0[0] = 0.f; v0[1] = 0.f; v0[2] = 0.f;
+    for (int k = 0; k < 3 * (K - 1); ++k) vr_[k] = 0.f;
     if (v_dirs) { v_dirs[3 * i] = 0.f; v_dirs[3 * i + 1] = 0.f; v_dirs[3 * i + 2] = 0.f; }
     return;
   }
@@ -160,23 +176,24 @@ sh_bwd_kernel(int64_t n, int K, int64_t n_coeff_rows, const float *__restrict__ 
   const bool want_dirs = (v_dirs != nullptr) && DEG > 0;
   if (want_dirs) sh_basis<DEG, true>(x, y, z, B, dB);
   else sh_basis<DEG, false>(x, y, z, B, nullptr);
+  v0[0] = B[0] * vr; v0[1] = B[0] * vg; v0[2] = B[0] * vb;
 #pragma unroll
-  for (int k = 0; k < NB; ++k) {
-    vc[3 * k] = B[k] * vr;
-    vc[3 * k + 1] = B[k] * vg;
-    vc[3 * k + 2] = B[k] * vb;
+  for (int k = 1; k < NB; ++k) {
+    vr_[3 * (k - 1)] = B[k] * vr;
+    vr_[3 * (k - 1) + 1] = B[k] * vg;
+    vr_[3 * (k - 1) + 2] = B[k] * vb;
   }
-  for (int k = 3 * NB; k < 3 * K; ++k) vc[k] = 0.f;
+  for (int k = 3 * (NB - 1); k < 3 * (K - 1); ++k) vr_[k] = 0.f;
   if (v_dirs) {
     if (DEG == 0) {
       v_dirs[3 * i] = 0.f; v_dirs[3 * i + 1] = 0.f; v_dirs[3 * i + 2] = 0.f;
       return;
     }
-    const float *cf = coeffs + (i % n_coeff_rows) * (int64_t)K * 3;
+    const float *pr = cf.cr + (i % n_coeff_rows) * cf.sr;
     float vx = 0.f, vy = 0.f, vz = 0.f;
 #pragma unroll
     for (int k = 1; k < NB; ++k) {
-      const float w = cf[3 * k] * vr + cf[3 * k + 1] * vg + cf[3 * k + 2] * vb;
+      const float w = pr[3 * (k - 1)] * vr + pr[3 * (k - 1) + 1] * vg + pr[3 * (k - 1) + 2] * vb;
       vx += dB[k][0] * w;
       vy += dB[k][1] * w;
       vz += dB[k][2] * w;
@@ -193,24 +210,30 @@ sh_bwd_kernel(int64_t n, int K, int64_t n_coeff_rows, const float *__restrict__ 
 
 using namespace gs;
 
-// coeffs: [n_coeff_rows, K, 3]; row i of dirs/colors uses coefficient row
-// i % n_coeff_rows, so a [N,K,3] tensor broadcast over C cameras is read in
-// place (n_coeff_rows = N) instead of being materialised as [C,N,K,3].
-extern "C" int gsplat_hip_sh_fwd(int degree, int64_t n, int64_t n_coeff_rows, int K, const float *dirs,
-                                 const float *coeffs, const uint8_t *masks, float *colors,
+static int sh_check(int degree, int64_t n, int64_t n_coeff_rows, int K, const char *who) {
+  GS_REQUIRE(degree >= 0 && degree <= 4, "%s: degree %d not in [0, 4]", who, degree);
+  GS_REQUIRE(K >= (degree + 1) * (degree + 1) && K <= 25, "%s: K=%d too small for degree %d",
+             who, K, degree);
+  GS_REQUIRE(n_coeff_rows > 0 && n % n_coeff_rows == 0,
+             "%s: n=%lld not a multiple of n_coeff_rows=%lld", who, (long long)n,
+             (long long)n_coeff_rows);
+  return 0;
+}
+
+extern "C" int gsplat_hip_sh_fwd(int degree, int64_t n, int64_t n_coeff_rows, int K,
+                                 const float *dirs, const float *coeffs,
+                                 const float *coeffs_rest, const uint8_t *masks, float *colors,
                                  void *stream) {
-  GS_REQUIRE(degree >= 0 && degree <= 4, "sh_fwd: degree %d not in [0, 4]", degree);
-  GS_REQUIRE(K >= (degree + 1) * (degree + 1) && K <= 25, "sh_fwd: K=%d too small for degree %d",
-             K, degree);
   if (n <= 0) return 0;
-  GS_REQUIRE(n_coeff_rows > 0 && n % n_coeff_rows == 0, "sh: n=%lld not a multiple of n_coeff_rows=%lld",
-             (long long)n, (long long)n_coeff_rows);
+  if (int e = sh_check(degree, n, n_coeff_rows, K, "sh_fwd")) return e;
+  Coeffs cf = coeffs_rest ? Coeffs{coeffs, coeffs_rest, 3, 3 * (int64_t)(K - 1)}
+                          : Coeffs{coeffs, coeffs + 3, 3 * (int64_t)K, 3 * (int64_t)K};
   dim3 grid((unsigned)((n + 255) / 256));
   hipStream_t st = (hipStream_t)stream;
-#define GS_SH_FWD(D)                                                                        \
-  case D:                                                                                   \
-    hipLaunchKernelGGL(sh_fwd_kernel<D>, grid, dim3(256), 0, st, n, K, n_coeff_rows, dirs, \
-                       coeffs, masks, colors);                                              \
+#define GS_SH_FWD(D)                                                                   \
+  case D:                                                                              \
+    hipLaunchKernelGGL(sh_fwd_kernel<D>, grid, dim3(256), 0, st, n, n_coeff_rows, cf, \
+                       dirs, masks, colors);                                           \
     break;
   switch (degree) { GS_SH_FWD(0) GS_SH_FWD(1) GS_SH_FWD(2) GS_SH_FWD(3) GS_SH_FWD(4) }
 #undef GS_SH_FWD
@@ -218,22 +241,25 @@ extern "C" int gsplat_hip_sh_fwd(int degree, int64_t n, int64_t n_coeff_rows, in
   return 0;
 }
 
-extern "C" int gsplat_hip_sh_bwd(int degree, int64_t n, int64_t n_coeff_rows, int K, const float *dirs,
-                                 const float *coeffs, const uint8_t *masks,
-                                 const float *v_colors, float *v_coeffs, float *v_dirs,
-                                 void *stream) {
-  GS_REQUIRE(degree >= 0 && degree <= 4, "sh_bwd: degree %d not in [0, 4]", degree);
-  GS_REQUIRE(K >= (degree + 1) * (degree + 1) && K <= 25, "sh_bwd: K=%d too small for degree %d",
-             K, degree);
+extern "C" int gsplat_hip_sh_bwd(int degree, int64_t n, int64_t n_coeff_rows, int K,
+                                 const float *dirs, const float *coeffs,
+                                 const float *coeffs_rest, const uint8_t *masks,
+                                 const float *v_colors, float *v_coeffs, float *v_coeffs_rest,
+                                 float *v_dirs, void *stream) {
   if (n <= 0) return 0;
-  GS_REQUIRE(n_coeff_rows > 0 && n % n_coeff_rows == 0, "sh: n=%lld not a multiple of n_coeff_rows=%lld",
-             (long long)n, (long long)n_coeff_rows);
+  if (int e = sh_check(degree, n, n_coeff_rows, K, "sh_bwd")) return e;
+  GS_REQUIRE(!coeffs_rest == !v_coeffs_rest,
+             "sh_bwd: coeffs_rest and v_coeffs_rest must both be given or both null");
+  Coeffs cf = coeffs_rest ? Coeffs{coeffs, coeffs_rest, 3, 3 * (int64_t)(K - 1)}
+                          : Coeffs{coeffs, coeffs + 3, 3 * (int64_t)K, 3 * (int64_t)K};
+  VCoeffs vc = v_coeffs_rest ? VCoeffs{v_coeffs, v_coeffs_rest, 3, 3 * (int64_t)(K - 1)}
+                             : VCoeffs{v_coeffs, v_coeffs + 3, 3 * (int64_t)K, 3 * (int64_t)K};
   dim3 grid((unsigned)((n + 255) / 256));
   hipStream_t st = (hipStream_t)stream;
-#define GS_SH_BWD(D)                                                                     \
-  case D:                                                                                \
-    hipLaunchKernelGGL(sh_bwd_kernel<D>, grid, dim3(256), 0, st, n, K, n_coeff_rows, dirs, coeffs, \
-                       masks, v_colors, v_coeffs, v_dirs);                               \
+#define GS_SH_BWD(D)                                                                       \
+  case D:                                                                                  \
+    hipLaunchKernelGGL(sh_bwd_kernel<D>, grid, dim3(256), 0, st, n, K, n_coeff_rows, cf,  \
+                       dirs, masks, v_colors, vc, v_dirs);                                 \
     break;
   switch (degree) { GS_SH_BWD(0) GS_SH_BWD(1) GS_SH_BWD(2) GS_SH_BWD(3) GS_SH_BWD(4) }
 #undef GS_SH_BWD

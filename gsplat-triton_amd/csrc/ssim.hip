@@ -30,7 +30,7 @@ constexpr float C1 = 0.01f * 0.01f, C2 = 0.03f * 0.03f;
 // maps: [B][C][3][Hm][Wm]
 __global__ void __launch_bounds__(256)
 fwd_kernel(int B, int H, int W, int C, const float *__restrict__ x, const float *__restrict__ y,
-           float *__restrict__ maps, float *__restrict__ sums) {
+           float *__restrict__ maps, float *__restrict__ partials) {
   __shared__ float sx[WIN][WIN], sy[WIN][WIN];
   __shared__ float h[5][WIN][TS];
   __shared__ float red[2][4];
@@ -120,9 +120,33 @@ fwd_kernel(int B, int H, int W, int C, const float *__restrict__ x, const float 
     red[1][tid >> 6] = lsum;
   }
   __syncthreads();
-  if (tid == 0) {
-    atomic_add_f32(sums, red[0][0] + red[0][1] + red[0][2] + red[0][3]);
-    atomic_add_f32(sums + 1, red[1][0] + red[1][1] + red[1][2] + red[1][3]);
+  if (tid == 0) {  // per-workgroup partials (no same-address atomics)
+    const int blk = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+    partials[2 * blk] = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+    partials[2 * blk + 1] = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+  }
+}
+
+// Deterministic sum of the per-workgroup partials -> sums[2].
+__global__ void __launch_bounds__(1024) reduce_partials_kernel(int n, const float *partials,
+                                                               float *sums) {
+  __shared__ float red[2][16];
+  float a = 0.f, b = 0.f;
+  for (int i = threadIdx.x; i < n; i += 1024) {
+    a += partials[2 * i];
+    b += partials[2 * i + 1];
+  }
+  a = wave_sum(a);
+  b = wave_sum(b);
+  if ((threadIdx.x & 63) == 0) {
+    red[0][threadIdx.x >> 6] = a;
+    red[1][threadIdx.x >> 6] = b;
+  }
+  __syncthreads();
+  if (threadIdx.x < 2) {
+    float t = 0.f;
+    for (int w = 0; w < 16; ++w) t += red[threadIdx.x][w];
+    sums[threadIdx.x] = t;
   }
 }
 
@@ -190,9 +214,16 @@ bwd_kernel(int B, int H, int W, int C, const float *__restrict__ x, const float 
 
 using namespace gs;
 
+static int64_t ssim_map_floats(int B, int H, int W, int C) {
+  return (int64_t)B * C * 3 * (int64_t)(H - 10) * (W - 10);
+}
+static int64_t ssim_blocks(int B, int H, int W) {
+  return (int64_t)((W - 10 + 15) / 16) * ((H - 10 + 15) / 16) * B;
+}
+
 extern "C" int64_t gsplat_hip_ssim_workspace_bytes(int B, int H, int W, int C) {
   if (H <= 10 || W <= 10) return 0;
-  return (int64_t)sizeof(float) * B * C * 3 * (int64_t)(H - 10) * (W - 10);
+  return (int64_t)sizeof(float) * (ssim_map_floats(B, H, W, C) + 2 * ssim_blocks(B, H, W));
 }
 
 extern "C" int gsplat_hip_ssim_l1_fwd(int B, int H, int W, int C, const float *img1,
@@ -201,10 +232,13 @@ extern "C" int gsplat_hip_ssim_l1_fwd(int B, int H, int W, int C, const float *i
   GS_REQUIRE(B > 0 && C > 0 && H > 10 && W > 10,
              "ssim_l1_fwd: images must be larger than the 11x11 window (got %dx%d)", H, W);
   hipStream_t st = (hipStream_t)stream;
-  GS_HIP(hipMemsetAsync(sums, 0, 2 * sizeof(float), st));
+  float *maps = reinterpret_cast<float *>(workspace);
+  float *partials = maps + ssim_map_floats(B, H, W, C);
   dim3 grid((W - 10 + 15) / 16, (H - 10 + 15) / 16, B);
-  hipLaunchKernelGGL(ssim::fwd_kernel, grid, dim3(256), 0, st, B, H, W, C, img1, img2,
-                     reinterpret_cast<float *>(workspace), sums);
+  hipLaunchKernelGGL(ssim::fwd_kernel, grid, dim3(256), 0, st, B, H, W, C, img1, img2, maps,
+                     partials);
+  hipLaunchKernelGGL(ssim::reduce_partials_kernel, dim3(1), dim3(1024), 0, st,
+                     (int)ssim_blocks(B, H, W), partials, sums);
   GS_CHECK_LAUNCH("ssim_l1_fwd");
   return 0;
 }

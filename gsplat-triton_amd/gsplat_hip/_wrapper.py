@@ -292,32 +292,46 @@ class _SphericalHarmonics(torch.autograd.Function):
     """Spherical harmonics (gsplat/triton_impl/_wrapper.py:552-593)."""
 
     @staticmethod
-    def forward(ctx, sh_degree, dirs, coeffs, masks, block_size=None):
+    def forward(ctx, sh_degree, dirs, coeffs, masks, block_size=None, coeffs_rest=None):
         dirs = _f32c(dirs)
         base, n_rows = _coeff_rows(coeffs)
-        _dev_check(dirs, base)
-        K = coeffs.shape[-2]
+        rest = None
+        if coeffs_rest is not None:  # split (sh0 [..,1,3], shN [..,K-1,3]) form
+            rest, n_rows_r = _coeff_rows(coeffs_rest)
+            assert n_rows_r == n_rows and coeffs.shape[-2] == 1, (coeffs.shape, coeffs_rest.shape)
+        _dev_check(dirs, base, rest)
+        K = coeffs.shape[-2] + (0 if rest is None else coeffs_rest.shape[-2])
         n = dirs.numel() // 3
         m = None if masks is None else masks.to(torch.bool).contiguous()
         colors = torch.empty(*dirs.shape[:-1], 3, device=dirs.device, dtype=torch.float32)
         _lib.call("gsplat_hip_sh_fwd", int(sh_degree), n, n_rows, K, _ptr(dirs), _ptr(base),
-                  _ptr(m), _ptr(colors), _stream())
-        ctx.save_for_backward(dirs, base, m)
-        ctx.sh_degree, ctx.n_rows, ctx.coeff_shape = int(sh_degree), n_rows, coeffs.shape
+                  _ptr(rest), _ptr(m), _ptr(colors), _stream())
+        ctx.save_for_backward(dirs, base, rest, m)
+        ctx.sh_degree, ctx.n_rows, ctx.K = int(sh_degree), n_rows, K
+        ctx.coeff_shape = coeffs.shape
+        ctx.rest_shape = None if coeffs_rest is None else coeffs_rest.shape
         return colors
 
     @staticmethod
     def backward(ctx, v_colors):
-        dirs, base, m = ctx.saved_tensors
-        K = ctx.coeff_shape[-2]
+        dirs, base, rest, m = ctx.saved_tensors
+        K = ctx.K
         n = dirs.numel() // 3
         v_colors = _f32c(v_colors)
-        v_coeffs = torch.empty(*dirs.shape[:-1], K, 3, device=dirs.device)
+        lead = dirs.shape[:-1]
+        if rest is None:
+            v_coeffs = torch.empty(*lead, K, 3, device=dirs.device)
+            v_rest = None
+        else:
+            v_coeffs = torch.empty(*lead, 1, 3, device=dirs.device)
+            v_rest = torch.empty(*lead, K - 1, 3, device=dirs.device)
         want_dirs = ctx.needs_input_grad[1]
         v_dirs = torch.empty_like(dirs) if want_dirs else None
         _lib.call("gsplat_hip_sh_bwd", ctx.sh_degree, n, ctx.n_rows, K, _ptr(dirs), _ptr(base),
-                  _ptr(m), _ptr(v_colors), _ptr(v_coeffs), _ptr(v_dirs), _stream())
-        return None, v_dirs, v_coeffs.view(ctx.coeff_shape), None, None
+                  _ptr(rest), _ptr(m), _ptr(v_colors), _ptr(v_coeffs), _ptr(v_rest),
+                  _ptr(v_dirs), _stream())
+        v_rest = None if v_rest is None else v_rest.view(ctx.rest_shape)
+        return None, v_dirs, v_coeffs.view(ctx.coeff_shape), None, None, v_rest
 
 
 def spherical_harmonics(
@@ -327,14 +341,23 @@ def spherical_harmonics(
     masks: Optional[Tensor] = None,
     block_size: int = None,
 ) -> Tensor:
-    """Computes spherical harmonics colours [..., 3] (_wrapper.py:596-620)."""
-    assert (degrees_to_use + 1) ** 2 <= coeffs.shape[-2], coeffs.shape
+    """Computes spherical harmonics colours [..., 3] (_wrapper.py:596-620).
+
+    Extension: `coeffs` may also be the pair (sh0 [...,1,3], shN [...,K-1,3])
+    as the trainer stores them; it is read in place instead of concatenated."""
+    rest = None
+    if isinstance(coeffs, (tuple, list)):
+        coeffs, rest = coeffs
+        assert coeffs.shape[-2] == 1 and rest.shape[:-2] == coeffs.shape[:-2], \
+            (coeffs.shape, rest.shape)
+    K = coeffs.shape[-2] + (0 if rest is None else rest.shape[-2])
+    assert (degrees_to_use + 1) ** 2 <= K, (coeffs.shape, K)
     assert dirs.shape[:-1] == coeffs.shape[:-2], (dirs.shape, coeffs.shape)
     assert dirs.shape[-1] == 3, dirs.shape
     assert coeffs.shape[-1] == 3, coeffs.shape
     if masks is not None:
         assert masks.shape == dirs.shape[:-1], masks.shape
-    return _SphericalHarmonics.apply(degrees_to_use, dirs, coeffs, masks, block_size)
+    return _SphericalHarmonics.apply(degrees_to_use, dirs, coeffs, masks, block_size, rest)
 
 
 # ============================================================ rasterization ==

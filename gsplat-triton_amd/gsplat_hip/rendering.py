@@ -68,7 +68,16 @@ def rasterization(
     assert viewmats.shape == (C, 4, 4), viewmats.shape
     assert Ks.shape == (C, 3, 3), Ks.shape
     assert render_mode in ["RGB", "D", "ED", "RGB+D", "RGB+ED"], render_mode
-    if sh_degree is None:
+    sh_rest = None
+    if isinstance(colors, (tuple, list)):
+        # extension: SH coefficients as the trainer stores them, (sh0 [N,1,3],
+        # shN [N,K-1,3]); read in place instead of torch.cat per step
+        assert sh_degree is not None, "a (sh0, shN) pair needs sh_degree"
+        colors, sh_rest = colors
+        assert colors.shape == (N, 1, 3) and sh_rest.shape[0] == N and sh_rest.shape[2] == 3, \
+            (colors.shape, sh_rest.shape)
+        assert (sh_degree + 1) ** 2 <= 1 + sh_rest.shape[1], sh_rest.shape
+    elif sh_degree is None:
         assert (colors.dim() == 2 and colors.shape[0] == N) or (
             colors.dim() == 3 and colors.shape[:2] == (C, N)), colors.shape
     else:
@@ -103,6 +112,8 @@ def rasterization(
         dirs = means[None, :, :] - camtoworlds[:, None, :3, 3]  # [C, N, 3]
         masks = radii > 0
         shs = colors.expand(C, -1, -1, -1) if colors.dim() == 3 else colors
+        if sh_rest is not None:
+            shs = (shs, sh_rest.expand(C, -1, -1, -1))
         colors = spherical_harmonics(sh_degree, dirs, shs, masks=masks)  # [C, N, 3]
         colors = torch.clamp_min(colors + 0.5, 0.0)
 

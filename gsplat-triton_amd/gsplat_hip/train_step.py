@@ -145,7 +145,7 @@ class Trainer:
         p = self.params
         return rasterization(
             p["means"], p["quats"], torch.exp(p["scales"]), torch.sigmoid(p["opacities"]),
-            torch.cat([p["sh0"], p["shN"]], 1), self.viewmats[ci:ci + 1], self.Ks[ci:ci + 1],
+            (p["sh0"], p["shN"]) if self.fused else torch.cat([p["sh0"], p["shN"]], 1), self.viewmats[ci:ci + 1], self.Ks[ci:ci + 1],
             self.width, self.height, sh_degree=self.sh_degree, packed=False,
             near_plane=0.01, far_plane=1e10, radius_clip=0.0, rasterize_mode="classic")
 
@@ -189,10 +189,16 @@ class Trainer:
         g = meta["means2d"].grad
         if g is None:
             return
-        scale = torch.tensor([meta["width"] / 2.0 * meta["n_cameras"],
-                              meta["height"] / 2.0 * meta["n_cameras"]], device=g.device)
-        sel = (meta["radii"] > 0).float()  # [C, N]
-        self.grad2d += ((g * scale).norm(dim=-1) * sel).sum(0)
-        self.count += sel.sum(0)
+        sx = meta["width"] / 2.0 * meta["n_cameras"]
+        sy = meta["height"] / 2.0 * meta["n_cameras"]
+        sel = meta["radii"] > 0  # [C, N]
+        # elementwise hypot instead of a reduction over a size-2 dim
+        nrm = torch.where(sel, torch.hypot(g[..., 0] * sx, g[..., 1] * sy), 0.0)
+        if nrm.shape[0] == 1:
+            self.grad2d.add_(nrm[0])
+            self.count.add_(sel[0])
+        else:
+            self.grad2d.add_(nrm.sum(0))
+            self.count.add_(sel.sum(0))
         # state["radii"] is only tracked when refine_scale2d_stop_iter > 0
         # (default 0, default.py:90,255-262)

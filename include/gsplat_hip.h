@@ -66,17 +66,22 @@ int gsplat_hip_projection_bwd(int C, int N, const float *means, const float *qua
  * mask zeroing of _SphericalHarmonics.forward (_wrapper.py:555-572).
  * dirs[n,3], coeffs[n_coeff_rows,K,3] (row i uses coeff row i % n_coeff_rows,
  * so [N,K,3] coefficients broadcast over C cameras need no copy),
- * masks u8[n] or NULL -> colors[n,3] (0 where masks[i] == 0). */
+ * masks u8[n] or NULL -> colors[n,3] (0 where masks[i] == 0).
+ * If coeffs_rest is non-NULL the coefficients are split as the trainer holds
+ * them: coeffs = DC term [rows,1,3], coeffs_rest = bases 1..K-1 [rows,K-1,3]
+ * (replaces the per-step torch.cat of sh0/shN, examples/simple_trainer.py:469). */
 int gsplat_hip_sh_fwd(int degree, int64_t n, int64_t n_coeff_rows, int K, const float *dirs,
-                      const float *coeffs, const uint8_t *masks, float *colors, void *stream);
+                      const float *coeffs, const float *coeffs_rest, const uint8_t *masks,
+                      float *colors, void *stream);
 
 /* Replaces sh_to_color_bwd() (gsplat/triton_impl/sh_bwd.py:383-436) and
  * _SphericalHarmonics.backward (_wrapper.py:574-593).
  * -> v_coeffs[n,K,3] (bases >= (degree+1)^2 and masked rows are 0),
- *    v_dirs[n,3] or NULL. */
+ *    v_dirs[n,3] or NULL.  Split form: v_coeffs [n,1,3] + v_coeffs_rest [n,K-1,3]. */
 int gsplat_hip_sh_bwd(int degree, int64_t n, int64_t n_coeff_rows, int K, const float *dirs,
-                      const float *coeffs, const uint8_t *masks, const float *v_colors,
-                      float *v_coeffs, float *v_dirs, void *stream);
+                      const float *coeffs, const float *coeffs_rest, const uint8_t *masks,
+                      const float *v_colors, float *v_coeffs, float *v_coeffs_rest,
+                      float *v_dirs, void *stream);
 
 /* ---------------------------------------------------------------------------
  * Tile intersection.  Replaces isect_tiles() (gsplat/triton_impl/isect_tiles.py:13-131)

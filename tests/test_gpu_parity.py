@@ -305,3 +305,24 @@ def test_full_size_invariants_m2():
     rc, ra = gsplat_hip.rasterize_to_pixels(m2, cn, cols, opac[None].to(DEV), W, H, 16, off, fids)
     assert torch.isfinite(rc).all() and (ra >= 0).all() and (ra < 1).all()
     assert (rc <= ra + 1e-5).all()  # colours in [0,1] => composite <= alpha
+
+
+def test_sh_split_coeffs_match_concatenated():
+    """(sh0, shN) read in place == the torch.cat'ed [N,K,3] tensor."""
+    import gsplat_hip
+    torch.manual_seed(1)
+    C, N = 2, 999
+    sh0 = torch.randn(N, 1, 3, device=DEV, requires_grad=True)
+    shN = torch.randn(N, 15, 3, device=DEV, requires_grad=True)
+    dirs = torch.randn(C, N, 3, device=DEV, requires_grad=True)
+    masks = torch.rand(C, N, device=DEV) > 0.25
+    a = gsplat_hip.spherical_harmonics(3, dirs, (sh0.expand(C, -1, -1, -1),
+                                                 shN.expand(C, -1, -1, -1)), masks=masks)
+    b = gsplat_hip.spherical_harmonics(3, dirs, torch.cat([sh0, shN], 1).expand(C, -1, -1, -1),
+                                       masks=masks)
+    assert torch.equal(a, b)
+    w = torch.randn_like(a)
+    ga = torch.autograd.grad((a * w).sum(), (sh0, shN, dirs))
+    gb = torch.autograd.grad((b * w).sum(), (sh0, shN, dirs))
+    for x, y in zip(ga, gb):
+        close(x, y, 1e-6, 1e-6)
