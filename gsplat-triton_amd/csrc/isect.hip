@@ -78,18 +78,25 @@ GS_INLINE T block_exclusive_scan(T v, T *lds /* [kIsectBlock/64 + 1] */, T *tota
   return lds[wid] + x - v;
 }
 
+// Per-Gaussian tile counts; per-block sums of the counts (block_sums[b]) and
+// of the number of Gaussians with at least one tile (vis_sums[b]).
 __global__ void __launch_bounds__(kIsectBlock)
 isect_count_kernel(int64_t G, const float *__restrict__ means2d, const int32_t *__restrict__ radii,
                    int ts, int tw, int th, int32_t *__restrict__ tiles_per_gauss,
-                   int64_t *__restrict__ block_sums) {
+                   int64_t *__restrict__ block_sums, int64_t *__restrict__ vis_sums) {
   __shared__ int64_t lds[kIsectBlock / 64 + 1];
   const int64_t i = (int64_t)blockIdx.x * kIsectBlock + threadIdx.x;
   Rect rc;
   int cnt = (i < G) ? tiles_of(means2d, radii, i, ts, tw, th, &rc) : 0;
   if (i < G) tiles_per_gauss[i] = cnt;
-  int64_t tot;
+  int64_t tot, vtot;
   block_exclusive_scan<int64_t>((int64_t)cnt, lds, &tot);
-  if (threadIdx.x == 0) block_sums[blockIdx.x] = tot;
+  __syncthreads();
+  block_exclusive_scan<int64_t>((int64_t)(cnt > 0), lds, &vtot);
+  if (threadIdx.x == 0) {
+    block_sums[blockIdx.x] = tot;
+    vis_sums[blockIdx.x] = vtot;
+  }
 }
 
 // Exclusive scan of the per-block sums in place; total -> block_sums[nb].
@@ -165,48 +172,150 @@ isect_offsets_kernel(int64_t n, const int64_t *__restrict__ isect_ids, int n_til
   if (i >= n) return;
   const int64_t tmask = (tile_bits >= 63) ? -1 : ((int64_t)1 << tile_bits) - 1;
   auto key_of = [&](int64_t id) -> int64_t {
+    // ids of negative-depth isects are sign-extended (all upper bits set, as
+    // the reference, isect_tiles.py:223); they sort past every real tile
+    if (id < 0) return n_tiles_total;
     const int64_t k = id >> 32;
-    return (k >> tile_bits) * n_tiles + (k & tmask);
+    const int64_t key = (k >> tile_bits) * n_tiles + (k & tmask);
+    return key < n_tiles_total ? key : n_tiles_total;
   };
   const int64_t cur = key_of(isect_ids[i]);
   if (i == 0) {
-    for (int64_t t = 0; t <= cur; ++t) offsets[t] = 0;
+    for (int64_t t = 0; t <= cur && t < n_tiles_total; ++t) offsets[t] = 0;
   } else {
     const int64_t prev = key_of(isect_ids[i - 1]);
     if (prev != cur)
-      for (int64_t t = prev + 1; t <= cur; ++t) offsets[t] = (int32_t)i;
+      for (int64_t t = prev + 1; t <= cur && t < n_tiles_total; ++t) offsets[t] = (int32_t)i;
   }
   if (i == n - 1)
     for (int64_t t = cur + 1; t < n_tiles_total; ++t) offsets[t] = (int32_t)n;
+}
+
+__global__ void isect_totals_kernel(const int64_t *n_isects, const int64_t *n_vis,
+                                    int64_t *totals) {
+  if (threadIdx.x == 0) {
+    totals[0] = *n_isects;
+    totals[1] = *n_vis;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Depth-first sorted emission (sort=True).  The reference's stable sort of
+// (cam | tile | depth) keys, restricted to one (cam, tile), orders isects by
+// depth bits and then by Gaussian index.  The same order results from
+//   (1) a stable sort of the visible Gaussians by depth bits (|V| ~ 0.3 N),
+//   (2) emitting every Gaussian's tiles in that order, and
+//   (3) a stable sort of the emitted isects by the (cam, tile) bits only
+//       (tile_bits + cam_bits, e.g. 13 bits at 1080p instead of 45).
+// Negative depths (near_plane <= 0) follow the reference's sign extension:
+// their (cam, tile) field becomes all ones.
+
+// (1a) compact the Gaussians with tiles, in index order, with their depth bits
+__global__ void __launch_bounds__(kIsectBlock)
+isect_compact_kernel(int64_t G, const int32_t *__restrict__ tiles_per_gauss,
+                     const float *__restrict__ depths, const int64_t *__restrict__ vis_prefix,
+                     int32_t *__restrict__ V, uint32_t *__restrict__ dkey) {
+  __shared__ int64_t lds[kIsectBlock / 64 + 1];
+  const int64_t i = (int64_t)blockIdx.x * kIsectBlock + threadIdx.x;
+  const int on = (i < G) && tiles_per_gauss[i] > 0;
+  int64_t tot;
+  const int64_t local = block_exclusive_scan<int64_t>((int64_t)on, lds, &tot);
+  if (!on) return;
+  const int64_t s = vis_prefix[blockIdx.x] + local;
+  V[s] = (int32_t)i;
+  dkey[s] = __float_as_uint(depths[i]);
+}
+
+// (2a) per-block sums of the tile counts in depth order
+__global__ void __launch_bounds__(kIsectBlock)
+isect_sorted_count_kernel(int64_t nV, const int32_t *__restrict__ Vs,
+                          const int32_t *__restrict__ tiles_per_gauss,
+                          int64_t *__restrict__ block_sums) {
+  __shared__ int64_t lds[kIsectBlock / 64 + 1];
+  const int64_t s = (int64_t)blockIdx.x * kIsectBlock + threadIdx.x;
+  const int cnt = (s < nV) ? tiles_per_gauss[Vs[s]] : 0;
+  int64_t tot;
+  block_exclusive_scan<int64_t>((int64_t)cnt, lds, &tot);
+  if (threadIdx.x == 0) block_sums[blockIdx.x] = tot;
+}
+
+// (2b) emit (cam|tile key, Gaussian index) in depth order
+__global__ void __launch_bounds__(kIsectBlock)
+isect_sorted_emit_kernel(int64_t nV, int N, const int32_t *__restrict__ Vs,
+                         const float *__restrict__ means2d, const int32_t *__restrict__ radii,
+                         const float *__restrict__ depths, const int32_t *__restrict__ camera_ids,
+                         int ts, int tw, int th, int tile_bits, uint32_t key_all_ones,
+                         const int64_t *__restrict__ block_prefix, uint32_t *__restrict__ tkey,
+                         int32_t *__restrict__ val) {
+  __shared__ int64_t lds[kIsectBlock / 64 + 1];
+  const int64_t s = (int64_t)blockIdx.x * kIsectBlock + threadIdx.x;
+  Rect rc{0, 0, 0, 0};
+  int32_t i = 0;
+  int cnt = 0;
+  if (s < nV) {
+    i = Vs[s];
+    cnt = tiles_of(means2d, radii, i, ts, tw, th, &rc);
+  }
+  int64_t tot;
+  const int64_t local = block_exclusive_scan<int64_t>((int64_t)cnt, lds, &tot);
+  if (cnt == 0) return;
+  int64_t cur = block_prefix[blockIdx.x] + local;
+  const uint32_t cam = camera_ids ? (uint32_t)camera_ids[i] : (uint32_t)(i / N);
+  const bool neg = __float_as_int(depths[i]) < 0;
+  const uint32_t hi = cam << tile_bits;
+  for (int y = rc.y0; y < rc.y1; ++y) {
+    for (int x = rc.x0; x < rc.x1; ++x) {
+      tkey[cur] = neg ? key_all_ones : (hi | (uint32_t)(y * tw + x));
+      val[cur] = i;
+      ++cur;
+    }
+  }
+}
+
+// (3b) assemble the reference's 64-bit ids from the sorted (key, Gaussian)
+__global__ void __launch_bounds__(256)
+isect_sorted_finalize_kernel(int64_t n, const uint32_t *__restrict__ tkey,
+                             const int32_t *__restrict__ val, const float *__restrict__ depths,
+                             int64_t *__restrict__ isect_ids, int32_t *__restrict__ flatten_ids) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n) return;
+  const int32_t i = val[p];
+  const int32_t db = __float_as_int(depths[i]);
+  isect_ids[p] = db < 0 ? (int64_t)db : (((int64_t)tkey[p] << 32) | (int64_t)(uint32_t)db);
+  flatten_ids[p] = i;
 }
 
 }  // namespace gs
 
 using namespace gs;
 
+// count workspace: [0, nb] scanned isect block sums (+ total), [nb+1, 2nb+1]
+// scanned visible-Gaussian block sums (+ total).
 extern "C" int64_t gsplat_hip_isect_workspace_bytes(int64_t n_gaussians) {
   const int64_t nb = (n_gaussians + kIsectBlock - 1) / kIsectBlock;
-  return (nb + 2) * (int64_t)sizeof(int64_t);
+  return (2 * nb + 2) * (int64_t)sizeof(int64_t);
 }
 
 extern "C" int gsplat_hip_isect_count(int64_t n_gaussians, const float *means2d,
                                       const int32_t *radii, int tile_size, int tile_width,
                                       int tile_height, int32_t *tiles_per_gauss,
-                                      void *workspace, int64_t *n_isects_device,
-                                      void *stream) {
+                                      void *workspace, int64_t *totals_device, void *stream) {
   GS_REQUIRE(n_gaussians >= 0 && tile_size > 0, "isect_count: bad sizes");
   hipStream_t st = (hipStream_t)stream;
   int64_t *ws = reinterpret_cast<int64_t *>(workspace);
   const int64_t nb = (n_gaussians + kIsectBlock - 1) / kIsectBlock;
   if (nb == 0) {
-    GS_HIP(hipMemsetAsync(n_isects_device, 0, sizeof(int64_t), st));
+    GS_HIP(hipMemsetAsync(totals_device, 0, 2 * sizeof(int64_t), st));
     return 0;
   }
+  int64_t *vis = ws + nb + 1;
   hipLaunchKernelGGL(isect_count_kernel, dim3((unsigned)nb), dim3(kIsectBlock), 0, st,
                      n_gaussians, means2d, radii, tile_size, tile_width, tile_height,
-                     tiles_per_gauss, ws);
+                     tiles_per_gauss, ws, vis);
   hipLaunchKernelGGL(isect_scan_blocks_kernel, dim3(1), dim3(1024), 0, st, nb, ws);
-  GS_HIP(hipMemcpyAsync(n_isects_device, ws + nb, sizeof(int64_t), hipMemcpyDeviceToDevice, st));
+  hipLaunchKernelGGL(isect_scan_blocks_kernel, dim3(1), dim3(1024), 0, st, nb, vis);
+  hipLaunchKernelGGL(isect_totals_kernel, dim3(1), dim3(64), 0, st, ws + nb, vis + nb,
+                     totals_device);
   GS_CHECK_LAUNCH("isect_count");
   return 0;
 }
@@ -267,5 +376,105 @@ extern "C" int gsplat_hip_isect_offsets(int64_t n_isects, const int64_t *isect_i
   hipLaunchKernelGGL(isect_offsets_kernel, dim3((unsigned)((n_isects + 255) / 256)), dim3(256), 0,
                      st, n_isects, isect_ids, C * n_tiles, n_tiles, tile_bits, offsets);
   GS_CHECK_LAUNCH("isect_offsets");
+  return 0;
+}
+
+// ------------------------------------------------------- depth-first path --
+namespace {
+struct SortedLayout {
+  size_t V, dkey, Vs, dkeys, blk, tkey, val, tkeys, vals, tmp, total;
+  size_t tmp_bytes;
+};
+
+size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+SortedLayout sorted_layout(int64_t nV, int64_t n, int key_bits) {
+  size_t t1 = 0, t2 = 0;
+  (void)rocprim::radix_sort_pairs(nullptr, t1, (const uint32_t *)nullptr, (uint32_t *)nullptr,
+                                  (const int32_t *)nullptr, (int32_t *)nullptr, (size_t)nV, 0u,
+                                  32u, (hipStream_t)0);
+  (void)rocprim::radix_sort_pairs(nullptr, t2, (const uint32_t *)nullptr, (uint32_t *)nullptr,
+                                  (const int32_t *)nullptr, (int32_t *)nullptr, (size_t)n, 0u,
+                                  (unsigned)(key_bits > 0 ? key_bits : 1), (hipStream_t)0);
+  SortedLayout L{};
+  size_t o = 0;
+  L.V = o; o = align256(o + 4 * (size_t)nV);
+  L.dkey = o; o = align256(o + 4 * (size_t)nV);
+  L.Vs = o; o = align256(o + 4 * (size_t)nV);
+  L.dkeys = o; o = align256(o + 4 * (size_t)nV);
+  L.blk = o; o = align256(o + 8 * (size_t)((nV + kIsectBlock - 1) / kIsectBlock + 2));
+  L.tkey = o; o = align256(o + 4 * (size_t)n);
+  L.val = o; o = align256(o + 4 * (size_t)n);
+  L.tkeys = o; o = align256(o + 4 * (size_t)n);
+  L.vals = o; o = align256(o + 4 * (size_t)n);
+  L.tmp = o;
+  L.tmp_bytes = t1 > t2 ? t1 : t2;
+  o = align256(o + L.tmp_bytes + 1);
+  L.total = o;
+  return L;
+}
+}  // namespace
+
+extern "C" int64_t gsplat_hip_isect_sorted_workspace_bytes(int64_t n_visible, int64_t n_isects,
+                                                           int key_bits) {
+  return (int64_t)sorted_layout(n_visible, n_isects, key_bits).total;
+}
+
+// Sorted isects without sorting 64-bit keys: see "Depth-first sorted emission".
+// count_workspace is the gsplat_hip_isect_count workspace (scanned block sums).
+extern "C" int gsplat_hip_isect_write_sorted(
+    int64_t n_gaussians, int N, const float *means2d, const int32_t *radii, const float *depths,
+    const int32_t *camera_ids, const int32_t *tiles_per_gauss, int tile_size, int tile_width,
+    int tile_height, int tile_bits, int cam_bits, const void *count_workspace, int64_t n_visible,
+    int64_t n_isects, void *workspace, int64_t workspace_bytes, int64_t *isect_ids,
+    int32_t *flatten_ids, void *stream) {
+  GS_REQUIRE(n_gaussians >= 0 && (camera_ids || N > 0 || n_gaussians == 0),
+             "isect_write_sorted: N must be > 0 when camera_ids is null");
+  GS_REQUIRE(tile_bits + cam_bits <= 32, "isect_write_sorted: tile_bits + cam_bits > 32");
+  if (n_isects <= 0 || n_visible <= 0) return 0;
+  const int key_bits = tile_bits + cam_bits;
+  const SortedLayout L = sorted_layout(n_visible, n_isects, key_bits);
+  GS_REQUIRE(workspace_bytes >= (int64_t)L.total, "isect_write_sorted: workspace %lld < %lld",
+             (long long)workspace_bytes, (long long)L.total);
+  hipStream_t st = (hipStream_t)stream;
+  char *ws = reinterpret_cast<char *>(workspace);
+  int32_t *V = reinterpret_cast<int32_t *>(ws + L.V), *Vs = reinterpret_cast<int32_t *>(ws + L.Vs);
+  uint32_t *dkey = reinterpret_cast<uint32_t *>(ws + L.dkey);
+  uint32_t *dkeys = reinterpret_cast<uint32_t *>(ws + L.dkeys);
+  int64_t *blk = reinterpret_cast<int64_t *>(ws + L.blk);
+  uint32_t *tkey = reinterpret_cast<uint32_t *>(ws + L.tkey);
+  uint32_t *tkeys = reinterpret_cast<uint32_t *>(ws + L.tkeys);
+  int32_t *val = reinterpret_cast<int32_t *>(ws + L.val), *vals = reinterpret_cast<int32_t *>(ws + L.vals);
+  void *tmp = ws + L.tmp;
+
+  const int64_t nbG = (n_gaussians + kIsectBlock - 1) / kIsectBlock;
+  const int64_t *vis_prefix = reinterpret_cast<const int64_t *>(count_workspace) + nbG + 1;
+  hipLaunchKernelGGL(isect_compact_kernel, dim3((unsigned)nbG), dim3(kIsectBlock), 0, st,
+                     n_gaussians, tiles_per_gauss, depths, vis_prefix, V, dkey);
+  size_t tb = L.tmp_bytes;
+  hipError_t e = rocprim::radix_sort_pairs(tmp, tb, dkey, dkeys, V, Vs, (size_t)n_visible, 0u, 32u,
+                                           st);
+  GS_REQUIRE(e == hipSuccess, "isect_write_sorted: depth sort: %s", hipGetErrorString(e));
+  const int64_t nbV = (n_visible + kIsectBlock - 1) / kIsectBlock;
+  hipLaunchKernelGGL(isect_sorted_count_kernel, dim3((unsigned)nbV), dim3(kIsectBlock), 0, st,
+                     n_visible, Vs, tiles_per_gauss, blk);
+  hipLaunchKernelGGL(isect_scan_blocks_kernel, dim3(1), dim3(1024), 0, st, nbV, blk);
+  const uint32_t all_ones = key_bits >= 32 ? 0xffffffffu : ((1u << key_bits) - 1u);
+  hipLaunchKernelGGL(isect_sorted_emit_kernel, dim3((unsigned)nbV), dim3(kIsectBlock), 0, st,
+                     n_visible, N, Vs, means2d, radii, depths, camera_ids, tile_size, tile_width,
+                     tile_height, tile_bits, all_ones, blk, tkey, val);
+  const uint32_t *fk = tkey;
+  const int32_t *fv = val;
+  if (key_bits > 0) {
+    tb = L.tmp_bytes;
+    e = rocprim::radix_sort_pairs(tmp, tb, tkey, tkeys, val, vals, (size_t)n_isects, 0u,
+                                  (unsigned)key_bits, st);
+    GS_REQUIRE(e == hipSuccess, "isect_write_sorted: tile sort: %s", hipGetErrorString(e));
+    fk = tkeys;
+    fv = vals;
+  }
+  hipLaunchKernelGGL(isect_sorted_finalize_kernel, dim3((unsigned)((n_isects + 255) / 256)),
+                     dim3(256), 0, st, n_isects, fk, fv, depths, isect_ids, flatten_ids);
+  GS_CHECK_LAUNCH("isect_write_sorted");
   return 0;
 }

@@ -12,7 +12,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GSPLAT_HIP_LIB", os.path.join(_HERE, "libgsplat_hip.so"))
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 _p = ctypes.c_void_p
 _i32 = ctypes.c_int
@@ -33,6 +33,9 @@ _SIGS = {
     "gsplat_hip_isect_count": (_i32, [_i64, _p, _p, _i32, _i32, _i32, _p, _p, _p, _p]),
     "gsplat_hip_isect_write": (_i32, [_i64, _i32, _p, _p, _p, _p, _i32, _i32, _i32, _i32, _p,
                                       _p, _p, _p]),
+    "gsplat_hip_isect_sorted_workspace_bytes": (_i64, [_i64, _i64, _i32]),
+    "gsplat_hip_isect_write_sorted": (_i32, [_i64, _i32, _p, _p, _p, _p, _p, _i32, _i32, _i32,
+                                             _i32, _i32, _p, _i64, _i64, _p, _i64, _p, _p, _p]),
     "gsplat_hip_sort_workspace_bytes": (_i64, [_i64]),
     "gsplat_hip_radix_sort": (_i32, [_i64, _i32, _p, _p, _p, _p, _p, _i64, _p]),
     "gsplat_hip_isect_offsets": (_i32, [_i64, _p, _i32, _i32, _i32, _p, _p]),

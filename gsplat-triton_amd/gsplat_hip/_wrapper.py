@@ -16,6 +16,7 @@ stream; there is no CPU or Triton fallback.
 """
 
 import math
+import os
 from typing import Optional, Tuple
 
 import torch
@@ -192,6 +193,12 @@ def fully_fused_projection(
 
 
 # =================================================================== isect ==
+# Sorted-isect strategy: "depth_first" (32-bit depth sort of the visible
+# Gaussians + 32-bit (camera, tile) sort of the isects, csrc/isect.hip) or
+# "full" (the reference's single 64-bit key sort).  Both give identical output.
+ISECT_SORT = os.environ.get("GSPLAT_HIP_ISECT_SORT", "depth_first")
+
+
 @torch.no_grad()
 def isect_tiles(
     means2d: Tensor,  # [C, N, 2] or [nnz, 2]
@@ -242,24 +249,34 @@ def isect_tiles(
     tpg = torch.empty(G, dtype=torch.int32, device=dev)
     ws = torch.empty(max(int(_lib.query("gsplat_hip_isect_workspace_bytes", G)), 8),
                      dtype=torch.uint8, device=dev)
-    n_dev = torch.empty(1, dtype=torch.int64, device=dev)
+    totals = torch.empty(2, dtype=torch.int64, device=dev)
     _lib.call("gsplat_hip_isect_count", G, _ptr(means2d), _ptr(radii), tile_size, tile_width,
-              tile_height, _ptr(tpg), _ptr(ws), _ptr(n_dev), st)
-    n_isects = int(n_dev.item())  # the single host sync (isect_tiles.py:102)
+              tile_height, _ptr(tpg), _ptr(ws), _ptr(totals), st)
+    n_isects, n_visible = totals.tolist()  # the single host sync (isect_tiles.py:102)
     isect_ids = torch.empty(n_isects, dtype=torch.int64, device=dev)
     flatten_ids = torch.empty(n_isects, dtype=torch.int32, device=dev)
-    _lib.call("gsplat_hip_isect_write", G, N, _ptr(means2d), _ptr(radii), _ptr(depths),
-              _ptr(camera_ids), tile_size, tile_width, tile_height, n_bit_tile, _ptr(ws),
-              _ptr(isect_ids), _ptr(flatten_ids), st)
-    if sort and n_isects > 0:
-        sws = torch.empty(max(int(_lib.query("gsplat_hip_sort_workspace_bytes", n_isects)), 8),
+    if sort and ISECT_SORT == "depth_first":
+        key_bits = n_bit_tile + n_bit_cam
+        sws = torch.empty(max(int(_lib.query("gsplat_hip_isect_sorted_workspace_bytes", n_visible,
+                                             n_isects, key_bits)), 8),
                           dtype=torch.uint8, device=dev)
-        keys = torch.empty_like(isect_ids)
-        vals = torch.empty_like(flatten_ids)
-        _lib.call("gsplat_hip_radix_sort", n_isects, 32 + n_bit_tile + n_bit_cam,
-                  _ptr(isect_ids), _ptr(flatten_ids), _ptr(keys), _ptr(vals), _ptr(sws),
-                  sws.numel(), st)
-        isect_ids, flatten_ids = keys, vals
+        _lib.call("gsplat_hip_isect_write_sorted", G, N, _ptr(means2d), _ptr(radii),
+                  _ptr(depths), _ptr(camera_ids), _ptr(tpg), tile_size, tile_width, tile_height,
+                  n_bit_tile, n_bit_cam, _ptr(ws), n_visible, n_isects, _ptr(sws), sws.numel(),
+                  _ptr(isect_ids), _ptr(flatten_ids), st)
+    else:
+        _lib.call("gsplat_hip_isect_write", G, N, _ptr(means2d), _ptr(radii), _ptr(depths),
+                  _ptr(camera_ids), tile_size, tile_width, tile_height, n_bit_tile, _ptr(ws),
+                  _ptr(isect_ids), _ptr(flatten_ids), st)
+        if sort and n_isects > 0:
+            sws = torch.empty(max(int(_lib.query("gsplat_hip_sort_workspace_bytes", n_isects)),
+                                  8), dtype=torch.uint8, device=dev)
+            keys = torch.empty_like(isect_ids)
+            vals = torch.empty_like(flatten_ids)
+            _lib.call("gsplat_hip_radix_sort", n_isects, 32 + n_bit_tile + n_bit_cam,
+                      _ptr(isect_ids), _ptr(flatten_ids), _ptr(keys), _ptr(vals), _ptr(sws),
+                      sws.numel(), st)
+            isect_ids, flatten_ids = keys, vals
     if not packed:
         tpg = tpg.view(C, N)
     return tpg, isect_ids, flatten_ids

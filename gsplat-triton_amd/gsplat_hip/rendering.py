@@ -98,7 +98,8 @@ def rasterization(
         near_plane=near_plane, far_plane=far_plane, radius_clip=radius_clip,
         sparse_grad=sparse_grad, calc_compensations=(rasterize_mode == "antialiased"),
         camera_model=camera_model)
-    opacities = opacities.repeat(C, 1)  # [C, N]
+    # [C, N]; for C == 1 a view, so backward is not a (copying) reduction
+    opacities = opacities[None] if C == 1 else opacities.repeat(C, 1)
     if compensations is not None:
         opacities = opacities * compensations
     meta.update({"camera_ids": None, "gaussian_ids": None, "radii": radii, "means2d": means2d,
@@ -106,14 +107,18 @@ def rasterization(
 
     if sh_degree is None:
         if colors.dim() == 2:
-            colors = colors.expand(C, -1, -1)
+            colors = colors[None] if C == 1 else colors.expand(C, -1, -1)
     else:
         camtoworlds = torch.inverse(viewmats)  # [C, 4, 4]
         dirs = means[None, :, :] - camtoworlds[:, None, :3, 3]  # [C, N, 3]
         masks = radii > 0
-        shs = colors.expand(C, -1, -1, -1) if colors.dim() == 3 else colors
+        # broadcast over cameras without copies (read in place by the SH
+        # kernel); C == 1 uses an unsqueeze view so backward needs no reduction
+        def bcast(x):
+            return x[None] if C == 1 else x.expand(C, -1, -1, -1)
+        shs = bcast(colors) if colors.dim() == 3 else colors
         if sh_rest is not None:
-            shs = (shs, sh_rest.expand(C, -1, -1, -1))
+            shs = (shs, bcast(sh_rest))
         colors = spherical_harmonics(sh_degree, dirs, shs, masks=masks)  # [C, N, 3]
         colors = torch.clamp_min(colors + 0.5, 0.0)
 

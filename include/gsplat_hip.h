@@ -87,9 +87,9 @@ int gsplat_hip_sh_bwd(int degree, int64_t n, int64_t n_coeff_rows, int K, const 
  * Tile intersection.  Replaces isect_tiles() (gsplat/triton_impl/isect_tiles.py:13-131)
  * as three calls so that the caller can size the outputs after ONE device->host
  * read of n_isects (the reference's cumsum(...)[-1].item(), isect_tiles.py:101-102):
- *   1. gsplat_hip_isect_count: tiles_per_gauss i32[G] + per-block prefix in
- *      `workspace` (gsplat_hip_isect_workspace_bytes(G) bytes) + total in
- *      *n_isects_device (int64 on device).
+ *   1. gsplat_hip_isect_count: tiles_per_gauss i32[G] + per-block prefixes in
+ *      `workspace` (gsplat_hip_isect_workspace_bytes(G) bytes) + totals_device[2]
+ *      (int64 on device): {n_isects, n_visible = #Gaussians with >= 1 tile}.
  *   2. gsplat_hip_isect_write: isect_ids i64[n_isects], flatten_ids i32[n_isects]
  *      (unsorted; Gaussian-major, tile-row-major order).  tile_bits =
  *      (tile_width*tile_height - 1).bit_length() (Triton convention, isect_tiles.py:105).
@@ -101,12 +101,26 @@ int64_t gsplat_hip_isect_workspace_bytes(int64_t n_gaussians);
 int gsplat_hip_isect_count(int64_t n_gaussians, const float *means2d, const int32_t *radii,
                            int tile_size, int tile_width, int tile_height,
                            int32_t *tiles_per_gauss, void *workspace,
-                           int64_t *n_isects_device, void *stream);
+                           int64_t *totals_device, void *stream);
 int gsplat_hip_isect_write(int64_t n_gaussians, int N, const float *means2d,
                            const int32_t *radii, const float *depths, const int32_t *camera_ids,
                            int tile_size, int tile_width, int tile_height, int tile_bits,
                            const void *workspace, int64_t *isect_ids, int32_t *flatten_ids,
                            void *stream);
+/* Sorted emission in one call (the sort=True path of isect_tiles): writes the
+ * SAME isect_ids / flatten_ids as write + radix_sort, but sorts only 32-bit
+ * keys: a stable depth sort of the n_visible Gaussians, emission in that
+ * order, then a stable sort by the tile_bits+cam_bits (camera, tile) bits.
+ * count_workspace is step 1's workspace; key_bits = tile_bits + cam_bits <= 32. */
+int64_t gsplat_hip_isect_sorted_workspace_bytes(int64_t n_visible, int64_t n_isects,
+                                                int key_bits);
+int gsplat_hip_isect_write_sorted(int64_t n_gaussians, int N, const float *means2d,
+                                  const int32_t *radii, const float *depths,
+                                  const int32_t *camera_ids, const int32_t *tiles_per_gauss,
+                                  int tile_size, int tile_width, int tile_height, int tile_bits,
+                                  int cam_bits, const void *count_workspace, int64_t n_visible,
+                                  int64_t n_isects, void *workspace, int64_t workspace_bytes,
+                                  int64_t *isect_ids, int32_t *flatten_ids, void *stream);
 int64_t gsplat_hip_sort_workspace_bytes(int64_t n);
 int gsplat_hip_radix_sort(int64_t n, int n_bits, const int64_t *keys_in, const int32_t *vals_in,
                           int64_t *keys_out, int32_t *vals_out, void *workspace,

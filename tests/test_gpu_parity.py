@@ -98,8 +98,16 @@ def test_sh_broadcast_coeffs_match_materialised():
 
 
 # ----------------------------------------------------------------- isect
+@pytest.fixture(params=["depth_first", "full"])
+def isect_mode(request, monkeypatch):
+    """Run an isect test under both sort strategies of _wrapper.isect_tiles."""
+    from gsplat_hip import _wrapper
+    monkeypatch.setattr(_wrapper, "ISECT_SORT", request.param)
+    return request.param
+
+
 @pytest.mark.parametrize("name", ["isect_garden_t16", "isect_garden_t4", "isect_pow2_c2"])
-def test_isect_bit_exact_vs_reference(name):
+def test_isect_bit_exact_vs_reference(name, isect_mode):
     import gsplat_hip
     g = load_golden(name)
     ts, tw, th, C = (int(g[k]) for k in ("tile_size", "tile_width", "tile_height", "C"))
@@ -112,7 +120,7 @@ def test_isect_bit_exact_vs_reference(name):
     assert np.array_equal(off.cpu().numpy(), g["isect_offsets"])
 
 
-def test_isect_edge_cases():
+def test_isect_edge_cases(isect_mode):
     import gsplat_hip
     from oracle import gsplat_oracle as O
     # empty input, all-invalid input, single isect
@@ -129,7 +137,7 @@ def test_isect_edge_cases():
     assert off.flatten().tolist() == O.isect_offset_encode(ids.cpu().numpy(), 1, 3, 2).reshape(-1).tolist()
 
 
-def test_isect_random_vs_oracle_large_radii():
+def test_isect_random_vs_oracle_large_radii(isect_mode):
     """Ragged input: huge and tiny radii, off-screen means, C=3, exact."""
     import gsplat_hip
     from oracle import gsplat_oracle as O
@@ -147,6 +155,48 @@ def test_isect_random_vs_oracle_large_radii():
     assert np.array_equal(fids.cpu().numpy(), ofids)
     off = gsplat_hip.isect_offset_encode(ids, C, tw, th)
     assert np.array_equal(off.cpu().numpy(), O.isect_offset_encode(oids, C, tw, th))
+
+
+@pytest.mark.parametrize("C,tw,th", [(1, 4, 4), (2, 5, 3), (4, 8, 8)])
+def test_isect_negative_and_tied_depths(isect_mode, C, tw, th):
+    """Negative depths (sign-extended ids that land in the all-ones (cam, tile)
+    key), +-0.0, many exact ties, and grids whose last tile id is all ones."""
+    import gsplat_hip
+    from oracle import gsplat_oracle as O
+    rng = np.random.default_rng(C * 100 + tw)
+    ts, N = 16, 700
+    m2 = rng.uniform(-20, 16 * max(tw, th) + 20, (C, N, 2)).astype(np.float32)
+    r = rng.choice([0, 3, 9, 30, 70], (C, N)).astype(np.int32)
+    d = rng.choice(np.array([-2.5, -1e-3, -0.0, 0.0, 0.5, 0.5, 1.0, 3.0, 1e6], np.float32), (C, N))
+    d = np.where(rng.random((C, N)) < 0.3, rng.uniform(-5, 5, (C, N)), d).astype(np.float32)
+    tpg, ids, fids = gsplat_hip.isect_tiles(T(m2), T(r), T(d), ts, tw, th)
+    otpg, oids, ofids = O.isect_tiles(m2, r, d, ts, tw, th)
+    assert np.array_equal(tpg.cpu().numpy(), otpg)
+    assert np.array_equal(ids.cpu().numpy(), oids)
+    assert np.array_equal(fids.cpu().numpy(), ofids)
+
+
+def test_isect_sort_strategies_agree_large():
+    """Both strategies on an M2-sized random workload (~1M isects)."""
+    import gsplat_hip
+    from gsplat_hip import _wrapper
+    g = torch.Generator(device=DEV).manual_seed(3)
+    C, N, ts, tw, th = 2, 200_000, 16, 120, 68
+    m2 = torch.rand(C, N, 2, device=DEV, generator=g) * torch.tensor([tw * ts, th * ts], device=DEV)
+    r = (torch.rand(C, N, device=DEV, generator=g) ** 4 * 60).int()
+    d = torch.rand(C, N, device=DEV, generator=g) * 10
+    d[:, ::7] = 1.0  # ties
+    old = _wrapper.ISECT_SORT
+    try:
+        out = {}
+        for mode in ("depth_first", "full"):
+            _wrapper.ISECT_SORT = mode
+            out[mode] = gsplat_hip.isect_tiles(m2, r, d, ts, tw, th)
+    finally:
+        _wrapper.ISECT_SORT = old
+    for a, b in zip(out["depth_first"], out["full"]):
+        assert torch.equal(a, b)
+    assert out["full"][1].numel() > 100_000
 
 
 # ------------------------------------------------------------ rasterize
