@@ -298,8 +298,10 @@ int rasterize16_fwd(int C, int D, int W, int H, int tw, int th, const float *mea
                     const float *conics, const float *colors, const float *opacities,
                     const float *backgrounds, const uint8_t *masks, const int32_t *offsets,
                     int64_t n_isects, const int32_t *flatten_ids, float *render_colors,
-                    float *render_alphas, int32_t *last_ids, hipStream_t st);
-int64_t rasterize16_bwd_workspace(int64_t G, int D, bool absgrad);
+                    float *render_alphas, int32_t *last_ids, void *state, int64_t state_bytes,
+                    hipStream_t st);
+int64_t rasterize16_fwd_state_bytes(int D, int64_t n_isects);
+int64_t rasterize16_bwd_workspace(int64_t G, int D, bool absgrad, int n_tiles, int64_t n_isects);
 int rasterize16_bwd(int C, int64_t G, int D, int W, int H, int tw, int th,
                     const float *means2d, const float *conics, const float *colors,
                     const float *opacities, const float *backgrounds, const uint8_t *masks,
@@ -307,7 +309,8 @@ int rasterize16_bwd(int C, int64_t G, int D, int W, int H, int tw, int th,
                     const float *render_alphas, const int32_t *last_ids,
                     const float *v_render_colors, const float *v_render_alphas,
                     float *v_means2d, float *v_conics, float *v_colors, float *v_opacities,
-                    float *v_abs, void *workspace, hipStream_t st);
+                    float *v_abs, const float *render_colors, const void *state,
+                    int64_t state_bytes, void *workspace, hipStream_t st);
 }  // namespace gs
 
 using namespace gs;
@@ -316,10 +319,21 @@ extern "C" int gsplat_hip_rasterize_supported_channels(int D) { return supported
 
 // 16x16 tiles (the gsplat default) run the wave-per-tile kernels of
 // rasterize16.hip; other tile sizes run the workgroup-per-tile kernels here.
-extern "C" int64_t gsplat_hip_rasterize_bwd_workspace_bytes(int64_t n_gaussians, int D,
-                                                            int tile_size, int absgrad) {
+extern "C" int64_t gsplat_hip_rasterize_fwd_state_bytes(int C, int D, int tile_size,
+                                                        int tile_width, int tile_height,
+                                                        int64_t n_isects) {
+  (void)C; (void)tile_width; (void)tile_height;
   if (tile_size != 16 || !supported_channels(D)) return 0;
-  return rasterize16_bwd_workspace(n_gaussians, D, absgrad != 0);
+  return rasterize16_fwd_state_bytes(D, n_isects);
+}
+
+extern "C" int64_t gsplat_hip_rasterize_bwd_workspace_bytes(int64_t n_gaussians, int D,
+                                                            int tile_size, int absgrad, int C,
+                                                            int tile_width, int tile_height,
+                                                            int64_t n_isects) {
+  if (tile_size != 16 || !supported_channels(D)) return 0;
+  return rasterize16_bwd_workspace(n_gaussians, D, absgrad != 0, C * tile_width * tile_height,
+                                   n_isects);
 }
 
 static int check_common(int C, int D, int W, int H, int ts, int tw, int th) {
@@ -340,7 +354,8 @@ extern "C" int gsplat_hip_rasterize_fwd(int C, int D, int width, int height, int
                                         const uint8_t *masks, const int32_t *isect_offsets,
                                         int64_t n_isects, const int32_t *flatten_ids,
                                         float *render_colors, float *render_alphas,
-                                        int32_t *last_ids, void *stream) {
+                                        int32_t *last_ids, void *state, int64_t state_bytes,
+                                        void *stream) {
   if (int e = check_common(C, D, width, height, tile_size, tile_width, tile_height)) return e;
   if ((int64_t)C * tile_width * tile_height == 0) return 0;
   RasterArgs a{};
@@ -354,7 +369,7 @@ extern "C" int gsplat_hip_rasterize_fwd(int C, int D, int width, int height, int
   if (tile_size == 16)
     return rasterize16_fwd(C, D, width, height, tile_width, tile_height, means2d, conics, colors,
                            opacities, backgrounds, masks, isect_offsets, n_isects, flatten_ids,
-                           render_colors, render_alphas, last_ids, st);
+                           render_colors, render_alphas, last_ids, state, state_bytes, st);
   const int thr = block_threads(tile_size);
   switch (D) {
     case 1: return launch_fwd<1>(a, thr, st);
@@ -376,13 +391,14 @@ extern "C" int gsplat_hip_rasterize_bwd(
     const int32_t *isect_offsets, int64_t n_isects, const int32_t *flatten_ids,
     const float *render_alphas, const int32_t *last_ids, const float *v_render_colors,
     const float *v_render_alphas, float *v_means2d, float *v_conics, float *v_colors,
-    float *v_opacities, float *v_means2d_abs, void *workspace, int64_t workspace_bytes,
-    void *stream) {
+    float *v_opacities, float *v_means2d_abs, const float *render_colors, const void *state,
+    int64_t state_bytes, void *workspace, int64_t workspace_bytes, void *stream) {
   if (int e = check_common(C, D, width, height, tile_size, tile_width, tile_height)) return e;
   hipStream_t st = (hipStream_t)stream;
   const size_t G = (size_t)n_gaussians;
   if (tile_size == 16) {
-    const int64_t need = rasterize16_bwd_workspace(n_gaussians, D, v_means2d_abs != nullptr);
+    const int64_t need = rasterize16_bwd_workspace(n_gaussians, D, v_means2d_abs != nullptr,
+                                                   C * tile_width * tile_height, n_isects);
     GS_REQUIRE(workspace_bytes >= need && (need == 0 || workspace),
                "rasterize_bwd: workspace of %lld bytes needed, %lld given", (long long)need,
                (long long)workspace_bytes);
@@ -390,7 +406,7 @@ extern "C" int gsplat_hip_rasterize_bwd(
                            conics, colors, opacities, backgrounds, masks, isect_offsets,
                            n_isects, flatten_ids, render_alphas, last_ids, v_render_colors,
                            v_render_alphas, v_means2d, v_conics, v_colors, v_opacities,
-                           v_means2d_abs, workspace, st);
+                           v_means2d_abs, render_colors, state, state_bytes, workspace, st);
   }
   GS_HIP(hipMemsetAsync(v_means2d, 0, sizeof(float) * 2 * G, st));
   GS_HIP(hipMemsetAsync(v_conics, 0, sizeof(float) * 3 * G, st));

@@ -22,9 +22,13 @@
 #include "common.h"
 #include "../../include/gsplat_hip.h"
 
+#include <stdio.h>
 #include <stdlib.h>
 
 namespace gs {
+static uint64_t *g_timeline = nullptr;
+static int64_t g_timeline_waves = 0;
+
 namespace r16 {
 
 constexpr int kTS = 16;
@@ -48,27 +52,43 @@ GS_INLINE float swap16_sum(float a, float b) {
   return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
-// Reduce-scatter of 16 per-lane values over the wave: returns, in every lane,
-// the wave-wide total of value (lane >> 2).
-GS_INLINE float reduce_scatter16(const float *v, int lane) {
-  float w[8], x[4], y[2];
+// Reduce-scatter of N <= 16 per-lane values over the wave: every lane ends
+// with the wave-wide total of field rs_field(lane).  Fields are paired
+// adjacently at each halving (lane bits 5, 4, 3, 2 choose the half), so an
+// odd count costs no padded swaps: 9 fields take 5 + 3 + 2 + 1 combining
+// steps plus two quad adds.
+// a[i] for i < M, else 0 (index clamped so that no access is out of range)
+template <int M>
+GS_INLINE float pick(const float (&a)[M], int i) {
+  return i < M ? a[i < M ? i : 0] : 0.f;
+}
+
+template <int N>
+GS_INLINE float reduce_scatter(const float *v, int lane) {
+  static_assert(N >= 1 && N <= 16, "reduce_scatter: 1..16 fields");
+  constexpr int N1 = (N + 1) / 2, N2 = (N1 + 1) / 2, N3 = (N2 + 1) / 2;
+  float w[N1], x[N2], y[N3];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) w[i] = swap32_sum(v[i], v[i + 8]);  // lane ^ 32
+  for (int i = 0; i < N1; ++i) w[i] = swap32_sum(v[2 * i], 2 * i + 1 < N ? v[2 * i + 1] : 0.f);
 #pragma unroll
-  for (int i = 0; i < 4; ++i) x[i] = swap16_sum(w[i], w[i + 4]);  // lane ^ 16
+  for (int i = 0; i < N2; ++i) x[i] = swap16_sum(w[2 * i], pick(w, 2 * i + 1));
   const bool b3 = lane & 8, b2 = lane & 4;
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {  // row mirror pairs lanes across bit 3
-    const float keep = b3 ? x[i + 2] : x[i];
-    const float send = b3 ? x[i] : x[i + 2];
-    y[i] = keep + dpp<0x140>(send);
+  for (int i = 0; i < N3; ++i) {  // row mirror pairs lanes across bit 3
+    const float lo = x[2 * i], hi = pick(x, 2 * i + 1);
+    y[i] = (b3 ? hi : lo) + dpp<0x140>(b3 ? lo : hi);
   }
-  const float keep = b2 ? y[1] : y[0];  // half-row mirror pairs across bit 2
-  const float send = b2 ? y[0] : y[1];
-  float z = keep + dpp<0x141>(send);
+  const float lo = y[0], hi = pick(y, 1);  // half-row mirror: bit 2
+  float z = (b2 ? hi : lo) + dpp<0x141>(b2 ? lo : hi);
   z += dpp<0xB1>(z);  // quad lane ^ 1
   z += dpp<0x4E>(z);  // quad lane ^ 2
   return z;
+}
+
+// The field whose total lane `lane` holds after reduce_scatter.
+GS_INLINE int rs_field(int lane) {
+  return ((lane >> 5) & 1) | (((lane >> 4) & 1) << 1) | (((lane >> 3) & 1) << 2) |
+         (((lane >> 2) & 1) << 3);
 }
 
 struct Args {
@@ -82,16 +102,29 @@ struct Args {
   const float *v_render_colors, *v_render_alphas;
   float *packed;  // [G][S] gradient rows (backward)
   int S;
+  // Chunk states (see "Chunked backward"): slot s = boundary isect index / L
+  // holds T[256] then acc[D][256] of the tile's pixels before that isect.
+  float *state;
+  int L;  // chunk length in isects (multiple of 64); 0 = no chunking
+  const int2 *items;  // backward work items (tile, chunk) and their count
+  const int32_t *n_items;
+  const float *render_colors_in;  // backward: forward colours (for suffix sums)
+  int dbg;  // experiments only (GSPLAT_HIP_DBG): bit 0 = backward skips its atomics
+  uint64_t *timeline;  // debug: per-wave (start, end) s_memrealtime stamps or null
 };
 
-template <int D>
-struct WaveStage {
-  float2 xy[64];
-  float4 con[64];
-  float col[64][D];
-  int32_t idx[64];  // global isect index
-  int32_t gid[64];
-};
+// Debug timeline (gsplat_hip_debug_set_timeline): lane 0 of every wave stores
+// its start/end stamps of the 100 MHz constant clock into its own slots.
+GS_INLINE uint64_t tl_now(const Args &a) {
+  return a.timeline ? __builtin_amdgcn_s_memrealtime() : 0;
+}
+GS_INLINE void tl_store(const Args &a, uint64_t t0, int lane) {
+  if (a.timeline && lane == 0) {
+    const int64_t w = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    a.timeline[2 * w] = t0;
+    a.timeline[2 * w + 1] = __builtin_amdgcn_s_memrealtime();
+  }
+}
 
 // Minimum over the rectangle [x0,x1]x[y0,y1] of
 //   q(dx,dy) = 0.5*(a dx^2 + c dy^2) + b dx dy,  (dx,dy) = (mx - x, my - y).
@@ -104,313 +137,428 @@ GS_INLINE float rect_min_sigma(float mx, float my, float a, float b, float c, fl
   const float dyl = my - y1, dyh = my - y0;
   auto q = [&](float dx, float dy) { return 0.5f * (a * dx * dx + c * dy * dy) + b * dx * dy; };
   float m = 3.0e38f;
+  // approximate reciprocals: an argmin off by an ulp moves q only to second
+  // order, far inside the caller's margin
+  const float rc = __builtin_amdgcn_rcpf(c), ra = __builtin_amdgcn_rcpf(a);
   // vertical edges: dx fixed, best dy = -b dx / c clamped
   for (int e = 0; e < 2; ++e) {
     const float dx = e ? dxh : dxl;
-    const float dy = fminf(fmaxf(-b * dx / c, dyl), dyh);
+    const float dy = fminf(fmaxf(-b * dx * rc, dyl), dyh);
     m = fminf(m, q(dx, dy));
   }
   for (int e = 0; e < 2; ++e) {
     const float dy = e ? dyh : dyl;
-    const float dx = fminf(fmaxf(-b * dy / a, dxl), dxh);
+    const float dx = fminf(fmaxf(-b * dy * ra, dxl), dxh);
     m = fminf(m, q(dx, dy));
   }
   return fmaxf(m, 0.f);
 }
 
-// Geometry of one wave: PPL pixels per lane, WPT = 4 / PPL waves share a
-// tile, each owning a 16 x (4*PPL) strip; lane l owns column (l & 15) and
-// rows strip_y0 + PPL*(l >> 4) + p, p < PPL.
-template <int PPL>
+// Gaussian record as staged in LDS, one per kept isect, read back as float4s
+// with one wave-uniform address:
+//   [0] x  [1] y  [2..4] conic terms  [5] opacity  [6] isect index
+//   forward:  [7 .. 7+D) colour              (D = 3: 40 B = b128 + b128 + b64)
+//   backward: [7] Gaussian id, [8 .. 8+D) colour
+// The forward stores the conic pre-scaled for exp2: (0.5 a, b, 0.5 c) * log2(e),
+// so sigma * log2(e) is three FMAs and the exponential is a bare v_exp_f32.
+template <int D, bool FWD>
+struct Rec {
+  static constexpr int C0 = FWD ? 7 : 8;  // first colour slot
+  static constexpr int NF = ((C0 + D + 3) / 4) * 4;  // floats per record
+  static constexpr int N4 = NF / 4;
+};
+
+constexpr float kLog2e = 1.4426950408889634f;
+
+// Attributes of one gathered record (registers of one lane).
+template <int D>
+struct Attr {
+  int32_t g;
+  float2 xy;
+  float3 con;
+  float op;
+  float col[D];
+};
+
+// Unconditional (the caller clamps the isect index into the tile's range and
+// masks the lanes past it), so the loads stay in flight across the batch.
+template <int D>
+GS_INLINE void load_attr(const Args &a, int32_t g, Attr<D> &at) {
+  at.g = g;
+  at.xy = *reinterpret_cast<const float2 *>(a.means2d + 2 * (int64_t)g);
+  const float *cn = a.conics + 3 * (int64_t)g;
+  at.con = make_float3(cn[0], cn[1], cn[2]);
+  at.op = a.opacities[g];
+  const float *cl = a.colors + (int64_t)g * D;
+#pragma unroll
+  for (int d = 0; d < D; ++d) at.col[d] = cl[d];
+}
+
+// Strip culling: keep iff some pixel centre of [x0,x1]x[y0,y1] can reach
+// opacity * exp(-sigma) >= 1/255 (margin 0.02 absorbs float rounding of the
+// per-pixel sigma and the exponential).
+template <int D>
+GS_INLINE bool keep_attr(const Attr<D> &at, float x0, float x1, float y0, float y1) {
+  if (!(at.op >= kAlphaMin)) return false;  // alpha <= opacity < 1/255 everywhere
+  const float ms = rect_min_sigma(at.xy.x, at.xy.y, at.con.x, at.con.y, at.con.z, x0, x1, y0, y1);
+  return ms <= 0.69314718f * __builtin_amdgcn_logf(255.f * at.op) + 0.02f;
+}
+
+template <int D, bool FWD>
+GS_INLINE void stage_attr(float4 *slot, const Attr<D> &at, int32_t idx) {
+  using R = Rec<D, FWD>;
+  const int32_t g = at.g;
+  float r[R::NF];
+  r[0] = at.xy.x;
+  r[1] = at.xy.y;
+  if (FWD) {
+    r[2] = 0.5f * kLog2e * at.con.x;
+    r[3] = kLog2e * at.con.y;
+    r[4] = 0.5f * kLog2e * at.con.z;
+  } else {
+    r[2] = at.con.x;
+    r[3] = at.con.y;
+    r[4] = at.con.z;
+  }
+  r[5] = at.op;
+  r[6] = __int_as_float(idx);
+  if (!FWD) r[7] = __int_as_float(g);
+#pragma unroll
+  for (int d = 0; d < D; ++d) r[R::C0 + d] = at.col[d];
+#pragma unroll
+  for (int d = R::C0 + D; d < R::NF; ++d) r[d] = 0.f;
+#pragma unroll
+  for (int q = 0; q < R::N4; ++q) slot[q] = make_float4(r[4 * q], r[4 * q + 1], r[4 * q + 2], r[4 * q + 3]);
+}
+
+// WIDE: whole float4s -- the empty asm keeps every component live so the
+// compiler cannot narrow a read to ds_read_b96 (8 LDS cycles per wave against
+// 4 for ds_read_b128, MI355X_MICROARCH.md "LDS").
+template <int D, bool FWD, bool WIDE>
+GS_INLINE void read_rec(const float4 *slot, float (&r)[Rec<D, FWD>::NF]) {
+  constexpr int N4 = Rec<D, FWD>::N4;
+  float4 v[N4];
+#pragma unroll
+  for (int q = 0; q < N4; ++q) v[q] = slot[q];
+#pragma unroll
+  for (int q = 0; q < N4; ++q) {
+    if (WIDE) asm volatile("" ::"v"(v[q].x), "v"(v[q].y), "v"(v[q].z), "v"(v[q].w));
+    r[4 * q] = v[q].x; r[4 * q + 1] = v[q].y; r[4 * q + 2] = v[q].z; r[4 * q + 3] = v[q].w;
+  }
+}
+
+GS_INLINE void wave_sync_lds() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+GS_INLINE int ballot_slot(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+}
+
+// Geometry of one wave: 4 waves share a 16x16 tile, each owning a 16x4
+// strip; lane l owns pixel column (l & 15), row strip_y0 + (l >> 4).
 struct WaveGeom {
-  static constexpr int WPT = 4 / PPL;
-  static constexpr int SH = 4 * PPL;
-  int tile, c, tx, ty, strip;
-  int px, py0;  // this lane's column and first row
+  int tile, c, px, py;
   float x0, x1, y0, y1;  // strip rectangle of pixel centres
 
-  GS_INLINE WaveGeom(const Args &a, int lane) {
+  GS_INLINE WaveGeom(const Args &a, int lane, int tile_) {
     const int w = threadIdx.x >> 6;
-    tile = blockIdx.x * PPL + w / WPT;
-    strip = w % WPT;
+    tile = tile_;
     const int ntile = a.tw * a.th;
     c = tile / ntile;
     const int rem = tile - c * ntile;
-    ty = rem / a.tw;
-    tx = rem - ty * a.tw;
+    const int ty = rem / a.tw, tx = rem - ty * a.tw;
     px = tx * kTS + (lane & 15);
-    py0 = ty * kTS + SH * strip + PPL * (lane >> 4);
+    py = ty * kTS + 4 * w + (lane >> 4);
     x0 = tx * kTS + 0.5f;
     x1 = x0 + (kTS - 1);
-    y0 = ty * kTS + SH * strip + 0.5f;
-    y1 = y0 + (SH - 1);
+    y0 = ty * kTS + 4 * w + 0.5f;
+    y1 = y0 + 3.f;
   }
 };
 
+// Forward.  The gather of batch b+1 (its attributes) and the flatten ids of
+// batch b+2 are in flight while batch b is composited, so a long tile pays
+// the two dependent global-load latencies once, not once per 64 isects.
 template <int D>
-GS_INLINE bool stage_record(const Args &a, int64_t j, float x0, float x1, float y0, float y1,
-                            float2 &xy, float4 &con, float (&col)[D], int32_t &g) {
-  g = a.flatten_ids[j];
-  xy = *reinterpret_cast<const float2 *>(a.means2d + 2 * (int64_t)g);
-  const float *cn = a.conics + 3 * (int64_t)g;
-  con = make_float4(cn[0], cn[1], cn[2], a.opacities[g]);
-  const float *cl = a.colors + (int64_t)g * D;
-#pragma unroll
-  for (int d = 0; d < D; ++d) col[d] = cl[d];
-  if (!(con.w >= kAlphaMin)) return false;  // alpha <= opacity < 1/255 everywhere
-  const float ms = rect_min_sigma(xy.x, xy.y, con.x, con.y, con.z, x0, x1, y0, y1);
-  // keep iff some pixel can have opacity*exp(-sigma) >= 1/255 (margin 0.02
-  // absorbs float rounding of the per-pixel sigma and __expf)
-  return ms <= 0.69314718f * __builtin_amdgcn_logf(255.f * con.w) + 0.02f;
-}
-
-template <int D, int PPL>
 __global__ void __launch_bounds__(256) fwd_kernel(Args a) {
-  __shared__ WaveStage<D> stage_all[4];
+  using R = Rec<D, true>;
+  constexpr int NF = R::NF, N4 = R::N4;
+  __shared__ float4 stage_all[4][64 * N4];
   const int lane = threadIdx.x & 63;
-  WaveStage<D> &st = stage_all[threadIdx.x >> 6];
-  const WaveGeom<PPL> geo(a, lane);
-  if (geo.tile >= a.n_tiles) return;
+  float4 *st = stage_all[threadIdx.x >> 6];
+  const uint64_t t_start = tl_now(a);
+  const WaveGeom geo(a, lane, blockIdx.x);
   const int tile = geo.tile, c = geo.c;
-  const float x0 = geo.x0, x1 = geo.x1, y0 = geo.y0, y1 = geo.y1;
-  float fx[PPL], fy[PPL];
-  bool inside[PPL];
-#pragma unroll
-  for (int p = 0; p < PPL; ++p) {
-    const int px = geo.px, py = geo.py0 + p;
-    inside[p] = px < a.W && py < a.H;
-    fx[p] = (float)px + 0.5f;
-    fy[p] = (float)py + 0.5f;
-  }
+  const bool inside = geo.px < a.W && geo.py < a.H;
+  const float fx = (float)geo.px + 0.5f, fy = (float)geo.py + 0.5f;
   const int64_t start = a.offsets[tile];
   const int64_t end = (tile == a.n_tiles - 1) ? a.n_isects : (int64_t)a.offsets[tile + 1];
-
-  float T[PPL];
-  float acc[PPL][D];
-#pragma unroll
-  for (int p = 0; p < PPL; ++p)
-#pragma unroll
-    for (int d = 0; d < D; ++d) acc[p][d] = 0.f;
-  int32_t last[PPL];
   const bool skip_tile = a.masks && a.masks[tile];
+
+  float acc[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d) acc[d] = 0.f;
+  int32_t last = 0;
   // A terminated (or outside) pixel is encoded by a negative T: |T| is its
-  // final transmittance.  Keeps the per-pixel state in plain floats.
-#pragma unroll
-  for (int p = 0; p < PPL; ++p) {
-    T[p] = (!inside[p] || skip_tile) ? -1.f : 1.f;
-    last[p] = 0;
-  }
-  auto any_alive = [&]() {
-    bool al = false;
-#pragma unroll
-    for (int p = 0; p < PPL; ++p) al |= T[p] > 0.f;
-    return al;
-  };
+  // final transmittance.
+  float T = (!inside || skip_tile) ? -1.f : 1.f;
 
-  for (int64_t b0 = start; b0 < end && !skip_tile; b0 += 64) {
-    if (__ballot(any_alive()) == 0) break;
-    const int64_t j = b0 + lane;
-    float2 xy;
-    float4 con;
-    float col[D];
-    int32_t g = 0;
-    bool keep = false;
-    if (j < end) keep = stage_record<D>(a, j, x0, x1, y0, y1, xy, con, col, g);
-    const uint64_t m = __ballot(keep);
-    const int slot = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                               __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
-    const int cnt = __popcll(m);
-    if (keep) {
-      st.xy[slot] = xy;
-      st.con[slot] = con;
+  if (!skip_tile && start < end) {
+    // flatten id of lane `lane` of the batch at b0, clamped into the range
+    auto id_at = [&](int64_t b0) -> int32_t {
+      return a.flatten_ids[min(b0 + lane, end - 1)];
+    };
+    bool done = false;
+    // composite one staged batch (cnt records), checking every 16 records
+    // whether the strip is still alive
+    auto composite = [&](int cnt) {
+      for (int kb = 0; kb < cnt; kb += 16) {
+        const int ke = min(cnt, kb + 16);
+#pragma unroll 2
+        for (int k = kb; k < ke; ++k) {
+          float r[NF];
+          read_rec<D, true, false>(st + k * N4, r);
+          const float dx = r[0] - fx, dy = r[1] - fy;
+          // sigma * log2(e) with the pre-scaled conic
+          const float s2 = dx * (r[2] * dx + r[3] * dy) + r[4] * dy * dy;
+          const float alpha = fminf(kAlphaMax, r[5] * __builtin_amdgcn_exp2f(-s2));
+          const float nT = T * (1.f - alpha);
+          const bool hit = (s2 >= 0.f) & (alpha >= kAlphaMin);
+          // dead lanes have T < 0, so nT < 0 and `ok` is false for them
+          const bool ok = hit & (nT > kTMin);
+          const bool term = hit & (nT <= kTMin) & (T > 0.f);  // exclusive stop: not blended
+          const float vis = ok ? alpha * T : 0.f;
 #pragma unroll
-      for (int d = 0; d < D; ++d) st.col[slot][d] = col[d];
-      st.idx[slot] = (int32_t)j;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    for (int k = 0; k < cnt; ++k) {
-      // wave-uniform record (broadcast LDS reads)
-      const float2 gxy = st.xy[k];
-      const float4 cn = st.con[k];
-      const int32_t gidx = st.idx[k];
-      float gc[D];
-#pragma unroll
-      for (int d = 0; d < D; ++d) gc[d] = st.col[k][d];
-      // branch-free per pixel: every update is a select, so the four pixels
-      // of a lane cost straight-line VALU with no exec-mask juggling
-#pragma unroll
-      for (int p = 0; p < PPL; ++p) {
-        const float dx = gxy.x - fx[p], dy = gxy.y - fy[p];
-        const float sigma = 0.5f * (cn.x * dx * dx + cn.z * dy * dy) + cn.y * dx * dy;
-        const float alpha = fminf(kAlphaMax, cn.w * __expf(-sigma));
-        const float Tp = T[p];
-        const bool hit = (Tp > 0.f) & (sigma >= 0.f) & (alpha >= kAlphaMin);
-        const float nT = Tp * (1.f - alpha);
-        const bool term = hit & (nT <= kTMin);  // exclusive stop: not blended
-        const bool ok = hit & (nT > kTMin);
-        const float vis = ok ? alpha * Tp : 0.f;
-#pragma unroll
-        for (int d = 0; d < D; ++d) acc[p][d] += vis * gc[d];
-        T[p] = ok ? nT : (term ? -Tp : Tp);
-        last[p] = ok ? gidx : last[p];
+          for (int d = 0; d < D; ++d) acc[d] += vis * r[R::C0 + d];
+          T = ok ? nT : (term ? -T : T);
+          last = ok ? __float_as_int(r[6]) : last;
+        }
+        if (__ballot(T > 0.f) == 0) {
+          done = true;
+          return;
+        }
       }
-      if ((k & 15) == 15 && __ballot(any_alive()) == 0) break;
+    };
+    auto stage = [&](const Attr<D> &at, int64_t b0) -> int {
+      const bool keep = (b0 + lane < end) && keep_attr<D>(at, geo.x0, geo.x1, geo.y0, geo.y1);
+      const uint64_t m = __ballot(keep);
+      if (keep) stage_attr<D, true>(st + ballot_slot(m) * N4, at, (int32_t)(b0 + lane));
+      wave_sync_lds();
+      return __popcll(m);
+    };
+    // two attribute buffers in alternation: while batch b is composited from
+    // one, the other receives batch b+1, and the ids of batch b+2 load
+    // chunk boundaries (isect index start + m*L, m >= 1): store the pixel
+    // state there for the chunked backward
+    const int64_t L = a.L;
+    auto save_state = [&](int64_t bidx) {
+      float *sl = a.state + (bidx / L) * (int64_t)(kTS * kTS * (1 + D));
+      const int p = (threadIdx.x >> 6) * 64 + lane;  // pixel of the tile, row-major
+      sl[p] = T;
+#pragma unroll
+      for (int d = 0; d < D; ++d) sl[(1 + d) * kTS * kTS + p] = acc[d];
+    };
+    const bool chunked = a.state && L > 0 && end - start > L;
+    Attr<D> A, B;
+    load_attr<D>(a, id_at(start), A);
+    int32_t g_n = id_at(start + 64);
+    int64_t b0 = start;
+    while (b0 < end) {
+      if (__ballot(T > 0.f) == 0) break;
+      if (chunked && b0 > start && (b0 - start) % L == 0) save_state(b0);
+      load_attr<D>(a, g_n, B);
+      g_n = id_at(b0 + 128);
+      composite(stage(A, b0));
+      wave_sync_lds();
+      b0 += 64;
+      if (done || b0 >= end) break;
+      if (chunked && (b0 - start) % L == 0) save_state(b0);
+      load_attr<D>(a, g_n, A);
+      g_n = id_at(b0 + 128);
+      composite(stage(B, b0));
+      wave_sync_lds();
+      b0 += 64;
+      if (done) break;
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (chunked) {
+      // boundaries the loop did not reach (all pixels finished): final state
+      const int64_t nb = start + ((b0 - start + L - 1) / L) * L;
+      for (int64_t bi = max(nb, start + L); bi < end; bi += L) save_state(bi);
+    }
   }
 
-#pragma unroll
-  for (int p = 0; p < PPL; ++p) {
-    if (!inside[p]) continue;
-    const int64_t pix = ((int64_t)c * a.H + geo.py0 + p) * a.W + geo.px;
+  if (inside) {
+    const int64_t pix = ((int64_t)c * a.H + geo.py) * a.W + geo.px;
     float *oc = a.render_colors + pix * D;
 #pragma unroll
     for (int d = 0; d < D; ++d) {
       const float bg = a.backgrounds ? a.backgrounds[c * D + d] : 0.f;
-      oc[d] = acc[p][d] + fabsf(T[p]) * bg;
+      oc[d] = acc[d] + fabsf(T) * bg;
     }
-    a.render_alphas[pix] = 1.f - fabsf(T[p]);
-    a.last_ids[pix] = last[p];
+    a.render_alphas[pix] = 1.f - fabsf(T);
+    a.last_ids[pix] = last;
   }
+  tl_store(a, t_start, lane);
 }
 
-template <int D, bool ABS, int PPL>
+// Backward: batches of 64 isects from the back, same two-deep gather pipeline.
+template <int D, bool ABS>
 __global__ void __launch_bounds__(256) bwd_kernel(Args a) {
+  using R = Rec<D, false>;
+  constexpr int NF = R::NF, N4 = R::N4;
   constexpr int F = D + 6 + (ABS ? 2 : 0);
-  constexpr int NV = (F + 15) / 16;
-  __shared__ WaveStage<D> stage_all[4];
+  constexpr int NV = (F + 15) / 16;  // reduce-scatter groups of <= 16 fields
+  __shared__ float4 stage_all[4][64 * N4];
   const int lane = threadIdx.x & 63;
-  WaveStage<D> &st = stage_all[threadIdx.x >> 6];
-  const WaveGeom<PPL> geo(a, lane);
-  if (geo.tile >= a.n_tiles) return;
-  const int tile = geo.tile, c = geo.c;
-  if (a.masks && a.masks[tile]) return;
-
-  float fx[PPL], fy[PPL], T[PPL], Tf[PPL], Dra[PPL], rD[PPL], bgt[PPL], Drc[PPL][D];
-  int32_t mylast[PPL];
-  int32_t lmax = -1;
-#pragma unroll
-  for (int p = 0; p < PPL; ++p) {
-    const int px = geo.px, py = geo.py0 + p;
-    const bool in = px < a.W && py < a.H;
-    fx[p] = (float)px + 0.5f;
-    fy[p] = (float)py + 0.5f;
-    Tf[p] = 1.f; Dra[p] = 0.f; mylast[p] = -1; rD[p] = 0.f; bgt[p] = 0.f;
-#pragma unroll
-    for (int d = 0; d < D; ++d) Drc[p][d] = 0.f;
-    if (in) {
-      const int64_t pix = ((int64_t)c * a.H + py) * a.W + px;
-      Tf[p] = 1.f - a.render_alphas[pix];
-      Dra[p] = a.v_render_alphas[pix];
-      mylast[p] = a.last_ids[pix];
-#pragma unroll
-      for (int d = 0; d < D; ++d) Drc[p][d] = a.v_render_colors[pix * D + d];
-      if (a.backgrounds) {
-        float s = 0.f;
-#pragma unroll
-        for (int d = 0; d < D; ++d) s += a.backgrounds[c * D + d] * Drc[p][d];
-        bgt[p] = s * Tf[p];
-      }
-    }
-    T[p] = Tf[p];
-    lmax = max(lmax, mylast[p]);
+  float4 *st = stage_all[threadIdx.x >> 6];
+  const uint64_t t_start = tl_now(a);
+  // work item: a whole tile, or chunk k = isects [start + kL, start + (k+1)L)
+  // of a long tile (a.items, see "Chunked backward")
+  int tile = blockIdx.x, k = 0;
+  if (a.items) {
+    if ((int)blockIdx.x >= *a.n_items) return;
+    const int2 it = a.items[blockIdx.x];
+    tile = it.x;
+    k = it.y;
   }
+  const WaveGeom geo(a, lane, tile);
+  const int c = geo.c;
+  if (a.masks && a.masks[tile]) return;
+  const int64_t tstart = a.offsets[tile];
+  const int64_t tend = (tile == a.n_tiles - 1) ? a.n_isects : (int64_t)a.offsets[tile + 1];
+  const int64_t start = a.items ? tstart + (int64_t)k * a.L : tstart;
+  const int64_t cend = a.items ? min(tend, start + a.L) : tend;
+
+  const bool in = geo.px < a.W && geo.py < a.H;
+  const float fx = (float)geo.px + 0.5f, fy = (float)geo.py + 0.5f;
+  float T = 1.f, Tf = 1.f, Dra = 0.f, rD = 0.f, bgt = 0.f, Drc[D];
+  int32_t mylast = -1;
+#pragma unroll
+  for (int d = 0; d < D; ++d) Drc[d] = 0.f;
+  if (in) {
+    const int64_t pix = ((int64_t)c * a.H + geo.py) * a.W + geo.px;
+    Tf = 1.f - a.render_alphas[pix];
+    Dra = a.v_render_alphas[pix];
+    mylast = a.last_ids[pix];
+#pragma unroll
+    for (int d = 0; d < D; ++d) Drc[d] = a.v_render_colors[pix * D + d];
+    float bgv = 0.f;
+    if (a.backgrounds) {
+#pragma unroll
+      for (int d = 0; d < D; ++d) bgv += a.backgrounds[c * D + d] * Drc[d];
+      bgt = bgv * Tf;
+    }
+    T = Tf;
+    if (cend < tend) {
+      // a chunk followed by others: start from the forward's state at the
+      // boundary cend (transmittance; colour accumulated before it), and the
+      // suffix colour sum of everything after it, dotted with dL/dcolour
+      const float *sl = a.state + (cend / a.L) * (int64_t)(kTS * kTS * (1 + D));
+      const int p = (threadIdx.x >> 6) * 64 + lane;
+      T = fabsf(sl[p]);
+      const float *rc = a.render_colors_in + pix * D;
+      float s = 0.f;
+#pragma unroll
+      for (int d = 0; d < D; ++d) s += (rc[d] - sl[(1 + d) * kTS * kTS + p]) * Drc[d];
+      rD = s - bgv * Tf;  // render_colors includes the background term
+    }
+  }
+  const float TfDra = Tf * Dra;
+  int32_t lmax = mylast;
 #pragma unroll
   for (int msk = 32; msk >= 1; msk >>= 1) lmax = max(lmax, __shfl_xor(lmax, msk, 64));
-  const float x0 = geo.x0, x1 = geo.x1, y0 = geo.y0, y1 = geo.y1;
-  const int64_t start = a.offsets[tile];
-  const int64_t tend = (tile == a.n_tiles - 1) ? a.n_isects : (int64_t)a.offsets[tile + 1];
-  const int64_t end = min(tend, (int64_t)lmax + 1);
+  const int64_t end = min(cend, (int64_t)lmax + 1);
 
-  for (int64_t b1 = end; b1 > start; b1 -= 64) {
-    const int64_t b0 = max(start, b1 - 64);
-    const int64_t j = b0 + lane;
-    float2 xy;
-    float4 con;
-    float col[D];
-    int32_t g = 0;
-    bool keep = false;
-    if (j < b1) keep = stage_record<D>(a, j, x0, x1, y0, y1, xy, con, col, g);
-    const uint64_t m = __ballot(keep);
-    const int slot = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                               __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
-    const int cnt = __popcll(m);
-    if (keep) {
-      st.xy[slot] = xy;
-      st.con[slot] = con;
+  if (start < end) {
+    // the batch ending at b1 covers [max(start, b1 - 64), b1); lane l holds
+    // isect b1 - 64 + l (clamped into the range, masked when below start)
+    auto id_at = [&](int64_t b1) -> int32_t {
+      return a.flatten_ids[max(b1 - 64 + lane, start)];
+    };
+    auto stage = [&](const Attr<D> &at, int64_t b1) -> int {
+      const int64_t j = b1 - 64 + lane;
+      const bool keep = (j >= start) && keep_attr<D>(at, geo.x0, geo.x1, geo.y0, geo.y1);
+      const uint64_t m = __ballot(keep);
+      if (keep) stage_attr<D, false>(st + ballot_slot(m) * N4, at, (int32_t)j);
+      wave_sync_lds();
+      return __popcll(m);
+    };
+    auto composite = [&](int cnt) {
+      for (int k = cnt - 1; k >= 0; --k) {
+        float r[NF];
+        read_rec<D, false, true>(st + k * N4, r);
+        const float ca = r[2], cb = r[3], cc = r[4];
+        const int32_t idx = __float_as_int(r[6]);
+        float v[NV * 16];
 #pragma unroll
-      for (int d = 0; d < D; ++d) st.col[slot][d] = col[d];
-      st.idx[slot] = (int32_t)j;
-      st.gid[slot] = g;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    for (int k = cnt - 1; k >= 0; --k) {
-      const float2 gxy = st.xy[k];
-      const float4 cn = st.con[k];
-      const int32_t idx = st.idx[k];
-      float v[NV * 16];
-#pragma unroll
-      for (int f = 0; f < NV * 16; ++f) v[f] = 0.f;
-      float gc[D];
-#pragma unroll
-      for (int d = 0; d < D; ++d) gc[d] = st.col[k][d];
-      bool any = false;
-      // branch-free per pixel (selects instead of divergent `continue`s)
-#pragma unroll
-      for (int p = 0; p < PPL; ++p) {
-        const float dx = gxy.x - fx[p], dy = gxy.y - fy[p];
-        const float sigma = 0.5f * cn.x * dx * dx + 0.5f * cn.z * dy * dy + cn.y * dx * dy;
+        for (int f = 0; f < NV * 16; ++f) v[f] = 0.f;
+        const float dx = r[0] - fx, dy = r[1] - fy;
+        const float sigma = 0.5f * ca * dx * dx + 0.5f * cc * dy * dy + cb * dx * dy;
         const float ex = __expf(-sigma);
-        const float alpha_raw = cn.w * ex;
-        const bool valid = (idx <= mylast[p]) & (sigma >= 0.f) & (alpha_raw >= kAlphaMin);
-        any |= valid;
-        const float alpha = fminf(kAlphaMax, alpha_raw);
+        const float alpha_raw = r[5] * ex;
+        const bool valid = (idx <= mylast) & (sigma >= 0.f) & (alpha_raw >= kAlphaMin);
+        if (__ballot(valid) == 0) continue;
+        const float alpha = __builtin_amdgcn_fmed3f(alpha_raw, -INFINITY, kAlphaMax);  // min
         const float ra = __builtin_amdgcn_rcpf(1.f - alpha);
-        T[p] = valid ? T[p] * ra : T[p];
-        const float w = valid ? alpha * T[p] : 0.f;
+        T = valid ? T * ra : T;
+        const float w = valid ? alpha * T : 0.f;
         float gD = 0.f;
 #pragma unroll
         for (int d = 0; d < D; ++d) {
-          v[d] += w * Drc[p][d];
-          gD += gc[d] * Drc[p][d];
+          v[d] = w * Drc[d];
+          gD += r[R::C0 + d] * Drc[d];
         }
-        rD[p] += gD * w;
-        const float Da_raw = ra * (Tf[p] * Dra[p] + T[p] * gD - rD[p] - bgt[p]);
+        rD += gD * w;
+        const float Da_raw = ra * (TfDra + T * gD - rD - bgt);
         // clamped alpha (> 0.999) has no gradient (rasterize_to_pixels_bwd.py:184-187)
         const float Da = (valid & (alpha_raw <= kAlphaMax)) ? Da_raw : 0.f;
         const float aD = alpha * Da;
-        const float gmx = -aD * (cn.x * dx + cn.y * dy);
-        const float gmy = -aD * (cn.y * dx + cn.z * dy);
-        v[D] += valid ? Da * ex : 0.f;
-        v[D + 1] += gmx;
-        v[D + 2] += gmy;
-        v[D + 3] += -0.5f * aD * dx * dx;
-        v[D + 4] += -aD * dx * dy;
-        v[D + 5] += -0.5f * aD * dy * dy;
+        const float gmx = -aD * (ca * dx + cb * dy);
+        const float gmy = -aD * (cb * dx + cc * dy);
+        v[D] = valid ? Da * ex : 0.f;
+        v[D + 1] = gmx;
+        v[D + 2] = gmy;
+        v[D + 3] = -0.5f * aD * dx * dx;
+        v[D + 4] = -aD * dx * dy;
+        v[D + 5] = -0.5f * aD * dy * dy;
         if (ABS) {
-          v[D + 6] += fabsf(gmx);
-          v[D + 7] += fabsf(gmy);
+          v[D + 6] = fabsf(gmx);
+          v[D + 7] = fabsf(gmy);
+        }
+        float *row = a.packed + (int64_t)__float_as_int(r[7]) * a.S;
+        const int lf = rs_field(lane);
+#pragma unroll
+        for (int q = 0; q < NV; ++q) {
+          constexpr int NQ = F - 16 * (NV - 1);  // fields in the last group
+          const float tot = q < NV - 1 ? reduce_scatter<16>(v + 16 * q, lane)
+                                       : reduce_scatter<NQ>(v + 16 * q, lane);
+          const int field = 16 * q + lf;
+          if ((lane & 3) == 0 && lf < (q < NV - 1 ? 16 : NQ) && tot != 0.f && !(a.dbg & 1))
+            atomic_add_f32(row + field, tot);
         }
       }
-      if (__ballot(any) == 0) continue;
-      float *row = a.packed + (int64_t)st.gid[k] * a.S;
-#pragma unroll
-      for (int q = 0; q < NV; ++q) {
-        const float tot = reduce_scatter16(v + 16 * q, lane);
-        const int field = 16 * q + (lane >> 2);
-        if ((lane & 3) == 0 && field < F && tot != 0.f) atomic_add_f32(row + field, tot);
-      }
+    };
+    Attr<D> A, B;
+    load_attr<D>(a, id_at(end), A);
+    int32_t g_n = id_at(end - 64);
+    for (int64_t b1 = end; b1 > start;) {
+      load_attr<D>(a, g_n, B);
+      g_n = id_at(b1 - 128);
+      composite(stage(A, b1));
+      wave_sync_lds();
+      b1 -= 64;
+      if (b1 <= start) break;
+      load_attr<D>(a, g_n, A);
+      g_n = id_at(b1 - 128);
+      composite(stage(B, b1));
+      wave_sync_lds();
+      b1 -= 64;
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
+  tl_store(a, t_start, lane);
 }
 
 // packed [G][S] -> the autograd tensors
@@ -432,27 +580,102 @@ unpack_kernel(int64_t G, int S, const float *__restrict__ packed, float *__restr
   if (ABS) *reinterpret_cast<float2 *>(v_abs + 2 * g) = make_float2(r[D + 6], r[D + 7]);
 }
 
-}  // namespace r16
-
-// pixels per lane (1: 4 waves per tile; 4: one wave per tile); GSPLAT_HIP_PPL
-// overrides it for experiments.
-static int ppl_choice(int dflt) {
-  static int v = [] {
-    const char *e = getenv("GSPLAT_HIP_PPL");
-    return e ? atoi(e) : 0;
-  }();
-  return (v == 1 || v == 2 || v == 4) ? v : dflt;
+// Backward work items.  A tile with n isects becomes ceil(n / L) items
+// (tile, k); the full-length chunks are listed first and the shorter tails
+// after them, so the longest items start first.  One 1024-lane workgroup.
+__global__ void __launch_bounds__(1024)
+chunk_items_kernel(int n_tiles, const int32_t *__restrict__ offsets, int64_t n_isects, int L,
+                   int2 *__restrict__ items, int32_t *__restrict__ n_items) {
+  __shared__ int wtot[2][16];
+  const int per = (n_tiles + 1023) / 1024;
+  const int t0 = min(n_tiles, (int)threadIdx.x * per), t1 = min(n_tiles, t0 + per);
+  auto len = [&](int t) -> int64_t {
+    const int64_t e = (t == n_tiles - 1) ? n_isects : (int64_t)offsets[t + 1];
+    return e - offsets[t];
+  };
+  int nf = 0, nt = 0;
+  for (int t = t0; t < t1; ++t) {
+    const int64_t n = len(t);
+    nf += (int)(n / L);
+    nt += (n % L) != 0;
+  }
+  // block exclusive scans of nf and nt
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int xf = nf, xt = nt;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int yf = __shfl_up(xf, o, 64), yt = __shfl_up(xt, o, 64);
+    if (lane >= o) {
+      xf += yf;
+      xt += yt;
+    }
+  }
+  if (lane == 63) {
+    wtot[0][w] = xf;
+    wtot[1][w] = xt;
+  }
+  __syncthreads();
+  int bf = 0, bt = 0, F = 0, TT = 0;
+  for (int i = 0; i < 16; ++i) {
+    if (i < w) {
+      bf += wtot[0][i];
+      bt += wtot[1][i];
+    }
+    F += wtot[0][i];
+    TT += wtot[1][i];
+  }
+  int pf = bf + xf - nf, pt = F + bt + xt - nt;
+  for (int t = t0; t < t1; ++t) {
+    const int64_t n = len(t);
+    const int full = (int)(n / L);
+    for (int k = 0; k < full; ++k) items[pf++] = make_int2(t, k);
+    if (n % L) items[pt++] = make_int2(t, full);
+  }
+  if (threadIdx.x == 0) *n_items = F + TT;
 }
 
+}  // namespace r16
+
+// Chunk length in isects for the chunked backward (multiple of 64; 0 turns
+// chunking off).  GSPLAT_HIP_CHUNK overrides it for experiments.
+static int g_chunk = -1;  // -1: not yet read from the environment
+
+static int chunk_len() {
+  if (g_chunk < 0) {
+    const char *e = getenv("GSPLAT_HIP_CHUNK");
+    const int x = e ? atoi(e) : 512;
+    g_chunk = x <= 0 ? 0 : ((x + 63) / 64) * 64;
+  }
+  return g_chunk;
+}
+
+static int64_t state_floats_per_slot(int D) { return (int64_t)r16::kTS * r16::kTS * (1 + D); }
+
+int64_t rasterize16_fwd_state_bytes(int D, int64_t n_isects) {
+  const int L = chunk_len();
+  if (L == 0 || n_isects <= 0) return 0;
+  return (n_isects / L + 1) * state_floats_per_slot(D) * (int64_t)sizeof(float);
+}
+
+static int64_t n_items_bound(int n_tiles, int64_t n_isects) {
+  const int L = chunk_len();
+  return L ? (int64_t)n_tiles + n_isects / L + 1 : (int64_t)n_tiles;
+}
+
+static int dbg_flags() {
+  static const int v = [] { const char *e = getenv("GSPLAT_HIP_DBG"); return e ? atoi(e) : 0; }();
+  return v;
+}
 template <int D>
-int r16_fwd(const r16::Args &a, hipStream_t st) {
-  const int ppl = ppl_choice(1);
-  const int blocks = (a.n_tiles + ppl - 1) / ppl;
-  if (ppl == 1) hipLaunchKernelGGL((r16::fwd_kernel<D, 1>), dim3(blocks), dim3(256), 0, st, a);
-  else if (ppl == 2) hipLaunchKernelGGL((r16::fwd_kernel<D, 2>), dim3(blocks), dim3(256), 0, st, a);
-  else hipLaunchKernelGGL((r16::fwd_kernel<D, 4>), dim3(blocks), dim3(256), 0, st, a);
+int r16_fwd(r16::Args a, hipStream_t st) {
+  hipLaunchKernelGGL((r16::fwd_kernel<D>), dim3(a.n_tiles), dim3(256), 0, st, a);
   GS_CHECK_LAUNCH("rasterize_fwd16");
   return 0;
+}
+
+static size_t packed_bytes(int D, bool absgrad, int64_t G) {
+  const int F = D + 6 + (absgrad ? 2 : 0);
+  return (((size_t)sizeof(float) * ((F + 15) / 16) * 16 * G + 255) / 256) * 256;
 }
 
 template <int D, bool ABS>
@@ -463,14 +686,21 @@ int r16_bwd(r16::Args a, int64_t G, float *v_means2d, float *v_conics, float *v_
   a.packed = reinterpret_cast<float *>(workspace);
   GS_HIP(hipMemsetAsync(a.packed, 0, sizeof(float) * (size_t)a.S * G, st));
   if (a.n_isects > 0) {
-    const int ppl = ppl_choice(1);
-    const int blocks = (a.n_tiles + ppl - 1) / ppl;
-    if (ppl == 1)
-      hipLaunchKernelGGL((r16::bwd_kernel<D, ABS, 1>), dim3(blocks), dim3(256), 0, st, a);
-    else if (ppl == 2)
-      hipLaunchKernelGGL((r16::bwd_kernel<D, ABS, 2>), dim3(blocks), dim3(256), 0, st, a);
-    else
-      hipLaunchKernelGGL((r16::bwd_kernel<D, ABS, 4>), dim3(blocks), dim3(256), 0, st, a);
+    int64_t grid = a.n_tiles;
+    if (a.state && a.L > 0 && a.render_colors_in) {
+      char *w = reinterpret_cast<char *>(workspace) + packed_bytes(D, ABS, G);
+      a.n_items = reinterpret_cast<int32_t *>(w);
+      a.items = reinterpret_cast<int2 *>(w + 256);
+      hipLaunchKernelGGL(r16::chunk_items_kernel, dim3(1), dim3(1024), 0, st, a.n_tiles,
+                         a.offsets, a.n_isects, a.L, const_cast<int2 *>(a.items),
+                         const_cast<int32_t *>(a.n_items));
+      grid = n_items_bound(a.n_tiles, a.n_isects);
+    } else {
+      a.state = nullptr;
+      a.items = nullptr;
+      a.n_items = nullptr;
+    }
+    hipLaunchKernelGGL((r16::bwd_kernel<D, ABS>), dim3((unsigned)grid), dim3(256), 0, st, a);
     GS_CHECK_LAUNCH("rasterize_bwd16");
   }
   if (G > 0) {
@@ -485,13 +715,21 @@ int rasterize16_fwd(int C, int D, int W, int H, int tw, int th, const float *mea
                     const float *conics, const float *colors, const float *opacities,
                     const float *backgrounds, const uint8_t *masks, const int32_t *offsets,
                     int64_t n_isects, const int32_t *flatten_ids, float *render_colors,
-                    float *render_alphas, int32_t *last_ids, hipStream_t st) {
+                    float *render_alphas, int32_t *last_ids, void *state, int64_t state_bytes,
+                    hipStream_t st) {
   r16::Args a{};
   a.C = C; a.W = W; a.H = H; a.tw = tw; a.th = th; a.n_tiles = C * tw * th;
   a.n_isects = n_isects;
+  a.timeline = (g_timeline && g_timeline_waves >= 4 * (int64_t)a.n_tiles) ? g_timeline : nullptr;
   a.means2d = means2d; a.conics = conics; a.colors = colors; a.opacities = opacities;
   a.backgrounds = backgrounds; a.masks = masks; a.offsets = offsets; a.flatten_ids = flatten_ids;
   a.render_colors = render_colors; a.render_alphas = render_alphas; a.last_ids = last_ids;
+  const int64_t need = rasterize16_fwd_state_bytes(D, n_isects);
+  GS_REQUIRE(state_bytes == 0 || state_bytes >= need,
+             "rasterize_fwd: state of %lld bytes needed, %lld given", (long long)need,
+             (long long)state_bytes);
+  a.L = chunk_len();
+  a.state = (state && need > 0) ? reinterpret_cast<float *>(state) : nullptr;
   switch (D) {
     case 1: return r16_fwd<1>(a, st);
     case 2: return r16_fwd<2>(a, st);
@@ -504,9 +742,10 @@ int rasterize16_fwd(int C, int D, int W, int H, int tw, int th, const float *mea
   GS_REQUIRE(false, "rasterize16_fwd: unsupported channels %d", D);
 }
 
-int64_t rasterize16_bwd_workspace(int64_t G, int D, bool absgrad) {
-  const int F = D + 6 + (absgrad ? 2 : 0);
-  return (int64_t)sizeof(float) * ((F + 15) / 16) * 16 * G;
+int64_t rasterize16_bwd_workspace(int64_t G, int D, bool absgrad, int n_tiles, int64_t n_isects) {
+  int64_t b = (int64_t)packed_bytes(D, absgrad, G);
+  if (chunk_len()) b += 256 + (int64_t)sizeof(int2) * n_items_bound(n_tiles, n_isects);
+  return b;
 }
 
 int rasterize16_bwd(int C, int64_t G, int D, int W, int H, int tw, int th,
@@ -516,15 +755,24 @@ int rasterize16_bwd(int C, int64_t G, int D, int W, int H, int tw, int th,
                     const float *render_alphas, const int32_t *last_ids,
                     const float *v_render_colors, const float *v_render_alphas,
                     float *v_means2d, float *v_conics, float *v_colors, float *v_opacities,
-                    float *v_abs, void *workspace, hipStream_t st) {
+                    float *v_abs, const float *render_colors, const void *state,
+                    int64_t state_bytes, void *workspace, hipStream_t st) {
   r16::Args a{};
   a.C = C; a.W = W; a.H = H; a.tw = tw; a.th = th; a.n_tiles = C * tw * th;
   a.n_isects = n_isects;
+  a.timeline = (g_timeline && g_timeline_waves >= 4 * n_items_bound(a.n_tiles, n_isects))
+                   ? g_timeline : nullptr;
   a.means2d = means2d; a.conics = conics; a.colors = colors; a.opacities = opacities;
   a.backgrounds = backgrounds; a.masks = masks; a.offsets = offsets; a.flatten_ids = flatten_ids;
   a.render_alphas = const_cast<float *>(render_alphas);
   a.last_ids = const_cast<int32_t *>(last_ids);
   a.v_render_colors = v_render_colors; a.v_render_alphas = v_render_alphas;
+  const int64_t need = rasterize16_fwd_state_bytes(D, n_isects);
+  a.L = chunk_len();
+  a.state = (state && need > 0 && state_bytes >= need)
+                ? const_cast<float *>(reinterpret_cast<const float *>(state)) : nullptr;
+  a.render_colors_in = render_colors;
+  a.dbg = dbg_flags();
   const bool ab = v_abs != nullptr;
 #define GS_R16B(DD)                                                                            \
   case DD:                                                                                     \
@@ -538,3 +786,14 @@ int rasterize16_bwd(int C, int64_t G, int D, int W, int H, int tw, int th,
 }
 
 }  // namespace gs
+
+extern "C" int gsplat_hip_debug_set_chunk(int isects) {
+  gs::g_chunk = isects <= 0 ? 0 : ((isects + 63) / 64) * 64;
+  return gs::g_chunk;
+}
+
+extern "C" int gsplat_hip_debug_set_timeline(uint64_t *device_buffer, int64_t capacity_waves) {
+  gs::g_timeline = device_buffer;
+  gs::g_timeline_waves = device_buffer ? capacity_waves : 0;
+  return 0;
+}

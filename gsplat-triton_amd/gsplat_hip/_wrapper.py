@@ -397,21 +397,26 @@ class _RasterizeToPixels(torch.autograd.Function):
         render_colors = torch.empty((C, height, width, D), device=dev)
         render_alphas = torch.empty((C, height, width, 1), device=dev)
         last_ids = torch.empty((C, height, width), dtype=torch.int32, device=dev)
+        # compositing state at the chunk boundaries of long tiles, for the
+        # chunked backward (csrc/rasterize16.hip); empty when not used
+        sb = int(_lib.query("gsplat_hip_rasterize_fwd_state_bytes", C, D, tile_size, tw, th,
+                            flatten_ids.numel()))
+        state = torch.empty(sb // 4, dtype=torch.float32, device=dev)
         with _Timed("rasterize_fwd"):
             _lib.call("gsplat_hip_rasterize_fwd", C, D, width, height, tile_size, tw, th,
                       _ptr(means2d), _ptr(conics), _ptr(colors), _ptr(opacities),
                       _ptr(backgrounds), _ptr(m), _ptr(isect_offsets), flatten_ids.numel(),
                       _ptr(flatten_ids), _ptr(render_colors), _ptr(render_alphas),
-                      _ptr(last_ids), _stream())
+                      _ptr(last_ids), _ptr(state) if sb else 0, sb, _stream())
         ctx.save_for_backward(means2d, conics, colors, opacities, backgrounds, m, isect_offsets,
-                              flatten_ids, render_alphas, last_ids)
+                              flatten_ids, render_alphas, last_ids, render_colors, state)
         ctx.width, ctx.height, ctx.tile_size, ctx.absgrad = width, height, tile_size, absgrad
         return render_colors, render_alphas
 
     @staticmethod
     def backward(ctx, v_render_colors, v_render_alphas):
         (means2d, conics, colors, opacities, backgrounds, m, isect_offsets, flatten_ids,
-         render_alphas, last_ids) = ctx.saved_tensors
+         render_alphas, last_ids, render_colors, state) = ctx.saved_tensors
         C, th, tw = isect_offsets.shape
         D = colors.shape[-1]
         G = opacities.numel()
@@ -423,7 +428,7 @@ class _RasterizeToPixels(torch.autograd.Function):
         v_opacities = torch.empty_like(opacities)
         v_abs = torch.empty_like(means2d) if ctx.absgrad else None
         wsb = int(_lib.query("gsplat_hip_rasterize_bwd_workspace_bytes", G, D, ctx.tile_size,
-                             int(bool(ctx.absgrad))))
+                             int(bool(ctx.absgrad)), C, tw, th, flatten_ids.numel()))
         ws = torch.empty(max(wsb, 4), dtype=torch.uint8, device=means2d.device)
         with _Timed("rasterize_bwd"):
             _lib.call("gsplat_hip_rasterize_bwd", C, G, D, ctx.width, ctx.height, ctx.tile_size,
@@ -431,8 +436,9 @@ class _RasterizeToPixels(torch.autograd.Function):
                       _ptr(backgrounds), _ptr(m), _ptr(isect_offsets), flatten_ids.numel(),
                       _ptr(flatten_ids), _ptr(render_alphas), _ptr(last_ids),
                       _ptr(v_render_colors), _ptr(v_render_alphas), _ptr(v_means2d),
-                      _ptr(v_conics), _ptr(v_colors), _ptr(v_opacities), _ptr(v_abs), _ptr(ws),
-                      wsb, _stream())
+                      _ptr(v_conics), _ptr(v_colors), _ptr(v_opacities), _ptr(v_abs),
+                      _ptr(render_colors), _ptr(state) if state.numel() else 0, state.numel() * 4,
+                      _ptr(ws), wsb, _stream())
         if ctx.absgrad:
             ctx.means2d_in.absgrad = v_abs
         v_backgrounds = None

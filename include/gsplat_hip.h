@@ -140,25 +140,34 @@ int gsplat_hip_isect_offsets(int64_t n_isects, const int64_t *isect_ids, int C, 
  * means2d[G,2] conics[G,3] colors[G,D] opacities[G] (G = C*N or nnz),
  * backgrounds[C,D] or NULL, masks u8[C,th,tw] or NULL (true = skip tile),
  * isect_offsets i32[C,th,tw], flatten_ids i32[n_isects]
- * -> render_colors[C,H,W,D], render_alphas[C,H,W], last_ids i32[C,H,W]. */
+ * -> render_colors[C,H,W,D], render_alphas[C,H,W], last_ids i32[C,H,W],
+ *    and, when `state` is non-NULL, the per-pixel compositing state at every
+ *    chunk boundary of a long tile (gsplat_hip_rasterize_fwd_state_bytes bytes;
+ *    0 bytes = no state) that lets the backward split long tiles into chunks
+ *    that run in parallel.  Keep it for the matching gsplat_hip_rasterize_bwd. */
 int gsplat_hip_rasterize_supported_channels(int D);
+int64_t gsplat_hip_rasterize_fwd_state_bytes(int C, int D, int tile_size, int tile_width,
+                                             int tile_height, int64_t n_isects);
 int gsplat_hip_rasterize_fwd(int C, int D, int width, int height, int tile_size, int tile_width,
                              int tile_height, const float *means2d, const float *conics,
                              const float *colors, const float *opacities,
                              const float *backgrounds, const uint8_t *masks,
                              const int32_t *isect_offsets, int64_t n_isects,
                              const int32_t *flatten_ids, float *render_colors,
-                             float *render_alphas, int32_t *last_ids, void *stream);
+                             float *render_alphas, int32_t *last_ids, void *state,
+                             int64_t state_bytes, void *stream);
 
 /* Replaces rasterize_to_pixels_bwd() (gsplat/triton_impl/rasterize_to_pixels_bwd.py:340-457)
  * called from _RasterizeToPixels.backward (_wrapper.py:104-182).
  * -> v_means2d[G,2], v_conics[G,3], v_colors[G,D], v_opacities[G],
  *    v_means2d_abs[G,2] or NULL (absgrad).
- * `workspace` must hold gsplat_hip_rasterize_bwd_workspace_bytes(G, D,
- * tile_size, absgrad) bytes (the packed per-Gaussian gradient rows the 16x16
- * kernel accumulates into; 0 bytes for other tile sizes). */
+ * `workspace` must hold gsplat_hip_rasterize_bwd_workspace_bytes(...) bytes
+ * (packed per-Gaussian gradient rows and the chunk work list of the 16x16
+ * kernels; 0 bytes for other tile sizes).  render_colors / state: the forward's
+ * outputs; with state == NULL every tile runs as one work item. */
 int64_t gsplat_hip_rasterize_bwd_workspace_bytes(int64_t n_gaussians, int D, int tile_size,
-                                                 int absgrad);
+                                                 int absgrad, int C, int tile_width,
+                                                 int tile_height, int64_t n_isects);
 int gsplat_hip_rasterize_bwd(int C, int64_t n_gaussians, int D, int width, int height,
                              int tile_size, int tile_width, int tile_height,
                              const float *means2d, const float *conics, const float *colors,
@@ -168,8 +177,21 @@ int gsplat_hip_rasterize_bwd(int C, int64_t n_gaussians, int D, int width, int h
                              const float *render_alphas, const int32_t *last_ids,
                              const float *v_render_colors, const float *v_render_alphas,
                              float *v_means2d, float *v_conics, float *v_colors,
-                             float *v_opacities, float *v_means2d_abs, void *workspace,
-                             int64_t workspace_bytes, void *stream);
+                             float *v_opacities, float *v_means2d_abs,
+                             const float *render_colors, const void *state,
+                             int64_t state_bytes, void *workspace, int64_t workspace_bytes,
+                             void *stream);
+
+/* Debug/profiling: when device_buffer (u64[2*capacity_waves]) is non-NULL, the
+ * 16x16 rasterizer kernels store each wave's (start, end) s_memrealtime stamps
+ * (100 MHz) at [2w, 2w+1], w = global wave index (4 waves per tile).  Not part
+ * of the reference surface; NULL disables (the default). */
+int gsplat_hip_debug_set_timeline(uint64_t *device_buffer, int64_t capacity_waves);
+/* Chunk length (isects, rounded up to a multiple of 64; <= 0 disables) of the
+ * chunked 16x16 backward; returns the value in effect.  Default 512, or the
+ * GSPLAT_HIP_CHUNK environment variable.  Forward and backward of one
+ * rasterization must run with the same setting. */
+int gsplat_hip_debug_set_chunk(int isects);
 
 /* ---------------------------------------------------------------------------
  * Trainer-side kernels of the training step (not part of the 5-function
