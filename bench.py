@@ -50,6 +50,15 @@ def parse():
     return ap.parse_args()
 
 
+def max_over_ranks(elapsed: float, world: int, device) -> float:
+    """The job's time: the slowest rank's (all_reduce MAX; identity at N=1)."""
+    if world == 1:
+        return elapsed
+    t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -87,12 +96,8 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    elapsed = time.perf_counter() - t0
+    elapsed = max_over_ranks(time.perf_counter() - t0, world, dev)
     _wrapper.enable_kernel_timers(False)
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
 
     # ---- per-kernel HIP-event times over the timed region
     def mean_ms(name):
