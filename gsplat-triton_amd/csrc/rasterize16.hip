@@ -85,6 +85,48 @@ GS_INLINE float reduce_scatter(const float *v, int lane) {
   return z;
 }
 
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+GS_INLINE f2v swap32_sum2(f2v a, f2v b) {
+  return f2v{swap32_sum(a.x, b.x), swap32_sum(a.y, b.y)};
+}
+GS_INLINE f2v swap16_sum2(f2v a, f2v b) {
+  return f2v{swap16_sum(a.x, b.x), swap16_sum(a.y, b.y)};
+}
+template <int CTRL>
+GS_INLINE f2v dpp2(f2v v) {
+  return f2v{dpp<CTRL>(v.x), dpp<CTRL>(v.y)};
+}
+template <int M>
+GS_INLINE f2v pick2(const f2v (&a)[M], int i) {
+  return i < M ? a[i < M ? i : 0] : f2v{0.f, 0.f};
+}
+
+// reduce_scatter for N float2 fields (two records at once, .x / .y); the
+// adds run as packed fp32, the lane exchanges per component.
+template <int N>
+GS_INLINE f2v reduce_scatter2(const f2v *v, int lane) {
+  static_assert(N >= 1 && N <= 16, "reduce_scatter2: 1..16 fields");
+  constexpr int N1 = (N + 1) / 2, N2 = (N1 + 1) / 2, N3 = (N2 + 1) / 2;
+  f2v w[N1], x[N2], y[N3];
+#pragma unroll
+  for (int i = 0; i < N1; ++i)
+    w[i] = swap32_sum2(v[2 * i], 2 * i + 1 < N ? v[2 * i + 1] : f2v{0.f, 0.f});
+#pragma unroll
+  for (int i = 0; i < N2; ++i) x[i] = swap16_sum2(w[2 * i], pick2(w, 2 * i + 1));
+  const bool b3 = lane & 8, b2 = lane & 4;
+#pragma unroll
+  for (int i = 0; i < N3; ++i) {
+    const f2v lo = x[2 * i], hi = pick2(x, 2 * i + 1);
+    y[i] = (b3 ? hi : lo) + dpp2<0x140>(b3 ? lo : hi);
+  }
+  const f2v lo = y[0], hi = pick2(y, 1);
+  f2v z = (b2 ? hi : lo) + dpp2<0x141>(b2 ? lo : hi);
+  z += dpp2<0xB1>(z);
+  z += dpp2<0x4E>(z);
+  return z;
+}
+
 // The field whose total lane `lane` holds after reduce_scatter.
 GS_INLINE int rs_field(int lane) {
   return ((lane >> 5) & 1) | (((lane >> 4) & 1) << 1) | (((lane >> 3) & 1) << 2) |
@@ -282,11 +324,89 @@ struct WaveGeom {
 // Forward.  The gather of batch b+1 (its attributes) and the flatten ids of
 // batch b+2 are in flight while batch b is composited, so a long tile pays
 // the two dependent global-load latencies once, not once per 64 isects.
+// Forward records are staged in PAIRS, field-interleaved: the pair holding
+// kept records 2p and 2p+1 stores every field f as the float2 (f_2p, f_2p+1),
+// so one ds_read_b128 yields two fields of both records in register pairs and
+// the per-record algebra runs as packed fp32 (v_pk_fma/mul/add_f32: two lanes'
+// worth per instruction; a wave64 v_fma_f32 costs 4 cycles per SIMD on
+// MI355X, a v_pk_fma_f32 about 4.7 for twice the work -- tools/valu_bench.hip).
+// Fields: x, y, (a, b, c) pre-scaled for exp2, opacity, smax = log2(255 op)
+// (hit iff 0 <= s2 <= smax, one unsigned compare), isect index, colour[D].
 template <int D>
-__global__ void __launch_bounds__(256) fwd_kernel(Args a) {
-  using R = Rec<D, true>;
-  constexpr int NF = R::NF, N4 = R::N4;
-  __shared__ float4 stage_all[4][64 * N4];
+struct FwdPair {
+  static constexpr int NFP = 8 + D;                  // fields per record
+  static constexpr int N4 = (2 * NFP + 3) / 4;       // float4s per pair
+};
+
+template <int D>
+GS_INLINE void stage_fwd_pair(float4 *st, int slot, const Attr<D> &at, int32_t idx) {
+  float *w = reinterpret_cast<float *>(st + (slot >> 1) * FwdPair<D>::N4) + (slot & 1);
+  w[0] = at.xy.x;
+  w[2] = at.xy.y;
+  w[4] = 0.5f * kLog2e * at.con.x;
+  w[6] = kLog2e * at.con.y;
+  w[8] = 0.5f * kLog2e * at.con.z;
+  w[10] = at.op;
+  w[12] = __builtin_amdgcn_logf(255.f * at.op);  // log2
+  w[14] = __int_as_float(idx);
+#pragma unroll
+  for (int d = 0; d < D; ++d) w[16 + 2 * d] = at.col[d];
+}
+
+// The odd slot of a final half-filled pair: x = NaN never hits.
+template <int D>
+GS_INLINE void stage_fwd_pad(float4 *st, int slot) {
+  float *w = reinterpret_cast<float *>(st + (slot >> 1) * FwdPair<D>::N4) + (slot & 1);
+  w[0] = __int_as_float(0x7fc00000);
+  w[12] = 0.f;
+#pragma unroll
+  for (int f = 1; f < FwdPair<D>::NFP; ++f)
+    if (f != 6) w[2 * f] = 0.f;
+}
+
+// Backward records, staged in pairs like the forward's.  Fields: x, y,
+// (a, b, c) * log2(e) / 2 (so that s2 = dx gx + dy gy with gx = A dx + B dy,
+// gy = B dx + C dy, and d s2 / d(dx, dy) = 2 (gx, gy)), opacity, smax, isect
+// index, Gaussian id, colour[D].
+template <int D>
+struct BwdPair {
+  static constexpr int NFP = 9 + D;
+  static constexpr int N4 = (2 * NFP + 3) / 4;
+};
+
+template <int D>
+GS_INLINE void stage_bwd_pair(float4 *st, int slot, const Attr<D> &at, int32_t idx) {
+  float *w = reinterpret_cast<float *>(st + (slot >> 1) * BwdPair<D>::N4) + (slot & 1);
+  w[0] = at.xy.x;
+  w[2] = at.xy.y;
+  w[4] = 0.5f * kLog2e * at.con.x;
+  w[6] = 0.5f * kLog2e * at.con.y;
+  w[8] = 0.5f * kLog2e * at.con.z;
+  w[10] = at.op;
+  w[12] = __builtin_amdgcn_logf(255.f * at.op);
+  w[14] = __int_as_float(idx);
+  w[16] = __int_as_float(at.g);
+#pragma unroll
+  for (int d = 0; d < D; ++d) w[18 + 2 * d] = at.col[d];
+}
+
+template <int D>
+GS_INLINE void stage_bwd_pad(float4 *st, int slot) {
+  float *w = reinterpret_cast<float *>(st + (slot >> 1) * BwdPair<D>::N4) + (slot & 1);
+  w[0] = __int_as_float(0x7fc00000);  // NaN: never valid
+  w[12] = 0.f;
+  w[16] = __int_as_float(-1);  // no gradient row
+#pragma unroll
+  for (int f = 1; f < BwdPair<D>::NFP; ++f)
+    if (f != 6 && f != 8) w[2 * f] = 0.f;
+}
+
+template <int D>
+// register budget: 80 VGPRs = 6 waves per SIMD without spills
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) fwd_kernel(Args a) {
+  using P = FwdPair<D>;
+  constexpr int N4 = P::N4;
+  __shared__ float4 stage_all[4][32 * N4];
   const int lane = threadIdx.x & 63;
   float4 *st = stage_all[threadIdx.x >> 6];
   const uint64_t t_start = tl_now(a);
@@ -298,9 +418,16 @@ __global__ void __launch_bounds__(256) fwd_kernel(Args a) {
   const int64_t end = (tile == a.n_tiles - 1) ? a.n_isects : (int64_t)a.offsets[tile + 1];
   const bool skip_tile = a.masks && a.masks[tile];
 
-  float acc[D];
+  // colour accumulated from even (.x) and odd (.y) records of each pair
+  // colour accumulated from even (.x) and odd (.y) records of each pair in the
+  // current chunk; tot: the chunks before it (see "chunk state" below)
+  f2v acc[D];
+  float tot[D];
 #pragma unroll
-  for (int d = 0; d < D; ++d) acc[d] = 0.f;
+  for (int d = 0; d < D; ++d) {
+    acc[d] = f2v{0.f, 0.f};
+    tot[d] = 0.f;
+  }
   int32_t last = 0;
   // A terminated (or outside) pixel is encoded by a negative T: |T| is its
   // final transmittance.
@@ -312,29 +439,50 @@ __global__ void __launch_bounds__(256) fwd_kernel(Args a) {
       return a.flatten_ids[min(b0 + lane, end - 1)];
     };
     bool done = false;
-    // composite one staged batch (cnt records), checking every 16 records
-    // whether the strip is still alive
+    // one record of a pair: sequential in T
+    auto blend = [&](float s2, float smax, float al, float idx) -> float {
+      const float nT = __builtin_fmaf(-T, al, T);  // T (1 - alpha)
+      const bool hit = __float_as_uint(s2) <= __float_as_uint(smax);  // 0 <= s2 <= smax
+      const bool gt = nT > kTMin;
+      const bool ok = hit & gt;
+      // plain selects (no control flow): blended -> nT; hit but T would drop
+      // to <= 1e-4 -> exclusive stop, -|T| marks the pixel (and keeps dead
+      // pixels dead); otherwise unchanged
+      const float Tsel = ok ? nT : T;
+      const float vis = T - Tsel;  // alpha * T when blended, else 0
+      T = (hit & !gt) ? -fabsf(T) : Tsel;
+      last = ok ? __float_as_int(idx) : last;
+      return vis;
+    };
+    // composite one staged batch (cnt records = (cnt+1)/2 pairs), checking
+    // every 8 pairs whether the strip is still alive
     auto composite = [&](int cnt) {
-      for (int kb = 0; kb < cnt; kb += 16) {
-        const int ke = min(cnt, kb + 16);
-#pragma unroll 2
-        for (int k = kb; k < ke; ++k) {
-          float r[NF];
-          read_rec<D, true, false>(st + k * N4, r);
-          const float dx = r[0] - fx, dy = r[1] - fy;
-          // sigma * log2(e) with the pre-scaled conic
-          const float s2 = dx * (r[2] * dx + r[3] * dy) + r[4] * dy * dy;
-          const float alpha = fminf(kAlphaMax, r[5] * __builtin_amdgcn_exp2f(-s2));
-          const float nT = T * (1.f - alpha);
-          const bool hit = (s2 >= 0.f) & (alpha >= kAlphaMin);
-          // dead lanes have T < 0, so nT < 0 and `ok` is false for them
-          const bool ok = hit & (nT > kTMin);
-          const bool term = hit & (nT <= kTMin) & (T > 0.f);  // exclusive stop: not blended
-          const float vis = ok ? alpha * T : 0.f;
+      const int np = (cnt + 1) >> 1;
+      for (int pb = 0; pb < np; pb += 8) {
+        const int pe = min(np, pb + 8);
+        for (int p = pb; p < pe; ++p) {
+          const float4 *q = st + p * N4;
+          f2v f[2 * N4];
+          float4 v[N4];
 #pragma unroll
-          for (int d = 0; d < D; ++d) acc[d] += vis * r[R::C0 + d];
-          T = ok ? nT : (term ? -T : T);
-          last = ok ? __float_as_int(r[6]) : last;
+          for (int i = 0; i < N4; ++i) v[i] = q[i];
+#pragma unroll
+          for (int i = 0; i < N4; ++i) {
+            // keep every field live: no load may sink into a select's branch
+            asm volatile("" ::"v"(v[i].x), "v"(v[i].y), "v"(v[i].z), "v"(v[i].w));
+            f[2 * i] = f2v{v[i].x, v[i].y};
+            f[2 * i + 1] = f2v{v[i].z, v[i].w};
+          }
+          const f2v dx = f[0] - fx, dy = f[1] - fy;
+          const f2v s2 = dx * (f[2] * dx + f[3] * dy) + f[4] * dy * dy;  // sigma * log2(e)
+          f2v al = f[5] * f2v{__builtin_amdgcn_exp2f(-s2.x), __builtin_amdgcn_exp2f(-s2.y)};
+          al.x = fminf(al.x, kAlphaMax);
+          al.y = fminf(al.y, kAlphaMax);
+          const float v0 = blend(s2.x, f[6].x, al.x, f[7].x);
+          const float v1 = blend(s2.y, f[6].y, al.y, f[7].y);
+          const f2v vis = f2v{v0, v1};
+#pragma unroll
+          for (int d = 0; d < D; ++d) acc[d] = __builtin_elementwise_fma(vis, f[8 + d], acc[d]);
         }
         if (__ballot(T > 0.f) == 0) {
           done = true;
@@ -345,23 +493,40 @@ __global__ void __launch_bounds__(256) fwd_kernel(Args a) {
     auto stage = [&](const Attr<D> &at, int64_t b0) -> int {
       const bool keep = (b0 + lane < end) && keep_attr<D>(at, geo.x0, geo.x1, geo.y0, geo.y1);
       const uint64_t m = __ballot(keep);
-      if (keep) stage_attr<D, true>(st + ballot_slot(m) * N4, at, (int32_t)(b0 + lane));
+      const int cnt = __popcll(m);
+      if (keep) stage_fwd_pair<D>(st, ballot_slot(m), at, (int32_t)(b0 + lane));
+      if ((cnt & 1) && lane == 0) stage_fwd_pad<D>(st, cnt);
       wave_sync_lds();
-      return __popcll(m);
+      return cnt;
     };
-    // two attribute buffers in alternation: while batch b is composited from
-    // one, the other receives batch b+1, and the ids of batch b+2 load
-    // chunk boundaries (isect index start + m*L, m >= 1): store the pixel
-    // state there for the chunked backward
+    // Chunk state for the chunked backward, one slot per chunk boundary
+    // b = start + m*L (m >= 1), slot b / L: T[256] = the pixel's transmittance
+    // before isect b, S[D][256] = the colour the chunk starting at b adds.
+    // Chunk-local sums keep the backward's suffix sums (sum of S over the
+    // later chunks) as accurate as its own back-to-front accumulation; a
+    // difference of running totals would cancel catastrophically.
     const int64_t L = a.L;
-    auto save_state = [&](int64_t bidx) {
-      float *sl = a.state + (bidx / L) * (int64_t)(kTS * kTS * (1 + D));
-      const int p = (threadIdx.x >> 6) * 64 + lane;  // pixel of the tile, row-major
-      sl[p] = T;
+    const int pix_in_tile = (threadIdx.x >> 6) * 64 + lane;  // row-major
+    auto slot = [&](int64_t bidx) { return a.state + (bidx / L) * (int64_t)(kTS * kTS * (1 + D)); };
+    int64_t cur_b = start;  // start of the chunk being accumulated
+    auto close_chunk = [&]() {  // fold acc into tot; store S of the chunk at cur_b
+      float *sl = slot(cur_b);
 #pragma unroll
-      for (int d = 0; d < D; ++d) sl[(1 + d) * kTS * kTS + p] = acc[d];
+      for (int d = 0; d < D; ++d) {
+        const float cs = acc[d].x + acc[d].y;
+        if (cur_b > start) sl[(1 + d) * kTS * kTS + pix_in_tile] = cs;
+        tot[d] += cs;
+        acc[d] = f2v{0.f, 0.f};
+      }
+    };
+    auto save_state = [&](int64_t bidx) {  // reached boundary bidx
+      close_chunk();
+      cur_b = bidx;
+      slot(bidx)[pix_in_tile] = T;
     };
     const bool chunked = a.state && L > 0 && end - start > L;
+    // two attribute buffers in alternation: while batch b is composited from
+    // one, the other receives batch b+1, and the ids of batch b+2 load
     Attr<D> A, B;
     load_attr<D>(a, id_at(start), A);
     int32_t g_n = id_at(start + 64);
@@ -384,11 +549,19 @@ __global__ void __launch_bounds__(256) fwd_kernel(Args a) {
       if (done) break;
     }
     if (chunked) {
-      // boundaries the loop did not reach (all pixels finished): final state
-      const int64_t nb = start + ((b0 - start + L - 1) / L) * L;
-      for (int64_t bi = max(nb, start + L); bi < end; bi += L) save_state(bi);
+      close_chunk();
+      // boundaries the loop did not reach (all pixels finished): final T,
+      // nothing added after them
+      for (int64_t bi = cur_b + L; bi < end; bi += L) {
+        float *sl = slot(bi);
+        sl[pix_in_tile] = T;
+#pragma unroll
+        for (int d = 0; d < D; ++d) sl[(1 + d) * kTS * kTS + pix_in_tile] = 0.f;
+      }
     }
   }
+#pragma unroll
+  for (int d = 0; d < D; ++d) tot[d] += acc[d].x + acc[d].y;
 
   if (inside) {
     const int64_t pix = ((int64_t)c * a.H + geo.py) * a.W + geo.px;
@@ -396,7 +569,7 @@ __global__ void __launch_bounds__(256) fwd_kernel(Args a) {
 #pragma unroll
     for (int d = 0; d < D; ++d) {
       const float bg = a.backgrounds ? a.backgrounds[c * D + d] : 0.f;
-      oc[d] = acc[d] + fabsf(T) * bg;
+      oc[d] = tot[d] + fabsf(T) * bg;
     }
     a.render_alphas[pix] = 1.f - fabsf(T);
     a.last_ids[pix] = last;
@@ -406,12 +579,13 @@ __global__ void __launch_bounds__(256) fwd_kernel(Args a) {
 
 // Backward: batches of 64 isects from the back, same two-deep gather pipeline.
 template <int D, bool ABS>
-__global__ void __launch_bounds__(256) bwd_kernel(Args a) {
-  using R = Rec<D, false>;
-  constexpr int NF = R::NF, N4 = R::N4;
+// register budget: 72 VGPRs = 7 waves per SIMD without spills
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) bwd_kernel(Args a) {
+  using P = BwdPair<D>;
+  constexpr int N4 = P::N4;
   constexpr int F = D + 6 + (ABS ? 2 : 0);
   constexpr int NV = (F + 15) / 16;  // reduce-scatter groups of <= 16 fields
-  __shared__ float4 stage_all[4][64 * N4];
+  __shared__ float4 stage_all[4][32 * N4];
   const int lane = threadIdx.x & 63;
   float4 *st = stage_all[threadIdx.x >> 6];
   const uint64_t t_start = tl_now(a);
@@ -454,16 +628,18 @@ __global__ void __launch_bounds__(256) bwd_kernel(Args a) {
     T = Tf;
     if (cend < tend) {
       // a chunk followed by others: start from the forward's state at the
-      // boundary cend (transmittance; colour accumulated before it), and the
-      // suffix colour sum of everything after it, dotted with dL/dcolour
-      const float *sl = a.state + (cend / a.L) * (int64_t)(kTS * kTS * (1 + D));
+      // boundary cend (transmittance), and the suffix colour sum of the later
+      // chunks (their chunk-local sums S), dotted with dL/dcolour
       const int p = (threadIdx.x >> 6) * 64 + lane;
-      T = fabsf(sl[p]);
-      const float *rc = a.render_colors_in + pix * D;
+      const int64_t per = (int64_t)(kTS * kTS * (1 + D));
+      T = fabsf(a.state[(cend / a.L) * per + p]);
       float s = 0.f;
+      for (int64_t bi = cend; bi < tend; bi += a.L) {
+        const float *sl = a.state + (bi / a.L) * per;
 #pragma unroll
-      for (int d = 0; d < D; ++d) s += (rc[d] - sl[(1 + d) * kTS * kTS + p]) * Drc[d];
-      rD = s - bgv * Tf;  // render_colors includes the background term
+        for (int d = 0; d < D; ++d) s += sl[(1 + d) * kTS * kTS + p] * Drc[d];
+      }
+      rD = s;
     }
   }
   const float TfDra = Tf * Dra;
@@ -482,80 +658,111 @@ __global__ void __launch_bounds__(256) bwd_kernel(Args a) {
       const int64_t j = b1 - 64 + lane;
       const bool keep = (j >= start) && keep_attr<D>(at, geo.x0, geo.x1, geo.y0, geo.y1);
       const uint64_t m = __ballot(keep);
-      if (keep) stage_attr<D, false>(st + ballot_slot(m) * N4, at, (int32_t)j);
+      const int cnt = __popcll(m);
+      if (keep) stage_bwd_pair<D>(st, ballot_slot(m), at, (int32_t)j);
+      if ((cnt & 1) && lane == 0) stage_bwd_pad<D>(st, cnt);
       wave_sync_lds();
-      return __popcll(m);
+      return cnt;
+    };
+    // per-field scale applied once after the lane reduction: colours,
+    // opacity as accumulated; means2d from aD * (gx, gy): -2 / log2(e);
+    // conic from aD * (dx^2, dx dy, dy^2): (-1/2, -1, -1/2); |means2d|: 2 / log2(e)
+    const int lf = rs_field(lane);
+    auto field_scale = [&](int f) -> float {
+      constexpr float m2 = -2.f / kLog2e;
+      if (f < D + 1) return 1.f;
+      if (f < D + 3) return m2;
+      if (f == D + 3 || f == D + 5) return -0.5f;
+      if (f == D + 4) return -1.f;
+      return -m2;
+    };
+    // one record of a pair, back to front: sequential in T and rD
+    auto grad_seq = [&](bool valid, bool unclamped, float al, float ra, float gD, float &w,
+                        float &Da) {
+      T = valid ? T * ra : T;
+      w = valid ? al * T : 0.f;
+      rD += gD * w;
+      const float Da_raw = ra * (TfDra + T * gD - rD - bgt);
+      // clamped alpha (> 0.999) has no gradient (rasterize_to_pixels_bwd.py:184-187)
+      Da = (valid & unclamped) ? Da_raw : 0.f;
     };
     auto composite = [&](int cnt) {
-      for (int k = cnt - 1; k >= 0; --k) {
-        float r[NF];
-        read_rec<D, false, true>(st + k * N4, r);
-        const float ca = r[2], cb = r[3], cc = r[4];
-        const int32_t idx = __float_as_int(r[6]);
-        float v[NV * 16];
+      for (int p = (cnt - 1) >> 1; p >= 0; --p) {
+        const float4 *q = st + p * N4;
+        float4 vv[N4];
 #pragma unroll
-        for (int f = 0; f < NV * 16; ++f) v[f] = 0.f;
-        const float dx = r[0] - fx, dy = r[1] - fy;
-        const float sigma = 0.5f * ca * dx * dx + 0.5f * cc * dy * dy + cb * dx * dy;
-        const float ex = __expf(-sigma);
-        const float alpha_raw = r[5] * ex;
-        const bool valid = (idx <= mylast) & (sigma >= 0.f) & (alpha_raw >= kAlphaMin);
-        if (__ballot(valid) == 0) continue;
-        const float alpha = __builtin_amdgcn_fmed3f(alpha_raw, -INFINITY, kAlphaMax);  // min
-        const float ra = __builtin_amdgcn_rcpf(1.f - alpha);
-        T = valid ? T * ra : T;
-        const float w = valid ? alpha * T : 0.f;
-        float gD = 0.f;
+        for (int i = 0; i < N4; ++i) vv[i] = q[i];
+        f2v f[2 * N4];
 #pragma unroll
-        for (int d = 0; d < D; ++d) {
-          v[d] = w * Drc[d];
-          gD += r[R::C0 + d] * Drc[d];
+        for (int i = 0; i < N4; ++i) {
+          asm volatile("" ::"v"(vv[i].x), "v"(vv[i].y), "v"(vv[i].z), "v"(vv[i].w));
+          f[2 * i] = f2v{vv[i].x, vv[i].y};
+          f[2 * i + 1] = f2v{vv[i].z, vv[i].w};
         }
-        rD += gD * w;
-        const float Da_raw = ra * (TfDra + T * gD - rD - bgt);
-        // clamped alpha (> 0.999) has no gradient (rasterize_to_pixels_bwd.py:184-187)
-        const float Da = (valid & (alpha_raw <= kAlphaMax)) ? Da_raw : 0.f;
-        const float aD = alpha * Da;
-        const float gmx = -aD * (ca * dx + cb * dy);
-        const float gmy = -aD * (cb * dx + cc * dy);
-        v[D] = valid ? Da * ex : 0.f;
-        v[D + 1] = gmx;
-        v[D + 2] = gmy;
-        v[D + 3] = -0.5f * aD * dx * dx;
-        v[D + 4] = -aD * dx * dy;
-        v[D + 5] = -0.5f * aD * dy * dy;
+        const f2v dx = f[0] - fx, dy = f[1] - fy;
+        const f2v gx = f[2] * dx + f[3] * dy, gy = f[3] * dx + f[4] * dy;
+        const f2v s2 = dx * gx + dy * gy;  // sigma * log2(e)
+        const f2v ex = f2v{__builtin_amdgcn_exp2f(-s2.x), __builtin_amdgcn_exp2f(-s2.y)};
+        const f2v ar = f[5] * ex;  // alpha before the 0.999 clamp
+        const bool v0 = (__float_as_uint(s2.x) <= __float_as_uint(f[6].x)) &&
+                        (__float_as_int(f[7].x) <= mylast);
+        const bool v1 = (__float_as_uint(s2.y) <= __float_as_uint(f[6].y)) &&
+                        (__float_as_int(f[7].y) <= mylast);
+        if (__ballot(v0 | v1) == 0) continue;
+        const f2v al = f2v{fminf(ar.x, kAlphaMax), fminf(ar.y, kAlphaMax)};
+        const f2v om = 1.f - al;
+        const f2v ra = f2v{__builtin_amdgcn_rcpf(om.x), __builtin_amdgcn_rcpf(om.y)};
+        f2v gD = f[9] * Drc[0];
+#pragma unroll
+        for (int d = 1; d < D; ++d) gD = __builtin_elementwise_fma(f[9 + d], f2v{Drc[d], Drc[d]}, gD);
+        float w1, Da1, w0, Da0;
+        grad_seq(v1, ar.y <= kAlphaMax, al.y, ra.y, gD.y, w1, Da1);  // later record first
+        grad_seq(v0, ar.x <= kAlphaMax, al.x, ra.x, gD.x, w0, Da0);
+        const f2v w = f2v{w0, w1}, Da = f2v{Da0, Da1};
+        const f2v aD = al * Da;
+        f2v v[NV * 16];
+#pragma unroll
+        for (int k = 0; k < NV * 16; ++k) v[k] = f2v{0.f, 0.f};
+#pragma unroll
+        for (int d = 0; d < D; ++d) v[d] = w * Drc[d];
+        v[D] = Da * ex;
+        v[D + 1] = aD * gx;
+        v[D + 2] = aD * gy;
+        const f2v P_ = aD * dx, Q_ = aD * dy;
+        v[D + 3] = P_ * dx;
+        v[D + 4] = P_ * dy;
+        v[D + 5] = Q_ * dy;
         if (ABS) {
-          v[D + 6] = fabsf(gmx);
-          v[D + 7] = fabsf(gmy);
+          v[D + 6] = f2v{fabsf(v[D + 1].x), fabsf(v[D + 1].y)};
+          v[D + 7] = f2v{fabsf(v[D + 2].x), fabsf(v[D + 2].y)};
         }
-        float *row = a.packed + (int64_t)__float_as_int(r[7]) * a.S;
-        const int lf = rs_field(lane);
+        const int g0 = __float_as_int(f[8].x), g1 = __float_as_int(f[8].y);
 #pragma unroll
-        for (int q = 0; q < NV; ++q) {
+        for (int qq = 0; qq < NV; ++qq) {
           constexpr int NQ = F - 16 * (NV - 1);  // fields in the last group
-          const float tot = q < NV - 1 ? reduce_scatter<16>(v + 16 * q, lane)
-                                       : reduce_scatter<NQ>(v + 16 * q, lane);
-          const int field = 16 * q + lf;
-          if ((lane & 3) == 0 && lf < (q < NV - 1 ? 16 : NQ) && tot != 0.f && !(a.dbg & 1))
-            atomic_add_f32(row + field, tot);
+          const f2v tot = qq < NV - 1 ? reduce_scatter2<16>(v + 16 * qq, lane)
+                                      : reduce_scatter2<NQ>(v + 16 * qq, lane);
+          const int field = 16 * qq + lf;
+          if ((lane & 3) == 0 && lf < (qq < NV - 1 ? 16 : NQ) && !(a.dbg & 1)) {
+            const float sc = field_scale(field);
+            if (tot.x != 0.f) atomic_add_f32(a.packed + (int64_t)g0 * a.S + field, sc * tot.x);
+            if (g1 >= 0 && tot.y != 0.f)
+              atomic_add_f32(a.packed + (int64_t)g1 * a.S + field, sc * tot.y);
+          }
         }
       }
     };
-    Attr<D> A, B;
-    load_attr<D>(a, id_at(end), A);
-    int32_t g_n = id_at(end - 64);
-    for (int64_t b1 = end; b1 > start;) {
-      load_attr<D>(a, g_n, B);
-      g_n = id_at(b1 - 128);
+    // The backward is throughput-bound (many waves per SIMD hide the gather
+    // latency; long tiles are split into chunk items), so it prefetches only
+    // the next batch's flatten ids and spends no registers on a second
+    // attribute buffer.
+    int32_t g_n = id_at(end);
+    for (int64_t b1 = end; b1 > start; b1 -= 64) {
+      Attr<D> A;
+      load_attr<D>(a, g_n, A);
+      g_n = id_at(b1 - 64);
       composite(stage(A, b1));
       wave_sync_lds();
-      b1 -= 64;
-      if (b1 <= start) break;
-      load_attr<D>(a, g_n, A);
-      g_n = id_at(b1 - 128);
-      composite(stage(B, b1));
-      wave_sync_lds();
-      b1 -= 64;
     }
   }
   tl_store(a, t_start, lane);
@@ -643,7 +850,7 @@ static int g_chunk = -1;  // -1: not yet read from the environment
 static int chunk_len() {
   if (g_chunk < 0) {
     const char *e = getenv("GSPLAT_HIP_CHUNK");
-    const int x = e ? atoi(e) : 512;
+    const int x = e ? atoi(e) : 1024;
     g_chunk = x <= 0 ? 0 : ((x + 63) / 64) * 64;
   }
   return g_chunk;

@@ -188,7 +188,7 @@ int gsplat_hip_rasterize_bwd(int C, int64_t n_gaussians, int D, int width, int h
  * of the reference surface; NULL disables (the default). */
 int gsplat_hip_debug_set_timeline(uint64_t *device_buffer, int64_t capacity_waves);
 /* Chunk length (isects, rounded up to a multiple of 64; <= 0 disables) of the
- * chunked 16x16 backward; returns the value in effect.  Default 512, or the
+ * chunked 16x16 backward; returns the value in effect.  Default 1024, or the
  * GSPLAT_HIP_CHUNK environment variable.  Forward and backward of one
  * rasterization must run with the same setting. */
 int gsplat_hip_debug_set_chunk(int isects);

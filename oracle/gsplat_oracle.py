@@ -24,11 +24,30 @@ Semantics followed (reference file:line):
 
 import numpy as np
 
-f32 = np.float32
+f32 = np.float32  # working precision; `precision(np.float64)` for an exact-math check
 
 
 def _f(x):
-    return np.asarray(x, dtype=np.float32)
+    return np.asarray(x, dtype=f32)
+
+
+class precision:
+    """Run the oracle in another float type, e.g. float64 to measure how far
+    an fp32 implementation (the reference's, or the HIP one) is from exact
+    arithmetic on long tiles:  `with precision(np.float64): raster_bwd(...)`."""
+
+    def __init__(self, dtype):
+        self.dtype = dtype
+
+    def __enter__(self):
+        global f32
+        self.prev, f32 = f32, self.dtype
+        return self
+
+    def __exit__(self, *exc):
+        global f32
+        f32 = self.prev
+        return False
 
 
 # ------------------------------------------------------------------ helpers

@@ -26,20 +26,25 @@ def close(a, b, rtol, atol, what=""):
     np.testing.assert_allclose(a, b, rtol=rtol, atol=atol, err_msg=what)
 
 
-def close_most(a, b, rtol, atol, what="", max_frac=1e-4, min_count=2):
+def close_most(a, b, rtol, atol, what="", max_frac=1e-4, min_count=2, rows=False):
     """allclose up to a handful of threshold flips: a Gaussian whose alpha is
     within float rounding of 1/255 (or a pixel whose T is within rounding of
     1e-4) can land on the other side of the cut in two correct fp32
     implementations (different FMA contraction / exp).  At most
-    max(min_count, max_frac * size) elements may exceed the tolerance."""
+    max(min_count, max_frac * n) elements -- or, with rows=True, rows of the
+    last axis (all gradient components of one Gaussian) -- may exceed the
+    tolerance."""
     a = a.detach().cpu().numpy() if isinstance(a, torch.Tensor) else np.asarray(a)
     b = b.detach().cpu().numpy() if isinstance(b, torch.Tensor) else np.asarray(b)
     assert a.shape == b.shape, (what, a.shape, b.shape)
     bad = ~np.isclose(a, b, rtol=rtol, atol=atol)
-    allowed = max(min_count, int(max_frac * a.size))
+    if rows and bad.ndim > 1:
+        bad = bad.reshape(-1, bad.shape[-1]).any(-1)
+    allowed = max(min_count, int(max_frac * bad.size))
     assert bad.sum() <= allowed, (
-        f"{what}: {bad.sum()} of {a.size} elements outside rtol={rtol} atol={atol} "
-        f"(allowed {allowed}); max abs diff {np.abs(a - b)[bad].max()}")
+        f"{what}: {bad.sum()} of {bad.size} {'rows' if rows else 'elements'} outside "
+        f"rtol={rtol} atol={atol} (allowed {allowed}); max abs diff "
+        f"{np.abs(a - b).max()}")
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -292,9 +297,9 @@ def test_raster_vs_oracle_random(D, tile):
     ref = O.raster_bwd(m2.cpu().numpy(), cn.cpu().numpy(), pad(cols.cpu().numpy()),
                        ops.cpu().numpy(), pad(bg.cpu().numpy()), W, H, tile, off.cpu().numpy(),
                        fids.cpu().numpy(), oa, ol, pad(vrc.cpu().numpy()), vra.cpu().numpy())
-    close_most(grads[0], ref[0], 5e-3, 5e-3, "v_means2d")
-    close_most(grads[1], ref[1], 1e-3, 1e-3, "v_conics")
-    close_most(grads[2], ref[2][..., :D], 1e-3, 1e-3, "v_colors")
+    close_most(grads[0], ref[0], 5e-3, 5e-3, "v_means2d", rows=True)
+    close_most(grads[1], ref[1], 1e-3, 1e-3, "v_conics", rows=True)
+    close_most(grads[2], ref[2][..., :D], 1e-3, 1e-3, "v_colors", rows=True)
     close_most(grads[3], ref[3], 2e-3, 2e-3, "v_opacities")
 
 
@@ -328,29 +333,57 @@ def test_raster_chunked_backward(chunk):
         try:
             ins = [x.detach().clone().requires_grad_(True) for x in (m2, cn, cols, ops)]
             rc, ra = gsplat_hip.rasterize_to_pixels(*ins, W, H, 16, off, fids, backgrounds=bg)
-            grads = torch.autograd.grad((rc * vrc).sum() + (ra * vra).sum(), ins)
+            grads = torch.autograd.grad((rc * vrc).sum() + (ra * vra).sum(), ins,
+                                        retain_graph=True)
         finally:
-            _lib.query("gsplat_hip_debug_set_chunk", 512)
+            _lib.query("gsplat_hip_debug_set_chunk", 1024)
         return rc, ra, grads
 
     rc0, ra0, g0 = run(0)
     rc1, ra1, g1 = run(chunk)
-    assert torch.equal(rc0, rc1) and torch.equal(ra0, ra1)
-    # both recover T by different routes (chunk-boundary state vs. dividing
-    # back from the final T), so they agree to float rounding, not bitwise
-    for a, b, name in zip(g1, g0, ("v_means2d", "v_conics", "v_colors", "v_opacities")):
-        close_most(a, b, 5e-3, 1e-3, name + " chunked vs whole")
-    oc, oa, ol = O.raster_fwd(m2.cpu().numpy(), cn.cpu().numpy(), cols.cpu().numpy(),
-                              ops.cpu().numpy(), bg.cpu().numpy(), W, H, 16,
-                              off.cpu().numpy(), fids.cpu().numpy())
-    ref = O.raster_bwd(m2.cpu().numpy(), cn.cpu().numpy(), cols.cpu().numpy(),
-                       ops.cpu().numpy(), bg.cpu().numpy(), W, H, 16, off.cpu().numpy(),
-                       fids.cpu().numpy(), oa, ol, vrc.cpu().numpy(), vra.cpu().numpy())
-    close_most(ra1, oa, 1e-5, 2e-5, "alphas")
-    close_most(g1[0], ref[0], 5e-3, 5e-3, "v_means2d")
-    close_most(g1[1], ref[1], 1e-3, 1e-3, "v_conics")
-    close_most(g1[2], ref[2], 1e-3, 1e-3, "v_colors")
-    close_most(g1[3], ref[3], 2e-3, 2e-3, "v_opacities")
+    # the forward sums colour per chunk when chunking: same up to rounding
+    assert torch.equal(ra0, ra1)
+    torch.testing.assert_close(rc0, rc1, rtol=1e-6, atol=1e-6)
+    # Truth: the oracle in float64.  On tiles this long the gradient of a few
+    # Gaussians is ill-conditioned (Da = ra * (T gD - rD + ...) cancels, and
+    # ra = 1 / (1 - alpha) reaches 500): the fp32 reference algorithm itself
+    # (the fp32 oracle) is ~1e-2 off on a few rows there.  Bar: "no worse than
+    # the fp32 reference" -- at most max(2, 3x the reference's) rows outside
+    # the reference tolerances of float64, and a max error within 2x the
+    # reference's max error (+ tolerance).
+    lid = _last_ids(rc1)
+    outs = {}
+    for prec in (np.float64, np.float32):
+        args = [x.detach().cpu().numpy().astype(prec) for x in (m2, cn, cols, ops, bg)]
+        with O.precision(prec):
+            oc, oa, ol = O.raster_fwd(*args, W, H, 16, off.cpu().numpy(), fids.cpu().numpy())
+            outs[prec] = (oc, oa) + tuple(O.raster_bwd(
+                *args, W, H, 16, off.cpu().numpy(), fids.cpu().numpy(),
+                ra1.detach().cpu().numpy().astype(prec), lid, vrc.cpu().numpy().astype(prec),
+                vra.cpu().numpy().astype(prec))[:4])
+    exact, ref32 = outs[np.float64], outs[np.float32]
+    close_most(ra1, exact[1], 1e-5, 2e-5, "alphas")
+    close_most(rc1, exact[0], 1e-5, 2e-5, "colors")
+
+    def bad_rows(e, truth, tol):
+        bad = e > tol + tol * np.abs(truth)
+        return bad.reshape(-1, bad.shape[-1]).any(-1) if bad.ndim > 1 else bad
+
+    for g, how in ((g1, "chunked"), (g0, "whole")):
+        for k, (tol, name) in enumerate(((5e-3, "v_means2d"), (1e-3, "v_conics"),
+                                         (1e-3, "v_colors"), (2e-3, "v_opacities"))):
+            truth = np.asarray(exact[2 + k], np.float64)
+            e_ours = np.abs(g[k].detach().cpu().numpy().astype(np.float64) - truth)
+            e_ref = np.abs(np.asarray(ref32[2 + k], np.float64) - truth)
+            n_ours, n_ref = bad_rows(e_ours, truth, tol).sum(), bad_rows(e_ref, truth, tol).sum()
+            assert n_ours <= max(2, 3 * n_ref), (name, how, n_ours, n_ref)
+            assert e_ours.max() <= 2 * e_ref.max() + tol, (name, how, e_ours.max(), e_ref.max())
+
+
+def _last_ids(render_colors):
+    """last_ids saved by the rasterize forward (autograd node of its output)."""
+    node = render_colors.grad_fn
+    return node.saved_tensors[9].cpu().numpy()
 
 
 def test_raster_tile_masks_skip():
