@@ -10,8 +10,9 @@
 // mu, sigma^2 and sigma_12 exactly (no approximation).
 //
 // Layout: images [B, H, W, C] fp32 (the renderer's native layout, no permute
-// copy).  Per 16x16 output tile a workgroup stages the 26x26 input window in
-// LDS and runs the separable blur in two LDS passes.  The forward stores, per
+// copy).  Per 32x32 output tile a workgroup stages the 42x42 input window in
+// LDS and runs the separable blur in two LDS passes with packed fp32 (the
+// (x, y) and (x^2, y^2) planes as float2, two sums per v_pk_fma_f32).  The forward stores, per
 // valid map pixel and channel, the three partials dSSIM/dmu1, dSSIM/dE[x^2]
 // and dSSIM/dE[xy]; the backward blurs those back onto the image.
 #include "common.h"
@@ -20,31 +21,131 @@
 namespace gs {
 namespace ssim {
 
-constexpr int R = 5, K = 11, TS = 16, WIN = TS + 2 * R;  // 26
+constexpr int R = 5, K = 11;
+constexpr int TW = 32, WN = TW + 2 * R;  // 32x32 output tile, 42x42 input window
 __constant__ float kG[K] = {1.028380084e-03f, 7.598758135e-03f, 3.600077213e-02f,
                             1.093606895e-01f, 2.130055377e-01f, 2.660117249e-01f,
                             2.130055377e-01f, 1.093606895e-01f, 3.600077213e-02f,
                             7.598758135e-03f, 1.028380084e-03f};
 constexpr float C1 = 0.01f * 0.01f, C2 = 0.03f * 0.03f;
 
-// maps: [B][C][3][Hm][Wm]
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+// Separable 11-tap blur of a 42x42 window to the 32x32 tile, three planes at
+// once (two packed float2 planes + one float plane).  256 threads: column
+// tq = tid & 31; the horizontal pass covers rows tr, tr+8, ...; the vertical
+// pass gives rows 4 tr .. 4 tr + 3 of column tq with a sliding window.
+struct Blur3 {
+  f2v a[4], b[4];
+  float c[4];
+};
+
+template <bool TWO>  // TWO: planes a, b (float2) and c; else a and c
+GS_INLINE void blur3(const f2v (*sa)[WN], const f2v (*sb)[WN], const float (*sc)[WN],
+                     f2v (*ha)[TW], f2v (*hb)[TW], float (*hc)[TW], int tid, Blur3 &o) {
+  const int tq = tid & 31, tr = tid >> 5;
+  for (int r = tr; r < WN; r += 8) {
+    f2v a = {0.f, 0.f}, b = {0.f, 0.f};
+    float c = 0.f;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const float g = kG[k];
+      a = __builtin_elementwise_fma(f2v{g, g}, sa[r][tq + k], a);
+      if (TWO) b = __builtin_elementwise_fma(f2v{g, g}, sb[r][tq + k], b);
+      c = __builtin_fmaf(g, sc[r][tq + k], c);
+    }
+    ha[r][tq] = a;
+    if (TWO) hb[r][tq] = b;
+    hc[r][tq] = c;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    o.a[j] = f2v{0.f, 0.f};
+    o.b[j] = f2v{0.f, 0.f};
+    o.c[j] = 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < K + 3; ++i) {
+    const int r = 4 * tr + i;
+    const f2v a = ha[r][tq], b = TWO ? hb[r][tq] : f2v{0.f, 0.f};
+    const float c = hc[r][tq];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k = i - j;
+      if (k >= 0 && k < K) {
+        const float g = kG[k];
+        o.a[j] = __builtin_elementwise_fma(f2v{g, g}, a, o.a[j]);
+        if (TWO) o.b[j] = __builtin_elementwise_fma(f2v{g, g}, b, o.b[j]);
+        o.c[j] = __builtin_fmaf(g, c, o.c[j]);
+      }
+    }
+  }
+}
+
+// Forward flavour: one staged plane (x, y); the horizontal pass forms
+// (x^2, y^2) and x y on the fly (LDS 41 KB -> 3 workgroups per CU).
+GS_INLINE void blur_xy(const f2v (*sa)[WN], f2v (*ha)[TW], f2v (*hb)[TW], float (*hc)[TW],
+                       int tid, Blur3 &o) {
+  const int tq = tid & 31, tr = tid >> 5;
+  for (int r = tr; r < WN; r += 8) {
+    f2v a = {0.f, 0.f}, b = {0.f, 0.f};
+    float c = 0.f;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const float g = kG[k];
+      const f2v v = sa[r][tq + k];
+      const f2v gv = f2v{g, g} * v;
+      a += gv;
+      b = __builtin_elementwise_fma(gv, v, b);
+      c = __builtin_fmaf(gv.x, v.y, c);
+    }
+    ha[r][tq] = a;
+    hb[r][tq] = b;
+    hc[r][tq] = c;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    o.a[j] = f2v{0.f, 0.f};
+    o.b[j] = f2v{0.f, 0.f};
+    o.c[j] = 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < K + 3; ++i) {
+    const int r = 4 * tr + i;
+    const f2v a = ha[r][tq], b = hb[r][tq];
+    const float c = hc[r][tq];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k = i - j;
+      if (k >= 0 && k < K) {
+        const float g = kG[k];
+        o.a[j] = __builtin_elementwise_fma(f2v{g, g}, a, o.a[j]);
+        o.b[j] = __builtin_elementwise_fma(f2v{g, g}, b, o.b[j]);
+        o.c[j] = __builtin_fmaf(g, c, o.c[j]);
+      }
+    }
+  }
+}
+
+// maps: [B][C][3][Hm][Wm] -- dSSIM/dmu1, dSSIM/dE[x^2], dSSIM/dE[xy] per map pixel
 __global__ void __launch_bounds__(256)
 fwd_kernel(int B, int H, int W, int C, const float *__restrict__ x, const float *__restrict__ y,
            float *__restrict__ maps, float *__restrict__ partials) {
-  __shared__ float sx[WIN][WIN], sy[WIN][WIN];
-  __shared__ float h[5][WIN][TS];
+  __shared__ f2v s_xy[WN][WN];  // (x, y)
+  __shared__ f2v h_xy[WN][TW], h_sq[WN][TW];
+  __shared__ float h_p[WN][TW];
   __shared__ float red[2][4];
   const int Hm = H - 2 * R, Wm = W - 2 * R;
-  const int b = blockIdx.z;
-  const int mi0 = blockIdx.y * TS, mj0 = blockIdx.x * TS;  // map tile origin
-  const int tid = threadIdx.x, ti = tid / TS, tj = tid % TS;
-  const int mi = mi0 + ti, mj = mj0 + tj;
-  const bool valid = mi < Hm && mj < Wm;
+  const int b = blockIdx.z / C, c = blockIdx.z - b * C;  // one channel per workgroup
+  const int mi0 = blockIdx.y * TW, mj0 = blockIdx.x * TW;  // map tile origin
+  const int tid = threadIdx.x, tq = tid & 31, tr = tid >> 5;
+  const int64_t plane = (int64_t)Hm * Wm;
   float ssum = 0.f, lsum = 0.f;
-  for (int c = 0; c < C; ++c) {
-    // image window rows [mi0, mi0+26), cols [mj0, mj0+26)
-    for (int e = tid; e < WIN * WIN; e += 256) {
-      const int r = e / WIN, q = e % WIN;
+  {
+    for (int e = tid; e < WN * WN; e += 256) {
+      const int r = e / WN, q = e - r * WN;
       const int gi = mi0 + r, gj = mj0 + q;
       float vx = 0.f, vy = 0.f;
       if (gi < H && gj < W) {
@@ -52,65 +153,41 @@ fwd_kernel(int B, int H, int W, int C, const float *__restrict__ x, const float 
         vx = x[o];
         vy = y[o];
       }
-      sx[r][q] = vx;
-      sy[r][q] = vy;
+      s_xy[r][q] = f2v{vx, vy};
     }
     __syncthreads();
-    for (int e = tid; e < WIN * TS; e += 256) {
-      const int r = e / TS, q = e % TS;
-      float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f, a4 = 0.f;
+    Blur3 o;
+    blur_xy(s_xy, h_xy, h_sq, h_p, tid, o);
 #pragma unroll
-      for (int k = 0; k < K; ++k) {
-        const float g = kG[k], vx = sx[r][q + k], vy = sy[r][q + k];
-        a0 += g * vx;
-        a1 += g * vy;
-        a2 += g * vx * vx;
-        a3 += g * vy * vy;
-        a4 += g * vx * vy;
+    for (int j = 0; j < 4; ++j) {
+      const int mi = mi0 + 4 * tr + j, mj = mj0 + tq;
+      if (mi < Hm && mj < Wm) {
+        const float m1 = o.a[j].x, m2 = o.a[j].y;
+        const float s11 = o.b[j].x - m1 * m1, s22 = o.b[j].y - m2 * m2, s12 = o.c[j] - m1 * m2;
+        const float A1 = 2.f * m1 * m2 + C1, A2 = 2.f * s12 + C2;
+        const float B1 = m1 * m1 + m2 * m2 + C1, B2 = s11 + s22 + C2;
+        const float inv = 1.f / (B1 * B2);
+        const float sv = A1 * A2 * inv;
+        ssum += sv;
+        // partials w.r.t. mu1, E[x^2], E[xy] (the E's independent of mu1)
+        const float dN = 2.f * m2 * (A2 - A1), dD = 2.f * m1 * (B2 - B1);
+        float *mp = maps + (((int64_t)b * C + c) * 3) * plane + (int64_t)mi * Wm + mj;
+        mp[0] = (dN - sv * dD) * inv;
+        mp[plane] = -sv * B1 * inv;
+        mp[2 * plane] = 2.f * A1 * inv;
       }
-      h[0][r][q] = a0; h[1][r][q] = a1; h[2][r][q] = a2; h[3][r][q] = a3; h[4][r][q] = a4;
     }
-    __syncthreads();
-    float m1 = 0.f, m2 = 0.f, e11 = 0.f, e22 = 0.f, e12 = 0.f;
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const float g = kG[k];
-      m1 += g * h[0][ti + k][tj];
-      m2 += g * h[1][ti + k][tj];
-      e11 += g * h[2][ti + k][tj];
-      e22 += g * h[3][ti + k][tj];
-      e12 += g * h[4][ti + k][tj];
-    }
-    if (valid) {
-      const float s11 = e11 - m1 * m1, s22 = e22 - m2 * m2, s12 = e12 - m1 * m2;
-      const float A1 = 2.f * m1 * m2 + C1, A2 = 2.f * s12 + C2;
-      const float B1 = m1 * m1 + m2 * m2 + C1, B2 = s11 + s22 + C2;
-      const float Dn = B1 * B2, inv = 1.f / Dn;
-      const float s = A1 * A2 * inv;
-      ssum += s;
-      // partials w.r.t. mu1, E[x^2], E[xy] (E's independent of mu1)
-      const float dN = 2.f * m2 * (A2 - A1), dD = 2.f * m1 * (B2 - B1);
-      const float d_mu1 = (dN - s * dD) * inv;
-      const float d_e11 = -s * B1 * inv;
-      const float d_e12 = 2.f * A1 * inv;
-      const int64_t plane = (int64_t)Hm * Wm;
-      float *mp = maps + (((int64_t)b * C + c) * 3) * plane + (int64_t)mi * Wm + mj;
-      mp[0] = d_mu1;
-      mp[plane] = d_e11;
-      mp[2 * plane] = d_e12;
-    }
-    __syncthreads();
   }
   // L1 over the whole image: each workgroup owns the image pixels of its map
-  // tile (edge workgroups also cover the 2R-pixel border beyond the map)
+  // tile in its channel (edge workgroups also cover the 2R-pixel border)
   {
-    const int ri0 = mi0, rj0 = mj0;
-    const int ri1 = (mi0 + TS >= Hm) ? H : mi0 + TS;
-    const int rj1 = (mj0 + TS >= Wm) ? W : mj0 + TS;
-    for (int e = tid; e < (ri1 - ri0) * (rj1 - rj0); e += 256) {
-      const int gi = ri0 + e / (rj1 - rj0), gj = rj0 + e % (rj1 - rj0);
-      const int64_t o = (((int64_t)b * H + gi) * W + gj) * C;
-      for (int c = 0; c < C; ++c) lsum += fabsf(x[o + c] - y[o + c]);
+    const int ri1 = (mi0 + TW >= Hm) ? H : mi0 + TW;
+    const int rj1 = (mj0 + TW >= Wm) ? W : mj0 + TW;
+    const int nc = rj1 - mj0;
+    for (int e = tid; e < (ri1 - mi0) * nc; e += 256) {
+      const int gi = mi0 + e / nc, gj = mj0 + e % nc;
+      const int64_t o = (((int64_t)b * H + gi) * W + gj) * C + c;
+      lsum += fabsf(x[o] - y[o]);
     }
   }
   ssum = wave_sum(ssum);
@@ -154,58 +231,44 @@ __global__ void __launch_bounds__(256)
 bwd_kernel(int B, int H, int W, int C, const float *__restrict__ x, const float *__restrict__ y,
            const float *__restrict__ maps, const float *__restrict__ dloss,
            float *__restrict__ grad) {
-  __shared__ float sm[3][WIN][WIN];
-  __shared__ float h[3][WIN][TS];
+  __shared__ f2v s_01[WN][WN];  // (dSSIM/dmu1, dSSIM/dE[x^2])
+  __shared__ float s_2[WN][WN];  // dSSIM/dE[xy]
+  __shared__ f2v h_01[WN][TW];
+  __shared__ float h_2[WN][TW];
   const int Hm = H - 2 * R, Wm = W - 2 * R;
-  const int b = blockIdx.z;
-  const int qi0 = blockIdx.y * TS, qj0 = blockIdx.x * TS;  // image tile origin
-  const int tid = threadIdx.x, ti = tid / TS, tj = tid % TS;
-  const int qi = qi0 + ti, qj = qj0 + tj;
+  const int b = blockIdx.z / C, c = blockIdx.z - b * C;  // one channel per workgroup
+  const int qi0 = blockIdx.y * TW, qj0 = blockIdx.x * TW;  // image tile origin
+  const int tid = threadIdx.x, tq = tid & 31, tr = tid >> 5;
   const float n_map = (float)B * C * Hm * Wm, n_img = (float)B * C * H * W;
   const float g_ssim = dloss[0] / n_map, g_l1 = dloss[1] / n_img;
   const int64_t plane = (int64_t)Hm * Wm;
-  for (int c = 0; c < C; ++c) {
+  {
     const float *mp = maps + (((int64_t)b * C + c) * 3) * plane;
-    // map window rows [qi0-10, qi0+16), cols [qj0-10, qj0+16)
-    for (int e = tid; e < WIN * WIN; e += 256) {
-      const int r = e / WIN, q = e % WIN;
+    // map window rows [qi0-10, qi0+32), cols [qj0-10, qj0+32), zero outside
+    for (int e = tid; e < WN * WN; e += 256) {
+      const int r = e / WN, q = e - r * WN;
       const int pi = qi0 - 2 * R + r, pj = qj0 - 2 * R + q;
       const bool in = pi >= 0 && pi < Hm && pj >= 0 && pj < Wm;
       const int64_t o = (int64_t)pi * Wm + pj;
-      sm[0][r][q] = in ? mp[o] : 0.f;
-      sm[1][r][q] = in ? mp[plane + o] : 0.f;
-      sm[2][r][q] = in ? mp[2 * plane + o] : 0.f;
+      s_01[r][q] = in ? f2v{mp[o], mp[plane + o]} : f2v{0.f, 0.f};
+      s_2[r][q] = in ? mp[2 * plane + o] : 0.f;
     }
     __syncthreads();
-    for (int e = tid; e < WIN * TS; e += 256) {
-      const int r = e / TS, q = e % TS;
-      float a0 = 0.f, a1 = 0.f, a2 = 0.f;
+    // the adjoint of the valid correlation is the full correlation with the
+    // flipped kernel, and the Gaussian window is symmetric
+    Blur3 o;
+    blur3<false>(s_01, nullptr, s_2, h_01, nullptr, h_2, tid, o);
 #pragma unroll
-      for (int k = 0; k < K; ++k) {
-        const float g = kG[k];
-        a0 += g * sm[0][r][q + k];
-        a1 += g * sm[1][r][q + k];
-        a2 += g * sm[2][r][q + k];
+    for (int j = 0; j < 4; ++j) {
+      const int qi = qi0 + 4 * tr + j, qj = qj0 + tq;
+      if (qi < H && qj < W) {
+        const int64_t off = (((int64_t)b * H + qi) * W + qj) * C + c;
+        const float vx = x[off], vy = y[off];
+        const float d = vx - vy;
+        const float sgn = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
+        grad[off] = g_ssim * (o.a[j].x + 2.f * vx * o.a[j].y + vy * o.c[j]) + g_l1 * sgn;
       }
-      h[0][r][q] = a0; h[1][r][q] = a1; h[2][r][q] = a2;
     }
-    __syncthreads();
-    float A = 0.f, Bv = 0.f, Cv = 0.f;
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const float g = kG[k];
-      A += g * h[0][ti + k][tj];
-      Bv += g * h[1][ti + k][tj];
-      Cv += g * h[2][ti + k][tj];
-    }
-    if (qi < H && qj < W) {
-      const int64_t o = (((int64_t)b * H + qi) * W + qj) * C + c;
-      const float vx = x[o], vy = y[o];
-      const float d = vx - vy;
-      const float sgn = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
-      grad[o] = g_ssim * (A + 2.f * vx * Bv + vy * Cv) + g_l1 * sgn;
-    }
-    __syncthreads();
   }
 }
 
@@ -217,13 +280,13 @@ using namespace gs;
 static int64_t ssim_map_floats(int B, int H, int W, int C) {
   return (int64_t)B * C * 3 * (int64_t)(H - 10) * (W - 10);
 }
-static int64_t ssim_blocks(int B, int H, int W) {
-  return (int64_t)((W - 10 + 15) / 16) * ((H - 10 + 15) / 16) * B;
+static int64_t ssim_blocks(int B, int H, int W, int C) {
+  return (int64_t)((W - 10 + 31) / 32) * ((H - 10 + 31) / 32) * B * C;
 }
 
 extern "C" int64_t gsplat_hip_ssim_workspace_bytes(int B, int H, int W, int C) {
   if (H <= 10 || W <= 10) return 0;
-  return (int64_t)sizeof(float) * (ssim_map_floats(B, H, W, C) + 2 * ssim_blocks(B, H, W));
+  return (int64_t)sizeof(float) * (ssim_map_floats(B, H, W, C) + 2 * ssim_blocks(B, H, W, C));
 }
 
 extern "C" int gsplat_hip_ssim_l1_fwd(int B, int H, int W, int C, const float *img1,
@@ -234,11 +297,11 @@ extern "C" int gsplat_hip_ssim_l1_fwd(int B, int H, int W, int C, const float *i
   hipStream_t st = (hipStream_t)stream;
   float *maps = reinterpret_cast<float *>(workspace);
   float *partials = maps + ssim_map_floats(B, H, W, C);
-  dim3 grid((W - 10 + 15) / 16, (H - 10 + 15) / 16, B);
+  dim3 grid((W - 10 + 31) / 32, (H - 10 + 31) / 32, B * C);
   hipLaunchKernelGGL(ssim::fwd_kernel, grid, dim3(256), 0, st, B, H, W, C, img1, img2, maps,
                      partials);
   hipLaunchKernelGGL(ssim::reduce_partials_kernel, dim3(1), dim3(1024), 0, st,
-                     (int)ssim_blocks(B, H, W), partials, sums);
+                     (int)ssim_blocks(B, H, W, C), partials, sums);
   GS_CHECK_LAUNCH("ssim_l1_fwd");
   return 0;
 }
@@ -247,7 +310,7 @@ extern "C" int gsplat_hip_ssim_l1_bwd(int B, int H, int W, int C, const float *i
                                       const float *img2, const void *workspace,
                                       const float *dloss, float *grad_img1, void *stream) {
   GS_REQUIRE(B > 0 && C > 0 && H > 10 && W > 10, "ssim_l1_bwd: bad image size %dx%d", H, W);
-  dim3 grid((W + 15) / 16, (H + 15) / 16, B);
+  dim3 grid((W + 31) / 32, (H + 31) / 32, B * C);
   hipLaunchKernelGGL(ssim::bwd_kernel, grid, dim3(256), 0, (hipStream_t)stream, B, H, W, C, img1,
                      img2, reinterpret_cast<const float *>(workspace), dloss, grad_img1);
   GS_CHECK_LAUNCH("ssim_l1_bwd");
