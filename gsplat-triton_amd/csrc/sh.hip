@@ -112,22 +112,53 @@ struct VCoeffs {
   int64_t s0, sr;
 };
 
-template <int DEG>
+// The rasterization() colour path fused in (gsplat/rendering.py:396-406):
+// dirs = means - camera centre (the centre from the world-to-camera matrix,
+// -R^T t, instead of torch.inverse), masks = radii > 0, and the output
+// transform clamp_min(sh + 0.5, 0) with its backward mask (input >= 0, as
+// torch.clamp_min).  Masked rows give 0.5, as `colors[~masks] = 0` then + 0.5.
+struct Fused {
+  const float *means;     // [N, 3]
+  const float *viewmats;  // [C, 4, 4]
+  const int32_t *radii;   // [C, N]
+  int64_t N;
+};
+
+GS_INLINE void fused_dir(const Fused &fz, int64_t i, float &x, float &y, float &z) {
+  const int64_t c = i / fz.N, g = i - c * fz.N;
+  const float *vm = fz.viewmats + 16 * c;
+  const float t0 = vm[3], t1 = vm[7], t2 = vm[11];
+  const float px = -(vm[0] * t0 + vm[4] * t1 + vm[8] * t2);
+  const float py = -(vm[1] * t0 + vm[5] * t1 + vm[9] * t2);
+  const float pz = -(vm[2] * t0 + vm[6] * t1 + vm[10] * t2);
+  const float *m = fz.means + 3 * g;
+  x = m[0] - px;
+  y = m[1] - py;
+  z = m[2] - pz;
+}
+
+template <int DEG, bool FUSED>
 __global__ void __launch_bounds__(256)
 sh_fwd_kernel(int64_t n, int64_t n_coeff_rows, Coeffs cf, const float *__restrict__ dirs,
-              const uint8_t *__restrict__ masks, float *__restrict__ colors) {
+              const uint8_t *__restrict__ masks, float *__restrict__ colors, Fused fz) {
   constexpr int NB = (DEG + 1) * (DEG + 1);
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   float *o = colors + 3 * i;
-  if (masks && !masks[i]) {
-    o[0] = 0.f; o[1] = 0.f; o[2] = 0.f;
+  const bool on = FUSED ? fz.radii[i] > 0 : (!masks || masks[i]);
+  if (!on) {
+    const float v = FUSED ? 0.5f : 0.f;
+    o[0] = v; o[1] = v; o[2] = v;
     return;
   }
   float x = 0.f, y = 0.f, z = 0.f;
   if (DEG > 0) {
-    const float *d = dirs + 3 * i;
-    x = d[0]; y = d[1]; z = d[2];
+    if (FUSED) {
+      fused_dir(fz, i, x, y, z);
+    } else {
+      const float *d = dirs + 3 * i;
+      x = d[0]; y = d[1]; z = d[2];
+    }
     const float inorm = rsqrtf(x * x + y * y + z * z);
     x *= inorm; y *= inorm; z *= inorm;
   }
@@ -143,31 +174,40 @@ sh_fwd_kernel(int64_t n, int64_t n_coeff_rows, Coeffs cf, const float *__restric
     g += B[k] * pr[3 * (k - 1) + 1];
     b += B[k] * pr[3 * (k - 1) + 2];
   }
+  if (FUSED) {
+    r = fmaxf(r + 0.5f, 0.f);
+    g = fmaxf(g + 0.5f, 0.f);
+    b = fmaxf(b + 0.5f, 0.f);
+  }
   o[0] = r; o[1] = g; o[2] = b;
 }
 
-template <int DEG>
+template <int DEG, bool FUSED>
 __global__ void __launch_bounds__(256)
 sh_bwd_kernel(int64_t n, int K, int64_t n_coeff_rows, Coeffs cf, const float *__restrict__ dirs,
               const uint8_t *__restrict__ masks, const float *__restrict__ v_colors, VCoeffs vc,
-              float *__restrict__ v_dirs) {
+              float *__restrict__ v_dirs, Fused fz) {
   constexpr int NB = (DEG + 1) * (DEG + 1);
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   float *v0 = vc.c0 + i * vc.s0;
   float *vr_ = vc.cr + i * vc.sr;
-  const bool on = !masks || masks[i];
+  const bool on = FUSED ? fz.radii[i] > 0 : (!masks || masks[i]);
   if (!on) {
     v0[0] = 0.f; v0[1] = 0.f; v0[2] = 0.f;
     for (int k = 0; k < 3 * (K - 1); ++k) vr_[k] = 0.f;
     if (v_dirs) { v_dirs[3 * i] = 0.f; v_dirs[3 * i + 1] = 0.f; v_dirs[3 * i + 2] = 0.f; }
     return;
   }
-  const float vr = v_colors[3 * i], vg = v_colors[3 * i + 1], vb = v_colors[3 * i + 2];
+  float vr = v_colors[3 * i], vg = v_colors[3 * i + 1], vb = v_colors[3 * i + 2];
   float x = 0.f, y = 0.f, z = 0.f, inorm = 0.f;
   if (DEG > 0) {
-    const float *d = dirs + 3 * i;
-    x = d[0]; y = d[1]; z = d[2];
+    if (FUSED) {
+      fused_dir(fz, i, x, y, z);
+    } else {
+      const float *d = dirs + 3 * i;
+      x = d[0]; y = d[1]; z = d[2];
+    }
     inorm = rsqrtf(x * x + y * y + z * z);
     x *= inorm; y *= inorm; z *= inorm;
   }
@@ -176,6 +216,21 @@ sh_bwd_kernel(int64_t n, int K, int64_t n_coeff_rows, Coeffs cf, const float *__
   const bool want_dirs = (v_dirs != nullptr) && DEG > 0;
   if (want_dirs) sh_basis<DEG, true>(x, y, z, B, dB);
   else sh_basis<DEG, false>(x, y, z, B, nullptr);
+  if (FUSED) {  // clamp_min(sh + 0.5, 0) passes the gradient where sh + 0.5 >= 0
+    const int64_t row = i % n_coeff_rows;
+    const float *p0 = cf.c0 + row * cf.s0;
+    const float *pr = cf.cr + row * cf.sr;
+    float r = B[0] * p0[0], g = B[0] * p0[1], b = B[0] * p0[2];
+#pragma unroll
+    for (int k = 1; k < NB; ++k) {
+      r += B[k] * pr[3 * (k - 1)];
+      g += B[k] * pr[3 * (k - 1) + 1];
+      b += B[k] * pr[3 * (k - 1) + 2];
+    }
+    vr = (r + 0.5f >= 0.f) ? vr : 0.f;
+    vg = (g + 0.5f >= 0.f) ? vg : 0.f;
+    vb = (b + 0.5f >= 0.f) ? vb : 0.f;
+  }
   v0[0] = B[0] * vr; v0[1] = B[0] * vg; v0[2] = B[0] * vb;
 #pragma unroll
   for (int k = 1; k < NB; ++k) {
@@ -232,8 +287,8 @@ extern "C" int gsplat_hip_sh_fwd(int degree, int64_t n, int64_t n_coeff_rows, in
   hipStream_t st = (hipStream_t)stream;
 #define GS_SH_FWD(D)                                                                   \
   case D:                                                                              \
-    hipLaunchKernelGGL(sh_fwd_kernel<D>, grid, dim3(256), 0, st, n, n_coeff_rows, cf, \
-                       dirs, masks, colors);                                           \
+    hipLaunchKernelGGL((sh_fwd_kernel<D, false>), grid, dim3(256), 0, st, n, n_coeff_rows, \
+                       cf, dirs, masks, colors, Fused{});                                \
     break;
   switch (degree) { GS_SH_FWD(0) GS_SH_FWD(1) GS_SH_FWD(2) GS_SH_FWD(3) GS_SH_FWD(4) }
 #undef GS_SH_FWD
@@ -258,11 +313,67 @@ extern "C" int gsplat_hip_sh_bwd(int degree, int64_t n, int64_t n_coeff_rows, in
   hipStream_t st = (hipStream_t)stream;
 #define GS_SH_BWD(D)                                                                       \
   case D:                                                                                  \
-    hipLaunchKernelGGL(sh_bwd_kernel<D>, grid, dim3(256), 0, st, n, K, n_coeff_rows, cf,  \
-                       dirs, masks, v_colors, vc, v_dirs);                                 \
+    hipLaunchKernelGGL((sh_bwd_kernel<D, false>), grid, dim3(256), 0, st, n, K, n_coeff_rows, \
+                       cf, dirs, masks, v_colors, vc, v_dirs, Fused{});                       \
     break;
   switch (degree) { GS_SH_BWD(0) GS_SH_BWD(1) GS_SH_BWD(2) GS_SH_BWD(3) GS_SH_BWD(4) }
 #undef GS_SH_BWD
   GS_CHECK_LAUNCH("sh_bwd");
+  return 0;
+}
+
+// rasterization()'s colour path in one kernel each way (see struct Fused):
+// colors[C,N,3] = clamp_min(SH(means - campos(viewmats)) + 0.5, 0), radii
+// masking.  Backward: v_coeffs (and v_coeffs_rest) per row, v_dirs[C,N,3]
+// (= the gradient of means per camera; NULL to skip).
+extern "C" int gsplat_hip_sh_colors_fwd(int degree, int C, int64_t N, int64_t n_coeff_rows, int K,
+                                        const float *means, const float *viewmats,
+                                        const float *coeffs, const float *coeffs_rest,
+                                        const int32_t *radii, float *colors, void *stream) {
+  const int64_t n = (int64_t)C * N;
+  if (n <= 0) return 0;
+  if (int e = sh_check(degree, n, n_coeff_rows, K, "sh_colors_fwd")) return e;
+  Coeffs cf = coeffs_rest ? Coeffs{coeffs, coeffs_rest, 3, 3 * (int64_t)(K - 1)}
+                          : Coeffs{coeffs, coeffs + 3, 3 * (int64_t)K, 3 * (int64_t)K};
+  const Fused fz{means, viewmats, radii, N};
+  dim3 grid((unsigned)((n + 255) / 256));
+  hipStream_t st = (hipStream_t)stream;
+#define GS_SH_FWD(D)                                                                        \
+  case D:                                                                                   \
+    hipLaunchKernelGGL((sh_fwd_kernel<D, true>), grid, dim3(256), 0, st, n, n_coeff_rows, cf, \
+                       nullptr, nullptr, colors, fz);                                       \
+    break;
+  switch (degree) { GS_SH_FWD(0) GS_SH_FWD(1) GS_SH_FWD(2) GS_SH_FWD(3) GS_SH_FWD(4) }
+#undef GS_SH_FWD
+  GS_CHECK_LAUNCH("sh_colors_fwd");
+  return 0;
+}
+
+extern "C" int gsplat_hip_sh_colors_bwd(int degree, int C, int64_t N, int64_t n_coeff_rows, int K,
+                                        const float *means, const float *viewmats,
+                                        const float *coeffs, const float *coeffs_rest,
+                                        const int32_t *radii, const float *v_colors,
+                                        float *v_coeffs, float *v_coeffs_rest, float *v_dirs,
+                                        void *stream) {
+  const int64_t n = (int64_t)C * N;
+  if (n <= 0) return 0;
+  if (int e = sh_check(degree, n, n_coeff_rows, K, "sh_colors_bwd")) return e;
+  GS_REQUIRE(!coeffs_rest == !v_coeffs_rest,
+             "sh_colors_bwd: coeffs_rest and v_coeffs_rest must both be given or both null");
+  Coeffs cf = coeffs_rest ? Coeffs{coeffs, coeffs_rest, 3, 3 * (int64_t)(K - 1)}
+                          : Coeffs{coeffs, coeffs + 3, 3 * (int64_t)K, 3 * (int64_t)K};
+  VCoeffs vc = v_coeffs_rest ? VCoeffs{v_coeffs, v_coeffs_rest, 3, 3 * (int64_t)(K - 1)}
+                             : VCoeffs{v_coeffs, v_coeffs + 3, 3 * (int64_t)K, 3 * (int64_t)K};
+  const Fused fz{means, viewmats, radii, N};
+  dim3 grid((unsigned)((n + 255) / 256));
+  hipStream_t st = (hipStream_t)stream;
+#define GS_SH_BWD(D)                                                                           \
+  case D:                                                                                      \
+    hipLaunchKernelGGL((sh_bwd_kernel<D, true>), grid, dim3(256), 0, st, n, K, n_coeff_rows, cf, \
+                       nullptr, nullptr, v_colors, vc, v_dirs, fz);                            \
+    break;
+  switch (degree) { GS_SH_BWD(0) GS_SH_BWD(1) GS_SH_BWD(2) GS_SH_BWD(3) GS_SH_BWD(4) }
+#undef GS_SH_BWD
+  GS_CHECK_LAUNCH("sh_colors_bwd");
   return 0;
 }

@@ -12,7 +12,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GSPLAT_HIP_LIB", os.path.join(_HERE, "libgsplat_hip.so"))
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 _p = ctypes.c_void_p
 _i32 = ctypes.c_int
@@ -29,6 +29,9 @@ _SIGS = {
                                          _p, _p, _p, _p, _p, _p, _p, _p, _p, _p]),
     "gsplat_hip_sh_fwd": (_i32, [_i32, _i64, _i64, _i32, _p, _p, _p, _p, _p, _p]),
     "gsplat_hip_sh_bwd": (_i32, [_i32, _i64, _i64, _i32, _p, _p, _p, _p, _p, _p, _p, _p, _p]),
+    "gsplat_hip_sh_colors_fwd": (_i32, [_i32, _i32, _i64, _i64, _i32, _p, _p, _p, _p, _p, _p, _p]),
+    "gsplat_hip_sh_colors_bwd": (_i32, [_i32, _i32, _i64, _i64, _i32, _p, _p, _p, _p, _p, _p, _p,
+                                        _p, _p, _p]),
     "gsplat_hip_isect_workspace_bytes": (_i64, [_i64]),
     "gsplat_hip_isect_count": (_i32, [_i64, _p, _p, _i32, _i32, _i32, _p, _p, _p, _p]),
     "gsplat_hip_isect_write": (_i32, [_i64, _i32, _p, _p, _p, _p, _i32, _i32, _i32, _i32, _p,

@@ -377,6 +377,74 @@ def spherical_harmonics(
     return _SphericalHarmonics.apply(degrees_to_use, dirs, coeffs, masks, block_size, rest)
 
 
+class _SHColors(torch.autograd.Function):
+    """rasterization()'s SH colour path in one kernel each way
+    (gsplat/rendering.py:396-406): clamp_min(SH(means - campos) + 0.5, 0)
+    with radii masking.  Differentiable w.r.t. means and the coefficients
+    (viewmats must not require grad -- the caller falls back otherwise)."""
+
+    @staticmethod
+    def forward(ctx, sh_degree, means, viewmats, coeffs, coeffs_rest, radii):
+        means, viewmats = _f32c(means), _f32c(viewmats)
+        base, n_rows = _coeff_rows(coeffs)
+        rest = None
+        if coeffs_rest is not None:
+            rest, n_rows_r = _coeff_rows(coeffs_rest)
+            assert n_rows_r == n_rows and coeffs.shape[-2] == 1, (coeffs.shape, coeffs_rest.shape)
+        radii = radii.to(torch.int32).contiguous()
+        _dev_check(means, viewmats, base, rest, radii)
+        C, N = radii.shape
+        K = coeffs.shape[-2] + (0 if rest is None else coeffs_rest.shape[-2])
+        colors = torch.empty(C, N, 3, device=means.device, dtype=torch.float32)
+        _lib.call("gsplat_hip_sh_colors_fwd", int(sh_degree), C, N, n_rows, K, _ptr(means),
+                  _ptr(viewmats), _ptr(base), _ptr(rest), _ptr(radii), _ptr(colors), _stream())
+        ctx.save_for_backward(means, viewmats, base, rest, radii)
+        ctx.sh_degree, ctx.n_rows, ctx.K = int(sh_degree), n_rows, K
+        ctx.coeff_shape = coeffs.shape
+        ctx.rest_shape = None if coeffs_rest is None else coeffs_rest.shape
+        return colors
+
+    @staticmethod
+    def backward(ctx, v_colors):
+        means, viewmats, base, rest, radii = ctx.saved_tensors
+        C, N = radii.shape
+        K = ctx.K
+        v_colors = _f32c(v_colors)
+        dev = means.device
+        if rest is None:
+            v_coeffs = torch.empty(C, N, K, 3, device=dev)
+            v_rest = None
+        else:
+            v_coeffs = torch.empty(C, N, 1, 3, device=dev)
+            v_rest = torch.empty(C, N, K - 1, 3, device=dev)
+        want_means = ctx.needs_input_grad[1]
+        v_dirs = torch.empty(C, N, 3, device=dev) if want_means else None
+        _lib.call("gsplat_hip_sh_colors_bwd", ctx.sh_degree, C, N, ctx.n_rows, K, _ptr(means),
+                  _ptr(viewmats), _ptr(base), _ptr(rest), _ptr(radii), _ptr(v_colors),
+                  _ptr(v_coeffs), _ptr(v_rest), _ptr(v_dirs), _stream())
+        v_means = None
+        if want_means:
+            v_means = v_dirs[0] if C == 1 else v_dirs.sum(0)
+        def fold(v, shape):  # [C,N,..] -> the input's shape (sum over cameras)
+            if v is None:
+                return None
+            if len(shape) == 3:  # shared [N,K,3] coefficients
+                v = v[0] if C == 1 else v.sum(0)
+            return v.view(shape)
+        return (None, v_means, None, fold(v_coeffs, ctx.coeff_shape), fold(v_rest, ctx.rest_shape),
+                None)
+
+
+def sh_colors(sh_degree: int, means: Tensor, viewmats: Tensor, coeffs, radii: Tensor) -> Tensor:
+    """colors [C,N,3] = clamp_min(SH(means - campos) + 0.5, 0), radii-masked:
+    the colour computation of rendering.rasterization (rendering.py:396-406)
+    fused.  `coeffs`: [N,K,3] / [C,N,K,3] or the pair (sh0, shN)."""
+    rest = None
+    if isinstance(coeffs, (tuple, list)):
+        coeffs, rest = coeffs
+    return _SHColors.apply(sh_degree, means, viewmats, coeffs, rest, radii)
+
+
 # ============================================================ rasterization ==
 class _RasterizeToPixels(torch.autograd.Function):
     """Rasterize Gaussians (gsplat/triton_impl/_wrapper.py:42-182)."""

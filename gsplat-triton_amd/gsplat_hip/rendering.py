@@ -20,6 +20,7 @@ from ._wrapper import (
     isect_offset_encode,
     isect_tiles,
     rasterize_to_pixels,
+    sh_colors,
     spherical_harmonics,
 )
 
@@ -108,6 +109,11 @@ def rasterization(
     if sh_degree is None:
         if colors.dim() == 2:
             colors = colors[None] if C == 1 else colors.expand(C, -1, -1)
+    elif not viewmats.requires_grad and (sh_rest is not None or colors.dim() == 3):
+        # one kernel each way: dirs from the camera centres, radii masking,
+        # clamp_min(sh + 0.5, 0) (same values as the branch below)
+        colors = sh_colors(sh_degree, means, viewmats,
+                           colors if sh_rest is None else (colors, sh_rest), radii)
     else:
         camtoworlds = torch.inverse(viewmats)  # [C, 4, 4]
         dirs = means[None, :, :] - camtoworlds[:, None, :3, 3]  # [C, N, 3]

@@ -83,6 +83,23 @@ int gsplat_hip_sh_bwd(int degree, int64_t n, int64_t n_coeff_rows, int K, const 
                       const float *v_colors, float *v_coeffs, float *v_coeffs_rest,
                       float *v_dirs, void *stream);
 
+/* rasterization()'s colour path fused (gsplat/rendering.py:396-406 with the
+ * SH of _wrapper.py:596-620): colors[C,N,3] = clamp_min(SH(degree, means -
+ * campos) + 0.5, 0) with campos = -R^T t from viewmats[C,4,4] (instead of
+ * torch.inverse), rows with radii[C,N] <= 0 -> 0.5 (the reference zeroes
+ * masked SH colours, then adds 0.5).  Coefficient layout as gsplat_hip_sh_fwd.
+ * Backward: v_coeffs(/v_coeffs_rest) per row with the clamp_min mask
+ * (sh + 0.5 >= 0), v_dirs[C,N,3] = d loss / d means per camera (NULL: skip). */
+int gsplat_hip_sh_colors_fwd(int degree, int C, int64_t N, int64_t n_coeff_rows, int K,
+                             const float *means, const float *viewmats, const float *coeffs,
+                             const float *coeffs_rest, const int32_t *radii, float *colors,
+                             void *stream);
+int gsplat_hip_sh_colors_bwd(int degree, int C, int64_t N, int64_t n_coeff_rows, int K,
+                             const float *means, const float *viewmats, const float *coeffs,
+                             const float *coeffs_rest, const int32_t *radii,
+                             const float *v_colors, float *v_coeffs, float *v_coeffs_rest,
+                             float *v_dirs, void *stream);
+
 /* ---------------------------------------------------------------------------
  * Tile intersection.  Replaces isect_tiles() (gsplat/triton_impl/isect_tiles.py:13-131)
  * as three calls so that the caller can size the outputs after ONE device->host

@@ -480,3 +480,52 @@ def test_sh_split_coeffs_match_concatenated():
     gb = torch.autograd.grad((b * w).sum(), (sh0, shN, dirs))
     for x, y in zip(ga, gb):
         close(x, y, 1e-6, 1e-6)
+
+
+@pytest.mark.parametrize("degree,C,split", [(3, 1, True), (3, 2, False), (0, 1, False),
+                                            (4, 2, True), (1, 1, False)])
+def test_sh_colors_fused_vs_unfused(degree, C, split):
+    """rendering.rasterization's colour path fused into one kernel (dirs from
+    -R^T t, radii masking, clamp_min(+0.5)) == the reference's torch glue
+    around spherical_harmonics (rendering.py:396-406), values and grads."""
+    import gsplat_hip
+    from gsplat_hip._wrapper import sh_colors
+    g = torch.Generator().manual_seed(degree * 10 + C)
+    N, K = 3000, (max(degree, 3) + 1) ** 2
+    means = (torch.randn(N, 3, generator=g) * 2).to(DEV)
+    sh = (torch.randn(N, K, 3, generator=g) * 0.5).to(DEV)
+    vm = torch.eye(4).repeat(C, 1, 1)
+    for c in range(C):
+        q = torch.nn.functional.normalize(torch.randn(4, generator=g), dim=0)
+        w, x, y, z = q.tolist()
+        vm[c, :3, :3] = torch.tensor([[1 - 2 * (y * y + z * z), 2 * (x * y - w * z), 2 * (x * z + w * y)],
+                                      [2 * (x * y + w * z), 1 - 2 * (x * x + z * z), 2 * (y * z - w * x)],
+                                      [2 * (x * z - w * y), 2 * (y * z + w * x), 1 - 2 * (x * x + y * y)]])
+        vm[c, :3, 3] = torch.randn(3, generator=g) * 3
+    vm = vm.to(DEV)
+    radii = (torch.rand(C, N, generator=g) > 0.3).int().to(DEV) * 5
+    vc = torch.randn(C, N, 3, generator=g).to(DEV)
+
+    def unfused(m, s0, sN):
+        shs = torch.cat([s0, sN], 1) if split else s0
+        dirs = m[None] - torch.inverse(vm)[:, None, :3, 3]
+        col = gsplat_hip.spherical_harmonics(degree, dirs, shs.expand(C, -1, -1, -1),
+                                             masks=radii > 0)
+        return torch.clamp_min(col + 0.5, 0.0)
+
+    def fused(m, s0, sN):
+        return sh_colors(degree, m, vm, (s0, sN) if split else s0, radii)
+
+    outs = []
+    for fn in (unfused, fused):
+        m = means.clone().requires_grad_(True)
+        s0 = (sh[:, :1] if split else sh).clone().requires_grad_(True)
+        sN = sh[:, 1:].clone().requires_grad_(True) if split else None
+        col = fn(m, s0, sN)
+        ins = [m, s0] + ([sN] if split else [])
+        grads = torch.autograd.grad((col * vc).sum(), ins)
+        outs.append((col,) + tuple(grads))
+    # campos = -R^T t vs torch.inverse differ by float rounding (R is
+    # orthonormal only to ~1e-7); the means gradient at degree 4 amplifies it
+    for a, b in zip(outs[0], outs[1]):
+        close(b, a, 1e-4, 5e-5)
