@@ -22,7 +22,10 @@
 #include "common.h"
 #include "../../include/gsplat_hip.h"
 
+#include <rocprim/block/block_radix_sort.hpp>
 #include <rocprim/device/device_radix_sort.hpp>
+
+#include "lsd_sort.h"
 
 namespace gs {
 
@@ -389,13 +392,8 @@ struct SortedLayout {
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 SortedLayout sorted_layout(int64_t nV, int64_t n, int key_bits) {
-  size_t t1 = 0, t2 = 0;
-  (void)rocprim::radix_sort_pairs(nullptr, t1, (const uint32_t *)nullptr, (uint32_t *)nullptr,
-                                  (const int32_t *)nullptr, (int32_t *)nullptr, (size_t)nV, 0u,
-                                  32u, (hipStream_t)0);
-  (void)rocprim::radix_sort_pairs(nullptr, t2, (const uint32_t *)nullptr, (uint32_t *)nullptr,
-                                  (const int32_t *)nullptr, (int32_t *)nullptr, (size_t)n, 0u,
-                                  (unsigned)(key_bits > 0 ? key_bits : 1), (hipStream_t)0);
+  (void)key_bits;
+  const size_t t1 = lsd_sort_scratch_bytes(nV), t2 = lsd_sort_scratch_bytes(n);
   SortedLayout L{};
   size_t o = 0;
   L.V = o; o = align256(o + 4 * (size_t)nV);
@@ -451,10 +449,8 @@ extern "C" int gsplat_hip_isect_write_sorted(
   const int64_t *vis_prefix = reinterpret_cast<const int64_t *>(count_workspace) + nbG + 1;
   hipLaunchKernelGGL(isect_compact_kernel, dim3((unsigned)nbG), dim3(kIsectBlock), 0, st,
                      n_gaussians, tiles_per_gauss, depths, vis_prefix, V, dkey);
-  size_t tb = L.tmp_bytes;
-  hipError_t e = rocprim::radix_sort_pairs(tmp, tb, dkey, dkeys, V, Vs, (size_t)n_visible, 0u, 32u,
-                                           st);
-  GS_REQUIRE(e == hipSuccess, "isect_write_sorted: depth sort: %s", hipGetErrorString(e));
+  // stable depth sort of the visible Gaussians (32 key bits)
+  if (lsd_sort_pairs(dkey, V, dkeys, Vs, n_visible, 0, 32, tmp, st) == 0) Vs = V;
   const int64_t nbV = (n_visible + kIsectBlock - 1) / kIsectBlock;
   hipLaunchKernelGGL(isect_sorted_count_kernel, dim3((unsigned)nbV), dim3(kIsectBlock), 0, st,
                      n_visible, Vs, tiles_per_gauss, blk);
@@ -463,18 +459,312 @@ extern "C" int gsplat_hip_isect_write_sorted(
   hipLaunchKernelGGL(isect_sorted_emit_kernel, dim3((unsigned)nbV), dim3(kIsectBlock), 0, st,
                      n_visible, N, Vs, means2d, radii, depths, camera_ids, tile_size, tile_width,
                      tile_height, tile_bits, all_ones, blk, tkey, val);
-  const uint32_t *fk = tkey;
-  const int32_t *fv = val;
-  if (key_bits > 0) {
-    tb = L.tmp_bytes;
-    e = rocprim::radix_sort_pairs(tmp, tb, tkey, tkeys, val, vals, (size_t)n_isects, 0u,
-                                  (unsigned)key_bits, st);
-    GS_REQUIRE(e == hipSuccess, "isect_write_sorted: tile sort: %s", hipGetErrorString(e));
-    fk = tkeys;
-    fv = vals;
-  }
+  // stable (camera, tile) sort keeps the depth order inside every tile
+  const bool in_alt = lsd_sort_pairs(tkey, val, tkeys, vals, n_isects, 0, key_bits, tmp, st) == 1;
+  const uint32_t *fk = in_alt ? tkeys : tkey;
+  const int32_t *fv = in_alt ? vals : val;
   hipLaunchKernelGGL(isect_sorted_finalize_kernel, dim3((unsigned)((n_isects + 255) / 256)),
                      dim3(256), 0, st, n_isects, fk, fv, depths, isect_ids, flatten_ids);
   GS_CHECK_LAUNCH("isect_write_sorted");
+  return 0;
+}
+
+// -------------------------------------------------------- tile-first path --
+// Sorted isects with two 32-bit sorts and no depth sort of the Gaussians:
+// (1) emission in Gaussian-major order with 32-bit (camera, tile) keys,
+// (2) a stable radix sort by those keys (tile_bits + cam_bits bits), which
+//     keeps Gaussian-index order inside every (camera, tile),
+// (3) a segmented radix sort of each (camera, tile) run by the depth bits
+//     (stable: equal depths stay in Gaussian-index order).
+// The result is the reference's stable sort of (cam | tile | depth) keys
+// element for element.  Negative depths: all-ones (camera, tile) key, and
+// unsigned depth order inside that run, exactly as the reference's masked
+// 64-bit keys.
+namespace gs {
+
+__global__ void __launch_bounds__(kIsectBlock)
+isect_write_tiles_kernel(int64_t G, int N, const float *__restrict__ means2d,
+                         const int32_t *__restrict__ radii, const float *__restrict__ depths,
+                         const int32_t *__restrict__ camera_ids, int ts, int tw, int th,
+                         int tile_bits, uint32_t key_all_ones,
+                         const int64_t *__restrict__ block_prefix, uint32_t *__restrict__ tkey,
+                         int32_t *__restrict__ val) {
+  __shared__ int64_t lds[kIsectBlock / 64 + 1];
+  const int64_t i = (int64_t)blockIdx.x * kIsectBlock + threadIdx.x;
+  Rect rc{0, 0, 0, 0};
+  const int cnt = (i < G) ? tiles_of(means2d, radii, i, ts, tw, th, &rc) : 0;
+  int64_t tot;
+  const int64_t local = block_exclusive_scan<int64_t>((int64_t)cnt, lds, &tot);
+  if (cnt == 0) return;
+  int64_t cur = block_prefix[blockIdx.x] + local;
+  const uint32_t cam = camera_ids ? (uint32_t)camera_ids[i] : (uint32_t)(i / N);
+  const bool neg = __float_as_int(depths[i]) < 0;
+  for (int y = rc.y0; y < rc.y1; ++y) {
+    for (int x = rc.x0; x < rc.x1; ++x) {
+      tkey[cur] = neg ? key_all_ones : ((cam << tile_bits) | (uint32_t)(y * tw + x));
+      val[cur] = (int32_t)i;
+      ++cur;
+    }
+  }
+}
+
+// starts[t] = first sorted isect with (camera, tile) key index >= t, for
+// t in [0, n_total]; starts[n_total + 1] = n.  Keys outside the grid (the
+// all-ones key when it is not a real tile) form the last run.
+__global__ void __launch_bounds__(256)
+isect_key_starts_kernel(int64_t n, const uint32_t *__restrict__ tkey, int n_total, int n_tiles,
+                        int tile_bits, int32_t *__restrict__ starts) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t tmask = (1u << tile_bits) - 1u;
+  auto idx_of = [&](uint32_t k) -> int64_t {
+    const int64_t t = (int64_t)(k >> tile_bits) * n_tiles + (k & tmask);
+    return t < n_total ? t : n_total;
+  };
+  const int64_t cur = idx_of(tkey[i]);
+  if (i == 0) {
+    for (int64_t t = 0; t <= cur; ++t) starts[t] = 0;
+  } else {
+    const int64_t prev = idx_of(tkey[i - 1]);
+    for (int64_t t = prev + 1; t <= cur; ++t) starts[t] = (int32_t)i;
+  }
+  if (i == n - 1) {
+    for (int64_t t = cur + 1; t <= n_total; ++t) starts[t] = (int32_t)n;
+    starts[n_total + 1] = (int32_t)n;
+  }
+}
+
+// Depth order inside every (camera, tile) run, and the final 64-bit ids.
+// A run (Gaussian-index order after the stable key sort) is sorted stably by
+// depth bits and written out as isect_ids / flatten_ids.
+//   isect_tile_sort_small_kernel: one 256-lane workgroup per run, rocPRIM
+//     block radix sort in LDS for runs up to kSmallCap; longer runs are
+//     appended to a list;
+//   isect_tile_sort_large_kernel: one 1024-lane workgroup per listed run,
+//     block radix sort up to kLargeCap, beyond that a bitonic sort of unique
+//     (depth bits, position) keys in a private global scratch region
+//     (pathological scenes).
+constexpr int kSmallCap = 4096;
+constexpr int kLargeCap = 16384;
+
+template <int NT>
+__device__ __forceinline__ void bitonic_sort(uint64_t *k, int P) {
+  for (int kk = 2; kk <= P; kk <<= 1) {
+    for (int j = kk >> 1; j > 0; j >>= 1) {
+      for (int i = threadIdx.x; i < P; i += NT) {
+        const int ixj = i ^ j;
+        if (ixj > i) {
+          const uint64_t a = k[i], b = k[ixj];
+          if ((a > b) == ((i & kk) == 0)) {
+            k[i] = b;
+            k[ixj] = a;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// One run of m <= NT * IPT isects with rocPRIM's block radix sort (LSD,
+// stable): keys = depth bits, values = positions in the run (Gaussian-index
+// order), blocked arrangement -- so equal depths keep Gaussian order.
+template <int NT, int IPT, class Storage>
+__device__ __forceinline__ void run_radix_sort(Storage &storage, int64_t b, int m, uint32_t key32,
+                                               const int32_t *__restrict__ val,
+                                               const float *__restrict__ depths,
+                                               int64_t *__restrict__ isect_ids,
+                                               int32_t *__restrict__ flatten_ids) {
+  using BRS = rocprim::block_radix_sort<uint32_t, NT, IPT, int32_t, 1, 1, 8>;  // 8-bit passes
+  uint32_t key[IPT];
+  int32_t pos[IPT], g[IPT];
+#pragma unroll
+  for (int e = 0; e < IPT; ++e) {
+    const int i = threadIdx.x * IPT + e;
+    g[e] = i < m ? val[b + i] : 0;
+  }
+#pragma unroll
+  for (int e = 0; e < IPT; ++e) {
+    const int i = threadIdx.x * IPT + e;
+    key[e] = i < m ? __float_as_uint(depths[g[e]]) : 0xffffffffu;
+    pos[e] = i;
+  }
+  BRS().sort(key, pos, reinterpret_cast<typename BRS::storage_type &>(storage));
+#pragma unroll
+  for (int e = 0; e < IPT; ++e) {
+    const int i = threadIdx.x * IPT + e;
+    if (i < m) {
+      const int32_t db = (int32_t)key[e];
+      isect_ids[b + i] = db < 0 ? (int64_t)db : (((int64_t)key32 << 32) | (int64_t)(uint32_t)db);
+      flatten_ids[b + i] = val[b + pos[e]];
+    }
+  }
+}
+
+union SmallSortStorage {
+  rocprim::block_radix_sort<uint32_t, 256, 1, int32_t, 1, 1, 8>::storage_type s1;
+  rocprim::block_radix_sort<uint32_t, 256, 2, int32_t, 1, 1, 8>::storage_type s2;
+  rocprim::block_radix_sort<uint32_t, 256, 4, int32_t, 1, 1, 8>::storage_type s4;
+  rocprim::block_radix_sort<uint32_t, 256, 8, int32_t, 1, 1, 8>::storage_type s8;
+  rocprim::block_radix_sort<uint32_t, 256, 16, int32_t, 1, 1, 8>::storage_type s16;
+};
+
+__global__ void __launch_bounds__(256)
+isect_tile_sort_small_kernel(const int32_t *__restrict__ starts, const uint32_t *__restrict__ tkey,
+                             const int32_t *__restrict__ val, const float *__restrict__ depths,
+                             int32_t *__restrict__ large_list, int32_t *__restrict__ n_large,
+                             int64_t *__restrict__ isect_ids, int32_t *__restrict__ flatten_ids) {
+  __shared__ SmallSortStorage storage;
+  const int64_t b = starts[blockIdx.x], e = starts[blockIdx.x + 1];
+  const int m = (int)(e - b);
+  if (m <= 0) return;
+  if (m > kSmallCap) {
+    if (threadIdx.x == 0) large_list[atomicAdd(n_large, 1)] = blockIdx.x;
+    return;
+  }
+  const uint32_t k32 = tkey[b];
+  if (m <= 256) run_radix_sort<256, 1>(storage, b, m, k32, val, depths, isect_ids, flatten_ids);
+  else if (m <= 512) run_radix_sort<256, 2>(storage, b, m, k32, val, depths, isect_ids, flatten_ids);
+  else if (m <= 1024) run_radix_sort<256, 4>(storage, b, m, k32, val, depths, isect_ids, flatten_ids);
+  else if (m <= 2048) run_radix_sort<256, 8>(storage, b, m, k32, val, depths, isect_ids, flatten_ids);
+  else run_radix_sort<256, 16>(storage, b, m, k32, val, depths, isect_ids, flatten_ids);
+}
+
+// Runs longer than kLargeCap sort in global scratch, in slices of kLargeCap
+// gathered per pass (the EPT registers cover kLargeCap elements).
+template <int NT>
+__device__ __forceinline__ void tile_run_sort_global(uint64_t *k, int64_t b, int m,
+                                                     uint32_t key32,
+                                                     const int32_t *__restrict__ val,
+                                                     const float *__restrict__ depths,
+                                                     int64_t *__restrict__ isect_ids,
+                                                     int32_t *__restrict__ flatten_ids) {
+  int P = 1;
+  while (P < m) P <<= 1;
+  for (int i = threadIdx.x; i < P; i += NT)
+    k[i] = i < m ? (((uint64_t)__float_as_uint(depths[val[b + i]]) << 32) | (uint32_t)i)
+                 : ~(uint64_t)0;
+  __syncthreads();
+  bitonic_sort<NT>(k, P);
+  for (int i = threadIdx.x; i < m; i += NT) {
+    const uint64_t kv = k[i];
+    const int32_t db = (int32_t)(kv >> 32);
+    isect_ids[b + i] = db < 0 ? (int64_t)db : (((int64_t)key32 << 32) | (int64_t)(uint32_t)db);
+    flatten_ids[b + i] = val[b + (int64_t)(uint32_t)kv];
+  }
+}
+
+union LargeSortStorage {
+  rocprim::block_radix_sort<uint32_t, 1024, 8, int32_t, 1, 1, 8>::storage_type s8;
+  rocprim::block_radix_sort<uint32_t, 1024, 16, int32_t, 1, 1, 8>::storage_type s16;
+};
+
+__global__ void __launch_bounds__(1024)
+isect_tile_sort_large_kernel(const int32_t *__restrict__ starts, const uint32_t *__restrict__ tkey,
+                             const int32_t *__restrict__ val, const float *__restrict__ depths,
+                             const int32_t *__restrict__ large_list,
+                             const int32_t *__restrict__ n_large, uint64_t *__restrict__ scratch,
+                             int64_t *__restrict__ isect_ids, int32_t *__restrict__ flatten_ids) {
+  __shared__ LargeSortStorage storage;
+  if ((int)blockIdx.x >= *n_large) return;
+  const int run = large_list[blockIdx.x];
+  const int64_t b = starts[run], e = starts[run + 1];
+  const int m = (int)(e - b);
+  const uint32_t k32 = tkey[b];
+  if (m <= 8192)
+    run_radix_sort<1024, 8>(storage, b, m, k32, val, depths, isect_ids, flatten_ids);
+  else if (m <= kLargeCap)
+    run_radix_sort<1024, 16>(storage, b, m, k32, val, depths, isect_ids, flatten_ids);
+  else  // runs are disjoint [b, b+m) and P < 2m: [2b, 2b+P) of scratch is private
+    tile_run_sort_global<1024>(scratch + 2 * b, b, m, k32, val, depths, isect_ids, flatten_ids);
+}
+
+namespace {
+// [tkeys 4n][vals 4n][starts][scratch 16n][rocPRIM temp]; the unsorted keys
+// and values (sort input, dead after the sort) live at the head of scratch.
+struct TileFirstLayout {
+  size_t tkeys, vals, starts, scratch, tmp, total, tmp_bytes;
+};
+
+TileFirstLayout tilefirst_layout(int64_t n, int n_total, int key_bits) {
+  (void)key_bits;
+  const size_t t1 = lsd_sort_scratch_bytes(n);
+  TileFirstLayout L{};
+  size_t o = 0;
+  auto take = [&](size_t bytes) {
+    const size_t at = o;
+    o = align256(o + bytes);
+    return at;
+  };
+  L.tkeys = take(4 * (size_t)n);
+  L.vals = take(4 * (size_t)n);
+  L.starts = take(4 * (size_t)(n_total + 2) + 4 * (size_t)(n_total + 2));  // + large-run list
+  L.scratch = take(16 * (size_t)n);
+  L.tmp_bytes = t1;
+  L.tmp = take(L.tmp_bytes + 1);
+  L.total = o;
+  return L;
+}
+}  // namespace
+}  // namespace gs
+
+extern "C" int64_t gsplat_hip_isect_tilefirst_workspace_bytes(int64_t n_isects, int n_tiles_total,
+                                                              int key_bits) {
+  return (int64_t)tilefirst_layout(n_isects, n_tiles_total, key_bits).total;
+}
+
+extern "C" int gsplat_hip_isect_write_tilefirst(
+    int64_t n_gaussians, int N, const float *means2d, const int32_t *radii, const float *depths,
+    const int32_t *camera_ids, int tile_size, int tile_width, int tile_height, int n_cameras,
+    int tile_bits, int cam_bits, const void *count_workspace, int64_t n_isects, void *workspace,
+    int64_t workspace_bytes, int64_t *isect_ids, int32_t *flatten_ids, void *stream) {
+  GS_REQUIRE(n_gaussians >= 0 && (camera_ids || N > 0 || n_gaussians == 0),
+             "isect_write_tilefirst: N must be > 0 when camera_ids is null");
+  GS_REQUIRE(tile_bits + cam_bits <= 32, "isect_write_tilefirst: tile_bits + cam_bits > 32");
+  GS_REQUIRE(n_isects < (int64_t)1 << 31, "isect_write_tilefirst: more than 2^31 isects");
+  if (n_isects <= 0) return 0;
+  const int key_bits = tile_bits + cam_bits;
+  const int n_tiles = tile_width * tile_height;
+  const int n_total = n_cameras * n_tiles;
+  const TileFirstLayout L = tilefirst_layout(n_isects, n_total, key_bits);
+  GS_REQUIRE(workspace_bytes >= (int64_t)L.total, "isect_write_tilefirst: workspace %lld < %lld",
+             (long long)workspace_bytes, (long long)L.total);
+  hipStream_t st = (hipStream_t)stream;
+  char *ws = reinterpret_cast<char *>(workspace);
+  uint32_t *tkeys = reinterpret_cast<uint32_t *>(ws + L.tkeys);
+  int32_t *vals = reinterpret_cast<int32_t *>(ws + L.vals);
+  int32_t *starts = reinterpret_cast<int32_t *>(ws + L.starts);
+  uint64_t *scratch = reinterpret_cast<uint64_t *>(ws + L.scratch);
+  // The LSD sort ping-pongs between the emission buffers and (tkeys, vals):
+  // emit where an even/odd number of passes ends in (tkeys, vals), so the
+  // global-scratch run sort below never overwrites live keys.
+  const bool emit_alt = ((key_bits + 7) / 8) % 2 == 1;
+  uint32_t *tkey = emit_alt ? reinterpret_cast<uint32_t *>(ws + L.scratch) : tkeys;
+  int32_t *val = emit_alt ? reinterpret_cast<int32_t *>(ws + L.scratch + 4 * (size_t)n_isects) : vals;
+  uint32_t *akey = emit_alt ? tkeys : reinterpret_cast<uint32_t *>(ws + L.scratch);
+  int32_t *aval = emit_alt ? vals : reinterpret_cast<int32_t *>(ws + L.scratch + 4 * (size_t)n_isects);
+  void *tmp = ws + L.tmp;
+
+  const int64_t nbG = (n_gaussians + kIsectBlock - 1) / kIsectBlock;
+  const uint32_t all_ones = key_bits >= 32 ? 0xffffffffu : ((1u << key_bits) - 1u);
+  hipLaunchKernelGGL(isect_write_tiles_kernel, dim3((unsigned)nbG), dim3(kIsectBlock), 0, st,
+                     n_gaussians, N, means2d, radii, depths, camera_ids, tile_size, tile_width,
+                     tile_height, tile_bits, all_ones,
+                     reinterpret_cast<const int64_t *>(count_workspace), tkey, val);
+  lsd_sort_pairs(tkey, val, akey, aval, n_isects, 0, key_bits, tmp, st);
+  const uint32_t *sk = tkeys;  // see emit_alt (key_bits == 0: no pass, emitted there)
+  const int32_t *sv = vals;
+  const unsigned nb = (unsigned)((n_isects + 255) / 256);
+  hipLaunchKernelGGL(isect_key_starts_kernel, dim3(nb), dim3(256), 0, st, n_isects, sk, n_total,
+                     n_tiles, tile_bits, starts);
+  int32_t *large_list = starts + (n_total + 2);
+  int32_t *n_large = reinterpret_cast<int32_t *>(ws + L.tmp);  // rocPRIM temp is free again
+  GS_HIP(hipMemsetAsync(n_large, 0, sizeof(int32_t), st));
+  hipLaunchKernelGGL(isect_tile_sort_small_kernel, dim3((unsigned)(n_total + 1)), dim3(256), 0,
+                     st, starts, sk, sv, depths, large_list, n_large, isect_ids, flatten_ids);
+  hipLaunchKernelGGL(isect_tile_sort_large_kernel,
+                     dim3((unsigned)(n_isects / (kSmallCap + 1) + 1)), dim3(1024), 0, st, starts,
+                     sk, sv, depths, large_list, n_large, scratch, isect_ids, flatten_ids);
+  GS_CHECK_LAUNCH("isect_write_tilefirst");
   return 0;
 }

@@ -39,6 +39,10 @@ _SIGS = {
     "gsplat_hip_isect_sorted_workspace_bytes": (_i64, [_i64, _i64, _i32]),
     "gsplat_hip_isect_write_sorted": (_i32, [_i64, _i32, _p, _p, _p, _p, _p, _i32, _i32, _i32,
                                              _i32, _i32, _p, _i64, _i64, _p, _i64, _p, _p, _p]),
+    "gsplat_hip_isect_tilefirst_workspace_bytes": (_i64, [_i64, _i32, _i32]),
+    "gsplat_hip_isect_write_tilefirst": (_i32, [_i64, _i32, _p, _p, _p, _p, _i32, _i32, _i32,
+                                                _i32, _i32, _i32, _p, _i64, _p, _i64, _p, _p,
+                                                _p]),
     "gsplat_hip_sort_workspace_bytes": (_i64, [_i64]),
     "gsplat_hip_radix_sort": (_i32, [_i64, _i32, _p, _p, _p, _p, _p, _i64, _p]),
     "gsplat_hip_isect_offsets": (_i32, [_i64, _p, _i32, _i32, _i32, _p, _p]),

@@ -193,9 +193,10 @@ def fully_fused_projection(
 
 
 # =================================================================== isect ==
-# Sorted-isect strategy: "depth_first" (32-bit depth sort of the visible
-# Gaussians + 32-bit (camera, tile) sort of the isects, csrc/isect.hip) or
-# "full" (the reference's single 64-bit key sort).  Both give identical output.
+# Sorted-isect strategy (csrc/isect.hip), all with identical output:
+#   "tile_first"  stable 32-bit (camera, tile) sort + segmented depth sort
+#   "depth_first" depth sort of the visible Gaussians + stable (camera, tile) sort
+#   "full"        the reference's single 64-bit key sort
 ISECT_SORT = os.environ.get("GSPLAT_HIP_ISECT_SORT", "depth_first")
 
 
@@ -255,7 +256,16 @@ def isect_tiles(
     n_isects, n_visible = totals.tolist()  # the single host sync (isect_tiles.py:102)
     isect_ids = torch.empty(n_isects, dtype=torch.int64, device=dev)
     flatten_ids = torch.empty(n_isects, dtype=torch.int32, device=dev)
-    if sort and ISECT_SORT == "depth_first":
+    if sort and ISECT_SORT == "tile_first" and n_isects > 0:
+        sws = torch.empty(max(int(_lib.query("gsplat_hip_isect_tilefirst_workspace_bytes",
+                                             n_isects, C * tile_width * tile_height,
+                                             n_bit_tile + n_bit_cam)), 8),
+                          dtype=torch.uint8, device=dev)
+        _lib.call("gsplat_hip_isect_write_tilefirst", G, N, _ptr(means2d), _ptr(radii),
+                  _ptr(depths), _ptr(camera_ids), tile_size, tile_width, tile_height, C,
+                  n_bit_tile, n_bit_cam, _ptr(ws), n_isects, _ptr(sws), sws.numel(),
+                  _ptr(isect_ids), _ptr(flatten_ids), st)
+    elif sort and ISECT_SORT == "depth_first":
         key_bits = n_bit_tile + n_bit_cam
         sws = torch.empty(max(int(_lib.query("gsplat_hip_isect_sorted_workspace_bytes", n_visible,
                                              n_isects, key_bits)), 8),

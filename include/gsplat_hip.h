@@ -138,6 +138,20 @@ int gsplat_hip_isect_write_sorted(int64_t n_gaussians, int N, const float *means
                                   int cam_bits, const void *count_workspace, int64_t n_visible,
                                   int64_t n_isects, void *workspace, int64_t workspace_bytes,
                                   int64_t *isect_ids, int32_t *flatten_ids, void *stream);
+/* Sorted emission, tile-first (the default of isect_tiles(sort=True)): the
+ * SAME isect_ids / flatten_ids again, from Gaussian-major emission with
+ * 32-bit (camera, tile) keys, a stable sort by those keys, and a segmented
+ * sort of each (camera, tile) run by depth bits.  No depth sort of the
+ * Gaussians; n_isects < 2^31. */
+int64_t gsplat_hip_isect_tilefirst_workspace_bytes(int64_t n_isects, int n_tiles_total,
+                                                   int key_bits);
+int gsplat_hip_isect_write_tilefirst(int64_t n_gaussians, int N, const float *means2d,
+                                     const int32_t *radii, const float *depths,
+                                     const int32_t *camera_ids, int tile_size, int tile_width,
+                                     int tile_height, int n_cameras, int tile_bits, int cam_bits,
+                                     const void *count_workspace, int64_t n_isects,
+                                     void *workspace, int64_t workspace_bytes,
+                                     int64_t *isect_ids, int32_t *flatten_ids, void *stream);
 int64_t gsplat_hip_sort_workspace_bytes(int64_t n);
 int gsplat_hip_radix_sort(int64_t n, int n_bits, const int64_t *keys_in, const int32_t *vals_in,
                           int64_t *keys_out, int32_t *vals_out, void *workspace,

@@ -119,7 +119,7 @@ def test_sh_broadcast_coeffs_match_materialised():
 
 
 # ----------------------------------------------------------------- isect
-@pytest.fixture(params=["depth_first", "full"])
+@pytest.fixture(params=["tile_first", "depth_first", "full"])
 def isect_mode(request, monkeypatch):
     """Run an isect test under both sort strategies of _wrapper.isect_tiles."""
     from gsplat_hip import _wrapper
@@ -210,13 +210,14 @@ def test_isect_sort_strategies_agree_large():
     old = _wrapper.ISECT_SORT
     try:
         out = {}
-        for mode in ("depth_first", "full"):
+        for mode in ("tile_first", "depth_first", "full"):
             _wrapper.ISECT_SORT = mode
             out[mode] = gsplat_hip.isect_tiles(m2, r, d, ts, tw, th)
     finally:
         _wrapper.ISECT_SORT = old
-    for a, b in zip(out["depth_first"], out["full"]):
-        assert torch.equal(a, b)
+    for mode in ("tile_first", "depth_first"):
+        for a, b in zip(out[mode], out["full"]):
+            assert torch.equal(a, b), mode
     assert out["full"][1].numel() > 100_000
 
 
@@ -529,3 +530,31 @@ def test_sh_colors_fused_vs_unfused(degree, C, split):
     # orthonormal only to ~1e-7); the means gradient at degree 4 amplifies it
     for a, b in zip(outs[0], outs[1]):
         close(b, a, 1e-4, 5e-5)
+
+
+@pytest.mark.parametrize("n_pile", [300, 5000, 20000])
+def test_isect_tile_first_long_runs(n_pile):
+    """Tiles with very long isect runs: the per-run depth sort switches from
+    32 KB LDS (<= 4096) to 128 KB LDS (<= 16384) to a global scratch path."""
+    import gsplat_hip
+    from gsplat_hip import _wrapper
+    g = torch.Generator(device=DEV).manual_seed(n_pile)
+    C, ts, tw, th = 2, 16, 6, 5
+    N = n_pile + 2000
+    m2 = torch.rand(C, N, 2, device=DEV, generator=g) * torch.tensor([tw * ts, th * ts], device=DEV)
+    m2[:, :n_pile] = torch.tensor([40.0, 40.0], device=DEV)  # a pile on one tile
+    r = (torch.rand(C, N, device=DEV, generator=g) * 6).int()
+    r[:, :n_pile] = 3
+    d = torch.rand(C, N, device=DEV, generator=g) * 10
+    d[:, : n_pile // 3] = 2.5  # ties inside the long run
+    d[0, 5:9] = -1.0           # negative depths
+    old = _wrapper.ISECT_SORT
+    try:
+        out = {}
+        for mode in ("tile_first", "full"):
+            _wrapper.ISECT_SORT = mode
+            out[mode] = gsplat_hip.isect_tiles(m2, r, d, ts, tw, th)
+    finally:
+        _wrapper.ISECT_SORT = old
+    for a, b in zip(out["tile_first"], out["full"]):
+        assert torch.equal(a, b)
