@@ -7,16 +7,14 @@
 //   lsd_scan     one workgroup per digit: exclusive scan of its row in place,
 //                row total -> totals[d]
 //   lsd_scatter  per tile: digit bases (scan of totals + hist[d][tile]),
-//                stable in-tile sort by the digit (rocPRIM block radix sort,
-//                one 8-bit internal pass), striped output -> coalesced stores
+//                stable in-tile ranks by wave ballots, reorder through LDS,
+//                digit-contiguous (coalesced) stores
 // The in-tile sort is stable and the tiles are laid out in input order, so the
 // pass is stable and the whole sort equals a stable sort on bits
 // [begin_bit, end_bit).  Traffic per pass: 4 B/item (hist) + 16 B/item
 // (scatter read + write).
 #pragma once
 #include "common.h"
-
-#include <rocprim/block/block_radix_sort.hpp>
 
 namespace gs {
 namespace lsd {
@@ -77,72 +75,115 @@ scan_kernel(uint32_t *__restrict__ hist, int64_t nt, uint32_t *__restrict__ tota
   if (threadIdx.x == 0) totals[blockIdx.x] = carry;
 }
 
+// Stable in-tile ranking without sorting the tile: wave w owns the items
+// [w*64*IPT, (w+1)*64*IPT) of the tile, visited e-major (coalesced loads).
+// For every item the lanes holding the same digit are found with nbits
+// ballots; the rank is the wave's running count for that digit plus the
+// number of such lanes below.  Cross-wave offsets and the tile's digit starts
+// come from the 4 x 256 wave counts; items are then reordered through LDS so
+// the global stores are digit-contiguous.
 template <int IPT>
 __global__ void __launch_bounds__(NT)
 scatter_kernel(const uint32_t *__restrict__ kin, const int32_t *__restrict__ vin,
                uint32_t *__restrict__ kout, int32_t *__restrict__ vout, int64_t n, int shift,
                int nbits, const uint32_t *__restrict__ hist, const uint32_t *__restrict__ totals,
                int64_t nt) {
-  using BRS = rocprim::block_radix_sort<uint32_t, NT, IPT, int32_t, 1, 1, 8>;
-  __shared__ typename BRS::storage_type storage;
-  __shared__ uint32_t gbase[RADIX];  // global destination of the tile's first item of digit d
-  __shared__ uint32_t lcnt[RADIX];
-  __shared__ uint32_t wsum[NT / 64];
+  constexpr int NW = NT / 64, TILE = NT * IPT;
+  __shared__ uint32_t cnt[NW][RADIX];
+  __shared__ uint32_t gbase[RADIX];  // global position of tile slot 0 of digit d's range
+  __shared__ uint32_t wsum[NW];
+  __shared__ uint32_t kbuf[TILE];
+  __shared__ int32_t vbuf[TILE];
   const uint32_t mask = (1u << nbits) - 1u;
-  const int d = threadIdx.x, lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  lcnt[d] = 0;
-  // exclusive scan of the digit totals (one digit per lane)
-  const uint32_t tv = totals[d];
-  uint32_t x = tv;
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
 #pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t y = __shfl_up(x, o, 64);
-    if (lane >= o) x += y;
-  }
-  if (lane == 63) wsum[wid] = x;
-  __syncthreads();
-  uint32_t before = 0;
-#pragma unroll
-  for (int w = 0; w < NT / 64; ++w) before += w < wid ? wsum[w] : 0u;
-  const uint32_t dbase = before + x - tv + hist[(int64_t)d * nt + blockIdx.x];
-
-  const int64_t base = (int64_t)blockIdx.x * NT * IPT;
-  const int nvalid = (int)min<int64_t>((int64_t)NT * IPT, n - base);
+  for (int w = 0; w < NW; ++w) cnt[w][t] = 0;
+  const int64_t base = (int64_t)blockIdx.x * TILE;
+  const int nvalid = (int)min<int64_t>((int64_t)TILE, n - base);
   uint32_t key[IPT];
   int32_t val[IPT];
 #pragma unroll
   for (int e = 0; e < IPT; ++e) {
-    const int j = threadIdx.x * IPT + e;  // blocked: input order = (thread, item)
-    key[e] = j < nvalid ? kin[base + j] : 0xffffffffu;
+    const int j = wid * 64 * IPT + e * 64 + lane;
+    key[e] = j < nvalid ? kin[base + j] : 0u;
     val[e] = j < nvalid ? vin[base + j] : 0;
-    if (j < nvalid) atomicAdd(&lcnt[(key[e] >> shift) & mask], 1u);
   }
   __syncthreads();
-  // exclusive scan of the in-tile digit counts -> gbase[d] = dbase - lstart[d]
-  const uint32_t c = lcnt[d];
-  x = c;
+  uint32_t rank[IPT];
+  const uint64_t lt = (1ull << lane) - 1ull;
+#pragma unroll
+  for (int e = 0; e < IPT; ++e) {
+    const int j = wid * 64 * IPT + e * 64 + lane;
+    const bool ok = j < nvalid;
+    const uint32_t dg = (key[e] >> shift) & mask;
+    uint64_t peers = __ballot(ok);
+    for (int b = 0; b < nbits; ++b) {
+      const bool bit = (dg >> b) & 1u;
+      const uint64_t bal = __ballot(bit);
+      peers &= bit ? bal : ~bal;
+    }
+    const uint32_t below = (uint32_t)__popcll(peers & lt);
+    const uint32_t old = ok ? cnt[wid][dg] : 0u;
+    // LDS ops of one wave complete in order: every peer read `old` above.
+    if (ok && below == 0) cnt[wid][dg] = old + (uint32_t)__popcll(peers);
+    rank[e] = old + below;
+  }
+  __syncthreads();
+  // digit t: offsets of the waves, tile total, tile-exclusive start
+  uint32_t woff[NW], tot = 0;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) {
+    woff[w] = tot;
+    tot += cnt[w][t];
+  }
+  uint32_t x = tot;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
     const uint32_t y = __shfl_up(x, o, 64);
     if (lane >= o) x += y;
   }
-  __syncthreads();  // wsum reuse
   if (lane == 63) wsum[wid] = x;
-  __syncthreads();
-  before = 0;
+  // global start of digit t: exclusive scan of the totals + this tile's row entry
+  const uint32_t tv = totals[t];
+  uint32_t g = tv;
 #pragma unroll
-  for (int w = 0; w < NT / 64; ++w) before += w < wid ? wsum[w] : 0u;
-  gbase[d] = dbase - (before + x - c);
-  BRS().sort_to_striped(key, val, storage, (unsigned)shift, (unsigned)(shift + nbits));
-  // sort_to_striped ends with a barrier-free exchange; gbase was written
-  // before its internal barriers.
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(g, o, 64);
+    if (lane >= o) g += y;
+  }
+  __syncthreads();
+  uint32_t lbefore = 0;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) lbefore += w < wid ? wsum[w] : 0u;
+  const uint32_t lstart = lbefore + x - tot;
+  __syncthreads();
+  if (lane == 63) wsum[wid] = g;
+  __syncthreads();
+  uint32_t gbefore = 0;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) gbefore += w < wid ? wsum[w] : 0u;
+  gbase[t] = gbefore + g - tv + hist[(int64_t)t * nt + blockIdx.x] - lstart;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) cnt[w][t] = lstart + woff[w];  // tile slot of wave w's first
+  __syncthreads();
 #pragma unroll
   for (int e = 0; e < IPT; ++e) {
-    const int s = e * NT + threadIdx.x;  // striped: sorted position in the tile
+    const int j = wid * 64 * IPT + e * 64 + lane;
+    if (j < nvalid) {
+      const uint32_t slot = cnt[wid][(key[e] >> shift) & mask] + rank[e];
+      kbuf[slot] = key[e];
+      vbuf[slot] = val[e];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int e = 0; e < IPT; ++e) {
+    const int s = e * NT + t;
     if (s < nvalid) {
-      const uint32_t dst = gbase[(key[e] >> shift) & mask] + (uint32_t)s;
-      kout[dst] = key[e];
-      vout[dst] = val[e];
+      const uint32_t k = kbuf[s];
+      const uint32_t dst = gbase[(k >> shift) & mask] + (uint32_t)s;
+      kout[dst] = k;
+      vout[dst] = vbuf[s];
     }
   }
 }

@@ -261,6 +261,110 @@ sh_bwd_kernel(int64_t n, int K, int64_t n_coeff_rows, Coeffs cf, const float *__
   }
 }
 
+// Backward with the coefficient rows staged through LDS (K == (DEG+1)^2 and
+// one coefficient row per lane row, i.e. C == 1).  One lane per row strides
+// the rows by 3K floats, so each of its 3K stores touches 64 cache lines; here
+// a wave copies its 64 visible rows' coefficients in and its 64 gradient rows
+// (zeros for masked rows) out with lane-contiguous accesses.  Rows are padded
+// to an odd LDS stride so the per-lane row reads are bank-conflict free.
+template <int DEG, bool FUSED>
+__global__ void __launch_bounds__(256)
+sh_bwd_staged_kernel(int64_t n, Coeffs cf, const float *__restrict__ dirs,
+                     const uint8_t *__restrict__ masks, const float *__restrict__ v_colors,
+                     VCoeffs vc, float *__restrict__ v_dirs, Fused fz) {
+  constexpr int NB = (DEG + 1) * (DEG + 1), W = 3 * NB, WR = W - 3, RS = W | 1;
+  __shared__ float lds[4][64 * RS];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int64_t i0 = (int64_t)blockIdx.x * 256 + wid * 64;
+  if (i0 >= n) return;
+  const int rows = (int)min<int64_t>(64, n - i0);
+  const int64_t i = i0 + lane;
+  float *sb = lds[wid];
+  const bool on = lane < rows && (FUSED ? fz.radii[i] > 0 : (!masks || masks[i]));
+  const uint64_t vis = __ballot(on);
+  if (vis) {
+    for (int e = lane; e < rows * 3; e += 64) {
+      const int rr = e / 3, c = e - 3 * rr;
+      if ((vis >> rr) & 1) sb[rr * RS + c] = cf.c0[(i0 + rr) * cf.s0 + c];
+    }
+    if (WR > 0)
+      for (int e = lane; e < rows * WR; e += 64) {
+        const int rr = e / WR, c = e - WR * rr;
+        if ((vis >> rr) & 1) sb[rr * RS + 3 + c] = cf.cr[(i0 + rr) * cf.sr + c];
+      }
+  }
+  __builtin_amdgcn_wave_barrier();
+  float *row = sb + lane * RS;
+  if (on) {
+    float vr = v_colors[3 * i], vg = v_colors[3 * i + 1], vb = v_colors[3 * i + 2];
+    float x = 0.f, y = 0.f, z = 0.f, inorm = 0.f;
+    if (DEG > 0) {
+      if (FUSED) {
+        fused_dir(fz, i, x, y, z);
+      } else {
+        x = dirs[3 * i]; y = dirs[3 * i + 1]; z = dirs[3 * i + 2];
+      }
+      inorm = rsqrtf(x * x + y * y + z * z);
+      x *= inorm; y *= inorm; z *= inorm;
+    }
+    float B[NB];
+    float dB[NB][3];
+    const bool want_dirs = (v_dirs != nullptr) && DEG > 0;
+    if (want_dirs) sh_basis<DEG, true>(x, y, z, B, dB);
+    else sh_basis<DEG, false>(x, y, z, B, nullptr);
+    if (FUSED) {  // clamp_min(sh + 0.5, 0) passes the gradient where sh + 0.5 >= 0
+      float r = 0.f, g = 0.f, b = 0.f;
+#pragma unroll
+      for (int k = 0; k < NB; ++k) {
+        r += B[k] * row[3 * k];
+        g += B[k] * row[3 * k + 1];
+        b += B[k] * row[3 * k + 2];
+      }
+      vr = (r + 0.5f >= 0.f) ? vr : 0.f;
+      vg = (g + 0.5f >= 0.f) ? vg : 0.f;
+      vb = (b + 0.5f >= 0.f) ? vb : 0.f;
+    }
+    if (v_dirs) {
+      float vx = 0.f, vy = 0.f, vz = 0.f;
+      if (DEG > 0) {
+#pragma unroll
+        for (int k = 1; k < NB; ++k) {
+          const float w = row[3 * k] * vr + row[3 * k + 1] * vg + row[3 * k + 2] * vb;
+          vx += dB[k][0] * w;
+          vy += dB[k][1] * w;
+          vz += dB[k][2] * w;
+        }
+        // VJP of the normalisation (sh_bwd.py:367-380)
+        const float dot = x * vx + y * vy + z * vz;
+        vx = (vx - dot * x) * inorm;
+        vy = (vy - dot * y) * inorm;
+        vz = (vz - dot * z) * inorm;
+      }
+      v_dirs[3 * i] = vx; v_dirs[3 * i + 1] = vy; v_dirs[3 * i + 2] = vz;
+    }
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
+      row[3 * k] = B[k] * vr;
+      row[3 * k + 1] = B[k] * vg;
+      row[3 * k + 2] = B[k] * vb;
+    }
+  } else if (lane < rows) {
+#pragma unroll
+    for (int k = 0; k < W; ++k) row[k] = 0.f;
+    if (v_dirs) { v_dirs[3 * i] = 0.f; v_dirs[3 * i + 1] = 0.f; v_dirs[3 * i + 2] = 0.f; }
+  }
+  __builtin_amdgcn_wave_barrier();
+  for (int e = lane; e < rows * 3; e += 64) {
+    const int rr = e / 3, c = e - 3 * rr;
+    vc.c0[(i0 + rr) * vc.s0 + c] = sb[rr * RS + c];
+  }
+  if (WR > 0)
+    for (int e = lane; e < rows * WR; e += 64) {
+      const int rr = e / WR, c = e - WR * rr;
+      vc.cr[(i0 + rr) * vc.sr + c] = sb[rr * RS + 3 + c];
+    }
+}
+
 }  // namespace gs
 
 using namespace gs;
@@ -311,10 +415,15 @@ extern "C" int gsplat_hip_sh_bwd(int degree, int64_t n, int64_t n_coeff_rows, in
                              : VCoeffs{v_coeffs, v_coeffs + 3, 3 * (int64_t)K, 3 * (int64_t)K};
   dim3 grid((unsigned)((n + 255) / 256));
   hipStream_t st = (hipStream_t)stream;
+  const bool staged = n_coeff_rows == n && K == (degree + 1) * (degree + 1);
 #define GS_SH_BWD(D)                                                                       \
   case D:                                                                                  \
-    hipLaunchKernelGGL((sh_bwd_kernel<D, false>), grid, dim3(256), 0, st, n, K, n_coeff_rows, \
-                       cf, dirs, masks, v_colors, vc, v_dirs, Fused{});                       \
+    if (staged)                                                                            \
+      hipLaunchKernelGGL((sh_bwd_staged_kernel<D, false>), grid, dim3(256), 0, st, n, cf,  \
+                         dirs, masks, v_colors, vc, v_dirs, Fused{});                      \
+    else                                                                                   \
+      hipLaunchKernelGGL((sh_bwd_kernel<D, false>), grid, dim3(256), 0, st, n, K,          \
+                         n_coeff_rows, cf, dirs, masks, v_colors, vc, v_dirs, Fused{});    \
     break;
   switch (degree) { GS_SH_BWD(0) GS_SH_BWD(1) GS_SH_BWD(2) GS_SH_BWD(3) GS_SH_BWD(4) }
 #undef GS_SH_BWD
@@ -367,10 +476,15 @@ extern "C" int gsplat_hip_sh_colors_bwd(int degree, int C, int64_t N, int64_t n_
   const Fused fz{means, viewmats, radii, N};
   dim3 grid((unsigned)((n + 255) / 256));
   hipStream_t st = (hipStream_t)stream;
-#define GS_SH_BWD(D)                                                                           \
-  case D:                                                                                      \
-    hipLaunchKernelGGL((sh_bwd_kernel<D, true>), grid, dim3(256), 0, st, n, K, n_coeff_rows, cf, \
-                       nullptr, nullptr, v_colors, vc, v_dirs, fz);                            \
+  const bool staged = n_coeff_rows == n && K == (degree + 1) * (degree + 1);
+#define GS_SH_BWD(D)                                                                       \
+  case D:                                                                                  \
+    if (staged)                                                                            \
+      hipLaunchKernelGGL((sh_bwd_staged_kernel<D, true>), grid, dim3(256), 0, st, n, cf,   \
+                         nullptr, nullptr, v_colors, vc, v_dirs, fz);                      \
+    else                                                                                   \
+      hipLaunchKernelGGL((sh_bwd_kernel<D, true>), grid, dim3(256), 0, st, n, K,           \
+                         n_coeff_rows, cf, nullptr, nullptr, v_colors, vc, v_dirs, fz);    \
     break;
   switch (degree) { GS_SH_BWD(0) GS_SH_BWD(1) GS_SH_BWD(2) GS_SH_BWD(3) GS_SH_BWD(4) }
 #undef GS_SH_BWD

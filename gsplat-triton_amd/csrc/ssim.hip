@@ -31,6 +31,20 @@ constexpr float C1 = 0.01f * 0.01f, C2 = 0.03f * 0.03f;
 
 typedef float f2v __attribute__((ext_vector_type(2)));
 
+constexpr int kLoads = (WN * WN + 255) / 256;  // window elements per thread
+
+// 1-D grid over (tile, image-channel) so that the channels of one tile run
+// back to back on the same XCD (workgroup i goes to XCD i % 8): the
+// interleaved [H, W, C] image lines fetched by channel 0 are L2 hits for
+// channels 1, 2.  Grid size roundup(n_tiles, 8) * n_bc.
+GS_INLINE bool decode_block(int n_tiles, int n_bc, int &t, int &bc) {
+  const int L = blockIdx.x, xcd = L & 7, q = L >> 3;
+  bc = q % n_bc;
+  t = (q / n_bc) * 8 + xcd;
+  return t < n_tiles;
+}
+inline int grid_blocks(int n_tiles, int n_bc) { return ((n_tiles + 7) / 8) * 8 * n_bc; }
+
 // Separable 11-tap blur of a 42x42 window to the 32x32 tile, three planes at
 // once (two packed float2 planes + one float plane).  256 threads: column
 // tq = tid & 31; the horizontal pass covers rows tr, tr+8, ...; the vertical
@@ -138,22 +152,41 @@ fwd_kernel(int B, int H, int W, int C, const float *__restrict__ x, const float 
   __shared__ float h_p[WN][TW];
   __shared__ float red[2][4];
   const int Hm = H - 2 * R, Wm = W - 2 * R;
-  const int b = blockIdx.z / C, c = blockIdx.z - b * C;  // one channel per workgroup
-  const int mi0 = blockIdx.y * TW, mj0 = blockIdx.x * TW;  // map tile origin
+  const int tx = (Wm + TW - 1) / TW, ty = (Hm + TW - 1) / TW;
+  int t, bc;
+  if (!decode_block(tx * ty, B * C, t, bc)) return;
+  const int b = bc / C, c = bc - b * C;  // one channel per workgroup
+  const int mi0 = (t / tx) * TW, mj0 = (t % tx) * TW;  // map tile origin
   const int tid = threadIdx.x, tq = tid & 31, tr = tid >> 5;
   const int64_t plane = (int64_t)Hm * Wm;
   float ssum = 0.f, lsum = 0.f;
   {
-    for (int e = tid; e < WN * WN; e += 256) {
+    // all window loads in flight before the first LDS store
+    float vx[kLoads], vy[kLoads];
+#pragma unroll
+    for (int k = 0; k < kLoads; ++k) {
+      const int e = tid + 256 * k;
       const int r = e / WN, q = e - r * WN;
       const int gi = mi0 + r, gj = mj0 + q;
-      float vx = 0.f, vy = 0.f;
-      if (gi < H && gj < W) {
+      vx[k] = vy[k] = 0.f;
+      if (e < WN * WN && gi < H && gj < W) {
         const int64_t o = (((int64_t)b * H + gi) * W + gj) * C + c;
-        vx = x[o];
-        vy = y[o];
+        vx[k] = x[o];
+        vy[k] = y[o];
       }
-      s_xy[r][q] = f2v{vx, vy};
+    }
+    // L1 over the whole image from the window: each workgroup owns the image
+    // pixels of its map tile (edge workgroups also the 2R-pixel border)
+    const int ri1 = (mi0 + TW >= Hm) ? H - mi0 : TW;
+    const int rj1 = (mj0 + TW >= Wm) ? W - mj0 : TW;
+#pragma unroll
+    for (int k = 0; k < kLoads; ++k) {
+      const int e = tid + 256 * k;
+      const int r = e / WN, q = e - r * WN;
+      if (e < WN * WN) {
+        s_xy[r][q] = f2v{vx[k], vy[k]};
+        if (r < ri1 && q < rj1) lsum += fabsf(vx[k] - vy[k]);
+      }
     }
     __syncthreads();
     Blur3 o;
@@ -178,18 +211,6 @@ fwd_kernel(int B, int H, int W, int C, const float *__restrict__ x, const float 
       }
     }
   }
-  // L1 over the whole image: each workgroup owns the image pixels of its map
-  // tile in its channel (edge workgroups also cover the 2R-pixel border)
-  {
-    const int ri1 = (mi0 + TW >= Hm) ? H : mi0 + TW;
-    const int rj1 = (mj0 + TW >= Wm) ? W : mj0 + TW;
-    const int nc = rj1 - mj0;
-    for (int e = tid; e < (ri1 - mi0) * nc; e += 256) {
-      const int gi = mi0 + e / nc, gj = mj0 + e % nc;
-      const int64_t o = (((int64_t)b * H + gi) * W + gj) * C + c;
-      lsum += fabsf(x[o] - y[o]);
-    }
-  }
   ssum = wave_sum(ssum);
   lsum = wave_sum(lsum);
   if ((tid & 63) == 0) {
@@ -198,15 +219,19 @@ fwd_kernel(int B, int H, int W, int C, const float *__restrict__ x, const float 
   }
   __syncthreads();
   if (tid == 0) {  // per-workgroup partials (no same-address atomics)
-    const int blk = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+    const int blk = bc * tx * ty + t;
     partials[2 * blk] = red[0][0] + red[0][1] + red[0][2] + red[0][3];
     partials[2 * blk + 1] = red[1][0] + red[1][1] + red[1][2] + red[1][3];
   }
 }
 
 // Deterministic sum of the per-workgroup partials -> sums[2].
+// With loss != nullptr also loss[0..2] = (w_l1 L1/n_img + lam (1 - S/n_map),
+// S/n_map, L1/n_img).
 __global__ void __launch_bounds__(1024) reduce_partials_kernel(int n, const float *partials,
-                                                               float *sums) {
+                                                               float *sums, float *loss,
+                                                               float lam, float n_map,
+                                                               float n_img) {
   __shared__ float red[2][16];
   float a = 0.f, b = 0.f;
   for (int i = threadIdx.x; i < n; i += 1024) {
@@ -220,38 +245,69 @@ __global__ void __launch_bounds__(1024) reduce_partials_kernel(int n, const floa
     red[1][threadIdx.x >> 6] = b;
   }
   __syncthreads();
-  if (threadIdx.x < 2) {
-    float t = 0.f;
-    for (int w = 0; w < 16; ++w) t += red[threadIdx.x][w];
-    sums[threadIdx.x] = t;
+  if (threadIdx.x == 0) {
+    float t[2] = {0.f, 0.f};
+    for (int w = 0; w < 16; ++w) {
+      t[0] += red[0][w];
+      t[1] += red[1][w];
+    }
+    if (sums) {
+      sums[0] = t[0];
+      sums[1] = t[1];
+    }
+    if (loss) {
+      const float s = t[0] / n_map, l1 = t[1] / n_img;
+      loss[0] = l1 * (1.f - lam) + (1.f - s) * lam;
+      loss[1] = s;
+      loss[2] = l1;
+    }
   }
 }
 
 __global__ void __launch_bounds__(256)
 bwd_kernel(int B, int H, int W, int C, const float *__restrict__ x, const float *__restrict__ y,
-           const float *__restrict__ maps, const float *__restrict__ dloss,
-           float *__restrict__ grad) {
+           const float *__restrict__ maps, const float *__restrict__ dloss, float s_ssim,
+           float s_l1, int l1_index, float *__restrict__ grad) {
   __shared__ f2v s_01[WN][WN];  // (dSSIM/dmu1, dSSIM/dE[x^2])
   __shared__ float s_2[WN][WN];  // dSSIM/dE[xy]
   __shared__ f2v h_01[WN][TW];
   __shared__ float h_2[WN][TW];
   const int Hm = H - 2 * R, Wm = W - 2 * R;
-  const int b = blockIdx.z / C, c = blockIdx.z - b * C;  // one channel per workgroup
-  const int qi0 = blockIdx.y * TW, qj0 = blockIdx.x * TW;  // image tile origin
+  const int tx = (W + TW - 1) / TW, ty = (H + TW - 1) / TW;
+  int t, bc;
+  if (!decode_block(tx * ty, B * C, t, bc)) return;
+  const int b = bc / C, c = bc - b * C;  // one channel per workgroup
+  const int qi0 = (t / tx) * TW, qj0 = (t % tx) * TW;  // image tile origin
   const int tid = threadIdx.x, tq = tid & 31, tr = tid >> 5;
-  const float n_map = (float)B * C * Hm * Wm, n_img = (float)B * C * H * W;
-  const float g_ssim = dloss[0] / n_map, g_l1 = dloss[1] / n_img;
+  // dL/d(SSIM map sum) and dL/d(L1 sum)
+  const float g_ssim = dloss[0] * s_ssim, g_l1 = dloss[l1_index] * s_l1;
   const int64_t plane = (int64_t)Hm * Wm;
   {
     const float *mp = maps + (((int64_t)b * C + c) * 3) * plane;
-    // map window rows [qi0-10, qi0+32), cols [qj0-10, qj0+32), zero outside
-    for (int e = tid; e < WN * WN; e += 256) {
+    // map window rows [qi0-10, qi0+32), cols [qj0-10, qj0+32), zero outside;
+    // all loads in flight before the first LDS store
+    float m0[kLoads], m1[kLoads], m2[kLoads];
+#pragma unroll
+    for (int k = 0; k < kLoads; ++k) {
+      const int e = tid + 256 * k;
       const int r = e / WN, q = e - r * WN;
       const int pi = qi0 - 2 * R + r, pj = qj0 - 2 * R + q;
-      const bool in = pi >= 0 && pi < Hm && pj >= 0 && pj < Wm;
-      const int64_t o = (int64_t)pi * Wm + pj;
-      s_01[r][q] = in ? f2v{mp[o], mp[plane + o]} : f2v{0.f, 0.f};
-      s_2[r][q] = in ? mp[2 * plane + o] : 0.f;
+      m0[k] = m1[k] = m2[k] = 0.f;
+      if (e < WN * WN && pi >= 0 && pi < Hm && pj >= 0 && pj < Wm) {
+        const int64_t o = (int64_t)pi * Wm + pj;
+        m0[k] = mp[o];
+        m1[k] = mp[plane + o];
+        m2[k] = mp[2 * plane + o];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kLoads; ++k) {
+      const int e = tid + 256 * k;
+      const int r = e / WN, q = e - r * WN;
+      if (e < WN * WN) {
+        s_01[r][q] = f2v{m0[k], m1[k]};
+        s_2[r][q] = m2[k];
+      }
     }
     __syncthreads();
     // the adjoint of the valid correlation is the full correlation with the
@@ -283,36 +339,69 @@ static int64_t ssim_map_floats(int B, int H, int W, int C) {
 static int64_t ssim_blocks(int B, int H, int W, int C) {
   return (int64_t)((W - 10 + 31) / 32) * ((H - 10 + 31) / 32) * B * C;
 }
+static dim3 ssim_grid(int B, int H, int W, int C, bool map_tiles) {
+  const int pad = map_tiles ? 10 : 0;
+  return dim3((unsigned)ssim::grid_blocks(((W - pad + 31) / 32) * ((H - pad + 31) / 32), B * C));
+}
 
 extern "C" int64_t gsplat_hip_ssim_workspace_bytes(int B, int H, int W, int C) {
   if (H <= 10 || W <= 10) return 0;
   return (int64_t)sizeof(float) * (ssim_map_floats(B, H, W, C) + 2 * ssim_blocks(B, H, W, C));
 }
 
-extern "C" int gsplat_hip_ssim_l1_fwd(int B, int H, int W, int C, const float *img1,
-                                      const float *img2, float *sums, void *workspace,
-                                      void *stream) {
+static float n_map(int B, int H, int W, int C) { return (float)B * C * (H - 10) * (W - 10); }
+static float n_img(int B, int H, int W, int C) { return (float)B * C * H * W; }
+
+static int ssim_fwd(int B, int H, int W, int C, const float *img1, const float *img2,
+                    float *sums, float *loss, float lam, void *workspace, void *stream) {
   GS_REQUIRE(B > 0 && C > 0 && H > 10 && W > 10,
              "ssim_l1_fwd: images must be larger than the 11x11 window (got %dx%d)", H, W);
   hipStream_t st = (hipStream_t)stream;
   float *maps = reinterpret_cast<float *>(workspace);
   float *partials = maps + ssim_map_floats(B, H, W, C);
-  dim3 grid((W - 10 + 31) / 32, (H - 10 + 31) / 32, B * C);
-  hipLaunchKernelGGL(ssim::fwd_kernel, grid, dim3(256), 0, st, B, H, W, C, img1, img2, maps,
+  hipLaunchKernelGGL(ssim::fwd_kernel, ssim_grid(B, H, W, C, true), dim3(256), 0, st, B, H, W, C, img1, img2, maps,
                      partials);
   hipLaunchKernelGGL(ssim::reduce_partials_kernel, dim3(1), dim3(1024), 0, st,
-                     (int)ssim_blocks(B, H, W, C), partials, sums);
+                     (int)ssim_blocks(B, H, W, C), partials, sums, loss, lam, n_map(B, H, W, C),
+                     n_img(B, H, W, C));
   GS_CHECK_LAUNCH("ssim_l1_fwd");
   return 0;
+}
+
+static int ssim_bwd(int B, int H, int W, int C, const float *img1, const float *img2,
+                    const void *workspace, const float *dloss, float s_ssim, float s_l1,
+                    int l1_index, float *grad_img1, void *stream) {
+  GS_REQUIRE(B > 0 && C > 0 && H > 10 && W > 10, "ssim_l1_bwd: bad image size %dx%d", H, W);
+  hipLaunchKernelGGL(ssim::bwd_kernel, ssim_grid(B, H, W, C, false), dim3(256), 0, (hipStream_t)stream, B, H, W, C, img1,
+                     img2, reinterpret_cast<const float *>(workspace), dloss, s_ssim, s_l1, l1_index,
+                     grad_img1);
+  GS_CHECK_LAUNCH("ssim_l1_bwd");
+  return 0;
+}
+
+extern "C" int gsplat_hip_ssim_l1_fwd(int B, int H, int W, int C, const float *img1,
+                                      const float *img2, float *sums, void *workspace,
+                                      void *stream) {
+  return ssim_fwd(B, H, W, C, img1, img2, sums, nullptr, 0.f, workspace, stream);
 }
 
 extern "C" int gsplat_hip_ssim_l1_bwd(int B, int H, int W, int C, const float *img1,
                                       const float *img2, const void *workspace,
                                       const float *dloss, float *grad_img1, void *stream) {
-  GS_REQUIRE(B > 0 && C > 0 && H > 10 && W > 10, "ssim_l1_bwd: bad image size %dx%d", H, W);
-  dim3 grid((W + 31) / 32, (H + 31) / 32, B * C);
-  hipLaunchKernelGGL(ssim::bwd_kernel, grid, dim3(256), 0, (hipStream_t)stream, B, H, W, C, img1,
-                     img2, reinterpret_cast<const float *>(workspace), dloss, grad_img1);
-  GS_CHECK_LAUNCH("ssim_l1_bwd");
-  return 0;
+  return ssim_bwd(B, H, W, C, img1, img2, workspace, dloss, 1.f / n_map(B, H, W, C),
+                  1.f / n_img(B, H, W, C), 1, grad_img1, stream);
+}
+
+extern "C" int gsplat_hip_l1_ssim_loss_fwd(int B, int H, int W, int C, const float *img1,
+                                           const float *img2, float lam, float *out,
+                                           void *workspace, void *stream) {
+  GS_REQUIRE(out != nullptr, "l1_ssim_loss_fwd: out is null");
+  return ssim_fwd(B, H, W, C, img1, img2, nullptr, out, lam, workspace, stream);
+}
+
+extern "C" int gsplat_hip_l1_ssim_loss_bwd(int B, int H, int W, int C, const float *img1,
+                                           const float *img2, const void *workspace, float lam,
+                                           const float *g_loss, float *grad_img1, void *stream) {
+  return ssim_bwd(B, H, W, C, img1, img2, workspace, g_loss, -lam / n_map(B, H, W, C),
+                  (1.f - lam) / n_img(B, H, W, C), 0, grad_img1, stream);
 }

@@ -60,6 +60,8 @@ _SIGS = {
     "gsplat_hip_ssim_workspace_bytes": (_i64, [_i32, _i32, _i32, _i32]),
     "gsplat_hip_ssim_l1_fwd": (_i32, [_i32, _i32, _i32, _i32, _p, _p, _p, _p, _p]),
     "gsplat_hip_ssim_l1_bwd": (_i32, [_i32, _i32, _i32, _i32, _p, _p, _p, _p, _p, _p]),
+    "gsplat_hip_l1_ssim_loss_fwd": (_i32, [_i32, _i32, _i32, _i32, _p, _p, _f, _p, _p, _p]),
+    "gsplat_hip_l1_ssim_loss_bwd": (_i32, [_i32, _i32, _i32, _i32, _p, _p, _p, _f, _p, _p, _p]),
     "gsplat_hip_adam_step": (_i32, [_i32, _p, _p, _p, _p, _p, _p, _f, _f, _f, _i32, _p]),
 }
 

@@ -49,9 +49,39 @@ def ssim_and_l1(img, gt):
     return _L1SSIM.apply(img, gt)
 
 
+class _L1SSIMLoss(torch.autograd.Function):
+    """The whole loss in one forward and one backward launch pair: the scalar
+    arithmetic is folded into the reduction / gradient kernels."""
+
+    @staticmethod
+    def forward(ctx, img, gt, lam):
+        assert img.dim() == 4 and img.shape == gt.shape, (img.shape, gt.shape)
+        img = img.contiguous().float()
+        gt = gt.contiguous().float()
+        B, H, W, C = img.shape
+        ws = torch.empty(max(int(_lib.query("gsplat_hip_ssim_workspace_bytes", B, H, W, C)), 4),
+                         dtype=torch.uint8, device=img.device)
+        out = torch.empty(3, device=img.device)
+        _lib.call("gsplat_hip_l1_ssim_loss_fwd", B, H, W, C, _ptr(img), _ptr(gt),
+                  ctypes.c_float(lam), _ptr(out), _ptr(ws), _stream())
+        ctx.save_for_backward(img, gt, ws)
+        ctx.lam = float(lam)
+        return out[0]
+
+    @staticmethod
+    def backward(ctx, g_loss):
+        img, gt, ws = ctx.saved_tensors
+        B, H, W, C = img.shape
+        g_loss = g_loss.float().contiguous()
+        grad = torch.empty_like(img)
+        _lib.call("gsplat_hip_l1_ssim_loss_bwd", B, H, W, C, _ptr(img), _ptr(gt), _ptr(ws),
+                  ctypes.c_float(ctx.lam), _ptr(g_loss), _ptr(grad), _stream())
+        return grad, None, None
+
+
 def l1_ssim_loss(img, gt, ssim_lambda=0.2):
-    s, l1 = _L1SSIM.apply(img, gt)
-    return l1 * (1.0 - ssim_lambda) + (1.0 - s) * ssim_lambda
+    """(1 - ssim_lambda) * mean L1 + ssim_lambda * (1 - mean SSIM_valid)."""
+    return _L1SSIMLoss.apply(img, gt, float(ssim_lambda))
 
 
 class FusedAdam:

@@ -241,6 +241,16 @@ int gsplat_hip_ssim_l1_fwd(int B, int H, int W, int C, const float *img1, const 
 int gsplat_hip_ssim_l1_bwd(int B, int H, int W, int C, const float *img1, const float *img2,
                            const void *workspace, const float *dloss, float *grad_img1,
                            void *stream);
+/* The trainer's whole loss in the same two launches (no scalar torch glue):
+ * fwd: out[0] = (1-lam)*mean L1 + lam*(1 - mean SSIM), out[1] = mean SSIM,
+ *      out[2] = mean L1 (device floats).
+ * bwd: grad_img1 = dL/dimg1 for dL = g_loss[0] (device scalar). */
+int gsplat_hip_l1_ssim_loss_fwd(int B, int H, int W, int C, const float *img1,
+                                const float *img2, float lam, float *out, void *workspace,
+                                void *stream);
+int gsplat_hip_l1_ssim_loss_bwd(int B, int H, int W, int C, const float *img1,
+                                const float *img2, const void *workspace, float lam,
+                                const float *g_loss, float *grad_img1, void *stream);
 
 /* One torch.optim.Adam step (amsgrad=False, no weight decay) over up to 8
  * parameter groups in a single launch (replaces the per-group optimizers of

@@ -32,6 +32,26 @@ def test_ssim_l1_matches_torch(B, H, W, C):
     torch.testing.assert_close(img.grad, img_r.grad, rtol=1e-3, atol=1e-8)
 
 
+@pytest.mark.parametrize("B,H,W,C,lam", [(1, 64, 80, 3, 0.2), (2, 37, 131, 3, 0.5), (1, 1080, 1920, 3, 0.2)])
+def test_l1_ssim_loss_matches_torch(B, H, W, C, lam):
+    """The one-launch-pair loss equals the simple_trainer.py:642-646 formula
+    evaluated with torch ops on the conv SSIM."""
+    from gsplat_hip.losses import l1_ssim_loss
+    from gsplat_hip.train_step import ssim
+    g = torch.Generator(device="cuda").manual_seed(W + C)
+    img = torch.rand(B, H, W, C, device="cuda", generator=g).requires_grad_(True)
+    gt = torch.rand(B, H, W, C, device="cuda", generator=g)
+    loss = l1_ssim_loss(img, gt, lam)
+    img_r = img.detach().clone().requires_grad_(True)
+    s_r = ssim(img_r.permute(0, 3, 1, 2), gt.permute(0, 3, 1, 2))
+    loss_r = (img_r - gt).abs().mean() * (1 - lam) + (1 - s_r) * lam
+    assert loss.dim() == 0
+    torch.testing.assert_close(loss, loss_r, rtol=1e-4, atol=1e-5)
+    (2.5 * loss).backward()
+    (2.5 * loss_r).backward()
+    torch.testing.assert_close(img.grad, img_r.grad, rtol=1e-3, atol=1e-9)
+
+
 def test_fused_adam_matches_torch():
     from gsplat_hip.losses import FusedAdam
     torch.manual_seed(0)
