@@ -141,7 +141,7 @@ struct ProjBwdArgs {
   const float *means, *quats, *scales, *viewmats, *Ks;
   const int32_t *radii;
   const float *conics, *comps;                                 // comps may be null
-  const float *v_means2d, *v_depths, *v_conics, *v_comps;      // v_comps may be null
+  const float *v_means2d, *v_depths, *v_conics, *v_comps;      // v_depths, v_comps may be null
   float *v_means, *v_quats, *v_scales, *v_viewmats;            // v_viewmats may be null
   int store_mode;  // 1: C == 1, every lane stores its own row (no atomics, no memset)
 };
@@ -222,7 +222,7 @@ __global__ void __launch_bounds__(256) projection_bwd_kernel(ProjBwdArgs a) {
     tmp -= p.clamp_x ? vJxz * p.Jxz : 0.f;
     tmp -= p.clamp_y ? vJyz * p.Jyz : 0.f;
     vmc[2] -= iz * tmp;
-    vmc[2] += a.v_depths[idx];
+    if (a.v_depths) vmc[2] += a.v_depths[idx];  // null: depths unused downstream
 
     // ---- world->camera VJP (transform.py:38-119, 184-297)
 #pragma unroll

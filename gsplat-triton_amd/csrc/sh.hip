@@ -261,41 +261,58 @@ sh_bwd_kernel(int64_t n, int K, int64_t n_coeff_rows, Coeffs cf, const float *__
   }
 }
 
-// Backward with the coefficient rows staged through LDS (K == (DEG+1)^2 and
-// one coefficient row per lane row, i.e. C == 1).  One lane per row strides
-// the rows by 3K floats, so each of its 3K stores touches 64 cache lines; here
-// a wave copies its 64 visible rows' coefficients in and its 64 gradient rows
-// (zeros for masked rows) out with lane-contiguous accesses.  Rows are padded
-// to an odd LDS stride so the per-lane row reads are bank-conflict free.
+// Walks the elements e = lane, lane + 64, ... of a block of rows of WID
+// floats, tracking (row, column) without divisions.
+template <int WID>
+struct RowWalk {
+  int rr, c;
+  GS_INLINE explicit RowWalk(int lane) : rr(lane / WID), c(lane % WID) {}
+  GS_INLINE void next() {
+    rr += 64 / WID;
+    c += 64 % WID;
+    if (c >= WID) {
+      c -= WID;
+      rr += 1;
+    }
+  }
+};
+
+// Backward with the gradient rows staged through LDS (K == (DEG+1)^2 and one
+// coefficient row per lane row, i.e. C == 1).  A visible lane loads its row's
+// coefficients straight into registers (all loads in flight at once) and
+// writes its gradient row to LDS; the wave then stores its 64 rows (zeros
+// for masked rows) lane-contiguously, instead of 3K stores per lane that each
+// touch 64 cache lines.  LDS rows have an odd stride (bank-conflict free).
 template <int DEG, bool FUSED>
 __global__ void __launch_bounds__(256)
 sh_bwd_staged_kernel(int64_t n, Coeffs cf, const float *__restrict__ dirs,
                      const uint8_t *__restrict__ masks, const float *__restrict__ v_colors,
                      VCoeffs vc, float *__restrict__ v_dirs, Fused fz) {
-  constexpr int NB = (DEG + 1) * (DEG + 1), W = 3 * NB, WR = W - 3, RS = W | 1;
-  __shared__ float lds[4][64 * RS];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  constexpr int NB = (DEG + 1) * (DEG + 1), WR = 3 * (NB - 1), RSR = WR | 1;
+  __shared__ float l_dc[4][64 * 3];               // row stride 3 (odd)
+  __shared__ float l_rest[4][64 * (RSR > 1 ? RSR : 1)];  // odd row stride
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t i0 = (int64_t)blockIdx.x * 256 + wid * 64;
   if (i0 >= n) return;
   const int rows = (int)min<int64_t>(64, n - i0);
   const int64_t i = i0 + lane;
-  float *sb = lds[wid];
+  float *sd = l_dc[wid], *sr = l_rest[wid];
   const bool on = lane < rows && (FUSED ? fz.radii[i] > 0 : (!masks || masks[i]));
-  const uint64_t vis = __ballot(on);
-  if (vis) {
-    for (int e = lane; e < rows * 3; e += 64) {
-      const int rr = e / 3, c = e - 3 * rr;
-      if ((vis >> rr) & 1) sb[rr * RS + c] = cf.c0[(i0 + rr) * cf.s0 + c];
-    }
-    if (WR > 0)
-      for (int e = lane; e < rows * WR; e += 64) {
-        const int rr = e / WR, c = e - WR * rr;
-        if ((vis >> rr) & 1) sb[rr * RS + 3 + c] = cf.cr[(i0 + rr) * cf.sr + c];
-      }
-  }
-  __builtin_amdgcn_wave_barrier();
-  float *row = sb + lane * RS;
+  float *rd = sd + lane * 3, *rw = sr + lane * RSR;
+  // this lane's gradient row in LDS (coefficient k, channel ch)
+  auto grow = [&](int k, int ch) -> float & { return k == 0 ? rd[ch] : rw[3 * (k - 1) + ch]; };
   if (on) {
+    // the row's coefficients straight into registers: all loads in flight at
+    // once (strided per lane, but every fetched line is used)
+    float cr[NB][3];
+    {
+      const float *p0 = cf.c0 + i * cf.s0, *pr = cf.cr + i * cf.sr;
+#pragma unroll
+      for (int k = 0; k < NB; ++k)
+#pragma unroll
+        for (int ch = 0; ch < 3; ++ch) cr[k][ch] = k == 0 ? p0[ch] : pr[3 * (k - 1) + ch];
+    }
+    auto coef = [&](int k, int ch) { return cr[k][ch]; };
     float vr = v_colors[3 * i], vg = v_colors[3 * i + 1], vb = v_colors[3 * i + 2];
     float x = 0.f, y = 0.f, z = 0.f, inorm = 0.f;
     if (DEG > 0) {
@@ -316,9 +333,9 @@ sh_bwd_staged_kernel(int64_t n, Coeffs cf, const float *__restrict__ dirs,
       float r = 0.f, g = 0.f, b = 0.f;
 #pragma unroll
       for (int k = 0; k < NB; ++k) {
-        r += B[k] * row[3 * k];
-        g += B[k] * row[3 * k + 1];
-        b += B[k] * row[3 * k + 2];
+        r += B[k] * coef(k, 0);
+        g += B[k] * coef(k, 1);
+        b += B[k] * coef(k, 2);
       }
       vr = (r + 0.5f >= 0.f) ? vr : 0.f;
       vg = (g + 0.5f >= 0.f) ? vg : 0.f;
@@ -329,7 +346,7 @@ sh_bwd_staged_kernel(int64_t n, Coeffs cf, const float *__restrict__ dirs,
       if (DEG > 0) {
 #pragma unroll
         for (int k = 1; k < NB; ++k) {
-          const float w = row[3 * k] * vr + row[3 * k + 1] * vg + row[3 * k + 2] * vb;
+          const float w = coef(k, 0) * vr + coef(k, 1) * vg + coef(k, 2) * vb;
           vx += dB[k][0] * w;
           vy += dB[k][1] * w;
           vz += dB[k][2] * w;
@@ -344,25 +361,28 @@ sh_bwd_staged_kernel(int64_t n, Coeffs cf, const float *__restrict__ dirs,
     }
 #pragma unroll
     for (int k = 0; k < NB; ++k) {
-      row[3 * k] = B[k] * vr;
-      row[3 * k + 1] = B[k] * vg;
-      row[3 * k + 2] = B[k] * vb;
+      grow(k, 0) = B[k] * vr;
+      grow(k, 1) = B[k] * vg;
+      grow(k, 2) = B[k] * vb;
     }
   } else if (lane < rows) {
 #pragma unroll
-    for (int k = 0; k < W; ++k) row[k] = 0.f;
+    for (int k = 0; k < NB; ++k) grow(k, 0) = grow(k, 1) = grow(k, 2) = 0.f;
     if (v_dirs) { v_dirs[3 * i] = 0.f; v_dirs[3 * i + 1] = 0.f; v_dirs[3 * i + 2] = 0.f; }
   }
   __builtin_amdgcn_wave_barrier();
-  for (int e = lane; e < rows * 3; e += 64) {
-    const int rr = e / 3, c = e - 3 * rr;
-    vc.c0[(i0 + rr) * vc.s0 + c] = sb[rr * RS + c];
-  }
-  if (WR > 0)
-    for (int e = lane; e < rows * WR; e += 64) {
-      const int rr = e / WR, c = e - WR * rr;
-      vc.cr[(i0 + rr) * vc.sr + c] = sb[rr * RS + 3 + c];
+  {  // gradient rows out, lane-contiguous
+    float *g0 = vc.c0 + i0 * vc.s0;
+    RowWalk<3> w0(lane);
+    for (int e = lane; e < rows * 3; e += 64, w0.next())
+      g0[(int64_t)w0.rr * vc.s0 + w0.c] = sd[w0.rr * 3 + w0.c];
+    if (WR > 0) {
+      float *gr = vc.cr + i0 * vc.sr;
+      RowWalk<(WR > 0 ? WR : 1)> wr(lane);
+      for (int e = lane; e < rows * WR; e += 64, wr.next())
+        gr[(int64_t)wr.rr * vc.sr + wr.c] = sr[wr.rr * RSR + wr.c];
     }
+  }
 }
 
 }  // namespace gs

@@ -31,7 +31,7 @@ constexpr float C1 = 0.01f * 0.01f, C2 = 0.03f * 0.03f;
 
 typedef float f2v __attribute__((ext_vector_type(2)));
 
-constexpr int kLoads = (WN * WN + 255) / 256;  // window elements per thread
+constexpr int kRows = (WN + 3) / 4;  // window rows per wave in the staging loops
 
 // 1-D grid over (tile, image-channel) so that the channels of one tile run
 // back to back on the same XCD (workgroup i goes to XCD i % 8): the
@@ -161,31 +161,39 @@ fwd_kernel(int B, int H, int W, int C, const float *__restrict__ x, const float 
   const int64_t plane = (int64_t)Hm * Wm;
   float ssum = 0.f, lsum = 0.f;
   {
-    // all window loads in flight before the first LDS store
-    float vx[kLoads], vy[kLoads];
+    // window staging: lane = window column, wave w = rows w, w+4, ...; row
+    // pointers are wave-uniform, so the loads are saddr + per-lane offset and
+    // all of them are in flight before the first LDS store
+    const int lane = tid & 63, w4 = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int gj = mj0 + lane;
+    const bool col_ok = lane < WN && gj < W;
+    const int64_t img0 = (int64_t)b * H * W * C + c;
+    const uint32_t lo = (uint32_t)(min(gj, W - 1) * C);  // clamped: loads are unconditional
+    float vx[kRows], vy[kRows];
 #pragma unroll
-    for (int k = 0; k < kLoads; ++k) {
-      const int e = tid + 256 * k;
-      const int r = e / WN, q = e - r * WN;
-      const int gi = mi0 + r, gj = mj0 + q;
-      vx[k] = vy[k] = 0.f;
-      if (e < WN * WN && gi < H && gj < W) {
-        const int64_t o = (((int64_t)b * H + gi) * W + gj) * C + c;
-        vx[k] = x[o];
-        vy[k] = y[o];
-      }
+    for (int k = 0; k < kRows; ++k) {
+      const int r = w4 + 4 * k, gi = min(mi0 + r, H - 1);
+      const float *xr = x + img0 + (int64_t)gi * W * C;
+      const float *yr = y + img0 + (int64_t)gi * W * C;
+      vx[k] = xr[lo];
+      vy[k] = yr[lo];
+    }
+#pragma unroll
+    for (int k = 0; k < kRows; ++k) {
+      const bool ok = col_ok && mi0 + w4 + 4 * k < H;
+      vx[k] = ok ? vx[k] : 0.f;
+      vy[k] = ok ? vy[k] : 0.f;
     }
     // L1 over the whole image from the window: each workgroup owns the image
     // pixels of its map tile (edge workgroups also the 2R-pixel border)
     const int ri1 = (mi0 + TW >= Hm) ? H - mi0 : TW;
     const int rj1 = (mj0 + TW >= Wm) ? W - mj0 : TW;
 #pragma unroll
-    for (int k = 0; k < kLoads; ++k) {
-      const int e = tid + 256 * k;
-      const int r = e / WN, q = e - r * WN;
-      if (e < WN * WN) {
-        s_xy[r][q] = f2v{vx[k], vy[k]};
-        if (r < ri1 && q < rj1) lsum += fabsf(vx[k] - vy[k]);
+    for (int k = 0; k < kRows; ++k) {
+      const int r = w4 + 4 * k;
+      if (r < WN && lane < WN) {
+        s_xy[r][lane] = f2v{vx[k], vy[k]};
+        if (r < ri1 && lane < rj1) lsum += fabsf(vx[k] - vy[k]);
       }
     }
     __syncthreads();
@@ -285,28 +293,34 @@ bwd_kernel(int B, int H, int W, int C, const float *__restrict__ x, const float 
   {
     const float *mp = maps + (((int64_t)b * C + c) * 3) * plane;
     // map window rows [qi0-10, qi0+32), cols [qj0-10, qj0+32), zero outside;
-    // all loads in flight before the first LDS store
-    float m0[kLoads], m1[kLoads], m2[kLoads];
+    // lane = window column, wave w = rows w, w+4, ... (see fwd_kernel)
+    const int lane = tid & 63, w4 = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int pj = qj0 - 2 * R + lane;
+    const bool col_ok = lane < WN && pj >= 0 && pj < Wm;
+    const int pjc = min(max(pj, 0), Wm - 1);  // clamped: loads are unconditional
+    float m0[kRows], m1[kRows], m2[kRows];
 #pragma unroll
-    for (int k = 0; k < kLoads; ++k) {
-      const int e = tid + 256 * k;
-      const int r = e / WN, q = e - r * WN;
-      const int pi = qi0 - 2 * R + r, pj = qj0 - 2 * R + q;
-      m0[k] = m1[k] = m2[k] = 0.f;
-      if (e < WN * WN && pi >= 0 && pi < Hm && pj >= 0 && pj < Wm) {
-        const int64_t o = (int64_t)pi * Wm + pj;
-        m0[k] = mp[o];
-        m1[k] = mp[plane + o];
-        m2[k] = mp[2 * plane + o];
-      }
+    for (int k = 0; k < kRows; ++k) {
+      const int pi = min(max(qi0 - 2 * R + w4 + 4 * k, 0), Hm - 1);
+      const float *row = mp + (int64_t)pi * Wm;
+      m0[k] = row[pjc];
+      m1[k] = row[plane + pjc];
+      m2[k] = row[2 * plane + pjc];
     }
 #pragma unroll
-    for (int k = 0; k < kLoads; ++k) {
-      const int e = tid + 256 * k;
-      const int r = e / WN, q = e - r * WN;
-      if (e < WN * WN) {
-        s_01[r][q] = f2v{m0[k], m1[k]};
-        s_2[r][q] = m2[k];
+    for (int k = 0; k < kRows; ++k) {
+      const int pi = qi0 - 2 * R + w4 + 4 * k;
+      const bool ok = col_ok && pi >= 0 && pi < Hm;
+      m0[k] = ok ? m0[k] : 0.f;
+      m1[k] = ok ? m1[k] : 0.f;
+      m2[k] = ok ? m2[k] : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < kRows; ++k) {
+      const int r = w4 + 4 * k;
+      if (r < WN && lane < WN) {
+        s_01[r][lane] = f2v{m0[k], m1[k]};
+        s_2[r][lane] = m2[k];
       }
     }
     __syncthreads();

@@ -128,7 +128,7 @@ class _FullyFusedProjection(torch.autograd.Function):
             return torch.zeros(shape, device=dev) if t is None else _f32c(t)
 
         v_means2d = g(v_means2d, (C, N, 2))
-        v_depths = g(v_depths, (C, N))
+        v_depths = None if v_depths is None else _f32c(v_depths)  # null = zeros in the kernel
         v_conics = g(v_conics, (C, N, 3))
         if comps is not None:
             v_compensations = g(v_compensations, (C, N))

@@ -1,0 +1,63 @@
+"""Trainer glue of the training step as single HIP launches (csrc/strategy.hip).
+
+`activate`     -- exp(log_scales), sigmoid(logits) with autograd, the
+                  activations of examples/simple_trainer.py:565-566.
+`update_state_` -- DefaultStrategy._update_state for packed=False
+                  (gsplat/strategy/default.py:213-262), in place, no host sync.
+"""
+
+import ctypes
+
+import torch
+
+from . import _lib
+from ._wrapper import _f32c, _ptr, _stream
+
+
+def _dev(*ts):
+    for t in ts:
+        if not t.is_cuda:
+            raise ValueError("gsplat_hip.strategy: tensors must be on the GPU")
+
+
+class _Activate(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, log_scales, logits):
+        log_scales, logits = _f32c(log_scales), _f32c(logits)
+        _dev(log_scales, logits)
+        scales = torch.empty_like(log_scales)
+        opac = torch.empty_like(logits)
+        _lib.call("gsplat_hip_activate_fwd", log_scales.numel(), logits.numel(),
+                  _ptr(log_scales), _ptr(logits), _ptr(scales), _ptr(opac), _stream())
+        ctx.save_for_backward(scales, opac)
+        return scales, opac
+
+    @staticmethod
+    def backward(ctx, v_scales, v_opac):
+        scales, opac = ctx.saved_tensors
+        v_scales = torch.zeros_like(scales) if v_scales is None else _f32c(v_scales)
+        v_opac = torch.zeros_like(opac) if v_opac is None else _f32c(v_opac)
+        v_log = torch.empty_like(scales)
+        v_logit = torch.empty_like(opac)
+        _lib.call("gsplat_hip_activate_bwd", scales.numel(), opac.numel(), _ptr(scales),
+                  _ptr(opac), _ptr(v_scales), _ptr(v_opac), _ptr(v_log), _ptr(v_logit),
+                  _stream())
+        return v_log, v_logit
+
+
+def activate(log_scales, logits):
+    """(exp(log_scales), sigmoid(logits)), differentiable."""
+    return _Activate.apply(log_scales, logits)
+
+
+@torch.no_grad()
+def update_state_(grad2d, count, means2d_grad, radii, width, height, n_cameras):
+    """grad2d/count += DefaultStrategy's per-step statistics (in place)."""
+    C, N = radii.shape
+    g = _f32c(means2d_grad)
+    radii = radii.to(torch.int32).contiguous()
+    _dev(grad2d, count, g, radii)
+    assert grad2d.is_contiguous() and count.is_contiguous() and grad2d.numel() == N
+    _lib.call("gsplat_hip_update_state", C, N, _ptr(g), _ptr(radii),
+              ctypes.c_float(width / 2.0 * n_cameras), ctypes.c_float(height / 2.0 * n_cameras),
+              _ptr(grad2d), _ptr(count), _stream())

@@ -22,6 +22,7 @@ import torch.nn.functional as F
 
 from .losses import FusedAdam, l1_ssim_loss
 from .rendering import rasterization
+from .strategy import activate, update_state_
 
 C0 = 0.28209479177387814
 
@@ -143,8 +144,12 @@ class Trainer:
 
     def render(self, ci: int):
         p = self.params
+        if self.fused:  # one HIP launch each way for both activations
+            scales, opac = activate(p["scales"], p["opacities"])
+        else:
+            scales, opac = torch.exp(p["scales"]), torch.sigmoid(p["opacities"])
         return rasterization(
-            p["means"], p["quats"], torch.exp(p["scales"]), torch.sigmoid(p["opacities"]),
+            p["means"], p["quats"], scales, opac,
             (p["sh0"], p["shN"]) if self.fused else torch.cat([p["sh0"], p["shN"]], 1), self.viewmats[ci:ci + 1], self.Ks[ci:ci + 1],
             self.width, self.height, sh_degree=self.sh_degree, packed=False,
             near_plane=0.01, far_plane=1e10, radius_clip=0.0, rasterize_mode="classic")
@@ -188,6 +193,10 @@ class Trainer:
         sync of torch.where (default.py:213-262): same sums, masked."""
         g = meta["means2d"].grad
         if g is None:
+            return
+        if self.fused:
+            update_state_(self.grad2d, self.count, g, meta["radii"], meta["width"],
+                          meta["height"], meta["n_cameras"])
             return
         sx = meta["width"] / 2.0 * meta["n_cameras"]
         sy = meta["height"] / 2.0 * meta["n_cameras"]

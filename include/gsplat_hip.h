@@ -50,7 +50,8 @@ int gsplat_hip_projection_fwd(int C, int N, const float *means, const float *qua
  *   gsplat/triton_impl/fused_projection_bwd.py:24-465, called from
  *   _FullyFusedProjection.backward (gsplat/triton_impl/_wrapper.py:355-426).
  * Only (c, n) with radii > 0 contribute.  v_viewmats[C,4,4] may be NULL
- * (viewmats does not require grad, _wrapper.py:394). */
+ * (viewmats does not require grad, _wrapper.py:394); v_depths may be NULL
+ * (depths without a gradient, read as zeros -- no zero-filled buffer). */
 int gsplat_hip_projection_bwd(int C, int N, const float *means, const float *quats,
                               const float *scales, const float *viewmats, const float *Ks,
                               int width, int height, float eps2d, const int32_t *radii,
@@ -251,6 +252,24 @@ int gsplat_hip_l1_ssim_loss_fwd(int B, int H, int W, int C, const float *img1,
 int gsplat_hip_l1_ssim_loss_bwd(int B, int H, int W, int C, const float *img1,
                                 const float *img2, const void *workspace, float lam,
                                 const float *g_loss, float *grad_img1, void *stream);
+
+/* DefaultStrategy._update_state for packed=False (gsplat/strategy/default.py:
+ * 213-262): for every (c, g) with radii[c,g] > 0, in camera order,
+ * grad2d[g] += |(means2d_grad[c,g,0]*scale_x, means2d_grad[c,g,1]*scale_y)|
+ * and count[g] += 1.  scale_x = width/2 * C, scale_y = height/2 * C. */
+int gsplat_hip_update_state(int C, int64_t N, const float *means2d_grad, const int32_t *radii,
+                            float scale_x, float scale_y, float *grad2d, float *count,
+                            void *stream);
+
+/* The trainer's parameter activations (examples/simple_trainer.py:565-566)
+ * in one launch each way: scales = exp(log_scales), opacities =
+ * sigmoid(logits); backward with torch's formulas (g * exp, g * (1-o) * o). */
+int gsplat_hip_activate_fwd(int64_t n_scales, int64_t n_opacities, const float *log_scales,
+                            const float *logits, float *scales, float *opacities, void *stream);
+int gsplat_hip_activate_bwd(int64_t n_scales, int64_t n_opacities, const float *scales,
+                            const float *opacities, const float *v_scales,
+                            const float *v_opacities, float *v_log_scales, float *v_logits,
+                            void *stream);
 
 /* One torch.optim.Adam step (amsgrad=False, no weight decay) over up to 8
  * parameter groups in a single launch (replaces the per-group optimizers of

@@ -72,3 +72,46 @@ def test_fused_adam_matches_torch():
         mine.step()
     for p, q in zip(ps, qs):
         torch.testing.assert_close(p, q, rtol=1e-5, atol=1e-6)
+
+
+def test_activate_matches_torch_exactly():
+    """exp / sigmoid and their VJPs in one launch each way equal torch's."""
+    from gsplat_hip.strategy import activate
+    g = torch.Generator(device="cuda").manual_seed(5)
+    ls = (torch.randn(10007, 3, device="cuda", generator=g) * 3).requires_grad_(True)
+    lg = (torch.randn(10007, device="cuda", generator=g) * 6).requires_grad_(True)
+    s, o = activate(ls, lg)
+    ls_r = ls.detach().clone().requires_grad_(True)
+    lg_r = lg.detach().clone().requires_grad_(True)
+    s_r, o_r = torch.exp(ls_r), torch.sigmoid(lg_r)
+    assert torch.equal(s, s_r) and torch.equal(o, o_r)
+    vs = torch.randn_like(s)
+    vo = torch.randn_like(o)
+    ((s * vs).sum() + (o * vo).sum()).backward()
+    ((s_r * vs).sum() + (o_r * vo).sum()).backward()
+    assert torch.equal(ls.grad, ls_r.grad) and torch.equal(lg.grad, lg_r.grad)
+
+
+@pytest.mark.parametrize("C", [1, 3])
+def test_update_state_matches_torch(C):
+    """DefaultStrategy._update_state (default.py:213-262) with torch ops vs the
+    one-launch HIP version, over two steps (accumulation)."""
+    from gsplat_hip.strategy import update_state_
+    N, W, H = 5003, 640, 480
+    g = torch.Generator(device="cuda").manual_seed(C)
+    grad2d = torch.zeros(N, device="cuda")
+    count = torch.zeros(N, device="cuda")
+    g_r, c_r = grad2d.clone(), count.clone()
+    for _ in range(2):
+        m2g = torch.randn(C, N, 2, device="cuda", generator=g) * 1e-3
+        radii = torch.randint(-1, 3, (C, N), device="cuda", generator=g, dtype=torch.int32)
+        update_state_(grad2d, count, m2g, radii, W, H, C)
+        grads = m2g.clone()
+        grads[..., 0] *= W / 2.0 * C
+        grads[..., 1] *= H / 2.0 * C
+        sel = radii > 0
+        ids = torch.where(sel)[1]
+        g_r.index_add_(0, ids, grads[sel].norm(dim=-1))
+        c_r.index_add_(0, ids, torch.ones_like(ids, dtype=torch.float32))
+    torch.testing.assert_close(grad2d, g_r, rtol=1e-6, atol=0)
+    assert torch.equal(count, c_r)
