@@ -163,7 +163,7 @@ __global__ void __launch_bounds__(256) rasterize_bwd_kernel(RasterArgs a) {
   for (int d = 0; d < D; ++d) Drc[d] = 0.f;
   if (t.inside) {
     T_final = 1.f - a.render_alphas[pix];
-    Dra = a.v_render_alphas[pix];
+    Dra = a.v_render_alphas ? a.v_render_alphas[pix] : 0.f;  // null: alphas unused
     my_last = a.last_ids[pix];
 #pragma unroll
     for (int d = 0; d < D; ++d) Drc[d] = a.v_render_colors[pix * D + d];

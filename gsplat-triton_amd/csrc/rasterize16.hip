@@ -615,7 +615,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) b
   if (in) {
     const int64_t pix = ((int64_t)c * a.H + geo.py) * a.W + geo.px;
     Tf = 1.f - a.render_alphas[pix];
-    Dra = a.v_render_alphas[pix];
+    Dra = a.v_render_alphas ? a.v_render_alphas[pix] : 0.f;  // null: alphas unused
     mylast = a.last_ids[pix];
 #pragma unroll
     for (int d = 0; d < D; ++d) Drc[d] = a.v_render_colors[pix * D + d];

@@ -98,6 +98,7 @@ class _FullyFusedProjection(torch.autograd.Function):
                 camera_model="pinhole", block_size=256):
         if camera_model != "pinhole":
             raise NotImplementedError(f"Unsupported camera model: {camera_model}")
+        ctx.set_materialize_grads(False)  # unused outputs: None, no zero-filled buffers
         assert (covars is None) and (quats is not None) and (scales is not None)
         means, quats, scales, viewmats, Ks = (_f32c(x) for x in (means, quats, scales, viewmats, Ks))
         quats = _aligned16(quats)
@@ -220,6 +221,14 @@ def isect_tiles(
     Returns tiles_per_gauss i32 [C,N] (or [nnz]), isect_ids i64 [n_isects]
     (camera | tile | depth bits, Triton tile-bit width) and flatten_ids i32.
     One device->host read of n_isects, as the reference."""
+    return isect_tiles_begin(means2d, radii, depths, tile_size, tile_width, tile_height, packed,
+                             n_cameras, camera_ids, gaussian_ids).finish(sort)
+
+
+def isect_tiles_begin(means2d, radii, depths, tile_size, tile_width, tile_height,
+                      packed=False, n_cameras=None, camera_ids=None, gaussian_ids=None):
+    """First half of isect_tiles (counts queued, totals on their way to the
+    host); `.finish(sort)` returns isect_tiles' outputs."""
     dev = means2d.device
     if packed:
         nnz = means2d.size(0)
@@ -246,50 +255,87 @@ def isect_tiles(
     n_bit_cam = _bit_length(C - 1)
     assert n_bit_tile + n_bit_cam <= 32, "tile_id and cam_id exceed 32 bits"
 
-    st = _stream()
-    tpg = torch.empty(G, dtype=torch.int32, device=dev)
-    ws = torch.empty(max(int(_lib.query("gsplat_hip_isect_workspace_bytes", G)), 8),
-                     dtype=torch.uint8, device=dev)
-    totals = torch.empty(2, dtype=torch.int64, device=dev)
-    _lib.call("gsplat_hip_isect_count", G, _ptr(means2d), _ptr(radii), tile_size, tile_width,
-              tile_height, _ptr(tpg), _ptr(ws), _ptr(totals), st)
-    n_isects, n_visible = totals.tolist()  # the single host sync (isect_tiles.py:102)
-    isect_ids = torch.empty(n_isects, dtype=torch.int64, device=dev)
-    flatten_ids = torch.empty(n_isects, dtype=torch.int32, device=dev)
-    if sort and ISECT_SORT == "tile_first" and n_isects > 0:
-        sws = torch.empty(max(int(_lib.query("gsplat_hip_isect_tilefirst_workspace_bytes",
-                                             n_isects, C * tile_width * tile_height,
-                                             n_bit_tile + n_bit_cam)), 8),
-                          dtype=torch.uint8, device=dev)
-        _lib.call("gsplat_hip_isect_write_tilefirst", G, N, _ptr(means2d), _ptr(radii),
-                  _ptr(depths), _ptr(camera_ids), tile_size, tile_width, tile_height, C,
-                  n_bit_tile, n_bit_cam, _ptr(ws), n_isects, _ptr(sws), sws.numel(),
-                  _ptr(isect_ids), _ptr(flatten_ids), st)
-    elif sort and ISECT_SORT == "depth_first":
-        key_bits = n_bit_tile + n_bit_cam
-        sws = torch.empty(max(int(_lib.query("gsplat_hip_isect_sorted_workspace_bytes", n_visible,
-                                             n_isects, key_bits)), 8),
-                          dtype=torch.uint8, device=dev)
-        _lib.call("gsplat_hip_isect_write_sorted", G, N, _ptr(means2d), _ptr(radii),
-                  _ptr(depths), _ptr(camera_ids), _ptr(tpg), tile_size, tile_width, tile_height,
-                  n_bit_tile, n_bit_cam, _ptr(ws), n_visible, n_isects, _ptr(sws), sws.numel(),
-                  _ptr(isect_ids), _ptr(flatten_ids), st)
-    else:
-        _lib.call("gsplat_hip_isect_write", G, N, _ptr(means2d), _ptr(radii), _ptr(depths),
-                  _ptr(camera_ids), tile_size, tile_width, tile_height, n_bit_tile, _ptr(ws),
-                  _ptr(isect_ids), _ptr(flatten_ids), st)
-        if sort and n_isects > 0:
-            sws = torch.empty(max(int(_lib.query("gsplat_hip_sort_workspace_bytes", n_isects)),
-                                  8), dtype=torch.uint8, device=dev)
-            keys = torch.empty_like(isect_ids)
-            vals = torch.empty_like(flatten_ids)
-            _lib.call("gsplat_hip_radix_sort", n_isects, 32 + n_bit_tile + n_bit_cam,
-                      _ptr(isect_ids), _ptr(flatten_ids), _ptr(keys), _ptr(vals), _ptr(sws),
-                      sws.numel(), st)
-            isect_ids, flatten_ids = keys, vals
-    if not packed:
-        tpg = tpg.view(C, N)
-    return tpg, isect_ids, flatten_ids
+    return _IsectCount(means2d, radii, depths, camera_ids, C, N, G, tile_size, tile_width,
+                       tile_height, n_bit_tile, n_bit_cam, packed)
+
+
+_PINNED = {}
+
+
+class _IsectCount:
+    """isect_tiles in two halves around its single host sync: the count
+    kernels and an asynchronous copy of (n_isects, n_visible) into pinned host
+    memory are queued on construction; `finish` waits for that copy only and
+    queues the emission and sort.  Work queued in between (rasterization()'s
+    SH colours) keeps the GPU busy across the host round trip."""
+
+    def __init__(self, means2d, radii, depths, camera_ids, C, N, G, tile_size, tile_width,
+                 tile_height, n_bit_tile, n_bit_cam, packed):
+        dev = means2d.device
+        self.args = (means2d, radii, depths, camera_ids, C, N, G, tile_size, tile_width,
+                     tile_height, n_bit_tile, n_bit_cam, packed)
+        self.tpg = torch.empty(G, dtype=torch.int32, device=dev)
+        self.ws = torch.empty(max(int(_lib.query("gsplat_hip_isect_workspace_bytes", G)), 8),
+                              dtype=torch.uint8, device=dev)
+        totals = torch.empty(2, dtype=torch.int64, device=dev)
+        _lib.call("gsplat_hip_isect_count", G, _ptr(means2d), _ptr(radii), tile_size,
+                  tile_width, tile_height, _ptr(self.tpg), _ptr(self.ws), _ptr(totals),
+                  _stream())
+        host = _PINNED.get(dev)
+        if host is None:
+            host = _PINNED[dev] = torch.empty(2, dtype=torch.int64, pin_memory=True)
+        host.copy_(totals, non_blocking=True)
+        self.host, self.totals = host, totals
+        self.event = torch.cuda.Event()
+        self.event.record()
+
+    @torch.no_grad()
+    def finish(self, sort: bool = True) -> Tuple[Tensor, Tensor, Tensor]:
+        (means2d, radii, depths, camera_ids, C, N, G, tile_size, tile_width, tile_height,
+         n_bit_tile, n_bit_cam, packed) = self.args
+        dev, st = means2d.device, _stream()
+        tpg, ws = self.tpg, self.ws
+        # the single host sync (isect_tiles.py:102); polling reacts within a
+        # few us where hipEventSynchronize's blocking wait took ~100 us
+        while not self.event.query():
+            pass
+        n_isects, n_visible = self.host.tolist()
+        isect_ids = torch.empty(n_isects, dtype=torch.int64, device=dev)
+        flatten_ids = torch.empty(n_isects, dtype=torch.int32, device=dev)
+        if sort and ISECT_SORT == "tile_first" and n_isects > 0:
+            sws = torch.empty(max(int(_lib.query("gsplat_hip_isect_tilefirst_workspace_bytes",
+                                                 n_isects, C * tile_width * tile_height,
+                                                 n_bit_tile + n_bit_cam)), 8),
+                              dtype=torch.uint8, device=dev)
+            _lib.call("gsplat_hip_isect_write_tilefirst", G, N, _ptr(means2d), _ptr(radii),
+                      _ptr(depths), _ptr(camera_ids), tile_size, tile_width, tile_height, C,
+                      n_bit_tile, n_bit_cam, _ptr(ws), n_isects, _ptr(sws), sws.numel(),
+                      _ptr(isect_ids), _ptr(flatten_ids), st)
+        elif sort and ISECT_SORT == "depth_first":
+            key_bits = n_bit_tile + n_bit_cam
+            sws = torch.empty(max(int(_lib.query("gsplat_hip_isect_sorted_workspace_bytes", n_visible,
+                                                 n_isects, key_bits)), 8),
+                              dtype=torch.uint8, device=dev)
+            _lib.call("gsplat_hip_isect_write_sorted", G, N, _ptr(means2d), _ptr(radii),
+                      _ptr(depths), _ptr(camera_ids), _ptr(tpg), tile_size, tile_width, tile_height,
+                      n_bit_tile, n_bit_cam, _ptr(ws), n_visible, n_isects, _ptr(sws), sws.numel(),
+                      _ptr(isect_ids), _ptr(flatten_ids), st)
+        else:
+            _lib.call("gsplat_hip_isect_write", G, N, _ptr(means2d), _ptr(radii), _ptr(depths),
+                      _ptr(camera_ids), tile_size, tile_width, tile_height, n_bit_tile, _ptr(ws),
+                      _ptr(isect_ids), _ptr(flatten_ids), st)
+            if sort and n_isects > 0:
+                sws = torch.empty(max(int(_lib.query("gsplat_hip_sort_workspace_bytes", n_isects)),
+                                      8), dtype=torch.uint8, device=dev)
+                keys = torch.empty_like(isect_ids)
+                vals = torch.empty_like(flatten_ids)
+                _lib.call("gsplat_hip_radix_sort", n_isects, 32 + n_bit_tile + n_bit_cam,
+                          _ptr(isect_ids), _ptr(flatten_ids), _ptr(keys), _ptr(vals), _ptr(sws),
+                          sws.numel(), st)
+                isect_ids, flatten_ids = keys, vals
+        if not packed:
+            tpg = tpg.view(C, N)
+        return tpg, isect_ids, flatten_ids
 
 
 @torch.no_grad()
@@ -463,6 +509,7 @@ class _RasterizeToPixels(torch.autograd.Function):
     def forward(ctx, means2d, conics, colors, opacities, backgrounds, masks, width, height,
                 tile_size, isect_offsets, flatten_ids, absgrad, block_size=8):
         ctx.means2d_in = means2d if absgrad else None  # receives .absgrad (_wrapper.py:156)
+        ctx.set_materialize_grads(False)  # alphas without a loss: None, not zeros
         means2d, conics, colors, opacities, backgrounds = (
             _f32c(x) for x in (means2d, conics, colors, opacities, backgrounds))
         _dev_check(means2d, conics, colors, opacities, isect_offsets, flatten_ids)
@@ -498,8 +545,10 @@ class _RasterizeToPixels(torch.autograd.Function):
         C, th, tw = isect_offsets.shape
         D = colors.shape[-1]
         G = opacities.numel()
+        if v_render_colors is None:
+            v_render_colors = torch.zeros_like(render_colors)
         v_render_colors = _f32c(v_render_colors)
-        v_render_alphas = _f32c(v_render_alphas)
+        v_render_alphas = _f32c(v_render_alphas)  # None: alphas unused (null in the ABI)
         v_means2d = torch.empty_like(means2d)
         v_conics = torch.empty_like(conics)
         v_colors = torch.empty_like(colors)

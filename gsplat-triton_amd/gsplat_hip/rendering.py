@@ -18,7 +18,7 @@ from torch import Tensor
 from ._wrapper import (
     fully_fused_projection,
     isect_offset_encode,
-    isect_tiles,
+    isect_tiles_begin,
     rasterize_to_pixels,
     sh_colors,
     spherical_harmonics,
@@ -106,6 +106,13 @@ def rasterization(
     meta.update({"camera_ids": None, "gaussian_ids": None, "radii": radii, "means2d": means2d,
                  "depths": depths, "conics": conics, "opacities": opacities})
 
+    # tile intersection first: its counts travel to the host (the one sync of
+    # the render) while the GPU computes the colours below
+    tile_width = math.ceil(width / float(tile_size))
+    tile_height = math.ceil(height / float(tile_size))
+    pending_isects = isect_tiles_begin(means2d, radii, depths, tile_size, tile_width, tile_height,
+                                       packed=False, n_cameras=C)
+
     if sh_degree is None:
         if colors.dim() == 2:
             colors = colors[None] if C == 1 else colors.expand(C, -1, -1)
@@ -137,10 +144,7 @@ def rasterization(
         if backgrounds is not None:
             backgrounds = torch.zeros(C, 1, device=backgrounds.device)
 
-    tile_width = math.ceil(width / float(tile_size))
-    tile_height = math.ceil(height / float(tile_size))
-    tiles_per_gauss, isect_ids, flatten_ids = isect_tiles(
-        means2d, radii, depths, tile_size, tile_width, tile_height, packed=False, n_cameras=C)
+    tiles_per_gauss, isect_ids, flatten_ids = pending_isects.finish(sort=True)
     isect_offsets = isect_offset_encode(isect_ids, C, tile_width, tile_height)
     meta.update({"tile_width": tile_width, "tile_height": tile_height,
                  "tiles_per_gauss": tiles_per_gauss, "isect_ids": isect_ids,

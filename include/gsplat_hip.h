@@ -200,6 +200,7 @@ int gsplat_hip_rasterize_fwd(int C, int D, int width, int height, int tile_size,
 int64_t gsplat_hip_rasterize_bwd_workspace_bytes(int64_t n_gaussians, int D, int tile_size,
                                                  int absgrad, int C, int tile_width,
                                                  int tile_height, int64_t n_isects);
+/* v_render_alphas may be NULL (alphas without a gradient: read as zeros). */
 int gsplat_hip_rasterize_bwd(int C, int64_t n_gaussians, int D, int width, int height,
                              int tile_size, int tile_width, int tile_height,
                              const float *means2d, const float *conics, const float *colors,
