@@ -148,7 +148,9 @@ struct Args {
   // holds T[256] then acc[D][256] of the tile's pixels before that isect.
   float *state;
   int L;  // chunk length in isects (multiple of 64); 0 = no chunking
-  const int2 *items;  // backward work items (tile, chunk) and their count
+  // backward work items (tile, chunk): n_items[0] full-length chunks at
+  // items[0..), n_items[1] tails at items_tail[0..)
+  const int2 *items, *items_tail;
   const int32_t *n_items;
   const float *render_colors_in;  // backward: forward colours (for suffix sums)
   int dbg;  // experiments only (GSPLAT_HIP_DBG): bit 0 = backward skips its atomics
@@ -593,8 +595,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) b
   // of a long tile (a.items, see "Chunked backward")
   int tile = blockIdx.x, k = 0;
   if (a.items) {
-    if ((int)blockIdx.x >= *a.n_items) return;
-    const int2 it = a.items[blockIdx.x];
+    const int nf = a.n_items[0];
+    int b = blockIdx.x;
+    if (b >= nf && b - nf >= a.n_items[1]) return;
+    const int2 it = b < nf ? a.items[b] : a.items_tail[b - nf];
     tile = it.x;
     k = it.y;
   }
@@ -788,27 +792,24 @@ unpack_kernel(int64_t G, int S, const float *__restrict__ packed, float *__restr
 }
 
 // Backward work items.  A tile with n isects becomes ceil(n / L) items
-// (tile, k); the full-length chunks are listed first and the shorter tails
-// after them, so the longest items start first.  One 1024-lane workgroup.
-__global__ void __launch_bounds__(1024)
+// (tile, k): the full-length chunks go to `full`, the shorter tails to `tail`
+// (the backward runs all full chunks first, so the longest items start
+// first).  One lane per tile; one atomic per wave and list on the counters
+// n_items[0..1], which the packed-gradient memset has zeroed.
+__global__ void __launch_bounds__(256)
 chunk_items_kernel(int n_tiles, const int32_t *__restrict__ offsets, int64_t n_isects, int L,
-                   int2 *__restrict__ items, int32_t *__restrict__ n_items) {
-  __shared__ int wtot[2][16];
-  const int per = (n_tiles + 1023) / 1024;
-  const int t0 = min(n_tiles, (int)threadIdx.x * per), t1 = min(n_tiles, t0 + per);
-  auto len = [&](int t) -> int64_t {
-    const int64_t e = (t == n_tiles - 1) ? n_isects : (int64_t)offsets[t + 1];
-    return e - offsets[t];
-  };
+                   int2 *__restrict__ full, int2 *__restrict__ tail,
+                   int32_t *__restrict__ n_items) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  const int lane = threadIdx.x & 63;
   int nf = 0, nt = 0;
-  for (int t = t0; t < t1; ++t) {
-    const int64_t n = len(t);
-    nf += (int)(n / L);
-    nt += (n % L) != 0;
+  if (t < n_tiles) {
+    const int64_t e = (t == n_tiles - 1) ? n_isects : (int64_t)offsets[t + 1];
+    const int64_t n = e - offsets[t];
+    nf = (int)(n / L);
+    nt = (n % L) != 0;
   }
-  // block exclusive scans of nf and nt
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  int xf = nf, xt = nt;
+  int xf = nf, xt = nt;  // inclusive wave scans
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
     const int yf = __shfl_up(xf, o, 64), yt = __shfl_up(xt, o, 64);
@@ -817,28 +818,15 @@ chunk_items_kernel(int n_tiles, const int32_t *__restrict__ offsets, int64_t n_i
       xt += yt;
     }
   }
+  int bf = 0, bt = 0;
   if (lane == 63) {
-    wtot[0][w] = xf;
-    wtot[1][w] = xt;
+    bf = xf ? atomicAdd(&n_items[0], xf) : 0;
+    bt = xt ? atomicAdd(&n_items[1], xt) : 0;
   }
-  __syncthreads();
-  int bf = 0, bt = 0, F = 0, TT = 0;
-  for (int i = 0; i < 16; ++i) {
-    if (i < w) {
-      bf += wtot[0][i];
-      bt += wtot[1][i];
-    }
-    F += wtot[0][i];
-    TT += wtot[1][i];
-  }
-  int pf = bf + xf - nf, pt = F + bt + xt - nt;
-  for (int t = t0; t < t1; ++t) {
-    const int64_t n = len(t);
-    const int full = (int)(n / L);
-    for (int k = 0; k < full; ++k) items[pf++] = make_int2(t, k);
-    if (n % L) items[pt++] = make_int2(t, full);
-  }
-  if (threadIdx.x == 0) *n_items = F + TT;
+  bf = __shfl(bf, 63, 64) + xf - nf;
+  bt = __shfl(bt, 63, 64) + xt - nt;
+  for (int k = 0; k < nf; ++k) full[bf + k] = make_int2(t, k);
+  if (nt) tail[bt] = make_int2(t, nf);
 }
 
 }  // namespace r16
@@ -891,15 +879,19 @@ int r16_bwd(r16::Args a, int64_t G, float *v_means2d, float *v_conics, float *v_
   constexpr int F = D + 6 + (ABS ? 2 : 0);
   a.S = ((F + 15) / 16) * 16;
   a.packed = reinterpret_cast<float *>(workspace);
-  GS_HIP(hipMemsetAsync(a.packed, 0, sizeof(float) * (size_t)a.S * G, st));
+  const bool chunked = a.n_isects > 0 && a.state && a.L > 0 && a.render_colors_in;
+  // one memset: the gradient rows and, right after them, the item counters
+  GS_HIP(hipMemsetAsync(a.packed, 0, packed_bytes(D, ABS, G) + (chunked ? 256 : 0), st));
   if (a.n_isects > 0) {
     int64_t grid = a.n_tiles;
-    if (a.state && a.L > 0 && a.render_colors_in) {
+    if (chunked) {
       char *w = reinterpret_cast<char *>(workspace) + packed_bytes(D, ABS, G);
       a.n_items = reinterpret_cast<int32_t *>(w);
       a.items = reinterpret_cast<int2 *>(w + 256);
-      hipLaunchKernelGGL(r16::chunk_items_kernel, dim3(1), dim3(1024), 0, st, a.n_tiles,
-                         a.offsets, a.n_isects, a.L, const_cast<int2 *>(a.items),
+      a.items_tail = a.items + (a.n_isects / a.L + 1);
+      hipLaunchKernelGGL(r16::chunk_items_kernel, dim3((unsigned)((a.n_tiles + 255) / 256)),
+                         dim3(256), 0, st, a.n_tiles, a.offsets, a.n_isects, a.L,
+                         const_cast<int2 *>(a.items), const_cast<int2 *>(a.items_tail),
                          const_cast<int32_t *>(a.n_items));
       grid = n_items_bound(a.n_tiles, a.n_isects);
     } else {
