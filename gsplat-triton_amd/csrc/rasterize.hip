@@ -300,7 +300,7 @@ int rasterize16_fwd(int C, int D, int W, int H, int tw, int th, const float *mea
                     int64_t n_isects, const int32_t *flatten_ids, float *render_colors,
                     float *render_alphas, int32_t *last_ids, void *state, int64_t state_bytes,
                     hipStream_t st);
-int64_t rasterize16_fwd_state_bytes(int D, int64_t n_isects);
+int64_t rasterize16_fwd_state_bytes(int D, int n_tiles, int64_t n_isects);
 int64_t rasterize16_bwd_workspace(int64_t G, int D, bool absgrad, int n_tiles, int64_t n_isects);
 int rasterize16_bwd(int C, int64_t G, int D, int W, int H, int tw, int th,
                     const float *means2d, const float *conics, const float *colors,
@@ -322,9 +322,8 @@ extern "C" int gsplat_hip_rasterize_supported_channels(int D) { return supported
 extern "C" int64_t gsplat_hip_rasterize_fwd_state_bytes(int C, int D, int tile_size,
                                                         int tile_width, int tile_height,
                                                         int64_t n_isects) {
-  (void)C; (void)tile_width; (void)tile_height;
   if (tile_size != 16 || !supported_channels(D)) return 0;
-  return rasterize16_fwd_state_bytes(D, n_isects);
+  return rasterize16_fwd_state_bytes(D, C * tile_width * tile_height, n_isects);
 }
 
 extern "C" int64_t gsplat_hip_rasterize_bwd_workspace_bytes(int64_t n_gaussians, int D,

@@ -152,6 +152,7 @@ struct Args {
   // items[0..), n_items[1] tails at items_tail[0..)
   const int2 *items, *items_tail;
   const int32_t *n_items;
+  const int32_t *order;  // forward: tile of workgroup b (heaviest tiles first) or null
   const float *render_colors_in;  // backward: forward colours (for suffix sums)
   int dbg;  // experiments only (GSPLAT_HIP_DBG): bit 0 = backward skips its atomics
   uint64_t *timeline;  // debug: per-wave (start, end) s_memrealtime stamps or null
@@ -412,7 +413,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) f
   const int lane = threadIdx.x & 63;
   float4 *st = stage_all[threadIdx.x >> 6];
   const uint64_t t_start = tl_now(a);
-  const WaveGeom geo(a, lane, blockIdx.x);
+  const WaveGeom geo(a, lane, a.order ? a.order[blockIdx.x] : (int)blockIdx.x);
   const int tile = geo.tile, c = geo.c;
   const bool inside = geo.px < a.W && geo.py < a.H;
   const float fx = (float)geo.px + 0.5f, fy = (float)geo.py + 0.5f;
@@ -791,6 +792,68 @@ unpack_kernel(int64_t G, int S, const float *__restrict__ packed, float *__restr
   if (ABS) *reinterpret_cast<float2 *>(v_abs + 2 * g) = make_float2(r[D + 6], r[D + 7]);
 }
 
+// Forward dispatch order: tiles bucketed by isect count (>= 2048, >= 1024,
+// >= 512, the rest), heaviest bucket first and raster order inside a bucket,
+// so the longest tiles start in the first wave of workgroups instead of
+// finishing last.  One 1024-lane workgroup; the four bucket counts of a
+// thread are packed into one u64 (16 bits each) for a single block scan.
+__global__ void __launch_bounds__(1024)
+tile_order_kernel(int n_tiles, const int32_t *__restrict__ offsets, int64_t n_isects,
+                  int32_t *__restrict__ order) {
+  constexpr int MAXPER = 16;  // tiles per thread (n_tiles <= 16384)
+  __shared__ uint64_t wsum[16];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  int bucket[MAXPER];
+  uint64_t mine = 0;
+#pragma unroll
+  for (int i = 0; i < MAXPER; ++i) {
+    const int t = tid + 1024 * i;
+    bucket[i] = -1;
+    if (t < n_tiles) {
+      const int64_t e = (t == n_tiles - 1) ? n_isects : (int64_t)offsets[t + 1];
+      const int64_t n = e - offsets[t];
+      bucket[i] = n >= 2048 ? 0 : n >= 1024 ? 1 : n >= 512 ? 2 : 3;
+      mine += (uint64_t)1 << (16 * bucket[i]);
+    }
+  }
+  uint64_t x = mine;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint64_t y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) wsum[w] = x;
+  __syncthreads();
+  uint64_t before = 0, total = 0;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    before += i < w ? wsum[i] : 0;
+    total += wsum[i];
+  }
+  before += x - mine;  // this thread's exclusive prefix, per bucket
+  int pos[4], base = 0;
+#pragma unroll
+  for (int bk = 0; bk < 4; ++bk) {
+    pos[bk] = base + (int)((before >> (16 * bk)) & 0xffff);
+    base += (int)((total >> (16 * bk)) & 0xffff);
+  }
+#pragma unroll
+  for (int i = 0; i < MAXPER; ++i) {
+    const int bk = bucket[i];
+    if (bk >= 0) {
+      int p = pos[0];
+      p = bk == 1 ? pos[1] : p;
+      p = bk == 2 ? pos[2] : p;
+      p = bk == 3 ? pos[3] : p;
+      order[p] = tid + 1024 * i;
+      pos[0] += bk == 0;
+      pos[1] += bk == 1;
+      pos[2] += bk == 2;
+      pos[3] += bk == 3;
+    }
+  }
+}
+
 // Backward work items.  A tile with n isects becomes ceil(n / L) items
 // (tile, k): the full-length chunks go to `full`, the shorter tails to `tail`
 // (the backward runs all full chunks first, so the longest items start
@@ -846,10 +909,20 @@ static int chunk_len() {
 
 static int64_t state_floats_per_slot(int D) { return (int64_t)r16::kTS * r16::kTS * (1 + D); }
 
-int64_t rasterize16_fwd_state_bytes(int D, int64_t n_isects) {
+// [chunk slots (L > 0)][tile order: n_tiles i32 (n_tiles <= 16384)]
+static int64_t chunk_slot_bytes(int D, int64_t n_isects) {
   const int L = chunk_len();
   if (L == 0 || n_isects <= 0) return 0;
   return (n_isects / L + 1) * state_floats_per_slot(D) * (int64_t)sizeof(float);
+}
+
+static bool use_order(int n_tiles, int64_t n_isects) {
+  return n_isects > 0 && n_tiles > 0 && n_tiles <= 16384;
+}
+
+int64_t rasterize16_fwd_state_bytes(int D, int n_tiles, int64_t n_isects) {
+  const int64_t ob = use_order(n_tiles, n_isects) ? 4 * (int64_t)n_tiles : 0;
+  return chunk_slot_bytes(D, n_isects) + ob;
 }
 
 static int64_t n_items_bound(int n_tiles, int64_t n_isects) {
@@ -863,6 +936,9 @@ static int dbg_flags() {
 }
 template <int D>
 int r16_fwd(r16::Args a, hipStream_t st) {
+  if (a.order)
+    hipLaunchKernelGGL(r16::tile_order_kernel, dim3(1), dim3(1024), 0, st, a.n_tiles, a.offsets,
+                       a.n_isects, const_cast<int32_t *>(a.order));
   hipLaunchKernelGGL((r16::fwd_kernel<D>), dim3(a.n_tiles), dim3(256), 0, st, a);
   GS_CHECK_LAUNCH("rasterize_fwd16");
   return 0;
@@ -923,12 +999,15 @@ int rasterize16_fwd(int C, int D, int W, int H, int tw, int th, const float *mea
   a.means2d = means2d; a.conics = conics; a.colors = colors; a.opacities = opacities;
   a.backgrounds = backgrounds; a.masks = masks; a.offsets = offsets; a.flatten_ids = flatten_ids;
   a.render_colors = render_colors; a.render_alphas = render_alphas; a.last_ids = last_ids;
-  const int64_t need = rasterize16_fwd_state_bytes(D, n_isects);
+  const int64_t need = rasterize16_fwd_state_bytes(D, a.n_tiles, n_isects);
   GS_REQUIRE(state_bytes == 0 || state_bytes >= need,
              "rasterize_fwd: state of %lld bytes needed, %lld given", (long long)need,
              (long long)state_bytes);
   a.L = chunk_len();
-  a.state = (state && need > 0) ? reinterpret_cast<float *>(state) : nullptr;
+  const int64_t slots = chunk_slot_bytes(D, n_isects);
+  a.state = (state && slots > 0) ? reinterpret_cast<float *>(state) : nullptr;
+  a.order = (state && use_order(a.n_tiles, n_isects))
+                ? reinterpret_cast<int32_t *>(reinterpret_cast<char *>(state) + slots) : nullptr;
   switch (D) {
     case 1: return r16_fwd<1>(a, st);
     case 2: return r16_fwd<2>(a, st);
@@ -966,9 +1045,9 @@ int rasterize16_bwd(int C, int64_t G, int D, int W, int H, int tw, int th,
   a.render_alphas = const_cast<float *>(render_alphas);
   a.last_ids = const_cast<int32_t *>(last_ids);
   a.v_render_colors = v_render_colors; a.v_render_alphas = v_render_alphas;
-  const int64_t need = rasterize16_fwd_state_bytes(D, n_isects);
+  const int64_t need = rasterize16_fwd_state_bytes(D, a.n_tiles, n_isects);
   a.L = chunk_len();
-  a.state = (state && need > 0 && state_bytes >= need)
+  a.state = (state && chunk_slot_bytes(D, n_isects) > 0 && state_bytes >= need)
                 ? const_cast<float *>(reinterpret_cast<const float *>(state)) : nullptr;
   a.render_colors_in = render_colors;
   a.dbg = dbg_flags();

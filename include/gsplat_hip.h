@@ -176,7 +176,8 @@ int gsplat_hip_isect_offsets(int64_t n_isects, const int64_t *isect_ids, int C, 
  *    and, when `state` is non-NULL, the per-pixel compositing state at every
  *    chunk boundary of a long tile (gsplat_hip_rasterize_fwd_state_bytes bytes;
  *    0 bytes = no state) that lets the backward split long tiles into chunks
- *    that run in parallel.  Keep it for the matching gsplat_hip_rasterize_bwd. */
+ *    that run in parallel, plus the forward's heaviest-tiles-first dispatch
+ *    order.  Keep it for the matching gsplat_hip_rasterize_bwd. */
 int gsplat_hip_rasterize_supported_channels(int D);
 int64_t gsplat_hip_rasterize_fwd_state_bytes(int C, int D, int tile_size, int tile_width,
                                              int tile_height, int64_t n_isects);
