@@ -102,9 +102,14 @@ isect_count_kernel(int64_t G, const float *__restrict__ means2d, const int32_t *
   }
 }
 
-// Exclusive scan of the per-block sums in place; total -> block_sums[nb].
-// One 1024-lane workgroup walks the (at most a few thousand) block sums.
-__global__ void __launch_bounds__(1024) isect_scan_blocks_kernel(int64_t nb, int64_t *block_sums) {
+// Exclusive scan of the per-block sums in place; total -> block_sums[nb] (and
+// -> totals[blockIdx.x] when totals is non-null).  One 1024-lane workgroup per
+// array walks its (at most a few thousand) block sums: workgroup 0 scans
+// `first`, workgroup 1 (if launched) `second`.
+__global__ void __launch_bounds__(1024) isect_scan_blocks_kernel(int64_t nb, int64_t *first,
+                                                                 int64_t *second,
+                                                                 int64_t *totals) {
+  int64_t *block_sums = blockIdx.x == 0 ? first : second;
   __shared__ int64_t wave_tot[16];
   __shared__ int64_t chunk_tot;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -134,7 +139,10 @@ __global__ void __launch_bounds__(1024) isect_scan_blocks_kernel(int64_t nb, int
     carry += chunk_tot;
     __syncthreads();
   }
-  if (threadIdx.x == 0) block_sums[nb] = carry;
+  if (threadIdx.x == 0) {
+    block_sums[nb] = carry;
+    if (totals) totals[blockIdx.x] = carry;
+  }
 }
 
 __global__ void __launch_bounds__(kIsectBlock)
@@ -194,13 +202,6 @@ isect_offsets_kernel(int64_t n, const int64_t *__restrict__ isect_ids, int n_til
     for (int64_t t = cur + 1; t < n_tiles_total; ++t) offsets[t] = (int32_t)n;
 }
 
-__global__ void isect_totals_kernel(const int64_t *n_isects, const int64_t *n_vis,
-                                    int64_t *totals) {
-  if (threadIdx.x == 0) {
-    totals[0] = *n_isects;
-    totals[1] = *n_vis;
-  }
-}
 
 // ---------------------------------------------------------------------------
 // Depth-first sorted emission (sort=True).  The reference's stable sort of
@@ -242,7 +243,13 @@ isect_sorted_count_kernel(int64_t nV, const int32_t *__restrict__ Vs,
   if (threadIdx.x == 0) block_sums[blockIdx.x] = tot;
 }
 
-// (2b) emit (cam|tile key, Gaussian index) in depth order
+// (2b) emit (cam|tile key, Gaussian index) in depth order.  A Gaussian with
+// at most kLaneTiles tiles is written by its own lane; a larger one by its
+// whole wave (lanes stride over its tiles, coalesced stores), so the few
+// huge near-camera Gaussians do not serialise one lane for thousands of
+// tiles.
+constexpr int kLaneTiles = 32;
+
 __global__ void __launch_bounds__(kIsectBlock)
 isect_sorted_emit_kernel(int64_t nV, int N, const int32_t *__restrict__ Vs,
                          const float *__restrict__ means2d, const int32_t *__restrict__ radii,
@@ -252,6 +259,7 @@ isect_sorted_emit_kernel(int64_t nV, int N, const int32_t *__restrict__ Vs,
                          int32_t *__restrict__ val) {
   __shared__ int64_t lds[kIsectBlock / 64 + 1];
   const int64_t s = (int64_t)blockIdx.x * kIsectBlock + threadIdx.x;
+  const int lane = threadIdx.x & 63;
   Rect rc{0, 0, 0, 0};
   int32_t i = 0;
   int cnt = 0;
@@ -261,16 +269,34 @@ isect_sorted_emit_kernel(int64_t nV, int N, const int32_t *__restrict__ Vs,
   }
   int64_t tot;
   const int64_t local = block_exclusive_scan<int64_t>((int64_t)cnt, lds, &tot);
-  if (cnt == 0) return;
-  int64_t cur = block_prefix[blockIdx.x] + local;
-  const uint32_t cam = camera_ids ? (uint32_t)camera_ids[i] : (uint32_t)(i / N);
-  const bool neg = __float_as_int(depths[i]) < 0;
-  const uint32_t hi = cam << tile_bits;
-  for (int y = rc.y0; y < rc.y1; ++y) {
-    for (int x = rc.x0; x < rc.x1; ++x) {
-      tkey[cur] = neg ? key_all_ones : (hi | (uint32_t)(y * tw + x));
-      val[cur] = i;
-      ++cur;
+  const int64_t cur0 = block_prefix[blockIdx.x] + local;
+  uint32_t hi = key_all_ones;  // all ones: negative depth (every tile gets the all-ones key)
+  if (cnt > 0 && __float_as_int(depths[i]) >= 0)
+    hi = (camera_ids ? (uint32_t)camera_ids[i] : (uint32_t)(i / N)) << tile_bits;
+  if (cnt > 0 && cnt <= kLaneTiles) {
+    int64_t cur = cur0;
+    for (int y = rc.y0; y < rc.y1; ++y)
+      for (int x = rc.x0; x < rc.x1; ++x) {
+        tkey[cur] = hi == key_all_ones ? key_all_ones : (hi | (uint32_t)(y * tw + x));
+        val[cur] = i;
+        ++cur;
+      }
+  }
+  uint64_t big = __ballot(cnt > kLaneTiles);
+  while (big) {
+    const int src = __builtin_ctzll(big);
+    big &= big - 1;
+    const int64_t c0 = __shfl(cur0, src, 64);
+    const int n = __shfl(cnt, src, 64);
+    const int gx0 = __shfl(rc.x0, src, 64), gy0 = __shfl(rc.y0, src, 64);
+    const uint32_t w = (uint32_t)(__shfl(rc.x1, src, 64) - gx0);
+    const uint32_t ghi = __shfl(hi, src, 64);
+    const int32_t gi = __shfl(i, src, 64);
+    for (int k = lane; k < n; k += 64) {
+      const uint32_t yy = (uint32_t)k / w, xx = (uint32_t)k - yy * w;
+      const uint32_t tile = (uint32_t)((gy0 + (int)yy) * tw + gx0 + (int)xx);
+      tkey[c0 + k] = ghi == key_all_ones ? key_all_ones : (ghi | tile);
+      val[c0 + k] = gi;
     }
   }
 }
@@ -315,9 +341,8 @@ extern "C" int gsplat_hip_isect_count(int64_t n_gaussians, const float *means2d,
   hipLaunchKernelGGL(isect_count_kernel, dim3((unsigned)nb), dim3(kIsectBlock), 0, st,
                      n_gaussians, means2d, radii, tile_size, tile_width, tile_height,
                      tiles_per_gauss, ws, vis);
-  hipLaunchKernelGGL(isect_scan_blocks_kernel, dim3(1), dim3(1024), 0, st, nb, ws);
-  hipLaunchKernelGGL(isect_scan_blocks_kernel, dim3(1), dim3(1024), 0, st, nb, vis);
-  hipLaunchKernelGGL(isect_totals_kernel, dim3(1), dim3(64), 0, st, ws + nb, vis + nb,
+  // both scans in one launch; their totals are (n_isects, n_visible)
+  hipLaunchKernelGGL(isect_scan_blocks_kernel, dim3(2), dim3(1024), 0, st, nb, ws, vis,
                      totals_device);
   GS_CHECK_LAUNCH("isect_count");
   return 0;
@@ -429,6 +454,7 @@ extern "C" int gsplat_hip_isect_write_sorted(
   GS_REQUIRE(n_gaussians >= 0 && (camera_ids || N > 0 || n_gaussians == 0),
              "isect_write_sorted: N must be > 0 when camera_ids is null");
   GS_REQUIRE(tile_bits + cam_bits <= 32, "isect_write_sorted: tile_bits + cam_bits > 32");
+  GS_REQUIRE(n_isects < ((int64_t)1 << 30), "isect_write_sorted: more than 2^30 isects");
   if (n_isects <= 0 || n_visible <= 0) return 0;
   const int key_bits = tile_bits + cam_bits;
   const SortedLayout L = sorted_layout(n_visible, n_isects, key_bits);
@@ -454,17 +480,21 @@ extern "C" int gsplat_hip_isect_write_sorted(
   const int64_t nbV = (n_visible + kIsectBlock - 1) / kIsectBlock;
   hipLaunchKernelGGL(isect_sorted_count_kernel, dim3((unsigned)nbV), dim3(kIsectBlock), 0, st,
                      n_visible, Vs, tiles_per_gauss, blk);
-  hipLaunchKernelGGL(isect_scan_blocks_kernel, dim3(1), dim3(1024), 0, st, nbV, blk);
+  hipLaunchKernelGGL(isect_scan_blocks_kernel, dim3(1), dim3(1024), 0, st, nbV, blk, nullptr,
+                     nullptr);
   const uint32_t all_ones = key_bits >= 32 ? 0xffffffffu : ((1u << key_bits) - 1u);
   hipLaunchKernelGGL(isect_sorted_emit_kernel, dim3((unsigned)nbV), dim3(kIsectBlock), 0, st,
                      n_visible, N, Vs, means2d, radii, depths, camera_ids, tile_size, tile_width,
                      tile_height, tile_bits, all_ones, blk, tkey, val);
-  // stable (camera, tile) sort keeps the depth order inside every tile
-  const bool in_alt = lsd_sort_pairs(tkey, val, tkeys, vals, n_isects, 0, key_bits, tmp, st) == 1;
-  const uint32_t *fk = in_alt ? tkeys : tkey;
-  const int32_t *fv = in_alt ? vals : val;
-  hipLaunchKernelGGL(isect_sorted_finalize_kernel, dim3((unsigned)((n_isects + 255) / 256)),
-                     dim3(256), 0, st, n_isects, fk, fv, depths, isect_ids, flatten_ids);
+  // stable (camera, tile) sort keeps the depth order inside every tile; its
+  // last pass writes isect_ids / flatten_ids directly
+  if (key_bits > 0) {
+    const lsd::FinalOut fo{depths, isect_ids, flatten_ids};
+    lsd_sort_pairs(tkey, val, tkeys, vals, n_isects, 0, key_bits, tmp, st, &fo);
+  } else {
+    hipLaunchKernelGGL(isect_sorted_finalize_kernel, dim3((unsigned)((n_isects + 255) / 256)),
+                       dim3(256), 0, st, n_isects, tkey, val, depths, isect_ids, flatten_ids);
+  }
   GS_CHECK_LAUNCH("isect_write_sorted");
   return 0;
 }
@@ -721,7 +751,7 @@ extern "C" int gsplat_hip_isect_write_tilefirst(
   GS_REQUIRE(n_gaussians >= 0 && (camera_ids || N > 0 || n_gaussians == 0),
              "isect_write_tilefirst: N must be > 0 when camera_ids is null");
   GS_REQUIRE(tile_bits + cam_bits <= 32, "isect_write_tilefirst: tile_bits + cam_bits > 32");
-  GS_REQUIRE(n_isects < (int64_t)1 << 31, "isect_write_tilefirst: more than 2^31 isects");
+  GS_REQUIRE(n_isects < (int64_t)1 << 30, "isect_write_tilefirst: more than 2^30 isects");
   if (n_isects <= 0) return 0;
   const int key_bits = tile_bits + cam_bits;
   const int n_tiles = tile_width * tile_height;

@@ -9,6 +9,10 @@
 //   lsd_scatter  per tile: digit bases (scan of totals + hist[d][tile]),
 //                stable in-tile ranks by wave ballots, reorder through LDS,
 //                digit-contiguous (coalesced) stores
+// The last pass can write the caller's final isect output directly (FinalOut).
+// (A single-launch onesweep pass with decoupled look-back was tried: with all
+// ~1000 tiles of a 4 M-item pass co-resident, the look-back chains cost more
+// than the two small launches it saves.)
 // The in-tile sort is stable and the tiles are laid out in input order, so the
 // pass is stable and the whole sort equals a stable sort on bits
 // [begin_bit, end_bit).  Traffic per pass: 4 B/item (hist) + 16 B/item
@@ -26,6 +30,16 @@ inline int64_t n_tiles(int64_t n, int ipt) { return (n + (int64_t)NT * ipt - 1) 
 
 // Few items: small tiles so the grid still covers the chip.
 inline int pick_ipt(int64_t n) { return n <= ((int64_t)1 << 20) ? 4 : 16; }
+
+// Last-pass output of the isect sorts: instead of (key, value) write
+// isect_ids[dst] = key << 32 | depth bits of depths[value] (the reference's
+// sign-extended int64 id when the depth bits are negative) and
+// flatten_ids[dst] = value.
+struct FinalOut {
+  const float *depths;
+  int64_t *isect_ids;
+  int32_t *flatten_ids;
+};
 
 template <int IPT>
 __global__ void __launch_bounds__(NT)
@@ -82,12 +96,12 @@ scan_kernel(uint32_t *__restrict__ hist, int64_t nt, uint32_t *__restrict__ tota
 // number of such lanes below.  Cross-wave offsets and the tile's digit starts
 // come from the 4 x 256 wave counts; items are then reordered through LDS so
 // the global stores are digit-contiguous.
-template <int IPT>
+template <int IPT, bool FINAL>
 __global__ void __launch_bounds__(NT)
 scatter_kernel(const uint32_t *__restrict__ kin, const int32_t *__restrict__ vin,
                uint32_t *__restrict__ kout, int32_t *__restrict__ vout, int64_t n, int shift,
                int nbits, const uint32_t *__restrict__ hist, const uint32_t *__restrict__ totals,
-               int64_t nt) {
+               int64_t nt, FinalOut fo) {
   constexpr int NW = NT / 64, TILE = NT * IPT;
   __shared__ uint32_t cnt[NW][RADIX];
   __shared__ uint32_t gbase[RADIX];  // global position of tile slot 0 of digit d's range
@@ -181,9 +195,16 @@ scatter_kernel(const uint32_t *__restrict__ kin, const int32_t *__restrict__ vin
     const int s = e * NT + t;
     if (s < nvalid) {
       const uint32_t k = kbuf[s];
+      const int32_t v = vbuf[s];
       const uint32_t dst = gbase[(k >> shift) & mask] + (uint32_t)s;
-      kout[dst] = k;
-      vout[dst] = vbuf[s];
+      if (FINAL) {
+        const int32_t db = __float_as_int(fo.depths[v]);
+        fo.isect_ids[dst] = db < 0 ? (int64_t)db : (((int64_t)k << 32) | (int64_t)(uint32_t)db);
+        fo.flatten_ids[dst] = v;
+      } else {
+        kout[dst] = k;
+        vout[dst] = v;
+      }
     }
   }
 }
@@ -198,9 +219,12 @@ inline size_t lsd_sort_scratch_bytes(int64_t n) {
 
 // Stable sort of n pairs by key bits [begin_bit, end_bit), ping-ponging
 // between (k0, v0) and (k1, v1).  Returns 0 if the result is in (k0, v0),
-// 1 if in (k1, v1).  n < 2^32.
+// 1 if in (k1, v1).  With `fo` non-null the last pass writes the final isect
+// output instead (see FinalOut; the return value is then meaningless).
+// n < 2^32.
 inline int lsd_sort_pairs(uint32_t *k0, int32_t *v0, uint32_t *k1, int32_t *v1, int64_t n,
-                          int begin_bit, int end_bit, void *scratch, hipStream_t st) {
+                          int begin_bit, int end_bit, void *scratch, hipStream_t st,
+                          const lsd::FinalOut *fo = nullptr) {
   if (n <= 0 || end_bit <= begin_bit) return 0;
   const int ipt = lsd::pick_ipt(n);
   const int64_t nt = lsd::n_tiles(n, ipt);
@@ -219,12 +243,17 @@ inline int lsd_sort_pairs(uint32_t *k0, int32_t *v0, uint32_t *k1, int32_t *v1, 
       hipLaunchKernelGGL(lsd::hist_kernel<16>, dim3((unsigned)nt), dim3(lsd::NT), 0, st, ki, n,
                          shift, mask, hist, nt);
     hipLaunchKernelGGL(lsd::scan_kernel, dim3(lsd::RADIX), dim3(lsd::NT), 0, st, hist, nt, totals);
-    if (ipt == 4)
-      hipLaunchKernelGGL(lsd::scatter_kernel<4>, dim3((unsigned)nt), dim3(lsd::NT), 0, st, ki, vi,
-                         ko, vo, n, shift, nbits, hist, totals, nt);
-    else
-      hipLaunchKernelGGL(lsd::scatter_kernel<16>, dim3((unsigned)nt), dim3(lsd::NT), 0, st, ki, vi,
-                         ko, vo, n, shift, nbits, hist, totals, nt);
+    const bool fin = fo && shift + 8 >= end_bit;
+    const lsd::FinalOut f = fin ? *fo : lsd::FinalOut{nullptr, nullptr, nullptr};
+#define GS_LSD_SCATTER(I, F)                                                                  \
+  hipLaunchKernelGGL((lsd::scatter_kernel<I, F>), dim3((unsigned)nt), dim3(lsd::NT), 0, st, ki, \
+                     vi, ko, vo, n, shift, nbits, hist, totals, nt, f)
+    if (ipt == 4) {
+      if (fin) GS_LSD_SCATTER(4, true); else GS_LSD_SCATTER(4, false);
+    } else {
+      if (fin) GS_LSD_SCATTER(16, true); else GS_LSD_SCATTER(16, false);
+    }
+#undef GS_LSD_SCATTER
     cur ^= 1;
   }
   return cur;
