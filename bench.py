@@ -47,7 +47,55 @@ def parse():
     ap.add_argument("--config", default="m2", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-tile-stride", type=int, default=24)
+    ap.add_argument("--no-traffic", action="store_true",
+                    help="skip the rocprofv3 PMC child runs that measure roofline.traffic")
+    ap.add_argument("--probe", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
+
+
+def pmc_traffic(config: str):
+    """HBM bytes of one rasterize-forward launch from rocprofv3 counters.
+
+    Two child runs of `bench.py --probe` under rocprofv3 (separate --pmc
+    passes: FETCH_SIZE and WRITE_SIZE cannot share one), started before this
+    process touches the GPU.  Corrections per MI355X_MICROARCH.md "HBM":
+    FETCH_SIZE is in KiB and counts half the bytes on gfx950 (x2);
+    WRITE_SIZE is in KiB.  Returns None when rocprofv3 is unavailable."""
+    import csv
+    import glob
+    import shutil
+    import subprocess
+    import tempfile
+    rp = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(rp):
+        return None
+    env = dict(os.environ, TMPDIR="/tmp")
+    per = {}
+    for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+        d = tempfile.mkdtemp(prefix="gsplat_pmc_", dir="/tmp")
+        cmd = [rp, "--kernel-include-regex", "r16::fwd_kernel", "--pmc", ctr, "-f", "csv",
+               "-d", d, "-o", "p", "--", sys.executable, os.path.abspath(__file__), "--probe",
+               "--config", config, "--warmup", "2"]
+        try:
+            subprocess.run(cmd, env=env, cwd="/tmp", timeout=300, check=True,
+                           stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+        except (subprocess.SubprocessError, OSError):
+            return None
+        vals = {}
+        for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+            for r in csv.DictReader(open(f)):
+                if r["Counter_Name"] == ctr:
+                    vals[r["Dispatch_Id"]] = vals.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
+        shutil.rmtree(d, ignore_errors=True)
+        if not vals:
+            return None
+        per[ctr] = float(np.mean(list(vals.values())))
+    fetch = 2.0 * per["FETCH_SIZE"] * 1024.0
+    write = per["WRITE_SIZE"] * 1024.0
+    return {"bytes_per_launch": fetch + write, "fetch_bytes": fetch, "write_bytes": write,
+            "fetch_size_kib": per["FETCH_SIZE"], "write_size_kib": per["WRITE_SIZE"],
+            "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py --probe "
+                      "(FETCH_SIZE x2 per MI355X_MICROARCH.md; gathers uncalibrated)"}
 
 
 def max_over_ranks(elapsed: float, world: int, device) -> float:
@@ -67,6 +115,9 @@ def main():
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    traffic = None
+    if rank == 0 and world == 1 and not args.no_traffic and not args.probe:
+        traffic = pmc_traffic(args.config)  # child processes, before this one uses the GPU
     dev = f"cuda:{local}"
     torch.cuda.set_device(dev)
 
@@ -85,6 +136,11 @@ def main():
     for it in range(args.warmup):
         tr.step(it)
     torch.cuda.synchronize()
+    if args.probe:  # PMC child run: a few steps, no output
+        for it in range(args.warmup, args.warmup + 2):
+            tr.step(it)
+        torch.cuda.synchronize()
+        return
 
     timers = _wrapper.enable_kernel_timers(True)
     if world > 1:
@@ -157,7 +213,9 @@ def main():
                    "loss": "0.8*L1+0.2*(1-SSIM valid)", "optimizer": "Adam (6 groups)"},
         "roofline": {"kernel": "rasterize_fwd", "bound": "hbm", "achieved": achieved,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                     "traffic": None, "algorithmic_bytes_per_launch": bytes_per_launch,
+                     "traffic": None if traffic is None else traffic["bytes_per_launch"],
+                     "traffic_detail": traffic,
+                     "algorithmic_bytes_per_launch": bytes_per_launch,
                      "launch_ms": fwd_ms, "rasterize_bwd_ms": bwd_ms},
     }
 

@@ -301,6 +301,8 @@ int rasterize16_fwd(int C, int D, int W, int H, int tw, int th, const float *mea
                     float *render_alphas, int32_t *last_ids, void *state, int64_t state_bytes,
                     hipStream_t st);
 int64_t rasterize16_fwd_state_bytes(int D, int n_tiles, int64_t n_isects);
+int rasterize16_prepare(int D, int n_tiles, const int32_t *offsets, int64_t n_isects,
+                        void *state, int64_t state_bytes, hipStream_t st);
 int64_t rasterize16_bwd_workspace(int64_t G, int D, bool absgrad, int n_tiles, int64_t n_isects);
 int rasterize16_bwd(int C, int64_t G, int D, int W, int H, int tw, int th,
                     const float *means2d, const float *conics, const float *colors,
@@ -324,6 +326,15 @@ extern "C" int64_t gsplat_hip_rasterize_fwd_state_bytes(int C, int D, int tile_s
                                                         int64_t n_isects) {
   if (tile_size != 16 || !supported_channels(D)) return 0;
   return rasterize16_fwd_state_bytes(D, C * tile_width * tile_height, n_isects);
+}
+
+extern "C" int gsplat_hip_rasterize_prepare(int C, int D, int tile_size, int tile_width,
+                                           int tile_height, const int32_t *isect_offsets,
+                                           int64_t n_isects, void *state, int64_t state_bytes,
+                                           void *stream) {
+  if (tile_size != 16 || !supported_channels(D)) return 0;
+  return rasterize16_prepare(D, C * tile_width * tile_height, isect_offsets, n_isects, state,
+                             state_bytes, (hipStream_t)stream);
 }
 
 extern "C" int64_t gsplat_hip_rasterize_bwd_workspace_bytes(int64_t n_gaussians, int D,

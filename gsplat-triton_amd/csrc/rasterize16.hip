@@ -934,11 +934,17 @@ static int dbg_flags() {
   static const int v = [] { const char *e = getenv("GSPLAT_HIP_DBG"); return e ? atoi(e) : 0; }();
   return v;
 }
+// State whose tile order gsplat_hip_rasterize_prepare already queued (so the
+// forward call does not launch the order kernel again); cleared by the
+// forward that consumes it.  Same host thread, same stream.
+static thread_local const void *g_prepared_state = nullptr;
+
 template <int D>
-int r16_fwd(r16::Args a, hipStream_t st) {
-  if (a.order)
+int r16_fwd(r16::Args a, const void *state, hipStream_t st) {
+  if (a.order && state != g_prepared_state)
     hipLaunchKernelGGL(r16::tile_order_kernel, dim3(1), dim3(1024), 0, st, a.n_tiles, a.offsets,
                        a.n_isects, const_cast<int32_t *>(a.order));
+  g_prepared_state = nullptr;
   hipLaunchKernelGGL((r16::fwd_kernel<D>), dim3(a.n_tiles), dim3(256), 0, st, a);
   GS_CHECK_LAUNCH("rasterize_fwd16");
   return 0;
@@ -1009,15 +1015,30 @@ int rasterize16_fwd(int C, int D, int W, int H, int tw, int th, const float *mea
   a.order = (state && use_order(a.n_tiles, n_isects))
                 ? reinterpret_cast<int32_t *>(reinterpret_cast<char *>(state) + slots) : nullptr;
   switch (D) {
-    case 1: return r16_fwd<1>(a, st);
-    case 2: return r16_fwd<2>(a, st);
-    case 3: return r16_fwd<3>(a, st);
-    case 4: return r16_fwd<4>(a, st);
-    case 8: return r16_fwd<8>(a, st);
-    case 16: return r16_fwd<16>(a, st);
-    case 32: return r16_fwd<32>(a, st);
+    case 1: return r16_fwd<1>(a, state, st);
+    case 2: return r16_fwd<2>(a, state, st);
+    case 3: return r16_fwd<3>(a, state, st);
+    case 4: return r16_fwd<4>(a, state, st);
+    case 8: return r16_fwd<8>(a, state, st);
+    case 16: return r16_fwd<16>(a, state, st);
+    case 32: return r16_fwd<32>(a, state, st);
   }
   GS_REQUIRE(false, "rasterize16_fwd: unsupported channels %d", D);
+}
+
+int rasterize16_prepare(int D, int n_tiles, const int32_t *offsets, int64_t n_isects,
+                        void *state, int64_t state_bytes, hipStream_t st) {
+  g_prepared_state = nullptr;
+  if (!state || !use_order(n_tiles, n_isects)) return 0;
+  GS_REQUIRE(state_bytes >= rasterize16_fwd_state_bytes(D, n_tiles, n_isects),
+             "rasterize_prepare: state too small");
+  int32_t *order = reinterpret_cast<int32_t *>(reinterpret_cast<char *>(state) +
+                                               chunk_slot_bytes(D, n_isects));
+  hipLaunchKernelGGL(r16::tile_order_kernel, dim3(1), dim3(1024), 0, st, n_tiles, offsets,
+                     n_isects, order);
+  GS_CHECK_LAUNCH("rasterize_prepare");
+  g_prepared_state = state;
+  return 0;
 }
 
 int64_t rasterize16_bwd_workspace(int64_t G, int D, bool absgrad, int n_tiles, int64_t n_isects) {

@@ -527,6 +527,9 @@ class _RasterizeToPixels(torch.autograd.Function):
         sb = int(_lib.query("gsplat_hip_rasterize_fwd_state_bytes", C, D, tile_size, tw, th,
                             flatten_ids.numel()))
         state = torch.empty(sb // 4, dtype=torch.float32, device=dev)
+        if sb:  # dispatch order into the state, outside the timed rasterizer launch
+            _lib.call("gsplat_hip_rasterize_prepare", C, D, tile_size, tw, th, _ptr(isect_offsets),
+                      flatten_ids.numel(), _ptr(state), sb, _stream())
         with _Timed("rasterize_fwd"):
             _lib.call("gsplat_hip_rasterize_fwd", C, D, width, height, tile_size, tw, th,
                       _ptr(means2d), _ptr(conics), _ptr(colors), _ptr(opacities),

@@ -179,6 +179,14 @@ int gsplat_hip_isect_offsets(int64_t n_isects, const int64_t *isect_ids, int C, 
  *    that run in parallel, plus the forward's heaviest-tiles-first dispatch
  *    order.  Keep it for the matching gsplat_hip_rasterize_bwd. */
 int gsplat_hip_rasterize_supported_channels(int D);
+/* Optional: queue the forward's per-launch preparation (its dispatch order,
+ * kept in `state`) ahead of gsplat_hip_rasterize_fwd on the same stream and
+ * host thread, so the forward call launches the rasterizer kernel alone
+ * (lets a caller time that kernel by itself).  Without it the forward does
+ * the preparation itself. */
+int gsplat_hip_rasterize_prepare(int C, int D, int tile_size, int tile_width, int tile_height,
+                                 const int32_t *isect_offsets, int64_t n_isects, void *state,
+                                 int64_t state_bytes, void *stream);
 int64_t gsplat_hip_rasterize_fwd_state_bytes(int C, int D, int tile_size, int tile_width,
                                              int tile_height, int64_t n_isects);
 int gsplat_hip_rasterize_fwd(int C, int D, int width, int height, int tile_size, int tile_width,
