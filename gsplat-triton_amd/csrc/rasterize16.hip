@@ -1010,6 +1010,7 @@ int rasterize16_fwd(int C, int D, int W, int H, int tw, int th, const float *mea
              "rasterize_fwd: state of %lld bytes needed, %lld given", (long long)need,
              (long long)state_bytes);
   a.L = chunk_len();
+  a.dbg = dbg_flags();
   const int64_t slots = chunk_slot_bytes(D, n_isects);
   a.state = (state && slots > 0) ? reinterpret_cast<float *>(state) : nullptr;
   a.order = (state && use_order(a.n_tiles, n_isects))
