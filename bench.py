@@ -69,6 +69,9 @@ def pmc_traffic(config: str):
     rp = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
     if not os.path.exists(rp):
         return None
+    if any("rocprof" in v.lower() for k, v in os.environ.items() if k in ("LD_PRELOAD", "HSA_TOOLS_LIB")) \
+            or any(k.startswith("ROCPROF") for k in os.environ):
+        return None  # already running under a profiler: no nested profiler runs
     env = dict(os.environ, TMPDIR="/tmp")
     per = {}
     for ctr in ("FETCH_SIZE", "WRITE_SIZE"):

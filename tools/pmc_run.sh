@@ -4,7 +4,7 @@ set -o pipefail
 export TMPDIR=/tmp
 OUT=$GRAFT_REPO_ROOT/gpurun_out/pmc7
 mkdir -p $OUT
-B="python bench.py --steps 3 --warmup 2 --no-cpu-baseline"
+B="/usr/bin/python3 bench.py --steps 3 --warmup 2 --no-cpu-baseline --no-traffic"
 R='r16|adam|sh_bwd|ssim'
 timeout -k 10 120 rocprofv3 -L > $OUT/counters.txt 2>&1 || true
 timeout -k 10 300 rocprofv3 --kernel-include-regex "$R" --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY -f csv -d $OUT/p1 -o p -- $B > $OUT/p1.log 2>&1 || exit 1

@@ -8,6 +8,6 @@ export TMPDIR=/tmp
 TAG=${1:-prof}
 OUT=$GRAFT_REPO_ROOT/gpurun_out/$TAG
 mkdir -p $OUT
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $OUT/trace -o run -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-traffic > $OUT/trace.log 2>&1 || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $OUT/trace -o run -- /usr/bin/python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-traffic > $OUT/trace.log 2>&1 || exit 1
 timeout -k 10 600 python bench.py > $OUT/bench.json 2> $OUT/bench.err || exit 2
 exit 0
