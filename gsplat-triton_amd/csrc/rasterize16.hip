@@ -27,6 +27,7 @@
 
 namespace gs {
 static uint64_t *g_timeline = nullptr;
+static unsigned long long *g_lanehist = nullptr;  // debug: [65] active-lane counts (backward)
 static int64_t g_timeline_waves = 0;
 
 namespace r16 {
@@ -41,6 +42,7 @@ GS_INLINE float dpp(float v) {
   return __builtin_bit_cast(
       float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xf, 0xf, false));
 }
+
 
 GS_INLINE float swap32_sum(float a, float b) {
   auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
@@ -87,6 +89,28 @@ GS_INLINE float reduce_scatter(const float *v, int lane) {
 
 typedef float f2v __attribute__((ext_vector_type(2)));
 
+// keep + (give permuted by DPP), for both components of a pair, as two
+// v_add_f32_dpp.  (The compiler packs such adds into v_pk_add_f32, which
+// takes no DPP operand, and then needs a v_mov_b32_dpp plus a zeroed old
+// value per component.)  s_nop 1: the VALU-write -> DPP-read hazard of gfx9
+// needs two wait states, which the compiler does not insert for inline asm;
+// one nop covers both adds.
+#define GS_ADD_DPP2(NAME, MOD)                                                             \
+  GS_INLINE f2v NAME(f2v keep, f2v give) {                                                \
+    float rx, ry;                                                                          \
+    asm("s_nop 1\n\t"                                                                      \
+        "v_add_f32_dpp %0, %2, %3 " MOD " row_mask:0xf bank_mask:0xf\n\t"                  \
+        "v_add_f32_dpp %1, %4, %5 " MOD " row_mask:0xf bank_mask:0xf"                       \
+        : "=&v"(rx), "=v"(ry)                                                              \
+        : "v"(give.x), "v"(keep.x), "v"(give.y), "v"(keep.y));                             \
+    return f2v{rx, ry};                                                                    \
+  }
+GS_ADD_DPP2(add_row_mirror2, "row_mirror")
+GS_ADD_DPP2(add_row_half_mirror2, "row_half_mirror")
+GS_ADD_DPP2(add_quad_10322, "quad_perm:[1,0,3,2]")
+GS_ADD_DPP2(add_quad_23012, "quad_perm:[2,3,0,1]")
+#undef GS_ADD_DPP2
+
 GS_INLINE f2v swap32_sum2(f2v a, f2v b) {
   return f2v{swap32_sum(a.x, b.x), swap32_sum(a.y, b.y)};
 }
@@ -115,15 +139,18 @@ GS_INLINE f2v reduce_scatter2(const f2v *v, int lane) {
 #pragma unroll
   for (int i = 0; i < N2; ++i) x[i] = swap16_sum2(w[2 * i], pick2(w, 2 * i + 1));
   const bool b3 = lane & 8, b2 = lane & 4;
+  // DPP steps per component, one v_add_f32_dpp per value and step
 #pragma unroll
   for (int i = 0; i < N3; ++i) {
     const f2v lo = x[2 * i], hi = pick2(x, 2 * i + 1);
-    y[i] = (b3 ? hi : lo) + dpp2<0x140>(b3 ? lo : hi);
+    const f2v keep = b3 ? hi : lo, give = b3 ? lo : hi;
+    y[i] = add_row_mirror2(keep, give);
   }
   const f2v lo = y[0], hi = pick2(y, 1);
-  f2v z = (b2 ? hi : lo) + dpp2<0x141>(b2 ? lo : hi);
-  z += dpp2<0xB1>(z);
-  z += dpp2<0x4E>(z);
+  const f2v keep = b2 ? hi : lo, give = b2 ? lo : hi;
+  f2v z = add_row_half_mirror2(keep, give);
+  z = add_quad_10322(z, z);
+  z = add_quad_23012(z, z);
   return z;
 }
 
@@ -156,6 +183,7 @@ struct Args {
   const float *render_colors_in;  // backward: forward colours (for suffix sums)
   int dbg;  // experiments only (GSPLAT_HIP_DBG): bit 0 = backward skips its atomics
   uint64_t *timeline;  // debug: per-wave (start, end) s_memrealtime stamps or null
+  unsigned long long *lanehist;  // debug: histogram of contributing lanes per (record, wave)
 };
 
 // Debug timeline (gsplat_hip_debug_set_timeline): lane 0 of every wave stores
@@ -714,6 +742,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) b
         const bool v1 = (__float_as_uint(s2.y) <= __float_as_uint(f[6].y)) &&
                         (__float_as_int(f[7].y) <= mylast);
         if (__ballot(v0 | v1) == 0) continue;
+        if (a.lanehist) {
+          const int c0 = __popcll(__ballot(v0)), c1 = __popcll(__ballot(v1));
+          if (lane == 0) {
+            atomicAdd(&a.lanehist[c0], 1ull);
+            if (__float_as_int(f[8].y) >= 0) atomicAdd(&a.lanehist[c1], 1ull);
+          }
+        }
         const f2v al = f2v{fminf(ar.x, kAlphaMax), fminf(ar.y, kAlphaMax)};
         const f2v om = 1.f - al;
         const f2v ra = f2v{__builtin_amdgcn_rcpf(om.x), __builtin_amdgcn_rcpf(om.y)};
@@ -1062,6 +1097,7 @@ int rasterize16_bwd(int C, int64_t G, int D, int W, int H, int tw, int th,
   a.n_isects = n_isects;
   a.timeline = (g_timeline && g_timeline_waves >= 4 * n_items_bound(a.n_tiles, n_isects))
                    ? g_timeline : nullptr;
+  a.lanehist = g_lanehist;
   a.means2d = means2d; a.conics = conics; a.colors = colors; a.opacities = opacities;
   a.backgrounds = backgrounds; a.masks = masks; a.offsets = offsets; a.flatten_ids = flatten_ids;
   a.render_alphas = const_cast<float *>(render_alphas);
@@ -1090,6 +1126,11 @@ int rasterize16_bwd(int C, int64_t G, int D, int W, int H, int tw, int th,
 extern "C" int gsplat_hip_debug_set_chunk(int isects) {
   gs::g_chunk = isects <= 0 ? 0 : ((isects + 63) / 64) * 64;
   return gs::g_chunk;
+}
+
+extern "C" int gsplat_hip_debug_set_lane_histogram(unsigned long long *device_buffer) {
+  gs::g_lanehist = device_buffer;
+  return 0;
 }
 
 extern "C" int gsplat_hip_debug_set_timeline(uint64_t *device_buffer, int64_t capacity_waves) {

@@ -57,6 +57,7 @@ _SIGS = {
                                         _p, _p, _p, _p, _p, _i64, _p, _p, _p, _p, _p, _p, _p,
                                         _p, _p, _p, _p, _p, _i64, _p, _i64, _p]),
     "gsplat_hip_debug_set_timeline": (_i32, [_p, _i64]),
+    "gsplat_hip_debug_set_lane_histogram": (_i32, [_p]),
     "gsplat_hip_debug_set_chunk": (_i32, [_i32]),
     "gsplat_hip_ssim_workspace_bytes": (_i64, [_i32, _i32, _i32, _i32]),
     "gsplat_hip_ssim_l1_fwd": (_i32, [_i32, _i32, _i32, _i32, _p, _p, _p, _p, _p]),

@@ -229,6 +229,10 @@ int gsplat_hip_rasterize_bwd(int C, int64_t n_gaussians, int D, int width, int h
  * (100 MHz) at [2w, 2w+1], w = global wave index (4 waves per tile).  Not part
  * of the reference surface; NULL disables (the default). */
 int gsplat_hip_debug_set_timeline(uint64_t *device_buffer, int64_t capacity_waves);
+/* Debug/profiling: when non-NULL, the 16x16 backward adds, for every record
+ * it composites on a wave, 1 to device_buffer[k] (u64[65]), k = number of the
+ * wave's lanes the record contributes to.  NULL disables (the default). */
+int gsplat_hip_debug_set_lane_histogram(unsigned long long *device_buffer);
 /* Chunk length (isects, rounded up to a multiple of 64; <= 0 disables) of the
  * chunked 16x16 backward; returns the value in effect.  Default 1024, or the
  * GSPLAT_HIP_CHUNK environment variable.  Forward and backward of one
