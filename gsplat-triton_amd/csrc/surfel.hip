@@ -1,0 +1,864 @@
+// 2DGS (surfel) hot path for gfx950: ray-splat projection and the surfel
+// rasterizer, forward and backward.
+//
+// Replaces the reference CUDA kernels (hieu1999210/gsplat-triton)
+//   projection_2dgs_fused_fwd_kernel   gsplat/cuda/csrc/Projection2DGSFused.cu:17-238
+//   projection_2dgs_fused_bwd_kernel   gsplat/cuda/csrc/Projection2DGSFused.cu:319-457
+//     (+ compute_ray_transforms_aabb_vjp, gsplat/cuda/csrc/Projection2DGS.cuh:10-87)
+//   rasterize_to_pixels_2dgs_fwd_kernel gsplat/cuda/csrc/RasterizeToPixels2DGSFwd.cu:18-452
+//   rasterize_to_pixels_2dgs_bwd_kernel gsplat/cuda/csrc/RasterizeToPixels2DGSBwd.cu:16-700
+// with the same per-pixel algebra, on a CDNA4 mapping:
+//
+//  * projection: one lane per (camera, surfel), grid (ceil(N/256), C) so the
+//    camera is a wave-uniform scalar load; the backward stores its gradients
+//    (atomics only when several cameras share a surfel).
+//  * rasterizer: a workgroup per tile, each wave64 owns 64 consecutive pixels
+//    of the tile (a 16x4 strip of a 16x16 tile) and walks the tile's isects on
+//    its own: the lanes gather 64 records into a per-wave LDS queue, then every
+//    lane composites its pixel against the queue with LDS broadcast reads.  No
+//    workgroup barriers, and a wave stops as soon as its 64 pixels are
+//    saturated.  The forward keeps the next batch's gather in flight while it
+//    composites the current one.
+//  * backward: per (record, wave) the D + 15 gradient fields are summed over
+//    the 64 lanes with reduce_scatter (wave_ops.h) and 16 lanes add the totals
+//    into the surfel's packed gradient row with one coalesced fp32 atomic;
+//    unpack_kernel scatters the rows into the autograd tensors and forms the
+//    densification gradient.
+#include "common.h"
+#include "wave_ops.h"
+#include "../../include/gsplat_hip.h"
+
+namespace gs {
+namespace surfel {
+
+constexpr float kAlphaMin = 1.f / 255.f;
+constexpr float kAlphaMax = 0.999f;
+constexpr float kTMin = 1e-4f;
+constexpr float kFilterInvSquare = 2.f;  // FILTER_INV_SQUARE_2DGS, Rasterization.h:11
+constexpr float kLog2e = 1.4426950408889634f;
+
+// ------------------------------------------------------------- projection
+struct ProjFwdArgs {
+  int C, N, W, H;
+  float near_plane, far_plane, radius_clip;
+  const float *means, *quats, *scales, *viewmats, *Ks;
+  int32_t *radii;
+  float *means2d, *depths, *ray_transforms, *normals;
+};
+
+struct Cam {
+  M3 R;
+  float t[3], fx, fy, cx, cy;
+};
+
+GS_INLINE Cam load_cam(const float *__restrict__ viewmats, const float *__restrict__ Ks, int c) {
+  Cam k;
+  const float *V = viewmats + 16 * c;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) k.R.m[i][j] = V[4 * i + j];
+    k.t[i] = V[4 * i + 3];
+  }
+  const float *K = Ks + 9 * c;  // the reference reads K[0], K[2], K[4], K[5] only
+  k.fx = K[0];
+  k.cx = K[2];
+  k.fy = K[4];
+  k.cy = K[5];
+  return k;
+}
+
+// Camera-space surfel: mean, the two scaled tangent axes and the normal axis
+// (columns of R_cw * R(q) * diag(s0, s1, 1), Projection2DGSFused.cu:164-167).
+struct Frame {
+  float mc[3], t0[3], t1[3], nz[3];
+  M3 Rq;
+};
+
+GS_INLINE Frame surfel_frame(const Cam &k, const float *m, float4 q, float s0, float s1) {
+  Frame f;
+  f.Rq = quat_to_rotmat(q.x, q.y, q.z, q.w);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    f.mc[i] = k.R.m[i][0] * m[0] + k.R.m[i][1] * m[1] + k.R.m[i][2] * m[2] + k.t[i];
+    float a = 0.f, b = 0.f, c = 0.f;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      a += k.R.m[i][j] * f.Rq.m[j][0];
+      b += k.R.m[i][j] * f.Rq.m[j][1];
+      c += k.R.m[i][j] * f.Rq.m[j][2];
+    }
+    f.t0[i] = a * s0;
+    f.t1[i] = b * s1;
+    f.nz[i] = c;
+  }
+  return f;
+}
+
+__global__ void __launch_bounds__(256) proj_fwd_kernel(ProjFwdArgs a) {
+  const int c = blockIdx.y;
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  const Cam k = load_cam(a.viewmats, a.Ks, c);
+  if (n >= a.N) return;
+  const size_t idx = (size_t)c * a.N + n;
+  const float4 q = *reinterpret_cast<const float4 *>(a.quats + 4 * (size_t)n);
+  const float *sp = a.scales + 3 * (size_t)n;
+  const Frame f = surfel_frame(k, a.means + 3 * (size_t)n, q, sp[0], sp[1]);
+  a.depths[idx] = f.mc[2];
+
+  // rows of K * [t0 | t1 | mc] (the ray transform, M0/M1/M2 of the reference)
+  float M[9];
+  M[0] = k.fx * f.t0[0] + k.cx * f.t0[2];
+  M[1] = k.fx * f.t1[0] + k.cx * f.t1[2];
+  M[2] = k.fx * f.mc[0] + k.cx * f.mc[2];
+  M[3] = k.fy * f.t0[1] + k.cy * f.t0[2];
+  M[4] = k.fy * f.t1[1] + k.cy * f.t1[2];
+  M[5] = k.fy * f.mc[1] + k.cy * f.mc[2];
+  M[6] = f.t0[2];
+  M[7] = f.t1[2];
+  M[8] = f.mc[2];
+
+  bool keep = !(f.mc[2] < a.near_plane || f.mc[2] > a.far_plane);
+  // AABB from the (1, 1, -1) corner (Projection2DGSFused.cu:200-219)
+  const float dist = M[6] * M[6] + M[7] * M[7] - M[8] * M[8];
+  keep &= dist != 0.f;
+  const float fi = 1.f / dist;
+  const float mx = (fi * M[0]) * M[6] + (fi * M[1]) * M[7] + (-fi * M[2]) * M[8];
+  const float my = (fi * M[3]) * M[6] + (fi * M[4]) * M[7] + (-fi * M[5]) * M[8];
+  const float ex = mx * mx - ((fi * M[0]) * M[0] + (fi * M[1]) * M[1] + (-fi * M[2]) * M[2]);
+  const float ey = my * my - ((fi * M[3]) * M[3] + (fi * M[4]) * M[4] + (-fi * M[5]) * M[5]);
+  const float radius = ceilf(3.f * sqrtf(fmaxf(1e-4f, fmaxf(ex, ey))));
+  keep &= radius > a.radius_clip;
+  keep &= !(mx + radius <= 0.f || mx - radius >= (float)a.W || my + radius <= 0.f ||
+            my - radius >= (float)a.H);
+
+  const float sgn = -(f.nz[0] * f.mc[0] + f.nz[1] * f.mc[1] + f.nz[2] * f.mc[2]) > 0.f ? 1.f : -1.f;
+  a.radii[idx] = keep ? (int32_t)radius : 0;
+  *reinterpret_cast<float2 *>(a.means2d + 2 * idx) = keep ? make_float2(mx, my) : make_float2(0.f, 0.f);
+  float *rt = a.ray_transforms + 9 * idx;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) rt[i] = keep ? M[i] : 0.f;
+  float *nr = a.normals + 3 * idx;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) nr[i] = keep ? sgn * f.nz[i] : 0.f;
+}
+
+struct ProjBwdArgs {
+  int C, N;
+  const float *means, *quats, *scales, *viewmats, *Ks;
+  const int32_t *radii;
+  const float *ray_transforms, *v_means2d, *v_depths, *v_normals, *v_ray_transforms;
+  float *v_means, *v_quats, *v_scales;
+  int store_mode;  // C == 1: plain stores of every row; else atomics of valid rows
+};
+
+__global__ void __launch_bounds__(256) proj_bwd_kernel(ProjBwdArgs a) {
+  const int c = blockIdx.y;
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  const Cam k = load_cam(a.viewmats, a.Ks, c);
+  if (n >= a.N) return;
+  const size_t idx = (size_t)c * a.N + n;
+  const bool valid = a.radii[idx] > 0;
+  float vm[3] = {0.f, 0.f, 0.f}, vq[4] = {0.f, 0.f, 0.f, 0.f}, vs[3] = {0.f, 0.f, 0.f};
+  if (valid) {
+    const float4 q = *reinterpret_cast<const float4 *>(a.quats + 4 * (size_t)n);
+    const float *sp = a.scales + 3 * (size_t)n;
+    const float s0 = sp[0], s1 = sp[1];
+    const Frame f = surfel_frame(k, a.means + 3 * (size_t)n, q, s0, s1);
+    const float *rt = a.ray_transforms + 9 * idx;
+    float V[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) V[i] = a.v_ray_transforms[9 * idx + i];
+    if (a.v_depths) V[8] += a.v_depths[idx];
+    // means2d through the AABB formula, as the reference differentiates it
+    // (Projection2DGS.cuh:25-65)
+    const float gx = a.v_means2d[2 * idx], gy = a.v_means2d[2 * idx + 1];
+    if (gx != 0.f || gy != 0.f) {
+      float r[9];
+#pragma unroll
+      for (int i = 0; i < 9; ++i) r[i] = rt[i];
+      const float fi = 1.f / (r[6] * r[6] + r[7] * r[7] - r[8] * r[8]);
+      const float f2 = 2.f * fi * fi;
+      V[0] += gx * (fi * r[6]);
+      V[1] += gx * (fi * r[7]);
+      V[2] += gx * (-fi * r[8]);
+      V[3] += gy * (fi * r[6]);
+      V[4] += gy * (fi * r[7]);
+      V[5] += gy * (-fi * r[8]);
+      const float e6 = fi - f2 * r[6] * r[6], e7 = fi - f2 * r[7] * r[7], e8 = fi + f2 * r[8] * r[8];
+      V[6] += gx * (r[0] * e6) + gy * (r[3] * e6);
+      V[7] += gx * (r[1] * e7) + gy * (r[4] * e7);
+      V[8] += gx * (-r[2] * e8) + gy * (-r[5] * e8);
+    }
+    // d/d[t0 | t1 | mc] = K^T V (camera space), then R^T to world
+    float dW[3][3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      dW[0][j] = k.fx * V[j];
+      dW[1][j] = k.fy * V[3 + j];
+      dW[2][j] = k.cx * V[j] + k.cy * V[3 + j] + V[6 + j];
+    }
+    float vRS[3][3];  // vRS[i][j]: world-space gradient of column j
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int j = 0; j < 3; ++j)
+        vRS[i][j] = k.R.m[0][i] * dW[0][j] + k.R.m[1][i] * dW[1][j] + k.R.m[2][i] * dW[2][j];
+    const float *gn = a.v_normals + 3 * idx;
+    const float sgn =
+        -(f.nz[0] * f.mc[0] + f.nz[1] * f.mc[1] + f.nz[2] * f.mc[2]) > 0.f ? 1.f : -1.f;
+    float vtn[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+      vtn[i] = sgn * (k.R.m[0][i] * gn[0] + k.R.m[1][i] * gn[1] + k.R.m[2][i] * gn[2]);
+    M3 dR;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      dR.m[i][0] = vRS[i][0] * s0;
+      dR.m[i][1] = vRS[i][1] * s1;
+      dR.m[i][2] = vtn[i];
+    }
+    quat_to_rotmat_vjp(q.x, q.y, q.z, q.w, dR, vq);
+    vs[0] = vRS[0][0] * f.Rq.m[0][0] + vRS[1][0] * f.Rq.m[1][0] + vRS[2][0] * f.Rq.m[2][0];
+    vs[1] = vRS[0][1] * f.Rq.m[0][1] + vRS[1][1] * f.Rq.m[1][1] + vRS[2][1] * f.Rq.m[2][1];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) vm[i] = vRS[i][2];
+  }
+  if (a.store_mode) {
+    float *o = a.v_means + 3 * (size_t)n;
+    o[0] = vm[0]; o[1] = vm[1]; o[2] = vm[2];
+    *reinterpret_cast<float4 *>(a.v_quats + 4 * (size_t)n) = make_float4(vq[0], vq[1], vq[2], vq[3]);
+    o = a.v_scales + 3 * (size_t)n;
+    o[0] = vs[0]; o[1] = vs[1]; o[2] = 0.f;
+  } else if (valid) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) atomic_add_f32(a.v_means + 3 * (size_t)n + j, vm[j]);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) atomic_add_f32(a.v_quats + 4 * (size_t)n + j, vq[j]);
+    atomic_add_f32(a.v_scales + 3 * (size_t)n, vs[0]);
+    atomic_add_f32(a.v_scales + 3 * (size_t)n + 1, vs[1]);
+  }
+}
+
+// ------------------------------------------------------------- rasterizer
+// Record of one isect in a wave's LDS queue (floats):
+//   [0] x [1] y [2] opacity [3] isect index (int bits)
+//   [4..13) ray transform rows u, v, w   [13] surfel id (int bits)
+//   [14..17) normal   [17..17+D) colour (the last channel is the depth that
+//   the distortion and median terms read, as in the reference)
+template <int D>
+struct Rec {
+  static constexpr int X = 0, Y = 1, OP = 2, IDX = 3, M = 4, G = 13, NRM = 14, COL = 17;
+  static constexpr int NF = ((COL + D + 3) / 4) * 4;
+  static constexpr int N4 = NF / 4;
+};
+
+struct RasterArgs {
+  int C, W, H, ts, tw, th, n_tiles;
+  int64_t n_isects;
+  const float *means2d, *ray_transforms, *colors, *opacities, *normals, *backgrounds;
+  const uint8_t *masks;
+  const int32_t *offsets, *flatten_ids;
+  // forward outputs / backward inputs
+  float *render_colors, *render_alphas, *render_normals, *render_distort, *render_median;
+  int32_t *last_ids, *median_ids;
+  // backward
+  const float *v_render_colors, *v_render_alphas, *v_render_normals, *v_render_distort,
+      *v_render_median;
+  float *packed;  // [G][S] gradient rows
+  int S;
+};
+
+// Pixel of lane `lane` in wave `w`: the 64w + lane-th pixel of the tile in
+// row-major order (a 16x4 strip for 16x16 tiles).
+struct Pix {
+  int c, tile, px, py;
+  bool inside;
+  int64_t pid;  // flat pixel index in [C*H*W] (clamped)
+  int64_t start, end;
+  GS_INLINE Pix(const RasterArgs &a, int tile_, int w, int lane) {
+    tile = tile_;
+    const int ntile = a.tw * a.th;
+    c = tile / ntile;
+    const int rem = tile - c * ntile;
+    const int ty = rem / a.tw, tx = rem - ty * a.tw;
+    const int p = 64 * w + lane;
+    const int ly = p / a.ts, lx = p - ly * a.ts;
+    px = tx * a.ts + lx;
+    py = ty * a.ts + ly;
+    inside = (p < a.ts * a.ts) && px < a.W && py < a.H;
+    const int64_t off = (int64_t)c * a.H * a.W;
+    pid = off + (inside ? (int64_t)py * a.W + px : 0);
+    start = a.offsets[tile];
+    end = (tile == a.n_tiles - 1) ? a.n_isects : (int64_t)a.offsets[tile + 1];
+  }
+};
+
+template <int D>
+struct Gathered {
+  int32_t g;
+  float2 xy;
+  float op;
+  float m[9];
+  float nrm[3];
+  float col[D];
+};
+
+template <int D>
+GS_INLINE void gather(const RasterArgs &a, int64_t j, bool ok, Gathered<D> &r) {
+  const int32_t g = ok ? a.flatten_ids[j] : 0;
+  r.g = g;
+  r.xy = *reinterpret_cast<const float2 *>(a.means2d + 2 * (int64_t)g);
+  r.op = a.opacities[g];
+  const float *m = a.ray_transforms + 9 * (int64_t)g;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) r.m[i] = m[i];
+  const float *nr = a.normals + 3 * (int64_t)g;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) r.nrm[i] = nr[i];
+  const float *cl = a.colors + D * (int64_t)g;
+#pragma unroll
+  for (int i = 0; i < D; ++i) r.col[i] = cl[i];
+}
+
+template <int D>
+GS_INLINE void stage(float *slot, const Gathered<D> &r, int32_t idx) {
+  using R = Rec<D>;
+  float v[R::NF];
+  v[R::X] = r.xy.x;
+  v[R::Y] = r.xy.y;
+  v[R::OP] = r.op;
+  v[R::IDX] = __int_as_float(idx);
+#pragma unroll
+  for (int i = 0; i < 9; ++i) v[R::M + i] = r.m[i];
+  v[R::G] = __int_as_float(r.g);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) v[R::NRM + i] = r.nrm[i];
+#pragma unroll
+  for (int i = 0; i < D; ++i) v[R::COL + i] = r.col[i];
+#pragma unroll
+  for (int i = R::COL + D; i < R::NF; ++i) v[i] = 0.f;
+  float4 *s4 = reinterpret_cast<float4 *>(slot);
+#pragma unroll
+  for (int q = 0; q < R::N4; ++q) s4[q] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+}
+
+template <int D>
+GS_INLINE void read_rec(const float *slot, float (&v)[Rec<D>::NF]) {
+  const float4 *s4 = reinterpret_cast<const float4 *>(slot);
+#pragma unroll
+  for (int q = 0; q < Rec<D>::N4; ++q) {
+    const float4 t = s4[q];
+    v[4 * q] = t.x; v[4 * q + 1] = t.y; v[4 * q + 2] = t.z; v[4 * q + 3] = t.w;
+  }
+}
+
+// Ray-splat evaluation of one record at pixel centre (px, py)
+// (RasterizeToPixels2DGSFwd.cu:333-361).
+struct Hit {
+  float hu[3], hv[3], rc[3], s[2], g3, g2, vis, alpha;
+  bool ok;
+};
+
+GS_INLINE Hit eval_hit(const float *m, float x, float y, float op, float px, float py) {
+  Hit h;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    h.hu[i] = px * m[6 + i] - m[i];
+    h.hv[i] = py * m[6 + i] - m[3 + i];
+  }
+  h.rc[0] = h.hu[1] * h.hv[2] - h.hu[2] * h.hv[1];
+  h.rc[1] = h.hu[2] * h.hv[0] - h.hu[0] * h.hv[2];
+  h.rc[2] = h.hu[0] * h.hv[1] - h.hu[1] * h.hv[0];
+  const float iz = __builtin_amdgcn_rcpf(h.rc[2]);
+  h.s[0] = h.rc[0] * iz;
+  h.s[1] = h.rc[1] * iz;
+  h.g3 = h.s[0] * h.s[0] + h.s[1] * h.s[1];
+  const float dx = x - px, dy = y - py;
+  h.g2 = kFilterInvSquare * (dx * dx + dy * dy);
+  const float sigma = 0.5f * fminf(h.g3, h.g2);
+  h.vis = __builtin_amdgcn_exp2f(-sigma * kLog2e);
+  h.alpha = fminf(kAlphaMax, op * h.vis);
+  h.ok = (h.rc[2] != 0.f) && !(sigma < 0.f) && !(h.alpha < kAlphaMin);
+  return h;
+}
+
+// One workgroup per tile, ceil(ts^2 / 64) waves, a 64-record queue per wave.
+template <int D>
+__global__ void __launch_bounds__(1024) fwd_kernel(RasterArgs a) {
+  using R = Rec<D>;
+  extern __shared__ float4 lds4[];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  float *q = reinterpret_cast<float *>(lds4) + (size_t)w * 64 * R::NF;
+  const Pix p(a, blockIdx.x, w, lane);
+  const float fx = (float)p.px + 0.5f, fy = (float)p.py + 0.5f;
+  const float *bg = a.backgrounds ? a.backgrounds + (int64_t)p.c * D : nullptr;
+
+  float T = 1.f, col[D], nrm[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+  for (int d = 0; d < D; ++d) col[d] = 0.f;
+  float distort = 0.f, acc_vd = 0.f, median = 0.f;
+  int32_t cur = 0, med = 0;
+  bool done = !p.inside;
+  const bool masked = a.masks && !a.masks[p.tile];
+  if (masked) done = true;
+
+  int64_t b = p.start;
+  const bool run = !masked && b < p.end;
+  Gathered<D> nxt;
+  if (run) gather<D>(a, b + lane, b + lane < p.end, nxt);
+  for (; run && b < p.end; b += 64) {
+    if (__ballot(!done) == 0) break;
+    const int n = (int)min((int64_t)64, p.end - b);
+    stage<D>(q + lane * R::NF, nxt, (int32_t)(b + lane));
+    wave_sync_lds();
+    if (b + 64 < p.end) gather<D>(a, b + 64 + lane, b + 64 + lane < p.end, nxt);
+    for (int t = 0; t < n; ++t) {
+      float r[R::NF];
+      read_rec<D>(q + t * R::NF, r);
+      if (!done) {
+        const Hit h = eval_hit(r + R::M, r[R::X], r[R::Y], r[R::OP], fx, fy);
+        if (h.ok) {
+          const float nT = T * (1.f - h.alpha);
+          if (nT <= kTMin) {
+            done = true;
+          } else {
+            const float vis = h.alpha * T;
+#pragma unroll
+            for (int d = 0; d < D; ++d) col[d] += r[R::COL + d] * vis;
+#pragma unroll
+            for (int i = 0; i < 3; ++i) nrm[i] += r[R::NRM + i] * vis;
+            const float depth = r[R::COL + D - 1];
+            distort += 2.f * (vis * depth * (1.f - T) - vis * acc_vd);
+            acc_vd += vis * depth;
+            const int32_t idx = __float_as_int(r[R::IDX]);
+            if (T > 0.5f) {
+              median = depth;
+              med = idx;
+            }
+            cur = idx;
+            T = nT;
+          }
+        }
+      }
+      if ((t & 7) == 7 && __ballot(!done) == 0) break;
+    }
+    wave_sync_lds();
+  }
+  if (!p.inside) return;
+  const int64_t pid = p.pid;
+  if (masked) {  // reference writes the background only; the rest is defined here as empty
+#pragma unroll
+    for (int d = 0; d < D; ++d) a.render_colors[pid * D + d] = bg ? bg[d] : 0.f;
+    a.render_alphas[pid] = 0.f;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) a.render_normals[pid * 3 + i] = 0.f;
+    a.render_distort[pid] = 0.f;
+    a.render_median[pid] = 0.f;
+    a.last_ids[pid] = 0;
+    a.median_ids[pid] = 0;
+    return;
+  }
+  a.render_alphas[pid] = 1.f - T;
+#pragma unroll
+  for (int d = 0; d < D; ++d) a.render_colors[pid * D + d] = bg ? col[d] + T * bg[d] : col[d];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) a.render_normals[pid * 3 + i] = nrm[i];
+  a.render_distort[pid] = distort;
+  a.render_median[pid] = median;
+  a.last_ids[pid] = cur;
+  a.median_ids[pid] = med;
+}
+
+// Gradient fields of a packed row: colour[D], normal[3], ray transform[9],
+// means2d[2], opacity, |means2d|[2] (absgrad only).
+template <int D, bool ABS>
+struct Fields {
+  static constexpr int COL = 0, NRM = D, M = D + 3, XY = D + 12, OP = D + 14, AB = D + 15;
+  static constexpr int NF = D + 15 + (ABS ? 2 : 0);
+  static constexpr int NV = (NF + 15) / 16;  // reduce_scatter groups
+  static constexpr int S = 16 * NV;          // packed row stride (floats)
+};
+
+template <int D, bool ABS>
+__global__ void __launch_bounds__(256) bwd_kernel(RasterArgs a) {
+  using R = Rec<D>;
+  using F = Fields<D, ABS>;
+  extern __shared__ float4 lds4[];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  float *q = reinterpret_cast<float *>(lds4) + (size_t)w * 64 * R::NF;
+  const Pix p(a, blockIdx.x, w, lane);
+  if (a.masks && !a.masks[p.tile]) return;
+  const float fx = (float)p.px + 0.5f, fy = (float)p.py + 0.5f;
+  const int64_t pid = p.pid;
+
+  const float Tf = 1.f - a.render_alphas[pid];
+  float T = Tf;
+  const int32_t bin_final = p.inside ? a.last_ids[pid] : 0;
+  const int32_t med_idx = p.inside ? a.median_ids[pid] : 0;
+  float vc[D], buf[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    vc[d] = a.v_render_colors[pid * D + d];
+    buf[d] = 0.f;
+  }
+  const float va = a.v_render_alphas[pid];
+  float vn[3], bufn[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < 3; ++i) vn[i] = a.v_render_normals[pid * 3 + i];
+  const float vdist = a.v_render_distort ? a.v_render_distort[pid] : 0.f;
+  const float accum_d = a.render_colors[pid * D + D - 1], accum_w = 1.f - Tf;
+  float accd_buf = accum_d, accw_buf = accum_w, dist_buf = 0.f;
+  const float vmed = a.v_render_median ? a.v_render_median[pid] : 0.f;
+  float bg_dot = 0.f;
+  if (a.backgrounds) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) bg_dot += a.backgrounds[(int64_t)p.c * D + d] * vc[d];
+  }
+  // records past every lane's last contributor are skipped (the reference's
+  // warp_bin_final, RasterizeToPixels2DGSBwd.cu:336-337)
+  int32_t wmax = bin_final;
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) wmax = max(wmax, __shfl_xor(wmax, m, 64));
+  const int64_t end = min(p.end, (int64_t)wmax + 1);
+  const int lf = rs_field(lane);
+
+  for (int64_t b1 = end; b1 > p.start; b1 -= 64) {
+    const int64_t b0 = max(p.start, b1 - 64);
+    const int n = (int)(b1 - b0);
+    {
+      Gathered<D> g;
+      const int64_t j = b0 + lane;
+      gather<D>(a, j, j < b1, g);
+      stage<D>(q + lane * R::NF, g, (int32_t)j);
+    }
+    wave_sync_lds();
+    for (int t = n - 1; t >= 0; --t) {
+      float r[R::NF];
+      read_rec<D>(q + t * R::NF, r);
+      const int32_t idx = __float_as_int(r[R::IDX]);
+      const float *m = r + R::M;
+      Hit h = eval_hit(m, r[R::X], r[R::Y], r[R::OP], fx, fy);
+      const bool valid = p.inside && idx <= bin_final && h.ok;
+      if (__ballot(valid) == 0) continue;
+      float v[16 * F::NV];
+#pragma unroll
+      for (int k = 0; k < 16 * F::NV; ++k) v[k] = 0.f;
+      if (valid) {
+        if (idx == med_idx) v[F::COL + D - 1] += vmed;
+        const float ra = __builtin_amdgcn_rcpf(1.f - h.alpha);
+        T *= ra;
+        const float fac = h.alpha * T;
+        float v_alpha = 0.f;
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+          v[F::COL + d] += fac * vc[d];
+          v_alpha += (r[R::COL + d] * T - buf[d] * ra) * vc[d];
+        }
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+          v[F::NRM + i] = fac * vn[i];
+          v_alpha += (r[R::NRM + i] * T - bufn[i] * ra) * vn[i];
+        }
+        v_alpha += Tf * ra * va;
+        v_alpha += -Tf * ra * bg_dot;
+        {  // distortion (RasterizeToPixels2DGSBwd.cu:483-503)
+          const float depth = r[R::COL + D - 1];
+          const float dl_dw =
+              2.f * (2.f * (depth * accw_buf - accd_buf) + (accum_d - depth * accum_w));
+          v_alpha += (dl_dw * T - dist_buf * ra) * vdist;
+          accd_buf -= fac * depth;
+          accw_buf -= fac;
+          dist_buf += dl_dw * fac;
+          v[F::COL + D - 1] += 2.f * fac * (2.f - 2.f * T - accum_w + fac) * vdist;
+        }
+        if (r[R::OP] * h.vis <= kAlphaMax) {
+          const float vG = r[R::OP] * v_alpha;
+          if (h.g3 <= h.g2) {
+            const float vsx = vG * -h.vis * h.s[0], vsy = vG * -h.vis * h.s[1];
+            const float iz = __builtin_amdgcn_rcpf(h.rc[2]);
+            const float ax = vsx * iz, ay = vsy * iz;
+            const float vrc[3] = {ax, ay, -(ax * h.s[0] + ay * h.s[1])};
+            // v_h_u = h_v x v_rc, v_h_v = v_rc x h_u
+            const float vhu[3] = {h.hv[1] * vrc[2] - h.hv[2] * vrc[1],
+                                  h.hv[2] * vrc[0] - h.hv[0] * vrc[2],
+                                  h.hv[0] * vrc[1] - h.hv[1] * vrc[0]};
+            const float vhv[3] = {vrc[1] * h.hu[2] - vrc[2] * h.hu[1],
+                                  vrc[2] * h.hu[0] - vrc[0] * h.hu[2],
+                                  vrc[0] * h.hu[1] - vrc[1] * h.hu[0]};
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+              v[F::M + i] = -vhu[i];
+              v[F::M + 3 + i] = -vhv[i];
+              v[F::M + 6 + i] = fx * vhu[i] + fy * vhv[i];
+            }
+          } else {
+            const float dx = r[R::X] - fx, dy = r[R::Y] - fy;
+            v[F::XY] = vG * (-h.vis * kFilterInvSquare * dx);
+            v[F::XY + 1] = vG * (-h.vis * kFilterInvSquare * dy);
+            if (ABS) {
+              v[F::AB] = fabsf(v[F::XY]);
+              v[F::AB + 1] = fabsf(v[F::XY + 1]);
+            }
+          }
+          v[F::OP] = h.vis * v_alpha;
+        }
+#pragma unroll
+        for (int d = 0; d < D; ++d) buf[d] += r[R::COL + d] * fac;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) bufn[i] += r[R::NRM + i] * fac;
+      }
+      const int32_t g = __float_as_int(r[R::G]);
+      float *row = a.packed + (int64_t)g * F::S;
+#pragma unroll
+      for (int k = 0; k < F::NV; ++k) {
+        constexpr int NQ = F::NF - 16 * (F::NV - 1);
+        const float tot = k < F::NV - 1 ? reduce_scatter<16>(v + 16 * k, lane)
+                                        : reduce_scatter<NQ>(v + 16 * k, lane);
+        if ((lane & 3) == 0 && lf < (k < F::NV - 1 ? 16 : NQ) && tot != 0.f)
+          atomic_add_f32(row + 16 * k + lf, tot);
+      }
+    }
+    wave_sync_lds();
+  }
+}
+
+// packed [G][S] -> autograd tensors; densify = (v_M[0][2], v_M[1][2]) * depth
+// with depth = M[2][2] (the reference writes this racily from partial sums,
+// RasterizeToPixels2DGSBwd.cu:689-697; here it is formed from the final sums).
+template <int D, bool ABS>
+__global__ void __launch_bounds__(256)
+unpack_kernel(int64_t G, const float *__restrict__ packed, const float *__restrict__ rt,
+              float *__restrict__ v_means2d, float *__restrict__ v_rt, float *__restrict__ v_colors,
+              float *__restrict__ v_opacities, float *__restrict__ v_normals,
+              float *__restrict__ v_densify, float *__restrict__ v_abs) {
+  using F = Fields<D, ABS>;
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= G) return;
+  const float *r = packed + g * F::S;
+#pragma unroll
+  for (int d = 0; d < D; ++d) v_colors[g * D + d] = r[F::COL + d];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) v_normals[g * 3 + i] = r[F::NRM + i];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) v_rt[g * 9 + i] = r[F::M + i];
+  *reinterpret_cast<float2 *>(v_means2d + 2 * g) = make_float2(r[F::XY], r[F::XY + 1]);
+  v_opacities[g] = r[F::OP];
+  const float depth = rt[g * 9 + 8];
+  *reinterpret_cast<float2 *>(v_densify + 2 * g) =
+      make_float2(r[F::M + 2] * depth, r[F::M + 5] * depth);
+  if (ABS) *reinterpret_cast<float2 *>(v_abs + 2 * g) = make_float2(r[F::AB], r[F::AB + 1]);
+}
+
+}  // namespace surfel
+}  // namespace gs
+
+using namespace gs;
+using namespace gs::surfel;
+
+namespace {
+
+// Colour channel counts with compiled kernels (the caller pads others).
+#define GS_SURFEL_CHANNELS(X) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(16) X(17) X(32) X(33)
+
+bool channels_supported(int D) {
+#define GS_CASE(n) if (D == n) return true;
+  GS_SURFEL_CHANNELS(GS_CASE)
+#undef GS_CASE
+  return false;
+}
+
+int fields_stride(int D, int absgrad) {
+  const int nf = D + 15 + (absgrad ? 2 : 0);
+  return 16 * ((nf + 15) / 16);
+}
+
+int check_tiles(int C, int W, int H, int ts, int tw, int th) {
+  GS_REQUIRE(C >= 0 && W >= 0 && H >= 0, "rasterize_2dgs: negative sizes");
+  GS_REQUIRE(ts >= 1 && ts <= 32, "rasterize_2dgs: tile_size %d not in [1, 32]", ts);
+  GS_REQUIRE((int64_t)tw * ts >= W && (int64_t)th * ts >= H,
+             "rasterize_2dgs: %dx%d tiles of %d do not cover %dx%d", tw, th, ts, W, H);
+  return 0;
+}
+
+}  // namespace
+
+extern "C" int gsplat_hip_projection_2dgs_fwd(int C, int N, const float *means, const float *quats,
+                                              const float *scales, const float *viewmats,
+                                              const float *Ks, int width, int height,
+                                              float near_plane, float far_plane,
+                                              float radius_clip, int32_t *radii, float *means2d,
+                                              float *depths, float *ray_transforms,
+                                              float *normals, void *stream) {
+  GS_REQUIRE(C >= 0 && N >= 0, "projection_2dgs_fwd: negative sizes C=%d N=%d", C, N);
+  if (C == 0 || N == 0) return 0;
+  GS_REQUIRE(means && quats && scales && viewmats && Ks && radii && means2d && depths &&
+                 ray_transforms && normals,
+             "projection_2dgs_fwd: null pointer argument");
+  GS_REQUIRE(((uintptr_t)quats & 15) == 0 && ((uintptr_t)means2d & 7) == 0,
+             "projection_2dgs_fwd: quats must be 16-B aligned, means2d 8-B aligned");
+  ProjFwdArgs a{C, N, width, height, near_plane, far_plane, radius_clip, means, quats, scales,
+                viewmats, Ks, radii, means2d, depths, ray_transforms, normals};
+  hipLaunchKernelGGL(proj_fwd_kernel, dim3((N + 255) / 256, C), dim3(256), 0, (hipStream_t)stream,
+                     a);
+  GS_CHECK_LAUNCH("projection_2dgs_fwd");
+  return 0;
+}
+
+extern "C" int gsplat_hip_projection_2dgs_bwd(
+    int C, int N, const float *means, const float *quats, const float *scales,
+    const float *viewmats, const float *Ks, int width, int height, const int32_t *radii,
+    const float *ray_transforms, const float *v_means2d, const float *v_depths,
+    const float *v_normals, const float *v_ray_transforms, float *v_means, float *v_quats,
+    float *v_scales, float *v_viewmats, void *stream) {
+  (void)width;
+  (void)height;
+  GS_REQUIRE(C >= 0 && N >= 0, "projection_2dgs_bwd: negative sizes C=%d N=%d", C, N);
+  hipStream_t st = (hipStream_t)stream;
+  // the reference allocates v_viewmats but its kernel never writes it
+  // (Projection2DGSFused.cu:319-457): zeros
+  if (v_viewmats && C > 0) GS_HIP(hipMemsetAsync(v_viewmats, 0, sizeof(float) * 16 * C, st));
+  if (N == 0) return 0;
+  const int store_mode = (C == 1);
+  if (!store_mode) {
+    GS_HIP(hipMemsetAsync(v_means, 0, sizeof(float) * 3 * N, st));
+    GS_HIP(hipMemsetAsync(v_quats, 0, sizeof(float) * 4 * N, st));
+    GS_HIP(hipMemsetAsync(v_scales, 0, sizeof(float) * 3 * N, st));
+  }
+  if (C == 0) return 0;
+  GS_REQUIRE(means && quats && scales && viewmats && Ks && radii && ray_transforms &&
+                 v_means2d && v_normals && v_ray_transforms && v_means && v_quats && v_scales,
+             "projection_2dgs_bwd: null pointer argument");
+  GS_REQUIRE(((uintptr_t)quats & 15) == 0 && ((uintptr_t)v_quats & 15) == 0,
+             "projection_2dgs_bwd: quats / v_quats must be 16-B aligned");
+  ProjBwdArgs a{C, N, means, quats, scales, viewmats, Ks, radii, ray_transforms, v_means2d,
+                v_depths, v_normals, v_ray_transforms, v_means, v_quats, v_scales, store_mode};
+  hipLaunchKernelGGL(proj_bwd_kernel, dim3((N + 255) / 256, C), dim3(256), 0, st, a);
+  GS_CHECK_LAUNCH("projection_2dgs_bwd");
+  return 0;
+}
+
+extern "C" int gsplat_hip_rasterize_2dgs_supported_channels(int D) {
+  return channels_supported(D) ? 1 : 0;
+}
+
+extern "C" int gsplat_hip_rasterize_2dgs_fwd(
+    int C, int D, int width, int height, int tile_size, int tile_width, int tile_height,
+    const float *means2d, const float *ray_transforms, const float *colors,
+    const float *opacities, const float *normals, const float *backgrounds,
+    const uint8_t *masks, const int32_t *isect_offsets, int64_t n_isects,
+    const int32_t *flatten_ids, float *render_colors, float *render_alphas,
+    float *render_normals, float *render_distort, float *render_median, int32_t *last_ids,
+    int32_t *median_ids, void *stream) {
+  if (int e = check_tiles(C, width, height, tile_size, tile_width, tile_height)) return e;
+  GS_REQUIRE(channels_supported(D), "rasterize_2dgs_fwd: unsupported channel count %d", D);
+  const int n_tiles = C * tile_width * tile_height;
+  if (n_tiles == 0 || width == 0 || height == 0) return 0;
+  GS_REQUIRE(isect_offsets && render_colors && render_alphas && render_normals &&
+                 render_distort && render_median && last_ids && median_ids,
+             "rasterize_2dgs_fwd: null pointer argument");
+  GS_REQUIRE(n_isects == 0 || (means2d && ray_transforms && colors && opacities && normals &&
+                               flatten_ids),
+             "rasterize_2dgs_fwd: null pointer argument");
+  GS_REQUIRE(((uintptr_t)means2d & 7) == 0, "rasterize_2dgs_fwd: means2d must be 8-B aligned");
+  RasterArgs a{};
+  a.C = C; a.W = width; a.H = height; a.ts = tile_size; a.tw = tile_width; a.th = tile_height;
+  a.n_tiles = n_tiles; a.n_isects = n_isects;
+  a.means2d = means2d; a.ray_transforms = ray_transforms; a.colors = colors;
+  a.opacities = opacities; a.normals = normals; a.backgrounds = backgrounds; a.masks = masks;
+  a.offsets = isect_offsets; a.flatten_ids = flatten_ids;
+  a.render_colors = render_colors; a.render_alphas = render_alphas;
+  a.render_normals = render_normals; a.render_distort = render_distort;
+  a.render_median = render_median; a.last_ids = last_ids; a.median_ids = median_ids;
+  const int waves = (tile_size * tile_size + 63) / 64;
+  hipStream_t st = (hipStream_t)stream;
+#define GS_CASE(n)                                                                            \
+  if (D == n) {                                                                               \
+    const size_t lds = (size_t)waves * 64 * Rec<n>::NF * sizeof(float);                       \
+    hipLaunchKernelGGL(fwd_kernel<n>, dim3(n_tiles), dim3(64 * waves), lds, st, a);           \
+  }
+  GS_SURFEL_CHANNELS(GS_CASE)
+#undef GS_CASE
+  GS_CHECK_LAUNCH("rasterize_2dgs_fwd");
+  return 0;
+}
+
+extern "C" int64_t gsplat_hip_rasterize_2dgs_bwd_workspace_bytes(int64_t n_gaussians, int D,
+                                                                 int absgrad) {
+  return n_gaussians * fields_stride(D, absgrad) * (int64_t)sizeof(float);
+}
+
+extern "C" int gsplat_hip_rasterize_2dgs_bwd(
+    int C, int D, int width, int height, int tile_size, int tile_width, int tile_height,
+    int64_t n_gaussians, const float *means2d, const float *ray_transforms, const float *colors,
+    const float *opacities, const float *normals, const float *backgrounds,
+    const uint8_t *masks, const int32_t *isect_offsets, int64_t n_isects,
+    const int32_t *flatten_ids, const float *render_colors, const float *render_alphas,
+    const int32_t *last_ids, const int32_t *median_ids, const float *v_render_colors,
+    const float *v_render_alphas, const float *v_render_normals, const float *v_render_distort,
+    const float *v_render_median, float *v_means2d, float *v_ray_transforms, float *v_colors,
+    float *v_opacities, float *v_normals, float *v_densify, float *v_means2d_abs,
+    void *workspace, int64_t workspace_bytes, void *stream) {
+  if (int e = check_tiles(C, width, height, tile_size, tile_width, tile_height)) return e;
+  GS_REQUIRE(channels_supported(D), "rasterize_2dgs_bwd: unsupported channel count %d", D);
+  GS_REQUIRE(tile_size * tile_size <= 256, "rasterize_2dgs_bwd: tile_size %d > 16", tile_size);
+  const int absgrad = v_means2d_abs != nullptr;
+  const int S = fields_stride(D, absgrad);
+  const int64_t G = n_gaussians;
+  GS_REQUIRE(workspace_bytes >= G * S * (int64_t)sizeof(float),
+             "rasterize_2dgs_bwd: workspace too small");
+  hipStream_t st = (hipStream_t)stream;
+  if (G == 0) return 0;
+  GS_REQUIRE(workspace && v_means2d && v_ray_transforms && v_colors && v_opacities && v_normals &&
+                 v_densify && ray_transforms,
+             "rasterize_2dgs_bwd: null pointer argument");
+  GS_HIP(hipMemsetAsync(workspace, 0, (size_t)G * S * sizeof(float), st));
+  const int n_tiles = C * tile_width * tile_height;
+  if (n_tiles > 0 && n_isects > 0 && width > 0 && height > 0) {
+    GS_REQUIRE(isect_offsets && flatten_ids && render_colors && render_alphas && last_ids &&
+                   median_ids && v_render_colors && v_render_alphas && v_render_normals,
+               "rasterize_2dgs_bwd: null pointer argument");
+    RasterArgs a{};
+    a.C = C; a.W = width; a.H = height; a.ts = tile_size; a.tw = tile_width;
+    a.th = tile_height; a.n_tiles = n_tiles; a.n_isects = n_isects;
+    a.means2d = means2d; a.ray_transforms = ray_transforms; a.colors = colors;
+    a.opacities = opacities; a.normals = normals; a.backgrounds = backgrounds; a.masks = masks;
+    a.offsets = isect_offsets; a.flatten_ids = flatten_ids;
+    a.render_colors = const_cast<float *>(render_colors);
+    a.render_alphas = const_cast<float *>(render_alphas);
+    a.last_ids = const_cast<int32_t *>(last_ids);
+    a.median_ids = const_cast<int32_t *>(median_ids);
+    a.v_render_colors = v_render_colors; a.v_render_alphas = v_render_alphas;
+    a.v_render_normals = v_render_normals; a.v_render_distort = v_render_distort;
+    a.v_render_median = v_render_median;
+    a.packed = (float *)workspace; a.S = S;
+    const int waves = (tile_size * tile_size + 63) / 64;
+#define GS_CASE(n)                                                                            \
+  if (D == n) {                                                                               \
+    const size_t lds = (size_t)waves * 64 * Rec<n>::NF * sizeof(float);                       \
+    if (absgrad)                                                                              \
+      hipLaunchKernelGGL((bwd_kernel<n, true>), dim3(n_tiles), dim3(64 * waves), lds, st, a);  \
+    else                                                                                      \
+      hipLaunchKernelGGL((bwd_kernel<n, false>), dim3(n_tiles), dim3(64 * waves), lds, st, a); \
+  }
+    GS_SURFEL_CHANNELS(GS_CASE)
+#undef GS_CASE
+    GS_CHECK_LAUNCH("rasterize_2dgs_bwd");
+  }
+  const dim3 grid((unsigned)((G + 255) / 256));
+#define GS_CASE(n)                                                                             \
+  if (D == n) {                                                                                \
+    if (absgrad)                                                                               \
+      hipLaunchKernelGGL((unpack_kernel<n, true>), grid, dim3(256), 0, st, G, (const float *)workspace, \
+                         ray_transforms, v_means2d, v_ray_transforms, v_colors, v_opacities,   \
+                         v_normals, v_densify, v_means2d_abs);                                 \
+    else                                                                                       \
+      hipLaunchKernelGGL((unpack_kernel<n, false>), grid, dim3(256), 0, st, G, (const float *)workspace, \
+                         ray_transforms, v_means2d, v_ray_transforms, v_colors, v_opacities,   \
+                         v_normals, v_densify, v_means2d_abs);                                 \
+  }
+  GS_SURFEL_CHANNELS(GS_CASE)
+#undef GS_CASE
+  GS_CHECK_LAUNCH("rasterize_2dgs_unpack");
+  return 0;
+}

@@ -13,7 +13,8 @@ from ._wrapper import (
     rasterize_to_pixels,
     spherical_harmonics,
 )
-from .rendering import rasterization
+from ._wrapper_2dgs import fully_fused_projection_2dgs, rasterize_to_pixels_2dgs
+from .rendering import depth_to_normal, rasterization, rasterization_2dgs
 
 __all__ = [
     "fully_fused_projection",
@@ -22,5 +23,9 @@ __all__ = [
     "spherical_harmonics",
     "rasterize_to_pixels",
     "rasterization",
+    "fully_fused_projection_2dgs",
+    "rasterize_to_pixels_2dgs",
+    "rasterization_2dgs",
+    "depth_to_normal",
 ]
 __version__ = "0.1.0"

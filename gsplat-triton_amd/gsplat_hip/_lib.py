@@ -12,7 +12,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GSPLAT_HIP_LIB", os.path.join(_HERE, "libgsplat_hip.so"))
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 _p = ctypes.c_void_p
 _i32 = ctypes.c_int
@@ -68,6 +68,19 @@ _SIGS = {
     "gsplat_hip_activate_fwd": (_i32, [_i64, _i64, _p, _p, _p, _p, _p]),
     "gsplat_hip_activate_bwd": (_i32, [_i64, _i64, _p, _p, _p, _p, _p, _p, _p]),
     "gsplat_hip_adam_step": (_i32, [_i32, _p, _p, _p, _p, _p, _p, _f, _f, _f, _i32, _p]),
+    "gsplat_hip_projection_2dgs_fwd": (_i32, [_i32, _i32, _p, _p, _p, _p, _p, _i32, _i32, _f, _f,
+                                              _f, _p, _p, _p, _p, _p, _p]),
+    "gsplat_hip_projection_2dgs_bwd": (_i32, [_i32, _i32, _p, _p, _p, _p, _p, _i32, _i32, _p, _p,
+                                              _p, _p, _p, _p, _p, _p, _p, _p, _p]),
+    "gsplat_hip_rasterize_2dgs_supported_channels": (_i32, [_i32]),
+    "gsplat_hip_rasterize_2dgs_fwd": (_i32, [_i32, _i32, _i32, _i32, _i32, _i32, _i32, _p, _p, _p,
+                                             _p, _p, _p, _p, _p, _i64, _p, _p, _p, _p, _p, _p,
+                                             _p, _p, _p]),
+    "gsplat_hip_rasterize_2dgs_bwd_workspace_bytes": (_i64, [_i64, _i32, _i32]),
+    "gsplat_hip_rasterize_2dgs_bwd": (_i32, [_i32, _i32, _i32, _i32, _i32, _i32, _i32, _i64, _p,
+                                             _p, _p, _p, _p, _p, _p, _p, _i64, _p, _p, _p, _p,
+                                             _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p,
+                                             _p, _i64, _p]),
 }
 
 EXPORTED = tuple(_SIGS)

@@ -1,0 +1,286 @@
+"""2DGS (surfel) ops backed by libgsplat_hip.so.
+
+Drop-in for the 2DGS functions that `gsplat/rendering.py:31-34` imports from
+`gsplat/cuda/_wrapper.py`:
+
+    fully_fused_projection_2dgs  _wrapper.py:1229-1330 (autograd: _FullyFusedProjection2DGS :1333)
+    rasterize_to_pixels_2dgs     _wrapper.py:1595-1726 (autograd: _RasterizeToPixels2DGS :1803)
+
+Same signatures, defaults, assertions and autograd contract (argument order,
+`None` gradients, `ctx.needs_input_grad[6]` gating of `v_backgrounds`,
+`means2d.absgrad`, the `densify` input whose gradient is the densification
+signal).  Every op runs through the HIP C ABI on torch's current stream; there
+is no CPU fallback.
+"""
+
+from typing import Optional, Tuple
+
+import torch
+from torch import Tensor
+
+from . import _lib
+from ._wrapper import _Timed, _aligned16, _dev_check, _f32c, _ptr, _stream
+
+
+# ============================================================== projection ==
+class _FullyFusedProjection2DGS(torch.autograd.Function):
+    """Projects surfels to 2D (gsplat/cuda/_wrapper.py:1333-1437)."""
+
+    @staticmethod
+    def forward(ctx, means, quats, scales, viewmats, Ks, width, height, eps2d, near_plane,
+                far_plane, radius_clip):
+        means, quats, scales, viewmats, Ks = (_f32c(x) for x in (means, quats, scales, viewmats, Ks))
+        quats = _aligned16(quats)
+        _dev_check(means, quats, scales, viewmats, Ks)
+        C, N = viewmats.shape[0], means.shape[0]
+        dev = means.device
+        radii = torch.empty((C, N), dtype=torch.int32, device=dev)
+        means2d = torch.empty((C, N, 2), dtype=torch.float32, device=dev)
+        depths = torch.empty((C, N), dtype=torch.float32, device=dev)
+        ray_transforms = torch.empty((C, N, 3, 3), dtype=torch.float32, device=dev)
+        normals = torch.empty((C, N, 3), dtype=torch.float32, device=dev)
+        _lib.call("gsplat_hip_projection_2dgs_fwd", C, N, _ptr(means), _ptr(quats), _ptr(scales),
+                  _ptr(viewmats), _ptr(Ks), int(width), int(height), float(near_plane),
+                  float(far_plane), float(radius_clip), _ptr(radii), _ptr(means2d),
+                  _ptr(depths), _ptr(ray_transforms), _ptr(normals), _stream())
+        ctx.save_for_backward(means, quats, scales, viewmats, Ks, radii, ray_transforms, normals)
+        ctx.width, ctx.height, ctx.eps2d = int(width), int(height), eps2d
+        ctx.mark_non_differentiable(radii)
+        return radii, means2d, depths, ray_transforms, normals
+
+    @staticmethod
+    def backward(ctx, v_radii, v_means2d, v_depths, v_ray_transforms, v_normals):
+        means, quats, scales, viewmats, Ks, radii, ray_transforms, normals = ctx.saved_tensors
+        C, N = viewmats.shape[0], means.shape[0]
+        dev = means.device
+
+        def grad(t, shape):
+            return torch.zeros(shape, device=dev) if t is None else _f32c(t)
+
+        v_means2d = grad(v_means2d, (C, N, 2))
+        v_ray_transforms = grad(v_ray_transforms, (C, N, 3, 3))
+        v_normals = grad(v_normals, (C, N, 3))
+        v_depths = None if v_depths is None else _f32c(v_depths)
+        v_means = torch.empty((N, 3), device=dev)
+        v_quats = torch.empty((N, 4), device=dev)
+        v_scales = torch.empty((N, 3), device=dev)
+        v_viewmats = torch.empty((C, 4, 4), device=dev) if ctx.needs_input_grad[3] else None
+        _lib.call("gsplat_hip_projection_2dgs_bwd", C, N, _ptr(means), _ptr(quats), _ptr(scales),
+                  _ptr(viewmats), _ptr(Ks), ctx.width, ctx.height, _ptr(radii),
+                  _ptr(ray_transforms), _ptr(v_means2d), _ptr(v_depths), _ptr(v_normals),
+                  _ptr(v_ray_transforms), _ptr(v_means), _ptr(v_quats), _ptr(v_scales),
+                  _ptr(v_viewmats), _stream())
+        if not ctx.needs_input_grad[0]:
+            v_means = None
+        if not ctx.needs_input_grad[1]:
+            v_quats = None
+        if not ctx.needs_input_grad[2]:
+            v_scales = None
+        return (v_means, v_quats, v_scales, v_viewmats, None, None, None, None, None, None, None)
+
+
+def fully_fused_projection_2dgs(
+    means: Tensor,  # [N, 3]
+    quats: Tensor,  # [N, 4]
+    scales: Tensor,  # [N, 3]
+    viewmats: Tensor,  # [C, 4, 4]
+    Ks: Tensor,  # [C, 3, 3]
+    width: int,
+    height: int,
+    eps2d: float = 0.3,
+    near_plane: float = 0.01,
+    far_plane: float = 1e10,
+    radius_clip: float = 0.0,
+    packed: bool = False,
+    sparse_grad: bool = False,
+) -> Tuple[Tensor, Tensor, Tensor, Tensor, Tensor]:
+    """Ray-splat transforms, 2D means, depths, radii and normals of surfels
+    (gsplat/cuda/_wrapper.py:1229-1330).  Returns (radii i32[C,N],
+    means2d[C,N,2], depths[C,N], ray_transforms[C,N,3,3], normals[C,N,3])."""
+    C = viewmats.size(0)
+    N = means.size(0)
+    assert means.size() == (N, 3), means.size()
+    assert viewmats.size() == (C, 4, 4), viewmats.size()
+    assert Ks.size() == (C, 3, 3), Ks.size()
+    means = means.contiguous()
+    assert quats is not None, "quats is required"
+    assert scales is not None, "scales is required"
+    assert quats.size() == (N, 4), quats.size()
+    assert scales.size() == (N, 3), scales.size()
+    quats = quats.contiguous()
+    scales = scales.contiguous()
+    if sparse_grad:
+        assert packed, "sparse_grad is only supported when packed is True"
+    viewmats = viewmats.contiguous()
+    Ks = Ks.contiguous()
+    if packed:
+        raise NotImplementedError("packed=True 2DGS projection is not built yet "
+                                  "(SURVEY §8 f3); pass packed=False")
+    return _FullyFusedProjection2DGS.apply(means, quats, scales, viewmats, Ks, width, height,
+                                           eps2d, near_plane, far_plane, radius_clip)
+
+
+# ============================================================ rasterization ==
+_SUPPORTED_D = (1, 2, 3, 4, 5, 6, 7, 8, 9, 16, 17, 32, 33)
+
+
+class _RasterizeToPixels2DGS(torch.autograd.Function):
+    """Surfel rasterizer (gsplat/cuda/_wrapper.py:1803-1971)."""
+
+    @staticmethod
+    def forward(ctx, means2d, ray_transforms, colors, opacities, normals, densify, backgrounds,
+                masks, width, height, tile_size, isect_offsets, flatten_ids, absgrad, distloss):
+        means2d, ray_transforms, colors, opacities, normals, backgrounds = (
+            _f32c(x) for x in (means2d, ray_transforms, colors, opacities, normals, backgrounds))
+        _dev_check(means2d, ray_transforms, colors, opacities, normals, isect_offsets, flatten_ids)
+        C, th, tw = isect_offsets.shape
+        D = colors.shape[-1]
+        dev = means2d.device
+        isect_offsets = isect_offsets.to(torch.int32).contiguous()
+        flatten_ids = flatten_ids.to(torch.int32).contiguous()
+        masks_u8 = None if masks is None else masks.to(torch.uint8).contiguous()
+        render_colors = torch.empty((C, height, width, D), device=dev)
+        render_alphas = torch.empty((C, height, width, 1), device=dev)
+        render_normals = torch.empty((C, height, width, 3), device=dev)
+        render_distort = torch.empty((C, height, width, 1), device=dev)
+        render_median = torch.empty((C, height, width, 1), device=dev)
+        last_ids = torch.empty((C, height, width), dtype=torch.int32, device=dev)
+        median_ids = torch.empty((C, height, width), dtype=torch.int32, device=dev)
+        with _Timed("rasterize_2dgs_fwd"):
+            _lib.call("gsplat_hip_rasterize_2dgs_fwd", C, D, int(width), int(height),
+                      int(tile_size), tw, th, _ptr(means2d), _ptr(ray_transforms), _ptr(colors),
+                      _ptr(opacities), _ptr(normals), _ptr(backgrounds), _ptr(masks_u8),
+                      _ptr(isect_offsets), flatten_ids.numel(), _ptr(flatten_ids),
+                      _ptr(render_colors), _ptr(render_alphas), _ptr(render_normals),
+                      _ptr(render_distort), _ptr(render_median), _ptr(last_ids),
+                      _ptr(median_ids), _stream())
+        ctx.save_for_backward(means2d, ray_transforms, colors, opacities, normals, densify,
+                              backgrounds, masks_u8, isect_offsets, flatten_ids, render_colors,
+                              render_alphas, last_ids, median_ids)
+        ctx.width, ctx.height, ctx.tile_size = int(width), int(height), int(tile_size)
+        ctx.absgrad, ctx.distloss = absgrad, distloss
+        return render_colors, render_alphas, render_normals, render_distort, render_median
+
+    @staticmethod
+    def backward(ctx, v_render_colors, v_render_alphas, v_render_normals, v_render_distort,
+                 v_render_median):
+        (means2d, ray_transforms, colors, opacities, normals, densify, backgrounds, masks_u8,
+         isect_offsets, flatten_ids, render_colors, render_alphas, last_ids,
+         median_ids) = ctx.saved_tensors
+        C, th, tw = isect_offsets.shape
+        D = colors.shape[-1]
+        H, W = ctx.height, ctx.width
+        dev = means2d.device
+
+        def grad(t, shape):
+            return torch.zeros(shape, device=dev) if t is None else _f32c(t)
+
+        v_render_colors = grad(v_render_colors, (C, H, W, D))
+        v_render_alphas = grad(v_render_alphas, (C, H, W, 1))
+        v_render_normals = grad(v_render_normals, (C, H, W, 3))
+        v_render_distort = None if v_render_distort is None else _f32c(v_render_distort)
+        v_render_median = None if v_render_median is None else _f32c(v_render_median)
+        G = opacities.numel()
+        v_means2d = torch.empty_like(means2d)
+        v_ray_transforms = torch.empty_like(ray_transforms)
+        v_colors = torch.empty_like(colors)
+        v_opacities = torch.empty_like(opacities)
+        v_normals = torch.empty_like(normals)
+        v_densify = torch.empty(densify.shape, device=dev)
+        v_abs = torch.empty_like(means2d) if ctx.absgrad else None
+        ws = torch.empty(max(int(_lib.query("gsplat_hip_rasterize_2dgs_bwd_workspace_bytes", G, D,
+                                            int(ctx.absgrad))), 4), dtype=torch.uint8, device=dev)
+        with _Timed("rasterize_2dgs_bwd"):
+            _lib.call("gsplat_hip_rasterize_2dgs_bwd", C, D, W, H, ctx.tile_size, tw, th, G,
+                      _ptr(means2d), _ptr(ray_transforms), _ptr(colors), _ptr(opacities),
+                      _ptr(normals), _ptr(backgrounds), _ptr(masks_u8), _ptr(isect_offsets),
+                      flatten_ids.numel(), _ptr(flatten_ids), _ptr(render_colors),
+                      _ptr(render_alphas), _ptr(last_ids), _ptr(median_ids),
+                      _ptr(v_render_colors), _ptr(v_render_alphas), _ptr(v_render_normals),
+                      _ptr(v_render_distort), _ptr(v_render_median), _ptr(v_means2d),
+                      _ptr(v_ray_transforms), _ptr(v_colors), _ptr(v_opacities), _ptr(v_normals),
+                      _ptr(v_densify), _ptr(v_abs), _ptr(ws), ws.numel(), _stream())
+        if ctx.absgrad:
+            means2d.absgrad = v_abs
+        v_backgrounds = None
+        if ctx.needs_input_grad[6]:  # _wrapper.py:1953-1958
+            v_backgrounds = (v_render_colors * (1.0 - render_alphas).float()).sum(dim=(1, 2))
+        return (v_means2d, v_ray_transforms, v_colors, v_opacities, v_normals, v_densify,
+                v_backgrounds, None, None, None, None, None, None, None, None)
+
+
+def rasterize_to_pixels_2dgs(
+    means2d: Tensor,  # [C, N, 2]
+    ray_transforms: Tensor,  # [C, N, 3, 3]
+    colors: Tensor,  # [C, N, channels]
+    opacities: Tensor,  # [C, N]
+    normals: Tensor,  # [C, N, 3]
+    densify: Tensor,  # [C, N, 2]
+    image_width: int,
+    image_height: int,
+    tile_size: int,
+    isect_offsets: Tensor,  # [C, tile_height, tile_width]
+    flatten_ids: Tensor,  # [n_isects]
+    backgrounds: Optional[Tensor] = None,  # [C, channels]
+    masks: Optional[Tensor] = None,  # [C, tile_height, tile_width]
+    packed: bool = False,
+    absgrad: bool = False,
+    distloss: bool = False,
+) -> Tuple[Tensor, Tensor, Tensor, Tensor, Tensor]:
+    """Rasterizes surfels to pixels (gsplat/cuda/_wrapper.py:1595-1726).
+
+    Returns render_colors [C,H,W,channels], render_alphas [C,H,W,1],
+    render_normals [C,H,W,3], render_distort [C,H,W,1], render_median
+    [C,H,W,1].  The depth used by the distortion and median terms is the last
+    colour channel, as in the reference."""
+    C = isect_offsets.size(0)
+    device = means2d.device
+    if packed:
+        raise NotImplementedError("packed=True 2DGS rasterization is not built yet "
+                                  "(SURVEY §8 f3); pass packed=False")
+    N = means2d.size(1)
+    assert means2d.shape == (C, N, 2), means2d.shape
+    assert ray_transforms.shape == (C, N, 3, 3), ray_transforms.shape
+    assert colors.shape[:2] == (C, N), colors.shape
+    assert opacities.shape == (C, N), opacities.shape
+    if backgrounds is not None:
+        assert backgrounds.shape == (C, colors.shape[-1]), backgrounds.shape
+        backgrounds = backgrounds.contiguous()
+
+    channels = colors.shape[-1]
+    if channels > 512 or channels == 0:
+        raise ValueError(f"Unsupported number of color channels: {channels}")
+    if channels not in _SUPPORTED_D:
+        # pad with zero channels before the last one so the depth stays last
+        # (the reference pads with uninitialised channels, _wrapper.py:1657-1683)
+        target = next((d for d in _SUPPORTED_D if d >= channels), None)
+        if target is None:
+            raise ValueError(f"Unsupported number of color channels: {channels} "
+                             f"(this backend compiles {_SUPPORTED_D})")
+        padded_channels = target - channels
+        colors = torch.cat([colors[..., :-1],
+                            torch.zeros(*colors.shape[:-1], padded_channels, device=device),
+                            colors[..., -1:]], dim=-1)
+        if backgrounds is not None:  # appended at the end, as the reference does
+            backgrounds = torch.cat([backgrounds,
+                                     torch.zeros(*backgrounds.shape[:-1], padded_channels,
+                                                 device=device)], dim=-1)
+    else:
+        padded_channels = 0
+
+    tile_height, tile_width = isect_offsets.shape[1:3]
+    assert tile_height * tile_size >= image_height, \
+        f"Assert Failed: {tile_height} * {tile_size} >= {image_height}"
+    assert tile_width * tile_size >= image_width, \
+        f"Assert Failed: {tile_width} * {tile_size} >= {image_width}"
+
+    render_colors, render_alphas, render_normals, render_distort, render_median = \
+        _RasterizeToPixels2DGS.apply(
+            means2d.contiguous(), ray_transforms.contiguous(), colors.contiguous(),
+            opacities.contiguous(), normals.contiguous(), densify.contiguous(), backgrounds,
+            masks, image_width, image_height, tile_size, isect_offsets.contiguous(),
+            flatten_ids.contiguous(), absgrad, distloss)
+    if padded_channels > 0:
+        render_colors = torch.cat([render_colors[..., : -padded_channels - 1],
+                                   render_colors[..., -1:]], dim=-1)
+    return render_colors, render_alphas, render_normals, render_distort, render_median

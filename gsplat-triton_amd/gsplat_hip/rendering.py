@@ -174,3 +174,150 @@ def rasterization(
             [render_colors[..., :-1],
              render_colors[..., -1:] / render_alphas.clamp(min=1e-10)], dim=-1)
     return render_colors, render_alphas, meta
+
+
+def _depth_to_points(depths: Tensor, camtoworlds: Tensor, Ks: Tensor, z_depth: bool = True) -> Tensor:
+    """Back-projects depth maps [..., H, W, 1] to world points (gsplat/utils.py:137-198)."""
+    height, width = depths.shape[-3:-1]
+    device = depths.device
+    x, y = torch.meshgrid(torch.arange(width, device=device), torch.arange(height, device=device),
+                          indexing="xy")
+    fx, fy = Ks[..., 0, 0], Ks[..., 1, 1]
+    cx, cy = Ks[..., 0, 2], Ks[..., 1, 2]
+    camera_dirs = torch.nn.functional.pad(torch.stack(
+        [(x - cx[..., None, None] + 0.5) / fx[..., None, None],
+         (y - cy[..., None, None] + 0.5) / fy[..., None, None]], dim=-1), (0, 1), value=1.0)
+    directions = torch.einsum("...ij,...hwj->...hwi", camtoworlds[..., :3, :3], camera_dirs)
+    origins = camtoworlds[..., :3, -1]
+    if not z_depth:
+        directions = torch.nn.functional.normalize(directions, dim=-1)
+    return origins[..., None, None, :] + depths * directions
+
+
+def depth_to_normal(depths: Tensor, camtoworlds: Tensor, Ks: Tensor, z_depth: bool = True) -> Tensor:
+    """Surface normals from depth maps by central differences
+    (gsplat/utils.py:201-224)."""
+    points = _depth_to_points(depths, camtoworlds, Ks, z_depth=z_depth)
+    dx = points[..., 2:, 1:-1, :] - points[..., :-2, 1:-1, :]
+    dy = points[..., 1:-1, 2:, :] - points[..., 1:-1, :-2, :]
+    normals = torch.nn.functional.normalize(torch.cross(dx, dy, dim=-1), dim=-1)
+    return torch.nn.functional.pad(normals, (0, 0, 1, 1, 1, 1), value=0.0)
+
+
+def rasterization_2dgs(
+    means: Tensor,  # [N, 3]
+    quats: Tensor,  # [N, 4]
+    scales: Tensor,  # [N, 3]
+    opacities: Tensor,  # [N]
+    colors: Tensor,  # [(C,) N, D] or [N, K, 3]
+    viewmats: Tensor,  # [C, 4, 4]
+    Ks: Tensor,  # [C, 3, 3]
+    width: int,
+    height: int,
+    near_plane: float = 0.01,
+    far_plane: float = 1e10,
+    radius_clip: float = 0.0,
+    eps2d: float = 0.3,
+    sh_degree: Optional[int] = None,
+    packed: bool = False,
+    tile_size: int = 16,
+    backgrounds: Optional[Tensor] = None,
+    render_mode: str = "RGB",
+    sparse_grad: bool = False,
+    absgrad: bool = False,
+    distloss: bool = False,
+    depth_mode: str = "expected",
+):
+    """Rasterize N surfels (2DGS) to C images (gsplat/rendering.py:1018-1339).
+
+    Returns (render_colors, render_alphas, render_normals,
+    render_normals_from_depth, render_distort, render_median, meta), with
+    meta["gradient_2dgs"] the densification input whose .grad the 2DGS
+    strategy reads."""
+    from ._wrapper_2dgs import fully_fused_projection_2dgs, rasterize_to_pixels_2dgs
+
+    N = means.shape[0]
+    C = viewmats.shape[0]
+    assert means.shape == (N, 3), means.shape
+    assert quats.shape == (N, 4), quats.shape
+    assert scales.shape == (N, 3), scales.shape
+    assert opacities.shape == (N,), opacities.shape
+    assert viewmats.shape == (C, 4, 4), viewmats.shape
+    assert Ks.shape == (C, 3, 3), Ks.shape
+    assert render_mode in ["RGB", "D", "ED", "RGB+D", "RGB+ED"], render_mode
+    if distloss:
+        assert render_mode in ["D", "ED", "RGB+D", "RGB+ED"], (
+            "distloss requires depth rendering, render_mode should be D, ED, RGB+D, RGB+ED, "
+            f"but got {render_mode}")
+    if sh_degree is None:
+        assert (colors.dim() == 2 and colors.shape[0] == N) or (
+            colors.dim() == 3 and colors.shape[:2] == (C, N)), colors.shape
+    else:
+        assert colors.dim() == 3 and colors.shape[0] == N and colors.shape[2] == 3, colors.shape
+        assert (sh_degree + 1) ** 2 <= colors.shape[1], colors.shape
+    if packed:
+        raise NotImplementedError("packed=True 2DGS is not built yet (SURVEY §8 f3)")
+
+    radii, means2d, depths, ray_transforms, normals = fully_fused_projection_2dgs(
+        means, quats, scales, viewmats, Ks, width, height, eps2d, near_plane, far_plane,
+        radius_clip, packed, sparse_grad)
+    opacities = opacities[None] if C == 1 else opacities.repeat(C, 1)
+    camera_ids, gaussian_ids = None, None
+    densify = torch.zeros_like(means2d, dtype=means.dtype, requires_grad=True)
+
+    tile_width = math.ceil(width / float(tile_size))
+    tile_height = math.ceil(height / float(tile_size))
+    pending_isects = isect_tiles_begin(means2d, radii, depths, tile_size, tile_width, tile_height,
+                                       packed=False, n_cameras=C)
+
+    if not (colors.dim() == 3 and sh_degree is None):
+        colors = colors[None] if C == 1 else colors.expand(C, *([-1] * colors.dim()))
+    if sh_degree is not None:
+        if not viewmats.requires_grad:
+            # one kernel: dirs from -R^T t, radii masking, clamp_min(sh + 0.5, 0)
+            colors = sh_colors(sh_degree, means, viewmats, colors[0], radii)
+        else:
+            camtoworlds = torch.inverse(viewmats)
+            dirs = means[None, :, :] - camtoworlds[:, None, :3, 3]
+            colors = spherical_harmonics(sh_degree, dirs, colors, masks=radii > 0)
+            colors = torch.clamp_min(colors + 0.5, 0.0)
+
+    if render_mode in ["RGB+D", "RGB+ED"]:
+        colors = torch.cat((colors, depths[..., None]), dim=-1)
+        if backgrounds is not None:
+            backgrounds = torch.cat((backgrounds, torch.zeros((C, 1), device=colors.device)), -1)
+    elif render_mode in ["D", "ED"]:
+        colors = depths[..., None]
+
+    tiles_per_gauss, isect_ids, flatten_ids = pending_isects.finish(sort=True)
+    isect_offsets = isect_offset_encode(isect_ids, C, tile_width, tile_height)
+
+    render_colors, render_alphas, render_normals, render_distort, render_median = \
+        rasterize_to_pixels_2dgs(means2d, ray_transforms, colors, opacities, normals, densify,
+                                 width, height, tile_size, isect_offsets, flatten_ids,
+                                 backgrounds=backgrounds, packed=packed, absgrad=absgrad,
+                                 distloss=distloss)
+    render_normals_from_depth = None
+    if render_mode in ["ED", "RGB+ED"]:
+        render_colors = torch.cat(
+            [render_colors[..., :-1],
+             render_colors[..., -1:] / render_alphas.clamp(min=1e-10)], dim=-1)
+    if render_mode in ["RGB+ED", "RGB+D"]:
+        if depth_mode == "expected":
+            depth_for_normal = render_colors[..., -1:]
+        elif depth_mode == "median":
+            depth_for_normal = render_median
+        render_normals_from_depth = depth_to_normal(
+            depth_for_normal, torch.linalg.inv(viewmats), Ks).squeeze(0)
+
+    meta = {"camera_ids": camera_ids, "gaussian_ids": gaussian_ids, "radii": radii,
+            "means2d": means2d, "depths": depths, "ray_transforms": ray_transforms,
+            "opacities": opacities, "normals": normals, "tile_width": tile_width,
+            "tile_height": tile_height, "tiles_per_gauss": tiles_per_gauss,
+            "isect_ids": isect_ids, "flatten_ids": flatten_ids, "isect_offsets": isect_offsets,
+            "width": width, "height": height, "tile_size": tile_size, "n_cameras": C,
+            "render_distort": render_distort, "gradient_2dgs": densify}
+    render_normals = torch.einsum("...ij,...hwj->...hwi",
+                                  torch.linalg.inv(viewmats)[..., :3, :3], render_normals)
+    return (render_colors, render_alphas, render_normals, render_normals_from_depth,
+            render_distort, render_median, meta)

@@ -293,6 +293,88 @@ int gsplat_hip_adam_step(int n_groups, float *const *params, const float *const 
                          const int64_t *numels, const float *lrs, float beta1, float beta2,
                          float eps, int step, void *stream);
 
+/* ---------------------------------------------------------------------------
+ * 2DGS (surfels).  Replaces the CUDA kernels that gsplat.rendering.rasterization_2dgs
+ * (gsplat/rendering.py:1018-1339) reaches through gsplat/cuda/_wrapper.py.
+ *
+ * Projection: replaces projection_2dgs_fused_fwd (gsplat/cuda/csrc/Projection2DGSFused.cu:17-238,
+ * host gsplat/cuda/csrc/Projection.cpp:517-567, bound by _FullyFusedProjection2DGS.forward,
+ * gsplat/cuda/_wrapper.py:1333-1389).
+ * means[N,3] quats[N,4] (16-B aligned) scales[N,3] viewmats[C,4,4] Ks[C,3,3]
+ * -> radii i32[C,N], means2d[C,N,2], depths[C,N], ray_transforms[C,N,3,3]
+ *    (rows of K [t_u | t_v | mean_c]), normals[C,N,3].
+ * Culled entries (near/far, degenerate AABB, radius <= radius_clip, off-screen)
+ * have radii 0 and zero means2d / ray_transforms / normals (the reference
+ * leaves them uninitialised). */
+int gsplat_hip_projection_2dgs_fwd(int C, int N, const float *means, const float *quats,
+                                   const float *scales, const float *viewmats, const float *Ks,
+                                   int width, int height, float near_plane, float far_plane,
+                                   float radius_clip, int32_t *radii, float *means2d,
+                                   float *depths, float *ray_transforms, float *normals,
+                                   void *stream);
+
+/* Replaces projection_2dgs_fused_bwd (Projection2DGSFused.cu:319-457 with
+ * compute_ray_transforms_aabb_vjp, Projection2DGS.cuh:10-87; host
+ * Projection.cpp:569-633; _FullyFusedProjection2DGS.backward, _wrapper.py:1391-1437).
+ * -> v_means[N,3], v_quats[N,4], v_scales[N,3] (v_scales[:,2] = 0).
+ * v_viewmats[C,4,4] (or NULL) is written as zeros, as the reference's kernel
+ * never writes it.  v_depths may be NULL. */
+int gsplat_hip_projection_2dgs_bwd(int C, int N, const float *means, const float *quats,
+                                   const float *scales, const float *viewmats, const float *Ks,
+                                   int width, int height, const int32_t *radii,
+                                   const float *ray_transforms, const float *v_means2d,
+                                   const float *v_depths, const float *v_normals,
+                                   const float *v_ray_transforms, float *v_means,
+                                   float *v_quats, float *v_scales, float *v_viewmats,
+                                   void *stream);
+
+/* Surfel rasterizer.  D in {1..9, 16, 17, 32, 33}
+ * (gsplat_hip_rasterize_2dgs_supported_channels); the caller pads other
+ * channel counts keeping the depth channel last, as
+ * rasterize_to_pixels_2dgs does (gsplat/cuda/_wrapper.py:1657-1683).
+ * tile_size <= 32 forward, <= 16 backward.
+ * Forward replaces rasterize_to_pixels_2dgs_fwd
+ * (gsplat/cuda/csrc/RasterizeToPixels2DGSFwd.cu:18-452, host
+ * gsplat/cuda/csrc/Rasterization.cpp:322-410): means2d[G,2],
+ * ray_transforms[G,3,3], colors[G,D], opacities[G], normals[G,3],
+ * backgrounds[C,D] or NULL, masks u8[C,th,tw] or NULL ->
+ * render_colors[C,H,W,D], render_alphas[C,H,W,1], render_normals[C,H,W,3],
+ * render_distort[C,H,W,1], render_median[C,H,W,1], last_ids i32[C,H,W],
+ * median_ids i32[C,H,W]. */
+int gsplat_hip_rasterize_2dgs_supported_channels(int D);
+int gsplat_hip_rasterize_2dgs_fwd(int C, int D, int width, int height, int tile_size,
+                                  int tile_width, int tile_height, const float *means2d,
+                                  const float *ray_transforms, const float *colors,
+                                  const float *opacities, const float *normals,
+                                  const float *backgrounds, const uint8_t *masks,
+                                  const int32_t *isect_offsets, int64_t n_isects,
+                                  const int32_t *flatten_ids, float *render_colors,
+                                  float *render_alphas, float *render_normals,
+                                  float *render_distort, float *render_median,
+                                  int32_t *last_ids, int32_t *median_ids, void *stream);
+
+/* Backward replaces rasterize_to_pixels_2dgs_bwd
+ * (gsplat/cuda/csrc/RasterizeToPixels2DGSBwd.cu:16-700, host Rasterization.cpp:441-560;
+ * _RasterizeToPixels2DGS.backward, gsplat/cuda/_wrapper.py:1893-1971).
+ * workspace: gsplat_hip_rasterize_2dgs_bwd_workspace_bytes(G, D, absgrad) bytes.
+ * -> v_means2d[G,2], v_ray_transforms[G,3,3], v_colors[G,D], v_opacities[G],
+ *    v_normals[G,3], v_densify[G,2] = (v_rt[0][2], v_rt[1][2]) * rt[2][2]
+ *    (formed from the final sums; the reference writes it racily from partial
+ *    sums), v_means2d_abs[G,2] or NULL (absgrad off).
+ * v_render_distort / v_render_median may be NULL (no gradient). */
+int64_t gsplat_hip_rasterize_2dgs_bwd_workspace_bytes(int64_t n_gaussians, int D, int absgrad);
+int gsplat_hip_rasterize_2dgs_bwd(
+    int C, int D, int width, int height, int tile_size, int tile_width, int tile_height,
+    int64_t n_gaussians, const float *means2d, const float *ray_transforms, const float *colors,
+    const float *opacities, const float *normals, const float *backgrounds,
+    const uint8_t *masks, const int32_t *isect_offsets, int64_t n_isects,
+    const int32_t *flatten_ids, const float *render_colors, const float *render_alphas,
+    const int32_t *last_ids, const int32_t *median_ids, const float *v_render_colors,
+    const float *v_render_alphas, const float *v_render_normals, const float *v_render_distort,
+    const float *v_render_median, float *v_means2d, float *v_ray_transforms, float *v_colors,
+    float *v_opacities, float *v_normals, float *v_densify, float *v_means2d_abs,
+    void *workspace, int64_t workspace_bytes, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,251 @@
+"""GPU parity of the 2DGS (surfel) path: the HIP kernels (through the C ABI)
+against the surfel oracle and the reference's own torch projection goldens.
+Tolerances: the reference test's (tests/test_2dgs.py:77-122, 390-396) unless
+stated; the rasterizer's ids are exact up to the threshold flips described in
+test_gpu_parity.close_most."""
+
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import gsplat_oracle as O
+from oracle import surfel_oracle as S
+from test_gpu_parity import DEV, T, close, close_most
+from test_surfel_oracle import _load, surfel_scene
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import gsplat_hip  # noqa: F401
+
+
+def _proj_inputs(g):
+    return (T(g["means"]), T(g["quats"]), T(g["scales"]), T(g["viewmats"]), T(g["Ks"]),
+            int(g["width"]), int(g["height"]))
+
+
+# -------------------------------------------------------------- projection
+@pytest.mark.parametrize("name", ["proj2dgs_testdata.npz", "proj2dgs_random.npz"])
+def test_proj2dgs_fwd(name):
+    from gsplat_hip import fully_fused_projection_2dgs
+    g = _load(name)
+    radii, m2, d, rt, nr = fully_fused_projection_2dgs(*_proj_inputs(g))
+    o = S.proj2dgs_fwd(g["means"], g["quats"], g["scales"], g["viewmats"], g["Ks"],
+                       int(g["width"]), int(g["height"]))
+    # against the oracle: radii exact up to a ceil() flip, floats to rounding
+    close_most(radii, o[0], 0, 0, "radii", max_frac=2e-3)
+    v = (radii.cpu().numpy() > 0) & (o[0] > 0)
+    close(m2.cpu().numpy()[v], o[1][v], 1e-4, 1e-4, "means2d")
+    close(d, o[2], 1e-5, 1e-6, "depths")
+    close(rt.cpu().numpy()[v], o[3][v], 1e-5, 1e-4, "ray_transforms")
+    close(nr.cpu().numpy()[v], o[4][v], 1e-5, 1e-6, "normals")
+    # against the reference torch implementation (tests/test_2dgs.py:79-85)
+    vr = (radii.cpu().numpy() > 0) & (g["radii"] > 0)
+    assert np.abs(radii.cpu().numpy() - g["radii"]).max() <= 1
+    close(m2.cpu().numpy()[vr], g["means2d"][vr], 1e-4, 1e-4, "means2d vs reference")
+    close(rt.cpu().numpy()[vr], g["ray_transforms"][vr], 1e-4, 1e-4, "rt vs reference")
+    close(nr.cpu().numpy()[vr], g["normals"][vr], 1e-4, 1e-4, "normals vs reference")
+
+
+@pytest.mark.parametrize("name", ["proj2dgs_testdata.npz", "proj2dgs_random.npz",
+                                  "proj2dgs_random_nomeans2d.npz"])
+def test_proj2dgs_bwd(name):
+    from gsplat_hip import fully_fused_projection_2dgs
+    g = _load(name)
+    means, quats, scales, vm, K, W, H = _proj_inputs(g)
+    leaves = [x.clone().requires_grad_(True) for x in (means, quats, scales)]
+    radii, m2, d, rt, nr = fully_fused_projection_2dgs(*leaves, vm, K, W, H)
+    loss = ((m2 * T(g["v_means2d"])).sum() + (d * T(g["v_depths"])).sum()
+            + (rt * T(g["v_ray_transforms"])).sum() + (nr * T(g["v_normals"])).sum())
+    v_means, v_quats, v_scales = torch.autograd.grad(loss, leaves)
+    o_rt = S.proj2dgs_fwd(g["means"], g["quats"], g["scales"], g["viewmats"], g["Ks"], W, H)
+    om, oq, os_ = S.proj2dgs_bwd(g["means"], g["quats"], g["scales"], g["viewmats"], g["Ks"],
+                                 radii.cpu().numpy(), o_rt[3], g["v_means2d"], g["v_depths"],
+                                 g["v_normals"], g["v_ray_transforms"])
+    for a, b, w in ((v_means, om, "v_means"), (v_quats, oq, "v_quats"), (v_scales, os_, "v_scales")):
+        close(a, b, 1e-3, 1e-4 * max(1.0, np.abs(b).max()), w)
+    assert float(v_scales[:, 2].abs().max()) == 0.0
+
+
+def test_proj2dgs_viewmats_grad_zero_like_reference():
+    """The reference kernel never writes v_viewmats (Projection2DGSFused.cu:319-457)."""
+    from gsplat_hip import fully_fused_projection_2dgs
+    g = _load("proj2dgs_random.npz")
+    means, quats, scales, vm, K, W, H = _proj_inputs(g)
+    vm = vm.clone().requires_grad_(True)
+    means = means.clone().requires_grad_(True)
+    _, m2, d, rt, nr = fully_fused_projection_2dgs(means, quats, scales, vm, K, W, H)
+    gv, gm = torch.autograd.grad(rt.sum() + d.sum(), (vm, means))
+    assert float(gv.abs().max()) == 0.0 and float(gm.abs().max()) > 0
+
+
+# ------------------------------------------------------------ rasterizer
+def _raster_gpu(sc, masks=None, absgrad=False, D=None):
+    from gsplat_hip import rasterize_to_pixels_2dgs
+    leaves = {k: T(sc[k]).requires_grad_(True) for k in ("m2", "rt", "colors", "opac", "nr")}
+    bg = None if sc["bg"] is None else T(sc["bg"]).requires_grad_(True)
+    densify = torch.zeros_like(leaves["m2"], requires_grad=True)
+    out = rasterize_to_pixels_2dgs(
+        leaves["m2"], leaves["rt"], leaves["colors"], leaves["opac"], leaves["nr"], densify,
+        sc["W"], sc["H"], sc["ts"], T(sc["off"]), T(sc["fids"]), backgrounds=bg,
+        masks=None if masks is None else T(masks), absgrad=absgrad, distloss=True)
+    return leaves, bg, densify, out
+
+
+def _oracle_fwd(sc, masks=None):
+    return S.raster2dgs_fwd(sc["m2"], sc["rt"], sc["colors"], sc["opac"], sc["nr"], sc["bg"],
+                            masks, sc["W"], sc["H"], sc["ts"], sc["off"], sc["fids"])
+
+
+@pytest.mark.parametrize("seed,D,bg,C", [(0, 4, True, 1), (1, 3, False, 1), (2, 1, True, 2),
+                                         (3, 8, True, 1), (4, 33, False, 1)])
+def test_raster2dgs_fwd(seed, D, bg, C):
+    sc = surfel_scene(seed, N=300, W=70, H=52, D=D, bg=bg, C=C)
+    assert len(sc["fids"]) > 200
+    _, _, _, (rc, ra, rn, rd, rm) = _raster_gpu(sc)
+    oc, oa, on, od, om, ol, omi = _oracle_fwd(sc)
+    close_most(rc, oc, 1e-4, 1e-4, "colors", max_frac=5e-3)
+    close_most(ra, oa, 1e-4, 1e-4, "alphas", max_frac=5e-3)
+    close_most(rn, on, 1e-4, 1e-4, "normals", max_frac=5e-3)
+    close_most(rd, od, 1e-3, 1e-3, "distort", max_frac=5e-3)
+    close_most(rm, om, 1e-4, 1e-4, "median", max_frac=5e-3)
+
+
+def test_raster2dgs_fwd_masks():
+    sc = surfel_scene(5, N=300, W=70, H=52, D=4, bg=True)
+    rng = np.random.default_rng(0)
+    masks = rng.random(sc["off"].shape) > 0.4
+    _, _, _, (rc, ra, rn, rd, rm) = _raster_gpu(sc, masks=masks)
+    oc, oa, on, od, om, _, _ = _oracle_fwd(sc, masks=masks)
+    close_most(rc, oc, 1e-4, 1e-4, "colors", max_frac=5e-3)
+    close_most(ra, oa, 1e-4, 1e-4, "alphas", max_frac=5e-3)
+
+
+@pytest.mark.parametrize("seed,D,bg,absgrad", [(0, 4, True, False), (1, 3, False, True),
+                                               (2, 1, True, False), (6, 9, True, True)])
+def test_raster2dgs_bwd(seed, D, bg, absgrad):
+    sc = surfel_scene(seed, N=300, W=70, H=52, D=D, bg=bg)
+    leaves, bgt, densify, outs = _raster_gpu(sc, absgrad=absgrad)
+    rng = np.random.default_rng(seed + 100)
+    vs = [rng.standard_normal(o.shape).astype(np.float32) for o in outs]
+    loss = sum((o * T(v)).sum() for o, v in zip(outs, vs))
+    wrt = list(leaves.values()) + ([bgt] if bgt is not None else []) + [densify]
+    grads = torch.autograd.grad(loss, wrt)
+    oc, oa, on, od, om, ol, omi = _oracle_fwd(sc)
+    ref = S.raster2dgs_bwd(sc["m2"], sc["rt"], sc["colors"], sc["opac"], sc["nr"], sc["bg"], None,
+                           sc["W"], sc["H"], sc["ts"], sc["off"], sc["fids"], oc, oa, ol, omi,
+                           *vs, absgrad=absgrad)
+    vm, vrt, vcl, vop, vnr, vden, vbg, vab = ref
+    names = ["v_means2d", "v_ray_transforms", "v_colors", "v_opacities", "v_normals"]
+    for gpu, o, n in zip(grads[:5], (vm, vrt, vcl, vop, vnr), names):
+        scale = max(1.0, float(np.abs(o).max()))
+        close_most(gpu, o, 1e-3, 1e-3 * scale, n, max_frac=5e-3, rows=True)
+    if bg:
+        close(grads[5], vbg, 1e-4, 1e-4, "v_backgrounds")
+    close_most(grads[-1], vden, 1e-3, 1e-3 * max(1.0, float(np.abs(vden).max())), "v_densify",
+               max_frac=5e-3, rows=True)
+    if absgrad:
+        m2 = leaves["m2"]
+        assert m2.absgrad is not None
+        close_most(m2.absgrad, vab, 1e-3, 1e-3 * max(1.0, float(np.abs(vab).max())), "absgrad",
+                   max_frac=5e-3, rows=True)
+
+
+def test_raster2dgs_channel_padding():
+    """10 channels are padded to the next compiled count with the depth kept
+    last (gsplat/cuda/_wrapper.py:1657-1683); results equal the oracle at 10."""
+    sc = surfel_scene(7, N=200, W=48, H=40, D=10, bg=True)
+    leaves, bgt, densify, (rc, ra, rn, rd, rm) = _raster_gpu(sc)
+    assert rc.shape[-1] == 10
+    oc, oa, on, od, om, _, _ = _oracle_fwd(sc)
+    # the reference appends the padded background at the end, so the depth
+    # channel's background is dropped; surfel_scene's depth background is 0
+    close_most(rc, oc, 1e-4, 1e-4, "colors", max_frac=5e-3)
+    close_most(rd, od, 1e-3, 1e-3, "distort", max_frac=5e-3)
+    g = torch.autograd.grad(rc.sum() + rd.sum(), leaves["colors"])[0]
+    assert torch.isfinite(g).all() and g.shape[-1] == 10
+
+
+def test_raster2dgs_empty():
+    from gsplat_hip import rasterize_to_pixels_2dgs
+    C, N, W, H = 1, 5, 32, 32
+    m2 = torch.zeros(C, N, 2, device=DEV, requires_grad=True)
+    rt = torch.zeros(C, N, 3, 3, device=DEV)
+    cols = torch.rand(C, N, 3, device=DEV)
+    op = torch.rand(C, N, device=DEV)
+    nr = torch.zeros(C, N, 3, device=DEV)
+    off = torch.zeros(C, 2, 2, dtype=torch.int32, device=DEV)
+    fids = torch.zeros(0, dtype=torch.int32, device=DEV)
+    bg = torch.rand(C, 3, device=DEV)
+    rc, ra, rn, rd, rm = rasterize_to_pixels_2dgs(m2, rt, cols, op, nr, torch.zeros_like(m2), W,
+                                                  H, 16, off, fids, backgrounds=bg)
+    close(rc, bg[:, None, None, :].expand(C, H, W, 3), 0, 0, "bg only")
+    assert float(ra.detach().abs().max()) == 0.0
+    (g,) = torch.autograd.grad(rc.sum(), m2)
+    assert float(g.abs().max()) == 0.0
+
+
+# ------------------------------------------------------------- end to end
+@pytest.mark.parametrize("mode,sh", [("RGB", None), ("RGB+D", 3), ("RGB+ED", None), ("D", None)])
+def test_rasterization_2dgs_e2e(mode, sh):
+    from gsplat_hip import rasterization_2dgs
+    rng = np.random.default_rng(11)
+    N, W, H = 500, 96, 80
+    means = (rng.standard_normal((N, 3)) * [0.6, 0.6, 0.3] + [0, 0, 3]).astype(np.float32)
+    quats = rng.standard_normal((N, 4)).astype(np.float32)
+    scales = (rng.random((N, 3)) * 0.1 + 0.02).astype(np.float32)
+    opac = rng.random(N).astype(np.float32)
+    if sh is None:
+        colors = rng.random((N, 3)).astype(np.float32)
+    else:
+        colors = (rng.standard_normal((N, (sh + 1) ** 2, 3)) * 0.3).astype(np.float32)
+    vm = np.eye(4, dtype=np.float32)[None]
+    K = np.array([[90.0, 0, W / 2], [0, 90.0, H / 2], [0, 0, 1]], np.float32)[None]
+    leaves = [T(x).requires_grad_(True) for x in (means, quats, scales, opac, colors)]
+    bg = T(rng.random((1, 3)).astype(np.float32))
+    out = rasterization_2dgs(*leaves, T(vm), T(K), W, H, sh_degree=sh, render_mode=mode,
+                             backgrounds=bg if mode != "D" else None, distloss=(mode != "RGB"))
+    rc, ra, rn, rnd, rdist, rmed, meta = out
+    # oracle composition of the same pipeline
+    radii, m2, d, rt, nr = S.proj2dgs_fwd(means, quats, scales, vm, K, W, H)
+    assert np.array_equal(meta["radii"].cpu().numpy(), radii)
+    tw, th = math.ceil(W / 16), math.ceil(H / 16)
+    _, ids, fids = O.isect_tiles(m2, radii, d, 16, tw, th)
+    assert np.array_equal(meta["isect_ids"].cpu().numpy(), ids)
+    assert np.array_equal(meta["flatten_ids"].cpu().numpy(), fids)
+    off = O.isect_offset_encode(ids, 1, tw, th)
+    if sh is None:
+        cols = colors[None]
+    else:
+        dirs = means[None] - np.linalg.inv(vm)[:, None, :3, 3]
+        cols = np.maximum(O.sh_fwd(sh, dirs, colors[None], masks=radii > 0) + 0.5, 0)
+    bgo = bg.cpu().numpy()
+    if mode in ("RGB+D", "RGB+ED"):
+        cols = np.concatenate([cols, d[..., None]], -1)
+        bgo = np.concatenate([bgo, np.zeros((1, 1), np.float32)], -1)
+    elif mode == "D":
+        cols, bgo = d[..., None], None
+    oc, oa, on, od, om, _, _ = S.raster2dgs_fwd(m2, rt, cols, opac[None], nr, bgo, None, W, H, 16,
+                                                off, fids)
+    if mode in ("ED", "RGB+ED"):
+        oc = np.concatenate([oc[..., :-1], oc[..., -1:] / np.maximum(oa, 1e-10)], -1)
+    close_most(rc, oc, 1e-4, 1e-4, "colors", max_frac=5e-3)
+    close_most(ra, oa, 1e-4, 1e-4, "alphas", max_frac=5e-3)
+    close_most(rn, on, 1e-4, 1e-4, "normals (camera = world here)", max_frac=5e-3)
+    if mode in ("RGB+D", "RGB+ED"):
+        assert rnd is not None and rnd.shape == (H, W, 3)
+    loss = rc.sum() + ra.sum() + rn.sum() + rdist.sum()
+    loss.backward()
+    for i, x in enumerate(leaves):
+        if mode == "D" and i == 4:  # colours are not rendered in depth mode
+            assert x.grad is None
+            continue
+        assert x.grad is not None and torch.isfinite(x.grad).all()
+    assert meta["gradient_2dgs"].grad is not None
+    assert float(meta["gradient_2dgs"].grad.abs().sum()) > 0
