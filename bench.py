@@ -36,7 +36,11 @@ CONFIGS = {
     "m2": (3, 1920, 1080, "garden scene_grid=3 (1,006,065 Gaussians), 1920x1080, SH deg 3"),
     "m3": (7, 1920, 1080, "garden scene_grid=7 (5,477,465 Gaussians), 1920x1080, SH deg 3"),
     "m1": (1, 648, 420, "garden crop (111,785 Gaussians), 648x420, SH deg 3"),
+    # BASELINE.json configs[4]: the 2DGS surfel pipeline on the M2 scene
+    "m5": (3, 1920, 1080, "2DGS surfels (simple_trainer_2dgs default step, RGB+D), garden "
+                          "scene_grid=3 (1,006,065 surfels), 1920x1080, SH deg 3"),
 }
+MODEL = {"m5": "2dgs"}
 
 
 def parse():
@@ -76,7 +80,8 @@ def pmc_traffic(config: str):
     per = {}
     for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
         d = tempfile.mkdtemp(prefix="gsplat_pmc_", dir="/tmp")
-        cmd = [rp, "--kernel-include-regex", "r16::fwd_kernel", "--pmc", ctr, "-f", "csv",
+        regex = "surfel::fwd_kernel" if MODEL.get(config) == "2dgs" else "r16::fwd_kernel"
+        cmd = [rp, "--kernel-include-regex", regex, "--pmc", ctr, "-f", "csv",
                "-d", d, "-o", "p", "--", sys.executable, os.path.abspath(__file__), "--probe",
                "--config", config, "--warmup", "2"]
         try:
@@ -132,8 +137,9 @@ def main():
     means, rgbs, vms, Ks, sw, sh_ = load_garden_scene(
         os.path.join(ROOT, "tests", "golden", "garden_scene.npz"), scene_grid=grid)
     vm_pool, K_pool = camera_pool(vms, Ks, sw, sh_, W, H, n=max(8, world))
+    model = MODEL.get(args.config, "3dgs")
     tr = Trainer(means, rgbs, vm_pool, K_pool, W, H, sh_degree=3, device=dev, world_size=world,
-                 rank=rank)
+                 rank=rank, model=model)
     N = means.shape[0]
 
     for it in range(args.warmup):
@@ -163,11 +169,22 @@ def main():
         evs = timers.get(name, [])
         return float(np.mean([a.elapsed_time(b) for a, b in evs])) if evs else float("nan")
 
-    fwd_ms, bwd_ms = mean_ms("rasterize_fwd"), mean_ms("rasterize_bwd")
+    two = model == "2dgs"
+    kname = "rasterize_2dgs_fwd" if two else "rasterize_fwd"
+    fwd_ms, bwd_ms = mean_ms(kname), mean_ms("rasterize_2dgs_bwd" if two else "rasterize_bwd")
 
     # ---- algorithmic bytes of one rasterize fwd launch, averaged over the
-    # cameras this rank renders (computed outside the timed region)
-    D = 3
+    # cameras this rank renders (computed outside the timed region).
+    # 3DGS: per isect id 4 + means2d 8 + conic 12 + opacity 4 + colour 4D,
+    #       per pixel colour 4D + alpha 4 + last id 4.
+    # 2DGS: per isect id 4 + means2d 8 + ray transform 36 + opacity 4 +
+    #       normal 12 + colour 4D; per pixel colour 4D + alpha, normal (12),
+    #       distortion, median, last id, median id.
+    D = 4 if two else 3
+    per_isect = (64 + 4 * D) if two else (28 + 4 * D)
+    per_px = (4 * D + 32) if two else (4 * D + 8)
+    node_name = "_RasterizeToPixels2DGSBackward" if two else "_RasterizeToPixelsBackward"
+    last_slot = 12 if two else 9
     byts, isects = [], []
     if True:  # graph needed to reach the forward's saved last_ids
         for it in range(args.warmup, args.warmup + min(args.steps, len(vm_pool))):
@@ -179,9 +196,9 @@ def main():
             n = meta["flatten_ids"].numel()
             ends = torch.cat([offs[1:], torch.tensor([n], device=dev)])
             node = colors.grad_fn
-            while node is not None and type(node).__name__ != "_RasterizeToPixelsBackward":
+            while node is not None and type(node).__name__ != node_name:
                 node = node.next_functions[0][0]
-            last = node.saved_tensors[9] if node is not None else None
+            last = node.saved_tensors[last_slot] if node is not None else None
             if last is not None:
                 ts = meta["tile_size"]
                 tw, th = meta["tile_width"], meta["tile_height"]
@@ -191,7 +208,7 @@ def main():
             else:
                 n_eff = n
             P = H * W
-            byts.append(n_eff * (28 + 4 * D) + P * (4 * D + 8) + 4 * tw * th)
+            byts.append(n_eff * per_isect + P * per_px + 4 * tw * th)
             isects.append(n)
     bytes_per_launch = float(np.mean(byts))
     achieved = bytes_per_launch / (fwd_ms * 1e-3) / 1e9
@@ -214,12 +231,13 @@ def main():
                    "cameras_per_rank_per_step": 1, "parallelism": f"dp{world}",
                    "n_isects_mean": float(np.mean(isects)), "packed": False,
                    "loss": "0.8*L1+0.2*(1-SSIM valid)", "optimizer": "Adam (6 groups)"},
-        "roofline": {"kernel": "rasterize_fwd", "bound": "hbm", "achieved": achieved,
+        "roofline": {"kernel": kname, "bound": "hbm", "achieved": achieved,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                      "traffic": None if traffic is None else traffic["bytes_per_launch"],
                      "traffic_detail": traffic,
                      "algorithmic_bytes_per_launch": bytes_per_launch,
                      "launch_ms": fwd_ms, "rasterize_bwd_ms": bwd_ms},
+        "model": model,
     }
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -291,8 +291,45 @@ struct Pix {
     pid = off + (inside ? (int64_t)py * a.W + px : 0);
     start = a.offsets[tile];
     end = (tile == a.n_tiles - 1) ? a.n_isects : (int64_t)a.offsets[tile + 1];
+    // pixel-centre rectangle of the wave's rows (whole tile width)
+    const int r0 = (64 * w) / a.ts, r1 = min(a.ts - 1, (64 * w + 63) / a.ts);
+    x0 = tx * a.ts + 0.5f;
+    x1 = x0 + (a.ts - 1);
+    y0 = ty * a.ts + r0 + 0.5f;
+    y1 = ty * a.ts + r1 + 0.5f;
   }
+  float x0, x1, y0, y1;
 };
+
+// Strip culling: false only if no pixel centre of [x0,x1]x[y0,y1] can reach
+// alpha >= 1/255, i.e. sigma = min(g3, g2) / 2 > ln(255 opacity) everywhere
+// (0.05 of margin on sigma and 1 px on the ellipse box absorb fp32 rounding).
+//  * g2 = 2 |mean2d - p|^2: the disk |d|^2 <= ln(255 op) against the rectangle;
+//  * g3 = |s(p)|^2 <= r^2 with r^2 = 2 ln(255 op) is the image of the surfel's
+//    UV disk of radius r, an ellipse whose exact bounding box follows from the
+//    dual conic T diag(r^2, r^2, -1) T^T of the ray transform T (the AABB
+//    formula of Projection2DGSFused.cu:200-209 with the axes scaled by r).
+//    It is bounded (c22 < 0) only when the whole disk lies in front of the
+//    camera; otherwise the record is kept.
+GS_INLINE bool surfel_keep(const float *m, float x, float y, float op, float x0, float x1,
+                           float y0, float y1) {
+  if (!(op >= kAlphaMin)) return false;  // alpha <= opacity < 1/255 everywhere
+  const float lnv = 0.69314718f * __builtin_amdgcn_logf(255.f * op) + 0.05f;
+  const float ddx = fmaxf(fmaxf(x0 - x, x - x1), 0.f), ddy = fmaxf(fmaxf(y0 - y, y - y1), 0.f);
+  if (ddx * ddx + ddy * ddy <= lnv) return true;
+  const float r2 = 2.f * lnv;
+  const float c22 = r2 * (m[6] * m[6] + m[7] * m[7]) - m[8] * m[8];
+  if (!(c22 < 0.f)) return true;
+  const float ic = 1.f / c22;
+  const float c00 = r2 * (m[0] * m[0] + m[1] * m[1]) - m[2] * m[2];
+  const float c11 = r2 * (m[3] * m[3] + m[4] * m[4]) - m[5] * m[5];
+  const float c02 = r2 * (m[0] * m[6] + m[1] * m[7]) - m[2] * m[8];
+  const float c12 = r2 * (m[3] * m[6] + m[4] * m[7]) - m[5] * m[8];
+  const float cx = c02 * ic, cy = c12 * ic;
+  const float hx = sqrtf(fmaxf(cx * cx - c00 * ic, 0.f)) + 1.f;
+  const float hy = sqrtf(fmaxf(cy * cy - c11 * ic, 0.f)) + 1.f;
+  return !(cx + hx < x0 || cx - hx > x1 || cy + hy < y0 || cy - hy > y1);
+}
 
 template <int D>
 struct Gathered {
@@ -343,6 +380,64 @@ GS_INLINE void stage(float *slot, const Gathered<D> &r, int32_t idx) {
   for (int q = 0; q < R::N4; ++q) s4[q] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
 }
 
+// Forward record: the ray-splat cross product is linear in the pixel centre,
+//   (px w - u) x (py w - v) = px (v x w) + py (w x u) + (u x v),
+// so the staging lane precomputes A = v x w, B = w x u, Cc = u x v (x and y
+// components pre-scaled by sqrt(log2(e) / 2), making |s|^2 come out as
+// sigma * log2(e) directly) and smax = log2(255 opacity): a pixel hits iff
+// min(g3, g2) * log2(e) / 2 <= smax and the exponential is a bare exp2.
+template <int D>
+struct FRec {
+  static constexpr int X = 0, Y = 1, OP = 2, IDX = 3, A = 4, B = 7, CC = 10, SMAX = 13, NRM = 14,
+                       COL = 17;
+  static constexpr int NF = ((COL + D + 3) / 4) * 4;
+  static constexpr int N4 = NF / 4;
+};
+
+constexpr float kSqrtHalfLog2e = 0.84932180028801907f;  // sqrt(log2(e) / 2)
+
+template <int D>
+GS_INLINE void stage_fwd(float *slot, const Gathered<D> &r, int32_t idx) {
+  using R = FRec<D>;
+  const float *u = r.m, *v = r.m + 3, *w = r.m + 6;
+  float v_[R::NF];
+  v_[R::X] = r.xy.x;
+  v_[R::Y] = r.xy.y;
+  v_[R::OP] = r.op;
+  v_[R::IDX] = __int_as_float(idx);
+  const float k = kSqrtHalfLog2e;
+  v_[R::A + 0] = k * (v[1] * w[2] - v[2] * w[1]);
+  v_[R::A + 1] = k * (v[2] * w[0] - v[0] * w[2]);
+  v_[R::A + 2] = v[0] * w[1] - v[1] * w[0];
+  v_[R::B + 0] = k * (w[1] * u[2] - w[2] * u[1]);
+  v_[R::B + 1] = k * (w[2] * u[0] - w[0] * u[2]);
+  v_[R::B + 2] = w[0] * u[1] - w[1] * u[0];
+  v_[R::CC + 0] = k * (u[1] * v[2] - u[2] * v[1]);
+  v_[R::CC + 1] = k * (u[2] * v[0] - u[0] * v[2]);
+  v_[R::CC + 2] = u[0] * v[1] - u[1] * v[0];
+  v_[R::SMAX] = __builtin_amdgcn_logf(255.f * r.op);  // log2
+#pragma unroll
+  for (int i = 0; i < 3; ++i) v_[R::NRM + i] = r.nrm[i];
+#pragma unroll
+  for (int i = 0; i < D; ++i) v_[R::COL + i] = r.col[i];
+#pragma unroll
+  for (int i = R::COL + D; i < R::NF; ++i) v_[i] = 0.f;
+  float4 *s4 = reinterpret_cast<float4 *>(slot);
+#pragma unroll
+  for (int q = 0; q < R::N4; ++q)
+    s4[q] = make_float4(v_[4 * q], v_[4 * q + 1], v_[4 * q + 2], v_[4 * q + 3]);
+}
+
+template <int NF>
+GS_INLINE void read_f4(const float *slot, float (&v)[NF]) {
+  const float4 *s4 = reinterpret_cast<const float4 *>(slot);
+#pragma unroll
+  for (int q = 0; q < NF / 4; ++q) {
+    const float4 t = s4[q];
+    v[4 * q] = t.x; v[4 * q + 1] = t.y; v[4 * q + 2] = t.z; v[4 * q + 3] = t.w;
+  }
+}
+
 template <int D>
 GS_INLINE void read_rec(const float *slot, float (&v)[Rec<D>::NF]) {
   const float4 *s4 = reinterpret_cast<const float4 *>(slot);
@@ -386,7 +481,7 @@ GS_INLINE Hit eval_hit(const float *m, float x, float y, float op, float px, flo
 // One workgroup per tile, ceil(ts^2 / 64) waves, a 64-record queue per wave.
 template <int D>
 __global__ void __launch_bounds__(1024) fwd_kernel(RasterArgs a) {
-  using R = Rec<D>;
+  using R = FRec<D>;
   extern __shared__ float4 lds4[];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   float *q = reinterpret_cast<float *>(lds4) + (size_t)w * 64 * R::NF;
@@ -409,21 +504,32 @@ __global__ void __launch_bounds__(1024) fwd_kernel(RasterArgs a) {
   if (run) gather<D>(a, b + lane, b + lane < p.end, nxt);
   for (; run && b < p.end; b += 64) {
     if (__ballot(!done) == 0) break;
-    const int n = (int)min((int64_t)64, p.end - b);
-    stage<D>(q + lane * R::NF, nxt, (int32_t)(b + lane));
+    const bool keep = (b + lane < p.end) &&
+                      surfel_keep(nxt.m, nxt.xy.x, nxt.xy.y, nxt.op, p.x0, p.x1, p.y0, p.y1);
+    const uint64_t km = __ballot(keep);
+    const int n = __popcll(km);
+    if (keep) stage_fwd<D>(q + ballot_slot(km) * R::NF, nxt, (int32_t)(b + lane));
     wave_sync_lds();
     if (b + 64 < p.end) gather<D>(a, b + 64 + lane, b + 64 + lane < p.end, nxt);
     for (int t = 0; t < n; ++t) {
       float r[R::NF];
-      read_rec<D>(q + t * R::NF, r);
+      read_f4<R::NF>(q + t * R::NF, r);
       if (!done) {
-        const Hit h = eval_hit(r + R::M, r[R::X], r[R::Y], r[R::OP], fx, fy);
-        if (h.ok) {
-          const float nT = T * (1.f - h.alpha);
+        const float rx = fx * r[R::A] + fy * r[R::B] + r[R::CC];
+        const float ry = fx * r[R::A + 1] + fy * r[R::B + 1] + r[R::CC + 1];
+        const float rz = fx * r[R::A + 2] + fy * r[R::B + 2] + r[R::CC + 2];
+        const float iz = __builtin_amdgcn_rcpf(rz);
+        const float g3 = (rx * rx + ry * ry) * (iz * iz);
+        const float dx = r[R::X] - fx, dy = r[R::Y] - fy;
+        const float g2 = kLog2e * (dx * dx + dy * dy);
+        const float m = fminf(g3, g2);  // sigma * log2(e)
+        if (rz != 0.f && m <= r[R::SMAX]) {
+          const float alpha = fminf(kAlphaMax, r[R::OP] * __builtin_amdgcn_exp2f(-m));
+          const float nT = T * (1.f - alpha);
           if (nT <= kTMin) {
             done = true;
           } else {
-            const float vis = h.alpha * T;
+            const float vis = alpha * T;
 #pragma unroll
             for (int d = 0; d < D; ++d) col[d] += r[R::COL + d] * vis;
 #pragma unroll
@@ -525,12 +631,15 @@ __global__ void __launch_bounds__(256) bwd_kernel(RasterArgs a) {
 
   for (int64_t b1 = end; b1 > p.start; b1 -= 64) {
     const int64_t b0 = max(p.start, b1 - 64);
-    const int n = (int)(b1 - b0);
+    int n;
     {
       Gathered<D> g;
       const int64_t j = b0 + lane;
       gather<D>(a, j, j < b1, g);
-      stage<D>(q + lane * R::NF, g, (int32_t)j);
+      const bool keep = (j < b1) && surfel_keep(g.m, g.xy.x, g.xy.y, g.op, p.x0, p.x1, p.y0, p.y1);
+      const uint64_t km = __ballot(keep);
+      n = __popcll(km);
+      if (keep) stage<D>(q + ballot_slot(km) * R::NF, g, (int32_t)j);
     }
     wave_sync_lds();
     for (int t = n - 1; t >= 0; --t) {

@@ -176,6 +176,16 @@ def rasterization(
     return render_colors, render_alphas, meta
 
 
+def _rotate(R: Tensor, v: Tensor) -> Tensor:
+    """out[..., i] = sum_j R[..., i, j] v[..., h, w, j] for R [..., 3, 3] and
+    v [..., H, W, 3] -- the einsum "...ij,...hwj->...hwi" of the reference as
+    three fused multiply-adds (the einsum lowers to a K=3 GEMM)."""
+    Rt = R.transpose(-1, -2)[..., None, None, :, :]  # [..., 1, 1, 3(j), 3(i)]
+    out = v[..., 0:1] * Rt[..., 0, :]
+    out = torch.addcmul(out, v[..., 1:2], Rt[..., 1, :])
+    return torch.addcmul(out, v[..., 2:3], Rt[..., 2, :])
+
+
 def _depth_to_points(depths: Tensor, camtoworlds: Tensor, Ks: Tensor, z_depth: bool = True) -> Tensor:
     """Back-projects depth maps [..., H, W, 1] to world points (gsplat/utils.py:137-198)."""
     height, width = depths.shape[-3:-1]
@@ -187,7 +197,7 @@ def _depth_to_points(depths: Tensor, camtoworlds: Tensor, Ks: Tensor, z_depth: b
     camera_dirs = torch.nn.functional.pad(torch.stack(
         [(x - cx[..., None, None] + 0.5) / fx[..., None, None],
          (y - cy[..., None, None] + 0.5) / fy[..., None, None]], dim=-1), (0, 1), value=1.0)
-    directions = torch.einsum("...ij,...hwj->...hwi", camtoworlds[..., :3, :3], camera_dirs)
+    directions = _rotate(camtoworlds[..., :3, :3], camera_dirs)
     origins = camtoworlds[..., :3, -1]
     if not z_depth:
         directions = torch.nn.functional.normalize(directions, dim=-1)
@@ -249,7 +259,15 @@ def rasterization_2dgs(
         assert render_mode in ["D", "ED", "RGB+D", "RGB+ED"], (
             "distloss requires depth rendering, render_mode should be D, ED, RGB+D, RGB+ED, "
             f"but got {render_mode}")
-    if sh_degree is None:
+    sh_rest = None
+    if isinstance(colors, (tuple, list)):
+        # extension (as rasterization()): SH coefficients as the trainer holds
+        # them, (sh0 [N,1,3], shN [N,K-1,3]), read in place
+        assert sh_degree is not None, "a (sh0, shN) pair needs sh_degree"
+        colors, sh_rest = colors
+        assert colors.shape == (N, 1, 3) and sh_rest.shape[0] == N and sh_rest.shape[2] == 3
+        assert (sh_degree + 1) ** 2 <= 1 + sh_rest.shape[1], sh_rest.shape
+    elif sh_degree is None:
         assert (colors.dim() == 2 and colors.shape[0] == N) or (
             colors.dim() == 3 and colors.shape[:2] == (C, N)), colors.shape
     else:
@@ -270,13 +288,16 @@ def rasterization_2dgs(
     pending_isects = isect_tiles_begin(means2d, radii, depths, tile_size, tile_width, tile_height,
                                        packed=False, n_cameras=C)
 
-    if not (colors.dim() == 3 and sh_degree is None):
-        colors = colors[None] if C == 1 else colors.expand(C, *([-1] * colors.dim()))
-    if sh_degree is not None:
-        if not viewmats.requires_grad:
-            # one kernel: dirs from -R^T t, radii masking, clamp_min(sh + 0.5, 0)
-            colors = sh_colors(sh_degree, means, viewmats, colors[0], radii)
-        else:
+    if sh_degree is not None and not viewmats.requires_grad:
+        # one kernel: dirs from -R^T t, radii masking, clamp_min(sh + 0.5, 0)
+        colors = sh_colors(sh_degree, means, viewmats,
+                           colors if sh_rest is None else (colors, sh_rest), radii)
+    else:
+        if sh_rest is not None:
+            colors = torch.cat([colors, sh_rest], 1)
+        if not (colors.dim() == 3 and sh_degree is None):
+            colors = colors[None] if C == 1 else colors.expand(C, *([-1] * colors.dim()))
+        if sh_degree is not None:
             camtoworlds = torch.inverse(viewmats)
             dirs = means[None, :, :] - camtoworlds[:, None, :3, 3]
             colors = spherical_harmonics(sh_degree, dirs, colors, masks=radii > 0)
@@ -317,7 +338,6 @@ def rasterization_2dgs(
             "isect_ids": isect_ids, "flatten_ids": flatten_ids, "isect_offsets": isect_offsets,
             "width": width, "height": height, "tile_size": tile_size, "n_cameras": C,
             "render_distort": render_distort, "gradient_2dgs": densify}
-    render_normals = torch.einsum("...ij,...hwj->...hwi",
-                                  torch.linalg.inv(viewmats)[..., :3, :3], render_normals)
+    render_normals = _rotate(torch.linalg.inv(viewmats)[..., :3, :3], render_normals)
     return (render_colors, render_alphas, render_normals, render_normals_from_depth,
             render_distort, render_median, meta)

@@ -7,6 +7,12 @@ config (sh_degree 3, packed=False, classic rasterize mode, batch 1):
   statistics (gsplat/strategy/default.py:213-262) -> Adam on every parameter
   group with the trainer's learning rates and batch scaling (:235-277).
 
+model="2dgs" runs examples/simple_trainer_2dgs.py's default step instead:
+rasterization_2dgs(render_mode="RGB+D") (simple_trainer_2dgs.py:549-563), the
+same loss on the RGB channels (:590-594; normal/distortion losses are off by
+default, :149-160), and the strategy statistics from meta["gradient_2dgs"]
+(key_for_gradient, :307-311).
+
 Multi-GPU is per-camera data parallelism: every rank holds the same
 Gaussians, renders its own camera, and the Gaussian gradients are summed with
 one RCCL all-reduce per parameter group over xGMI.
@@ -21,7 +27,7 @@ import torch
 import torch.nn.functional as F
 
 from .losses import FusedAdam, l1_ssim_loss
-from .rendering import rasterization
+from .rendering import rasterization, rasterization_2dgs
 from .strategy import activate, update_state_
 
 C0 = 0.28209479177387814
@@ -98,7 +104,9 @@ class Trainer:
 
     def __init__(self, points, rgbs, viewmats, Ks, width, height, sh_degree=3, device="cuda",
                  seed=42, world_size=1, rank=0, ssim_lambda=0.2, scene_scale=1.0,
-                 fused=True):
+                 fused=True, model="3dgs"):
+        assert model in ("3dgs", "2dgs"), model
+        self.model = model
         g = torch.Generator().manual_seed(seed)  # identical on every rank (replicas)
         N = points.shape[0]
         self.device = device
@@ -148,6 +156,13 @@ class Trainer:
             scales, opac = activate(p["scales"], p["opacities"])
         else:
             scales, opac = torch.exp(p["scales"]), torch.sigmoid(p["opacities"])
+        if self.model == "2dgs":
+            rc, ra, _, _, _, _, meta = rasterization_2dgs(
+                p["means"], p["quats"], scales, opac, (p["sh0"], p["shN"]),
+                self.viewmats[ci:ci + 1], self.Ks[ci:ci + 1], self.width, self.height,
+                sh_degree=self.sh_degree, packed=False, near_plane=0.01, far_plane=1e10,
+                render_mode="RGB+D")
+            return rc[..., :3], ra, meta
         return rasterization(
             p["means"], p["quats"], scales, opac,
             (p["sh0"], p["shN"]) if self.fused else torch.cat([p["sh0"], p["shN"]], 1), self.viewmats[ci:ci + 1], self.Ks[ci:ci + 1],
@@ -157,7 +172,8 @@ class Trainer:
     def step(self, it: int):
         ci = self.camera_index(it)
         colors, alphas, meta = self.render(ci)
-        meta["means2d"].retain_grad()  # DefaultStrategy.step_pre_backward
+        if self.model == "3dgs":
+            meta["means2d"].retain_grad()  # DefaultStrategy.step_pre_backward
         gt = self.targets[ci:ci + 1]
         if self.fused:
             loss = l1_ssim_loss(colors, gt, self.ssim_lambda)
@@ -191,7 +207,7 @@ class Trainer:
     def update_state(self, meta):
         """DefaultStrategy._update_state for packed=False without the host
         sync of torch.where (default.py:213-262): same sums, masked."""
-        g = meta["means2d"].grad
+        g = meta["gradient_2dgs" if self.model == "2dgs" else "means2d"].grad
         if g is None:
             return
         if self.fused:
