@@ -1,0 +1,240 @@
+// Auxiliary per-Gaussian kernels that the reference's strategies and
+// optimizers reach through its CUDA extension even on the Triton backend
+// (SURVEY L15, §8 f4), for gfx950:
+//
+//   quat_scale_to_covar_preci_{fwd,bwd}  gsplat/cuda/csrc/QuatScaleToCovarCUDA.cu
+//       (+ quat_scale_to_covar_vjp / quat_scale_to_preci_vjp,
+//        gsplat/cuda/include/Utils.cuh:224-303) -- MCMCStrategy's position noise
+//        (gsplat/strategy/ops.py:352)
+//   relocation                           gsplat/cuda/csrc/RelocationCUDA.cu:10-44
+//       -- MCMCStrategy relocate / sample_add (gsplat/strategy/ops.py:272,314)
+//   selective adam                       gsplat/cuda/csrc/AdamCUDA.cu:12-46
+//       -- SelectiveAdam (gsplat/optimizers/selective_adam.py)
+//
+// One lane per Gaussian (per element for Adam); HBM-bound streaming kernels.
+#include "common.h"
+#include "../../include/gsplat_hip.h"
+
+namespace gs {
+namespace auxk {
+
+// ---------------------------------------------------- covariance / precision
+// Row-major R S^2 R^T (covar) and R S^-2 R^T (preci); triu = [xx, xy, xz, yy, yz, zz].
+__global__ void __launch_bounds__(256)
+covar_preci_fwd_kernel(int64_t N, const float *__restrict__ quats,
+                       const float *__restrict__ scales, int triu, float *__restrict__ covars,
+                       float *__restrict__ precis) {
+  const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  const float4 q = *reinterpret_cast<const float4 *>(quats + 4 * n);
+  const M3 R = quat_to_rotmat(q.x, q.y, q.z, q.w);
+  const float s[3] = {scales[3 * n], scales[3 * n + 1], scales[3 * n + 2]};
+  for (int which = 0; which < 2; ++which) {
+    float *out = which ? precis : covars;
+    if (!out) continue;
+    float w[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) w[k] = which ? 1.f / (s[k] * s[k]) : s[k] * s[k];
+    float c[3][3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int j = 0; j < 3; ++j)
+        c[i][j] = R.m[i][0] * w[0] * R.m[j][0] + R.m[i][1] * w[1] * R.m[j][1] +
+                  R.m[i][2] * w[2] * R.m[j][2];
+    if (triu) {
+      float *o = out + 6 * n;
+      o[0] = c[0][0]; o[1] = c[0][1]; o[2] = c[0][2];
+      o[3] = c[1][1]; o[4] = c[1][2]; o[5] = c[2][2];
+    } else {
+      float *o = out + 9 * n;
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) o[3 * i + j] = c[i][j];
+    }
+  }
+}
+
+// d/d(q, s) of C = (R S)(R S)^T with S = diag(s) (covar) or diag(1/s) (preci):
+// v_M = (G + G^T) M, v_R = v_M S, v_s_k from v_M (Utils.cuh:224-303).
+GS_INLINE void sym_vjp(const M3 &R, const float sk[3], bool inv, const float G[3][3], float4 q,
+                       float vq[4], float vs[3]) {
+  float S[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) S[k] = inv ? 1.f / sk[k] : sk[k];
+  float vM[3][3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      float a = 0.f;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) a += (G[i][k] + G[k][i]) * R.m[k][j] * S[j];
+      vM[i][j] = a;
+    }
+  M3 vR;
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) vR.m[i][j] = vM[i][j] * S[j];
+  float dq[4];
+  quat_to_rotmat_vjp(q.x, q.y, q.z, q.w, vR, dq);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) vq[k] += dq[k];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const float d = R.m[0][j] * vM[0][j] + R.m[1][j] * vM[1][j] + R.m[2][j] * vM[2][j];
+    vs[j] += inv ? -S[j] * S[j] * d : d;
+  }
+}
+
+__global__ void __launch_bounds__(256)
+covar_preci_bwd_kernel(int64_t N, const float *__restrict__ quats,
+                       const float *__restrict__ scales, int triu,
+                       const float *__restrict__ v_covars, const float *__restrict__ v_precis,
+                       float *__restrict__ v_quats, float *__restrict__ v_scales) {
+  const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  const float4 q = *reinterpret_cast<const float4 *>(quats + 4 * n);
+  const M3 R = quat_to_rotmat(q.x, q.y, q.z, q.w);
+  const float s[3] = {scales[3 * n], scales[3 * n + 1], scales[3 * n + 2]};
+  float vq[4] = {0.f, 0.f, 0.f, 0.f}, vs[3] = {0.f, 0.f, 0.f};
+  for (int which = 0; which < 2; ++which) {
+    const float *g = which ? v_precis : v_covars;
+    if (!g) continue;
+    float G[3][3];
+    if (triu) {  // off-diagonal gradients split over the symmetric pair
+      const float *t = g + 6 * n;
+      G[0][0] = t[0]; G[1][1] = t[3]; G[2][2] = t[5];
+      G[0][1] = G[1][0] = 0.5f * t[1];
+      G[0][2] = G[2][0] = 0.5f * t[2];
+      G[1][2] = G[2][1] = 0.5f * t[4];
+    } else {
+      const float *t = g + 9 * n;
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) G[i][j] = t[3 * i + j];
+    }
+    sym_vjp(R, s, which == 1, G, q, vq, vs);
+  }
+  *reinterpret_cast<float4 *>(v_quats + 4 * n) = make_float4(vq[0], vq[1], vq[2], vq[3]);
+  v_scales[3 * n] = vs[0];
+  v_scales[3 * n + 1] = vs[1];
+  v_scales[3 * n + 2] = vs[2];
+}
+
+// ------------------------------------------------------------- relocation
+// MCMC relocation (RelocationCUDA.cu:10-44): o' = 1 - (1 - o)^(1/n),
+// s' = s * o / sum_{i=1..n} sum_{k<i} C(i-1, k) (-1)^k o'^(k+1) / sqrt(k+1).
+__global__ void __launch_bounds__(256)
+relocation_kernel(int64_t N, const float *__restrict__ opacities, const float *__restrict__ scales,
+                  const int32_t *__restrict__ ratios, const float *__restrict__ binoms, int n_max,
+                  float *__restrict__ new_opacities, float *__restrict__ new_scales) {
+  const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  const int r = ratios[n];
+  const float o = opacities[n];
+  const float no = 1.f - powf(1.f - o, 1.f / (float)r);
+  float denom = 0.f;
+  for (int i = 1; i <= r; ++i) {
+    float pk = no;  // no^(k+1)
+    for (int k = 0; k <= i - 1; ++k) {
+      const float term = ((k & 1) ? -1.f : 1.f) / sqrtf((float)(k + 1)) * pk;
+      denom += binoms[(i - 1) * n_max + k] * term;
+      pk *= no;
+    }
+  }
+  new_opacities[n] = no;
+  const float coeff = o / denom;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) new_scales[3 * n + k] = coeff * scales[3 * n + k];
+}
+
+// -------------------------------------------------------- selective adam
+// The reference's fused Adam (AdamCUDA.cu:12-46): no bias correction,
+// m = b1 m + (1-b1) g, v = b2 v + (1-b2) g^2, p -= lr m / (sqrt(v) + eps);
+// rows whose visibility is false are untouched.  A row is the `row`
+// consecutive elements of one Gaussian.
+__global__ void __launch_bounds__(256)
+selective_adam_kernel(int64_t n_rows, int64_t row, float *__restrict__ param,
+                      const float *__restrict__ grad, float *__restrict__ exp_avg,
+                      float *__restrict__ exp_avg_sq, const uint8_t *__restrict__ visible,
+                      float lr, float b1, float b2, float eps) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n_rows * row) return;
+  if (visible && !visible[e / row]) return;
+  const float g = grad[e];
+  const float m = b1 * exp_avg[e] + (1.f - b1) * g;
+  const float v = b2 * exp_avg_sq[e] + (1.f - b2) * g * g;
+  param[e] += -lr * m / (sqrtf(v) + eps);
+  exp_avg[e] = m;
+  exp_avg_sq[e] = v;
+}
+
+}  // namespace auxk
+}  // namespace gs
+
+using namespace gs;
+
+extern "C" int gsplat_hip_quat_scale_to_covar_preci_fwd(int64_t N, const float *quats,
+                                                        const float *scales, int triu,
+                                                        float *covars, float *precis,
+                                                        void *stream) {
+  GS_REQUIRE(N >= 0, "quat_scale_to_covar_preci_fwd: negative N");
+  if (N == 0) return 0;
+  GS_REQUIRE(quats && scales && (covars || precis), "quat_scale_to_covar_preci_fwd: null pointer");
+  GS_REQUIRE(((uintptr_t)quats & 15) == 0,
+             "quat_scale_to_covar_preci_fwd: quats must be 16-B aligned");
+  hipLaunchKernelGGL(auxk::covar_preci_fwd_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, N, quats, scales, triu, covars, precis);
+  GS_CHECK_LAUNCH("quat_scale_to_covar_preci_fwd");
+  return 0;
+}
+
+extern "C" int gsplat_hip_quat_scale_to_covar_preci_bwd(int64_t N, const float *quats,
+                                                        const float *scales, int triu,
+                                                        const float *v_covars,
+                                                        const float *v_precis, float *v_quats,
+                                                        float *v_scales, void *stream) {
+  GS_REQUIRE(N >= 0, "quat_scale_to_covar_preci_bwd: negative N");
+  if (N == 0) return 0;
+  GS_REQUIRE(quats && scales && v_quats && v_scales, "quat_scale_to_covar_preci_bwd: null pointer");
+  GS_REQUIRE(((uintptr_t)quats & 15) == 0 && ((uintptr_t)v_quats & 15) == 0,
+             "quat_scale_to_covar_preci_bwd: quats / v_quats must be 16-B aligned");
+  hipLaunchKernelGGL(auxk::covar_preci_bwd_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, N, quats, scales, triu, v_covars, v_precis, v_quats,
+                     v_scales);
+  GS_CHECK_LAUNCH("quat_scale_to_covar_preci_bwd");
+  return 0;
+}
+
+extern "C" int gsplat_hip_relocation(int64_t N, const float *opacities, const float *scales,
+                                     const int32_t *ratios, const float *binoms, int n_max,
+                                     float *new_opacities, float *new_scales, void *stream) {
+  GS_REQUIRE(N >= 0 && n_max >= 1, "relocation: bad sizes");
+  if (N == 0) return 0;
+  GS_REQUIRE(opacities && scales && ratios && binoms && new_opacities && new_scales,
+             "relocation: null pointer");
+  hipLaunchKernelGGL(auxk::relocation_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, N, opacities, scales, ratios, binoms, n_max,
+                     new_opacities, new_scales);
+  GS_CHECK_LAUNCH("relocation");
+  return 0;
+}
+
+extern "C" int gsplat_hip_selective_adam(int64_t n_rows, int64_t row, float *param,
+                                         const float *grad, float *exp_avg, float *exp_avg_sq,
+                                         const uint8_t *visible, float lr, float beta1,
+                                         float beta2, float eps, void *stream) {
+  GS_REQUIRE(n_rows >= 0 && row >= 1, "selective_adam: bad sizes");
+  const int64_t n = n_rows * row;
+  if (n == 0) return 0;
+  GS_REQUIRE(param && grad && exp_avg && exp_avg_sq, "selective_adam: null pointer");
+  hipLaunchKernelGGL(auxk::selective_adam_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, n_rows, row, param, grad, exp_avg, exp_avg_sq, visible,
+                     lr, beta1, beta2, eps);
+  GS_CHECK_LAUNCH("selective_adam");
+  return 0;
+}

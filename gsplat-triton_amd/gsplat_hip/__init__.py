@@ -13,6 +13,7 @@ from ._wrapper import (
     rasterize_to_pixels,
     spherical_harmonics,
 )
+from ._wrapper_aux import SelectiveAdam, adam, compute_relocation, quat_scale_to_covar_preci
 from ._wrapper_2dgs import fully_fused_projection_2dgs, rasterize_to_pixels_2dgs
 from .rendering import depth_to_normal, rasterization, rasterization_2dgs
 
@@ -27,5 +28,9 @@ __all__ = [
     "rasterize_to_pixels_2dgs",
     "rasterization_2dgs",
     "depth_to_normal",
+    "quat_scale_to_covar_preci",
+    "compute_relocation",
+    "adam",
+    "SelectiveAdam",
 ]
 __version__ = "0.1.0"

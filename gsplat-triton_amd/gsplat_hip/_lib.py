@@ -12,7 +12,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GSPLAT_HIP_LIB", os.path.join(_HERE, "libgsplat_hip.so"))
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 _p = ctypes.c_void_p
 _i32 = ctypes.c_int
@@ -81,6 +81,10 @@ _SIGS = {
                                              _p, _p, _p, _p, _p, _p, _p, _i64, _p, _p, _p, _p,
                                              _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p,
                                              _p, _i64, _p]),
+    "gsplat_hip_quat_scale_to_covar_preci_fwd": (_i32, [_i64, _p, _p, _i32, _p, _p, _p]),
+    "gsplat_hip_quat_scale_to_covar_preci_bwd": (_i32, [_i64, _p, _p, _i32, _p, _p, _p, _p, _p]),
+    "gsplat_hip_relocation": (_i32, [_i64, _p, _p, _p, _p, _i32, _p, _p, _p]),
+    "gsplat_hip_selective_adam": (_i32, [_i64, _i64, _p, _p, _p, _p, _p, _f, _f, _f, _f, _p]),
 }
 
 EXPORTED = tuple(_SIGS)

@@ -375,6 +375,39 @@ int gsplat_hip_rasterize_2dgs_bwd(
     float *v_opacities, float *v_normals, float *v_densify, float *v_means2d_abs,
     void *workspace, int64_t workspace_bytes, void *stream);
 
+/* ---------------------------------------------------------------------------
+ * Auxiliary kernels reached by the reference's strategies / optimizers through
+ * its CUDA extension on every backend.
+ *
+ * Replaces quat_scale_to_covar_preci_fwd/bwd (gsplat/cuda/csrc/QuatScaleToCovarCUDA.cu,
+ * gsplat/cuda/_wrapper.py:111-142,651-689; used by MCMCStrategy,
+ * gsplat/strategy/ops.py:352).  quats[N,4] (16-B aligned), scales[N,3] ->
+ * covars / precis [N,3,3] or, with triu, [N,6] (xx, xy, xz, yy, yz, zz);
+ * either output may be NULL.  Backward: v_quats[N,4], v_scales[N,3]. */
+int gsplat_hip_quat_scale_to_covar_preci_fwd(int64_t N, const float *quats, const float *scales,
+                                             int triu, float *covars, float *precis,
+                                             void *stream);
+int gsplat_hip_quat_scale_to_covar_preci_bwd(int64_t N, const float *quats, const float *scales,
+                                             int triu, const float *v_covars,
+                                             const float *v_precis, float *v_quats,
+                                             float *v_scales, void *stream);
+
+/* Replaces relocation (gsplat/cuda/csrc/RelocationCUDA.cu:10-44, gsplat/relocation.py:10-51;
+ * MCMC relocate / sample_add, gsplat/strategy/ops.py:272,314).
+ * opacities[N], scales[N,3], ratios i32[N] (clamped to [1, n_max] by the
+ * caller), binoms[n_max,n_max] -> new_opacities[N], new_scales[N,3]. */
+int gsplat_hip_relocation(int64_t N, const float *opacities, const float *scales,
+                          const int32_t *ratios, const float *binoms, int n_max,
+                          float *new_opacities, float *new_scales, void *stream);
+
+/* Replaces adam (gsplat/cuda/csrc/AdamCUDA.cu:12-46, used by SelectiveAdam,
+ * gsplat/optimizers/selective_adam.py): the reference's update without bias
+ * correction on the rows (`row` consecutive elements each) whose visible[] is
+ * non-zero; visible may be NULL (every row). */
+int gsplat_hip_selective_adam(int64_t n_rows, int64_t row, float *param, const float *grad,
+                              float *exp_avg, float *exp_avg_sq, const uint8_t *visible,
+                              float lr, float beta1, float beta2, float eps, void *stream);
+
 #ifdef __cplusplus
 }
 #endif
