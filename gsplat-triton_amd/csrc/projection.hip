@@ -88,13 +88,23 @@ struct ProjFwdArgs {
   const float *means, *quats, *scales, *viewmats, *Ks;
   int32_t *radii;
   float *means2d, *depths, *conics, *comps;  // comps may be null
+  // packed mode (projection_ewa_3dgs_packed_fwd): per-block counts of kept
+  // (camera, Gaussian) pairs, then their exclusive prefix, in (c, n) order
+  int64_t *block_cnt;
+  const int64_t *block_off;
+  int64_t *camera_ids, *gaussian_ids;
 };
 
+// MODE 0: dense [C, N] outputs.  MODE 1: count the kept pairs per block.
+// MODE 2: write the kept pairs packed at block_off[block] + rank in block.
+template <int MODE>
 __global__ void __launch_bounds__(256) projection_fwd_kernel(ProjFwdArgs a) {
   const int c = blockIdx.y;
-  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  const int n_raw = blockIdx.x * blockDim.x + threadIdx.x;
   const Cam k = load_cam(a.viewmats, a.Ks, c);
-  if (n >= a.N) return;
+  if (MODE == 0 && n_raw >= a.N) return;
+  const bool in = n_raw < a.N;
+  const int n = in ? n_raw : a.N - 1;  // packed modes: every lane reaches the block scan
   const float4 q = *reinterpret_cast<const float4 *>(a.quats + 4 * (size_t)n);
   const float *sp = a.scales + 3 * (size_t)n;
   const float *mp = a.means + 3 * (size_t)n;
@@ -109,8 +119,8 @@ __global__ void __launch_bounds__(256) projection_fwd_kernel(ProjFwdArgs a) {
   const M3 Cc = mul(mul(k.R, C3), transpose(k.R));
 
   const size_t idx = (size_t)c * a.N + n;
-  a.depths[idx] = mc[2];
-  bool keep = (mc[2] > a.near_plane) & (mc[2] < a.far_plane);
+  if (MODE == 0) a.depths[idx] = mc[2];
+  bool keep = in & (mc[2] > a.near_plane) & (mc[2] < a.far_plane);
 
   ProjOut p = persp(mc[0], mc[1], mc[2], Cc, k, a.W, a.H);
   // add blur (util_kernels.py:64-94)
@@ -125,14 +135,80 @@ __global__ void __launch_bounds__(256) projection_fwd_kernel(ProjFwdArgs a) {
   keep &= (r > a.radius_clip) & (p.mx + r > 0.f) & (p.mx - r < (float)a.W) &
           (p.my + r > 0.f) & (p.my - r < (float)a.H);
 
-  a.radii[idx] = keep ? (int32_t)r : 0;
-  float2 m2d = keep ? make_float2(p.mx, p.my) : make_float2(0.f, 0.f);
-  *reinterpret_cast<float2 *>(a.means2d + 2 * idx) = m2d;
-  float *cn = a.conics + 3 * idx;
-  cn[0] = keep ? inv_det * byy : 0.f;
-  cn[1] = keep ? -inv_det * p.cxy : 0.f;
-  cn[2] = keep ? inv_det * bxx : 0.f;
-  if (a.comps) a.comps[idx] = keep ? sqrtf(fmaxf(det0 / det, 0.f)) : 0.f;
+  if (MODE == 0) {
+    a.radii[idx] = keep ? (int32_t)r : 0;
+    float2 m2d = keep ? make_float2(p.mx, p.my) : make_float2(0.f, 0.f);
+    *reinterpret_cast<float2 *>(a.means2d + 2 * idx) = m2d;
+    float *cn = a.conics + 3 * idx;
+    cn[0] = keep ? inv_det * byy : 0.f;
+    cn[1] = keep ? -inv_det * p.cxy : 0.f;
+    cn[2] = keep ? inv_det * bxx : 0.f;
+    if (a.comps) a.comps[idx] = keep ? sqrtf(fmaxf(det0 / det, 0.f)) : 0.f;
+    return;
+  }
+  // packed: rank of this pair among the block's kept pairs (wave ballots)
+  __shared__ int wave_cnt[4];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const uint64_t m = __ballot(keep);
+  if (lane == 0) wave_cnt[wid] = __popcll(m);
+  __syncthreads();
+  const int64_t blk = (int64_t)c * gridDim.x + blockIdx.x;
+  if (MODE == 1) {
+    if (threadIdx.x == 0) a.block_cnt[blk] = wave_cnt[0] + wave_cnt[1] + wave_cnt[2] + wave_cnt[3];
+    return;
+  }
+  if (!keep) return;
+  int before = 0;
+  for (int w = 0; w < wid; ++w) before += wave_cnt[w];
+  const int64_t o = a.block_off[blk] + before +
+                    __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                              __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+  a.camera_ids[o] = c;
+  a.gaussian_ids[o] = n;
+  a.radii[o] = (int32_t)r;
+  *reinterpret_cast<float2 *>(a.means2d + 2 * o) = make_float2(p.mx, p.my);
+  a.depths[o] = mc[2];
+  float *cn = a.conics + 3 * o;
+  cn[0] = inv_det * byy;
+  cn[1] = -inv_det * p.cxy;
+  cn[2] = inv_det * bxx;
+  if (a.comps) a.comps[o] = sqrtf(fmaxf(det0 / det, 0.f));
+}
+
+// Exclusive scan of the packed per-block counts in place, total -> total[0]
+// (one 1024-lane workgroup walking the C * blocks_per_row counts).
+__global__ void __launch_bounds__(1024) packed_scan_kernel(int64_t nb, int64_t *cnt,
+                                                           int64_t *total) {
+  __shared__ int64_t wave_tot[16];
+  __shared__ int64_t chunk_tot;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  int64_t carry = 0;
+  for (int64_t base = 0; base < nb; base += 1024) {
+    const int64_t i = base + threadIdx.x;
+    const int64_t v = i < nb ? cnt[i] : 0;
+    int64_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int64_t y = __shfl_up(x, o, 64);
+      if (lane >= o) x += y;
+    }
+    if (lane == 63) wave_tot[wid] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int64_t run = 0;
+      for (int w = 0; w < 16; ++w) {
+        const int64_t t = wave_tot[w];
+        wave_tot[w] = run;
+        run += t;
+      }
+      chunk_tot = run;
+    }
+    __syncthreads();
+    if (i < nb) cnt[i] = carry + wave_tot[wid] + x - v;
+    carry += chunk_tot;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) total[0] = carry;
 }
 
 struct ProjBwdArgs {
@@ -144,14 +220,31 @@ struct ProjBwdArgs {
   const float *v_means2d, *v_depths, *v_conics, *v_comps;      // v_depths, v_comps may be null
   float *v_means, *v_quats, *v_scales, *v_viewmats;            // v_viewmats may be null
   int store_mode;  // 1: C == 1, every lane stores its own row (no atomics, no memset)
+  // packed inputs (projection_ewa_3dgs_packed_bwd): entry e is the pair
+  // (camera_ids[e], gaussian_ids[e]); sparse: per-entry gradient rows [nnz, .]
+  const int64_t *camera_ids, *gaussian_ids;
+  int64_t nnz;
+  int sparse;
 };
 
 __global__ void __launch_bounds__(256) projection_bwd_kernel(ProjBwdArgs a) {
-  const int c = blockIdx.y;
-  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool packed = a.camera_ids != nullptr;
+  int c, n;
+  size_t idx;
+  bool valid;
+  if (packed) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    valid = e < a.nnz;
+    c = valid ? (int)a.camera_ids[e] : 0;
+    n = valid ? (int)a.gaussian_ids[e] : 0;
+    idx = valid ? (size_t)e : 0;
+  } else {
+    c = blockIdx.y;
+    n = blockIdx.x * blockDim.x + threadIdx.x;
+    idx = (size_t)c * a.N + n;
+    valid = (n < a.N) && (a.radii[idx] > 0);
+  }
   const Cam k = load_cam(a.viewmats, a.Ks, c);
-  const size_t idx = (size_t)c * a.N + n;
-  const bool valid = (n < a.N) && (a.radii[idx] > 0);
 
   float vR[3][3] = {{0.f}}, vt[3] = {0.f, 0.f, 0.f};
   float vm[3] = {0.f, 0.f, 0.f}, vq[4] = {0.f, 0.f, 0.f, 0.f}, vs[3] = {0.f, 0.f, 0.f};
@@ -261,7 +354,15 @@ __global__ void __launch_bounds__(256) projection_bwd_kernel(ProjBwdArgs a) {
       vs[j] = Rq.m[0][j] * dRS.m[0][j] + Rq.m[1][j] * dRS.m[1][j] + Rq.m[2][j] * dRS.m[2][j];
   }
 
-  if (a.store_mode) {
+  if (a.sparse) {
+    if (valid) {  // COO values, one row per packed entry
+      float *o = a.v_means + 3 * idx;
+      o[0] = vm[0]; o[1] = vm[1]; o[2] = vm[2];
+      *reinterpret_cast<float4 *>(a.v_quats + 4 * idx) = make_float4(vq[0], vq[1], vq[2], vq[3]);
+      o = a.v_scales + 3 * idx;
+      o[0] = vs[0]; o[1] = vs[1]; o[2] = vs[2];
+    }
+  } else if (a.store_mode) {
     if (n < a.N) {
       float *o = a.v_means + 3 * (size_t)n;
       o[0] = vm[0]; o[1] = vm[1]; o[2] = vm[2];
@@ -278,7 +379,29 @@ __global__ void __launch_bounds__(256) projection_bwd_kernel(ProjBwdArgs a) {
     for (int j = 0; j < 3; ++j) atomic_add_f32(a.v_scales + 3 * (size_t)n + j, vs[j]);
   }
 
-  if (a.v_viewmats) {
+  if (a.v_viewmats && packed) {
+    // entries are camera-major: a wave spans one camera except at camera
+    // boundaries, where its lanes add their partials one by one
+    const int lane = threadIdx.x & 63;
+    float v[12];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+#pragma unroll
+      for (int j = 0; j < 3; ++j) v[i * 4 + j] = vR[i][j];
+      v[i * 4 + 3] = vt[i];
+    }
+    const int c0 = __shfl(c, 0, 64);
+    if (__ballot(valid && c != c0) == 0) {
+#pragma unroll
+      for (int e = 0; e < 12; ++e) v[e] = wave_sum(v[e]);
+      if (lane == 0)
+        for (int e = 0; e < 12; ++e)
+          if (v[e] != 0.f) atomic_add_f32(a.v_viewmats + c0 * 16 + e, v[e]);
+    } else if (valid) {
+      for (int e = 0; e < 12; ++e)
+        if (v[e] != 0.f) atomic_add_f32(a.v_viewmats + c * 16 + e, v[e]);
+    }
+  } else if (a.v_viewmats) {
     // block reduction of the 12 viewmat partials: wave butterfly, then LDS
     __shared__ float red[4][12];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -323,7 +446,7 @@ extern "C" int gsplat_hip_projection_fwd(int C, int N, const float *means, const
   ProjFwdArgs a{C, N, width, height, eps2d, near_plane, far_plane, radius_clip,
                 means, quats, scales, viewmats, Ks, radii, means2d, depths, conics, compensations};
   dim3 grid((N + 255) / 256, C);
-  hipLaunchKernelGGL(projection_fwd_kernel, grid, dim3(256), 0, (hipStream_t)stream, a);
+  hipLaunchKernelGGL(projection_fwd_kernel<0>, grid, dim3(256), 0, (hipStream_t)stream, a);
   GS_CHECK_LAUNCH("projection_fwd");
   return 0;
 }
@@ -361,5 +484,105 @@ extern "C" int gsplat_hip_projection_bwd(
   dim3 grid((N + 255) / 256, C);
   hipLaunchKernelGGL(projection_bwd_kernel, grid, dim3(256), 0, st, a);
   GS_CHECK_LAUNCH("projection_bwd");
+  return 0;
+}
+
+// ------------------------------------------------------------------ packed --
+// projection_ewa_3dgs_packed_fwd (gsplat/cuda/csrc/ProjectionEWA3DGSPacked.cu:17-244):
+// a counting pass, a scan of the per-block counts, and a pass that recomputes
+// and writes the kept (camera, Gaussian) pairs in (camera, Gaussian) order.
+extern "C" int64_t gsplat_hip_projection_packed_workspace_bytes(int C, int N) {
+  const int64_t nb = (int64_t)C * ((N + 255) / 256);
+  return (nb + 1) * (int64_t)sizeof(int64_t);
+}
+
+extern "C" int gsplat_hip_projection_packed_count(int C, int N, const float *means,
+                                                  const float *quats, const float *scales,
+                                                  const float *viewmats, const float *Ks,
+                                                  int width, int height, float eps2d,
+                                                  float near_plane, float far_plane,
+                                                  float radius_clip, void *workspace,
+                                                  int64_t *nnz_device, void *stream) {
+  GS_REQUIRE(C >= 0 && N >= 0, "projection_packed_count: negative sizes C=%d N=%d", C, N);
+  hipStream_t st = (hipStream_t)stream;
+  if (C == 0 || N == 0) {
+    GS_HIP(hipMemsetAsync(nnz_device, 0, sizeof(int64_t), st));
+    return 0;
+  }
+  GS_REQUIRE(means && quats && scales && viewmats && Ks && workspace && nnz_device,
+             "projection_packed_count: null pointer argument");
+  GS_REQUIRE(((uintptr_t)quats & 15) == 0, "projection_packed_count: quats must be 16-B aligned");
+  ProjFwdArgs a{C, N, width, height, eps2d, near_plane, far_plane, radius_clip,
+                means, quats, scales, viewmats, Ks, nullptr, nullptr, nullptr, nullptr, nullptr};
+  a.block_cnt = reinterpret_cast<int64_t *>(workspace);
+  dim3 grid((N + 255) / 256, C);
+  hipLaunchKernelGGL(projection_fwd_kernel<1>, grid, dim3(256), 0, st, a);
+  hipLaunchKernelGGL(packed_scan_kernel, dim3(1), dim3(1024), 0, st,
+                     (int64_t)grid.x * grid.y, a.block_cnt, nnz_device);
+  GS_CHECK_LAUNCH("projection_packed_count");
+  return 0;
+}
+
+extern "C" int gsplat_hip_projection_packed_fwd(
+    int C, int N, const float *means, const float *quats, const float *scales,
+    const float *viewmats, const float *Ks, int width, int height, float eps2d,
+    float near_plane, float far_plane, float radius_clip, const void *workspace,
+    int64_t *camera_ids, int64_t *gaussian_ids, int32_t *radii, float *means2d, float *depths,
+    float *conics, float *compensations, void *stream) {
+  GS_REQUIRE(C >= 0 && N >= 0, "projection_packed_fwd: negative sizes C=%d N=%d", C, N);
+  if (C == 0 || N == 0) return 0;
+  GS_REQUIRE(means && quats && scales && viewmats && Ks && workspace && camera_ids &&
+                 gaussian_ids && radii && means2d && depths && conics,
+             "projection_packed_fwd: null pointer argument");
+  GS_REQUIRE(((uintptr_t)quats & 15) == 0 && ((uintptr_t)means2d & 7) == 0,
+             "projection_packed_fwd: quats must be 16-B aligned, means2d 8-B aligned");
+  ProjFwdArgs a{C, N, width, height, eps2d, near_plane, far_plane, radius_clip,
+                means, quats, scales, viewmats, Ks, radii, means2d, depths, conics, compensations};
+  a.block_off = reinterpret_cast<const int64_t *>(workspace);
+  a.camera_ids = camera_ids;
+  a.gaussian_ids = gaussian_ids;
+  dim3 grid((N + 255) / 256, C);
+  hipLaunchKernelGGL(projection_fwd_kernel<2>, grid, dim3(256), 0, (hipStream_t)stream, a);
+  GS_CHECK_LAUNCH("projection_packed_fwd");
+  return 0;
+}
+
+// projection_ewa_3dgs_packed_bwd (ProjectionEWA3DGSPacked.cu:348-630): one lane
+// per packed entry; dense [N, .] gradients by atomics, or (sparse_grad) one
+// row per entry for the COO gradients of _wrapper.py:1127-1170.
+extern "C" int gsplat_hip_projection_packed_bwd(
+    int C, int N, int64_t nnz, const float *means, const float *quats, const float *scales,
+    const float *viewmats, const float *Ks, int width, int height, float eps2d,
+    const int64_t *camera_ids, const int64_t *gaussian_ids, const float *conics,
+    const float *compensations, const float *v_means2d, const float *v_depths,
+    const float *v_conics, const float *v_compensations, int sparse_grad, float *v_means,
+    float *v_quats, float *v_scales, float *v_viewmats, void *stream) {
+  GS_REQUIRE(C >= 0 && N >= 0 && nnz >= 0, "projection_packed_bwd: negative sizes");
+  hipStream_t st = (hipStream_t)stream;
+  if (v_viewmats && C > 0) GS_HIP(hipMemsetAsync(v_viewmats, 0, sizeof(float) * 16 * C, st));
+  if (!sparse_grad && N > 0) {
+    GS_HIP(hipMemsetAsync(v_means, 0, sizeof(float) * 3 * N, st));
+    GS_HIP(hipMemsetAsync(v_quats, 0, sizeof(float) * 4 * N, st));
+    GS_HIP(hipMemsetAsync(v_scales, 0, sizeof(float) * 3 * N, st));
+  }
+  if (nnz == 0) return 0;
+  GS_REQUIRE(!compensations == !v_compensations,
+             "projection_packed_bwd: compensations and v_compensations must both be given or "
+             "both null");
+  GS_REQUIRE(camera_ids && gaussian_ids && conics && v_means2d && v_conics && v_means && v_quats &&
+                 v_scales,
+             "projection_packed_bwd: null pointer argument");
+  GS_REQUIRE(((uintptr_t)quats & 15) == 0 && ((uintptr_t)v_quats & 15) == 0,
+             "projection_packed_bwd: quats / v_quats must be 16-B aligned");
+  ProjBwdArgs a{C, N, width, height, eps2d, means, quats, scales, viewmats, Ks, nullptr, conics,
+                compensations, v_means2d, v_depths, v_conics, v_compensations, v_means, v_quats,
+                v_scales, v_viewmats, 0};
+  a.camera_ids = camera_ids;
+  a.gaussian_ids = gaussian_ids;
+  a.nnz = nnz;
+  a.sparse = sparse_grad;
+  hipLaunchKernelGGL(projection_bwd_kernel, dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, st,
+                     a);
+  GS_CHECK_LAUNCH("projection_packed_bwd");
   return 0;
 }

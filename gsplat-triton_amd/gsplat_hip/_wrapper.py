@@ -151,6 +151,86 @@ class _FullyFusedProjection(torch.autograd.Function):
                 v_viewmats, None, None, None, None, None, None, None, None, None, None)
 
 
+class _FullyFusedProjectionPacked(torch.autograd.Function):
+    """Projects Gaussians to 2D, packed [nnz] outputs
+    (gsplat/cuda/_wrapper.py:998-1190; broken on the Triton backend).
+    One host read of nnz, as the reference's cumsum(...)[-1].item()."""
+
+    @staticmethod
+    def forward(ctx, means, covars, quats, scales, viewmats, Ks, width, height, eps2d,
+                near_plane, far_plane, radius_clip, sparse_grad, calc_compensations,
+                camera_model="pinhole"):
+        if camera_model != "pinhole":
+            raise NotImplementedError(f"Unsupported camera model: {camera_model}")
+        assert covars is None and quats is not None and scales is not None
+        means, quats, scales, viewmats, Ks = (_f32c(x) for x in (means, quats, scales, viewmats, Ks))
+        quats = _aligned16(quats)
+        _dev_check(means, quats, scales, viewmats, Ks)
+        C, N = viewmats.shape[0], means.shape[0]
+        dev = means.device
+        ws = torch.empty(max(int(_lib.query("gsplat_hip_projection_packed_workspace_bytes", C, N))
+                             // 8, 1), dtype=torch.int64, device=dev)
+        nnz_dev = torch.empty(1, dtype=torch.int64, device=dev)
+        args = (_ptr(means), _ptr(quats), _ptr(scales), _ptr(viewmats), _ptr(Ks), int(width),
+                int(height), float(eps2d), float(near_plane), float(far_plane), float(radius_clip))
+        _lib.call("gsplat_hip_projection_packed_count", C, N, *args, _ptr(ws), _ptr(nnz_dev),
+                  _stream())
+        nnz = int(nnz_dev.item())
+        camera_ids = torch.empty(nnz, dtype=torch.int64, device=dev)
+        gaussian_ids = torch.empty(nnz, dtype=torch.int64, device=dev)
+        radii = torch.empty(nnz, dtype=torch.int32, device=dev)
+        means2d = torch.empty((nnz, 2), device=dev)
+        depths = torch.empty(nnz, device=dev)
+        conics = torch.empty((nnz, 3), device=dev)
+        comps = torch.empty(nnz, device=dev) if calc_compensations else None
+        _lib.call("gsplat_hip_projection_packed_fwd", C, N, *args, _ptr(ws), _ptr(camera_ids),
+                  _ptr(gaussian_ids), _ptr(radii), _ptr(means2d), _ptr(depths), _ptr(conics),
+                  _ptr(comps), _stream())
+        ctx.save_for_backward(camera_ids, gaussian_ids, means, quats, scales, viewmats, Ks,
+                              conics, comps)
+        ctx.width, ctx.height, ctx.eps2d = int(width), int(height), float(eps2d)
+        ctx.sparse_grad = sparse_grad
+        ctx.mark_non_differentiable(camera_ids, gaussian_ids, radii)
+        return camera_ids, gaussian_ids, radii, means2d, depths, conics, comps
+
+    @staticmethod
+    def backward(ctx, v_camera_ids, v_gaussian_ids, v_radii, v_means2d, v_depths, v_conics,
+                 v_compensations):
+        camera_ids, gaussian_ids, means, quats, scales, viewmats, Ks, conics, comps = \
+            ctx.saved_tensors
+        C, N, nnz = viewmats.shape[0], means.shape[0], camera_ids.numel()
+        dev = means.device
+
+        def g(t, shape):
+            return torch.zeros(shape, device=dev) if t is None else _f32c(t)
+
+        v_means2d = g(v_means2d, (nnz, 2))
+        v_conics = g(v_conics, (nnz, 3))
+        v_depths = None if v_depths is None else _f32c(v_depths)
+        v_comps = g(v_compensations, (nnz,)) if comps is not None else None
+        rows = nnz if ctx.sparse_grad else N
+        v_means = torch.empty((rows, 3), device=dev)
+        v_quats = torch.empty((rows, 4), device=dev)
+        v_scales = torch.empty((rows, 3), device=dev)
+        v_viewmats = torch.empty((C, 4, 4), device=dev) if ctx.needs_input_grad[4] else None
+        _lib.call("gsplat_hip_projection_packed_bwd", C, N, nnz, _ptr(means), _ptr(quats),
+                  _ptr(scales), _ptr(viewmats), _ptr(Ks), ctx.width, ctx.height, ctx.eps2d,
+                  _ptr(camera_ids), _ptr(gaussian_ids), _ptr(conics), _ptr(comps),
+                  _ptr(v_means2d), _ptr(v_depths), _ptr(v_conics), _ptr(v_comps),
+                  int(bool(ctx.sparse_grad)), _ptr(v_means), _ptr(v_quats), _ptr(v_scales),
+                  _ptr(v_viewmats), _stream())
+        if ctx.sparse_grad:  # COO gradients (_wrapper.py:1127-1170)
+            def coo(v, like):
+                return torch.sparse_coo_tensor(indices=gaussian_ids[None], values=v,
+                                               size=like.size(), is_coalesced=C == 1)
+            v_means, v_quats, v_scales = coo(v_means, means), coo(v_quats, quats), \
+                coo(v_scales, scales)
+        return (v_means if ctx.needs_input_grad[0] else None, None,
+                v_quats if ctx.needs_input_grad[2] else None,
+                v_scales if ctx.needs_input_grad[3] else None,
+                v_viewmats, None, None, None, None, None, None, None, None, None, None)
+
+
 def fully_fused_projection(
     means: Tensor,  # [N, 3]
     covars: Optional[Tensor],  # must be None (quats/scales path only, as the Triton backend)
@@ -174,7 +254,11 @@ def fully_fused_projection(
 
     Returns radii i32[C,N], means2d [C,N,2], depths [C,N], conics [C,N,3],
     compensations [C,N] or None.  Entries with radii == 0 are invalid (written
-    as zeros here; the reference leaves them uninitialised)."""
+    as zeros here; the reference leaves them uninitialised).  packed=True
+    returns (camera_ids, gaussian_ids, radii, means2d, depths, conics,
+    compensations) over the nnz kept pairs, as the CUDA backend
+    (gsplat/cuda/_wrapper.py:998-1190); sparse_grad makes the gradients of
+    means/quats/scales COO tensors."""
     C = viewmats.size(0)
     N = means.size(0)
     assert means.size() == (N, 3), means.size()
@@ -185,9 +269,13 @@ def fully_fused_projection(
     assert scales is not None, "covars or scales is required"
     assert quats.size() == (N, 4), quats.size()
     assert scales.size() == (N, 3), scales.size()
-    if packed or sparse_grad:
-        # The Triton reference cannot run packed either.
-        raise NotImplementedError("packed / sparse_grad projection is not supported yet")
+    if sparse_grad:
+        assert packed, "sparse_grad is only supported when packed is True"
+    if packed:
+        return _FullyFusedProjectionPacked.apply(
+            means.contiguous(), covars, quats.contiguous(), scales.contiguous(),
+            viewmats.contiguous(), Ks.contiguous(), width, height, eps2d, near_plane, far_plane,
+            radius_clip, sparse_grad, calc_compensations, camera_model)
     return _FullyFusedProjection.apply(means, covars, quats, scales, viewmats, Ks, width, height,
                                        eps2d, near_plane, far_plane, radius_clip,
                                        calc_compensations, camera_model, block_size)

@@ -87,33 +87,51 @@ def rasterization(
         assert (sh_degree + 1) ** 2 <= colors.shape[-2], colors.shape
     if absgrad:
         assert not distributed, "AbsGrad is not supported in distributed mode."
-    if packed:
-        raise NotImplementedError("packed=True is not supported yet (the Triton reference "
-                                  "backend cannot run it either, SURVEY L11); pass packed=False")
     if distributed:
         raise NotImplementedError("distributed=True (Gaussian-sharded rendering) is not wired "
                                   "yet; per-camera data parallelism lives in gsplat_hip.distributed")
 
-    radii, means2d, depths, conics, compensations = fully_fused_projection(
-        means, None, quats, scales, viewmats, Ks, width, height, eps2d=eps2d, packed=False,
+    proj = fully_fused_projection(
+        means, None, quats, scales, viewmats, Ks, width, height, eps2d=eps2d, packed=packed,
         near_plane=near_plane, far_plane=far_plane, radius_clip=radius_clip,
         sparse_grad=sparse_grad, calc_compensations=(rasterize_mode == "antialiased"),
         camera_model=camera_model)
-    # [C, N]; for C == 1 a view, so backward is not a (copying) reduction
-    opacities = opacities[None] if C == 1 else opacities.repeat(C, 1)
+    if packed:  # [nnz] pairs, all valid (gsplat/rendering.py:332-343)
+        camera_ids, gaussian_ids, radii, means2d, depths, conics, compensations = proj
+        opacities = opacities[gaussian_ids]
+    else:
+        radii, means2d, depths, conics, compensations = proj
+        # [C, N]; for C == 1 a view, so backward is not a (copying) reduction
+        opacities = opacities[None] if C == 1 else opacities.repeat(C, 1)
+        camera_ids, gaussian_ids = None, None
     if compensations is not None:
         opacities = opacities * compensations
-    meta.update({"camera_ids": None, "gaussian_ids": None, "radii": radii, "means2d": means2d,
-                 "depths": depths, "conics": conics, "opacities": opacities})
+    meta.update({"camera_ids": camera_ids, "gaussian_ids": gaussian_ids, "radii": radii,
+                 "means2d": means2d, "depths": depths, "conics": conics, "opacities": opacities})
 
     # tile intersection first: its counts travel to the host (the one sync of
     # the render) while the GPU computes the colours below
     tile_width = math.ceil(width / float(tile_size))
     tile_height = math.ceil(height / float(tile_size))
     pending_isects = isect_tiles_begin(means2d, radii, depths, tile_size, tile_width, tile_height,
-                                       packed=False, n_cameras=C)
+                                       packed=packed, n_cameras=C, camera_ids=camera_ids,
+                                       gaussian_ids=gaussian_ids)
 
-    if sh_degree is None:
+    if packed:  # colours of the nnz pairs (gsplat/rendering.py:368-408)
+        if sh_degree is None:
+            colors = colors[gaussian_ids] if colors.dim() == 2 else colors[camera_ids, gaussian_ids]
+        else:
+            camtoworlds = torch.inverse(viewmats)
+            dirs = means[gaussian_ids, :] - camtoworlds[camera_ids, :3, 3]
+            if sh_rest is not None:
+                shs = (colors[gaussian_ids], sh_rest[gaussian_ids])
+            elif colors.dim() == 3:
+                shs = colors[gaussian_ids]
+            else:
+                shs = colors[camera_ids, gaussian_ids]
+            colors = spherical_harmonics(sh_degree, dirs, shs, masks=radii > 0)
+            colors = torch.clamp_min(colors + 0.5, 0.0)
+    elif sh_degree is None:
         if colors.dim() == 2:
             colors = colors[None] if C == 1 else colors.expand(C, -1, -1)
     elif not viewmats.requires_grad and (sh_rest is not None or colors.dim() == 3):
@@ -160,7 +178,7 @@ def rasterization(
                 means2d, conics, colors[..., sl], opacities, width, height, tile_size,
                 isect_offsets, flatten_ids,
                 backgrounds=None if backgrounds is None else backgrounds[..., sl],
-                packed=False, absgrad=absgrad)
+                packed=packed, absgrad=absgrad)
             render_colors.append(rc)
             render_alphas.append(ra)
         render_colors = torch.cat(render_colors, dim=-1)
@@ -168,7 +186,7 @@ def rasterization(
     else:
         render_colors, render_alphas = rasterize_to_pixels(
             means2d, conics, colors, opacities, width, height, tile_size, isect_offsets,
-            flatten_ids, backgrounds=backgrounds, packed=False, absgrad=absgrad)
+            flatten_ids, backgrounds=backgrounds, packed=packed, absgrad=absgrad)
     if render_mode in ["ED", "RGB+ED"]:
         render_colors = torch.cat(
             [render_colors[..., :-1],

@@ -408,6 +408,48 @@ int gsplat_hip_selective_adam(int64_t n_rows, int64_t row, float *param, const f
                               float *exp_avg, float *exp_avg_sq, const uint8_t *visible,
                               float lr, float beta1, float beta2, float eps, void *stream);
 
+/* ---------------------------------------------------------------------------
+ * Packed projection (§8 f3).  Replaces projection_ewa_3dgs_packed_fwd/bwd
+ * (gsplat/cuda/csrc/ProjectionEWA3DGSPacked.cu:17-244,348-630, bound by
+ * _FullyFusedProjectionPacked, gsplat/cuda/_wrapper.py:998-1190; the Triton
+ * backend cannot run packed mode).  Same algebra as
+ * gsplat_hip_projection_fwd; the kept (camera, Gaussian) pairs are written in
+ * (camera, Gaussian) order, so the packed outputs equal the dense ones
+ * compacted.  Three calls around the one host read of nnz:
+ *   1. gsplat_hip_projection_packed_count: per-block counts and their scan in
+ *      `workspace` (gsplat_hip_projection_packed_workspace_bytes(C, N) bytes),
+ *      nnz -> nnz_device[0];
+ *   2. gsplat_hip_projection_packed_fwd: camera_ids i64[nnz], gaussian_ids
+ *      i64[nnz], radii i32[nnz], means2d[nnz,2], depths[nnz], conics[nnz,3],
+ *      compensations[nnz] or NULL;
+ *   3. gsplat_hip_projection_packed_bwd: v_means[N,3], v_quats[N,4],
+ *      v_scales[N,3] (zeroed, then summed over entries), or with sparse_grad
+ *      one row per entry ([nnz,3], [nnz,4], [nnz,3]: the COO values);
+ *      v_viewmats[C,4,4] or NULL; v_depths may be NULL. */
+int64_t gsplat_hip_projection_packed_workspace_bytes(int C, int N);
+int gsplat_hip_projection_packed_count(int C, int N, const float *means, const float *quats,
+                                       const float *scales, const float *viewmats,
+                                       const float *Ks, int width, int height, float eps2d,
+                                       float near_plane, float far_plane, float radius_clip,
+                                       void *workspace, int64_t *nnz_device, void *stream);
+int gsplat_hip_projection_packed_fwd(int C, int N, const float *means, const float *quats,
+                                     const float *scales, const float *viewmats, const float *Ks,
+                                     int width, int height, float eps2d, float near_plane,
+                                     float far_plane, float radius_clip, const void *workspace,
+                                     int64_t *camera_ids, int64_t *gaussian_ids, int32_t *radii,
+                                     float *means2d, float *depths, float *conics,
+                                     float *compensations, void *stream);
+int gsplat_hip_projection_packed_bwd(int C, int N, int64_t nnz, const float *means,
+                                     const float *quats, const float *scales,
+                                     const float *viewmats, const float *Ks, int width, int height,
+                                     float eps2d, const int64_t *camera_ids,
+                                     const int64_t *gaussian_ids, const float *conics,
+                                     const float *compensations, const float *v_means2d,
+                                     const float *v_depths, const float *v_conics,
+                                     const float *v_compensations, int sparse_grad,
+                                     float *v_means, float *v_quats, float *v_scales,
+                                     float *v_viewmats, void *stream);
+
 #ifdef __cplusplus
 }
 #endif
