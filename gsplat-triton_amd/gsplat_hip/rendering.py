@@ -25,6 +25,14 @@ from ._wrapper import (
 )
 
 
+def _reshape_view(C: int, world_view: Tensor, N_world: list) -> Tensor:
+    """[sum_i C*N_i, ...] blocks by source rank -> [C, sum_i N_i, ...]
+    (gsplat/rendering.py:260-267)."""
+    view_list = [x.split(int(x.shape[0] / C), dim=0)
+                 for x in world_view.split([C * N_i for N_i in N_world], dim=0)]
+    return torch.stack([torch.cat(parts, dim=0) for parts in zip(*view_list)], dim=0)
+
+
 def rasterization(
     means: Tensor,  # [N, 3]
     quats: Tensor,  # [N, 4]
@@ -88,8 +96,19 @@ def rasterization(
     if absgrad:
         assert not distributed, "AbsGrad is not supported in distributed mode."
     if distributed:
-        raise NotImplementedError("distributed=True (Gaussian-sharded rendering) is not wired "
-                                  "yet; per-camera data parallelism lives in gsplat_hip.distributed")
+        # Gaussian-sharded rendering (gsplat/rendering.py:298-310): project the
+        # local Gaussians into every rank's cameras, exchange the projected
+        # pairs, rasterize the local cameras
+        from . import distributed as gdist
+        assert (sh_degree is None and colors.dim() == 2) or (
+            sh_degree is not None and (sh_rest is not None or colors.dim() == 3)), \
+            "Distributed mode only supports per-Gaussian colors."
+        world_rank = torch.distributed.get_rank()
+        world_size = torch.distributed.get_world_size()
+        N_world = gdist.all_gather_int32(world_size, N, device=device)
+        C_world = [C] * world_size
+        viewmats, Ks = gdist.all_gather_tensor_list(world_size, [viewmats, Ks])
+        C = len(viewmats)
 
     proj = fully_fused_projection(
         means, None, quats, scales, viewmats, Ks, width, height, eps2d=eps2d, packed=packed,
@@ -113,9 +132,11 @@ def rasterization(
     # the render) while the GPU computes the colours below
     tile_width = math.ceil(width / float(tile_size))
     tile_height = math.ceil(height / float(tile_size))
-    pending_isects = isect_tiles_begin(means2d, radii, depths, tile_size, tile_width, tile_height,
-                                       packed=packed, n_cameras=C, camera_ids=camera_ids,
-                                       gaussian_ids=gaussian_ids)
+    pending_isects = None
+    if not distributed:
+        pending_isects = isect_tiles_begin(means2d, radii, depths, tile_size, tile_width,
+                                           tile_height, packed=packed, n_cameras=C,
+                                           camera_ids=camera_ids, gaussian_ids=gaussian_ids)
 
     if packed:  # colours of the nnz pairs (gsplat/rendering.py:368-408)
         if sh_degree is None:
@@ -152,6 +173,42 @@ def rasterization(
             shs = (shs, bcast(sh_rest))
         colors = spherical_harmonics(sh_degree, dirs, shs, masks=masks)  # [C, N, 3]
         colors = torch.clamp_min(colors + 0.5, 0.0)
+
+    if distributed:  # gsplat/rendering.py:413-494
+        if packed:
+            cnts = torch.bincount(camera_ids, minlength=C).split(C_world, dim=0)
+            cnts = [c.sum() for c in cnts]
+            got = gdist.all_to_all_int32(world_size, cnts, device=device)
+            (radii,) = gdist.all_to_all_tensor_list(world_size, [radii], cnts, output_splits=got)
+            means2d, depths, conics, opacities, colors = gdist.all_to_all_tensor_list(
+                world_size, [means2d, depths, conics, opacities, colors], cnts, output_splits=got)
+            # camera ids global -> local, Gaussian ids local -> global
+            reps = torch.stack(cnts)
+            off = torch.cumsum(torch.tensor([0] + C_world[:-1], device=device,
+                                            dtype=camera_ids.dtype), 0).repeat_interleave(reps)
+            camera_ids = camera_ids - off
+            off = torch.cumsum(torch.tensor([0] + N_world[:-1], device=device,
+                                            dtype=gaussian_ids.dtype), 0).repeat_interleave(reps)
+            gaussian_ids = gaussian_ids + off
+            camera_ids, gaussian_ids = gdist.all_to_all_tensor_list(
+                world_size, [camera_ids, gaussian_ids], cnts, output_splits=got)
+            C = C_world[world_rank]
+        else:
+            C = C_world[world_rank]
+            splits = [C_i * N for C_i in C_world]
+            outs = [C * N_i for N_i in N_world]
+            (radii,) = gdist.all_to_all_tensor_list(world_size, [radii.flatten(0, 1)], splits=splits,
+                                                    output_splits=outs)
+            radii = _reshape_view(C, radii, N_world)
+            parts = gdist.all_to_all_tensor_list(
+                world_size, [means2d.flatten(0, 1), depths.flatten(0, 1), conics.flatten(0, 1),
+                             opacities.flatten(0, 1), colors.flatten(0, 1)],
+                splits=splits, output_splits=outs)
+            means2d, depths, conics, opacities, colors = (_reshape_view(C, t, N_world)
+                                                          for t in parts)
+        pending_isects = isect_tiles_begin(means2d, radii, depths, tile_size, tile_width,
+                                           tile_height, packed=packed, n_cameras=C,
+                                           camera_ids=camera_ids, gaussian_ids=gaussian_ids)
 
     if render_mode in ["RGB+D", "RGB+ED"]:
         colors = torch.cat((colors, depths[..., None]), dim=-1)

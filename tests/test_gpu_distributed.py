@@ -1,0 +1,48 @@
+"""rasterization(distributed=True) on the GPU (RCCL, one rank): the
+Gaussian-sharded path (camera all-gather, projected-pair exchange, local
+rasterization; gsplat/rendering.py:298-494) renders and differentiates like
+the single-process path.  The many-rank exchange itself is covered on gloo
+by tests/test_distributed.py."""
+
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+
+from test_gpu_packed import scene
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _pg():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    yield
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("packed", [False, True])
+def test_distributed_single_rank_matches(packed):
+    import gsplat_hip
+    means, quats, scales, opac, sh, vms, K, W, H = scene(C=2, seed=4)
+    res = []
+    for distributed in (False, True):
+        ins = [x.clone().requires_grad_(True) for x in (means, quats, scales, opac, sh)]
+        rc, ra, meta = gsplat_hip.rasterization(*ins, vms, K, W, H, sh_degree=3, packed=packed,
+                                                distributed=distributed)
+        loss = (rc * torch.linspace(0, 1, rc.numel(), device=DEV).view_as(rc)).sum() + ra.sum()
+        res.append((rc.detach(), ra.detach(), torch.autograd.grad(loss, ins)))
+    (rc0, ra0, g0), (rc1, ra1, g1) = res
+    torch.testing.assert_close(rc1, rc0, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(ra1, ra0, rtol=1e-5, atol=1e-5)
+    for a, b in zip(g1, g0):
+        torch.testing.assert_close(a, b, rtol=1e-3, atol=1e-4 * float(b.abs().max()))
