@@ -78,7 +78,7 @@ def pmc_traffic(config: str):
         return None  # already running under a profiler: no nested profiler runs
     env = dict(os.environ, TMPDIR="/tmp")
     per = {}
-    for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+    for ctr in ("FETCH_SIZE", "WRITE_SIZE", "SQ_INSTS_VALU"):
         d = tempfile.mkdtemp(prefix="gsplat_pmc_", dir="/tmp")
         regex = "surfel::fwd_kernel" if MODEL.get(config) == "2dgs" else "r16::fwd_kernel"
         cmd = [rp, "--kernel-include-regex", regex, "--pmc", ctr, "-f", "csv",
@@ -96,14 +96,27 @@ def pmc_traffic(config: str):
                     vals[r["Dispatch_Id"]] = vals.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
         shutil.rmtree(d, ignore_errors=True)
         if not vals:
+            if ctr == "SQ_INSTS_VALU":  # optional: VALU issue rate of the same launch
+                continue
             return None
         per[ctr] = float(np.mean(list(vals.values())))
     fetch = 2.0 * per["FETCH_SIZE"] * 1024.0
     write = per["WRITE_SIZE"] * 1024.0
     return {"bytes_per_launch": fetch + write, "fetch_bytes": fetch, "write_bytes": write,
             "fetch_size_kib": per["FETCH_SIZE"], "write_size_kib": per["WRITE_SIZE"],
+            "valu_insts": per.get("SQ_INSTS_VALU"),
             "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py --probe "
                       "(FETCH_SIZE x2 per MI355X_MICROARCH.md; gathers uncalibrated)"}
+
+
+def _valu_frac(traffic, launch_ms):
+    if not traffic or not traffic.get("valu_insts") or not launch_ms == launch_ms:
+        return None
+    insts = traffic["valu_insts"]
+    peak = 1024 * 2.4e9 / 2.0  # wave64 VALU instructions per second, whole chip
+    achieved = insts / (launch_ms * 1e-3)
+    return {"bound": "valu", "insts_per_launch": insts, "achieved": achieved, "peak": peak,
+            "unit": "wave-instr/s", "frac": achieved / peak}
 
 
 def max_over_ranks(elapsed: float, world: int, device) -> float:
@@ -240,6 +253,11 @@ def main():
         "model": model,
     }
 
+    # the kernel's binding ceiling is VALU issue, not HBM: wave64
+    # VALU instructions x 2 cycles each (MI355X_MICROARCH.md constants:
+    # v_fma_f32 2 cyc per SIMD) against 1024 SIMDs x 2.4 GHz over the launch
+    # time; SQ_INSTS_VALU from a rocprofv3 --pmc pass of the same workload
+    result["roofline"]["valu"] = _valu_frac(traffic, fwd_ms)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(tr, args.cpu_tile_stride)
     if rank == 0:
