@@ -15,6 +15,12 @@ from ._wrapper import (
 )
 from ._wrapper_aux import SelectiveAdam, adam, compute_relocation, quat_scale_to_covar_preci
 from ._wrapper_2dgs import fully_fused_projection_2dgs, rasterize_to_pixels_2dgs
+from ._wrapper_indices import (
+    accumulate,
+    accumulate_2dgs,
+    rasterize_to_indices_in_range,
+    rasterize_to_indices_in_range_2dgs,
+)
 from .rendering import depth_to_normal, rasterization, rasterization_2dgs
 
 __all__ = [
@@ -32,5 +38,9 @@ __all__ = [
     "compute_relocation",
     "adam",
     "SelectiveAdam",
+    "rasterize_to_indices_in_range",
+    "rasterize_to_indices_in_range_2dgs",
+    "accumulate",
+    "accumulate_2dgs",
 ]
 __version__ = "0.1.0"

@@ -12,7 +12,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GSPLAT_HIP_LIB", os.path.join(_HERE, "libgsplat_hip.so"))
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 _p = ctypes.c_void_p
 _i32 = ctypes.c_int
@@ -93,6 +93,12 @@ _SIGS = {
     "gsplat_hip_projection_packed_bwd": (_i32, [_i32, _i32, _i64, _p, _p, _p, _p, _p, _i32, _i32,
                                                 _f, _p, _p, _p, _p, _p, _p, _p, _p, _i32, _p, _p,
                                                 _p, _p, _p]),
+    "gsplat_hip_rasterize_to_indices_count": (_i32, [_i32, _i32, _i32, _i32, _i32, _i32, _i32,
+                                                     _i32, _i64, _i64, _i64, _p, _p, _p, _p, _p,
+                                                     _p, _p, _p]),
+    "gsplat_hip_rasterize_to_indices_write": (_i32, [_i32, _i32, _i32, _i32, _i32, _i32, _i32,
+                                                     _i32, _i64, _i64, _i64, _p, _p, _p, _p, _p,
+                                                     _p, _p, _p, _p, _p]),
 }
 
 EXPORTED = tuple(_SIGS)

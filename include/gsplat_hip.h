@@ -450,6 +450,38 @@ int gsplat_hip_projection_packed_bwd(int C, int N, int64_t nnz, const float *mea
                                      float *v_means, float *v_quats, float *v_scales,
                                      float *v_viewmats, void *stream);
 
+/* ---------------------------------------------------------------------------
+ * Per-pixel contributor lists (§8 f4).  Replace rasterize_to_indices_3dgs /
+ * _2dgs (gsplat/cuda/csrc/RasterizeToIndices3DGS.cu:14-185,
+ * RasterizeToIndices2DGS.cu:14-200) and their two-pass host driver
+ * (gsplat/cuda/csrc/Rasterization.cpp:224-296, 586-660), bound by
+ * rasterize_to_indices_in_range{,_2dgs} (gsplat/cuda/_wrapper.py:577-650,
+ * 1729-1800).
+ *   kind 0 = 3DGS, shape = conics[C,N,3]; kind 1 = 2DGS, shape =
+ *   ray_transforms[C,N,3,3].  Ranges are in batches of tile_size^2 records of
+ *   each tile's list, [range_start, range_end); transmittances[C,H,W] is the
+ *   starting T per pixel.
+ *   count: chunk_cnts[C,H,W] (every pixel written) = contributors per pixel.
+ *   The caller forms chunk_starts = exclusive scan of chunk_cnts (pixel-major)
+ *   and M = its total, allocates gaussian_ids/pixel_ids int64[M], then
+ *   write: gaussian_ids = flatten_id % N, pixel_ids = c*H*W + y*W + x, in
+ *   pixel-major, front-to-back order (the reference's output order). */
+int gsplat_hip_rasterize_to_indices_count(int kind, int C, int N, int W, int H, int tile_size,
+                                          int tile_width, int tile_height, int64_t n_isects,
+                                          int64_t range_start, int64_t range_end,
+                                          const float *transmittances, const float *means2d,
+                                          const float *shape, const float *opacities,
+                                          const int32_t *offsets, const int32_t *flatten_ids,
+                                          int32_t *chunk_cnts, void *stream);
+int gsplat_hip_rasterize_to_indices_write(int kind, int C, int N, int W, int H, int tile_size,
+                                          int tile_width, int tile_height, int64_t n_isects,
+                                          int64_t range_start, int64_t range_end,
+                                          const float *transmittances, const float *means2d,
+                                          const float *shape, const float *opacities,
+                                          const int32_t *offsets, const int32_t *flatten_ids,
+                                          const int32_t *chunk_starts, int64_t *gaussian_ids,
+                                          int64_t *pixel_ids, void *stream);
+
 #ifdef __cplusplus
 }
 #endif
