@@ -743,6 +743,223 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) b
   tl_store(a, t_start, lane);
 }
 
+// Backward, PX pixels per lane (PX = 2 or 4): a wave owns a 16 x 4PX band
+// of the tile, lane l the pixels (l & 15, 4PX w + 4q + (l >> 4)), q < PX, and
+// the 4/PX waves of a workgroup cover the tile.  Each record's gradient
+// terms of the PX pixels are summed in-lane before the one reduce-scatter and
+// the atomics, which divides the cross-lane work and the LDS reads per pixel
+// by PX; the price is coarser culling (16 x 4PX rectangles instead of 16x4)
+// and fewer waves per SIMD.  Same arithmetic per pixel as bwd_kernel.
+template <int PX>
+struct BwdOcc {  // waves per SIMD that fit the VGPRs without spills
+  static constexpr int W = PX == 2 ? 4 : 3;
+};
+
+template <int D, bool ABS, int PX>
+__global__ void __launch_bounds__(256 / PX)
+__attribute__((amdgpu_waves_per_eu(BwdOcc<PX>::W))) bwd2_kernel(Args a) {
+  using P = BwdPair<D>;
+  constexpr int N4 = P::N4;
+  constexpr int F = D + 6 + (ABS ? 2 : 0);
+  constexpr int NV = (F + 15) / 16;
+  __shared__ float4 stage_all[4 / PX][32 * N4];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  float4 *st = stage_all[w];
+  const uint64_t t_start = tl_now(a);
+  int tile = blockIdx.x, k = 0;
+  if (a.items) {
+    const int nf = a.n_items[0];
+    int b = blockIdx.x;
+    if (b >= nf && b - nf >= a.n_items[1]) return;
+    const int2 it = b < nf ? a.items[b] : a.items_tail[b - nf];
+    tile = it.x;
+    k = it.y;
+  }
+  const int ntile = a.tw * a.th;
+  const int c = tile / ntile;
+  const int rem = tile - c * ntile;
+  const int ty = rem / a.tw, tx = rem - ty * a.tw;
+  const int px = tx * kTS + (lane & 15);
+  const int py0 = ty * kTS + 4 * PX * w + (lane >> 4);
+  const float rx0 = tx * kTS + 0.5f, rx1 = rx0 + (kTS - 1);
+  const float ry0 = ty * kTS + 4 * PX * w + 0.5f, ry1 = ry0 + (4 * PX - 1);
+  if (a.masks && a.masks[tile]) return;
+  const int64_t tstart = a.offsets[tile];
+  const int64_t tend = (tile == a.n_tiles - 1) ? a.n_isects : (int64_t)a.offsets[tile + 1];
+  const int64_t start = a.items ? tstart + (int64_t)k * a.L : tstart;
+  const int64_t cend = a.items ? min(tend, start + a.L) : tend;
+
+  const float fx = (float)px + 0.5f;
+  float fy[PX], T[PX], rD[PX], bgt[PX], TfDra[PX], Drc[PX][D];
+  int32_t mylast[PX];
+#pragma unroll
+  for (int q = 0; q < PX; ++q) {
+    const int py = py0 + 4 * q;
+    fy[q] = (float)py + 0.5f;
+    T[q] = 1.f, rD[q] = 0.f, bgt[q] = 0.f, TfDra[q] = 0.f, mylast[q] = -1;
+#pragma unroll
+    for (int d = 0; d < D; ++d) Drc[q][d] = 0.f;
+    if (px < a.W && py < a.H) {
+      const int64_t pix = ((int64_t)c * a.H + py) * a.W + px;
+      const float Tf = 1.f - a.render_alphas[pix];
+      const float Dra = a.v_render_alphas ? a.v_render_alphas[pix] : 0.f;
+      mylast[q] = a.last_ids[pix];
+#pragma unroll
+      for (int d = 0; d < D; ++d) Drc[q][d] = a.v_render_colors[pix * D + d];
+      if (a.backgrounds) {
+        float bgv = 0.f;
+#pragma unroll
+        for (int d = 0; d < D; ++d) bgv += a.backgrounds[c * D + d] * Drc[q][d];
+        bgt[q] = bgv * Tf;
+      }
+      TfDra[q] = Tf * Dra;
+      T[q] = Tf;
+      if (cend < tend) {
+        // chunk followed by others: the forward's state at the boundary cend
+        const int p = 64 * PX * w + 64 * q + lane;  // row-major pixel of the tile
+        const int64_t per = (int64_t)(kTS * kTS * (1 + D));
+        T[q] = fabsf(a.state[(cend / a.L) * per + p]);
+        float s = 0.f;
+        for (int64_t bi = cend; bi < tend; bi += a.L) {
+          const float *sl = a.state + (bi / a.L) * per;
+#pragma unroll
+          for (int d = 0; d < D; ++d) s += sl[(1 + d) * kTS * kTS + p] * Drc[q][d];
+        }
+        rD[q] = s;
+      }
+    }
+  }
+  int32_t lmax = mylast[0];
+#pragma unroll
+  for (int q = 1; q < PX; ++q) lmax = max(lmax, mylast[q]);
+#pragma unroll
+  for (int msk = 32; msk >= 1; msk >>= 1) lmax = max(lmax, __shfl_xor(lmax, msk, 64));
+  const int64_t end = min(cend, (int64_t)lmax + 1);
+
+  if (start < end) {
+    auto id_at = [&](int64_t b1) -> int32_t {
+      return a.flatten_ids[max(b1 - 64 + lane, start)];
+    };
+    auto stage = [&](const Attr<D> &at, int64_t b1) -> int {
+      const int64_t j = b1 - 64 + lane;
+      const bool keep = (j >= start) && keep_attr<D>(at, rx0, rx1, ry0, ry1);
+      const uint64_t m = __ballot(keep);
+      const int cnt = __popcll(m);
+      if (keep) stage_bwd_pair<D>(st, ballot_slot(m), at, (int32_t)j);
+      if ((cnt & 1) && lane == 0) stage_bwd_pad<D>(st, cnt);
+      wave_sync_lds();
+      return cnt;
+    };
+    const int lf = rs_field(lane);
+    auto field_scale = [&](int f) -> float {
+      constexpr float m2 = -2.f / kLog2e;
+      if (f < D + 1) return 1.f;
+      if (f < D + 3) return m2;
+      if (f == D + 3 || f == D + 5) return -0.5f;
+      if (f == D + 4) return -1.f;
+      return -m2;
+    };
+    auto grad_seq = [&](int q, bool valid, bool unclamped, float al, float ra, float gD, float &wt,
+                        float &Da) {
+      T[q] = valid ? T[q] * ra : T[q];
+      wt = valid ? al * T[q] : 0.f;
+      rD[q] += gD * wt;
+      const float Da_raw = ra * (TfDra[q] + T[q] * gD - rD[q] - bgt[q]);
+      Da = (valid & unclamped) ? Da_raw : 0.f;
+    };
+    auto composite = [&](int cnt) {
+      for (int p = (cnt - 1) >> 1; p >= 0; --p) {
+        const float4 *qp = st + p * N4;
+        float4 vv[N4];
+#pragma unroll
+        for (int i = 0; i < N4; ++i) vv[i] = qp[i];
+        f2v f[2 * N4];
+#pragma unroll
+        for (int i = 0; i < N4; ++i) {
+          asm volatile("" ::"v"(vv[i].x), "v"(vv[i].y), "v"(vv[i].z), "v"(vv[i].w));
+          f[2 * i] = f2v{vv[i].x, vv[i].y};
+          f[2 * i + 1] = f2v{vv[i].z, vv[i].w};
+        }
+        const f2v dx = f[0] - fx;
+        f2v dy[PX], gx[PX], gy[PX], s2[PX], ex[PX], ar[PX];
+        bool v0[PX], v1[PX];
+        bool any = false;
+#pragma unroll
+        for (int q = 0; q < PX; ++q) {
+          dy[q] = f[1] - fy[q];
+          gx[q] = f[2] * dx + f[3] * dy[q];
+          gy[q] = f[3] * dx + f[4] * dy[q];
+          s2[q] = dx * gx[q] + dy[q] * gy[q];
+          v0[q] = (__float_as_uint(s2[q].x) <= __float_as_uint(f[6].x)) &&
+                  (__float_as_int(f[7].x) <= mylast[q]);
+          v1[q] = (__float_as_uint(s2[q].y) <= __float_as_uint(f[6].y)) &&
+                  (__float_as_int(f[7].y) <= mylast[q]);
+          any |= v0[q] | v1[q];
+        }
+        if (__ballot(any) == 0) continue;
+        f2v v[NV * 16];
+#pragma unroll
+        for (int kk = 0; kk < NV * 16; ++kk) v[kk] = f2v{0.f, 0.f};
+#pragma unroll
+        for (int q = 0; q < PX; ++q) {
+          ex[q] = f2v{__builtin_amdgcn_exp2f(-s2[q].x), __builtin_amdgcn_exp2f(-s2[q].y)};
+          ar[q] = f[5] * ex[q];
+          const f2v al = f2v{fminf(ar[q].x, kAlphaMax), fminf(ar[q].y, kAlphaMax)};
+          const f2v om = 1.f - al;
+          const f2v ra = f2v{__builtin_amdgcn_rcpf(om.x), __builtin_amdgcn_rcpf(om.y)};
+          f2v gD = f[9] * Drc[q][0];
+#pragma unroll
+          for (int d = 1; d < D; ++d)
+            gD = __builtin_elementwise_fma(f[9 + d], f2v{Drc[q][d], Drc[q][d]}, gD);
+          float w1, Da1, w0, Da0;
+          grad_seq(q, v1[q], ar[q].y <= kAlphaMax, al.y, ra.y, gD.y, w1, Da1);
+          grad_seq(q, v0[q], ar[q].x <= kAlphaMax, al.x, ra.x, gD.x, w0, Da0);
+          const f2v wt = f2v{w0, w1}, Da = f2v{Da0, Da1};
+          const f2v aD = al * Da;
+#pragma unroll
+          for (int d = 0; d < D; ++d)
+            v[d] = __builtin_elementwise_fma(wt, f2v{Drc[q][d], Drc[q][d]}, v[d]);
+          v[D] = __builtin_elementwise_fma(Da, ex[q], v[D]);
+          const f2v tgx = aD * gx[q], tgy = aD * gy[q];
+          v[D + 1] += tgx;
+          v[D + 2] += tgy;
+          const f2v P_ = aD * dx, Q_ = aD * dy[q];
+          v[D + 3] = __builtin_elementwise_fma(P_, dx, v[D + 3]);
+          v[D + 4] = __builtin_elementwise_fma(P_, dy[q], v[D + 4]);
+          v[D + 5] = __builtin_elementwise_fma(Q_, dy[q], v[D + 5]);
+          if (ABS) {
+            v[D + 6] += f2v{fabsf(tgx.x), fabsf(tgx.y)};
+            v[D + 7] += f2v{fabsf(tgy.x), fabsf(tgy.y)};
+          }
+        }
+        const int g0 = __float_as_int(f[8].x), g1 = __float_as_int(f[8].y);
+#pragma unroll
+        for (int qq = 0; qq < NV; ++qq) {
+          constexpr int NQ = F - 16 * (NV - 1);
+          const f2v tot = qq < NV - 1 ? reduce_scatter2<16>(v + 16 * qq, lane)
+                                      : reduce_scatter2<NQ>(v + 16 * qq, lane);
+          const int field = 16 * qq + lf;
+          if ((lane & 3) == 0 && lf < (qq < NV - 1 ? 16 : NQ) && !(a.dbg & 1)) {
+            const float sc = field_scale(field);
+            if (tot.x != 0.f) atomic_add_f32(a.packed + (int64_t)g0 * a.S + field, sc * tot.x);
+            if (g1 >= 0 && tot.y != 0.f)
+              atomic_add_f32(a.packed + (int64_t)g1 * a.S + field, sc * tot.y);
+          }
+        }
+      }
+    };
+    int32_t g_n = id_at(end);
+    for (int64_t b1 = end; b1 > start; b1 -= 64) {
+      Attr<D> A;
+      load_attr<D>(a, g_n, A);
+      g_n = id_at(b1 - 64);
+      composite(stage(A, b1));
+      wave_sync_lds();
+    }
+  }
+  tl_store(a, t_start, lane);
+}
+
 // packed [G][S] -> the autograd tensors
 template <int D, bool ABS>
 __global__ void __launch_bounds__(256)
@@ -900,6 +1117,17 @@ static int64_t n_items_bound(int n_tiles, int64_t n_isects) {
   return L ? (int64_t)n_tiles + n_isects / L + 1 : (int64_t)n_tiles;
 }
 
+// Pixels per lane in the backward (1: bwd_kernel, 16x4 per wave; 2 or 4:
+// bwd2_kernel, 16x8 or 16x16 per wave).  GSPLAT_HIP_BWD_PX overrides it.
+static int bwd_px() {
+  static const int v = [] {
+    const char *e = getenv("GSPLAT_HIP_BWD_PX");
+    const int x = e ? atoi(e) : 2;
+    return (x == 1 || x == 4) ? x : 2;
+  }();
+  return v;
+}
+
 static int dbg_flags() {
   static const int v = [] { const char *e = getenv("GSPLAT_HIP_DBG"); return e ? atoi(e) : 0; }();
   return v;
@@ -951,7 +1179,12 @@ int r16_bwd(r16::Args a, int64_t G, float *v_means2d, float *v_conics, float *v_
       a.items = nullptr;
       a.n_items = nullptr;
     }
-    hipLaunchKernelGGL((r16::bwd_kernel<D, ABS>), dim3((unsigned)grid), dim3(256), 0, st, a);
+    if (bwd_px() == 2)
+      hipLaunchKernelGGL((r16::bwd2_kernel<D, ABS, 2>), dim3((unsigned)grid), dim3(128), 0, st, a);
+    else if (bwd_px() == 4)
+      hipLaunchKernelGGL((r16::bwd2_kernel<D, ABS, 4>), dim3((unsigned)grid), dim3(64), 0, st, a);
+    else
+      hipLaunchKernelGGL((r16::bwd_kernel<D, ABS>), dim3((unsigned)grid), dim3(256), 0, st, a);
     GS_CHECK_LAUNCH("rasterize_bwd16");
   }
   if (G > 0) {
