@@ -12,6 +12,7 @@ gloo on the CPU for the tests.  The backward of an exchange is the exchange
 with input and output splits swapped.
 """
 
+import math
 from typing import List, Optional, Union
 
 import torch
@@ -127,3 +128,106 @@ def all_to_all_tensor_list(world_size: int, tensor_list: List[Tensor],
     collected = _AllToAll.apply(data, splits, output_splits)
     return [o.reshape(-1, *t.shape[1:]) for o, t in
             zip(torch.split(collected, sizes, dim=-1), tensor_list)]
+
+
+# ------------------------------------------- per-camera data parallelism --
+
+def _adam_torch(params, grads, exp_avgs, exp_avg_sqs, lrs, betas, eps, step):
+    """torch restatement of csrc/adam.hip's update (same operation order), for
+    running ShardedAdam's collectives on the CPU (gloo tests)."""
+    b1, b2 = betas
+    bc1, bc2 = 1.0 - b1 ** step, 1.0 - b2 ** step
+    for p, g, m, v, lr in zip(params, grads, exp_avgs, exp_avg_sqs, lrs):
+        g = torch.zeros_like(p) if g is None else g
+        m.add_((1.0 - b1) * (g - m))
+        v.mul_(b2).add_((1.0 - b2) * g * g)
+        p.sub_((lr / bc1) * m / (v.sqrt() * (1.0 / math.sqrt(bc2)) + eps))
+
+
+class ShardedAdam:
+    """Adam for per-camera data parallelism with the optimizer state sharded
+    over the ranks: per parameter, the summed gradient is reduce-scattered
+    (each rank receives the sum of its 1/world_size of the rows), each rank
+    updates its rows only, and the updated rows are all-gathered back into
+    every replica.  Same bytes on the wire as one all-reduce of the gradients
+    (a ring all-reduce is a reduce-scatter plus an all-gather), but the Adam
+    pass and its 2 x 4 B/element moment state shrink to 1/world_size per rank.
+
+    Rows are split in multiples of 4 (16-B aligned shards for the fused
+    kernel); the < 4 * world_size remainder rows are all-reduced and updated
+    redundantly on every rank.  Collectives run on the default group, largest
+    tensor first.  `update` is the Adam kernel (csrc/adam.hip by default).
+    """
+
+    def __init__(self, params, lrs, betas=(0.9, 0.999), eps=1e-8, update=None):
+        self.params = list(params)
+        self.lrs = [float(x) for x in lrs]
+        self.betas, self.eps = betas, eps
+        self.world, self.rank = dist.get_world_size(), dist.get_rank()
+        if update is None:
+            from .losses import adam_groups
+            update = adam_groups
+        self.update = update
+        self.step_count = 0
+        w, r = self.world, self.rank
+        self.layout = []  # (row floats, shard rows q, main floats w*q*row, total floats)
+        for p in self.params:
+            assert p.is_contiguous() and p.dtype == torch.float32
+            row = p[0].numel() if p.dim() > 0 and p.shape[0] > 0 else 1
+            q = (p.shape[0] // (4 * w)) * 4
+            self.layout.append((row, q, w * q * row, p.numel()))
+        dev = self.params[0].device
+        z = lambda n: torch.zeros(n, device=dev)  # noqa: E731
+        self.m = [z(q * row) for row, q, _, _ in self.layout]
+        self.v = [z(q * row) for row, q, _, _ in self.layout]
+        self.m_tail = [z(tot - main) for _, _, main, tot in self.layout]
+        self.v_tail = [z(tot - main) for _, _, main, tot in self.layout]
+        self.g_shard = [torch.empty(q * row, device=dev) for row, q, _, _ in self.layout]
+        self.order = sorted(range(len(self.params)), key=lambda i: -self.params[i].numel())
+
+    def _shard(self, i, flat):
+        row, q, _, _ = self.layout[i]
+        return flat[self.rank * q * row:(self.rank + 1) * q * row]
+
+    @torch.no_grad()
+    def step(self):
+        self.step_count += 1
+        flats, works = {}, []
+        for i in self.order:
+            p = self.params[i]
+            g = p.grad if p.grad is not None else torch.zeros_like(p)
+            gf = g.contiguous().view(-1)
+            flats[i] = gf
+            _, _, main, tot = self.layout[i]
+            if main:
+                works.append(dist.reduce_scatter_tensor(self.g_shard[i], gf[:main],
+                                                        async_op=True))
+            if tot > main:
+                works.append(dist.all_reduce(gf[main:], async_op=True))
+        for wk in works:
+            wk.wait()
+        idx = [i for i in range(len(self.params)) if self.layout[i][2]]
+        if idx:
+            self.update([self._shard(i, self.params[i].data.view(-1)) for i in idx],
+                        [self.g_shard[i] for i in idx], [self.m[i] for i in idx],
+                        [self.v[i] for i in idx], [self.lrs[i] for i in idx], self.betas,
+                        self.eps, self.step_count)
+        tails = [i for i in range(len(self.params)) if self.layout[i][3] > self.layout[i][2]]
+        if tails:
+            self.update([self.params[i].data.view(-1)[self.layout[i][2]:] for i in tails],
+                        [flats[i][self.layout[i][2]:] for i in tails],
+                        [self.m_tail[i] for i in tails], [self.v_tail[i] for i in tails],
+                        [self.lrs[i] for i in tails], self.betas, self.eps, self.step_count)
+        works = []
+        for i in self.order:
+            _, _, main, _ = self.layout[i]
+            if main:
+                full = self.params[i].data.view(-1)[:main]
+                works.append(dist.all_gather_into_tensor(full, self._shard(i, full).clone(),
+                                                         async_op=True))
+        for wk in works:
+            wk.wait()
+
+    def zero_grad(self, set_to_none=True):
+        for p in self.params:
+            p.grad = None

@@ -84,6 +84,21 @@ def l1_ssim_loss(img, gt, ssim_lambda=0.2):
     return _L1SSIMLoss.apply(img, gt, float(ssim_lambda))
 
 
+def adam_groups(params, grads, exp_avgs, exp_avg_sqs, lrs, betas, eps, step):
+    """One fused Adam launch (csrc/adam.hip) over flat float32 tensors: group
+    i updates params[i] in place from grads[i] (None = zero) with its lr."""
+    n = len(params)
+    P = ctypes.c_void_p * n
+    for t in list(params) + list(exp_avgs) + list(exp_avg_sqs):
+        assert t.is_contiguous() and t.dtype == torch.float32
+    _lib.call("gsplat_hip_adam_step", n, P(*[p.data_ptr() for p in params]),
+              P(*[0 if g is None else g.data_ptr() for g in grads]),
+              P(*[m.data_ptr() for m in exp_avgs]), P(*[v.data_ptr() for v in exp_avg_sqs]),
+              (ctypes.c_int64 * n)(*[p.numel() for p in params]),
+              (ctypes.c_float * n)(*[float(x) for x in lrs]), float(betas[0]), float(betas[1]),
+              float(eps), int(step), _stream())
+
+
 class FusedAdam:
     """torch.optim.Adam semantics (per-group lr, shared betas/eps) in one launch."""
 
@@ -94,26 +109,17 @@ class FusedAdam:
         self.exp_avg = [torch.zeros_like(p) for p in self.params]
         self.exp_avg_sq = [torch.zeros_like(p) for p in self.params]
         self.step_count = 0
-        n = len(self.params)
-        self._numels = (ctypes.c_int64 * n)(*[p.numel() for p in self.params])
-        self._lrs = (ctypes.c_float * n)(*self.lrs)
         for p in self.params:
             assert p.is_contiguous() and p.dtype == torch.float32
 
     @torch.no_grad()
     def step(self):
         self.step_count += 1
-        n = len(self.params)
-        P = ctypes.c_void_p * n
         grads = [p.grad for p in self.params]
         for gr in grads:
             assert gr is None or gr.is_contiguous()
-        _lib.call("gsplat_hip_adam_step", n, P(*[p.data_ptr() for p in self.params]),
-                  P(*[0 if g is None else g.data_ptr() for g in grads]),
-                  P(*[m.data_ptr() for m in self.exp_avg]),
-                  P(*[v.data_ptr() for v in self.exp_avg_sq]), self._numels, self._lrs,
-                  float(self.betas[0]), float(self.betas[1]), float(self.eps), self.step_count,
-                  _stream())
+        adam_groups([p.data for p in self.params], grads, self.exp_avg, self.exp_avg_sq,
+                    self.lrs, self.betas, self.eps, self.step_count)
 
     def zero_grad(self, set_to_none=True):
         for p in self.params:

@@ -14,8 +14,10 @@ default, :149-160), and the strategy statistics from meta["gradient_2dgs"]
 (key_for_gradient, :307-311).
 
 Multi-GPU is per-camera data parallelism: every rank holds the same
-Gaussians, renders its own camera, and the Gaussian gradients are summed with
-one RCCL all-reduce per parameter group over xGMI.
+Gaussians and renders its own camera; the Gaussian gradients are summed over
+RCCL/xGMI by reduce-scatter, each rank runs Adam on its share of the rows,
+and the updated rows are all-gathered (distributed.ShardedAdam; the plain
+per-group all-reduce + full Adam is `sharded_optimizer=False`).
 """
 
 import math
@@ -104,7 +106,7 @@ class Trainer:
 
     def __init__(self, points, rgbs, viewmats, Ks, width, height, sh_degree=3, device="cuda",
                  seed=42, world_size=1, rank=0, ssim_lambda=0.2, scene_scale=1.0,
-                 fused=True, model="3dgs"):
+                 fused=True, model="3dgs", sharded_optimizer=True):
         assert model in ("3dgs", "2dgs"), model
         self.model = model
         g = torch.Generator().manual_seed(seed)  # identical on every rank (replicas)
@@ -134,7 +136,14 @@ class Trainer:
                    * math.sqrt(BS), "name": k} for k, p in self.params.items()]
         kw = dict(eps=1e-15 / math.sqrt(BS), betas=(1 - BS * (1 - 0.9), 1 - BS * (1 - 0.999)))
         self.fused = fused
-        if fused:  # HIP loss + one-launch Adam (csrc/ssim.hip, csrc/adam.hip)
+        # N > 1: gradients reduce-scattered, Adam on this rank's rows, rows
+        # all-gathered (distributed.ShardedAdam) instead of all-reduce + full Adam
+        self.sharded = fused and sharded_optimizer and world_size > 1
+        if self.sharded:
+            from .distributed import ShardedAdam
+            self.opt = ShardedAdam([g["params"][0] for g in groups], [g["lr"] for g in groups],
+                                   **kw)
+        elif fused:  # HIP loss + one-launch Adam (csrc/ssim.hip, csrc/adam.hip)
             self.opt = FusedAdam([g["params"][0] for g in groups], [g["lr"] for g in groups], **kw)
         else:  # torch reference path (conv SSIM, torch.optim.Adam)
             self.opt = torch.optim.Adam(groups, foreach=True, **kw)
@@ -183,7 +192,7 @@ class Trainer:
                                    self.window)
             loss = l1 * (1.0 - self.ssim_lambda) + ssim_loss * self.ssim_lambda
         loss.backward()
-        if self.world_size > 1:
+        if self.world_size > 1 and not self.sharded:
             self.allreduce_grads()
         self.update_state(meta)
         self.opt.step()

@@ -147,3 +147,65 @@ def test_reshape_view_blocks():
     world = torch.cat([blk0.flatten(), blk1.flatten()])
     out = _reshape_view(C, world, N_world)
     assert out.tolist() == [[0, 1, 2, 3, 4], [10, 11, 12, 13, 14]]
+
+
+def _sharded_worker(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from gsplat_hip.distributed import ShardedAdam, _adam_torch
+        g = torch.Generator().manual_seed(0)  # identical replicas on every rank
+        # row counts: divisible, with remainder rows, and fewer rows than ranks*4
+        shapes = [(37, 15, 3), (37, 3), (37,), (40, 4), (5, 3)]
+        init = [torch.randn(s, generator=g) for s in shapes]
+        lrs = [1e-2, 2e-3, 5e-2, 1e-3, 3e-3]
+        kw = dict(betas=(0.8, 0.99), eps=1e-8)
+        ps = [torch.nn.Parameter(t.clone()) for t in init]
+        ref = [t.clone() for t in init]
+        opt = ShardedAdam(ps, lrs, update=_adam_torch, **kw)
+        m = [torch.zeros_like(t).view(-1) for t in init]
+        v = [torch.zeros_like(t).view(-1) for t in init]
+        for step in range(1, 4):
+            gr = torch.Generator().manual_seed(100 * step + rank)  # per-rank gradients
+            grads = [torch.randn(s, generator=gr) for s in shapes]
+            for p, gg in zip(ps, grads):
+                p.grad = gg.clone()
+            opt.step()
+            opt.zero_grad()
+            # reference: all-reduce SUM of the gradients, full Adam on every rank
+            summed = [gg.clone() for gg in grads]
+            for t in summed:
+                dist.all_reduce(t)
+            _adam_torch([t.view(-1) for t in ref], [t.view(-1) for t in summed], m, v, lrs,
+                        kw["betas"], kw["eps"], step)
+        err = max(float((p.detach() - r).abs().max()) for p, r in zip(ps, ref))
+        same = [p.detach().clone() for p in ps]
+        q.put((rank, err, [t.tolist() for t in same]))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:
+        q.put((rank, repr(e), None))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_adam_matches_allreduce_adam_gloo(world):
+    """ShardedAdam (reduce-scatter -> Adam on own rows -> all-gather) equals
+    all-reduce + full Adam on every rank, and the replicas stay identical."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sharded_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = {}
+    for _ in range(world):
+        rank, err, vals = q.get(timeout=120)
+        out[rank] = (err, vals)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank in range(world):
+        err, vals = out[rank]
+        assert not isinstance(err, str), err
+        assert err < 1e-5, (rank, err)
+        assert vals == out[0][1], "replicas diverged"

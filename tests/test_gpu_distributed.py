@@ -46,3 +46,29 @@ def test_distributed_single_rank_matches(packed):
     torch.testing.assert_close(ra1, ra0, rtol=1e-5, atol=1e-5)
     for a, b in zip(g1, g0):
         torch.testing.assert_close(a, b, rtol=1e-3, atol=1e-4 * float(b.abs().max()))
+
+
+def test_sharded_adam_single_rank_rccl_matches_fused_adam():
+    """ShardedAdam's RCCL path (reduce-scatter, HIP Adam on the shard and the
+    remainder rows, all-gather) on one rank equals FusedAdam."""
+    from gsplat_hip.distributed import ShardedAdam
+    from gsplat_hip.losses import FusedAdam
+    g = torch.Generator(device=DEV).manual_seed(0)
+    shapes = [(1003, 15, 3), (1003, 3), (1003,), (1000, 4)]
+    init = [torch.randn(s, device=DEV, generator=g) for s in shapes]
+    lrs = [1e-3, 2e-3, 5e-2, 1e-2]
+    a = [torch.nn.Parameter(t.clone()) for t in init]
+    b = [torch.nn.Parameter(t.clone()) for t in init]
+    oa = ShardedAdam(a, lrs, betas=(0.9, 0.999), eps=1e-15)
+    ob = FusedAdam(b, lrs, betas=(0.9, 0.999), eps=1e-15)
+    for _ in range(3):
+        grads = [torch.randn(s, device=DEV, generator=g) for s in shapes]
+        for p, q, gg in zip(a, b, grads):
+            p.grad, q.grad = gg.clone(), gg.clone()
+        oa.step()
+        ob.step()
+        oa.zero_grad()
+        ob.zero_grad()
+    torch.cuda.synchronize()
+    for p, q in zip(a, b):
+        torch.testing.assert_close(p.detach(), q.detach(), rtol=0, atol=0)
