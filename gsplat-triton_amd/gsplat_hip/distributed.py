@@ -184,13 +184,25 @@ class ShardedAdam:
         self.v_tail = [z(tot - main) for _, _, main, tot in self.layout]
         self.g_shard = [torch.empty(q * row, device=dev) for row, q, _, _ in self.layout]
         self.order = sorted(range(len(self.params)), key=lambda i: -self.params[i].numel())
+        self._pending = {}  # parameter index -> all-gather still in flight
+
+    def wait(self, indices=None):
+        """Order the current stream after the deferred all-gathers of these
+        parameters (all when None); no host synchronisation."""
+        for i in list(self._pending) if indices is None else indices:
+            wk = self._pending.pop(i, None)
+            if wk is not None:
+                wk.wait()
 
     def _shard(self, i, flat):
         row, q, _, _ = self.layout[i]
         return flat[self.rank * q * row:(self.rank + 1) * q * row]
 
     @torch.no_grad()
-    def step(self):
+    def step(self, defer_gather=False):
+        """defer_gather: leave the all-gathers in flight; the caller orders
+        each parameter's next use after `wait([i])` (stream order only)."""
+        self.wait()
         self.step_count += 1
         flats, works = {}, []
         for i in self.order:
@@ -218,15 +230,16 @@ class ShardedAdam:
                         [flats[i][self.layout[i][2]:] for i in tails],
                         [self.m_tail[i] for i in tails], [self.v_tail[i] for i in tails],
                         [self.lrs[i] for i in tails], self.betas, self.eps, self.step_count)
-        works = []
-        for i in self.order:
+        # geometry first (the next forward's projection needs it first), the
+        # large SH rows last
+        for i in sorted(self.order, key=lambda i: self.params[i].numel()):
             _, _, main, _ = self.layout[i]
             if main:
                 full = self.params[i].data.view(-1)[:main]
-                works.append(dist.all_gather_into_tensor(full, self._shard(i, full).clone(),
-                                                         async_op=True))
-        for wk in works:
-            wk.wait()
+                self._pending[i] = dist.all_gather_into_tensor(
+                    full, self._shard(i, full).clone(), async_op=True)
+        if not defer_gather:
+            self.wait()
 
     def zero_grad(self, set_to_none=True):
         for p in self.params:

@@ -10,7 +10,7 @@ the hot path can be exercised end to end without the rest of gsplat.
 """
 
 import math
-from typing import Dict, Optional, Tuple
+from typing import Callable, Dict, Optional, Tuple
 
 import torch
 from torch import Tensor
@@ -59,6 +59,7 @@ def rasterization(
     distributed: bool = False,
     camera_model: str = "pinhole",
     covars: Optional[Tensor] = None,
+    _colors_ready: Optional[Callable[[], None]] = None,
 ) -> Tuple[Tensor, Tensor, Dict]:
     """Rasterize N 3D Gaussians to C images (gsplat/rendering.py:44-598)."""
     meta = {}
@@ -138,41 +139,51 @@ def rasterization(
                                            tile_height, packed=packed, n_cameras=C,
                                            camera_ids=camera_ids, gaussian_ids=gaussian_ids)
 
-    if packed:  # colours of the nnz pairs (gsplat/rendering.py:368-408)
-        if sh_degree is None:
-            colors = colors[gaussian_ids] if colors.dim() == 2 else colors[camera_ids, gaussian_ids]
-        else:
-            camtoworlds = torch.inverse(viewmats)
-            dirs = means[gaussian_ids, :] - camtoworlds[camera_ids, :3, 3]
-            if sh_rest is not None:
-                shs = (colors[gaussian_ids], sh_rest[gaussian_ids])
-            elif colors.dim() == 3:
-                shs = colors[gaussian_ids]
+    def eval_colors(colors):
+        if packed:  # colours of the nnz pairs (gsplat/rendering.py:368-408)
+            if sh_degree is None:
+                colors = colors[gaussian_ids] if colors.dim() == 2 else colors[camera_ids, gaussian_ids]
             else:
-                shs = colors[camera_ids, gaussian_ids]
-            colors = spherical_harmonics(sh_degree, dirs, shs, masks=radii > 0)
+                camtoworlds = torch.inverse(viewmats)
+                dirs = means[gaussian_ids, :] - camtoworlds[camera_ids, :3, 3]
+                if sh_rest is not None:
+                    shs = (colors[gaussian_ids], sh_rest[gaussian_ids])
+                elif colors.dim() == 3:
+                    shs = colors[gaussian_ids]
+                else:
+                    shs = colors[camera_ids, gaussian_ids]
+                colors = spherical_harmonics(sh_degree, dirs, shs, masks=radii > 0)
+                colors = torch.clamp_min(colors + 0.5, 0.0)
+        elif sh_degree is None:
+            if colors.dim() == 2:
+                colors = colors[None] if C == 1 else colors.expand(C, -1, -1)
+        elif not viewmats.requires_grad and (sh_rest is not None or colors.dim() == 3):
+            # one kernel each way: dirs from the camera centres, radii masking,
+            # clamp_min(sh + 0.5, 0) (same values as the branch below)
+            colors = sh_colors(sh_degree, means, viewmats,
+                               colors if sh_rest is None else (colors, sh_rest), radii)
+        else:
+            camtoworlds = torch.inverse(viewmats)  # [C, 4, 4]
+            dirs = means[None, :, :] - camtoworlds[:, None, :3, 3]  # [C, N, 3]
+            masks = radii > 0
+            # broadcast over cameras without copies (read in place by the SH
+            # kernel); C == 1 uses an unsqueeze view so backward needs no reduction
+            def bcast(x):
+                return x[None] if C == 1 else x.expand(C, -1, -1, -1)
+            shs = bcast(colors) if colors.dim() == 3 else colors
+            if sh_rest is not None:
+                shs = (shs, bcast(sh_rest))
+            colors = spherical_harmonics(sh_degree, dirs, shs, masks=masks)  # [C, N, 3]
             colors = torch.clamp_min(colors + 0.5, 0.0)
-    elif sh_degree is None:
-        if colors.dim() == 2:
-            colors = colors[None] if C == 1 else colors.expand(C, -1, -1)
-    elif not viewmats.requires_grad and (sh_rest is not None or colors.dim() == 3):
-        # one kernel each way: dirs from the camera centres, radii masking,
-        # clamp_min(sh + 0.5, 0) (same values as the branch below)
-        colors = sh_colors(sh_degree, means, viewmats,
-                           colors if sh_rest is None else (colors, sh_rest), radii)
-    else:
-        camtoworlds = torch.inverse(viewmats)  # [C, 4, 4]
-        dirs = means[None, :, :] - camtoworlds[:, None, :3, 3]  # [C, N, 3]
-        masks = radii > 0
-        # broadcast over cameras without copies (read in place by the SH
-        # kernel); C == 1 uses an unsqueeze view so backward needs no reduction
-        def bcast(x):
-            return x[None] if C == 1 else x.expand(C, -1, -1, -1)
-        shs = bcast(colors) if colors.dim() == 3 else colors
-        if sh_rest is not None:
-            shs = (shs, bcast(sh_rest))
-        colors = spherical_harmonics(sh_degree, dirs, shs, masks=masks)  # [C, N, 3]
-        colors = torch.clamp_min(colors + 0.5, 0.0)
+        return colors
+
+    # _colors_ready (private, bench harness): a callable run right before the
+    # colours are evaluated, which are then evaluated after the tile
+    # intersection -- lets a sharded optimizer's all-gather of the SH
+    # coefficients overlap projection and isect (train_step.Trainer)
+    late = _colors_ready is not None and not packed and not distributed
+    if not late:
+        colors = eval_colors(colors)
 
     if distributed:  # gsplat/rendering.py:413-494
         if packed:
@@ -210,17 +221,26 @@ def rasterization(
                                            tile_height, packed=packed, n_cameras=C,
                                            camera_ids=camera_ids, gaussian_ids=gaussian_ids)
 
-    if render_mode in ["RGB+D", "RGB+ED"]:
-        colors = torch.cat((colors, depths[..., None]), dim=-1)
-        if backgrounds is not None:
-            backgrounds = torch.cat([backgrounds, torch.zeros(C, 1, device=backgrounds.device)], -1)
-    elif render_mode in ["D", "ED"]:
-        colors = depths[..., None]
-        if backgrounds is not None:
-            backgrounds = torch.zeros(C, 1, device=backgrounds.device)
+    def add_depth(colors, backgrounds):
+        if render_mode in ["RGB+D", "RGB+ED"]:
+            colors = torch.cat((colors, depths[..., None]), dim=-1)
+            if backgrounds is not None:
+                backgrounds = torch.cat([backgrounds, torch.zeros(C, 1, device=backgrounds.device)],
+                                        -1)
+        elif render_mode in ["D", "ED"]:
+            colors = depths[..., None]
+            if backgrounds is not None:
+                backgrounds = torch.zeros(C, 1, device=backgrounds.device)
+        return colors, backgrounds
+
+    if not late:
+        colors, backgrounds = add_depth(colors, backgrounds)
 
     tiles_per_gauss, isect_ids, flatten_ids = pending_isects.finish(sort=True)
     isect_offsets = isect_offset_encode(isect_ids, C, tile_width, tile_height)
+    if late:
+        _colors_ready()
+        colors, backgrounds = add_depth(eval_colors(colors), backgrounds)
     meta.update({"tile_width": tile_width, "tile_height": tile_height,
                  "tiles_per_gauss": tiles_per_gauss, "isect_ids": isect_ids,
                  "flatten_ids": flatten_ids, "isect_offsets": isect_offsets, "width": width,

@@ -106,7 +106,7 @@ class Trainer:
 
     def __init__(self, points, rgbs, viewmats, Ks, width, height, sh_degree=3, device="cuda",
                  seed=42, world_size=1, rank=0, ssim_lambda=0.2, scene_scale=1.0,
-                 fused=True, model="3dgs", sharded_optimizer=True):
+                 fused=True, model="3dgs", sharded_optimizer=None):
         assert model in ("3dgs", "2dgs"), model
         self.model = model
         g = torch.Generator().manual_seed(seed)  # identical on every rank (replicas)
@@ -138,7 +138,10 @@ class Trainer:
         self.fused = fused
         # N > 1: gradients reduce-scattered, Adam on this rank's rows, rows
         # all-gathered (distributed.ShardedAdam) instead of all-reduce + full Adam
-        self.sharded = fused and sharded_optimizer and world_size > 1
+        # (None: when world_size > 1; True also at world_size 1, for tests)
+        if sharded_optimizer is None:
+            sharded_optimizer = world_size > 1
+        self.sharded = fused and sharded_optimizer
         if self.sharded:
             from .distributed import ShardedAdam
             self.opt = ShardedAdam([g["params"][0] for g in groups], [g["lr"] for g in groups],
@@ -161,11 +164,21 @@ class Trainer:
 
     def render(self, ci: int):
         p = self.params
+        hook = None
+        if self.sharded:
+            # the previous step's all-gathers: geometry before the projection,
+            # the SH rows only before the colours (evaluated after isect)
+            names = list(self.params)
+            self.opt.wait([names.index(k) for k in ("means", "scales", "quats", "opacities")])
+            sh_idx = [names.index(k) for k in ("sh0", "shN")]
+            hook = lambda: self.opt.wait(sh_idx)  # noqa: E731
         if self.fused:  # one HIP launch each way for both activations
             scales, opac = activate(p["scales"], p["opacities"])
         else:
             scales, opac = torch.exp(p["scales"]), torch.sigmoid(p["opacities"])
         if self.model == "2dgs":
+            if hook is not None:
+                hook()
             rc, ra, _, _, _, _, meta = rasterization_2dgs(
                 p["means"], p["quats"], scales, opac, (p["sh0"], p["shN"]),
                 self.viewmats[ci:ci + 1], self.Ks[ci:ci + 1], self.width, self.height,
@@ -176,7 +189,8 @@ class Trainer:
             p["means"], p["quats"], scales, opac,
             (p["sh0"], p["shN"]) if self.fused else torch.cat([p["sh0"], p["shN"]], 1), self.viewmats[ci:ci + 1], self.Ks[ci:ci + 1],
             self.width, self.height, sh_degree=self.sh_degree, packed=False,
-            near_plane=0.01, far_plane=1e10, radius_clip=0.0, rasterize_mode="classic")
+            near_plane=0.01, far_plane=1e10, radius_clip=0.0, rasterize_mode="classic",
+            _colors_ready=hook)
 
     def step(self, it: int):
         ci = self.camera_index(it)
@@ -195,7 +209,10 @@ class Trainer:
         if self.world_size > 1 and not self.sharded:
             self.allreduce_grads()
         self.update_state(meta)
-        self.opt.step()
+        if self.sharded:
+            self.opt.step(defer_gather=True)
+        else:
+            self.opt.step()
         self.opt.zero_grad(set_to_none=True)
         self.last_meta = meta
         return loss
