@@ -103,10 +103,14 @@ def _oracle_fwd(sc, masks=None):
                             masks, sc["W"], sc["H"], sc["ts"], sc["off"], sc["fids"])
 
 
-@pytest.mark.parametrize("seed,D,bg,C", [(0, 4, True, 1), (1, 3, False, 1), (2, 1, True, 2),
-                                         (3, 8, True, 1), (4, 33, False, 1)])
-def test_raster2dgs_fwd(seed, D, bg, C):
-    sc = surfel_scene(seed, N=300, W=70, H=52, D=D, bg=bg, C=C)
+@pytest.mark.parametrize("seed,D,bg,C,thin", [(0, 4, True, 1, False), (1, 3, False, 1, False),
+                                              (2, 1, True, 2, False), (3, 8, True, 1, False),
+                                              (4, 33, False, 1, False), (5, 4, True, 1, True),
+                                              (6, 3, False, 2, True)])
+def test_raster2dgs_fwd(seed, D, bg, C, thin):
+    """thin: needle surfels, many edge-on -- the strip culling's ellipse test
+    (surfel_keep) must never drop a contributing record."""
+    sc = surfel_scene(seed, N=300, W=70, H=52, D=D, bg=bg, C=C, thin=thin)
     assert len(sc["fids"]) > 200
     _, _, _, (rc, ra, rn, rd, rm) = _raster_gpu(sc)
     oc, oa, on, od, om, ol, omi = _oracle_fwd(sc)
@@ -127,10 +131,13 @@ def test_raster2dgs_fwd_masks():
     close_most(ra, oa, 1e-4, 1e-4, "alphas", max_frac=5e-3)
 
 
-@pytest.mark.parametrize("seed,D,bg,absgrad", [(0, 4, True, False), (1, 3, False, True),
-                                               (2, 1, True, False), (6, 9, True, True)])
-def test_raster2dgs_bwd(seed, D, bg, absgrad):
-    sc = surfel_scene(seed, N=300, W=70, H=52, D=D, bg=bg)
+@pytest.mark.parametrize("seed,D,bg,absgrad,thin", [(0, 4, True, False, False),
+                                                    (1, 3, False, True, False),
+                                                    (2, 1, True, False, False),
+                                                    (6, 9, True, True, False),
+                                                    (7, 4, True, False, True)])
+def test_raster2dgs_bwd(seed, D, bg, absgrad, thin):
+    sc = surfel_scene(seed, N=300, W=70, H=52, D=D, bg=bg, thin=thin)
     leaves, bgt, densify, outs = _raster_gpu(sc, absgrad=absgrad)
     rng = np.random.default_rng(seed + 100)
     vs = [rng.standard_normal(o.shape).astype(np.float32) for o in outs]

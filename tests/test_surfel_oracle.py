@@ -80,11 +80,14 @@ def test_proj2dgs_bwd_golden_exact_part():
 
 
 # ---------------------------------------------------------------- raster ---
-def surfel_scene(seed=0, N=60, W=40, H=36, D=4, bg=True, C=1):
+def surfel_scene(seed=0, N=60, W=40, H=36, D=4, bg=True, C=1, thin=False):
     rng = np.random.default_rng(seed)
     means = (rng.standard_normal((N, 3)) * [0.5, 0.5, 0.3] + [0, 0, 3]).astype(np.float32)
     quats = rng.standard_normal((N, 4)).astype(np.float32)
     scales = (rng.random((N, 3)) * 0.25 + 0.05).astype(np.float32)
+    if thin:  # needle-like surfels (one axis 100x shorter), many seen edge-on
+        scales[:, 0] = rng.uniform(0.2, 0.8, N)
+        scales[:, 1] = rng.uniform(0.001, 0.008, N)
     vm = np.tile(np.eye(4, dtype=np.float32), (C, 1, 1))
     vm[:, 0, 3] = np.arange(C) * 0.1
     K = np.tile(np.array([[60.0, 0, W / 2], [0, 60.0, H / 2], [0, 0, 1]], np.float32), (C, 1, 1))
