@@ -26,6 +26,7 @@
 #include <rocprim/device/device_radix_sort.hpp>
 
 #include "lsd_sort.h"
+#include "wave_ops.h"
 
 namespace gs {
 
@@ -234,8 +235,9 @@ isect_compact_kernel(int64_t G, const int32_t *__restrict__ tiles_per_gauss,
 __global__ void __launch_bounds__(kIsectBlock)
 isect_sorted_count_kernel(int64_t nV, const int32_t *__restrict__ Vs,
                           const int32_t *__restrict__ tiles_per_gauss,
-                          int64_t *__restrict__ block_sums) {
+                          int64_t *__restrict__ block_sums, int32_t *__restrict__ n_big) {
   __shared__ int64_t lds[kIsectBlock / 64 + 1];
+  if (blockIdx.x == 0 && threadIdx.x == 0) *n_big = 0;  // big list of the emit kernel
   const int64_t s = (int64_t)blockIdx.x * kIsectBlock + threadIdx.x;
   const int cnt = (s < nV) ? tiles_per_gauss[Vs[s]] : 0;
   int64_t tot;
@@ -245,10 +247,19 @@ isect_sorted_count_kernel(int64_t nV, const int32_t *__restrict__ Vs,
 
 // (2b) emit (cam|tile key, Gaussian index) in depth order.  A Gaussian with
 // at most kLaneTiles tiles is written by its own lane; a larger one by its
-// whole wave (lanes stride over its tiles, coalesced stores), so the few
-// huge near-camera Gaussians do not serialise one lane for thousands of
-// tiles.
+// whole wave (lanes stride over its tiles, coalesced stores); one with more
+// than kGridTiles (near-camera or near-degenerate 2DGS surfels cover the
+// whole image) goes to a list that isect_big_emit_kernel spreads over the
+// whole grid -- adjacent in depth order, such Gaussians would otherwise
+// serialise a few waves for hundreds of thousands of stores.
 constexpr int kLaneTiles = 32;
+constexpr int kGridTiles = 1024;
+
+struct BigEmit {
+  int64_t cur;  // first output slot
+  int32_t i, n, x0, y0, w;
+  uint32_t hi;
+};
 
 __global__ void __launch_bounds__(kIsectBlock)
 isect_sorted_emit_kernel(int64_t nV, int N, const int32_t *__restrict__ Vs,
@@ -256,7 +267,8 @@ isect_sorted_emit_kernel(int64_t nV, int N, const int32_t *__restrict__ Vs,
                          const float *__restrict__ depths, const int32_t *__restrict__ camera_ids,
                          int ts, int tw, int th, int tile_bits, uint32_t key_all_ones,
                          const int64_t *__restrict__ block_prefix, uint32_t *__restrict__ tkey,
-                         int32_t *__restrict__ val) {
+                         int32_t *__restrict__ val, BigEmit *__restrict__ big_list,
+                         int32_t *__restrict__ n_big) {
   __shared__ int64_t lds[kIsectBlock / 64 + 1];
   const int64_t s = (int64_t)blockIdx.x * kIsectBlock + threadIdx.x;
   const int lane = threadIdx.x & 63;
@@ -282,7 +294,25 @@ isect_sorted_emit_kernel(int64_t nV, int N, const int32_t *__restrict__ Vs,
         ++cur;
       }
   }
-  uint64_t big = __ballot(cnt > kLaneTiles);
+  // huge: one slot per lane in the big list (one atomic per wave)
+  const uint64_t huge = __ballot(cnt > kGridTiles);
+  if (huge) {
+    int base = 0;
+    if (lane == 0) base = atomicAdd(n_big, __popcll(huge));
+    base = __shfl(base, 0, 64);
+    if (cnt > kGridTiles) {
+      BigEmit e;
+      e.cur = cur0;
+      e.i = i;
+      e.n = cnt;
+      e.x0 = rc.x0;
+      e.y0 = rc.y0;
+      e.w = rc.x1 - rc.x0;
+      e.hi = hi;
+      big_list[base + ballot_slot(huge)] = e;
+    }
+  }
+  uint64_t big = __ballot(cnt > kLaneTiles && cnt <= kGridTiles);
   while (big) {
     const int src = __builtin_ctzll(big);
     big &= big - 1;
@@ -297,6 +327,31 @@ isect_sorted_emit_kernel(int64_t nV, int N, const int32_t *__restrict__ Vs,
       const uint32_t tile = (uint32_t)((gy0 + (int)yy) * tw + gx0 + (int)xx);
       tkey[c0 + k] = ghi == key_all_ones ? key_all_ones : (ghi | tile);
       val[c0 + k] = gi;
+    }
+  }
+}
+
+// (2c) the huge Gaussians of the list: kBigParts workgroups per Gaussian,
+// each writing a contiguous 1/kBigParts of its tiles (coalesced).
+constexpr int kBigParts = 16;
+constexpr int kBigBlocks = 4096;
+
+__global__ void __launch_bounds__(256)
+isect_big_emit_kernel(const BigEmit *__restrict__ big_list, const int32_t *__restrict__ n_big,
+                      int tw, uint32_t key_all_ones, uint32_t *__restrict__ tkey,
+                      int32_t *__restrict__ val) {
+  const int nb = *n_big;
+  const int part = blockIdx.x % kBigParts;
+  for (int e = blockIdx.x / kBigParts; e < nb; e += kBigBlocks / kBigParts) {
+    const BigEmit g = big_list[e];
+    const int k0 = (int)(((int64_t)g.n * part) / kBigParts);
+    const int k1 = (int)(((int64_t)g.n * (part + 1)) / kBigParts);
+    const uint32_t w = (uint32_t)g.w;
+    for (int k = k0 + threadIdx.x; k < k1; k += 256) {
+      const uint32_t yy = (uint32_t)k / w, xx = (uint32_t)k - yy * w;
+      const uint32_t tile = (uint32_t)((g.y0 + (int)yy) * tw + g.x0 + (int)xx);
+      tkey[g.cur + k] = g.hi == key_all_ones ? key_all_ones : (g.hi | tile);
+      val[g.cur + k] = g.i;
     }
   }
 }
@@ -410,7 +465,7 @@ extern "C" int gsplat_hip_isect_offsets(int64_t n_isects, const int64_t *isect_i
 // ------------------------------------------------------- depth-first path --
 namespace {
 struct SortedLayout {
-  size_t V, dkey, Vs, dkeys, blk, tkey, val, tkeys, vals, tmp, total;
+  size_t V, dkey, Vs, dkeys, blk, big, nbig, tkey, val, tkeys, vals, tmp, total;
   size_t tmp_bytes;
 };
 
@@ -426,6 +481,8 @@ SortedLayout sorted_layout(int64_t nV, int64_t n, int key_bits) {
   L.Vs = o; o = align256(o + 4 * (size_t)nV);
   L.dkeys = o; o = align256(o + 4 * (size_t)nV);
   L.blk = o; o = align256(o + 8 * (size_t)((nV + kIsectBlock - 1) / kIsectBlock + 2));
+  L.big = o; o = align256(o + sizeof(BigEmit) * (size_t)nV);
+  L.nbig = o; o = align256(o + 4);
   L.tkey = o; o = align256(o + 4 * (size_t)n);
   L.val = o; o = align256(o + 4 * (size_t)n);
   L.tkeys = o; o = align256(o + 4 * (size_t)n);
@@ -478,14 +535,18 @@ extern "C" int gsplat_hip_isect_write_sorted(
   // stable depth sort of the visible Gaussians (32 key bits)
   if (lsd_sort_pairs(dkey, V, dkeys, Vs, n_visible, 0, 32, tmp, st) == 0) Vs = V;
   const int64_t nbV = (n_visible + kIsectBlock - 1) / kIsectBlock;
+  BigEmit *big_list = reinterpret_cast<BigEmit *>(ws + L.big);
+  int32_t *n_big = reinterpret_cast<int32_t *>(ws + L.nbig);
   hipLaunchKernelGGL(isect_sorted_count_kernel, dim3((unsigned)nbV), dim3(kIsectBlock), 0, st,
-                     n_visible, Vs, tiles_per_gauss, blk);
+                     n_visible, Vs, tiles_per_gauss, blk, n_big);
   hipLaunchKernelGGL(isect_scan_blocks_kernel, dim3(1), dim3(1024), 0, st, nbV, blk, nullptr,
                      nullptr);
   const uint32_t all_ones = key_bits >= 32 ? 0xffffffffu : ((1u << key_bits) - 1u);
   hipLaunchKernelGGL(isect_sorted_emit_kernel, dim3((unsigned)nbV), dim3(kIsectBlock), 0, st,
                      n_visible, N, Vs, means2d, radii, depths, camera_ids, tile_size, tile_width,
-                     tile_height, tile_bits, all_ones, blk, tkey, val);
+                     tile_height, tile_bits, all_ones, blk, tkey, val, big_list, n_big);
+  hipLaunchKernelGGL(isect_big_emit_kernel, dim3(kBigBlocks), dim3(256), 0, st, big_list, n_big,
+                     tile_width, all_ones, tkey, val);
   // stable (camera, tile) sort keeps the depth order inside every tile; its
   // last pass writes isect_ids / flatten_ids directly
   if (key_bits > 0) {

@@ -178,6 +178,30 @@ def test_isect_random_vs_oracle_large_radii(isect_mode):
     assert np.array_equal(off.cpu().numpy(), O.isect_offset_encode(oids, C, tw, th))
 
 
+def test_isect_huge_gaussians_vs_oracle(isect_mode):
+    """Gaussians covering thousands of tiles (the grid-wide emission path,
+    > 1024 tiles), many of them adjacent in depth order, some with negative
+    depth (all-ones key), mixed with small ones: exact."""
+    import gsplat_hip
+    from oracle import gsplat_oracle as O
+    rng = np.random.default_rng(7)
+    C, N, W, H, ts = 2, 2500, 1100, 900, 16
+    tw, th = math.ceil(W / ts), math.ceil(H / ts)
+    m2 = rng.uniform(-100, 1200, (C, N, 2)).astype(np.float32)
+    r = rng.choice([0, 2, 9, 40, 200], (C, N)).astype(np.int32)
+    d = rng.uniform(1.0, 50, (C, N)).astype(np.float32)
+    huge = rng.choice(N, 150, replace=False)
+    r[:, huge] = rng.integers(300, 5000, (C, 150))
+    d[:, huge] = rng.uniform(0.01, 0.02, (C, 150))  # nearest: adjacent after the depth sort
+    d[0, huge[:10]] = -1.0
+    tpg, ids, fids = gsplat_hip.isect_tiles(T(m2), T(r), T(d), ts, tw, th)
+    otpg, oids, ofids = O.isect_tiles(m2, r, d, ts, tw, th)
+    assert int((otpg > 1024).sum()) >= 100
+    assert np.array_equal(tpg.cpu().numpy(), otpg)
+    assert np.array_equal(ids.cpu().numpy(), oids)
+    assert np.array_equal(fids.cpu().numpy(), ofids)
+
+
 @pytest.mark.parametrize("C,tw,th", [(1, 4, 4), (2, 5, 3), (4, 8, 8)])
 def test_isect_negative_and_tied_depths(isect_mode, C, tw, th):
     """Negative depths (sign-extended ids that land in the all-ones (cam, tile)
