@@ -623,6 +623,136 @@ __global__ void __launch_bounds__(1024) fwd_kernel(RasterArgs a) {
   a.median_ids[pid] = med;
 }
 
+// Forward with two pixels per lane (tile_size 16): wave w of the 2 owns the
+// 16x8 band of rows 8w..8w+7, lane l the pixels (l & 15, 8w + (l >> 4)) and
+// 4 rows below.  Two independent transmittance chains per lane give the
+// scheduler independent work between dependent steps, and the gather,
+// culling test and LDS reads of a record are shared by both pixels.  Same
+// per-pixel arithmetic as fwd_kernel.
+template <int D>
+__global__ void __launch_bounds__(128) fwd2_kernel(RasterArgs a) {
+  using R = FRec<D>;
+  extern __shared__ float4 lds4[];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  float *q = reinterpret_cast<float *>(lds4) + (size_t)w * 64 * R::NF;
+  const int tile = blockIdx.x;
+  const int ntile = a.tw * a.th;
+  const int c = tile / ntile;
+  const int rem = tile - c * ntile;
+  const int ty = rem / a.tw, tx = rem - ty * a.tw;
+  const int64_t start = a.offsets[tile];
+  const int64_t end = (tile == a.n_tiles - 1) ? a.n_isects : (int64_t)a.offsets[tile + 1];
+  const float rx0 = tx * 16 + 0.5f, rx1 = rx0 + 15.f;
+  const float ry0 = ty * 16 + 8 * w + 0.5f, ry1 = ry0 + 7.f;
+  const float *bg = a.backgrounds ? a.backgrounds + (int64_t)c * D : nullptr;
+  const bool masked = a.masks && !a.masks[tile];
+  const float fx = (float)(tx * 16 + (lane & 15)) + 0.5f;
+  float fy[2], T[2], col[2][D], nrm[2][3], distort[2], acc_vd[2], median[2];
+  int32_t cur[2], med[2];
+  bool done[2], inside[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int py = ty * 16 + 8 * w + 4 * k + (lane >> 4);
+    fy[k] = (float)py + 0.5f;
+    inside[k] = (tx * 16 + (lane & 15)) < a.W && py < a.H;
+    T[k] = 1.f;
+#pragma unroll
+    for (int d = 0; d < D; ++d) col[k][d] = 0.f;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) nrm[k][i] = 0.f;
+    distort[k] = acc_vd[k] = median[k] = 0.f;
+    cur[k] = med[k] = 0;
+    done[k] = !inside[k] || masked;
+  }
+
+  int64_t b = start;
+  const bool run = !masked && b < end;
+  Gathered<D> nxt;
+  if (run) gather<D>(a, b + lane, b + lane < end, nxt);
+  for (; run && b < end; b += 64) {
+    if (__ballot(!(done[0] & done[1])) == 0) break;
+    const bool keep = (b + lane < end) &&
+                      surfel_keep(nxt.m, nxt.xy.x, nxt.xy.y, nxt.op, rx0, rx1, ry0, ry1);
+    const uint64_t km = __ballot(keep);
+    const int n = __popcll(km);
+    if (keep) stage_fwd<D>(q + ballot_slot(km) * R::NF, nxt, (int32_t)(b + lane));
+    wave_sync_lds();
+    if (b + 64 < end) gather<D>(a, b + 64 + lane, b + 64 + lane < end, nxt);
+    for (int t = 0; t < n; ++t) {
+      float r[R::NF];
+      read_f4<R::NF>(q + t * R::NF, r);
+      const float rxb = fx * r[R::A] + r[R::CC], ryb = fx * r[R::A + 1] + r[R::CC + 1],
+                  rzb = fx * r[R::A + 2] + r[R::CC + 2];
+      const float dx = r[R::X] - fx, dx2 = dx * dx;
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        if (done[k]) continue;
+        const float rx = fy[k] * r[R::B] + rxb;
+        const float ry = fy[k] * r[R::B + 1] + ryb;
+        const float rz = fy[k] * r[R::B + 2] + rzb;
+        const float iz = __builtin_amdgcn_rcpf(rz);
+        const float g3 = (rx * rx + ry * ry) * (iz * iz);
+        const float dy = r[R::Y] - fy[k];
+        const float g2 = kLog2e * (dx2 + dy * dy);
+        const float m = fminf(g3, g2);  // sigma * log2(e)
+        if (rz != 0.f && m <= r[R::SMAX]) {
+          const float alpha = fminf(kAlphaMax, r[R::OP] * __builtin_amdgcn_exp2f(-m));
+          const float nT = T[k] * (1.f - alpha);
+          if (nT <= kTMin) {
+            done[k] = true;
+          } else {
+            const float vis = alpha * T[k];
+#pragma unroll
+            for (int d = 0; d < D; ++d) col[k][d] += r[R::COL + d] * vis;
+#pragma unroll
+            for (int i = 0; i < 3; ++i) nrm[k][i] += r[R::NRM + i] * vis;
+            const float depth = r[R::COL + D - 1];
+            distort[k] += 2.f * (vis * depth * (1.f - T[k]) - vis * acc_vd[k]);
+            acc_vd[k] += vis * depth;
+            const int32_t idx = __float_as_int(r[R::IDX]);
+            if (T[k] > 0.5f) {
+              median[k] = depth;
+              med[k] = idx;
+            }
+            cur[k] = idx;
+            T[k] = nT;
+          }
+        }
+      }
+      if ((t & 7) == 7 && __ballot(!(done[0] & done[1])) == 0) break;
+    }
+    wave_sync_lds();
+  }
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    if (!inside[k]) continue;
+    const int64_t pid = ((int64_t)c * a.H + (ty * 16 + 8 * w + 4 * k + (lane >> 4))) * a.W +
+                        tx * 16 + (lane & 15);
+    if (masked) {  // as fwd_kernel
+#pragma unroll
+      for (int d = 0; d < D; ++d) a.render_colors[pid * D + d] = bg ? bg[d] : 0.f;
+      a.render_alphas[pid] = 0.f;
+#pragma unroll
+      for (int i = 0; i < 3; ++i) a.render_normals[pid * 3 + i] = 0.f;
+      a.render_distort[pid] = 0.f;
+      a.render_median[pid] = 0.f;
+      a.last_ids[pid] = 0;
+      a.median_ids[pid] = 0;
+      continue;
+    }
+    a.render_alphas[pid] = 1.f - T[k];
+#pragma unroll
+    for (int d = 0; d < D; ++d)
+      a.render_colors[pid * D + d] = bg ? col[k][d] + T[k] * bg[d] : col[k][d];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) a.render_normals[pid * 3 + i] = nrm[k][i];
+    a.render_distort[pid] = distort[k];
+    a.render_median[pid] = median[k];
+    a.last_ids[pid] = cur[k];
+    a.median_ids[pid] = med[k];
+  }
+}
+
 // Gradient fields of a packed row: colour[D], normal[3], ray transform[9],
 // means2d[2], opacity, |means2d|[2] (absgrad only).
 template <int D, bool ABS>
@@ -1009,6 +1139,14 @@ bool channels_supported(int D) {
   return false;
 }
 
+bool fwd2_enabled() {
+  static const bool v = [] {
+    const char *e = getenv("GSPLAT_HIP_FWD_PX");
+    return !(e && atoi(e) == 1);
+  }();
+  return v;
+}
+
 bool bwd2_enabled() {
   static const bool v = [] {
     const char *e = getenv("GSPLAT_HIP_BWD_PX");
@@ -1121,10 +1259,15 @@ extern "C" int gsplat_hip_rasterize_2dgs_fwd(
   a.render_median = render_median; a.last_ids = last_ids; a.median_ids = median_ids;
   const int waves = (tile_size * tile_size + 63) / 64;
   hipStream_t st = (hipStream_t)stream;
+  // 16x16 tiles: two pixels per lane (fwd2_kernel) unless GSPLAT_HIP_FWD_PX=1
+  const bool px2 = tile_size == 16 && fwd2_enabled();
 #define GS_CASE(n)                                                                            \
   if (D == n) {                                                                               \
     const size_t lds = (size_t)waves * 64 * Rec<n>::NF * sizeof(float);                       \
-    hipLaunchKernelGGL(fwd_kernel<n>, dim3(n_tiles), dim3(64 * waves), lds, st, a);           \
+    if (px2)                                                                                  \
+      hipLaunchKernelGGL(fwd2_kernel<n>, dim3(n_tiles), dim3(128), lds / 2, st, a);           \
+    else                                                                                      \
+      hipLaunchKernelGGL(fwd_kernel<n>, dim3(n_tiles), dim3(64 * waves), lds, st, a);         \
   }
   GS_SURFEL_CHANNELS(GS_CASE)
 #undef GS_CASE
