@@ -543,6 +543,201 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) f
   tl_store(a, t_start, lane);
 }
 
+// Forward, two pixels per lane: a wave owns the 16x8 band of rows 8w..8w+7
+// of its tile, lane l the pixels (l & 15, 8w + (l >> 4)) and 4 rows below;
+// the two waves of a workgroup cover the tile.  Each lane runs two
+// independent transmittance chains over the same records, which hides the
+// per-record dependency latency that bounds the one-pixel kernel, and the
+// gather, strip culling and LDS reads of a record are shared by both
+// pixels.  Same per-pixel arithmetic as fwd_kernel; not the default (see
+// fwd_px()).
+template <int D>
+// register budget: 168 VGPRs = 3 waves per SIMD
+__global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(3))) fwd2_kernel(Args a) {
+  using P = FwdPair<D>;
+  constexpr int N4 = P::N4;
+  __shared__ float4 stage_all[2][32 * N4];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  float4 *st = stage_all[w];
+  const uint64_t t_start = tl_now(a);
+  const int tile = a.order ? a.order[blockIdx.x] : (int)blockIdx.x;
+  const int ntile = a.tw * a.th;
+  const int c = tile / ntile;
+  const int rem = tile - c * ntile;
+  const int ty = rem / a.tw, tx = rem - ty * a.tw;
+  const int px = tx * kTS + (lane & 15);
+  const int py0 = ty * kTS + 8 * w + (lane >> 4);
+  const float rx0 = tx * kTS + 0.5f, rx1 = rx0 + (kTS - 1);
+  const float ry0 = ty * kTS + 8 * w + 0.5f, ry1 = ry0 + 7.f;
+  const float fx = (float)px + 0.5f;
+  const int64_t start = a.offsets[tile];
+  const int64_t end = (tile == a.n_tiles - 1) ? a.n_isects : (int64_t)a.offsets[tile + 1];
+  const bool skip_tile = a.masks && a.masks[tile];
+
+  // per pixel k: colour of even (.x) / odd (.y) records of each pair in the
+  // current chunk, tot: the chunks before it; T < 0 marks a finished pixel
+  f2v acc[2][D];
+  float tot[2][D], T[2], fy[2];
+  int32_t last[2];
+  bool inside[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int py = py0 + 4 * k;
+    fy[k] = (float)py + 0.5f;
+    inside[k] = px < a.W && py < a.H;
+    T[k] = (!inside[k] || skip_tile) ? -1.f : 1.f;
+    last[k] = 0;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      acc[k][d] = f2v{0.f, 0.f};
+      tot[k][d] = 0.f;
+    }
+  }
+  auto alive = [&]() { return __ballot((T[0] > 0.f) | (T[1] > 0.f)) != 0; };
+
+  if (!skip_tile && start < end) {
+    auto id_at = [&](int64_t b0) -> int32_t {
+      return a.flatten_ids[min(b0 + lane, end - 1)];
+    };
+    bool done = false;
+    auto blend = [&](int k, float s2, float smax, float al, float idx) -> float {
+      const float nT = __builtin_fmaf(-T[k], al, T[k]);
+      const bool hit = __float_as_uint(s2) <= __float_as_uint(smax);
+      const bool gt = nT > kTMin;
+      const bool ok = hit & gt;
+      const float Tsel = ok ? nT : T[k];
+      const float vis = T[k] - Tsel;
+      T[k] = (hit & !gt) ? -fabsf(T[k]) : Tsel;
+      last[k] = ok ? __float_as_int(idx) : last[k];
+      return vis;
+    };
+    auto composite = [&](int cnt) {
+      const int np = (cnt + 1) >> 1;
+      for (int pb = 0; pb < np; pb += 8) {
+        const int pe = min(np, pb + 8);
+        for (int p = pb; p < pe; ++p) {
+          const float4 *q = st + p * N4;
+          f2v f[2 * N4];
+          float4 v[N4];
+#pragma unroll
+          for (int i = 0; i < N4; ++i) v[i] = q[i];
+#pragma unroll
+          for (int i = 0; i < N4; ++i) {
+            asm volatile("" ::"v"(v[i].x), "v"(v[i].y), "v"(v[i].z), "v"(v[i].w));
+            f[2 * i] = f2v{v[i].x, v[i].y};
+            f[2 * i + 1] = f2v{v[i].z, v[i].w};
+          }
+          const f2v dx = f[0] - fx;
+          const f2v adx = f[2] * dx;
+#pragma unroll
+          for (int k = 0; k < 2; ++k) {
+            const f2v dy = f[1] - fy[k];
+            const f2v s2 = dx * (adx + f[3] * dy) + f[4] * dy * dy;  // sigma * log2(e)
+            f2v al = f[5] * f2v{__builtin_amdgcn_exp2f(-s2.x), __builtin_amdgcn_exp2f(-s2.y)};
+            al.x = fminf(al.x, kAlphaMax);
+            al.y = fminf(al.y, kAlphaMax);
+            const float v0 = blend(k, s2.x, f[6].x, al.x, f[7].x);
+            const float v1 = blend(k, s2.y, f[6].y, al.y, f[7].y);
+            const f2v vis = f2v{v0, v1};
+#pragma unroll
+            for (int d = 0; d < D; ++d)
+              acc[k][d] = __builtin_elementwise_fma(vis, f[8 + d], acc[k][d]);
+          }
+        }
+        if (!alive()) {
+          done = true;
+          return;
+        }
+      }
+    };
+    auto stage = [&](const Attr<D> &at, int64_t b0) -> int {
+      const bool keep = (b0 + lane < end) && keep_attr<D>(at, rx0, rx1, ry0, ry1);
+      const uint64_t m = __ballot(keep);
+      const int cnt = __popcll(m);
+      if (keep) stage_fwd_pair<D>(st, ballot_slot(m), at, (int32_t)(b0 + lane));
+      if ((cnt & 1) && lane == 0) stage_fwd_pad<D>(st, cnt);
+      wave_sync_lds();
+      return cnt;
+    };
+    // chunk state for the chunked backward, as fwd_kernel
+    const int64_t L = a.L;
+    auto slot = [&](int64_t bidx) { return a.state + (bidx / L) * (int64_t)(kTS * kTS * (1 + D)); };
+    int64_t cur_b = start;
+    auto close_chunk = [&]() {
+      float *sl = slot(cur_b);
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int pit = 128 * w + 64 * k + lane;  // row-major pixel of the tile
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+          const float cs = acc[k][d].x + acc[k][d].y;
+          if (cur_b > start) sl[(1 + d) * kTS * kTS + pit] = cs;
+          tot[k][d] += cs;
+          acc[k][d] = f2v{0.f, 0.f};
+        }
+      }
+    };
+    auto save_state = [&](int64_t bidx) {
+      close_chunk();
+      cur_b = bidx;
+#pragma unroll
+      for (int k = 0; k < 2; ++k) slot(bidx)[128 * w + 64 * k + lane] = T[k];
+    };
+    const bool chunked = a.state && L > 0 && end - start > L;
+    Attr<D> A, B;
+    load_attr<D>(a, id_at(start), A);
+    int32_t g_n = id_at(start + 64);
+    int64_t b0 = start;
+    while (b0 < end) {
+      if (!alive()) break;
+      if (chunked && b0 > start && (b0 - start) % L == 0) save_state(b0);
+      load_attr<D>(a, g_n, B);
+      g_n = id_at(b0 + 128);
+      composite(stage(A, b0));
+      wave_sync_lds();
+      b0 += 64;
+      if (done || b0 >= end) break;
+      if (chunked && (b0 - start) % L == 0) save_state(b0);
+      load_attr<D>(a, g_n, A);
+      g_n = id_at(b0 + 128);
+      composite(stage(B, b0));
+      wave_sync_lds();
+      b0 += 64;
+      if (done) break;
+    }
+    if (chunked) {
+      close_chunk();
+      for (int64_t bi = cur_b + L; bi < end; bi += L) {
+        float *sl = slot(bi);
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          const int pit = 128 * w + 64 * k + lane;
+          sl[pit] = T[k];
+#pragma unroll
+          for (int d = 0; d < D; ++d) sl[(1 + d) * kTS * kTS + pit] = 0.f;
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) tot[k][d] += acc[k][d].x + acc[k][d].y;
+    if (inside[k]) {
+      const int64_t pix = ((int64_t)c * a.H + py0 + 4 * k) * a.W + px;
+      float *oc = a.render_colors + pix * D;
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        const float bg = a.backgrounds ? a.backgrounds[c * D + d] : 0.f;
+        oc[d] = tot[k][d] + fabsf(T[k]) * bg;
+      }
+      a.render_alphas[pix] = 1.f - fabsf(T[k]);
+      a.last_ids[pix] = last[k];
+    }
+  }
+  tl_store(a, t_start, lane);
+}
+
 // Backward: batches of 64 isects from the back, same two-deep gather pipeline.
 template <int D, bool ABS>
 // register budget: 72 VGPRs = 7 waves per SIMD without spills
@@ -1128,6 +1323,19 @@ static int bwd_px() {
   return v;
 }
 
+// Pixels per lane in the forward (1: fwd_kernel, 16x4 per wave, default;
+// 2: fwd2_kernel, 16x8 per wave, GSPLAT_HIP_FWD_PX=2).  At M2 the two-pixel
+// kernel measured 0.29 ms against 0.216 ms (158 VGPRs, 3 waves per SIMD, and
+// the heaviest tiles' serial work per wave doubles) -- unlike the 2DGS
+// forward, where two pixels per lane won 32 %.
+static int fwd_px() {
+  static const int v = [] {
+    const char *e = getenv("GSPLAT_HIP_FWD_PX");
+    return (e && atoi(e) == 2) ? 2 : 1;
+  }();
+  return v;
+}
+
 static int dbg_flags() {
   static const int v = [] { const char *e = getenv("GSPLAT_HIP_DBG"); return e ? atoi(e) : 0; }();
   return v;
@@ -1143,7 +1351,10 @@ int r16_fwd(r16::Args a, const void *state, hipStream_t st) {
     hipLaunchKernelGGL(r16::tile_order_kernel, dim3(1), dim3(1024), 0, st, a.n_tiles, a.offsets,
                        a.n_isects, const_cast<int32_t *>(a.order));
   g_prepared_state = nullptr;
-  hipLaunchKernelGGL((r16::fwd_kernel<D>), dim3(a.n_tiles), dim3(256), 0, st, a);
+  if (fwd_px() == 2)
+    hipLaunchKernelGGL((r16::fwd2_kernel<D>), dim3(a.n_tiles), dim3(128), 0, st, a);
+  else
+    hipLaunchKernelGGL((r16::fwd_kernel<D>), dim3(a.n_tiles), dim3(256), 0, st, a);
   GS_CHECK_LAUNCH("rasterize_fwd16");
   return 0;
 }
