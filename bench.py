@@ -80,7 +80,7 @@ def pmc_traffic(config: str):
     per = {}
     for ctr in ("FETCH_SIZE", "WRITE_SIZE", "SQ_INSTS_VALU"):
         d = tempfile.mkdtemp(prefix="gsplat_pmc_", dir="/tmp")
-        regex = "surfel::fwd_kernel" if MODEL.get(config) == "2dgs" else "r16::fwd_kernel"
+        regex = "surfel::fwd2?_kernel" if MODEL.get(config) == "2dgs" else "r16::fwd2?_kernel"
         cmd = [rp, "--kernel-include-regex", regex, "--pmc", ctr, "-f", "csv",
                "-d", d, "-o", "p", "--", sys.executable, os.path.abspath(__file__), "--probe",
                "--config", config, "--warmup", "2"]
