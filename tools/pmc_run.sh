@@ -2,7 +2,7 @@
 # PMC passes on the bench workload, rasterizer + main kernels only.
 set -o pipefail
 export TMPDIR=/tmp
-OUT=$GRAFT_REPO_ROOT/gpurun_out/pmc7
+OUT=$GRAFT_REPO_ROOT/gpurun_out/${PMC_TAG:-pmc8}
 mkdir -p $OUT
 B="/usr/bin/python3 bench.py --steps 3 --warmup 2 --no-cpu-baseline --no-traffic"
 R='r16|adam|sh_bwd|ssim'
