@@ -1282,13 +1282,15 @@ chunk_items_kernel(int n_tiles, const int32_t *__restrict__ offsets, int64_t n_i
 }  // namespace r16
 
 // Chunk length in isects for the chunked backward (multiple of 64; 0 turns
-// chunking off).  GSPLAT_HIP_CHUNK overrides it for experiments.
+// chunking off).  GSPLAT_HIP_CHUNK overrides it for experiments.  256: at M2
+// the two-pixel backward took 0.47 ms against 0.51 (512) and 0.61 (1024) on
+// one box, for +6 us of chunk-state stores in the forward (tools/ab_chunk.sh).
 static int g_chunk = -1;  // -1: not yet read from the environment
 
 static int chunk_len() {
   if (g_chunk < 0) {
     const char *e = getenv("GSPLAT_HIP_CHUNK");
-    const int x = e ? atoi(e) : 1024;
+    const int x = e ? atoi(e) : 256;
     g_chunk = x <= 0 ? 0 : ((x + 63) / 64) * 64;
   }
   return g_chunk;

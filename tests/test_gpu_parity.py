@@ -361,7 +361,7 @@ def test_raster_chunked_backward(chunk):
             grads = torch.autograd.grad((rc * vrc).sum() + (ra * vra).sum(), ins,
                                         retain_graph=True)
         finally:
-            _lib.query("gsplat_hip_debug_set_chunk", 1024)
+            _lib.query("gsplat_hip_debug_set_chunk", 256)  # the library default
         return rc, ra, grads
 
     rc0, ra0, g0 = run(0)

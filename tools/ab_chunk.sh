@@ -1,0 +1,7 @@
+# Backward chunk length (GSPLAT_HIP_CHUNK) A/B on the M2 bench.
+set -o pipefail
+O=gpurun_out/${AB_TAG:-abchunk}; mkdir -p $O
+B="python bench.py --steps 40 --warmup 5 --no-cpu-baseline --no-traffic"
+for L in 1024 256 128 512 256 1024 128; do
+  GSPLAT_HIP_CHUNK=$L timeout -k 10 200 $B > $O/L$L.$RANDOM.json 2>>$O/err.log || exit 2
+done
