@@ -2,6 +2,6 @@
 set -o pipefail
 O=gpurun_out/${AB_TAG:-abchunk}; mkdir -p $O
 B="python bench.py --steps 40 --warmup 5 --no-cpu-baseline --no-traffic"
-for L in 1024 256 128 512 256 1024 128; do
+for L in 256 192 320 384 256 192 320; do
   GSPLAT_HIP_CHUNK=$L timeout -k 10 200 $B > $O/L$L.$RANDOM.json 2>>$O/err.log || exit 2
 done
