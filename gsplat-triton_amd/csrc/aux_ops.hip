@@ -173,6 +173,59 @@ selective_adam_kernel(int64_t n_rows, int64_t row, float *__restrict__ param,
   exp_avg_sq[e] = v;
 }
 
+
+// Normals from depth maps by central differences (gsplat/utils.py:137-224,
+// depth_to_normal): back-project the 4-neighbourhood of each pixel,
+// n = normalize((p[y+1,x] - p[y-1,x]) x (p[y,x+1] - p[y,x-1])), zero on the
+// one-pixel border.  One lane per pixel; the torch formula is a dozen
+// full-image passes.
+__device__ __forceinline__ void d2n_point(const float *dep, const float *c2w, const float *K,
+                                          int W, int x, int y, int z_depth, float p[3]) {
+  const float dx = ((float)x - K[2] + 0.5f) / K[0], dy = ((float)y - K[5] + 0.5f) / K[4];
+  float d[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) d[i] = c2w[4 * i] * dx + c2w[4 * i + 1] * dy + c2w[4 * i + 2];
+  if (!z_depth) {
+    const float n = fmaxf(sqrtf(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]), 1e-12f);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) d[i] /= n;
+  }
+  const float z = dep[(int64_t)y * W + x];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) p[i] = c2w[4 * i + 3] + z * d[i];
+}
+
+__global__ void __launch_bounds__(256)
+depth_to_normal_kernel(int C, int H, int W, const float *__restrict__ depths,
+                       const float *__restrict__ camtoworlds, const float *__restrict__ Ks,
+                       int z_depth, float *__restrict__ normals) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t HW = (int64_t)H * W;
+  if (i >= C * HW) return;
+  const int c = (int)(i / HW);
+  const int64_t r = i - c * HW;
+  const int y = (int)(r / W), x = (int)(r - (int64_t)y * W);
+  float *out = normals + 3 * i;
+  if (x == 0 || y == 0 || x == W - 1 || y == H - 1) {
+    out[0] = out[1] = out[2] = 0.f;
+    return;
+  }
+  const float *dep = depths + c * HW, *c2w = camtoworlds + 16 * c, *K = Ks + 9 * c;
+  float pu[3], pd[3], pl[3], pr[3];
+  d2n_point(dep, c2w, K, W, x, y + 1, z_depth, pd);
+  d2n_point(dep, c2w, K, W, x, y - 1, z_depth, pu);
+  d2n_point(dep, c2w, K, W, x + 1, y, z_depth, pr);
+  d2n_point(dep, c2w, K, W, x - 1, y, z_depth, pl);
+  const float a[3] = {pd[0] - pu[0], pd[1] - pu[1], pd[2] - pu[2]};
+  const float b[3] = {pr[0] - pl[0], pr[1] - pl[1], pr[2] - pl[2]};
+  const float n[3] = {a[1] * b[2] - a[2] * b[1], a[2] * b[0] - a[0] * b[2],
+                      a[0] * b[1] - a[1] * b[0]};
+  const float l = fmaxf(sqrtf(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]), 1e-12f);
+  out[0] = n[0] / l;
+  out[1] = n[1] / l;
+  out[2] = n[2] / l;
+}
+
 }  // namespace auxk
 }  // namespace gs
 
@@ -236,5 +289,18 @@ extern "C" int gsplat_hip_selective_adam(int64_t n_rows, int64_t row, float *par
                      (hipStream_t)stream, n_rows, row, param, grad, exp_avg, exp_avg_sq, visible,
                      lr, beta1, beta2, eps);
   GS_CHECK_LAUNCH("selective_adam");
+  return 0;
+}
+
+extern "C" int gsplat_hip_depth_to_normal(int C, int H, int W, const float *depths,
+                                          const float *camtoworlds, const float *Ks, int z_depth,
+                                          float *normals, void *stream) {
+  GS_REQUIRE(C >= 0 && H >= 0 && W >= 0, "depth_to_normal: negative sizes");
+  const int64_t n = (int64_t)C * H * W;
+  if (n == 0) return 0;
+  GS_REQUIRE(depths && camtoworlds && Ks && normals, "depth_to_normal: null pointer");
+  hipLaunchKernelGGL(auxk::depth_to_normal_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256),
+                     0, (hipStream_t)stream, C, H, W, depths, camtoworlds, Ks, z_depth, normals);
+  GS_CHECK_LAUNCH("depth_to_normal");
   return 0;
 }

@@ -12,7 +12,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GSPLAT_HIP_LIB", os.path.join(_HERE, "libgsplat_hip.so"))
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 _p = ctypes.c_void_p
 _i32 = ctypes.c_int
@@ -99,6 +99,7 @@ _SIGS = {
     "gsplat_hip_rasterize_to_indices_write": (_i32, [_i32, _i32, _i32, _i32, _i32, _i32, _i32,
                                                      _i32, _i64, _i64, _i64, _p, _p, _p, _p, _p,
                                                      _p, _p, _p, _p, _p]),
+    "gsplat_hip_depth_to_normal": (_i32, [_i32, _i32, _i32, _p, _p, _p, _i32, _p, _p]),
 }
 
 EXPORTED = tuple(_SIGS)

@@ -15,7 +15,12 @@ from typing import Callable, Dict, Optional, Tuple
 import torch
 from torch import Tensor
 
+from . import _lib
 from ._wrapper import (
+    _dev_check,
+    _f32c,
+    _ptr,
+    _stream,
     fully_fused_projection,
     isect_offset_encode,
     isect_tiles_begin,
@@ -299,14 +304,57 @@ def _depth_to_points(depths: Tensor, camtoworlds: Tensor, Ks: Tensor, z_depth: b
     return origins[..., None, None, :] + depths * directions
 
 
-def depth_to_normal(depths: Tensor, camtoworlds: Tensor, Ks: Tensor, z_depth: bool = True) -> Tensor:
-    """Surface normals from depth maps by central differences
-    (gsplat/utils.py:201-224)."""
+def _depth_to_normal_torch(depths: Tensor, camtoworlds: Tensor, Ks: Tensor,
+                           z_depth: bool = True) -> Tensor:
+    """The formula of gsplat/utils.py:201-224 in torch ops (differentiated by
+    _DepthToNormal.backward)."""
     points = _depth_to_points(depths, camtoworlds, Ks, z_depth=z_depth)
     dx = points[..., 2:, 1:-1, :] - points[..., :-2, 1:-1, :]
     dy = points[..., 1:-1, 2:, :] - points[..., 1:-1, :-2, :]
     normals = torch.nn.functional.normalize(torch.cross(dx, dy, dim=-1), dim=-1)
     return torch.nn.functional.pad(normals, (0, 0, 1, 1, 1, 1), value=0.0)
+
+
+class _DepthToNormal(torch.autograd.Function):
+    """Forward: one HIP launch (csrc/aux_ops.hip depth_to_normal_kernel)
+    instead of a dozen full-image torch passes; backward (only when a loss
+    uses the normals, e.g. the 2DGS normal-consistency term): autograd of the
+    same formula in torch."""
+
+    @staticmethod
+    def forward(ctx, depths, camtoworlds, Ks, z_depth):
+        _dev_check(depths, camtoworlds, Ks)
+        H, W = depths.shape[-3:-1]
+        lead = depths.shape[:-3]
+        d = _f32c(depths).reshape(-1, H, W)
+        C = d.shape[0]
+        c2w = _f32c(camtoworlds).reshape(-1, 4, 4)
+        k = _f32c(Ks).reshape(-1, 3, 3)
+        assert c2w.shape[0] == C and k.shape[0] == C, (depths.shape, camtoworlds.shape, Ks.shape)
+        out = torch.empty((C, H, W, 3), device=depths.device)
+        _lib.call("gsplat_hip_depth_to_normal", C, H, W, _ptr(d), _ptr(c2w), _ptr(k),
+                  int(bool(z_depth)), _ptr(out), _stream())
+        ctx.save_for_backward(depths, camtoworlds, Ks)
+        ctx.z_depth = z_depth
+        return out.reshape(*lead, H, W, 3)
+
+    @staticmethod
+    def backward(ctx, g):
+        depths, camtoworlds, Ks = ctx.saved_tensors
+        with torch.enable_grad():
+            ins = [t.detach().requires_grad_(t.requires_grad)
+                   for t in (depths, camtoworlds, Ks)]
+            out = _depth_to_normal_torch(*ins, z_depth=ctx.z_depth)
+            want = [t for t in ins if t.requires_grad]
+            grads = iter(torch.autograd.grad(out, want, g, allow_unused=True)) if want else iter(())
+        return tuple(next(grads) if t.requires_grad else None for t in ins) + (None,)
+
+
+def depth_to_normal(depths: Tensor, camtoworlds: Tensor, Ks: Tensor, z_depth: bool = True) -> Tensor:
+    """Surface normals from depth maps by central differences
+    (gsplat/utils.py:201-224): depths [..., H, W, 1], camtoworlds [..., 4, 4],
+    Ks [..., 3, 3] -> [..., H, W, 3]."""
+    return _DepthToNormal.apply(depths, camtoworlds, Ks, z_depth)
 
 
 def rasterization_2dgs(

@@ -482,6 +482,13 @@ int gsplat_hip_rasterize_to_indices_write(int kind, int C, int N, int W, int H, 
                                           const int32_t *chunk_starts, int64_t *gaussian_ids,
                                           int64_t *pixel_ids, void *stream);
 
+/* Normals from depth maps (gsplat/utils.py:201-224, depth_to_normal, called by
+ * rasterization_2dgs for render_normals_from_depth): depths[C,H,W] (the [..,1]
+ * channel), camtoworlds[C,4,4], Ks[C,3,3] -> normals[C,H,W,3], zero border.
+ * Forward only; the Python binding differentiates the torch formula. */
+int gsplat_hip_depth_to_normal(int C, int H, int W, const float *depths, const float *camtoworlds,
+                               const float *Ks, int z_depth, float *normals, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

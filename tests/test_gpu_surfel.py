@@ -256,3 +256,24 @@ def test_rasterization_2dgs_e2e(mode, sh):
         assert x.grad is not None and torch.isfinite(x.grad).all()
     assert meta["gradient_2dgs"].grad is not None
     assert float(meta["gradient_2dgs"].grad.abs().sum()) > 0
+
+
+@pytest.mark.parametrize("z_depth,C", [(True, 1), (False, 2)])
+def test_depth_to_normal_matches_torch_formula(z_depth, C):
+    """HIP depth_to_normal (forward) against the reference formula
+    (gsplat/utils.py:201-224) in torch, and its gradient."""
+    from gsplat_hip.rendering import _depth_to_normal_torch, depth_to_normal
+    g = torch.Generator(device=DEV).manual_seed(3)
+    H, W = 37, 53
+    d = (2.0 + torch.rand(C, H, W, 1, device=DEV, generator=g)).requires_grad_(True)
+    vm = torch.eye(4, device=DEV).repeat(C, 1, 1)
+    vm[:, :3, 3] = torch.randn(C, 3, device=DEV, generator=g) * 0.3
+    c2w = torch.linalg.inv(vm)
+    K = torch.tensor([[60.0, 0, W / 2], [0, 55.0, H / 2], [0, 0, 1]], device=DEV).repeat(C, 1, 1)
+    a = depth_to_normal(d, c2w, K, z_depth=z_depth)
+    b = _depth_to_normal_torch(d, c2w, K, z_depth=z_depth)
+    torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-5)
+    w = torch.randn_like(b)
+    ga, = torch.autograd.grad((a * w).sum(), d)
+    gb, = torch.autograd.grad((b * w).sum(), d)
+    torch.testing.assert_close(ga, gb, rtol=1e-5, atol=1e-6)
