@@ -149,7 +149,7 @@ def test_reshape_view_blocks():
     assert out.tolist() == [[0, 1, 2, 3, 4], [10, 11, 12, 13, 14]]
 
 
-def _sharded_worker(rank, world, port, q):
+def _sharded_worker(rank, world, port, q, defer=False):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -170,7 +170,9 @@ def _sharded_worker(rank, world, port, q):
             grads = [torch.randn(s, generator=gr) for s in shapes]
             for p, gg in zip(ps, grads):
                 p.grad = gg.clone()
-            opt.step()
+            opt.step(defer_gather=defer)
+            if defer:  # the trainer waits before the next use of the rows
+                opt.wait()
             opt.zero_grad()
             # reference: all-reduce SUM of the gradients, full Adam on every rank
             summed = [gg.clone() for gg in grads]
@@ -187,14 +189,15 @@ def _sharded_worker(rank, world, port, q):
         q.put((rank, repr(e), None))
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_sharded_adam_matches_allreduce_adam_gloo(world):
+@pytest.mark.parametrize("world,defer", [(2, False), (3, False), (2, True)])
+def test_sharded_adam_matches_allreduce_adam_gloo(world, defer):
     """ShardedAdam (reduce-scatter -> Adam on own rows -> all-gather) equals
     all-reduce + full Adam on every rank, and the replicas stay identical."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_sharded_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_sharded_worker, args=(r, world, port, q, defer))
+             for r in range(world)]
     for p in procs:
         p.start()
     out = {}
