@@ -41,6 +41,13 @@ CONFIGS = {
                           "scene_grid=3 (1,006,065 surfels), 1920x1080, SH deg 3"),
 }
 MODEL = {"m5": "2dgs"}
+# BASELINE.json configs[2] "densification on": simple_trainer.py's default run
+# (SfM init with knn scales, SH degree schedule, means ExponentialLR,
+# DefaultStrategy refine/reset); the timed window is centred on a refine step
+# after the SH degree has reached 3 (steps numbered from REFINE_AT - warmup -
+# steps // 2)
+DENSIFY = {"m3"}
+REFINE_AT = 3100
 
 
 def parse():
@@ -50,23 +57,32 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="m2", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-tile-stride", type=int, default=24)
+    ap.add_argument("--cpu-tile-stride", type=int, default=0,
+                    help="rasterize every k-th tile in the CPU baseline (0: auto)")
     ap.add_argument("--no-traffic", action="store_true",
                     help="skip the rocprofv3 PMC child runs that measure roofline.traffic")
     ap.add_argument("--probe", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
 
 
-def pmc_traffic(config: str):
-    """HBM bytes of one rasterize-forward launch from rocprofv3 counters.
+PMC_PASSES = (("FETCH_SIZE",), ("WRITE_SIZE",),
+              ("SQ_INSTS_VALU", "SQ_WAIT_INST_ANY", "SQ_WAVE_CYCLES", "SQ_INSTS_LDS",
+               "SQ_LDS_BANK_CONFLICT", "SQ_INSTS_VMEM_WR"))
 
-    Two child runs of `bench.py --probe` under rocprofv3 (separate --pmc
-    passes: FETCH_SIZE and WRITE_SIZE cannot share one), started before this
-    process touches the GPU.  Corrections per MI355X_MICROARCH.md "HBM":
-    FETCH_SIZE is in KiB and counts half the bytes on gfx950 (x2);
-    WRITE_SIZE is in KiB.  Returns None when rocprofv3 is unavailable."""
+
+def pmc_traffic(config: str):
+    """Counters of the rasterize forward and backward launches from rocprofv3.
+
+    One child run of `bench.py --probe` under rocprofv3 per --pmc pass
+    (FETCH_SIZE and WRITE_SIZE cannot share a pass; the SQ counters share
+    one), started before this process touches the GPU.  Corrections per
+    MI355X_MICROARCH.md "HBM": FETCH_SIZE is in KiB and counts half the bytes
+    of a wide read on gfx950 (x2); WRITE_SIZE is in KiB (exact for float
+    atomics and 16-B stores).  Returns {"fwd": {...}, "bwd": {...}} or None
+    when rocprofv3 is unavailable."""
     import csv
     import glob
+    import re
     import shutil
     import subprocess
     import tempfile
@@ -77,46 +93,62 @@ def pmc_traffic(config: str):
             or any(k.startswith("ROCPROF") for k in os.environ):
         return None  # already running under a profiler: no nested profiler runs
     env = dict(os.environ, TMPDIR="/tmp")
-    per = {}
-    for ctr in ("FETCH_SIZE", "WRITE_SIZE", "SQ_INSTS_VALU"):
+    ns = "surfel" if MODEL.get(config) == "2dgs" else "r16"
+    regex = f"{ns}::(fwd|bwd)2?_kernel"
+    per = {"fwd": {}, "bwd": {}}
+    for ctrs in PMC_PASSES:
         d = tempfile.mkdtemp(prefix="gsplat_pmc_", dir="/tmp")
-        regex = "surfel::fwd2?_kernel" if MODEL.get(config) == "2dgs" else "r16::fwd2?_kernel"
-        cmd = [rp, "--kernel-include-regex", regex, "--pmc", ctr, "-f", "csv",
+        cmd = [rp, "--kernel-include-regex", regex, "--pmc", *ctrs, "-f", "csv",
                "-d", d, "-o", "p", "--", sys.executable, os.path.abspath(__file__), "--probe",
                "--config", config, "--warmup", "2"]
         try:
             subprocess.run(cmd, env=env, cwd="/tmp", timeout=300, check=True,
                            stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
         except (subprocess.SubprocessError, OSError):
+            shutil.rmtree(d, ignore_errors=True)
+            if ctrs[0].startswith("SQ_"):
+                continue  # optional pass
             return None
         vals = {}
         for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
             for r in csv.DictReader(open(f)):
-                if r["Counter_Name"] == ctr:
-                    vals[r["Dispatch_Id"]] = vals.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
+                m = re.search(rf"{ns}::(fwd|bwd)", r["Kernel_Name"])
+                if m is None or r["Counter_Name"] not in ctrs:
+                    continue
+                key = (m.group(1), r["Counter_Name"], r["Dispatch_Id"])
+                vals[key] = vals.get(key, 0.0) + float(r["Counter_Value"])
         shutil.rmtree(d, ignore_errors=True)
-        if not vals:
-            if ctr == "SQ_INSTS_VALU":  # optional: VALU issue rate of the same launch
-                continue
+        for (k, c, _), v in vals.items():
+            per[k].setdefault(c, []).append(v)
+    out = {}
+    for k, cs in per.items():
+        mean = {c: float(np.mean(v)) for c, v in cs.items()}
+        if "FETCH_SIZE" not in mean or "WRITE_SIZE" not in mean:
             return None
-        per[ctr] = float(np.mean(list(vals.values())))
-    fetch = 2.0 * per["FETCH_SIZE"] * 1024.0
-    write = per["WRITE_SIZE"] * 1024.0
-    return {"bytes_per_launch": fetch + write, "fetch_bytes": fetch, "write_bytes": write,
-            "fetch_size_kib": per["FETCH_SIZE"], "write_size_kib": per["WRITE_SIZE"],
-            "valu_insts": per.get("SQ_INSTS_VALU"),
-            "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py --probe "
-                      "(FETCH_SIZE x2 per MI355X_MICROARCH.md; gathers uncalibrated)"}
+        fetch = 2.0 * mean["FETCH_SIZE"] * 1024.0
+        write = mean["WRITE_SIZE"] * 1024.0
+        out[k] = {"bytes_per_launch": fetch + write, "fetch_bytes": fetch, "write_bytes": write,
+                  "counters": mean}
+    out["source"] = ("rocprofv3 --pmc passes of bench.py --probe: " +
+                     "; ".join(",".join(p) for p in PMC_PASSES) +
+                     " (FETCH_SIZE x2 per MI355X_MICROARCH.md; gathers uncalibrated)")
+    return out
 
 
-def _valu_frac(traffic, launch_ms):
-    if not traffic or not traffic.get("valu_insts") or not launch_ms == launch_ms:
+def _valu_frac(pmc, launch_ms):
+    """VALU issue: wave64 VALU instructions x 2 cycles (SIMD-32) against 1024
+    SIMDs x 2.4 GHz over the launch (MI355X_MICROARCH.md constants)."""
+    ctr = (pmc or {}).get("counters", {})
+    insts = ctr.get("SQ_INSTS_VALU")
+    if not insts or not launch_ms == launch_ms:
         return None
-    insts = traffic["valu_insts"]
     peak = 1024 * 2.4e9 / 2.0  # wave64 VALU instructions per second, whole chip
     achieved = insts / (launch_ms * 1e-3)
-    return {"bound": "valu", "insts_per_launch": insts, "achieved": achieved, "peak": peak,
-            "unit": "wave-instr/s", "frac": achieved / peak}
+    res = {"bound": "valu", "insts_per_launch": insts, "achieved": achieved, "peak": peak,
+           "unit": "wave-instr/s", "frac": achieved / peak}
+    if ctr.get("SQ_WAVE_CYCLES"):
+        res["wait_inst_any_frac"] = ctr.get("SQ_WAIT_INST_ANY", 0.0) / ctr["SQ_WAVE_CYCLES"]
+    return res
 
 
 def max_over_ranks(elapsed: float, world: int, device) -> float:
@@ -128,11 +160,48 @@ def max_over_ranks(elapsed: float, world: int, device) -> float:
     return float(t.item())
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_cmd(n: int, argv, port: int):
+    """The child command that runs `n` ranks of this script, one per GPU:
+    torch.distributed.run on one node, rendezvous on 127.0.0.1 (the reference's
+    `cli` spawns one process per visible GPU the same way,
+    gsplat/distributed.py:304-360)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+            f"--nproc-per-node={n}", "--master-addr", "127.0.0.1", "--master-port", str(port),
+            os.path.abspath(__file__)] + list(argv)
+
+
+def launch(n: int, argv) -> int:
+    """`bench.py --gpus N` without a torchrun environment: start the N ranks as a
+    CHILD process (this parent never touches the GPU and never execs), let rank
+    0's JSON line through on the shared stdout, return the children's exit code."""
+    import subprocess
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.run(launch_cmd(n, argv, _free_port()), env=env).returncode
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    cpu_pool = None
+    if rank == 0 and not args.no_cpu_baseline and not args.probe:
+        # the CPU baseline's worker processes start before this process
+        # touches the GPU (spawned interpreters running numpy only)
+        from oracle.cpu_step import CpuPool
+        cpu_pool = CpuPool(host_threads())
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -151,15 +220,22 @@ def main():
         os.path.join(ROOT, "tests", "golden", "garden_scene.npz"), scene_grid=grid)
     vm_pool, K_pool = camera_pool(vms, Ks, sw, sh_, W, H, n=max(8, world))
     model = MODEL.get(args.config, "3dgs")
+    kw = {}
+    start = 0
+    if args.config in DENSIFY:
+        from gsplat_hip.densify import DefaultStrategyConfig
+        kw = dict(strategy=DefaultStrategyConfig(), sh_degree_interval=1000, max_steps=30_000,
+                  init="sfm")
+        start = max(0, REFINE_AT - args.warmup - args.steps // 2)
     tr = Trainer(means, rgbs, vm_pool, K_pool, W, H, sh_degree=3, device=dev, world_size=world,
-                 rank=rank, model=model)
+                 rank=rank, model=model, **kw)
     N = means.shape[0]
 
-    for it in range(args.warmup):
+    for it in range(start, start + args.warmup):
         tr.step(it)
     torch.cuda.synchronize()
     if args.probe:  # PMC child run: a few steps, no output
-        for it in range(args.warmup, args.warmup + 2):
+        for it in range(start + args.warmup, start + args.warmup + 2):
             tr.step(it)
         torch.cuda.synchronize()
         return
@@ -169,7 +245,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for it in range(args.warmup, args.warmup + args.steps):
+    for it in range(start + args.warmup, start + args.warmup + args.steps):
         tr.step(it)
     torch.cuda.synchronize()
     if world > 1:
@@ -196,41 +272,55 @@ def main():
     D = 4 if two else 3
     per_isect = (64 + 4 * D) if two else (28 + 4 * D)
     per_px = (4 * D + 32) if two else (4 * D + 8)
+    # backward (SURVEY §8 d): the forward's gathered record plus an 8-B
+    # read-modify-write per gradient field (3DGS: D colour + 2 means2d + 3
+    # conic + 1 opacity; 2DGS: D colour + 3 normal + 9 ray transform +
+    # 2 means2d + 1 opacity); per pixel the forward outputs it re-reads and
+    # the incoming gradients (3DGS: colour 4D + alpha 4 + render alpha 4 +
+    # last id 4; 2DGS: the same plus normal 12, distortion 4, median 8).
+    per_isect_bwd = per_isect + 8 * ((D + 15) if two else (D + 6))
+    per_px_bwd = (4 * D + 40) if two else (4 * D + 12)
     node_name = "_RasterizeToPixels2DGSBackward" if two else "_RasterizeToPixelsBackward"
     last_slot = 12 if two else 9
-    byts, isects = [], []
-    if True:  # graph needed to reach the forward's saved last_ids
-        for it in range(args.warmup, args.warmup + min(args.steps, len(vm_pool))):
-            ci = tr.camera_index(it)
-            colors, alphas, meta = tr.render(ci)
-            # last_ids are internal to the autograd node; recompute n_eff from
-            # the forward outputs with the same kernel
-            offs = meta["isect_offsets"].flatten().long()
-            n = meta["flatten_ids"].numel()
-            ends = torch.cat([offs[1:], torch.tensor([n], device=dev)])
-            node = colors.grad_fn
-            while node is not None and type(node).__name__ != node_name:
-                node = node.next_functions[0][0]
-            last = node.saved_tensors[last_slot] if node is not None else None
-            if last is not None:
-                ts = meta["tile_size"]
-                tw, th = meta["tile_width"], meta["tile_height"]
-                lp = torch.nn.functional.pad(last[0], (0, tw * ts - W, 0, th * ts - H))
-                tmax = lp.view(th, ts, tw, ts).amax(dim=(1, 3)).flatten().long()
-                n_eff = int(torch.clamp(torch.minimum(ends, tmax + 1) - offs, min=0).sum())
-            else:
-                n_eff = n
-            P = H * W
-            byts.append(n_eff * per_isect + P * per_px + 4 * tw * th)
-            isects.append(n)
+    byts, byts_bwd, isects, n_effs = [], [], [], []
+    for it in range(start + args.warmup, start + args.warmup + min(args.steps, len(vm_pool))):
+        ci = tr.camera_index(it)
+        colors, alphas, meta = tr.render(ci)
+        # last_ids are internal to the autograd node (the forward's saved
+        # tensors); n_eff = sum over tiles of min(end, max last_id + 1) - start
+        offs = meta["isect_offsets"].flatten().long()
+        n = meta["flatten_ids"].numel()
+        ends = torch.cat([offs[1:], torch.tensor([n], device=dev)])
+        node = colors.grad_fn
+        while node is not None and type(node).__name__ != node_name:
+            node = node.next_functions[0][0]
+        last = node.saved_tensors[last_slot] if node is not None else None
+        ts = meta["tile_size"]
+        tw, th = meta["tile_width"], meta["tile_height"]
+        if last is not None:
+            lp = torch.nn.functional.pad(last[0], (0, tw * ts - W, 0, th * ts - H))
+            tmax = lp.view(th, ts, tw, ts).amax(dim=(1, 3)).flatten().long()
+            n_eff = int(torch.clamp(torch.minimum(ends, tmax + 1) - offs, min=0).sum())
+        else:
+            n_eff = n
+        P = H * W
+        byts.append(n_eff * per_isect + P * per_px + 4 * tw * th)
+        byts_bwd.append(n_eff * per_isect_bwd + P * per_px_bwd + 4 * tw * th)
+        isects.append(n)
+        n_effs.append(n_eff)
+        del colors, alphas, meta, node, last
     bytes_per_launch = float(np.mean(byts))
+    bytes_bwd = float(np.mean(byts_bwd))
     achieved = bytes_per_launch / (fwd_ms * 1e-3) / 1e9
+    achieved_bwd = bytes_bwd / (bwd_ms * 1e-3) / 1e9
 
+    pf = None if traffic is None else traffic["fwd"]
+    pb = None if traffic is None else traffic["bwd"]
     result = {
         "metric": "train-step images/sec + rasterize fwd HBM GB/s, garden 1080p, 1/2/4/8 MI355X",
         "value": world * args.steps / elapsed,
         "unit": "images/s",
-        "n_gpus": world,
+        "n_gpus": dist.get_world_size() if world > 1 else 1,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": 1e3 * elapsed / args.steps,
@@ -238,28 +328,44 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic: garden SfM points (assets/test_garden.npz crop) tiled 3x3, random "
-                "scales/quats/opacities, random target images",
-        "config": {"workload": desc, "gaussians": N, "width": W, "height": H,
+        "data": "synthetic: garden SfM points (assets/test_garden.npz crop) tiled "
+                f"{grid}x{grid}, random scales/quats/opacities, random target images",
+        "config": {"workload": desc, "gaussians": N,
+                   "gaussians_after": int(tr.params["means"].shape[0]),
+                   "first_timed_step": start + args.warmup, "width": W, "height": H,
                    "cameras_per_rank_per_step": 1, "parallelism": f"dp{world}",
-                   "n_isects_mean": float(np.mean(isects)), "packed": False,
-                   "loss": "0.8*L1+0.2*(1-SSIM valid)", "optimizer": "Adam (6 groups)"},
+                   "n_isects_mean": float(np.mean(isects)), "n_eff_mean": float(np.mean(n_effs)),
+                   "packed": False, "loss": "0.8*L1+0.2*(1-SSIM valid)",
+                   "optimizer": "Adam (6 groups)" + (", sharded over ranks" if world > 1 else ""),
+                   "densification": tr.densify_desc()},
         "roofline": {"kernel": kname, "bound": "hbm", "achieved": achieved,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                     "traffic": None if traffic is None else traffic["bytes_per_launch"],
-                     "traffic_detail": traffic,
+                     "traffic": None if pf is None else pf["bytes_per_launch"],
+                     "traffic_detail": pf,
                      "algorithmic_bytes_per_launch": bytes_per_launch,
-                     "launch_ms": fwd_ms, "rasterize_bwd_ms": bwd_ms},
+                     "bytes_per_isect": per_isect, "bytes_per_pixel": per_px,
+                     "launch_ms": fwd_ms,
+                     # the kernel's binding ceiling is VALU issue, not HBM
+                     "valu": _valu_frac(pf, fwd_ms),
+                     "bwd": {"kernel": kname.replace("fwd", "bwd"), "bound": "hbm",
+                             "achieved": achieved_bwd, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                             "frac": achieved_bwd / HBM_PEAK_GBS,
+                             "traffic": None if pb is None else pb["bytes_per_launch"],
+                             "traffic_detail": pb,
+                             "algorithmic_bytes_per_launch": bytes_bwd,
+                             "bytes_per_isect": per_isect_bwd, "bytes_per_pixel": per_px_bwd,
+                             "launch_ms": bwd_ms, "valu": _valu_frac(pb, bwd_ms)},
+                     "pmc_source": None if traffic is None else traffic["source"],
+                     "pmc_note": None if world == 1 else "PMC passes run at N=1 only "
+                                 "(per-GPU workload is the same at every N)"},
         "model": model,
     }
-
-    # the kernel's binding ceiling is VALU issue, not HBM: wave64
-    # VALU instructions x 2 cycles each (MI355X_MICROARCH.md constants:
-    # v_fma_f32 2 cyc per SIMD) against 1024 SIMDs x 2.4 GHz over the launch
-    # time; SQ_INSTS_VALU from a rocprofv3 --pmc pass of the same workload
-    result["roofline"]["valu"] = _valu_frac(traffic, fwd_ms)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(tr, args.cpu_tile_stride)
+    if rank == 0 and not args.no_cpu_baseline:
+        # after the timed region; the other ranks wait at the barrier below
+        try:
+            result["cpu_baseline"] = cpu_baseline(tr, args.cpu_tile_stride, cpu_pool)
+        finally:
+            cpu_pool.close()
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
@@ -267,19 +373,44 @@ def main():
         dist.destroy_process_group()
 
 
-def cpu_baseline(tr, stride):
+def host_threads() -> int:
+    """Host cores this job may use: the box's share (OMP_NUM_THREADS, set to
+    the GPU's CPU share on the GPU box) or, failing that, the affinity mask."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    env = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(aff, int(env)) if env and env.isdigit() else aff)
+
+
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(tr, stride, pool):
+    """The numpy oracle's train step (oracle/cpu_step.py) on the host's cores."""
     from oracle.cpu_step import cpu_train_step
     p = {k: v.detach().cpu().numpy() for k, v in tr.params.items()}
     sh = np.concatenate([p["sh0"], p["shN"]], 1)
     ci = 0
+    threads = pool.workers
+    if stride <= 0:  # auto: whole image with >= 8 threads, else a 1/24 tile sample
+        stride = 1 if threads >= 8 else 24
     total, parts, sample = cpu_train_step(
         p["means"], p["quats"], p["scales"], p["opacities"], sh, tr.viewmats[ci].cpu().numpy(),
         tr.Ks[ci].cpu().numpy(), tr.width, tr.height, tr.targets[ci].cpu().numpy(),
-        tile_stride=stride)
-    return {"value": 1.0 / total, "unit": "images/s", "cores": 1, "kind": "port",
-            "sample": sample, "seconds_per_step_estimate": total,
+        tile_stride=stride, pool=pool)
+    return {"value": 1.0 / total, "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": sample, "seconds_per_step": total,
             "breakdown_s": {k: round(v, 3) for k, v in parts.items()},
-            "host_cpus": os.cpu_count()}
+            "host_cpus": os.cpu_count(), "cpu_model": cpu_model()}
 
 
 if __name__ == "__main__":

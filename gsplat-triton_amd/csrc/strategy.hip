@@ -9,6 +9,14 @@
 //   activate_bwd   their VJPs with torch's formulas (exp: g * out;
 //                  sigmoid_backward: g * (1 - out) * out), as the trainer's
 //                  torch.exp / torch.sigmoid (examples/simple_trainer.py:565-566).
+//   densify_*      DefaultStrategy's refine step (gsplat/strategy/default.py:
+//                  264-340 _grow_gs / _prune_gs over ops.py:86-211 duplicate /
+//                  split / remove) as ONE compaction: the reference rebuilds
+//                  every parameter and both Adam moments three times (torch.cat
+//                  for the duplicates, again for the split, index for the
+//                  prune); here a plan pass classifies each Gaussian, a scan
+//                  places the survivors, and one apply pass writes the final
+//                  layout of all arrays once.
 // All HBM-bound streaming kernels, one lane per Gaussian.
 #include "common.h"
 #include "../../include/gsplat_hip.h"
@@ -62,6 +70,221 @@ activate_bwd_kernel(int64_t n_s, int64_t n_o, const float *__restrict__ scales,
   }
 }
 
+
+// ------------------------------------------------------------ densification
+// Final layout of the reference's duplicate -> split -> remove sequence:
+//   [originals neither split nor pruned] ++ [duplicates not pruned]
+//   ++ [first split child of each split Gaussian not pruned]
+//   ++ [second split children, same order]
+// (duplicate appends p[sel]; split keeps p[rest] -- the duplicates included,
+// they are never split -- and appends the children sampled as [2, n, 3];
+// remove is a stable filter).  A duplicate has its parent's parameters and
+// so its prune decision; both children of a split share theirs (same scales
+// and opacity).
+enum : uint8_t { kKeep = 1, kDup = 2, kChild = 4, kSplit = 8, kDupAny = 16 };
+constexpr int kRows = 5;  // block-count rows: one per flag bit
+constexpr int kDB = 256;  // Gaussians per block
+
+struct DensifyCfg {
+  float grow_grad2d, grow_scale3d, prune_opa, prune_scale3d;
+  float grow_scale2d, prune_scale2d;  // used only with radii2d (scale2d refine)
+  int prune_big, revised_opacity;
+};
+
+GS_INLINE float sigmoid_t(float x) { return 1.f / (1.f + expf(-x)); }
+// the split children's opacity logit and log-scale, as the reference's torch
+// expressions (ops.py:152-167): log(exp(s) / 1.6) (a CUDA/HIP division by a
+// CPU scalar is a multiplication by its float reciprocal), and
+// logit(1 - sqrt(1 - sigmoid(o))) when revised
+GS_INLINE float child_log_scale(float s) { return logf(expf(s) * (1.f / 1.6f)); }
+GS_INLINE float child_logit(float o, bool revised) {
+  if (!revised) return o;
+  const float p = 1.f - sqrtf(1.f - sigmoid_t(o));
+  return logf(p / (1.f - p));
+}
+
+__global__ void __launch_bounds__(kDB)
+densify_plan_kernel(int64_t N, const float *__restrict__ grad2d, const float *__restrict__ count,
+                    const float *__restrict__ log_scales, const float *__restrict__ logits,
+                    const float *__restrict__ radii2d, DensifyCfg cfg, uint8_t *__restrict__ flags,
+                    int64_t *__restrict__ block_counts /* [kRows][nb] */, int64_t nb) {
+  __shared__ int wcnt[kRows][kDB / 64];
+  const int64_t i = (int64_t)blockIdx.x * kDB + threadIdx.x;
+  uint8_t f = 0;
+  if (i < N) {
+    const float g = grad2d[i] / fmaxf(count[i], 1.f);  // grad2d / count.clamp_min(1)
+    const bool high = g > cfg.grow_grad2d;
+    const float s0 = log_scales[3 * i], s1 = log_scales[3 * i + 1], s2 = log_scales[3 * i + 2];
+    const float smax = fmaxf(fmaxf(expf(s0), expf(s1)), expf(s2));
+    const bool small = smax <= cfg.grow_scale3d;
+    const bool dup = high && small;
+    bool split = high && !small;
+    const float o = logits[i];
+    bool prune = sigmoid_t(o) < cfg.prune_opa || (cfg.prune_big && smax > cfg.prune_scale3d);
+    if (radii2d) {  // refine_scale2d_stop_iter > 0 (default.py:283-284, 325-326)
+      split = split || radii2d[i] > cfg.grow_scale2d;
+      prune = prune || (cfg.prune_big && radii2d[i] > cfg.prune_scale2d);
+    }
+    if (!split && !prune) f |= kKeep;
+    if (dup && !prune) f |= kDup;
+    if (dup) f |= kDupAny;
+    if (split) {
+      f |= kSplit;
+      const float co = child_logit(o, cfg.revised_opacity);
+      const float cmax = fmaxf(fmaxf(expf(child_log_scale(s0)), expf(child_log_scale(s1))),
+                               expf(child_log_scale(s2)));
+      bool cprune = sigmoid_t(co) < cfg.prune_opa || (cfg.prune_big && cmax > cfg.prune_scale3d);
+      // the children inherit the running state, radii included (ops.py:172-176)
+      if (radii2d) cprune = cprune || (cfg.prune_big && radii2d[i] > cfg.prune_scale2d);
+      if (!cprune) f |= kChild;
+    }
+    flags[i] = f;
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < kRows; ++k) {
+    const uint64_t m = __ballot((f >> k) & 1);
+    if (lane == 0) wcnt[k][w] = __popcll(m);
+  }
+  __syncthreads();
+  if (threadIdx.x < kRows) {
+    int64_t t = 0;
+    for (int q = 0; q < kDB / 64; ++q) t += wcnt[threadIdx.x][q];
+    block_counts[threadIdx.x * nb + blockIdx.x] = t;
+  }
+}
+
+// Exclusive scan of each of the kRows block-count rows (workgroup k scans row k);
+// its total goes to totals[k].
+__global__ void __launch_bounds__(1024)
+densify_scan_kernel(int64_t nb, int64_t *__restrict__ block_counts, int64_t *__restrict__ totals) {
+  int64_t *row = block_counts + blockIdx.x * nb;
+  __shared__ int64_t wave_tot[16];
+  __shared__ int64_t chunk_tot;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  int64_t carry = 0;
+  for (int64_t base = 0; base < nb; base += 1024) {
+    const int64_t i = base + threadIdx.x;
+    const int64_t v = (i < nb) ? row[i] : 0;
+    int64_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int64_t y = __shfl_up(x, o, 64);
+      if (lane >= o) x += y;
+    }
+    if (lane == 63) wave_tot[wid] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int64_t run = 0;
+      for (int q = 0; q < 16; ++q) {
+        const int64_t t = wave_tot[q];
+        wave_tot[q] = run;
+        run += t;
+      }
+      chunk_tot = run;
+    }
+    __syncthreads();
+    if (i < nb) row[i] = carry + wave_tot[wid] + x - v;
+    carry += chunk_tot;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) totals[blockIdx.x] = carry;
+}
+
+constexpr int kMaxArrays = 24;
+struct DensifyArrays {
+  const float *src[kMaxArrays];
+  float *dst[kMaxArrays];
+  int row[kMaxArrays];   // floats per Gaussian
+  int kind[kMaxArrays];  // GSPLAT_HIP_DENSIFY_* (include/gsplat_hip.h)
+  int n;
+  const float *means, *quats, *log_scales, *logits;  // the sources the children derive from
+};
+
+__global__ void __launch_bounds__(kDB)
+densify_apply_kernel(int64_t N, const uint8_t *__restrict__ flags,
+                     const int64_t *__restrict__ block_offsets /* [4][nb] scanned */, int64_t nb,
+                     const int64_t *__restrict__ totals, const float *__restrict__ randn,
+                     int revised_opacity, DensifyArrays arr) {
+  __shared__ int wpre[4][kDB / 64];
+  const int64_t i = (int64_t)blockIdx.x * kDB + threadIdx.x;
+  const uint8_t f = i < N ? flags[i] : 0;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int rank[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint64_t m = __ballot((f >> k) & 1);
+    rank[k] = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                        __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    if (lane == 0) wpre[k][w] = __popcll(m);
+  }
+  __syncthreads();
+  if (i >= N || f == 0) return;
+  int64_t pos[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    int64_t p = block_offsets[k * nb + blockIdx.x] + rank[k];
+    for (int q = 0; q < w; ++q) p += wpre[k][q];
+    pos[k] = p;
+  }
+  const int64_t nA = totals[0], nB = totals[1], nC = totals[2], nS = totals[3];
+  const int64_t dA = pos[0], dB = nA + pos[1], dC0 = nA + nB + pos[2],
+                dC1 = nA + nB + nC + pos[2];
+  const bool isA = f & kKeep, isB = f & kDup, isC = f & kChild;
+  // split children: mean + R(normalize(q)) diag(exp(s)) z_b  (ops.py:143-152),
+  // z = randn[2, n_split, 3] indexed by this Gaussian's rank among ALL split
+  // Gaussians (pruned children included)
+  float c_mean[2][3], c_ls[3], c_logit = 0.f;
+  if (isC) {
+    const float *q = arr.quats + 4 * i;
+    const float qn = fmaxf(sqrtf(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]), 1e-12f);
+    const float qw = q[0] / qn, qx = q[1] / qn, qy = q[2] / qn, qz = q[3] / qn;
+    const float R[3][3] = {
+        {1.f - 2.f * (qy * qy + qz * qz), 2.f * (qx * qy - qw * qz), 2.f * (qx * qz + qw * qy)},
+        {2.f * (qx * qy + qw * qz), 1.f - 2.f * (qx * qx + qz * qz), 2.f * (qy * qz - qw * qx)},
+        {2.f * (qx * qz - qw * qy), 2.f * (qy * qz + qw * qx), 1.f - 2.f * (qx * qx + qy * qy)}};
+    float sc[3];
+    for (int k = 0; k < 3; ++k) {
+      sc[k] = expf(arr.log_scales[3 * i + k]);
+      c_ls[k] = child_log_scale(arr.log_scales[3 * i + k]);
+    }
+    const int64_t j = pos[3];
+    for (int b = 0; b < 2; ++b) {
+      const float *z = randn + ((int64_t)b * nS + j) * 3;
+      for (int r = 0; r < 3; ++r)
+        c_mean[b][r] = arr.means[3 * i + r] +
+                       (R[r][0] * sc[0] * z[0] + R[r][1] * sc[1] * z[1] + R[r][2] * sc[2] * z[2]);
+    }
+    c_logit = child_logit(arr.logits[i], revised_opacity);
+  }
+  for (int a = 0; a < arr.n; ++a) {
+    const int row = arr.row[a], kind = arr.kind[a];
+    const float *src = arr.src[a] + (int64_t)row * i;
+    float *dst = arr.dst[a];
+    const bool moment = kind == GSPLAT_HIP_DENSIFY_MOMENT;
+    for (int e = 0; e < row; ++e) {
+      const float v = src[e];
+      if (isA) dst[dA * row + e] = v;
+      if (isB) dst[dB * row + e] = moment ? 0.f : v;
+      if (isC) {
+        float v0 = v, v1 = v;
+        if (moment) {
+          v0 = v1 = 0.f;
+        } else if (kind == GSPLAT_HIP_DENSIFY_MEANS) {
+          v0 = c_mean[0][e];
+          v1 = c_mean[1][e];
+        } else if (kind == GSPLAT_HIP_DENSIFY_SCALES) {
+          v0 = v1 = c_ls[e];
+        } else if (kind == GSPLAT_HIP_DENSIFY_OPACITIES) {
+          v0 = v1 = c_logit;
+        }
+        dst[dC0 * row + e] = v0;
+        dst[dC1 * row + e] = v1;
+      }
+    }
+  }
+}
+
 }  // namespace strat
 }  // namespace gs
 
@@ -101,5 +324,76 @@ extern "C" int gsplat_hip_activate_bwd(int64_t n_scales, int64_t n_opacities, co
                      (hipStream_t)stream, n_scales, n_opacities, scales, opacities, v_scales,
                      v_opacities, v_log_scales, v_logits);
   GS_CHECK_LAUNCH("activate_bwd");
+  return 0;
+}
+
+extern "C" int64_t gsplat_hip_densify_workspace_bytes(int64_t N) {
+  const int64_t nb = (N + strat::kDB - 1) / strat::kDB;
+  return strat::kRows * nb * (int64_t)sizeof(int64_t) + ((N + 15) / 16) * 16;
+}
+
+extern "C" int gsplat_hip_densify_plan(int64_t N, const float *grad2d, const float *count,
+                                       const float *log_scales, const float *logits,
+                                       const float *radii2d, float grow_grad2d,
+                                       float grow_scale3d, float prune_opa, int prune_big,
+                                       float prune_scale3d, float grow_scale2d,
+                                       float prune_scale2d, int revised_opacity, void *workspace,
+                                       int64_t *totals, void *stream) {
+  GS_REQUIRE(N >= 0, "densify_plan: bad N=%lld", (long long)N);
+  const int64_t nb = (N + strat::kDB - 1) / strat::kDB;
+  int64_t *bc = (int64_t *)workspace;
+  uint8_t *flags = (uint8_t *)(bc + strat::kRows * nb);
+  hipStream_t st = (hipStream_t)stream;
+  if (N == 0) {
+    GS_HIP(hipMemsetAsync(totals, 0, strat::kRows * sizeof(int64_t), st));
+    return 0;
+  }
+  strat::DensifyCfg cfg{grow_grad2d, grow_scale3d, prune_opa, prune_scale3d,
+                        grow_scale2d, prune_scale2d, prune_big, revised_opacity};
+  hipLaunchKernelGGL(strat::densify_plan_kernel, dim3((unsigned)nb), dim3(strat::kDB), 0, st, N,
+                     grad2d, count, log_scales, logits, radii2d, cfg, flags, bc, nb);
+  GS_CHECK_LAUNCH("densify_plan");
+  hipLaunchKernelGGL(strat::densify_scan_kernel, dim3(strat::kRows), dim3(1024), 0, st, nb, bc,
+                     totals);
+  GS_CHECK_LAUNCH("densify_scan");
+  return 0;
+}
+
+extern "C" int gsplat_hip_densify_apply(int64_t N, const void *workspace, const int64_t *totals,
+                                        const float *randn, int revised_opacity, int n_arrays,
+                                        const float *const *src, float *const *dst,
+                                        const int32_t *row_floats, const int32_t *kinds,
+                                        const float *means, const float *quats,
+                                        const float *log_scales, const float *logits,
+                                        void *stream) {
+  GS_REQUIRE(N >= 0 && n_arrays >= 0 && n_arrays <= strat::kMaxArrays,
+             "densify_apply: bad sizes N=%lld n_arrays=%d (max %d)", (long long)N, n_arrays,
+             strat::kMaxArrays);
+  if (N == 0) return 0;
+  const int64_t nb = (N + strat::kDB - 1) / strat::kDB;
+  strat::DensifyArrays a{};
+  a.n = n_arrays;
+  for (int k = 0; k < n_arrays; ++k) {
+    GS_REQUIRE(kinds[k] >= GSPLAT_HIP_DENSIFY_COPY && kinds[k] <= GSPLAT_HIP_DENSIFY_MOMENT,
+               "densify_apply: array %d has unknown kind %d", k, kinds[k]);
+    GS_REQUIRE(row_floats[k] > 0 && (kinds[k] != GSPLAT_HIP_DENSIFY_MEANS || row_floats[k] == 3) &&
+                   (kinds[k] != GSPLAT_HIP_DENSIFY_SCALES || row_floats[k] == 3) &&
+                   (kinds[k] != GSPLAT_HIP_DENSIFY_OPACITIES || row_floats[k] == 1),
+               "densify_apply: array %d: %d floats per Gaussian for kind %d", k, row_floats[k],
+               kinds[k]);
+    a.src[k] = src[k];
+    a.dst[k] = dst[k];
+    a.row[k] = row_floats[k];
+    a.kind[k] = kinds[k];
+  }
+  a.means = means;
+  a.quats = quats;
+  a.log_scales = log_scales;
+  a.logits = logits;
+  const int64_t *bc = (const int64_t *)workspace;
+  const uint8_t *flags = (const uint8_t *)(bc + strat::kRows * nb);
+  hipLaunchKernelGGL(strat::densify_apply_kernel, dim3((unsigned)nb), dim3(strat::kDB), 0,
+                     (hipStream_t)stream, N, flags, bc, nb, totals, randn, revised_opacity, a);
+  GS_CHECK_LAUNCH("densify_apply");
   return 0;
 }

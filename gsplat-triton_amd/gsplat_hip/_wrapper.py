@@ -16,6 +16,7 @@ stream; there is no CPU or Triton fallback.
 """
 
 import math
+import time
 import os
 from typing import Optional, Tuple
 
@@ -347,9 +348,6 @@ def isect_tiles_begin(means2d, radii, depths, tile_size, tile_width, tile_height
                        tile_height, n_bit_tile, n_bit_cam, packed)
 
 
-_PINNED = {}
-
-
 class _IsectCount:
     """isect_tiles in two halves around its single host sync: the count
     kernels and an asynchronous copy of (n_isects, n_visible) into pinned host
@@ -369,9 +367,10 @@ class _IsectCount:
         _lib.call("gsplat_hip_isect_count", G, _ptr(means2d), _ptr(radii), tile_size,
                   tile_width, tile_height, _ptr(self.tpg), _ptr(self.ws), _ptr(totals),
                   _stream())
-        host = _PINNED.get(dev)
-        if host is None:
-            host = _PINNED[dev] = torch.empty(2, dtype=torch.int64, pin_memory=True)
+        # a pinned buffer of its own per call (torch's caching host allocator
+        # recycles it only after the copy's event): concurrent begins on other
+        # streams or threads cannot overwrite each other's totals
+        host = torch.empty(2, dtype=torch.int64, pin_memory=True)
         host.copy_(totals, non_blocking=True)
         self.host, self.totals = host, totals
         self.event = torch.cuda.Event()
@@ -386,7 +385,7 @@ class _IsectCount:
         # the single host sync (isect_tiles.py:102); polling reacts within a
         # few us where hipEventSynchronize's blocking wait took ~100 us
         while not self.event.query():
-            pass
+            time.sleep(0)  # yields the core (and the GIL) between polls
         n_isects, n_visible = self.host.tolist()
         isect_ids = torch.empty(n_isects, dtype=torch.int64, device=dev)
         flatten_ids = torch.empty(n_isects, dtype=torch.int32, device=dev)

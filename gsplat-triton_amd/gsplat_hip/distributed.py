@@ -244,3 +244,42 @@ class ShardedAdam:
     def zero_grad(self, set_to_none=True):
         for p in self.params:
             p.grad = None
+
+    @torch.no_grad()
+    def full_state(self):
+        """[(exp_avg, exp_avg_sq)] per parameter as full tensors shaped like it:
+        the shards all-gathered (the replicated tail rows appended).  For the
+        optimizer-state surgery of a densification step (every rank gets the
+        same tensors)."""
+        self.wait()
+        out = []
+        for i, p in enumerate(self.params):
+            _, _, main, tot = self.layout[i]
+            pair = []
+            for shard, tail in ((self.m[i], self.m_tail[i]), (self.v[i], self.v_tail[i])):
+                full = torch.empty(tot, device=p.device, dtype=p.dtype)
+                if main:
+                    dist.all_gather_into_tensor(full[:main], shard)
+                full[main:] = tail
+                pair.append(full.view_as(p))
+            out.append(tuple(pair))
+        return out
+
+    @torch.no_grad()
+    def load_full_state(self, moments, step_count):
+        """Inverse of full_state for this optimizer's (new) parameters: keep
+        this rank's shard and the tail rows of each full moment tensor."""
+        self.step_count = int(step_count)
+        for i, (m, v) in enumerate(moments):
+            _, _, main, _ = self.layout[i]
+            for full, shard, tail in ((m, self.m[i], self.m_tail[i]), (v, self.v[i], self.v_tail[i])):
+                f = full.reshape(-1)
+                if main:
+                    shard.copy_(self._shard(i, f[:main]))
+                tail.copy_(f[main:])
+
+    @torch.no_grad()
+    def zero_moments(self, i):
+        """Zero both moments of parameter i (reset_opa's optimizer state)."""
+        for t in (self.m[i], self.v[i], self.m_tail[i], self.v_tail[i]):
+            t.zero_()

@@ -188,6 +188,8 @@ def rasterization(
     # coefficients overlap projection and isect (train_step.Trainer)
     late = _colors_ready is not None and not packed and not distributed
     if not late:
+        if _colors_ready is not None:  # packed / distributed: wait before, not after
+            _colors_ready()
         colors = eval_colors(colors)
 
     if distributed:  # gsplat/rendering.py:413-494

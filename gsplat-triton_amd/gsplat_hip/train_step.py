@@ -13,11 +13,24 @@ same loss on the RGB channels (:590-594; normal/distortion losses are off by
 default, :149-160), and the strategy statistics from meta["gradient_2dgs"]
 (key_for_gradient, :307-311).
 
+With `strategy=DefaultStrategyConfig()` the step also runs the reference's
+DefaultStrategy schedule after the optimizer step (simple_trainer.py:808-826
+-> gsplat/strategy/default.py:164-211): refine (grow + prune, one HIP
+compaction of every parameter and both Adam moments, gsplat_hip.densify)
+every `refine_every` steps in (refine_start_iter, refine_stop_iter), opacity
+reset every `reset_every` steps.  `sh_degree_interval` enables the SH degree
+schedule (simple_trainer.py:600), `max_steps` the means ExponentialLR
+(:523-528), `init="sfm"` the SfM initialisation with knn scales, uniform
+quaternions and init_opacity (:212-233).
+
 Multi-GPU is per-camera data parallelism: every rank holds the same
 Gaussians and renders its own camera; the Gaussian gradients are summed over
 RCCL/xGMI by reduce-scatter, each rank runs Adam on its share of the rows,
 and the updated rows are all-gathered (distributed.ShardedAdam; the plain
-per-group all-reduce + full Adam is `sharded_optimizer=False`).
+per-group all-reduce + full Adam is `sharded_optimizer=False`).  Before a
+refine the densification statistics are summed over the ranks and the split
+noise comes from a generator seeded identically on every rank, so the
+replicas stay identical.
 """
 
 import math
@@ -28,6 +41,8 @@ import numpy as np
 import torch
 import torch.nn.functional as F
 
+from . import densify
+from .densify import DefaultStrategyConfig
 from .losses import FusedAdam, l1_ssim_loss
 from .rendering import rasterization, rasterization_2dgs
 from .strategy import activate, update_state_
@@ -72,6 +87,17 @@ def camera_pool(viewmats, Ks, src_w, src_h, width, height, n, seed=0):
     return torch.stack(vms), torch.stack(ks)
 
 
+def knn_log_scales(points: torch.Tensor, init_scale: float = 1.0) -> torch.Tensor:
+    """log of the RMS distance to the 3 nearest neighbours, repeated over the
+    3 axes (simple_trainer.py:221-224 with examples/utils.py:141-151 knn):
+    the SfM initialisation's scales.  One-off host work (a k-d tree)."""
+    from scipy.spatial import cKDTree
+    pts = points.detach().cpu().double().numpy()
+    d, _ = cKDTree(pts).query(pts, k=4, workers=-1)
+    dist2_avg = torch.from_numpy((d[:, 1:] ** 2).mean(-1)).float()
+    return torch.log(torch.sqrt(dist2_avg) * init_scale).unsqueeze(-1).repeat(1, 3)
+
+
 def _gauss_window(size=11, sigma=1.5, device="cpu"):
     x = torch.arange(size, dtype=torch.float32, device=device) - size // 2
     w = torch.exp(-(x ** 2) / (2 * sigma ** 2))
@@ -106,8 +132,13 @@ class Trainer:
 
     def __init__(self, points, rgbs, viewmats, Ks, width, height, sh_degree=3, device="cuda",
                  seed=42, world_size=1, rank=0, ssim_lambda=0.2, scene_scale=1.0,
-                 fused=True, model="3dgs", sharded_optimizer=None):
+                 fused=True, model="3dgs", sharded_optimizer=None,
+                 strategy: Optional[DefaultStrategyConfig] = None,
+                 sh_degree_interval: Optional[int] = None, max_steps: Optional[int] = None,
+                 init: str = "random", init_opacity: float = 0.1, init_scale: float = 1.0,
+                 targets: Optional[torch.Tensor] = None):
         assert model in ("3dgs", "2dgs"), model
+        assert init in ("random", "sfm"), init
         self.model = model
         g = torch.Generator().manual_seed(seed)  # identical on every rank (replicas)
         N = points.shape[0]
@@ -116,25 +147,37 @@ class Trainer:
         self.sh_degree = sh_degree
         self.ssim_lambda = ssim_lambda
         self.world_size, self.rank = world_size, rank
-        # initial attributes as load_test_data(): scales U(0,0.02), unit quats,
-        # opacities U(0,1); colours from the SfM points as SH DC terms.
-        scales = torch.rand(N, 3, generator=g) * 0.02 + 1e-4
-        quats = F.normalize(torch.randn(N, 4, generator=g), dim=-1)
-        opac = torch.rand(N, generator=g).clamp(1e-3, 1 - 1e-3)
+        self.scene_scale = scene_scale
+        self.strategy = strategy
+        if strategy is not None and model == "2dgs":
+            strategy.key_for_gradient = "gradient_2dgs"  # simple_trainer_2dgs.py:307-311
+        self.sh_degree_interval = sh_degree_interval
+        self.max_steps = max_steps
         K = (sh_degree + 1) ** 2
         sh = torch.zeros(N, K, 3)
         sh[:, 0, :] = rgb_to_sh(rgbs)
-        sh[:, 1:, :] = torch.randn(N, K - 1, 3, generator=g) * 0.01
+        if init == "random":
+            # load_test_data(): scales U(0,0.02), unit quats, opacities U(0,1);
+            # colours from the SfM points as SH DC terms
+            scales = torch.log(torch.rand(N, 3, generator=g) * 0.02 + 1e-4)
+            quats = F.normalize(torch.randn(N, 4, generator=g), dim=-1)
+            opac = torch.logit(torch.rand(N, generator=g).clamp(1e-3, 1 - 1e-3))
+            sh[:, 1:, :] = torch.randn(N, K - 1, 3, generator=g) * 0.01
+        else:  # simple_trainer.create_splats_with_optimizers, init_type="sfm"
+            scales = knn_log_scales(points, init_scale)
+            quats = torch.rand(N, 4, generator=g)
+            opac = torch.logit(torch.full((N,), float(init_opacity)))
         self.params = {
-            "means": points.clone(), "scales": torch.log(scales), "quats": quats,
-            "opacities": torch.logit(opac), "sh0": sh[:, :1].contiguous(),
-            "shN": sh[:, 1:].contiguous(),
+            "means": points.clone(), "scales": scales, "quats": quats, "opacities": opac,
+            "sh0": sh[:, :1].contiguous(), "shN": sh[:, 1:].contiguous(),
         }
-        self.params = {k: torch.nn.Parameter(v.to(device)) for k, v in self.params.items()}
+        self.params = {k: torch.nn.Parameter(v.float().contiguous().to(device))
+                       for k, v in self.params.items()}
         BS = world_size  # batch 1 per rank (simple_trainer.py:261-277)
-        groups = [{"params": [p], "lr": self.LRS[k] * (scene_scale if k == "means" else 1.0)
-                   * math.sqrt(BS), "name": k} for k, p in self.params.items()]
-        kw = dict(eps=1e-15 / math.sqrt(BS), betas=(1 - BS * (1 - 0.9), 1 - BS * (1 - 0.999)))
+        self.lrs = [self.LRS[k] * (scene_scale if k == "means" else 1.0) * math.sqrt(BS)
+                    for k in self.params]
+        self.adam_kw = dict(eps=1e-15 / math.sqrt(BS),
+                            betas=(1 - BS * (1 - 0.9), 1 - BS * (1 - 0.999)))
         self.fused = fused
         # N > 1: gradients reduce-scattered, Adam on this rank's rows, rows
         # all-gathered (distributed.ShardedAdam) instead of all-reduce + full Adam
@@ -142,28 +185,102 @@ class Trainer:
         if sharded_optimizer is None:
             sharded_optimizer = world_size > 1
         self.sharded = fused and sharded_optimizer
-        if self.sharded:
-            from .distributed import ShardedAdam
-            self.opt = ShardedAdam([g["params"][0] for g in groups], [g["lr"] for g in groups],
-                                   **kw)
-        elif fused:  # HIP loss + one-launch Adam (csrc/ssim.hip, csrc/adam.hip)
-            self.opt = FusedAdam([g["params"][0] for g in groups], [g["lr"] for g in groups], **kw)
-        else:  # torch reference path (conv SSIM, torch.optim.Adam)
-            self.opt = torch.optim.Adam(groups, foreach=True, **kw)
+        self.opt = self._make_optimizer(list(self.params.values()))
         self.viewmats = viewmats.to(device)
         self.Ks = Ks.to(device)
-        gt = torch.Generator().manual_seed(1234)
-        self.targets = torch.rand(len(viewmats), height, width, 3, generator=gt).to(device)
+        if targets is None:
+            gt = torch.Generator().manual_seed(1234)
+            targets = torch.rand(len(viewmats), height, width, 3, generator=gt)
+        self.targets = targets.to(device)
         self.grad2d = torch.zeros(N, device=device)
         self.count = torch.zeros(N, device=device)
+        # split noise: the same stream on every rank (replicas stay identical)
+        self.rng = torch.Generator(device=device).manual_seed(seed)
         self.window = _gauss_window(device=device)
         self.last_meta = None
+        self.refine_log = []  # (step, n_dupli, n_split, n_prune, N after)
 
+    # ------------------------------------------------------------ optimizer
+    def _make_optimizer(self, params):
+        if self.sharded:
+            from .distributed import ShardedAdam
+            return ShardedAdam(params, self.lrs, **self.adam_kw)
+        if self.fused:  # HIP loss + one-launch Adam (csrc/ssim.hip, csrc/adam.hip)
+            return FusedAdam(params, self.lrs, **self.adam_kw)
+        groups = [{"params": [p], "lr": lr, "name": k}
+                  for (k, p), lr in zip(self.params.items(), self.lrs)]
+        return torch.optim.Adam(groups, foreach=True, **self.adam_kw)
+
+    def _set_means_lr(self, lr):
+        if isinstance(self.opt, torch.optim.Optimizer):
+            self.opt.param_groups[0]["lr"] = lr
+        else:
+            self.opt.lrs[0] = lr
+
+    def moments(self):
+        """name -> [exp_avg, exp_avg_sq] as full tensors shaped like the
+        parameter (gathered over the ranks for the sharded optimizer)."""
+        names = list(self.params)
+        if self.sharded:
+            return {k: list(mv) for k, mv in zip(names, self.opt.full_state())}
+        if self.fused:
+            return {k: [self.opt.exp_avg[i], self.opt.exp_avg_sq[i]]
+                    for i, k in enumerate(names)}
+        out = {}
+        for k in names:
+            st = self.opt.state.get(self.params[k], {})
+            if "exp_avg" not in st:  # no step taken yet
+                z = torch.zeros_like(self.params[k])
+                st = {"exp_avg": z, "exp_avg_sq": z.clone()}
+            out[k] = [st["exp_avg"], st["exp_avg_sq"]]
+        return out
+
+    def _load_moments(self, moments):
+        params = list(self.params.values())
+        names = list(self.params)
+        if self.sharded:
+            step = self.opt.step_count
+            self.opt = self._make_optimizer(params)
+            self.opt.load_full_state([moments[k] for k in names], step)
+        elif self.fused:
+            self.opt.params = params
+            self.opt.exp_avg = [moments[k][0] for k in names]
+            self.opt.exp_avg_sq = [moments[k][1] for k in names]
+        else:
+            old = self.opt
+            step = next(iter(old.state.values()), {}).get("step")
+            lrs = [g["lr"] for g in old.param_groups]
+            self.opt = self._make_optimizer(params)
+            for g, lr in zip(self.opt.param_groups, lrs):
+                g["lr"] = lr
+            if step is not None:
+                for k, p in self.params.items():
+                    self.opt.state[p] = {"step": step.clone(), "exp_avg": moments[k][0],
+                                         "exp_avg_sq": moments[k][1]}
+
+    def sync(self):
+        """Order the current stream after any optimizer communication still in
+        flight (the sharded optimizer's deferred all-gathers): call before
+        reading the parameters outside the training step (checkpoint, eval)."""
+        if self.sharded:
+            self.opt.wait()
+
+    def synced_params(self):
+        self.sync()
+        return self.params
+
+    # ---------------------------------------------------------------- step
     def camera_index(self, it: int) -> int:
         return (it * self.world_size + self.rank) % len(self.viewmats)
 
-    def render(self, ci: int):
+    def sh_degree_at(self, it: int) -> int:
+        if self.sh_degree_interval is None:
+            return self.sh_degree
+        return min(it // self.sh_degree_interval, self.sh_degree)
+
+    def render(self, ci: int, sh_degree: Optional[int] = None):
         p = self.params
+        deg = self.sh_degree if sh_degree is None else sh_degree
         hook = None
         if self.sharded:
             # the previous step's all-gathers: geometry before the projection,
@@ -176,25 +293,26 @@ class Trainer:
             scales, opac = activate(p["scales"], p["opacities"])
         else:
             scales, opac = torch.exp(p["scales"]), torch.sigmoid(p["opacities"])
+        absgrad = self.strategy is not None and self.strategy.absgrad
         if self.model == "2dgs":
             if hook is not None:
                 hook()
             rc, ra, _, _, _, _, meta = rasterization_2dgs(
                 p["means"], p["quats"], scales, opac, (p["sh0"], p["shN"]),
                 self.viewmats[ci:ci + 1], self.Ks[ci:ci + 1], self.width, self.height,
-                sh_degree=self.sh_degree, packed=False, near_plane=0.01, far_plane=1e10,
-                render_mode="RGB+D")
+                sh_degree=deg, packed=False, near_plane=0.01, far_plane=1e10,
+                render_mode="RGB+D", absgrad=absgrad)
             return rc[..., :3], ra, meta
         return rasterization(
             p["means"], p["quats"], scales, opac,
-            (p["sh0"], p["shN"]) if self.fused else torch.cat([p["sh0"], p["shN"]], 1), self.viewmats[ci:ci + 1], self.Ks[ci:ci + 1],
-            self.width, self.height, sh_degree=self.sh_degree, packed=False,
-            near_plane=0.01, far_plane=1e10, radius_clip=0.0, rasterize_mode="classic",
-            _colors_ready=hook)
+            (p["sh0"], p["shN"]) if self.fused else torch.cat([p["sh0"], p["shN"]], 1),
+            self.viewmats[ci:ci + 1], self.Ks[ci:ci + 1], self.width, self.height,
+            sh_degree=deg, packed=False, near_plane=0.01, far_plane=1e10, radius_clip=0.0,
+            rasterize_mode="classic", absgrad=absgrad, _colors_ready=hook)
 
     def step(self, it: int):
         ci = self.camera_index(it)
-        colors, alphas, meta = self.render(ci)
+        colors, alphas, meta = self.render(ci, self.sh_degree_at(it))
         if self.model == "3dgs":
             meta["means2d"].retain_grad()  # DefaultStrategy.step_pre_backward
         gt = self.targets[ci:ci + 1]
@@ -208,14 +326,75 @@ class Trainer:
         loss.backward()
         if self.world_size > 1 and not self.sharded:
             self.allreduce_grads()
-        self.update_state(meta)
+        if self.strategy is None or it < self.strategy.refine_stop_iter:
+            self.update_state(meta)
+        if self.max_steps:  # means ExponentialLR, stepped after every optimizer step
+            self._set_means_lr(self.lrs[0] * (0.01 ** (1.0 / self.max_steps)) ** it)
         if self.sharded:
             self.opt.step(defer_gather=True)
         else:
             self.opt.step()
         self.opt.zero_grad(set_to_none=True)
         self.last_meta = meta
+        if self.strategy is not None:
+            self.post_step(it)
         return loss
+
+    # ------------------------------------------------------------ strategy
+    def post_step(self, it: int):
+        """DefaultStrategy.step_post_backward after the statistics
+        (default.py:175-211): refine, then the opacity reset."""
+        cfg = self.strategy
+        if it >= cfg.refine_stop_iter:
+            return
+        if cfg.is_refine_step(it):
+            self.refine(it)
+        if cfg.is_reset_step(it):
+            self.reset_opacity()
+
+    @torch.no_grad()
+    def refine(self, it: int):
+        self.sync()
+        self.last_meta = None  # its tensors are sized for the old Gaussians
+        if self.world_size > 1:
+            # every rank accumulated its own cameras: the batch statistics are
+            # the sums (radii are not tracked: refine_scale2d_stop_iter = 0)
+            import torch.distributed as dist
+            works = [dist.all_reduce(t, op=dist.ReduceOp.SUM, async_op=True)
+                     for t in (self.grad2d, self.count)]
+            for w in works:
+                w.wait()
+        params = {k: p.data for k, p in self.params.items()}
+        new_p, new_m, counts = densify.refine(params, self.moments(), self.grad2d, self.count,
+                                              it, self.strategy, self.scene_scale,
+                                              generator=self.rng)
+        self.params = {k: torch.nn.Parameter(v) for k, v in new_p.items()}
+        self._load_moments(new_m)
+        n = self.params["means"].shape[0]
+        self.grad2d = torch.zeros(n, device=self.device)
+        self.count = torch.zeros(n, device=self.device)
+        self.refine_log.append((it,) + tuple(counts) + (n,))
+
+    @torch.no_grad()
+    def reset_opacity(self):
+        self.sync()
+        value = self.strategy.prune_opa * 2.0
+        if self.sharded:
+            lim = float(torch.logit(torch.tensor(value, dtype=torch.float32)))
+            self.params["opacities"].data.clamp_(max=lim)
+            self.opt.zero_moments(list(self.params).index("opacities"))
+        else:
+            moms = self.moments()
+            densify.reset_opacity({"opacities": self.params["opacities"].data},
+                                  {"opacities": moms["opacities"]}, value)
+
+    def densify_desc(self):
+        if self.strategy is None:
+            return "off (DefaultStrategy statistics only; fixed Gaussian count)"
+        c = self.strategy
+        return (f"DefaultStrategy refine every {c.refine_every} steps in "
+                f"({c.refine_start_iter}, {c.refine_stop_iter}), opacity reset every "
+                f"{c.reset_every}; refines so far: {self.refine_log}")
 
     def allreduce_grads(self):
         """SUM the Gaussian gradients over ranks (RCCL over xGMI); issued
@@ -233,7 +412,9 @@ class Trainer:
     def update_state(self, meta):
         """DefaultStrategy._update_state for packed=False without the host
         sync of torch.where (default.py:213-262): same sums, masked."""
-        g = meta["gradient_2dgs" if self.model == "2dgs" else "means2d"].grad
+        key = "gradient_2dgs" if self.model == "2dgs" else "means2d"
+        absgrad = self.strategy is not None and self.strategy.absgrad
+        g = meta[key].absgrad if absgrad else meta[key].grad
         if g is None:
             return
         if self.fused:

@@ -285,6 +285,47 @@ int gsplat_hip_activate_bwd(int64_t n_scales, int64_t n_opacities, const float *
                             const float *v_opacities, float *v_log_scales, float *v_logits,
                             void *stream);
 
+/* DefaultStrategy's refine step -- _grow_gs + _prune_gs of
+ * gsplat/strategy/default.py:264-340 over duplicate / split / remove of
+ * gsplat/strategy/ops.py:86-211 -- as one compaction around one host sync.
+ *
+ * gsplat_hip_densify_plan classifies every Gaussian (grad2d / max(count, 1)
+ * against grow_grad2d, max exp(log_scales) against grow_scale3d [absolute:
+ * the caller multiplies by scene_scale], sigmoid(logits) against prune_opa,
+ * and with prune_big also max exp(log_scales) against prune_scale3d; radii2d
+ * (nullable) adds the refine_scale2d rules with grow_scale2d / prune_scale2d)
+ * and writes totals[5] (device int64) = (originals kept, duplicates kept,
+ * split Gaussians whose children are kept, split Gaussians, duplicated
+ * Gaussians).  The caller reads them (the sync), allocates n_out = t0 + t1 +
+ * 2 t2 rows per array and draws randn[2, t3, 3] (ops.py:147-152 draws
+ * torch.randn(2, n_split, 3)); the reference's pruned count is
+ * N + t4 + t3 - n_out.
+ *
+ * gsplat_hip_densify_apply writes the final layout
+ *   [kept originals] ++ [kept duplicates] ++ [first children] ++ [second children]
+ * of every array: kind COPY copies the row to every output, MEANS / SCALES /
+ * OPACITIES give the children mean + R(q) diag(exp(s)) z_b, log(exp(s) / 1.6)
+ * and (revised_opacity) logit(1 - sqrt(1 - sigmoid(o))), MOMENT copies the
+ * row of a kept original and zero-fills the new rows (the optimizer state of
+ * ops.py:104-105,169-170).  means/quats/log_scales/logits are the sources the
+ * children derive from.  At most 24 arrays. */
+#define GSPLAT_HIP_DENSIFY_COPY 0
+#define GSPLAT_HIP_DENSIFY_MEANS 1
+#define GSPLAT_HIP_DENSIFY_SCALES 2
+#define GSPLAT_HIP_DENSIFY_OPACITIES 3
+#define GSPLAT_HIP_DENSIFY_MOMENT 4
+int64_t gsplat_hip_densify_workspace_bytes(int64_t N);
+int gsplat_hip_densify_plan(int64_t N, const float *grad2d, const float *count,
+                            const float *log_scales, const float *logits, const float *radii2d,
+                            float grow_grad2d, float grow_scale3d, float prune_opa, int prune_big,
+                            float prune_scale3d, float grow_scale2d, float prune_scale2d,
+                            int revised_opacity, void *workspace, int64_t *totals, void *stream);
+int gsplat_hip_densify_apply(int64_t N, const void *workspace, const int64_t *totals,
+                             const float *randn, int revised_opacity, int n_arrays,
+                             const float *const *src, float *const *dst, const int32_t *row_floats,
+                             const int32_t *kinds, const float *means, const float *quats,
+                             const float *log_scales, const float *logits, void *stream);
+
 /* One torch.optim.Adam step (amsgrad=False, no weight decay) over up to 8
  * parameter groups in a single launch (replaces the per-group optimizers of
  * examples/simple_trainer.py:265-276).  Host arrays of length n_groups. */

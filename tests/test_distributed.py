@@ -212,3 +212,151 @@ def test_sharded_adam_matches_allreduce_adam_gloo(world, defer):
         assert not isinstance(err, str), err
         assert err < 1e-5, (rank, err)
         assert vals == out[0][1], "replicas diverged"
+
+
+# ------------------------------------------- densification under DP (gloo) --
+def _oracle_refine(params, moments, grad2d, count, step, cfg, scene_scale=1.0, generator=None,
+                   z=None, radii2d=None):
+    """gsplat_hip.densify.refine's contract computed by the CPU oracle (the
+    HIP kernels need a GPU): split noise drawn from `generator` exactly as the
+    HIP path draws it (randn(2, n_split, 3) after the plan)."""
+    import numpy as np
+    from oracle import strategy_oracle as S
+    grads = grad2d / count.clamp_min(1)
+    high = grads > cfg.grow_grad2d
+    n_split = int((high & (torch.exp(params["scales"]).max(-1).values
+                           > cfg.grow_scale3d * scene_scale)).sum())
+    if z is None:
+        z = torch.randn(2, n_split, 3, generator=generator)
+    p, m, counts = S.refine({k: v.numpy() for k, v in params.items()},
+                            {k: (a.numpy(), b.numpy()) for k, (a, b) in moments.items()},
+                            grad2d.numpy(), count.numpy(), step, z.numpy(), scene_scale,
+                            revised_opacity=cfg.revised_opacity)
+    return ({k: torch.from_numpy(np.ascontiguousarray(v)) for k, v in p.items()},
+            {k: [torch.from_numpy(np.ascontiguousarray(t)) for t in v] for k, v in m.items()},
+            counts)
+
+
+def _trainer_skeleton(rank, world, sharded):
+    """A Trainer with CPU parameters (no rendering): what refine touches."""
+    from gsplat_hip import train_step
+    from gsplat_hip.densify import DefaultStrategyConfig
+    from gsplat_hip.distributed import ShardedAdam, _adam_torch
+    from gsplat_hip.losses import FusedAdam
+    g = torch.Generator().manual_seed(0)  # identical replicas
+    N = 203
+    init = {"means": torch.randn(N, 3, generator=g),
+            "scales": torch.rand(N, 3, generator=g) * 5.7 - 6.9,
+            "quats": torch.randn(N, 4, generator=g),
+            "opacities": torch.randn(N, generator=g) * 3 - 2,
+            "sh0": torch.randn(N, 1, 3, generator=g), "shN": torch.randn(N, 15, 3, generator=g)}
+    tr = train_step.Trainer.__new__(train_step.Trainer)
+    tr.params = {k: torch.nn.Parameter(v.clone()) for k, v in init.items()}
+    tr.world_size, tr.rank, tr.device = world, rank, "cpu"
+    tr.sharded, tr.fused = sharded, True
+    tr.strategy = DefaultStrategyConfig()
+    tr.scene_scale = 1.0
+    tr.lrs = [1e-3] * 6
+    tr.adam_kw = dict(betas=(0.9, 0.999), eps=1e-15)
+    tr.rng = torch.Generator().manual_seed(42)
+    tr.refine_log, tr.last_meta = [], None
+    if sharded:
+        tr.opt = ShardedAdam(list(tr.params.values()), tr.lrs, update=_adam_torch, **tr.adam_kw)
+    else:
+        tr.opt = FusedAdam.__new__(FusedAdam)
+        tr.opt.params = list(tr.params.values())
+        tr.opt.lrs, tr.opt.step_count = tr.lrs, 0
+        tr.opt.exp_avg = [torch.zeros_like(p) for p in tr.opt.params]
+        tr.opt.exp_avg_sq = [torch.zeros_like(p) for p in tr.opt.params]
+    # populate the moments with two identical-on-every-rank Adam steps
+    for step in range(2):
+        gr = torch.Generator().manual_seed(7 + step)
+        grads = [torch.randn(p.shape, generator=gr) * 1e-2 for p in tr.params.values()]
+        if sharded:
+            for p, gg in zip(tr.params.values(), grads):
+                p.grad = gg / world  # the ranks' gradients sum to gg
+            tr.opt.step()
+            tr.opt.zero_grad()
+        else:
+            tr.opt.step_count += 1
+            _adam_torch([p.data.view(-1) for p in tr.opt.params], [x.view(-1) for x in grads],
+                        [m.view(-1) for m in tr.opt.exp_avg],
+                        [v.view(-1) for v in tr.opt.exp_avg_sq], tr.lrs,
+                        tr.adam_kw["betas"], tr.adam_kw["eps"], tr.opt.step_count)
+    # per-rank statistics (each rank saw its own cameras)
+    gs = torch.Generator().manual_seed(100 + rank)
+    tr.count = torch.randint(0, 4, (N,), generator=gs).float()
+    tr.grad2d = torch.rand(N, generator=gs) * 4e-4 * tr.count
+    return tr
+
+
+def _refine_worker(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from gsplat_hip import train_step
+        train_step.densify.refine = _oracle_refine
+        tr = _trainer_skeleton(rank, world, sharded=True)
+        tr.refine(3100)
+        moms = tr.moments()  # all-gathered from the new shards
+        # numpy, not tensors: a tensor in the queue lives in the worker's
+        # shared memory, gone when the worker exits
+        out = {"params": {k: v.detach().numpy().copy() for k, v in tr.params.items()},
+               "m": {k: [t.numpy().copy() for t in v] for k, v in moms.items()},
+               "log": tr.refine_log, "grad2d": float(tr.grad2d.abs().sum())}
+        q.put((rank, out))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:
+        import traceback
+        q.put((rank, traceback.format_exc() + repr(e)))
+
+
+def test_refine_under_dp_keeps_replicas_identical_gloo():
+    """Trainer.refine on two gloo ranks with different per-rank statistics:
+    the statistics are summed before the decision, the split noise comes from
+    the shared-seed generator, the sharded Adam moments are gathered, pushed
+    through the compaction and re-sharded -- both replicas end bit-identical
+    and equal a single-process refine on the summed statistics."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    world = 2
+    procs = [ctx.Process(target=_refine_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=180) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    import numpy as np
+    for r in range(world):
+        assert isinstance(res[r], dict), res[r]
+    a, b = res[0], res[1]
+    assert a["log"] == b["log"] and a["log"][0][0] == 3100
+    for k in a["params"]:
+        assert np.array_equal(a["params"][k], b["params"][k]), k
+        assert np.array_equal(a["m"][k][0], b["m"][k][0])
+        assert np.array_equal(a["m"][k][1], b["m"][k][1])
+    assert a["grad2d"] == 0.0  # statistics restart after a refine
+
+    # single process, unsharded, on the summed statistics: the same result
+    import numpy as np  # noqa: F811
+    from gsplat_hip import train_step
+    saved = train_step.densify.refine
+    train_step.densify.refine = _oracle_refine
+    try:
+        trs = [_trainer_skeleton(r, world, sharded=False) for r in range(world)]
+        ref = trs[0]
+        ref.world_size = 1
+        ref.grad2d = trs[0].grad2d + trs[1].grad2d
+        ref.count = trs[0].count + trs[1].count
+        ref.refine(3100)
+    finally:
+        train_step.densify.refine = saved
+    assert ref.refine_log == a["log"]
+    for k, p in ref.params.items():
+        np.testing.assert_array_equal(p.detach().numpy(), a["params"][k], err_msg=k)
+        mm = ref.moments()[k]
+        np.testing.assert_allclose(mm[0].numpy(), a["m"][k][0], rtol=1e-6, atol=1e-9)
+        np.testing.assert_allclose(mm[1].numpy(), a["m"][k][1], rtol=1e-6, atol=1e-12)

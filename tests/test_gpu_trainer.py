@@ -2,6 +2,8 @@
 fused SSIM+L1 (vs the conv formulation of fused_ssim's algorithm, autograd)
 and the one-launch Adam (vs torch.optim.Adam)."""
 
+import math
+
 import pytest
 import torch
 
@@ -115,3 +117,71 @@ def test_update_state_matches_torch(C):
         c_r.index_add_(0, ids, torch.ones_like(ids, dtype=torch.float32))
     torch.testing.assert_close(grad2d, g_r, rtol=1e-6, atol=0)
     assert torch.equal(count, c_r)
+
+
+def _small_scene(n_cams=4, W=320, H=240):
+    import os as _os
+    from gsplat_hip.train_step import camera_pool, load_garden_scene
+    root = _os.path.dirname(_os.path.dirname(_os.path.abspath(__file__)))
+    means, rgbs, vms, Ks, sw, sh_ = load_garden_scene(
+        _os.path.join(root, "tests", "golden", "garden_scene.npz"), scene_grid=1)
+    means, rgbs = means[::8].contiguous(), rgbs[::8].contiguous()
+    vm, K = camera_pool(vms, Ks, sw, sh_, W, H, n=n_cams)
+    return means, rgbs, vm, K, W, H
+
+
+@pytest.mark.parametrize("sharded", [False, True])
+def test_trainer_densification_schedule(sharded):
+    """The simple_trainer default schedule on the HIP path (compressed in
+    time): SfM init with knn scales, SH degree schedule, means LR decay,
+    refine every 2 steps and opacity reset every 5.  Every refine rebuilds the
+    parameters and the optimizer state consistently (sizes; the decisions
+    themselves are pinned by test_gpu_strategy.py) and training keeps going,
+    with the fused optimizer and with the sharded one on one RCCL rank (its
+    state gathered, compacted and re-sharded).  The multi-rank statistics sum
+    and shared noise: tests/test_distributed.py (gloo)."""
+    import torch.distributed as dist
+    own_pg = sharded and not dist.is_initialized()
+    if own_pg:
+        import os as _os
+        import socket
+        with socket.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            port = sk.getsockname()[1]
+        _os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        _densification_schedule(sharded)
+    finally:
+        if own_pg:
+            dist.destroy_process_group()
+
+
+def _densification_schedule(sharded):
+    from gsplat_hip.densify import DefaultStrategyConfig
+    from gsplat_hip.train_step import Trainer
+    means, rgbs, vm, K, W, H = _small_scene()
+    cfg = DefaultStrategyConfig(refine_start_iter=1, refine_every=2, reset_every=5)
+    tr = Trainer(means, rgbs, vm, K, W, H, device="cuda", strategy=cfg, sh_degree_interval=2,
+                 max_steps=100, init="sfm", sharded_optimizer=sharded)
+    losses = []
+    for it in range(7):
+        losses.append(float(tr.step(it)))
+        n = tr.params["means"].shape[0]
+        for k, p in tr.params.items():
+            assert p.shape[0] == n, k
+        for k, (m, v) in tr.moments().items():
+            assert m.shape == tr.params[k].shape and v.shape == tr.params[k].shape, k
+        assert tr.grad2d.numel() == n and tr.count.numel() == n
+        if it == 5:  # reset_every: opacities clamped to logit(0.01), moments zero
+            tr.sync()
+            lim = float(torch.logit(torch.tensor(0.01)))
+            assert float(tr.params["opacities"].max()) <= lim + 1e-6
+            assert float(tr.moments()["opacities"][0].abs().max()) == 0.0
+    assert [r[0] for r in tr.refine_log] == [2, 4, 6], tr.refine_log
+    assert all(math.isfinite(x) for x in losses), losses
+    n0 = means.shape[0]
+    assert tr.refine_log[0][4] == n0 + tr.refine_log[0][1] + tr.refine_log[0][2] \
+        - tr.refine_log[0][3], tr.refine_log
+    assert tr.refine_log[0][1] + tr.refine_log[0][2] > 0  # random targets: something grows
+    tr.sync()
