@@ -298,8 +298,12 @@ int rasterize16_fwd(int C, int D, int W, int H, int tw, int th, const float *mea
                     const float *conics, const float *colors, const float *opacities,
                     const float *backgrounds, const uint8_t *masks, const int32_t *offsets,
                     int64_t n_isects, const int32_t *flatten_ids, float *render_colors,
-                    float *render_alphas, int32_t *last_ids, void *state, int64_t state_bytes,
-                    hipStream_t st);
+                    float *render_alphas, int32_t *last_ids, const float *records, void *state,
+                    int64_t state_bytes, hipStream_t st);
+int rasterize16_record_floats(int D);
+int rasterize16_pack_records(int64_t G, int D, const float *means2d, const float *conics,
+                             const float *colors, const float *opacities, const int32_t *visible,
+                             float *records, hipStream_t st);
 int64_t rasterize16_fwd_state_bytes(int D, int n_tiles, int64_t n_isects);
 int rasterize16_prepare(int D, int n_tiles, const int32_t *offsets, int64_t n_isects,
                         void *state, int64_t state_bytes, hipStream_t st);
@@ -311,8 +315,8 @@ int rasterize16_bwd(int C, int64_t G, int D, int W, int H, int tw, int th,
                     const float *render_alphas, const int32_t *last_ids,
                     const float *v_render_colors, const float *v_render_alphas,
                     float *v_means2d, float *v_conics, float *v_colors, float *v_opacities,
-                    float *v_abs, const float *render_colors, const void *state,
-                    int64_t state_bytes, void *workspace, hipStream_t st);
+                    float *v_abs, const float *render_colors, const float *records,
+                    const void *state, int64_t state_bytes, void *workspace, hipStream_t st);
 }  // namespace gs
 
 using namespace gs;
@@ -346,6 +350,18 @@ extern "C" int64_t gsplat_hip_rasterize_bwd_workspace_bytes(int64_t n_gaussians,
                                    n_isects);
 }
 
+extern "C" int gsplat_hip_rasterize_record_floats(int D, int tile_size) {
+  return tile_size == 16 ? rasterize16_record_floats(D) : 0;
+}
+
+extern "C" int gsplat_hip_rasterize_pack_records(int64_t n_gaussians, int D, const float *means2d,
+                                                 const float *conics, const float *colors,
+                                                 const float *opacities, const int32_t *visible,
+                                                 float *records, void *stream) {
+  return rasterize16_pack_records(n_gaussians, D, means2d, conics, colors, opacities, visible,
+                                  records, (hipStream_t)stream);
+}
+
 static int check_common(int C, int D, int W, int H, int ts, int tw, int th) {
   GS_REQUIRE(supported_channels(D), "rasterize: unsupported channel count %d", D);
   GS_REQUIRE(ts > 0 && ts * ts <= 256, "rasterize: tile_size %d not in [1, 16]", ts);
@@ -364,8 +380,8 @@ extern "C" int gsplat_hip_rasterize_fwd(int C, int D, int width, int height, int
                                         const uint8_t *masks, const int32_t *isect_offsets,
                                         int64_t n_isects, const int32_t *flatten_ids,
                                         float *render_colors, float *render_alphas,
-                                        int32_t *last_ids, void *state, int64_t state_bytes,
-                                        void *stream) {
+                                        int32_t *last_ids, const float *records, void *state,
+                                        int64_t state_bytes, void *stream) {
   if (int e = check_common(C, D, width, height, tile_size, tile_width, tile_height)) return e;
   if ((int64_t)C * tile_width * tile_height == 0) return 0;
   RasterArgs a{};
@@ -379,7 +395,8 @@ extern "C" int gsplat_hip_rasterize_fwd(int C, int D, int width, int height, int
   if (tile_size == 16)
     return rasterize16_fwd(C, D, width, height, tile_width, tile_height, means2d, conics, colors,
                            opacities, backgrounds, masks, isect_offsets, n_isects, flatten_ids,
-                           render_colors, render_alphas, last_ids, state, state_bytes, st);
+                           render_colors, render_alphas, last_ids, records, state, state_bytes,
+                           st);
   const int thr = block_threads(tile_size);
   switch (D) {
     case 1: return launch_fwd<1>(a, thr, st);
@@ -401,8 +418,9 @@ extern "C" int gsplat_hip_rasterize_bwd(
     const int32_t *isect_offsets, int64_t n_isects, const int32_t *flatten_ids,
     const float *render_alphas, const int32_t *last_ids, const float *v_render_colors,
     const float *v_render_alphas, float *v_means2d, float *v_conics, float *v_colors,
-    float *v_opacities, float *v_means2d_abs, const float *render_colors, const void *state,
-    int64_t state_bytes, void *workspace, int64_t workspace_bytes, void *stream) {
+    float *v_opacities, float *v_means2d_abs, const float *render_colors, const float *records,
+    const void *state, int64_t state_bytes, void *workspace, int64_t workspace_bytes,
+    void *stream) {
   if (int e = check_common(C, D, width, height, tile_size, tile_width, tile_height)) return e;
   hipStream_t st = (hipStream_t)stream;
   const size_t G = (size_t)n_gaussians;
@@ -416,7 +434,8 @@ extern "C" int gsplat_hip_rasterize_bwd(
                            conics, colors, opacities, backgrounds, masks, isect_offsets,
                            n_isects, flatten_ids, render_alphas, last_ids, v_render_colors,
                            v_render_alphas, v_means2d, v_conics, v_colors, v_opacities,
-                           v_means2d_abs, render_colors, state, state_bytes, workspace, st);
+                           v_means2d_abs, render_colors, records, state, state_bytes, workspace,
+                           st);
   }
   GS_HIP(hipMemsetAsync(v_means2d, 0, sizeof(float) * 2 * G, st));
   GS_HIP(hipMemsetAsync(v_conics, 0, sizeof(float) * 3 * G, st));

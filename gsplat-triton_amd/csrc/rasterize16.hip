@@ -105,10 +105,20 @@ GS_INLINE f2v reduce_scatter2(const f2v *v, int lane) {
   return z;
 }
 
+// Render records: one 64-B row per Gaussian, [x, y, a, b, c, opacity,
+// colour[D], pad] (D <= kRecMaxD), so the per-isect gather of a batch touches
+// one 64-B sector per lane instead of four lines of four arrays
+// (rasterize_to_pixels_fwd.py:93-145 loads the four arrays separately).
+constexpr int kRecFloats = 16;
+constexpr int kHead = 32, kHeadStride = 32;  // queue[] layout (see Args::queue)
+constexpr int kQueueInts = kHead + 8 * kHeadStride;
+constexpr int kRecMaxD = kRecFloats - 6;
+
 struct Args {
   int C, W, H, tw, th, n_tiles;
   int64_t n_isects;
   const float *means2d, *conics, *colors, *opacities, *backgrounds;
+  const float *records;  // [G][kRecFloats] render records, or null (gather the arrays)
   const uint8_t *masks;
   const int32_t *offsets, *flatten_ids;
   float *render_colors, *render_alphas;
@@ -125,6 +135,12 @@ struct Args {
   const int2 *items, *items_tail;
   const int32_t *n_items;
   const int32_t *order;  // forward: tile of workgroup b (heaviest tiles first) or null
+  // forward, XCD-aware dispatch (order_xcd_kernel): order[] holds 8 segments
+  // of spatially contiguous tiles; queue[0..8) their starts, [8..16) their
+  // lengths, queue[kHead + kHeadStride q] the dequeue head of segment q (one
+  // 128-B line each: heads sharing a line serialise the returning atomics,
+  // ~85 per us -- tools/xcc_probe.hip).  null: order[blockIdx.x]
+  int32_t *queue;
   const float *render_colors_in;  // backward: forward colours (for suffix sums)
   int dbg;  // experiments only (GSPLAT_HIP_DBG): bit 0 = backward skips its atomics
   uint64_t *timeline;  // debug: per-wave (start, end) s_memrealtime stamps or null
@@ -203,6 +219,24 @@ struct Attr {
 template <int D>
 GS_INLINE void load_attr(const Args &a, int32_t g, Attr<D> &at) {
   at.g = g;
+  if constexpr (D <= kRecMaxD) {
+    if (a.records) {  // wave-uniform
+      constexpr int N4 = (6 + D + 3) / 4;
+      const float4 *r = reinterpret_cast<const float4 *>(a.records + (int64_t)g * kRecFloats);
+      float v[4 * N4];
+#pragma unroll
+      for (int q = 0; q < N4; ++q) {
+        const float4 x = r[q];
+        v[4 * q] = x.x; v[4 * q + 1] = x.y; v[4 * q + 2] = x.z; v[4 * q + 3] = x.w;
+      }
+      at.xy = make_float2(v[0], v[1]);
+      at.con = make_float3(v[2], v[3], v[4]);
+      at.op = v[5];
+#pragma unroll
+      for (int d = 0; d < D; ++d) at.col[d] = v[6 + d];
+      return;
+    }
+  }
   at.xy = *reinterpret_cast<const float2 *>(a.means2d + 2 * (int64_t)g);
   const float *cn = a.conics + 3 * (int64_t)g;
   at.con = make_float3(cn[0], cn[1], cn[2]);
@@ -263,6 +297,34 @@ GS_INLINE void read_rec(const float4 *slot, float (&r)[Rec<D, FWD>::NF]) {
     if (WIDE) asm volatile("" ::"v"(v[q].x), "v"(v[q].y), "v"(v[q].z), "v"(v[q].w));
     r[4 * q] = v[q].x; r[4 * q + 1] = v[q].y; r[4 * q + 2] = v[q].z; r[4 * q + 3] = v[q].w;
   }
+}
+
+// The forward's tile of this workgroup.  With the XCD queues, segment x of
+// the tiles (a band of the image holding 1/8 of the work) is served to the
+// XCD whose id is x, so the Gaussians a band's tiles share stay in that XCD's
+// L2 (MI355X_MICROARCH.md "L2 (per XCD)"); an XCD whose band is exhausted
+// takes tiles from the next bands.  Every workgroup gets exactly one tile:
+// the queues hold n_tiles tiles and the grid is n_tiles workgroups.  The XCD
+// id only steers speed -- the result of a tile does not depend on who runs it.
+GS_INLINE int fwd_tile(const Args &a) {
+  if (!a.queue) return a.order ? a.order[blockIdx.x] : (int)blockIdx.x;
+  __shared__ int s_tile;
+  if (threadIdx.x == 0) {
+    const int x = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 7;  // HW_REG_XCC_ID
+    int t = -1;
+    for (int k = 0; k < 8 && t < 0; ++k) {
+      const int q = (x + k) & 7;
+      int *head = &a.queue[kHead + kHeadStride * q];
+      const int len = a.queue[8 + q];
+      // a stale read is low (heads only grow): skipping on it is always right
+      if (__atomic_load_n(head, __ATOMIC_RELAXED) >= len) continue;
+      const int i = atomicAdd(head, 1);
+      if (i < len) t = a.order[a.queue[q] + i];
+    }
+    s_tile = t;
+  }
+  __syncthreads();
+  return s_tile;
 }
 
 // Geometry of one wave: 4 waves share a 16x16 tile, each owning a 16x4
@@ -380,7 +442,9 @@ __attribute__((amdgpu_waves_per_eu(U == 1 ? 6 : U == 2 ? 5 : 4))) fwd_kernel(Arg
   const int lane = threadIdx.x & 63;
   float4 *st = stage_all[threadIdx.x >> 6];
   const uint64_t t_start = tl_now(a);
-  const WaveGeom geo(a, lane, a.order ? a.order[blockIdx.x] : (int)blockIdx.x);
+  const int tile_ = fwd_tile(a);
+  if (tile_ < 0) return;  // unreachable: the queues hold one tile per workgroup
+  const WaveGeom geo(a, lane, tile_);
   const int tile = geo.tile, c = geo.c;
   const bool inside = geo.px < a.W && geo.py < a.H;
   const float fx = (float)geo.px + 0.5f, fy = (float)geo.py + 0.5f;
@@ -565,7 +629,8 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(3))) f
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   float4 *st = stage_all[w];
   const uint64_t t_start = tl_now(a);
-  const int tile = a.order ? a.order[blockIdx.x] : (int)blockIdx.x;
+  const int tile = fwd_tile(a);
+  if (tile < 0) return;
   const int ntile = a.tw * a.th;
   const int c = tile / ntile;
   const int rem = tile - c * ntile;
@@ -1241,6 +1306,104 @@ tile_order_kernel(int n_tiles, const int32_t *__restrict__ offsets, int64_t n_is
   }
 }
 
+// XCD-aware forward dispatch order.  Tile t (raster order, cameras
+// concatenated) goes to segment min(7, 8 w(t) / W) with w(t) = offsets[t] +
+// kTileCost t the work before it (isects plus a per-tile cost) and W the
+// total, so the 8 segments are bands of the image with equal work.  Inside a
+// segment the tiles are bucketed as in tile_order_kernel (>= 2048, >= 1024,
+// >= 512 isects, the rest: heaviest first), raster order inside a bucket.
+// Output: order[] sorted by (segment, bucket, tile); queue[q] = start of
+// segment q, queue[8+q] = its length, its dequeue head = 0.
+// One 1024-lane workgroup, 16 consecutive tiles per lane (n_tiles <= 16384);
+// the 32 (segment, bucket) counts of a lane are packed 4 per u64 (16 bits).
+constexpr int kTileCost = 32;
+
+__global__ void __launch_bounds__(1024)
+order_xcd_kernel(int n_tiles, const int32_t *__restrict__ offsets, int64_t n_isects,
+                 int32_t *__restrict__ order, int32_t *__restrict__ queue) {
+  constexpr int PER = 16;
+  __shared__ uint64_t wsum[16][8];
+  __shared__ int base[32];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int64_t W = n_isects + (int64_t)kTileCost * n_tiles;
+  int key[PER];
+  uint64_t c[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) c[j] = 0;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int t = tid * PER + i;
+    key[i] = -1;
+    if (t < n_tiles) {
+      const int64_t o = offsets[t];
+      const int64_t e = (t == n_tiles - 1) ? n_isects : (int64_t)offsets[t + 1];
+      const int64_t n = e - o;
+      const int seg = (int)min((int64_t)7, (8 * (o + (int64_t)kTileCost * t)) / max(W, (int64_t)1));
+      const int bk = n >= 2048 ? 0 : n >= 1024 ? 1 : n >= 512 ? 2 : 3;
+      key[i] = 4 * seg + bk;
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        c[j] += (key[i] >> 2) == j ? (uint64_t)1 << (16 * (key[i] & 3)) : 0;
+    }
+  }
+  uint64_t x[8];  // inclusive lane scan of the packed counts
+#pragma unroll
+  for (int j = 0; j < 8; ++j) x[j] = c[j];
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint64_t y = __shfl_up(x[j], o, 64);
+      if (lane >= o) x[j] += y;
+    }
+  }
+  if (lane == 63) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) wsum[w][j] = x[j];
+  }
+  __syncthreads();
+  if (tid < 32) {  // exclusive scan over the 32 keys of the block totals
+    int tot = 0;
+    for (int k = 0; k < tid; ++k) {
+      uint64_t s = 0;
+      for (int ww = 0; ww < 16; ++ww) s += wsum[ww][k >> 2];
+      tot += (int)((s >> (16 * (k & 3))) & 0xffff);
+    }
+    base[tid] = tot;
+    if ((tid & 3) == 0) {  // segment q = tid / 4: start, length, head
+      uint64_t s = 0;
+      for (int ww = 0; ww < 16; ++ww) s += wsum[ww][tid >> 2];
+      int len = 0;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) len += (int)((s >> (16 * b)) & 0xffff);
+      queue[tid >> 2] = tot;
+      queue[8 + (tid >> 2)] = len;
+      queue[kHead + kHeadStride * (tid >> 2)] = 0;
+    }
+  }
+  __syncthreads();
+  uint64_t before[8];  // this lane's exclusive prefix: earlier waves + earlier lanes
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    uint64_t b = x[j] - c[j];
+    for (int ww = 0; ww < w; ++ww) b += wsum[ww][j];
+    before[j] = b;
+  }
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int k = key[i];
+    if (k >= 0) {
+      uint64_t word = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) word = (k >> 2) == j ? before[j] : word;
+      int p = base[k] + (int)((word >> (16 * (k & 3))) & 0xffff);
+#pragma unroll
+      for (int i2 = 0; i2 < i; ++i2) p += key[i2] == k;
+      order[p] = tid * PER + i;
+    }
+  }
+}
+
 // Backward work items.  A tile with n isects becomes ceil(n / L) items
 // (tile, k): the full-length chunks go to `full`, the shorter tails to `tail`
 // (the backward runs all full chunks first, so the longest items start
@@ -1279,7 +1442,59 @@ chunk_items_kernel(int n_tiles, const int32_t *__restrict__ offsets, int64_t n_i
   if (nt) tail[bt] = make_int2(t, nf);
 }
 
+// Render records (see kRecFloats): one thread per Gaussian; rows whose
+// `visible` count is 0 are never gathered and are skipped.
+template <int D>
+__global__ void __launch_bounds__(256)
+pack_records_kernel(int64_t G, const float *__restrict__ means2d, const float *__restrict__ conics,
+                    const float *__restrict__ colors, const float *__restrict__ opacities,
+                    const int32_t *__restrict__ visible, float *__restrict__ records) {
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= G || (visible && visible[g] <= 0)) return;
+  constexpr int N4 = (6 + D + 3) / 4;
+  float r[4 * N4];
+  const float2 xy = *reinterpret_cast<const float2 *>(means2d + 2 * g);
+  r[0] = xy.x;
+  r[1] = xy.y;
+  r[2] = conics[3 * g];
+  r[3] = conics[3 * g + 1];
+  r[4] = conics[3 * g + 2];
+  r[5] = opacities[g];
+#pragma unroll
+  for (int d = 0; d < D; ++d) r[6 + d] = colors[g * D + d];
+#pragma unroll
+  for (int d = 6 + D; d < 4 * N4; ++d) r[d] = 0.f;
+  float4 *o = reinterpret_cast<float4 *>(records + g * kRecFloats);
+#pragma unroll
+  for (int q = 0; q < N4; ++q) o[q] = make_float4(r[4 * q], r[4 * q + 1], r[4 * q + 2], r[4 * q + 3]);
+}
+
 }  // namespace r16
+
+int rasterize16_record_floats(int D) {
+  return (D >= 1 && D <= r16::kRecMaxD) ? r16::kRecFloats : 0;
+}
+
+int rasterize16_pack_records(int64_t G, int D, const float *means2d, const float *conics,
+                             const float *colors, const float *opacities, const int32_t *visible,
+                             float *records, hipStream_t st) {
+  GS_REQUIRE(rasterize16_record_floats(D) > 0, "rasterize_pack_records: %d channels > %d", D,
+             r16::kRecMaxD);
+  if (G <= 0) return 0;
+  const dim3 grid((unsigned)((G + 255) / 256));
+  switch (D) {
+#define GS_PACK(DD)                                                                              \
+  case DD:                                                                                       \
+    hipLaunchKernelGGL(r16::pack_records_kernel<DD>, grid, dim3(256), 0, st, G, means2d, conics, \
+                       colors, opacities, visible, records);                                    \
+    break;
+    GS_PACK(1) GS_PACK(2) GS_PACK(3) GS_PACK(4) GS_PACK(5) GS_PACK(6) GS_PACK(7) GS_PACK(8)
+    GS_PACK(9) GS_PACK(10)
+#undef GS_PACK
+  }
+  GS_CHECK_LAUNCH("rasterize_pack_records");
+  return 0;
+}
 
 // Chunk length in isects for the chunked backward (multiple of 64; 0 turns
 // chunking off).  GSPLAT_HIP_CHUNK overrides it for experiments.  256: at M2
@@ -1309,8 +1524,21 @@ static bool use_order(int n_tiles, int64_t n_isects) {
   return n_isects > 0 && n_tiles > 0 && n_tiles <= 16384;
 }
 
+// XCD-aware forward dispatch (order_xcd_kernel, GSPLAT_HIP_XCD=1); default:
+// the heaviest-first order of tile_order_kernel.  With render records the
+// XCD bands measured slower at M2 (fwd 0.30 vs 0.19 ms) and M3 (0.77 vs 0.61
+// ms): the records already cut the gather to one sector per isect, and the
+// per-band order starts the globally heaviest tiles later.
+static bool use_xcd() {
+  static const bool v = [] {
+    const char *e = getenv("GSPLAT_HIP_XCD");
+    return e && atoi(e) == 1;
+  }();
+  return v;
+}
+
 int64_t rasterize16_fwd_state_bytes(int D, int n_tiles, int64_t n_isects) {
-  const int64_t ob = use_order(n_tiles, n_isects) ? 4 * (int64_t)n_tiles : 0;
+  const int64_t ob = use_order(n_tiles, n_isects) ? 4 * ((int64_t)n_tiles + r16::kQueueInts) : 0;
   return chunk_slot_bytes(D, n_isects) + ob;
 }
 
@@ -1362,11 +1590,20 @@ static int dbg_flags() {
 // forward that consumes it.  Same host thread, same stream.
 static thread_local const void *g_prepared_state = nullptr;
 
+static void launch_order(int n_tiles, const int32_t *offsets, int64_t n_isects, int32_t *order,
+                         hipStream_t st) {
+  if (use_xcd())
+    hipLaunchKernelGGL(r16::order_xcd_kernel, dim3(1), dim3(1024), 0, st, n_tiles, offsets,
+                       n_isects, order, order + n_tiles);
+  else
+    hipLaunchKernelGGL(r16::tile_order_kernel, dim3(1), dim3(1024), 0, st, n_tiles, offsets,
+                       n_isects, order);
+}
+
 template <int D>
 int r16_fwd(r16::Args a, const void *state, hipStream_t st) {
   if (a.order && state != g_prepared_state)
-    hipLaunchKernelGGL(r16::tile_order_kernel, dim3(1), dim3(1024), 0, st, a.n_tiles, a.offsets,
-                       a.n_isects, const_cast<int32_t *>(a.order));
+    launch_order(a.n_tiles, a.offsets, a.n_isects, const_cast<int32_t *>(a.order), st);
   g_prepared_state = nullptr;
   if (fwd_px() == 2)
     hipLaunchKernelGGL((r16::fwd2_kernel<D>), dim3(a.n_tiles), dim3(128), 0, st, a);
@@ -1431,9 +1668,10 @@ int rasterize16_fwd(int C, int D, int W, int H, int tw, int th, const float *mea
                     const float *conics, const float *colors, const float *opacities,
                     const float *backgrounds, const uint8_t *masks, const int32_t *offsets,
                     int64_t n_isects, const int32_t *flatten_ids, float *render_colors,
-                    float *render_alphas, int32_t *last_ids, void *state, int64_t state_bytes,
-                    hipStream_t st) {
+                    float *render_alphas, int32_t *last_ids, const float *records, void *state,
+                    int64_t state_bytes, hipStream_t st) {
   r16::Args a{};
+  a.records = rasterize16_record_floats(D) ? records : nullptr;
   a.C = C; a.W = W; a.H = H; a.tw = tw; a.th = th; a.n_tiles = C * tw * th;
   a.n_isects = n_isects;
   a.timeline = (g_timeline && g_timeline_waves >= 4 * (int64_t)a.n_tiles) ? g_timeline : nullptr;
@@ -1450,6 +1688,7 @@ int rasterize16_fwd(int C, int D, int W, int H, int tw, int th, const float *mea
   a.state = (state && slots > 0) ? reinterpret_cast<float *>(state) : nullptr;
   a.order = (state && use_order(a.n_tiles, n_isects))
                 ? reinterpret_cast<int32_t *>(reinterpret_cast<char *>(state) + slots) : nullptr;
+  a.queue = (a.order && use_xcd()) ? const_cast<int32_t *>(a.order) + a.n_tiles : nullptr;
   switch (D) {
     case 1: return r16_fwd<1>(a, state, st);
     case 2: return r16_fwd<2>(a, state, st);
@@ -1470,8 +1709,7 @@ int rasterize16_prepare(int D, int n_tiles, const int32_t *offsets, int64_t n_is
              "rasterize_prepare: state too small");
   int32_t *order = reinterpret_cast<int32_t *>(reinterpret_cast<char *>(state) +
                                                chunk_slot_bytes(D, n_isects));
-  hipLaunchKernelGGL(r16::tile_order_kernel, dim3(1), dim3(1024), 0, st, n_tiles, offsets,
-                     n_isects, order);
+  launch_order(n_tiles, offsets, n_isects, order, st);
   GS_CHECK_LAUNCH("rasterize_prepare");
   g_prepared_state = state;
   return 0;
@@ -1490,9 +1728,10 @@ int rasterize16_bwd(int C, int64_t G, int D, int W, int H, int tw, int th,
                     const float *render_alphas, const int32_t *last_ids,
                     const float *v_render_colors, const float *v_render_alphas,
                     float *v_means2d, float *v_conics, float *v_colors, float *v_opacities,
-                    float *v_abs, const float *render_colors, const void *state,
-                    int64_t state_bytes, void *workspace, hipStream_t st) {
+                    float *v_abs, const float *render_colors, const float *records,
+                    const void *state, int64_t state_bytes, void *workspace, hipStream_t st) {
   r16::Args a{};
+  a.records = rasterize16_record_floats(D) ? records : nullptr;
   a.C = C; a.W = W; a.H = H; a.tw = tw; a.th = th; a.n_tiles = C * tw * th;
   a.n_isects = n_isects;
   a.timeline = (g_timeline && g_timeline_waves >= 4 * n_items_bound(a.n_tiles, n_isects))

@@ -12,7 +12,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GSPLAT_HIP_LIB", os.path.join(_HERE, "libgsplat_hip.so"))
-ABI_VERSION = 14
+ABI_VERSION = 15
 
 _p = ctypes.c_void_p
 _i32 = ctypes.c_int
@@ -49,13 +49,15 @@ _SIGS = {
     "gsplat_hip_rasterize_supported_channels": (_i32, [_i32]),
     "gsplat_hip_rasterize_fwd_state_bytes": (_i64, [_i32, _i32, _i32, _i32, _i32, _i64]),
     "gsplat_hip_rasterize_prepare": (_i32, [_i32, _i32, _i32, _i32, _i32, _p, _i64, _p, _i64, _p]),
+    "gsplat_hip_rasterize_record_floats": (_i32, [_i32, _i32]),
+    "gsplat_hip_rasterize_pack_records": (_i32, [_i64, _i32, _p, _p, _p, _p, _p, _p, _p]),
     "gsplat_hip_rasterize_fwd": (_i32, [_i32, _i32, _i32, _i32, _i32, _i32, _i32, _p, _p, _p, _p,
-                                        _p, _p, _p, _i64, _p, _p, _p, _p, _p, _i64, _p]),
+                                        _p, _p, _p, _i64, _p, _p, _p, _p, _p, _p, _i64, _p]),
     "gsplat_hip_rasterize_bwd_workspace_bytes": (_i64, [_i64, _i32, _i32, _i32, _i32, _i32, _i32,
                                                         _i64]),
     "gsplat_hip_rasterize_bwd": (_i32, [_i32, _i64, _i32, _i32, _i32, _i32, _i32, _i32, _p, _p,
                                         _p, _p, _p, _p, _p, _i64, _p, _p, _p, _p, _p, _p, _p,
-                                        _p, _p, _p, _p, _p, _i64, _p, _i64, _p]),
+                                        _p, _p, _p, _p, _p, _p, _i64, _p, _i64, _p]),
     "gsplat_hip_debug_set_timeline": (_i32, [_p, _i64]),
     "gsplat_hip_debug_set_lane_histogram": (_i32, [_p]),
     "gsplat_hip_debug_set_chunk": (_i32, [_i32]),

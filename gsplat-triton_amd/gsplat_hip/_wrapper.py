@@ -288,6 +288,9 @@ def fully_fused_projection(
 #   "depth_first" depth sort of the visible Gaussians + stable (camera, tile) sort
 #   "full"        the reference's single 64-bit key sort
 ISECT_SORT = os.environ.get("GSPLAT_HIP_ISECT_SORT", "depth_first")
+# 16x16 rasterizer gathers from packed 64-B render records (GSPLAT_HIP_RECORDS=0:
+# from the four attribute arrays, as before ABI 15)
+RECORDS = os.environ.get("GSPLAT_HIP_RECORDS", "1") != "0"
 
 
 @torch.no_grad()
@@ -594,7 +597,7 @@ class _RasterizeToPixels(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, means2d, conics, colors, opacities, backgrounds, masks, width, height,
-                tile_size, isect_offsets, flatten_ids, absgrad, block_size=8):
+                tile_size, isect_offsets, flatten_ids, absgrad, block_size=8, visible=None):
         ctx.means2d_in = means2d if absgrad else None  # receives .absgrad (_wrapper.py:156)
         ctx.set_materialize_grads(False)  # alphas without a loss: None, not zeros
         means2d, conics, colors, opacities, backgrounds = (
@@ -614,6 +617,15 @@ class _RasterizeToPixels(torch.autograd.Function):
         sb = int(_lib.query("gsplat_hip_rasterize_fwd_state_bytes", C, D, tile_size, tw, th,
                             flatten_ids.numel()))
         state = torch.empty(sb // 4, dtype=torch.float32, device=dev)
+        # one 64-B render record per Gaussian for the 16x16 kernels' gathers
+        # (only the rows `visible` marks are referenced by flatten_ids)
+        rf = int(_lib.query("gsplat_hip_rasterize_record_floats", D, tile_size)) if RECORDS else 0
+        records = torch.empty(opacities.numel() * rf if rf else 0, dtype=torch.float32, device=dev)
+        if rf:
+            vis = None if visible is None else visible.to(torch.int32).contiguous()
+            _lib.call("gsplat_hip_rasterize_pack_records", opacities.numel(), D, _ptr(means2d),
+                      _ptr(conics), _ptr(colors), _ptr(opacities), _ptr(vis), _ptr(records),
+                      _stream())
         if sb:  # dispatch order into the state, outside the timed rasterizer launch
             _lib.call("gsplat_hip_rasterize_prepare", C, D, tile_size, tw, th, _ptr(isect_offsets),
                       flatten_ids.numel(), _ptr(state), sb, _stream())
@@ -622,16 +634,17 @@ class _RasterizeToPixels(torch.autograd.Function):
                       _ptr(means2d), _ptr(conics), _ptr(colors), _ptr(opacities),
                       _ptr(backgrounds), _ptr(m), _ptr(isect_offsets), flatten_ids.numel(),
                       _ptr(flatten_ids), _ptr(render_colors), _ptr(render_alphas),
-                      _ptr(last_ids), _ptr(state) if sb else 0, sb, _stream())
+                      _ptr(last_ids), _ptr(records) if rf else 0, _ptr(state) if sb else 0, sb,
+                      _stream())
         ctx.save_for_backward(means2d, conics, colors, opacities, backgrounds, m, isect_offsets,
-                              flatten_ids, render_alphas, last_ids, render_colors, state)
+                              flatten_ids, render_alphas, last_ids, render_colors, state, records)
         ctx.width, ctx.height, ctx.tile_size, ctx.absgrad = width, height, tile_size, absgrad
         return render_colors, render_alphas
 
     @staticmethod
     def backward(ctx, v_render_colors, v_render_alphas):
         (means2d, conics, colors, opacities, backgrounds, m, isect_offsets, flatten_ids,
-         render_alphas, last_ids, render_colors, state) = ctx.saved_tensors
+         render_alphas, last_ids, render_colors, state, records) = ctx.saved_tensors
         C, th, tw = isect_offsets.shape
         D = colors.shape[-1]
         G = opacities.numel()
@@ -654,15 +667,16 @@ class _RasterizeToPixels(torch.autograd.Function):
                       _ptr(flatten_ids), _ptr(render_alphas), _ptr(last_ids),
                       _ptr(v_render_colors), _ptr(v_render_alphas), _ptr(v_means2d),
                       _ptr(v_conics), _ptr(v_colors), _ptr(v_opacities), _ptr(v_abs),
-                      _ptr(render_colors), _ptr(state) if state.numel() else 0, state.numel() * 4,
-                      _ptr(ws), wsb, _stream())
+                      _ptr(render_colors), _ptr(records) if records.numel() else 0,
+                      _ptr(state) if state.numel() else 0, state.numel() * 4, _ptr(ws), wsb,
+                      _stream())
         if ctx.absgrad:
             ctx.means2d_in.absgrad = v_abs
         v_backgrounds = None
         if ctx.needs_input_grad[4]:
             v_backgrounds = (v_render_colors * (1.0 - render_alphas)).sum(dim=(1, 2))
         return (v_means2d, v_conics, v_colors, v_opacities, v_backgrounds,
-                None, None, None, None, None, None, None, None)
+                None, None, None, None, None, None, None, None, None)
 
 
 def rasterize_to_pixels(
@@ -686,6 +700,16 @@ def rasterize_to_pixels(
     Returns render_colors [C,H,W,channels] and render_alphas [C,H,W,1].
     Channel counts outside {1,2,3,4,8,16,32} are zero-padded to the next one;
     above 32 they are rendered in chunks of 32."""
+    return _rasterize_to_pixels(means2d, conics, colors, opacities, image_width, image_height,
+                                tile_size, isect_offsets, flatten_ids, backgrounds, masks, packed,
+                                absgrad, block_size)
+
+
+def _rasterize_to_pixels(means2d, conics, colors, opacities, image_width, image_height, tile_size,
+                         isect_offsets, flatten_ids, backgrounds=None, masks=None, packed=False,
+                         absgrad=False, block_size=8, visible=None):
+    """rasterize_to_pixels with rasterization()'s private hint `visible`
+    ([C,N] tiles_per_gauss): only those Gaussians' render records are packed."""
     C = isect_offsets.size(0)
     device = means2d.device
     if packed:
@@ -723,7 +747,7 @@ def rasterize_to_pixels(
                 bgs = torch.cat([bgs, torch.zeros(*bgs.shape[:-1], Dp - D, device=device)], -1)
         rc, ra = _RasterizeToPixels.apply(means2d, conics, cols, opacities, bgs, masks,
                                           image_width, image_height, tile_size, isect_offsets,
-                                          flatten_ids, absgrad, block_size)
+                                          flatten_ids, absgrad, block_size, visible)
         return (rc[..., :D] if Dp != D else rc), ra
 
     if channels <= 32:

@@ -24,6 +24,7 @@ from ._wrapper import (
     fully_fused_projection,
     isect_offset_encode,
     isect_tiles_begin,
+    _rasterize_to_pixels,
     rasterize_to_pixels,
     sh_colors,
     spherical_harmonics,
@@ -253,24 +254,26 @@ def rasterization(
                  "flatten_ids": flatten_ids, "isect_offsets": isect_offsets, "width": width,
                  "height": height, "tile_size": tile_size, "n_cameras": C})
 
+    # only Gaussians with a tile are gathered: pack just their render records
+    visible = None if packed else tiles_per_gauss
     if colors.shape[-1] > channel_chunk:
         n_chunks = (colors.shape[-1] + channel_chunk - 1) // channel_chunk
         render_colors, render_alphas = [], []
         for i in range(n_chunks):
             sl = slice(i * channel_chunk, (i + 1) * channel_chunk)
-            rc, ra = rasterize_to_pixels(
+            rc, ra = _rasterize_to_pixels(
                 means2d, conics, colors[..., sl], opacities, width, height, tile_size,
                 isect_offsets, flatten_ids,
                 backgrounds=None if backgrounds is None else backgrounds[..., sl],
-                packed=packed, absgrad=absgrad)
+                packed=packed, absgrad=absgrad, visible=visible)
             render_colors.append(rc)
             render_alphas.append(ra)
         render_colors = torch.cat(render_colors, dim=-1)
         render_alphas = render_alphas[0]
     else:
-        render_colors, render_alphas = rasterize_to_pixels(
+        render_colors, render_alphas = _rasterize_to_pixels(
             means2d, conics, colors, opacities, width, height, tile_size, isect_offsets,
-            flatten_ids, backgrounds=backgrounds, packed=packed, absgrad=absgrad)
+            flatten_ids, backgrounds=backgrounds, packed=packed, absgrad=absgrad, visible=visible)
     if render_mode in ["ED", "RGB+ED"]:
         render_colors = torch.cat(
             [render_colors[..., :-1],

@@ -189,14 +189,28 @@ int gsplat_hip_rasterize_prepare(int C, int D, int tile_size, int tile_width, in
                                  int64_t state_bytes, void *stream);
 int64_t gsplat_hip_rasterize_fwd_state_bytes(int C, int D, int tile_size, int tile_width,
                                              int tile_height, int64_t n_isects);
+/* Optional render records (16x16 tiles, D <= 10): one 64-B row per Gaussian
+ * [x, y, conic(3), opacity, colour(D), pad] packed from the four attribute
+ * arrays, so that the rasterizer's per-isect gather (the four separate loads
+ * of rasterize_to_pixels_fwd.py:93-145 / rasterize_to_pixels_bwd.py:110-125)
+ * reads one 64-B sector.  record_floats: floats per row (16), 0 when the
+ * configuration has no record path.  pack_records writes records f32[G][16];
+ * rows with visible[g] <= 0 (e.g. tiles_per_gauss; NULL = all rows) are never
+ * gathered and are left unwritten.  Pass the same records (or NULL for the
+ * plain gathers) to gsplat_hip_rasterize_fwd and _bwd. */
+int gsplat_hip_rasterize_record_floats(int D, int tile_size);
+int gsplat_hip_rasterize_pack_records(int64_t n_gaussians, int D, const float *means2d,
+                                      const float *conics, const float *colors,
+                                      const float *opacities, const int32_t *visible,
+                                      float *records, void *stream);
 int gsplat_hip_rasterize_fwd(int C, int D, int width, int height, int tile_size, int tile_width,
                              int tile_height, const float *means2d, const float *conics,
                              const float *colors, const float *opacities,
                              const float *backgrounds, const uint8_t *masks,
                              const int32_t *isect_offsets, int64_t n_isects,
                              const int32_t *flatten_ids, float *render_colors,
-                             float *render_alphas, int32_t *last_ids, void *state,
-                             int64_t state_bytes, void *stream);
+                             float *render_alphas, int32_t *last_ids, const float *records,
+                             void *state, int64_t state_bytes, void *stream);
 
 /* Replaces rasterize_to_pixels_bwd() (gsplat/triton_impl/rasterize_to_pixels_bwd.py:340-457)
  * called from _RasterizeToPixels.backward (_wrapper.py:104-182).
@@ -220,9 +234,9 @@ int gsplat_hip_rasterize_bwd(int C, int64_t n_gaussians, int D, int width, int h
                              const float *v_render_colors, const float *v_render_alphas,
                              float *v_means2d, float *v_conics, float *v_colors,
                              float *v_opacities, float *v_means2d_abs,
-                             const float *render_colors, const void *state,
-                             int64_t state_bytes, void *workspace, int64_t workspace_bytes,
-                             void *stream);
+                             const float *render_colors, const float *records,
+                             const void *state, int64_t state_bytes, void *workspace,
+                             int64_t workspace_bytes, void *stream);
 
 /* Debug/profiling: when device_buffer (u64[2*capacity_waves]) is non-NULL, the
  * 16x16 rasterizer kernels store each wave's (start, end) s_memrealtime stamps

@@ -1,0 +1,117 @@
+"""GPU: the 16x16 rasterizer's data layout and dispatch choices change speed
+only, never results.
+
+* render records (gsplat_hip_rasterize_pack_records, ABI 15): the forward
+  through the packed 64-B records is bit-identical to the forward gathering
+  the four attribute arrays (the same floats reach the same arithmetic), and
+  the backward agrees up to the order of its float atomics;
+* XCD-aware dispatch (order_xcd_kernel): the order is a permutation of the
+  tiles, its 8 segments are consecutive raster ranges holding about 1/8 of the
+  work each, heaviest bucket first inside a segment, raster order inside a
+  bucket, and the dequeue heads start at 0.
+"""
+
+import math
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _scene(N=20000, W=640, H=480, seed=3):
+    g = torch.Generator().manual_seed(seed)
+    means = torch.randn(N, 3, generator=g) * torch.tensor([1.6, 1.2, 0.6])
+    means[:, 2] += 4.0
+    quats = torch.randn(N, 4, generator=g)
+    scales = torch.rand(N, 3, generator=g) * 0.08 + 0.004
+    opac = torch.rand(N, generator=g)
+    colors = torch.rand(N, 3, generator=g)
+    vm = torch.eye(4)[None]
+    K = torch.tensor([[500.0, 0, W / 2], [0, 500.0, H / 2], [0, 0, 1]])[None]
+    return [x.to(DEV) for x in (means, quats, scales, opac, colors, vm, K)], W, H
+
+
+def _render(ins, W, H, records, mode="RGB"):
+    import gsplat_hip
+    from gsplat_hip import _wrapper
+    saved = _wrapper.RECORDS
+    _wrapper.RECORDS = records
+    try:
+        leaves = [x.clone().requires_grad_(True) for x in ins[:5]]
+        rc, ra, meta = gsplat_hip.rasterization(*leaves, ins[5], ins[6], W, H, packed=False,
+                                                render_mode=mode)
+        g = torch.Generator(device=DEV).manual_seed(1)
+        w = torch.rand(rc.shape, generator=g, device=DEV)
+        (rc * w).sum().backward()
+        torch.cuda.synchronize()
+        return rc.detach(), ra.detach(), meta, [x.grad for x in leaves]
+    finally:
+        _wrapper.RECORDS = saved
+
+
+@pytest.mark.parametrize("mode", ["RGB", "RGB+D"])
+def test_records_match_plain_gathers(mode):
+    ins, W, H = _scene()
+    rc0, ra0, m0, g0 = _render(ins, W, H, False, mode)
+    rc1, ra1, m1, g1 = _render(ins, W, H, True, mode)
+    assert m0["flatten_ids"].numel() > 50000
+    assert torch.equal(rc0, rc1) and torch.equal(ra0, ra1)
+    for a, b, name in zip(g0, g1, ["means", "quats", "scales", "opacities", "colors"]):
+        scale = b.abs().max().item()
+        err = (a - b).abs().max().item()
+        assert err <= 1e-5 * scale + 1e-9, (name, err, scale)
+
+
+def test_xcd_order_is_banded_permutation():
+    if os.environ.get("GSPLAT_HIP_XCD") != "1":
+        pytest.skip("XCD-aware dispatch is off (GSPLAT_HIP_XCD=1 turns it on)")
+    from gsplat_hip import _lib
+    from gsplat_hip._wrapper import _ptr, _stream
+    import gsplat_hip
+    ins, W, H = _scene(N=60000, W=1280, H=720)
+    with torch.no_grad():
+        _, _, meta = gsplat_hip.rasterization(*ins[:5], ins[5], ins[6], W, H, packed=False)
+    offs = meta["isect_offsets"].contiguous()
+    n = meta["flatten_ids"].numel()
+    C, th, tw = offs.shape
+    nt = C * th * tw
+    D = 3
+    sb = int(_lib.query("gsplat_hip_rasterize_fwd_state_bytes", C, D, 16, tw, th, n))
+    state = torch.full((sb // 4,), -7, dtype=torch.int32, device=DEV)
+    _lib.call("gsplat_hip_rasterize_prepare", C, D, 16, tw, th, _ptr(offs), n, _ptr(state), sb,
+              _stream())
+    torch.cuda.synchronize()
+    QI = 32 + 8 * 32  # starts[8], lens[8], pad, then one 128-B line per dequeue head
+    tail = state[-(nt + QI):].cpu().numpy()
+    order, queue = tail[:nt], tail[nt:]
+    assert np.array_equal(np.sort(order), np.arange(nt)), "not a permutation"
+    starts, lens, heads = queue[:8], queue[8:16], queue[32::32]
+    assert np.all(heads == 0)
+    assert lens.sum() == nt and np.array_equal(starts, np.concatenate([[0], np.cumsum(lens)[:-1]]))
+    o = offs.flatten().cpu().numpy().astype(np.int64)
+    cnt = np.diff(np.concatenate([o, [n]]))
+    work = cnt + 32
+    seg_work = []
+    prev_hi = -1
+    for q in range(8):
+        tiles = order[starts[q]:starts[q] + lens[q]]
+        if tiles.size == 0:
+            seg_work.append(0)
+            continue
+        lo, hi = tiles.min(), tiles.max()
+        assert lo == prev_hi + 1 and hi - lo + 1 == tiles.size, f"segment {q} not a raster range"
+        prev_hi = hi
+        b = np.where(cnt[tiles] >= 2048, 0, np.where(cnt[tiles] >= 1024, 1,
+                                                      np.where(cnt[tiles] >= 512, 2, 3)))
+        assert np.all(np.diff(b) >= 0), f"segment {q}: buckets not heaviest first"
+        for bk in range(4):
+            tb = tiles[b == bk]
+            assert np.all(np.diff(tb) > 0), f"segment {q} bucket {bk}: not raster order"
+        seg_work.append(work[tiles].sum())
+    seg_work = np.array(seg_work, dtype=np.float64)
+    # bands of equal work up to one tile's work
+    assert np.all(np.abs(seg_work - work.sum() / 8) <= work.max() + 1), seg_work
