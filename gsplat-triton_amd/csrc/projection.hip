@@ -487,6 +487,13 @@ extern "C" int gsplat_hip_projection_bwd(
   return 0;
 }
 
+namespace gs {
+// the packed-count scan, shared with the 2DGS packed projection (surfel.hip)
+void launch_packed_scan(int64_t nb, int64_t *cnt, int64_t *total, hipStream_t st) {
+  hipLaunchKernelGGL(packed_scan_kernel, dim3(1), dim3(1024), 0, st, nb, cnt, total);
+}
+}  // namespace gs
+
 // ------------------------------------------------------------------ packed --
 // projection_ewa_3dgs_packed_fwd (gsplat/cuda/csrc/ProjectionEWA3DGSPacked.cu:17-244):
 // a counting pass, a scan of the per-block counts, and a pass that recomputes

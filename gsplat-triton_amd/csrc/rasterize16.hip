@@ -381,15 +381,14 @@ GS_INLINE void stage_fwd_pair(float4 *st, int slot, const Attr<D> &at, int32_t i
   for (int d = 0; d < D; ++d) w[16 + 2 * d] = at.col[d];
 }
 
-// The odd slot of a final half-filled pair: x = NaN never hits.
+// A pad slot (the odd slot of a final half-filled pair, or a whole padding
+// pair): x = NaN never hits, and opacity = colour = 0 add nothing.
 template <int D>
 GS_INLINE void stage_fwd_pad(float4 *st, int slot) {
   float *w = reinterpret_cast<float *>(st + (slot >> 1) * FwdPair<D>::N4) + (slot & 1);
   w[0] = __int_as_float(0x7fc00000);
-  w[12] = 0.f;
 #pragma unroll
-  for (int f = 1; f < FwdPair<D>::NFP; ++f)
-    if (f != 6) w[2 * f] = 0.f;
+  for (int f = 1; f < FwdPair<D>::NFP; ++f) w[2 * f] = 0.f;
 }
 
 // Backward records, staged in pairs like the forward's.  Fields: x, y,
@@ -429,13 +428,18 @@ GS_INLINE void stage_bwd_pad(float4 *st, int slot) {
     if (f != 6 && f != 8) w[2 * f] = 0.f;
 }
 
-// U: the pair loop unrolled U times (pair p+1's alpha math can issue under
-// pair p's blend chain); register budget 80 VGPRs = 6 waves per SIMD for
-// U = 1, 96 / 5 for U = 2, 128 / 4 for U = 4 (uses 92: 5 waves).  At M2:
-// 0.216 ms (U = 1), 0.207-0.209 (2), 0.205 (4, default).
-template <int D, int U = 4>
+// U: pairs per iteration of the composite loop (explicitly unrolled: their
+// LDS reads issue together and pair p+1's alpha math issues under pair p's
+// blend chain); register budget 80 VGPRs = 6 waves per SIMD for U = 1,
+// 96 / 5 for U = 2, 128 / 4 for U = 4.
+// PF: gather depth.  1: the attributes of batch b+1 are gathered while batch
+// b composites (two register buffers); 2: those of b+1 and b+2 (three
+// buffers, one wave per SIMD fewer); 0: only the flatten ids are prefetched,
+// the gather waits at the batch start, and 18 fewer VGPRs allow two more
+// waves.  At M2 / M3: PF 0 0.198 / 0.686 ms, PF 1 0.184-0.193 / 0.590.
+template <int D, int U = 1, int PF = 1>
 __global__ void __launch_bounds__(256)
-__attribute__((amdgpu_waves_per_eu(U == 1 ? 6 : U == 2 ? 5 : 4))) fwd_kernel(Args a) {
+__attribute__((amdgpu_waves_per_eu((U == 1 ? 5 : U == 2 ? 4 : 3) + (PF == 0 ? 2 : PF == 2 ? -1 : 0)))) fwd_kernel(Args a) {
   using P = FwdPair<D>;
   constexpr int N4 = P::N4;
   __shared__ float4 stage_all[4][32 * N4];
@@ -488,36 +492,47 @@ __attribute__((amdgpu_waves_per_eu(U == 1 ? 6 : U == 2 ? 5 : 4))) fwd_kernel(Arg
       last = ok ? __float_as_int(idx) : last;
       return vis;
     };
-    // composite one staged batch (cnt records = (cnt+1)/2 pairs), checking
-    // every 8 pairs whether the strip is still alive
+    // composite one staged batch: its pairs, padded to a multiple of U with
+    // never-hitting pairs (stage), U pairs per iteration -- all their LDS
+    // reads issue first and U independent alpha computations overlap the
+    // serial blend chain -- checking every 8 pairs whether the strip is alive
     auto composite = [&](int cnt) {
-      const int np = (cnt + 1) >> 1;
+      const int np = (((cnt + 1) >> 1) + U - 1) / U * U;
       for (int pb = 0; pb < np; pb += 8) {
         const int pe = min(np, pb + 8);
-#pragma unroll(U)
-        for (int p = pb; p < pe; ++p) {
-          const float4 *q = st + p * N4;
-          f2v f[2 * N4];
-          float4 v[N4];
+        for (int p = pb; p < pe; p += U) {
+          f2v f[U][2 * N4];
+          float4 v[U][N4];
 #pragma unroll
-          for (int i = 0; i < N4; ++i) v[i] = q[i];
+          for (int u = 0; u < U; ++u)
 #pragma unroll
-          for (int i = 0; i < N4; ++i) {
-            // keep every field live: no load may sink into a select's branch
-            asm volatile("" ::"v"(v[i].x), "v"(v[i].y), "v"(v[i].z), "v"(v[i].w));
-            f[2 * i] = f2v{v[i].x, v[i].y};
-            f[2 * i + 1] = f2v{v[i].z, v[i].w};
+            for (int i = 0; i < N4; ++i) v[u][i] = st[(p + u) * N4 + i];
+#pragma unroll
+          for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int i = 0; i < N4; ++i) {
+              // keep every field live: no load may sink into a select's branch
+              asm volatile("" ::"v"(v[u][i].x), "v"(v[u][i].y), "v"(v[u][i].z), "v"(v[u][i].w));
+              f[u][2 * i] = f2v{v[u][i].x, v[u][i].y};
+              f[u][2 * i + 1] = f2v{v[u][i].z, v[u][i].w};
+            }
+          f2v s2[U], al[U];
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            const f2v dx = f[u][0] - fx, dy = f[u][1] - fy;
+            s2[u] = dx * (f[u][2] * dx + f[u][3] * dy) + f[u][4] * dy * dy;  // sigma * log2(e)
+            al[u] = f[u][5] * f2v{__builtin_amdgcn_exp2f(-s2[u].x), __builtin_amdgcn_exp2f(-s2[u].y)};
+            al[u].x = fminf(al[u].x, kAlphaMax);
+            al[u].y = fminf(al[u].y, kAlphaMax);
           }
-          const f2v dx = f[0] - fx, dy = f[1] - fy;
-          const f2v s2 = dx * (f[2] * dx + f[3] * dy) + f[4] * dy * dy;  // sigma * log2(e)
-          f2v al = f[5] * f2v{__builtin_amdgcn_exp2f(-s2.x), __builtin_amdgcn_exp2f(-s2.y)};
-          al.x = fminf(al.x, kAlphaMax);
-          al.y = fminf(al.y, kAlphaMax);
-          const float v0 = blend(s2.x, f[6].x, al.x, f[7].x);
-          const float v1 = blend(s2.y, f[6].y, al.y, f[7].y);
-          const f2v vis = f2v{v0, v1};
 #pragma unroll
-          for (int d = 0; d < D; ++d) acc[d] = __builtin_elementwise_fma(vis, f[8 + d], acc[d]);
+          for (int u = 0; u < U; ++u) {
+            const float v0 = blend(s2[u].x, f[u][6].x, al[u].x, f[u][7].x);
+            const float v1 = blend(s2[u].y, f[u][6].y, al[u].y, f[u][7].y);
+            const f2v vis = f2v{v0, v1};
+#pragma unroll
+            for (int d = 0; d < D; ++d) acc[d] = __builtin_elementwise_fma(vis, f[u][8 + d], acc[d]);
+          }
         }
         if (__ballot(T > 0.f) == 0) {
           done = true;
@@ -530,7 +545,9 @@ __attribute__((amdgpu_waves_per_eu(U == 1 ? 6 : U == 2 ? 5 : 4))) fwd_kernel(Arg
       const uint64_t m = __ballot(keep);
       const int cnt = __popcll(m);
       if (keep) stage_fwd_pair<D>(st, ballot_slot(m), at, (int32_t)(b0 + lane));
-      if ((cnt & 1) && lane == 0) stage_fwd_pad<D>(st, cnt);
+      // pad slots up to a multiple of 2U records (<= 64: U divides 32)
+      const int npad = ((cnt + 2 * U - 1) / (2 * U)) * (2 * U) - cnt;
+      if (lane < npad) stage_fwd_pad<D>(st, cnt + lane);
       wave_sync_lds();
       return cnt;
     };
@@ -560,13 +577,50 @@ __attribute__((amdgpu_waves_per_eu(U == 1 ? 6 : U == 2 ? 5 : 4))) fwd_kernel(Arg
       slot(bidx)[pix_in_tile] = T;
     };
     const bool chunked = a.state && L > 0 && end - start > L;
+    int64_t b0 = start;
+    if constexpr (PF == 0) {
+      int32_t g_n = id_at(start);
+      while (b0 < end) {
+        if (__ballot(T > 0.f) == 0) break;
+        if (chunked && b0 > start && (b0 - start) % L == 0) save_state(b0);
+        Attr<D> A;
+        load_attr<D>(a, g_n, A);
+        g_n = id_at(b0 + 64);
+        composite(stage(A, b0));
+        wave_sync_lds();
+        b0 += 64;
+        if (done) break;
+      }
+    }
     // two attribute buffers in alternation: while batch b is composited from
     // one, the other receives batch b+1, and the ids of batch b+2 load
+    if constexpr (PF == 2) {
+      // three buffers in rotation: batch b composites while b+1 and b+2 are
+      // in flight and the ids of b+3 load
+      Attr<D> A, B, C;
+      load_attr<D>(a, id_at(start), A);
+      load_attr<D>(a, id_at(start + 64), B);
+      int32_t g_n = id_at(start + 128);
+      auto step = [&](const Attr<D> &cur, Attr<D> &fill) -> bool {  // false: stop
+        if (__ballot(T > 0.f) == 0) return false;
+        if (chunked && b0 > start && (b0 - start) % L == 0) save_state(b0);
+        load_attr<D>(a, g_n, fill);
+        g_n = id_at(b0 + 192);
+        composite(stage(cur, b0));
+        wave_sync_lds();
+        b0 += 64;
+        return !done && b0 < end;
+      };
+      while (step(A, C) && step(B, A) && step(C, B)) {
+      }
+    }
     Attr<D> A, B;
-    load_attr<D>(a, id_at(start), A);
-    int32_t g_n = id_at(start + 64);
-    int64_t b0 = start;
-    while (b0 < end) {
+    int32_t g_n = 0;
+    if constexpr (PF == 1) {
+      load_attr<D>(a, id_at(start), A);
+      g_n = id_at(start + 64);
+    }
+    while (PF == 1 && b0 < end) {
       if (__ballot(T > 0.f) == 0) break;
       if (chunked && b0 > start && (b0 - start) % L == 0) save_state(b0);
       load_attr<D>(a, g_n, B);
@@ -1575,8 +1629,18 @@ static int fwd_px() {
 static int fwd_unroll() {
   static const int v = [] {
     const char *e = getenv("GSPLAT_HIP_FWD_UNROLL");
-    const int x = e ? atoi(e) : 4;
-    return (x == 1 || x == 2) ? x : 4;
+    const int x = e ? atoi(e) : 1;
+    return (x == 2 || x == 4) ? x : 1;
+  }();
+  return v;
+}
+
+// Gather depth of the forward (GSPLAT_HIP_FWD_PF = 0, 1, 2; see fwd_kernel).
+static int fwd_pf() {
+  static const int v = [] {
+    const char *e = getenv("GSPLAT_HIP_FWD_PF");
+    const int x = e ? atoi(e) : 1;
+    return (x == 0 || x == 2) ? x : 1;
   }();
   return v;
 }
@@ -1607,6 +1671,10 @@ int r16_fwd(r16::Args a, const void *state, hipStream_t st) {
   g_prepared_state = nullptr;
   if (fwd_px() == 2)
     hipLaunchKernelGGL((r16::fwd2_kernel<D>), dim3(a.n_tiles), dim3(128), 0, st, a);
+  else if (fwd_unroll() == 1 && fwd_pf() == 0)
+    hipLaunchKernelGGL((r16::fwd_kernel<D, 1, 0>), dim3(a.n_tiles), dim3(256), 0, st, a);
+  else if (fwd_unroll() == 1 && fwd_pf() == 2)
+    hipLaunchKernelGGL((r16::fwd_kernel<D, 1, 2>), dim3(a.n_tiles), dim3(256), 0, st, a);
   else if (fwd_unroll() == 1)
     hipLaunchKernelGGL((r16::fwd_kernel<D, 1>), dim3(a.n_tiles), dim3(256), 0, st, a);
   else if (fwd_unroll() == 2)

@@ -44,6 +44,12 @@ struct ProjFwdArgs {
   const float *means, *quats, *scales, *viewmats, *Ks;
   int32_t *radii;
   float *means2d, *depths, *ray_transforms, *normals;
+  // packed mode (projection_2dgs_packed_fwd, Projection2DGSPacked.cu:17-205):
+  // per-block counts of kept (camera, surfel) pairs, then their exclusive
+  // prefix, in (c, n) order
+  int64_t *block_cnt;
+  const int64_t *block_off;
+  int64_t *camera_ids, *gaussian_ids;
 };
 
 struct Cam {
@@ -95,16 +101,21 @@ GS_INLINE Frame surfel_frame(const Cam &k, const float *m, float4 q, float s0, f
   return f;
 }
 
+// MODE 0: dense [C, N] outputs.  MODE 1: count the kept pairs per block.
+// MODE 2: write the kept pairs packed at block_off[block] + rank in block.
+template <int MODE>
 __global__ void __launch_bounds__(256) proj_fwd_kernel(ProjFwdArgs a) {
   const int c = blockIdx.y;
-  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  const int n_raw = blockIdx.x * blockDim.x + threadIdx.x;
   const Cam k = load_cam(a.viewmats, a.Ks, c);
-  if (n >= a.N) return;
+  if (MODE == 0 && n_raw >= a.N) return;
+  const bool in = n_raw < a.N;
+  const int n = in ? n_raw : a.N - 1;  // packed modes: every lane reaches the block scan
   const size_t idx = (size_t)c * a.N + n;
   const float4 q = *reinterpret_cast<const float4 *>(a.quats + 4 * (size_t)n);
   const float *sp = a.scales + 3 * (size_t)n;
   const Frame f = surfel_frame(k, a.means + 3 * (size_t)n, q, sp[0], sp[1]);
-  a.depths[idx] = f.mc[2];
+  if (MODE == 0) a.depths[idx] = f.mc[2];
 
   // rows of K * [t0 | t1 | mc] (the ray transform, M0/M1/M2 of the reference)
   float M[9];
@@ -118,7 +129,7 @@ __global__ void __launch_bounds__(256) proj_fwd_kernel(ProjFwdArgs a) {
   M[7] = f.t1[2];
   M[8] = f.mc[2];
 
-  bool keep = !(f.mc[2] < a.near_plane || f.mc[2] > a.far_plane);
+  bool keep = in && !(f.mc[2] < a.near_plane || f.mc[2] > a.far_plane);
   // AABB from the (1, 1, -1) corner (Projection2DGSFused.cu:200-219)
   const float dist = M[6] * M[6] + M[7] * M[7] - M[8] * M[8];
   keep &= dist != 0.f;
@@ -133,14 +144,45 @@ __global__ void __launch_bounds__(256) proj_fwd_kernel(ProjFwdArgs a) {
             my - radius >= (float)a.H);
 
   const float sgn = -(f.nz[0] * f.mc[0] + f.nz[1] * f.mc[1] + f.nz[2] * f.mc[2]) > 0.f ? 1.f : -1.f;
-  a.radii[idx] = keep ? (int32_t)radius : 0;
-  *reinterpret_cast<float2 *>(a.means2d + 2 * idx) = keep ? make_float2(mx, my) : make_float2(0.f, 0.f);
-  float *rt = a.ray_transforms + 9 * idx;
+  if (MODE == 0) {
+    a.radii[idx] = keep ? (int32_t)radius : 0;
+    *reinterpret_cast<float2 *>(a.means2d + 2 * idx) = keep ? make_float2(mx, my) : make_float2(0.f, 0.f);
+    float *rt = a.ray_transforms + 9 * idx;
 #pragma unroll
-  for (int i = 0; i < 9; ++i) rt[i] = keep ? M[i] : 0.f;
-  float *nr = a.normals + 3 * idx;
+    for (int i = 0; i < 9; ++i) rt[i] = keep ? M[i] : 0.f;
+    float *nr = a.normals + 3 * idx;
 #pragma unroll
-  for (int i = 0; i < 3; ++i) nr[i] = keep ? sgn * f.nz[i] : 0.f;
+    for (int i = 0; i < 3; ++i) nr[i] = keep ? sgn * f.nz[i] : 0.f;
+    return;
+  }
+  // packed: rank of this pair among the block's kept pairs (wave ballots)
+  __shared__ int wave_cnt[4];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const uint64_t m = __ballot(keep);
+  if (lane == 0) wave_cnt[wid] = __popcll(m);
+  __syncthreads();
+  const int64_t blk = (int64_t)c * gridDim.x + blockIdx.x;
+  if (MODE == 1) {
+    if (threadIdx.x == 0) a.block_cnt[blk] = wave_cnt[0] + wave_cnt[1] + wave_cnt[2] + wave_cnt[3];
+    return;
+  }
+  if (!keep) return;
+  int before = 0;
+  for (int w = 0; w < wid; ++w) before += wave_cnt[w];
+  const int64_t o = a.block_off[blk] + before +
+                    __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                              __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+  a.camera_ids[o] = c;
+  a.gaussian_ids[o] = n;
+  a.radii[o] = (int32_t)radius;
+  *reinterpret_cast<float2 *>(a.means2d + 2 * o) = make_float2(mx, my);
+  a.depths[o] = f.mc[2];
+  float *rt = a.ray_transforms + 9 * o;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) rt[i] = M[i];
+  float *nr = a.normals + 3 * o;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) nr[i] = sgn * f.nz[i];
 }
 
 struct ProjBwdArgs {
@@ -150,15 +192,34 @@ struct ProjBwdArgs {
   const float *ray_transforms, *v_means2d, *v_depths, *v_normals, *v_ray_transforms;
   float *v_means, *v_quats, *v_scales;
   int store_mode;  // C == 1: plain stores of every row; else atomics of valid rows
+  // packed inputs (projection_2dgs_packed_bwd, Projection2DGSPacked.cu:274-420):
+  // entry e is the pair (camera_ids[e], gaussian_ids[e]); sparse: one
+  // gradient row per entry [nnz, .]
+  const int64_t *camera_ids, *gaussian_ids;
+  int64_t nnz;
+  int sparse;
 };
 
 __global__ void __launch_bounds__(256) proj_bwd_kernel(ProjBwdArgs a) {
-  const int c = blockIdx.y;
-  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  int c, n;
+  size_t idx;
+  bool valid;
+  const bool packed = a.camera_ids != nullptr;
+  if (packed) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= a.nnz) return;
+    c = (int)a.camera_ids[e];
+    n = (int)a.gaussian_ids[e];
+    idx = (size_t)e;
+    valid = true;
+  } else {
+    c = blockIdx.y;
+    n = blockIdx.x * blockDim.x + threadIdx.x;
+    if (n >= a.N) return;
+    idx = (size_t)c * a.N + n;
+    valid = a.radii[idx] > 0;
+  }
   const Cam k = load_cam(a.viewmats, a.Ks, c);
-  if (n >= a.N) return;
-  const size_t idx = (size_t)c * a.N + n;
-  const bool valid = a.radii[idx] > 0;
   float vm[3] = {0.f, 0.f, 0.f}, vq[4] = {0.f, 0.f, 0.f, 0.f}, vs[3] = {0.f, 0.f, 0.f};
   if (valid) {
     const float4 q = *reinterpret_cast<const float4 *>(a.quats + 4 * (size_t)n);
@@ -224,7 +285,13 @@ __global__ void __launch_bounds__(256) proj_bwd_kernel(ProjBwdArgs a) {
 #pragma unroll
     for (int i = 0; i < 3; ++i) vm[i] = vRS[i][2];
   }
-  if (a.store_mode) {
+  if (packed && a.sparse) {  // COO values, one row per packed entry
+    float *o = a.v_means + 3 * idx;
+    o[0] = vm[0]; o[1] = vm[1]; o[2] = vm[2];
+    *reinterpret_cast<float4 *>(a.v_quats + 4 * idx) = make_float4(vq[0], vq[1], vq[2], vq[3]);
+    o = a.v_scales + 3 * idx;
+    o[0] = vs[0]; o[1] = vs[1]; o[2] = 0.f;
+  } else if (a.store_mode) {
     float *o = a.v_means + 3 * (size_t)n;
     o[0] = vm[0]; o[1] = vm[1]; o[2] = vm[2];
     *reinterpret_cast<float4 *>(a.v_quats + 4 * (size_t)n) = make_float4(vq[0], vq[1], vq[2], vq[3]);
@@ -1186,8 +1253,8 @@ extern "C" int gsplat_hip_projection_2dgs_fwd(int C, int N, const float *means, 
              "projection_2dgs_fwd: quats must be 16-B aligned, means2d 8-B aligned");
   ProjFwdArgs a{C, N, width, height, near_plane, far_plane, radius_clip, means, quats, scales,
                 viewmats, Ks, radii, means2d, depths, ray_transforms, normals};
-  hipLaunchKernelGGL(proj_fwd_kernel, dim3((N + 255) / 256, C), dim3(256), 0, (hipStream_t)stream,
-                     a);
+  hipLaunchKernelGGL(proj_fwd_kernel<0>, dim3((N + 255) / 256, C), dim3(256), 0,
+                     (hipStream_t)stream, a);
   GS_CHECK_LAUNCH("projection_2dgs_fwd");
   return 0;
 }
@@ -1222,6 +1289,106 @@ extern "C" int gsplat_hip_projection_2dgs_bwd(
                 v_depths, v_normals, v_ray_transforms, v_means, v_quats, v_scales, store_mode};
   hipLaunchKernelGGL(proj_bwd_kernel, dim3((N + 255) / 256, C), dim3(256), 0, st, a);
   GS_CHECK_LAUNCH("projection_2dgs_bwd");
+  return 0;
+}
+
+// ------------------------------------------------------------------ packed --
+// projection_2dgs_packed_fwd (gsplat/cuda/csrc/Projection2DGSPacked.cu:17-270):
+// a counting pass, a scan of the per-block counts and a pass that recomputes
+// and writes the kept (camera, surfel) pairs in (camera, surfel) order.
+namespace gs {
+void launch_packed_scan(int64_t nb, int64_t *cnt, int64_t *total, hipStream_t st);
+}
+
+extern "C" int64_t gsplat_hip_projection_2dgs_packed_workspace_bytes(int C, int N) {
+  const int64_t nb = (int64_t)C * ((N + 255) / 256);
+  return (nb + 1) * (int64_t)sizeof(int64_t);
+}
+
+extern "C" int gsplat_hip_projection_2dgs_packed_count(
+    int C, int N, const float *means, const float *quats, const float *scales,
+    const float *viewmats, const float *Ks, int width, int height, float near_plane,
+    float far_plane, float radius_clip, void *workspace, int64_t *nnz_device, void *stream) {
+  GS_REQUIRE(C >= 0 && N >= 0, "projection_2dgs_packed_count: negative sizes C=%d N=%d", C, N);
+  hipStream_t st = (hipStream_t)stream;
+  if (C == 0 || N == 0) {
+    GS_HIP(hipMemsetAsync(nnz_device, 0, sizeof(int64_t), st));
+    return 0;
+  }
+  GS_REQUIRE(means && quats && scales && viewmats && Ks && workspace && nnz_device,
+             "projection_2dgs_packed_count: null pointer argument");
+  GS_REQUIRE(((uintptr_t)quats & 15) == 0,
+             "projection_2dgs_packed_count: quats must be 16-B aligned");
+  ProjFwdArgs a{C, N, width, height, near_plane, far_plane, radius_clip, means, quats, scales,
+                viewmats, Ks};
+  a.block_cnt = reinterpret_cast<int64_t *>(workspace);
+  const dim3 grid((N + 255) / 256, C);
+  hipLaunchKernelGGL(proj_fwd_kernel<1>, grid, dim3(256), 0, st, a);
+  gs::launch_packed_scan((int64_t)grid.x * grid.y, a.block_cnt, nnz_device, st);
+  GS_CHECK_LAUNCH("projection_2dgs_packed_count");
+  return 0;
+}
+
+extern "C" int gsplat_hip_projection_2dgs_packed_fwd(
+    int C, int N, const float *means, const float *quats, const float *scales,
+    const float *viewmats, const float *Ks, int width, int height, float near_plane,
+    float far_plane, float radius_clip, const void *workspace, int64_t *camera_ids,
+    int64_t *gaussian_ids, int32_t *radii, float *means2d, float *depths, float *ray_transforms,
+    float *normals, void *stream) {
+  GS_REQUIRE(C >= 0 && N >= 0, "projection_2dgs_packed_fwd: negative sizes C=%d N=%d", C, N);
+  if (C == 0 || N == 0) return 0;
+  GS_REQUIRE(means && quats && scales && viewmats && Ks && workspace && camera_ids &&
+                 gaussian_ids && radii && means2d && depths && ray_transforms && normals,
+             "projection_2dgs_packed_fwd: null pointer argument");
+  GS_REQUIRE(((uintptr_t)quats & 15) == 0 && ((uintptr_t)means2d & 7) == 0,
+             "projection_2dgs_packed_fwd: quats must be 16-B aligned, means2d 8-B aligned");
+  ProjFwdArgs a{C, N, width, height, near_plane, far_plane, radius_clip, means, quats, scales,
+                viewmats, Ks, radii, means2d, depths, ray_transforms, normals};
+  a.block_off = reinterpret_cast<const int64_t *>(workspace);
+  a.camera_ids = camera_ids;
+  a.gaussian_ids = gaussian_ids;
+  hipLaunchKernelGGL(proj_fwd_kernel<2>, dim3((N + 255) / 256, C), dim3(256), 0,
+                     (hipStream_t)stream, a);
+  GS_CHECK_LAUNCH("projection_2dgs_packed_fwd");
+  return 0;
+}
+
+// projection_2dgs_packed_bwd (Projection2DGSPacked.cu:274-420): one lane per
+// packed entry; dense [N, .] gradients by atomics, or (sparse_grad) one row
+// per entry for the COO gradients of _wrapper.py:1529-1570.  v_viewmats, as
+// in the reference, is not differentiated (zeros).
+extern "C" int gsplat_hip_projection_2dgs_packed_bwd(
+    int C, int N, int64_t nnz, const float *means, const float *quats, const float *scales,
+    const float *viewmats, const float *Ks, int width, int height, const int64_t *camera_ids,
+    const int64_t *gaussian_ids, const float *ray_transforms, const float *v_means2d,
+    const float *v_depths, const float *v_normals, const float *v_ray_transforms,
+    int sparse_grad, float *v_means, float *v_quats, float *v_scales, float *v_viewmats,
+    void *stream) {
+  (void)width;
+  (void)height;
+  GS_REQUIRE(C >= 0 && N >= 0 && nnz >= 0, "projection_2dgs_packed_bwd: negative sizes");
+  hipStream_t st = (hipStream_t)stream;
+  if (v_viewmats && C > 0) GS_HIP(hipMemsetAsync(v_viewmats, 0, sizeof(float) * 16 * C, st));
+  if (!sparse_grad && N > 0) {
+    GS_HIP(hipMemsetAsync(v_means, 0, sizeof(float) * 3 * N, st));
+    GS_HIP(hipMemsetAsync(v_quats, 0, sizeof(float) * 4 * N, st));
+    GS_HIP(hipMemsetAsync(v_scales, 0, sizeof(float) * 3 * N, st));
+  }
+  if (nnz == 0) return 0;
+  GS_REQUIRE(means && quats && scales && viewmats && Ks && camera_ids && gaussian_ids &&
+                 ray_transforms && v_means2d && v_normals && v_ray_transforms && v_means &&
+                 v_quats && v_scales,
+             "projection_2dgs_packed_bwd: null pointer argument");
+  GS_REQUIRE(((uintptr_t)quats & 15) == 0 && ((uintptr_t)v_quats & 15) == 0,
+             "projection_2dgs_packed_bwd: quats / v_quats must be 16-B aligned");
+  ProjBwdArgs a{C, N, means, quats, scales, viewmats, Ks, nullptr, ray_transforms, v_means2d,
+                v_depths, v_normals, v_ray_transforms, v_means, v_quats, v_scales, 0};
+  a.camera_ids = camera_ids;
+  a.gaussian_ids = gaussian_ids;
+  a.nnz = nnz;
+  a.sparse = sparse_grad;
+  hipLaunchKernelGGL(proj_bwd_kernel, dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, st, a);
+  GS_CHECK_LAUNCH("projection_2dgs_packed_bwd");
   return 0;
 }
 

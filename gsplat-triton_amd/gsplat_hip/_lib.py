@@ -79,6 +79,14 @@ _SIGS = {
                                               _f, _p, _p, _p, _p, _p, _p]),
     "gsplat_hip_projection_2dgs_bwd": (_i32, [_i32, _i32, _p, _p, _p, _p, _p, _i32, _i32, _p, _p,
                                               _p, _p, _p, _p, _p, _p, _p, _p, _p]),
+    "gsplat_hip_projection_2dgs_packed_workspace_bytes": (_i64, [_i32, _i32]),
+    "gsplat_hip_projection_2dgs_packed_count": (_i32, [_i32, _i32, _p, _p, _p, _p, _p, _i32, _i32,
+                                                       _f, _f, _f, _p, _p, _p]),
+    "gsplat_hip_projection_2dgs_packed_fwd": (_i32, [_i32, _i32, _p, _p, _p, _p, _p, _i32, _i32, _f,
+                                                     _f, _f, _p, _p, _p, _p, _p, _p, _p, _p, _p]),
+    "gsplat_hip_projection_2dgs_packed_bwd": (_i32, [_i32, _i32, _i64, _p, _p, _p, _p, _p, _i32,
+                                                     _i32, _p, _p, _p, _p, _p, _p, _p, _i32, _p,
+                                                     _p, _p, _p, _p]),
     "gsplat_hip_rasterize_2dgs_supported_channels": (_i32, [_i32]),
     "gsplat_hip_rasterize_2dgs_fwd": (_i32, [_i32, _i32, _i32, _i32, _i32, _i32, _i32, _p, _p, _p,
                                              _p, _p, _p, _p, _p, _i64, _p, _p, _p, _p, _p, _p,

@@ -79,6 +79,81 @@ class _FullyFusedProjection2DGS(torch.autograd.Function):
         return (v_means, v_quats, v_scales, v_viewmats, None, None, None, None, None, None, None)
 
 
+class _FullyFusedProjectionPacked2DGS(torch.autograd.Function):
+    """Projects surfels to 2D, packed [nnz] outputs
+    (gsplat/cuda/_wrapper.py:1440-1592).  One host read of nnz, as the
+    reference's packed projection (its indptr / block_accum total)."""
+
+    @staticmethod
+    def forward(ctx, means, quats, scales, viewmats, Ks, width, height, near_plane, far_plane,
+                radius_clip, sparse_grad):
+        means, quats, scales, viewmats, Ks = (_f32c(x) for x in (means, quats, scales, viewmats, Ks))
+        quats = _aligned16(quats)
+        _dev_check(means, quats, scales, viewmats, Ks)
+        C, N = viewmats.shape[0], means.shape[0]
+        dev = means.device
+        ws = torch.empty(max(int(_lib.query("gsplat_hip_projection_2dgs_packed_workspace_bytes",
+                                            C, N)) // 8, 1), dtype=torch.int64, device=dev)
+        nnz_dev = torch.empty(1, dtype=torch.int64, device=dev)
+        args = (_ptr(means), _ptr(quats), _ptr(scales), _ptr(viewmats), _ptr(Ks), int(width),
+                int(height), float(near_plane), float(far_plane), float(radius_clip))
+        _lib.call("gsplat_hip_projection_2dgs_packed_count", C, N, *args, _ptr(ws),
+                  _ptr(nnz_dev), _stream())
+        nnz = int(nnz_dev.item())
+        camera_ids = torch.empty(nnz, dtype=torch.int64, device=dev)
+        gaussian_ids = torch.empty(nnz, dtype=torch.int64, device=dev)
+        radii = torch.empty(nnz, dtype=torch.int32, device=dev)
+        means2d = torch.empty((nnz, 2), device=dev)
+        depths = torch.empty(nnz, device=dev)
+        ray_transforms = torch.empty((nnz, 3, 3), device=dev)
+        normals = torch.empty((nnz, 3), device=dev)
+        _lib.call("gsplat_hip_projection_2dgs_packed_fwd", C, N, *args, _ptr(ws),
+                  _ptr(camera_ids), _ptr(gaussian_ids), _ptr(radii), _ptr(means2d),
+                  _ptr(depths), _ptr(ray_transforms), _ptr(normals), _stream())
+        ctx.save_for_backward(camera_ids, gaussian_ids, means, quats, scales, viewmats, Ks,
+                              ray_transforms)
+        ctx.width, ctx.height, ctx.sparse_grad = int(width), int(height), sparse_grad
+        ctx.mark_non_differentiable(camera_ids, gaussian_ids, radii)
+        return camera_ids, gaussian_ids, radii, means2d, depths, ray_transforms, normals
+
+    @staticmethod
+    def backward(ctx, v_camera_ids, v_gaussian_ids, v_radii, v_means2d, v_depths,
+                 v_ray_transforms, v_normals):
+        camera_ids, gaussian_ids, means, quats, scales, viewmats, Ks, ray_transforms = \
+            ctx.saved_tensors
+        C, N, nnz = viewmats.shape[0], means.shape[0], camera_ids.numel()
+        dev = means.device
+
+        def g(t, shape):
+            return torch.zeros(shape, device=dev) if t is None else _f32c(t)
+
+        v_means2d = g(v_means2d, (nnz, 2))
+        v_ray_transforms = g(v_ray_transforms, (nnz, 3, 3))
+        v_normals = g(v_normals, (nnz, 3))
+        v_depths = None if v_depths is None else _f32c(v_depths)
+        rows = nnz if ctx.sparse_grad else N
+        v_means = torch.empty((rows, 3), device=dev)
+        v_quats = torch.empty((rows, 4), device=dev)
+        v_scales = torch.empty((rows, 3), device=dev)
+        v_viewmats = torch.empty((C, 4, 4), device=dev) if ctx.needs_input_grad[3] else None
+        _lib.call("gsplat_hip_projection_2dgs_packed_bwd", C, N, nnz, _ptr(means), _ptr(quats),
+                  _ptr(scales), _ptr(viewmats), _ptr(Ks), ctx.width, ctx.height,
+                  _ptr(camera_ids), _ptr(gaussian_ids), _ptr(ray_transforms), _ptr(v_means2d),
+                  _ptr(v_depths), _ptr(v_normals), _ptr(v_ray_transforms),
+                  int(bool(ctx.sparse_grad)), _ptr(v_means), _ptr(v_quats), _ptr(v_scales),
+                  _ptr(v_viewmats), _stream())
+        if ctx.sparse_grad:  # COO gradients (_wrapper.py:1529-1570)
+            def coo(v, like):
+                return torch.sparse_coo_tensor(indices=gaussian_ids[None], values=v,
+                                               size=like.size(), is_coalesced=C == 1)
+            v_means, v_quats, v_scales = coo(v_means, means), coo(v_quats, quats), \
+                coo(v_scales, scales)
+        return (v_means if ctx.needs_input_grad[0] else None,
+                v_quats if ctx.needs_input_grad[1] else None,
+                v_scales if ctx.needs_input_grad[2] else None,
+                v_viewmats, None, None, None, None, None, None, None)
+
+
 def fully_fused_projection_2dgs(
     means: Tensor,  # [N, 3]
     quats: Tensor,  # [N, 4]
@@ -96,7 +171,10 @@ def fully_fused_projection_2dgs(
 ) -> Tuple[Tensor, Tensor, Tensor, Tensor, Tensor]:
     """Ray-splat transforms, 2D means, depths, radii and normals of surfels
     (gsplat/cuda/_wrapper.py:1229-1330).  Returns (radii i32[C,N],
-    means2d[C,N,2], depths[C,N], ray_transforms[C,N,3,3], normals[C,N,3])."""
+    means2d[C,N,2], depths[C,N], ray_transforms[C,N,3,3], normals[C,N,3]), or
+    with packed=True (camera_ids i64[nnz], gaussian_ids i64[nnz], radii
+    i32[nnz], means2d[nnz,2], depths[nnz], ray_transforms[nnz,3,3],
+    normals[nnz,3])."""
     C = viewmats.size(0)
     N = means.size(0)
     assert means.size() == (N, 3), means.size()
@@ -114,8 +192,9 @@ def fully_fused_projection_2dgs(
     viewmats = viewmats.contiguous()
     Ks = Ks.contiguous()
     if packed:
-        raise NotImplementedError("packed=True 2DGS projection is not built yet "
-                                  "(SURVEY §8 f3); pass packed=False")
+        return _FullyFusedProjectionPacked2DGS.apply(means, quats, scales, viewmats, Ks, width,
+                                                     height, near_plane, far_plane, radius_clip,
+                                                     sparse_grad)
     return _FullyFusedProjection2DGS.apply(means, quats, scales, viewmats, Ks, width, height,
                                            eps2d, near_plane, far_plane, radius_clip)
 
@@ -235,14 +314,18 @@ def rasterize_to_pixels_2dgs(
     colour channel, as in the reference."""
     C = isect_offsets.size(0)
     device = means2d.device
-    if packed:
-        raise NotImplementedError("packed=True 2DGS rasterization is not built yet "
-                                  "(SURVEY §8 f3); pass packed=False")
-    N = means2d.size(1)
-    assert means2d.shape == (C, N, 2), means2d.shape
-    assert ray_transforms.shape == (C, N, 3, 3), ray_transforms.shape
-    assert colors.shape[:2] == (C, N), colors.shape
-    assert opacities.shape == (C, N), opacities.shape
+    if packed:  # flatten_ids index the [nnz] rows directly (_wrapper.py:1628-1636)
+        nnz = means2d.size(0)
+        assert means2d.shape == (nnz, 2), means2d.shape
+        assert ray_transforms.shape == (nnz, 3, 3), ray_transforms.shape
+        assert colors.shape[0] == nnz, colors.shape
+        assert opacities.shape == (nnz,), opacities.shape
+    else:
+        N = means2d.size(1)
+        assert means2d.shape == (C, N, 2), means2d.shape
+        assert ray_transforms.shape == (C, N, 3, 3), ray_transforms.shape
+        assert colors.shape[:2] == (C, N), colors.shape
+        assert opacities.shape == (C, N), opacities.shape
     if backgrounds is not None:
         assert backgrounds.shape == (C, colors.shape[-1]), backgrounds.shape
         backgrounds = backgrounds.contiguous()

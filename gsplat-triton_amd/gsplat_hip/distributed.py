@@ -13,6 +13,7 @@ with input and output splits swapped.
 """
 
 import math
+from contextlib import nullcontext as _nullcontext
 from typing import List, Optional, Union
 
 import torch
@@ -155,11 +156,20 @@ class ShardedAdam:
 
     Rows are split in multiples of 4 (16-B aligned shards for the fused
     kernel); the < 4 * world_size remainder rows are all-reduced and updated
-    redundantly on every rank.  Collectives run on the default group, largest
-    tensor first.  `update` is the Adam kernel (csrc/adam.hip by default).
+    redundantly on every rank.  Collectives run on the default group.  `update`
+    is the Adam kernel (csrc/adam.hip by default).
+
+    `groups` (lists of parameter indices, in issue order; default one group)
+    pipelines the step: per group, its reduce-scatters are issued from the
+    current stream (after the backward), and on a side stream the group's Adam
+    waits for them, updates the shards and issues the group's all-gathers.  So
+    the RCCL stream runs RS(g0), AG(g0), RS(g1), AG(g1) ...: the trainer puts
+    the geometry first (the next projection needs it, 44 B/Gaussian) and the SH
+    rows last (192 B/Gaussian, needed only by the colours after the next
+    isect), and neither the host nor the compute stream waits for any of it.
     """
 
-    def __init__(self, params, lrs, betas=(0.9, 0.999), eps=1e-8, update=None):
+    def __init__(self, params, lrs, betas=(0.9, 0.999), eps=1e-8, update=None, groups=None):
         self.params = list(params)
         self.lrs = [float(x) for x in lrs]
         self.betas, self.eps = betas, eps
@@ -184,7 +194,12 @@ class ShardedAdam:
         self.v_tail = [z(tot - main) for _, _, main, tot in self.layout]
         self.g_shard = [torch.empty(q * row, device=dev) for row, q, _, _ in self.layout]
         self.order = sorted(range(len(self.params)), key=lambda i: -self.params[i].numel())
+        self.groups = [list(g) for g in groups] if groups else [list(self.order)]
+        assert sorted(i for g in self.groups for i in g) == list(range(len(self.params))), \
+            self.groups
         self._pending = {}  # parameter index -> all-gather still in flight
+        # Adam + all-gather issue stream (CUDA only; gloo runs them inline)
+        self.side = torch.cuda.Stream(device=dev) if dev.type == "cuda" else None
 
     def wait(self, indices=None):
         """Order the current stream after the deferred all-gathers of these
@@ -204,42 +219,51 @@ class ShardedAdam:
         each parameter's next use after `wait([i])` (stream order only)."""
         self.wait()
         self.step_count += 1
-        flats, works = {}, []
-        for i in self.order:
-            p = self.params[i]
-            g = p.grad if p.grad is not None else torch.zeros_like(p)
-            gf = g.contiguous().view(-1)
-            flats[i] = gf
-            _, _, main, tot = self.layout[i]
-            if main:
-                works.append(dist.reduce_scatter_tensor(self.g_shard[i], gf[:main],
-                                                        async_op=True))
-            if tot > main:
-                works.append(dist.all_reduce(gf[main:], async_op=True))
-        for wk in works:
-            wk.wait()
-        idx = [i for i in range(len(self.params)) if self.layout[i][2]]
+        side = self.side
+        if side is not None:  # the side stream starts after everything queued so far
+            side.wait_stream(torch.cuda.current_stream(side.device))
+        for grp in self.groups:
+            flats, works = {}, []
+            for i in sorted(grp, key=lambda i: -self.params[i].numel()):
+                p = self.params[i]
+                g = p.grad if p.grad is not None else torch.zeros_like(p)
+                gf = g.contiguous().view(-1)
+                flats[i] = gf
+                if side is not None:  # its tail rows are read on the side stream
+                    gf.record_stream(side)
+                _, _, main, tot = self.layout[i]
+                if main:
+                    works.append(dist.reduce_scatter_tensor(self.g_shard[i], gf[:main],
+                                                            async_op=True))
+                if tot > main:
+                    works.append(dist.all_reduce(gf[main:], async_op=True))
+            with (torch.cuda.stream(side) if side is not None else _nullcontext()):
+                for wk in works:  # the side stream (gloo: the host) waits
+                    wk.wait()
+                self._update_group(grp, flats)
+                # issued from the side stream: RCCL waits for this Adam only
+                for i in sorted(grp, key=lambda i: self.params[i].numel()):
+                    _, _, main, _ = self.layout[i]
+                    if main:
+                        full = self.params[i].data.view(-1)[:main]
+                        self._pending[i] = dist.all_gather_into_tensor(
+                            full, self._shard(i, full).clone(), async_op=True)
+        if not defer_gather:
+            self.wait()
+
+    def _update_group(self, grp, flats):
+        idx = [i for i in grp if self.layout[i][2]]
         if idx:
             self.update([self._shard(i, self.params[i].data.view(-1)) for i in idx],
                         [self.g_shard[i] for i in idx], [self.m[i] for i in idx],
                         [self.v[i] for i in idx], [self.lrs[i] for i in idx], self.betas,
                         self.eps, self.step_count)
-        tails = [i for i in range(len(self.params)) if self.layout[i][3] > self.layout[i][2]]
+        tails = [i for i in grp if self.layout[i][3] > self.layout[i][2]]
         if tails:
             self.update([self.params[i].data.view(-1)[self.layout[i][2]:] for i in tails],
                         [flats[i][self.layout[i][2]:] for i in tails],
                         [self.m_tail[i] for i in tails], [self.v_tail[i] for i in tails],
                         [self.lrs[i] for i in tails], self.betas, self.eps, self.step_count)
-        # geometry first (the next forward's projection needs it first), the
-        # large SH rows last
-        for i in sorted(self.order, key=lambda i: self.params[i].numel()):
-            _, _, main, _ = self.layout[i]
-            if main:
-                full = self.params[i].data.view(-1)[:main]
-                self._pending[i] = dist.all_gather_into_tensor(
-                    full, self._shard(i, full).clone(), async_op=True)
-        if not defer_gather:
-            self.wait()
 
     def zero_grad(self, set_to_none=True):
         for p in self.params:

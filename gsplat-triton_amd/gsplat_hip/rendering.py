@@ -421,22 +421,34 @@ def rasterization_2dgs(
     else:
         assert colors.dim() == 3 and colors.shape[0] == N and colors.shape[2] == 3, colors.shape
         assert (sh_degree + 1) ** 2 <= colors.shape[1], colors.shape
-    if packed:
-        raise NotImplementedError("packed=True 2DGS is not built yet (SURVEY §8 f3)")
-
-    radii, means2d, depths, ray_transforms, normals = fully_fused_projection_2dgs(
+    proj = fully_fused_projection_2dgs(
         means, quats, scales, viewmats, Ks, width, height, eps2d, near_plane, far_plane,
         radius_clip, packed, sparse_grad)
-    opacities = opacities[None] if C == 1 else opacities.repeat(C, 1)
-    camera_ids, gaussian_ids = None, None
+    if packed:  # gsplat/rendering.py:1188-1199
+        camera_ids, gaussian_ids, radii, means2d, depths, ray_transforms, normals = proj
+        opacities = opacities[gaussian_ids]
+    else:
+        radii, means2d, depths, ray_transforms, normals = proj
+        opacities = opacities[None] if C == 1 else opacities.repeat(C, 1)
+        camera_ids, gaussian_ids = None, None
     densify = torch.zeros_like(means2d, dtype=means.dtype, requires_grad=True)
 
     tile_width = math.ceil(width / float(tile_size))
     tile_height = math.ceil(height / float(tile_size))
     pending_isects = isect_tiles_begin(means2d, radii, depths, tile_size, tile_width, tile_height,
-                                       packed=False, n_cameras=C)
+                                       packed=packed, n_cameras=C, camera_ids=camera_ids,
+                                       gaussian_ids=gaussian_ids)
 
-    if sh_degree is not None and not viewmats.requires_grad:
+    if packed:  # gsplat/rendering.py:1216-1236
+        if sh_degree is None:
+            colors = colors[gaussian_ids] if colors.dim() == 2 else colors[camera_ids, gaussian_ids]
+        else:
+            shs = colors[gaussian_ids] if sh_rest is None else \
+                (colors[gaussian_ids], sh_rest[gaussian_ids])
+            dirs = means[gaussian_ids, :] - torch.inverse(viewmats)[camera_ids, :3, 3]
+            colors = spherical_harmonics(sh_degree, dirs, shs, masks=radii > 0)
+            colors = torch.clamp_min(colors + 0.5, 0.0)
+    elif sh_degree is not None and not viewmats.requires_grad:
         # one kernel: dirs from -R^T t, radii masking, clamp_min(sh + 0.5, 0)
         colors = sh_colors(sh_degree, means, viewmats,
                            colors if sh_rest is None else (colors, sh_rest), radii)

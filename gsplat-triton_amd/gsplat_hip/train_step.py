@@ -204,7 +204,12 @@ class Trainer:
     def _make_optimizer(self, params):
         if self.sharded:
             from .distributed import ShardedAdam
-            return ShardedAdam(params, self.lrs, **self.adam_kw)
+            # geometry first: the next projection waits for it; the SH rows
+            # only before the next step's colours (after its isect)
+            names = list(self.params)
+            groups = [[names.index(k) for k in ("means", "scales", "quats", "opacities")],
+                      [names.index(k) for k in ("sh0", "shN")]]
+            return ShardedAdam(params, self.lrs, groups=groups, **self.adam_kw)
         if self.fused:  # HIP loss + one-launch Adam (csrc/ssim.hip, csrc/adam.hip)
             return FusedAdam(params, self.lrs, **self.adam_kw)
         groups = [{"params": [p], "lr": lr, "name": k}

@@ -382,6 +382,42 @@ int gsplat_hip_projection_2dgs_bwd(int C, int N, const float *means, const float
                                    const float *v_ray_transforms, float *v_means,
                                    float *v_quats, float *v_scales, float *v_viewmats,
                                    void *stream);
+/* Packed 2DGS projection.  Replaces projection_2dgs_packed_fwd / _bwd
+ * (gsplat/cuda/csrc/Projection2DGSPacked.cu:17-270, 274-420) behind
+ * _FullyFusedProjectionPacked2DGS (gsplat/cuda/_wrapper.py:1440-1592).
+ * count: per-block counts of the kept (camera, surfel) pairs into `workspace`
+ * (gsplat_hip_projection_2dgs_packed_workspace_bytes), scanned in place,
+ * nnz -> nnz_device[0].  fwd (same inputs and workspace): the nnz kept pairs
+ * in (camera, surfel) order -> camera_ids i64[nnz], gaussian_ids i64[nnz],
+ * radii i32[nnz], means2d[nnz,2], depths[nnz], ray_transforms[nnz,3,3],
+ * normals[nnz,3].  bwd: dense v_means[N,3] v_quats[N,4] v_scales[N,3]
+ * (zeroed here, atomics), or with sparse_grad one row per entry [nnz, .];
+ * v_viewmats[C,4,4] or NULL is zeroed (the reference does not differentiate
+ * it). */
+int64_t gsplat_hip_projection_2dgs_packed_workspace_bytes(int C, int N);
+int gsplat_hip_projection_2dgs_packed_count(int C, int N, const float *means, const float *quats,
+                                            const float *scales, const float *viewmats,
+                                            const float *Ks, int width, int height,
+                                            float near_plane, float far_plane, float radius_clip,
+                                            void *workspace, int64_t *nnz_device, void *stream);
+int gsplat_hip_projection_2dgs_packed_fwd(int C, int N, const float *means, const float *quats,
+                                          const float *scales, const float *viewmats,
+                                          const float *Ks, int width, int height,
+                                          float near_plane, float far_plane, float radius_clip,
+                                          const void *workspace, int64_t *camera_ids,
+                                          int64_t *gaussian_ids, int32_t *radii, float *means2d,
+                                          float *depths, float *ray_transforms, float *normals,
+                                          void *stream);
+int gsplat_hip_projection_2dgs_packed_bwd(int C, int N, int64_t nnz, const float *means,
+                                          const float *quats, const float *scales,
+                                          const float *viewmats, const float *Ks, int width,
+                                          int height, const int64_t *camera_ids,
+                                          const int64_t *gaussian_ids,
+                                          const float *ray_transforms, const float *v_means2d,
+                                          const float *v_depths, const float *v_normals,
+                                          const float *v_ray_transforms, int sparse_grad,
+                                          float *v_means, float *v_quats, float *v_scales,
+                                          float *v_viewmats, void *stream);
 
 /* Surfel rasterizer.  D in {1..9, 16, 17, 32, 33}
  * (gsplat_hip_rasterize_2dgs_supported_channels); the caller pads other

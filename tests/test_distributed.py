@@ -149,7 +149,7 @@ def test_reshape_view_blocks():
     assert out.tolist() == [[0, 1, 2, 3, 4], [10, 11, 12, 13, 14]]
 
 
-def _sharded_worker(rank, world, port, q, defer=False):
+def _sharded_worker(rank, world, port, q, defer=False, groups=None):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -162,7 +162,7 @@ def _sharded_worker(rank, world, port, q, defer=False):
         kw = dict(betas=(0.8, 0.99), eps=1e-8)
         ps = [torch.nn.Parameter(t.clone()) for t in init]
         ref = [t.clone() for t in init]
-        opt = ShardedAdam(ps, lrs, update=_adam_torch, **kw)
+        opt = ShardedAdam(ps, lrs, update=_adam_torch, groups=groups, **kw)
         m = [torch.zeros_like(t).view(-1) for t in init]
         v = [torch.zeros_like(t).view(-1) for t in init]
         for step in range(1, 4):
@@ -189,14 +189,17 @@ def _sharded_worker(rank, world, port, q, defer=False):
         q.put((rank, repr(e), None))
 
 
-@pytest.mark.parametrize("world,defer", [(2, False), (3, False), (2, True)])
-def test_sharded_adam_matches_allreduce_adam_gloo(world, defer):
+@pytest.mark.parametrize("world,defer,groups", [(2, False, None), (3, False, None),
+                                               (2, True, None), (2, True, [[3, 1], [0, 2, 4]]),
+                                               (3, False, [[2], [4, 0], [1, 3]])])
+def test_sharded_adam_matches_allreduce_adam_gloo(world, defer, groups):
     """ShardedAdam (reduce-scatter -> Adam on own rows -> all-gather) equals
-    all-reduce + full Adam on every rank, and the replicas stay identical."""
+    all-reduce + full Adam on every rank, and the replicas stay identical --
+    also pipelined per parameter group (the trainer's geometry / SH split)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_sharded_worker, args=(r, world, port, q, defer))
+    procs = [ctx.Process(target=_sharded_worker, args=(r, world, port, q, defer, groups))
              for r in range(world)]
     for p in procs:
         p.start()
