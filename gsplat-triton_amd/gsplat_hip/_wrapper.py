@@ -597,7 +597,8 @@ class _RasterizeToPixels(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, means2d, conics, colors, opacities, backgrounds, masks, width, height,
-                tile_size, isect_offsets, flatten_ids, absgrad, block_size=8, visible=None):
+                tile_size, isect_offsets, flatten_ids, absgrad, block_size=8, visible=None,
+                records=None):
         ctx.means2d_in = means2d if absgrad else None  # receives .absgrad (_wrapper.py:156)
         ctx.set_materialize_grads(False)  # alphas without a loss: None, not zeros
         means2d, conics, colors, opacities, backgrounds = (
@@ -618,14 +619,10 @@ class _RasterizeToPixels(torch.autograd.Function):
                             flatten_ids.numel()))
         state = torch.empty(sb // 4, dtype=torch.float32, device=dev)
         # one 64-B render record per Gaussian for the 16x16 kernels' gathers
-        # (only the rows `visible` marks are referenced by flatten_ids)
-        rf = int(_lib.query("gsplat_hip_rasterize_record_floats", D, tile_size)) if RECORDS else 0
-        records = torch.empty(opacities.numel() * rf if rf else 0, dtype=torch.float32, device=dev)
-        if rf:
-            vis = None if visible is None else visible.to(torch.int32).contiguous()
-            _lib.call("gsplat_hip_rasterize_pack_records", opacities.numel(), D, _ptr(means2d),
-                      _ptr(conics), _ptr(colors), _ptr(opacities), _ptr(vis), _ptr(records),
-                      _stream())
+        # (rasterization() may have packed them already, before its isect sync)
+        if records is None:
+            records = pack_render_records(means2d, conics, colors, opacities, tile_size, visible)
+        rf = 1 if records.numel() else 0
         if sb:  # dispatch order into the state, outside the timed rasterizer launch
             _lib.call("gsplat_hip_rasterize_prepare", C, D, tile_size, tw, th, _ptr(isect_offsets),
                       flatten_ids.numel(), _ptr(state), sb, _stream())
@@ -676,7 +673,7 @@ class _RasterizeToPixels(torch.autograd.Function):
         if ctx.needs_input_grad[4]:
             v_backgrounds = (v_render_colors * (1.0 - render_alphas)).sum(dim=(1, 2))
         return (v_means2d, v_conics, v_colors, v_opacities, v_backgrounds,
-                None, None, None, None, None, None, None, None, None)
+                None, None, None, None, None, None, None, None, None, None)
 
 
 def rasterize_to_pixels(
@@ -705,11 +702,33 @@ def rasterize_to_pixels(
                                 absgrad, block_size)
 
 
+@torch.no_grad()
+def pack_render_records(means2d, conics, colors, opacities, tile_size, visible=None) -> Tensor:
+    """The 16x16 rasterizer's render records (gsplat_hip_rasterize_pack_records):
+    one 64-B row [x, y, conic, opacity, colour] per Gaussian, only the rows
+    whose `visible` count (tiles_per_gauss) is > 0 written.  Empty when the
+    configuration has no record path (then the kernels gather the arrays)."""
+    D = colors.shape[-1]
+    rf = int(_lib.query("gsplat_hip_rasterize_record_floats", D, tile_size)) if RECORDS else 0
+    G = opacities.numel()
+    records = torch.empty(G * rf if rf else 0, dtype=torch.float32, device=means2d.device)
+    if rf:
+        means2d, conics, colors, opacities = (_f32c(x) for x in (means2d, conics, colors,
+                                                                 opacities))
+        vis = None if visible is None else visible.to(torch.int32).contiguous()
+        assert vis is None or vis.numel() == G, (vis.shape, G)
+        _lib.call("gsplat_hip_rasterize_pack_records", G, D, _ptr(means2d), _ptr(conics),
+                  _ptr(colors), _ptr(opacities), _ptr(vis), _ptr(records), _stream())
+    return records
+
+
 def _rasterize_to_pixels(means2d, conics, colors, opacities, image_width, image_height, tile_size,
                          isect_offsets, flatten_ids, backgrounds=None, masks=None, packed=False,
-                         absgrad=False, block_size=8, visible=None):
-    """rasterize_to_pixels with rasterization()'s private hint `visible`
-    ([C,N] tiles_per_gauss): only those Gaussians' render records are packed."""
+                         absgrad=False, block_size=8, visible=None, records=None):
+    """rasterize_to_pixels with rasterization()'s private hints: `visible`
+    ([C,N] tiles_per_gauss: only those Gaussians' render records are packed)
+    and `records` (already packed by pack_render_records for these exact
+    colours; used when no channel padding or chunking applies)."""
     C = isect_offsets.size(0)
     device = means2d.device
     if packed:
@@ -747,7 +766,8 @@ def _rasterize_to_pixels(means2d, conics, colors, opacities, image_width, image_
                 bgs = torch.cat([bgs, torch.zeros(*bgs.shape[:-1], Dp - D, device=device)], -1)
         rc, ra = _RasterizeToPixels.apply(means2d, conics, cols, opacities, bgs, masks,
                                           image_width, image_height, tile_size, isect_offsets,
-                                          flatten_ids, absgrad, block_size, visible)
+                                          flatten_ids, absgrad, block_size, visible,
+                                          records if Dp == D and cols is colors else None)
         return (rc[..., :D] if Dp != D else rc), ra
 
     if channels <= 32:

@@ -25,6 +25,7 @@ from ._wrapper import (
     isect_offset_encode,
     isect_tiles_begin,
     _rasterize_to_pixels,
+    pack_render_records,
     rasterize_to_pixels,
     sh_colors,
     spherical_harmonics,
@@ -241,8 +242,14 @@ def rasterization(
                 backgrounds = torch.zeros(C, 1, device=backgrounds.device)
         return colors, backgrounds
 
+    records = None
     if not late:
         colors, backgrounds = add_depth(colors, backgrounds)
+        if colors.shape[-1] <= channel_chunk:
+            # queued before the isect sync, so the GPU has it to run while the
+            # host waits for n_isects
+            records = pack_render_records(means2d, conics, colors, opacities, tile_size,
+                                          None if packed else pending_isects.tpg)
 
     tiles_per_gauss, isect_ids, flatten_ids = pending_isects.finish(sort=True)
     isect_offsets = isect_offset_encode(isect_ids, C, tile_width, tile_height)
@@ -273,7 +280,8 @@ def rasterization(
     else:
         render_colors, render_alphas = _rasterize_to_pixels(
             means2d, conics, colors, opacities, width, height, tile_size, isect_offsets,
-            flatten_ids, backgrounds=backgrounds, packed=packed, absgrad=absgrad, visible=visible)
+            flatten_ids, backgrounds=backgrounds, packed=packed, absgrad=absgrad, visible=visible,
+            records=records)
     if render_mode in ["ED", "RGB+ED"]:
         render_colors = torch.cat(
             [render_colors[..., :-1],
