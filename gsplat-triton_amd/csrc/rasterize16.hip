@@ -26,6 +26,8 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+#include <algorithm>
+
 namespace gs {
 static uint64_t *g_timeline = nullptr;
 static unsigned long long *g_lanehist = nullptr;  // debug: [65] active-lane counts (backward)
@@ -141,6 +143,19 @@ struct Args {
   // 128-B line each: heads sharing a line serialise the returning atomics,
   // ~85 per us -- tools/xcc_probe.hip).  null: order[blockIdx.x]
   int32_t *queue;
+  // forward, split heavy tiles (fwd_plan_kernel): fitems[b] = (tile, -1) a
+  // whole tile or (tile, k) chunk k of a split tile; p1items the chunks whose
+  // transmittance product fwd_prod_kernel computes; heavy the split tiles as
+  // (tile, id of its chunk 0); fcount = {#fitems, #p1items, #heavy, index in
+  // fitems of the first chunk}.  prod: per boundary slot (b / L) the product
+  // of (1 - alpha) over the chunk ending at b; cout: per chunk id (its index
+  // in fitems minus fcount[3]), the chunk's end T, last id and colour sum
+  // [2 + D][256] (chunk START slots are not unique: a tile's first chunk can
+  // share b / L with the previous tile's last one).
+  const int2 *fitems, *p1items, *heavy;
+  const int32_t *fcount;
+  float *prod, *cout;
+  int SL;  // split tiles: isects per chunk (a multiple of L)
   const float *render_colors_in;  // backward: forward colours (for suffix sums)
   int dbg;  // experiments only (GSPLAT_HIP_DBG): bit 0 = backward skips its atomics
   uint64_t *timeline;  // debug: per-wave (start, end) s_memrealtime stamps or null
@@ -446,14 +461,24 @@ __attribute__((amdgpu_waves_per_eu((U == 1 ? 5 : U == 2 ? 4 : 3) + (PF == 0 ? 2 
   const int lane = threadIdx.x & 63;
   float4 *st = stage_all[threadIdx.x >> 6];
   const uint64_t t_start = tl_now(a);
-  const int tile_ = fwd_tile(a);
-  if (tile_ < 0) return;  // unreachable: the queues hold one tile per workgroup
+  int tile_, kc = -1;  // kc >= 0: chunk kc of a split tile
+  if (a.fitems) {
+    if ((int)blockIdx.x >= a.fcount[0]) return;  // grid is an upper bound
+    const int2 it = a.fitems[blockIdx.x];
+    tile_ = it.x;
+    kc = it.y;
+  } else {
+    tile_ = fwd_tile(a);
+    if (tile_ < 0) return;  // unreachable: the queues hold one tile per workgroup
+  }
   const WaveGeom geo(a, lane, tile_);
   const int tile = geo.tile, c = geo.c;
   const bool inside = geo.px < a.W && geo.py < a.H;
   const float fx = (float)geo.px + 0.5f, fy = (float)geo.py + 0.5f;
-  const int64_t start = a.offsets[tile];
-  const int64_t end = (tile == a.n_tiles - 1) ? a.n_isects : (int64_t)a.offsets[tile + 1];
+  const int64_t tstart = a.offsets[tile];
+  const int64_t tend = (tile == a.n_tiles - 1) ? a.n_isects : (int64_t)a.offsets[tile + 1];
+  const int64_t start = kc >= 0 ? tstart + (int64_t)kc * a.SL : tstart;
+  const int64_t end = kc >= 0 ? min(tend, start + (int64_t)a.SL) : tend;
   const bool skip_tile = a.masks && a.masks[tile];
 
   // colour accumulated from even (.x) and odd (.y) records of each pair
@@ -470,6 +495,17 @@ __attribute__((amdgpu_waves_per_eu((U == 1 ? 5 : U == 2 ? 4 : 3) + (PF == 0 ? 2 
   // A terminated (or outside) pixel is encoded by a negative T: |T| is its
   // final transmittance.
   float T = (!inside || skip_tile) ? -1.f : 1.f;
+  const int pix_in_tile = (threadIdx.x >> 6) * 64 + lane;  // row-major
+  if (kc > 0 && inside && !skip_tile) {
+    // chunk kc of a split tile: the transmittance entering it is the product
+    // of the earlier chunks' (fwd_prod_kernel).  At or below 1e-4 the pixel
+    // terminated in an earlier chunk (every blended factor kept it above);
+    // -Tin marks it finished with about that transmittance.
+    float Tin = 1.f;
+    for (int j = 0; j < kc; ++j)
+      Tin *= a.prod[((tstart + (int64_t)(j + 1) * a.SL) / a.L) * (kTS * kTS) + pix_in_tile];
+    T = Tin > kTMin ? Tin : -fmaxf(Tin, 1e-30f);
+  }
 
   if (!skip_tile && start < end) {
     // flatten id of lane `lane` of the batch at b0, clamped into the range
@@ -558,7 +594,6 @@ __attribute__((amdgpu_waves_per_eu((U == 1 ? 5 : U == 2 ? 4 : 3) + (PF == 0 ? 2 
     // later chunks) as accurate as its own back-to-front accumulation; a
     // difference of running totals would cancel catastrophically.
     const int64_t L = a.L;
-    const int pix_in_tile = (threadIdx.x >> 6) * 64 + lane;  // row-major
     auto slot = [&](int64_t bidx) { return a.state + (bidx / L) * (int64_t)(kTS * kTS * (1 + D)); };
     int64_t cur_b = start;  // start of the chunk being accumulated
     auto close_chunk = [&]() {  // fold acc into tot; store S of the chunk at cur_b
@@ -566,7 +601,7 @@ __attribute__((amdgpu_waves_per_eu((U == 1 ? 5 : U == 2 ? 4 : 3) + (PF == 0 ? 2 
 #pragma unroll
       for (int d = 0; d < D; ++d) {
         const float cs = acc[d].x + acc[d].y;
-        if (cur_b > start) sl[(1 + d) * kTS * kTS + pix_in_tile] = cs;
+        if (cur_b > tstart) sl[(1 + d) * kTS * kTS + pix_in_tile] = cs;
         tot[d] += cs;
         acc[d] = f2v{0.f, 0.f};
       }
@@ -576,7 +611,9 @@ __attribute__((amdgpu_waves_per_eu((U == 1 ? 5 : U == 2 ? 4 : 3) + (PF == 0 ? 2 
       cur_b = bidx;
       slot(bidx)[pix_in_tile] = T;
     };
-    const bool chunked = a.state && L > 0 && end - start > L;
+    // a chunk of a split tile writes the state of the boundaries inside it
+    // and the colour it adds at its own start boundary
+    const bool chunked = a.state && L > 0 && (end - start > L || kc > 0);
     int64_t b0 = start;
     if constexpr (PF == 0) {
       int32_t g_n = id_at(start);
@@ -652,7 +689,19 @@ __attribute__((amdgpu_waves_per_eu((U == 1 ? 5 : U == 2 ? 4 : 3) + (PF == 0 ? 2 
 #pragma unroll
   for (int d = 0; d < D; ++d) tot[d] += acc[d].x + acc[d].y;
 
-  if (inside) {
+  if (kc >= 0) {
+    // chunk of a split tile: its end T, last id and colour for
+    // fwd_combine_kernel; and its end T at the next boundary of the
+    // backward's chunk state (the running T the unsplit forward stores there;
+    // the loop above wrote the boundaries inside the chunk and the colours)
+    const int64_t sz = kTS * kTS;
+    float *co = a.cout + (int64_t)((int)blockIdx.x - a.fcount[3]) * sz * (2 + D);
+    co[pix_in_tile] = T;
+    co[sz + pix_in_tile] = __int_as_float(last);
+#pragma unroll
+    for (int d = 0; d < D; ++d) co[(2 + d) * sz + pix_in_tile] = tot[d];
+    if (end < tend && a.state) a.state[(end / a.L) * sz * (1 + D) + pix_in_tile] = T;
+  } else if (inside) {
     const int64_t pix = ((int64_t)c * a.H + geo.py) * a.W + geo.px;
     float *oc = a.render_colors + pix * D;
 #pragma unroll
@@ -664,6 +713,117 @@ __attribute__((amdgpu_waves_per_eu((U == 1 ? 5 : U == 2 ? 4 : 3) + (PF == 0 ? 2 
     a.last_ids[pix] = last;
   }
   tl_store(a, t_start, lane);
+}
+
+// Split heavy tiles, pass 1: for chunk k of a split tile (every chunk but the
+// last), the product over its records of (1 - alpha) where a record hits,
+// per pixel, from 1 and without the termination rule (a product at or below
+// 1e-4 is kept as 0: every pixel past it is finished).  Same culling, alpha
+// and fma as the compositing.  One 16x4 strip per wave, as fwd_kernel.
+template <int D>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5)))
+fwd_prod_kernel(Args a) {
+  using P = FwdPair<D>;
+  constexpr int N4 = P::N4;
+  __shared__ float4 stage_all[4][32 * N4];
+  const int lane = threadIdx.x & 63;
+  float4 *st = stage_all[threadIdx.x >> 6];
+  for (int item = blockIdx.x; item < a.fcount[1]; item += gridDim.x) {
+  const int2 it = a.p1items[item];
+  const WaveGeom geo(a, lane, it.x);
+  const int64_t tstart = a.offsets[geo.tile];
+  const int64_t start = tstart + (int64_t)it.y * a.SL;
+  const int64_t end = start + a.SL;  // never the last chunk: full length
+  const float fx = (float)geo.px + 0.5f, fy = (float)geo.py + 0.5f;
+  float Pp = 1.f;
+  auto id_at = [&](int64_t b0) -> int32_t { return a.flatten_ids[min(b0 + lane, end - 1)]; };
+  int32_t g_n = id_at(start);
+  for (int64_t b0 = start; b0 < end; b0 += 64) {
+    if (__ballot(Pp > 0.f) == 0) break;
+    Attr<D> A;
+    load_attr<D>(a, g_n, A);
+    g_n = id_at(b0 + 64);
+    const bool keep = (b0 + lane < end) && keep_attr<D>(A, geo.x0, geo.x1, geo.y0, geo.y1);
+    const uint64_t m = __ballot(keep);
+    const int cnt = __popcll(m);
+    if (keep) stage_fwd_pair<D>(st, ballot_slot(m), A, (int32_t)(b0 + lane));
+    if ((cnt & 1) && lane == 0) stage_fwd_pad<D>(st, cnt);
+    wave_sync_lds();
+    for (int p = 0; p < (cnt + 1) >> 1; ++p) {
+      f2v f[2 * N4];
+      float4 v[N4];
+#pragma unroll
+      for (int i = 0; i < N4; ++i) v[i] = st[p * N4 + i];
+#pragma unroll
+      for (int i = 0; i < N4; ++i) {
+        asm volatile("" ::"v"(v[i].x), "v"(v[i].y), "v"(v[i].z), "v"(v[i].w));
+        f[2 * i] = f2v{v[i].x, v[i].y};
+        f[2 * i + 1] = f2v{v[i].z, v[i].w};
+      }
+      const f2v dx = f[0] - fx, dy = f[1] - fy;
+      const f2v s2 = dx * (f[2] * dx + f[3] * dy) + f[4] * dy * dy;
+      f2v al = f[5] * f2v{__builtin_amdgcn_exp2f(-s2.x), __builtin_amdgcn_exp2f(-s2.y)};
+      al.x = fminf(al.x, kAlphaMax);
+      al.y = fminf(al.y, kAlphaMax);
+      const bool h0 = __float_as_uint(s2.x) <= __float_as_uint(f[6].x);
+      const bool h1 = __float_as_uint(s2.y) <= __float_as_uint(f[6].y);
+      float n0 = h0 ? __builtin_fmaf(-Pp, al.x, Pp) : Pp;
+      n0 = n0 > kTMin ? n0 : 0.f;
+      float n1 = h1 ? __builtin_fmaf(-n0, al.y, n0) : n0;
+      Pp = n1 > kTMin ? n1 : 0.f;
+    }
+    wave_sync_lds();
+  }
+  const int pit = (threadIdx.x >> 6) * 64 + lane;
+  a.prod[(end / a.L) * (kTS * kTS) + pit] = Pp;
+  }
+}
+
+// Split heavy tiles, pass 3: per pixel of a split tile, its colour (the sum
+// of the chunks' colours), its final T (the end T of the chunk where it
+// terminated -- the first negative -- else of the last chunk) and its last id
+// (the largest of the chunks').  One thread per pixel.
+template <int D>
+__global__ void __launch_bounds__(256) fwd_combine_kernel(Args a) {
+  if ((int)blockIdx.x >= a.fcount[2]) return;
+  const int2 hv = a.heavy[blockIdx.x];
+  const int tile = hv.x;
+  const int ntile = a.tw * a.th;
+  const int c = tile / ntile, rem = tile - c * ntile;
+  const int ty = rem / a.tw, tx = rem - ty * a.tw;
+  const int pit = threadIdx.x;
+  const int px = tx * kTS + (pit & 15), py = ty * kTS + (pit >> 4);
+  if (px >= a.W || py >= a.H) return;
+  const int64_t tstart = a.offsets[tile];
+  const int64_t tend = (tile == a.n_tiles - 1) ? a.n_isects : (int64_t)a.offsets[tile + 1];
+  const int64_t sz = kTS * kTS;
+  float col[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d) col[d] = 0.f;
+  int32_t last = 0;
+  float Tf = 1.f;
+  bool fin = false;
+  int64_t cid = hv.y;
+  for (int64_t b = tstart; b < tend; b += a.SL, ++cid) {
+    const float *co = a.cout + cid * sz * (2 + D);
+    const float Te = co[pit];
+    last = max(last, __float_as_int(co[sz + pit]));
+#pragma unroll
+    for (int d = 0; d < D; ++d) col[d] += co[(2 + d) * sz + pit];
+    if (!fin) {
+      Tf = fabsf(Te);
+      fin = Te < 0.f;
+    }
+  }
+  const int64_t pix = ((int64_t)c * a.H + py) * a.W + px;
+  float *oc = a.render_colors + pix * D;
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    const float bg = a.backgrounds ? a.backgrounds[c * D + d] : 0.f;
+    oc[d] = col[d] + Tf * bg;
+  }
+  a.render_alphas[pix] = 1.f - Tf;
+  a.last_ids[pix] = last;
 }
 
 // Forward, two pixels per lane: a wave owns the 16x8 band of rows 8w..8w+7
@@ -1298,6 +1458,21 @@ unpack_kernel(int64_t G, int S, const float *__restrict__ packed, float *__restr
   if (ABS) *reinterpret_cast<float2 *>(v_abs + 2 * g) = make_float2(r[D + 6], r[D + 7]);
 }
 
+// The largest tile's isect count -> *out (lane 0 of the block; out may be
+// null): read back by the host on a LATER render to decide whether to split
+// heavy tiles (use_split_now), never for correctness.  Uses one barrier.
+GS_INLINE void block_max_out(int64_t v, int32_t *out) {
+  __shared__ int smax;
+  if (threadIdx.x == 0) smax = 0;
+  __syncthreads();
+  int x = (int)min(v, (int64_t)INT32_MAX);
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) x = max(x, __shfl_xor(x, o, 64));
+  if ((threadIdx.x & 63) == 0) atomicMax(&smax, x);
+  __syncthreads();
+  if (threadIdx.x == 0 && out) *out = smax;
+}
+
 // Forward dispatch order: tiles bucketed by isect count (>= 2048, >= 1024,
 // >= 512, the rest), heaviest bucket first and raster order inside a bucket,
 // so the longest tiles start in the first wave of workgroups instead of
@@ -1305,12 +1480,13 @@ unpack_kernel(int64_t G, int S, const float *__restrict__ packed, float *__restr
 // thread are packed into one u64 (16 bits each) for a single block scan.
 __global__ void __launch_bounds__(1024)
 tile_order_kernel(int n_tiles, const int32_t *__restrict__ offsets, int64_t n_isects,
-                  int32_t *__restrict__ order) {
+                  int32_t *__restrict__ order, int32_t *__restrict__ max_out) {
   constexpr int MAXPER = 16;  // tiles per thread (n_tiles <= 16384)
   __shared__ uint64_t wsum[16];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   int bucket[MAXPER];
   uint64_t mine = 0;
+  int64_t nmax = 0;
 #pragma unroll
   for (int i = 0; i < MAXPER; ++i) {
     const int t = tid + 1024 * i;
@@ -1318,10 +1494,12 @@ tile_order_kernel(int n_tiles, const int32_t *__restrict__ offsets, int64_t n_is
     if (t < n_tiles) {
       const int64_t e = (t == n_tiles - 1) ? n_isects : (int64_t)offsets[t + 1];
       const int64_t n = e - offsets[t];
+      nmax = max(nmax, n);
       bucket[i] = n >= 2048 ? 0 : n >= 1024 ? 1 : n >= 512 ? 2 : 3;
       mine += (uint64_t)1 << (16 * bucket[i]);
     }
   }
+  block_max_out(nmax, max_out);
   uint64_t x = mine;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
@@ -1458,6 +1636,115 @@ order_xcd_kernel(int n_tiles, const int32_t *__restrict__ offsets, int64_t n_ise
   }
 }
 
+// Forward plan with split heavy tiles.  A tile with more than `split` isects
+// (and not masked) is rendered as ceil(n / L) chunks that run in parallel
+// (fwd_prod_kernel -> fwd_kernel chunk items -> fwd_combine_kernel), so the
+// longest tiles no longer serialise the end of the launch.  Work items, in
+// dispatch order (tile_order_kernel's heaviest-first buckets, a chunk
+// counted as a tile of its length): unsplit tiles with >= 2048 isects, the
+// chunks, unsplit tiles with >= 1024, >= 512, the rest.  One 1024-lane
+// workgroup, 16 tiles per lane (n_tiles <= 16384).
+__global__ void __launch_bounds__(1024)
+fwd_plan_kernel(int n_tiles, const int32_t *__restrict__ offsets, int64_t n_isects,
+                const uint8_t *__restrict__ masks, int SL, int split, int32_t *__restrict__ hdr,
+                int2 *__restrict__ fitems, int2 *__restrict__ p1items,
+                int2 *__restrict__ heavy, int32_t *__restrict__ max_out) {
+  // quantities: [0] unsplit >= 2048, [1] chunks, [2] unsplit >= 1024,
+  // [3] unsplit >= 512, [4] unsplit rest, [5] split tiles
+  constexpr int PER = 16, NQ = 6;
+  __shared__ int wsum[16][NQ];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  // category and chunk count of tile t (recomputed in the write pass: keeps
+  // the 16 tiles' state out of registers)
+  auto classify = [&](int t, int &nch) -> int {
+    const int64_t e = (t == n_tiles - 1) ? n_isects : (int64_t)offsets[t + 1];
+    const int64_t n = e - offsets[t];
+    nch = 0;
+    if (n > split && !(masks && masks[t])) {
+      nch = (int)((n + SL - 1) / SL);
+      return 1;
+    }
+    return n >= 2048 ? 0 : n >= 1024 ? 2 : n >= 512 ? 3 : 4;
+  };
+  int mine[NQ] = {0, 0, 0, 0, 0, 0};
+  int64_t nmax = 0;
+  for (int i = 0; i < PER; ++i) {
+    const int t = tid + 1024 * i;
+    if (t >= n_tiles) break;
+    int nch;
+    const int kd = classify(t, nch);
+    const int64_t e = (t == n_tiles - 1) ? n_isects : (int64_t)offsets[t + 1];
+    nmax = max(nmax, e - offsets[t]);
+#pragma unroll
+    for (int q = 0; q < NQ; ++q)
+      mine[q] += (q == kd && kd != 1) ? 1 : (q == 1 ? nch : (q == 5 && kd == 1 ? 1 : 0));
+  }
+  block_max_out(nmax, max_out);
+  int x[NQ];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    x[q] = mine[q];
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(x[q], o, 64);
+      if (lane >= o) x[q] += y;
+    }
+  }
+  if (lane == 63) {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) wsum[w][q] = x[q];
+  }
+  __syncthreads();
+  int before[NQ], total[NQ];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    before[q] = x[q] - mine[q];
+    total[q] = 0;
+    for (int ww = 0; ww < 16; ++ww) {
+      before[q] += ww < w ? wsum[ww][q] : 0;
+      total[q] += wsum[ww][q];
+    }
+  }
+  // positions: fitems = the categories in order; p1items and heavy
+  int pos[5];
+  int base = 0;
+#pragma unroll
+  for (int q = 0; q < 5; ++q) {
+    pos[q] = base + before[q];
+    base += total[q];
+  }
+  int pP = before[1] - before[5], pH = before[5];  // p1 items: chunks minus one per split tile
+  for (int i = 0; i < PER; ++i) {
+    const int t = tid + 1024 * i;
+    if (t >= n_tiles) break;
+    int nch;
+    const int kd = classify(t, nch);
+    if (kd == 1) {
+      heavy[pH++] = make_int2(t, pos[1] - total[0]);
+      for (int k = 0; k < nch; ++k) {
+        fitems[pos[1]++] = make_int2(t, k);
+        if (k < nch - 1) p1items[pP++] = make_int2(t, k);
+      }
+    } else {
+      int p = pos[0];
+      p = kd == 2 ? pos[2] : p;
+      p = kd == 3 ? pos[3] : p;
+      p = kd == 4 ? pos[4] : p;
+      fitems[p] = make_int2(t, -1);
+      pos[0] += kd == 0;
+      pos[2] += kd == 2;
+      pos[3] += kd == 3;
+      pos[4] += kd == 4;
+    }
+  }
+  if (tid == 0) {
+    hdr[0] = total[0] + total[1] + total[2] + total[3] + total[4];
+    hdr[1] = total[1] - total[5];
+    hdr[2] = total[5];
+    hdr[3] = total[0];
+  }
+}
+
 // Backward work items.  A tile with n isects becomes ceil(n / L) items
 // (tile, k): the full-length chunks go to `full`, the shorter tails to `tail`
 // (the backward runs all full chunks first, so the longest items start
@@ -1591,9 +1878,125 @@ static bool use_xcd() {
   return v;
 }
 
+// Split heavy tiles in the forward (fwd_plan_kernel): a tile with more
+// isects than the threshold is rendered as parallel chunks of split_chunk()
+// isects, so that it no longer runs alone for the end of the launch.  Mode
+// (GSPLAT_HIP_FWD_SPLIT / gsplat_hip_debug_set_fwd_split): unset or < 0 =
+// adaptive, threshold max(2048, n_isects / GSPLAT_HIP_FWD_SPLIT_DIV (550)) --
+// a tile longer than ~1/550 of all isects outlasts the rest of the launch
+// (measured: at M3 the heaviest, 21 k-isect tile ran 415 us against 250 us
+// for 99 % of the waves; at M2 no tile passes it) -- and only when the
+// previous render had such a tile (use_split_now); > 0 = that fixed
+// threshold; 0 = off, the default.  Measured (chunks of 512, adaptive): M3
+// forward 0.584 -> 0.526 ms, but M2 0.183 -> 0.202 ms -- the product pass and
+// the combine are serialised launches on the critical path, which costs more
+// than the ~10 us tail of M2's heaviest tiles; M3 step time +1 %, M2 -1.5 %.
+static int g_fwd_split = INT32_MIN;  // not yet read from the environment
+
+static int fwd_split_mode() {
+  if (g_fwd_split == INT32_MIN) {
+    const char *e = getenv("GSPLAT_HIP_FWD_SPLIT");
+    g_fwd_split = e ? atoi(e) : 0;  // off by default (measured below)
+    if (g_fwd_split < 0) g_fwd_split = -1;
+  }
+  return g_fwd_split;
+}
+
+static int64_t split_threshold(int64_t n_isects) {
+  const int m = fwd_split_mode();
+  if (m > 0) return m;
+  static const int64_t div = [] {
+    const char *e = getenv("GSPLAT_HIP_FWD_SPLIT_DIV");
+    const int x = e ? atoi(e) : 550;
+    return (int64_t)(x > 0 ? x : 550);
+  }();
+  return std::max<int64_t>(2048, n_isects / div);
+}
+
+static int chunk_len();
+// Isects per chunk of a split tile (GSPLAT_HIP_FWD_SPLIT_CHUNK, default
+// 1024), a multiple of the backward's chunk length.
+static int split_chunk() {
+  static const int x = [] {
+    const char *e = getenv("GSPLAT_HIP_FWD_SPLIT_CHUNK");
+    return e ? atoi(e) : 1024;
+  }();
+  const int L = chunk_len();
+  return L > 0 ? std::max(L, (x + L - 1) / L * L) : 0;
+}
+
+// After the chunk slots and the tile order, the split area:
+// [hdr 64 B][fitems int2 x (n_tiles + n_isects/SL + 1)][p1items int2 x
+// (n_isects/SL + 1)][heavy int2 x n_tiles][prod f32 x (n_isects/L + 1) x 256,
+// by boundary slot][cout f32 x (n_tiles + n_isects/SL + 1) x 256 x (2 + D)],
+// each part 256-B aligned (chunks: sum over split tiles of ceil(n / SL) <=
+// n_tiles + n_isects / SL).
+struct SplitLayout {
+  int64_t hdr, fitems, p1, heavy, prod, cout, bytes;
+};
+
+static int64_t align256(int64_t x) { return (x + 255) / 256 * 256; }
+
+static int fwd_px();
+
+// The state has room for the split forward whenever it can run; whether a
+// render splits is decided per render (use_split_now).
+static bool split_capable(int n_tiles, int64_t n_isects) {
+  return fwd_split_mode() != 0 && chunk_len() > 0 && use_order(n_tiles, n_isects) &&
+         fwd_px() == 1;
+}
+
+// Largest tile of the most recent dispatch-order kernel, written by the
+// kernel into mapped pinned host memory (no copy, no sync).
+static int32_t *g_stat_host = nullptr, *g_stat_dev = nullptr;
+
+static int32_t *stat_dev() {
+  if (!g_stat_host) {
+    if (hipHostMalloc((void **)&g_stat_host, 64, hipHostMallocMapped) != hipSuccess) {
+      g_stat_host = nullptr;
+      return nullptr;
+    }
+    g_stat_host[0] = 0;
+    if (hipHostGetDevicePointer((void **)&g_stat_dev, g_stat_host, 0) != hipSuccess)
+      g_stat_dev = nullptr;
+  }
+  return g_stat_dev;
+}
+
+// Split this render?  Fixed mode: always; adaptive: when an earlier render's
+// largest tile exceeded this render's threshold (tiles are similar from one
+// training step to the next; a wrong guess costs speed only: an unsplit
+// render of a heavy tile, or the split passes' ~7 us with nothing to split).
+static bool use_split_now(int n_tiles, int64_t n_isects) {
+  if (!split_capable(n_tiles, n_isects)) return false;
+  if (fwd_split_mode() > 0) return true;
+  stat_dev();
+  const int32_t prev = g_stat_host ? *(volatile int32_t *)g_stat_host : 0;
+  return prev > split_threshold(n_isects);
+}
+
+static SplitLayout split_layout(int D, int n_tiles, int64_t n_isects) {
+  SplitLayout l{};
+  if (!split_capable(n_tiles, n_isects)) return l;
+  const int64_t nc = n_isects / chunk_len() + 1, ns = n_isects / split_chunk() + 1;
+  const int64_t px = r16::kTS * r16::kTS;
+  l.hdr = 0;
+  l.fitems = 256;
+  l.p1 = l.fitems + align256(8 * ((int64_t)n_tiles + ns));
+  l.heavy = l.p1 + align256(8 * ns);
+  l.prod = l.heavy + align256(8 * (int64_t)n_tiles);
+  l.cout = l.prod + align256(4 * nc * px);
+  l.bytes = l.cout + align256(4 * ((int64_t)n_tiles + ns) * px * (2 + D));
+  return l;
+}
+
+static int64_t order_bytes(int n_tiles, int64_t n_isects) {
+  return use_order(n_tiles, n_isects) ? align256(4 * ((int64_t)n_tiles + r16::kQueueInts)) : 0;
+}
+
 int64_t rasterize16_fwd_state_bytes(int D, int n_tiles, int64_t n_isects) {
-  const int64_t ob = use_order(n_tiles, n_isects) ? 4 * ((int64_t)n_tiles + r16::kQueueInts) : 0;
-  return chunk_slot_bytes(D, n_isects) + ob;
+  return chunk_slot_bytes(D, n_isects) + order_bytes(n_tiles, n_isects) +
+         split_layout(D, n_tiles, n_isects).bytes;
 }
 
 static int64_t n_items_bound(int n_tiles, int64_t n_isects) {
@@ -1653,22 +2056,62 @@ static int dbg_flags() {
 // forward call does not launch the order kernel again); cleared by the
 // forward that consumes it.  Same host thread, same stream.
 static thread_local const void *g_prepared_state = nullptr;
+static thread_local bool g_prepared_split = false;  // the split decision of that preparation
 
 static void launch_order(int n_tiles, const int32_t *offsets, int64_t n_isects, int32_t *order,
-                         hipStream_t st) {
-  if (use_xcd())
+                         hipStream_t st, char *split_base = nullptr, int D = 0) {
+  if (split_base) {
+    const SplitLayout l = split_layout(D, n_tiles, n_isects);
+    hipLaunchKernelGGL(r16::fwd_plan_kernel, dim3(1), dim3(1024), 0, st, n_tiles, offsets,
+                       n_isects, (const uint8_t *)nullptr, split_chunk(),
+                       (int)std::min<int64_t>(split_threshold(n_isects), INT32_MAX),
+                       reinterpret_cast<int32_t *>(split_base + l.hdr),
+                       reinterpret_cast<int2 *>(split_base + l.fitems),
+                       reinterpret_cast<int2 *>(split_base + l.p1),
+                       reinterpret_cast<int2 *>(split_base + l.heavy), stat_dev());
+  } else if (use_xcd())
     hipLaunchKernelGGL(r16::order_xcd_kernel, dim3(1), dim3(1024), 0, st, n_tiles, offsets,
                        n_isects, order, order + n_tiles);
   else
     hipLaunchKernelGGL(r16::tile_order_kernel, dim3(1), dim3(1024), 0, st, n_tiles, offsets,
-                       n_isects, order);
+                       n_isects, order, split_capable(n_tiles, n_isects) ? stat_dev() : nullptr);
 }
 
 template <int D>
-int r16_fwd(r16::Args a, const void *state, hipStream_t st) {
+int r16_fwd(r16::Args a, const void *state, char *split_base, hipStream_t st) {
   if (a.order && state != g_prepared_state)
-    launch_order(a.n_tiles, a.offsets, a.n_isects, const_cast<int32_t *>(a.order), st);
+    launch_order(a.n_tiles, a.offsets, a.n_isects, const_cast<int32_t *>(a.order), st, split_base,
+                 D);
   g_prepared_state = nullptr;
+  if (split_base) {
+    // split heavy tiles: chunk products, every work item (tiles and chunks),
+    // then the split tiles' pixels from their chunks; grids are upper bounds
+    // (the plan's counts are on the device; surplus workgroups exit)
+    const int64_t nc = a.n_isects / a.SL + 1;
+    const int64_t n_heavy_max =
+        std::min<int64_t>(a.n_tiles, a.n_isects / split_threshold(a.n_isects) + 1);
+    hipLaunchKernelGGL((r16::fwd_prod_kernel<D>), dim3((unsigned)std::min<int64_t>(nc, 2048)),
+                       dim3(256), 0, st, a);
+    if (fwd_unroll() == 1 && fwd_pf() == 0)
+      hipLaunchKernelGGL((r16::fwd_kernel<D, 1, 0>), dim3((unsigned)(a.n_tiles + nc)), dim3(256),
+                         0, st, a);
+    else if (fwd_unroll() == 1 && fwd_pf() == 2)
+      hipLaunchKernelGGL((r16::fwd_kernel<D, 1, 2>), dim3((unsigned)(a.n_tiles + nc)), dim3(256),
+                         0, st, a);
+    else if (fwd_unroll() == 1)
+      hipLaunchKernelGGL((r16::fwd_kernel<D, 1>), dim3((unsigned)(a.n_tiles + nc)), dim3(256), 0,
+                         st, a);
+    else if (fwd_unroll() == 2)
+      hipLaunchKernelGGL((r16::fwd_kernel<D, 2>), dim3((unsigned)(a.n_tiles + nc)), dim3(256), 0,
+                         st, a);
+    else
+      hipLaunchKernelGGL((r16::fwd_kernel<D, 4>), dim3((unsigned)(a.n_tiles + nc)), dim3(256), 0,
+                         st, a);
+    hipLaunchKernelGGL((r16::fwd_combine_kernel<D>), dim3((unsigned)n_heavy_max), dim3(256), 0, st,
+                       a);
+    GS_CHECK_LAUNCH("rasterize_fwd16_split");
+    return 0;
+  }
   if (fwd_px() == 2)
     hipLaunchKernelGGL((r16::fwd2_kernel<D>), dim3(a.n_tiles), dim3(128), 0, st, a);
   else if (fwd_unroll() == 1 && fwd_pf() == 0)
@@ -1756,15 +2199,31 @@ int rasterize16_fwd(int C, int D, int W, int H, int tw, int th, const float *mea
   a.state = (state && slots > 0) ? reinterpret_cast<float *>(state) : nullptr;
   a.order = (state && use_order(a.n_tiles, n_isects))
                 ? reinterpret_cast<int32_t *>(reinterpret_cast<char *>(state) + slots) : nullptr;
-  a.queue = (a.order && use_xcd()) ? const_cast<int32_t *>(a.order) + a.n_tiles : nullptr;
+  char *split_base = nullptr;
+  const bool split = state == g_prepared_state ? g_prepared_split
+                                               : use_split_now(a.n_tiles, n_isects);
+  if (a.order && a.state && split) {
+    split_base = reinterpret_cast<char *>(state) + slots + order_bytes(a.n_tiles, n_isects);
+    const SplitLayout l = split_layout(D, a.n_tiles, n_isects);
+    a.fcount = reinterpret_cast<const int32_t *>(split_base + l.hdr);
+    a.fitems = reinterpret_cast<const int2 *>(split_base + l.fitems);
+    a.p1items = reinterpret_cast<const int2 *>(split_base + l.p1);
+    a.heavy = reinterpret_cast<const int2 *>(split_base + l.heavy);
+    a.prod = reinterpret_cast<float *>(split_base + l.prod);
+    a.cout = reinterpret_cast<float *>(split_base + l.cout);
+    a.SL = split_chunk();
+    a.timeline = nullptr;  // per-wave stamps index blocks of the unsplit grid
+  }
+  a.queue = (a.order && use_xcd() && !split_base) ? const_cast<int32_t *>(a.order) + a.n_tiles
+                                                  : nullptr;
   switch (D) {
-    case 1: return r16_fwd<1>(a, state, st);
-    case 2: return r16_fwd<2>(a, state, st);
-    case 3: return r16_fwd<3>(a, state, st);
-    case 4: return r16_fwd<4>(a, state, st);
-    case 8: return r16_fwd<8>(a, state, st);
-    case 16: return r16_fwd<16>(a, state, st);
-    case 32: return r16_fwd<32>(a, state, st);
+    case 1: return r16_fwd<1>(a, state, split_base, st);
+    case 2: return r16_fwd<2>(a, state, split_base, st);
+    case 3: return r16_fwd<3>(a, state, split_base, st);
+    case 4: return r16_fwd<4>(a, state, split_base, st);
+    case 8: return r16_fwd<8>(a, state, split_base, st);
+    case 16: return r16_fwd<16>(a, state, split_base, st);
+    case 32: return r16_fwd<32>(a, state, split_base, st);
   }
   GS_REQUIRE(false, "rasterize16_fwd: unsupported channels %d", D);
 }
@@ -1775,11 +2234,14 @@ int rasterize16_prepare(int D, int n_tiles, const int32_t *offsets, int64_t n_is
   if (!state || !use_order(n_tiles, n_isects)) return 0;
   GS_REQUIRE(state_bytes >= rasterize16_fwd_state_bytes(D, n_tiles, n_isects),
              "rasterize_prepare: state too small");
-  int32_t *order = reinterpret_cast<int32_t *>(reinterpret_cast<char *>(state) +
-                                               chunk_slot_bytes(D, n_isects));
-  launch_order(n_tiles, offsets, n_isects, order, st);
+  char *base = reinterpret_cast<char *>(state) + chunk_slot_bytes(D, n_isects);
+  int32_t *order = reinterpret_cast<int32_t *>(base);
+  const bool split = chunk_slot_bytes(D, n_isects) > 0 && use_split_now(n_tiles, n_isects);
+  launch_order(n_tiles, offsets, n_isects, order, st,
+               split ? base + order_bytes(n_tiles, n_isects) : nullptr, D);
   GS_CHECK_LAUNCH("rasterize_prepare");
   g_prepared_state = state;
+  g_prepared_split = split;
   return 0;
 }
 
@@ -1829,6 +2291,12 @@ int rasterize16_bwd(int C, int64_t G, int D, int W, int H, int tw, int th,
 }
 
 }  // namespace gs
+
+extern "C" int gsplat_hip_debug_set_fwd_split(int isects) {
+  const int old = gs::fwd_split_mode();
+  gs::g_fwd_split = isects < 0 ? -1 : isects;
+  return old;
+}
 
 extern "C" int gsplat_hip_debug_set_chunk(int isects) {
   gs::g_chunk = isects <= 0 ? 0 : ((isects + 63) / 64) * 64;

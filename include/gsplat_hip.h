@@ -252,6 +252,13 @@ int gsplat_hip_debug_set_lane_histogram(unsigned long long *device_buffer);
  * GSPLAT_HIP_CHUNK environment variable.  Forward and backward of one
  * rasterization must run with the same setting. */
 int gsplat_hip_debug_set_chunk(int isects);
+/* Split mode of the 16x16 forward: tiles with more isects than the
+ * threshold are rendered as parallel chunks.  isects > 0: that threshold;
+ * 0: off (the default); < 0: adaptive (max(2048, n_isects / 550) when the
+ * previous render had a tile above it), or
+ * GSPLAT_HIP_FWD_SPLIT).  Returns the previous mode.  Results do not depend
+ * on it beyond the float rounding of the chunks' transmittance products. */
+int gsplat_hip_debug_set_fwd_split(int isects);
 
 /* ---------------------------------------------------------------------------
  * Trainer-side kernels of the training step (not part of the 5-function

@@ -367,7 +367,10 @@ def test_raster_chunked_backward(chunk):
     vra = torch.randn(C, H, W, 1, generator=g).to(DEV)
 
     def run(L):
+        # the unsplit forward (its colours are the same up to the chunk sums'
+        # rounding); the split forward is tested in test_gpu_raster_dispatch
         _lib.query("gsplat_hip_debug_set_chunk", L)
+        split = _lib.query("gsplat_hip_debug_set_fwd_split", 0)
         try:
             ins = [x.detach().clone().requires_grad_(True) for x in (m2, cn, cols, ops)]
             rc, ra = gsplat_hip.rasterize_to_pixels(*ins, W, H, 16, off, fids, backgrounds=bg)
@@ -375,6 +378,7 @@ def test_raster_chunked_backward(chunk):
                                         retain_graph=True)
         finally:
             _lib.query("gsplat_hip_debug_set_chunk", 256)  # the library default
+            _lib.query("gsplat_hip_debug_set_fwd_split", split)
         return rc, ra, grads
 
     rc0, ra0, g0 = run(0)

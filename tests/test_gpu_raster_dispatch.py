@@ -115,3 +115,77 @@ def test_xcd_order_is_banded_permutation():
     seg_work = np.array(seg_work, dtype=np.float64)
     # bands of equal work up to one tile's work
     assert np.all(np.abs(seg_work - work.sum() / 8) <= work.max() + 1), seg_work
+
+
+def _heavy_scene(N=60000, W=320, H=240, seed=5):
+    """Many large Gaussians over a small image: tiles with thousands of isects."""
+    g = torch.Generator().manual_seed(seed)
+    means = torch.randn(N, 3, generator=g) * torch.tensor([1.0, 0.8, 0.5])
+    means[:, 2] += 5.0
+    quats = torch.randn(N, 4, generator=g)
+    scales = torch.rand(N, 3, generator=g) * 0.12 + 0.01
+    opac = torch.rand(N, generator=g) * 0.3  # low opacity: long tiles before saturation
+    colors = torch.rand(N, 3, generator=g)
+    vm = torch.eye(4)[None]
+    K = torch.tensor([[300.0, 0, W / 2], [0, 300.0, H / 2], [0, 0, 1]])[None]
+    return [x.to(DEV) for x in (means, quats, scales, opac, colors, vm, K)], W, H
+
+
+def _render_split(ins, W, H, split, mode="RGB"):
+    from gsplat_hip import _lib
+    old = _lib.query("gsplat_hip_debug_set_fwd_split", split)
+    try:
+        return _render(ins, W, H, True, mode)
+    finally:
+        _lib.query("gsplat_hip_debug_set_fwd_split", old)
+
+
+@pytest.mark.parametrize("split,mode", [(2048, "RGB"), (300, "RGB+D"), (64, "RGB")])
+def test_split_forward_matches_unsplit(split, mode):
+    """Tiles above `split` isects rendered as parallel chunks (transmittance
+    products, chunk compositing, combine) give the unsplit forward's images up
+    to the float rounding of the chunk products (and the threshold flips it can
+    cause), and the backward -- which reads the chunk state the split forward
+    writes -- the same gradients."""
+    ins, W, H = _heavy_scene()
+    rc0, ra0, m0, g0 = _render_split(ins, W, H, 0, mode)
+    rc1, ra1, m1, g1 = _render_split(ins, W, H, split, mode)
+    offs = m0["isect_offsets"].flatten().long()
+    n = m0["flatten_ids"].numel()
+    cnt = torch.diff(torch.cat([offs, torch.tensor([n], device=DEV)]))
+    assert int((cnt > split).sum()) >= 4, "scene has too few heavy tiles"
+    from test_gpu_parity import close_most
+    close_most(rc1, rc0, 1e-5, 1e-5, "colors", max_frac=1e-3)
+    close_most(ra1, ra0, 1e-5, 1e-5, "alphas", max_frac=1e-3)
+    for a, b, name in zip(g1, g0, ["means", "quats", "scales", "opacities", "colors"]):
+        scale = max(1e-12, float(b.abs().max()))
+        close_most(a, b, 1e-3, 1e-4 * scale, name, max_frac=2e-3, rows=True,
+                   out_bound=0.05 * scale)
+
+
+def test_split_forward_vs_oracle():
+    """The split forward against the CPU oracle on a scene with heavy tiles."""
+    import numpy as np
+    from oracle import gsplat_oracle as O
+    from gsplat_hip import _lib
+    import gsplat_hip
+    default = _lib.query("gsplat_hip_debug_set_fwd_split", 200)
+    try:
+        ins, W, H = _heavy_scene(N=20000, W=128, H=96, seed=7)
+        with torch.no_grad():
+            rc, ra, meta = gsplat_hip.rasterization(*ins[:5], ins[5], ins[6], W, H, packed=False)
+    finally:
+        _lib.query("gsplat_hip_debug_set_fwd_split", default)
+    offs = meta["isect_offsets"].cpu().numpy()
+    fids = meta["flatten_ids"].cpu().numpy()
+    n = fids.size
+    cnt = np.diff(np.concatenate([offs.ravel(), [n]]))
+    assert (cnt > 200).sum() >= 4
+    m2 = meta["means2d"].cpu().numpy()
+    cn = meta["conics"].cpu().numpy()
+    op = meta["opacities"].cpu().numpy()
+    cols = ins[4].cpu().numpy()[None]
+    oc, oa, _ = O.raster_fwd(m2, cn, cols, op, None, W, H, 16, offs, fids)
+    from test_gpu_parity import close_most
+    close_most(ra, oa, 1e-4, 1e-4, "alphas", max_frac=1e-3)
+    close_most(rc, oc, 1e-4, 1e-4, "colors", max_frac=1e-3)
