@@ -43,7 +43,7 @@ import torch.nn.functional as F
 
 from . import densify
 from .densify import DefaultStrategyConfig
-from .losses import FusedAdam, l1_ssim_loss
+from .losses import FusedAdam, l1_ssim_loss, ssim_and_l1
 from .rendering import rasterization, rasterization_2dgs
 from .strategy import activate, update_state_
 
@@ -344,6 +344,35 @@ class Trainer:
         if self.strategy is not None:
             self.post_step(it)
         return loss
+
+    # ---------------------------------------------------------------- eval
+    @torch.no_grad()
+    def evaluate(self, cameras=None, viewmats=None, Ks=None, images=None):
+        """simple_trainer.py:854-932's eval metrics: render each camera,
+        clamp to [0, 1], PSNR (data range 1) and SSIM (11x11 Gaussian, the
+        fused "valid" SSIM of the loss) against the target, averaged.  Either
+        indices into the trainer's camera pool / targets, or explicit
+        viewmats [M,4,4], Ks [M,3,3] and images [M,H,W,3].  LPIPS is not
+        computed (its network weights are a download)."""
+        self.sync()
+        if viewmats is None:
+            idx = list(range(len(self.viewmats))) if cameras is None else list(cameras)
+            viewmats, Ks, images = self.viewmats[idx], self.Ks[idx], self.targets[idx]
+        psnrs, ssims = [], []
+        saved = self.viewmats, self.Ks
+        try:
+            self.viewmats, self.Ks = viewmats.to(self.device), Ks.to(self.device)
+            for i in range(len(viewmats)):
+                colors, _, _ = self.render(i)
+                colors = torch.clamp(colors, 0.0, 1.0)
+                gt = images[i:i + 1].to(self.device)
+                mse = torch.mean((colors - gt) ** 2)
+                psnrs.append(float(-10.0 * torch.log10(mse)))
+                ssims.append(float(ssim_and_l1(colors, gt)[0]))
+        finally:
+            self.viewmats, self.Ks = saved
+        return {"psnr": sum(psnrs) / len(psnrs), "ssim": sum(ssims) / len(ssims),
+                "num_images": len(psnrs)}
 
     # ------------------------------------------------------------ strategy
     def post_step(self, it: int):

@@ -185,3 +185,30 @@ def _densification_schedule(sharded):
         - tr.refine_log[0][3], tr.refine_log
     assert tr.refine_log[0][1] + tr.refine_log[0][2] > 0  # random targets: something grows
     tr.sync()
+
+
+def test_trainer_evaluate_psnr_ssim():
+    """Trainer.evaluate (simple_trainer.py:854-932 metrics): PSNR of the
+    clamped render equals -10 log10(MSE) computed here, SSIM is the fused
+    valid SSIM; a target equal to the render gives SSIM 1 and a huge PSNR."""
+    from gsplat_hip.losses import ssim_and_l1
+    from gsplat_hip.train_step import Trainer
+    means, rgbs, vm, K, W, H = _small_scene()
+    tr = Trainer(means, rgbs, vm, K, W, H, device="cuda")
+    for it in range(3):
+        tr.step(it)
+    m = tr.evaluate([0, 2])
+    with torch.no_grad():
+        ps, ss = [], []
+        for ci in (0, 2):
+            c, _, _ = tr.render(ci)
+            c = c.clamp(0, 1)
+            gt = tr.targets[ci:ci + 1]
+            ps.append(float(-10 * torch.log10(((c - gt) ** 2).mean())))
+            ss.append(float(ssim_and_l1(c, gt)[0]))
+    assert m["num_images"] == 2
+    assert abs(m["psnr"] - sum(ps) / 2) < 1e-4 and abs(m["ssim"] - sum(ss) / 2) < 1e-5
+    with torch.no_grad():
+        c, _, _ = tr.render(1)
+    same = tr.evaluate(viewmats=vm[1:2], Ks=K[1:2], images=c.clamp(0, 1).cpu())
+    assert same["ssim"] > 0.999 and same["psnr"] > 60
