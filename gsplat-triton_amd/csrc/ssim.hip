@@ -233,6 +233,106 @@ fwd_kernel(int B, int H, int W, int C, const float *__restrict__ x, const float 
   }
 }
 
+// Forward, all C channels of a 32x32 map tile in one workgroup: the 42-row
+// window of both images is loaded as 42 contiguous runs of 42*C floats (the
+// [H, W, C] rows: coalesced, every load of the three channels in flight at
+// once), then each channel is staged to LDS from registers and blurred in
+// turn.  One workgroup per (tile, image) instead of per (tile, image,
+// channel): a third of the prologues and of the load-latency rounds.
+// Partials: one (ssim, l1) pair per workgroup, channels summed.
+template <int C>
+__global__ void __launch_bounds__(256)
+fwd_c_kernel(int B, int H, int W, const float *__restrict__ x, const float *__restrict__ y,
+             float *__restrict__ maps, float *__restrict__ partials) {
+  constexpr int SPAN = WN * C;             // floats per window row
+  constexpr int PER_ROW = (SPAN + 63) / 64;  // loads per lane per row
+  __shared__ f2v s_xy[WN][WN];
+  __shared__ f2v h_xy[WN][TW], h_sq[WN][TW];
+  __shared__ float h_p[WN][TW];
+  __shared__ float red[2][4];
+  const int Hm = H - 2 * R, Wm = W - 2 * R;
+  const int tx = (Wm + TW - 1) / TW, ty = (Hm + TW - 1) / TW;
+  const int t = blockIdx.x % (tx * ty), b = blockIdx.x / (tx * ty);
+  if (b >= B) return;
+  const int mi0 = (t / tx) * TW, mj0 = (t % tx) * TW;
+  const int tid = threadIdx.x, tq = tid & 31, tr = tid >> 5;
+  const int lane = tid & 63, w4 = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t plane = (int64_t)Hm * Wm;
+  const int ri1 = (mi0 + TW >= Hm) ? H - mi0 : TW;  // image rows / cols this tile owns for L1
+  const int rj1 = (mj0 + TW >= Wm) ? W - mj0 : TW;
+  float vx[kRows][PER_ROW], vy[kRows][PER_ROW];
+#pragma unroll
+  for (int k = 0; k < kRows; ++k) {
+    const int r = w4 + 4 * k, gi = min(mi0 + r, H - 1);
+    const int64_t row0 = (((int64_t)b * H + gi) * W + mj0) * C;
+#pragma unroll
+    for (int q = 0; q < PER_ROW; ++q) {
+      const int e = lane + 64 * q;
+      const int gj = mj0 + e / C;
+      const int64_t off = gj < W ? row0 + e : row0;  // clamped: loads are unconditional
+      vx[k][q] = x[off];
+      vy[k][q] = y[off];
+    }
+  }
+  float lsum = 0.f, ssum = 0.f;
+#pragma unroll
+  for (int k = 0; k < kRows; ++k) {
+    const int r = w4 + 4 * k;
+#pragma unroll
+    for (int q = 0; q < PER_ROW; ++q) {
+      const int e = lane + 64 * q, col = e / C;
+      const bool ok = r < WN && e < SPAN && mi0 + r < H && mj0 + col < W;
+      vx[k][q] = ok ? vx[k][q] : 0.f;
+      vy[k][q] = ok ? vy[k][q] : 0.f;
+      if (ok && r < ri1 && col < rj1) lsum += fabsf(vx[k][q] - vy[k][q]);
+    }
+  }
+  for (int c = 0; c < C; ++c) {
+#pragma unroll
+    for (int k = 0; k < kRows; ++k) {
+      const int r = w4 + 4 * k;
+#pragma unroll
+      for (int q = 0; q < PER_ROW; ++q) {
+        const int e = lane + 64 * q;
+        if (r < WN && e < SPAN && e % C == c) s_xy[r][e / C] = f2v{vx[k][q], vy[k][q]};
+      }
+    }
+    __syncthreads();
+    Blur3 o;
+    blur_xy(s_xy, h_xy, h_sq, h_p, tid, o);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int mi = mi0 + 4 * tr + j, mj = mj0 + tq;
+      if (mi < Hm && mj < Wm) {
+        const float m1 = o.a[j].x, m2 = o.a[j].y;
+        const float s11 = o.b[j].x - m1 * m1, s22 = o.b[j].y - m2 * m2, s12 = o.c[j] - m1 * m2;
+        const float A1 = 2.f * m1 * m2 + C1, A2 = 2.f * s12 + C2;
+        const float B1 = m1 * m1 + m2 * m2 + C1, B2 = s11 + s22 + C2;
+        const float inv = 1.f / (B1 * B2);
+        const float sv = A1 * A2 * inv;
+        ssum += sv;
+        const float dN = 2.f * m2 * (A2 - A1), dD = 2.f * m1 * (B2 - B1);
+        float *mp = maps + (((int64_t)b * C + c) * 3) * plane + (int64_t)mi * Wm + mj;
+        mp[0] = (dN - sv * dD) * inv;
+        mp[plane] = -sv * B1 * inv;
+        mp[2 * plane] = 2.f * A1 * inv;
+      }
+    }
+    __syncthreads();  // s_xy / h_* are rewritten for the next channel
+  }
+  ssum = wave_sum(ssum);
+  lsum = wave_sum(lsum);
+  if ((tid & 63) == 0) {
+    red[0][tid >> 6] = ssum;
+    red[1][tid >> 6] = lsum;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    partials[2 * blockIdx.x] = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+    partials[2 * blockIdx.x + 1] = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+  }
+}
+
 // Deterministic sum of the per-workgroup partials -> sums[2].
 // With loss != nullptr also loss[0..2] = (w_l1 L1/n_img + lam (1 - S/n_map),
 // S/n_map, L1/n_img).
@@ -366,6 +466,16 @@ extern "C" int64_t gsplat_hip_ssim_workspace_bytes(int B, int H, int W, int C) {
 static float n_map(int B, int H, int W, int C) { return (float)B * C * (H - 10) * (W - 10); }
 static float n_img(int B, int H, int W, int C) { return (float)B * C * H * W; }
 
+// The forward with all channels of a tile in one workgroup (fwd_c_kernel, C = 3);
+// GSPLAT_HIP_SSIM_PER_IMAGE=0 selects the one-channel-per-workgroup kernel.
+static bool ssim_per_image() {
+  static const bool v = [] {
+    const char *e = getenv("GSPLAT_HIP_SSIM_PER_IMAGE");
+    return !(e && atoi(e) == 0);
+  }();
+  return v;
+}
+
 static int ssim_fwd(int B, int H, int W, int C, const float *img1, const float *img2,
                     float *sums, float *loss, float lam, void *workspace, void *stream) {
   GS_REQUIRE(B > 0 && C > 0 && H > 10 && W > 10,
@@ -373,11 +483,19 @@ static int ssim_fwd(int B, int H, int W, int C, const float *img1, const float *
   hipStream_t st = (hipStream_t)stream;
   float *maps = reinterpret_cast<float *>(workspace);
   float *partials = maps + ssim_map_floats(B, H, W, C);
-  hipLaunchKernelGGL(ssim::fwd_kernel, ssim_grid(B, H, W, C, true), dim3(256), 0, st, B, H, W, C, img1, img2, maps,
-                     partials);
-  hipLaunchKernelGGL(ssim::reduce_partials_kernel, dim3(1), dim3(1024), 0, st,
-                     (int)ssim_blocks(B, H, W, C), partials, sums, loss, lam, n_map(B, H, W, C),
-                     n_img(B, H, W, C));
+  const int n_tiles = ((W - 10 + 31) / 32) * ((H - 10 + 31) / 32);
+  if (C == 3 && ssim_per_image()) {
+    hipLaunchKernelGGL(ssim::fwd_c_kernel<3>, dim3((unsigned)(n_tiles * B)), dim3(256), 0, st, B,
+                       H, W, img1, img2, maps, partials);
+    hipLaunchKernelGGL(ssim::reduce_partials_kernel, dim3(1), dim3(1024), 0, st, n_tiles * B,
+                       partials, sums, loss, lam, n_map(B, H, W, C), n_img(B, H, W, C));
+  } else {
+    hipLaunchKernelGGL(ssim::fwd_kernel, ssim_grid(B, H, W, C, true), dim3(256), 0, st, B, H, W,
+                       C, img1, img2, maps, partials);
+    hipLaunchKernelGGL(ssim::reduce_partials_kernel, dim3(1), dim3(1024), 0, st,
+                       (int)ssim_blocks(B, H, W, C), partials, sums, loss, lam, n_map(B, H, W, C),
+                       n_img(B, H, W, C));
+  }
   GS_CHECK_LAUNCH("ssim_l1_fwd");
   return 0;
 }
