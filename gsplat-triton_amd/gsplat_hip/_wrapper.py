@@ -291,6 +291,8 @@ ISECT_SORT = os.environ.get("GSPLAT_HIP_ISECT_SORT", "depth_first")
 # 16x16 rasterizer gathers from packed 64-B render records (GSPLAT_HIP_RECORDS=0:
 # from the four attribute arrays, as before ABI 15)
 RECORDS = os.environ.get("GSPLAT_HIP_RECORDS", "1") != "0"
+# longest busy-poll of the n_isects copy before a blocking event wait (s)
+SPIN_S = float(os.environ.get("GSPLAT_HIP_SYNC_SPIN_US", "2000")) * 1e-6
 
 
 @torch.no_grad()
@@ -376,7 +378,7 @@ class _IsectCount:
         host = torch.empty(2, dtype=torch.int64, pin_memory=True)
         host.copy_(totals, non_blocking=True)
         self.host, self.totals = host, totals
-        self.event = torch.cuda.Event()
+        self.event = torch.cuda.Event(blocking=True)
         self.event.record()
 
     @torch.no_grad()
@@ -386,8 +388,15 @@ class _IsectCount:
         dev, st = means2d.device, _stream()
         tpg, ws = self.tpg, self.ws
         # the single host sync (isect_tiles.py:102); polling reacts within a
-        # few us where hipEventSynchronize's blocking wait took ~100 us
+        # few us where hipEventSynchronize's blocking wait took ~100 us, so
+        # poll for up to SPIN_S (the counts normally land well inside it),
+        # then park the thread in the blocking-sync event wait instead of
+        # holding a core when the stream is deep in other work
+        t_end = time.perf_counter() + SPIN_S
         while not self.event.query():
+            if time.perf_counter() > t_end:
+                self.event.synchronize()
+                break
             time.sleep(0)  # yields the core (and the GIL) between polls
         n_isects, n_visible = self.host.tolist()
         isect_ids = torch.empty(n_isects, dtype=torch.int64, device=dev)

@@ -419,7 +419,7 @@ class Dataset:
             raise NotImplementedError("undistortion of a non-pinhole COLMAP camera needs "
                                       "OpenCV's remap (colmap.py:364-372), not in this image")
         with PILImage.open(self.parser.image_paths[index]) as img:
-            image = np.asarray(img.convert("RGB"))
+            image = np.array(img.convert("RGB"))
         K = self.parser.Ks_dict[cid].copy()
         if self.patch_size is not None:
             h, w = image.shape[:2]

@@ -9,6 +9,7 @@ groups in one kernel (csrc/adam.hip).
 
 import ctypes
 import math
+import os
 
 import torch
 
@@ -79,8 +80,49 @@ class _L1SSIMLoss(torch.autograd.Function):
         return grad, None, None
 
 
-def l1_ssim_loss(img, gt, ssim_lambda=0.2):
-    """(1 - ssim_lambda) * mean L1 + ssim_lambda * (1 - mean SSIM_valid)."""
+class _L1SSIMLossFused(torch.autograd.Function):
+    """The same loss with dloss/dimg computed in the forward launch
+    (csrc/ssim.hip fused_kernel); the backward scales it by the incoming
+    gradient.  The training path: no per-pixel SSIM partials through HBM."""
+
+    @staticmethod
+    def forward(ctx, img, gt, lam):
+        assert img.dim() == 4 and img.shape == gt.shape, (img.shape, gt.shape)
+        img = img.contiguous().float()
+        gt = gt.contiguous().float()
+        B, H, W, C = img.shape
+        ws = torch.empty(max(int(_lib.query("gsplat_hip_l1_ssim_loss_fused_workspace_bytes",
+                                            B, H, W, C)), 4),
+                         dtype=torch.uint8, device=img.device)
+        out = torch.empty(3, device=img.device)
+        unit = torch.empty_like(img)
+        _lib.call("gsplat_hip_l1_ssim_loss_fused_fwd", B, H, W, C, _ptr(img), _ptr(gt),
+                  ctypes.c_float(lam), _ptr(out), _ptr(unit), _ptr(ws), _stream())
+        ctx.save_for_backward(unit)
+        return out[0]
+
+    @staticmethod
+    def backward(ctx, g_loss):
+        (unit,) = ctx.saved_tensors
+        g_loss = g_loss.float().contiguous()
+        grad = torch.empty_like(unit)
+        _lib.call("gsplat_hip_l1_ssim_loss_fused_bwd", unit.numel(), _ptr(unit), _ptr(g_loss),
+                  _ptr(grad), _stream())
+        return grad, None, None
+
+
+# GSPLAT_HIP_SSIM_FUSED=0: the two-pass loss (partials to HBM) for training too
+SSIM_FUSED = os.environ.get("GSPLAT_HIP_SSIM_FUSED", "1") != "0"
+
+
+def l1_ssim_loss(img, gt, ssim_lambda=0.2, fused=None):
+    """(1 - ssim_lambda) * mean L1 + ssim_lambda * (1 - mean SSIM_valid).
+    With a gradient to compute (and C in {1, 3}) the one-pass fused kernel
+    runs, unless `fused=False` (or GSPLAT_HIP_SSIM_FUSED=0)."""
+    if fused is None:
+        fused = SSIM_FUSED and torch.is_grad_enabled() and img.requires_grad
+    if fused and img.dim() == 4 and img.shape[-1] in (1, 3):
+        return _L1SSIMLossFused.apply(img, gt, float(ssim_lambda))
     return _L1SSIMLoss.apply(img, gt, float(ssim_lambda))
 
 

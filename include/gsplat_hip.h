@@ -287,6 +287,19 @@ int gsplat_hip_l1_ssim_loss_fwd(int B, int H, int W, int C, const float *img1,
 int gsplat_hip_l1_ssim_loss_bwd(int B, int H, int W, int C, const float *img1,
                                 const float *img2, const void *workspace, float lam,
                                 const float *g_loss, float *grad_img1, void *stream);
+/* The same loss with its gradient computed in the forward pass (ABI 16), the
+ * training path: one kernel per 32x32 image tile recomputes the SSIM map
+ * partials of the map pixels its pixels depend on and blurs them back, so no
+ * per-pixel partials reach HBM.  C is 1 or 3.
+ * fused_fwd: out[0..2] as l1_ssim_loss_fwd; grad_unit [B,H,W,C] = dout[0]/dimg1;
+ *            workspace = gsplat_hip_l1_ssim_loss_fused_workspace_bytes.
+ * fused_bwd: grad_img1[i] = g_loss[0] * grad_unit[i] (16-B aligned buffers). */
+int64_t gsplat_hip_l1_ssim_loss_fused_workspace_bytes(int B, int H, int W, int C);
+int gsplat_hip_l1_ssim_loss_fused_fwd(int B, int H, int W, int C, const float *img1,
+                                      const float *img2, float lam, float *out,
+                                      float *grad_unit, void *workspace, void *stream);
+int gsplat_hip_l1_ssim_loss_fused_bwd(int64_t n, const float *grad_unit, const float *g_loss,
+                                      float *grad_img1, void *stream);
 
 /* DefaultStrategy._update_state for packed=False (gsplat/strategy/default.py:
  * 213-262): for every (c, g) with radii[c,g] > 0, in camera order,

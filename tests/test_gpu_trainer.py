@@ -34,16 +34,20 @@ def test_ssim_l1_matches_torch(B, H, W, C):
     torch.testing.assert_close(img.grad, img_r.grad, rtol=1e-3, atol=1e-8)
 
 
-@pytest.mark.parametrize("B,H,W,C,lam", [(1, 64, 80, 3, 0.2), (2, 37, 131, 3, 0.5), (1, 1080, 1920, 3, 0.2)])
-def test_l1_ssim_loss_matches_torch(B, H, W, C, lam):
-    """The one-launch-pair loss equals the simple_trainer.py:642-646 formula
-    evaluated with torch ops on the conv SSIM."""
+@pytest.mark.parametrize("fused", [False, True])
+@pytest.mark.parametrize("B,H,W,C,lam", [(1, 64, 80, 3, 0.2), (2, 37, 131, 3, 0.5),
+                                         (1, 1080, 1920, 3, 0.2), (1, 11, 11, 1, 0.3),
+                                         (3, 45, 33, 1, 0.2), (1, 100, 12, 3, 0.8)])
+def test_l1_ssim_loss_matches_torch(B, H, W, C, lam, fused):
+    """The one-launch-pair loss (and the one-pass fused loss + gradient)
+    equals the simple_trainer.py:642-646 formula evaluated with torch ops on
+    the conv SSIM."""
     from gsplat_hip.losses import l1_ssim_loss
     from gsplat_hip.train_step import ssim
     g = torch.Generator(device="cuda").manual_seed(W + C)
     img = torch.rand(B, H, W, C, device="cuda", generator=g).requires_grad_(True)
     gt = torch.rand(B, H, W, C, device="cuda", generator=g)
-    loss = l1_ssim_loss(img, gt, lam)
+    loss = l1_ssim_loss(img, gt, lam, fused=fused)
     img_r = img.detach().clone().requires_grad_(True)
     s_r = ssim(img_r.permute(0, 3, 1, 2), gt.permute(0, 3, 1, 2))
     loss_r = (img_r - gt).abs().mean() * (1 - lam) + (1 - s_r) * lam
@@ -52,6 +56,30 @@ def test_l1_ssim_loss_matches_torch(B, H, W, C, lam):
     (2.5 * loss).backward()
     (2.5 * loss_r).backward()
     torch.testing.assert_close(img.grad, img_r.grad, rtol=1e-3, atol=1e-9)
+
+
+def test_fused_loss_matches_two_pass_on_renders():
+    """Fused vs two-pass loss on a smooth, correlated image pair (a render
+    and a shifted copy, as in training): same loss, same gradient up to the
+    summation order of the blurs, and a second backward gives the same."""
+    from gsplat_hip.losses import l1_ssim_loss
+    g = torch.Generator(device="cuda").manual_seed(4)
+    base = torch.nn.functional.avg_pool2d(torch.rand(1, 3, 300, 420, device="cuda",
+                                                     generator=g), 5, 1, 2)
+    img = base[:, :, :, 2:].permute(0, 2, 3, 1).contiguous()
+    gt = base[:, :, :, :-2].permute(0, 2, 3, 1).contiguous()
+    a = img.clone().requires_grad_(True)
+    b = img.clone().requires_grad_(True)
+    la = l1_ssim_loss(a, gt, 0.2, fused=True)
+    lb = l1_ssim_loss(b, gt, 0.2, fused=False)
+    torch.testing.assert_close(la, lb, rtol=1e-5, atol=1e-6)
+    (3.0 * la).backward(retain_graph=True)
+    (3.0 * lb).backward()
+    torch.testing.assert_close(a.grad, b.grad, rtol=1e-4, atol=1e-10)
+    g1 = a.grad.clone()
+    a.grad = None
+    (3.0 * la).backward()
+    assert torch.equal(a.grad, g1)
 
 
 def test_fused_adam_matches_torch():
