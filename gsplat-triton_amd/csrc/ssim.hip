@@ -455,32 +455,45 @@ bwd_kernel(int B, int H, int W, int C, const float *__restrict__ x, const float 
 // The map pixels of the tile's own 32x32 range (every map pixel has exactly
 // one) feed the loss sum.  Against fwd (maps to HBM) + bwd (maps back) it
 // trades a 1.7x recompute of the map statistics for 150 MB less traffic at
-// 1080p and one launch less; the gradient is for dL/dloss = 1 and the
-// backward only scales it (fused_scale_kernel).
+// 1080p, one launch and the 75 MB map workspace less; the gradient is for
+// dL/dloss = 1 and the backward only scales it (fused_scale_kernel).
+// Measured at 1080p RGB (profiles/r2_s4_ssim): 117.6 us vs 55 + 62 us for
+// the pair -- parity, not a win: the kernel is neither HBM- nor VALU-bound
+// (VALU issue ~0.3, ~42 % of wave cycles waiting on the per-channel window
+// loads and the four barriers per channel at 2 workgroups per CU).
 constexpr int FT = 32, FM = FT + 2 * R, FI = FM + 2 * R;  // 32, 42, 52
 constexpr int kFThreads = 512, kFRows = (FI + 7) / 8;     // window rows per wave
-// LDS: s_xy f2v[FI][FI] | hA f2v[FI][FM] | hB f2v[FI][FM] | hC float[FI][FM];
-// the maps (f2v[FM][FM] + float[FM][FM]) reuse hB/hC, the backward's
-// horizontal pass (f2v[FM][FT] + float[FM][FT]) reuses hA.
-constexpr int kOffA = FI * FI * 8, kOffB = kOffA + FI * FM * 8, kOffC = kOffB + FI * FM * 8;
-constexpr int kFusedLds = kOffC + FI * FM * 4;
-static_assert(FM * FM * 12 <= FI * FM * 12, "maps fit in hB + hC");
-static_assert(FM * FT * 12 <= FI * FM * 8, "backward h-pass fits in hA");
+// LDS (rows padded by one element so that the column-blocked passes, whose
+// lanes walk down consecutive rows, hit distinct banks):
+//   s_xy f2v[FI][SX] | hA f2v[FI][SH] | hB f2v[FI][SH] | hC float[FI][SH].
+// Once pass A has read the window (each thread keeps the (x, y) of its two
+// output pixels in registers) the maps (f2v[FM][SH] + float[FM][SH]) reuse
+// s_xy; the backward's horizontal pass (f2v[FM][SG] + float[FM][SG]) reuses
+// hA.  Four barriers per channel.
+constexpr int SX = FI + 1, SH = FM + 1, SG = FT + 1;
+constexpr int kOffA = FI * SX * 8, kOffB = kOffA + FI * SH * 8, kOffC = kOffB + FI * SH * 8;
+constexpr int kFusedLds = kOffC + FI * SH * 4;
+static_assert(FM * SH * 12 <= FI * SX * 8, "maps fit in s_xy");
+static_assert(FM * SG * 12 <= FI * SH * 8, "backward h-pass fits in hA");
+constexpr int kHA = 6, kHC = 4;  // adjacent outputs per work item in passes A, C1
 
-template <int C>
+// BR: map rows per work item of pass B (sliding window of K + BR - 1 rows).
+// Passes A and C1 are register-blocked: kHA / kHC adjacent outputs of one
+// row from one run of K + kHA - 1 / K + kHC - 1 LDS values.
+template <int C, int BR>
 __global__ void __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(4)))
 fused_kernel(int B, int H, int W, const float *__restrict__ x, const float *__restrict__ y,
              float cs, float cl, float *__restrict__ grad, float *__restrict__ partials) {
   __shared__ __attribute__((aligned(16))) char lds[kFusedLds];
   __shared__ float red[2][kFThreads / 64];
-  f2v(*s_xy)[FI] = reinterpret_cast<f2v(*)[FI]>(lds);
-  f2v(*hA)[FM] = reinterpret_cast<f2v(*)[FM]>(lds + kOffA);
-  f2v(*hB)[FM] = reinterpret_cast<f2v(*)[FM]>(lds + kOffB);
-  float(*hC)[FM] = reinterpret_cast<float(*)[FM]>(lds + kOffC);
-  f2v(*m01)[FM] = reinterpret_cast<f2v(*)[FM]>(lds + kOffB);
-  float(*m2)[FM] = reinterpret_cast<float(*)[FM]>(lds + kOffB + FM * FM * 8);
-  f2v(*g01)[FT] = reinterpret_cast<f2v(*)[FT]>(lds + kOffA);
-  float(*g2)[FT] = reinterpret_cast<float(*)[FT]>(lds + kOffA + FM * FT * 8);
+  f2v(*s_xy)[SX] = reinterpret_cast<f2v(*)[SX]>(lds);
+  f2v(*hA)[SH] = reinterpret_cast<f2v(*)[SH]>(lds + kOffA);
+  f2v(*hB)[SH] = reinterpret_cast<f2v(*)[SH]>(lds + kOffB);
+  float(*hC)[SH] = reinterpret_cast<float(*)[SH]>(lds + kOffC);
+  f2v(*m01)[SH] = reinterpret_cast<f2v(*)[SH]>(lds);
+  float(*m2)[SH] = reinterpret_cast<float(*)[SH]>(lds + FM * SH * 8);
+  f2v(*g01)[SG] = reinterpret_cast<f2v(*)[SG]>(lds + kOffA);
+  float(*g2)[SG] = reinterpret_cast<float(*)[SG]>(lds + kOffA + FM * SG * 8);
 
   const int Hm = H - 2 * R, Wm = W - 2 * R;
   const int tx = (W + FT - 1) / FT, ty = (H + FT - 1) / FT, nt = tx * ty;
@@ -513,8 +526,6 @@ fused_kernel(int B, int H, int W, const float *__restrict__ x, const float *__re
   float lsum = 0.f, ssum = 0.f;
   // backward vertical pass mapping: column gc, image rows 2 gr, 2 gr + 1
   const int gc = tid & 31, gr = tid >> 5;
-  const int mc = tid % FM, mg = tid / FM;  // map pass: column mc, rows 4 mg .. 4 mg + 3
-
 #pragma nounroll
   for (int c = 0; c < C; ++c) {
     // ---- stage channel c (+ its L1 over the tile's own pixels, window
@@ -530,44 +541,56 @@ fused_kernel(int B, int H, int W, const float *__restrict__ x, const float *__re
         lsum += fabsf(a - bb);
     }
     __syncthreads();
+    const f2v px0 = s_xy[2 * R + 2 * gr][2 * R + gc], px1 = s_xy[2 * R + 2 * gr + 1][2 * R + gc];
     // ---- A: horizontal blur of the statistics, FI rows x FM columns
-    for (int idx = tid; idx < FI * FM; idx += kFThreads) {
-      const int r = idx / FM, j = idx - r * FM;
-      f2v a = {0.f, 0.f}, bb = {0.f, 0.f};
-      float cc = 0.f;
+    static_assert(FM % kHA == 0 && FT % kHC == 0, "pass A / C1 blocking");
+    for (int idx = tid; idx < FI * (FM / kHA); idx += kFThreads) {
+      const int jg = idx / FI, r = idx - jg * FI, j0 = jg * kHA;
+      f2v v[K + kHA - 1], sq[K + kHA - 1];
+      float xy[K + kHA - 1];
 #pragma unroll
-      for (int k = 0; k < K; ++k) {
-        const float g = kG[k];
-        const f2v v = s_xy[r][j + k];
-        const f2v gv = f2v{g, g} * v;
-        a += gv;
-        bb = __builtin_elementwise_fma(gv, v, bb);
-        cc = __builtin_fmaf(gv.x, v.y, cc);
+      for (int i = 0; i < K + kHA - 1; ++i) {
+        v[i] = s_xy[r][j0 + i];
+        sq[i] = v[i] * v[i];
+        xy[i] = v[i].x * v[i].y;
       }
-      hA[r][j] = a;
-      hB[r][j] = bb;
-      hC[r][j] = cc;
+#pragma unroll
+      for (int o = 0; o < kHA; ++o) {
+        f2v a = {0.f, 0.f}, bb = {0.f, 0.f};
+        float cc = 0.f;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          const float g = kG[k];
+          a = __builtin_elementwise_fma(f2v{g, g}, v[o + k], a);
+          bb = __builtin_elementwise_fma(f2v{g, g}, sq[o + k], bb);
+          cc = __builtin_fmaf(g, xy[o + k], cc);
+        }
+        hA[r][j0 + o] = a;
+        hB[r][j0 + o] = bb;
+        hC[r][j0 + o] = cc;
+      }
     }
     __syncthreads();
-    // ---- B: vertical blur -> the partials of map pixels (local rows /
-    // cols 0..FM-1 = map coords ri0.., rj0..; zero outside the valid map)
-    float p0[4], p1[4], p2[4];
-    if (mg < (FM + 3) / 4) {
-      f2v oa[4], ob[4];
-      float oc[4];
+    // ---- B: vertical blur -> the partials of map pixels (local rows / cols
+    // 0..FM-1 = map coords ri0.., rj0..; zero outside the valid map), into s_xy
+    constexpr int kItems = (FM + BR - 1) / BR * FM;
+    for (int it = tid; it < kItems; it += kFThreads) {
+      const int mg = it / FM, mc = it - mg * FM;
+      f2v oa[BR], ob[BR];
+      float oc[BR];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < BR; ++j) {
         oa[j] = f2v{0.f, 0.f};
         ob[j] = f2v{0.f, 0.f};
         oc[j] = 0.f;
       }
-#pragma unroll 2
-      for (int i = 0; i < K + 3; ++i) {  // (partly rolled: bounds the live LDS values)
-        const int r = min(4 * mg + i, FI - 1);  // rows past FI only feed discarded outputs
+#pragma unroll
+      for (int i = 0; i < K + BR - 1; ++i) {
+        const int r = min(BR * mg + i, FI - 1);  // rows past FI only feed discarded outputs
         const f2v a = hA[r][mc], bb = hB[r][mc];
         const float cc = hC[r][mc];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < BR; ++j) {
           const int k = i - j;
           if (k >= 0 && k < K) {
             const float g = kG[k];
@@ -578,54 +601,60 @@ fused_kernel(int B, int H, int W, const float *__restrict__ x, const float *__re
         }
       }
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int mr = 4 * mg + j, pi = ri0 + mr, pj = rj0 + mc;
-        p0[j] = p1[j] = p2[j] = 0.f;
-        if (mr < FM && pi >= 0 && pi < Hm && pj >= 0 && pj < Wm) {
+      for (int j = 0; j < BR; ++j) {
+        const int mr = BR * mg + j, pi = ri0 + mr, pj = rj0 + mc;
+        float p0 = 0.f, p1 = 0.f, p2 = 0.f;
+        if (pi >= 0 && pi < Hm && pj >= 0 && pj < Wm) {
           const float u1 = oa[j].x, u2 = oa[j].y;
           const float s11 = ob[j].x - u1 * u1, s22 = ob[j].y - u2 * u2, s12 = oc[j] - u1 * u2;
           const float A1 = 2.f * u1 * u2 + C1, A2 = 2.f * s12 + C2;
           const float B1 = u1 * u1 + u2 * u2 + C1, B2 = s11 + s22 + C2;
           const float inv = 1.f / (B1 * B2);
           const float sv = A1 * A2 * inv;
-          if (mr >= 2 * R && mc >= 2 * R) ssum += sv;  // the tile's own map pixels
+          if (mr >= 2 * R && mr < FM && mc >= 2 * R) ssum += sv;  // the tile's own map pixels
           const float dN = 2.f * u2 * (A2 - A1), dD = 2.f * u1 * (B2 - B1);
-          p0[j] = (dN - sv * dD) * inv;
-          p1[j] = -sv * B1 * inv;
-          p2[j] = 2.f * A1 * inv;
+          p0 = (dN - sv * dD) * inv;
+          p1 = -sv * B1 * inv;
+          p2 = 2.f * A1 * inv;
         }
-      }
-    }
-    __syncthreads();  // hB / hC are read above and rewritten below
-    if (mg < (FM + 3) / 4) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int mr = 4 * mg + j;
         if (mr < FM) {
-          m01[mr][mc] = f2v{p0[j], p1[j]};
-          m2[mr][mc] = p2[j];
+          m01[mr][mc] = f2v{p0, p1};
+          m2[mr][mc] = p2;
         }
       }
     }
     __syncthreads();
     // ---- C1: horizontal blur of the partials, FM rows x FT columns (the
     // adjoint of the valid correlation: full correlation with the symmetric
-    // kernel, see bwd_kernel)
-    for (int idx = tid; idx < FM * FT; idx += kFThreads) {
-      const int r = idx / FT, j = idx - r * FT;
-      f2v a = {0.f, 0.f};
-      float cc = 0.f;
+    // kernel, see bwd_kernel), into hA
+    for (int idx = tid; idx < FM * (FT / kHC); idx += kFThreads) {
+      const int jg = idx / FM, r = idx - jg * FM, j0 = jg * kHC;
+      f2v v[K + kHC - 1];
+      float w[K + kHC - 1];
 #pragma unroll
-      for (int k = 0; k < K; ++k) {
-        const float g = kG[k];
-        a = __builtin_elementwise_fma(f2v{g, g}, m01[r][j + k], a);
-        cc = __builtin_fmaf(g, m2[r][j + k], cc);
+      for (int i = 0; i < K + kHC - 1; ++i) {
+        v[i] = m01[r][j0 + i];
+        w[i] = m2[r][j0 + i];
       }
-      g01[r][j] = a;
-      g2[r][j] = cc;
+#pragma unroll
+      for (int o = 0; o < kHC; ++o) {
+        f2v a = {0.f, 0.f};
+        float cc = 0.f;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          const float g = kG[k];
+          a = __builtin_elementwise_fma(f2v{g, g}, v[o + k], a);
+          cc = __builtin_fmaf(g, w[o + k], cc);
+        }
+        g01[r][j0 + o] = a;
+        g2[r][j0 + o] = cc;
+      }
     }
     __syncthreads();
-    // ---- C2: vertical blur onto the tile pixels, gradient out
+    // ---- C2: vertical blur onto the tile pixels, gradient out.  (The next
+    // channel's staging writes only s_xy, whose last readers, pass C1, are
+    // behind the barrier above; its pass A rewrites hA only after the
+    // staging barrier, which every thread reaches after its C2.)
     {
       f2v oa[2] = {f2v{0.f, 0.f}, f2v{0.f, 0.f}};
       float oc[2] = {0.f, 0.f};
@@ -647,7 +676,7 @@ fused_kernel(int B, int H, int W, const float *__restrict__ x, const float *__re
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int qi = qi0 + 2 * gr + j, qj = qj0 + gc;
-        const f2v v = s_xy[2 * R + 2 * gr + j][2 * R + gc];
+        const f2v v = j ? px1 : px0;
         const float d = v.x - v.y;
         const float sgn = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
         if (qi < H && qj < W)
@@ -655,7 +684,6 @@ fused_kernel(int B, int H, int W, const float *__restrict__ x, const float *__re
               cs * (oa[j].x + 2.f * v.x * oa[j].y + v.y * oc[j]) + cl * sgn;
       }
     }
-    __syncthreads();  // s_xy and hA (= g01 / g2) are rewritten for the next channel
   }
   ssum = wave_sum(ssum);
   lsum = wave_sum(lsum);
@@ -817,12 +845,19 @@ extern "C" int gsplat_hip_l1_ssim_loss_fused_fwd(int B, int H, int W, int C, con
   const int64_t nt = fused_tiles(H, W), per = (nt + 7) / 8;
   const dim3 grid((unsigned)(B * 8 * per));
   const float cs = -lam / n_map(B, H, W, C), cl = (1.f - lam) / n_img(B, H, W, C);
-  if (C == 3)
-    hipLaunchKernelGGL(ssim::fused_kernel<3>, grid, dim3(ssim::kFThreads), 0, st, B, H, W, img1,
-                       img2, cs, cl, grad_unit, partials);
-  else
-    hipLaunchKernelGGL(ssim::fused_kernel<1>, grid, dim3(ssim::kFThreads), 0, st, B, H, W, img1,
-                       img2, cs, cl, grad_unit, partials);
+  static const int fv = [] {
+    const char *e = getenv("GSPLAT_HIP_SSIM_FV");
+    return e ? atoi(e) : 0;
+  }();
+#define GS_FUSED(CC, BR)                                                                   \
+  hipLaunchKernelGGL((ssim::fused_kernel<CC, BR>), grid, dim3(ssim::kFThreads), 0, st, B, H, W, \
+                     img1, img2, cs, cl, grad_unit, partials)
+  if (C == 3) {
+    if (fv == 1) GS_FUSED(3, 2); else GS_FUSED(3, 4);
+  } else {
+    GS_FUSED(1, 2);
+  }
+#undef GS_FUSED
   hipLaunchKernelGGL(ssim::reduce_partials_kernel, dim3(1), dim3(1024), 0, st, (int)(B * nt),
                      partials, nullptr, out, lam, n_map(B, H, W, C), n_img(B, H, W, C));
   GS_CHECK_LAUNCH("l1_ssim_loss_fused_fwd");

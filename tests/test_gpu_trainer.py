@@ -75,7 +75,9 @@ def test_fused_loss_matches_two_pass_on_renders():
     torch.testing.assert_close(la, lb, rtol=1e-5, atol=1e-6)
     (3.0 * la).backward(retain_graph=True)
     (3.0 * lb).backward()
-    torch.testing.assert_close(a.grad, b.grad, rtol=1e-4, atol=1e-10)
+    # near-cancelling pixels: absolute bound relative to the gradient's scale
+    scale = float(b.grad.abs().max())
+    torch.testing.assert_close(a.grad, b.grad, rtol=1e-4, atol=1e-4 * scale)
     g1 = a.grad.clone()
     a.grad = None
     (3.0 * la).backward()
