@@ -2,7 +2,8 @@
 // the isect paths in place of rocPRIM's device sort (whose per-pass fixed cost,
 // ~25 us for a 0.3 M-item onesweep pass, dominated the depth sort).
 //
-// One pass = 8 key bits, three launches:
+// One pass = 8 key bits (11 for keys of more than 24 bits: three passes
+// instead of four over 32-bit depth keys), three launches:
 //   lsd_hist     per tile of NT*IPT items: LDS digit histogram -> hist[d][tile]
 //   lsd_scan     one workgroup per digit: exclusive scan of its row in place,
 //                row total -> totals[d]
@@ -24,7 +25,8 @@ namespace gs {
 namespace lsd {
 
 constexpr int NT = 256;
-constexpr int RADIX = 256;
+constexpr int RADIX = 256;          // 8-bit digits
+constexpr int RADIX_WIDE = 2048;    // 11-bit digits
 
 inline int64_t n_tiles(int64_t n, int ipt) { return (n + (int64_t)NT * ipt - 1) / ((int64_t)NT * ipt); }
 
@@ -41,12 +43,13 @@ struct FinalOut {
   int32_t *flatten_ids;
 };
 
-template <int IPT>
+template <int IPT, int RX>
 __global__ void __launch_bounds__(NT)
 hist_kernel(const uint32_t *__restrict__ keys, int64_t n, int shift, uint32_t mask,
             uint32_t *__restrict__ hist, int64_t nt) {
-  __shared__ uint32_t h[RADIX];
-  h[threadIdx.x] = 0;
+  __shared__ uint32_t h[RX];
+#pragma unroll
+  for (int d = threadIdx.x; d < RX; d += NT) h[d] = 0;
   __syncthreads();
   const int64_t base = (int64_t)blockIdx.x * NT * IPT;
 #pragma unroll
@@ -55,7 +58,8 @@ hist_kernel(const uint32_t *__restrict__ keys, int64_t n, int shift, uint32_t ma
     if (i < n) atomicAdd(&h[(keys[i] >> shift) & mask], 1u);
   }
   __syncthreads();
-  hist[(int64_t)threadIdx.x * nt + blockIdx.x] = h[threadIdx.x];
+#pragma unroll
+  for (int d = threadIdx.x; d < RX; d += NT) hist[(int64_t)d * nt + blockIdx.x] = h[d];
 }
 
 // Exclusive scan of row d (nt entries) in place; the row sum -> totals[d].
@@ -96,22 +100,24 @@ scan_kernel(uint32_t *__restrict__ hist, int64_t nt, uint32_t *__restrict__ tota
 // number of such lanes below.  Cross-wave offsets and the tile's digit starts
 // come from the 4 x 256 wave counts; items are then reordered through LDS so
 // the global stores are digit-contiguous.
-template <int IPT, bool FINAL>
+template <int IPT, bool FINAL, int RX>
 __global__ void __launch_bounds__(NT)
 scatter_kernel(const uint32_t *__restrict__ kin, const int32_t *__restrict__ vin,
                uint32_t *__restrict__ kout, int32_t *__restrict__ vout, int64_t n, int shift,
                int nbits, const uint32_t *__restrict__ hist, const uint32_t *__restrict__ totals,
                int64_t nt, FinalOut fo) {
-  constexpr int NW = NT / 64, TILE = NT * IPT;
-  __shared__ uint32_t cnt[NW][RADIX];
-  __shared__ uint32_t gbase[RADIX];  // global position of tile slot 0 of digit d's range
+  constexpr int NW = NT / 64, TILE = NT * IPT, DPT = RX / NT;  // digits per thread
+  __shared__ uint32_t cnt[NW][RX];
+  __shared__ uint32_t gbase[RX];  // global position of tile slot 0 of digit d's range
   __shared__ uint32_t wsum[NW];
   __shared__ uint32_t kbuf[TILE];
   __shared__ int32_t vbuf[TILE];
   const uint32_t mask = (1u << nbits) - 1u;
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
 #pragma unroll
-  for (int w = 0; w < NW; ++w) cnt[w][t] = 0;
+  for (int w = 0; w < NW; ++w)
+#pragma unroll
+    for (int j = 0; j < DPT; ++j) cnt[w][t * DPT + j] = 0;
   const int64_t base = (int64_t)blockIdx.x * TILE;
   const int nvalid = (int)min<int64_t>((int64_t)TILE, n - base);
   uint32_t key[IPT];
@@ -143,42 +149,53 @@ scatter_kernel(const uint32_t *__restrict__ kin, const int32_t *__restrict__ vin
     rank[e] = old + below;
   }
   __syncthreads();
-  // digit t: offsets of the waves, tile total, tile-exclusive start
-  uint32_t woff[NW], tot = 0;
+  // digits t*DPT .. t*DPT+DPT-1: offsets of the waves, tile totals, and the
+  // exclusive scans (tile-local and global) across all digits
+  uint32_t woff[DPT][NW], tot[DPT], tsum = 0, gv[DPT], gsum = 0;
 #pragma unroll
-  for (int w = 0; w < NW; ++w) {
-    woff[w] = tot;
-    tot += cnt[w][t];
+  for (int j = 0; j < DPT; ++j) {
+    const int d = t * DPT + j;
+    tot[j] = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      woff[j][w] = tot[j];
+      tot[j] += cnt[w][d];
+    }
+    tsum += tot[j];
+    gv[j] = totals[d];
+    gsum += gv[j];
   }
-  uint32_t x = tot;
+  uint32_t x = tsum, g = gsum;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t y = __shfl_up(x, o, 64);
-    if (lane >= o) x += y;
+    const uint32_t y = __shfl_up(x, o, 64), z = __shfl_up(g, o, 64);
+    if (lane >= o) {
+      x += y;
+      g += z;
+    }
   }
   if (lane == 63) wsum[wid] = x;
-  // global start of digit t: exclusive scan of the totals + this tile's row entry
-  const uint32_t tv = totals[t];
-  uint32_t g = tv;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t y = __shfl_up(g, o, 64);
-    if (lane >= o) g += y;
-  }
   __syncthreads();
   uint32_t lbefore = 0;
 #pragma unroll
   for (int w = 0; w < NW; ++w) lbefore += w < wid ? wsum[w] : 0u;
-  const uint32_t lstart = lbefore + x - tot;
+  uint32_t lrun = lbefore + x - tsum;  // tile slot of digit t*DPT's first item
   __syncthreads();
   if (lane == 63) wsum[wid] = g;
   __syncthreads();
   uint32_t gbefore = 0;
 #pragma unroll
   for (int w = 0; w < NW; ++w) gbefore += w < wid ? wsum[w] : 0u;
-  gbase[t] = gbefore + g - tv + hist[(int64_t)t * nt + blockIdx.x] - lstart;
+  uint32_t grun = gbefore + g - gsum;  // global start of digit t*DPT
 #pragma unroll
-  for (int w = 0; w < NW; ++w) cnt[w][t] = lstart + woff[w];  // tile slot of wave w's first
+  for (int j = 0; j < DPT; ++j) {
+    const int d = t * DPT + j;
+    gbase[d] = grun + hist[(int64_t)d * nt + blockIdx.x] - lrun;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) cnt[w][d] = lrun + woff[j][w];  // tile slot of wave w's first
+    lrun += tot[j];
+    grun += gv[j];
+  }
   __syncthreads();
 #pragma unroll
   for (int e = 0; e < IPT; ++e) {
@@ -211,47 +228,57 @@ scatter_kernel(const uint32_t *__restrict__ kin, const int32_t *__restrict__ vin
 
 }  // namespace lsd
 
-// Scratch for lsd_sort_pairs: hist rows + totals.
+// Scratch for lsd_sort_pairs: hist rows + totals (sized for 11-bit digits).
 inline size_t lsd_sort_scratch_bytes(int64_t n) {
   const int64_t nt = lsd::n_tiles(n, lsd::pick_ipt(n));
-  return 4 * (size_t)(lsd::RADIX * nt + lsd::RADIX);
+  return 4 * (size_t)(lsd::RADIX_WIDE * nt + lsd::RADIX_WIDE);
 }
 
 // Stable sort of n pairs by key bits [begin_bit, end_bit), ping-ponging
 // between (k0, v0) and (k1, v1).  Returns 0 if the result is in (k0, v0),
 // 1 if in (k1, v1).  With `fo` non-null the last pass writes the final isect
 // output instead (see FinalOut; the return value is then meaningless).
-// n < 2^32.
+// n < 2^32.  Ranges of more than 24 bits (without `fo`: the depth sort) use
+// 11-bit digits, 3 passes for 32 bits.
 inline int lsd_sort_pairs(uint32_t *k0, int32_t *v0, uint32_t *k1, int32_t *v1, int64_t n,
                           int begin_bit, int end_bit, void *scratch, hipStream_t st,
                           const lsd::FinalOut *fo = nullptr) {
   if (n <= 0 || end_bit <= begin_bit) return 0;
   const int ipt = lsd::pick_ipt(n);
   const int64_t nt = lsd::n_tiles(n, ipt);
+  const bool wide = end_bit - begin_bit > 24 && fo == nullptr;
+  const int dbits = wide ? 11 : 8, radix = wide ? lsd::RADIX_WIDE : lsd::RADIX;
   uint32_t *hist = reinterpret_cast<uint32_t *>(scratch);
-  uint32_t *totals = hist + (int64_t)lsd::RADIX * nt;
+  uint32_t *totals = hist + (int64_t)radix * nt;
   int cur = 0;
-  for (int shift = begin_bit; shift < end_bit; shift += 8) {
-    const int nbits = end_bit - shift < 8 ? end_bit - shift : 8;
+  for (int shift = begin_bit; shift < end_bit; shift += dbits) {
+    const int nbits = end_bit - shift < dbits ? end_bit - shift : dbits;
     const uint32_t mask = (1u << nbits) - 1u;
     uint32_t *ki = cur ? k1 : k0, *ko = cur ? k0 : k1;
     int32_t *vi = cur ? v1 : v0, *vo = cur ? v0 : v1;
-    if (ipt == 4)
-      hipLaunchKernelGGL(lsd::hist_kernel<4>, dim3((unsigned)nt), dim3(lsd::NT), 0, st, ki, n,
-                         shift, mask, hist, nt);
-    else
-      hipLaunchKernelGGL(lsd::hist_kernel<16>, dim3((unsigned)nt), dim3(lsd::NT), 0, st, ki, n,
-                         shift, mask, hist, nt);
-    hipLaunchKernelGGL(lsd::scan_kernel, dim3(lsd::RADIX), dim3(lsd::NT), 0, st, hist, nt, totals);
-    const bool fin = fo && shift + 8 >= end_bit;
-    const lsd::FinalOut f = fin ? *fo : lsd::FinalOut{nullptr, nullptr, nullptr};
-#define GS_LSD_SCATTER(I, F)                                                                  \
-  hipLaunchKernelGGL((lsd::scatter_kernel<I, F>), dim3((unsigned)nt), dim3(lsd::NT), 0, st, ki, \
-                     vi, ko, vo, n, shift, nbits, hist, totals, nt, f)
-    if (ipt == 4) {
-      if (fin) GS_LSD_SCATTER(4, true); else GS_LSD_SCATTER(4, false);
+#define GS_LSD_HIST(I, RX)                                                                     \
+  hipLaunchKernelGGL((lsd::hist_kernel<I, RX>), dim3((unsigned)nt), dim3(lsd::NT), 0, st, ki, n, \
+                     shift, mask, hist, nt)
+    if (wide) {
+      if (ipt == 4) GS_LSD_HIST(4, lsd::RADIX_WIDE); else GS_LSD_HIST(16, lsd::RADIX_WIDE);
     } else {
-      if (fin) GS_LSD_SCATTER(16, true); else GS_LSD_SCATTER(16, false);
+      if (ipt == 4) GS_LSD_HIST(4, lsd::RADIX); else GS_LSD_HIST(16, lsd::RADIX);
+    }
+#undef GS_LSD_HIST
+    hipLaunchKernelGGL(lsd::scan_kernel, dim3((unsigned)radix), dim3(lsd::NT), 0, st, hist, nt,
+                       totals);
+    const bool fin = fo && shift + dbits >= end_bit;
+    const lsd::FinalOut f = fin ? *fo : lsd::FinalOut{nullptr, nullptr, nullptr};
+#define GS_LSD_SCATTER(I, F, RX)                                                              \
+  hipLaunchKernelGGL((lsd::scatter_kernel<I, F, RX>), dim3((unsigned)nt), dim3(lsd::NT), 0, st, \
+                     ki, vi, ko, vo, n, shift, nbits, hist, totals, nt, f)
+    if (wide) {
+      if (ipt == 4) GS_LSD_SCATTER(4, false, lsd::RADIX_WIDE);
+      else GS_LSD_SCATTER(16, false, lsd::RADIX_WIDE);
+    } else if (ipt == 4) {
+      if (fin) GS_LSD_SCATTER(4, true, lsd::RADIX); else GS_LSD_SCATTER(4, false, lsd::RADIX);
+    } else {
+      if (fin) GS_LSD_SCATTER(16, true, lsd::RADIX); else GS_LSD_SCATTER(16, false, lsd::RADIX);
     }
 #undef GS_LSD_SCATTER
     cur ^= 1;

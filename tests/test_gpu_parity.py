@@ -234,14 +234,17 @@ def test_isect_negative_and_tied_depths(isect_mode, C, tw, th):
     assert np.array_equal(fids.cpu().numpy(), ofids)
 
 
-def test_isect_sort_strategies_agree_large():
-    """Both strategies on an M2-sized random workload (~1M isects)."""
+@pytest.mark.parametrize("N,rmax", [(200_000, 60), (1_000_000, 12)])
+def test_isect_sort_strategies_agree_large(N, rmax):
+    """Both strategies on an M2-sized random workload (~1M isects); the
+    second size has > 2^20 visible Gaussians (the 16-items-per-thread tiles
+    of the 11-bit depth sort)."""
     import gsplat_hip
     from gsplat_hip import _wrapper
     g = torch.Generator(device=DEV).manual_seed(3)
-    C, N, ts, tw, th = 2, 200_000, 16, 120, 68
+    C, ts, tw, th = 2, 16, 120, 68
     m2 = torch.rand(C, N, 2, device=DEV, generator=g) * torch.tensor([tw * ts, th * ts], device=DEV)
-    r = (torch.rand(C, N, device=DEV, generator=g) ** 4 * 60).int()
+    r = (torch.rand(C, N, device=DEV, generator=g) ** 4 * rmax).int()
     d = torch.rand(C, N, device=DEV, generator=g) * 10
     d[:, ::7] = 1.0  # ties
     old = _wrapper.ISECT_SORT
