@@ -2,8 +2,8 @@
 // the isect paths in place of rocPRIM's device sort (whose per-pass fixed cost,
 // ~25 us for a 0.3 M-item onesweep pass, dominated the depth sort).
 //
-// One pass = 8 key bits (11 for keys of more than 24 bits: three passes
-// instead of four over 32-bit depth keys), three launches:
+// One pass = 8 key bits (optionally 11 for keys of more than 24 bits, see
+// lsd_sort_pairs), three launches:
 //   lsd_hist     per tile of NT*IPT items: LDS digit histogram -> hist[d][tile]
 //   lsd_scan     one workgroup per digit: exclusive scan of its row in place,
 //                row total -> totals[d]
@@ -19,6 +19,8 @@
 // [begin_bit, end_bit).  Traffic per pass: 4 B/item (hist) + 16 B/item
 // (scatter read + write).
 #pragma once
+#include <stdlib.h>
+
 #include "common.h"
 
 namespace gs {
@@ -52,10 +54,31 @@ hist_kernel(const uint32_t *__restrict__ keys, int64_t n, int shift, uint32_t ma
   for (int d = threadIdx.x; d < RX; d += NT) h[d] = 0;
   __syncthreads();
   const int64_t base = (int64_t)blockIdx.x * NT * IPT;
+  if (mask < 64u) {
+    // few digits (the short last pass of the tile sort): runs of equal
+    // digits would serialise on one LDS address, so the lanes of a wave
+    // holding the same digit are matched by ballots and one adds their count
+    const int lane = threadIdx.x & 63;
+    const uint64_t lt = (1ull << lane) - 1ull;
 #pragma unroll
-  for (int e = 0; e < IPT; ++e) {
-    const int64_t i = base + e * NT + threadIdx.x;
-    if (i < n) atomicAdd(&h[(keys[i] >> shift) & mask], 1u);
+    for (int e = 0; e < IPT; ++e) {
+      const int64_t i = base + e * NT + threadIdx.x;
+      const bool ok = i < n;
+      const uint32_t dg = ok ? (keys[i] >> shift) & mask : 0u;
+      uint64_t peers = __ballot(ok);
+      for (uint32_t b = 1; b <= mask; b <<= 1) {
+        const bool bit = (dg & b) != 0u;
+        const uint64_t bal = __ballot(bit);
+        peers &= bit ? bal : ~bal;
+      }
+      if (ok && (peers & lt) == 0) atomicAdd(&h[dg], (uint32_t)__popcll(peers));
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < IPT; ++e) {
+      const int64_t i = base + e * NT + threadIdx.x;
+      if (i < n) atomicAdd(&h[(keys[i] >> shift) & mask], 1u);
+    }
   }
   __syncthreads();
 #pragma unroll
@@ -246,7 +269,14 @@ inline int lsd_sort_pairs(uint32_t *k0, int32_t *v0, uint32_t *k1, int32_t *v1, 
   if (n <= 0 || end_bit <= begin_bit) return 0;
   const int ipt = lsd::pick_ipt(n);
   const int64_t nt = lsd::n_tiles(n, ipt);
-  const bool wide = end_bit - begin_bit > 24 && fo == nullptr;
+  // 11-bit digits for the 32-bit depth sort measured slower at M2 (3 passes
+  // 78 us vs 4 passes 68 us: the 2048-bin histograms and scans cost more
+  // than the pass they save); GSPLAT_HIP_LSD_WIDE=1 turns them on
+  static const bool wide_ok = [] {
+    const char *e = getenv("GSPLAT_HIP_LSD_WIDE");
+    return e && atoi(e) == 1;
+  }();
+  const bool wide = wide_ok && end_bit - begin_bit > 24 && fo == nullptr;
   const int dbits = wide ? 11 : 8, radix = wide ? lsd::RADIX_WIDE : lsd::RADIX;
   uint32_t *hist = reinterpret_cast<uint32_t *>(scratch);
   uint32_t *totals = hist + (int64_t)radix * nt;
