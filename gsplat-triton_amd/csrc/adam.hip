@@ -111,10 +111,10 @@ using namespace gs;
 // One Adam step over n_groups parameter groups.  Arrays are host arrays of
 // length n_groups; grads[i] may be NULL (treated as zero).  Every pointer must
 // be 16-B aligned.  `step` is the 1-based step count.
-extern "C" int gsplat_hip_adam_step(int n_groups, float *const *params, const float *const *grads,
-                                    float *const *exp_avgs, float *const *exp_avg_sqs,
-                                    const int64_t *numels, const float *lrs, float beta1,
-                                    float beta2, float eps, int step, void *stream) {
+static int adam_launch(int n_groups, float *const *params, const float *const *grads,
+                       float *const *exp_avgs, float *const *exp_avg_sqs, const int64_t *numels,
+                       const float *lrs, float beta1, float beta2, float eps, int step,
+                       int max_blocks, void *stream) {
   GS_REQUIRE(n_groups > 0 && n_groups <= adam::kMaxGroups, "adam: 1..%d groups supported",
              adam::kMaxGroups);
   GS_REQUIRE(step >= 1, "adam: step must be >= 1");
@@ -138,11 +138,37 @@ extern "C" int gsplat_hip_adam_step(int n_groups, float *const *params, const fl
   for (int i = n_groups; i < adam::kMaxGroups; ++i) g.begin[i + 1] = g.begin[n_groups];
   const int64_t total = g.begin[n_groups];
   if (total == 0) return 0;
-  // one 16-B slot per lane per iteration; deeper unrolling and non-temporal
-  // accesses measured no faster (tools/adam_bench.py: ~5.8 TB/s)
-  const int blocks = (int)std::min<int64_t>((total + 255) / 256, 256 * 64);
-  hipLaunchKernelGGL((adam::step_kernel<1, false>), dim3(blocks), dim3(256), 0,
-                     (hipStream_t)stream, g, beta1, beta2, eps);
+  if (max_blocks > 0) {
+    // a bounded grid (an update overlapping other streams' kernels leaves
+    // them CU slots): four 16-B slots per lane in flight per iteration
+    const int blocks = (int)std::min<int64_t>((total + 1023) / 1024, max_blocks);
+    hipLaunchKernelGGL((adam::step_kernel<4, false>), dim3(blocks), dim3(256), 0,
+                       (hipStream_t)stream, g, beta1, beta2, eps);
+  } else {
+    // one 16-B slot per lane per iteration; deeper unrolling and non-temporal
+    // accesses measured no faster (tools/adam_bench.py: ~5.8 TB/s)
+    const int blocks = (int)std::min<int64_t>((total + 255) / 256, 256 * 64);
+    hipLaunchKernelGGL((adam::step_kernel<1, false>), dim3(blocks), dim3(256), 0,
+                       (hipStream_t)stream, g, beta1, beta2, eps);
+  }
   GS_CHECK_LAUNCH("adam_step");
   return 0;
+}
+
+extern "C" int gsplat_hip_adam_step(int n_groups, float *const *params, const float *const *grads,
+                                    float *const *exp_avgs, float *const *exp_avg_sqs,
+                                    const int64_t *numels, const float *lrs, float beta1,
+                                    float beta2, float eps, int step, void *stream) {
+  return adam_launch(n_groups, params, grads, exp_avgs, exp_avg_sqs, numels, lrs, beta1, beta2,
+                     eps, step, 0, stream);
+}
+
+extern "C" int gsplat_hip_adam_step_bounded(int n_groups, float *const *params,
+                                            const float *const *grads, float *const *exp_avgs,
+                                            float *const *exp_avg_sqs, const int64_t *numels,
+                                            const float *lrs, float beta1, float beta2, float eps,
+                                            int step, int max_blocks, void *stream) {
+  GS_REQUIRE(max_blocks > 0, "adam_step_bounded: max_blocks must be > 0");
+  return adam_launch(n_groups, params, grads, exp_avgs, exp_avg_sqs, numels, lrs, beta1, beta2,
+                     eps, step, max_blocks, stream);
 }

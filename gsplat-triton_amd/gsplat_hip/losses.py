@@ -126,25 +126,43 @@ def l1_ssim_loss(img, gt, ssim_lambda=0.2, fused=None):
     return _L1SSIMLoss.apply(img, gt, float(ssim_lambda))
 
 
-def adam_groups(params, grads, exp_avgs, exp_avg_sqs, lrs, betas, eps, step):
+def adam_groups(params, grads, exp_avgs, exp_avg_sqs, lrs, betas, eps, step, max_blocks=0):
     """One fused Adam launch (csrc/adam.hip) over flat float32 tensors: group
-    i updates params[i] in place from grads[i] (None = zero) with its lr."""
+    i updates params[i] in place from grads[i] (None = zero) with its lr.
+    max_blocks > 0 bounds the grid (gsplat_hip_adam_step_bounded)."""
     n = len(params)
     P = ctypes.c_void_p * n
     for t in list(params) + list(exp_avgs) + list(exp_avg_sqs):
         assert t.is_contiguous() and t.dtype == torch.float32
-    _lib.call("gsplat_hip_adam_step", n, P(*[p.data_ptr() for p in params]),
-              P(*[0 if g is None else g.data_ptr() for g in grads]),
-              P(*[m.data_ptr() for m in exp_avgs]), P(*[v.data_ptr() for v in exp_avg_sqs]),
-              (ctypes.c_int64 * n)(*[p.numel() for p in params]),
-              (ctypes.c_float * n)(*[float(x) for x in lrs]), float(betas[0]), float(betas[1]),
-              float(eps), int(step), _stream())
+    args = [n, P(*[p.data_ptr() for p in params]),
+            P(*[0 if g is None else g.data_ptr() for g in grads]),
+            P(*[m.data_ptr() for m in exp_avgs]), P(*[v.data_ptr() for v in exp_avg_sqs]),
+            (ctypes.c_int64 * n)(*[p.numel() for p in params]),
+            (ctypes.c_float * n)(*[float(x) for x in lrs]), float(betas[0]), float(betas[1]),
+            float(eps), int(step)]
+    if max_blocks > 0:
+        _lib.call("gsplat_hip_adam_step_bounded", *args, int(max_blocks), _stream())
+    else:
+        _lib.call("gsplat_hip_adam_step", *args, _stream())
+
+
+# workgroups of the deferred (side-stream) update: few enough that the main
+# stream's projection / isect kernels still find CU slots
+DEFER_BLOCKS = int(os.environ.get("GSPLAT_HIP_DEFER_BLOCKS", "512"))
 
 
 class FusedAdam:
-    """torch.optim.Adam semantics (per-group lr, shared betas/eps) in one launch."""
+    """torch.optim.Adam semantics (per-group lr, shared betas/eps) in one launch.
 
-    def __init__(self, params, lrs, betas=(0.9, 0.999), eps=1e-8):
+    deferred: indices of parameters whose update may run on a side stream
+    (after everything queued so far on the current stream): `step()` then
+    launches the other groups on the current stream and these on the side
+    stream, and `wait()` orders the current stream after them.  The trainer
+    defers the SH coefficients (81 % of the optimizer bytes at SH degree 3):
+    the next step needs them only for its colours, after projection and tile
+    intersection, which run meanwhile."""
+
+    def __init__(self, params, lrs, betas=(0.9, 0.999), eps=1e-8, deferred=()):
         self.params = list(params)
         self.lrs = [float(x) for x in lrs]
         self.betas, self.eps = betas, eps
@@ -153,15 +171,45 @@ class FusedAdam:
         self.step_count = 0
         for p in self.params:
             assert p.is_contiguous() and p.dtype == torch.float32
+        self.deferred = sorted(set(deferred))
+        self.side = None
+        if self.deferred and self.params and self.params[0].is_cuda:
+            self.side = torch.cuda.Stream(device=self.params[0].device)
+        self._event = None
+
+    def _launch(self, idx, grads, max_blocks=0):
+        adam_groups([self.params[i].data for i in idx], [grads[i] for i in idx],
+                    [self.exp_avg[i] for i in idx], [self.exp_avg_sq[i] for i in idx],
+                    [self.lrs[i] for i in idx], self.betas, self.eps, self.step_count,
+                    max_blocks)
 
     @torch.no_grad()
     def step(self):
+        self.wait()  # a previous deferred update is ordered before this one
         self.step_count += 1
         grads = [p.grad for p in self.params]
         for gr in grads:
             assert gr is None or gr.is_contiguous()
-        adam_groups([p.data for p in self.params], grads, self.exp_avg, self.exp_avg_sq,
-                    self.lrs, self.betas, self.eps, self.step_count)
+        if self.side is None:
+            self._launch(range(len(self.params)), grads)
+            return
+        now = [i for i in range(len(self.params)) if i not in self.deferred]
+        if now:
+            self._launch(now, grads)
+        self.side.wait_stream(torch.cuda.current_stream(self.side.device))
+        for i in self.deferred:  # read on the side stream after zero_grad frees them
+            if grads[i] is not None:
+                grads[i].record_stream(self.side)
+        with torch.cuda.stream(self.side):
+            self._launch(self.deferred, grads, DEFER_BLOCKS)
+            self._event = torch.cuda.Event()
+            self._event.record(self.side)
+
+    def wait(self):
+        """Order the current stream after a deferred update still in flight."""
+        if self._event is not None:
+            torch.cuda.current_stream(self.side.device).wait_event(self._event)
+            self._event = None
 
     def zero_grad(self, set_to_none=True):
         for p in self.params:

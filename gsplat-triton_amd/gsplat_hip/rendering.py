@@ -256,6 +256,9 @@ def rasterization(
     if late:
         _colors_ready()
         colors, backgrounds = add_depth(eval_colors(colors), backgrounds)
+        if colors.shape[-1] <= channel_chunk:
+            records = pack_render_records(means2d, conics, colors, opacities, tile_size,
+                                          tiles_per_gauss)
     meta.update({"tile_width": tile_width, "tile_height": tile_height,
                  "tiles_per_gauss": tiles_per_gauss, "isect_ids": isect_ids,
                  "flatten_ids": flatten_ids, "isect_offsets": isect_offsets, "width": width,

@@ -185,6 +185,13 @@ class Trainer:
         if sharded_optimizer is None:
             sharded_optimizer = world_size > 1
         self.sharded = fused and sharded_optimizer
+        # GSPLAT_HIP_DEFER_SH=1: the SH rows' Adam on a side stream beside the
+        # next step's projection and isect (colours evaluated after the isect).
+        # Measured slower at M2 (620-630 vs 660 images/s): the
+        # sort kernels and the update split the HBM bandwidth instead of
+        # filling each other's gaps, so it is off by default.
+        self.defer_sh = (fused and not self.sharded and torch.device(device).type == "cuda"
+                         and os.environ.get("GSPLAT_HIP_DEFER_SH", "0") == "1")
         self.opt = self._make_optimizer(list(self.params.values()))
         self.viewmats = viewmats.to(device)
         self.Ks = Ks.to(device)
@@ -211,7 +218,11 @@ class Trainer:
                       [names.index(k) for k in ("sh0", "shN")]]
             return ShardedAdam(params, self.lrs, groups=groups, **self.adam_kw)
         if self.fused:  # HIP loss + one-launch Adam (csrc/ssim.hip, csrc/adam.hip)
-            return FusedAdam(params, self.lrs, **self.adam_kw)
+            # the SH rows' update on a side stream, overlapping the next
+            # step's projection and isect (render() waits before the colours)
+            names = list(self.params)
+            deferred = [names.index(k) for k in ("sh0", "shN")] if self.defer_sh else []
+            return FusedAdam(params, self.lrs, deferred=deferred, **self.adam_kw)
         groups = [{"params": [p], "lr": lr, "name": k}
                   for (k, p), lr in zip(self.params.items(), self.lrs)]
         return torch.optim.Adam(groups, foreach=True, **self.adam_kw)
@@ -229,6 +240,7 @@ class Trainer:
         if self.sharded:
             return {k: list(mv) for k, mv in zip(names, self.opt.full_state())}
         if self.fused:
+            self.sync()
             return {k: [self.opt.exp_avg[i], self.opt.exp_avg_sq[i]]
                     for i, k in enumerate(names)}
         out = {}
@@ -267,7 +279,7 @@ class Trainer:
         """Order the current stream after any optimizer communication still in
         flight (the sharded optimizer's deferred all-gathers): call before
         reading the parameters outside the training step (checkpoint, eval)."""
-        if self.sharded:
+        if self.sharded or getattr(self, "defer_sh", False):
             self.opt.wait()
 
     def synced_params(self):
@@ -294,6 +306,8 @@ class Trainer:
             self.opt.wait([names.index(k) for k in ("means", "scales", "quats", "opacities")])
             sh_idx = [names.index(k) for k in ("sh0", "shN")]
             hook = lambda: self.opt.wait(sh_idx)  # noqa: E731
+        elif getattr(self, "defer_sh", False):
+            hook = self.opt.wait  # the previous step's SH update (side stream)
         if self.fused:  # one HIP launch each way for both activations
             scales, opac = activate(p["scales"], p["opacities"])
         else:

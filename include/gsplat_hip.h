@@ -367,6 +367,13 @@ int gsplat_hip_adam_step(int n_groups, float *const *params, const float *const 
                          float *const *exp_avgs, float *const *exp_avg_sqs,
                          const int64_t *numels, const float *lrs, float beta1, float beta2,
                          float eps, int step, void *stream);
+/* The same update on a grid of at most max_blocks workgroups (ABI 17): an
+ * update running on a side stream beside other kernels leaves them CU slots
+ * (the trainer's deferred SH-coefficient update). */
+int gsplat_hip_adam_step_bounded(int n_groups, float *const *params, const float *const *grads,
+                                 float *const *exp_avgs, float *const *exp_avg_sqs,
+                                 const int64_t *numels, const float *lrs, float beta1,
+                                 float beta2, float eps, int step, int max_blocks, void *stream);
 
 /* ---------------------------------------------------------------------------
  * 2DGS (surfels).  Replaces the CUDA kernels that gsplat.rendering.rasterization_2dgs
