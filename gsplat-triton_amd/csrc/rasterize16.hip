@@ -1234,7 +1234,9 @@ struct BwdOcc {  // waves per SIMD that fit the VGPRs without spills
   static constexpr int W = PX == 2 ? 4 : 3;
 };
 
-template <int D, bool ABS, int PX>
+// PFB: gather the next batch's records while compositing this one (one
+// batch of latency hidden per wave; costs the record's registers).
+template <int D, bool ABS, int PX, bool PFB = false>
 __global__ void __launch_bounds__(256 / PX)
 __attribute__((amdgpu_waves_per_eu(BwdOcc<PX>::W))) bwd2_kernel(Args a) {
   using P = BwdPair<D>;
@@ -1428,12 +1430,26 @@ __attribute__((amdgpu_waves_per_eu(BwdOcc<PX>::W))) bwd2_kernel(Args a) {
       }
     };
     int32_t g_n = id_at(end);
-    for (int64_t b1 = end; b1 > start; b1 -= 64) {
+    if (PFB) {
       Attr<D> A;
       load_attr<D>(a, g_n, A);
-      g_n = id_at(b1 - 64);
-      composite(stage(A, b1));
-      wave_sync_lds();
+      g_n = id_at(end - 64);
+      for (int64_t b1 = end; b1 > start; b1 -= 64) {
+        Attr<D> An;
+        load_attr<D>(a, g_n, An);  // clamped ids: valid past the last batch too
+        g_n = id_at(b1 - 128);
+        composite(stage(A, b1));
+        wave_sync_lds();
+        A = An;
+      }
+    } else {
+      for (int64_t b1 = end; b1 > start; b1 -= 64) {
+        Attr<D> A;
+        load_attr<D>(a, g_n, A);
+        g_n = id_at(b1 - 64);
+        composite(stage(A, b1));
+        wave_sync_lds();
+      }
     }
   }
   tl_store(a, t_start, lane);
@@ -2006,11 +2022,25 @@ static int64_t n_items_bound(int n_tiles, int64_t n_isects) {
 
 // Pixels per lane in the backward (1: bwd_kernel, 16x4 per wave; 2 or 4:
 // bwd2_kernel, 16x8 or 16x16 per wave).  GSPLAT_HIP_BWD_PX overrides it.
+// With render records and the batch prefetch, 2 measured 0.427-0.430 ms at
+// M2 against 0.465-0.473 for 4 (profiles/r2_s4_bwdpf; 4 was ahead before
+// the records: its 160 VGPRs leave 3 waves per SIMD, 2 keeps 4).
 static int bwd_px() {
   static const int v = [] {
     const char *e = getenv("GSPLAT_HIP_BWD_PX");
-    const int x = e ? atoi(e) : 4;
-    return (x == 1 || x == 2) ? x : 4;
+    const int x = e ? atoi(e) : 2;
+    return (x == 1 || x == 4) ? x : 2;
+  }();
+  return v;
+}
+
+// Backward record prefetch one batch ahead (bwd2_kernel PFB), default on
+// (PX 2: 0.427 vs 0.430 ms; PX 4 spills and runs slower with it);
+// GSPLAT_HIP_BWD_PF=0 turns it off.
+static bool bwd_pf() {
+  static const bool v = [] {
+    const char *e = getenv("GSPLAT_HIP_BWD_PF");
+    return !(e && atoi(e) == 0) && bwd_px() == 2;
   }();
   return v;
 }
@@ -2159,8 +2189,14 @@ int r16_bwd(r16::Args a, int64_t G, float *v_means2d, float *v_conics, float *v_
       a.items = nullptr;
       a.n_items = nullptr;
     }
-    if (bwd_px() == 2)
+    if (bwd_px() == 2 && bwd_pf())
+      hipLaunchKernelGGL((r16::bwd2_kernel<D, ABS, 2, true>), dim3((unsigned)grid), dim3(128), 0,
+                         st, a);
+    else if (bwd_px() == 2)
       hipLaunchKernelGGL((r16::bwd2_kernel<D, ABS, 2>), dim3((unsigned)grid), dim3(128), 0, st, a);
+    else if (bwd_px() == 4 && bwd_pf())
+      hipLaunchKernelGGL((r16::bwd2_kernel<D, ABS, 4, true>), dim3((unsigned)grid), dim3(64), 0,
+                         st, a);
     else if (bwd_px() == 4)
       hipLaunchKernelGGL((r16::bwd2_kernel<D, ABS, 4>), dim3((unsigned)grid), dim3(64), 0, st, a);
     else
