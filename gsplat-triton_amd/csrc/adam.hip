@@ -28,9 +28,7 @@ struct Groups {
 
 GS_INLINE void upd(float &p, float gr, float &m, float &v, float b1, float b2, float eps,
                    float ss, float ib) {
-  m = m + (1.f - b1) * (gr - m);  // lerp(m, g, 1 - beta1)
-  v = b2 * v + (1.f - b2) * gr * gr;
-  p -= ss * m / (sqrtf(v) * ib + eps);
+  adam_update(p, gr, m, v, b1, b2, eps, ss, ib);
 }
 
 typedef float f4v __attribute__((ext_vector_type(4)));

@@ -42,6 +42,21 @@ void set_error(const char *fmt, ...);
     }                                                                          \
   } while (0)
 
+// ------------------------------------------------------------------- Adam
+// torch.optim.Adam's element update (amsgrad=False, no weight decay):
+// exp_avg via lerp, bias corrections folded into ss = lr / (1 - beta1^t) and
+// ib = 1 / sqrt(1 - beta2^t).  Shared by adam.hip and the SH backward with
+// the update fused in (sh.hip), so both round identically.
+// Every operation is spelled out (explicit fma / rounded mul, add, div) so
+// the compiler's contraction choices cannot differ between the two callers.
+GS_INLINE void adam_update(float &p, float gr, float &m, float &v, float b1, float b2, float eps,
+                           float ss, float ib) {
+  m = __fmaf_rn(1.f - b1, __fsub_rn(gr, m), m);  // lerp(m, g, 1 - beta1)
+  v = __fmaf_rn(b2, v, __fmul_rn(__fmul_rn(1.f - b2, gr), gr));
+  const float den = __fmaf_rn(sqrtf(v), ib, eps);
+  p = __fsub_rn(p, __fdiv_rn(__fmul_rn(ss, m), den));
+}
+
 // ------------------------------------------------------------- wave reduce
 // Butterfly sum over the 64 lanes; every lane ends with the total.
 GS_INLINE float wave_sum(float v) {

@@ -283,12 +283,24 @@ struct RowWalk {
 // writes its gradient row to LDS; the wave then stores its 64 rows (zeros
 // for masked rows) lane-contiguously, instead of 3K stores per lane that each
 // touch 64 cache lines.  LDS rows have an odd stride (bank-conflict free).
-template <int DEG, bool FUSED>
+//
+// ADAM: instead of storing the gradient rows, apply torch.optim.Adam to the
+// coefficient rows in place (the optimizer step fused into its producer:
+// the gradient never goes through HBM).  KR = rest coefficients per row
+// (the parameter's K - 1; those above the active degree get zero gradient
+// and still their Adam update).
+struct AdamSH {
+  float *m0, *v0, *mr, *vr;  // moments of coeffs / coeffs_rest, same layout
+  float ss0, ssr, ib, b1, b2, eps;
+};
+
+template <int DEG, bool FUSED, int KR = (DEG + 1) * (DEG + 1) - 1, bool ADAM = false>
 __global__ void __launch_bounds__(256)
 sh_bwd_staged_kernel(int64_t n, Coeffs cf, const float *__restrict__ dirs,
                      const uint8_t *__restrict__ masks, const float *__restrict__ v_colors,
-                     VCoeffs vc, float *__restrict__ v_dirs, Fused fz) {
-  constexpr int NB = (DEG + 1) * (DEG + 1), WR = 3 * (NB - 1), RSR = WR | 1;
+                     VCoeffs vc, float *__restrict__ v_dirs, Fused fz, AdamSH ad = AdamSH{}) {
+  constexpr int NB = (DEG + 1) * (DEG + 1), WR = 3 * KR, RSR = WR | 1;
+  static_assert(KR >= NB - 1, "KR covers the active coefficients");
   __shared__ float l_dc[4][64 * 3];               // row stride 3 (odd)
   __shared__ float l_rest[4][64 * (RSR > 1 ? RSR : 1)];  // odd row stride
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -365,12 +377,39 @@ sh_bwd_staged_kernel(int64_t n, Coeffs cf, const float *__restrict__ dirs,
       grow(k, 1) = B[k] * vg;
       grow(k, 2) = B[k] * vb;
     }
+#pragma unroll
+    for (int k = NB; k <= KR; ++k) grow(k, 0) = grow(k, 1) = grow(k, 2) = 0.f;
   } else if (lane < rows) {
 #pragma unroll
-    for (int k = 0; k < NB; ++k) grow(k, 0) = grow(k, 1) = grow(k, 2) = 0.f;
+    for (int k = 0; k <= KR; ++k) grow(k, 0) = grow(k, 1) = grow(k, 2) = 0.f;
     if (v_dirs) { v_dirs[3 * i] = 0.f; v_dirs[3 * i + 1] = 0.f; v_dirs[3 * i + 2] = 0.f; }
   }
   __builtin_amdgcn_wave_barrier();
+  if (ADAM) {  // Adam on the wave's 64 coefficient rows, lane-contiguous
+    float *P0 = const_cast<float *>(cf.c0) + i0 * cf.s0;
+    RowWalk<3> w0(lane);
+    for (int e = lane; e < rows * 3; e += 64, w0.next()) {
+      const int64_t o = (int64_t)w0.rr * cf.s0 + w0.c;
+      float pp = P0[o], mm = ad.m0[i0 * cf.s0 + o], vv = ad.v0[i0 * cf.s0 + o];
+      adam_update(pp, sd[w0.rr * 3 + w0.c], mm, vv, ad.b1, ad.b2, ad.eps, ad.ss0, ad.ib);
+      P0[o] = pp;
+      ad.m0[i0 * cf.s0 + o] = mm;
+      ad.v0[i0 * cf.s0 + o] = vv;
+    }
+    if (WR > 0) {
+      float *Pr = const_cast<float *>(cf.cr) + i0 * cf.sr;
+      RowWalk<(WR > 0 ? WR : 1)> wr(lane);
+      for (int e = lane; e < rows * WR; e += 64, wr.next()) {
+        const int64_t o = (int64_t)wr.rr * cf.sr + wr.c;
+        float pp = Pr[o], mm = ad.mr[i0 * cf.sr + o], vv = ad.vr[i0 * cf.sr + o];
+        adam_update(pp, sr[wr.rr * RSR + wr.c], mm, vv, ad.b1, ad.b2, ad.eps, ad.ssr, ad.ib);
+        Pr[o] = pp;
+        ad.mr[i0 * cf.sr + o] = mm;
+        ad.vr[i0 * cf.sr + o] = vv;
+      }
+    }
+    return;
+  }
   {  // gradient rows out, lane-contiguous
     float *g0 = vc.c0 + i0 * vc.s0;
     RowWalk<3> w0(lane);
@@ -509,5 +548,41 @@ extern "C" int gsplat_hip_sh_colors_bwd(int degree, int C, int64_t N, int64_t n_
   switch (degree) { GS_SH_BWD(0) GS_SH_BWD(1) GS_SH_BWD(2) GS_SH_BWD(3) GS_SH_BWD(4) }
 #undef GS_SH_BWD
   GS_CHECK_LAUNCH("sh_colors_bwd");
+  return 0;
+}
+
+// gsplat_hip_sh_colors_bwd with the coefficients' Adam step fused in (C == 1,
+// one coefficient row per Gaussian, K == 16 with coeffs_rest): coeffs and
+// coeffs_rest are updated in place with torch.optim.Adam (lr0 / lr_rest,
+// shared betas / eps, 1-based step) from the gradient this backward computes,
+// which is never stored; v_dirs as in gsplat_hip_sh_colors_bwd.
+extern "C" int gsplat_hip_sh_colors_bwd_adam(int degree, int64_t N, const float *means,
+                                             const float *viewmats, float *coeffs,
+                                             float *coeffs_rest, const int32_t *radii,
+                                             const float *v_colors, float *v_dirs, float *m0,
+                                             float *v0, float *m_rest, float *v_rest, float lr0,
+                                             float lr_rest, float beta1, float beta2, float eps,
+                                             int step, void *stream) {
+  if (N <= 0) return 0;
+  GS_REQUIRE(degree >= 0 && degree <= 3, "sh_colors_bwd_adam: degree %d not in [0, 3]", degree);
+  GS_REQUIRE(coeffs && coeffs_rest && m0 && v0 && m_rest && v_rest,
+             "sh_colors_bwd_adam: null coefficient or moment buffer");
+  GS_REQUIRE(step >= 1, "sh_colors_bwd_adam: step must be >= 1");
+  const double bc1 = 1.0 - pow((double)beta1, step), bc2 = 1.0 - pow((double)beta2, step);
+  AdamSH ad{m0, v0, m_rest, v_rest, (float)(lr0 / bc1), (float)(lr_rest / bc1),
+            (float)(1.0 / sqrt(bc2)), beta1, beta2, eps};
+  Coeffs cf{coeffs, coeffs_rest, 3, 45};
+  VCoeffs vc{nullptr, nullptr, 3, 45};
+  const Fused fz{means, viewmats, radii, N};
+  dim3 grid((unsigned)((N + 255) / 256));
+  hipStream_t st = (hipStream_t)stream;
+#define GS_SH_BWD_ADAM(D)                                                                      \
+  case D:                                                                                      \
+    hipLaunchKernelGGL((sh_bwd_staged_kernel<D, true, 15, true>), grid, dim3(256), 0, st, N, cf, \
+                       nullptr, nullptr, v_colors, vc, v_dirs, fz, ad);                        \
+    break;
+  switch (degree) { GS_SH_BWD_ADAM(0) GS_SH_BWD_ADAM(1) GS_SH_BWD_ADAM(2) GS_SH_BWD_ADAM(3) }
+#undef GS_SH_BWD_ADAM
+  GS_CHECK_LAUNCH("sh_colors_bwd_adam");
   return 0;
 }

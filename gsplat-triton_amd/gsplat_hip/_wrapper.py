@@ -15,9 +15,10 @@ Same signatures, defaults, assertions, error types and autograd contract
 stream; there is no CPU or Triton fallback.
 """
 
+import ctypes
 import math
-import time
 import os
+import time
 from typing import Optional, Tuple
 
 import torch
@@ -532,6 +533,30 @@ def spherical_harmonics(
     return _SphericalHarmonics.apply(degrees_to_use, dirs, coeffs, masks, block_size, rest)
 
 
+class ShAdamInBackward:
+    """Arms the next SH-colour backward (C == 1, coefficients [N,1,3] +
+    [N,15,3]) to apply torch.optim.Adam to these coefficient tensors in place
+    instead of returning their gradients (gsplat_hip_sh_colors_bwd_adam): the
+    trainer's optimizer step for the SH groups fused into their producer.
+    `applied` tells the caller whether it ran (else: take the normal step)."""
+
+    def __init__(self, coeffs, coeffs_rest, m0, v0, m_rest, v_rest, lr0, lr_rest, betas, eps,
+                 step):
+        self.coeffs, self.coeffs_rest = coeffs, coeffs_rest
+        self.moments = (m0, v0, m_rest, v_rest)
+        self.lr0, self.lr_rest, self.betas, self.eps, self.step = lr0, lr_rest, betas, eps, step
+        self.applied = False
+
+    def matches(self, base, rest, C, N, K, n_rows, degree):
+        return (not self.applied and C == 1 and rest is not None and K == 16 and n_rows == N
+                and degree <= 3 and base.data_ptr() == self.coeffs.data_ptr()
+                and rest.data_ptr() == self.coeffs_rest.data_ptr()
+                and self.coeffs.is_contiguous() and self.coeffs_rest.is_contiguous())
+
+
+_SH_ADAM = None  # an armed ShAdamInBackward (set around loss.backward() by the trainer)
+
+
 class _SHColors(torch.autograd.Function):
     """rasterization()'s SH colour path in one kernel each way
     (gsplat/rendering.py:396-406): clamp_min(SH(means - campos) + 0.5, 0)
@@ -574,6 +599,17 @@ class _SHColors(torch.autograd.Function):
             v_rest = torch.empty(C, N, K - 1, 3, device=dev)
         want_means = ctx.needs_input_grad[1]
         v_dirs = torch.empty(C, N, 3, device=dev) if want_means else None
+        fa = _SH_ADAM
+        if fa is not None and fa.matches(base, rest, C, N, K, ctx.n_rows, ctx.sh_degree):
+            m0, v0, mr, vr = fa.moments
+            _lib.call("gsplat_hip_sh_colors_bwd_adam", ctx.sh_degree, N, _ptr(means),
+                      _ptr(viewmats), _ptr(base), _ptr(rest), _ptr(radii), _ptr(v_colors),
+                      _ptr(v_dirs), _ptr(m0), _ptr(v0), _ptr(mr), _ptr(vr),
+                      ctypes.c_float(fa.lr0), ctypes.c_float(fa.lr_rest),
+                      ctypes.c_float(fa.betas[0]), ctypes.c_float(fa.betas[1]),
+                      ctypes.c_float(fa.eps), int(fa.step), _stream())
+            fa.applied = True
+            return (None, v_dirs[0] if want_means else None, None, None, None, None)
         _lib.call("gsplat_hip_sh_colors_bwd", ctx.sh_degree, C, N, ctx.n_rows, K, _ptr(means),
                   _ptr(viewmats), _ptr(base), _ptr(rest), _ptr(radii), _ptr(v_colors),
                   _ptr(v_coeffs), _ptr(v_rest), _ptr(v_dirs), _stream())

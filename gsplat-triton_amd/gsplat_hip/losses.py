@@ -184,15 +184,20 @@ class FusedAdam:
                     max_blocks)
 
     @torch.no_grad()
-    def step(self):
+    def step(self, skip=()):
+        """skip: indices already updated for this step (by the SH backward
+        with the update fused in, train_step.Trainer)."""
         self.wait()  # a previous deferred update is ordered before this one
         self.step_count += 1
         grads = [p.grad for p in self.params]
         for gr in grads:
             assert gr is None or gr.is_contiguous()
         if self.side is None:
-            self._launch(range(len(self.params)), grads)
+            idx = [i for i in range(len(self.params)) if i not in skip]
+            if idx:
+                self._launch(idx, grads)
             return
+        assert not skip, "skip and deferred groups are exclusive"
         now = [i for i in range(len(self.params)) if i not in self.deferred]
         if now:
             self._launch(now, grads)

@@ -44,6 +44,7 @@ import torch.nn.functional as F
 from . import densify
 from .densify import DefaultStrategyConfig
 from .losses import FusedAdam, l1_ssim_loss, ssim_and_l1
+from . import _wrapper
 from .rendering import rasterization, rasterization_2dgs
 from .strategy import activate, update_state_
 
@@ -192,6 +193,12 @@ class Trainer:
         # filling each other's gaps, so it is off by default.
         self.defer_sh = (fused and not self.sharded and torch.device(device).type == "cuda"
                          and os.environ.get("GSPLAT_HIP_DEFER_SH", "0") == "1")
+        # one rank, fused path: the SH coefficients' Adam step runs inside the
+        # SH-colour backward (gsplat_hip_sh_colors_bwd_adam), so their
+        # gradients never go through HBM; GSPLAT_HIP_SH_ADAM_IN_BWD=0 turns it off
+        self.sh_adam_in_bwd = (fused and not self.sharded and not self.defer_sh
+                               and world_size == 1 and model == "3dgs"
+                               and os.environ.get("GSPLAT_HIP_SH_ADAM_IN_BWD", "0") == "1")
         self.opt = self._make_optimizer(list(self.params.values()))
         self.viewmats = viewmats.to(device)
         self.Ks = Ks.to(device)
@@ -342,7 +349,11 @@ class Trainer:
             ssim_loss = 1.0 - ssim(colors.permute(0, 3, 1, 2), gt.permute(0, 3, 1, 2),
                                    self.window)
             loss = l1 * (1.0 - self.ssim_lambda) + ssim_loss * self.ssim_lambda
-        loss.backward()
+        fa = self._arm_sh_adam()
+        try:
+            loss.backward()
+        finally:
+            _wrapper._SH_ADAM = None
         if self.world_size > 1 and not self.sharded:
             self.allreduce_grads()
         if self.strategy is None or it < self.strategy.refine_stop_iter:
@@ -351,6 +362,9 @@ class Trainer:
             self._set_means_lr(self.lrs[0] * (0.01 ** (1.0 / self.max_steps)) ** it)
         if self.sharded:
             self.opt.step(defer_gather=True)
+        elif fa is not None and fa.applied:
+            names = list(self.params)
+            self.opt.step(skip=(names.index("sh0"), names.index("shN")))
         else:
             self.opt.step()
         self.opt.zero_grad(set_to_none=True)
@@ -358,6 +372,21 @@ class Trainer:
         if self.strategy is not None:
             self.post_step(it)
         return loss
+
+    def _arm_sh_adam(self):
+        """Arm the SH-colour backward of this step to apply the SH groups'
+        Adam update in place (see sh_adam_in_bwd); None when off."""
+        if not getattr(self, "sh_adam_in_bwd", False) or not isinstance(self.opt, FusedAdam):
+            return None
+        names = list(self.params)
+        i0, i1 = names.index("sh0"), names.index("shN")
+        o = self.opt
+        fa = _wrapper.ShAdamInBackward(
+            self.params["sh0"].data, self.params["shN"].data, o.exp_avg[i0], o.exp_avg_sq[i0],
+            o.exp_avg[i1], o.exp_avg_sq[i1], o.lrs[i0], o.lrs[i1], o.betas, o.eps,
+            o.step_count + 1)
+        _wrapper._SH_ADAM = fa
+        return fa
 
     # ---------------------------------------------------------------- eval
     @torch.no_grad()

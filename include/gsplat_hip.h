@@ -360,6 +360,20 @@ int gsplat_hip_densify_apply(int64_t N, const void *workspace, const int64_t *to
                              const int32_t *kinds, const float *means, const float *quats,
                              const float *log_scales, const float *logits, void *stream);
 
+/* gsplat_hip_sh_colors_bwd for C == 1 with the coefficients' Adam step fused
+ * in (ABI 18): coeffs [N,1,3] and coeffs_rest [N,15,3] are updated in place
+ * by torch.optim.Adam (lr0 / lr_rest, shared betas and eps, 1-based step,
+ * moments m0/v0 and m_rest/v_rest in the coefficients' layout) from the
+ * gradient this backward computes, which is never written; v_dirs [N,3] as
+ * in gsplat_hip_sh_colors_bwd.  degree 0..3 (zero gradient above it).  The
+ * trainer's optimizer-in-backward for the SH groups (81 % of Adam's bytes). */
+int gsplat_hip_sh_colors_bwd_adam(int degree, int64_t N, const float *means,
+                                  const float *viewmats, float *coeffs, float *coeffs_rest,
+                                  const int32_t *radii, const float *v_colors, float *v_dirs,
+                                  float *m0, float *v0, float *m_rest, float *v_rest, float lr0,
+                                  float lr_rest, float beta1, float beta2, float eps, int step,
+                                  void *stream);
+
 /* One torch.optim.Adam step (amsgrad=False, no weight decay) over up to 8
  * parameter groups in a single launch (replaces the per-group optimizers of
  * examples/simple_trainer.py:265-276).  Host arrays of length n_groups. */

@@ -294,3 +294,54 @@ def test_trainer_deferred_sh_runs_through_refines(monkeypatch):
     assert out["0"][1] == out["1"][1] == [2, 4]
     for a, b in zip(out["0"][0], out["1"][0]):
         assert abs(a - b) <= 1e-3 * abs(a) + 1e-6, (out["0"][0], out["1"][0])
+
+
+@pytest.mark.parametrize("degree", [3, 1])
+def test_sh_adam_in_backward_is_exact(degree):
+    """The SH-colour backward with the coefficients' Adam step fused in
+    (gsplat_hip_sh_colors_bwd_adam) leaves the coefficients and moments
+    bit-identical to the plain backward + FusedAdam, over several steps, and
+    returns the same means gradient; invisible rows and coefficients above
+    the active degree get their zero-gradient Adam update too."""
+    from gsplat_hip import _wrapper
+    from gsplat_hip.losses import FusedAdam
+    g = torch.Generator(device="cuda").manual_seed(5)
+    N = 3000
+    means = torch.randn(N, 3, device="cuda", generator=g) * 2
+    vm = torch.eye(4, device="cuda")[None]
+    vm[0, 2, 3] = 6.0
+    radii = (torch.rand(1, N, device="cuda", generator=g) > 0.4).int() * 3
+    sh0 = torch.randn(N, 1, 3, device="cuda", generator=g) * 0.3
+    shN = torch.randn(N, 15, 3, device="cuda", generator=g) * 0.1
+    ws = [torch.rand(1, N, 3, device="cuda", generator=g) - 0.5 for _ in range(4)]
+    res = []
+    for fused in (False, True):
+        p0 = sh0.clone().requires_grad_(True)
+        p1 = shN.clone().requires_grad_(True)
+        mm = means.clone().requires_grad_(True)
+        opt = FusedAdam([p0, p1], [2.5e-3, 2.5e-3 / 20], betas=(0.9, 0.999), eps=1e-15)
+        gm = []
+        for it in range(4):
+            fa = None
+            if fused:
+                fa = _wrapper.ShAdamInBackward(p0.data, p1.data, opt.exp_avg[0], opt.exp_avg_sq[0],
+                                               opt.exp_avg[1], opt.exp_avg_sq[1], opt.lrs[0],
+                                               opt.lrs[1], opt.betas, opt.eps, opt.step_count + 1)
+                _wrapper._SH_ADAM = fa
+            try:
+                colors = _wrapper.sh_colors(degree, mm, vm, (p0, p1), radii)
+                (colors * ws[it]).sum().backward()
+            finally:
+                _wrapper._SH_ADAM = None
+            if fused:
+                assert fa.applied and p0.grad is None and p1.grad is None
+                opt.step(skip=(0, 1))
+            else:
+                opt.step()
+            opt.zero_grad()
+            gm.append(mm.grad.clone())
+            mm.grad = None
+        torch.cuda.synchronize()
+        res.append((p0.detach().clone(), p1.detach().clone(), *opt.exp_avg, *opt.exp_avg_sq, *gm))
+    for a, b in zip(res[0], res[1]):
+        assert torch.equal(a, b)
