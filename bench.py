@@ -336,7 +336,10 @@ def main():
                    "cameras_per_rank_per_step": 1, "parallelism": f"dp{world}",
                    "n_isects_mean": float(np.mean(isects)), "n_eff_mean": float(np.mean(n_effs)),
                    "packed": False, "loss": "0.8*L1+0.2*(1-SSIM valid)",
-                   "optimizer": "Adam (6 groups)" + (", sharded over ranks" if world > 1 else ""),
+                   "optimizer": "Adam (6 groups)" + (
+                       ", sharded over ranks" if world > 1 else
+                       ", SH groups' step fused into the SH backward"
+                       if getattr(tr, "sh_adam_in_bwd", False) else ""),
                    "densification": tr.densify_desc()},
         "roofline": {"kernel": kname, "bound": "hbm", "achieved": achieved,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,

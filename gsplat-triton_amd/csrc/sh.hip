@@ -289,10 +289,46 @@ struct RowWalk {
 // the gradient never goes through HBM).  KR = rest coefficients per row
 // (the parameter's K - 1; those above the active degree get zero gradient
 // and still their Adam update).
+
+
 struct AdamSH {
   float *m0, *v0, *mr, *vr;  // moments of coeffs / coeffs_rest, same layout
   float ss0, ssr, ib, b1, b2, eps;
 };
+
+// Adam over `rows` consecutive rows of WID floats (16-B aligned start): the
+// gradient of element (r, c) is g[r * GS + c] (LDS); 4 elements per lane and
+// iteration as float4, a scalar tail.
+template <int WID, int GS>
+GS_INLINE void adam_rows(float *P, float *M, float *V, const float *g, int rows, int lane,
+                         float ss, const AdamSH &ad) {
+  const int count = rows * WID, n4 = count >> 2;
+  float4 *P4 = reinterpret_cast<float4 *>(P);
+  float4 *M4 = reinterpret_cast<float4 *>(M);
+  float4 *V4 = reinterpret_cast<float4 *>(V);
+  auto gr = [&](int e) {
+    const int r = e / WID;
+    return g[r * GS + (e - r * WID)];
+  };
+  for (int q = lane; q < n4; q += 64) {
+    float4 p = P4[q], m = M4[q], v = V4[q];
+    const int e = 4 * q;
+    adam_update(p.x, gr(e), m.x, v.x, ad.b1, ad.b2, ad.eps, ss, ad.ib);
+    adam_update(p.y, gr(e + 1), m.y, v.y, ad.b1, ad.b2, ad.eps, ss, ad.ib);
+    adam_update(p.z, gr(e + 2), m.z, v.z, ad.b1, ad.b2, ad.eps, ss, ad.ib);
+    adam_update(p.w, gr(e + 3), m.w, v.w, ad.b1, ad.b2, ad.eps, ss, ad.ib);
+    P4[q] = p;
+    M4[q] = m;
+    V4[q] = v;
+  }
+  for (int e = 4 * n4 + lane; e < count; e += 64) {
+    float pp = P[e], mm = M[e], vv = V[e];
+    adam_update(pp, gr(e), mm, vv, ad.b1, ad.b2, ad.eps, ss, ad.ib);
+    P[e] = pp;
+    M[e] = mm;
+    V[e] = vv;
+  }
+}
 
 template <int DEG, bool FUSED, int KR = (DEG + 1) * (DEG + 1) - 1, bool ADAM = false>
 __global__ void __launch_bounds__(256)
@@ -385,29 +421,12 @@ sh_bwd_staged_kernel(int64_t n, Coeffs cf, const float *__restrict__ dirs,
     if (v_dirs) { v_dirs[3 * i] = 0.f; v_dirs[3 * i + 1] = 0.f; v_dirs[3 * i + 2] = 0.f; }
   }
   __builtin_amdgcn_wave_barrier();
-  if (ADAM) {  // Adam on the wave's 64 coefficient rows, lane-contiguous
-    float *P0 = const_cast<float *>(cf.c0) + i0 * cf.s0;
-    RowWalk<3> w0(lane);
-    for (int e = lane; e < rows * 3; e += 64, w0.next()) {
-      const int64_t o = (int64_t)w0.rr * cf.s0 + w0.c;
-      float pp = P0[o], mm = ad.m0[i0 * cf.s0 + o], vv = ad.v0[i0 * cf.s0 + o];
-      adam_update(pp, sd[w0.rr * 3 + w0.c], mm, vv, ad.b1, ad.b2, ad.eps, ad.ss0, ad.ib);
-      P0[o] = pp;
-      ad.m0[i0 * cf.s0 + o] = mm;
-      ad.v0[i0 * cf.s0 + o] = vv;
-    }
-    if (WR > 0) {
-      float *Pr = const_cast<float *>(cf.cr) + i0 * cf.sr;
-      RowWalk<(WR > 0 ? WR : 1)> wr(lane);
-      for (int e = lane; e < rows * WR; e += 64, wr.next()) {
-        const int64_t o = (int64_t)wr.rr * cf.sr + wr.c;
-        float pp = Pr[o], mm = ad.mr[i0 * cf.sr + o], vv = ad.vr[i0 * cf.sr + o];
-        adam_update(pp, sr[wr.rr * RSR + wr.c], mm, vv, ad.b1, ad.b2, ad.eps, ad.ssr, ad.ib);
-        Pr[o] = pp;
-        ad.mr[i0 * cf.sr + o] = mm;
-        ad.vr[i0 * cf.sr + o] = vv;
-      }
-    }
+  if (ADAM) {  // Adam on the wave's 64 coefficient rows: 16-B vectors, lane-contiguous
+    adam_rows<3, 3>(const_cast<float *>(cf.c0) + i0 * 3, ad.m0 + i0 * 3, ad.v0 + i0 * 3, sd,
+                    rows, lane, ad.ss0, ad);
+    if (WR > 0)
+      adam_rows<(WR > 0 ? WR : 1), RSR>(const_cast<float *>(cf.cr) + i0 * WR, ad.mr + i0 * WR,
+                                         ad.vr + i0 * WR, sr, rows, lane, ad.ssr, ad);
     return;
   }
   {  // gradient rows out, lane-contiguous
@@ -568,6 +587,9 @@ extern "C" int gsplat_hip_sh_colors_bwd_adam(int degree, int64_t N, const float 
   GS_REQUIRE(coeffs && coeffs_rest && m0 && v0 && m_rest && v_rest,
              "sh_colors_bwd_adam: null coefficient or moment buffer");
   GS_REQUIRE(step >= 1, "sh_colors_bwd_adam: step must be >= 1");
+  GS_REQUIRE((((uintptr_t)coeffs | (uintptr_t)coeffs_rest | (uintptr_t)m0 | (uintptr_t)v0 |
+               (uintptr_t)m_rest | (uintptr_t)v_rest) & 15) == 0,
+             "sh_colors_bwd_adam: coefficient and moment buffers must be 16-B aligned");
   const double bc1 = 1.0 - pow((double)beta1, step), bc2 = 1.0 - pow((double)beta2, step);
   AdamSH ad{m0, v0, m_rest, v_rest, (float)(lr0 / bc1), (float)(lr_rest / bc1),
             (float)(1.0 / sqrt(bc2)), beta1, beta2, eps};

@@ -548,8 +548,11 @@ class ShAdamInBackward:
         self.applied = False
 
     def matches(self, base, rest, C, N, K, n_rows, degree):
+        # degree 3 only: the staged kernel of the unfused backward at K == 16,
+        # so the two paths are bit-identical (lower degrees of the SH schedule
+        # take the unfused path)
         return (not self.applied and C == 1 and rest is not None and K == 16 and n_rows == N
-                and degree <= 3 and base.data_ptr() == self.coeffs.data_ptr()
+                and degree == 3 and base.data_ptr() == self.coeffs.data_ptr()
                 and rest.data_ptr() == self.coeffs_rest.data_ptr()
                 and self.coeffs.is_contiguous() and self.coeffs_rest.is_contiguous())
 

@@ -301,12 +301,12 @@ def test_sh_adam_in_backward_is_exact(degree):
     """The SH-colour backward with the coefficients' Adam step fused in
     (gsplat_hip_sh_colors_bwd_adam) leaves the coefficients and moments
     bit-identical to the plain backward + FusedAdam, over several steps, and
-    returns the same means gradient; invisible rows and coefficients above
-    the active degree get their zero-gradient Adam update too."""
+    returns the same means gradient; invisible rows get their zero-gradient
+    Adam update too.  Below degree 3 the armed backward declines (unfused)."""
     from gsplat_hip import _wrapper
     from gsplat_hip.losses import FusedAdam
     g = torch.Generator(device="cuda").manual_seed(5)
-    N = 3000
+    N = 3001  # a last wave of 57 rows: scalar tails of the float4 walk
     means = torch.randn(N, 3, device="cuda", generator=g) * 2
     vm = torch.eye(4, device="cuda")[None]
     vm[0, 2, 3] = 6.0
@@ -333,10 +333,11 @@ def test_sh_adam_in_backward_is_exact(degree):
                 (colors * ws[it]).sum().backward()
             finally:
                 _wrapper._SH_ADAM = None
-            if fused:
+            if fused and degree == 3:
                 assert fa.applied and p0.grad is None and p1.grad is None
                 opt.step(skip=(0, 1))
-            else:
+            else:  # lower degrees: the armed backward falls back to the unfused one
+                assert fa is None or not fa.applied
                 opt.step()
             opt.zero_grad()
             gm.append(mm.grad.clone())

@@ -11,5 +11,5 @@ for r in 1 2; do
     GSPLAT_HIP_SH_ADAM_IN_BWD=$f timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-traffic > $O/bench_f$f.$r.json 2>/dev/null || exit 2
   done
 done
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $O/trace -o run -- /usr/bin/python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-traffic > $O/trace.log 2>&1 || exit 3
+GSPLAT_HIP_SH_ADAM_IN_BWD=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $O/trace -o run -- /usr/bin/python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-traffic > $O/trace.log 2>&1 || exit 3
 exit 0
