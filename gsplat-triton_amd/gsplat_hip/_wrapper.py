@@ -601,7 +601,10 @@ class _SHColors(torch.autograd.Function):
             v_coeffs = torch.empty(C, N, 1, 3, device=dev)
             v_rest = torch.empty(C, N, K - 1, 3, device=dev)
         want_means = ctx.needs_input_grad[1]
-        v_dirs = torch.empty(C, N, 3, device=dev) if want_means else None
+        # C == 1: a plain [N, 3] tensor (same bytes as [1, N, 3]), so autograd's
+        # gradient accumulation can take it over instead of copying a view
+        v_dirs = (torch.empty(N, 3, device=dev) if C == 1 else
+                  torch.empty(C, N, 3, device=dev)) if want_means else None
         fa = _SH_ADAM
         if fa is not None and fa.matches(base, rest, C, N, K, ctx.n_rows, ctx.sh_degree):
             m0, v0, mr, vr = fa.moments
@@ -612,13 +615,13 @@ class _SHColors(torch.autograd.Function):
                       ctypes.c_float(fa.betas[0]), ctypes.c_float(fa.betas[1]),
                       ctypes.c_float(fa.eps), int(fa.step), _stream())
             fa.applied = True
-            return (None, v_dirs[0] if want_means else None, None, None, None, None)
+            return (None, v_dirs, None, None, None, None)
         _lib.call("gsplat_hip_sh_colors_bwd", ctx.sh_degree, C, N, ctx.n_rows, K, _ptr(means),
                   _ptr(viewmats), _ptr(base), _ptr(rest), _ptr(radii), _ptr(v_colors),
                   _ptr(v_coeffs), _ptr(v_rest), _ptr(v_dirs), _stream())
         v_means = None
         if want_means:
-            v_means = v_dirs[0] if C == 1 else v_dirs.sum(0)
+            v_means = v_dirs if C == 1 else v_dirs.sum(0)
         def fold(v, shape):  # [C,N,..] -> the input's shape (sum over cameras)
             if v is None:
                 return None
