@@ -197,7 +197,7 @@ class Trainer:
         # SH-colour backward (gsplat_hip_sh_colors_bwd_adam), so their
         # gradients never go through HBM; GSPLAT_HIP_SH_ADAM_IN_BWD=0 turns it off
         self.sh_adam_in_bwd = (fused and not self.sharded and not self.defer_sh
-                               and world_size == 1 and model == "3dgs"
+                               and world_size == 1
                                and os.environ.get("GSPLAT_HIP_SH_ADAM_IN_BWD", "1") != "0")
         self.opt = self._make_optimizer(list(self.params.values()))
         self.viewmats = viewmats.to(device)
