@@ -14,9 +14,21 @@ namespace adam {
 
 constexpr int kMaxGroups = 8;
 
+// Gradient transform per group (gsplat_hip_adam_step_ex): the update's
+// gradient is formed in-register from what the backward left, replacing the
+// separate VJP / accumulation launches.  Same arithmetic as those kernels.
+enum GradMode : int {
+  kGrad = 0,     // g
+  kSum = 1,      // g + aux        (two gradient contributions, autograd's sum)
+  kExpVjp = 2,   // g * aux        (exp: aux = exp(x), activate_bwd_kernel)
+  kSigVjp = 3,   // g * (1 - aux) * aux   (sigmoid: aux = sigmoid(x))
+};
+
 struct Groups {
   float *param[kMaxGroups];
   const float *grad[kMaxGroups];
+  const float *aux[kMaxGroups];  // second gradient or activation (modes 1-3)
+  int mode[kMaxGroups];
   float *m[kMaxGroups];
   float *v[kMaxGroups];
   int64_t numel[kMaxGroups];
@@ -29,6 +41,13 @@ struct Groups {
 GS_INLINE void upd(float &p, float gr, float &m, float &v, float b1, float b2, float eps,
                    float ss, float ib) {
   adam_update(p, gr, m, v, b1, b2, eps, ss, ib);
+}
+
+GS_INLINE float xform(int mode, float g, float a) {
+  if (mode == kSum) return g + a;
+  if (mode == kExpVjp) return g * a;
+  if (mode == kSigVjp) return g * (1.f - a) * a;
+  return g;
 }
 
 typedef float f4v __attribute__((ext_vector_type(4)));
@@ -55,7 +74,7 @@ step_kernel(Groups g, float beta1, float beta2, float eps) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t s0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s0 < total;
        s0 += stride * U) {
-    float4 p[U], gr[U], m[U], v[U];
+    float4 p[U], gr[U], m[U], v[U], ax[U];
     int grp[U];
     int64_t k0[U];
     bool full[U];
@@ -70,6 +89,7 @@ step_kernel(Groups g, float beta1, float beta2, float eps) {
       if (full[u]) {
         p[u] = ld4<NT>(g.param[gi] + k0[u]);
         gr[u] = g.grad[gi] ? ld4<NT>(g.grad[gi] + k0[u]) : make_float4(0, 0, 0, 0);
+        ax[u] = g.aux[gi] ? ld4<NT>(g.aux[gi] + k0[u]) : make_float4(0, 0, 0, 0);
         m[u] = ld4<NT>(g.m[gi] + k0[u]);
         v[u] = ld4<NT>(g.v[gi] + k0[u]);
       }
@@ -79,19 +99,21 @@ step_kernel(Groups g, float beta1, float beta2, float eps) {
       const int gi = grp[u];
       const float ss = g.step_size[gi], ib = g.inv_bc2_sqrt[gi];
       if (full[u]) {
-        upd(p[u].x, gr[u].x, m[u].x, v[u].x, beta1, beta2, eps, ss, ib);
-        upd(p[u].y, gr[u].y, m[u].y, v[u].y, beta1, beta2, eps, ss, ib);
-        upd(p[u].z, gr[u].z, m[u].z, v[u].z, beta1, beta2, eps, ss, ib);
-        upd(p[u].w, gr[u].w, m[u].w, v[u].w, beta1, beta2, eps, ss, ib);
+        const int md = g.mode[gi];
+        upd(p[u].x, xform(md, gr[u].x, ax[u].x), m[u].x, v[u].x, beta1, beta2, eps, ss, ib);
+        upd(p[u].y, xform(md, gr[u].y, ax[u].y), m[u].y, v[u].y, beta1, beta2, eps, ss, ib);
+        upd(p[u].z, xform(md, gr[u].z, ax[u].z), m[u].z, v[u].z, beta1, beta2, eps, ss, ib);
+        upd(p[u].w, xform(md, gr[u].w, ax[u].w), m[u].w, v[u].w, beta1, beta2, eps, ss, ib);
         st4<NT>(g.param[gi] + k0[u], p[u]);
         st4<NT>(g.m[gi] + k0[u], m[u]);
         st4<NT>(g.v[gi] + k0[u], v[u]);
       } else if (s0 + u * stride < total) {  // scalar tail of a group
         float *P = g.param[gi], *M = g.m[gi], *V = g.v[gi];
-        const float *G = g.grad[gi];
+        const float *G = g.grad[gi], *A = g.aux[gi];
+        const int md = g.mode[gi];
         for (int64_t k = k0[u]; k < g.numel[gi]; ++k) {
           float pp = P[k], mm = M[k], vv = V[k];
-          upd(pp, G ? G[k] : 0.f, mm, vv, beta1, beta2, eps, ss, ib);
+          upd(pp, xform(md, G ? G[k] : 0.f, A ? A[k] : 0.f), mm, vv, beta1, beta2, eps, ss, ib);
           P[k] = pp;
           M[k] = mm;
           V[k] = vv;
@@ -110,9 +132,10 @@ using namespace gs;
 // length n_groups; grads[i] may be NULL (treated as zero).  Every pointer must
 // be 16-B aligned.  `step` is the 1-based step count.
 static int adam_launch(int n_groups, float *const *params, const float *const *grads,
-                       float *const *exp_avgs, float *const *exp_avg_sqs, const int64_t *numels,
-                       const float *lrs, float beta1, float beta2, float eps, int step,
-                       int max_blocks, void *stream) {
+                       const float *const *aux, const int32_t *modes, float *const *exp_avgs,
+                       float *const *exp_avg_sqs, const int64_t *numels, const float *lrs,
+                       float beta1, float beta2, float eps, int step, int max_blocks,
+                       void *stream) {
   GS_REQUIRE(n_groups > 0 && n_groups <= adam::kMaxGroups, "adam: 1..%d groups supported",
              adam::kMaxGroups);
   GS_REQUIRE(step >= 1, "adam: step must be >= 1");
@@ -126,6 +149,13 @@ static int adam_launch(int n_groups, float *const *params, const float *const *g
     GS_REQUIRE((al & 15) == 0, "adam: group %d pointers must be 16-B aligned", i);
     g.param[i] = params[i];
     g.grad[i] = grads[i];
+    g.aux[i] = aux ? aux[i] : nullptr;
+    g.mode[i] = modes ? modes[i] : 0;
+    GS_REQUIRE(g.mode[i] >= 0 && g.mode[i] <= 3, "adam: group %d mode %d not in [0, 3]", i,
+               g.mode[i]);
+    GS_REQUIRE(g.mode[i] == 0 || g.aux[i] != nullptr, "adam: group %d mode %d needs aux", i,
+               g.mode[i]);
+    GS_REQUIRE(((uintptr_t)g.aux[i] & 15) == 0, "adam: group %d aux must be 16-B aligned", i);
     g.m[i] = exp_avgs[i];
     g.v[i] = exp_avg_sqs[i];
     g.numel[i] = numels[i];
@@ -157,8 +187,8 @@ extern "C" int gsplat_hip_adam_step(int n_groups, float *const *params, const fl
                                     float *const *exp_avgs, float *const *exp_avg_sqs,
                                     const int64_t *numels, const float *lrs, float beta1,
                                     float beta2, float eps, int step, void *stream) {
-  return adam_launch(n_groups, params, grads, exp_avgs, exp_avg_sqs, numels, lrs, beta1, beta2,
-                     eps, step, 0, stream);
+  return adam_launch(n_groups, params, grads, nullptr, nullptr, exp_avgs, exp_avg_sqs, numels, lrs,
+                     beta1, beta2, eps, step, 0, stream);
 }
 
 extern "C" int gsplat_hip_adam_step_bounded(int n_groups, float *const *params,
@@ -167,6 +197,16 @@ extern "C" int gsplat_hip_adam_step_bounded(int n_groups, float *const *params,
                                             const float *lrs, float beta1, float beta2, float eps,
                                             int step, int max_blocks, void *stream) {
   GS_REQUIRE(max_blocks > 0, "adam_step_bounded: max_blocks must be > 0");
-  return adam_launch(n_groups, params, grads, exp_avgs, exp_avg_sqs, numels, lrs, beta1, beta2,
-                     eps, step, max_blocks, stream);
+  return adam_launch(n_groups, params, grads, nullptr, nullptr, exp_avgs, exp_avg_sqs, numels, lrs,
+                     beta1, beta2, eps, step, max_blocks, stream);
+}
+
+extern "C" int gsplat_hip_adam_step_ex(int n_groups, float *const *params,
+                                       const float *const *grads, const float *const *aux,
+                                       const int32_t *modes, float *const *exp_avgs,
+                                       float *const *exp_avg_sqs, const int64_t *numels,
+                                       const float *lrs, float beta1, float beta2, float eps,
+                                       int step, void *stream) {
+  return adam_launch(n_groups, params, grads, aux, modes, exp_avgs, exp_avg_sqs, numels, lrs,
+                     beta1, beta2, eps, step, 0, stream);
 }

@@ -533,6 +533,17 @@ def spherical_harmonics(
     return _SphericalHarmonics.apply(degrees_to_use, dirs, coeffs, masks, block_size, rest)
 
 
+def _stash_means_grad(means, v_means):
+    """Hand the SH backward's means gradient to an armed geometry stash
+    (returns None then) or back to autograd."""
+    st = _GEOM_STASH
+    if (v_means is not None and st is not None and "v_dirs" not in st
+            and st.get("means_ptr") == means.data_ptr()):
+        st["v_dirs"] = v_means
+        return None
+    return v_means
+
+
 class ShAdamInBackward:
     """Arms the next SH-colour backward (C == 1, coefficients [N,1,3] +
     [N,15,3]) to apply torch.optim.Adam to these coefficient tensors in place
@@ -558,6 +569,11 @@ class ShAdamInBackward:
 
 
 _SH_ADAM = None  # an armed ShAdamInBackward (set around loss.backward() by the trainer)
+# The trainer's geometry-update stash (train_step.Trainer._arm_geom): a dict
+# with "means_ptr" (and the activation outputs' pointers, strategy.py); the
+# SH-colour backward leaves its means gradient here instead of returning it,
+# and the geometry groups' Adam adds it in-register (adam_step_ex mode 1).
+_GEOM_STASH = None
 
 
 class _SHColors(torch.autograd.Function):
@@ -615,13 +631,13 @@ class _SHColors(torch.autograd.Function):
                       ctypes.c_float(fa.betas[0]), ctypes.c_float(fa.betas[1]),
                       ctypes.c_float(fa.eps), int(fa.step), _stream())
             fa.applied = True
-            return (None, v_dirs, None, None, None, None)
+            return (None, _stash_means_grad(means, v_dirs), None, None, None, None)
         _lib.call("gsplat_hip_sh_colors_bwd", ctx.sh_degree, C, N, ctx.n_rows, K, _ptr(means),
                   _ptr(viewmats), _ptr(base), _ptr(rest), _ptr(radii), _ptr(v_colors),
                   _ptr(v_coeffs), _ptr(v_rest), _ptr(v_dirs), _stream())
         v_means = None
         if want_means:
-            v_means = v_dirs if C == 1 else v_dirs.sum(0)
+            v_means = _stash_means_grad(means, v_dirs) if C == 1 else v_dirs.sum(0)
         def fold(v, shape):  # [C,N,..] -> the input's shape (sum over cameras)
             if v is None:
                 return None

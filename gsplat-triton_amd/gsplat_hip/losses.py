@@ -126,20 +126,31 @@ def l1_ssim_loss(img, gt, ssim_lambda=0.2, fused=None):
     return _L1SSIMLoss.apply(img, gt, float(ssim_lambda))
 
 
-def adam_groups(params, grads, exp_avgs, exp_avg_sqs, lrs, betas, eps, step, max_blocks=0):
+def adam_groups(params, grads, exp_avgs, exp_avg_sqs, lrs, betas, eps, step, max_blocks=0,
+                aux=None, modes=None):
     """One fused Adam launch (csrc/adam.hip) over flat float32 tensors: group
     i updates params[i] in place from grads[i] (None = zero) with its lr.
-    max_blocks > 0 bounds the grid (gsplat_hip_adam_step_bounded)."""
+    max_blocks > 0 bounds the grid (gsplat_hip_adam_step_bounded); aux/modes
+    form the gradient in-register (gsplat_hip_adam_step_ex)."""
     n = len(params)
     P = ctypes.c_void_p * n
     for t in list(params) + list(exp_avgs) + list(exp_avg_sqs):
         assert t.is_contiguous() and t.dtype == torch.float32
-    args = [n, P(*[p.data_ptr() for p in params]),
-            P(*[0 if g is None else g.data_ptr() for g in grads]),
-            P(*[m.data_ptr() for m in exp_avgs]), P(*[v.data_ptr() for v in exp_avg_sqs]),
+    head = [n, P(*[p.data_ptr() for p in params]),
+            P(*[0 if g is None else g.data_ptr() for g in grads])]
+    tail = [P(*[m.data_ptr() for m in exp_avgs]), P(*[v.data_ptr() for v in exp_avg_sqs]),
             (ctypes.c_int64 * n)(*[p.numel() for p in params]),
             (ctypes.c_float * n)(*[float(x) for x in lrs]), float(betas[0]), float(betas[1]),
             float(eps), int(step)]
+    if modes is not None and any(modes):
+        assert max_blocks == 0
+        for a in aux:
+            assert a is None or (a.is_contiguous() and a.dtype == torch.float32)
+        _lib.call("gsplat_hip_adam_step_ex", *head,
+                  P(*[0 if a is None else a.data_ptr() for a in aux]),
+                  (ctypes.c_int32 * n)(*[int(m) for m in modes]), *tail, _stream())
+        return
+    args = head + tail
     if max_blocks > 0:
         _lib.call("gsplat_hip_adam_step_bounded", *args, int(max_blocks), _stream())
     else:
@@ -177,16 +188,23 @@ class FusedAdam:
             self.side = torch.cuda.Stream(device=self.params[0].device)
         self._event = None
 
-    def _launch(self, idx, grads, max_blocks=0):
+    def _launch(self, idx, grads, max_blocks=0, xform=None):
+        aux = modes = None
+        if xform:
+            aux = [xform[i][1] if i in xform else None for i in idx]
+            modes = [xform[i][2] if i in xform else 0 for i in idx]
+            grads = [xform[i][0] if i in xform else g for i, g in enumerate(grads)]
         adam_groups([self.params[i].data for i in idx], [grads[i] for i in idx],
                     [self.exp_avg[i] for i in idx], [self.exp_avg_sq[i] for i in idx],
                     [self.lrs[i] for i in idx], self.betas, self.eps, self.step_count,
-                    max_blocks)
+                    max_blocks, aux, modes)
 
     @torch.no_grad()
-    def step(self, skip=()):
+    def step(self, skip=(), xform=None):
         """skip: indices already updated for this step (by the SH backward
-        with the update fused in, train_step.Trainer)."""
+        with the update fused in, train_step.Trainer).  xform: {index:
+        (grad, aux, mode)} -- the gradient of that group formed in-register
+        (adam_step_ex modes: 1 sum, 2 exp VJP, 3 sigmoid VJP)."""
         self.wait()  # a previous deferred update is ordered before this one
         self.step_count += 1
         grads = [p.grad for p in self.params]
@@ -195,9 +213,9 @@ class FusedAdam:
         if self.side is None:
             idx = [i for i in range(len(self.params)) if i not in skip]
             if idx:
-                self._launch(idx, grads)
+                self._launch(idx, grads, xform=xform)
             return
-        assert not skip, "skip and deferred groups are exclusive"
+        assert not skip and not xform, "skip / xform and deferred groups are exclusive"
         now = [i for i in range(len(self.params)) if i not in self.deferred]
         if now:
             self._launch(now, grads)

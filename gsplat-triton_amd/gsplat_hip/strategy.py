@@ -10,7 +10,7 @@ import ctypes
 
 import torch
 
-from . import _lib
+from . import _lib, _wrapper
 from ._wrapper import _f32c, _ptr, _stream
 
 
@@ -35,6 +35,15 @@ class _Activate(torch.autograd.Function):
     @staticmethod
     def backward(ctx, v_scales, v_opac):
         scales, opac = ctx.saved_tensors
+        st = _wrapper._GEOM_STASH
+        if (st is not None and "v_scales" not in st and st.get("scales_ptr") == scales.data_ptr()
+                and st.get("opac_ptr") == opac.data_ptr()):
+            # the trainer's geometry update applies the VJPs in-register
+            # (adam_step_ex modes 2 / 3): hand over the incoming gradients
+            st["v_scales"] = None if v_scales is None else _f32c(v_scales)
+            st["v_opac"] = None if v_opac is None else _f32c(v_opac)
+            st["scales"], st["opac"] = scales, opac
+            return None, None
         v_scales = torch.zeros_like(scales) if v_scales is None else _f32c(v_scales)
         v_opac = torch.zeros_like(opac) if v_opac is None else _f32c(v_opac)
         v_log = torch.empty_like(scales)

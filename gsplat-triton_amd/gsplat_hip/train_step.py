@@ -199,6 +199,11 @@ class Trainer:
         self.sh_adam_in_bwd = (fused and not self.sharded and not self.defer_sh
                                and world_size == 1
                                and os.environ.get("GSPLAT_HIP_SH_ADAM_IN_BWD", "1") != "0")
+        # same conditions: the exp / sigmoid VJPs and the means-gradient sum
+        # formed inside the geometry groups' Adam (gsplat_hip_adam_step_ex)
+        self.geom_fuse = (fused and not self.sharded and not self.defer_sh and world_size == 1
+                          and os.environ.get("GSPLAT_HIP_GEOM_FUSE", "1") != "0")
+        self._act = None
         self.opt = self._make_optimizer(list(self.params.values()))
         self.viewmats = viewmats.to(device)
         self.Ks = Ks.to(device)
@@ -317,6 +322,7 @@ class Trainer:
             hook = self.opt.wait  # the previous step's SH update (side stream)
         if self.fused:  # one HIP launch each way for both activations
             scales, opac = activate(p["scales"], p["opacities"])
+            self._act = (scales, opac)
         else:
             scales, opac = torch.exp(p["scales"]), torch.sigmoid(p["opacities"])
         absgrad = self.strategy is not None and self.strategy.absgrad
@@ -350,10 +356,13 @@ class Trainer:
                                    self.window)
             loss = l1 * (1.0 - self.ssim_lambda) + ssim_loss * self.ssim_lambda
         fa = self._arm_sh_adam()
+        gs = self._arm_geom()
         try:
             loss.backward()
         finally:
             _wrapper._SH_ADAM = None
+            _wrapper._GEOM_STASH = None
+            self._act = None
         if self.world_size > 1 and not self.sharded:
             self.allreduce_grads()
         if self.strategy is None or it < self.strategy.refine_stop_iter:
@@ -362,16 +371,44 @@ class Trainer:
             self._set_means_lr(self.lrs[0] * (0.01 ** (1.0 / self.max_steps)) ** it)
         if self.sharded:
             self.opt.step(defer_gather=True)
-        elif fa is not None and fa.applied:
-            names = list(self.params)
-            self.opt.step(skip=(names.index("sh0"), names.index("shN")))
         else:
-            self.opt.step()
+            names = list(self.params)
+            skip = (names.index("sh0"), names.index("shN")) if fa is not None and fa.applied \
+                else ()
+            self.opt.step(skip=skip, xform=self._geom_xform(gs))
         self.opt.zero_grad(set_to_none=True)
         self.last_meta = meta
         if self.strategy is not None:
             self.post_step(it)
         return loss
+
+    def _arm_geom(self):
+        """Arm the geometry stash (see geom_fuse); None when off."""
+        if not getattr(self, "geom_fuse", False) or self._act is None \
+                or not isinstance(self.opt, FusedAdam):
+            return None
+        scales, opac = self._act
+        gs = {"means_ptr": self.params["means"].data_ptr(),
+              "scales_ptr": scales.data_ptr(), "opac_ptr": opac.data_ptr()}
+        _wrapper._GEOM_STASH = gs
+        return gs
+
+    def _geom_xform(self, gs):
+        """FusedAdam xform of the stashed gradients: means = its .grad + the
+        SH backward's part (autograd's sum), log-scales / logits = the exp /
+        sigmoid VJPs of the activation backward, formed in-register."""
+        if gs is None:
+            return None
+        names = list(self.params)
+        xf = {}
+        if "v_dirs" in gs:
+            gm = self.params["means"].grad
+            xf[names.index("means")] = (gs["v_dirs"], None, 0) if gm is None else \
+                (gm, gs["v_dirs"], 1)
+        if "v_scales" in gs:
+            xf[names.index("scales")] = (gs["v_scales"], gs["scales"], 2)
+            xf[names.index("opacities")] = (gs["v_opac"], gs["opac"], 3)
+        return xf or None
 
     def _arm_sh_adam(self):
         """Arm the SH-colour backward of this step to apply the SH groups'

@@ -381,6 +381,17 @@ int gsplat_hip_adam_step(int n_groups, float *const *params, const float *const 
                          float *const *exp_avgs, float *const *exp_avg_sqs,
                          const int64_t *numels, const float *lrs, float beta1, float beta2,
                          float eps, int step, void *stream);
+/* The same update with the gradient formed in-register per group (ABI 19):
+ * modes[i] 0: grads[i]; 1: grads[i] + aux[i] (two gradient contributions);
+ * 2: grads[i] * aux[i] (VJP of exp, aux = exp(x)); 3: grads[i] * (1 - aux[i])
+ * * aux[i] (VJP of sigmoid, aux = sigmoid(x)) -- the trainer's activation
+ * VJPs and means-gradient sum folded into the geometry groups' update.
+ * aux / modes may be NULL (all mode 0); aux pointers 16-B aligned. */
+int gsplat_hip_adam_step_ex(int n_groups, float *const *params, const float *const *grads,
+                            const float *const *aux, const int32_t *modes,
+                            float *const *exp_avgs, float *const *exp_avg_sqs,
+                            const int64_t *numels, const float *lrs, float beta1, float beta2,
+                            float eps, int step, void *stream);
 /* The same update on a grid of at most max_blocks workgroups (ABI 17): an
  * update running on a side stream beside other kernels leaves them CU slots
  * (the trainer's deferred SH-coefficient update). */

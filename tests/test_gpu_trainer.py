@@ -346,3 +346,58 @@ def test_sh_adam_in_backward_is_exact(degree):
         res.append((p0.detach().clone(), p1.detach().clone(), *opt.exp_avg, *opt.exp_avg_sq, *gm))
     for a, b in zip(res[0], res[1]):
         assert torch.equal(a, b)
+
+
+def test_adam_gradient_transforms_are_exact():
+    """gsplat_hip_adam_step_ex's in-register gradients (sum, exp VJP, sigmoid
+    VJP) give the same bits as forming them first (activate_bwd's formulas)
+    and stepping FusedAdam on the result."""
+    from gsplat_hip.losses import FusedAdam
+    torch.manual_seed(1)
+    N = 4099  # scalar tails
+    shapes = [(N, 3), (N, 4), (N, 3), (N,)]
+    base = [torch.randn(s, device="cuda") for s in shapes]
+    lrs = [1.6e-4, 1e-3, 5e-3, 5e-2]
+    res = []
+    for fused in (False, True):
+        ps = [b.clone().requires_grad_(True) for b in base]
+        opt = FusedAdam(ps, lrs, betas=(0.9, 0.999), eps=1e-15)
+        for it in range(3):
+            g = torch.Generator(device="cuda").manual_seed(10 + it)
+            ga, gb = (torch.randn(N, 3, device="cuda", generator=g) for _ in range(2))
+            gq = torch.randn(N, 4, device="cuda", generator=g)
+            vs = torch.randn(N, 3, device="cuda", generator=g)
+            vo = torch.randn(N, device="cuda", generator=g)
+            s_act = torch.exp(ps[2].detach())
+            o_act = torch.sigmoid(ps[3].detach())
+            if fused:
+                ps[0].grad, ps[1].grad = ga, gq
+                opt.step(xform={0: (ga, gb, 1), 2: (vs, s_act, 2), 3: (vo, o_act, 3)})
+            else:
+                ps[0].grad, ps[1].grad = ga + gb, gq
+                ps[2].grad, ps[3].grad = vs * s_act, vo * (1 - o_act) * o_act
+                opt.step()
+            opt.zero_grad()
+        torch.cuda.synchronize()
+        res.append([p.detach().clone() for p in ps] + opt.exp_avg + opt.exp_avg_sq)
+    for a, b in zip(res[0], res[1]):
+        assert torch.equal(a, b)
+
+
+def test_trainer_geometry_fusion_close(monkeypatch):
+    """The trainer with the activation VJPs / means sum folded into the
+    geometry update (GSPLAT_HIP_GEOM_FUSE=1) tracks the unfused trainer (the
+    rasterizer's backward atomics make two runs differ in the last bits)."""
+    from gsplat_hip.train_step import Trainer
+    means, rgbs, vm, K, W, H = _small_scene()
+    out = {}
+    for f in ("0", "1"):
+        monkeypatch.setenv("GSPLAT_HIP_GEOM_FUSE", f)
+        tr = Trainer(means, rgbs, vm, K, W, H, device="cuda")
+        assert tr.geom_fuse == (f == "1")
+        losses = [float(tr.step(it)) for it in range(5)]
+        out[f] = (losses, {k: p.detach().clone() for k, p in tr.params.items()})
+    for a, b in zip(out["0"][0], out["1"][0]):
+        assert abs(a - b) <= 1e-4 * abs(a) + 1e-7, (out["0"][0], out["1"][0])
+    for k in out["0"][1]:
+        torch.testing.assert_close(out["1"][1][k], out["0"][1][k], rtol=1e-3, atol=1e-5)
