@@ -104,12 +104,19 @@ class _L1SSIMLossFused(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g_loss):
         (unit,) = ctx.saved_tensors
+        if g_loss is ONE_GRAD:  # the trainer's constant 1.0 seed: the unit gradient as is
+            return unit, None, None
         g_loss = g_loss.float().contiguous()
         grad = torch.empty_like(unit)
         _lib.call("gsplat_hip_l1_ssim_loss_fused_bwd", unit.numel(), _ptr(unit), _ptr(g_loss),
                   _ptr(grad), _stream())
         return grad, None, None
 
+
+# A constant scalar 1.0 the trainer seeds loss.backward() with (never written):
+# seen as the incoming gradient, the fused loss's backward returns its stored
+# unit gradient without the scaling launch.
+ONE_GRAD = None
 
 # GSPLAT_HIP_SSIM_FUSED=0: the two-pass loss (partials to HBM) for training too
 SSIM_FUSED = os.environ.get("GSPLAT_HIP_SSIM_FUSED", "1") != "0"

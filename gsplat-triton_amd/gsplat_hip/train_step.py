@@ -358,7 +358,15 @@ class Trainer:
         fa = self._arm_sh_adam()
         gs = self._arm_geom()
         try:
-            loss.backward()
+            if self.fused and loss.dim() == 0:
+                # a constant 1.0 seed (no fill launch; the fused loss's
+                # backward recognises it and skips its scaling launch)
+                from . import losses as _losses
+                if _losses.ONE_GRAD is None or _losses.ONE_GRAD.device != loss.device:
+                    _losses.ONE_GRAD = torch.ones((), device=loss.device)
+                torch.autograd.backward(loss, _losses.ONE_GRAD)
+            else:
+                loss.backward()
         finally:
             _wrapper._SH_ADAM = None
             _wrapper._GEOM_STASH = None

@@ -401,3 +401,24 @@ def test_trainer_geometry_fusion_close(monkeypatch):
         assert abs(a - b) <= 1e-4 * abs(a) + 1e-7, (out["0"][0], out["1"][0])
     for k in out["0"][1]:
         torch.testing.assert_close(out["1"][1][k], out["0"][1][k], rtol=1e-3, atol=1e-5)
+
+
+def test_fused_loss_constant_seed_skips_scaling_exactly():
+    """Seeded with losses.ONE_GRAD, the fused loss's backward returns its
+    unit gradient as is: the same bits as the scaled path with a 1.0 seed."""
+    from gsplat_hip import losses
+    g = torch.Generator(device="cuda").manual_seed(8)
+    img = torch.rand(1, 70, 90, 3, device="cuda", generator=g)
+    gt = torch.rand(1, 70, 90, 3, device="cuda", generator=g)
+    a = img.clone().requires_grad_(True)
+    b = img.clone().requires_grad_(True)
+    old = losses.ONE_GRAD
+    losses.ONE_GRAD = torch.ones((), device="cuda")
+    try:
+        torch.autograd.backward(losses.l1_ssim_loss(a, gt, 0.2, fused=True), losses.ONE_GRAD)
+    finally:
+        seed, losses.ONE_GRAD = losses.ONE_GRAD, old
+    torch.autograd.backward(losses.l1_ssim_loss(b, gt, 0.2, fused=True),
+                            torch.ones((), device="cuda"))
+    assert torch.equal(a.grad, b.grad)
+    assert float(seed) == 1.0
