@@ -346,7 +346,9 @@ class Trainer:
         ci = self.camera_index(it)
         colors, alphas, meta = self.render(ci, self.sh_degree_at(it))
         if self.model == "3dgs":
-            meta["means2d"].retain_grad()  # DefaultStrategy.step_pre_backward
+            # DefaultStrategy.step_pre_backward: the means2d gradient is
+            # captured by a hook (retain_grad would clone it into .grad)
+            meta["means2d"].register_hook(lambda g: meta.__setitem__("means2d_grad", g))
         gt = self.targets[ci:ci + 1]
         if self.fused:
             loss = l1_ssim_loss(colors, gt, self.ssim_lambda)
@@ -536,7 +538,11 @@ class Trainer:
         sync of torch.where (default.py:213-262): same sums, masked."""
         key = "gradient_2dgs" if self.model == "2dgs" else "means2d"
         absgrad = self.strategy is not None and self.strategy.absgrad
-        g = meta[key].absgrad if absgrad else meta[key].grad
+        if absgrad:
+            g = meta[key].absgrad
+        else:
+            g = meta.get("means2d_grad") if key == "means2d" else None
+            g = meta[key].grad if g is None else g
         if g is None:
             return
         if self.fused:
