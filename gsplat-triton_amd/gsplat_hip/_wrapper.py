@@ -542,15 +542,46 @@ def spherical_harmonics(
     return _SphericalHarmonics.apply(degrees_to_use, dirs, coeffs, masks, block_size, rest)
 
 
-def _stash_means_grad(means, v_means):
-    """Hand the SH backward's means gradient to an armed geometry stash
-    (returns None then) or back to autograd."""
-    st = _GEOM_STASH
-    if (v_means is not None and st is not None and "v_dirs" not in st
-            and st.get("means_ptr") == means.data_ptr()):
-        st["v_dirs"] = v_means
-        return None
-    return v_means
+class StepFusion:
+    """The optimizer work one training step folds into its own backward,
+    handed EXPLICITLY to the forward calls that create the autograd nodes
+    (`rasterization(_fusion=...)`, `strategy.activate(..., fusion=...)`), so
+    nothing is armed in module state: a render or backward that was not given
+    this object is never affected.
+
+    sh_adam -- a ShAdamInBackward: the SH-colour backward applies Adam to the
+               SH coefficients in place instead of returning their gradients;
+    geom    -- the SH-colour backward hands its dL/dmeans (`v_dirs`) and the
+               activation backward its incoming dL/dscales, dL/dopacities
+               (`v_scales`, `v_opac`, with the activations `scales`, `opac`)
+               to the trainer, whose geometry Adam forms the sums / VJPs
+               in-register (gsplat_hip_adam_step_ex).
+    Each hand-over happens at most once: a second backward through the same
+    nodes (retain_graph) returns ordinary gradients, which the trainer then
+    adds as extra terms."""
+
+    def __init__(self, sh_adam: Optional["ShAdamInBackward"] = None, geom: bool = False):
+        self.sh_adam = sh_adam
+        self.geom = bool(geom)
+        self.v_dirs = None
+        self.v_scales = self.v_opac = self.scales = self.opac = None
+        self.act_taken = False
+
+    def take_means_grad(self, v_means: Optional[Tensor]) -> Optional[Tensor]:
+        """The SH backward's means gradient: kept here (returns None) when the
+        geometry update takes it, else handed back to autograd."""
+        if v_means is not None and self.geom and self.v_dirs is None:
+            self.v_dirs = v_means
+            return None
+        return v_means
+
+    def take_activation_grads(self, v_scales, v_opac, scales, opac) -> bool:
+        """The activation backward's incoming gradients (True: taken)."""
+        if not self.geom or self.act_taken:
+            return False
+        self.act_taken = True
+        self.v_scales, self.v_opac, self.scales, self.opac = v_scales, v_opac, scales, opac
+        return True
 
 
 class ShAdamInBackward:
@@ -577,22 +608,16 @@ class ShAdamInBackward:
                 and self.coeffs.is_contiguous() and self.coeffs_rest.is_contiguous())
 
 
-_SH_ADAM = None  # an armed ShAdamInBackward (set around loss.backward() by the trainer)
-# The trainer's geometry-update stash (train_step.Trainer._arm_geom): a dict
-# with "means_ptr" (and the activation outputs' pointers, strategy.py); the
-# SH-colour backward leaves its means gradient here instead of returning it,
-# and the geometry groups' Adam adds it in-register (adam_step_ex mode 1).
-_GEOM_STASH = None
-
-
 class _SHColors(torch.autograd.Function):
     """rasterization()'s SH colour path in one kernel each way
     (gsplat/rendering.py:396-406): clamp_min(SH(means - campos) + 0.5, 0)
     with radii masking.  Differentiable w.r.t. means and the coefficients
-    (viewmats must not require grad -- the caller falls back otherwise)."""
+    (viewmats must not require grad -- the caller falls back otherwise).
+    `fusion`: the training step's StepFusion or None."""
 
     @staticmethod
-    def forward(ctx, sh_degree, means, viewmats, coeffs, coeffs_rest, radii):
+    def forward(ctx, sh_degree, means, viewmats, coeffs, coeffs_rest, radii, fusion=None):
+        ctx.fusion = fusion
         means, viewmats = _f32c(means), _f32c(viewmats)
         base, n_rows = _coeff_rows(coeffs)
         rest = None
@@ -630,7 +655,8 @@ class _SHColors(torch.autograd.Function):
         # gradient accumulation can take it over instead of copying a view
         v_dirs = (torch.empty(N, 3, device=dev) if C == 1 else
                   torch.empty(C, N, 3, device=dev)) if want_means else None
-        fa = _SH_ADAM
+        fusion = ctx.fusion
+        fa = None if fusion is None else fusion.sh_adam
         if fa is not None and fa.matches(base, rest, C, N, K, ctx.n_rows, ctx.sh_degree):
             m0, v0, mr, vr = fa.moments
             _lib.call("gsplat_hip_sh_colors_bwd_adam", ctx.sh_degree, N, _ptr(means),
@@ -640,13 +666,15 @@ class _SHColors(torch.autograd.Function):
                       ctypes.c_float(fa.betas[0]), ctypes.c_float(fa.betas[1]),
                       ctypes.c_float(fa.eps), int(fa.step), _stream())
             fa.applied = True
-            return (None, _stash_means_grad(means, v_dirs), None, None, None, None)
+            return (None, fusion.take_means_grad(v_dirs), None, None, None, None, None)
         _lib.call("gsplat_hip_sh_colors_bwd", ctx.sh_degree, C, N, ctx.n_rows, K, _ptr(means),
                   _ptr(viewmats), _ptr(base), _ptr(rest), _ptr(radii), _ptr(v_colors),
                   _ptr(v_coeffs), _ptr(v_rest), _ptr(v_dirs), _stream())
         v_means = None
         if want_means:
-            v_means = _stash_means_grad(means, v_dirs) if C == 1 else v_dirs.sum(0)
+            v_means = v_dirs if C == 1 else v_dirs.sum(0)
+            if fusion is not None:
+                v_means = fusion.take_means_grad(v_means)
         def fold(v, shape):  # [C,N,..] -> the input's shape (sum over cameras)
             if v is None:
                 return None
@@ -654,17 +682,19 @@ class _SHColors(torch.autograd.Function):
                 v = v[0] if C == 1 else v.sum(0)
             return v.view(shape)
         return (None, v_means, None, fold(v_coeffs, ctx.coeff_shape), fold(v_rest, ctx.rest_shape),
-                None)
+                None, None)
 
 
-def sh_colors(sh_degree: int, means: Tensor, viewmats: Tensor, coeffs, radii: Tensor) -> Tensor:
+def sh_colors(sh_degree: int, means: Tensor, viewmats: Tensor, coeffs, radii: Tensor,
+              fusion: Optional[StepFusion] = None) -> Tensor:
     """colors [C,N,3] = clamp_min(SH(means - campos) + 0.5, 0), radii-masked:
     the colour computation of rendering.rasterization (rendering.py:396-406)
-    fused.  `coeffs`: [N,K,3] / [C,N,K,3] or the pair (sh0, shN)."""
+    fused.  `coeffs`: [N,K,3] / [C,N,K,3] or the pair (sh0, shN).  `fusion`:
+    the training step's StepFusion (optimizer work folded into the backward)."""
     rest = None
     if isinstance(coeffs, (tuple, list)):
         coeffs, rest = coeffs
-    return _SHColors.apply(sh_degree, means, viewmats, coeffs, rest, radii)
+    return _SHColors.apply(sh_degree, means, viewmats, coeffs, rest, radii, fusion)
 
 
 # ============================================================ rasterization ==

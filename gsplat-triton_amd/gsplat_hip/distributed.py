@@ -198,13 +198,20 @@ class ShardedAdam:
         assert sorted(i for g in self.groups for i in g) == list(range(len(self.params))), \
             self.groups
         self._pending = {}  # parameter index -> all-gather still in flight
+        # parameter index -> event after its group's update on the side stream
+        # (tail rows and parameters too short for a shard are updated there
+        # and have no all-gather to wait on)
+        self._updated = {}
         # Adam + all-gather issue stream (CUDA only; gloo runs them inline)
         self.side = torch.cuda.Stream(device=dev) if dev.type == "cuda" else None
 
     def wait(self, indices=None):
         """Order the current stream after the deferred all-gathers of these
         parameters (all when None); no host synchronisation."""
-        for i in list(self._pending) if indices is None else indices:
+        for i in (set(self._pending) | set(self._updated)) if indices is None else indices:
+            ev = self._updated.pop(i, None)
+            if ev is not None:
+                torch.cuda.current_stream(self.params[i].device).wait_event(ev)
             wk = self._pending.pop(i, None)
             if wk is not None:
                 wk.wait()
@@ -241,6 +248,11 @@ class ShardedAdam:
                 for wk in works:  # the side stream (gloo: the host) waits
                     wk.wait()
                 self._update_group(grp, flats)
+                if side is not None:
+                    ev = torch.cuda.Event()
+                    ev.record(side)
+                    for i in grp:
+                        self._updated[i] = ev
                 # issued from the side stream: RCCL waits for this Adam only
                 for i in sorted(grp, key=lambda i: self.params[i].numel()):
                     _, _, main, _ = self.layout[i]

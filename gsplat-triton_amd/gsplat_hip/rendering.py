@@ -67,8 +67,13 @@ def rasterization(
     camera_model: str = "pinhole",
     covars: Optional[Tensor] = None,
     _colors_ready: Optional[Callable[[], None]] = None,
+    _fusion=None,
 ) -> Tuple[Tensor, Tensor, Dict]:
-    """Rasterize N 3D Gaussians to C images (gsplat/rendering.py:44-598)."""
+    """Rasterize N 3D Gaussians to C images (gsplat/rendering.py:44-598).
+
+    Private arguments of the training harness (train_step.Trainer):
+    `_colors_ready` (see below) and `_fusion`, a _wrapper.StepFusion handed
+    to the fused SH-colour node (optimizer work folded into its backward)."""
     meta = {}
     N = means.shape[0]
     C = viewmats.shape[0]
@@ -168,7 +173,8 @@ def rasterization(
             # one kernel each way: dirs from the camera centres, radii masking,
             # clamp_min(sh + 0.5, 0) (same values as the branch below)
             colors = sh_colors(sh_degree, means, viewmats,
-                               colors if sh_rest is None else (colors, sh_rest), radii)
+                               colors if sh_rest is None else (colors, sh_rest), radii,
+                               fusion=_fusion)
         else:
             camtoworlds = torch.inverse(viewmats)  # [C, 4, 4]
             dirs = means[None, :, :] - camtoworlds[:, None, :3, 3]  # [C, N, 3]
@@ -396,6 +402,7 @@ def rasterization_2dgs(
     absgrad: bool = False,
     distloss: bool = False,
     depth_mode: str = "expected",
+    _fusion=None,
 ):
     """Rasterize N surfels (2DGS) to C images (gsplat/rendering.py:1018-1339).
 
@@ -462,7 +469,8 @@ def rasterization_2dgs(
     elif sh_degree is not None and not viewmats.requires_grad:
         # one kernel: dirs from -R^T t, radii masking, clamp_min(sh + 0.5, 0)
         colors = sh_colors(sh_degree, means, viewmats,
-                           colors if sh_rest is None else (colors, sh_rest), radii)
+                           colors if sh_rest is None else (colors, sh_rest), radii,
+                           fusion=_fusion)
     else:
         if sh_rest is not None:
             colors = torch.cat([colors, sh_rest], 1)

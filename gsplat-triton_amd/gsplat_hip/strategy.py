@@ -10,7 +10,7 @@ import ctypes
 
 import torch
 
-from . import _lib, _wrapper
+from . import _lib
 from ._wrapper import _f32c, _ptr, _stream
 
 
@@ -22,7 +22,7 @@ def _dev(*ts):
 
 class _Activate(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, log_scales, logits):
+    def forward(ctx, log_scales, logits, fusion=None):
         log_scales, logits = _f32c(log_scales), _f32c(logits)
         _dev(log_scales, logits)
         scales = torch.empty_like(log_scales)
@@ -30,20 +30,18 @@ class _Activate(torch.autograd.Function):
         _lib.call("gsplat_hip_activate_fwd", log_scales.numel(), logits.numel(),
                   _ptr(log_scales), _ptr(logits), _ptr(scales), _ptr(opac), _stream())
         ctx.save_for_backward(scales, opac)
+        ctx.fusion = fusion
         return scales, opac
 
     @staticmethod
     def backward(ctx, v_scales, v_opac):
         scales, opac = ctx.saved_tensors
-        st = _wrapper._GEOM_STASH
-        if (st is not None and "v_scales" not in st and st.get("scales_ptr") == scales.data_ptr()
-                and st.get("opac_ptr") == opac.data_ptr()):
-            # the trainer's geometry update applies the VJPs in-register
-            # (adam_step_ex modes 2 / 3): hand over the incoming gradients
-            st["v_scales"] = None if v_scales is None else _f32c(v_scales)
-            st["v_opac"] = None if v_opac is None else _f32c(v_opac)
-            st["scales"], st["opac"] = scales, opac
-            return None, None
+        # the trainer's geometry update applies the VJPs in-register
+        # (adam_step_ex modes 2 / 3): hand over the incoming gradients
+        if ctx.fusion is not None and ctx.fusion.take_activation_grads(
+                None if v_scales is None else _f32c(v_scales),
+                None if v_opac is None else _f32c(v_opac), scales, opac):
+            return None, None, None
         v_scales = torch.zeros_like(scales) if v_scales is None else _f32c(v_scales)
         v_opac = torch.zeros_like(opac) if v_opac is None else _f32c(v_opac)
         v_log = torch.empty_like(scales)
@@ -51,12 +49,14 @@ class _Activate(torch.autograd.Function):
         _lib.call("gsplat_hip_activate_bwd", scales.numel(), opac.numel(), _ptr(scales),
                   _ptr(opac), _ptr(v_scales), _ptr(v_opac), _ptr(v_log), _ptr(v_logit),
                   _stream())
-        return v_log, v_logit
+        return v_log, v_logit, None
 
 
-def activate(log_scales, logits):
-    """(exp(log_scales), sigmoid(logits)), differentiable."""
-    return _Activate.apply(log_scales, logits)
+def activate(log_scales, logits, fusion=None):
+    """(exp(log_scales), sigmoid(logits)), differentiable.  `fusion`: a
+    training step's _wrapper.StepFusion whose geometry update takes the
+    incoming gradients instead (the VJPs are then formed inside Adam)."""
+    return _Activate.apply(log_scales, logits, fusion)
 
 
 @torch.no_grad()

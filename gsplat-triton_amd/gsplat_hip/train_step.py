@@ -33,6 +33,7 @@ noise comes from a generator seeded identically on every rank, so the
 replicas stay identical.
 """
 
+import dataclasses
 import math
 import os
 from typing import Dict, Optional
@@ -137,7 +138,8 @@ class Trainer:
                  strategy: Optional[DefaultStrategyConfig] = None,
                  sh_degree_interval: Optional[int] = None, max_steps: Optional[int] = None,
                  init: str = "random", init_opacity: float = 0.1, init_scale: float = 1.0,
-                 targets: Optional[torch.Tensor] = None):
+                 targets: Optional[torch.Tensor] = None, opacity_reg: float = 0.0,
+                 scale_reg: float = 0.0):
         assert model in ("3dgs", "2dgs"), model
         assert init in ("random", "sfm"), init
         self.model = model
@@ -149,9 +151,13 @@ class Trainer:
         self.ssim_lambda = ssim_lambda
         self.world_size, self.rank = world_size, rank
         self.scene_scale = scene_scale
-        self.strategy = strategy
-        if strategy is not None and model == "2dgs":
-            strategy.key_for_gradient = "gradient_2dgs"  # simple_trainer_2dgs.py:307-311
+        # the caller's config object is not modified (a private copy)
+        self.strategy = None if strategy is None else dataclasses.replace(strategy)
+        if self.strategy is not None and model == "2dgs":
+            self.strategy.key_for_gradient = "gradient_2dgs"  # simple_trainer_2dgs.py:307-311
+        # simple_trainer.py:135-137, 671-681: |sigmoid(opacities)| / |exp(scales)|
+        # mean terms on the raw parameters (0 = off, the default config)
+        self.opacity_reg, self.scale_reg = float(opacity_reg), float(scale_reg)
         self.sh_degree_interval = sh_degree_interval
         self.max_steps = max_steps
         K = (sh_degree + 1) ** 2
@@ -203,7 +209,6 @@ class Trainer:
         # formed inside the geometry groups' Adam (gsplat_hip_adam_step_ex)
         self.geom_fuse = (fused and not self.sharded and not self.defer_sh and world_size == 1
                           and os.environ.get("GSPLAT_HIP_GEOM_FUSE", "1") != "0")
-        self._act = None
         self.opt = self._make_optimizer(list(self.params.values()))
         self.viewmats = viewmats.to(device)
         self.Ks = Ks.to(device)
@@ -213,6 +218,10 @@ class Trainer:
         self.targets = targets.to(device)
         self.grad2d = torch.zeros(N, device=device)
         self.count = torch.zeros(N, device=device)
+        # state["radii"] (default.py:235-262): the largest screen radius of each
+        # Gaussian normalised by max(W, H), tracked only while it is used
+        self.radii2d = (torch.zeros(N, device=device) if self.strategy is not None
+                        and self.strategy.refine_scale2d_stop_iter > 0 else None)
         # split noise: the same stream on every rank (replicas stay identical)
         self.rng = torch.Generator(device=device).manual_seed(seed)
         self.window = _gauss_window(device=device)
@@ -307,7 +316,10 @@ class Trainer:
             return self.sh_degree
         return min(it // self.sh_degree_interval, self.sh_degree)
 
-    def render(self, ci: int, sh_degree: Optional[int] = None):
+    def render(self, ci: int, sh_degree: Optional[int] = None,
+               fusion: Optional[_wrapper.StepFusion] = None):
+        """Render camera `ci`; `fusion` (a training step's StepFusion) goes to
+        the nodes whose backward hands their gradients to the optimizer."""
         p = self.params
         deg = self.sh_degree if sh_degree is None else sh_degree
         hook = None
@@ -321,8 +333,7 @@ class Trainer:
         elif getattr(self, "defer_sh", False):
             hook = self.opt.wait  # the previous step's SH update (side stream)
         if self.fused:  # one HIP launch each way for both activations
-            scales, opac = activate(p["scales"], p["opacities"])
-            self._act = (scales, opac)
+            scales, opac = activate(p["scales"], p["opacities"], fusion)
         else:
             scales, opac = torch.exp(p["scales"]), torch.sigmoid(p["opacities"])
         absgrad = self.strategy is not None and self.strategy.absgrad
@@ -333,18 +344,19 @@ class Trainer:
                 p["means"], p["quats"], scales, opac, (p["sh0"], p["shN"]),
                 self.viewmats[ci:ci + 1], self.Ks[ci:ci + 1], self.width, self.height,
                 sh_degree=deg, packed=False, near_plane=0.01, far_plane=1e10,
-                render_mode="RGB+D", absgrad=absgrad)
+                render_mode="RGB+D", absgrad=absgrad, _fusion=fusion)
             return rc[..., :3], ra, meta
         return rasterization(
             p["means"], p["quats"], scales, opac,
             (p["sh0"], p["shN"]) if self.fused else torch.cat([p["sh0"], p["shN"]], 1),
             self.viewmats[ci:ci + 1], self.Ks[ci:ci + 1], self.width, self.height,
             sh_degree=deg, packed=False, near_plane=0.01, far_plane=1e10, radius_clip=0.0,
-            rasterize_mode="classic", absgrad=absgrad, _colors_ready=hook)
+            rasterize_mode="classic", absgrad=absgrad, _colors_ready=hook, _fusion=fusion)
 
     def step(self, it: int):
         ci = self.camera_index(it)
-        colors, alphas, meta = self.render(ci, self.sh_degree_at(it))
+        fusion = self._make_fusion()
+        colors, alphas, meta = self.render(ci, self.sh_degree_at(it), fusion)
         if self.model == "3dgs":
             # DefaultStrategy.step_pre_backward: the means2d gradient is
             # captured by a hook (retain_grad would clone it into .grad)
@@ -357,22 +369,16 @@ class Trainer:
             ssim_loss = 1.0 - ssim(colors.permute(0, 3, 1, 2), gt.permute(0, 3, 1, 2),
                                    self.window)
             loss = l1 * (1.0 - self.ssim_lambda) + ssim_loss * self.ssim_lambda
-        fa = self._arm_sh_adam()
-        gs = self._arm_geom()
-        try:
-            if self.fused and loss.dim() == 0:
-                # a constant 1.0 seed (no fill launch; the fused loss's
-                # backward recognises it and skips its scaling launch)
-                from . import losses as _losses
-                if _losses.ONE_GRAD is None or _losses.ONE_GRAD.device != loss.device:
-                    _losses.ONE_GRAD = torch.ones((), device=loss.device)
-                torch.autograd.backward(loss, _losses.ONE_GRAD)
-            else:
-                loss.backward()
-        finally:
-            _wrapper._SH_ADAM = None
-            _wrapper._GEOM_STASH = None
-            self._act = None
+        loss = self._regularise(loss)
+        if self.fused and loss.dim() == 0:
+            # a constant 1.0 seed (no fill launch; the fused loss's backward
+            # recognises it and skips its scaling launch)
+            from . import losses as _losses
+            if _losses.ONE_GRAD is None or _losses.ONE_GRAD.device != loss.device:
+                _losses.ONE_GRAD = torch.ones((), device=loss.device)
+            torch.autograd.backward(loss, _losses.ONE_GRAD)
+        else:
+            loss.backward()
         if self.world_size > 1 and not self.sharded:
             self.allreduce_grads()
         if self.strategy is None or it < self.strategy.refine_stop_iter:
@@ -382,58 +388,87 @@ class Trainer:
         if self.sharded:
             self.opt.step(defer_gather=True)
         else:
-            names = list(self.params)
-            skip = (names.index("sh0"), names.index("shN")) if fa is not None and fa.applied \
-                else ()
-            self.opt.step(skip=skip, xform=self._geom_xform(gs))
+            self.opt.step(skip=self._sh_skip(fusion), xform=self._geom_xform(fusion))
         self.opt.zero_grad(set_to_none=True)
         self.last_meta = meta
         if self.strategy is not None:
             self.post_step(it)
         return loss
 
-    def _arm_geom(self):
-        """Arm the geometry stash (see geom_fuse); None when off."""
-        if not getattr(self, "geom_fuse", False) or self._act is None \
-                or not isinstance(self.opt, FusedAdam):
-            return None
-        scales, opac = self._act
-        gs = {"means_ptr": self.params["means"].data_ptr(),
-              "scales_ptr": scales.data_ptr(), "opac_ptr": opac.data_ptr()}
-        _wrapper._GEOM_STASH = gs
-        return gs
+    def _regularise(self, loss):
+        """simple_trainer.py:671-681: the opacity / scale regularisers on the raw
+        parameters (their gradients reach .grad of the raw tensors through
+        torch autograd; the fused optimizer adds them as extra terms)."""
+        p = self.params
+        if self.opacity_reg > 0.0:
+            loss = loss + self.opacity_reg * torch.abs(torch.sigmoid(p["opacities"])).mean()
+        if self.scale_reg > 0.0:
+            loss = loss + self.scale_reg * torch.abs(torch.exp(p["scales"])).mean()
+        return loss
 
-    def _geom_xform(self, gs):
-        """FusedAdam xform of the stashed gradients: means = its .grad + the
-        SH backward's part (autograd's sum), log-scales / logits = the exp /
-        sigmoid VJPs of the activation backward, formed in-register."""
-        if gs is None:
+    def _make_fusion(self) -> Optional[_wrapper.StepFusion]:
+        """This step's StepFusion (None when nothing is fused): the SH groups'
+        Adam inside the SH backward (sh_adam_in_bwd) and the geometry groups'
+        gradient transforms inside their Adam (geom_fuse)."""
+        if not isinstance(self.opt, FusedAdam):
+            return None
+        fa = None
+        if getattr(self, "sh_adam_in_bwd", False):
+            names = list(self.params)
+            i0, i1 = names.index("sh0"), names.index("shN")
+            o = self.opt
+            fa = _wrapper.ShAdamInBackward(
+                self.params["sh0"].data, self.params["shN"].data, o.exp_avg[i0],
+                o.exp_avg_sq[i0], o.exp_avg[i1], o.exp_avg_sq[i1], o.lrs[i0], o.lrs[i1],
+                o.betas, o.eps, o.step_count + 1)
+        geom = getattr(self, "geom_fuse", False)
+        if fa is None and not geom:
+            return None
+        return _wrapper.StepFusion(sh_adam=fa, geom=geom)
+
+    def _sh_skip(self, fusion):
+        """Indices of the SH groups when the SH backward already applied their
+        update.  Their .grad must then be empty: a loss term reaching sh0 /
+        shN by another path would have been left out of that update."""
+        if fusion is None or fusion.sh_adam is None or not fusion.sh_adam.applied:
+            return ()
+        names = list(self.params)
+        for k in ("sh0", "shN"):
+            if self.params[k].grad is not None:
+                raise RuntimeError(
+                    f"{k} received a gradient outside the SH-colour backward while its Adam "
+                    "step was fused into that backward; set GSPLAT_HIP_SH_ADAM_IN_BWD=0 for "
+                    "losses with extra terms on the SH coefficients")
+        return (names.index("sh0"), names.index("shN"))
+
+    def _geom_xform(self, fusion):
+        """FusedAdam xform of the gradients the fusion took: means = its .grad +
+        the SH backward's part (autograd's sum), log-scales / logits = the exp
+        / sigmoid VJPs of the activation backward formed in-register.  A
+        gradient that also reached .grad of the raw log-scales / logits (a
+        regulariser, simple_trainer.py:671-681) is added as an extra term:
+        the VJP is then formed in torch with activate_bwd's operation order
+        and summed with it, which is autograd's accumulation exactly."""
+        if fusion is None or not fusion.geom:
             return None
         names = list(self.params)
         xf = {}
-        if "v_dirs" in gs:
+        if fusion.v_dirs is not None:
             gm = self.params["means"].grad
-            xf[names.index("means")] = (gs["v_dirs"], None, 0) if gm is None else \
-                (gm, gs["v_dirs"], 1)
-        if "v_scales" in gs:
-            xf[names.index("scales")] = (gs["v_scales"], gs["scales"], 2)
-            xf[names.index("opacities")] = (gs["v_opac"], gs["opac"], 3)
+            xf[names.index("means")] = (fusion.v_dirs, None, 0) if gm is None else \
+                (gm, fusion.v_dirs, 1)
+        if fusion.act_taken:
+            for key, v, act, mode in (("scales", fusion.v_scales, fusion.scales, 2),
+                                      ("opacities", fusion.v_opac, fusion.opac, 3)):
+                if v is None:
+                    continue  # that activation did not reach the loss
+                extra = self.params[key].grad
+                if extra is None:
+                    xf[names.index(key)] = (v, act, mode)
+                else:
+                    vjp = v * act if mode == 2 else v * (1.0 - act) * act
+                    xf[names.index(key)] = ((vjp + extra).contiguous(), None, 0)
         return xf or None
-
-    def _arm_sh_adam(self):
-        """Arm the SH-colour backward of this step to apply the SH groups'
-        Adam update in place (see sh_adam_in_bwd); None when off."""
-        if not getattr(self, "sh_adam_in_bwd", False) or not isinstance(self.opt, FusedAdam):
-            return None
-        names = list(self.params)
-        i0, i1 = names.index("sh0"), names.index("shN")
-        o = self.opt
-        fa = _wrapper.ShAdamInBackward(
-            self.params["sh0"].data, self.params["shN"].data, o.exp_avg[i0], o.exp_avg_sq[i0],
-            o.exp_avg[i1], o.exp_avg_sq[i1], o.lrs[i0], o.lrs[i1], o.betas, o.eps,
-            o.step_count + 1)
-        _wrapper._SH_ADAM = fa
-        return fa
 
     # ---------------------------------------------------------------- eval
     @torch.no_grad()
@@ -482,21 +517,26 @@ class Trainer:
         self.last_meta = None  # its tensors are sized for the old Gaussians
         if self.world_size > 1:
             # every rank accumulated its own cameras: the batch statistics are
-            # the sums (radii are not tracked: refine_scale2d_stop_iter = 0)
+            # the sums (the screen radii: their maximum)
             import torch.distributed as dist
             works = [dist.all_reduce(t, op=dist.ReduceOp.SUM, async_op=True)
                      for t in (self.grad2d, self.count)]
+            if self.radii2d is not None:
+                works.append(dist.all_reduce(self.radii2d, op=dist.ReduceOp.MAX, async_op=True))
             for w in works:
                 w.wait()
         params = {k: p.data for k, p in self.params.items()}
+        radii2d = self.radii2d if it < self.strategy.refine_scale2d_stop_iter else None
         new_p, new_m, counts = densify.refine(params, self.moments(), self.grad2d, self.count,
                                               it, self.strategy, self.scene_scale,
-                                              generator=self.rng)
+                                              generator=self.rng, radii2d=radii2d)
         self.params = {k: torch.nn.Parameter(v) for k, v in new_p.items()}
         self._load_moments(new_m)
         n = self.params["means"].shape[0]
         self.grad2d = torch.zeros(n, device=self.device)
         self.count = torch.zeros(n, device=self.device)
+        if self.radii2d is not None:
+            self.radii2d = torch.zeros(n, device=self.device)
         self.refine_log.append((it,) + tuple(counts) + (n,))
 
     @torch.no_grad()
@@ -535,8 +575,19 @@ class Trainer:
     @torch.no_grad()
     def update_state(self, meta):
         """DefaultStrategy._update_state for packed=False without the host
-        sync of torch.where (default.py:213-262): same sums, masked."""
-        key = "gradient_2dgs" if self.model == "2dgs" else "means2d"
+        sync of torch.where (default.py:213-262): same sums, masked; the
+        screen-radius maximum of state["radii"] while refine_scale2d_stop_iter
+        > 0 (default.py:255-262)."""
+        if self.strategy is not None:
+            key = self.strategy.key_for_gradient
+        else:
+            key = "gradient_2dgs" if self.model == "2dgs" else "means2d"
+        if self.radii2d is not None:
+            # radii / max(W, H) in float32 (int tensor / python float); the
+            # reference's "should be scatter max" over the visible pairs --
+            # invisible entries have radius 0 and leave the maximum unchanged
+            r = meta["radii"].float() / float(max(meta["width"], meta["height"]))
+            self.radii2d = torch.maximum(self.radii2d, r.amax(0))
         absgrad = self.strategy is not None and self.strategy.absgrad
         if absgrad:
             g = meta[key].absgrad
@@ -560,5 +611,3 @@ class Trainer:
         else:
             self.grad2d.add_(nrm.sum(0))
             self.count.add_(sel.sum(0))
-        # state["radii"] is only tracked when refine_scale2d_stop_iter > 0
-        # (default 0, default.py:90,255-262)

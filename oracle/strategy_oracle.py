@@ -21,7 +21,7 @@ import numpy as np
 f32 = np.float32
 
 DEFAULTS = dict(prune_opa=0.005, grow_grad2d=0.0002, grow_scale3d=0.01, prune_scale3d=0.1,
-                reset_every=3000, revised_opacity=False)
+                grow_scale2d=0.05, prune_scale2d=0.15, reset_every=3000, revised_opacity=False)
 
 
 def _sigmoid(x):
@@ -42,9 +42,12 @@ def _cat(*xs):
     return np.concatenate(xs, 0)
 
 
-def refine(params, moments, grad2d, count, step, z, scene_scale=1.0, **cfg):
+def refine(params, moments, grad2d, count, step, z, scene_scale=1.0, radii2d=None, **cfg):
     """One refine step (grow, then prune).  Returns (params, moments,
-    (n_dupli, n_split, n_prune))."""
+    (n_dupli, n_split, n_prune)).  radii2d: state["radii"] when the caller is
+    before refine_scale2d_stop_iter (screen-size split and prune,
+    default.py:283-284, 325-326), carried through duplicate / split as the
+    reference's running state (ops.py:108-111, 172-176)."""
     c = dict(DEFAULTS, **cfg)
     p = {k: np.asarray(v, f32).copy() for k, v in params.items()}
     m = {k: (np.asarray(a, f32).copy(), np.asarray(b, f32).copy()) for k, (a, b) in moments.items()}
@@ -55,6 +58,9 @@ def refine(params, moments, grad2d, count, step, z, scene_scale=1.0, **cfg):
     small = np.exp(p["scales"]).max(-1) <= c["grow_scale3d"] * scene_scale
     dup = high & small
     split = high & ~small
+    rad = None if radii2d is None else np.asarray(radii2d, f32).copy()
+    if rad is not None:
+        split = split | (rad > c["grow_scale2d"])
     n_dupli, n_split = int(dup.sum()), int(split.sum())
     # duplicate (ops.py:86-112): append copies, zero moments
     sel = np.nonzero(dup)[0]
@@ -62,6 +68,8 @@ def refine(params, moments, grad2d, count, step, z, scene_scale=1.0, **cfg):
         p[k] = _cat(p[k], p[k][sel])
         m[k] = tuple(_cat(v, np.zeros((len(sel),) + v.shape[1:], f32)) for v in m[k])
     split = _cat(split, np.zeros(n_dupli, bool))
+    if rad is not None:
+        rad = _cat(rad, rad[sel])
     # split (ops.py:115-176): keep the rest, append the two children batches
     sel = np.nonzero(split)[0]
     rest = np.nonzero(~split)[0]
@@ -82,10 +90,14 @@ def refine(params, moments, grad2d, count, step, z, scene_scale=1.0, **cfg):
             child = np.concatenate([v[sel], v[sel]], 0)
         p[k] = _cat(v[rest], child.astype(f32))
         m[k] = tuple(_cat(a[rest], np.zeros((2 * len(sel),) + a.shape[1:], f32)) for a in m[k])
+    if rad is not None:
+        rad = _cat(rad[rest], rad[sel], rad[sel])
     # _prune_gs (default.py:313-340) + remove (ops.py:179-211)
     prune = _sigmoid(p["opacities"].reshape(-1)) < c["prune_opa"]
     if step > c["reset_every"]:
         prune |= np.exp(p["scales"]).max(-1) > c["prune_scale3d"] * scene_scale
+        if rad is not None:
+            prune |= rad > c["prune_scale2d"]
     keep = np.nonzero(~prune)[0]
     for k in p:
         p[k] = p[k][keep]

@@ -60,7 +60,7 @@ def scene(N, seed):
     return p, grad2d, count, g
 
 
-def run(name, N, seed, step, scene_scale=1.0, revised=False, reset=False):
+def run(name, N, seed, step, scene_scale=1.0, revised=False, reset=False, scale2d_stop=0):
     DefaultStrategy, reset_opa = _import_reference()
     p, grad2d, count, g = scene(N, seed)
     params = {k: torch.nn.Parameter(v.clone()) for k, v in p.items()}
@@ -76,8 +76,14 @@ def run(name, N, seed, step, scene_scale=1.0, revised=False, reset=False):
     m0 = {k: opts[k].state[params[k]]["exp_avg"].clone() for k in NAMES}
     v0 = {k: opts[k].state[params[k]]["exp_avg_sq"].clone() for k in NAMES}
 
-    strat = DefaultStrategy(revised_opacity=revised)
+    strat = DefaultStrategy(revised_opacity=revised, refine_scale2d_stop_iter=scale2d_stop)
     state = {"grad2d": grad2d.clone(), "count": count.clone(), "scene_scale": scene_scale}
+    radii = None
+    if scale2d_stop > 0:
+        # state["radii"] (max screen radius / max(W, H)) straddling
+        # grow_scale2d = 0.05 and prune_scale2d = 0.15
+        radii = torch.rand(N, generator=g) ** 3 * 0.25
+        state["radii"] = radii.clone()
     torch.manual_seed(1000 + seed)
     n_dupli, n_split = strat._grow_gs(params, opts, state, step)
     n_prune = strat._prune_gs(params, opts, state, step)
@@ -88,7 +94,10 @@ def run(name, N, seed, step, scene_scale=1.0, revised=False, reset=False):
 
     out = {"N": N, "step": step, "scene_scale": scene_scale, "revised": int(revised),
            "reset": int(reset), "grad2d": grad2d.numpy(), "count": count.numpy(),
-           "n_dupli": n_dupli, "n_split": n_split, "n_prune": n_prune, "z": z.numpy()}
+           "n_dupli": n_dupli, "n_split": n_split, "n_prune": n_prune, "z": z.numpy(),
+           "scale2d_stop": scale2d_stop}
+    if radii is not None:
+        out["radii2d"] = radii.numpy()
     for k in NAMES:
         out[f"in_{k}"] = before[k].numpy()
         out[f"in_m_{k}"] = m0[k].numpy()
@@ -101,8 +110,16 @@ def run(name, N, seed, step, scene_scale=1.0, revised=False, reset=False):
           "prune", n_prune)
 
 
+CASES = {
+    "densify_early": dict(N=1200, seed=0, step=600),                  # no size pruning (< 3000)
+    "densify_late": dict(N=1200, seed=1, step=3100, scene_scale=1.3),  # + prune_scale3d
+    "densify_revised": dict(N=1000, seed=2, step=3100, revised=True),
+    "densify_reset": dict(N=1000, seed=3, step=6000, reset=True),      # refine then opacity reset
+    # screen-size split / prune (refine_scale2d_stop_iter > 0, default.py:283-284, 325-326)
+    "densify_scale2d": dict(N=1200, seed=4, step=3100, scale2d_stop=4000),
+}
+
 if __name__ == "__main__":
-    run("densify_early", 1200, 0, step=600)                  # no size pruning (step < 3000)
-    run("densify_late", 1200, 1, step=3100, scene_scale=1.3)  # + prune_scale3d
-    run("densify_revised", 1000, 2, step=3100, revised=True)
-    run("densify_reset", 1000, 3, step=6000, reset=True)       # refine then opacity reset
+    # python make_golden_strategy.py [case ...]  (default: all)
+    for name in (sys.argv[1:] or list(CASES)):
+        run(name, **CASES[name])

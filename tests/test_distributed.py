@@ -191,7 +191,8 @@ def _sharded_worker(rank, world, port, q, defer=False, groups=None):
 
 @pytest.mark.parametrize("world,defer,groups", [(2, False, None), (3, False, None),
                                                (2, True, None), (2, True, [[3, 1], [0, 2, 4]]),
-                                               (3, False, [[2], [4, 0], [1, 3]])])
+                                               (3, False, [[2], [4, 0], [1, 3]]),
+                                               (8, True, [[3, 1], [0, 2, 4]])])
 def test_sharded_adam_matches_allreduce_adam_gloo(world, defer, groups):
     """ShardedAdam (reduce-scatter -> Adam on own rows -> all-gather) equals
     all-reduce + full Adam on every rank, and the replicas stay identical --
@@ -227,20 +228,23 @@ def _oracle_refine(params, moments, grad2d, count, step, cfg, scene_scale=1.0, g
     from oracle import strategy_oracle as S
     grads = grad2d / count.clamp_min(1)
     high = grads > cfg.grow_grad2d
-    n_split = int((high & (torch.exp(params["scales"]).max(-1).values
-                           > cfg.grow_scale3d * scene_scale)).sum())
+    split = high & (torch.exp(params["scales"]).max(-1).values > cfg.grow_scale3d * scene_scale)
+    if radii2d is not None:
+        split = split | (radii2d > cfg.grow_scale2d)
+    n_split = int(split.sum())
     if z is None:
         z = torch.randn(2, n_split, 3, generator=generator)
     p, m, counts = S.refine({k: v.numpy() for k, v in params.items()},
                             {k: (a.numpy(), b.numpy()) for k, (a, b) in moments.items()},
                             grad2d.numpy(), count.numpy(), step, z.numpy(), scene_scale,
-                            revised_opacity=cfg.revised_opacity)
+                            revised_opacity=cfg.revised_opacity,
+                            radii2d=None if radii2d is None else radii2d.numpy())
     return ({k: torch.from_numpy(np.ascontiguousarray(v)) for k, v in p.items()},
             {k: [torch.from_numpy(np.ascontiguousarray(t)) for t in v] for k, v in m.items()},
             counts)
 
 
-def _trainer_skeleton(rank, world, sharded):
+def _trainer_skeleton(rank, world, sharded, scale2d=False):
     """A Trainer with CPU parameters (no rendering): what refine touches."""
     from gsplat_hip import train_step
     from gsplat_hip.densify import DefaultStrategyConfig
@@ -257,7 +261,7 @@ def _trainer_skeleton(rank, world, sharded):
     tr.params = {k: torch.nn.Parameter(v.clone()) for k, v in init.items()}
     tr.world_size, tr.rank, tr.device = world, rank, "cpu"
     tr.sharded, tr.fused = sharded, True
-    tr.strategy = DefaultStrategyConfig()
+    tr.strategy = DefaultStrategyConfig(refine_scale2d_stop_iter=4000 if scale2d else 0)
     tr.scene_scale = 1.0
     tr.lrs = [1e-3] * 6
     tr.adam_kw = dict(betas=(0.9, 0.999), eps=1e-15)
@@ -277,7 +281,8 @@ def _trainer_skeleton(rank, world, sharded):
         grads = [torch.randn(p.shape, generator=gr) * 1e-2 for p in tr.params.values()]
         if sharded:
             for p, gg in zip(tr.params.values(), grads):
-                p.grad = gg / world  # the ranks' gradients sum to gg
+                # the ranks' gradients sum to gg exactly (any world size)
+                p.grad = gg if rank == 0 else torch.zeros_like(gg)
             tr.opt.step()
             tr.opt.zero_grad()
         else:
@@ -290,16 +295,18 @@ def _trainer_skeleton(rank, world, sharded):
     gs = torch.Generator().manual_seed(100 + rank)
     tr.count = torch.randint(0, 4, (N,), generator=gs).float()
     tr.grad2d = torch.rand(N, generator=gs) * 4e-4 * tr.count
+    # state["radii"] of this rank's cameras (MAX-reduced before the refine)
+    tr.radii2d = torch.rand(N, generator=gs) ** 3 * 0.25 if scale2d else None
     return tr
 
 
-def _refine_worker(rank, world, port, q):
+def _refine_worker(rank, world, port, q, scale2d):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         dist.init_process_group("gloo", rank=rank, world_size=world)
         from gsplat_hip import train_step
         train_step.densify.refine = _oracle_refine
-        tr = _trainer_skeleton(rank, world, sharded=True)
+        tr = _trainer_skeleton(rank, world, sharded=True, scale2d=scale2d)
         tr.refine(3100)
         moms = tr.moments()  # all-gathered from the new shards
         # numpy, not tensors: a tensor in the queue lives in the worker's
@@ -315,17 +322,20 @@ def _refine_worker(rank, world, port, q):
         q.put((rank, traceback.format_exc() + repr(e)))
 
 
-def test_refine_under_dp_keeps_replicas_identical_gloo():
-    """Trainer.refine on two gloo ranks with different per-rank statistics:
-    the statistics are summed before the decision, the split noise comes from
-    the shared-seed generator, the sharded Adam moments are gathered, pushed
-    through the compaction and re-sharded -- both replicas end bit-identical
-    and equal a single-process refine on the summed statistics."""
+@pytest.mark.parametrize("world,scale2d", [(2, False), (2, True), (8, True)])
+def test_refine_under_dp_keeps_replicas_identical_gloo(world, scale2d):
+    """Trainer.refine on gloo ranks with different per-rank statistics: the
+    statistics are summed (the screen radii MAX-reduced) before the decision,
+    the split noise comes from the shared-seed generator, the sharded Adam
+    moments are gathered, pushed through the compaction and re-sharded --
+    every replica ends bit-identical and equal to a single-process refine on
+    the combined statistics.  World 8 (configs[3]): 203 Gaussians give 24-row
+    shards and 11 remainder rows (rows split in multiples of 4 * 8)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    world = 2
-    procs = [ctx.Process(target=_refine_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_refine_worker, args=(r, world, port, q, scale2d))
+             for r in range(world)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=180) for _ in range(world))
@@ -335,12 +345,15 @@ def test_refine_under_dp_keeps_replicas_identical_gloo():
     import numpy as np
     for r in range(world):
         assert isinstance(res[r], dict), res[r]
-    a, b = res[0], res[1]
-    assert a["log"] == b["log"] and a["log"][0][0] == 3100
-    for k in a["params"]:
-        assert np.array_equal(a["params"][k], b["params"][k]), k
-        assert np.array_equal(a["m"][k][0], b["m"][k][0])
-        assert np.array_equal(a["m"][k][1], b["m"][k][1])
+    a = res[0]
+    assert a["log"][0][0] == 3100
+    for r in range(1, world):
+        b = res[r]
+        assert a["log"] == b["log"]
+        for k in a["params"]:
+            assert np.array_equal(a["params"][k], b["params"][k]), k
+            assert np.array_equal(a["m"][k][0], b["m"][k][0])
+            assert np.array_equal(a["m"][k][1], b["m"][k][1])
     assert a["grad2d"] == 0.0  # statistics restart after a refine
 
     # single process, unsharded, on the summed statistics: the same result
@@ -349,11 +362,16 @@ def test_refine_under_dp_keeps_replicas_identical_gloo():
     saved = train_step.densify.refine
     train_step.densify.refine = _oracle_refine
     try:
-        trs = [_trainer_skeleton(r, world, sharded=False) for r in range(world)]
+        trs = [_trainer_skeleton(r, world, sharded=False, scale2d=scale2d)
+               for r in range(world)]
         ref = trs[0]
         ref.world_size = 1
-        ref.grad2d = trs[0].grad2d + trs[1].grad2d
-        ref.count = trs[0].count + trs[1].count
+        # summed in rank order, as the ring reduction of the tests' gloo
+        # group does for these small integers / exact sums
+        ref.grad2d = sum((t.grad2d for t in trs[1:]), trs[0].grad2d.clone())
+        ref.count = sum((t.count for t in trs[1:]), trs[0].count.clone())
+        if scale2d:
+            ref.radii2d = torch.stack([t.radii2d for t in trs]).amax(0)
         ref.refine(3100)
     finally:
         train_step.densify.refine = saved

@@ -33,8 +33,10 @@ def test_refine_matches_reference(name):
     params = {k: T(g[f"in_{k}"]) for k in NAMES}
     moments = {k: [T(g[f"in_m_{k}"]), T(g[f"in_v_{k}"])] for k in NAMES}
     cfg = densify.DefaultStrategyConfig(revised_opacity=bool(g["revised"]))
+    r2d = T(g["radii2d"]) if "radii2d" in g else None
     p, m, counts = densify.refine(params, moments, T(g["grad2d"]), T(g["count"]), int(g["step"]),
-                                  cfg, scene_scale=float(g["scene_scale"]), z=T(g["z"]))
+                                  cfg, scene_scale=float(g["scene_scale"]), z=T(g["z"]),
+                                  radii2d=r2d)
     if int(g["reset"]):
         densify.reset_opacity(p, m, cfg.prune_opa * 2.0)
     torch.cuda.synchronize()

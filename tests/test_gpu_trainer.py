@@ -322,17 +322,14 @@ def test_sh_adam_in_backward_is_exact(degree):
         opt = FusedAdam([p0, p1], [2.5e-3, 2.5e-3 / 20], betas=(0.9, 0.999), eps=1e-15)
         gm = []
         for it in range(4):
-            fa = None
+            fa = fusion = None
             if fused:
                 fa = _wrapper.ShAdamInBackward(p0.data, p1.data, opt.exp_avg[0], opt.exp_avg_sq[0],
                                                opt.exp_avg[1], opt.exp_avg_sq[1], opt.lrs[0],
                                                opt.lrs[1], opt.betas, opt.eps, opt.step_count + 1)
-                _wrapper._SH_ADAM = fa
-            try:
-                colors = _wrapper.sh_colors(degree, mm, vm, (p0, p1), radii)
-                (colors * ws[it]).sum().backward()
-            finally:
-                _wrapper._SH_ADAM = None
+                fusion = _wrapper.StepFusion(sh_adam=fa)
+            colors = _wrapper.sh_colors(degree, mm, vm, (p0, p1), radii, fusion=fusion)
+            (colors * ws[it]).sum().backward()
             if fused and degree == 3:
                 assert fa.applied and p0.grad is None and p1.grad is None
                 opt.step(skip=(0, 1))
@@ -422,3 +419,96 @@ def test_fused_loss_constant_seed_skips_scaling_exactly():
                             torch.ones((), device="cuda"))
     assert torch.equal(a.grad, b.grad)
     assert float(seed) == 1.0
+
+
+def test_fusion_context_is_per_render():
+    """The fused optimizer work travels with the StepFusion handed to one
+    forward: a second render in between (no fusion object) keeps ordinary
+    gradients, and the fused node still applies its Adam step exactly once."""
+    from gsplat_hip import _wrapper
+    from gsplat_hip.losses import FusedAdam
+    g = torch.Generator(device="cuda").manual_seed(7)
+    N = 777
+    means = (torch.randn(N, 3, device="cuda", generator=g) * 2).requires_grad_(True)
+    vm = torch.eye(4, device="cuda")[None]
+    vm[0, 2, 3] = 6.0
+    radii = (torch.rand(1, N, device="cuda", generator=g) > 0.3).int() * 3
+    p0 = (torch.randn(N, 1, 3, device="cuda", generator=g) * 0.3).requires_grad_(True)
+    p1 = (torch.randn(N, 15, 3, device="cuda", generator=g) * 0.1).requires_grad_(True)
+    w = torch.rand(1, N, 3, device="cuda", generator=g) - 0.5
+    opt = FusedAdam([p0, p1], [2.5e-3, 1.25e-4], eps=1e-15)
+    fa = _wrapper.ShAdamInBackward(p0.data, p1.data, opt.exp_avg[0], opt.exp_avg_sq[0],
+                                   opt.exp_avg[1], opt.exp_avg_sq[1], opt.lrs[0], opt.lrs[1],
+                                   opt.betas, opt.eps, 1)
+    fusion = _wrapper.StepFusion(sh_adam=fa, geom=True)
+    c_fused = _wrapper.sh_colors(3, means, vm, (p0, p1), radii, fusion=fusion)
+    before = p0.detach().clone()
+    # an unrelated render + backward between the fused forward and its backward
+    other = _wrapper.sh_colors(3, means, vm, (p0, p1), radii)
+    (other * w).sum().backward()
+    assert p0.grad is not None and p1.grad is not None and means.grad is not None
+    assert not fa.applied and fusion.v_dirs is None
+    assert torch.equal(p0.detach(), before)
+    g_other = (p0.grad.clone(), means.grad.clone())
+    p0.grad = p1.grad = means.grad = None
+    (c_fused * w).sum().backward()
+    assert fa.applied and p0.grad is None and p1.grad is None
+    assert means.grad is None and fusion.v_dirs is not None  # handed to the geometry update
+    torch.testing.assert_close(fusion.v_dirs, g_other[1], rtol=0, atol=0)
+    assert not torch.equal(p0.detach(), before)  # updated in place, once
+
+
+def test_trainer_regulariser_with_fusions_matches_unfused(monkeypatch):
+    """simple_trainer's opacity / scale regularisers (terms on the raw
+    parameters, simple_trainer.py:671-681) reach .grad outside the fused
+    nodes; the fused geometry update adds them as extra terms, so the fused
+    trainer tracks the unfused one (nothing is dropped)."""
+    from gsplat_hip.train_step import Trainer
+    means, rgbs, vm, K, W, H = _small_scene()
+    out = {}
+    for f in ("0", "1"):
+        monkeypatch.setenv("GSPLAT_HIP_GEOM_FUSE", f)
+        tr = Trainer(means, rgbs, vm, K, W, H, device="cuda", opacity_reg=0.5, scale_reg=5.0)
+        assert tr.geom_fuse == (f == "1")
+        losses = [float(tr.step(it)) for it in range(4)]
+        out[f] = (losses, {k: p.detach().clone() for k, p in tr.params.items()})
+    for a, b in zip(out["0"][0], out["1"][0]):
+        assert abs(a - b) <= 1e-4 * abs(a) + 1e-7, (out["0"][0], out["1"][0])
+    for k in out["0"][1]:
+        torch.testing.assert_close(out["1"][1][k], out["0"][1][k], rtol=1e-3, atol=1e-5)
+    # and the regulariser changes the result (it is not silently dropped)
+    monkeypatch.setenv("GSPLAT_HIP_GEOM_FUSE", "1")
+    tr = Trainer(means, rgbs, vm, K, W, H, device="cuda")
+    for it in range(4):
+        tr.step(it)
+    assert not torch.allclose(tr.params["opacities"], out["1"][1]["opacities"], rtol=0, atol=1e-6)
+
+
+def test_trainer_tracks_screen_radii_for_scale2d_refine():
+    """refine_scale2d_stop_iter > 0 (default.py:235-262, 283-284, 325-326):
+    the trainer keeps state["radii"] (max screen radius / max(W, H)), hands
+    it to the refine before the stop step and restarts it after a refine;
+    the kernel's use of it is pinned by the densify_scale2d golden
+    (test_gpu_strategy.py)."""
+    from gsplat_hip.densify import DefaultStrategyConfig
+    from gsplat_hip.train_step import Trainer
+    means, rgbs, vm, K, W, H = _small_scene()
+    cfg = DefaultStrategyConfig(refine_start_iter=1, refine_every=2, reset_every=100,
+                                refine_scale2d_stop_iter=3)
+    tr = Trainer(means, rgbs, vm, K, W, H, device="cuda", strategy=cfg, init="sfm")
+    assert cfg.key_for_gradient == "means2d" and tr.strategy is not cfg  # caller's config untouched
+    tr.step(0)
+    meta = tr.last_meta
+    exp = meta["radii"][0].float() / float(max(W, H))
+    torch.testing.assert_close(tr.radii2d, exp, rtol=0, atol=0)
+    tr.step(1)
+    n_before = tr.params["means"].shape[0]
+    tr.step(2)  # refine with the screen-size split / prune
+    assert [r[0] for r in tr.refine_log] == [2]
+    n_after = tr.params["means"].shape[0]
+    assert n_after == tr.refine_log[0][-1] and tr.radii2d.shape == (n_after,)
+    assert float(tr.radii2d.abs().sum()) == 0.0
+    # splits happened (the screen-size rule adds every Gaussian over 5 % of the image)
+    assert tr.refine_log[0][2] > 0 and n_before > 0
+    for it in range(3, 6):
+        assert math.isfinite(float(tr.step(it)))

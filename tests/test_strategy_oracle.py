@@ -14,7 +14,7 @@ from conftest import load_golden
 from oracle import strategy_oracle as S
 
 NAMES = ("means", "scales", "quats", "opacities", "sh0", "shN")
-CASES = ["densify_early", "densify_late", "densify_revised", "densify_reset"]
+CASES = ["densify_early", "densify_late", "densify_revised", "densify_reset", "densify_scale2d"]
 
 
 def golden_inputs(g):
@@ -44,7 +44,7 @@ def test_refine_oracle_matches_reference(name):
     params, moments = golden_inputs(g)
     p, m, counts = S.refine(params, moments, g["grad2d"], g["count"], int(g["step"]), g["z"],
                             scene_scale=float(g["scene_scale"]),
-                            revised_opacity=bool(g["revised"]))
+                            revised_opacity=bool(g["revised"]), radii2d=g.get("radii2d"))
     if int(g["reset"]):
         p, m = S.reset_opacity(p, m, 0.01)
     check_against_golden(g, p, m, counts)
