@@ -61,6 +61,10 @@ def parse():
                     help="rasterize every k-th tile in the CPU baseline (0: auto)")
     ap.add_argument("--no-traffic", action="store_true",
                     help="skip the rocprofv3 PMC child runs that measure roofline.traffic")
+    ap.add_argument("--dp-path", action="store_true",
+                    help="at N=1: run the N>1 code path (sharded Adam, early SH "
+                         "reduce-scatter, per-group communicators) over a 1-rank RCCL "
+                         "group -- the per-rank step of the data-parallel configuration")
     ap.add_argument("--probe", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
 
@@ -202,9 +206,16 @@ def main():
         # touches the GPU (spawned interpreters running numpy only)
         from oracle.cpu_step import CpuPool
         cpu_pool = CpuPool(host_threads())
+    dp_path = world > 1 or args.dp_path
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    elif args.dp_path:  # a 1-rank RCCL group: the N>1 code path on one GPU
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(_free_port()))
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", rank=0, world_size=1,
+                                device_id=torch.device("cuda", local))
     traffic = None
     if rank == 0 and world == 1 and not args.no_traffic and not args.probe:
         traffic = pmc_traffic(args.config)  # child processes, before this one uses the GPU
@@ -228,7 +239,7 @@ def main():
                   init="sfm")
         start = max(0, REFINE_AT - args.warmup - args.steps // 2)
     tr = Trainer(means, rgbs, vm_pool, K_pool, W, H, sh_degree=3, device=dev, world_size=world,
-                 rank=rank, model=model, **kw)
+                 rank=rank, model=model, sharded_optimizer=dp_path, **kw)
     N = means.shape[0]
 
     for it in range(start, start + args.warmup):
@@ -333,11 +344,14 @@ def main():
         "config": {"workload": desc, "gaussians": N,
                    "gaussians_after": int(tr.params["means"].shape[0]),
                    "first_timed_step": start + args.warmup, "width": W, "height": H,
-                   "cameras_per_rank_per_step": 1, "parallelism": f"dp{world}",
+                   "cameras_per_rank_per_step": 1,
+                   "parallelism": f"dp{world}" + (
+                       " (the N>1 code path on a 1-rank RCCL group: sharded Adam, "
+                       "early SH reduce-scatter)" if dp_path and world == 1 else ""),
                    "n_isects_mean": float(np.mean(isects)), "n_eff_mean": float(np.mean(n_effs)),
                    "packed": False, "loss": "0.8*L1+0.2*(1-SSIM valid)",
                    "optimizer": "Adam (6 groups)" + (
-                       ", sharded over ranks" if world > 1 else
+                       ", sharded over ranks" if dp_path else
                        ", SH groups' step fused into the SH backward"
                        if getattr(tr, "sh_adam_in_bwd", False) else ""),
                    "densification": tr.densify_desc()},
@@ -373,6 +387,7 @@ def main():
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.barrier()
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

@@ -133,13 +133,23 @@ def all_to_all_tensor_list(world_size: int, tensor_list: List[Tensor],
 
 # ------------------------------------------- per-camera data parallelism --
 
-def _adam_torch(params, grads, exp_avgs, exp_avg_sqs, lrs, betas, eps, step):
-    """torch restatement of csrc/adam.hip's update (same operation order), for
-    running ShardedAdam's collectives on the CPU (gloo tests)."""
+def _adam_torch(params, grads, exp_avgs, exp_avg_sqs, lrs, betas, eps, step, max_blocks=0,
+                aux=None, modes=None):
+    """torch restatement of csrc/adam.hip's update (same operation order, the
+    gradient transforms of gsplat_hip_adam_step_ex included), for running
+    ShardedAdam's collectives on the CPU (gloo tests)."""
     b1, b2 = betas
     bc1, bc2 = 1.0 - b1 ** step, 1.0 - b2 ** step
-    for p, g, m, v, lr in zip(params, grads, exp_avgs, exp_avg_sqs, lrs):
+    aux = aux or [None] * len(params)
+    modes = modes or [0] * len(params)
+    for p, g, m, v, lr, a, md in zip(params, grads, exp_avgs, exp_avg_sqs, lrs, aux, modes):
         g = torch.zeros_like(p) if g is None else g
+        if md == 1:
+            g = g + a
+        elif md == 2:
+            g = g * a
+        elif md == 3:
+            g = g * (1.0 - a) * a
         m.add_((1.0 - b1) * (g - m))
         v.mul_(b2).add_((1.0 - b2) * g * g)
         p.sub_((lr / bc1) * m / (v.sqrt() * (1.0 / math.sqrt(bc2)) + eps))
@@ -167,9 +177,24 @@ class ShardedAdam:
     the geometry first (the next projection needs it, 44 B/Gaussian) and the SH
     rows last (192 B/Gaussian, needed only by the colours after the next
     isect), and neither the host nor the compute stream waits for any of it.
+
+    `group_pgs` gives each group its own process group (communicator), so the
+    groups' collectives do not queue behind each other: the trainer issues
+    the SH group's reduce-scatter from a gradient hook while the backward is
+    still running (`reduce_early`) on one communicator, and the geometry's
+    after the backward on another -- the small, latency-critical geometry
+    exchange never waits for the 4x larger SH one.
+
+    `step(xform=...)` folds the trainer's gradient transforms into the update
+    (gsplat_hip_adam_step_ex): the activation VJPs (modes 2 / 3) are linear
+    in the incoming gradient, so that gradient is what is reduce-scattered
+    and the VJP is applied to the summed shard in-register (its `aux`, the
+    activation, is replicated and sliced like the parameter); a second
+    gradient term (mode 1) is summed locally before the reduction.
     """
 
-    def __init__(self, params, lrs, betas=(0.9, 0.999), eps=1e-8, update=None, groups=None):
+    def __init__(self, params, lrs, betas=(0.9, 0.999), eps=1e-8, update=None, groups=None,
+                 group_pgs=None):
         self.params = list(params)
         self.lrs = [float(x) for x in lrs]
         self.betas, self.eps = betas, eps
@@ -197,6 +222,9 @@ class ShardedAdam:
         self.groups = [list(g) for g in groups] if groups else [list(self.order)]
         assert sorted(i for g in self.groups for i in g) == list(range(len(self.params))), \
             self.groups
+        self.group_pgs = list(group_pgs) if group_pgs else [None] * len(self.groups)
+        assert len(self.group_pgs) == len(self.groups)
+        self._early = {}  # group index -> (flats, works) issued by reduce_early
         self._pending = {}  # parameter index -> all-gather still in flight
         # parameter index -> event after its group's update on the side stream
         # (tail rows and parameters too short for a shard are updated there
@@ -220,34 +248,63 @@ class ShardedAdam:
         row, q, _, _ = self.layout[i]
         return flat[self.rank * q * row:(self.rank + 1) * q * row]
 
+    def _issue_reduce(self, gi, grads):
+        """Reduce-scatter (main rows) and all-reduce (remainder rows) of group
+        gi's gradients on its process group, issued from the current stream."""
+        pg = self.group_pgs[gi]
+        flats, works = {}, []
+        for i in sorted(self.groups[gi], key=lambda i: -self.params[i].numel()):
+            g = grads.get(i)
+            gf = (torch.zeros_like(self.params[i]) if g is None else g).contiguous().view(-1)
+            flats[i] = gf
+            if self.side is not None:  # its tail rows are read on the side stream
+                gf.record_stream(self.side)
+            _, _, main, tot = self.layout[i]
+            if main:
+                works.append(dist.reduce_scatter_tensor(self.g_shard[i], gf[:main], group=pg,
+                                                        async_op=True))
+            if tot > main:
+                works.append(dist.all_reduce(gf[main:], group=pg, async_op=True))
+        return flats, works
+
+    def _grads(self, grp, xform):
+        out = {}
+        for i in grp:
+            if xform and i in xform:
+                g, a, mode = xform[i]
+                out[i] = g + a if mode == 1 else g  # modes 2 / 3: applied after the reduction
+            else:
+                out[i] = self.params[i].grad
+        return out
+
     @torch.no_grad()
-    def step(self, defer_gather=False):
+    def reduce_early(self, gi, xform=None):
+        """Issue group gi's reductions now (from a gradient hook, while the
+        rest of the backward is still being queued); the next step() only
+        waits for them.  Stream order only, no host synchronisation."""
+        if gi not in self._early:
+            self._early[gi] = self._issue_reduce(gi, self._grads(self.groups[gi], xform))
+
+    @torch.no_grad()
+    def step(self, defer_gather=False, xform=None):
         """defer_gather: leave the all-gathers in flight; the caller orders
-        each parameter's next use after `wait([i])` (stream order only)."""
+        each parameter's next use after `wait([i])` (stream order only).
+        xform: {index: (grad, aux, mode)} as FusedAdam.step (see the class
+        docstring for where each mode is applied)."""
         self.wait()
         self.step_count += 1
         side = self.side
-        if side is not None:  # the side stream starts after everything queued so far
-            side.wait_stream(torch.cuda.current_stream(side.device))
-        for grp in self.groups:
-            flats, works = {}, []
-            for i in sorted(grp, key=lambda i: -self.params[i].numel()):
-                p = self.params[i]
-                g = p.grad if p.grad is not None else torch.zeros_like(p)
-                gf = g.contiguous().view(-1)
-                flats[i] = gf
-                if side is not None:  # its tail rows are read on the side stream
-                    gf.record_stream(side)
-                _, _, main, tot = self.layout[i]
-                if main:
-                    works.append(dist.reduce_scatter_tensor(self.g_shard[i], gf[:main],
-                                                            async_op=True))
-                if tot > main:
-                    works.append(dist.all_reduce(gf[main:], async_op=True))
+        for gi, grp in enumerate(self.groups):
+            if gi in self._early:
+                flats, works = self._early.pop(gi)
+            else:
+                flats, works = self._issue_reduce(gi, self._grads(grp, xform))
+            if side is not None:  # the side stream starts after everything queued so far
+                side.wait_stream(torch.cuda.current_stream(side.device))
             with (torch.cuda.stream(side) if side is not None else _nullcontext()):
                 for wk in works:  # the side stream (gloo: the host) waits
                     wk.wait()
-                self._update_group(grp, flats)
+                self._update_group(grp, flats, xform)
                 if side is not None:
                     ev = torch.cuda.Event()
                     ev.record(side)
@@ -259,23 +316,35 @@ class ShardedAdam:
                     if main:
                         full = self.params[i].data.view(-1)[:main]
                         self._pending[i] = dist.all_gather_into_tensor(
-                            full, self._shard(i, full).clone(), async_op=True)
+                            full, self._shard(i, full).clone(), group=self.group_pgs[gi],
+                            async_op=True)
         if not defer_gather:
             self.wait()
 
-    def _update_group(self, grp, flats):
+    def _update_group(self, grp, flats, xform=None):
+        def tx(i):  # (aux, mode) of a post-reduction transform, else (None, 0)
+            if xform and i in xform and xform[i][2] in (2, 3):
+                return xform[i][1].reshape(-1), xform[i][2]
+            return None, 0
         idx = [i for i in grp if self.layout[i][2]]
         if idx:
+            aux = [tx(i)[0] for i in idx]
             self.update([self._shard(i, self.params[i].data.view(-1)) for i in idx],
                         [self.g_shard[i] for i in idx], [self.m[i] for i in idx],
                         [self.v[i] for i in idx], [self.lrs[i] for i in idx], self.betas,
-                        self.eps, self.step_count)
+                        self.eps, self.step_count,
+                        aux=[None if a is None else self._shard(i, a) for i, a in zip(idx, aux)],
+                        modes=[tx(i)[1] for i in idx])
         tails = [i for i in grp if self.layout[i][3] > self.layout[i][2]]
         if tails:
+            aux = [tx(i)[0] for i in tails]
             self.update([self.params[i].data.view(-1)[self.layout[i][2]:] for i in tails],
                         [flats[i][self.layout[i][2]:] for i in tails],
                         [self.m_tail[i] for i in tails], [self.v_tail[i] for i in tails],
-                        [self.lrs[i] for i in tails], self.betas, self.eps, self.step_count)
+                        [self.lrs[i] for i in tails], self.betas, self.eps, self.step_count,
+                        aux=[None if a is None else a[self.layout[i][2]:]
+                             for i, a in zip(tails, aux)],
+                        modes=[tx(i)[1] for i in tails])
 
     def zero_grad(self, set_to_none=True):
         for p in self.params:

@@ -205,11 +205,21 @@ class Trainer:
         self.sh_adam_in_bwd = (fused and not self.sharded and not self.defer_sh
                                and world_size == 1
                                and os.environ.get("GSPLAT_HIP_SH_ADAM_IN_BWD", "1") != "0")
-        # same conditions: the exp / sigmoid VJPs and the means-gradient sum
-        # formed inside the geometry groups' Adam (gsplat_hip_adam_step_ex)
-        self.geom_fuse = (fused and not self.sharded and not self.defer_sh and world_size == 1
+        # the exp / sigmoid VJPs and the means-gradient sum formed inside the
+        # geometry groups' Adam (gsplat_hip_adam_step_ex): at one rank, and
+        # under the sharded optimizer on the reduced shard (ShardedAdam.step)
+        self.geom_fuse = (fused and not self.defer_sh and (world_size == 1 or self.sharded)
                           and os.environ.get("GSPLAT_HIP_GEOM_FUSE", "1") != "0")
+        # sharded optimizer: the SH group's collectives on a communicator of
+        # their own (issued from a gradient hook during the backward), the
+        # geometry's on the default group
+        self._sh_pg = None
+        if self.sharded:
+            import torch.distributed as dist
+            self._sh_pg = dist.new_group(list(range(dist.get_world_size())))
+        self._sh_ready = 0
         self.opt = self._make_optimizer(list(self.params.values()))
+        self._register_hooks()
         self.viewmats = viewmats.to(device)
         self.Ks = Ks.to(device)
         if targets is None:
@@ -237,7 +247,9 @@ class Trainer:
             names = list(self.params)
             groups = [[names.index(k) for k in ("means", "scales", "quats", "opacities")],
                       [names.index(k) for k in ("sh0", "shN")]]
-            return ShardedAdam(params, self.lrs, groups=groups, **self.adam_kw)
+            return ShardedAdam(params, self.lrs, groups=groups,
+                               group_pgs=[None, getattr(self, "_sh_pg", None)],
+                               **self.adam_kw)
         if self.fused:  # HIP loss + one-launch Adam (csrc/ssim.hip, csrc/adam.hip)
             # the SH rows' update on a side stream, overlapping the next
             # step's projection and isect (render() waits before the colours)
@@ -247,6 +259,21 @@ class Trainer:
         groups = [{"params": [p], "lr": lr, "name": k}
                   for (k, p), lr in zip(self.params.items(), self.lrs)]
         return torch.optim.Adam(groups, foreach=True, **self.adam_kw)
+
+    def _register_hooks(self):
+        """Sharded optimizer: reduce-scatter the SH group as soon as the
+        SH-colour backward has produced both of its gradients (the rest of
+        the backward -- projection, activations -- is still to run), from a
+        post-accumulate hook on sh0 and shN."""
+        if not self.sharded:
+            return
+        for k in ("sh0", "shN"):
+            self.params[k].register_post_accumulate_grad_hook(self._sh_grad_ready)
+
+    def _sh_grad_ready(self, param):
+        self._sh_ready += 1
+        if self._sh_ready == 2:
+            self.opt.reduce_early(1)
 
     def _set_means_lr(self, lr):
         if isinstance(self.opt, torch.optim.Optimizer):
@@ -355,6 +382,7 @@ class Trainer:
 
     def step(self, it: int):
         ci = self.camera_index(it)
+        self._sh_ready = 0
         fusion = self._make_fusion()
         colors, alphas, meta = self.render(ci, self.sh_degree_at(it), fusion)
         if self.model == "3dgs":
@@ -386,7 +414,7 @@ class Trainer:
         if self.max_steps:  # means ExponentialLR, stepped after every optimizer step
             self._set_means_lr(self.lrs[0] * (0.01 ** (1.0 / self.max_steps)) ** it)
         if self.sharded:
-            self.opt.step(defer_gather=True)
+            self.opt.step(defer_gather=True, xform=self._geom_xform(fusion))
         else:
             self.opt.step(skip=self._sh_skip(fusion), xform=self._geom_xform(fusion))
         self.opt.zero_grad(set_to_none=True)
@@ -410,10 +438,8 @@ class Trainer:
         """This step's StepFusion (None when nothing is fused): the SH groups'
         Adam inside the SH backward (sh_adam_in_bwd) and the geometry groups'
         gradient transforms inside their Adam (geom_fuse)."""
-        if not isinstance(self.opt, FusedAdam):
-            return None
         fa = None
-        if getattr(self, "sh_adam_in_bwd", False):
+        if getattr(self, "sh_adam_in_bwd", False) and isinstance(self.opt, FusedAdam):
             names = list(self.params)
             i0, i1 = names.index("sh0"), names.index("shN")
             o = self.opt
@@ -421,7 +447,8 @@ class Trainer:
                 self.params["sh0"].data, self.params["shN"].data, o.exp_avg[i0],
                 o.exp_avg_sq[i0], o.exp_avg[i1], o.exp_avg_sq[i1], o.lrs[i0], o.lrs[i1],
                 o.betas, o.eps, o.step_count + 1)
-        geom = getattr(self, "geom_fuse", False)
+        geom = getattr(self, "geom_fuse", False) and (isinstance(self.opt, FusedAdam) or
+                                                      self.sharded)
         if fa is None and not geom:
             return None
         return _wrapper.StepFusion(sh_adam=fa, geom=geom)
@@ -532,6 +559,7 @@ class Trainer:
                                               generator=self.rng, radii2d=radii2d)
         self.params = {k: torch.nn.Parameter(v) for k, v in new_p.items()}
         self._load_moments(new_m)
+        self._register_hooks()
         n = self.params["means"].shape[0]
         self.grad2d = torch.zeros(n, device=self.device)
         self.count = torch.zeros(n, device=self.device)

@@ -321,6 +321,56 @@ def gen_e2e():
         print(f"   {name} n_isects={len(meta['flatten_ids'])} {time.time()-t0:.1f}s")
 
 
+def gen_e2e_aa():
+    """rasterization() with rasterize_mode="antialiased" (the compensation
+    multiply, gsplat/rendering.py:328,347-351), which the two M1 fixtures
+    above leave out."""
+    print("end-to-end rasterization() options")
+    from gsplat.rendering import rasterization
+    # antialiased, SH degree 3, RGB
+    t0 = time.time()
+    means, quats, scales, opac, sh, vm, K, W_, H_ = synthetic_m1(seed=3)
+    ins = [x.clone().requires_grad_(True) for x in (means, quats, scales, opac, sh)]
+    rc, ra, meta = rasterization(ins[0], ins[1], ins[2], ins[3], ins[4], vm, K, W_, H_,
+                                 sh_degree=3, packed=False, rasterize_mode="antialiased")
+    g = torch.Generator().manual_seed(6)
+    v_rc = torch.randn(rc.shape, generator=g)
+    v_ra = torch.randn(ra.shape, generator=g)
+    grads = torch.autograd.grad((rc * v_rc).sum() + (ra * v_ra).sum(), ins)
+    save("e2e_m1_aa", means=means, quats=quats, scales=scales, opacities=opac, sh=sh,
+         viewmats=vm, Ks=K, width=W_, height=H_, render_colors=rc, render_alphas=ra,
+         radii=meta["radii"], isect_ids=meta["isect_ids"], flatten_ids=meta["flatten_ids"],
+         opacities_eff=meta["opacities"], v_render_colors=v_rc, v_render_alphas=v_ra,
+         v_means=grads[0], v_quats=grads[1], v_scales=grads[2], v_opacities=grads[3],
+         v_sh=grads[4])
+    print(f"   e2e_m1_aa n_isects={len(meta['flatten_ids'])} {time.time()-t0:.1f}s")
+
+
+def gen_e2e_d40():
+    """40 colour channels (no SH): two chunks, 32 + 8, with backgrounds
+    (gsplat/rendering.py:544-572); a 96x96 image keeps the fixture small."""
+    from gsplat.rendering import rasterization
+    t0 = time.time()
+    means, quats, scales, opac, _, vm, K, W_, H_ = synthetic_m1(seed=4, N=600, W_=96, H_=96)
+    D = 40
+    cols = torch.rand(len(means), D, generator=torch.Generator().manual_seed(7))
+    bg = torch.linspace(0.0, 1.0, D)[None]
+    ins = [x.clone().requires_grad_(True) for x in (means, quats, scales, opac, cols)]
+    rc, ra, meta = rasterization(ins[0], ins[1], ins[2], ins[3], ins[4], vm, K, W_, H_,
+                                 packed=False, backgrounds=bg, channel_chunk=32)
+    g = torch.Generator().manual_seed(8)
+    v_rc = torch.randn(rc.shape, generator=g)
+    v_ra = torch.randn(ra.shape, generator=g)
+    grads = torch.autograd.grad((rc * v_rc).sum() + (ra * v_ra).sum(), ins)
+    save("e2e_m1_d40", means=means, quats=quats, scales=scales, opacities=opac, colors=cols,
+         viewmats=vm, Ks=K, width=W_, height=H_, backgrounds=bg, render_colors=rc,
+         render_alphas=ra, radii=meta["radii"], isect_ids=meta["isect_ids"],
+         flatten_ids=meta["flatten_ids"], v_render_colors=v_rc, v_render_alphas=v_ra,
+         v_means=grads[0], v_quats=grads[1], v_scales=grads[2], v_opacities=grads[3],
+         v_colors=grads[4])
+    print(f"   e2e_m1_d40 n_isects={len(meta['flatten_ids'])} {time.time()-t0:.1f}s")
+
+
 def gen_scene():
     """Benchmark scene: assets/test_garden.npz cropped to [-2,2]^3 exactly as
     load_test_data() does (gsplat/_helper.py:30-36) -- SfM points, colours and
@@ -340,4 +390,5 @@ if __name__ == "__main__":
     torch.set_num_threads(8)
     for w in which:
         {"projection": gen_projection, "sh": gen_sh, "isect": gen_isect,
-         "raster": gen_raster, "e2e": gen_e2e, "scene": gen_scene}[w]()
+         "raster": gen_raster, "e2e": gen_e2e, "e2e_aa": gen_e2e_aa, "e2e_d40": gen_e2e_d40,
+         "scene": gen_scene}[w]()

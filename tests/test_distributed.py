@@ -189,6 +189,85 @@ def _sharded_worker(rank, world, port, q, defer=False, groups=None):
         q.put((rank, repr(e), None))
 
 
+def _sharded_xform_worker(rank, world, port, q):
+    """ShardedAdam with the trainer's DP configuration: two groups on two
+    process groups, the second reduced early (reduce_early, as from the SH
+    gradient hook), and gradient transforms (mode 1 summed before the
+    reduction, modes 2 / 3 applied to the reduced shard)."""
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from gsplat_hip.distributed import ShardedAdam, _adam_torch
+        g = torch.Generator().manual_seed(0)
+        shapes = [(41, 3), (41, 3), (41, 4), (41,), (41, 1, 3), (41, 15, 3)]
+        init = [torch.randn(s, generator=g) for s in shapes]
+        lrs = [1.6e-4, 5e-3, 1e-3, 5e-2, 2.5e-3, 1.25e-4]
+        kw = dict(betas=(0.9, 0.999), eps=1e-15)
+        ps = [torch.nn.Parameter(t.clone()) for t in init]
+        ref = [t.clone() for t in init]
+        pg2 = dist.new_group(list(range(world)))
+        opt = ShardedAdam(ps, lrs, update=_adam_torch, groups=[[0, 1, 2, 3], [4, 5]],
+                          group_pgs=[None, pg2], **kw)
+        m = [torch.zeros_like(t).view(-1) for t in init]
+        v = [torch.zeros_like(t).view(-1) for t in init]
+        for step in range(1, 4):
+            gr = torch.Generator().manual_seed(100 * step + rank)
+            grads = [torch.randn(s, generator=gr) for s in shapes]
+            v_dirs = torch.randn(shapes[0], generator=gr)  # second means term
+            s_act = torch.exp(ps[1].detach())             # replicated activations
+            o_act = torch.sigmoid(ps[3].detach())
+            for i in (0, 2, 4, 5):
+                ps[i].grad = grads[i].clone()
+            xf = {0: (ps[0].grad, v_dirs, 1), 1: (grads[1], s_act, 2), 3: (grads[3], o_act, 3)}
+            opt.reduce_early(1)  # the SH group, before the rest
+            opt.step(defer_gather=True, xform=xf)
+            opt.wait()
+            opt.zero_grad()
+            # reference: all-reduce the per-rank gradients of the parameters
+            # (VJPs on every rank's own gradient), full Adam
+            loc = [grads[0] + v_dirs, grads[1] * s_act, grads[2], grads[3] * (1 - o_act) * o_act,
+                   grads[4], grads[5]]
+            for t in loc:
+                dist.all_reduce(t)
+            _adam_torch([t.view(-1) for t in ref], [t.view(-1) for t in loc], m, v, lrs,
+                        kw["betas"], kw["eps"], step)
+        err = max(float((p.detach() - r).abs().max() / (r.abs().max() + 1e-12))
+                  for p, r in zip(ps, ref))
+        q.put((rank, err, [p.detach().tolist() for p in ps]))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:
+        import traceback
+        q.put((rank, traceback.format_exc() + repr(e), None))
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_sharded_adam_dp_fusions_gloo(world):
+    """The DP step's fusions: each group's collectives on its own process
+    group, the SH group reduced early, the activation VJPs applied to the
+    reduced shard (sum of VJPs == VJP of the sum up to rounding: 1e-5
+    relative), replicas identical."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sharded_xform_worker, args=(r, world, port, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    out = {}
+    for _ in range(world):
+        rank, err, vals = q.get(timeout=180)
+        out[rank] = (err, vals)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank in range(world):
+        err, vals = out[rank]
+        assert not isinstance(err, str), err
+        assert err < 1e-5, (rank, err)
+        assert vals == out[0][1], "replicas diverged"
+
+
 @pytest.mark.parametrize("world,defer,groups", [(2, False, None), (3, False, None),
                                                (2, True, None), (2, True, [[3, 1], [0, 2, 4]]),
                                                (3, False, [[2], [4, 0], [1, 3]]),

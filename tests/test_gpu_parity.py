@@ -462,7 +462,8 @@ def test_raster_tile_masks_skip():
 # coefficients, loosened to the rasterizer's 1e-3 bar that feeds them).  The
 # achieved errors are written to gpurun_out/e2e_parity_errors.json.
 E2E_TOL = {"v_means": (1e-3, 1e-3), "v_quats": (5e-3, 5e-3), "v_scales": (5e-3, 5e-3),
-           "v_opacities": (2e-3, 2e-3), "v_sh": (1e-3, 1e-3)}
+           "v_opacities": (2e-3, 2e-3), "v_sh": (1e-3, 1e-3),
+           "v_colors": (1e-3, 1e-3)}  # test_ras2pix.py:160
 
 
 def _record_errors(name, errs):
@@ -479,21 +480,22 @@ def _record_errors(name, errs):
     json.dump(cur, open(path, "w"), indent=1, sort_keys=True)
 
 
-def _e2e_check(name, g, rc, ra, ins):
+def _e2e_check(name, g, rc, ra, ins, keys=("v_means", "v_quats", "v_scales", "v_opacities",
+                                             "v_sh")):
     errs = {"render_alphas": float(np.abs(ra.detach().cpu().numpy() - g["render_alphas"]).max()),
             "render_colors": float(np.abs(rc.detach().cpu().numpy() - g["render_colors"]).max())}
     close(ra, g["render_alphas"], 1e-4, 1e-4, "alphas")
     close(rc, g["render_colors"], 1e-4, 1e-4, "colors")  # tests/test_rasterization.py:88-89
     grads = torch.autograd.grad((rc * T(g["v_render_colors"])).sum()
                                 + (ra * T(g["v_render_alphas"])).sum(), ins)
-    for k, gr in zip(("v_means", "v_quats", "v_scales", "v_opacities", "v_sh"), grads):
+    for k, gr in zip(keys, grads):
         ref = g[k]
         scale = max(1e-12, float(np.abs(ref).max()))
         d = np.abs(gr.detach().cpu().numpy().astype(np.float64) - ref)
         errs[k] = {"max_abs": float(d.max()), "max_abs_over_max_ref": float(d.max() / scale),
                    "max_rel_where_big": float((d / np.maximum(np.abs(ref), 1e-3 * scale)).max())}
     _record_errors(name, errs)
-    for k, gr in zip(("v_means", "v_quats", "v_scales", "v_opacities", "v_sh"), grads):
+    for k, gr in zip(keys, grads):
         ref = g[k]
         rtol, atol = E2E_TOL[k]
         close(gr, ref, rtol, atol * max(1e-12, float(np.abs(ref).max())), k)
@@ -539,6 +541,45 @@ def test_rasterization_packed_vs_reference(name):
     assert np.array_equal(cam[fids] * N + gid[fids], g["flatten_ids"])
     assert np.array_equal(meta["isect_offsets"].cpu().numpy(), g["isect_offsets"])
     _e2e_check(name + "_packed", g, rc, ra, ins)
+
+
+def test_rasterization_antialiased_vs_reference():
+    """rasterize_mode="antialiased": opacities multiplied by the projection's
+    compensation (gsplat/rendering.py:328,347-351), whose backward runs the
+    compensation VJP (fused_projection_bwd.py with calc_compensations)."""
+    import gsplat_hip
+    g = load_golden("e2e_m1_aa")
+    ins = [T(g[k]).requires_grad_(True) for k in ("means", "quats", "scales", "opacities", "sh")]
+    rc, ra, meta = gsplat_hip.rasterization(
+        *ins, T(g["viewmats"]), T(g["Ks"]), int(g["width"]), int(g["height"]), sh_degree=3,
+        packed=False, rasterize_mode="antialiased")
+    assert np.array_equal(meta["radii"].cpu().numpy(), g["radii"])
+    assert np.array_equal(meta["isect_ids"].cpu().numpy(), g["isect_ids"])
+    assert np.array_equal(meta["flatten_ids"].cpu().numpy(), g["flatten_ids"])
+    vis = g["radii"] > 0
+    # the compensated opacities (test_fused_proj.py:120 bar for compensations)
+    close(meta["opacities"].detach().cpu().numpy()[vis], g["opacities_eff"][vis], 5e-4, 1e-3,
+          "opacities * compensations")
+    _e2e_check("e2e_m1_aa", g, rc, ra, ins)
+
+
+def test_rasterization_channel_chunks_vs_reference():
+    """40 colour channels: rendered in chunks of channel_chunk = 32 (32 + 8,
+    gsplat/rendering.py:544-572) with per-channel backgrounds; the alphas of
+    the first chunk are returned."""
+    import gsplat_hip
+    g = load_golden("e2e_m1_d40")
+    ins = [T(g[k]).requires_grad_(True)
+           for k in ("means", "quats", "scales", "opacities", "colors")]
+    rc, ra, meta = gsplat_hip.rasterization(
+        *ins, T(g["viewmats"]), T(g["Ks"]), int(g["width"]), int(g["height"]), packed=False,
+        backgrounds=T(g["backgrounds"]), channel_chunk=32)
+    assert rc.shape[-1] == 40
+    assert np.array_equal(meta["radii"].cpu().numpy(), g["radii"])
+    assert np.array_equal(meta["isect_ids"].cpu().numpy(), g["isect_ids"])
+    assert np.array_equal(meta["flatten_ids"].cpu().numpy(), g["flatten_ids"])
+    _e2e_check("e2e_m1_d40", g, rc, ra, ins,
+               keys=("v_means", "v_quats", "v_scales", "v_opacities", "v_colors"))
 
 
 # ------------------------------------------- size-independent properties
