@@ -61,10 +61,17 @@ def parse():
                     help="rasterize every k-th tile in the CPU baseline (0: auto)")
     ap.add_argument("--no-traffic", action="store_true",
                     help="skip the rocprofv3 PMC child runs that measure roofline.traffic")
+    ap.add_argument("--eager", action="store_true",
+                    help="issue every launch from the host each step instead of replaying "
+                         "the step captured as a HIP graph")
     ap.add_argument("--dp-path", action="store_true",
                     help="at N=1: run the N>1 code path (sharded Adam, early SH "
                          "reduce-scatter, per-group communicators) over a 1-rank RCCL "
                          "group -- the per-rank step of the data-parallel configuration")
+    ap.add_argument("--dp-emulate", type=int, default=0, metavar="W",
+                    help="with --dp-path: shard the optimizer rows as W ranks would and "
+                         "update this rank's share (the per-rank compute of a W-GPU step; "
+                         "the collectives of W ranks are not executed)")
     ap.add_argument("--probe", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
 
@@ -195,6 +202,12 @@ def main():
     args = parse()
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(launch(args.gpus, sys.argv[1:]))
+    # stdout carries exactly one line, rank 0's JSON: everything else written
+    # to fd 1 from here on (RCCL's version banner, library prints) goes to
+    # stderr.  The launcher parent above keeps its stdout for the children.
+    json_fd = os.dup(1)
+    sys.stdout.flush()
+    os.dup2(2, 1)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -206,6 +219,9 @@ def main():
         # touches the GPU (spawned interpreters running numpy only)
         from oracle.cpu_step import CpuPool
         cpu_pool = CpuPool(host_threads())
+    if args.dp_emulate:
+        args.dp_path = True
+        assert world == 1, "--dp-emulate is a one-GPU measurement"
     dp_path = world > 1 or args.dp_path
     if world > 1:
         torch.cuda.set_device(local)
@@ -239,7 +255,10 @@ def main():
                   init="sfm")
         start = max(0, REFINE_AT - args.warmup - args.steps // 2)
     tr = Trainer(means, rgbs, vm_pool, K_pool, W, H, sh_degree=3, device=dev, world_size=world,
-                 rank=rank, model=model, sharded_optimizer=dp_path, **kw)
+                 rank=rank, model=model, sharded_optimizer=dp_path,
+                 dp_emulate_world=args.dp_emulate or None,
+                 graph=not (args.eager or args.probe), **kw)
+    graphed = getattr(tr, "_graph", None) is not None
     N = means.shape[0]
 
     for it in range(start, start + args.warmup):
@@ -258,10 +277,25 @@ def main():
     t0 = time.perf_counter()
     for it in range(start + args.warmup, start + args.warmup + args.steps):
         tr.step(it)
+    tr.sync()  # graph replays: every step's overflow check settled inside the timed region
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = max_over_ranks(time.perf_counter() - t0, world, dev)
+    if graphed:
+        # kernel durations: a graph replay runs the same kernels as an eager
+        # step, but HIP events cannot be recorded per replay -- time the
+        # rasterizer launches over eager steps right after the timed region
+        g = tr._graph
+        graph_info = {"replays": g.replays, "captures": g.recaptures,
+                      "isect_capacity": g.capacity, "max_isects": g.max_isects}
+        tr._graph = None
+        timers = _wrapper.enable_kernel_timers(True)
+        n_t = min(args.steps, 10)
+        for it in range(start + args.warmup + args.steps,
+                        start + args.warmup + args.steps + n_t):
+            tr.step(it)
+        torch.cuda.synchronize()
     _wrapper.enable_kernel_timers(False)
 
     # ---- per-kernel HIP-event times over the timed region
@@ -346,10 +380,15 @@ def main():
                    "first_timed_step": start + args.warmup, "width": W, "height": H,
                    "cameras_per_rank_per_step": 1,
                    "parallelism": f"dp{world}" + (
+                       f" emulating the per-rank compute of dp{args.dp_emulate}: optimizer rows "
+                       f"sharded {args.dp_emulate} ways, this rank's share updated, no "
+                       "collectives executed (measurement only)" if args.dp_emulate else
                        " (the N>1 code path on a 1-rank RCCL group: sharded Adam, "
                        "early SH reduce-scatter)" if dp_path and world == 1 else ""),
                    "n_isects_mean": float(np.mean(isects)), "n_eff_mean": float(np.mean(n_effs)),
                    "packed": False, "loss": "0.8*L1+0.2*(1-SSIM valid)",
+                   "step_issue": ("HIP graph replay of the captured step (sync-free isect, "
+                                  f"{graph_info})" if graphed else "eager launches"),
                    "optimizer": "Adam (6 groups)" + (
                        ", sharded over ranks" if dp_path else
                        ", SH groups' step fused into the SH backward"
@@ -362,6 +401,10 @@ def main():
                      "algorithmic_bytes_per_launch": bytes_per_launch,
                      "bytes_per_isect": per_isect, "bytes_per_pixel": per_px,
                      "launch_ms": fwd_ms,
+                     "launch_ms_source": ("HIP events around the launch on its stream, over "
+                                          + ("eager steps right after the graph-replayed timed "
+                                             "region (same kernels)" if graphed else
+                                             "the timed region")),
                      # the kernel's binding ceiling is VALU issue, not HBM
                      "valu": _valu_frac(pf, fwd_ms),
                      "bwd": {"kernel": kname.replace("fwd", "bwd"), "bound": "hbm",
@@ -384,7 +427,7 @@ def main():
         finally:
             cpu_pool.close()
     if rank == 0:
-        print(json.dumps(result), flush=True)
+        os.write(json_fd, (json.dumps(result) + "\n").encode())
     if world > 1:
         dist.barrier()
     if dist.is_initialized():

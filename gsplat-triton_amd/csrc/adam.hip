@@ -35,6 +35,11 @@ struct Groups {
   int64_t begin[kMaxGroups + 1];  // prefix offsets in 4-element slots
   float step_size[kMaxGroups];    // lr / (1 - beta1^t)
   float inv_bc2_sqrt[kMaxGroups]; // 1 / sqrt(1 - beta2^t)
+  // captured-step form (gsplat_hip_adam_step_dev): the two factors per group
+  // read on the device ([2 i], [2 i + 1]), and a void step (*skip != 0)
+  // updates nothing
+  const float *hyper;
+  const int32_t *skip;
   int n;
 };
 
@@ -70,6 +75,7 @@ GS_INLINE void st4(float *p, float4 v) {
 template <int U, bool NT>
 __global__ void __launch_bounds__(256)
 step_kernel(Groups g, float beta1, float beta2, float eps) {
+  if (g.skip && *g.skip) return;
   const int64_t total = g.begin[g.n];
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t s0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s0 < total;
@@ -97,7 +103,8 @@ step_kernel(Groups g, float beta1, float beta2, float eps) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int gi = grp[u];
-      const float ss = g.step_size[gi], ib = g.inv_bc2_sqrt[gi];
+      const float ss = g.hyper ? g.hyper[2 * gi] : g.step_size[gi];
+      const float ib = g.hyper ? g.hyper[2 * gi + 1] : g.inv_bc2_sqrt[gi];
       if (full[u]) {
         const int md = g.mode[gi];
         upd(p[u].x, xform(md, gr[u].x, ax[u].x), m[u].x, v[u].x, beta1, beta2, eps, ss, ib);
@@ -135,14 +142,18 @@ static int adam_launch(int n_groups, float *const *params, const float *const *g
                        const float *const *aux, const int32_t *modes, float *const *exp_avgs,
                        float *const *exp_avg_sqs, const int64_t *numels, const float *lrs,
                        float beta1, float beta2, float eps, int step, int max_blocks,
-                       void *stream) {
+                       void *stream, const float *hyper = nullptr,
+                       const int32_t *skip = nullptr) {
   GS_REQUIRE(n_groups > 0 && n_groups <= adam::kMaxGroups, "adam: 1..%d groups supported",
              adam::kMaxGroups);
-  GS_REQUIRE(step >= 1, "adam: step must be >= 1");
+  GS_REQUIRE(hyper || step >= 1, "adam: step must be >= 1");
   adam::Groups g{};
   g.n = n_groups;
+  g.hyper = hyper;
+  g.skip = skip;
   g.begin[0] = 0;
-  const double bc1 = 1.0 - pow((double)beta1, step), bc2 = 1.0 - pow((double)beta2, step);
+  const int t = step >= 1 ? step : 1;
+  const double bc1 = 1.0 - pow((double)beta1, t), bc2 = 1.0 - pow((double)beta2, t);
   for (int i = 0; i < n_groups; ++i) {
     const uintptr_t al = (uintptr_t)params[i] | (uintptr_t)grads[i] | (uintptr_t)exp_avgs[i] |
                          (uintptr_t)exp_avg_sqs[i];
@@ -160,8 +171,8 @@ static int adam_launch(int n_groups, float *const *params, const float *const *g
     g.v[i] = exp_avg_sqs[i];
     g.numel[i] = numels[i];
     g.begin[i + 1] = g.begin[i] + (numels[i] + 3) / 4;
-    g.step_size[i] = (float)(lrs[i] / bc1);
-    g.inv_bc2_sqrt[i] = (float)(1.0 / sqrt(bc2));
+    g.step_size[i] = hyper ? 0.f : (float)(lrs[i] / bc1);
+    g.inv_bc2_sqrt[i] = hyper ? 0.f : (float)(1.0 / sqrt(bc2));
   }
   for (int i = n_groups; i < adam::kMaxGroups; ++i) g.begin[i + 1] = g.begin[n_groups];
   const int64_t total = g.begin[n_groups];
@@ -209,4 +220,20 @@ extern "C" int gsplat_hip_adam_step_ex(int n_groups, float *const *params,
                                        int step, void *stream) {
   return adam_launch(n_groups, params, grads, aux, modes, exp_avgs, exp_avg_sqs, numels, lrs,
                      beta1, beta2, eps, step, 0, stream);
+}
+
+// The gsplat_hip_adam_step_ex update with the step-dependent factors read on
+// the device (ABI 20, a captured training step): hyper_device[2 i] =
+// lr_i / (1 - beta1^t), hyper_device[2 i + 1] = 1 / sqrt(1 - beta2^t), which
+// the host computes as gsplat_hip_adam_step does; skip_device (may be NULL)
+// non-zero: nothing is updated (a void step).
+extern "C" int gsplat_hip_adam_step_dev(int n_groups, float *const *params,
+                                        const float *const *grads, const float *const *aux,
+                                        const int32_t *modes, float *const *exp_avgs,
+                                        float *const *exp_avg_sqs, const int64_t *numels,
+                                        const float *hyper_device, float beta1, float beta2,
+                                        float eps, const int32_t *skip_device, void *stream) {
+  GS_REQUIRE(hyper_device != nullptr, "adam_step_dev: null hyper_device");
+  return adam_launch(n_groups, params, grads, aux, modes, exp_avgs, exp_avg_sqs, numels, nullptr,
+                     beta1, beta2, eps, 0, 0, stream, hyper_device, skip_device);
 }

@@ -178,9 +178,17 @@ isect_write_kernel(int64_t G, int N, const float *__restrict__ means2d,
 // One lane per sorted isect: fill offsets for the (cam, tile) keys between
 // the previous key and this one (CUDA-style fill; Triton tile-bit layout).
 __global__ void __launch_bounds__(256)
-isect_offsets_kernel(int64_t n, const int64_t *__restrict__ isect_ids, int n_tiles_total,
-                     int n_tiles, int tile_bits, int32_t *__restrict__ offsets) {
+isect_offsets_kernel(int64_t n, const int64_t *__restrict__ n_dev,
+                     const int64_t *__restrict__ isect_ids, int n_tiles_total, int n_tiles,
+                     int tile_bits, int32_t *__restrict__ offsets) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (n_dev) {  // capacity mode: the grid covers max(capacity, tiles)
+    n = min(n, *n_dev);
+    if (n == 0) {
+      if (i < n_tiles_total) offsets[i] = 0;
+      return;
+    }
+  }
   if (i >= n) return;
   const int64_t tmask = (tile_bits >= 63) ? -1 : ((int64_t)1 << tile_bits) - 1;
   auto key_of = [&](int64_t id) -> int64_t {
@@ -233,10 +241,12 @@ isect_compact_kernel(int64_t G, const int32_t *__restrict__ tiles_per_gauss,
 
 // (2a) per-block sums of the tile counts in depth order
 __global__ void __launch_bounds__(kIsectBlock)
-isect_sorted_count_kernel(int64_t nV, const int32_t *__restrict__ Vs,
+isect_sorted_count_kernel(int64_t nV, const int64_t *__restrict__ nV_dev,
+                          const int32_t *__restrict__ Vs,
                           const int32_t *__restrict__ tiles_per_gauss,
                           int64_t *__restrict__ block_sums, int32_t *__restrict__ n_big) {
   __shared__ int64_t lds[kIsectBlock / 64 + 1];
+  if (nV_dev) nV = min(nV, *nV_dev);
   if (blockIdx.x == 0 && threadIdx.x == 0) *n_big = 0;  // big list of the emit kernel
   const int64_t s = (int64_t)blockIdx.x * kIsectBlock + threadIdx.x;
   const int cnt = (s < nV) ? tiles_per_gauss[Vs[s]] : 0;
@@ -268,8 +278,14 @@ isect_sorted_emit_kernel(int64_t nV, int N, const int32_t *__restrict__ Vs,
                          int ts, int tw, int th, int tile_bits, uint32_t key_all_ones,
                          const int64_t *__restrict__ block_prefix, uint32_t *__restrict__ tkey,
                          int32_t *__restrict__ val, BigEmit *__restrict__ big_list,
-                         int32_t *__restrict__ n_big) {
+                         int32_t *__restrict__ n_big, const int64_t *__restrict__ cap_state) {
   __shared__ int64_t lds[kIsectBlock / 64 + 1];
+  // capacity mode: cap_state = {n_isects if it fits else 0, n_visible,
+  // overflow of this call}; nothing is written past the arrays on overflow
+  if (cap_state) {
+    if (cap_state[2]) return;
+    nV = min(nV, cap_state[1]);
+  }
   const int64_t s = (int64_t)blockIdx.x * kIsectBlock + threadIdx.x;
   const int lane = threadIdx.x & 63;
   Rect rc{0, 0, 0, 0};
@@ -360,15 +376,34 @@ isect_big_emit_kernel(const BigEmit *__restrict__ big_list, const int32_t *__res
 
 // (3b) assemble the reference's 64-bit ids from the sorted (key, Gaussian)
 __global__ void __launch_bounds__(256)
-isect_sorted_finalize_kernel(int64_t n, const uint32_t *__restrict__ tkey,
+isect_sorted_finalize_kernel(int64_t n, const int64_t *__restrict__ n_dev,
+                             const uint32_t *__restrict__ tkey,
                              const int32_t *__restrict__ val, const float *__restrict__ depths,
                              int64_t *__restrict__ isect_ids, int32_t *__restrict__ flatten_ids) {
   const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (n_dev) n = min(n, *n_dev);
   if (p >= n) return;
   const int32_t i = val[p];
   const int32_t db = __float_as_int(depths[i]);
   isect_ids[p] = db < 0 ? (int64_t)db : (((int64_t)tkey[p] << 32) | (int64_t)(uint32_t)db);
   flatten_ids[p] = i;
+}
+
+// Capacity check of the sync-free isect: cap_state = {n_isects if it fits
+// in `capacity` else 0, n_visible, 1 if it did not fit, n_isects}; status[0] |= 1 on
+// overflow (sticky: the training step's state updates read it and become
+// no-ops until the host has grown the arrays and cleared it).
+__global__ void isect_capacity_kernel(const int64_t *__restrict__ totals, int64_t capacity,
+                                      int64_t *__restrict__ cap_state,
+                                      int32_t *__restrict__ status) {
+  if (threadIdx.x != 0) return;
+  const int64_t n = totals[0];
+  const bool over = n > capacity;
+  cap_state[0] = over ? 0 : n;
+  cap_state[1] = totals[1];
+  cap_state[2] = over ? 1 : 0;
+  cap_state[3] = n;
+  if (over && status) status[0] |= 1;
 }
 
 }  // namespace gs
@@ -446,12 +481,22 @@ extern "C" int gsplat_hip_radix_sort(int64_t n, int n_bits, const int64_t *keys_
   return 0;
 }
 
-extern "C" int gsplat_hip_isect_offsets(int64_t n_isects, const int64_t *isect_ids, int C,
-                                        int tile_width, int tile_height, int32_t *offsets,
-                                        void *stream) {
+extern "C" int gsplat_hip_isect_offsets(int64_t n_isects, const int64_t *n_isects_device,
+                                        const int64_t *isect_ids, int C, int tile_width,
+                                        int tile_height, int32_t *offsets, void *stream) {
   const int n_tiles = tile_width * tile_height;
   hipStream_t st = (hipStream_t)stream;
   if ((int64_t)C * n_tiles == 0) return 0;
+  if (n_isects_device) {  // capacity mode: n_isects is the arrays' capacity
+    int tile_bits = 0;
+    while ((1 << tile_bits) < n_tiles) ++tile_bits;
+    const int64_t span = std::max<int64_t>(n_isects, (int64_t)C * n_tiles);
+    hipLaunchKernelGGL(isect_offsets_kernel, dim3((unsigned)((span + 255) / 256)), dim3(256), 0,
+                       st, n_isects, n_isects_device, isect_ids, C * n_tiles, n_tiles, tile_bits,
+                       offsets);
+    GS_CHECK_LAUNCH("isect_offsets");
+    return 0;
+  }
   if (n_isects <= 0) {
     GS_HIP(hipMemsetAsync(offsets, 0, sizeof(int32_t) * (size_t)C * n_tiles, st));
     return 0;
@@ -459,7 +504,8 @@ extern "C" int gsplat_hip_isect_offsets(int64_t n_isects, const int64_t *isect_i
   int tile_bits = 0;
   while ((1 << tile_bits) < n_tiles) ++tile_bits;  // == (n_tiles - 1).bit_length()
   hipLaunchKernelGGL(isect_offsets_kernel, dim3((unsigned)((n_isects + 255) / 256)), dim3(256), 0,
-                     st, n_isects, isect_ids, C * n_tiles, n_tiles, tile_bits, offsets);
+                     st, n_isects, (const int64_t *)nullptr, isect_ids, C * n_tiles, n_tiles,
+                     tile_bits, offsets);
   GS_CHECK_LAUNCH("isect_offsets");
   return 0;
 }
@@ -504,12 +550,14 @@ extern "C" int64_t gsplat_hip_isect_sorted_workspace_bytes(int64_t n_visible, in
 
 // Sorted isects without sorting 64-bit keys: see "Depth-first sorted emission".
 // count_workspace is the gsplat_hip_isect_count workspace (scanned block sums).
-extern "C" int gsplat_hip_isect_write_sorted(
+// cnt_dev (capacity mode): the {n_isects, n_visible, overflow} state on the
+// device; n_visible / n_isects are then the capacities the grids are sized for.
+static int isect_write_sorted_impl(
     int64_t n_gaussians, int N, const float *means2d, const int32_t *radii, const float *depths,
     const int32_t *camera_ids, const int32_t *tiles_per_gauss, int tile_size, int tile_width,
     int tile_height, int tile_bits, int cam_bits, const void *count_workspace, int64_t n_visible,
-    int64_t n_isects, void *workspace, int64_t workspace_bytes, int64_t *isect_ids,
-    int32_t *flatten_ids, void *stream) {
+    int64_t n_isects, const int64_t *cnt_dev, void *workspace, int64_t workspace_bytes,
+    int64_t *isect_ids, int32_t *flatten_ids, hipStream_t st) {
   GS_REQUIRE(n_gaussians >= 0 && (camera_ids || N > 0 || n_gaussians == 0),
              "isect_write_sorted: N must be > 0 when camera_ids is null");
   GS_REQUIRE(tile_bits + cam_bits <= 32, "isect_write_sorted: tile_bits + cam_bits > 32");
@@ -519,7 +567,6 @@ extern "C" int gsplat_hip_isect_write_sorted(
   const SortedLayout L = sorted_layout(n_visible, n_isects, key_bits);
   GS_REQUIRE(workspace_bytes >= (int64_t)L.total, "isect_write_sorted: workspace %lld < %lld",
              (long long)workspace_bytes, (long long)L.total);
-  hipStream_t st = (hipStream_t)stream;
   char *ws = reinterpret_cast<char *>(workspace);
   int32_t *V = reinterpret_cast<int32_t *>(ws + L.V), *Vs = reinterpret_cast<int32_t *>(ws + L.Vs);
   uint32_t *dkey = reinterpret_cast<uint32_t *>(ws + L.dkey);
@@ -535,31 +582,83 @@ extern "C" int gsplat_hip_isect_write_sorted(
   hipLaunchKernelGGL(isect_compact_kernel, dim3((unsigned)nbG), dim3(kIsectBlock), 0, st,
                      n_gaussians, tiles_per_gauss, depths, vis_prefix, V, dkey);
   // stable depth sort of the visible Gaussians (32 key bits)
-  if (lsd_sort_pairs(dkey, V, dkeys, Vs, n_visible, 0, 32, tmp, st) == 0) Vs = V;
+  if (lsd_sort_pairs(dkey, V, dkeys, Vs, n_visible, 0, 32, tmp, st, nullptr,
+                     cnt_dev ? cnt_dev + 1 : nullptr) == 0)
+    Vs = V;
   const int64_t nbV = (n_visible + kIsectBlock - 1) / kIsectBlock;
   BigEmit *big_list = reinterpret_cast<BigEmit *>(ws + L.big);
   int32_t *n_big = reinterpret_cast<int32_t *>(ws + L.nbig);
   hipLaunchKernelGGL(isect_sorted_count_kernel, dim3((unsigned)nbV), dim3(kIsectBlock), 0, st,
-                     n_visible, Vs, tiles_per_gauss, blk, n_big);
+                     n_visible, cnt_dev ? cnt_dev + 1 : nullptr, Vs, tiles_per_gauss, blk, n_big);
   hipLaunchKernelGGL(isect_scan_blocks_kernel, dim3(1), dim3(1024), 0, st, nbV, blk, nullptr,
                      nullptr);
   const uint32_t all_ones = key_bits >= 32 ? 0xffffffffu : ((1u << key_bits) - 1u);
   hipLaunchKernelGGL(isect_sorted_emit_kernel, dim3((unsigned)nbV), dim3(kIsectBlock), 0, st,
                      n_visible, N, Vs, means2d, radii, depths, camera_ids, tile_size, tile_width,
-                     tile_height, tile_bits, all_ones, blk, tkey, val, big_list, n_big);
+                     tile_height, tile_bits, all_ones, blk, tkey, val, big_list, n_big, cnt_dev);
   hipLaunchKernelGGL(isect_big_emit_kernel, dim3(kBigBlocks), dim3(256), 0, st, big_list, n_big,
                      tile_width, all_ones, tkey, val);
   // stable (camera, tile) sort keeps the depth order inside every tile; its
   // last pass writes isect_ids / flatten_ids directly
   if (key_bits > 0) {
     const lsd::FinalOut fo{depths, isect_ids, flatten_ids};
-    lsd_sort_pairs(tkey, val, tkeys, vals, n_isects, 0, key_bits, tmp, st, &fo);
+    lsd_sort_pairs(tkey, val, tkeys, vals, n_isects, 0, key_bits, tmp, st, &fo, cnt_dev);
   } else {
     hipLaunchKernelGGL(isect_sorted_finalize_kernel, dim3((unsigned)((n_isects + 255) / 256)),
-                       dim3(256), 0, st, n_isects, tkey, val, depths, isect_ids, flatten_ids);
+                       dim3(256), 0, st, n_isects, cnt_dev, tkey, val, depths, isect_ids,
+                       flatten_ids);
   }
   GS_CHECK_LAUNCH("isect_write_sorted");
   return 0;
+}
+
+extern "C" int gsplat_hip_isect_write_sorted(
+    int64_t n_gaussians, int N, const float *means2d, const int32_t *radii, const float *depths,
+    const int32_t *camera_ids, const int32_t *tiles_per_gauss, int tile_size, int tile_width,
+    int tile_height, int tile_bits, int cam_bits, const void *count_workspace, int64_t n_visible,
+    int64_t n_isects, void *workspace, int64_t workspace_bytes, int64_t *isect_ids,
+    int32_t *flatten_ids, void *stream) {
+  return isect_write_sorted_impl(n_gaussians, N, means2d, radii, depths, camera_ids,
+                                 tiles_per_gauss, tile_size, tile_width, tile_height, tile_bits,
+                                 cam_bits, count_workspace, n_visible, n_isects, nullptr,
+                                 workspace, workspace_bytes, isect_ids, flatten_ids,
+                                 (hipStream_t)stream);
+}
+
+extern "C" int64_t gsplat_hip_isect_sorted_capped_workspace_bytes(int64_t n_gaussians,
+                                                                  int64_t capacity, int key_bits) {
+  // the visible Gaussians are at most n_gaussians; + the capacity state
+  return (int64_t)sorted_layout(n_gaussians, capacity, key_bits).total + 256;
+}
+
+// The sorted emission without a host sync: the counts stay on the device
+// (totals_device from gsplat_hip_isect_count), isect_ids / flatten_ids have
+// `capacity` slots and every grid is sized for it.  counts_device[0] receives
+// the number of isects written (0 when they did not fit: status_device[0]
+// gets bit 0 set, sticky), counts_device[1] the visible Gaussians; pass
+// counts_device to offsets / rasterize as their n_isects_device.
+extern "C" int gsplat_hip_isect_write_sorted_capped(
+    int64_t n_gaussians, int N, const float *means2d, const int32_t *radii, const float *depths,
+    const int32_t *camera_ids, const int32_t *tiles_per_gauss, int tile_size, int tile_width,
+    int tile_height, int tile_bits, int cam_bits, const void *count_workspace,
+    const int64_t *totals_device, int64_t capacity, int64_t *counts_device,
+    int32_t *status_device, void *workspace, int64_t workspace_bytes, int64_t *isect_ids,
+    int32_t *flatten_ids, void *stream) {
+  GS_REQUIRE(capacity >= 0 && capacity < ((int64_t)1 << 30),
+             "isect_write_sorted_capped: capacity %lld out of range", (long long)capacity);
+  GS_REQUIRE(counts_device && totals_device, "isect_write_sorted_capped: null count buffers");
+  const int64_t need = gsplat_hip_isect_sorted_capped_workspace_bytes(n_gaussians, capacity,
+                                                                      tile_bits + cam_bits);
+  GS_REQUIRE(workspace_bytes >= need, "isect_write_sorted_capped: workspace %lld < %lld",
+             (long long)workspace_bytes, (long long)need);
+  hipStream_t st = (hipStream_t)stream;
+  // cap_state [3] lives in the caller's counts buffer
+  hipLaunchKernelGGL(isect_capacity_kernel, dim3(1), dim3(64), 0, st, totals_device, capacity,
+                     counts_device, status_device);
+  return isect_write_sorted_impl(n_gaussians, N, means2d, radii, depths, camera_ids,
+                                 tiles_per_gauss, tile_size, tile_width, tile_height, tile_bits,
+                                 cam_bits, count_workspace, n_gaussians, capacity, counts_device,
+                                 workspace, workspace_bytes - 256, isect_ids, flatten_ids, st);
 }
 
 // -------------------------------------------------------- tile-first path --

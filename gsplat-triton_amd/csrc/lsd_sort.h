@@ -18,6 +18,9 @@
 // pass is stable and the whole sort equals a stable sort on bits
 // [begin_bit, end_bit).  Traffic per pass: 4 B/item (hist) + 16 B/item
 // (scatter read + write).
+// Device count (n_dev non-null, the sync-free isect of a captured step): the
+// grids are sized for the capacity n and every kernel reads the item count
+// min(*n_dev, n) itself; tiles past it contribute empty histograms.
 #pragma once
 #include <stdlib.h>
 
@@ -47,9 +50,10 @@ struct FinalOut {
 
 template <int IPT, int RX>
 __global__ void __launch_bounds__(NT)
-hist_kernel(const uint32_t *__restrict__ keys, int64_t n, int shift, uint32_t mask,
-            uint32_t *__restrict__ hist, int64_t nt) {
+hist_kernel(const uint32_t *__restrict__ keys, int64_t n, const int64_t *__restrict__ n_dev,
+            int shift, uint32_t mask, uint32_t *__restrict__ hist, int64_t nt) {
   __shared__ uint32_t h[RX];
+  if (n_dev) n = min(n, *n_dev);
 #pragma unroll
   for (int d = threadIdx.x; d < RX; d += NT) h[d] = 0;
   __syncthreads();
@@ -126,9 +130,10 @@ scan_kernel(uint32_t *__restrict__ hist, int64_t nt, uint32_t *__restrict__ tota
 template <int IPT, bool FINAL, int RX>
 __global__ void __launch_bounds__(NT)
 scatter_kernel(const uint32_t *__restrict__ kin, const int32_t *__restrict__ vin,
-               uint32_t *__restrict__ kout, int32_t *__restrict__ vout, int64_t n, int shift,
-               int nbits, const uint32_t *__restrict__ hist, const uint32_t *__restrict__ totals,
-               int64_t nt, FinalOut fo) {
+               uint32_t *__restrict__ kout, int32_t *__restrict__ vout, int64_t n,
+               const int64_t *__restrict__ n_dev, int shift, int nbits,
+               const uint32_t *__restrict__ hist, const uint32_t *__restrict__ totals, int64_t nt,
+               FinalOut fo) {
   constexpr int NW = NT / 64, TILE = NT * IPT, DPT = RX / NT;  // digits per thread
   __shared__ uint32_t cnt[NW][RX];
   __shared__ uint32_t gbase[RX];  // global position of tile slot 0 of digit d's range
@@ -142,7 +147,8 @@ scatter_kernel(const uint32_t *__restrict__ kin, const int32_t *__restrict__ vin
 #pragma unroll
     for (int j = 0; j < DPT; ++j) cnt[w][t * DPT + j] = 0;
   const int64_t base = (int64_t)blockIdx.x * TILE;
-  const int nvalid = (int)min<int64_t>((int64_t)TILE, n - base);
+  if (n_dev) n = min(n, *n_dev);
+  const int nvalid = (int)max<int64_t>(0, min<int64_t>((int64_t)TILE, n - base));
   uint32_t key[IPT];
   int32_t val[IPT];
 #pragma unroll
@@ -265,7 +271,7 @@ inline size_t lsd_sort_scratch_bytes(int64_t n) {
 // 11-bit digits, 3 passes for 32 bits.
 inline int lsd_sort_pairs(uint32_t *k0, int32_t *v0, uint32_t *k1, int32_t *v1, int64_t n,
                           int begin_bit, int end_bit, void *scratch, hipStream_t st,
-                          const lsd::FinalOut *fo = nullptr) {
+                          const lsd::FinalOut *fo = nullptr, const int64_t *n_dev = nullptr) {
   if (n <= 0 || end_bit <= begin_bit) return 0;
   const int ipt = lsd::pick_ipt(n);
   const int64_t nt = lsd::n_tiles(n, ipt);
@@ -288,7 +294,7 @@ inline int lsd_sort_pairs(uint32_t *k0, int32_t *v0, uint32_t *k1, int32_t *v1, 
     int32_t *vi = cur ? v1 : v0, *vo = cur ? v0 : v1;
 #define GS_LSD_HIST(I, RX)                                                                     \
   hipLaunchKernelGGL((lsd::hist_kernel<I, RX>), dim3((unsigned)nt), dim3(lsd::NT), 0, st, ki, n, \
-                     shift, mask, hist, nt)
+                     n_dev, shift, mask, hist, nt)
     if (wide) {
       if (ipt == 4) GS_LSD_HIST(4, lsd::RADIX_WIDE); else GS_LSD_HIST(16, lsd::RADIX_WIDE);
     } else {
@@ -301,7 +307,7 @@ inline int lsd_sort_pairs(uint32_t *k0, int32_t *v0, uint32_t *k1, int32_t *v1, 
     const lsd::FinalOut f = fin ? *fo : lsd::FinalOut{nullptr, nullptr, nullptr};
 #define GS_LSD_SCATTER(I, F, RX)                                                              \
   hipLaunchKernelGGL((lsd::scatter_kernel<I, F, RX>), dim3((unsigned)nt), dim3(lsd::NT), 0, st, \
-                     ki, vi, ko, vo, n, shift, nbits, hist, totals, nt, f)
+                     ki, vi, ko, vo, n, n_dev, shift, nbits, hist, totals, nt, f)
     if (wide) {
       if (ipt == 4) GS_LSD_SCATTER(4, false, lsd::RADIX_WIDE);
       else GS_LSD_SCATTER(16, false, lsd::RADIX_WIDE);

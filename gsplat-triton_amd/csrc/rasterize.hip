@@ -297,26 +297,28 @@ namespace gs {
 int rasterize16_fwd(int C, int D, int W, int H, int tw, int th, const float *means2d,
                     const float *conics, const float *colors, const float *opacities,
                     const float *backgrounds, const uint8_t *masks, const int32_t *offsets,
-                    int64_t n_isects, const int32_t *flatten_ids, float *render_colors,
-                    float *render_alphas, int32_t *last_ids, const float *records, void *state,
-                    int64_t state_bytes, hipStream_t st);
+                    int64_t n_isects, const int64_t *n_isects_dev, const int32_t *flatten_ids,
+                    float *render_colors, float *render_alphas, int32_t *last_ids,
+                    const float *records, void *state, int64_t state_bytes, hipStream_t st);
 int rasterize16_record_floats(int D);
 int rasterize16_pack_records(int64_t G, int D, const float *means2d, const float *conics,
                              const float *colors, const float *opacities, const int32_t *visible,
                              float *records, hipStream_t st);
 int64_t rasterize16_fwd_state_bytes(int D, int n_tiles, int64_t n_isects);
 int rasterize16_prepare(int D, int n_tiles, const int32_t *offsets, int64_t n_isects,
-                        void *state, int64_t state_bytes, hipStream_t st);
+                        const int64_t *n_isects_dev, void *state, int64_t state_bytes,
+                        hipStream_t st);
 int64_t rasterize16_bwd_workspace(int64_t G, int D, bool absgrad, int n_tiles, int64_t n_isects);
 int rasterize16_bwd(int C, int64_t G, int D, int W, int H, int tw, int th,
                     const float *means2d, const float *conics, const float *colors,
                     const float *opacities, const float *backgrounds, const uint8_t *masks,
-                    const int32_t *offsets, int64_t n_isects, const int32_t *flatten_ids,
-                    const float *render_alphas, const int32_t *last_ids,
-                    const float *v_render_colors, const float *v_render_alphas,
-                    float *v_means2d, float *v_conics, float *v_colors, float *v_opacities,
-                    float *v_abs, const float *render_colors, const float *records,
-                    const void *state, int64_t state_bytes, void *workspace, hipStream_t st);
+                    const int32_t *offsets, int64_t n_isects, const int64_t *n_isects_dev,
+                    const int32_t *flatten_ids, const float *render_alphas,
+                    const int32_t *last_ids, const float *v_render_colors,
+                    const float *v_render_alphas, float *v_means2d, float *v_conics,
+                    float *v_colors, float *v_opacities, float *v_abs, const float *render_colors,
+                    const float *records, const void *state, int64_t state_bytes,
+                    void *workspace, hipStream_t st);
 }  // namespace gs
 
 using namespace gs;
@@ -334,11 +336,11 @@ extern "C" int64_t gsplat_hip_rasterize_fwd_state_bytes(int C, int D, int tile_s
 
 extern "C" int gsplat_hip_rasterize_prepare(int C, int D, int tile_size, int tile_width,
                                            int tile_height, const int32_t *isect_offsets,
-                                           int64_t n_isects, void *state, int64_t state_bytes,
-                                           void *stream) {
+                                           int64_t n_isects, const int64_t *n_isects_device,
+                                           void *state, int64_t state_bytes, void *stream) {
   if (tile_size != 16 || !supported_channels(D)) return 0;
-  return rasterize16_prepare(D, C * tile_width * tile_height, isect_offsets, n_isects, state,
-                             state_bytes, (hipStream_t)stream);
+  return rasterize16_prepare(D, C * tile_width * tile_height, isect_offsets, n_isects,
+                             n_isects_device, state, state_bytes, (hipStream_t)stream);
 }
 
 extern "C" int64_t gsplat_hip_rasterize_bwd_workspace_bytes(int64_t n_gaussians, int D,
@@ -378,11 +380,14 @@ extern "C" int gsplat_hip_rasterize_fwd(int C, int D, int width, int height, int
                                         const float *conics, const float *colors,
                                         const float *opacities, const float *backgrounds,
                                         const uint8_t *masks, const int32_t *isect_offsets,
-                                        int64_t n_isects, const int32_t *flatten_ids,
-                                        float *render_colors, float *render_alphas,
-                                        int32_t *last_ids, const float *records, void *state,
-                                        int64_t state_bytes, void *stream) {
+                                        int64_t n_isects, const int64_t *n_isects_device,
+                                        const int32_t *flatten_ids, float *render_colors,
+                                        float *render_alphas, int32_t *last_ids,
+                                        const float *records, void *state, int64_t state_bytes,
+                                        void *stream) {
   if (int e = check_common(C, D, width, height, tile_size, tile_width, tile_height)) return e;
+  GS_REQUIRE(tile_size == 16 || !n_isects_device,
+             "rasterize_fwd: a device isect count needs 16x16 tiles");
   if ((int64_t)C * tile_width * tile_height == 0) return 0;
   RasterArgs a{};
   a.C = C; a.W = width; a.H = height; a.ts = tile_size; a.tw = tile_width; a.th = tile_height;
@@ -394,9 +399,9 @@ extern "C" int gsplat_hip_rasterize_fwd(int C, int D, int width, int height, int
   hipStream_t st = (hipStream_t)stream;
   if (tile_size == 16)
     return rasterize16_fwd(C, D, width, height, tile_width, tile_height, means2d, conics, colors,
-                           opacities, backgrounds, masks, isect_offsets, n_isects, flatten_ids,
-                           render_colors, render_alphas, last_ids, records, state, state_bytes,
-                           st);
+                           opacities, backgrounds, masks, isect_offsets, n_isects,
+                           n_isects_device, flatten_ids, render_colors, render_alphas, last_ids,
+                           records, state, state_bytes, st);
   const int thr = block_threads(tile_size);
   switch (D) {
     case 1: return launch_fwd<1>(a, thr, st);
@@ -415,13 +420,16 @@ extern "C" int gsplat_hip_rasterize_bwd(
     int C, int64_t n_gaussians, int D, int width, int height, int tile_size, int tile_width,
     int tile_height, const float *means2d, const float *conics, const float *colors,
     const float *opacities, const float *backgrounds, const uint8_t *masks,
-    const int32_t *isect_offsets, int64_t n_isects, const int32_t *flatten_ids,
-    const float *render_alphas, const int32_t *last_ids, const float *v_render_colors,
+    const int32_t *isect_offsets, int64_t n_isects, const int64_t *n_isects_device,
+    const int32_t *flatten_ids, const float *render_alphas, const int32_t *last_ids,
+    const float *v_render_colors,
     const float *v_render_alphas, float *v_means2d, float *v_conics, float *v_colors,
     float *v_opacities, float *v_means2d_abs, const float *render_colors, const float *records,
     const void *state, int64_t state_bytes, void *workspace, int64_t workspace_bytes,
     void *stream) {
   if (int e = check_common(C, D, width, height, tile_size, tile_width, tile_height)) return e;
+  GS_REQUIRE(tile_size == 16 || !n_isects_device,
+             "rasterize_bwd: a device isect count needs 16x16 tiles");
   hipStream_t st = (hipStream_t)stream;
   const size_t G = (size_t)n_gaussians;
   if (tile_size == 16) {
@@ -432,7 +440,8 @@ extern "C" int gsplat_hip_rasterize_bwd(
                (long long)workspace_bytes);
     return rasterize16_bwd(C, n_gaussians, D, width, height, tile_width, tile_height, means2d,
                            conics, colors, opacities, backgrounds, masks, isect_offsets,
-                           n_isects, flatten_ids, render_alphas, last_ids, v_render_colors,
+                           n_isects, n_isects_device, flatten_ids, render_alphas, last_ids,
+                           v_render_colors,
                            v_render_alphas, v_means2d, v_conics, v_colors, v_opacities,
                            v_means2d_abs, render_colors, records, state, state_bytes, workspace,
                            st);

@@ -118,7 +118,8 @@ constexpr int kRecMaxD = kRecFloats - 6;
 
 struct Args {
   int C, W, H, tw, th, n_tiles;
-  int64_t n_isects;
+  int64_t n_isects;  // isect count, or with n_dev the capacity of the isect arrays
+  const int64_t *n_dev;  // the isect count on the device (capacity mode) or null
   const float *means2d, *conics, *colors, *opacities, *backgrounds;
   const float *records;  // [G][kRecFloats] render records, or null (gather the arrays)
   const uint8_t *masks;
@@ -161,6 +162,18 @@ struct Args {
   uint64_t *timeline;  // debug: per-wave (start, end) s_memrealtime stamps or null
   unsigned long long *lanehist;  // debug: histogram of contributing lanes per (record, wave)
 };
+
+// Isect count and the end of tile t's isect range.  Capacity mode (n_dev
+// non-null, the sync-free isect of a captured training step): the arrays
+// hold n_isects slots, the count is read on the device.
+GS_INLINE int64_t isect_count(const int64_t *n_dev, int64_t n) { return n_dev ? *n_dev : n; }
+GS_INLINE int64_t tile_end(const int32_t *offsets, int t, int n_tiles, const int64_t *n_dev,
+                           int64_t n) {
+  return t == n_tiles - 1 ? isect_count(n_dev, n) : (int64_t)offsets[t + 1];
+}
+GS_INLINE int64_t tile_end(const Args &a, int t) {
+  return tile_end(a.offsets, t, a.n_tiles, a.n_dev, a.n_isects);
+}
 
 // Debug timeline (gsplat_hip_debug_set_timeline): lane 0 of every wave stores
 // its start/end stamps of the 100 MHz constant clock into its own slots.
@@ -476,7 +489,7 @@ __attribute__((amdgpu_waves_per_eu((U == 1 ? 5 : U == 2 ? 4 : 3) + (PF == 0 ? 2 
   const bool inside = geo.px < a.W && geo.py < a.H;
   const float fx = (float)geo.px + 0.5f, fy = (float)geo.py + 0.5f;
   const int64_t tstart = a.offsets[tile];
-  const int64_t tend = (tile == a.n_tiles - 1) ? a.n_isects : (int64_t)a.offsets[tile + 1];
+  const int64_t tend = tile_end(a, tile);
   const int64_t start = kc >= 0 ? tstart + (int64_t)kc * a.SL : tstart;
   const int64_t end = kc >= 0 ? min(tend, start + (int64_t)a.SL) : tend;
   const bool skip_tile = a.masks && a.masks[tile];
@@ -795,7 +808,7 @@ __global__ void __launch_bounds__(256) fwd_combine_kernel(Args a) {
   const int px = tx * kTS + (pit & 15), py = ty * kTS + (pit >> 4);
   if (px >= a.W || py >= a.H) return;
   const int64_t tstart = a.offsets[tile];
-  const int64_t tend = (tile == a.n_tiles - 1) ? a.n_isects : (int64_t)a.offsets[tile + 1];
+  const int64_t tend = tile_end(a, tile);
   const int64_t sz = kTS * kTS;
   float col[D];
 #pragma unroll
@@ -855,7 +868,7 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(3))) f
   const float ry0 = ty * kTS + 8 * w + 0.5f, ry1 = ry0 + 7.f;
   const float fx = (float)px + 0.5f;
   const int64_t start = a.offsets[tile];
-  const int64_t end = (tile == a.n_tiles - 1) ? a.n_isects : (int64_t)a.offsets[tile + 1];
+  const int64_t end = tile_end(a, tile);
   const bool skip_tile = a.masks && a.masks[tile];
 
   // per pixel k: colour of even (.x) / odd (.y) records of each pair in the
@@ -1049,7 +1062,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) b
   const int c = geo.c;
   if (a.masks && a.masks[tile]) return;
   const int64_t tstart = a.offsets[tile];
-  const int64_t tend = (tile == a.n_tiles - 1) ? a.n_isects : (int64_t)a.offsets[tile + 1];
+  const int64_t tend = tile_end(a, tile);
   const int64_t start = a.items ? tstart + (int64_t)k * a.L : tstart;
   const int64_t cend = a.items ? min(tend, start + a.L) : tend;
 
@@ -1266,7 +1279,7 @@ __attribute__((amdgpu_waves_per_eu(BwdOcc<PX>::W))) bwd2_kernel(Args a) {
   const float ry0 = ty * kTS + 4 * PX * w + 0.5f, ry1 = ry0 + (4 * PX - 1);
   if (a.masks && a.masks[tile]) return;
   const int64_t tstart = a.offsets[tile];
-  const int64_t tend = (tile == a.n_tiles - 1) ? a.n_isects : (int64_t)a.offsets[tile + 1];
+  const int64_t tend = tile_end(a, tile);
   const int64_t start = a.items ? tstart + (int64_t)k * a.L : tstart;
   const int64_t cend = a.items ? min(tend, start + a.L) : tend;
 
@@ -1496,7 +1509,8 @@ GS_INLINE void block_max_out(int64_t v, int32_t *out) {
 // thread are packed into one u64 (16 bits each) for a single block scan.
 __global__ void __launch_bounds__(1024)
 tile_order_kernel(int n_tiles, const int32_t *__restrict__ offsets, int64_t n_isects,
-                  int32_t *__restrict__ order, int32_t *__restrict__ max_out) {
+                  const int64_t *__restrict__ n_dev, int32_t *__restrict__ order,
+                  int32_t *__restrict__ max_out) {
   constexpr int MAXPER = 16;  // tiles per thread (n_tiles <= 16384)
   __shared__ uint64_t wsum[16];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -1508,7 +1522,7 @@ tile_order_kernel(int n_tiles, const int32_t *__restrict__ offsets, int64_t n_is
     const int t = tid + 1024 * i;
     bucket[i] = -1;
     if (t < n_tiles) {
-      const int64_t e = (t == n_tiles - 1) ? n_isects : (int64_t)offsets[t + 1];
+      const int64_t e = tile_end(offsets, t, n_tiles, n_dev, n_isects);
       const int64_t n = e - offsets[t];
       nmax = max(nmax, n);
       bucket[i] = n >= 2048 ? 0 : n >= 1024 ? 1 : n >= 512 ? 2 : 3;
@@ -1568,12 +1582,13 @@ constexpr int kTileCost = 32;
 
 __global__ void __launch_bounds__(1024)
 order_xcd_kernel(int n_tiles, const int32_t *__restrict__ offsets, int64_t n_isects,
-                 int32_t *__restrict__ order, int32_t *__restrict__ queue) {
+                 const int64_t *__restrict__ n_dev, int32_t *__restrict__ order,
+                 int32_t *__restrict__ queue) {
   constexpr int PER = 16;
   __shared__ uint64_t wsum[16][8];
   __shared__ int base[32];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int64_t W = n_isects + (int64_t)kTileCost * n_tiles;
+  const int64_t W = isect_count(n_dev, n_isects) + (int64_t)kTileCost * n_tiles;
   int key[PER];
   uint64_t c[8];
 #pragma unroll
@@ -1584,7 +1599,7 @@ order_xcd_kernel(int n_tiles, const int32_t *__restrict__ offsets, int64_t n_ise
     key[i] = -1;
     if (t < n_tiles) {
       const int64_t o = offsets[t];
-      const int64_t e = (t == n_tiles - 1) ? n_isects : (int64_t)offsets[t + 1];
+      const int64_t e = tile_end(offsets, t, n_tiles, n_dev, n_isects);
       const int64_t n = e - o;
       const int seg = (int)min((int64_t)7, (8 * (o + (int64_t)kTileCost * t)) / max(W, (int64_t)1));
       const int bk = n >= 2048 ? 0 : n >= 1024 ? 1 : n >= 512 ? 2 : 3;
@@ -1662,7 +1677,7 @@ order_xcd_kernel(int n_tiles, const int32_t *__restrict__ offsets, int64_t n_ise
 // workgroup, 16 tiles per lane (n_tiles <= 16384).
 __global__ void __launch_bounds__(1024)
 fwd_plan_kernel(int n_tiles, const int32_t *__restrict__ offsets, int64_t n_isects,
-                const uint8_t *__restrict__ masks, int SL, int split, int32_t *__restrict__ hdr,
+                const int64_t *__restrict__ n_dev, const uint8_t *__restrict__ masks, int SL, int split, int32_t *__restrict__ hdr,
                 int2 *__restrict__ fitems, int2 *__restrict__ p1items,
                 int2 *__restrict__ heavy, int32_t *__restrict__ max_out) {
   // quantities: [0] unsplit >= 2048, [1] chunks, [2] unsplit >= 1024,
@@ -1673,7 +1688,7 @@ fwd_plan_kernel(int n_tiles, const int32_t *__restrict__ offsets, int64_t n_isec
   // category and chunk count of tile t (recomputed in the write pass: keeps
   // the 16 tiles' state out of registers)
   auto classify = [&](int t, int &nch) -> int {
-    const int64_t e = (t == n_tiles - 1) ? n_isects : (int64_t)offsets[t + 1];
+    const int64_t e = tile_end(offsets, t, n_tiles, n_dev, n_isects);
     const int64_t n = e - offsets[t];
     nch = 0;
     if (n > split && !(masks && masks[t])) {
@@ -1689,7 +1704,7 @@ fwd_plan_kernel(int n_tiles, const int32_t *__restrict__ offsets, int64_t n_isec
     if (t >= n_tiles) break;
     int nch;
     const int kd = classify(t, nch);
-    const int64_t e = (t == n_tiles - 1) ? n_isects : (int64_t)offsets[t + 1];
+    const int64_t e = tile_end(offsets, t, n_tiles, n_dev, n_isects);
     nmax = max(nmax, e - offsets[t]);
 #pragma unroll
     for (int q = 0; q < NQ; ++q)
@@ -1767,14 +1782,15 @@ fwd_plan_kernel(int n_tiles, const int32_t *__restrict__ offsets, int64_t n_isec
 // first).  One lane per tile; one atomic per wave and list on the counters
 // n_items[0..1], which the packed-gradient memset has zeroed.
 __global__ void __launch_bounds__(256)
-chunk_items_kernel(int n_tiles, const int32_t *__restrict__ offsets, int64_t n_isects, int L,
+chunk_items_kernel(int n_tiles, const int32_t *__restrict__ offsets, int64_t n_isects,
+                   const int64_t *__restrict__ n_dev, int L,
                    int2 *__restrict__ full, int2 *__restrict__ tail,
                    int32_t *__restrict__ n_items) {
   const int t = blockIdx.x * 256 + threadIdx.x;
   const int lane = threadIdx.x & 63;
   int nf = 0, nt = 0;
   if (t < n_tiles) {
-    const int64_t e = (t == n_tiles - 1) ? n_isects : (int64_t)offsets[t + 1];
+    const int64_t e = tile_end(offsets, t, n_tiles, n_dev, n_isects);
     const int64_t n = e - offsets[t];
     nf = (int)(n / L);
     nt = (n % L) != 0;
@@ -2088,12 +2104,13 @@ static int dbg_flags() {
 static thread_local const void *g_prepared_state = nullptr;
 static thread_local bool g_prepared_split = false;  // the split decision of that preparation
 
-static void launch_order(int n_tiles, const int32_t *offsets, int64_t n_isects, int32_t *order,
-                         hipStream_t st, char *split_base = nullptr, int D = 0) {
+static void launch_order(int n_tiles, const int32_t *offsets, int64_t n_isects,
+                         const int64_t *n_dev, int32_t *order, hipStream_t st,
+                         char *split_base = nullptr, int D = 0) {
   if (split_base) {
     const SplitLayout l = split_layout(D, n_tiles, n_isects);
     hipLaunchKernelGGL(r16::fwd_plan_kernel, dim3(1), dim3(1024), 0, st, n_tiles, offsets,
-                       n_isects, (const uint8_t *)nullptr, split_chunk(),
+                       n_isects, n_dev, (const uint8_t *)nullptr, split_chunk(),
                        (int)std::min<int64_t>(split_threshold(n_isects), INT32_MAX),
                        reinterpret_cast<int32_t *>(split_base + l.hdr),
                        reinterpret_cast<int2 *>(split_base + l.fitems),
@@ -2101,17 +2118,18 @@ static void launch_order(int n_tiles, const int32_t *offsets, int64_t n_isects, 
                        reinterpret_cast<int2 *>(split_base + l.heavy), stat_dev());
   } else if (use_xcd())
     hipLaunchKernelGGL(r16::order_xcd_kernel, dim3(1), dim3(1024), 0, st, n_tiles, offsets,
-                       n_isects, order, order + n_tiles);
+                       n_isects, n_dev, order, order + n_tiles);
   else
     hipLaunchKernelGGL(r16::tile_order_kernel, dim3(1), dim3(1024), 0, st, n_tiles, offsets,
-                       n_isects, order, split_capable(n_tiles, n_isects) ? stat_dev() : nullptr);
+                       n_isects, n_dev, order,
+                       split_capable(n_tiles, n_isects) ? stat_dev() : nullptr);
 }
 
 template <int D>
 int r16_fwd(r16::Args a, const void *state, char *split_base, hipStream_t st) {
   if (a.order && state != g_prepared_state)
-    launch_order(a.n_tiles, a.offsets, a.n_isects, const_cast<int32_t *>(a.order), st, split_base,
-                 D);
+    launch_order(a.n_tiles, a.offsets, a.n_isects, a.n_dev, const_cast<int32_t *>(a.order), st,
+                 split_base, D);
   g_prepared_state = nullptr;
   if (split_base) {
     // split heavy tiles: chunk products, every work item (tiles and chunks),
@@ -2180,7 +2198,7 @@ int r16_bwd(r16::Args a, int64_t G, float *v_means2d, float *v_conics, float *v_
       a.items = reinterpret_cast<int2 *>(w + 256);
       a.items_tail = a.items + (a.n_isects / a.L + 1);
       hipLaunchKernelGGL(r16::chunk_items_kernel, dim3((unsigned)((a.n_tiles + 255) / 256)),
-                         dim3(256), 0, st, a.n_tiles, a.offsets, a.n_isects, a.L,
+                         dim3(256), 0, st, a.n_tiles, a.offsets, a.n_isects, a.n_dev, a.L,
                          const_cast<int2 *>(a.items), const_cast<int2 *>(a.items_tail),
                          const_cast<int32_t *>(a.n_items));
       grid = n_items_bound(a.n_tiles, a.n_isects);
@@ -2214,10 +2232,11 @@ int r16_bwd(r16::Args a, int64_t G, float *v_means2d, float *v_conics, float *v_
 int rasterize16_fwd(int C, int D, int W, int H, int tw, int th, const float *means2d,
                     const float *conics, const float *colors, const float *opacities,
                     const float *backgrounds, const uint8_t *masks, const int32_t *offsets,
-                    int64_t n_isects, const int32_t *flatten_ids, float *render_colors,
-                    float *render_alphas, int32_t *last_ids, const float *records, void *state,
-                    int64_t state_bytes, hipStream_t st) {
+                    int64_t n_isects, const int64_t *n_isects_dev, const int32_t *flatten_ids,
+                    float *render_colors, float *render_alphas, int32_t *last_ids,
+                    const float *records, void *state, int64_t state_bytes, hipStream_t st) {
   r16::Args a{};
+  a.n_dev = n_isects_dev;
   a.records = rasterize16_record_floats(D) ? records : nullptr;
   a.C = C; a.W = W; a.H = H; a.tw = tw; a.th = th; a.n_tiles = C * tw * th;
   a.n_isects = n_isects;
@@ -2265,7 +2284,8 @@ int rasterize16_fwd(int C, int D, int W, int H, int tw, int th, const float *mea
 }
 
 int rasterize16_prepare(int D, int n_tiles, const int32_t *offsets, int64_t n_isects,
-                        void *state, int64_t state_bytes, hipStream_t st) {
+                        const int64_t *n_isects_dev, void *state, int64_t state_bytes,
+                        hipStream_t st) {
   g_prepared_state = nullptr;
   if (!state || !use_order(n_tiles, n_isects)) return 0;
   GS_REQUIRE(state_bytes >= rasterize16_fwd_state_bytes(D, n_tiles, n_isects),
@@ -2273,7 +2293,7 @@ int rasterize16_prepare(int D, int n_tiles, const int32_t *offsets, int64_t n_is
   char *base = reinterpret_cast<char *>(state) + chunk_slot_bytes(D, n_isects);
   int32_t *order = reinterpret_cast<int32_t *>(base);
   const bool split = chunk_slot_bytes(D, n_isects) > 0 && use_split_now(n_tiles, n_isects);
-  launch_order(n_tiles, offsets, n_isects, order, st,
+  launch_order(n_tiles, offsets, n_isects, n_isects_dev, order, st,
                split ? base + order_bytes(n_tiles, n_isects) : nullptr, D);
   GS_CHECK_LAUNCH("rasterize_prepare");
   g_prepared_state = state;
@@ -2290,13 +2310,15 @@ int64_t rasterize16_bwd_workspace(int64_t G, int D, bool absgrad, int n_tiles, i
 int rasterize16_bwd(int C, int64_t G, int D, int W, int H, int tw, int th,
                     const float *means2d, const float *conics, const float *colors,
                     const float *opacities, const float *backgrounds, const uint8_t *masks,
-                    const int32_t *offsets, int64_t n_isects, const int32_t *flatten_ids,
-                    const float *render_alphas, const int32_t *last_ids,
-                    const float *v_render_colors, const float *v_render_alphas,
-                    float *v_means2d, float *v_conics, float *v_colors, float *v_opacities,
-                    float *v_abs, const float *render_colors, const float *records,
-                    const void *state, int64_t state_bytes, void *workspace, hipStream_t st) {
+                    const int32_t *offsets, int64_t n_isects, const int64_t *n_isects_dev,
+                    const int32_t *flatten_ids, const float *render_alphas,
+                    const int32_t *last_ids, const float *v_render_colors,
+                    const float *v_render_alphas, float *v_means2d, float *v_conics,
+                    float *v_colors, float *v_opacities, float *v_abs, const float *render_colors,
+                    const float *records, const void *state, int64_t state_bytes,
+                    void *workspace, hipStream_t st) {
   r16::Args a{};
+  a.n_dev = n_isects_dev;
   a.records = rasterize16_record_floats(D) ? records : nullptr;
   a.C = C; a.W = W; a.H = H; a.tw = tw; a.th = th; a.n_tiles = C * tw * th;
   a.n_isects = n_isects;

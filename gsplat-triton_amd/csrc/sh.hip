@@ -294,6 +294,10 @@ struct RowWalk {
 struct AdamSH {
   float *m0, *v0, *mr, *vr;  // moments of coeffs / coeffs_rest, same layout
   float ss0, ssr, ib, b1, b2, eps;
+  // captured-step form (gsplat_hip_sh_colors_bwd_adam_dev): {ss0, ssr, ib}
+  // read on the device, and a void step (*skip != 0) leaves the state alone
+  const float *hyper;
+  const int32_t *skip;
 };
 
 // Adam over `rows` consecutive rows of WID floats (16-B aligned start): the
@@ -422,11 +426,18 @@ sh_bwd_staged_kernel(int64_t n, Coeffs cf, const float *__restrict__ dirs,
   }
   __builtin_amdgcn_wave_barrier();
   if (ADAM) {  // Adam on the wave's 64 coefficient rows: 16-B vectors, lane-contiguous
-    adam_rows<3, 3>(const_cast<float *>(cf.c0) + i0 * 3, ad.m0 + i0 * 3, ad.v0 + i0 * 3, sd,
-                    rows, lane, ad.ss0, ad);
+    if (ad.skip && *ad.skip) return;
+    AdamSH a = ad;
+    if (ad.hyper) {
+      a.ss0 = ad.hyper[0];
+      a.ssr = ad.hyper[1];
+      a.ib = ad.hyper[2];
+    }
+    adam_rows<3, 3>(const_cast<float *>(cf.c0) + i0 * 3, a.m0 + i0 * 3, a.v0 + i0 * 3, sd,
+                    rows, lane, a.ss0, a);
     if (WR > 0)
-      adam_rows<(WR > 0 ? WR : 1), RSR>(const_cast<float *>(cf.cr) + i0 * WR, ad.mr + i0 * WR,
-                                         ad.vr + i0 * WR, sr, rows, lane, ad.ssr, ad);
+      adam_rows<(WR > 0 ? WR : 1), RSR>(const_cast<float *>(cf.cr) + i0 * WR, a.mr + i0 * WR,
+                                         a.vr + i0 * WR, sr, rows, lane, a.ssr, a);
     return;
   }
   {  // gradient rows out, lane-contiguous
@@ -575,6 +586,11 @@ extern "C" int gsplat_hip_sh_colors_bwd(int degree, int C, int64_t N, int64_t n_
 // coeffs_rest are updated in place with torch.optim.Adam (lr0 / lr_rest,
 // shared betas / eps, 1-based step) from the gradient this backward computes,
 // which is never stored; v_dirs as in gsplat_hip_sh_colors_bwd.
+static int sh_colors_bwd_adam_launch(int degree, int64_t N, const float *means,
+                                     const float *viewmats, float *coeffs, float *coeffs_rest,
+                                     const int32_t *radii, const float *v_colors, float *v_dirs,
+                                     const AdamSH &ad, hipStream_t st);
+
 extern "C" int gsplat_hip_sh_colors_bwd_adam(int degree, int64_t N, const float *means,
                                              const float *viewmats, float *coeffs,
                                              float *coeffs_rest, const int32_t *radii,
@@ -592,12 +608,43 @@ extern "C" int gsplat_hip_sh_colors_bwd_adam(int degree, int64_t N, const float 
              "sh_colors_bwd_adam: coefficient and moment buffers must be 16-B aligned");
   const double bc1 = 1.0 - pow((double)beta1, step), bc2 = 1.0 - pow((double)beta2, step);
   AdamSH ad{m0, v0, m_rest, v_rest, (float)(lr0 / bc1), (float)(lr_rest / bc1),
-            (float)(1.0 / sqrt(bc2)), beta1, beta2, eps};
+            (float)(1.0 / sqrt(bc2)), beta1, beta2, eps, nullptr, nullptr};
+  return sh_colors_bwd_adam_launch(degree, N, means, viewmats, coeffs, coeffs_rest, radii,
+                                   v_colors, v_dirs, ad, (hipStream_t)stream);
+}
+
+// The same with the step-dependent factors read on the device (ABI 20, a
+// captured training step): hyper_device = {lr0 / (1 - beta1^t),
+// lr_rest / (1 - beta1^t), 1 / sqrt(1 - beta2^t)}; skip_device (may be NULL)
+// non-zero: the coefficients and moments are left alone (v_dirs is written).
+extern "C" int gsplat_hip_sh_colors_bwd_adam_dev(int degree, int64_t N, const float *means,
+                                                 const float *viewmats, float *coeffs,
+                                                 float *coeffs_rest, const int32_t *radii,
+                                                 const float *v_colors, float *v_dirs, float *m0,
+                                                 float *v0, float *m_rest, float *v_rest,
+                                                 const float *hyper_device, float beta1,
+                                                 float beta2, float eps,
+                                                 const int32_t *skip_device, void *stream) {
+  if (N <= 0) return 0;
+  GS_REQUIRE(degree >= 0 && degree <= 3, "sh_colors_bwd_adam: degree %d not in [0, 3]", degree);
+  GS_REQUIRE(coeffs && coeffs_rest && m0 && v0 && m_rest && v_rest && hyper_device,
+             "sh_colors_bwd_adam: null coefficient, moment or hyper buffer");
+  GS_REQUIRE((((uintptr_t)coeffs | (uintptr_t)coeffs_rest | (uintptr_t)m0 | (uintptr_t)v0 |
+               (uintptr_t)m_rest | (uintptr_t)v_rest) & 15) == 0,
+             "sh_colors_bwd_adam: coefficient and moment buffers must be 16-B aligned");
+  AdamSH ad{m0, v0, m_rest, v_rest, 0.f, 0.f, 0.f, beta1, beta2, eps, hyper_device, skip_device};
+  return sh_colors_bwd_adam_launch(degree, N, means, viewmats, coeffs, coeffs_rest, radii,
+                                   v_colors, v_dirs, ad, (hipStream_t)stream);
+}
+
+static int sh_colors_bwd_adam_launch(int degree, int64_t N, const float *means,
+                                     const float *viewmats, float *coeffs, float *coeffs_rest,
+                                     const int32_t *radii, const float *v_colors, float *v_dirs,
+                                     const AdamSH &ad, hipStream_t st) {
   Coeffs cf{coeffs, coeffs_rest, 3, 45};
   VCoeffs vc{nullptr, nullptr, 3, 45};
   const Fused fz{means, viewmats, radii, N};
   dim3 grid((unsigned)((N + 255) / 256));
-  hipStream_t st = (hipStream_t)stream;
 #define GS_SH_BWD_ADAM(D)                                                                      \
   case D:                                                                                      \
     hipLaunchKernelGGL((sh_bwd_staged_kernel<D, true, 15, true>), grid, dim3(256), 0, st, N, cf, \

@@ -27,9 +27,10 @@ namespace strat {
 __global__ void __launch_bounds__(256)
 update_state_kernel(int C, int64_t N, const float *__restrict__ g2d,
                     const int32_t *__restrict__ radii, float sx, float sy,
-                    float *__restrict__ grad2d, float *__restrict__ count) {
+                    float *__restrict__ grad2d, float *__restrict__ count,
+                    const int32_t *__restrict__ skip) {
   const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (g >= N) return;
+  if (g >= N || (skip && *skip)) return;
   float acc = grad2d[g], cnt = count[g];
   bool any = false;
   for (int c = 0; c < C; ++c) {
@@ -292,12 +293,13 @@ using namespace gs;
 
 extern "C" int gsplat_hip_update_state(int C, int64_t N, const float *means2d_grad,
                                        const int32_t *radii, float scale_x, float scale_y,
-                                       float *grad2d, float *count, void *stream) {
+                                       float *grad2d, float *count, const int32_t *skip_device,
+                                       void *stream) {
   GS_REQUIRE(C >= 0 && N >= 0, "update_state: bad sizes C=%d N=%lld", C, (long long)N);
   if (N == 0 || C == 0) return 0;
   hipLaunchKernelGGL(strat::update_state_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0,
                      (hipStream_t)stream, C, N, means2d_grad, radii, scale_x, scale_y, grad2d,
-                     count);
+                     count, skip_device);
   GS_CHECK_LAUNCH("update_state");
   return 0;
 }

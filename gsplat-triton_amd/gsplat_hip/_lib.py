@@ -12,7 +12,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GSPLAT_HIP_LIB", os.path.join(_HERE, "libgsplat_hip.so"))
-ABI_VERSION = 19
+ABI_VERSION = 20
 
 _p = ctypes.c_void_p
 _i32 = ctypes.c_int
@@ -40,23 +40,28 @@ _SIGS = {
     "gsplat_hip_isect_write_sorted": (_i32, [_i64, _i32, _p, _p, _p, _p, _p, _i32, _i32, _i32,
                                              _i32, _i32, _p, _i64, _i64, _p, _i64, _p, _p, _p]),
     "gsplat_hip_isect_tilefirst_workspace_bytes": (_i64, [_i64, _i32, _i32]),
+    "gsplat_hip_isect_sorted_capped_workspace_bytes": (_i64, [_i64, _i64, _i32]),
+    "gsplat_hip_isect_write_sorted_capped": (_i32, [_i64, _i32, _p, _p, _p, _p, _p, _i32, _i32,
+                                                    _i32, _i32, _i32, _p, _p, _i64, _p, _p, _p,
+                                                    _i64, _p, _p, _p]),
     "gsplat_hip_isect_write_tilefirst": (_i32, [_i64, _i32, _p, _p, _p, _p, _i32, _i32, _i32,
                                                 _i32, _i32, _i32, _p, _i64, _p, _i64, _p, _p,
                                                 _p]),
     "gsplat_hip_sort_workspace_bytes": (_i64, [_i64]),
     "gsplat_hip_radix_sort": (_i32, [_i64, _i32, _p, _p, _p, _p, _p, _i64, _p]),
-    "gsplat_hip_isect_offsets": (_i32, [_i64, _p, _i32, _i32, _i32, _p, _p]),
+    "gsplat_hip_isect_offsets": (_i32, [_i64, _p, _p, _i32, _i32, _i32, _p, _p]),
     "gsplat_hip_rasterize_supported_channels": (_i32, [_i32]),
     "gsplat_hip_rasterize_fwd_state_bytes": (_i64, [_i32, _i32, _i32, _i32, _i32, _i64]),
-    "gsplat_hip_rasterize_prepare": (_i32, [_i32, _i32, _i32, _i32, _i32, _p, _i64, _p, _i64, _p]),
+    "gsplat_hip_rasterize_prepare": (_i32, [_i32, _i32, _i32, _i32, _i32, _p, _i64, _p, _p, _i64,
+                                            _p]),
     "gsplat_hip_rasterize_record_floats": (_i32, [_i32, _i32]),
     "gsplat_hip_rasterize_pack_records": (_i32, [_i64, _i32, _p, _p, _p, _p, _p, _p, _p]),
     "gsplat_hip_rasterize_fwd": (_i32, [_i32, _i32, _i32, _i32, _i32, _i32, _i32, _p, _p, _p, _p,
-                                        _p, _p, _p, _i64, _p, _p, _p, _p, _p, _p, _i64, _p]),
+                                        _p, _p, _p, _i64, _p, _p, _p, _p, _p, _p, _p, _i64, _p]),
     "gsplat_hip_rasterize_bwd_workspace_bytes": (_i64, [_i64, _i32, _i32, _i32, _i32, _i32, _i32,
                                                         _i64]),
     "gsplat_hip_rasterize_bwd": (_i32, [_i32, _i64, _i32, _i32, _i32, _i32, _i32, _i32, _p, _p,
-                                        _p, _p, _p, _p, _p, _i64, _p, _p, _p, _p, _p, _p, _p,
+                                        _p, _p, _p, _p, _p, _i64, _p, _p, _p, _p, _p, _p, _p, _p,
                                         _p, _p, _p, _p, _p, _p, _i64, _p, _i64, _p]),
     "gsplat_hip_debug_set_timeline": (_i32, [_p, _i64]),
     "gsplat_hip_debug_set_lane_histogram": (_i32, [_p]),
@@ -70,12 +75,15 @@ _SIGS = {
     "gsplat_hip_l1_ssim_loss_fused_workspace_bytes": (_i64, [_i32, _i32, _i32, _i32]),
     "gsplat_hip_l1_ssim_loss_fused_fwd": (_i32, [_i32, _i32, _i32, _i32, _p, _p, _f, _p, _p, _p, _p]),
     "gsplat_hip_l1_ssim_loss_fused_bwd": (_i32, [_i64, _p, _p, _p, _p]),
-    "gsplat_hip_update_state": (_i32, [_i32, _i64, _p, _p, _f, _f, _p, _p, _p]),
+    "gsplat_hip_update_state": (_i32, [_i32, _i64, _p, _p, _f, _f, _p, _p, _p, _p]),
     "gsplat_hip_activate_fwd": (_i32, [_i64, _i64, _p, _p, _p, _p, _p]),
     "gsplat_hip_activate_bwd": (_i32, [_i64, _i64, _p, _p, _p, _p, _p, _p, _p]),
     "gsplat_hip_adam_step": (_i32, [_i32, _p, _p, _p, _p, _p, _p, _f, _f, _f, _i32, _p]),
     "gsplat_hip_sh_colors_bwd_adam": (_i32, [_i32, _i64, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p,
                                              _p, _f, _f, _f, _f, _f, _i32, _p]),
+    "gsplat_hip_sh_colors_bwd_adam_dev": (_i32, [_i32, _i64, _p, _p, _p, _p, _p, _p, _p, _p, _p,
+                                                 _p, _p, _p, _f, _f, _f, _p, _p]),
+    "gsplat_hip_adam_step_dev": (_i32, [_i32, _p, _p, _p, _p, _p, _p, _p, _p, _f, _f, _f, _p, _p]),
     "gsplat_hip_adam_step_ex": (_i32, [_i32, _p, _p, _p, _p, _p, _p, _p, _p, _f, _f, _f, _i32, _p]),
     "gsplat_hip_adam_step_bounded": (_i32, [_i32, _p, _p, _p, _p, _p, _p, _f, _f, _f, _i32, _i32,
                                             _p]),

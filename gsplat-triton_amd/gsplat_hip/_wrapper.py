@@ -330,9 +330,12 @@ def isect_tiles(
 
 
 def isect_tiles_begin(means2d, radii, depths, tile_size, tile_width, tile_height,
-                      packed=False, n_cameras=None, camera_ids=None, gaussian_ids=None):
+                      packed=False, n_cameras=None, camera_ids=None, gaussian_ids=None,
+                      sync=True):
     """First half of isect_tiles (counts queued, totals on their way to the
-    host); `.finish(sort)` returns isect_tiles' outputs."""
+    host); `.finish(sort)` returns isect_tiles' outputs.  sync=False: the
+    totals stay on the device and `.finish_capped(capacity)` emits into
+    fixed-size arrays without any host synchronisation."""
     dev = means2d.device
     if packed:
         nnz = means2d.size(0)
@@ -360,7 +363,7 @@ def isect_tiles_begin(means2d, radii, depths, tile_size, tile_width, tile_height
     assert n_bit_tile + n_bit_cam <= 32, "tile_id and cam_id exceed 32 bits"
 
     return _IsectCount(means2d, radii, depths, camera_ids, C, N, G, tile_size, tile_width,
-                       tile_height, n_bit_tile, n_bit_cam, packed)
+                       tile_height, n_bit_tile, n_bit_cam, packed, sync)
 
 
 class _IsectCount:
@@ -371,7 +374,7 @@ class _IsectCount:
     SH colours) keeps the GPU busy across the host round trip."""
 
     def __init__(self, means2d, radii, depths, camera_ids, C, N, G, tile_size, tile_width,
-                 tile_height, n_bit_tile, n_bit_cam, packed):
+                 tile_height, n_bit_tile, n_bit_cam, packed, sync=True):
         dev = means2d.device
         self.args = (means2d, radii, depths, camera_ids, C, N, G, tile_size, tile_width,
                      tile_height, n_bit_tile, n_bit_cam, packed)
@@ -382,6 +385,10 @@ class _IsectCount:
         _lib.call("gsplat_hip_isect_count", G, _ptr(means2d), _ptr(radii), tile_size,
                   tile_width, tile_height, _ptr(self.tpg), _ptr(self.ws), _ptr(totals),
                   _stream())
+        self.totals = totals
+        if not sync:
+            self.host = self.event = None
+            return
         # a pinned buffer of its own per call (torch's caching host allocator
         # recycles it only after the copy's event): concurrent begins on other
         # streams or threads cannot overwrite each other's totals
@@ -446,16 +453,49 @@ class _IsectCount:
             tpg = tpg.view(C, N)
         return tpg, isect_ids, flatten_ids
 
+    @torch.no_grad()
+    def finish_capped(self, capacity: int, status: Optional[Tensor] = None):
+        """The sorted isects with NO host synchronisation (the one sync of
+        isect_tiles, isect_tiles.py:101-102, removed so that a training step
+        can be captured into a HIP graph): isect_ids / flatten_ids have
+        `capacity` slots, of which counts[0] (device i64) are written --
+        the same isects as finish(sort=True) -- or none if they do not fit
+        (counts[2] = 1; status[0] |= 1, sticky, when given); counts[1] = the
+        visible Gaussians, counts[3] = n_isects whether it fit or not.  Returns
+        (tiles_per_gauss, isect_ids, flatten_ids, counts)."""
+        (means2d, radii, depths, camera_ids, C, N, G, tile_size, tile_width, tile_height,
+         n_bit_tile, n_bit_cam, packed) = self.args
+        dev = means2d.device
+        capacity = int(capacity)
+        key_bits = n_bit_tile + n_bit_cam
+        ws = torch.empty(max(int(_lib.query("gsplat_hip_isect_sorted_capped_workspace_bytes", G,
+                                            capacity, key_bits)), 8),
+                         dtype=torch.uint8, device=dev)
+        isect_ids = torch.empty(capacity, dtype=torch.int64, device=dev)
+        flatten_ids = torch.empty(capacity, dtype=torch.int32, device=dev)
+        counts = torch.zeros(4, dtype=torch.int64, device=dev)
+        if status is not None:
+            assert status.dtype == torch.int32 and status.is_cuda
+        _lib.call("gsplat_hip_isect_write_sorted_capped", G, N, _ptr(means2d), _ptr(radii),
+                  _ptr(depths), _ptr(camera_ids), _ptr(self.tpg), tile_size, tile_width,
+                  tile_height, n_bit_tile, n_bit_cam, _ptr(self.ws), _ptr(self.totals), capacity,
+                  _ptr(counts), _ptr(status), _ptr(ws), ws.numel(), _ptr(isect_ids),
+                  _ptr(flatten_ids), _stream())
+        tpg = self.tpg if packed else self.tpg.view(C, N)
+        return tpg, isect_ids, flatten_ids, counts
+
 
 @torch.no_grad()
-def isect_offset_encode(isect_ids: Tensor, C: int, tile_width: int, tile_height: int) -> Tensor:
+def isect_offset_encode(isect_ids: Tensor, C: int, tile_width: int, tile_height: int,
+                        _n_isects_device: Optional[Tensor] = None) -> Tensor:
     """First sorted isect index of every tile, i32 [C, tile_height, tile_width]
-    (isect_offset.py:8-33)."""
+    (isect_offset.py:8-33).  `_n_isects_device` (private): the count on the
+    device when isect_ids is a capacity-sized array (finish_capped)."""
     _dev_check(isect_ids)
     isect_ids = isect_ids.contiguous()
     offsets = torch.empty((C, tile_height, tile_width), dtype=torch.int32, device=isect_ids.device)
-    _lib.call("gsplat_hip_isect_offsets", isect_ids.numel(), _ptr(isect_ids), C, tile_width,
-              tile_height, _ptr(offsets), _stream())
+    _lib.call("gsplat_hip_isect_offsets", isect_ids.numel(), _ptr(_n_isects_device),
+              _ptr(isect_ids), C, tile_width, tile_height, _ptr(offsets), _stream())
     return offsets
 
 
@@ -592,10 +632,14 @@ class ShAdamInBackward:
     `applied` tells the caller whether it ran (else: take the normal step)."""
 
     def __init__(self, coeffs, coeffs_rest, m0, v0, m_rest, v_rest, lr0, lr_rest, betas, eps,
-                 step):
+                 step, hyper=None, skip=None):
         self.coeffs, self.coeffs_rest = coeffs, coeffs_rest
         self.moments = (m0, v0, m_rest, v_rest)
         self.lr0, self.lr_rest, self.betas, self.eps, self.step = lr0, lr_rest, betas, eps, step
+        # captured-step form: the step's factors {lr0 / bc1, lr_rest / bc1,
+        # 1 / sqrt(bc2)} in a device f32[3] view, and a device i32 void-step
+        # flag (gsplat_hip_sh_colors_bwd_adam_dev)
+        self.hyper, self.skip = hyper, skip
         self.applied = False
 
     def matches(self, base, rest, C, N, K, n_rows, degree):
@@ -659,12 +703,19 @@ class _SHColors(torch.autograd.Function):
         fa = None if fusion is None else fusion.sh_adam
         if fa is not None and fa.matches(base, rest, C, N, K, ctx.n_rows, ctx.sh_degree):
             m0, v0, mr, vr = fa.moments
-            _lib.call("gsplat_hip_sh_colors_bwd_adam", ctx.sh_degree, N, _ptr(means),
-                      _ptr(viewmats), _ptr(base), _ptr(rest), _ptr(radii), _ptr(v_colors),
-                      _ptr(v_dirs), _ptr(m0), _ptr(v0), _ptr(mr), _ptr(vr),
-                      ctypes.c_float(fa.lr0), ctypes.c_float(fa.lr_rest),
-                      ctypes.c_float(fa.betas[0]), ctypes.c_float(fa.betas[1]),
-                      ctypes.c_float(fa.eps), int(fa.step), _stream())
+            if fa.hyper is not None:
+                _lib.call("gsplat_hip_sh_colors_bwd_adam_dev", ctx.sh_degree, N, _ptr(means),
+                          _ptr(viewmats), _ptr(base), _ptr(rest), _ptr(radii), _ptr(v_colors),
+                          _ptr(v_dirs), _ptr(m0), _ptr(v0), _ptr(mr), _ptr(vr), _ptr(fa.hyper),
+                          ctypes.c_float(fa.betas[0]), ctypes.c_float(fa.betas[1]),
+                          ctypes.c_float(fa.eps), _ptr(fa.skip), _stream())
+            else:
+                _lib.call("gsplat_hip_sh_colors_bwd_adam", ctx.sh_degree, N, _ptr(means),
+                          _ptr(viewmats), _ptr(base), _ptr(rest), _ptr(radii), _ptr(v_colors),
+                          _ptr(v_dirs), _ptr(m0), _ptr(v0), _ptr(mr), _ptr(vr),
+                          ctypes.c_float(fa.lr0), ctypes.c_float(fa.lr_rest),
+                          ctypes.c_float(fa.betas[0]), ctypes.c_float(fa.betas[1]),
+                          ctypes.c_float(fa.eps), int(fa.step), _stream())
             fa.applied = True
             return (None, fusion.take_means_grad(v_dirs), None, None, None, None, None)
         _lib.call("gsplat_hip_sh_colors_bwd", ctx.sh_degree, C, N, ctx.n_rows, K, _ptr(means),
@@ -704,7 +755,7 @@ class _RasterizeToPixels(torch.autograd.Function):
     @staticmethod
     def forward(ctx, means2d, conics, colors, opacities, backgrounds, masks, width, height,
                 tile_size, isect_offsets, flatten_ids, absgrad, block_size=8, visible=None,
-                records=None):
+                records=None, n_dev=None):
         ctx.means2d_in = means2d if absgrad else None  # receives .absgrad (_wrapper.py:156)
         ctx.set_materialize_grads(False)  # alphas without a loss: None, not zeros
         means2d, conics, colors, opacities, backgrounds = (
@@ -731,17 +782,18 @@ class _RasterizeToPixels(torch.autograd.Function):
         rf = 1 if records.numel() else 0
         if sb:  # dispatch order into the state, outside the timed rasterizer launch
             _lib.call("gsplat_hip_rasterize_prepare", C, D, tile_size, tw, th, _ptr(isect_offsets),
-                      flatten_ids.numel(), _ptr(state), sb, _stream())
+                      flatten_ids.numel(), _ptr(n_dev), _ptr(state), sb, _stream())
         with _Timed("rasterize_fwd"):
             _lib.call("gsplat_hip_rasterize_fwd", C, D, width, height, tile_size, tw, th,
                       _ptr(means2d), _ptr(conics), _ptr(colors), _ptr(opacities),
                       _ptr(backgrounds), _ptr(m), _ptr(isect_offsets), flatten_ids.numel(),
-                      _ptr(flatten_ids), _ptr(render_colors), _ptr(render_alphas),
+                      _ptr(n_dev), _ptr(flatten_ids), _ptr(render_colors), _ptr(render_alphas),
                       _ptr(last_ids), _ptr(records) if rf else 0, _ptr(state) if sb else 0, sb,
                       _stream())
         ctx.save_for_backward(means2d, conics, colors, opacities, backgrounds, m, isect_offsets,
                               flatten_ids, render_alphas, last_ids, render_colors, state, records)
         ctx.width, ctx.height, ctx.tile_size, ctx.absgrad = width, height, tile_size, absgrad
+        ctx.n_dev = n_dev
         return render_colors, render_alphas
 
     @staticmethod
@@ -767,7 +819,7 @@ class _RasterizeToPixels(torch.autograd.Function):
             _lib.call("gsplat_hip_rasterize_bwd", C, G, D, ctx.width, ctx.height, ctx.tile_size,
                       tw, th, _ptr(means2d), _ptr(conics), _ptr(colors), _ptr(opacities),
                       _ptr(backgrounds), _ptr(m), _ptr(isect_offsets), flatten_ids.numel(),
-                      _ptr(flatten_ids), _ptr(render_alphas), _ptr(last_ids),
+                      _ptr(ctx.n_dev), _ptr(flatten_ids), _ptr(render_alphas), _ptr(last_ids),
                       _ptr(v_render_colors), _ptr(v_render_alphas), _ptr(v_means2d),
                       _ptr(v_conics), _ptr(v_colors), _ptr(v_opacities), _ptr(v_abs),
                       _ptr(render_colors), _ptr(records) if records.numel() else 0,
@@ -779,7 +831,7 @@ class _RasterizeToPixels(torch.autograd.Function):
         if ctx.needs_input_grad[4]:
             v_backgrounds = (v_render_colors * (1.0 - render_alphas)).sum(dim=(1, 2))
         return (v_means2d, v_conics, v_colors, v_opacities, v_backgrounds,
-                None, None, None, None, None, None, None, None, None, None)
+                None, None, None, None, None, None, None, None, None, None, None)
 
 
 def rasterize_to_pixels(
@@ -830,11 +882,15 @@ def pack_render_records(means2d, conics, colors, opacities, tile_size, visible=N
 
 def _rasterize_to_pixels(means2d, conics, colors, opacities, image_width, image_height, tile_size,
                          isect_offsets, flatten_ids, backgrounds=None, masks=None, packed=False,
-                         absgrad=False, block_size=8, visible=None, records=None):
+                         absgrad=False, block_size=8, visible=None, records=None,
+                         n_isects_device=None):
     """rasterize_to_pixels with rasterization()'s private hints: `visible`
     ([C,N] tiles_per_gauss: only those Gaussians' render records are packed)
     and `records` (already packed by pack_render_records for these exact
-    colours; used when no channel padding or chunking applies)."""
+    colours; used when no channel padding or chunking applies), and
+    `n_isects_device` (flatten_ids is a capacity-sized array, finish_capped)."""
+    if n_isects_device is not None:
+        assert tile_size == 16, "a device isect count needs 16x16 tiles"
     C = isect_offsets.size(0)
     device = means2d.device
     if packed:
@@ -873,7 +929,8 @@ def _rasterize_to_pixels(means2d, conics, colors, opacities, image_width, image_
         rc, ra = _RasterizeToPixels.apply(means2d, conics, cols, opacities, bgs, masks,
                                           image_width, image_height, tile_size, isect_offsets,
                                           flatten_ids, absgrad, block_size, visible,
-                                          records if Dp == D and cols is colors else None)
+                                          records if Dp == D and cols is colors else None,
+                                          n_isects_device)
         return (rc[..., :D] if Dp != D else rc), ra
 
     if channels <= 32:

@@ -194,11 +194,21 @@ class ShardedAdam:
     """
 
     def __init__(self, params, lrs, betas=(0.9, 0.999), eps=1e-8, update=None, groups=None,
-                 group_pgs=None):
+                 group_pgs=None, emulate_world=None):
         self.params = list(params)
         self.lrs = [float(x) for x in lrs]
         self.betas, self.eps = betas, eps
         self.world, self.rank = dist.get_world_size(), dist.get_rank()
+        # a group of one rank exchanges nothing: the collectives are skipped
+        # (the shard is the gradient itself, the rows are updated in place)
+        self.solo = self.world == 1
+        if emulate_world:
+            # measurement only (bench.py --dp-emulate): on ONE rank, shard the
+            # rows as `emulate_world` ranks would and update rank 0's share --
+            # the per-rank optimizer work of that world size, without its
+            # collectives; the other shards are left stale
+            assert self.solo, "emulate_world needs a 1-rank group"
+            self.world = int(emulate_world)
         if update is None:
             from .losses import adam_groups
             update = adam_groups
@@ -217,7 +227,8 @@ class ShardedAdam:
         self.v = [z(q * row) for row, q, _, _ in self.layout]
         self.m_tail = [z(tot - main) for _, _, main, tot in self.layout]
         self.v_tail = [z(tot - main) for _, _, main, tot in self.layout]
-        self.g_shard = [torch.empty(q * row, device=dev) for row, q, _, _ in self.layout]
+        self.g_shard = [torch.empty(0 if self.solo else q * row, device=dev)
+                        for row, q, _, _ in self.layout]
         self.order = sorted(range(len(self.params)), key=lambda i: -self.params[i].numel())
         self.groups = [list(g) for g in groups] if groups else [list(self.order)]
         assert sorted(i for g in self.groups for i in g) == list(range(len(self.params))), \
@@ -260,6 +271,8 @@ class ShardedAdam:
             if self.side is not None:  # its tail rows are read on the side stream
                 gf.record_stream(self.side)
             _, _, main, tot = self.layout[i]
+            if self.solo:
+                continue  # the shard is this gradient's own rows (_update_group)
             if main:
                 works.append(dist.reduce_scatter_tensor(self.g_shard[i], gf[:main], group=pg,
                                                         async_op=True))
@@ -310,14 +323,17 @@ class ShardedAdam:
                     ev.record(side)
                     for i in grp:
                         self._updated[i] = ev
-                # issued from the side stream: RCCL waits for this Adam only
+                # issued from the side stream: RCCL waits for this Adam only.
+                # RCCL gathers in place (the send buffer is this rank's slice
+                # of the output, NCCL's in-place all-gather); gloo gets a copy
                 for i in sorted(grp, key=lambda i: self.params[i].numel()):
                     _, _, main, _ = self.layout[i]
-                    if main:
+                    if main and not self.solo:
                         full = self.params[i].data.view(-1)[:main]
+                        mine = self._shard(i, full)
                         self._pending[i] = dist.all_gather_into_tensor(
-                            full, self._shard(i, full).clone(), group=self.group_pgs[gi],
-                            async_op=True)
+                            full, mine if full.is_cuda else mine.clone(),
+                            group=self.group_pgs[gi], async_op=True)
         if not defer_gather:
             self.wait()
 
@@ -329,8 +345,10 @@ class ShardedAdam:
         idx = [i for i in grp if self.layout[i][2]]
         if idx:
             aux = [tx(i)[0] for i in idx]
+            # one rank: the reduce-scatter's output is the gradient's own rows
+            gsh = [self._shard(i, flats[i]) if self.solo else self.g_shard[i] for i in idx]
             self.update([self._shard(i, self.params[i].data.view(-1)) for i in idx],
-                        [self.g_shard[i] for i in idx], [self.m[i] for i in idx],
+                        gsh, [self.m[i] for i in idx],
                         [self.v[i] for i in idx], [self.lrs[i] for i in idx], self.betas,
                         self.eps, self.step_count,
                         aux=[None if a is None else self._shard(i, a) for i, a in zip(idx, aux)],
@@ -356,6 +374,7 @@ class ShardedAdam:
         the shards all-gathered (the replicated tail rows appended).  For the
         optimizer-state surgery of a densification step (every rank gets the
         same tensors)."""
+        assert self.world == dist.get_world_size(), "full_state: not with emulate_world"
         self.wait()
         out = []
         for i, p in enumerate(self.params):

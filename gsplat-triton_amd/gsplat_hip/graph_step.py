@@ -1,0 +1,264 @@
+"""The training step captured into a HIP graph and replayed.
+
+Eager, a step is ~70 host-side launches plus the one host synchronisation of
+the tile intersection (the reference's `.item()` of n_isects,
+gsplat/triton_impl/isect_tiles.py:101-102).  On a slow host the GPU waits
+for the launches (one box ran 520 against 731 images/s with
+identical kernel times).  Here the step is captured once with
+torch.cuda.CUDAGraph (HIP graphs on ROCm) and replayed: one replay, two
+small host->device copies and one device->host copy per step.
+
+What makes the step capturable:
+* the sync-free intersection (`rasterization(_isect_capacity=...)`,
+  gsplat_hip_isect_write_sorted_capped): isect arrays of a fixed capacity,
+  every count stays on the device;
+* the step-dependent scalars (the Adam factors lr / (1 - b1^t),
+  1 / sqrt(1 - b2^t) with the means learning-rate schedule, and the camera
+  of this step) are device buffers the host refreshes before each replay
+  (gsplat_hip_adam_step_dev, gsplat_hip_sh_colors_bwd_adam_dev), computed with
+  the eager path's own arithmetic (losses.adam_factors);
+* overflow: if a step's isects do not fit, the capped emission writes none,
+  sets a sticky device flag, and every state update of that and the later
+  steps reads the flag and does nothing.  The host reads each step's counts
+  one step late (a device->host copy, no wait), then waits for the GPU,
+  grows the capacity, re-captures and re-runs the void steps in order -- so
+  the result is the eager step sequence's.
+
+Scope: the fused one-rank 3DGS trainer without a densification schedule
+(the bench's M2 configuration); anything else runs eagerly (Trainer.step).
+"""
+
+import collections
+import math
+
+import numpy as np
+import torch
+
+from . import _wrapper
+from .losses import FusedAdam, adam_factors, l1_ssim_loss
+from .rendering import rasterization
+from .strategy import activate, update_state_
+
+
+def graphable(tr) -> bool:
+    """Whether Trainer `tr` can run its steps as graph replays."""
+    return (tr.fused and not tr.sharded and tr.world_size == 1 and tr.model == "3dgs"
+            and not getattr(tr, "defer_sh", False) and tr.strategy is None
+            and isinstance(tr.opt, FusedAdam) and torch.device(tr.device).type == "cuda")
+
+
+class GraphStep:
+    """Trainer.step as HIP graph replays (see the module docstring)."""
+
+    RING = 8  # pinned host slots for the per-step scalars and counts
+
+    def __init__(self, tr, capacity=None, headroom=1.25, lag=2):
+        assert graphable(tr), "GraphStep: a fused one-rank 3DGS trainer without densification"
+        self.tr = tr
+        dev = torch.device(tr.device)
+        self.dev = dev
+        self.headroom = float(headroom)
+        self.lag = int(lag)  # steps the host may run ahead of its overflow check
+        self.capacity = None if capacity is None else int(capacity)
+        # device inputs of the graph: per-step scalars (f32 factors + i64 camera)
+        self.n_groups = len(tr.params)
+        self.scal = torch.zeros(64, dtype=torch.float32, device=dev)
+        self.cam = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.status = torch.zeros(1, dtype=torch.int32, device=dev)  # sticky overflow flag
+        self._pin_f = [torch.zeros(64, dtype=torch.float32).pin_memory() for _ in range(self.RING)]
+        self._pin_c = [torch.zeros(1, dtype=torch.int64).pin_memory() for _ in range(self.RING)]
+        self._pin_n = [torch.zeros(4, dtype=torch.int64).pin_memory() for _ in range(self.RING)]
+        self._slot_ev = [None] * self.RING
+        self.graph = None
+        self.key = None
+        self.counts = None  # the graph's isect counts (device i64[4])
+        self.loss = None
+        self.pending = collections.deque()  # (it, slot, event) awaiting the overflow check
+        self.issued = 0
+        self.recaptures = 0
+        self.replays = 0
+        self.max_isects = 0
+
+    # ------------------------------------------------------------------ body
+    def _layout(self):
+        """(groups of the Adam launch, offset of the SH-Adam factors)."""
+        names = list(self.tr.params)
+        sh = {names.index("sh0"), names.index("shN")}
+        idx = [i for i in range(self.n_groups) if not (self.tr.sh_adam_in_bwd and i in sh)]
+        return idx, 2 * len(idx)
+
+    def _body(self, deg):
+        tr = self.tr
+        p = tr.params
+        names = list(p)
+        idx, sh_off = self._layout()
+        fa = None
+        if tr.sh_adam_in_bwd:
+            o = tr.opt
+            i0, i1 = names.index("sh0"), names.index("shN")
+            fa = _wrapper.ShAdamInBackward(
+                p["sh0"].data, p["shN"].data, o.exp_avg[i0], o.exp_avg_sq[i0], o.exp_avg[i1],
+                o.exp_avg_sq[i1], o.lrs[i0], o.lrs[i1], o.betas, o.eps, 1,
+                hyper=self.scal[sh_off:sh_off + 3], skip=self.status)
+        fusion = _wrapper.StepFusion(sh_adam=fa, geom=tr.geom_fuse) \
+            if (fa is not None or tr.geom_fuse) else None
+        vm = tr.viewmats.index_select(0, self.cam)
+        K = tr.Ks.index_select(0, self.cam)
+        gt = tr.targets.index_select(0, self.cam)
+        scales, opac = activate(p["scales"], p["opacities"], fusion)
+        colors, _, meta = rasterization(
+            p["means"], p["quats"], scales, opac, (p["sh0"], p["shN"]), vm, K, tr.width,
+            tr.height, sh_degree=deg, packed=False, near_plane=0.01, far_plane=1e10,
+            radius_clip=0.0, rasterize_mode="classic", _fusion=fusion,
+            _isect_capacity=self.capacity, _isect_status=self.status)
+        grad_box = {}
+        meta["means2d"].register_hook(lambda g: grad_box.__setitem__("g", g))
+        loss = tr._regularise(l1_ssim_loss(colors, gt, tr.ssim_lambda))
+        from . import losses as _losses
+        torch.autograd.backward(loss, _losses.ONE_GRAD)
+        if "g" in grad_box:
+            update_state_(tr.grad2d, tr.count, grad_box["g"], meta["radii"], meta["width"],
+                          meta["height"], meta["n_cameras"], skip=self.status)
+        skip = tr._sh_skip(fusion)
+        assert tuple(i for i in range(self.n_groups) if i not in skip) == tuple(idx), \
+            (skip, idx)
+        tr.opt.step(skip=skip, xform=tr._geom_xform(fusion), hyper=self.scal[:sh_off],
+                    void=self.status)
+        tr.opt.zero_grad(set_to_none=True)
+        return loss, meta["isect_counts"]
+
+    def _capture(self, deg):
+        tr = self.tr
+        from . import losses as _losses
+        if _losses.ONE_GRAD is None or _losses.ONE_GRAD.device != self.dev:
+            _losses.ONE_GRAD = torch.ones((), device=self.dev)
+        if self.capacity is None:
+            self.capacity = self._probe_capacity(deg)
+        timers = _wrapper._timers
+        _wrapper._timers = None  # no timing events inside the graph
+        torch.cuda.synchronize(self.dev)
+        try:
+            # warm-up on a side stream (torch's capture recipe) as a VOID
+            # step: the flag makes every state update a no-op
+            self.status.fill_(1)
+            s = torch.cuda.Stream(device=self.dev)
+            s.wait_stream(torch.cuda.current_stream(self.dev))
+            with torch.cuda.stream(s):
+                self._body(deg)
+            torch.cuda.current_stream(self.dev).wait_stream(s)
+            self.graph = None
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self.loss, self.counts = self._body(deg)
+            self.graph = g
+            self.status.zero_()
+            torch.cuda.synchronize(self.dev)
+        finally:
+            _wrapper._timers = timers
+        self.key = (deg, tr.params["means"].shape[0], self.capacity)
+        self.recaptures += 1
+
+    def _probe_capacity(self, deg):
+        """n_isects of the first camera, from one eager render (no grad)."""
+        tr = self.tr
+        with torch.no_grad():
+            _, _, meta = tr.render(0, deg)
+            n = int(meta["flatten_ids"].numel())
+        return max(1 << 16, int(math.ceil(n * self.headroom)))
+
+    # ------------------------------------------------------------ host side
+    def _fill(self, it, slot):
+        """The per-step scalars of step `it` into pinned slot `slot`."""
+        tr = self.tr
+        o = tr.opt
+        step = o.step_count + 1
+        lrs = list(o.lrs)
+        if tr.max_steps:  # means ExponentialLR (Trainer.step sets it before Adam)
+            lrs[0] = tr.lrs[0] * (0.01 ** (1.0 / tr.max_steps)) ** it
+        idx, sh_off = self._layout()
+        f = self._pin_f[slot].numpy()
+        fac = adam_factors([lrs[i] for i in idx], o.betas, step)
+        for k, (ss, ib) in enumerate(fac):
+            f[2 * k], f[2 * k + 1] = ss, ib
+        if tr.sh_adam_in_bwd:
+            names = list(tr.params)
+            (s0, ib), (sr, _) = adam_factors([lrs[names.index("sh0")], lrs[names.index("shN")]],
+                                             o.betas, step)
+            f[sh_off:sh_off + 3] = (s0, sr, ib)
+        self._pin_c[slot][0] = tr.camera_index(it)
+        if tr.max_steps:
+            tr._set_means_lr(lrs[0])
+
+    def step(self, it):
+        tr = self.tr
+        deg = tr.sh_degree_at(it)
+        key = (deg, tr.params["means"].shape[0], self.capacity)
+        if self.graph is None or key[:2] != self.key[:2]:
+            self._drain()
+            self._capture(deg)
+        self._check(block=len(self.pending) >= self.lag)
+        self._issue(it)
+        return self.loss
+
+    def _issue(self, it):
+        slot = self.issued % self.RING
+        ev = self._slot_ev[slot]
+        if ev is not None:
+            ev.synchronize()  # that slot's copies of RING steps ago are done
+        self._fill(it, slot)
+        cur = torch.cuda.current_stream(self.dev)
+        self.scal.copy_(self._pin_f[slot], non_blocking=True)
+        self.cam.copy_(self._pin_c[slot], non_blocking=True)
+        self.graph.replay()
+        self.tr.opt.step_count += 1
+        self._pin_n[slot].copy_(self.counts, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(cur)
+        self._slot_ev[slot] = ev
+        self.pending.append((it, slot, ev))
+        self.issued += 1
+        self.replays += 1
+
+    def _check(self, block=False):
+        """Read the counts of finished steps; on an overflow, redo from there."""
+        while self.pending:
+            it, slot, ev = self.pending[0]
+            if not ev.query():
+                if not block:
+                    return
+                ev.synchronize()
+            block = False
+            n_written, _, over, n_total = (int(x) for x in self._pin_n[slot].tolist())
+            self.max_isects = max(self.max_isects, n_total)
+            if over:
+                self._recover()
+                return
+            self.pending.popleft()
+
+    def _recover(self):
+        """Every pending step from the first overflowed one was void (sticky
+        flag): grow, re-capture, re-run them in order."""
+        tr = self.tr
+        torch.cuda.synchronize(self.dev)
+        redo = [it for it, _, _ in self.pending]
+        for _, slot, _ in self.pending:
+            self.max_isects = max(self.max_isects, int(self._pin_n[slot][3]))
+        self.pending.clear()
+        tr.opt.step_count -= len(redo)  # their Adam steps did not happen
+        self.capacity = int(math.ceil(self.max_isects * self.headroom)) + 1
+        self.status.zero_()
+        self._capture(tr.sh_degree_at(redo[0]))
+        for it in redo:
+            self._issue(it)
+            self._check(block=True)
+
+    def _drain(self):
+        if self.pending:
+            self._check(block=True)
+            while self.pending:
+                self._check(block=True)
+
+    def sync(self):
+        """Wait for every issued step and settle its overflow check."""
+        self._drain()
+        torch.cuda.synchronize(self.dev)

@@ -133,18 +133,45 @@ def l1_ssim_loss(img, gt, ssim_lambda=0.2, fused=None):
     return _L1SSIMLoss.apply(img, gt, float(ssim_lambda))
 
 
+def adam_factors(lrs, betas, step):
+    """The per-group factors gsplat_hip_adam_step computes on the host, with
+    its arithmetic (float lr and beta promoted to double, double pow / sqrt,
+    rounded to float): [lr_i / (1 - beta1^t), 1 / sqrt(1 - beta2^t)] per
+    group -- what the captured step's device-side variants read."""
+    import numpy as np
+    b1, b2 = float(np.float32(betas[0])), float(np.float32(betas[1]))
+    bc1, bc2 = 1.0 - b1 ** int(step), 1.0 - b2 ** int(step)
+    ib = float(np.float32(1.0 / math.sqrt(bc2)))
+    return [(float(np.float32(float(np.float32(lr)) / bc1)), ib) for lr in lrs]
+
+
 def adam_groups(params, grads, exp_avgs, exp_avg_sqs, lrs, betas, eps, step, max_blocks=0,
-                aux=None, modes=None):
+                aux=None, modes=None, hyper=None, skip=None):
     """One fused Adam launch (csrc/adam.hip) over flat float32 tensors: group
     i updates params[i] in place from grads[i] (None = zero) with its lr.
     max_blocks > 0 bounds the grid (gsplat_hip_adam_step_bounded); aux/modes
-    form the gradient in-register (gsplat_hip_adam_step_ex)."""
+    form the gradient in-register (gsplat_hip_adam_step_ex); hyper (device
+    f32[2 n], adam_factors' values) / skip (device i32 flag): the captured
+    step's form (gsplat_hip_adam_step_dev; lrs and step unused)."""
     n = len(params)
     P = ctypes.c_void_p * n
     for t in list(params) + list(exp_avgs) + list(exp_avg_sqs):
         assert t.is_contiguous() and t.dtype == torch.float32
     head = [n, P(*[p.data_ptr() for p in params]),
             P(*[0 if g is None else g.data_ptr() for g in grads])]
+    if hyper is not None:
+        assert max_blocks == 0 and hyper.dtype == torch.float32 and hyper.numel() >= 2 * n
+        ax = [None] * n if aux is None else aux
+        for a in ax:
+            assert a is None or (a.is_contiguous() and a.dtype == torch.float32)
+        _lib.call("gsplat_hip_adam_step_dev", *head,
+                  P(*[0 if a is None else a.data_ptr() for a in ax]),
+                  (ctypes.c_int32 * n)(*[int(m) for m in (modes or [0] * n)]),
+                  P(*[m.data_ptr() for m in exp_avgs]), P(*[v.data_ptr() for v in exp_avg_sqs]),
+                  (ctypes.c_int64 * n)(*[p.numel() for p in params]), hyper.data_ptr(),
+                  float(betas[0]), float(betas[1]), float(eps),
+                  0 if skip is None else skip.data_ptr(), _stream())
+        return
     tail = [P(*[m.data_ptr() for m in exp_avgs]), P(*[v.data_ptr() for v in exp_avg_sqs]),
             (ctypes.c_int64 * n)(*[p.numel() for p in params]),
             (ctypes.c_float * n)(*[float(x) for x in lrs]), float(betas[0]), float(betas[1]),
@@ -195,7 +222,7 @@ class FusedAdam:
             self.side = torch.cuda.Stream(device=self.params[0].device)
         self._event = None
 
-    def _launch(self, idx, grads, max_blocks=0, xform=None):
+    def _launch(self, idx, grads, max_blocks=0, xform=None, hyper=None, void=None):
         aux = modes = None
         if xform:
             aux = [xform[i][1] if i in xform else None for i in idx]
@@ -204,24 +231,29 @@ class FusedAdam:
         adam_groups([self.params[i].data for i in idx], [grads[i] for i in idx],
                     [self.exp_avg[i] for i in idx], [self.exp_avg_sq[i] for i in idx],
                     [self.lrs[i] for i in idx], self.betas, self.eps, self.step_count,
-                    max_blocks, aux, modes)
+                    max_blocks, aux, modes, hyper, void)
 
     @torch.no_grad()
-    def step(self, skip=(), xform=None):
+    def step(self, skip=(), xform=None, hyper=None, void=None):
         """skip: indices already updated for this step (by the SH backward
         with the update fused in, train_step.Trainer).  xform: {index:
         (grad, aux, mode)} -- the gradient of that group formed in-register
-        (adam_step_ex modes: 1 sum, 2 exp VJP, 3 sigmoid VJP)."""
+        (adam_step_ex modes: 1 sum, 2 exp VJP, 3 sigmoid VJP).  hyper / void:
+        the captured step's device-side factors of the launched groups (in
+        launch order, adam_factors) and void-step flag (step_count is then
+        the caller's business)."""
         self.wait()  # a previous deferred update is ordered before this one
-        self.step_count += 1
+        if hyper is None:
+            self.step_count += 1
         grads = [p.grad for p in self.params]
         for gr in grads:
             assert gr is None or gr.is_contiguous()
         if self.side is None:
             idx = [i for i in range(len(self.params)) if i not in skip]
             if idx:
-                self._launch(idx, grads, xform=xform)
+                self._launch(idx, grads, xform=xform, hyper=hyper, void=void)
             return
+        assert hyper is None, "the captured step has no deferred groups"
         assert not skip and not xform, "skip / xform and deferred groups are exclusive"
         now = [i for i in range(len(self.params)) if i not in self.deferred]
         if now:

@@ -68,12 +68,20 @@ def rasterization(
     covars: Optional[Tensor] = None,
     _colors_ready: Optional[Callable[[], None]] = None,
     _fusion=None,
+    _isect_capacity: Optional[int] = None,
+    _isect_status: Optional[Tensor] = None,
 ) -> Tuple[Tensor, Tensor, Dict]:
     """Rasterize N 3D Gaussians to C images (gsplat/rendering.py:44-598).
 
     Private arguments of the training harness (train_step.Trainer):
     `_colors_ready` (see below) and `_fusion`, a _wrapper.StepFusion handed
-    to the fused SH-colour node (optimizer work folded into its backward)."""
+    to the fused SH-colour node (optimizer work folded into its backward);
+    `_isect_capacity`: the sync-free tile intersection (no host read of
+    n_isects, so the render can be captured into a HIP graph) into arrays of
+    that many slots -- meta["isect_ids"] / ["flatten_ids"] are then
+    capacity-sized, meta["isect_counts"] (device i64[4]: written, visible,
+    overflow, n_isects) says how many are valid; an overflow also sets
+    `_isect_status[0]` (sticky)."""
     meta = {}
     N = means.shape[0]
     C = viewmats.shape[0]
@@ -146,10 +154,14 @@ def rasterization(
     tile_width = math.ceil(width / float(tile_size))
     tile_height = math.ceil(height / float(tile_size))
     pending_isects = None
+    capped = _isect_capacity is not None
+    if capped:
+        assert not distributed and tile_size == 16, "the sync-free isect: local 16x16 renders"
     if not distributed:
         pending_isects = isect_tiles_begin(means2d, radii, depths, tile_size, tile_width,
                                            tile_height, packed=packed, n_cameras=C,
-                                           camera_ids=camera_ids, gaussian_ids=gaussian_ids)
+                                           camera_ids=camera_ids, gaussian_ids=gaussian_ids,
+                                           sync=not capped)
 
     def eval_colors(colors):
         if packed:  # colours of the nnz pairs (gsplat/rendering.py:368-408)
@@ -257,8 +269,15 @@ def rasterization(
             records = pack_render_records(means2d, conics, colors, opacities, tile_size,
                                           None if packed else pending_isects.tpg)
 
-    tiles_per_gauss, isect_ids, flatten_ids = pending_isects.finish(sort=True)
-    isect_offsets = isect_offset_encode(isect_ids, C, tile_width, tile_height)
+    counts = None
+    if capped:
+        tiles_per_gauss, isect_ids, flatten_ids, counts = pending_isects.finish_capped(
+            _isect_capacity, _isect_status)
+        meta["isect_counts"] = counts
+    else:
+        tiles_per_gauss, isect_ids, flatten_ids = pending_isects.finish(sort=True)
+    isect_offsets = isect_offset_encode(isect_ids, C, tile_width, tile_height,
+                                        _n_isects_device=counts)
     if late:
         _colors_ready()
         colors, backgrounds = add_depth(eval_colors(colors), backgrounds)
@@ -281,7 +300,7 @@ def rasterization(
                 means2d, conics, colors[..., sl], opacities, width, height, tile_size,
                 isect_offsets, flatten_ids,
                 backgrounds=None if backgrounds is None else backgrounds[..., sl],
-                packed=packed, absgrad=absgrad, visible=visible)
+                packed=packed, absgrad=absgrad, visible=visible, n_isects_device=counts)
             render_colors.append(rc)
             render_alphas.append(ra)
         render_colors = torch.cat(render_colors, dim=-1)
@@ -290,7 +309,7 @@ def rasterization(
         render_colors, render_alphas = _rasterize_to_pixels(
             means2d, conics, colors, opacities, width, height, tile_size, isect_offsets,
             flatten_ids, backgrounds=backgrounds, packed=packed, absgrad=absgrad, visible=visible,
-            records=records)
+            records=records, n_isects_device=counts)
     if render_mode in ["ED", "RGB+ED"]:
         render_colors = torch.cat(
             [render_colors[..., :-1],

@@ -60,8 +60,10 @@ def activate(log_scales, logits, fusion=None):
 
 
 @torch.no_grad()
-def update_state_(grad2d, count, means2d_grad, radii, width, height, n_cameras):
-    """grad2d/count += DefaultStrategy's per-step statistics (in place)."""
+def update_state_(grad2d, count, means2d_grad, radii, width, height, n_cameras, skip=None):
+    """grad2d/count += DefaultStrategy's per-step statistics (in place).
+    skip: device i32 flag; non-zero leaves the statistics alone (a void
+    step of a captured training step)."""
     C, N = radii.shape
     g = _f32c(means2d_grad)
     radii = radii.to(torch.int32).contiguous()
@@ -69,4 +71,4 @@ def update_state_(grad2d, count, means2d_grad, radii, width, height, n_cameras):
     assert grad2d.is_contiguous() and count.is_contiguous() and grad2d.numel() == N
     _lib.call("gsplat_hip_update_state", C, N, _ptr(g), _ptr(radii),
               ctypes.c_float(width / 2.0 * n_cameras), ctypes.c_float(height / 2.0 * n_cameras),
-              _ptr(grad2d), _ptr(count), _stream())
+              _ptr(grad2d), _ptr(count), _ptr(skip), _stream())

@@ -139,7 +139,8 @@ class Trainer:
                  sh_degree_interval: Optional[int] = None, max_steps: Optional[int] = None,
                  init: str = "random", init_opacity: float = 0.1, init_scale: float = 1.0,
                  targets: Optional[torch.Tensor] = None, opacity_reg: float = 0.0,
-                 scale_reg: float = 0.0):
+                 scale_reg: float = 0.0, dp_emulate_world: Optional[int] = None,
+                 graph: bool = False, isect_capacity: Optional[int] = None):
         assert model in ("3dgs", "2dgs"), model
         assert init in ("random", "sfm"), init
         self.model = model
@@ -192,6 +193,9 @@ class Trainer:
         if sharded_optimizer is None:
             sharded_optimizer = world_size > 1
         self.sharded = fused and sharded_optimizer
+        # measurement only (bench.py --dp-emulate W): one rank shards its
+        # optimizer rows as W ranks would (ShardedAdam emulate_world)
+        self.dp_emulate_world = dp_emulate_world if self.sharded else None
         # GSPLAT_HIP_DEFER_SH=1: the SH rows' Adam on a side stream beside the
         # next step's projection and isect (colours evaluated after the isect).
         # Measured slower at M2 (620-630 vs 660 images/s): the
@@ -237,6 +241,15 @@ class Trainer:
         self.window = _gauss_window(device=device)
         self.last_meta = None
         self.refine_log = []  # (step, n_dupli, n_split, n_prune, N after)
+        # graph=True: the step as HIP graph replays where the configuration
+        # allows (graph_step.graphable: fused one-rank 3DGS, no densification
+        # schedule); isect_capacity: its isect arrays' initial size (default:
+        # 1.25 x the first camera's count)
+        self._graph = None
+        if graph:
+            from .graph_step import GraphStep, graphable
+            if graphable(self):
+                self._graph = GraphStep(self, capacity=isect_capacity)
 
     # ------------------------------------------------------------ optimizer
     def _make_optimizer(self, params):
@@ -249,6 +262,7 @@ class Trainer:
                       [names.index(k) for k in ("sh0", "shN")]]
             return ShardedAdam(params, self.lrs, groups=groups,
                                group_pgs=[None, getattr(self, "_sh_pg", None)],
+                               emulate_world=getattr(self, "dp_emulate_world", None),
                                **self.adam_kw)
         if self.fused:  # HIP loss + one-launch Adam (csrc/ssim.hip, csrc/adam.hip)
             # the SH rows' update on a side stream, overlapping the next
@@ -327,6 +341,8 @@ class Trainer:
         """Order the current stream after any optimizer communication still in
         flight (the sharded optimizer's deferred all-gathers): call before
         reading the parameters outside the training step (checkpoint, eval)."""
+        if getattr(self, "_graph", None) is not None:
+            self._graph.sync()
         if self.sharded or getattr(self, "defer_sh", False):
             self.opt.wait()
 
@@ -381,6 +397,8 @@ class Trainer:
             rasterize_mode="classic", absgrad=absgrad, _colors_ready=hook, _fusion=fusion)
 
     def step(self, it: int):
+        if getattr(self, "_graph", None) is not None:
+            return self._graph.step(it)
         ci = self.camera_index(it)
         self._sh_ready = 0
         fusion = self._make_fusion()

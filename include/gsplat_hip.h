@@ -139,6 +139,24 @@ int gsplat_hip_isect_write_sorted(int64_t n_gaussians, int N, const float *means
                                   int cam_bits, const void *count_workspace, int64_t n_visible,
                                   int64_t n_isects, void *workspace, int64_t workspace_bytes,
                                   int64_t *isect_ids, int32_t *flatten_ids, void *stream);
+/* The same sorted emission with NO host sync (ABI 20; the reference reads
+ * n_isects with .item(), isect_tiles.py:101-102): the totals stay on the
+ * device (step 1's totals_device), isect_ids / flatten_ids have `capacity`
+ * slots and every launch is sized for it.  counts_device i64[4] receives
+ * {isects written -- 0 when they do not fit --, n_visible, 1 if they did not
+ * fit, n_isects}; status_device[0] (may be NULL) gets bit 0 set on overflow and keeps it
+ * (sticky, cleared by the caller).  Pass counts_device as the n_isects_device
+ * of gsplat_hip_isect_offsets / gsplat_hip_rasterize_*, with n_isects =
+ * capacity.  The written isects equal gsplat_hip_isect_write_sorted's. */
+int64_t gsplat_hip_isect_sorted_capped_workspace_bytes(int64_t n_gaussians, int64_t capacity,
+                                                       int key_bits);
+int gsplat_hip_isect_write_sorted_capped(
+    int64_t n_gaussians, int N, const float *means2d, const int32_t *radii, const float *depths,
+    const int32_t *camera_ids, const int32_t *tiles_per_gauss, int tile_size, int tile_width,
+    int tile_height, int tile_bits, int cam_bits, const void *count_workspace,
+    const int64_t *totals_device, int64_t capacity, int64_t *counts_device,
+    int32_t *status_device, void *workspace, int64_t workspace_bytes, int64_t *isect_ids,
+    int32_t *flatten_ids, void *stream);
 /* Sorted emission, tile-first (the default of isect_tiles(sort=True)): the
  * SAME isect_ids / flatten_ids again, from Gaussian-major emission with
  * 32-bit (camera, tile) keys, a stable sort by those keys, and a segmented
@@ -160,9 +178,12 @@ int gsplat_hip_radix_sort(int64_t n, int n_bits, const int64_t *keys_in, const i
 
 /* Replaces get_isect_offsets() (gsplat/triton_impl/isect_offset.py:8-63).
  * offsets i32[C,tile_height,tile_width]: index of the first sorted isect of
- * each tile (= number of isects with a smaller (camera, tile) key). */
-int gsplat_hip_isect_offsets(int64_t n_isects, const int64_t *isect_ids, int C, int tile_width,
-                             int tile_height, int32_t *offsets, void *stream);
+ * each tile (= number of isects with a smaller (camera, tile) key).
+ * n_isects_device (ABI 20, may be NULL): the count on the device, n_isects
+ * then being the capacity of isect_ids (gsplat_hip_isect_write_sorted_capped). */
+int gsplat_hip_isect_offsets(int64_t n_isects, const int64_t *n_isects_device,
+                             const int64_t *isect_ids, int C, int tile_width, int tile_height,
+                             int32_t *offsets, void *stream);
 
 /* ---------------------------------------------------------------------------
  * Rasterization.  D in {1,2,3,4,8,16,32} (gsplat_hip_rasterize_supported_channels);
@@ -184,8 +205,12 @@ int gsplat_hip_rasterize_supported_channels(int D);
  * host thread, so the forward call launches the rasterizer kernel alone
  * (lets a caller time that kernel by itself).  Without it the forward does
  * the preparation itself. */
+/* n_isects_device (here, in _fwd and in _bwd; ABI 20; 16x16 tiles, else
+ * NULL): the isect count on the device, n_isects being the capacity of
+ * flatten_ids (the sync-free isect, gsplat_hip_isect_write_sorted_capped). */
 int gsplat_hip_rasterize_prepare(int C, int D, int tile_size, int tile_width, int tile_height,
-                                 const int32_t *isect_offsets, int64_t n_isects, void *state,
+                                 const int32_t *isect_offsets, int64_t n_isects,
+                                 const int64_t *n_isects_device, void *state,
                                  int64_t state_bytes, void *stream);
 int64_t gsplat_hip_rasterize_fwd_state_bytes(int C, int D, int tile_size, int tile_width,
                                              int tile_height, int64_t n_isects);
@@ -208,9 +233,10 @@ int gsplat_hip_rasterize_fwd(int C, int D, int width, int height, int tile_size,
                              const float *colors, const float *opacities,
                              const float *backgrounds, const uint8_t *masks,
                              const int32_t *isect_offsets, int64_t n_isects,
-                             const int32_t *flatten_ids, float *render_colors,
-                             float *render_alphas, int32_t *last_ids, const float *records,
-                             void *state, int64_t state_bytes, void *stream);
+                             const int64_t *n_isects_device, const int32_t *flatten_ids,
+                             float *render_colors, float *render_alphas, int32_t *last_ids,
+                             const float *records, void *state, int64_t state_bytes,
+                             void *stream);
 
 /* Replaces rasterize_to_pixels_bwd() (gsplat/triton_impl/rasterize_to_pixels_bwd.py:340-457)
  * called from _RasterizeToPixels.backward (_wrapper.py:104-182).
@@ -229,7 +255,8 @@ int gsplat_hip_rasterize_bwd(int C, int64_t n_gaussians, int D, int width, int h
                              const float *means2d, const float *conics, const float *colors,
                              const float *opacities, const float *backgrounds,
                              const uint8_t *masks, const int32_t *isect_offsets,
-                             int64_t n_isects, const int32_t *flatten_ids,
+                             int64_t n_isects, const int64_t *n_isects_device,
+                             const int32_t *flatten_ids,
                              const float *render_alphas, const int32_t *last_ids,
                              const float *v_render_colors, const float *v_render_alphas,
                              float *v_means2d, float *v_conics, float *v_colors,
@@ -305,9 +332,11 @@ int gsplat_hip_l1_ssim_loss_fused_bwd(int64_t n, const float *grad_unit, const f
  * 213-262): for every (c, g) with radii[c,g] > 0, in camera order,
  * grad2d[g] += |(means2d_grad[c,g,0]*scale_x, means2d_grad[c,g,1]*scale_y)|
  * and count[g] += 1.  scale_x = width/2 * C, scale_y = height/2 * C. */
+/* skip_device (ABI 20, may be NULL): when *skip_device != 0 nothing is
+ * accumulated (a void step of a captured training step). */
 int gsplat_hip_update_state(int C, int64_t N, const float *means2d_grad, const int32_t *radii,
                             float scale_x, float scale_y, float *grad2d, float *count,
-                            void *stream);
+                            const int32_t *skip_device, void *stream);
 
 /* The trainer's parameter activations (examples/simple_trainer.py:565-566)
  * in one launch each way: scales = exp(log_scales), opacities =
@@ -373,6 +402,17 @@ int gsplat_hip_sh_colors_bwd_adam(int degree, int64_t N, const float *means,
                                   float *m0, float *v0, float *m_rest, float *v_rest, float lr0,
                                   float lr_rest, float beta1, float beta2, float eps, int step,
                                   void *stream);
+/* The same with the step's factors on the device (ABI 20; a captured
+ * training step replays with a new step count): hyper_device = {lr0 /
+ * (1 - beta1^t), lr_rest / (1 - beta1^t), 1 / sqrt(1 - beta2^t)}, computed
+ * on the host as above; skip_device (may be NULL) != 0 leaves the
+ * coefficients and moments unchanged (v_dirs is still written). */
+int gsplat_hip_sh_colors_bwd_adam_dev(int degree, int64_t N, const float *means,
+                                      const float *viewmats, float *coeffs, float *coeffs_rest,
+                                      const int32_t *radii, const float *v_colors, float *v_dirs,
+                                      float *m0, float *v0, float *m_rest, float *v_rest,
+                                      const float *hyper_device, float beta1, float beta2,
+                                      float eps, const int32_t *skip_device, void *stream);
 
 /* One torch.optim.Adam step (amsgrad=False, no weight decay) over up to 8
  * parameter groups in a single launch (replaces the per-group optimizers of
@@ -392,6 +432,16 @@ int gsplat_hip_adam_step_ex(int n_groups, float *const *params, const float *con
                             float *const *exp_avgs, float *const *exp_avg_sqs,
                             const int64_t *numels, const float *lrs, float beta1, float beta2,
                             float eps, int step, void *stream);
+/* gsplat_hip_adam_step_ex with the step's factors on the device (ABI 20):
+ * hyper_device[2 i] = lr_i / (1 - beta1^t), hyper_device[2 i + 1] =
+ * 1 / sqrt(1 - beta2^t) (the host's double-precision values rounded to
+ * float, as gsplat_hip_adam_step computes them); skip_device (may be NULL)
+ * != 0 updates nothing. */
+int gsplat_hip_adam_step_dev(int n_groups, float *const *params, const float *const *grads,
+                             const float *const *aux, const int32_t *modes,
+                             float *const *exp_avgs, float *const *exp_avg_sqs,
+                             const int64_t *numels, const float *hyper_device, float beta1,
+                             float beta2, float eps, const int32_t *skip_device, void *stream);
 /* The same update on a grid of at most max_blocks workgroups (ABI 17): an
  * update running on a side stream beside other kernels leaves them CU slots
  * (the trainer's deferred SH-coefficient update). */

@@ -1,0 +1,217 @@
+"""GPU: the sync-free tile intersection and the training step replayed as a
+HIP graph (gsplat_hip/graph_step.py).
+
+* capacity-mode isect (gsplat_hip_isect_write_sorted_capped): the written
+  isects are bit-identical to the synchronous path's, offsets and renders
+  too; on overflow nothing is written, the counts say so and the sticky
+  status flag is set;
+* the device-side Adam factors (gsplat_hip_adam_step_dev,
+  gsplat_hip_sh_colors_bwd_adam_dev) give the same bits as the host-scalar
+  launches, and a set void flag updates nothing;
+* the graph-replayed trainer tracks the eager trainer (the rasterizer's
+  float atomics make two runs differ in the last bits), also when its isect
+  capacity is too small at first: the overflowed steps are voided, the
+  capacity grows, the step is re-captured and the void steps re-run."""
+
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import gsplat_hip  # noqa: F401
+
+
+def _scene(N=30000, W=640, H=480, seed=2):
+    g = torch.Generator().manual_seed(seed)
+    means = torch.randn(N, 3, generator=g) * torch.tensor([1.6, 1.2, 0.6])
+    means[:, 2] += 4.0
+    quats = torch.randn(N, 4, generator=g)
+    scales = torch.rand(N, 3, generator=g) * 0.06 + 0.004
+    opac = torch.rand(N, generator=g)
+    sh = torch.randn(N, 16, 3, generator=g) * 0.3
+    vm = torch.eye(4)[None]
+    K = torch.tensor([[500.0, 0, W / 2], [0, 500.0, H / 2], [0, 0, 1]])[None]
+    return [x.to(DEV) for x in (means, quats, scales, opac, sh, vm, K)], W, H
+
+
+def _render(ins, W, H, **kw):
+    import gsplat_hip
+    leaves = [x.clone().requires_grad_(True) for x in ins[:5]]
+    rc, ra, meta = gsplat_hip.rasterization(*leaves, ins[5], ins[6], W, H, sh_degree=3,
+                                            packed=False, **kw)
+    w = torch.rand(rc.shape, device=DEV, generator=torch.Generator(device=DEV).manual_seed(4))
+    (rc * w).sum().backward()
+    torch.cuda.synchronize()
+    return rc.detach(), ra.detach(), meta, [x.grad for x in leaves]
+
+
+def test_capped_isect_matches_synchronous():
+    ins, W, H = _scene()
+    rc0, ra0, m0, g0 = _render(ins, W, H)
+    n = m0["flatten_ids"].numel()
+    status = torch.zeros(1, dtype=torch.int32, device=DEV)
+    rc1, ra1, m1, g1 = _render(ins, W, H, _isect_capacity=n + 12345, _isect_status=status)
+    counts = m1["isect_counts"].tolist()
+    assert counts[0] == n and counts[2] == 0 and counts[3] == n and int(status) == 0
+    assert counts[1] == int((m0["tiles_per_gauss"] > 0).sum())
+    assert m1["isect_ids"].numel() == n + 12345
+    assert torch.equal(m1["isect_ids"][:n], m0["isect_ids"])
+    assert torch.equal(m1["flatten_ids"][:n], m0["flatten_ids"])
+    assert torch.equal(m1["isect_offsets"], m0["isect_offsets"])
+    # the same per-tile lists through the same deterministic forward
+    assert torch.equal(rc1, rc0) and torch.equal(ra1, ra0)
+    for a, b in zip(g1, g0):
+        scale = float(b.abs().max())
+        assert float((a - b).abs().max()) <= 1e-5 * scale + 1e-9
+    # exactly full is not an overflow
+    _, _, m2, _ = _render(ins, W, H, _isect_capacity=n, _isect_status=status)
+    assert m2["isect_counts"].tolist()[2] == 0 and int(status) == 0
+    assert torch.equal(m2["isect_ids"], m0["isect_ids"])
+
+
+def test_capped_isect_overflow_writes_nothing():
+    ins, W, H = _scene(N=8000)
+    _, _, m0, _ = _render(ins, W, H)
+    n = m0["flatten_ids"].numel()
+    status = torch.zeros(1, dtype=torch.int32, device=DEV)
+    rc, ra, m1, grads = _render(ins, W, H, _isect_capacity=n - 1, _isect_status=status)
+    written, _, over, total = m1["isect_counts"].tolist()
+    assert (written, over, total) == (0, 1, n) and int(status) == 1
+    assert int(m1["isect_offsets"].abs().sum()) == 0  # every tile empty
+    assert float(ra.abs().max()) == 0.0 and torch.isfinite(rc).all()
+    assert all(torch.isfinite(g).all() for g in grads)
+    # sticky: a later render that fits leaves the flag set
+    _render(ins, W, H, _isect_capacity=2 * n, _isect_status=status)
+    assert int(status) == 1
+
+
+def test_adam_device_factors_are_exact():
+    """adam_factors + gsplat_hip_adam_step_dev == gsplat_hip_adam_step, bit
+    for bit, over steps and a changing learning rate; a void step changes
+    nothing."""
+    from gsplat_hip.losses import adam_factors, adam_groups
+    torch.manual_seed(3)
+    shapes = [(4099, 3), (4099, 4), (4099,), (4099, 15, 3)]
+    lrs = [1.6e-4, 1e-3, 5e-2, 1.25e-4]
+    betas, eps = (0.9, 0.999), 1e-15
+    base = [torch.randn(s, device=DEV) for s in shapes]
+    res = []
+    for dev_form in (False, True):
+        ps = [b.clone() for b in base]
+        ms = [torch.zeros_like(b) for b in base]
+        vs = [torch.zeros_like(b) for b in base]
+        hyper = torch.zeros(2 * len(shapes), device=DEV)
+        void = torch.zeros(1, dtype=torch.int32, device=DEV)
+        for step in range(1, 6):
+            g = torch.Generator(device=DEV).manual_seed(step)
+            grads = [torch.randn(s, device=DEV, generator=g) for s in shapes]
+            lr_t = [lr * (0.99 ** step) for lr in lrs]
+            flat = lambda ts: [t.view(-1) for t in ts]  # noqa: E731
+            if dev_form:
+                hyper.copy_(torch.tensor([x for f in adam_factors(lr_t, betas, step) for x in f]))
+                adam_groups(flat(ps), flat(grads), flat(ms), flat(vs), lr_t, betas, eps, 0,
+                            hyper=hyper, skip=void)
+            else:
+                adam_groups(flat(ps), flat(grads), flat(ms), flat(vs), lr_t, betas, eps, step)
+        if dev_form:  # a void step
+            before = [p.clone() for p in ps]
+            void.fill_(1)
+            adam_groups(flat(ps), flat(grads), flat(ms), flat(vs), lr_t, betas, eps, 0,
+                        hyper=hyper, skip=void)
+            assert all(torch.equal(a, b) for a, b in zip(before, ps))
+        torch.cuda.synchronize()
+        res.append(ps + ms + vs)
+    for a, b in zip(res[0], res[1]):
+        assert torch.equal(a, b)
+
+
+def test_sh_adam_device_factors_are_exact():
+    from gsplat_hip import _wrapper
+    from gsplat_hip.losses import FusedAdam, adam_factors
+    g = torch.Generator(device=DEV).manual_seed(9)
+    N = 2049
+    means = torch.randn(N, 3, device=DEV, generator=g) * 2
+    vm = torch.eye(4, device=DEV)[None]
+    vm[0, 2, 3] = 6.0
+    radii = (torch.rand(1, N, device=DEV, generator=g) > 0.4).int() * 3
+    sh0 = torch.randn(N, 1, 3, device=DEV, generator=g) * 0.3
+    shN = torch.randn(N, 15, 3, device=DEV, generator=g) * 0.1
+    ws = [torch.rand(1, N, 3, device=DEV, generator=g) - 0.5 for _ in range(3)]
+    res = []
+    for dev_form in (False, True):
+        p0, p1 = sh0.clone().requires_grad_(True), shN.clone().requires_grad_(True)
+        opt = FusedAdam([p0, p1], [2.5e-3, 1.25e-4], eps=1e-15)
+        hyper = torch.zeros(3, device=DEV)
+        void = torch.zeros(1, dtype=torch.int32, device=DEV)
+        for it in range(3):
+            step = opt.step_count + 1
+            if dev_form:
+                (s0, ib), (sr, _) = adam_factors(opt.lrs, opt.betas, step)
+                hyper.copy_(torch.tensor([s0, sr, ib]))
+                fa = _wrapper.ShAdamInBackward(p0.data, p1.data, opt.exp_avg[0],
+                                               opt.exp_avg_sq[0], opt.exp_avg[1],
+                                               opt.exp_avg_sq[1], opt.lrs[0], opt.lrs[1],
+                                               opt.betas, opt.eps, 1, hyper=hyper, skip=void)
+            else:
+                fa = _wrapper.ShAdamInBackward(p0.data, p1.data, opt.exp_avg[0],
+                                               opt.exp_avg_sq[0], opt.exp_avg[1],
+                                               opt.exp_avg_sq[1], opt.lrs[0], opt.lrs[1],
+                                               opt.betas, opt.eps, step)
+            colors = _wrapper.sh_colors(3, means, vm, (p0, p1), radii,
+                                        fusion=_wrapper.StepFusion(sh_adam=fa))
+            (colors * ws[it]).sum().backward()
+            assert fa.applied
+            opt.step_count += 1
+        torch.cuda.synchronize()
+        res.append((p0.detach().clone(), p1.detach().clone(), *opt.exp_avg, *opt.exp_avg_sq))
+    for a, b in zip(res[0], res[1]):
+        assert torch.equal(a, b)
+
+
+def _trainer_scene(n_cams=3, W=320, H=240):
+    import os
+    from gsplat_hip.train_step import camera_pool, load_garden_scene
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    means, rgbs, vms, Ks, sw, sh_ = load_garden_scene(
+        os.path.join(root, "tests", "golden", "garden_scene.npz"), scene_grid=1)
+    means, rgbs = means[::8].contiguous(), rgbs[::8].contiguous()
+    vm, K = camera_pool(vms, Ks, sw, sh_, W, H, n=n_cams)
+    return means, rgbs, vm, K, W, H
+
+
+@pytest.mark.parametrize("capacity", [None, 1000])
+def test_graph_trainer_tracks_eager(capacity):
+    from gsplat_hip.train_step import Trainer
+    means, rgbs, vm, K, W, H = _trainer_scene()
+    out = {}
+    for graph in (False, True):
+        tr = Trainer(means, rgbs, vm, K, W, H, device=DEV, graph=graph, isect_capacity=capacity,
+                     max_steps=100)
+        assert (tr._graph is not None) == graph
+        for it in range(6):
+            tr.step(it)
+        tr.sync()
+        out[graph] = ({k: p.detach().clone() for k, p in tr.params.items()},
+                      [m.clone() for m in tr.opt.exp_avg], tr.opt.step_count,
+                      tr.grad2d.clone(), tr.count.clone())
+        if graph:
+            g = tr._graph
+            assert g.replays >= 6
+            if capacity is not None:  # started too small: grown and re-captured
+                assert g.recaptures >= 2 and g.capacity > g.max_isects > capacity
+    a, b = out[False], out[True]
+    assert a[2] == b[2] == 6
+    for k in a[0]:
+        torch.testing.assert_close(b[0][k], a[0][k], rtol=1e-3, atol=1e-5)
+    for x, y in zip(a[1], b[1]):
+        torch.testing.assert_close(y, x, rtol=1e-2, atol=1e-6)
+    torch.testing.assert_close(b[4], a[4], rtol=0, atol=0)  # visibility counts: exact
+    torch.testing.assert_close(b[3], a[3], rtol=1e-3, atol=1e-7)

@@ -71,8 +71,11 @@ def test_eight_cameras_vs_oracle_m1():
     assert np.array_equal(meta["isect_offsets"].cpu().numpy(), off)
     oc, oa, _ = O.raster_fwd(m2, cn, cols.numpy(), np.broadcast_to(opac.numpy(), (C, N)),
                              bg.numpy(), W, H, 16, off, fids)
-    np.testing.assert_allclose(ra.cpu().numpy(), oa, rtol=1e-4, atol=1e-4)
-    np.testing.assert_allclose(rc.cpu().numpy(), oc, rtol=1e-4, atol=1e-4)
+    # the rasterizer bars of test_gpu_parity.py (a handful of alpha / T
+    # threshold flips between two correct fp32 implementations allowed)
+    from test_gpu_parity import close_most
+    close_most(ra, oa, 1e-4, 1e-4, "alphas")
+    close_most(rc, oc, 1e-4, 1e-4, "colors")
     # every camera occupies its own id range (camera bits above the tile bits)
     cam = (meta["isect_ids"] >> (32 + (tw * th - 1).bit_length())).cpu().numpy()
     assert np.all(np.diff(cam) >= 0) and set(np.unique(cam)) <= set(range(C))

@@ -82,7 +82,7 @@ def test_xcd_order_is_banded_permutation():
     D = 3
     sb = int(_lib.query("gsplat_hip_rasterize_fwd_state_bytes", C, D, 16, tw, th, n))
     state = torch.full((sb // 4,), -7, dtype=torch.int32, device=DEV)
-    _lib.call("gsplat_hip_rasterize_prepare", C, D, 16, tw, th, _ptr(offs), n, _ptr(state), sb,
+    _lib.call("gsplat_hip_rasterize_prepare", C, D, 16, tw, th, _ptr(offs), n, None, _ptr(state), sb,
               _stream())
     torch.cuda.synchronize()
     QI = 32 + 8 * 32  # starts[8], lens[8], pad, then one 128-B line per dequeue head
