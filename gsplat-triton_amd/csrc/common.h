@@ -7,6 +7,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #define GS_INLINE __device__ __forceinline__
 
 namespace gs {
@@ -41,6 +43,43 @@ void set_error(const char *fmt, ...);
       return 1;                                                                \
     }                                                                          \
   } while (0)
+
+// ------------------------------------------------------------- zero fill
+// Zeroing as a kernel instead of hipMemsetAsync: a captured training step
+// (gsplat_hip/graph_step.py) then holds kernel nodes only -- its replays
+// faulted with the backward's memset nodes in the graph (the forward,
+// without memsets, replayed cleanly).  16-B stores where the buffer allows.
+template <int V>
+__global__ void __launch_bounds__(256) zero_fill_kernel(void *p, int64_t n_vec, int64_t bytes) {
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (V == 16) {
+    uint4 *q = reinterpret_cast<uint4 *>(p);
+    for (int64_t k = i; k < n_vec; k += stride) q[k] = make_uint4(0u, 0u, 0u, 0u);
+  } else {
+    uint32_t *q = reinterpret_cast<uint32_t *>(p);
+    for (int64_t k = i; k < n_vec; k += stride) q[k] = 0u;
+  }
+  // the bytes past the last whole vector
+  const int64_t t = n_vec * V + i;
+  if (t < bytes && i < V) reinterpret_cast<uint8_t *>(p)[t] = 0;
+}
+
+inline hipError_t zero_async(void *p, size_t bytes, hipStream_t st) {
+  if (bytes == 0) return hipSuccess;
+  const bool v16 = (reinterpret_cast<uintptr_t>(p) & 15) == 0;
+  const int V = v16 ? 16 : 4;
+  if (!v16 && (reinterpret_cast<uintptr_t>(p) & 3)) return hipErrorInvalidValue;
+  const int64_t n_vec = (int64_t)(bytes / V);
+  const int64_t blocks = std::min<int64_t>(std::max<int64_t>((n_vec + 255) / 256, 1), 2048);
+  if (v16)
+    hipLaunchKernelGGL(zero_fill_kernel<16>, dim3((unsigned)blocks), dim3(256), 0, st, p, n_vec,
+                       (int64_t)bytes);
+  else
+    hipLaunchKernelGGL(zero_fill_kernel<4>, dim3((unsigned)blocks), dim3(256), 0, st, p, n_vec,
+                       (int64_t)bytes);
+  return hipGetLastError();
+}
 
 // ------------------------------------------------------------------- Adam
 // torch.optim.Adam's element update (amsgrad=False, no weight decay):

@@ -426,7 +426,7 @@ extern "C" int gsplat_hip_isect_count(int64_t n_gaussians, const float *means2d,
   int64_t *ws = reinterpret_cast<int64_t *>(workspace);
   const int64_t nb = (n_gaussians + kIsectBlock - 1) / kIsectBlock;
   if (nb == 0) {
-    GS_HIP(hipMemsetAsync(totals_device, 0, 2 * sizeof(int64_t), st));
+    GS_HIP(gs::zero_async(totals_device, 2 * sizeof(int64_t), st));
     return 0;
   }
   int64_t *vis = ws + nb + 1;
@@ -498,7 +498,7 @@ extern "C" int gsplat_hip_isect_offsets(int64_t n_isects, const int64_t *n_isect
     return 0;
   }
   if (n_isects <= 0) {
-    GS_HIP(hipMemsetAsync(offsets, 0, sizeof(int32_t) * (size_t)C * n_tiles, st));
+    GS_HIP(gs::zero_async(offsets, sizeof(int32_t) * (size_t)C * n_tiles, st));
     return 0;
   }
   int tile_bits = 0;
@@ -951,7 +951,7 @@ extern "C" int gsplat_hip_isect_write_tilefirst(
                      n_tiles, tile_bits, starts);
   int32_t *large_list = starts + (n_total + 2);
   int32_t *n_large = reinterpret_cast<int32_t *>(ws + L.tmp);  // rocPRIM temp is free again
-  GS_HIP(hipMemsetAsync(n_large, 0, sizeof(int32_t), st));
+  GS_HIP(gs::zero_async(n_large, sizeof(int32_t), st));
   hipLaunchKernelGGL(isect_tile_sort_small_kernel, dim3((unsigned)(n_total + 1)), dim3(256), 0,
                      st, starts, sk, sv, depths, large_list, n_large, isect_ids, flatten_ids);
   hipLaunchKernelGGL(isect_tile_sort_large_kernel,

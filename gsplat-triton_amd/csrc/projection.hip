@@ -460,12 +460,12 @@ extern "C" int gsplat_hip_projection_bwd(
     float *v_viewmats, void *stream) {
   GS_REQUIRE(C >= 0 && N >= 0, "projection_bwd: negative sizes C=%d N=%d", C, N);
   hipStream_t st = (hipStream_t)stream;
-  if (v_viewmats && C > 0) GS_HIP(hipMemsetAsync(v_viewmats, 0, sizeof(float) * 16 * C, st));
+  if (v_viewmats && C > 0) GS_HIP(gs::zero_async(v_viewmats, sizeof(float) * 16 * C, st));
   if (N == 0) return 0;
   if (C == 0) {
-    GS_HIP(hipMemsetAsync(v_means, 0, sizeof(float) * 3 * N, st));
-    GS_HIP(hipMemsetAsync(v_quats, 0, sizeof(float) * 4 * N, st));
-    GS_HIP(hipMemsetAsync(v_scales, 0, sizeof(float) * 3 * N, st));
+    GS_HIP(gs::zero_async(v_means, sizeof(float) * 3 * N, st));
+    GS_HIP(gs::zero_async(v_quats, sizeof(float) * 4 * N, st));
+    GS_HIP(gs::zero_async(v_scales, sizeof(float) * 3 * N, st));
     return 0;
   }
   GS_REQUIRE(!compensations == !v_compensations,
@@ -474,9 +474,9 @@ extern "C" int gsplat_hip_projection_bwd(
              "projection_bwd: quats / v_quats must be 16-B aligned");
   const int store_mode = (C == 1);
   if (!store_mode) {
-    GS_HIP(hipMemsetAsync(v_means, 0, sizeof(float) * 3 * N, st));
-    GS_HIP(hipMemsetAsync(v_quats, 0, sizeof(float) * 4 * N, st));
-    GS_HIP(hipMemsetAsync(v_scales, 0, sizeof(float) * 3 * N, st));
+    GS_HIP(gs::zero_async(v_means, sizeof(float) * 3 * N, st));
+    GS_HIP(gs::zero_async(v_quats, sizeof(float) * 4 * N, st));
+    GS_HIP(gs::zero_async(v_scales, sizeof(float) * 3 * N, st));
   }
   ProjBwdArgs a{C, N, width, height, eps2d, means, quats, scales, viewmats, Ks, radii, conics,
                 compensations, v_means2d, v_depths, v_conics, v_compensations, v_means, v_quats,
@@ -513,7 +513,7 @@ extern "C" int gsplat_hip_projection_packed_count(int C, int N, const float *mea
   GS_REQUIRE(C >= 0 && N >= 0, "projection_packed_count: negative sizes C=%d N=%d", C, N);
   hipStream_t st = (hipStream_t)stream;
   if (C == 0 || N == 0) {
-    GS_HIP(hipMemsetAsync(nnz_device, 0, sizeof(int64_t), st));
+    GS_HIP(gs::zero_async(nnz_device, sizeof(int64_t), st));
     return 0;
   }
   GS_REQUIRE(means && quats && scales && viewmats && Ks && workspace && nnz_device,
@@ -566,11 +566,11 @@ extern "C" int gsplat_hip_projection_packed_bwd(
     float *v_quats, float *v_scales, float *v_viewmats, void *stream) {
   GS_REQUIRE(C >= 0 && N >= 0 && nnz >= 0, "projection_packed_bwd: negative sizes");
   hipStream_t st = (hipStream_t)stream;
-  if (v_viewmats && C > 0) GS_HIP(hipMemsetAsync(v_viewmats, 0, sizeof(float) * 16 * C, st));
+  if (v_viewmats && C > 0) GS_HIP(gs::zero_async(v_viewmats, sizeof(float) * 16 * C, st));
   if (!sparse_grad && N > 0) {
-    GS_HIP(hipMemsetAsync(v_means, 0, sizeof(float) * 3 * N, st));
-    GS_HIP(hipMemsetAsync(v_quats, 0, sizeof(float) * 4 * N, st));
-    GS_HIP(hipMemsetAsync(v_scales, 0, sizeof(float) * 3 * N, st));
+    GS_HIP(gs::zero_async(v_means, sizeof(float) * 3 * N, st));
+    GS_HIP(gs::zero_async(v_quats, sizeof(float) * 4 * N, st));
+    GS_HIP(gs::zero_async(v_scales, sizeof(float) * 3 * N, st));
   }
   if (nnz == 0) return 0;
   GS_REQUIRE(!compensations == !v_compensations,

@@ -446,11 +446,11 @@ extern "C" int gsplat_hip_rasterize_bwd(
                            v_means2d_abs, render_colors, records, state, state_bytes, workspace,
                            st);
   }
-  GS_HIP(hipMemsetAsync(v_means2d, 0, sizeof(float) * 2 * G, st));
-  GS_HIP(hipMemsetAsync(v_conics, 0, sizeof(float) * 3 * G, st));
-  GS_HIP(hipMemsetAsync(v_colors, 0, sizeof(float) * D * G, st));
-  GS_HIP(hipMemsetAsync(v_opacities, 0, sizeof(float) * G, st));
-  if (v_means2d_abs) GS_HIP(hipMemsetAsync(v_means2d_abs, 0, sizeof(float) * 2 * G, st));
+  GS_HIP(gs::zero_async(v_means2d, sizeof(float) * 2 * G, st));
+  GS_HIP(gs::zero_async(v_conics, sizeof(float) * 3 * G, st));
+  GS_HIP(gs::zero_async(v_colors, sizeof(float) * D * G, st));
+  GS_HIP(gs::zero_async(v_opacities, sizeof(float) * G, st));
+  if (v_means2d_abs) GS_HIP(gs::zero_async(v_means2d_abs, sizeof(float) * 2 * G, st));
   if ((int64_t)C * tile_width * tile_height == 0 || n_isects == 0) return 0;
   RasterArgs a{};
   a.C = C; a.W = width; a.H = height; a.ts = tile_size; a.tw = tile_width; a.th = tile_height;

@@ -2189,7 +2189,7 @@ int r16_bwd(r16::Args a, int64_t G, float *v_means2d, float *v_conics, float *v_
   a.packed = reinterpret_cast<float *>(workspace);
   const bool chunked = a.n_isects > 0 && a.state && a.L > 0 && a.render_colors_in;
   // one memset: the gradient rows and, right after them, the item counters
-  GS_HIP(hipMemsetAsync(a.packed, 0, packed_bytes(D, ABS, G) + (chunked ? 256 : 0), st));
+  GS_HIP(gs::zero_async(a.packed, packed_bytes(D, ABS, G) + (chunked ? 256 : 0), st));
   if (a.n_isects > 0) {
     int64_t grid = a.n_tiles;
     if (chunked) {

@@ -347,7 +347,7 @@ extern "C" int gsplat_hip_densify_plan(int64_t N, const float *grad2d, const flo
   uint8_t *flags = (uint8_t *)(bc + strat::kRows * nb);
   hipStream_t st = (hipStream_t)stream;
   if (N == 0) {
-    GS_HIP(hipMemsetAsync(totals, 0, strat::kRows * sizeof(int64_t), st));
+    GS_HIP(gs::zero_async(totals, strat::kRows * sizeof(int64_t), st));
     return 0;
   }
   strat::DensifyCfg cfg{grow_grad2d, grow_scale3d, prune_opa, prune_scale3d,

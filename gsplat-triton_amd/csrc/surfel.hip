@@ -1271,13 +1271,13 @@ extern "C" int gsplat_hip_projection_2dgs_bwd(
   hipStream_t st = (hipStream_t)stream;
   // the reference allocates v_viewmats but its kernel never writes it
   // (Projection2DGSFused.cu:319-457): zeros
-  if (v_viewmats && C > 0) GS_HIP(hipMemsetAsync(v_viewmats, 0, sizeof(float) * 16 * C, st));
+  if (v_viewmats && C > 0) GS_HIP(gs::zero_async(v_viewmats, sizeof(float) * 16 * C, st));
   if (N == 0) return 0;
   const int store_mode = (C == 1);
   if (!store_mode) {
-    GS_HIP(hipMemsetAsync(v_means, 0, sizeof(float) * 3 * N, st));
-    GS_HIP(hipMemsetAsync(v_quats, 0, sizeof(float) * 4 * N, st));
-    GS_HIP(hipMemsetAsync(v_scales, 0, sizeof(float) * 3 * N, st));
+    GS_HIP(gs::zero_async(v_means, sizeof(float) * 3 * N, st));
+    GS_HIP(gs::zero_async(v_quats, sizeof(float) * 4 * N, st));
+    GS_HIP(gs::zero_async(v_scales, sizeof(float) * 3 * N, st));
   }
   if (C == 0) return 0;
   GS_REQUIRE(means && quats && scales && viewmats && Ks && radii && ray_transforms &&
@@ -1312,7 +1312,7 @@ extern "C" int gsplat_hip_projection_2dgs_packed_count(
   GS_REQUIRE(C >= 0 && N >= 0, "projection_2dgs_packed_count: negative sizes C=%d N=%d", C, N);
   hipStream_t st = (hipStream_t)stream;
   if (C == 0 || N == 0) {
-    GS_HIP(hipMemsetAsync(nnz_device, 0, sizeof(int64_t), st));
+    GS_HIP(gs::zero_async(nnz_device, sizeof(int64_t), st));
     return 0;
   }
   GS_REQUIRE(means && quats && scales && viewmats && Ks && workspace && nnz_device,
@@ -1368,11 +1368,11 @@ extern "C" int gsplat_hip_projection_2dgs_packed_bwd(
   (void)height;
   GS_REQUIRE(C >= 0 && N >= 0 && nnz >= 0, "projection_2dgs_packed_bwd: negative sizes");
   hipStream_t st = (hipStream_t)stream;
-  if (v_viewmats && C > 0) GS_HIP(hipMemsetAsync(v_viewmats, 0, sizeof(float) * 16 * C, st));
+  if (v_viewmats && C > 0) GS_HIP(gs::zero_async(v_viewmats, sizeof(float) * 16 * C, st));
   if (!sparse_grad && N > 0) {
-    GS_HIP(hipMemsetAsync(v_means, 0, sizeof(float) * 3 * N, st));
-    GS_HIP(hipMemsetAsync(v_quats, 0, sizeof(float) * 4 * N, st));
-    GS_HIP(hipMemsetAsync(v_scales, 0, sizeof(float) * 3 * N, st));
+    GS_HIP(gs::zero_async(v_means, sizeof(float) * 3 * N, st));
+    GS_HIP(gs::zero_async(v_quats, sizeof(float) * 4 * N, st));
+    GS_HIP(gs::zero_async(v_scales, sizeof(float) * 3 * N, st));
   }
   if (nnz == 0) return 0;
   GS_REQUIRE(means && quats && scales && viewmats && Ks && camera_ids && gaussian_ids &&
@@ -1471,7 +1471,7 @@ extern "C" int gsplat_hip_rasterize_2dgs_bwd(
   GS_REQUIRE(workspace && v_means2d && v_ray_transforms && v_colors && v_opacities && v_normals &&
                  v_densify && ray_transforms,
              "rasterize_2dgs_bwd: null pointer argument");
-  GS_HIP(hipMemsetAsync(workspace, 0, (size_t)G * S * sizeof(float), st));
+  GS_HIP(gs::zero_async(workspace, (size_t)G * S * sizeof(float), st));
   const int n_tiles = C * tile_width * tile_height;
   if (n_tiles > 0 && n_isects > 0 && width > 0 && height > 0) {
     GS_REQUIRE(isect_offsets && flatten_ids && render_colors && render_alphas && last_ids &&
