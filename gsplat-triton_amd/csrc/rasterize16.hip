@@ -112,8 +112,6 @@ GS_INLINE f2v reduce_scatter2(const f2v *v, int lane) {
 // one 64-B sector per lane instead of four lines of four arrays
 // (rasterize_to_pixels_fwd.py:93-145 loads the four arrays separately).
 constexpr int kRecFloats = 16;
-constexpr int kHead = 32, kHeadStride = 32;  // queue[] layout (see Args::queue)
-constexpr int kQueueInts = kHead + 8 * kHeadStride;
 constexpr int kRecMaxD = kRecFloats - 6;
 
 struct Args {
@@ -138,12 +136,6 @@ struct Args {
   const int2 *items, *items_tail;
   const int32_t *n_items;
   const int32_t *order;  // forward: tile of workgroup b (heaviest tiles first) or null
-  // forward, XCD-aware dispatch (order_xcd_kernel): order[] holds 8 segments
-  // of spatially contiguous tiles; queue[0..8) their starts, [8..16) their
-  // lengths, queue[kHead + kHeadStride q] the dequeue head of segment q (one
-  // 128-B line each: heads sharing a line serialise the returning atomics,
-  // ~85 per us -- tools/xcc_probe.hip).  null: order[blockIdx.x]
-  int32_t *queue;
   // forward, split heavy tiles (fwd_plan_kernel): fitems[b] = (tile, -1) a
   // whole tile or (tile, k) chunk k of a split tile; p1items the chunks whose
   // transmittance product fwd_prod_kernel computes; heavy the split tiles as
@@ -327,33 +319,9 @@ GS_INLINE void read_rec(const float4 *slot, float (&r)[Rec<D, FWD>::NF]) {
   }
 }
 
-// The forward's tile of this workgroup.  With the XCD queues, segment x of
-// the tiles (a band of the image holding 1/8 of the work) is served to the
-// XCD whose id is x, so the Gaussians a band's tiles share stay in that XCD's
-// L2 (MI355X_MICROARCH.md "L2 (per XCD)"); an XCD whose band is exhausted
-// takes tiles from the next bands.  Every workgroup gets exactly one tile:
-// the queues hold n_tiles tiles and the grid is n_tiles workgroups.  The XCD
-// id only steers speed -- the result of a tile does not depend on who runs it.
-GS_INLINE int fwd_tile(const Args &a) {
-  if (!a.queue) return a.order ? a.order[blockIdx.x] : (int)blockIdx.x;
-  __shared__ int s_tile;
-  if (threadIdx.x == 0) {
-    const int x = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 7;  // HW_REG_XCC_ID
-    int t = -1;
-    for (int k = 0; k < 8 && t < 0; ++k) {
-      const int q = (x + k) & 7;
-      int *head = &a.queue[kHead + kHeadStride * q];
-      const int len = a.queue[8 + q];
-      // a stale read is low (heads only grow): skipping on it is always right
-      if (__atomic_load_n(head, __ATOMIC_RELAXED) >= len) continue;
-      const int i = atomicAdd(head, 1);
-      if (i < len) t = a.order[a.queue[q] + i];
-    }
-    s_tile = t;
-  }
-  __syncthreads();
-  return s_tile;
-}
+// The forward's tile of this workgroup: heaviest tiles first when the
+// dispatch order is present (tile_order_kernel).
+GS_INLINE int fwd_tile(const Args &a) { return a.order ? a.order[blockIdx.x] : (int)blockIdx.x; }
 
 // Geometry of one wave: 4 waves share a 16x16 tile, each owning a 16x4
 // strip; lane l owns pixel column (l & 15), row strip_y0 + (l >> 4).
@@ -456,18 +424,16 @@ GS_INLINE void stage_bwd_pad(float4 *st, int slot) {
     if (f != 6 && f != 8) w[2 * f] = 0.f;
 }
 
-// U: pairs per iteration of the composite loop (explicitly unrolled: their
-// LDS reads issue together and pair p+1's alpha math issues under pair p's
-// blend chain); register budget 80 VGPRs = 6 waves per SIMD for U = 1,
-// 96 / 5 for U = 2, 128 / 4 for U = 4.
-// PF: gather depth.  1: the attributes of batch b+1 are gathered while batch
-// b composites (two register buffers); 2: those of b+1 and b+2 (three
-// buffers, one wave per SIMD fewer); 0: only the flatten ids are prefetched,
-// the gather waits at the batch start, and 18 fewer VGPRs allow two more
-// waves.  At M2 / M3: PF 0 0.198 / 0.686 ms, PF 1 0.184-0.193 / 0.590.
-template <int D, int U = 1, int PF = 1>
-__global__ void __launch_bounds__(256)
-__attribute__((amdgpu_waves_per_eu((U == 1 ? 5 : U == 2 ? 4 : 3) + (PF == 0 ? 2 : PF == 2 ? -1 : 0)))) fwd_kernel(Args a) {
+// One pair per iteration of the composite loop (80 VGPRs, 5-6 waves per
+// SIMD).  Unrolling 2 or 4 pairs (their LDS reads together, the next pair's
+// alpha math under this pair's blend chain) measured 0.193 / 0.23 ms against
+// 0.184 at M2: the extra VGPRs cost more waves than the overlap gained.
+// Gather depth one batch: the attributes of batch b+1 are gathered while
+// batch b composites (two register buffers).  Depth 0 (only the flatten ids
+// ahead, two more waves) measured 0.198 / 0.686 ms at M2 / M3 against 0.184 /
+// 0.590, depth 2 (three buffers) no better than 1.
+template <int D>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) fwd_kernel(Args a) {
   using P = FwdPair<D>;
   constexpr int N4 = P::N4;
   __shared__ float4 stage_all[4][32 * N4];
@@ -482,7 +448,6 @@ __attribute__((amdgpu_waves_per_eu((U == 1 ? 5 : U == 2 ? 4 : 3) + (PF == 0 ? 2 
     kc = it.y;
   } else {
     tile_ = fwd_tile(a);
-    if (tile_ < 0) return;  // unreachable: the queues hold one tile per workgroup
   }
   const WaveGeom geo(a, lane, tile_);
   const int tile = geo.tile, c = geo.c;
@@ -494,7 +459,6 @@ __attribute__((amdgpu_waves_per_eu((U == 1 ? 5 : U == 2 ? 4 : 3) + (PF == 0 ? 2 
   const int64_t end = kc >= 0 ? min(tend, start + (int64_t)a.SL) : tend;
   const bool skip_tile = a.masks && a.masks[tile];
 
-  // colour accumulated from even (.x) and odd (.y) records of each pair
   // colour accumulated from even (.x) and odd (.y) records of each pair in the
   // current chunk; tot: the chunks before it (see "chunk state" below)
   f2v acc[D];
@@ -541,47 +505,34 @@ __attribute__((amdgpu_waves_per_eu((U == 1 ? 5 : U == 2 ? 4 : 3) + (PF == 0 ? 2 
       last = ok ? __float_as_int(idx) : last;
       return vis;
     };
-    // composite one staged batch: its pairs, padded to a multiple of U with
-    // never-hitting pairs (stage), U pairs per iteration -- all their LDS
-    // reads issue first and U independent alpha computations overlap the
-    // serial blend chain -- checking every 8 pairs whether the strip is alive
+    // composite one staged batch pair by pair, checking every 8 pairs
+    // whether the strip is alive
     auto composite = [&](int cnt) {
-      const int np = (((cnt + 1) >> 1) + U - 1) / U * U;
+      const int np = (cnt + 1) >> 1;
       for (int pb = 0; pb < np; pb += 8) {
         const int pe = min(np, pb + 8);
-        for (int p = pb; p < pe; p += U) {
-          f2v f[U][2 * N4];
-          float4 v[U][N4];
+        for (int p = pb; p < pe; ++p) {
+          f2v f[2 * N4];
+          float4 v[N4];
 #pragma unroll
-          for (int u = 0; u < U; ++u)
+          for (int i = 0; i < N4; ++i) v[i] = st[p * N4 + i];
 #pragma unroll
-            for (int i = 0; i < N4; ++i) v[u][i] = st[(p + u) * N4 + i];
-#pragma unroll
-          for (int u = 0; u < U; ++u)
-#pragma unroll
-            for (int i = 0; i < N4; ++i) {
-              // keep every field live: no load may sink into a select's branch
-              asm volatile("" ::"v"(v[u][i].x), "v"(v[u][i].y), "v"(v[u][i].z), "v"(v[u][i].w));
-              f[u][2 * i] = f2v{v[u][i].x, v[u][i].y};
-              f[u][2 * i + 1] = f2v{v[u][i].z, v[u][i].w};
-            }
-          f2v s2[U], al[U];
-#pragma unroll
-          for (int u = 0; u < U; ++u) {
-            const f2v dx = f[u][0] - fx, dy = f[u][1] - fy;
-            s2[u] = dx * (f[u][2] * dx + f[u][3] * dy) + f[u][4] * dy * dy;  // sigma * log2(e)
-            al[u] = f[u][5] * f2v{__builtin_amdgcn_exp2f(-s2[u].x), __builtin_amdgcn_exp2f(-s2[u].y)};
-            al[u].x = fminf(al[u].x, kAlphaMax);
-            al[u].y = fminf(al[u].y, kAlphaMax);
+          for (int i = 0; i < N4; ++i) {
+            // keep every field live: no load may sink into a select's branch
+            asm volatile("" ::"v"(v[i].x), "v"(v[i].y), "v"(v[i].z), "v"(v[i].w));
+            f[2 * i] = f2v{v[i].x, v[i].y};
+            f[2 * i + 1] = f2v{v[i].z, v[i].w};
           }
+          const f2v dx = f[0] - fx, dy = f[1] - fy;
+          const f2v s2 = dx * (f[2] * dx + f[3] * dy) + f[4] * dy * dy;  // sigma * log2(e)
+          f2v al = f[5] * f2v{__builtin_amdgcn_exp2f(-s2.x), __builtin_amdgcn_exp2f(-s2.y)};
+          al.x = fminf(al.x, kAlphaMax);
+          al.y = fminf(al.y, kAlphaMax);
+          const float v0 = blend(s2.x, f[6].x, al.x, f[7].x);
+          const float v1 = blend(s2.y, f[6].y, al.y, f[7].y);
+          const f2v vis = f2v{v0, v1};
 #pragma unroll
-          for (int u = 0; u < U; ++u) {
-            const float v0 = blend(s2[u].x, f[u][6].x, al[u].x, f[u][7].x);
-            const float v1 = blend(s2[u].y, f[u][6].y, al[u].y, f[u][7].y);
-            const f2v vis = f2v{v0, v1};
-#pragma unroll
-            for (int d = 0; d < D; ++d) acc[d] = __builtin_elementwise_fma(vis, f[u][8 + d], acc[d]);
-          }
+          for (int d = 0; d < D; ++d) acc[d] = __builtin_elementwise_fma(vis, f[8 + d], acc[d]);
         }
         if (__ballot(T > 0.f) == 0) {
           done = true;
@@ -594,9 +545,8 @@ __attribute__((amdgpu_waves_per_eu((U == 1 ? 5 : U == 2 ? 4 : 3) + (PF == 0 ? 2 
       const uint64_t m = __ballot(keep);
       const int cnt = __popcll(m);
       if (keep) stage_fwd_pair<D>(st, ballot_slot(m), at, (int32_t)(b0 + lane));
-      // pad slots up to a multiple of 2U records (<= 64: U divides 32)
-      const int npad = ((cnt + 2 * U - 1) / (2 * U)) * (2 * U) - cnt;
-      if (lane < npad) stage_fwd_pad<D>(st, cnt + lane);
+      // the odd slot of a final half-filled pair
+      if ((cnt & 1) && lane == 0) stage_fwd_pad<D>(st, cnt);
       wave_sync_lds();
       return cnt;
     };
@@ -628,49 +578,12 @@ __attribute__((amdgpu_waves_per_eu((U == 1 ? 5 : U == 2 ? 4 : 3) + (PF == 0 ? 2 
     // and the colour it adds at its own start boundary
     const bool chunked = a.state && L > 0 && (end - start > L || kc > 0);
     int64_t b0 = start;
-    if constexpr (PF == 0) {
-      int32_t g_n = id_at(start);
-      while (b0 < end) {
-        if (__ballot(T > 0.f) == 0) break;
-        if (chunked && b0 > start && (b0 - start) % L == 0) save_state(b0);
-        Attr<D> A;
-        load_attr<D>(a, g_n, A);
-        g_n = id_at(b0 + 64);
-        composite(stage(A, b0));
-        wave_sync_lds();
-        b0 += 64;
-        if (done) break;
-      }
-    }
     // two attribute buffers in alternation: while batch b is composited from
     // one, the other receives batch b+1, and the ids of batch b+2 load
-    if constexpr (PF == 2) {
-      // three buffers in rotation: batch b composites while b+1 and b+2 are
-      // in flight and the ids of b+3 load
-      Attr<D> A, B, C;
-      load_attr<D>(a, id_at(start), A);
-      load_attr<D>(a, id_at(start + 64), B);
-      int32_t g_n = id_at(start + 128);
-      auto step = [&](const Attr<D> &cur, Attr<D> &fill) -> bool {  // false: stop
-        if (__ballot(T > 0.f) == 0) return false;
-        if (chunked && b0 > start && (b0 - start) % L == 0) save_state(b0);
-        load_attr<D>(a, g_n, fill);
-        g_n = id_at(b0 + 192);
-        composite(stage(cur, b0));
-        wave_sync_lds();
-        b0 += 64;
-        return !done && b0 < end;
-      };
-      while (step(A, C) && step(B, A) && step(C, B)) {
-      }
-    }
     Attr<D> A, B;
-    int32_t g_n = 0;
-    if constexpr (PF == 1) {
-      load_attr<D>(a, id_at(start), A);
-      g_n = id_at(start + 64);
-    }
-    while (PF == 1 && b0 < end) {
+    load_attr<D>(a, id_at(start), A);
+    int32_t g_n = id_at(start + 64);
+    while (b0 < end) {
       if (__ballot(T > 0.f) == 0) break;
       if (chunked && b0 > start && (b0 - start) % L == 0) save_state(b0);
       load_attr<D>(a, g_n, B);
@@ -837,202 +750,6 @@ __global__ void __launch_bounds__(256) fwd_combine_kernel(Args a) {
   }
   a.render_alphas[pix] = 1.f - Tf;
   a.last_ids[pix] = last;
-}
-
-// Forward, two pixels per lane: a wave owns the 16x8 band of rows 8w..8w+7
-// of its tile, lane l the pixels (l & 15, 8w + (l >> 4)) and 4 rows below;
-// the two waves of a workgroup cover the tile.  Each lane runs two
-// independent transmittance chains over the same records, which hides the
-// per-record dependency latency that bounds the one-pixel kernel, and the
-// gather, strip culling and LDS reads of a record are shared by both
-// pixels.  Same per-pixel arithmetic as fwd_kernel; not the default (see
-// fwd_px()).
-template <int D>
-// register budget: 168 VGPRs = 3 waves per SIMD
-__global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(3))) fwd2_kernel(Args a) {
-  using P = FwdPair<D>;
-  constexpr int N4 = P::N4;
-  __shared__ float4 stage_all[2][32 * N4];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  float4 *st = stage_all[w];
-  const uint64_t t_start = tl_now(a);
-  const int tile = fwd_tile(a);
-  if (tile < 0) return;
-  const int ntile = a.tw * a.th;
-  const int c = tile / ntile;
-  const int rem = tile - c * ntile;
-  const int ty = rem / a.tw, tx = rem - ty * a.tw;
-  const int px = tx * kTS + (lane & 15);
-  const int py0 = ty * kTS + 8 * w + (lane >> 4);
-  const float rx0 = tx * kTS + 0.5f, rx1 = rx0 + (kTS - 1);
-  const float ry0 = ty * kTS + 8 * w + 0.5f, ry1 = ry0 + 7.f;
-  const float fx = (float)px + 0.5f;
-  const int64_t start = a.offsets[tile];
-  const int64_t end = tile_end(a, tile);
-  const bool skip_tile = a.masks && a.masks[tile];
-
-  // per pixel k: colour of even (.x) / odd (.y) records of each pair in the
-  // current chunk, tot: the chunks before it; T < 0 marks a finished pixel
-  f2v acc[2][D];
-  float tot[2][D], T[2], fy[2];
-  int32_t last[2];
-  bool inside[2];
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const int py = py0 + 4 * k;
-    fy[k] = (float)py + 0.5f;
-    inside[k] = px < a.W && py < a.H;
-    T[k] = (!inside[k] || skip_tile) ? -1.f : 1.f;
-    last[k] = 0;
-#pragma unroll
-    for (int d = 0; d < D; ++d) {
-      acc[k][d] = f2v{0.f, 0.f};
-      tot[k][d] = 0.f;
-    }
-  }
-  auto alive = [&]() { return __ballot((T[0] > 0.f) | (T[1] > 0.f)) != 0; };
-
-  if (!skip_tile && start < end) {
-    auto id_at = [&](int64_t b0) -> int32_t {
-      return a.flatten_ids[min(b0 + lane, end - 1)];
-    };
-    bool done = false;
-    auto blend = [&](int k, float s2, float smax, float al, float idx) -> float {
-      const float nT = __builtin_fmaf(-T[k], al, T[k]);
-      const bool hit = __float_as_uint(s2) <= __float_as_uint(smax);
-      const bool gt = nT > kTMin;
-      const bool ok = hit & gt;
-      const float Tsel = ok ? nT : T[k];
-      const float vis = T[k] - Tsel;
-      T[k] = (hit & !gt) ? -fabsf(T[k]) : Tsel;
-      last[k] = ok ? __float_as_int(idx) : last[k];
-      return vis;
-    };
-    auto composite = [&](int cnt) {
-      const int np = (cnt + 1) >> 1;
-      for (int pb = 0; pb < np; pb += 8) {
-        const int pe = min(np, pb + 8);
-        for (int p = pb; p < pe; ++p) {
-          const float4 *q = st + p * N4;
-          f2v f[2 * N4];
-          float4 v[N4];
-#pragma unroll
-          for (int i = 0; i < N4; ++i) v[i] = q[i];
-#pragma unroll
-          for (int i = 0; i < N4; ++i) {
-            asm volatile("" ::"v"(v[i].x), "v"(v[i].y), "v"(v[i].z), "v"(v[i].w));
-            f[2 * i] = f2v{v[i].x, v[i].y};
-            f[2 * i + 1] = f2v{v[i].z, v[i].w};
-          }
-          const f2v dx = f[0] - fx;
-          const f2v adx = f[2] * dx;
-#pragma unroll
-          for (int k = 0; k < 2; ++k) {
-            const f2v dy = f[1] - fy[k];
-            const f2v s2 = dx * (adx + f[3] * dy) + f[4] * dy * dy;  // sigma * log2(e)
-            f2v al = f[5] * f2v{__builtin_amdgcn_exp2f(-s2.x), __builtin_amdgcn_exp2f(-s2.y)};
-            al.x = fminf(al.x, kAlphaMax);
-            al.y = fminf(al.y, kAlphaMax);
-            const float v0 = blend(k, s2.x, f[6].x, al.x, f[7].x);
-            const float v1 = blend(k, s2.y, f[6].y, al.y, f[7].y);
-            const f2v vis = f2v{v0, v1};
-#pragma unroll
-            for (int d = 0; d < D; ++d)
-              acc[k][d] = __builtin_elementwise_fma(vis, f[8 + d], acc[k][d]);
-          }
-        }
-        if (!alive()) {
-          done = true;
-          return;
-        }
-      }
-    };
-    auto stage = [&](const Attr<D> &at, int64_t b0) -> int {
-      const bool keep = (b0 + lane < end) && keep_attr<D>(at, rx0, rx1, ry0, ry1);
-      const uint64_t m = __ballot(keep);
-      const int cnt = __popcll(m);
-      if (keep) stage_fwd_pair<D>(st, ballot_slot(m), at, (int32_t)(b0 + lane));
-      if ((cnt & 1) && lane == 0) stage_fwd_pad<D>(st, cnt);
-      wave_sync_lds();
-      return cnt;
-    };
-    // chunk state for the chunked backward, as fwd_kernel
-    const int64_t L = a.L;
-    auto slot = [&](int64_t bidx) { return a.state + (bidx / L) * (int64_t)(kTS * kTS * (1 + D)); };
-    int64_t cur_b = start;
-    auto close_chunk = [&]() {
-      float *sl = slot(cur_b);
-#pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        const int pit = 128 * w + 64 * k + lane;  // row-major pixel of the tile
-#pragma unroll
-        for (int d = 0; d < D; ++d) {
-          const float cs = acc[k][d].x + acc[k][d].y;
-          if (cur_b > start) sl[(1 + d) * kTS * kTS + pit] = cs;
-          tot[k][d] += cs;
-          acc[k][d] = f2v{0.f, 0.f};
-        }
-      }
-    };
-    auto save_state = [&](int64_t bidx) {
-      close_chunk();
-      cur_b = bidx;
-#pragma unroll
-      for (int k = 0; k < 2; ++k) slot(bidx)[128 * w + 64 * k + lane] = T[k];
-    };
-    const bool chunked = a.state && L > 0 && end - start > L;
-    Attr<D> A, B;
-    load_attr<D>(a, id_at(start), A);
-    int32_t g_n = id_at(start + 64);
-    int64_t b0 = start;
-    while (b0 < end) {
-      if (!alive()) break;
-      if (chunked && b0 > start && (b0 - start) % L == 0) save_state(b0);
-      load_attr<D>(a, g_n, B);
-      g_n = id_at(b0 + 128);
-      composite(stage(A, b0));
-      wave_sync_lds();
-      b0 += 64;
-      if (done || b0 >= end) break;
-      if (chunked && (b0 - start) % L == 0) save_state(b0);
-      load_attr<D>(a, g_n, A);
-      g_n = id_at(b0 + 128);
-      composite(stage(B, b0));
-      wave_sync_lds();
-      b0 += 64;
-      if (done) break;
-    }
-    if (chunked) {
-      close_chunk();
-      for (int64_t bi = cur_b + L; bi < end; bi += L) {
-        float *sl = slot(bi);
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-          const int pit = 128 * w + 64 * k + lane;
-          sl[pit] = T[k];
-#pragma unroll
-          for (int d = 0; d < D; ++d) sl[(1 + d) * kTS * kTS + pit] = 0.f;
-        }
-      }
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-#pragma unroll
-    for (int d = 0; d < D; ++d) tot[k][d] += acc[k][d].x + acc[k][d].y;
-    if (inside[k]) {
-      const int64_t pix = ((int64_t)c * a.H + py0 + 4 * k) * a.W + px;
-      float *oc = a.render_colors + pix * D;
-#pragma unroll
-      for (int d = 0; d < D; ++d) {
-        const float bg = a.backgrounds ? a.backgrounds[c * D + d] : 0.f;
-        oc[d] = tot[k][d] + fabsf(T[k]) * bg;
-      }
-      a.render_alphas[pix] = 1.f - fabsf(T[k]);
-      a.last_ids[pix] = last[k];
-    }
-  }
-  tl_store(a, t_start, lane);
 }
 
 // Backward: batches of 64 isects from the back, same two-deep gather pipeline.
@@ -1568,105 +1285,6 @@ tile_order_kernel(int n_tiles, const int32_t *__restrict__ offsets, int64_t n_is
   }
 }
 
-// XCD-aware forward dispatch order.  Tile t (raster order, cameras
-// concatenated) goes to segment min(7, 8 w(t) / W) with w(t) = offsets[t] +
-// kTileCost t the work before it (isects plus a per-tile cost) and W the
-// total, so the 8 segments are bands of the image with equal work.  Inside a
-// segment the tiles are bucketed as in tile_order_kernel (>= 2048, >= 1024,
-// >= 512 isects, the rest: heaviest first), raster order inside a bucket.
-// Output: order[] sorted by (segment, bucket, tile); queue[q] = start of
-// segment q, queue[8+q] = its length, its dequeue head = 0.
-// One 1024-lane workgroup, 16 consecutive tiles per lane (n_tiles <= 16384);
-// the 32 (segment, bucket) counts of a lane are packed 4 per u64 (16 bits).
-constexpr int kTileCost = 32;
-
-__global__ void __launch_bounds__(1024)
-order_xcd_kernel(int n_tiles, const int32_t *__restrict__ offsets, int64_t n_isects,
-                 const int64_t *__restrict__ n_dev, int32_t *__restrict__ order,
-                 int32_t *__restrict__ queue) {
-  constexpr int PER = 16;
-  __shared__ uint64_t wsum[16][8];
-  __shared__ int base[32];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int64_t W = isect_count(n_dev, n_isects) + (int64_t)kTileCost * n_tiles;
-  int key[PER];
-  uint64_t c[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) c[j] = 0;
-#pragma unroll
-  for (int i = 0; i < PER; ++i) {
-    const int t = tid * PER + i;
-    key[i] = -1;
-    if (t < n_tiles) {
-      const int64_t o = offsets[t];
-      const int64_t e = tile_end(offsets, t, n_tiles, n_dev, n_isects);
-      const int64_t n = e - o;
-      const int seg = (int)min((int64_t)7, (8 * (o + (int64_t)kTileCost * t)) / max(W, (int64_t)1));
-      const int bk = n >= 2048 ? 0 : n >= 1024 ? 1 : n >= 512 ? 2 : 3;
-      key[i] = 4 * seg + bk;
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        c[j] += (key[i] >> 2) == j ? (uint64_t)1 << (16 * (key[i] & 3)) : 0;
-    }
-  }
-  uint64_t x[8];  // inclusive lane scan of the packed counts
-#pragma unroll
-  for (int j = 0; j < 8; ++j) x[j] = c[j];
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const uint64_t y = __shfl_up(x[j], o, 64);
-      if (lane >= o) x[j] += y;
-    }
-  }
-  if (lane == 63) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) wsum[w][j] = x[j];
-  }
-  __syncthreads();
-  if (tid < 32) {  // exclusive scan over the 32 keys of the block totals
-    int tot = 0;
-    for (int k = 0; k < tid; ++k) {
-      uint64_t s = 0;
-      for (int ww = 0; ww < 16; ++ww) s += wsum[ww][k >> 2];
-      tot += (int)((s >> (16 * (k & 3))) & 0xffff);
-    }
-    base[tid] = tot;
-    if ((tid & 3) == 0) {  // segment q = tid / 4: start, length, head
-      uint64_t s = 0;
-      for (int ww = 0; ww < 16; ++ww) s += wsum[ww][tid >> 2];
-      int len = 0;
-#pragma unroll
-      for (int b = 0; b < 4; ++b) len += (int)((s >> (16 * b)) & 0xffff);
-      queue[tid >> 2] = tot;
-      queue[8 + (tid >> 2)] = len;
-      queue[kHead + kHeadStride * (tid >> 2)] = 0;
-    }
-  }
-  __syncthreads();
-  uint64_t before[8];  // this lane's exclusive prefix: earlier waves + earlier lanes
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    uint64_t b = x[j] - c[j];
-    for (int ww = 0; ww < w; ++ww) b += wsum[ww][j];
-    before[j] = b;
-  }
-#pragma unroll
-  for (int i = 0; i < PER; ++i) {
-    const int k = key[i];
-    if (k >= 0) {
-      uint64_t word = 0;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) word = (k >> 2) == j ? before[j] : word;
-      int p = base[k] + (int)((word >> (16 * (k & 3))) & 0xffff);
-#pragma unroll
-      for (int i2 = 0; i2 < i; ++i2) p += key[i2] == k;
-      order[p] = tid * PER + i;
-    }
-  }
-}
-
 // Forward plan with split heavy tiles.  A tile with more than `split` isects
 // (and not masked) is rendered as ceil(n / L) chunks that run in parallel
 // (fwd_prod_kernel -> fwd_kernel chunk items -> fwd_combine_kernel), so the
@@ -1897,19 +1515,6 @@ static bool use_order(int n_tiles, int64_t n_isects) {
   return n_isects > 0 && n_tiles > 0 && n_tiles <= 16384;
 }
 
-// XCD-aware forward dispatch (order_xcd_kernel, GSPLAT_HIP_XCD=1); default:
-// the heaviest-first order of tile_order_kernel.  With render records the
-// XCD bands measured slower at M2 (fwd 0.30 vs 0.19 ms) and M3 (0.77 vs 0.61
-// ms): the records already cut the gather to one sector per isect, and the
-// per-band order starts the globally heaviest tiles later.
-static bool use_xcd() {
-  static const bool v = [] {
-    const char *e = getenv("GSPLAT_HIP_XCD");
-    return e && atoi(e) == 1;
-  }();
-  return v;
-}
-
 // Split heavy tiles in the forward (fwd_plan_kernel): a tile with more
 // isects than the threshold is rendered as parallel chunks of split_chunk()
 // isects, so that it no longer runs alone for the end of the launch.  Mode
@@ -1969,13 +1574,10 @@ struct SplitLayout {
 
 static int64_t align256(int64_t x) { return (x + 255) / 256 * 256; }
 
-static int fwd_px();
-
 // The state has room for the split forward whenever it can run; whether a
 // render splits is decided per render (use_split_now).
 static bool split_capable(int n_tiles, int64_t n_isects) {
-  return fwd_split_mode() != 0 && chunk_len() > 0 && use_order(n_tiles, n_isects) &&
-         fwd_px() == 1;
+  return fwd_split_mode() != 0 && chunk_len() > 0 && use_order(n_tiles, n_isects);
 }
 
 // Largest tile of the most recent dispatch-order kernel, written by the
@@ -2023,7 +1625,7 @@ static SplitLayout split_layout(int D, int n_tiles, int64_t n_isects) {
 }
 
 static int64_t order_bytes(int n_tiles, int64_t n_isects) {
-  return use_order(n_tiles, n_isects) ? align256(4 * ((int64_t)n_tiles + r16::kQueueInts)) : 0;
+  return use_order(n_tiles, n_isects) ? align256(4 * (int64_t)n_tiles) : 0;
 }
 
 int64_t rasterize16_fwd_state_bytes(int D, int n_tiles, int64_t n_isects) {
@@ -2061,38 +1663,11 @@ static bool bwd_pf() {
   return v;
 }
 
-// Pixels per lane in the forward (1: fwd_kernel, 16x4 per wave, default;
-// 2: fwd2_kernel, 16x8 per wave, GSPLAT_HIP_FWD_PX=2).  At M2 the two-pixel
-// kernel measured 0.29 ms against 0.216 ms (158 VGPRs, 3 waves per SIMD, and
-// the heaviest tiles' serial work per wave doubles) -- unlike the 2DGS
-// forward, where two pixels per lane won 32 %.
-static int fwd_px() {
-  static const int v = [] {
-    const char *e = getenv("GSPLAT_HIP_FWD_PX");
-    return (e && atoi(e) == 2) ? 2 : 1;
-  }();
-  return v;
-}
-
-// Unroll of the forward's pair loop (GSPLAT_HIP_FWD_UNROLL = 1, 2, 4).
-static int fwd_unroll() {
-  static const int v = [] {
-    const char *e = getenv("GSPLAT_HIP_FWD_UNROLL");
-    const int x = e ? atoi(e) : 1;
-    return (x == 2 || x == 4) ? x : 1;
-  }();
-  return v;
-}
-
-// Gather depth of the forward (GSPLAT_HIP_FWD_PF = 0, 1, 2; see fwd_kernel).
-static int fwd_pf() {
-  static const int v = [] {
-    const char *e = getenv("GSPLAT_HIP_FWD_PF");
-    const int x = e ? atoi(e) : 1;
-    return (x == 0 || x == 2) ? x : 1;
-  }();
-  return v;
-}
+// One pixel per lane in the forward (16x4 per wave).  A two-pixel kernel
+// (16x8 per wave, two transmittance chains per lane) measured 0.29 ms against
+// 0.216 at M2 (158 VGPRs, 3 waves per SIMD, and the heaviest tiles' serial
+// work per wave doubles) -- unlike the 2DGS forward, where two pixels per
+// lane won 32 % -- and was removed.
 
 static int dbg_flags() {
   static const int v = [] { const char *e = getenv("GSPLAT_HIP_DBG"); return e ? atoi(e) : 0; }();
@@ -2116,10 +1691,7 @@ static void launch_order(int n_tiles, const int32_t *offsets, int64_t n_isects,
                        reinterpret_cast<int2 *>(split_base + l.fitems),
                        reinterpret_cast<int2 *>(split_base + l.p1),
                        reinterpret_cast<int2 *>(split_base + l.heavy), stat_dev());
-  } else if (use_xcd())
-    hipLaunchKernelGGL(r16::order_xcd_kernel, dim3(1), dim3(1024), 0, st, n_tiles, offsets,
-                       n_isects, n_dev, order, order + n_tiles);
-  else
+  } else
     hipLaunchKernelGGL(r16::tile_order_kernel, dim3(1), dim3(1024), 0, st, n_tiles, offsets,
                        n_isects, n_dev, order,
                        split_capable(n_tiles, n_isects) ? stat_dev() : nullptr);
@@ -2140,38 +1712,13 @@ int r16_fwd(r16::Args a, const void *state, char *split_base, hipStream_t st) {
         std::min<int64_t>(a.n_tiles, a.n_isects / split_threshold(a.n_isects) + 1);
     hipLaunchKernelGGL((r16::fwd_prod_kernel<D>), dim3((unsigned)std::min<int64_t>(nc, 2048)),
                        dim3(256), 0, st, a);
-    if (fwd_unroll() == 1 && fwd_pf() == 0)
-      hipLaunchKernelGGL((r16::fwd_kernel<D, 1, 0>), dim3((unsigned)(a.n_tiles + nc)), dim3(256),
-                         0, st, a);
-    else if (fwd_unroll() == 1 && fwd_pf() == 2)
-      hipLaunchKernelGGL((r16::fwd_kernel<D, 1, 2>), dim3((unsigned)(a.n_tiles + nc)), dim3(256),
-                         0, st, a);
-    else if (fwd_unroll() == 1)
-      hipLaunchKernelGGL((r16::fwd_kernel<D, 1>), dim3((unsigned)(a.n_tiles + nc)), dim3(256), 0,
-                         st, a);
-    else if (fwd_unroll() == 2)
-      hipLaunchKernelGGL((r16::fwd_kernel<D, 2>), dim3((unsigned)(a.n_tiles + nc)), dim3(256), 0,
-                         st, a);
-    else
-      hipLaunchKernelGGL((r16::fwd_kernel<D, 4>), dim3((unsigned)(a.n_tiles + nc)), dim3(256), 0,
-                         st, a);
+    hipLaunchKernelGGL((r16::fwd_kernel<D>), dim3((unsigned)(a.n_tiles + nc)), dim3(256), 0, st, a);
     hipLaunchKernelGGL((r16::fwd_combine_kernel<D>), dim3((unsigned)n_heavy_max), dim3(256), 0, st,
                        a);
     GS_CHECK_LAUNCH("rasterize_fwd16_split");
     return 0;
   }
-  if (fwd_px() == 2)
-    hipLaunchKernelGGL((r16::fwd2_kernel<D>), dim3(a.n_tiles), dim3(128), 0, st, a);
-  else if (fwd_unroll() == 1 && fwd_pf() == 0)
-    hipLaunchKernelGGL((r16::fwd_kernel<D, 1, 0>), dim3(a.n_tiles), dim3(256), 0, st, a);
-  else if (fwd_unroll() == 1 && fwd_pf() == 2)
-    hipLaunchKernelGGL((r16::fwd_kernel<D, 1, 2>), dim3(a.n_tiles), dim3(256), 0, st, a);
-  else if (fwd_unroll() == 1)
-    hipLaunchKernelGGL((r16::fwd_kernel<D, 1>), dim3(a.n_tiles), dim3(256), 0, st, a);
-  else if (fwd_unroll() == 2)
-    hipLaunchKernelGGL((r16::fwd_kernel<D, 2>), dim3(a.n_tiles), dim3(256), 0, st, a);
-  else
-    hipLaunchKernelGGL((r16::fwd_kernel<D, 4>), dim3(a.n_tiles), dim3(256), 0, st, a);
+  hipLaunchKernelGGL((r16::fwd_kernel<D>), dim3(a.n_tiles), dim3(256), 0, st, a);
   GS_CHECK_LAUNCH("rasterize_fwd16");
   return 0;
 }
@@ -2269,8 +1816,6 @@ int rasterize16_fwd(int C, int D, int W, int H, int tw, int th, const float *mea
     a.SL = split_chunk();
     a.timeline = nullptr;  // per-wave stamps index blocks of the unsplit grid
   }
-  a.queue = (a.order && use_xcd() && !split_base) ? const_cast<int32_t *>(a.order) + a.n_tiles
-                                                  : nullptr;
   switch (D) {
     case 1: return r16_fwd<1>(a, state, split_base, st);
     case 2: return r16_fwd<2>(a, state, split_base, st);

@@ -5,14 +5,11 @@ only, never results.
   through the packed 64-B records is bit-identical to the forward gathering
   the four attribute arrays (the same floats reach the same arithmetic), and
   the backward agrees up to the order of its float atomics;
-* XCD-aware dispatch (order_xcd_kernel): the order is a permutation of the
-  tiles, its 8 segments are consecutive raster ranges holding about 1/8 of the
-  work each, heaviest bucket first inside a segment, raster order inside a
-  bucket, and the dequeue heads start at 0.
+* the forward's dispatch order (tile_order_kernel): a permutation of the
+  tiles, heaviest bucket first, raster order inside a bucket;
+* split heavy tiles (GSPLAT_HIP_FWD_SPLIT): the images of the unsplit
+  forward up to chunk-product rounding, and against the oracle.
 """
-
-import math
-import os
 
 import numpy as np
 import pytest
@@ -66,9 +63,10 @@ def test_records_match_plain_gathers(mode):
         assert err <= 1e-5 * scale + 1e-9, (name, err, scale)
 
 
-def test_xcd_order_is_banded_permutation():
-    if os.environ.get("GSPLAT_HIP_XCD") != "1":
-        pytest.skip("XCD-aware dispatch is off (GSPLAT_HIP_XCD=1 turns it on)")
+def test_dispatch_order_is_heaviest_first_permutation():
+    """gsplat_hip_rasterize_prepare's tile order (tile_order_kernel): a
+    permutation of the tiles, buckets of >= 2048 / >= 1024 / >= 512 isects and
+    the rest in that order, raster order inside a bucket."""
     from gsplat_hip import _lib
     from gsplat_hip._wrapper import _ptr, _stream
     import gsplat_hip
@@ -80,41 +78,26 @@ def test_xcd_order_is_banded_permutation():
     C, th, tw = offs.shape
     nt = C * th * tw
     D = 3
-    sb = int(_lib.query("gsplat_hip_rasterize_fwd_state_bytes", C, D, 16, tw, th, n))
-    state = torch.full((sb // 4,), -7, dtype=torch.int32, device=DEV)
-    _lib.call("gsplat_hip_rasterize_prepare", C, D, 16, tw, th, _ptr(offs), n, None, _ptr(state), sb,
-              _stream())
-    torch.cuda.synchronize()
-    QI = 32 + 8 * 32  # starts[8], lens[8], pad, then one 128-B line per dequeue head
-    tail = state[-(nt + QI):].cpu().numpy()
-    order, queue = tail[:nt], tail[nt:]
+    old = _lib.query("gsplat_hip_debug_set_fwd_split", 0)  # no split area after the order
+    try:
+        sb = int(_lib.query("gsplat_hip_rasterize_fwd_state_bytes", C, D, 16, tw, th, n))
+        state = torch.full((sb // 4,), -7, dtype=torch.int32, device=DEV)
+        _lib.call("gsplat_hip_rasterize_prepare", C, D, 16, tw, th, _ptr(offs), n, None,
+                  _ptr(state), sb, _stream())
+        torch.cuda.synchronize()
+    finally:
+        _lib.query("gsplat_hip_debug_set_fwd_split", old)
+    order_ints = (4 * nt + 255) // 256 * 64  # the order area, 256-B aligned, at the end
+    order = state[-order_ints:][:nt].cpu().numpy()
     assert np.array_equal(np.sort(order), np.arange(nt)), "not a permutation"
-    starts, lens, heads = queue[:8], queue[8:16], queue[32::32]
-    assert np.all(heads == 0)
-    assert lens.sum() == nt and np.array_equal(starts, np.concatenate([[0], np.cumsum(lens)[:-1]]))
     o = offs.flatten().cpu().numpy().astype(np.int64)
     cnt = np.diff(np.concatenate([o, [n]]))
-    work = cnt + 32
-    seg_work = []
-    prev_hi = -1
-    for q in range(8):
-        tiles = order[starts[q]:starts[q] + lens[q]]
-        if tiles.size == 0:
-            seg_work.append(0)
-            continue
-        lo, hi = tiles.min(), tiles.max()
-        assert lo == prev_hi + 1 and hi - lo + 1 == tiles.size, f"segment {q} not a raster range"
-        prev_hi = hi
-        b = np.where(cnt[tiles] >= 2048, 0, np.where(cnt[tiles] >= 1024, 1,
-                                                      np.where(cnt[tiles] >= 512, 2, 3)))
-        assert np.all(np.diff(b) >= 0), f"segment {q}: buckets not heaviest first"
-        for bk in range(4):
-            tb = tiles[b == bk]
-            assert np.all(np.diff(tb) > 0), f"segment {q} bucket {bk}: not raster order"
-        seg_work.append(work[tiles].sum())
-    seg_work = np.array(seg_work, dtype=np.float64)
-    # bands of equal work up to one tile's work
-    assert np.all(np.abs(seg_work - work.sum() / 8) <= work.max() + 1), seg_work
+    assert (cnt[order] >= 512).any(), "scene has no heavy tiles"
+    b = np.where(cnt[order] >= 2048, 0, np.where(cnt[order] >= 1024, 1,
+                                                  np.where(cnt[order] >= 512, 2, 3)))
+    assert np.all(np.diff(b) >= 0), "buckets not heaviest first"
+    for bk in range(4):
+        assert np.all(np.diff(order[b == bk]) > 0), f"bucket {bk}: not raster order"
 
 
 def _heavy_scene(N=60000, W=320, H=240, seed=5):
