@@ -223,12 +223,33 @@ isect_offsets_kernel(int64_t n, const int64_t *__restrict__ n_dev,
 // Negative depths (near_plane <= 0) follow the reference's sign extension:
 // their (cam, tile) field becomes all ones.
 
-// (1a) compact the Gaussians with tiles, in index order, with their depth bits
+// Capacity check of the sync-free isect (see isect_capacity_kernel).
+struct CapCheck {
+  const int64_t *totals;  // (n_isects, n_visible) of gsplat_hip_isect_count
+  int64_t capacity;
+  int64_t *cap_state;     // [4], the caller's counts buffer
+  int32_t *status;        // sticky overflow flag or null
+};
+
+GS_INLINE void cap_check(const CapCheck &cc) {
+  const int64_t n = cc.totals[0];
+  const bool over = n > cc.capacity;
+  cc.cap_state[0] = over ? 0 : n;
+  cc.cap_state[1] = cc.totals[1];
+  cc.cap_state[2] = over ? 1 : 0;
+  cc.cap_state[3] = n;
+  if (over && cc.status) cc.status[0] |= 1;
+}
+
+// (1a) compact the Gaussians with tiles, in index order, with their depth bits.
+// Capacity mode: workgroup 0 also writes the capacity state (one launch less;
+// every reader of it runs after this kernel).
 __global__ void __launch_bounds__(kIsectBlock)
 isect_compact_kernel(int64_t G, const int32_t *__restrict__ tiles_per_gauss,
                      const float *__restrict__ depths, const int64_t *__restrict__ vis_prefix,
-                     int32_t *__restrict__ V, uint32_t *__restrict__ dkey) {
+                     int32_t *__restrict__ V, uint32_t *__restrict__ dkey, CapCheck cc) {
   __shared__ int64_t lds[kIsectBlock / 64 + 1];
+  if (cc.cap_state && blockIdx.x == 0 && threadIdx.x == 0) cap_check(cc);
   const int64_t i = (int64_t)blockIdx.x * kIsectBlock + threadIdx.x;
   const int on = (i < G) && tiles_per_gauss[i] > 0;
   int64_t tot;
@@ -393,17 +414,8 @@ isect_sorted_finalize_kernel(int64_t n, const int64_t *__restrict__ n_dev,
 // in `capacity` else 0, n_visible, 1 if it did not fit, n_isects}; status[0] |= 1 on
 // overflow (sticky: the training step's state updates read it and become
 // no-ops until the host has grown the arrays and cleared it).
-__global__ void isect_capacity_kernel(const int64_t *__restrict__ totals, int64_t capacity,
-                                      int64_t *__restrict__ cap_state,
-                                      int32_t *__restrict__ status) {
-  if (threadIdx.x != 0) return;
-  const int64_t n = totals[0];
-  const bool over = n > capacity;
-  cap_state[0] = over ? 0 : n;
-  cap_state[1] = totals[1];
-  cap_state[2] = over ? 1 : 0;
-  cap_state[3] = n;
-  if (over && status) status[0] |= 1;
+__global__ void isect_capacity_kernel(CapCheck cc) {
+  if (threadIdx.x == 0) cap_check(cc);
 }
 
 }  // namespace gs
@@ -557,7 +569,7 @@ static int isect_write_sorted_impl(
     const int32_t *camera_ids, const int32_t *tiles_per_gauss, int tile_size, int tile_width,
     int tile_height, int tile_bits, int cam_bits, const void *count_workspace, int64_t n_visible,
     int64_t n_isects, const int64_t *cnt_dev, void *workspace, int64_t workspace_bytes,
-    int64_t *isect_ids, int32_t *flatten_ids, hipStream_t st) {
+    int64_t *isect_ids, int32_t *flatten_ids, hipStream_t st, CapCheck cc = CapCheck{}) {
   GS_REQUIRE(n_gaussians >= 0 && (camera_ids || N > 0 || n_gaussians == 0),
              "isect_write_sorted: N must be > 0 when camera_ids is null");
   GS_REQUIRE(tile_bits + cam_bits <= 32, "isect_write_sorted: tile_bits + cam_bits > 32");
@@ -580,7 +592,7 @@ static int isect_write_sorted_impl(
   const int64_t nbG = (n_gaussians + kIsectBlock - 1) / kIsectBlock;
   const int64_t *vis_prefix = reinterpret_cast<const int64_t *>(count_workspace) + nbG + 1;
   hipLaunchKernelGGL(isect_compact_kernel, dim3((unsigned)nbG), dim3(kIsectBlock), 0, st,
-                     n_gaussians, tiles_per_gauss, depths, vis_prefix, V, dkey);
+                     n_gaussians, tiles_per_gauss, depths, vis_prefix, V, dkey, cc);
   // stable depth sort of the visible Gaussians (32 key bits)
   if (lsd_sort_pairs(dkey, V, dkeys, Vs, n_visible, 0, 32, tmp, st, nullptr,
                      cnt_dev ? cnt_dev + 1 : nullptr) == 0)
@@ -652,13 +664,17 @@ extern "C" int gsplat_hip_isect_write_sorted_capped(
   GS_REQUIRE(workspace_bytes >= need, "isect_write_sorted_capped: workspace %lld < %lld",
              (long long)workspace_bytes, (long long)need);
   hipStream_t st = (hipStream_t)stream;
-  // cap_state [3] lives in the caller's counts buffer
-  hipLaunchKernelGGL(isect_capacity_kernel, dim3(1), dim3(64), 0, st, totals_device, capacity,
-                     counts_device, status_device);
+  // cap_state [4] lives in the caller's counts buffer; the compact kernel
+  // writes it, or this one when the emission launches nothing
+  const CapCheck cc{totals_device, capacity, counts_device, status_device};
+  if (capacity <= 0 || n_gaussians <= 0) {
+    hipLaunchKernelGGL(isect_capacity_kernel, dim3(1), dim3(64), 0, st, cc);
+    GS_CHECK_LAUNCH("isect_write_sorted_capped");
+  }
   return isect_write_sorted_impl(n_gaussians, N, means2d, radii, depths, camera_ids,
                                  tiles_per_gauss, tile_size, tile_width, tile_height, tile_bits,
                                  cam_bits, count_workspace, n_gaussians, capacity, counts_device,
-                                 workspace, workspace_bytes - 256, isect_ids, flatten_ids, st);
+                                 workspace, workspace_bytes - 256, isect_ids, flatten_ids, st, cc);
 }
 
 // -------------------------------------------------------- tile-first path --

@@ -1220,10 +1220,11 @@ GS_INLINE void block_max_out(int64_t v, int32_t *out) {
 }
 
 // Forward dispatch order: tiles bucketed by isect count (>= 2048, >= 1024,
-// >= 512, the rest), heaviest bucket first and raster order inside a bucket,
-// so the longest tiles start in the first wave of workgroups instead of
-// finishing last.  One 1024-lane workgroup; the four bucket counts of a
-// thread are packed into one u64 (16 bits each) for a single block scan.
+// >= 512, the rest), heaviest bucket first, so the longest tiles start in the
+// first wave of workgroups instead of finishing last.  Inside a bucket: lane
+// order (lane l holds tiles l, l + 1024, ...).  One 1024-lane workgroup; the
+// four bucket counts of a lane are packed into one u64 (16 bits each) for a
+// single block scan.
 __global__ void __launch_bounds__(1024)
 tile_order_kernel(int n_tiles, const int32_t *__restrict__ offsets, int64_t n_isects,
                   const int64_t *__restrict__ n_dev, int32_t *__restrict__ order,

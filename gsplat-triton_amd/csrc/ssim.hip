@@ -483,7 +483,8 @@ constexpr int kHA = 6, kHC = 4;  // adjacent outputs per work item in passes A, 
 template <int C, int BR>
 __global__ void __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(4)))
 fused_kernel(int B, int H, int W, const float *__restrict__ x, const float *__restrict__ y,
-             float cs, float cl, float *__restrict__ grad, float *__restrict__ partials) {
+             const int64_t *__restrict__ y_index, float cs, float cl, float *__restrict__ grad,
+             float *__restrict__ partials) {
   __shared__ __attribute__((aligned(16))) char lds[kFusedLds];
   __shared__ float red[2][kFThreads / 64];
   f2v(*s_xy)[SX] = reinterpret_cast<f2v(*)[SX]>(lds);
@@ -503,6 +504,7 @@ fused_kernel(int B, int H, int W, const float *__restrict__ x, const float *__re
   const int b = L / (8 * per), q = L - b * 8 * per;
   const int t = (q & 7) * per + (q >> 3);
   if (b >= B || t >= nt) return;
+  if (y_index) y += y_index[0] * ((int64_t)B * H * W * C);  // image y_index of a stack
   const int qi0 = (t / tx) * FT, qj0 = (t % tx) * FT;  // image tile origin
   const int ri0 = qi0 - 2 * R, rj0 = qj0 - 2 * R;       // window origin (image coords)
   const int tid = threadIdx.x, lane = tid & 63;
@@ -832,9 +834,9 @@ extern "C" int64_t gsplat_hip_l1_ssim_loss_fused_workspace_bytes(int B, int H, i
 }
 
 extern "C" int gsplat_hip_l1_ssim_loss_fused_fwd(int B, int H, int W, int C, const float *img1,
-                                                 const float *img2, float lam, float *out,
-                                                 float *grad_unit, void *workspace,
-                                                 void *stream) {
+                                                 const float *img2, const int64_t *img2_index,
+                                                 float lam, float *out, float *grad_unit,
+                                                 void *workspace, void *stream) {
   GS_REQUIRE(B > 0 && H > 10 && W > 10,
              "l1_ssim_loss_fused_fwd: images must be larger than the 11x11 window (got %dx%d)", H,
              W);
@@ -851,7 +853,7 @@ extern "C" int gsplat_hip_l1_ssim_loss_fused_fwd(int B, int H, int W, int C, con
   }();
 #define GS_FUSED(CC, BR)                                                                   \
   hipLaunchKernelGGL((ssim::fused_kernel<CC, BR>), grid, dim3(ssim::kFThreads), 0, st, B, H, W, \
-                     img1, img2, cs, cl, grad_unit, partials)
+                     img1, img2, img2_index, cs, cl, grad_unit, partials)
   if (C == 3) {
     if (fv == 1) GS_FUSED(3, 2); else GS_FUSED(3, 4);
   } else {

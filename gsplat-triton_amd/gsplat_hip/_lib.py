@@ -12,7 +12,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GSPLAT_HIP_LIB", os.path.join(_HERE, "libgsplat_hip.so"))
-ABI_VERSION = 20
+ABI_VERSION = 21
 
 _p = ctypes.c_void_p
 _i32 = ctypes.c_int
@@ -73,7 +73,8 @@ _SIGS = {
     "gsplat_hip_l1_ssim_loss_fwd": (_i32, [_i32, _i32, _i32, _i32, _p, _p, _f, _p, _p, _p]),
     "gsplat_hip_l1_ssim_loss_bwd": (_i32, [_i32, _i32, _i32, _i32, _p, _p, _p, _f, _p, _p, _p]),
     "gsplat_hip_l1_ssim_loss_fused_workspace_bytes": (_i64, [_i32, _i32, _i32, _i32]),
-    "gsplat_hip_l1_ssim_loss_fused_fwd": (_i32, [_i32, _i32, _i32, _i32, _p, _p, _f, _p, _p, _p, _p]),
+    "gsplat_hip_l1_ssim_loss_fused_fwd": (_i32, [_i32, _i32, _i32, _i32, _p, _p, _p, _f, _p, _p, _p,
+                                                  _p]),
     "gsplat_hip_l1_ssim_loss_fused_bwd": (_i32, [_i64, _p, _p, _p, _p]),
     "gsplat_hip_update_state": (_i32, [_i32, _i64, _p, _p, _f, _f, _p, _p, _p, _p]),
     "gsplat_hip_activate_fwd": (_i32, [_i64, _i64, _p, _p, _p, _p, _p]),

@@ -473,7 +473,7 @@ class _IsectCount:
                          dtype=torch.uint8, device=dev)
         isect_ids = torch.empty(capacity, dtype=torch.int64, device=dev)
         flatten_ids = torch.empty(capacity, dtype=torch.int32, device=dev)
-        counts = torch.zeros(4, dtype=torch.int64, device=dev)
+        counts = torch.empty(4, dtype=torch.int64, device=dev)  # written by the emission
         if status is not None:
             assert status.dtype == torch.int32 and status.is_cuda
         _lib.call("gsplat_hip_isect_write_sorted_capped", G, N, _ptr(means2d), _ptr(radii),

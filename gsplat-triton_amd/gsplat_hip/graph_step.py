@@ -12,11 +12,13 @@ What makes the step capturable:
 * the sync-free intersection (`rasterization(_isect_capacity=...)`,
   gsplat_hip_isect_write_sorted_capped): isect arrays of a fixed capacity,
   every count stays on the device;
-* the step-dependent scalars (the Adam factors lr / (1 - b1^t),
-  1 / sqrt(1 - b2^t) with the means learning-rate schedule, and the camera
-  of this step) are device buffers the host refreshes before each replay
-  (gsplat_hip_adam_step_dev, gsplat_hip_sh_colors_bwd_adam_dev), computed with
-  the eager path's own arithmetic (losses.adam_factors);
+* the step-dependent inputs -- the Adam factors lr / (1 - b1^t),
+  1 / sqrt(1 - b2^t) with the means learning-rate schedule
+  (gsplat_hip_adam_step_dev, gsplat_hip_sh_colors_bwd_adam_dev; computed with
+  the eager path's own arithmetic, losses.adam_factors), the camera's
+  viewmat and K, and its index (the loss reads that camera's target image
+  in place, l1_ssim_loss(gt_index=...)) -- are one 512-B device block the
+  host refreshes with a single copy before each replay;
 * overflow: if a step's isects do not fit, the capped emission writes none,
   sets a sticky device flag, and every state update of that and the later
   steps reads the flag and does nothing.  The host reads each step's counts
@@ -60,15 +62,25 @@ class GraphStep:
         self.headroom = float(headroom)
         self.lag = int(lag)  # steps the host may run ahead of its overflow check
         self.capacity = None if capacity is None else int(capacity)
-        # device inputs of the graph: per-step scalars (f32 factors + i64 camera)
+        # device input of the graph: one 512-B block per step -- f32 [0, 64) the
+        # Adam factors, f32 [64, 80) the camera's viewmat, [80, 89) its K,
+        # i64 [48] (byte 384) the camera index
         self.n_groups = len(tr.params)
-        self.scal = torch.zeros(64, dtype=torch.float32, device=dev)
-        self.cam = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.blk = torch.zeros(512, dtype=torch.uint8, device=dev)
+        f = self.blk[:384].view(torch.float32)
+        self.scal = f[:64]
+        self.vm = f[64:80].view(1, 4, 4)
+        self.K = f[80:89].view(1, 3, 3)
+        self.cam = self.blk[384:392].view(torch.int64)
         self.status = torch.zeros(1, dtype=torch.int32, device=dev)  # sticky overflow flag
-        self._pin_f = [torch.zeros(64, dtype=torch.float32).pin_memory() for _ in range(self.RING)]
-        self._pin_c = [torch.zeros(1, dtype=torch.int64).pin_memory() for _ in range(self.RING)]
+        self._pin_b = [torch.zeros(512, dtype=torch.uint8).pin_memory() for _ in range(self.RING)]
         self._pin_n = [torch.zeros(4, dtype=torch.int64).pin_memory() for _ in range(self.RING)]
         self._slot_ev = [None] * self.RING
+        self._vm_host = tr.viewmats.detach().float().cpu().numpy()
+        self._K_host = tr.Ks.detach().float().cpu().numpy()
+        # the counts' device->host copy runs here, beside the next step's input copy
+        self._side = torch.cuda.Stream(device=dev)
+        self._copied = None  # event: the last counts copy is done (before the next replay)
         self.graph = None
         self.key = None
         self.counts = None  # the graph's isect counts (device i64[4])
@@ -102,18 +114,15 @@ class GraphStep:
                 hyper=self.scal[sh_off:sh_off + 3], skip=self.status)
         fusion = _wrapper.StepFusion(sh_adam=fa, geom=tr.geom_fuse) \
             if (fa is not None or tr.geom_fuse) else None
-        vm = tr.viewmats.index_select(0, self.cam)
-        K = tr.Ks.index_select(0, self.cam)
-        gt = tr.targets.index_select(0, self.cam)
         scales, opac = activate(p["scales"], p["opacities"], fusion)
         colors, _, meta = rasterization(
-            p["means"], p["quats"], scales, opac, (p["sh0"], p["shN"]), vm, K, tr.width,
+            p["means"], p["quats"], scales, opac, (p["sh0"], p["shN"]), self.vm, self.K, tr.width,
             tr.height, sh_degree=deg, packed=False, near_plane=0.01, far_plane=1e10,
             radius_clip=0.0, rasterize_mode="classic", _fusion=fusion,
             _isect_capacity=self.capacity, _isect_status=self.status)
         grad_box = {}
         meta["means2d"].register_hook(lambda g: grad_box.__setitem__("g", g))
-        loss = tr._regularise(l1_ssim_loss(colors, gt, tr.ssim_lambda))
+        loss = tr._regularise(l1_ssim_loss(colors, tr.targets, tr.ssim_lambda, gt_index=self.cam))
         from . import losses as _losses
         torch.autograd.backward(loss, _losses.ONE_GRAD)
         if "g" in grad_box:
@@ -168,7 +177,7 @@ class GraphStep:
 
     # ------------------------------------------------------------ host side
     def _fill(self, it, slot):
-        """The per-step scalars of step `it` into pinned slot `slot`."""
+        """The step block of step `it` into pinned slot `slot`."""
         tr = self.tr
         o = tr.opt
         step = o.step_count + 1
@@ -176,7 +185,8 @@ class GraphStep:
         if tr.max_steps:  # means ExponentialLR (Trainer.step sets it before Adam)
             lrs[0] = tr.lrs[0] * (0.01 ** (1.0 / tr.max_steps)) ** it
         idx, sh_off = self._layout()
-        f = self._pin_f[slot].numpy()
+        b = self._pin_b[slot].numpy()
+        f = b[:384].view(np.float32)
         fac = adam_factors([lrs[i] for i in idx], o.betas, step)
         for k, (ss, ib) in enumerate(fac):
             f[2 * k], f[2 * k + 1] = ss, ib
@@ -185,7 +195,10 @@ class GraphStep:
             (s0, ib), (sr, _) = adam_factors([lrs[names.index("sh0")], lrs[names.index("shN")]],
                                              o.betas, step)
             f[sh_off:sh_off + 3] = (s0, sr, ib)
-        self._pin_c[slot][0] = tr.camera_index(it)
+        ci = tr.camera_index(it)
+        f[64:80] = self._vm_host[ci].reshape(-1)
+        f[80:89] = self._K_host[ci].reshape(-1)
+        b[384:392].view(np.int64)[0] = ci
         if tr.max_steps:
             tr._set_means_lr(lrs[0])
 
@@ -207,13 +220,18 @@ class GraphStep:
             ev.synchronize()  # that slot's copies of RING steps ago are done
         self._fill(it, slot)
         cur = torch.cuda.current_stream(self.dev)
-        self.scal.copy_(self._pin_f[slot], non_blocking=True)
-        self.cam.copy_(self._pin_c[slot], non_blocking=True)
+        self.blk.copy_(self._pin_b[slot], non_blocking=True)
+        if self._copied is not None:  # the previous counts are read before they change
+            cur.wait_event(self._copied)
         self.graph.replay()
         self.tr.opt.step_count += 1
-        self._pin_n[slot].copy_(self.counts, non_blocking=True)
+        side = self._side
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            self._pin_n[slot].copy_(self.counts, non_blocking=True)
         ev = torch.cuda.Event()
-        ev.record(cur)
+        ev.record(side)
+        self._copied = ev
         self._slot_ev[slot] = ev
         self.pending.append((it, slot, ev))
         self.issued += 1

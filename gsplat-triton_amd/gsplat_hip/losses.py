@@ -86,8 +86,15 @@ class _L1SSIMLossFused(torch.autograd.Function):
     gradient.  The training path: no per-pixel SSIM partials through HBM."""
 
     @staticmethod
-    def forward(ctx, img, gt, lam):
-        assert img.dim() == 4 and img.shape == gt.shape, (img.shape, gt.shape)
+    def forward(ctx, img, gt, lam, gt_index=None):
+        # gt_index: device int64 [1]; gt is then a stack [n, H, W, C] of
+        # single-image targets and gt[gt_index] is this image's target
+        if gt_index is None:
+            assert img.dim() == 4 and img.shape == gt.shape, (img.shape, gt.shape)
+        else:
+            assert img.dim() == 4 and img.shape[0] == 1 and gt.shape[1:] == img.shape[1:], \
+                (img.shape, gt.shape)
+            assert gt_index.dtype == torch.int64 and gt_index.is_cuda and gt.is_contiguous()
         img = img.contiguous().float()
         gt = gt.contiguous().float()
         B, H, W, C = img.shape
@@ -97,7 +104,7 @@ class _L1SSIMLossFused(torch.autograd.Function):
         out = torch.empty(3, device=img.device)
         unit = torch.empty_like(img)
         _lib.call("gsplat_hip_l1_ssim_loss_fused_fwd", B, H, W, C, _ptr(img), _ptr(gt),
-                  ctypes.c_float(lam), _ptr(out), _ptr(unit), _ptr(ws), _stream())
+                  _ptr(gt_index), ctypes.c_float(lam), _ptr(out), _ptr(unit), _ptr(ws), _stream())
         ctx.save_for_backward(unit)
         return out[0]
 
@@ -105,12 +112,12 @@ class _L1SSIMLossFused(torch.autograd.Function):
     def backward(ctx, g_loss):
         (unit,) = ctx.saved_tensors
         if g_loss is ONE_GRAD:  # the trainer's constant 1.0 seed: the unit gradient as is
-            return unit, None, None
+            return unit, None, None, None
         g_loss = g_loss.float().contiguous()
         grad = torch.empty_like(unit)
         _lib.call("gsplat_hip_l1_ssim_loss_fused_bwd", unit.numel(), _ptr(unit), _ptr(g_loss),
                   _ptr(grad), _stream())
-        return grad, None, None
+        return grad, None, None, None
 
 
 # A constant scalar 1.0 the trainer seeds loss.backward() with (never written):
@@ -122,12 +129,19 @@ ONE_GRAD = None
 SSIM_FUSED = os.environ.get("GSPLAT_HIP_SSIM_FUSED", "1") != "0"
 
 
-def l1_ssim_loss(img, gt, ssim_lambda=0.2, fused=None):
+def l1_ssim_loss(img, gt, ssim_lambda=0.2, fused=None, gt_index=None):
     """(1 - ssim_lambda) * mean L1 + ssim_lambda * (1 - mean SSIM_valid).
     With a gradient to compute (and C in {1, 3}) the one-pass fused kernel
-    runs, unless `fused=False` (or GSPLAT_HIP_SSIM_FUSED=0)."""
+    runs, unless `fused=False` (or GSPLAT_HIP_SSIM_FUSED=0).  `gt_index`
+    (device int64 [1], fused kernel only): `gt` is a stack of targets and
+    gt[gt_index] the one of this [1, H, W, C] image -- chosen on the device,
+    no copy (the captured training step)."""
     if fused is None:
         fused = SSIM_FUSED and torch.is_grad_enabled() and img.requires_grad
+    if gt_index is not None:
+        if not (fused and img.dim() == 4 and img.shape[-1] in (1, 3)):
+            raise ValueError("l1_ssim_loss: gt_index needs the fused kernel (grad, C in {1, 3})")
+        return _L1SSIMLossFused.apply(img, gt, float(ssim_lambda), gt_index)
     if fused and img.dim() == 4 and img.shape[-1] in (1, 3):
         return _L1SSIMLossFused.apply(img, gt, float(ssim_lambda))
     return _L1SSIMLoss.apply(img, gt, float(ssim_lambda))

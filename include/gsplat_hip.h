@@ -320,11 +320,15 @@ int gsplat_hip_l1_ssim_loss_bwd(int B, int H, int W, int C, const float *img1,
  * per-pixel partials reach HBM.  C is 1 or 3.
  * fused_fwd: out[0..2] as l1_ssim_loss_fwd; grad_unit [B,H,W,C] = dout[0]/dimg1;
  *            workspace = gsplat_hip_l1_ssim_loss_fused_workspace_bytes.
+ *            img2_index (ABI 21, may be NULL): device int64; img2 is then a
+ *            stack of [B,H,W,C] images and image img2_index[0] is the target
+ *            (a captured training step picks its camera's target on the device).
  * fused_bwd: grad_img1[i] = g_loss[0] * grad_unit[i] (16-B aligned buffers). */
 int64_t gsplat_hip_l1_ssim_loss_fused_workspace_bytes(int B, int H, int W, int C);
 int gsplat_hip_l1_ssim_loss_fused_fwd(int B, int H, int W, int C, const float *img1,
-                                      const float *img2, float lam, float *out,
-                                      float *grad_unit, void *workspace, void *stream);
+                                      const float *img2, const int64_t *img2_index, float lam,
+                                      float *out, float *grad_unit, void *workspace,
+                                      void *stream);
 int gsplat_hip_l1_ssim_loss_fused_bwd(int64_t n, const float *grad_unit, const float *g_loss,
                                       float *grad_img1, void *stream);
 

@@ -215,3 +215,20 @@ def test_graph_trainer_tracks_eager(capacity):
         torch.testing.assert_close(y, x, rtol=1e-2, atol=1e-6)
     torch.testing.assert_close(b[4], a[4], rtol=0, atol=0)  # visibility counts: exact
     torch.testing.assert_close(b[3], a[3], rtol=1e-3, atol=1e-7)
+
+
+def test_loss_target_index_is_exact():
+    """l1_ssim_loss(gt_index=...): the target picked on the device from a
+    stack gives the loss and gradient of that target passed directly."""
+    from gsplat_hip.losses import l1_ssim_loss
+    g = torch.Generator(device=DEV).manual_seed(11)
+    stack = torch.rand(4, 96, 128, 3, device=DEV, generator=g)
+    img = torch.rand(1, 96, 128, 3, device=DEV, generator=g)
+    for ci in (0, 3):
+        a = img.clone().requires_grad_(True)
+        b = img.clone().requires_grad_(True)
+        la = l1_ssim_loss(a, stack[ci:ci + 1].contiguous())
+        lb = l1_ssim_loss(b, stack, gt_index=torch.tensor([ci], device=DEV))
+        la.backward()
+        lb.backward()
+        assert torch.equal(la.detach(), lb.detach()) and torch.equal(a.grad, b.grad)

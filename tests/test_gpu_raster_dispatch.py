@@ -6,7 +6,7 @@ only, never results.
   the four attribute arrays (the same floats reach the same arithmetic), and
   the backward agrees up to the order of its float atomics;
 * the forward's dispatch order (tile_order_kernel): a permutation of the
-  tiles, heaviest bucket first, raster order inside a bucket;
+  tiles, heaviest bucket first;
 * split heavy tiles (GSPLAT_HIP_FWD_SPLIT): the images of the unsplit
   forward up to chunk-product rounding, and against the oracle.
 """
@@ -66,7 +66,7 @@ def test_records_match_plain_gathers(mode):
 def test_dispatch_order_is_heaviest_first_permutation():
     """gsplat_hip_rasterize_prepare's tile order (tile_order_kernel): a
     permutation of the tiles, buckets of >= 2048 / >= 1024 / >= 512 isects and
-    the rest in that order, raster order inside a bucket."""
+    the rest in that order, lane order inside a bucket."""
     from gsplat_hip import _lib
     from gsplat_hip._wrapper import _ptr, _stream
     import gsplat_hip
@@ -96,8 +96,9 @@ def test_dispatch_order_is_heaviest_first_permutation():
     b = np.where(cnt[order] >= 2048, 0, np.where(cnt[order] >= 1024, 1,
                                                   np.where(cnt[order] >= 512, 2, 3)))
     assert np.all(np.diff(b) >= 0), "buckets not heaviest first"
-    for bk in range(4):
-        assert np.all(np.diff(order[b == bk]) > 0), f"bucket {bk}: not raster order"
+    for bk in range(4):  # lane t % 1024 holds tiles t, t + 1024, ...: lane-major
+        t = order[b == bk].astype(np.int64)
+        assert np.all(np.diff((t % 1024) * 16 + t // 1024) > 0), f"bucket {bk}: not lane order"
 
 
 def _heavy_scene(N=60000, W=320, H=240, seed=5):
