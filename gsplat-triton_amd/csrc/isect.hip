@@ -229,6 +229,10 @@ struct CapCheck {
   int64_t capacity;
   int64_t *cap_state;     // [4], the caller's counts buffer
   int32_t *status;        // sticky overflow flag or null
+  // the same four counts also into row *slot of a host-mapped ring (the
+  // captured step's overflow check reads them there, no copy); or null
+  int64_t *host_ring;
+  const int64_t *slot;
 };
 
 GS_INLINE void cap_check(const CapCheck &cc) {
@@ -239,6 +243,13 @@ GS_INLINE void cap_check(const CapCheck &cc) {
   cc.cap_state[2] = over ? 1 : 0;
   cc.cap_state[3] = n;
   if (over && cc.status) cc.status[0] |= 1;
+  if (cc.host_ring) {
+    int64_t *h = cc.host_ring + 4 * (*cc.slot);
+    h[0] = over ? 0 : n;
+    h[1] = cc.totals[1];
+    h[2] = over ? 1 : 0;
+    h[3] = n;
+  }
 }
 
 // (1a) compact the Gaussians with tiles, in index order, with their depth bits.
@@ -654,11 +665,14 @@ extern "C" int gsplat_hip_isect_write_sorted_capped(
     const int32_t *camera_ids, const int32_t *tiles_per_gauss, int tile_size, int tile_width,
     int tile_height, int tile_bits, int cam_bits, const void *count_workspace,
     const int64_t *totals_device, int64_t capacity, int64_t *counts_device,
-    int32_t *status_device, void *workspace, int64_t workspace_bytes, int64_t *isect_ids,
-    int32_t *flatten_ids, void *stream) {
+    int32_t *status_device, int64_t *counts_host_ring, const int64_t *slot_device,
+    void *workspace, int64_t workspace_bytes, int64_t *isect_ids, int32_t *flatten_ids,
+    void *stream) {
   GS_REQUIRE(capacity >= 0 && capacity < ((int64_t)1 << 30),
              "isect_write_sorted_capped: capacity %lld out of range", (long long)capacity);
   GS_REQUIRE(counts_device && totals_device, "isect_write_sorted_capped: null count buffers");
+  GS_REQUIRE(!counts_host_ring == !slot_device,
+             "isect_write_sorted_capped: counts_host_ring and slot_device go together");
   const int64_t need = gsplat_hip_isect_sorted_capped_workspace_bytes(n_gaussians, capacity,
                                                                       tile_bits + cam_bits);
   GS_REQUIRE(workspace_bytes >= need, "isect_write_sorted_capped: workspace %lld < %lld",
@@ -666,7 +680,8 @@ extern "C" int gsplat_hip_isect_write_sorted_capped(
   hipStream_t st = (hipStream_t)stream;
   // cap_state [4] lives in the caller's counts buffer; the compact kernel
   // writes it, or this one when the emission launches nothing
-  const CapCheck cc{totals_device, capacity, counts_device, status_device};
+  const CapCheck cc{totals_device, capacity, counts_device, status_device, counts_host_ring,
+                    slot_device};
   if (capacity <= 0 || n_gaussians <= 0) {
     hipLaunchKernelGGL(isect_capacity_kernel, dim3(1), dim3(64), 0, st, cc);
     GS_CHECK_LAUNCH("isect_write_sorted_capped");

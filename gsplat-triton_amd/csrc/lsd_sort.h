@@ -20,7 +20,8 @@
 // (scatter read + write).
 // Device count (n_dev non-null, the sync-free isect of a captured step): the
 // grids are sized for the capacity n and every kernel reads the item count
-// min(*n_dev, n) itself; tiles past it contribute empty histograms.
+// min(*n_dev, n) itself; the tiles past it exit at once and the scans stop
+// at the last tile holding items.
 #pragma once
 #include <stdlib.h>
 
@@ -54,10 +55,11 @@ hist_kernel(const uint32_t *__restrict__ keys, int64_t n, const int64_t *__restr
             int shift, uint32_t mask, uint32_t *__restrict__ hist, int64_t nt) {
   __shared__ uint32_t h[RX];
   if (n_dev) n = min(n, *n_dev);
+  const int64_t base = (int64_t)blockIdx.x * NT * IPT;
+  if (n_dev && base >= n) return;  // past the items: the scan does not read this tile
 #pragma unroll
   for (int d = threadIdx.x; d < RX; d += NT) h[d] = 0;
   __syncthreads();
-  const int64_t base = (int64_t)blockIdx.x * NT * IPT;
   if (mask < 64u) {
     // few digits (the short last pass of the tile sort): runs of equal
     // digits would serialise on one LDS address, so the lanes of a wave
@@ -90,10 +92,13 @@ hist_kernel(const uint32_t *__restrict__ keys, int64_t n, const int64_t *__restr
 }
 
 // Exclusive scan of row d (nt entries) in place; the row sum -> totals[d].
+// Device count: only the tiles holding items (tile = tile_items items).
 __global__ void __launch_bounds__(NT)
-scan_kernel(uint32_t *__restrict__ hist, int64_t nt, uint32_t *__restrict__ totals) {
+scan_kernel(uint32_t *__restrict__ hist, int64_t nt, uint32_t *__restrict__ totals,
+            const int64_t *__restrict__ n_dev, int64_t n, int64_t tile_items) {
   __shared__ uint32_t wsum[NT / 64];
   uint32_t *row = hist + (int64_t)blockIdx.x * nt;
+  if (n_dev) nt = min(nt, (min(n, *n_dev) + tile_items - 1) / tile_items);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   uint32_t carry = 0;
   for (int64_t b0 = 0; b0 < nt; b0 += NT) {
@@ -149,6 +154,7 @@ scatter_kernel(const uint32_t *__restrict__ kin, const int32_t *__restrict__ vin
   const int64_t base = (int64_t)blockIdx.x * TILE;
   if (n_dev) n = min(n, *n_dev);
   const int nvalid = (int)max<int64_t>(0, min<int64_t>((int64_t)TILE, n - base));
+  if (n_dev && nvalid == 0) return;  // past the items
   uint32_t key[IPT];
   int32_t val[IPT];
 #pragma unroll
@@ -302,7 +308,7 @@ inline int lsd_sort_pairs(uint32_t *k0, int32_t *v0, uint32_t *k1, int32_t *v1, 
     }
 #undef GS_LSD_HIST
     hipLaunchKernelGGL(lsd::scan_kernel, dim3((unsigned)radix), dim3(lsd::NT), 0, st, hist, nt,
-                       totals);
+                       totals, n_dev, n, (int64_t)lsd::NT * ipt);
     const bool fin = fo && shift + dbits >= end_bit;
     const lsd::FinalOut f = fin ? *fo : lsd::FinalOut{nullptr, nullptr, nullptr};
 #define GS_LSD_SCATTER(I, F, RX)                                                              \

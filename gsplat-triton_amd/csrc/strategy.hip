@@ -18,6 +18,8 @@
 //                  places the survivors, and one apply pass writes the final
 //                  layout of all arrays once.
 // All HBM-bound streaming kernels, one lane per Gaussian.
+#include <string.h>
+
 #include "common.h"
 #include "../../include/gsplat_hip.h"
 
@@ -286,10 +288,64 @@ densify_apply_kernel(int64_t N, const uint8_t *__restrict__ flags,
   }
 }
 
+// The captured training step's input block (gsplat_hip_step_fetch): slot
+// seq % ring of a host-mapped ring into the device block, its slot index into
+// the block's last 8 bytes, seq += 1.  One wave; every later kernel of the
+// step reads the block after this one (stream order).
+__global__ void __launch_bounds__(64)
+step_fetch_kernel(const uint32_t *__restrict__ ring, int64_t slot_words, int n_ring,
+                  int64_t *__restrict__ seq, uint32_t *__restrict__ blk) {
+  const int64_t q = *seq;
+  const int64_t slot = q % n_ring;
+  const uint32_t *src = ring + slot * slot_words;
+  for (int64_t w = threadIdx.x; w < slot_words - 2; w += 64) blk[w] = src[w];
+  if (threadIdx.x == 0) {
+    reinterpret_cast<int64_t *>(blk)[slot_words / 2 - 1] = slot;
+    *seq = q + 1;
+  }
+}
+
 }  // namespace strat
 }  // namespace gs
 
 using namespace gs;
+
+// Host-mapped, coherent memory (fine-grained: GPU reads see the host's
+// latest stores at kernel start, GPU stores are visible to the host once the
+// kernel is complete), zeroed.  For the captured step's input and count rings.
+extern "C" int gsplat_hip_host_mapped_alloc(int64_t bytes, void **host_ptr, void **device_ptr) {
+  GS_REQUIRE(bytes > 0 && host_ptr && device_ptr, "host_mapped_alloc: bad arguments");
+  void *h = nullptr;
+  GS_HIP(hipHostMalloc(&h, (size_t)bytes, hipHostMallocMapped | hipHostMallocCoherent));
+  memset(h, 0, (size_t)bytes);
+  void *d = nullptr;
+  if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
+    (void)hipHostFree(h);
+    GS_REQUIRE(false, "host_mapped_alloc: no device pointer");
+  }
+  *host_ptr = h;
+  *device_ptr = d;
+  return 0;
+}
+
+extern "C" int gsplat_hip_host_mapped_free(void *host_ptr) {
+  if (host_ptr) GS_HIP(hipHostFree(host_ptr));
+  return 0;
+}
+
+extern "C" int gsplat_hip_step_fetch(const void *ring_device, int64_t slot_bytes, int n_ring,
+                                     int64_t *seq_device, void *block_device, void *stream) {
+  GS_REQUIRE(ring_device && seq_device && block_device && n_ring > 0,
+             "step_fetch: null buffer or empty ring");
+  GS_REQUIRE(slot_bytes >= 16 && slot_bytes % 8 == 0 && slot_bytes <= 65536,
+             "step_fetch: slot_bytes %lld not a multiple of 8 in [16, 65536]",
+             (long long)slot_bytes);
+  hipLaunchKernelGGL(strat::step_fetch_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream,
+                     reinterpret_cast<const uint32_t *>(ring_device), slot_bytes / 4, n_ring,
+                     seq_device, reinterpret_cast<uint32_t *>(block_device));
+  GS_CHECK_LAUNCH("step_fetch");
+  return 0;
+}
 
 extern "C" int gsplat_hip_update_state(int C, int64_t N, const float *means2d_grad,
                                        const int32_t *radii, float scale_x, float scale_y,

@@ -454,14 +454,16 @@ class _IsectCount:
         return tpg, isect_ids, flatten_ids
 
     @torch.no_grad()
-    def finish_capped(self, capacity: int, status: Optional[Tensor] = None):
+    def finish_capped(self, capacity: int, status: Optional[Tensor] = None, report=None):
         """The sorted isects with NO host synchronisation (the one sync of
         isect_tiles, isect_tiles.py:101-102, removed so that a training step
         can be captured into a HIP graph): isect_ids / flatten_ids have
         `capacity` slots, of which counts[0] (device i64) are written --
         the same isects as finish(sort=True) -- or none if they do not fit
         (counts[2] = 1; status[0] |= 1, sticky, when given); counts[1] = the
-        visible Gaussians, counts[3] = n_isects whether it fit or not.  Returns
+        visible Gaussians, counts[3] = n_isects whether it fit or not.
+        `report` = (device pointer of a host-mapped i64[ring][4], device i64
+        slot tensor): the counts also go to that ring row.  Returns
         (tiles_per_gauss, isect_ids, flatten_ids, counts)."""
         (means2d, radii, depths, camera_ids, C, N, G, tile_size, tile_width, tile_height,
          n_bit_tile, n_bit_cam, packed) = self.args
@@ -476,11 +478,14 @@ class _IsectCount:
         counts = torch.empty(4, dtype=torch.int64, device=dev)  # written by the emission
         if status is not None:
             assert status.dtype == torch.int32 and status.is_cuda
+        ring, slot = (None, None) if report is None else report
+        if slot is not None:
+            assert slot.dtype == torch.int64 and slot.is_cuda and ring
         _lib.call("gsplat_hip_isect_write_sorted_capped", G, N, _ptr(means2d), _ptr(radii),
                   _ptr(depths), _ptr(camera_ids), _ptr(self.tpg), tile_size, tile_width,
                   tile_height, n_bit_tile, n_bit_cam, _ptr(self.ws), _ptr(self.totals), capacity,
-                  _ptr(counts), _ptr(status), _ptr(ws), ws.numel(), _ptr(isect_ids),
-                  _ptr(flatten_ids), _stream())
+                  _ptr(counts), _ptr(status), ring, _ptr(slot), _ptr(ws), ws.numel(),
+                  _ptr(isect_ids), _ptr(flatten_ids), _stream())
         tpg = self.tpg if packed else self.tpg.view(C, N)
         return tpg, isect_ids, flatten_ids, counts
 

@@ -17,26 +17,31 @@ What makes the step capturable:
   (gsplat_hip_adam_step_dev, gsplat_hip_sh_colors_bwd_adam_dev; computed with
   the eager path's own arithmetic, losses.adam_factors), the camera's
   viewmat and K, and its index (the loss reads that camera's target image
-  in place, l1_ssim_loss(gt_index=...)) -- are one 512-B device block the
-  host refreshes with a single copy before each replay;
+  in place, l1_ssim_loss(gt_index=...)) -- are one 512-B block.  The host
+  writes it into a slot of a host-mapped ring; the graph's first kernel
+  (gsplat_hip_step_fetch) copies slot seq % RING into device memory and
+  counts seq up, so a step needs no copy-engine transfer (each one cost a
+  cross-queue hand-off of ~15 us before and after it);
 * overflow: if a step's isects do not fit, the capped emission writes none,
   sets a sticky device flag, and every state update of that and the later
-  steps reads the flag and does nothing.  The host reads each step's counts
-  one step late (a device->host copy, no wait), then waits for the GPU,
-  grows the capacity, re-captures and re-runs the void steps in order -- so
-  the result is the eager step sequence's.
+  steps reads the flag and does nothing.  The emission also writes each
+  step's counts into that step's row of a host-mapped ring; the host reads
+  them once the step is done (up to `lag` steps late), then waits for the
+  GPU, grows the capacity, re-captures and re-runs the void steps in order
+  -- so the result is the eager step sequence's.
 
 Scope: the fused one-rank 3DGS trainer without a densification schedule
 (the bench's M2 configuration); anything else runs eagerly (Trainer.step).
 """
 
 import collections
+import ctypes
 import math
 
 import numpy as np
 import torch
 
-from . import _wrapper
+from . import _lib, _wrapper
 from .losses import FusedAdam, adam_factors, l1_ssim_loss
 from .rendering import rasterization
 from .strategy import activate, update_state_
@@ -49,10 +54,31 @@ def graphable(tr) -> bool:
             and isinstance(tr.opt, FusedAdam) and torch.device(tr.device).type == "cuda")
 
 
+class _Mapped:
+    """Host-mapped, coherent memory (gsplat_hip_host_mapped_alloc): `np` for
+    the host, `dev` (a pointer) for kernels."""
+
+    def __init__(self, nbytes):
+        h, d = ctypes.c_void_p(), ctypes.c_void_p()
+        _lib.call("gsplat_hip_host_mapped_alloc", int(nbytes), ctypes.addressof(h),
+                  ctypes.addressof(d))
+        self.host, self.dev = h.value, d.value
+        self.np = np.ctypeslib.as_array((ctypes.c_uint8 * int(nbytes)).from_address(self.host))
+
+    def __del__(self):
+        host, self.host = getattr(self, "host", None), None
+        if host and _lib is not None:
+            try:
+                _lib.call("gsplat_hip_host_mapped_free", host)
+            except Exception:  # interpreter shutdown
+                pass
+
+
 class GraphStep:
     """Trainer.step as HIP graph replays (see the module docstring)."""
 
-    RING = 8  # pinned host slots for the per-step scalars and counts
+    RING = 8  # host-mapped slots for the per-step input block and counts
+    SLOT = 512  # bytes per input block
 
     def __init__(self, tr, capacity=None, headroom=1.25, lag=2):
         assert graphable(tr), "GraphStep: a fused one-rank 3DGS trainer without densification"
@@ -64,23 +90,24 @@ class GraphStep:
         self.capacity = None if capacity is None else int(capacity)
         # device input of the graph: one 512-B block per step -- f32 [0, 64) the
         # Adam factors, f32 [64, 80) the camera's viewmat, [80, 89) its K,
-        # i64 [48] (byte 384) the camera index
+        # i64 at byte 384 the camera index, i64 at byte 504 the ring slot
+        # (written by gsplat_hip_step_fetch)
         self.n_groups = len(tr.params)
-        self.blk = torch.zeros(512, dtype=torch.uint8, device=dev)
+        self.blk = torch.zeros(self.SLOT, dtype=torch.uint8, device=dev)
         f = self.blk[:384].view(torch.float32)
         self.scal = f[:64]
         self.vm = f[64:80].view(1, 4, 4)
         self.K = f[80:89].view(1, 3, 3)
         self.cam = self.blk[384:392].view(torch.int64)
+        self.slot = self.blk[self.SLOT - 8:].view(torch.int64)
+        self.seq = torch.zeros(1, dtype=torch.int64, device=dev)  # steps fetched
         self.status = torch.zeros(1, dtype=torch.int32, device=dev)  # sticky overflow flag
-        self._pin_b = [torch.zeros(512, dtype=torch.uint8).pin_memory() for _ in range(self.RING)]
-        self._pin_n = [torch.zeros(4, dtype=torch.int64).pin_memory() for _ in range(self.RING)]
+        self.ring_in = _Mapped(self.RING * self.SLOT)
+        self.ring_out = _Mapped(self.RING * 4 * 8)
+        self._out = self.ring_out.np.view(np.int64).reshape(self.RING, 4)
         self._slot_ev = [None] * self.RING
         self._vm_host = tr.viewmats.detach().float().cpu().numpy()
         self._K_host = tr.Ks.detach().float().cpu().numpy()
-        # the counts' device->host copy runs here, beside the next step's input copy
-        self._side = torch.cuda.Stream(device=dev)
-        self._copied = None  # event: the last counts copy is done (before the next replay)
         self.graph = None
         self.key = None
         self.counts = None  # the graph's isect counts (device i64[4])
@@ -114,12 +141,15 @@ class GraphStep:
                 hyper=self.scal[sh_off:sh_off + 3], skip=self.status)
         fusion = _wrapper.StepFusion(sh_adam=fa, geom=tr.geom_fuse) \
             if (fa is not None or tr.geom_fuse) else None
+        _lib.call("gsplat_hip_step_fetch", self.ring_in.dev, self.SLOT, self.RING,
+                  _wrapper._ptr(self.seq), _wrapper._ptr(self.blk), _wrapper._stream())
         scales, opac = activate(p["scales"], p["opacities"], fusion)
         colors, _, meta = rasterization(
             p["means"], p["quats"], scales, opac, (p["sh0"], p["shN"]), self.vm, self.K, tr.width,
             tr.height, sh_degree=deg, packed=False, near_plane=0.01, far_plane=1e10,
             radius_clip=0.0, rasterize_mode="classic", _fusion=fusion,
-            _isect_capacity=self.capacity, _isect_status=self.status)
+            _isect_capacity=self.capacity, _isect_status=self.status,
+            _isect_report=(self.ring_out.dev, self.slot))
         grad_box = {}
         meta["means2d"].register_hook(lambda g: grad_box.__setitem__("g", g))
         loss = tr._regularise(l1_ssim_loss(colors, tr.targets, tr.ssim_lambda, gt_index=self.cam))
@@ -161,6 +191,7 @@ class GraphStep:
                 self.loss, self.counts = self._body(deg)
             self.graph = g
             self.status.zero_()
+            self.seq.fill_(self.issued)  # the next replay fetches slot issued % RING
             torch.cuda.synchronize(self.dev)
         finally:
             _wrapper._timers = timers
@@ -185,7 +216,7 @@ class GraphStep:
         if tr.max_steps:  # means ExponentialLR (Trainer.step sets it before Adam)
             lrs[0] = tr.lrs[0] * (0.01 ** (1.0 / tr.max_steps)) ** it
         idx, sh_off = self._layout()
-        b = self._pin_b[slot].numpy()
+        b = self.ring_in.np[slot * self.SLOT:(slot + 1) * self.SLOT]
         f = b[:384].view(np.float32)
         fac = adam_factors([lrs[i] for i in idx], o.betas, step)
         for k, (ss, ib) in enumerate(fac):
@@ -217,21 +248,12 @@ class GraphStep:
         slot = self.issued % self.RING
         ev = self._slot_ev[slot]
         if ev is not None:
-            ev.synchronize()  # that slot's copies of RING steps ago are done
+            ev.synchronize()  # the step that used this slot RING steps ago is done
         self._fill(it, slot)
-        cur = torch.cuda.current_stream(self.dev)
-        self.blk.copy_(self._pin_b[slot], non_blocking=True)
-        if self._copied is not None:  # the previous counts are read before they change
-            cur.wait_event(self._copied)
         self.graph.replay()
         self.tr.opt.step_count += 1
-        side = self._side
-        side.wait_stream(cur)
-        with torch.cuda.stream(side):
-            self._pin_n[slot].copy_(self.counts, non_blocking=True)
         ev = torch.cuda.Event()
-        ev.record(side)
-        self._copied = ev
+        ev.record(torch.cuda.current_stream(self.dev))
         self._slot_ev[slot] = ev
         self.pending.append((it, slot, ev))
         self.issued += 1
@@ -246,7 +268,7 @@ class GraphStep:
                     return
                 ev.synchronize()
             block = False
-            n_written, _, over, n_total = (int(x) for x in self._pin_n[slot].tolist())
+            n_written, _, over, n_total = (int(x) for x in self._out[slot])
             self.max_isects = max(self.max_isects, n_total)
             if over:
                 self._recover()
@@ -260,7 +282,7 @@ class GraphStep:
         torch.cuda.synchronize(self.dev)
         redo = [it for it, _, _ in self.pending]
         for _, slot, _ in self.pending:
-            self.max_isects = max(self.max_isects, int(self._pin_n[slot][3]))
+            self.max_isects = max(self.max_isects, int(self._out[slot][3]))
         self.pending.clear()
         tr.opt.step_count -= len(redo)  # their Adam steps did not happen
         self.capacity = int(math.ceil(self.max_isects * self.headroom)) + 1

@@ -70,6 +70,7 @@ def rasterization(
     _fusion=None,
     _isect_capacity: Optional[int] = None,
     _isect_status: Optional[Tensor] = None,
+    _isect_report=None,
 ) -> Tuple[Tensor, Tensor, Dict]:
     """Rasterize N 3D Gaussians to C images (gsplat/rendering.py:44-598).
 
@@ -81,7 +82,8 @@ def rasterization(
     that many slots -- meta["isect_ids"] / ["flatten_ids"] are then
     capacity-sized, meta["isect_counts"] (device i64[4]: written, visible,
     overflow, n_isects) says how many are valid; an overflow also sets
-    `_isect_status[0]` (sticky)."""
+    `_isect_status[0]` (sticky).  `_isect_report` = (host-mapped i64[ring][4]
+    device pointer, device i64 slot): the counts also go to that ring row."""
     meta = {}
     N = means.shape[0]
     C = viewmats.shape[0]
@@ -272,7 +274,7 @@ def rasterization(
     counts = None
     if capped:
         tiles_per_gauss, isect_ids, flatten_ids, counts = pending_isects.finish_capped(
-            _isect_capacity, _isect_status)
+            _isect_capacity, _isect_status, _isect_report)
         meta["isect_counts"] = counts
     else:
         tiles_per_gauss, isect_ids, flatten_ids = pending_isects.finish(sort=True)

@@ -147,7 +147,11 @@ int gsplat_hip_isect_write_sorted(int64_t n_gaussians, int N, const float *means
  * fit, n_isects}; status_device[0] (may be NULL) gets bit 0 set on overflow and keeps it
  * (sticky, cleared by the caller).  Pass counts_device as the n_isects_device
  * of gsplat_hip_isect_offsets / gsplat_hip_rasterize_*, with n_isects =
- * capacity.  The written isects equal gsplat_hip_isect_write_sorted's. */
+ * capacity.  The written isects equal gsplat_hip_isect_write_sorted's.
+ * counts_host_ring / slot_device (ABI 22, both NULL or both set): the four
+ * counts also go to row slot_device[0] of an i64[ring][4] host-mapped
+ * buffer (gsplat_hip_host_mapped_alloc) -- a captured step's overflow check
+ * reads them there without a device->host copy. */
 int64_t gsplat_hip_isect_sorted_capped_workspace_bytes(int64_t n_gaussians, int64_t capacity,
                                                        int key_bits);
 int gsplat_hip_isect_write_sorted_capped(
@@ -155,8 +159,9 @@ int gsplat_hip_isect_write_sorted_capped(
     const int32_t *camera_ids, const int32_t *tiles_per_gauss, int tile_size, int tile_width,
     int tile_height, int tile_bits, int cam_bits, const void *count_workspace,
     const int64_t *totals_device, int64_t capacity, int64_t *counts_device,
-    int32_t *status_device, void *workspace, int64_t workspace_bytes, int64_t *isect_ids,
-    int32_t *flatten_ids, void *stream);
+    int32_t *status_device, int64_t *counts_host_ring, const int64_t *slot_device,
+    void *workspace, int64_t workspace_bytes, int64_t *isect_ids, int32_t *flatten_ids,
+    void *stream);
 /* Sorted emission, tile-first (the default of isect_tiles(sort=True)): the
  * SAME isect_ids / flatten_ids again, from Gaussian-major emission with
  * 32-bit (camera, tile) keys, a stable sort by those keys, and a segmented
@@ -331,6 +336,22 @@ int gsplat_hip_l1_ssim_loss_fused_fwd(int B, int H, int W, int C, const float *i
                                       void *stream);
 int gsplat_hip_l1_ssim_loss_fused_bwd(int64_t n, const float *grad_unit, const float *g_loss,
                                       float *grad_img1, void *stream);
+
+/* The captured training step's per-step input without copy engines (ABI 22;
+ * gsplat_hip/graph_step.py, not a reference function):
+ * host_mapped_alloc: `bytes` of zeroed host memory, mapped and coherent
+ *   (fine-grained), *host_ptr for the host, *device_ptr for kernels; free
+ *   with host_mapped_free.
+ * step_fetch: one-wave launch: slot = seq_device[0] % n_ring; copies the
+ *   first slot_bytes - 8 bytes of ring slot `slot` (ring_device, n_ring
+ *   slots of slot_bytes, a multiple of 8) into block_device, writes `slot`
+ *   (i64) into its last 8 bytes and increments seq_device[0].  The host
+ *   fills slot k % n_ring before the k-th launch and reuses it only after
+ *   that launch's step has run. */
+int gsplat_hip_host_mapped_alloc(int64_t bytes, void **host_ptr, void **device_ptr);
+int gsplat_hip_host_mapped_free(void *host_ptr);
+int gsplat_hip_step_fetch(const void *ring_device, int64_t slot_bytes, int n_ring,
+                          int64_t *seq_device, void *block_device, void *stream);
 
 /* DefaultStrategy._update_state for packed=False (gsplat/strategy/default.py:
  * 213-262): for every (c, g) with radii[c,g] > 0, in camera order,
