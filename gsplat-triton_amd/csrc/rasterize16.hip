@@ -1113,6 +1113,9 @@ __attribute__((amdgpu_waves_per_eu(BwdOcc<PX>::W))) bwd2_kernel(Args a) {
         for (int kk = 0; kk < NV * 16; ++kk) v[kk] = f2v{0.f, 0.f};
 #pragma unroll
         for (int q = 0; q < PX; ++q) {
+          // this pair misses the wave's q-th 16x4 strip entirely (small
+          // Gaussians touch one strip of the band): nothing to add, T unchanged
+          if (PX > 1 && __ballot(v0[q] | v1[q]) == 0) continue;
           ex[q] = f2v{__builtin_amdgcn_exp2f(-s2[q].x), __builtin_amdgcn_exp2f(-s2[q].y)};
           ar[q] = f[5] * ex[q];
           const f2v al = f2v{fminf(ar[q].x, kAlphaMax), fminf(ar[q].y, kAlphaMax)};
