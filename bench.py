@@ -65,9 +65,10 @@ def parse():
                     help="issue every launch from the host each step instead of replaying "
                          "the step captured as a HIP graph")
     ap.add_argument("--dp-path", action="store_true",
-                    help="at N=1: run the N>1 code path (sharded Adam, early SH "
-                         "reduce-scatter, per-group communicators) over a 1-rank RCCL "
-                         "group -- the per-rank step of the data-parallel configuration")
+                    help="replicated data parallelism instead of the default Gaussian "
+                         "sharding at N>1 (every rank holds all Gaussians; sharded Adam, "
+                         "early SH reduce-scatter, per-group communicators); at N=1 that "
+                         "code path over a 1-rank RCCL group")
     ap.add_argument("--dp-emulate", type=int, default=0, metavar="W",
                     help="with --dp-path: shard the optimizer rows as W ranks would and "
                          "update this rank's share (the per-rank compute of a W-GPU step; "
@@ -147,13 +148,14 @@ def pmc_traffic(config: str):
 
 
 def _valu_frac(pmc, launch_ms):
-    """VALU issue: wave64 VALU instructions x 2 cycles (SIMD-32) against 1024
-    SIMDs x 2.4 GHz over the launch (MI355X_MICROARCH.md constants)."""
+    """VALU issue: wave64 VALU instructions x 4 cycles (a wave64 v_fma_f32
+    issues every 4 cycles per SIMD, tools/valu_bench.hip) against 1024 SIMDs
+    x 2.4 GHz over the launch."""
     ctr = (pmc or {}).get("counters", {})
     insts = ctr.get("SQ_INSTS_VALU")
     if not insts or not launch_ms == launch_ms:
         return None
-    peak = 1024 * 2.4e9 / 2.0  # wave64 VALU instructions per second, whole chip
+    peak = 1024 * 2.4e9 / 4.0  # wave64 VALU instructions per second, whole chip
     achieved = insts / (launch_ms * 1e-3)
     res = {"bound": "valu", "insts_per_launch": insts, "achieved": achieved, "peak": peak,
            "unit": "wave-instr/s", "frac": achieved / peak}
@@ -214,6 +216,8 @@ def main():
     if world != args.gpus:
         sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     cpu_pool = None
+    if world > 1:
+        args.no_cpu_baseline = True  # the CPU baseline is an N=1 measurement
     if rank == 0 and not args.no_cpu_baseline and not args.probe:
         # the CPU baseline's worker processes start before this process
         # touches the GPU (spawned interpreters running numpy only)
@@ -222,7 +226,10 @@ def main():
     if args.dp_emulate:
         args.dp_path = True
         assert world == 1, "--dp-emulate is a one-GPU measurement"
-    dp_path = world > 1 or args.dp_path
+    # N > 1: Gaussian-sharded training (the reference's multi-GPU scheme) unless
+    # --dp-path asks for the replicated one
+    dp_path = args.dp_path
+    gshard = world > 1 and not dp_path
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -255,7 +262,7 @@ def main():
                   init="sfm")
         start = max(0, REFINE_AT - args.warmup - args.steps // 2)
     tr = Trainer(means, rgbs, vm_pool, K_pool, W, H, sh_degree=3, device=dev, world_size=world,
-                 rank=rank, model=model, sharded_optimizer=dp_path,
+                 rank=rank, model=model, sharded_optimizer=dp_path, gaussian_shard=gshard,
                  dp_emulate_world=args.dp_emulate or None,
                  graph=not (args.eager or args.probe), **kw)
     graphed = getattr(tr, "_graph", None) is not None
@@ -376,10 +383,15 @@ def main():
         "data": "synthetic: garden SfM points (assets/test_garden.npz crop) tiled "
                 f"{grid}x{grid}, random scales/quats/opacities, random target images",
         "config": {"workload": desc, "gaussians": N,
-                   "gaussians_after": int(tr.params["means"].shape[0]),
+                   "gaussians_after": int(sum(tr._n_world) if gshard
+                                          else tr.params["means"].shape[0]),
                    "first_timed_step": start + args.warmup, "width": W, "height": H,
                    "cameras_per_rank_per_step": 1,
-                   "parallelism": f"dp{world}" + (
+                   "parallelism": (
+                       f"gshard{world}: rank r holds Gaussians [r::{world}] and renders its own "
+                       "camera; projected pairs exchanged peer to peer over RCCL/xGMI "
+                       "(rasterization(distributed=True)), per-shard Adam, no gradient "
+                       "all-reduce") if gshard else f"dp{world}" + (
                        f" emulating the per-rank compute of dp{args.dp_emulate}: optimizer rows "
                        f"sharded {args.dp_emulate} ways, this rank's share updated, no "
                        "collectives executed (measurement only)" if args.dp_emulate else
@@ -390,6 +402,7 @@ def main():
                    "step_issue": ("HIP graph replay of the captured step (sync-free isect, "
                                   f"{graph_info})" if graphed else "eager launches"),
                    "optimizer": "Adam (6 groups)" + (
+                       ", each rank on its own Gaussians" if gshard else
                        ", sharded over ranks" if dp_path else
                        ", SH groups' step fused into the SH backward"
                        if getattr(tr, "sh_adam_in_bwd", False) else ""),

@@ -38,8 +38,17 @@ def all_gather_int32(world_size: int, value: Union[int, Tensor],
 
 
 def _exchange(send: List[Tensor], recv: List[Tensor]) -> None:
-    """recv[j] <- rank j's send[me]; send[j] -> rank j (P2P, one op per peer)."""
+    """recv[j] <- rank j's send[me]; send[j] -> rank j (P2P, one op per peer).
+    gloo with GPU tensors (several ranks sharing one GPU in the tests) goes
+    through host copies: gloo's P2P moves host memory only."""
     me = dist.get_rank()
+    if send and send[0].is_cuda and dist.get_backend() == "gloo":
+        hs = [t.cpu() for t in send]
+        hr = [torch.empty(r.shape, dtype=r.dtype) for r in recv]
+        _exchange(hs, hr)
+        for r, h in zip(recv, hr):
+            r.copy_(h)
+        return
     recv[me].copy_(send[me])
     ops = []
     for j in range(len(send)):

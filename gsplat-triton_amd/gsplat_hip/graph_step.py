@@ -50,6 +50,7 @@ from .strategy import activate, update_state_
 def graphable(tr) -> bool:
     """Whether Trainer `tr` can run its steps as graph replays."""
     return (tr.fused and not tr.sharded and tr.world_size == 1 and tr.model == "3dgs"
+            and not getattr(tr, "gshard", False)
             and not getattr(tr, "defer_sh", False) and tr.strategy is None
             and isinstance(tr.opt, FusedAdam) and torch.device(tr.device).type == "cuda")
 

@@ -71,6 +71,8 @@ def rasterization(
     _isect_capacity: Optional[int] = None,
     _isect_status: Optional[Tensor] = None,
     _isect_report=None,
+    _world_cameras=None,
+    _world_counts=None,
 ) -> Tuple[Tensor, Tensor, Dict]:
     """Rasterize N 3D Gaussians to C images (gsplat/rendering.py:44-598).
 
@@ -83,7 +85,12 @@ def rasterization(
     capacity-sized, meta["isect_counts"] (device i64[4]: written, visible,
     overflow, n_isects) says how many are valid; an overflow also sets
     `_isect_status[0]` (sticky).  `_isect_report` = (host-mapped i64[ring][4]
-    device pointer, device i64 slot): the counts also go to that ring row."""
+    device pointer, device i64 slot): the counts also go to that ring row.
+    distributed=True: `_world_cameras` = (viewmats, Ks) of every rank's
+    cameras in rank order and `_world_counts` = every rank's Gaussian count,
+    when the caller knows them (a trainer's camera schedule and shard sizes):
+    the all-gathers of gsplat/rendering.py:303-308 -- one of them a host
+    read -- are then skipped."""
     meta = {}
     N = means.shape[0]
     C = viewmats.shape[0]
@@ -128,9 +135,19 @@ def rasterization(
             "Distributed mode only supports per-Gaussian colors."
         world_rank = torch.distributed.get_rank()
         world_size = torch.distributed.get_world_size()
-        N_world = gdist.all_gather_int32(world_size, N, device=device)
+        if _world_counts is not None:
+            N_world = [int(n) for n in _world_counts]
+            assert len(N_world) == world_size and N_world[world_rank] == N, (N_world, N)
+        else:
+            N_world = gdist.all_gather_int32(world_size, N, device=device)
         C_world = [C] * world_size
-        viewmats, Ks = gdist.all_gather_tensor_list(world_size, [viewmats, Ks])
+        if _world_cameras is not None:
+            vm_all, K_all = _world_cameras
+            assert vm_all.shape == (C * world_size, 4, 4) and K_all.shape == (C * world_size, 3, 3)
+            assert not viewmats.requires_grad, "_world_cameras: cameras without gradients"
+            viewmats, Ks = vm_all, K_all
+        else:
+            viewmats, Ks = gdist.all_gather_tensor_list(world_size, [viewmats, Ks])
         C = len(viewmats)
 
     proj = fully_fused_projection(

@@ -23,14 +23,26 @@ schedule (simple_trainer.py:600), `max_steps` the means ExponentialLR
 (:523-528), `init="sfm"` the SfM initialisation with knn scales, uniform
 quaternions and init_opacity (:212-233).
 
-Multi-GPU is per-camera data parallelism: every rank holds the same
-Gaussians and renders its own camera; the Gaussian gradients are summed over
-RCCL/xGMI by reduce-scatter, each rank runs Adam on its share of the rows,
-and the updated rows are all-gathered (distributed.ShardedAdam; the plain
-per-group all-reduce + full Adam is `sharded_optimizer=False`).  Before a
-refine the densification statistics are summed over the ranks and the split
-noise comes from a generator seeded identically on every rank, so the
-replicas stay identical.
+Multi-GPU, two schemes, one process per GPU, every rank rendering its own
+camera each step:
+* `gaussian_shard=True` (the reference's multi-GPU training,
+  simple_trainer.py:227-229,501 with gsplat/rendering.py:298-494): rank r
+  holds the Gaussians [r::world] with their own Adam state and strategy
+  statistics; the render is rasterization(distributed=True) -- the local
+  Gaussians projected into every rank's camera, the projected pairs
+  exchanged peer to peer over RCCL/xGMI, each rank rasterizing its camera
+  with all Gaussians -- and the backward exchanges their gradients back, so
+  each Gaussian's owner receives its gradient summed over all cameras.  No
+  gradient all-reduce: per step a rank moves its shard's projected pairs
+  (44 B each way per (Gaussian, camera)), not the whole scene's gradients.
+  Densification runs per rank on its own shard, as the reference does.
+* replicated (`sharded_optimizer`): every rank holds all Gaussians; the
+  gradients are summed over RCCL/xGMI by reduce-scatter, each rank runs Adam
+  on its share of the rows, and the updated rows are all-gathered
+  (distributed.ShardedAdam; the plain per-group all-reduce + full Adam is
+  `sharded_optimizer=False`).  Before a refine the densification statistics
+  are summed over the ranks and the split noise comes from a generator seeded
+  identically on every rank, so the replicas stay identical.
 """
 
 import dataclasses
@@ -140,7 +152,8 @@ class Trainer:
                  init: str = "random", init_opacity: float = 0.1, init_scale: float = 1.0,
                  targets: Optional[torch.Tensor] = None, opacity_reg: float = 0.0,
                  scale_reg: float = 0.0, dp_emulate_world: Optional[int] = None,
-                 graph: bool = False, isect_capacity: Optional[int] = None):
+                 graph: bool = False, isect_capacity: Optional[int] = None,
+                 gaussian_shard: bool = False):
         assert model in ("3dgs", "2dgs"), model
         assert init in ("random", "sfm"), init
         self.model = model
@@ -179,6 +192,16 @@ class Trainer:
             "means": points.clone(), "scales": scales, "quats": quats, "opacities": opac,
             "sh0": sh[:, :1].contiguous(), "shN": sh[:, 1:].contiguous(),
         }
+        # Gaussian-sharded: this rank's Gaussians [rank::world] of the scene
+        # initialised as a whole (simple_trainer.py:221-229: knn scales over
+        # all points, then the slice), so the shards together are the
+        # one-GPU scene exactly
+        self.gshard = bool(gaussian_shard)
+        if self.gshard:
+            assert model == "3dgs", "gaussian_shard: the 3DGS trainer"
+            self.params = {k: v[rank::world_size].contiguous() for k, v in self.params.items()}
+            self._n_world = [len(range(r, N, world_size)) for r in range(world_size)]
+            N = self.params["means"].shape[0]
         self.params = {k: torch.nn.Parameter(v.float().contiguous().to(device))
                        for k, v in self.params.items()}
         BS = world_size  # batch 1 per rank (simple_trainer.py:261-277)
@@ -191,7 +214,8 @@ class Trainer:
         # all-gathered (distributed.ShardedAdam) instead of all-reduce + full Adam
         # (None: when world_size > 1; True also at world_size 1, for tests)
         if sharded_optimizer is None:
-            sharded_optimizer = world_size > 1
+            sharded_optimizer = world_size > 1 and not self.gshard
+        assert not (self.gshard and sharded_optimizer), "gaussian_shard: a local optimizer"
         self.sharded = fused and sharded_optimizer
         # measurement only (bench.py --dp-emulate W): one rank shards its
         # optimizer rows as W ranks would (ShardedAdam emulate_world)
@@ -207,12 +231,13 @@ class Trainer:
         # SH-colour backward (gsplat_hip_sh_colors_bwd_adam), so their
         # gradients never go through HBM; GSPLAT_HIP_SH_ADAM_IN_BWD=0 turns it off
         self.sh_adam_in_bwd = (fused and not self.sharded and not self.defer_sh
-                               and world_size == 1
+                               and world_size == 1 and not self.gshard
                                and os.environ.get("GSPLAT_HIP_SH_ADAM_IN_BWD", "1") != "0")
         # the exp / sigmoid VJPs and the means-gradient sum formed inside the
         # geometry groups' Adam (gsplat_hip_adam_step_ex): at one rank, and
         # under the sharded optimizer on the reduced shard (ShardedAdam.step)
-        self.geom_fuse = (fused and not self.defer_sh and (world_size == 1 or self.sharded)
+        self.geom_fuse = (fused and not self.defer_sh
+                          and (world_size == 1 or self.sharded or self.gshard)
                           and os.environ.get("GSPLAT_HIP_GEOM_FUSE", "1") != "0")
         # sharded optimizer: the SH group's collectives on a communicator of
         # their own (issued from a gradient hook during the backward), the
@@ -236,8 +261,10 @@ class Trainer:
         # Gaussian normalised by max(W, H), tracked only while it is used
         self.radii2d = (torch.zeros(N, device=device) if self.strategy is not None
                         and self.strategy.refine_scale2d_stop_iter > 0 else None)
-        # split noise: the same stream on every rank (replicas stay identical)
-        self.rng = torch.Generator(device=device).manual_seed(seed)
+        # split noise: the same stream on every rank (replicas stay identical);
+        # Gaussian-sharded: a stream per shard
+        self.rng = torch.Generator(device=device).manual_seed(
+            seed + (7919 * rank if self.gshard else 0))
         self.window = _gauss_window(device=device)
         self.last_meta = None
         self.refine_log = []  # (step, n_dupli, n_split, n_prune, N after)
@@ -359,10 +386,28 @@ class Trainer:
             return self.sh_degree
         return min(it // self.sh_degree_interval, self.sh_degree)
 
+    def world_cameras(self, ci: int, world_ci=None):
+        """Gaussian-sharded: the (viewmats, Ks) of every rank's camera, rank
+        order -- the training schedule's (rank r renders (it*world + r) % n)
+        or an explicit list `world_ci`."""
+        n = len(self.viewmats)
+        if world_ci is None:
+            world_ci = [(ci - self.rank + r) % n for r in range(self.world_size)]
+        key = tuple(int(c) for c in world_ci)
+        cache = self.__dict__.setdefault("_wcam_cache", {})
+        if key not in cache:
+            if len(cache) > 4 * n:
+                cache.clear()
+            idx = torch.tensor(key, device=self.viewmats.device)
+            cache[key] = (self.viewmats.index_select(0, idx), self.Ks.index_select(0, idx))
+        return cache[key]
+
     def render(self, ci: int, sh_degree: Optional[int] = None,
-               fusion: Optional[_wrapper.StepFusion] = None):
+               fusion: Optional[_wrapper.StepFusion] = None, world_ci=None):
         """Render camera `ci`; `fusion` (a training step's StepFusion) goes to
-        the nodes whose backward hands their gradients to the optimizer."""
+        the nodes whose backward hands their gradients to the optimizer.
+        Gaussian-sharded: a collective -- every rank renders its own camera
+        with all ranks' Gaussians (`world_ci`: see world_cameras)."""
         p = self.params
         deg = self.sh_degree if sh_degree is None else sh_degree
         hook = None
@@ -389,12 +434,17 @@ class Trainer:
                 sh_degree=deg, packed=False, near_plane=0.01, far_plane=1e10,
                 render_mode="RGB+D", absgrad=absgrad, _fusion=fusion)
             return rc[..., :3], ra, meta
+        dkw = {}
+        if getattr(self, "gshard", False):
+            dkw = dict(distributed=True, _world_cameras=self.world_cameras(ci, world_ci),
+                       _world_counts=self._n_world)
         return rasterization(
             p["means"], p["quats"], scales, opac,
             (p["sh0"], p["shN"]) if self.fused else torch.cat([p["sh0"], p["shN"]], 1),
             self.viewmats[ci:ci + 1], self.Ks[ci:ci + 1], self.width, self.height,
             sh_degree=deg, packed=False, near_plane=0.01, far_plane=1e10, radius_clip=0.0,
-            rasterize_mode="classic", absgrad=absgrad, _colors_ready=hook, _fusion=fusion)
+            rasterize_mode="classic", absgrad=absgrad, _colors_ready=hook, _fusion=fusion,
+            **dkw)
 
     def step(self, it: int):
         if getattr(self, "_graph", None) is not None:
@@ -425,7 +475,7 @@ class Trainer:
             torch.autograd.backward(loss, _losses.ONE_GRAD)
         else:
             loss.backward()
-        if self.world_size > 1 and not self.sharded:
+        if self.world_size > 1 and not self.sharded and not getattr(self, "gshard", False):
             self.allreduce_grads()
         if self.strategy is None or it < self.strategy.refine_stop_iter:
             self.update_state(meta)
@@ -532,8 +582,10 @@ class Trainer:
         saved = self.viewmats, self.Ks
         try:
             self.viewmats, self.Ks = viewmats.to(self.device), Ks.to(self.device)
+            self.__dict__.pop("_wcam_cache", None)
             for i in range(len(viewmats)):
-                colors, _, _ = self.render(i)
+                # Gaussian-sharded: every rank renders camera i (a collective)
+                colors, _, _ = self.render(i, world_ci=[i] * self.world_size)
                 colors = torch.clamp(colors, 0.0, 1.0)
                 gt = images[i:i + 1].to(self.device)
                 mse = torch.mean((colors - gt) ** 2)
@@ -541,6 +593,7 @@ class Trainer:
                 ssims.append(float(ssim_and_l1(colors, gt)[0]))
         finally:
             self.viewmats, self.Ks = saved
+            self.__dict__.pop("_wcam_cache", None)
         return {"psnr": sum(psnrs) / len(psnrs), "ssim": sum(ssims) / len(ssims),
                 "num_images": len(psnrs)}
 
@@ -560,7 +613,7 @@ class Trainer:
     def refine(self, it: int):
         self.sync()
         self.last_meta = None  # its tensors are sized for the old Gaussians
-        if self.world_size > 1:
+        if self.world_size > 1 and not getattr(self, "gshard", False):
             # every rank accumulated its own cameras: the batch statistics are
             # the sums (the screen radii: their maximum)
             import torch.distributed as dist
@@ -584,6 +637,9 @@ class Trainer:
         if self.radii2d is not None:
             self.radii2d = torch.zeros(n, device=self.device)
         self.refine_log.append((it,) + tuple(counts) + (n,))
+        if getattr(self, "gshard", False) and self.world_size > 1:  # each shard refined alone
+            from .distributed import all_gather_int32
+            self._n_world = all_gather_int32(self.world_size, n, device=self.device)
 
     @torch.no_grad()
     def reset_opacity(self):

@@ -1,0 +1,187 @@
+"""GPU: Gaussian-sharded multi-GPU training (rasterization(distributed=True),
+Trainer(gaussian_shard=True)) at world size 2 -- two processes sharing the
+one GPU of the box, talking over gloo (the exchange stages GPU tensors
+through host memory there; on a node RCCL moves them over xGMI).
+
+* each rank renders its own camera with both ranks' Gaussians: the images
+  equal a one-process render of the whole scene, and each rank's local
+  gradients equal the whole-scene gradients of the two cameras' summed loss
+  at its Gaussians [rank::2] (float atomics: last bits);
+* one trainer step per rank equals one whole-scene step that renders both
+  cameras, sums their losses and runs Adam with the batch-2 hyperparameters
+  (simple_trainer.py:261-277) -- the reference's multi-GPU training step.
+"""
+
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import gsplat_hip  # noqa: F401
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _scene(N=24000, W=320, H=240, seed=5):
+    g = torch.Generator().manual_seed(seed)
+    means = torch.randn(N, 3, generator=g) * torch.tensor([1.4, 1.0, 0.6])
+    means[:, 2] += 4.0
+    quats = torch.randn(N, 4, generator=g)
+    scales = torch.rand(N, 3, generator=g) * 0.05 + 0.005
+    opac = torch.rand(N, generator=g)
+    sh0 = torch.randn(N, 1, 3, generator=g) * 0.3
+    shN = torch.randn(N, 15, 3, generator=g) * 0.05
+    vm = torch.eye(4).repeat(2, 1, 1)
+    vm[1, 0, 3] = 0.3
+    K = torch.tensor([[300.0, 0, W / 2], [0, 300.0, H / 2], [0, 0, 1]]).repeat(2, 1, 1)
+    w = torch.rand(2, H, W, 3, generator=g) - 0.5
+    return (means, quats, scales, opac, sh0, shN), vm, K, w, W, H
+
+
+def _render_rank(rank, world, port, out_dir):
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    try:
+        import gsplat_hip
+        ins, vm, K, w, W, H = _scene()
+        N = ins[0].shape[0]
+        local = [t[rank::world].contiguous().to(DEV).requires_grad_(True) for t in ins]
+        n_world = [len(range(r, N, world)) for r in range(world)]
+        rc, ra, meta = gsplat_hip.rasterization(
+            local[0], local[1], local[2], local[3], (local[4], local[5]),
+            vm[rank:rank + 1].to(DEV), K[rank:rank + 1].to(DEV), W, H, sh_degree=3,
+            packed=False, distributed=True,
+            _world_cameras=(vm.to(DEV), K.to(DEV)), _world_counts=n_world)
+        (rc * w[rank:rank + 1].to(DEV)).sum().backward()
+        torch.cuda.synchronize()
+        torch.save({"rc": rc.detach().cpu(), "ra": ra.detach().cpu(),
+                    "grads": [t.grad.cpu() for t in local],
+                    "n_cameras": meta["n_cameras"], "radii": meta["radii"].cpu()},
+                   os.path.join(out_dir, f"render{rank}.pt"))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gshard_render_matches_whole_scene(tmp_path):
+    import torch.multiprocessing as mp
+    import gsplat_hip
+    from test_gpu_parity import close_most
+    mp.spawn(_render_rank, args=(2, _port(), str(tmp_path)), nprocs=2, join=True)
+    ins, vm, K, w, W, H = _scene()
+    full = [t.to(DEV).requires_grad_(True) for t in ins]
+    rc, ra, meta = gsplat_hip.rasterization(
+        full[0], full[1], full[2], full[3], (full[4], full[5]), vm.to(DEV), K.to(DEV), W, H,
+        sh_degree=3, packed=False)
+    (rc * w.to(DEV)).sum().backward()
+    for r in range(2):
+        got = torch.load(os.path.join(tmp_path, f"render{r}.pt"), weights_only=True)
+        assert got["n_cameras"] == 1
+        assert torch.equal(got["radii"], meta["radii"][:, r::2].cpu())  # [C_world, N_local]
+        # the same Gaussians per tile in the same depth order: ties aside, the same image
+        close_most(got["rc"][0], rc[r], 1e-5, 1e-5, f"colors rank {r}")
+        close_most(got["ra"][0], ra[r], 1e-5, 1e-5, f"alphas rank {r}")
+        for name, a, t in zip(("means", "quats", "scales", "opacities", "sh0", "shN"),
+                              got["grads"], full):
+            b = t.grad[r::2].cpu()
+            scale = max(1e-12, float(b.abs().max()))
+            close_most(a, b, 1e-3, 1e-4 * scale, f"{name} grad rank {r}", rows=a.dim() > 1,
+                       out_bound=0.05 * scale)
+
+
+def _trainer_rank(rank, world, port, out_dir):
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    try:
+        from gsplat_hip.train_step import Trainer
+        means, rgbs, vm, K, W, H = _trainer_scene()
+        tr = Trainer(means, rgbs, vm, K, W, H, device=DEV, world_size=world, rank=rank,
+                     gaussian_shard=True)
+        assert tr.gshard and not tr.sharded and not tr.sh_adam_in_bwd
+        tr.step(0)
+        tr.sync()
+        torch.save({"params": {k: p.detach().cpu() for k, p in tr.params.items()},
+                    "count": tr.count.cpu(), "grad2d": tr.grad2d.cpu(),
+                    "n_world": tr._n_world},
+                   os.path.join(out_dir, f"trainer{rank}.pt"))
+    finally:
+        dist.destroy_process_group()
+
+
+def _trainer_scene(W=320, H=240):
+    from gsplat_hip.train_step import camera_pool, load_garden_scene
+    means, rgbs, vms, Ks, sw, sh_ = load_garden_scene(
+        os.path.join(ROOT, "tests", "golden", "garden_scene.npz"), scene_grid=1)
+    means, rgbs = means[::8].contiguous(), rgbs[::8].contiguous()
+    vm, K = camera_pool(vms, Ks, sw, sh_, W, H, n=4)
+    return means, rgbs, vm, K, W, H
+
+
+def test_gshard_trainer_step_matches_whole_scene_step(tmp_path):
+    import math
+    import torch.multiprocessing as mp
+    from gsplat_hip.losses import FusedAdam, l1_ssim_loss
+    from gsplat_hip.rendering import rasterization
+    from gsplat_hip.strategy import update_state_
+    from gsplat_hip.train_step import Trainer
+    from test_gpu_parity import close_most
+    mp.spawn(_trainer_rank, args=(2, _port(), str(tmp_path)), nprocs=2, join=True)
+    means, rgbs, vm, K, W, H = _trainer_scene()
+    # the whole scene, initialised as the shards were (same generator draws)
+    ref = Trainer(means, rgbs, vm, K, W, H, device=DEV, world_size=1, fused=True)
+    params = {k: torch.nn.Parameter(p.detach().clone()) for k, p in ref.params.items()}
+    N = params["means"].shape[0]
+    BS = 2
+    lrs = [Trainer.LRS[k] * math.sqrt(BS) for k in params]
+    opt = FusedAdam(list(params.values()), lrs, eps=1e-15 / math.sqrt(BS),
+                    betas=(1 - BS * (1 - 0.9), 1 - BS * (1 - 0.999)))
+    grad2d = torch.zeros(N, device=DEV)
+    count = torch.zeros(N, device=DEV)
+    loss = 0.0
+    metas = []
+    for ci in (0, 1):  # step 0: rank r renders camera (0 * 2 + r) % n = r
+        scales, opac = torch.exp(params["scales"]), torch.sigmoid(params["opacities"])
+        colors, _, meta = rasterization(
+            params["means"], params["quats"], scales, opac, (params["sh0"], params["shN"]),
+            vm[ci:ci + 1].to(DEV), K[ci:ci + 1].to(DEV), W, H, sh_degree=3, packed=False,
+            near_plane=0.01, far_plane=1e10, radius_clip=0.0)
+        meta["means2d"].retain_grad()
+        metas.append(meta)
+        loss = loss + l1_ssim_loss(colors, ref.targets[ci:ci + 1], 0.2)
+    loss.backward()
+    for meta in metas:
+        update_state_(grad2d, count, meta["means2d"].grad, meta["radii"], W, H, 1)
+    opt.step()
+    for r in range(2):
+        got = torch.load(os.path.join(tmp_path, f"trainer{r}.pt"), weights_only=True)
+        assert got["n_world"] == [len(range(0, N, 2)), len(range(1, N, 2))]
+        assert torch.equal(got["count"], count[r::2].cpu())
+        close_most(got["grad2d"], grad2d[r::2].cpu(), 1e-4, 1e-6, f"grad2d rank {r}")
+        for k, p in params.items():
+            b = p.detach()[r::2].cpu()
+            a = got["params"][k]
+            assert a.shape == b.shape, (k, a.shape, b.shape)
+            # Adam's first step moves each entry by about +-lr: a gradient
+            # within rounding of zero may take either sign (a few entries)
+            close_most(a, b, 1e-5, 1e-6, f"{k} rank {r}", max_frac=2e-3,
+                       out_bound=2.5 * lrs[list(params).index(k)])
