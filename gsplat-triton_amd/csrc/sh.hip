@@ -334,11 +334,21 @@ GS_INLINE void adam_rows(float *P, float *M, float *V, const float *g, int rows,
   }
 }
 
-template <int DEG, bool FUSED, int KR = (DEG + 1) * (DEG + 1) - 1, bool ADAM = false>
+// CAMS (FUSED): the row of lane i is Gaussian i seen from all C cameras of
+// fz (C = fz's camera count, rows c * N + i of radii / v_colors): the
+// coefficients are read once, the gradient rows and the means gradient
+// (v_dirs [N, 3]) are summed over the cameras in registers -- the shared
+// coefficients of a Gaussian-sharded render's N-camera colours, whose sum
+// is also what the fused Adam needs.  C == 1 is the one-camera kernel.
+template <int DEG, bool FUSED, int KR = (DEG + 1) * (DEG + 1) - 1, bool ADAM = false,
+          bool CAMS = false>
 __global__ void __launch_bounds__(256)
 sh_bwd_staged_kernel(int64_t n, Coeffs cf, const float *__restrict__ dirs,
                      const uint8_t *__restrict__ masks, const float *__restrict__ v_colors,
-                     VCoeffs vc, float *__restrict__ v_dirs, Fused fz, AdamSH ad = AdamSH{}) {
+                     VCoeffs vc, float *__restrict__ v_dirs, Fused fz, AdamSH ad = AdamSH{},
+                     int C = 1) {
+  static_assert(!CAMS || FUSED, "the camera loop is the fused colour path's");
+  if (!CAMS) C = 1;
   constexpr int NB = (DEG + 1) * (DEG + 1), WR = 3 * KR, RSR = WR | 1;
   static_assert(KR >= NB - 1, "KR covers the active coefficients");
   __shared__ float l_dc[4][64 * 3];               // row stride 3 (odd)
@@ -349,7 +359,10 @@ sh_bwd_staged_kernel(int64_t n, Coeffs cf, const float *__restrict__ dirs,
   const int rows = (int)min<int64_t>(64, n - i0);
   const int64_t i = i0 + lane;
   float *sd = l_dc[wid], *sr = l_rest[wid];
-  const bool on = lane < rows && (FUSED ? fz.radii[i] > 0 : (!masks || masks[i]));
+  bool seen = false;
+  if (FUSED && lane < rows)
+    for (int c = 0; c < (CAMS ? C : 1); ++c) seen |= fz.radii[(int64_t)c * fz.N + i] > 0;
+  const bool on = lane < rows && (FUSED ? seen : (!masks || masks[i]));
   float *rd = sd + lane * 3, *rw = sr + lane * RSR;
   // this lane's gradient row in LDS (coefficient k, channel ch)
   auto grow = [&](int k, int ch) -> float & { return k == 0 ? rd[ch] : rw[3 * (k - 1) + ch]; };
@@ -365,37 +378,43 @@ sh_bwd_staged_kernel(int64_t n, Coeffs cf, const float *__restrict__ dirs,
         for (int ch = 0; ch < 3; ++ch) cr[k][ch] = k == 0 ? p0[ch] : pr[3 * (k - 1) + ch];
     }
     auto coef = [&](int k, int ch) { return cr[k][ch]; };
-    float vr = v_colors[3 * i], vg = v_colors[3 * i + 1], vb = v_colors[3 * i + 2];
-    float x = 0.f, y = 0.f, z = 0.f, inorm = 0.f;
-    if (DEG > 0) {
-      if (FUSED) {
-        fused_dir(fz, i, x, y, z);
-      } else {
-        x = dirs[3 * i]; y = dirs[3 * i + 1]; z = dirs[3 * i + 2];
-      }
-      inorm = rsqrtf(x * x + y * y + z * z);
-      x *= inorm; y *= inorm; z *= inorm;
-    }
-    float B[NB];
-    float dB[NB][3];
     const bool want_dirs = (v_dirs != nullptr) && DEG > 0;
-    if (want_dirs) sh_basis<DEG, true>(x, y, z, B, dB);
-    else sh_basis<DEG, false>(x, y, z, B, nullptr);
-    if (FUSED) {  // clamp_min(sh + 0.5, 0) passes the gradient where sh + 0.5 >= 0
-      float r = 0.f, g = 0.f, b = 0.f;
+    float ga[NB][3];
 #pragma unroll
-      for (int k = 0; k < NB; ++k) {
-        r += B[k] * coef(k, 0);
-        g += B[k] * coef(k, 1);
-        b += B[k] * coef(k, 2);
-      }
-      vr = (r + 0.5f >= 0.f) ? vr : 0.f;
-      vg = (g + 0.5f >= 0.f) ? vg : 0.f;
-      vb = (b + 0.5f >= 0.f) ? vb : 0.f;
-    }
-    if (v_dirs) {
-      float vx = 0.f, vy = 0.f, vz = 0.f;
+    for (int k = 0; k < NB; ++k) ga[k][0] = ga[k][1] = ga[k][2] = 0.f;
+    float sx = 0.f, sy = 0.f, sz = 0.f;  // the means gradient, summed over cameras
+    for (int c = 0; c < (CAMS ? C : 1); ++c) {
+      const int64_t ri = CAMS ? (int64_t)c * fz.N + i : i;
+      if (CAMS && !(fz.radii[ri] > 0)) continue;
+      float vr = v_colors[3 * ri], vg = v_colors[3 * ri + 1], vb = v_colors[3 * ri + 2];
+      float x = 0.f, y = 0.f, z = 0.f, inorm = 0.f;
       if (DEG > 0) {
+        if (FUSED) {
+          fused_dir(fz, ri, x, y, z);
+        } else {
+          x = dirs[3 * i]; y = dirs[3 * i + 1]; z = dirs[3 * i + 2];
+        }
+        inorm = rsqrtf(x * x + y * y + z * z);
+        x *= inorm; y *= inorm; z *= inorm;
+      }
+      float B[NB];
+      float dB[NB][3];
+      if (want_dirs) sh_basis<DEG, true>(x, y, z, B, dB);
+      else sh_basis<DEG, false>(x, y, z, B, nullptr);
+      if (FUSED) {  // clamp_min(sh + 0.5, 0) passes the gradient where sh + 0.5 >= 0
+        float r = 0.f, g = 0.f, b = 0.f;
+#pragma unroll
+        for (int k = 0; k < NB; ++k) {
+          r += B[k] * coef(k, 0);
+          g += B[k] * coef(k, 1);
+          b += B[k] * coef(k, 2);
+        }
+        vr = (r + 0.5f >= 0.f) ? vr : 0.f;
+        vg = (g + 0.5f >= 0.f) ? vg : 0.f;
+        vb = (b + 0.5f >= 0.f) ? vb : 0.f;
+      }
+      if (want_dirs) {
+        float vx = 0.f, vy = 0.f, vz = 0.f;
 #pragma unroll
         for (int k = 1; k < NB; ++k) {
           const float w = coef(k, 0) * vr + coef(k, 1) * vg + coef(k, 2) * vb;
@@ -405,17 +424,25 @@ sh_bwd_staged_kernel(int64_t n, Coeffs cf, const float *__restrict__ dirs,
         }
         // VJP of the normalisation (sh_bwd.py:367-380)
         const float dot = x * vx + y * vy + z * vz;
-        vx = (vx - dot * x) * inorm;
-        vy = (vy - dot * y) * inorm;
-        vz = (vz - dot * z) * inorm;
+        sx += (vx - dot * x) * inorm;
+        sy += (vy - dot * y) * inorm;
+        sz += (vz - dot * z) * inorm;
       }
-      v_dirs[3 * i] = vx; v_dirs[3 * i + 1] = vy; v_dirs[3 * i + 2] = vz;
+#pragma unroll
+      for (int k = 0; k < NB; ++k) {
+        ga[k][0] += B[k] * vr;
+        ga[k][1] += B[k] * vg;
+        ga[k][2] += B[k] * vb;
+      }
+    }
+    if (v_dirs) {
+      v_dirs[3 * i] = sx; v_dirs[3 * i + 1] = sy; v_dirs[3 * i + 2] = sz;
     }
 #pragma unroll
     for (int k = 0; k < NB; ++k) {
-      grow(k, 0) = B[k] * vr;
-      grow(k, 1) = B[k] * vg;
-      grow(k, 2) = B[k] * vb;
+      grow(k, 0) = ga[k][0];
+      grow(k, 1) = ga[k][1];
+      grow(k, 2) = ga[k][2];
     }
 #pragma unroll
     for (int k = NB; k <= KR; ++k) grow(k, 0) = grow(k, 1) = grow(k, 2) = 0.f;
@@ -586,12 +613,12 @@ extern "C" int gsplat_hip_sh_colors_bwd(int degree, int C, int64_t N, int64_t n_
 // coeffs_rest are updated in place with torch.optim.Adam (lr0 / lr_rest,
 // shared betas / eps, 1-based step) from the gradient this backward computes,
 // which is never stored; v_dirs as in gsplat_hip_sh_colors_bwd.
-static int sh_colors_bwd_adam_launch(int degree, int64_t N, const float *means,
+static int sh_colors_bwd_adam_launch(int degree, int C, int64_t N, const float *means,
                                      const float *viewmats, float *coeffs, float *coeffs_rest,
                                      const int32_t *radii, const float *v_colors, float *v_dirs,
                                      const AdamSH &ad, hipStream_t st);
 
-extern "C" int gsplat_hip_sh_colors_bwd_adam(int degree, int64_t N, const float *means,
+extern "C" int gsplat_hip_sh_colors_bwd_adam(int degree, int C, int64_t N, const float *means,
                                              const float *viewmats, float *coeffs,
                                              float *coeffs_rest, const int32_t *radii,
                                              const float *v_colors, float *v_dirs, float *m0,
@@ -609,7 +636,7 @@ extern "C" int gsplat_hip_sh_colors_bwd_adam(int degree, int64_t N, const float 
   const double bc1 = 1.0 - pow((double)beta1, step), bc2 = 1.0 - pow((double)beta2, step);
   AdamSH ad{m0, v0, m_rest, v_rest, (float)(lr0 / bc1), (float)(lr_rest / bc1),
             (float)(1.0 / sqrt(bc2)), beta1, beta2, eps, nullptr, nullptr};
-  return sh_colors_bwd_adam_launch(degree, N, means, viewmats, coeffs, coeffs_rest, radii,
+  return sh_colors_bwd_adam_launch(degree, C, N, means, viewmats, coeffs, coeffs_rest, radii,
                                    v_colors, v_dirs, ad, (hipStream_t)stream);
 }
 
@@ -617,7 +644,8 @@ extern "C" int gsplat_hip_sh_colors_bwd_adam(int degree, int64_t N, const float 
 // captured training step): hyper_device = {lr0 / (1 - beta1^t),
 // lr_rest / (1 - beta1^t), 1 / sqrt(1 - beta2^t)}; skip_device (may be NULL)
 // non-zero: the coefficients and moments are left alone (v_dirs is written).
-extern "C" int gsplat_hip_sh_colors_bwd_adam_dev(int degree, int64_t N, const float *means,
+extern "C" int gsplat_hip_sh_colors_bwd_adam_dev(int degree, int C, int64_t N,
+                                                 const float *means,
                                                  const float *viewmats, float *coeffs,
                                                  float *coeffs_rest, const int32_t *radii,
                                                  const float *v_colors, float *v_dirs, float *m0,
@@ -633,25 +661,61 @@ extern "C" int gsplat_hip_sh_colors_bwd_adam_dev(int degree, int64_t N, const fl
                (uintptr_t)m_rest | (uintptr_t)v_rest) & 15) == 0,
              "sh_colors_bwd_adam: coefficient and moment buffers must be 16-B aligned");
   AdamSH ad{m0, v0, m_rest, v_rest, 0.f, 0.f, 0.f, beta1, beta2, eps, hyper_device, skip_device};
-  return sh_colors_bwd_adam_launch(degree, N, means, viewmats, coeffs, coeffs_rest, radii,
+  return sh_colors_bwd_adam_launch(degree, C, N, means, viewmats, coeffs, coeffs_rest, radii,
                                    v_colors, v_dirs, ad, (hipStream_t)stream);
 }
 
-static int sh_colors_bwd_adam_launch(int degree, int64_t N, const float *means,
+static int sh_colors_bwd_adam_launch(int degree, int C, int64_t N, const float *means,
                                      const float *viewmats, float *coeffs, float *coeffs_rest,
                                      const int32_t *radii, const float *v_colors, float *v_dirs,
                                      const AdamSH &ad, hipStream_t st) {
+  GS_REQUIRE(C >= 1, "sh_colors_bwd_adam: C=%d cameras", C);
   Coeffs cf{coeffs, coeffs_rest, 3, 45};
   VCoeffs vc{nullptr, nullptr, 3, 45};
   const Fused fz{means, viewmats, radii, N};
   dim3 grid((unsigned)((N + 255) / 256));
-#define GS_SH_BWD_ADAM(D)                                                                      \
-  case D:                                                                                      \
-    hipLaunchKernelGGL((sh_bwd_staged_kernel<D, true, 15, true>), grid, dim3(256), 0, st, N, cf, \
-                       nullptr, nullptr, v_colors, vc, v_dirs, fz, ad);                        \
+#define GS_SH_BWD_ADAM(D)                                                                        \
+  case D:                                                                                        \
+    if (C == 1)                                                                                  \
+      hipLaunchKernelGGL((sh_bwd_staged_kernel<D, true, 15, true>), grid, dim3(256), 0, st, N,   \
+                         cf, nullptr, nullptr, v_colors, vc, v_dirs, fz, ad, 1);                 \
+    else                                                                                         \
+      hipLaunchKernelGGL((sh_bwd_staged_kernel<D, true, 15, true, true>), grid, dim3(256), 0, st, \
+                         N, cf, nullptr, nullptr, v_colors, vc, v_dirs, fz, ad, C);              \
     break;
   switch (degree) { GS_SH_BWD_ADAM(0) GS_SH_BWD_ADAM(1) GS_SH_BWD_ADAM(2) GS_SH_BWD_ADAM(3) }
 #undef GS_SH_BWD_ADAM
   GS_CHECK_LAUNCH("sh_colors_bwd_adam");
+  return 0;
+}
+
+// rasterization()'s colour backward for C cameras sharing the coefficient
+// rows (one [N] row set, the trainer's sh0 [N,1,3] + shN [N,15,3]): v_coeffs
+// / v_coeffs_rest [N] and v_dirs [N, 3] are the sums over the cameras, formed
+// in registers (gsplat_hip_sh_colors_bwd writes per-camera rows that torch
+// then sums).  The Gaussian-sharded render's colours (C = world cameras).
+extern "C" int gsplat_hip_sh_colors_bwd_sum(int degree, int C, int64_t N, const float *means,
+                                            const float *viewmats, const float *coeffs,
+                                            const float *coeffs_rest, const int32_t *radii,
+                                            const float *v_colors, float *v_coeffs,
+                                            float *v_coeffs_rest, float *v_dirs, void *stream) {
+  if (N <= 0) return 0;
+  GS_REQUIRE(degree >= 0 && degree <= 3, "sh_colors_bwd_sum: degree %d not in [0, 3]", degree);
+  GS_REQUIRE(C >= 1, "sh_colors_bwd_sum: C=%d cameras", C);
+  GS_REQUIRE(coeffs && coeffs_rest && v_coeffs && v_coeffs_rest,
+             "sh_colors_bwd_sum: coefficients as (sh0 [N,1,3], shN [N,15,3]) and both gradients");
+  Coeffs cf{coeffs, coeffs_rest, 3, 45};
+  VCoeffs vc{v_coeffs, v_coeffs_rest, 3, 45};
+  const Fused fz{means, viewmats, radii, N};
+  dim3 grid((unsigned)((N + 255) / 256));
+  hipStream_t st = (hipStream_t)stream;
+#define GS_SH_BWD_SUM(D)                                                                        \
+  case D:                                                                                       \
+    hipLaunchKernelGGL((sh_bwd_staged_kernel<D, true, 15, false, true>), grid, dim3(256), 0, st, \
+                       N, cf, nullptr, nullptr, v_colors, vc, v_dirs, fz, AdamSH{}, C);         \
+    break;
+  switch (degree) { GS_SH_BWD_SUM(0) GS_SH_BWD_SUM(1) GS_SH_BWD_SUM(2) GS_SH_BWD_SUM(3) }
+#undef GS_SH_BWD_SUM
+  GS_CHECK_LAUNCH("sh_colors_bwd_sum");
   return 0;
 }

@@ -650,8 +650,9 @@ class ShAdamInBackward:
     def matches(self, base, rest, C, N, K, n_rows, degree):
         # degree 3 only: the staged kernel of the unfused backward at K == 16,
         # so the two paths are bit-identical (lower degrees of the SH schedule
-        # take the unfused path)
-        return (not self.applied and C == 1 and rest is not None and K == 16 and n_rows == N
+        # take the unfused path); C cameras sharing the coefficient rows (a
+        # Gaussian-sharded render) sum their gradients in the kernel first
+        return (not self.applied and rest is not None and K == 16 and n_rows == N
                 and degree == 3 and base.data_ptr() == self.coeffs.data_ptr()
                 and rest.data_ptr() == self.coeffs_rest.data_ptr()
                 and self.coeffs.is_contiguous() and self.coeffs_rest.is_contiguous())
@@ -693,29 +694,28 @@ class _SHColors(torch.autograd.Function):
         K = ctx.K
         v_colors = _f32c(v_colors)
         dev = means.device
-        if rest is None:
-            v_coeffs = torch.empty(C, N, K, 3, device=dev)
-            v_rest = None
-        else:
-            v_coeffs = torch.empty(C, N, 1, 3, device=dev)
-            v_rest = torch.empty(C, N, K - 1, 3, device=dev)
         want_means = ctx.needs_input_grad[1]
         # C == 1: a plain [N, 3] tensor (same bytes as [1, N, 3]), so autograd's
         # gradient accumulation can take it over instead of copying a view
-        v_dirs = (torch.empty(N, 3, device=dev) if C == 1 else
-                  torch.empty(C, N, 3, device=dev)) if want_means else None
         fusion = ctx.fusion
         fa = None if fusion is None else fusion.sh_adam
-        if fa is not None and fa.matches(base, rest, C, N, K, ctx.n_rows, ctx.sh_degree):
+        fused_adam = fa is not None and fa.matches(base, rest, C, N, K, ctx.n_rows, ctx.sh_degree)
+        # C cameras sharing the coefficient rows (the trainer's layout): the
+        # sums over the cameras formed in the kernel (gsplat_hip_sh_colors_bwd_sum)
+        shared = (C > 1 and rest is not None and K == 16 and ctx.n_rows == N
+                  and ctx.sh_degree <= 3 and len(ctx.coeff_shape) == 3)
+        v_dirs = (torch.empty(N, 3, device=dev) if C == 1 or fused_adam or shared else
+                  torch.empty(C, N, 3, device=dev)) if want_means else None
+        if fused_adam:
             m0, v0, mr, vr = fa.moments
             if fa.hyper is not None:
-                _lib.call("gsplat_hip_sh_colors_bwd_adam_dev", ctx.sh_degree, N, _ptr(means),
+                _lib.call("gsplat_hip_sh_colors_bwd_adam_dev", ctx.sh_degree, C, N, _ptr(means),
                           _ptr(viewmats), _ptr(base), _ptr(rest), _ptr(radii), _ptr(v_colors),
                           _ptr(v_dirs), _ptr(m0), _ptr(v0), _ptr(mr), _ptr(vr), _ptr(fa.hyper),
                           ctypes.c_float(fa.betas[0]), ctypes.c_float(fa.betas[1]),
                           ctypes.c_float(fa.eps), _ptr(fa.skip), _stream())
             else:
-                _lib.call("gsplat_hip_sh_colors_bwd_adam", ctx.sh_degree, N, _ptr(means),
+                _lib.call("gsplat_hip_sh_colors_bwd_adam", ctx.sh_degree, C, N, _ptr(means),
                           _ptr(viewmats), _ptr(base), _ptr(rest), _ptr(radii), _ptr(v_colors),
                           _ptr(v_dirs), _ptr(m0), _ptr(v0), _ptr(mr), _ptr(vr),
                           ctypes.c_float(fa.lr0), ctypes.c_float(fa.lr_rest),
@@ -723,6 +723,23 @@ class _SHColors(torch.autograd.Function):
                           ctypes.c_float(fa.eps), int(fa.step), _stream())
             fa.applied = True
             return (None, fusion.take_means_grad(v_dirs), None, None, None, None, None)
+        if shared:
+            v_base = torch.empty(N, 1, 3, device=dev)
+            v_rest_s = torch.empty(N, K - 1, 3, device=dev)
+            _lib.call("gsplat_hip_sh_colors_bwd_sum", ctx.sh_degree, C, N, _ptr(means),
+                      _ptr(viewmats), _ptr(base), _ptr(rest), _ptr(radii), _ptr(v_colors),
+                      _ptr(v_base), _ptr(v_rest_s), _ptr(v_dirs), _stream())
+            v_means = v_dirs
+            if v_means is not None and fusion is not None:
+                v_means = fusion.take_means_grad(v_means)
+            return (None, v_means, None, v_base.view(ctx.coeff_shape),
+                    v_rest_s.view(ctx.rest_shape), None, None)
+        if rest is None:
+            v_coeffs = torch.empty(C, N, K, 3, device=dev)
+            v_rest = None
+        else:
+            v_coeffs = torch.empty(C, N, 1, 3, device=dev)
+            v_rest = torch.empty(C, N, K - 1, 3, device=dev)
         _lib.call("gsplat_hip_sh_colors_bwd", ctx.sh_degree, C, N, ctx.n_rows, K, _ptr(means),
                   _ptr(viewmats), _ptr(base), _ptr(rest), _ptr(radii), _ptr(v_colors),
                   _ptr(v_coeffs), _ptr(v_rest), _ptr(v_dirs), _stream())

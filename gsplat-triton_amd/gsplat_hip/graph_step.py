@@ -36,6 +36,7 @@ Scope: the fused one-rank 3DGS trainer without a densification schedule
 
 import collections
 import ctypes
+import gc
 import math
 
 import numpy as np
@@ -57,7 +58,11 @@ def graphable(tr) -> bool:
 
 class _Mapped:
     """Host-mapped, coherent memory (gsplat_hip_host_mapped_alloc): `np` for
-    the host, `dev` (a pointer) for kernels."""
+    the host, `dev` (a pointer) for kernels.  Never freed: a captured graph
+    keeps the device pointer in its kernel arguments and may still be
+    replaying when its GraphStep becomes garbage, and freeing pinned memory
+    from a garbage-collector pass aborted a test process; the rings are
+    4.3 KB per GraphStep."""
 
     def __init__(self, nbytes):
         h, d = ctypes.c_void_p(), ctypes.c_void_p()
@@ -65,14 +70,6 @@ class _Mapped:
                   ctypes.addressof(d))
         self.host, self.dev = h.value, d.value
         self.np = np.ctypeslib.as_array((ctypes.c_uint8 * int(nbytes)).from_address(self.host))
-
-    def __del__(self):
-        host, self.host = getattr(self, "host", None), None
-        if host and _lib is not None:
-            try:
-                _lib.call("gsplat_hip_host_mapped_free", host)
-            except Exception:  # interpreter shutdown
-                pass
 
 
 class GraphStep:
@@ -188,8 +185,18 @@ class GraphStep:
             torch.cuda.current_stream(self.dev).wait_stream(s)
             self.graph = None
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                self.loss, self.counts = self._body(deg)
+            # no garbage collection while capturing: a collected object that
+            # owns a HIP resource (an earlier trainer's graph or event) would
+            # free it with a call that is illegal during a capture -- a test
+            # process aborted there.  torch.cuda.graph collects right before.
+            gc_on = gc.isenabled()
+            gc.disable()
+            try:
+                with torch.cuda.graph(g):
+                    self.loss, self.counts = self._body(deg)
+            finally:
+                if gc_on:
+                    gc.enable()
             self.graph = g
             self.status.zero_()
             self.seq.fill_(self.issued)  # the next replay fetches slot issued % RING

@@ -230,8 +230,10 @@ class Trainer:
         # one rank, fused path: the SH coefficients' Adam step runs inside the
         # SH-colour backward (gsplat_hip_sh_colors_bwd_adam), so their
         # gradients never go through HBM; GSPLAT_HIP_SH_ADAM_IN_BWD=0 turns it off
+        # (Gaussian-sharded too: the SH backward sums its shard's gradient over
+        # every rank's camera in the kernel before the update)
         self.sh_adam_in_bwd = (fused and not self.sharded and not self.defer_sh
-                               and world_size == 1 and not self.gshard
+                               and (world_size == 1 or self.gshard)
                                and os.environ.get("GSPLAT_HIP_SH_ADAM_IN_BWD", "1") != "0")
         # the exp / sigmoid VJPs and the means-gradient sum formed inside the
         # geometry groups' Adam (gsplat_hip_adam_step_ex): at one rank, and

@@ -414,14 +414,17 @@ int gsplat_hip_densify_apply(int64_t N, const void *workspace, const int64_t *to
                              const int32_t *kinds, const float *means, const float *quats,
                              const float *log_scales, const float *logits, void *stream);
 
-/* gsplat_hip_sh_colors_bwd for C == 1 with the coefficients' Adam step fused
- * in (ABI 18): coeffs [N,1,3] and coeffs_rest [N,15,3] are updated in place
+/* gsplat_hip_sh_colors_bwd with the coefficients' Adam step fused in (ABI 18;
+ * C cameras sharing the coefficient rows since ABI 23: the gradient is the
+ * sum over the C rows c*N + g of radii / v_colors, formed in registers
+ * first): coeffs [N,1,3] and coeffs_rest [N,15,3] are updated in place
  * by torch.optim.Adam (lr0 / lr_rest, shared betas and eps, 1-based step,
  * moments m0/v0 and m_rest/v_rest in the coefficients' layout) from the
- * gradient this backward computes, which is never written; v_dirs [N,3] as
- * in gsplat_hip_sh_colors_bwd.  degree 0..3 (zero gradient above it).  The
- * trainer's optimizer-in-backward for the SH groups (81 % of Adam's bytes). */
-int gsplat_hip_sh_colors_bwd_adam(int degree, int64_t N, const float *means,
+ * gradient this backward computes, which is never written; v_dirs [N,3] =
+ * the means gradient summed over the cameras.  degree 0..3 (zero gradient
+ * above it).  The trainer's optimizer-in-backward for the SH groups (81 % of
+ * Adam's bytes). */
+int gsplat_hip_sh_colors_bwd_adam(int degree, int C, int64_t N, const float *means,
                                   const float *viewmats, float *coeffs, float *coeffs_rest,
                                   const int32_t *radii, const float *v_colors, float *v_dirs,
                                   float *m0, float *v0, float *m_rest, float *v_rest, float lr0,
@@ -432,12 +435,23 @@ int gsplat_hip_sh_colors_bwd_adam(int degree, int64_t N, const float *means,
  * (1 - beta1^t), lr_rest / (1 - beta1^t), 1 / sqrt(1 - beta2^t)}, computed
  * on the host as above; skip_device (may be NULL) != 0 leaves the
  * coefficients and moments unchanged (v_dirs is still written). */
-int gsplat_hip_sh_colors_bwd_adam_dev(int degree, int64_t N, const float *means,
+int gsplat_hip_sh_colors_bwd_adam_dev(int degree, int C, int64_t N, const float *means,
                                       const float *viewmats, float *coeffs, float *coeffs_rest,
                                       const int32_t *radii, const float *v_colors, float *v_dirs,
                                       float *m0, float *v0, float *m_rest, float *v_rest,
                                       const float *hyper_device, float beta1, float beta2,
                                       float eps, const int32_t *skip_device, void *stream);
+/* gsplat_hip_sh_colors_bwd for C cameras sharing one set of coefficient rows
+ * in the trainer's layout (coeffs [N,1,3], coeffs_rest [N,15,3], degree
+ * 0..3; ABI 23): v_coeffs [N,1,3], v_coeffs_rest [N,15,3] and v_dirs [N,3]
+ * are the sums over the cameras (gsplat_hip_sh_colors_bwd writes C rows per
+ * Gaussian for the caller to sum).  The colours of a Gaussian-sharded
+ * render (gsplat/rendering.py:298-310: every rank's cameras). */
+int gsplat_hip_sh_colors_bwd_sum(int degree, int C, int64_t N, const float *means,
+                                 const float *viewmats, const float *coeffs,
+                                 const float *coeffs_rest, const int32_t *radii,
+                                 const float *v_colors, float *v_coeffs, float *v_coeffs_rest,
+                                 float *v_dirs, void *stream);
 
 /* One torch.optim.Adam step (amsgrad=False, no weight decay) over up to 8
  * parameter groups in a single launch (replaces the per-group optimizers of

@@ -117,7 +117,7 @@ def _trainer_rank(rank, world, port, out_dir):
         means, rgbs, vm, K, W, H = _trainer_scene()
         tr = Trainer(means, rgbs, vm, K, W, H, device=DEV, world_size=world, rank=rank,
                      gaussian_shard=True)
-        assert tr.gshard and not tr.sharded and not tr.sh_adam_in_bwd
+        assert tr.gshard and not tr.sharded and tr.sh_adam_in_bwd and tr.geom_fuse
         tr.step(0)
         tr.sync()
         torch.save({"params": {k: p.detach().cpu() for k, p in tr.params.items()},
@@ -185,3 +185,80 @@ def test_gshard_trainer_step_matches_whole_scene_step(tmp_path):
             # within rounding of zero may take either sign (a few entries)
             close_most(a, b, 1e-5, 1e-6, f"{k} rank {r}", max_frac=2e-3,
                        out_bound=2.5 * lrs[list(params).index(k)])
+
+
+def _sh_case(C=5, N=3001, seed=3):
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    means = torch.randn(N, 3, device=DEV, generator=g) * 2
+    vm = torch.eye(4, device=DEV).repeat(C, 1, 1)
+    vm[:, 2, 3] = 6.0 + torch.arange(C, device=DEV)
+    vm[:, 0, 3] = torch.linspace(-1, 1, C, device=DEV)
+    radii = (torch.rand(C, N, device=DEV, generator=g) > 0.5).int() * 2
+    sh0 = torch.randn(N, 1, 3, device=DEV, generator=g) * 0.3
+    shN = torch.randn(N, 15, 3, device=DEV, generator=g) * 0.1
+    vcol = torch.rand(C, N, 3, device=DEV, generator=g) - 0.5
+    return means, vm, radii, sh0, shN, vcol
+
+
+def test_sh_backward_summed_over_cameras():
+    """gsplat_hip_sh_colors_bwd_sum (C cameras sharing the coefficient rows,
+    summed in registers) against the per-camera rows of gsplat_hip_sh_colors_bwd
+    summed by torch."""
+    from gsplat_hip import _lib
+    from gsplat_hip._wrapper import _ptr, _stream
+    for C in (1, 2, 5):
+        means, vm, radii, sh0, shN, vcol = _sh_case(C)
+        N = means.shape[0]
+        per0 = torch.empty(C, N, 1, 3, device=DEV)
+        perr = torch.empty(C, N, 15, 3, device=DEV)
+        perd = torch.empty(C, N, 3, device=DEV)
+        _lib.call("gsplat_hip_sh_colors_bwd", 3, C, N, N, 16, _ptr(means), _ptr(vm), _ptr(sh0),
+                  _ptr(shN), _ptr(radii), _ptr(vcol), _ptr(per0), _ptr(perr), _ptr(perd),
+                  _stream())
+        s0 = torch.empty(N, 1, 3, device=DEV)
+        sr = torch.empty(N, 15, 3, device=DEV)
+        sd = torch.empty(N, 3, device=DEV)
+        _lib.call("gsplat_hip_sh_colors_bwd_sum", 3, C, N, _ptr(means), _ptr(vm), _ptr(sh0),
+                  _ptr(shN), _ptr(radii), _ptr(vcol), _ptr(s0), _ptr(sr), _ptr(sd), _stream())
+        torch.cuda.synchronize()
+        for a, b in ((s0, per0.sum(0)), (sr, perr.sum(0)), (sd, perd.sum(0))):
+            if C == 1:
+                assert torch.equal(a, b)
+            else:
+                torch.testing.assert_close(a, b, rtol=1e-6, atol=1e-7)
+
+
+def test_sh_adam_in_backward_over_cameras_is_exact():
+    """The fused SH Adam with C cameras == the summed gradient + FusedAdam,
+    bit for bit (the same in-register sum, the shared element update)."""
+    from gsplat_hip import _lib
+    from gsplat_hip._wrapper import _ptr, _stream
+    from gsplat_hip.losses import adam_groups
+    C = 4
+    means, vm, radii, sh0, shN, vcol = _sh_case(C, N=2048)
+    N = means.shape[0]
+    out = []
+    for fused in (False, True):
+        p0, pr = sh0.clone(), shN.clone()
+        m0, v0 = torch.zeros_like(p0), torch.zeros_like(p0)
+        mr, vr = torch.zeros_like(pr), torch.zeros_like(pr)
+        vd = torch.empty(N, 3, device=DEV)
+        for step in (1, 2, 3):
+            if fused:
+                _lib.call("gsplat_hip_sh_colors_bwd_adam", 3, C, N, _ptr(means), _ptr(vm),
+                          _ptr(p0), _ptr(pr), _ptr(radii), _ptr(vcol), _ptr(vd), _ptr(m0),
+                          _ptr(v0), _ptr(mr), _ptr(vr), 2.5e-3, 1.25e-4, 0.9, 0.999, 1e-15,
+                          step, _stream())
+            else:
+                g0 = torch.empty_like(p0)
+                gr = torch.empty_like(pr)
+                _lib.call("gsplat_hip_sh_colors_bwd_sum", 3, C, N, _ptr(means), _ptr(vm),
+                          _ptr(p0), _ptr(pr), _ptr(radii), _ptr(vcol), _ptr(g0), _ptr(gr),
+                          _ptr(vd), _stream())
+                adam_groups([p0.view(-1), pr.view(-1)], [g0.view(-1), gr.view(-1)],
+                            [m0.view(-1), mr.view(-1)], [v0.view(-1), vr.view(-1)],
+                            [2.5e-3, 1.25e-4], (0.9, 0.999), 1e-15, step)
+        torch.cuda.synchronize()
+        out.append((p0, pr, m0, v0, mr, vr, vd))
+    for a, b in zip(*out):
+        assert torch.equal(a, b)
