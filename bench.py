@@ -148,14 +148,15 @@ def pmc_traffic(config: str):
 
 
 def _valu_frac(pmc, launch_ms):
-    """VALU issue: wave64 VALU instructions x 4 cycles (a wave64 v_fma_f32
-    issues every 4 cycles per SIMD, tools/valu_bench.hip) against 1024 SIMDs
-    x 2.4 GHz over the launch."""
+    """VALU issue: wave64 VALU instructions x 2 cycles (a wave64 v_fma_f32
+    / v_mul_f32 issues every 2.3-2.4 cycles per SIMD at the nominal 2.4 GHz,
+    tools/valu_bench.hip -> profiles/r3_valu/valu_bench.txt) against 1024
+    SIMDs x 2.4 GHz over the launch."""
     ctr = (pmc or {}).get("counters", {})
     insts = ctr.get("SQ_INSTS_VALU")
     if not insts or not launch_ms == launch_ms:
         return None
-    peak = 1024 * 2.4e9 / 4.0  # wave64 VALU instructions per second, whole chip
+    peak = 1024 * 2.4e9 / 2.0  # wave64 VALU instructions per second, whole chip
     achieved = insts / (launch_ms * 1e-3)
     res = {"bound": "valu", "insts_per_launch": insts, "achieved": achieved, "peak": peak,
            "unit": "wave-instr/s", "frac": achieved / peak}

@@ -68,9 +68,9 @@ def test_capped_isect_matches_synchronous():
     assert torch.equal(m1["isect_offsets"], m0["isect_offsets"])
     # the same per-tile lists through the same deterministic forward
     assert torch.equal(rc1, rc0) and torch.equal(ra1, ra0)
-    for a, b in zip(g1, g0):
+    for a, b in zip(g1, g0):  # the backward's float atomics: summation order only
         scale = float(b.abs().max())
-        assert float((a - b).abs().max()) <= 1e-5 * scale + 1e-9
+        assert float((a - b).abs().max()) <= 5e-5 * scale + 1e-9
     # exactly full is not an overflow
     _, _, m2, _ = _render(ins, W, H, _isect_capacity=n, _isect_status=status)
     assert m2["isect_counts"].tolist()[2] == 0 and int(status) == 0
