@@ -432,7 +432,7 @@ GS_INLINE void stage_bwd_pad(float4 *st, int slot) {
 // batch b composites (two register buffers).  Depth 0 (only the flatten ids
 // ahead, two more waves) measured 0.198 / 0.686 ms at M2 / M3 against 0.184 /
 // 0.590, depth 2 (three buffers) no better than 1.
-template <int D>
+template <int D, int BLEND = 0>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) fwd_kernel(Args a) {
   using P = FwdPair<D>;
   constexpr int N4 = P::N4;
@@ -492,8 +492,23 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) f
     bool done = false;
     // one record of a pair: sequential in T
     auto blend = [&](float s2, float smax, float al, float idx) -> float {
-      const float nT = __builtin_fmaf(-T, al, T);  // T (1 - alpha)
       const bool hit = __float_as_uint(s2) <= __float_as_uint(smax);  // 0 <= s2 <= smax
+      if (BLEND == 1) {
+        // every select takes its compare's mask directly (no SALU mask
+        // arithmetic between the compare and the select): a miss blends
+        // alpha 0; a live pixel keeps T > 1e-4 through a miss, a dead one
+        // (T < 0) stays below it, so `gt` alone decides
+        const float a = hit ? al : 0.f;
+        const float nT = __builtin_fmaf(-T, a, T);
+        const bool gt = nT > kTMin;
+        const float Tsel = gt ? nT : T;
+        const float vis = T - Tsel;  // alpha * T when blended, else 0
+        const int32_t li = hit ? __float_as_int(idx) : last;
+        last = gt ? li : last;
+        T = gt ? nT : -fabsf(T);
+        return vis;
+      }
+      const float nT = __builtin_fmaf(-T, al, T);  // T (1 - alpha)
       const bool gt = nT > kTMin;
       const bool ok = hit & gt;
       // plain selects (no control flow): blended -> nT; hit but T would drop
@@ -1673,6 +1688,16 @@ static bool bwd_pf() {
 // work per wave doubles) -- unlike the 2DGS forward, where two pixels per
 // lane won 32 % -- and was removed.
 
+// Forward blend form (GSPLAT_HIP_FWD_BLEND, A/B): 0 = masks combined on the
+// SALU, 1 = every select on its own compare's mask.
+static int fwd_blend() {
+  static const int v = [] {
+    const char *e = getenv("GSPLAT_HIP_FWD_BLEND");
+    return (e && atoi(e) == 1) ? 1 : 0;
+  }();
+  return v;
+}
+
 static int dbg_flags() {
   static const int v = [] { const char *e = getenv("GSPLAT_HIP_DBG"); return e ? atoi(e) : 0; }();
   return v;
@@ -1716,13 +1741,21 @@ int r16_fwd(r16::Args a, const void *state, char *split_base, hipStream_t st) {
         std::min<int64_t>(a.n_tiles, a.n_isects / split_threshold(a.n_isects) + 1);
     hipLaunchKernelGGL((r16::fwd_prod_kernel<D>), dim3((unsigned)std::min<int64_t>(nc, 2048)),
                        dim3(256), 0, st, a);
-    hipLaunchKernelGGL((r16::fwd_kernel<D>), dim3((unsigned)(a.n_tiles + nc)), dim3(256), 0, st, a);
+    if (fwd_blend() == 1)
+      hipLaunchKernelGGL((r16::fwd_kernel<D, 1>), dim3((unsigned)(a.n_tiles + nc)), dim3(256), 0,
+                         st, a);
+    else
+      hipLaunchKernelGGL((r16::fwd_kernel<D>), dim3((unsigned)(a.n_tiles + nc)), dim3(256), 0, st,
+                         a);
     hipLaunchKernelGGL((r16::fwd_combine_kernel<D>), dim3((unsigned)n_heavy_max), dim3(256), 0, st,
                        a);
     GS_CHECK_LAUNCH("rasterize_fwd16_split");
     return 0;
   }
-  hipLaunchKernelGGL((r16::fwd_kernel<D>), dim3(a.n_tiles), dim3(256), 0, st, a);
+  if (fwd_blend() == 1)
+    hipLaunchKernelGGL((r16::fwd_kernel<D, 1>), dim3(a.n_tiles), dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL((r16::fwd_kernel<D>), dim3(a.n_tiles), dim3(256), 0, st, a);
   GS_CHECK_LAUNCH("rasterize_fwd16");
   return 0;
 }

@@ -5,11 +5,11 @@ MI355X (torch.distributed "nccl" = RCCL, xGMI).
 Same helper surface as gsplat/distributed.py:10-257:
     all_gather_int32, all_to_all_int32, all_gather_tensor_list,
     all_to_all_tensor_list (differentiable).
-The many-to-many exchange is written as explicit per-peer P2P transfers
-(`batch_isend_irecv`): on a fully connected xGMI node every peer pair has its
-own link, so the exchange is one transfer per link; the same code runs over
-gloo on the CPU for the tests.  The backward of an exchange is the exchange
-with input and output splits swapped.
+The many-to-many exchange of rows is one RCCL `all_to_all_single` over
+contiguous buffers (on a fully connected xGMI node every peer pair has its
+own link); on other backends (gloo: the CPU tests, and several ranks sharing
+one GPU) explicit per-peer P2P transfers (`batch_isend_irecv`).  The backward
+of an exchange is the exchange with input and output splits swapped.
 """
 
 import math
@@ -99,22 +99,32 @@ def all_gather_tensor_list(world_size: int, tensor_list: List[Tensor]) -> List[T
             zip(torch.split(collected, sizes, dim=-1), tensor_list)]
 
 
+def _all_to_all_rows(data: Tensor, splits: List[int], out_splits: List[int]) -> Tensor:
+    """Rows data[sum(splits[:j]) : ...] to rank j; rank j's rows for me, in
+    rank order.  RCCL: one all_to_all_single over contiguous buffers (the
+    collective xGMI is built for, no per-peer concat); other backends: the
+    per-peer P2P exchange."""
+    data = data.contiguous()
+    if data.is_cuda and dist.get_backend() == "nccl":
+        out = data.new_empty((sum(out_splits),) + data.shape[1:])
+        dist.all_to_all_single(out, data, output_split_sizes=out_splits,
+                               input_split_sizes=splits)
+        return out
+    send = list(data.split(splits, dim=0))
+    recv = [data.new_empty((n,) + data.shape[1:]) for n in out_splits]
+    _exchange(send, recv)
+    return torch.cat(recv, dim=0)
+
+
 class _AllToAll(torch.autograd.Function):
     @staticmethod
     def forward(ctx, data, splits, out_splits):
         ctx.splits, ctx.out_splits = splits, out_splits
-        send = list(data.split(splits, dim=0))
-        recv = [data.new_empty((n,) + data.shape[1:]) for n in out_splits]
-        _exchange(send, recv)
-        return torch.cat(recv, dim=0)
+        return _all_to_all_rows(data, splits, out_splits)
 
     @staticmethod
     def backward(ctx, grad):
-        grad = grad.contiguous()
-        send = list(grad.split(ctx.out_splits, dim=0))
-        recv = [grad.new_empty((n,) + grad.shape[1:]) for n in ctx.splits]
-        _exchange(send, recv)
-        return torch.cat(recv, dim=0), None, None
+        return _all_to_all_rows(grad, ctx.out_splits, ctx.splits), None, None
 
 
 def all_to_all_tensor_list(world_size: int, tensor_list: List[Tensor],

@@ -48,6 +48,22 @@ def test_distributed_single_rank_matches(packed):
         torch.testing.assert_close(a, b, rtol=1e-3, atol=1e-4 * float(b.abs().max()))
 
 
+def test_rccl_row_exchange_and_its_backward():
+    """The projected-pair exchange on RCCL (all_to_all_single, the path of
+    every N > 1 Gaussian-sharded render) and its autograd backward, on one
+    rank: rows come back in place, gradients pass through unchanged."""
+    from gsplat_hip.distributed import _AllToAll, _all_to_all_rows
+    g = torch.Generator(device=DEV).manual_seed(2)
+    data = torch.randn(777, 11, device=DEV, generator=g)
+    out = _all_to_all_rows(data, [777], [777])
+    assert torch.equal(out, data)
+    x = data.clone().requires_grad_(True)
+    y = _AllToAll.apply(x, [777], [777])
+    w = torch.randn_like(y)
+    (y * w).sum().backward()
+    assert torch.equal(y.detach(), data) and torch.equal(x.grad, w)
+
+
 def test_sharded_adam_single_rank_rccl_matches_fused_adam():
     """ShardedAdam's RCCL path (reduce-scatter, HIP Adam on the shard and the
     remainder rows, all-gather) on one rank equals FusedAdam."""
