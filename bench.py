@@ -296,7 +296,8 @@ def main():
         # rasterizer launches over eager steps right after the timed region
         g = tr._graph
         graph_info = {"replays": g.replays, "captures": g.recaptures,
-                      "isect_capacity": g.capacity, "max_isects": g.max_isects}
+                      "isect_capacity": g.capacity, "max_isects": g.max_isects,
+                      "host_issue_ms_per_step": 1e3 * g.host_s / max(g.replays, 1)}
         tr._graph = None
         timers = _wrapper.enable_kernel_timers(True)
         n_t = min(args.steps, 10)
@@ -362,6 +363,20 @@ def main():
         isects.append(n)
         n_effs.append(n_eff)
         del colors, alphas, meta, node, last
+    # fraction of the Gaussians visible from at least one of the pool's first
+    # 8 cameras -- what a replicated 8-GPU step would have to reduce
+    # (DESIGN §6); projection only, outside the timed region
+    union_visible = per_cam_visible = None
+    if model == "3dgs":
+        from gsplat_hip import fully_fused_projection
+        p = tr.params
+        nc = min(8, len(vm_pool))
+        with torch.no_grad():
+            radii = fully_fused_projection(
+                p["means"], None, p["quats"], torch.exp(p["scales"]), tr.viewmats[:nc],
+                tr.Ks[:nc], W, H, packed=False, near_plane=0.01, far_plane=1e10)[0]
+        union_visible = float((radii > 0).any(0).float().mean())
+        per_cam_visible = float((radii > 0).float().mean())
     bytes_per_launch = float(np.mean(byts))
     bytes_bwd = float(np.mean(byts_bwd))
     achieved = bytes_per_launch / (fwd_ms * 1e-3) / 1e9
@@ -399,6 +414,8 @@ def main():
                        " (the N>1 code path on a 1-rank RCCL group: sharded Adam, "
                        "early SH reduce-scatter)" if dp_path and world == 1 else ""),
                    "n_isects_mean": float(np.mean(isects)), "n_eff_mean": float(np.mean(n_effs)),
+                   "visible_per_camera": per_cam_visible,
+                   "visible_union_8_cameras": union_visible,
                    "packed": False, "loss": "0.8*L1+0.2*(1-SSIM valid)",
                    "step_issue": ("HIP graph replay of the captured step (sync-free isect, "
                                   f"{graph_info})" if graphed else "eager launches"),

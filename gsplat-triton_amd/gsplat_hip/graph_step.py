@@ -38,6 +38,7 @@ import collections
 import ctypes
 import gc
 import math
+import time
 
 import numpy as np
 import torch
@@ -115,6 +116,7 @@ class GraphStep:
         self.recaptures = 0
         self.replays = 0
         self.max_isects = 0
+        self.host_s = 0.0
 
     # ------------------------------------------------------------------ body
     def _layout(self):
@@ -257,6 +259,7 @@ class GraphStep:
         ev = self._slot_ev[slot]
         if ev is not None:
             ev.synchronize()  # the step that used this slot RING steps ago is done
+        t0 = time.perf_counter()
         self._fill(it, slot)
         self.graph.replay()
         self.tr.opt.step_count += 1
@@ -266,6 +269,7 @@ class GraphStep:
         self.pending.append((it, slot, ev))
         self.issued += 1
         self.replays += 1
+        self.host_s += time.perf_counter() - t0  # host work of the step, waits excluded
 
     def _check(self, block=False):
         """Read the counts of finished steps; on an overflow, redo from there."""
