@@ -51,10 +51,35 @@ update_state_kernel(int C, int64_t N, const float *__restrict__ g2d,
   }
 }
 
+// The captured training step's input block (gsplat_hip_step_fetch): slot
+// seq % ring of a host-mapped ring into the device block, its slot index
+// into the block's last 8 bytes, seq += 1 -- by one wave.
+struct StepFetch {
+  const uint32_t *ring;  // null: nothing to fetch
+  int64_t slot_words;
+  int n_ring;
+  int64_t *seq;
+  uint32_t *blk;
+};
+
+GS_INLINE void step_fetch_wave(const StepFetch &f, int lane) {
+  const int64_t q = *f.seq;
+  const int64_t slot = q % f.n_ring;
+  const uint32_t *src = f.ring + slot * f.slot_words;
+  for (int64_t w = lane; w < f.slot_words - 2; w += 64) f.blk[w] = src[w];
+  if (lane == 0) {
+    reinterpret_cast<int64_t *>(f.blk)[f.slot_words / 2 - 1] = slot;
+    *f.seq = q + 1;
+  }
+}
+
+// fetch (the first kernel of a captured step): its first wave also fetches
+// the step's input block
 __global__ void __launch_bounds__(256)
 activate_fwd_kernel(int64_t n_s, int64_t n_o, const float *__restrict__ log_scales,
                     const float *__restrict__ logits, float *__restrict__ scales,
-                    float *__restrict__ opacities) {
+                    float *__restrict__ opacities, StepFetch fetch) {
+  if (fetch.ring && blockIdx.x == 0 && threadIdx.x < 64) step_fetch_wave(fetch, threadIdx.x);
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i < n_s) scales[i] = expf(log_scales[i]);
   if (i < n_o) opacities[i] = 1.f / (1.f + expf(-logits[i]));
@@ -288,21 +313,10 @@ densify_apply_kernel(int64_t N, const uint8_t *__restrict__ flags,
   }
 }
 
-// The captured training step's input block (gsplat_hip_step_fetch): slot
-// seq % ring of a host-mapped ring into the device block, its slot index into
-// the block's last 8 bytes, seq += 1.  One wave; every later kernel of the
+// gsplat_hip_step_fetch on its own: one wave; every later kernel of the
 // step reads the block after this one (stream order).
-__global__ void __launch_bounds__(64)
-step_fetch_kernel(const uint32_t *__restrict__ ring, int64_t slot_words, int n_ring,
-                  int64_t *__restrict__ seq, uint32_t *__restrict__ blk) {
-  const int64_t q = *seq;
-  const int64_t slot = q % n_ring;
-  const uint32_t *src = ring + slot * slot_words;
-  for (int64_t w = threadIdx.x; w < slot_words - 2; w += 64) blk[w] = src[w];
-  if (threadIdx.x == 0) {
-    reinterpret_cast<int64_t *>(blk)[slot_words / 2 - 1] = slot;
-    *seq = q + 1;
-  }
+__global__ void __launch_bounds__(64) step_fetch_kernel(StepFetch f) {
+  step_fetch_wave(f, threadIdx.x);
 }
 
 }  // namespace strat
@@ -340,9 +354,9 @@ extern "C" int gsplat_hip_step_fetch(const void *ring_device, int64_t slot_bytes
   GS_REQUIRE(slot_bytes >= 16 && slot_bytes % 8 == 0 && slot_bytes <= 65536,
              "step_fetch: slot_bytes %lld not a multiple of 8 in [16, 65536]",
              (long long)slot_bytes);
-  hipLaunchKernelGGL(strat::step_fetch_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream,
-                     reinterpret_cast<const uint32_t *>(ring_device), slot_bytes / 4, n_ring,
-                     seq_device, reinterpret_cast<uint32_t *>(block_device));
+  const strat::StepFetch f{reinterpret_cast<const uint32_t *>(ring_device), slot_bytes / 4, n_ring,
+                           seq_device, reinterpret_cast<uint32_t *>(block_device)};
+  hipLaunchKernelGGL(strat::step_fetch_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, f);
   GS_CHECK_LAUNCH("step_fetch");
   return 0;
 }
@@ -367,8 +381,29 @@ extern "C" int gsplat_hip_activate_fwd(int64_t n_scales, int64_t n_opacities,
   if (n <= 0) return 0;
   hipLaunchKernelGGL(strat::activate_fwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
                      (hipStream_t)stream, n_scales, n_opacities, log_scales, logits, scales,
-                     opacities);
+                     opacities, strat::StepFetch{});
   GS_CHECK_LAUNCH("activate_fwd");
+  return 0;
+}
+
+extern "C" int gsplat_hip_activate_fwd_fetch(int64_t n_scales, int64_t n_opacities,
+                                             const float *log_scales, const float *logits,
+                                             float *scales, float *opacities,
+                                             const void *ring_device, int64_t slot_bytes,
+                                             int n_ring, int64_t *seq_device,
+                                             void *block_device, void *stream) {
+  GS_REQUIRE(ring_device && seq_device && block_device && n_ring > 0,
+             "activate_fwd_fetch: null buffer or empty ring");
+  GS_REQUIRE(slot_bytes >= 16 && slot_bytes % 8 == 0 && slot_bytes <= 65536,
+             "activate_fwd_fetch: slot_bytes %lld not a multiple of 8 in [16, 65536]",
+             (long long)slot_bytes);
+  const strat::StepFetch f{reinterpret_cast<const uint32_t *>(ring_device), slot_bytes / 4, n_ring,
+                           seq_device, reinterpret_cast<uint32_t *>(block_device)};
+  const int64_t n = n_scales > n_opacities ? n_scales : n_opacities;
+  hipLaunchKernelGGL(strat::activate_fwd_kernel, dim3((unsigned)std::max<int64_t>((n + 255) / 256, 1)),
+                     dim3(256), 0, (hipStream_t)stream, n_scales, n_opacities, log_scales, logits,
+                     scales, opacities, f);
+  GS_CHECK_LAUNCH("activate_fwd_fetch");
   return 0;
 }
 

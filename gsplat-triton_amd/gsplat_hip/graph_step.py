@@ -19,8 +19,9 @@ What makes the step capturable:
   viewmat and K, and its index (the loss reads that camera's target image
   in place, l1_ssim_loss(gt_index=...)) -- are one 512-B block.  The host
   writes it into a slot of a host-mapped ring; the graph's first kernel
-  (gsplat_hip_step_fetch) copies slot seq % RING into device memory and
-  counts seq up, so a step needs no copy-engine transfer (each one cost a
+  (the activations, gsplat_hip_activate_fwd_fetch) copies slot seq % RING
+  into device memory and counts seq up, so a step needs no copy-engine
+  transfer (each one cost a
   cross-queue hand-off of ~15 us before and after it);
 * overflow: if a step's isects do not fit, the capped emission writes none,
   sets a sticky device flag, and every state update of that and the later
@@ -141,9 +142,9 @@ class GraphStep:
                 hyper=self.scal[sh_off:sh_off + 3], skip=self.status)
         fusion = _wrapper.StepFusion(sh_adam=fa, geom=tr.geom_fuse) \
             if (fa is not None or tr.geom_fuse) else None
-        _lib.call("gsplat_hip_step_fetch", self.ring_in.dev, self.SLOT, self.RING,
-                  _wrapper._ptr(self.seq), _wrapper._ptr(self.blk), _wrapper._stream())
-        scales, opac = activate(p["scales"], p["opacities"], fusion)
+        # the first launch also fetches this step's input block (the ring slot)
+        scales, opac = activate(p["scales"], p["opacities"], fusion,
+                                fetch=(self.ring_in.dev, self.SLOT, self.RING, self.seq, self.blk))
         colors, _, meta = rasterization(
             p["means"], p["quats"], scales, opac, (p["sh0"], p["shN"]), self.vm, self.K, tr.width,
             tr.height, sh_degree=deg, packed=False, near_plane=0.01, far_plane=1e10,

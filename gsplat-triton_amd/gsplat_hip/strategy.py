@@ -22,13 +22,19 @@ def _dev(*ts):
 
 class _Activate(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, log_scales, logits, fusion=None):
+    def forward(ctx, log_scales, logits, fusion=None, fetch=None):
         log_scales, logits = _f32c(log_scales), _f32c(logits)
         _dev(log_scales, logits)
         scales = torch.empty_like(log_scales)
         opac = torch.empty_like(logits)
-        _lib.call("gsplat_hip_activate_fwd", log_scales.numel(), logits.numel(),
-                  _ptr(log_scales), _ptr(logits), _ptr(scales), _ptr(opac), _stream())
+        if fetch is not None:  # the captured step's input block, same launch
+            ring, slot_bytes, n_ring, seq, blk = fetch
+            _lib.call("gsplat_hip_activate_fwd_fetch", log_scales.numel(), logits.numel(),
+                      _ptr(log_scales), _ptr(logits), _ptr(scales), _ptr(opac), ring,
+                      int(slot_bytes), int(n_ring), _ptr(seq), _ptr(blk), _stream())
+        else:
+            _lib.call("gsplat_hip_activate_fwd", log_scales.numel(), logits.numel(),
+                      _ptr(log_scales), _ptr(logits), _ptr(scales), _ptr(opac), _stream())
         ctx.save_for_backward(scales, opac)
         ctx.fusion = fusion
         return scales, opac
@@ -41,7 +47,7 @@ class _Activate(torch.autograd.Function):
         if ctx.fusion is not None and ctx.fusion.take_activation_grads(
                 None if v_scales is None else _f32c(v_scales),
                 None if v_opac is None else _f32c(v_opac), scales, opac):
-            return None, None, None
+            return None, None, None, None
         v_scales = torch.zeros_like(scales) if v_scales is None else _f32c(v_scales)
         v_opac = torch.zeros_like(opac) if v_opac is None else _f32c(v_opac)
         v_log = torch.empty_like(scales)
@@ -49,14 +55,16 @@ class _Activate(torch.autograd.Function):
         _lib.call("gsplat_hip_activate_bwd", scales.numel(), opac.numel(), _ptr(scales),
                   _ptr(opac), _ptr(v_scales), _ptr(v_opac), _ptr(v_log), _ptr(v_logit),
                   _stream())
-        return v_log, v_logit, None
+        return v_log, v_logit, None, None
 
 
-def activate(log_scales, logits, fusion=None):
+def activate(log_scales, logits, fusion=None, fetch=None):
     """(exp(log_scales), sigmoid(logits)), differentiable.  `fusion`: a
     training step's _wrapper.StepFusion whose geometry update takes the
-    incoming gradients instead (the VJPs are then formed inside Adam)."""
-    return _Activate.apply(log_scales, logits, fusion)
+    incoming gradients instead (the VJPs are then formed inside Adam).
+    `fetch` = (ring device pointer, slot bytes, slots, seq, block): the same
+    launch also performs gsplat_hip_step_fetch (graph_step.GraphStep)."""
+    return _Activate.apply(log_scales, logits, fusion, fetch)
 
 
 @torch.no_grad()

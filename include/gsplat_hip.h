@@ -352,6 +352,14 @@ int gsplat_hip_host_mapped_alloc(int64_t bytes, void **host_ptr, void **device_p
 int gsplat_hip_host_mapped_free(void *host_ptr);
 int gsplat_hip_step_fetch(const void *ring_device, int64_t slot_bytes, int n_ring,
                           int64_t *seq_device, void *block_device, void *stream);
+/* gsplat_hip_activate_fwd whose launch also performs gsplat_hip_step_fetch
+ * (its first wave; ABI 24): the first kernel of a captured step, one launch
+ * instead of two. */
+int gsplat_hip_activate_fwd_fetch(int64_t n_scales, int64_t n_opacities,
+                                  const float *log_scales, const float *logits, float *scales,
+                                  float *opacities, const void *ring_device, int64_t slot_bytes,
+                                  int n_ring, int64_t *seq_device, void *block_device,
+                                  void *stream);
 
 /* DefaultStrategy._update_state for packed=False (gsplat/strategy/default.py:
  * 213-262): for every (c, g) with radii[c,g] > 0, in camera order,
