@@ -570,16 +570,21 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) f
     // before isect b, S[D][256] = the colour the chunk starting at b adds.
     // Chunk-local sums keep the backward's suffix sums (sum of S over the
     // later chunks) as accurate as its own back-to-front accumulation; a
-    // difference of running totals would cancel catastrophically.
+    // difference of running totals would cancel catastrophically.  A pixel's
+    // slot b is written only while it is alive at b: the backward reads slot
+    // b of a pixel only when b <= its last id (bwd2_kernel), and a pixel that
+    // blends record last_id was alive at every boundary up to it.  Boundaries
+    // past the strip's end (all pixels finished) are not written at all.
     const int64_t L = a.L;
     auto slot = [&](int64_t bidx) { return a.state + (bidx / L) * (int64_t)(kTS * kTS * (1 + D)); };
     int64_t cur_b = start;  // start of the chunk being accumulated
+    bool live_b = T > 0.f;  // the pixel was alive at cur_b
     auto close_chunk = [&]() {  // fold acc into tot; store S of the chunk at cur_b
       float *sl = slot(cur_b);
 #pragma unroll
       for (int d = 0; d < D; ++d) {
         const float cs = acc[d].x + acc[d].y;
-        if (cur_b > tstart) sl[(1 + d) * kTS * kTS + pix_in_tile] = cs;
+        if (cur_b > tstart && live_b) sl[(1 + d) * kTS * kTS + pix_in_tile] = cs;
         tot[d] += cs;
         acc[d] = f2v{0.f, 0.f};
       }
@@ -587,7 +592,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) f
     auto save_state = [&](int64_t bidx) {  // reached boundary bidx
       close_chunk();
       cur_b = bidx;
-      slot(bidx)[pix_in_tile] = T;
+      live_b = T > 0.f;
+      if (live_b) slot(bidx)[pix_in_tile] = T;
     };
     // a chunk of a split tile writes the state of the boundaries inside it
     // and the colour it adds at its own start boundary
@@ -615,17 +621,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) f
       b0 += 64;
       if (done) break;
     }
-    if (chunked) {
-      close_chunk();
-      // boundaries the loop did not reach (all pixels finished): final T,
-      // nothing added after them
-      for (int64_t bi = cur_b + L; bi < end; bi += L) {
-        float *sl = slot(bi);
-        sl[pix_in_tile] = T;
-#pragma unroll
-        for (int d = 0; d < D; ++d) sl[(1 + d) * kTS * kTS + pix_in_tile] = 0.f;
-      }
-    }
+    if (chunked) close_chunk();
   }
 #pragma unroll
   for (int d = 0; d < D; ++d) tot[d] += acc[d].x + acc[d].y;
@@ -818,15 +814,17 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) b
       bgt = bgv * Tf;
     }
     T = Tf;
-    if (cend < tend) {
-      // a chunk followed by others: start from the forward's state at the
-      // boundary cend (transmittance), and the suffix colour sum of the later
-      // chunks (their chunk-local sums S), dotted with dL/dcolour
+    if (cend < tend && mylast >= cend) {
+      // a chunk followed by others in which the pixel still blends: start
+      // from the forward's state at the boundary cend (transmittance), and
+      // the suffix colour sum of the later chunks up to its last id (their
+      // chunk-local sums S), dotted with dL/dcolour.  (mylast < cend: the
+      // transmittance at cend is the final one, Tf, and nothing follows.)
       const int p = (threadIdx.x >> 6) * 64 + lane;
       const int64_t per = (int64_t)(kTS * kTS * (1 + D));
       T = fabsf(a.state[(cend / a.L) * per + p]);
       float s = 0.f;
-      for (int64_t bi = cend; bi < tend; bi += a.L) {
+      for (int64_t bi = cend; bi <= mylast; bi += a.L) {
         const float *sl = a.state + (bi / a.L) * per;
 #pragma unroll
         for (int d = 0; d < D; ++d) s += sl[(1 + d) * kTS * kTS + p] * Drc[d];
@@ -1040,13 +1038,15 @@ __attribute__((amdgpu_waves_per_eu(BwdOcc<PX>::W))) bwd2_kernel(Args a) {
       }
       TfDra[q] = Tf * Dra;
       T[q] = Tf;
-      if (cend < tend) {
-        // chunk followed by others: the forward's state at the boundary cend
+      if (cend < tend && mylast[q] >= cend) {
+        // chunk followed by others in which the pixel still blends: the
+        // forward's state at the boundary cend, suffix sums up to its last id
+        // (as in bwd_kernel)
         const int p = 64 * PX * w + 64 * q + lane;  // row-major pixel of the tile
         const int64_t per = (int64_t)(kTS * kTS * (1 + D));
         T[q] = fabsf(a.state[(cend / a.L) * per + p]);
         float s = 0.f;
-        for (int64_t bi = cend; bi < tend; bi += a.L) {
+        for (int64_t bi = cend; bi <= mylast[q]; bi += a.L) {
           const float *sl = a.state + (bi / a.L) * per;
 #pragma unroll
           for (int d = 0; d < D; ++d) s += sl[(1 + d) * kTS * kTS + p] * Drc[q][d];
