@@ -136,21 +136,23 @@ struct Args {
   const int2 *items, *items_tail;
   const int32_t *n_items;
   const int32_t *order;  // forward: tile of workgroup b (heaviest tiles first) or null
-  // forward, split heavy tiles (fwd_plan_kernel): fitems[b] = (tile, -1) a
-  // whole tile or (tile, k) chunk k of a split tile; p1items the chunks whose
-  // transmittance product fwd_prod_kernel computes; heavy the split tiles as
-  // (tile, id of its chunk 0); fcount = {#fitems, #p1items, #heavy, index in
-  // fitems of the first chunk}.  prod: per boundary slot (b / L) the product
-  // of (1 - alpha) over the chunk ending at b; cout: per chunk id (its index
-  // in fitems minus fcount[3]), the chunk's end T, last id and colour sum
-  // [2 + D][256] (chunk START slots are not unique: a tile's first chunk can
-  // share b / L with the previous tile's last one).
-  const int2 *fitems, *p1items, *heavy;
-  const int32_t *fcount;
+  const int32_t *n_whole;  // forward: the number of tiles in `order` (device), or null: all
+  // forward, split heavy tiles (fwd_plan_kernel, "Split heavy tiles"):
+  // fitems[b] = (tile, k), chunk k of a split tile, n_chunks of them (device).
+  // prod: per boundary slot (b / L) the product of (1 - alpha) over the chunk
+  // ending at b, pflag[4 * slot + wave] its ready flags; cout: per chunk (its
+  // index in fitems), the chunk's end T, last id and colour sum [2 + D][256];
+  // ctr[index of chunk 0] the tile's finished chunks (chunk START slots are
+  // not unique: a tile's first chunk can share b / L with the previous
+  // tile's last one).
+  const int2 *fitems;
+  const int32_t *n_chunks;
   float *prod, *cout;
+  int32_t *pflag, *ctr;
   int SL;  // split tiles: isects per chunk (a multiple of L)
   const float *render_colors_in;  // backward: forward colours (for suffix sums)
-  int dbg;  // experiments only (GSPLAT_HIP_DBG): bit 0 = backward skips its atomics
+  int dbg;  // debug flags (gsplat_hip_debug_set_flags): bit 0 = backward skips its
+            // atomics, bit 1 = split chunks never wait for a published product
   uint64_t *timeline;  // debug: per-wave (start, end) s_memrealtime stamps or null
   unsigned long long *lanehist;  // debug: histogram of contributing lanes per (record, wave)
 };
@@ -236,8 +238,8 @@ struct Attr {
 
 // Unconditional (the caller clamps the isect index into the tile's range and
 // masks the lanes past it), so the loads stay in flight across the batch.
-template <int D>
-GS_INLINE void load_attr(const Args &a, int32_t g, Attr<D> &at) {
+template <int D, class A>
+GS_INLINE void load_attr(const A &a, int32_t g, Attr<D> &at) {
   at.g = g;
   if constexpr (D <= kRecMaxD) {
     if (a.records) {  // wave-uniform
@@ -319,9 +321,6 @@ GS_INLINE void read_rec(const float4 *slot, float (&r)[Rec<D, FWD>::NF]) {
   }
 }
 
-// The forward's tile of this workgroup: heaviest tiles first when the
-// dispatch order is present (tile_order_kernel).
-GS_INLINE int fwd_tile(const Args &a) { return a.order ? a.order[blockIdx.x] : (int)blockIdx.x; }
 
 // Geometry of one wave: 4 waves share a 16x16 tile, each owning a 16x4
 // strip; lane l owns pixel column (l & 15), row strip_y0 + (l >> 4).
@@ -432,31 +431,118 @@ GS_INLINE void stage_bwd_pad(float4 *st, int slot) {
 // batch b composites (two register buffers).  Depth 0 (only the flatten ids
 // ahead, two more waves) measured 0.198 / 0.686 ms at M2 / M3 against 0.184 /
 // 0.590, depth 2 (three buffers) no better than 1.
-template <int D, int BLEND = 0>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) fwd_kernel(Args a) {
+// ---- Split heavy tiles.  A tile with more isects than the threshold is
+// rendered as chunks of SL isects by separate workgroups of a launch of its
+// own (fwd_kernel<SPLIT>, on a second, high-priority stream concurrent with
+// the whole tiles' launch; a tile's chunks at increasing block indices).
+// Chunk k needs the transmittance entering it, the product of the earlier
+// chunks' (1 - alpha) products: every chunk but the last first computes its
+// own product (chunk_product) and publishes it per wave, then takes the
+// earlier chunks' products, composites from their product and publishes its
+// end T, last id and colour; the tile's last chunk to finish combines them
+// into the pixels.  Hand-offs (MI355X_MICROARCH.md "inter-workgroup
+// visibility"): every published word is stored sc1 (relaxed agent-scope
+// atomic store) and drained (s_waitcnt vmcnt(0)) before the flag store /
+// counter add, and every load of it is an sc1 load behind the matched poll or
+// the returned add.  A chunk waits only for chunks at lower block indices,
+// dispatched before it; the wait is bounded anyway -- on timeout the chunk
+// computes the missing product itself (same code, same value), so no
+// schedule can hang it.
+GS_INLINE void store_sc1(float *p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+GS_INLINE float load_sc1(const float *p) {
+  return __hip_atomic_load(const_cast<float *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+GS_INLINE void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+constexpr int kSpinPolls = 2048;  // >= ~1 ms of polling before the fallback
+GS_INLINE bool wait_flag(const int32_t *f) {
+  for (int i = 0; i < kSpinPolls; ++i) {
+    if (__hip_atomic_load(const_cast<int32_t *>(f), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+      return true;
+    __builtin_amdgcn_s_sleep(8);
+  }
+  return false;
+}
+
+// The product over the records of [start, end) of (1 - alpha) where a record
+// hits the lane's pixel, from 1 and without the termination rule (a product
+// at or below 1e-4 is kept as 0: the pixel is finished).  Same culling, alpha
+// and fma as the compositing.  The wave's strip; uses its LDS stage buffer.
+template <int D>
+GS_INLINE float chunk_product(const Args &a, const WaveGeom &geo, int64_t start, int64_t end,
+                              float4 *st, int lane, float fx, float fy) {
+  constexpr int N4 = FwdPair<D>::N4;
+  float Pp = 1.f;
+  auto id_at = [&](int64_t b0) -> int32_t { return a.flatten_ids[min(b0 + lane, end - 1)]; };
+  int32_t g_n = id_at(start);
+  for (int64_t b0 = start; b0 < end; b0 += 64) {
+    if (__ballot(Pp > 0.f) == 0) break;
+    Attr<D> A;
+    load_attr<D>(a, g_n, A);
+    g_n = id_at(b0 + 64);
+    const bool keep = (b0 + lane < end) && keep_attr<D>(A, geo.x0, geo.x1, geo.y0, geo.y1);
+    const uint64_t m = __ballot(keep);
+    const int cnt = __popcll(m);
+    if (keep) stage_fwd_pair<D>(st, ballot_slot(m), A, (int32_t)(b0 + lane));
+    if ((cnt & 1) && lane == 0) stage_fwd_pad<D>(st, cnt);
+    wave_sync_lds();
+    for (int p = 0; p < (cnt + 1) >> 1; ++p) {
+      f2v f[2 * N4];
+      float4 v[N4];
+#pragma unroll
+      for (int i = 0; i < N4; ++i) v[i] = st[p * N4 + i];
+#pragma unroll
+      for (int i = 0; i < N4; ++i) {
+        asm volatile("" ::"v"(v[i].x), "v"(v[i].y), "v"(v[i].z), "v"(v[i].w));
+        f[2 * i] = f2v{v[i].x, v[i].y};
+        f[2 * i + 1] = f2v{v[i].z, v[i].w};
+      }
+      const f2v dx = f[0] - fx, dy = f[1] - fy;
+      const f2v s2 = dx * (f[2] * dx + f[3] * dy) + f[4] * dy * dy;
+      f2v al = f[5] * f2v{__builtin_amdgcn_exp2f(-s2.x), __builtin_amdgcn_exp2f(-s2.y)};
+      al.x = fminf(al.x, kAlphaMax);
+      al.y = fminf(al.y, kAlphaMax);
+      const bool h0 = __float_as_uint(s2.x) <= __float_as_uint(f[6].x);
+      const bool h1 = __float_as_uint(s2.y) <= __float_as_uint(f[6].y);
+      float n0 = h0 ? __builtin_fmaf(-Pp, al.x, Pp) : Pp;
+      n0 = n0 > kTMin ? n0 : 0.f;
+      float n1 = h1 ? __builtin_fmaf(-n0, al.y, n0) : n0;
+      Pp = n1 > kTMin ? n1 : 0.f;
+    }
+    wave_sync_lds();
+  }
+  return Pp;
+}
+
+// One work item of the forward: SPLIT = chunk `item` of the split tiles'
+// list, else the whole tile `item` of the dispatch order (past the plan's
+// count of whole tiles: nothing).
+template <int D, int BLEND, bool SPLIT>
+GS_INLINE void fwd_item(const Args &a, float4 *st, int item) {
   using P = FwdPair<D>;
   constexpr int N4 = P::N4;
-  __shared__ float4 stage_all[4][32 * N4];
   const int lane = threadIdx.x & 63;
-  float4 *st = stage_all[threadIdx.x >> 6];
-  const uint64_t t_start = tl_now(a);
+  const uint64_t t_start = SPLIT ? 0 : tl_now(a);
   int tile_, kc = -1;  // kc >= 0: chunk kc of a split tile
-  if (a.fitems) {
-    if ((int)blockIdx.x >= a.fcount[0]) return;  // grid is an upper bound
-    const int2 it = a.fitems[blockIdx.x];
+  if constexpr (SPLIT) {
+    const int2 it = a.fitems[item];
     tile_ = it.x;
     kc = it.y;
   } else {
-    tile_ = fwd_tile(a);
+    if (a.n_whole && item >= a.n_whole[0]) return;  // the split tiles' slots
+    tile_ = a.order ? a.order[item] : item;
   }
   const WaveGeom geo(a, lane, tile_);
   const int tile = geo.tile, c = geo.c;
   const bool inside = geo.px < a.W && geo.py < a.H;
   const float fx = (float)geo.px + 0.5f, fy = (float)geo.py + 0.5f;
-  const int64_t tstart = a.offsets[tile];
-  const int64_t tend = tile_end(a, tile);
-  const int64_t start = kc >= 0 ? tstart + (int64_t)kc * a.SL : tstart;
-  const int64_t end = kc >= 0 ? min(tend, start + (int64_t)a.SL) : tend;
+  // isect indices fit 32 bits (the offsets are int32); wave-uniform, kept
+  // in SGPRs
+  const int tstart = __builtin_amdgcn_readfirstlane(a.offsets[tile]);
+  const int tend = __builtin_amdgcn_readfirstlane((int)tile_end(a, tile));
+  const int start = kc >= 0 ? tstart + kc * a.SL : tstart;
+  const int end = kc >= 0 ? min(tend, start + a.SL) : tend;
   const bool skip_tile = a.masks && a.masks[tile];
 
   // colour accumulated from even (.x) and odd (.y) records of each pair in the
@@ -473,21 +559,50 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) f
   // final transmittance.
   float T = (!inside || skip_tile) ? -1.f : 1.f;
   const int pix_in_tile = (threadIdx.x >> 6) * 64 + lane;  // row-major
-  if (kc > 0 && inside && !skip_tile) {
-    // chunk kc of a split tile: the transmittance entering it is the product
-    // of the earlier chunks' (fwd_prod_kernel).  At or below 1e-4 the pixel
-    // terminated in an earlier chunk (every blended factor kept it above);
-    // -Tin marks it finished with about that transmittance.
+  const int wv = threadIdx.x >> 6;
+  // split tiles (see "Split heavy tiles"): product passes (this
+  // chunk's own, then any earlier one not published in time), then the
+  // transmittance entering the chunk
+  const int nch = SPLIT ? (int)((tend - tstart + a.SL - 1) / a.SL) : 0;
+  if (SPLIT && nch > 1 && !skip_tile) {
+    bool own = kc < nch - 1;  // this chunk's product still to publish
+    int jn = 0;               // next earlier chunk whose product to take
     float Tin = 1.f;
-    for (int j = 0; j < kc; ++j)
-      Tin *= a.prod[((tstart + (int64_t)(j + 1) * a.SL) / a.L) * (kTS * kTS) + pix_in_tile];
-    T = Tin > kTMin ? Tin : -fmaxf(Tin, 1e-30f);
+    for (;;) {
+      int ps = start;
+      if (!own) {
+        for (; jn < kc; ++jn) {
+          const int64_t sl = (tstart + (jn + 1) * a.SL) / a.L;
+          if ((a.dbg & 2) || !wait_flag(a.pflag + 4 * sl + wv)) break;
+          Tin *= load_sc1(a.prod + sl * (kTS * kTS) + pix_in_tile);
+        }
+        if (jn == kc) break;
+        ps = tstart + jn * a.SL;
+      }
+      const float Pp = chunk_product<D>(a, geo, ps, ps + a.SL, st, lane, fx, fy);
+      if (own) {
+        const int64_t sl = end / a.L;
+        store_sc1(a.prod + sl * (kTS * kTS) + pix_in_tile, Pp);
+        drain_stores();
+        if (lane == 0)
+          __hip_atomic_store(a.pflag + 4 * sl + wv, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        own = false;
+      } else {
+        Tin *= Pp;
+        ++jn;
+      }
+    }
+    // at or below 1e-4 the pixel terminated in an earlier chunk (every
+    // blended factor kept it above): -Tin marks it finished with about that
+    // transmittance
+    if (kc > 0 && inside) T = Tin > kTMin ? Tin : -fmaxf(Tin, 1e-30f);
   }
+  const int rs = start, re = end;
 
-  if (!skip_tile && start < end) {
+  if (!skip_tile && rs < re) {
     // flatten id of lane `lane` of the batch at b0, clamped into the range
-    auto id_at = [&](int64_t b0) -> int32_t {
-      return a.flatten_ids[min(b0 + lane, end - 1)];
+    auto id_at = [&](int b0) -> int32_t {
+      return a.flatten_ids[min(b0 + lane, re - 1)];
     };
     bool done = false;
     // one record of a pair: sequential in T
@@ -555,8 +670,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) f
         }
       }
     };
-    auto stage = [&](const Attr<D> &at, int64_t b0) -> int {
-      const bool keep = (b0 + lane < end) && keep_attr<D>(at, geo.x0, geo.x1, geo.y0, geo.y1);
+    auto stage = [&](const Attr<D> &at, int b0) -> int {
+      const bool keep = (b0 + lane < re) && keep_attr<D>(at, geo.x0, geo.x1, geo.y0, geo.y1);
       const uint64_t m = __ballot(keep);
       const int cnt = __popcll(m);
       if (keep) stage_fwd_pair<D>(st, ballot_slot(m), at, (int32_t)(b0 + lane));
@@ -575,9 +690,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) f
     // b of a pixel only when b <= its last id (bwd2_kernel), and a pixel that
     // blends record last_id was alive at every boundary up to it.  Boundaries
     // past the strip's end (all pixels finished) are not written at all.
-    const int64_t L = a.L;
-    auto slot = [&](int64_t bidx) { return a.state + (bidx / L) * (int64_t)(kTS * kTS * (1 + D)); };
-    int64_t cur_b = start;  // start of the chunk being accumulated
+    const int L = a.L;
+    auto slot = [&](int bidx) { return a.state + (int64_t)(bidx / L) * (kTS * kTS * (1 + D)); };
+    int cur_b = start;  // start of the chunk being accumulated
     bool live_b = T > 0.f;  // the pixel was alive at cur_b
     auto close_chunk = [&]() {  // fold acc into tot; store S of the chunk at cur_b
       float *sl = slot(cur_b);
@@ -589,7 +704,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) f
         acc[d] = f2v{0.f, 0.f};
       }
     };
-    auto save_state = [&](int64_t bidx) {  // reached boundary bidx
+    auto save_state = [&](int bidx) {  // reached boundary bidx
       close_chunk();
       cur_b = bidx;
       live_b = T > 0.f;
@@ -598,13 +713,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) f
     // a chunk of a split tile writes the state of the boundaries inside it
     // and the colour it adds at its own start boundary
     const bool chunked = a.state && L > 0 && (end - start > L || kc > 0);
-    int64_t b0 = start;
+    int b0 = rs;
     // two attribute buffers in alternation: while batch b is composited from
     // one, the other receives batch b+1, and the ids of batch b+2 load
     Attr<D> A, B;
-    load_attr<D>(a, id_at(start), A);
-    int32_t g_n = id_at(start + 64);
-    while (b0 < end) {
+    load_attr<D>(a, id_at(rs), A);
+    int32_t g_n = id_at(rs + 64);
+    while (b0 < re) {
       if (__ballot(T > 0.f) == 0) break;
       if (chunked && b0 > start && (b0 - start) % L == 0) save_state(b0);
       load_attr<D>(a, g_n, B);
@@ -612,7 +727,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) f
       composite(stage(A, b0));
       wave_sync_lds();
       b0 += 64;
-      if (done || b0 >= end) break;
+      if (done || b0 >= re) break;
       if (chunked && (b0 - start) % L == 0) save_state(b0);
       load_attr<D>(a, g_n, A);
       g_n = id_at(b0 + 128);
@@ -623,21 +738,62 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) f
     }
     if (chunked) close_chunk();
   }
+
 #pragma unroll
   for (int d = 0; d < D; ++d) tot[d] += acc[d].x + acc[d].y;
 
-  if (kc >= 0) {
-    // chunk of a split tile: its end T, last id and colour for
-    // fwd_combine_kernel; and its end T at the next boundary of the
-    // backward's chunk state (the running T the unsplit forward stores there;
-    // the loop above wrote the boundaries inside the chunk and the colours)
+  if constexpr (SPLIT) {
+    // chunk of a split tile: its end T, last id and colour for the combine;
+    // and its end T at the next boundary of the backward's chunk state (the
+    // running T the unsplit forward stores there; the loop above wrote the
+    // boundaries inside the chunk and the colours)
     const int64_t sz = kTS * kTS;
-    float *co = a.cout + (int64_t)((int)blockIdx.x - a.fcount[3]) * sz * (2 + D);
-    co[pix_in_tile] = T;
-    co[sz + pix_in_tile] = __int_as_float(last);
+    const int cid = item;
+    float *co = a.cout + (int64_t)cid * sz * (2 + D);
+    store_sc1(co + pix_in_tile, T);
+    store_sc1(co + sz + pix_in_tile, __int_as_float(last));
 #pragma unroll
-    for (int d = 0; d < D; ++d) co[(2 + d) * sz + pix_in_tile] = tot[d];
+    for (int d = 0; d < D; ++d) store_sc1(co + (2 + d) * sz + pix_in_tile, tot[d]);
     if (end < tend && a.state) a.state[(end / a.L) * sz * (1 + D) + pix_in_tile] = T;
+    drain_stores();
+    __syncthreads();
+    __shared__ int s_last;
+    if (threadIdx.x == 0)
+      s_last = __hip_atomic_fetch_add(a.ctr + (cid - kc), 1, __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT) == nch - 1;
+    __syncthreads();
+    if (s_last && inside) {
+      // the tile's last chunk to finish: per pixel the sum of the chunks'
+      // colours, the final T (the end T of the chunk where the pixel
+      // terminated -- the first negative -- else of the last chunk) and the
+      // largest last id
+      float col[D];
+#pragma unroll
+      for (int d = 0; d < D; ++d) col[d] = 0.f;
+      int32_t lst = 0;
+      float Tf = 1.f;
+      bool fin = false;
+      for (int k = 0; k < nch; ++k) {
+        const float *ck = a.cout + (int64_t)(cid - kc + k) * sz * (2 + D);
+        const float Te = load_sc1(ck + pix_in_tile);
+        lst = max(lst, __float_as_int(load_sc1(ck + sz + pix_in_tile)));
+#pragma unroll
+        for (int d = 0; d < D; ++d) col[d] += load_sc1(ck + (2 + d) * sz + pix_in_tile);
+        if (!fin) {
+          Tf = fabsf(Te);
+          fin = Te < 0.f;
+        }
+      }
+      const int64_t pix = ((int64_t)c * a.H + geo.py) * a.W + geo.px;
+      float *oc = a.render_colors + pix * D;
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        const float bg = a.backgrounds ? a.backgrounds[c * D + d] : 0.f;
+        oc[d] = col[d] + Tf * bg;
+      }
+      a.render_alphas[pix] = 1.f - Tf;
+      a.last_ids[pix] = lst;
+    }
   } else if (inside) {
     const int64_t pix = ((int64_t)c * a.H + geo.py) * a.W + geo.px;
     float *oc = a.render_colors + pix * D;
@@ -649,118 +805,27 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) f
     a.render_alphas[pix] = 1.f - fabsf(T);
     a.last_ids[pix] = last;
   }
-  tl_store(a, t_start, lane);
+  if (!SPLIT) tl_store(a, t_start, lane);
 }
 
-// Split heavy tiles, pass 1: for chunk k of a split tile (every chunk but the
-// last), the product over its records of (1 - alpha) where a record hits,
-// per pixel, from 1 and without the termination rule (a product at or below
-// 1e-4 is kept as 0: every pixel past it is finished).  Same culling, alpha
-// and fma as the compositing.  One 16x4 strip per wave, as fwd_kernel.
-template <int D>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5)))
-fwd_prod_kernel(Args a) {
-  using P = FwdPair<D>;
-  constexpr int N4 = P::N4;
-  __shared__ float4 stage_all[4][32 * N4];
-  const int lane = threadIdx.x & 63;
+// SPLIT: the split tiles' chunks (workgroups 0 .. n_chunks - 1, dispatched
+// first: they are the longest work) and the other tiles in one launch, so the
+// chunks overlap the whole tiles; else the whole tiles only (the split path's
+// code costs registers: 80 -> 95 VGPRs, 6 -> 5 waves per SIMD at D = 3).
+template <int D, int BLEND = 0, bool SPLIT = false>
+__global__ void __launch_bounds__(256)
+__attribute__((amdgpu_waves_per_eu(!SPLIT && D <= 3 ? 6 : 5))) fwd_kernel(Args a) {
+  __shared__ float4 stage_all[4][32 * FwdPair<D>::N4];
   float4 *st = stage_all[threadIdx.x >> 6];
-  for (int item = blockIdx.x; item < a.fcount[1]; item += gridDim.x) {
-  const int2 it = a.p1items[item];
-  const WaveGeom geo(a, lane, it.x);
-  const int64_t tstart = a.offsets[geo.tile];
-  const int64_t start = tstart + (int64_t)it.y * a.SL;
-  const int64_t end = start + a.SL;  // never the last chunk: full length
-  const float fx = (float)geo.px + 0.5f, fy = (float)geo.py + 0.5f;
-  float Pp = 1.f;
-  auto id_at = [&](int64_t b0) -> int32_t { return a.flatten_ids[min(b0 + lane, end - 1)]; };
-  int32_t g_n = id_at(start);
-  for (int64_t b0 = start; b0 < end; b0 += 64) {
-    if (__ballot(Pp > 0.f) == 0) break;
-    Attr<D> A;
-    load_attr<D>(a, g_n, A);
-    g_n = id_at(b0 + 64);
-    const bool keep = (b0 + lane < end) && keep_attr<D>(A, geo.x0, geo.x1, geo.y0, geo.y1);
-    const uint64_t m = __ballot(keep);
-    const int cnt = __popcll(m);
-    if (keep) stage_fwd_pair<D>(st, ballot_slot(m), A, (int32_t)(b0 + lane));
-    if ((cnt & 1) && lane == 0) stage_fwd_pad<D>(st, cnt);
-    wave_sync_lds();
-    for (int p = 0; p < (cnt + 1) >> 1; ++p) {
-      f2v f[2 * N4];
-      float4 v[N4];
-#pragma unroll
-      for (int i = 0; i < N4; ++i) v[i] = st[p * N4 + i];
-#pragma unroll
-      for (int i = 0; i < N4; ++i) {
-        asm volatile("" ::"v"(v[i].x), "v"(v[i].y), "v"(v[i].z), "v"(v[i].w));
-        f[2 * i] = f2v{v[i].x, v[i].y};
-        f[2 * i + 1] = f2v{v[i].z, v[i].w};
-      }
-      const f2v dx = f[0] - fx, dy = f[1] - fy;
-      const f2v s2 = dx * (f[2] * dx + f[3] * dy) + f[4] * dy * dy;
-      f2v al = f[5] * f2v{__builtin_amdgcn_exp2f(-s2.x), __builtin_amdgcn_exp2f(-s2.y)};
-      al.x = fminf(al.x, kAlphaMax);
-      al.y = fminf(al.y, kAlphaMax);
-      const bool h0 = __float_as_uint(s2.x) <= __float_as_uint(f[6].x);
-      const bool h1 = __float_as_uint(s2.y) <= __float_as_uint(f[6].y);
-      float n0 = h0 ? __builtin_fmaf(-Pp, al.x, Pp) : Pp;
-      n0 = n0 > kTMin ? n0 : 0.f;
-      float n1 = h1 ? __builtin_fmaf(-n0, al.y, n0) : n0;
-      Pp = n1 > kTMin ? n1 : 0.f;
-    }
-    wave_sync_lds();
+  if constexpr (SPLIT) {
+    const int nc = a.n_chunks[0];
+    if ((int)blockIdx.x < nc)
+      fwd_item<D, BLEND, true>(a, st, (int)blockIdx.x);
+    else
+      fwd_item<D, BLEND, false>(a, st, (int)blockIdx.x - nc);
+  } else {
+    fwd_item<D, BLEND, false>(a, st, (int)blockIdx.x);
   }
-  const int pit = (threadIdx.x >> 6) * 64 + lane;
-  a.prod[(end / a.L) * (kTS * kTS) + pit] = Pp;
-  }
-}
-
-// Split heavy tiles, pass 3: per pixel of a split tile, its colour (the sum
-// of the chunks' colours), its final T (the end T of the chunk where it
-// terminated -- the first negative -- else of the last chunk) and its last id
-// (the largest of the chunks').  One thread per pixel.
-template <int D>
-__global__ void __launch_bounds__(256) fwd_combine_kernel(Args a) {
-  if ((int)blockIdx.x >= a.fcount[2]) return;
-  const int2 hv = a.heavy[blockIdx.x];
-  const int tile = hv.x;
-  const int ntile = a.tw * a.th;
-  const int c = tile / ntile, rem = tile - c * ntile;
-  const int ty = rem / a.tw, tx = rem - ty * a.tw;
-  const int pit = threadIdx.x;
-  const int px = tx * kTS + (pit & 15), py = ty * kTS + (pit >> 4);
-  if (px >= a.W || py >= a.H) return;
-  const int64_t tstart = a.offsets[tile];
-  const int64_t tend = tile_end(a, tile);
-  const int64_t sz = kTS * kTS;
-  float col[D];
-#pragma unroll
-  for (int d = 0; d < D; ++d) col[d] = 0.f;
-  int32_t last = 0;
-  float Tf = 1.f;
-  bool fin = false;
-  int64_t cid = hv.y;
-  for (int64_t b = tstart; b < tend; b += a.SL, ++cid) {
-    const float *co = a.cout + cid * sz * (2 + D);
-    const float Te = co[pit];
-    last = max(last, __float_as_int(co[sz + pit]));
-#pragma unroll
-    for (int d = 0; d < D; ++d) col[d] += co[(2 + d) * sz + pit];
-    if (!fin) {
-      Tf = fabsf(Te);
-      fin = Te < 0.f;
-    }
-  }
-  const int64_t pix = ((int64_t)c * a.H + py) * a.W + px;
-  float *oc = a.render_colors + pix * D;
-#pragma unroll
-  for (int d = 0; d < D; ++d) {
-    const float bg = a.backgrounds ? a.backgrounds[c * D + d] : 0.f;
-    oc[d] = col[d] + Tf * bg;
-  }
-  a.render_alphas[pix] = 1.f - Tf;
-  a.last_ids[pix] = last;
 }
 
 // Backward: batches of 64 isects from the back, same two-deep gather pipeline.
@@ -1008,10 +1073,11 @@ __attribute__((amdgpu_waves_per_eu(BwdOcc<PX>::W))) bwd2_kernel(Args a) {
   const float rx0 = tx * kTS + 0.5f, rx1 = rx0 + (kTS - 1);
   const float ry0 = ty * kTS + 4 * PX * w + 0.5f, ry1 = ry0 + (4 * PX - 1);
   if (a.masks && a.masks[tile]) return;
-  const int64_t tstart = a.offsets[tile];
-  const int64_t tend = tile_end(a, tile);
-  const int64_t start = a.items ? tstart + (int64_t)k * a.L : tstart;
-  const int64_t cend = a.items ? min(tend, start + a.L) : tend;
+  // isect indices fit 32 bits (the offsets are int32); wave-uniform
+  const int tstart = __builtin_amdgcn_readfirstlane(a.offsets[tile]);
+  const int tend = __builtin_amdgcn_readfirstlane((int)tile_end(a, tile));
+  const int start = a.items ? tstart + k * a.L : tstart;
+  const int cend = a.items ? min(tend, start + a.L) : tend;
 
   const float fx = (float)px + 0.5f;
   float fy[PX], T[PX], rD[PX], bgt[PX], TfDra[PX], Drc[PX][D];
@@ -1046,7 +1112,7 @@ __attribute__((amdgpu_waves_per_eu(BwdOcc<PX>::W))) bwd2_kernel(Args a) {
         const int64_t per = (int64_t)(kTS * kTS * (1 + D));
         T[q] = fabsf(a.state[(cend / a.L) * per + p]);
         float s = 0.f;
-        for (int64_t bi = cend; bi <= mylast[q]; bi += a.L) {
+        for (int bi = cend; bi <= mylast[q]; bi += a.L) {
           const float *sl = a.state + (bi / a.L) * per;
 #pragma unroll
           for (int d = 0; d < D; ++d) s += sl[(1 + d) * kTS * kTS + p] * Drc[q][d];
@@ -1060,14 +1126,14 @@ __attribute__((amdgpu_waves_per_eu(BwdOcc<PX>::W))) bwd2_kernel(Args a) {
   for (int q = 1; q < PX; ++q) lmax = max(lmax, mylast[q]);
 #pragma unroll
   for (int msk = 32; msk >= 1; msk >>= 1) lmax = max(lmax, __shfl_xor(lmax, msk, 64));
-  const int64_t end = min(cend, (int64_t)lmax + 1);
+  const int end = min(cend, lmax + 1);
 
   if (start < end) {
-    auto id_at = [&](int64_t b1) -> int32_t {
+    auto id_at = [&](int b1) -> int32_t {
       return a.flatten_ids[max(b1 - 64 + lane, start)];
     };
-    auto stage = [&](const Attr<D> &at, int64_t b1) -> int {
-      const int64_t j = b1 - 64 + lane;
+    auto stage = [&](const Attr<D> &at, int b1) -> int {
+      const int j = b1 - 64 + lane;
       const bool keep = (j >= start) && keep_attr<D>(at, rx0, rx1, ry0, ry1);
       const uint64_t m = __ballot(keep);
       const int cnt = __popcll(m);
@@ -1182,7 +1248,7 @@ __attribute__((amdgpu_waves_per_eu(BwdOcc<PX>::W))) bwd2_kernel(Args a) {
       Attr<D> A;
       load_attr<D>(a, g_n, A);
       g_n = id_at(end - 64);
-      for (int64_t b1 = end; b1 > start; b1 -= 64) {
+      for (int b1 = end; b1 > start; b1 -= 64) {
         Attr<D> An;
         load_attr<D>(a, g_n, An);  // clamped ids: valid past the last batch too
         g_n = id_at(b1 - 128);
@@ -1191,7 +1257,7 @@ __attribute__((amdgpu_waves_per_eu(BwdOcc<PX>::W))) bwd2_kernel(Args a) {
         A = An;
       }
     } else {
-      for (int64_t b1 = end; b1 > start; b1 -= 64) {
+      for (int b1 = end; b1 > start; b1 -= 64) {
         Attr<D> A;
         load_attr<D>(a, g_n, A);
         g_n = id_at(b1 - 64);
@@ -1223,8 +1289,9 @@ unpack_kernel(int64_t G, int S, const float *__restrict__ packed, float *__restr
 }
 
 // The largest tile's isect count -> *out (lane 0 of the block; out may be
-// null): read back by the host on a LATER render to decide whether to split
-// heavy tiles (use_split_now), never for correctness.  Uses one barrier.
+// null): read back by the host on a LATER render to decide whether to launch
+// the split-capable forward (use_split_now), never for correctness.  Uses
+// one barrier.
 GS_INLINE void block_max_out(int64_t v, int32_t *out) {
   __shared__ int smax;
   if (threadIdx.x == 0) smax = 0;
@@ -1304,48 +1371,47 @@ tile_order_kernel(int n_tiles, const int32_t *__restrict__ offsets, int64_t n_is
   }
 }
 
-// Forward plan with split heavy tiles.  A tile with more than `split` isects
-// (and not masked) is rendered as ceil(n / L) chunks that run in parallel
-// (fwd_prod_kernel -> fwd_kernel chunk items -> fwd_combine_kernel), so the
-// longest tiles no longer serialise the end of the launch.  Work items, in
-// dispatch order (tile_order_kernel's heaviest-first buckets, a chunk
-// counted as a tile of its length): unsplit tiles with >= 2048 isects, the
-// chunks, unsplit tiles with >= 1024, >= 512, the rest.  One 1024-lane
+// Forward plan with split heavy tiles, decided on this render's tiles.  A
+// tile with more than `split` isects is rendered as ceil(n / SL) chunks that
+// run in parallel in a launch of their own (see "Split heavy tiles"), so the
+// longest tiles no longer serialise the end of the forward.  Outputs: `order` = the other tiles in tile_order_kernel's
+// dispatch order (buckets of >= 2048, >= 1024, >= 512 isects, the rest; lane
+// order inside a bucket), hdr[0] their number; `chunks` = (tile, k) of the
+// split tiles, a tile's chunks consecutive in k, hdr[1] their number; the
+// split tiles' hand-off flags and chunk counters cleared.  One 1024-lane
 // workgroup, 16 tiles per lane (n_tiles <= 16384).
 __global__ void __launch_bounds__(1024)
 fwd_plan_kernel(int n_tiles, const int32_t *__restrict__ offsets, int64_t n_isects,
-                const int64_t *__restrict__ n_dev, const uint8_t *__restrict__ masks, int SL, int split, int32_t *__restrict__ hdr,
-                int2 *__restrict__ fitems, int2 *__restrict__ p1items,
-                int2 *__restrict__ heavy, int32_t *__restrict__ max_out) {
-  // quantities: [0] unsplit >= 2048, [1] chunks, [2] unsplit >= 1024,
-  // [3] unsplit >= 512, [4] unsplit rest, [5] split tiles
-  constexpr int PER = 16, NQ = 6;
+                const int64_t *__restrict__ n_dev, const uint8_t *__restrict__ masks, int SL,
+                int L, int split, int32_t *__restrict__ hdr, int32_t *__restrict__ order,
+                int2 *__restrict__ chunks, int32_t *__restrict__ pflag,
+                int32_t *__restrict__ ctr, int32_t *__restrict__ max_out) {
+  // quantities: [0..3] whole tiles per bucket, [4] chunks
+  constexpr int PER = 16, NQ = 5;
   __shared__ int wsum[16][NQ];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  // category and chunk count of tile t (recomputed in the write pass: keeps
-  // the 16 tiles' state out of registers)
+  // bucket (or -1: split) and chunk count of tile t (recomputed in the write
+  // pass: keeps the 16 tiles' state out of registers)
   auto classify = [&](int t, int &nch) -> int {
-    const int64_t e = tile_end(offsets, t, n_tiles, n_dev, n_isects);
-    const int64_t n = e - offsets[t];
+    const int64_t n = tile_end(offsets, t, n_tiles, n_dev, n_isects) - offsets[t];
     nch = 0;
     if (n > split && !(masks && masks[t])) {
       nch = (int)((n + SL - 1) / SL);
-      return 1;
+      return -1;
     }
-    return n >= 2048 ? 0 : n >= 1024 ? 2 : n >= 512 ? 3 : 4;
+    return n >= 2048 ? 0 : n >= 1024 ? 1 : n >= 512 ? 2 : 3;
   };
-  int mine[NQ] = {0, 0, 0, 0, 0, 0};
+  int mine[NQ] = {0, 0, 0, 0, 0};
   int64_t nmax = 0;
   for (int i = 0; i < PER; ++i) {
     const int t = tid + 1024 * i;
     if (t >= n_tiles) break;
     int nch;
     const int kd = classify(t, nch);
-    const int64_t e = tile_end(offsets, t, n_tiles, n_dev, n_isects);
-    nmax = max(nmax, e - offsets[t]);
 #pragma unroll
-    for (int q = 0; q < NQ; ++q)
-      mine[q] += (q == kd && kd != 1) ? 1 : (q == 1 ? nch : (q == 5 && kd == 1 ? 1 : 0));
+    for (int q = 0; q < 4; ++q) mine[q] += q == kd;
+    mine[4] += nch;
+    nmax = max(nmax, tile_end(offsets, t, n_tiles, n_dev, n_isects) - offsets[t]);
   }
   block_max_out(nmax, max_out);
   int x[NQ];
@@ -1363,53 +1429,52 @@ fwd_plan_kernel(int n_tiles, const int32_t *__restrict__ offsets, int64_t n_isec
     for (int q = 0; q < NQ; ++q) wsum[w][q] = x[q];
   }
   __syncthreads();
-  int before[NQ], total[NQ];
+  int pos[NQ], total[NQ];
 #pragma unroll
   for (int q = 0; q < NQ; ++q) {
-    before[q] = x[q] - mine[q];
+    pos[q] = x[q] - mine[q];
     total[q] = 0;
     for (int ww = 0; ww < 16; ++ww) {
-      before[q] += ww < w ? wsum[ww][q] : 0;
+      pos[q] += ww < w ? wsum[ww][q] : 0;
       total[q] += wsum[ww][q];
     }
   }
-  // positions: fitems = the categories in order; p1items and heavy
-  int pos[5];
+  // bucket q's whole tiles start after the heavier buckets
   int base = 0;
 #pragma unroll
-  for (int q = 0; q < 5; ++q) {
-    pos[q] = base + before[q];
+  for (int q = 0; q < 4; ++q) {
+    pos[q] += base;
     base += total[q];
   }
-  int pP = before[1] - before[5], pH = before[5];  // p1 items: chunks minus one per split tile
   for (int i = 0; i < PER; ++i) {
     const int t = tid + 1024 * i;
     if (t >= n_tiles) break;
     int nch;
     const int kd = classify(t, nch);
-    if (kd == 1) {
-      heavy[pH++] = make_int2(t, pos[1] - total[0]);
+    if (kd < 0) {
+      ctr[pos[4]] = 0;  // index of chunk 0
       for (int k = 0; k < nch; ++k) {
-        fitems[pos[1]++] = make_int2(t, k);
-        if (k < nch - 1) p1items[pP++] = make_int2(t, k);
+        chunks[pos[4]++] = make_int2(t, k);
+        if (k < nch - 1) {
+          const int64_t sl = ((int64_t)offsets[t] + (int64_t)(k + 1) * SL) / L;
+          reinterpret_cast<int4 *>(pflag)[sl] = make_int4(0, 0, 0, 0);
+        }
       }
     } else {
       int p = pos[0];
+      p = kd == 1 ? pos[1] : p;
       p = kd == 2 ? pos[2] : p;
       p = kd == 3 ? pos[3] : p;
-      p = kd == 4 ? pos[4] : p;
-      fitems[p] = make_int2(t, -1);
+      order[p] = t;
       pos[0] += kd == 0;
+      pos[1] += kd == 1;
       pos[2] += kd == 2;
       pos[3] += kd == 3;
-      pos[4] += kd == 4;
     }
   }
   if (tid == 0) {
-    hdr[0] = total[0] + total[1] + total[2] + total[3] + total[4];
-    hdr[1] = total[1] - total[5];
-    hdr[2] = total[5];
-    hdr[3] = total[0];
+    hdr[0] = base;
+    hdr[1] = total[4];
   }
 }
 
@@ -1534,25 +1599,22 @@ static bool use_order(int n_tiles, int64_t n_isects) {
   return n_isects > 0 && n_tiles > 0 && n_tiles <= 16384;
 }
 
-// Split heavy tiles in the forward (fwd_plan_kernel): a tile with more
-// isects than the threshold is rendered as parallel chunks of split_chunk()
-// isects, so that it no longer runs alone for the end of the launch.  Mode
+// Split heavy tiles in the forward (fwd_plan_kernel, "Split heavy tiles"):
+// a tile with more isects than the threshold is rendered as parallel chunks
+// of split_chunk() isects, concurrently with the other tiles, so that it no
+// longer runs alone for the end of the launch.  Mode
 // (GSPLAT_HIP_FWD_SPLIT / gsplat_hip_debug_set_fwd_split): unset or < 0 =
-// adaptive, threshold max(2048, n_isects / GSPLAT_HIP_FWD_SPLIT_DIV (550)) --
-// a tile longer than ~1/550 of all isects outlasts the rest of the launch
-// (measured: at M3 the heaviest, 21 k-isect tile ran 415 us against 250 us
-// for 99 % of the waves; at M2 no tile passes it) -- and only when the
-// previous render had such a tile (use_split_now); > 0 = that fixed
-// threshold; 0 = off, the default.  Measured (chunks of 512, adaptive): M3
-// forward 0.584 -> 0.526 ms, but M2 0.183 -> 0.202 ms -- the product pass and
-// the combine are serialised launches on the critical path, which costs more
-// than the ~10 us tail of M2's heaviest tiles; M3 step time +1 %, M2 -1.5 %.
+// adaptive, threshold max(2048, n_isects / GSPLAT_HIP_FWD_SPLIT_DIV) -- a
+// tile longer than that fraction of all isects outlasts the rest of the
+// launch (at M3 the heaviest, 21 k-isect tile ran 415 us against 250 us for
+// 99 % of the waves) -- decided per tile on the device, so a render without
+// such a tile runs the plain forward; > 0 = that fixed threshold; 0 = off.
 static int g_fwd_split = INT32_MIN;  // not yet read from the environment
 
 static int fwd_split_mode() {
   if (g_fwd_split == INT32_MIN) {
     const char *e = getenv("GSPLAT_HIP_FWD_SPLIT");
-    g_fwd_split = e ? atoi(e) : 0;  // off by default (measured below)
+    g_fwd_split = e ? atoi(e) : -1;
     if (g_fwd_split < 0) g_fwd_split = -1;
   }
   return g_fwd_split;
@@ -1582,19 +1644,19 @@ static int split_chunk() {
 }
 
 // After the chunk slots and the tile order, the split area:
-// [hdr 64 B][fitems int2 x (n_tiles + n_isects/SL + 1)][p1items int2 x
-// (n_isects/SL + 1)][heavy int2 x n_tiles][prod f32 x (n_isects/L + 1) x 256,
-// by boundary slot][cout f32 x (n_tiles + n_isects/SL + 1) x 256 x (2 + D)],
-// each part 256-B aligned (chunks: sum over split tiles of ceil(n / SL) <=
-// n_tiles + n_isects / SL).
+// [hdr 64 B][chunks int2 x (n_tiles + n_isects/SL + 1)][prod f32 x
+// (n_isects/L + 1) x 256, by boundary slot][pflag i32 x (n_isects/L + 1) x 4]
+// [ctr i32 x (n_tiles + n_isects/SL + 1)][cout f32 x (n_tiles + n_isects/SL
+// + 1) x 256 x (2 + D)], each part 256-B aligned (chunks: sum over split
+// tiles of ceil(n / SL) <= n_tiles + n_isects / SL).
 struct SplitLayout {
-  int64_t hdr, fitems, p1, heavy, prod, cout, bytes;
+  int64_t hdr, fitems, prod, pflag, ctr, cout, bytes;
 };
 
 static int64_t align256(int64_t x) { return (x + 255) / 256 * 256; }
 
-// The state has room for the split forward whenever it can run; whether a
-// render splits is decided per render (use_split_now).
+// The state has room for the split forward whenever it can run; which tiles
+// split is decided per render on the device (fwd_plan_kernel).
 static bool split_capable(int n_tiles, int64_t n_isects) {
   return fwd_split_mode() != 0 && chunk_len() > 0 && use_order(n_tiles, n_isects);
 }
@@ -1616,10 +1678,13 @@ static int32_t *stat_dev() {
   return g_stat_dev;
 }
 
-// Split this render?  Fixed mode: always; adaptive: when an earlier render's
-// largest tile exceeded this render's threshold (tiles are similar from one
-// training step to the next; a wrong guess costs speed only: an unsplit
-// render of a heavy tile, or the split passes' ~7 us with nothing to split).
+// Launch the split-capable forward?  Fixed threshold: always; adaptive: when
+// an earlier render's largest tile exceeded this render's threshold (tiles
+// are similar from one training step to the next).  Which tiles split is
+// then decided on the device from this render's tiles (fwd_plan_kernel); a
+// wrong guess costs speed only: an unsplit heavy tile, or the split-capable
+// kernel's lower occupancy with nothing to split.  A captured step keeps the
+// choice of its capture.
 static bool use_split_now(int n_tiles, int64_t n_isects) {
   if (!split_capable(n_tiles, n_isects)) return false;
   if (fwd_split_mode() > 0) return true;
@@ -1635,10 +1700,10 @@ static SplitLayout split_layout(int D, int n_tiles, int64_t n_isects) {
   const int64_t px = r16::kTS * r16::kTS;
   l.hdr = 0;
   l.fitems = 256;
-  l.p1 = l.fitems + align256(8 * ((int64_t)n_tiles + ns));
-  l.heavy = l.p1 + align256(8 * ns);
-  l.prod = l.heavy + align256(8 * (int64_t)n_tiles);
-  l.cout = l.prod + align256(4 * nc * px);
+  l.prod = l.fitems + align256(8 * ((int64_t)n_tiles + ns));
+  l.pflag = l.prod + align256(4 * nc * px);
+  l.ctr = l.pflag + align256(16 * nc);
+  l.cout = l.ctr + align256(4 * ((int64_t)n_tiles + ns));
   l.bytes = l.cout + align256(4 * ((int64_t)n_tiles + ns) * px * (2 + D));
   return l;
 }
@@ -1698,9 +1763,13 @@ static int fwd_blend() {
   return v;
 }
 
+static int g_dbg = INT32_MIN;  // not yet read from the environment
 static int dbg_flags() {
-  static const int v = [] { const char *e = getenv("GSPLAT_HIP_DBG"); return e ? atoi(e) : 0; }();
-  return v;
+  if (g_dbg == INT32_MIN) {
+    const char *e = getenv("GSPLAT_HIP_DBG");
+    g_dbg = e ? atoi(e) : 0;
+  }
+  return g_dbg;
 }
 // State whose tile order gsplat_hip_rasterize_prepare already queued (so the
 // forward call does not launch the order kernel again); cleared by the
@@ -1714,12 +1783,12 @@ static void launch_order(int n_tiles, const int32_t *offsets, int64_t n_isects,
   if (split_base) {
     const SplitLayout l = split_layout(D, n_tiles, n_isects);
     hipLaunchKernelGGL(r16::fwd_plan_kernel, dim3(1), dim3(1024), 0, st, n_tiles, offsets,
-                       n_isects, n_dev, (const uint8_t *)nullptr, split_chunk(),
+                       n_isects, n_dev, (const uint8_t *)nullptr, split_chunk(), chunk_len(),
                        (int)std::min<int64_t>(split_threshold(n_isects), INT32_MAX),
-                       reinterpret_cast<int32_t *>(split_base + l.hdr),
+                       reinterpret_cast<int32_t *>(split_base + l.hdr), order,
                        reinterpret_cast<int2 *>(split_base + l.fitems),
-                       reinterpret_cast<int2 *>(split_base + l.p1),
-                       reinterpret_cast<int2 *>(split_base + l.heavy), stat_dev());
+                       reinterpret_cast<int32_t *>(split_base + l.pflag),
+                       reinterpret_cast<int32_t *>(split_base + l.ctr), stat_dev());
   } else
     hipLaunchKernelGGL(r16::tile_order_kernel, dim3(1), dim3(1024), 0, st, n_tiles, offsets,
                        n_isects, n_dev, order,
@@ -1733,22 +1802,18 @@ int r16_fwd(r16::Args a, const void *state, char *split_base, hipStream_t st) {
                  split_base, D);
   g_prepared_state = nullptr;
   if (split_base) {
-    // split heavy tiles: chunk products, every work item (tiles and chunks),
-    // then the split tiles' pixels from their chunks; grids are upper bounds
-    // (the plan's counts are on the device; surplus workgroups exit)
-    const int64_t nc = a.n_isects / a.SL + 1;
-    const int64_t n_heavy_max =
-        std::min<int64_t>(a.n_tiles, a.n_isects / split_threshold(a.n_isects) + 1);
-    hipLaunchKernelGGL((r16::fwd_prod_kernel<D>), dim3((unsigned)std::min<int64_t>(nc, 2048)),
-                       dim3(256), 0, st, a);
+    // the split tiles' chunks and the other tiles in one launch; the grid is
+    // an upper bound (the plan's counts are on the device; surplus
+    // workgroups exit)
+    const int64_t nc = std::min<int64_t>(
+        (int64_t)a.n_tiles + a.n_isects / a.SL + 1,
+        a.n_isects / a.SL + a.n_isects / std::max<int64_t>(1, split_threshold(a.n_isects)) + 1);
     if (fwd_blend() == 1)
-      hipLaunchKernelGGL((r16::fwd_kernel<D, 1>), dim3((unsigned)(a.n_tiles + nc)), dim3(256), 0,
-                         st, a);
+      hipLaunchKernelGGL((r16::fwd_kernel<D, 1, true>), dim3((unsigned)(a.n_tiles + nc)), dim3(256),
+                         0, st, a);
     else
-      hipLaunchKernelGGL((r16::fwd_kernel<D>), dim3((unsigned)(a.n_tiles + nc)), dim3(256), 0, st,
-                         a);
-    hipLaunchKernelGGL((r16::fwd_combine_kernel<D>), dim3((unsigned)n_heavy_max), dim3(256), 0, st,
-                       a);
+      hipLaunchKernelGGL((r16::fwd_kernel<D, 0, true>), dim3((unsigned)(a.n_tiles + nc)), dim3(256),
+                         0, st, a);
     GS_CHECK_LAUNCH("rasterize_fwd16_split");
     return 0;
   }
@@ -1844,11 +1909,12 @@ int rasterize16_fwd(int C, int D, int W, int H, int tw, int th, const float *mea
   if (a.order && a.state && split) {
     split_base = reinterpret_cast<char *>(state) + slots + order_bytes(a.n_tiles, n_isects);
     const SplitLayout l = split_layout(D, a.n_tiles, n_isects);
-    a.fcount = reinterpret_cast<const int32_t *>(split_base + l.hdr);
+    a.n_whole = reinterpret_cast<const int32_t *>(split_base + l.hdr);
+    a.n_chunks = a.n_whole + 1;
     a.fitems = reinterpret_cast<const int2 *>(split_base + l.fitems);
-    a.p1items = reinterpret_cast<const int2 *>(split_base + l.p1);
-    a.heavy = reinterpret_cast<const int2 *>(split_base + l.heavy);
     a.prod = reinterpret_cast<float *>(split_base + l.prod);
+    a.pflag = reinterpret_cast<int32_t *>(split_base + l.pflag);
+    a.ctr = reinterpret_cast<int32_t *>(split_base + l.ctr);
     a.cout = reinterpret_cast<float *>(split_base + l.cout);
     a.SL = split_chunk();
     a.timeline = nullptr;  // per-wave stamps index blocks of the unsplit grid
@@ -1935,6 +2001,12 @@ int rasterize16_bwd(int C, int64_t G, int D, int W, int H, int tw, int th,
 extern "C" int gsplat_hip_debug_set_fwd_split(int isects) {
   const int old = gs::fwd_split_mode();
   gs::g_fwd_split = isects < 0 ? -1 : isects;
+  return old;
+}
+
+extern "C" int gsplat_hip_debug_set_flags(int flags) {
+  const int old = gs::dbg_flags();
+  gs::g_dbg = flags;
   return old;
 }
 

@@ -12,7 +12,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GSPLAT_HIP_LIB", os.path.join(_HERE, "libgsplat_hip.so"))
-ABI_VERSION = 24
+ABI_VERSION = 25
 
 _p = ctypes.c_void_p
 _i32 = ctypes.c_int
@@ -71,6 +71,7 @@ _SIGS = {
     "gsplat_hip_debug_set_timeline": (_i32, [_p, _i64]),
     "gsplat_hip_debug_set_lane_histogram": (_i32, [_p]),
     "gsplat_hip_debug_set_chunk": (_i32, [_i32]),
+    "gsplat_hip_debug_set_flags": (_i32, [_i32]),
     "gsplat_hip_debug_set_fwd_split": (_i32, [_i32]),
     "gsplat_hip_ssim_workspace_bytes": (_i64, [_i32, _i32, _i32, _i32]),
     "gsplat_hip_ssim_l1_fwd": (_i32, [_i32, _i32, _i32, _i32, _p, _p, _p, _p, _p]),

@@ -285,12 +285,20 @@ int gsplat_hip_debug_set_lane_histogram(unsigned long long *device_buffer);
  * rasterization must run with the same setting. */
 int gsplat_hip_debug_set_chunk(int isects);
 /* Split mode of the 16x16 forward: tiles with more isects than the
- * threshold are rendered as parallel chunks.  isects > 0: that threshold;
- * 0: off (the default); < 0: adaptive (max(2048, n_isects / 550) when the
- * previous render had a tile above it), or
- * GSPLAT_HIP_FWD_SPLIT).  Returns the previous mode.  Results do not depend
- * on it beyond the float rounding of the chunks' transmittance products. */
+ * threshold are rendered as parallel chunks (ABI 25: a launch of their own on
+ * a second stream, concurrent with the other tiles' and joined back into the
+ * caller's stream; which tiles split is decided per render on the device).
+ * isects > 0: that threshold; 0: off; < 0: adaptive, max(2048, n_isects /
+ * GSPLAT_HIP_FWD_SPLIT_DIV) (the default, or GSPLAT_HIP_FWD_SPLIT).  Returns
+ * the previous mode.  Results do not depend on it beyond the float rounding
+ * of the chunks' transmittance products. */
 int gsplat_hip_debug_set_fwd_split(int isects);
+/* Debug flags of the 16x16 rasterizer (ABI 25; default 0, or GSPLAT_HIP_DBG):
+ * bit 0 = the backward skips its gradient atomics (timing experiments);
+ * bit 1 = a chunk of a split tile never waits for an earlier chunk's
+ * published product and computes it itself (the timeout path; results are
+ * identical).  Returns the previous flags. */
+int gsplat_hip_debug_set_flags(int flags);
 
 /* ---------------------------------------------------------------------------
  * Trainer-side kernels of the training step (not part of the 5-function

@@ -8,7 +8,9 @@ only, never results.
 * the forward's dispatch order (tile_order_kernel): a permutation of the
   tiles, heaviest bucket first;
 * split heavy tiles (GSPLAT_HIP_FWD_SPLIT): the images of the unsplit
-  forward up to chunk-product rounding, and against the oracle.
+  forward up to chunk-product rounding, and against the oracle; the chunks'
+  hand-off of transmittance products inside the one launch gives the same
+  bits as every chunk computing the earlier products itself.
 """
 
 import numpy as np
@@ -145,6 +147,29 @@ def test_split_forward_matches_unsplit(split, mode):
         scale = max(1e-12, float(b.abs().max()))
         close_most(a, b, 1e-3, 1e-4 * scale, name, max_frac=2e-3, rows=True,
                    out_bound=0.05 * scale)
+
+
+def test_split_handoff_equals_local_products():
+    """A chunk of a split tile takes the earlier chunks' transmittance
+    products from their workgroups (sc1 hand-off, bounded wait) or, when one
+    is late, computes it itself: both give the same bits (debug flag bit 1
+    forces the local path for every chunk)."""
+    from gsplat_hip import _lib
+    ins, W, H = _heavy_scene()
+    rc0, ra0, m0, g0 = _render_split(ins, W, H, 300)
+    old = _lib.query("gsplat_hip_debug_set_flags", 2)
+    try:
+        rc1, ra1, m1, g1 = _render_split(ins, W, H, 300)
+    finally:
+        _lib.query("gsplat_hip_debug_set_flags", old)
+    offs = m0["isect_offsets"].flatten().long()
+    n = m0["flatten_ids"].numel()
+    cnt = torch.diff(torch.cat([offs, torch.tensor([n], device=DEV)]))
+    assert int((cnt > 2048).sum()) >= 4, "scene has too few multi-chunk tiles"
+    assert torch.equal(rc0, rc1) and torch.equal(ra0, ra1)
+    for a, b, name in zip(g1, g0, ["means", "quats", "scales", "opacities", "colors"]):
+        scale = max(1e-12, float(b.abs().max()))
+        assert float((a - b).abs().max()) <= 1e-5 * scale, name
 
 
 def test_split_forward_vs_oracle():

@@ -1,0 +1,24 @@
+#!/bin/bash
+# Split forward (chunk kernel before the whole tiles' on the same stream):
+# raster / parity / graph tests, then M2 and M3 lines for split thresholds
+# (GSPLAT_HIP_FWD_SPLIT_DIV), off (GSPLAT_HIP_FWD_SPLIT=0) and the HEAD build
+# (base: ab_lib/base.so).
+cd "$GRAFT_REPO_ROOT" || exit 1
+export TMPDIR=/tmp
+O=gpurun_out/${1:-ab_split6}; mkdir -p $O
+[ -n "$AB_NOTEST" ] || timeout -k 10 400 python -u -m pytest tests/test_gpu_raster_dispatch.py tests/test_gpu_parity.py tests/test_gpu_graph.py -x -q --timeout 120 --timeout-method thread > $O/tests.log 2>&1
+rc=$?; echo "tests rc=$rc"; tail -2 $O/tests.log; [ $rc -eq 0 ] || exit $rc
+summ() { python3 -c "import json;d=json.loads(open('$1').read().strip().splitlines()[-1]);r=d['roofline'];print(round(d['value'],1), round(r['launch_ms'],4), round(r['bwd']['launch_ms'],4), d['config'].get('step_issue','')[:20])"; }
+B="python -u bench.py --no-traffic --no-cpu-baseline"
+for cfg in ${AB_CFGS:-m2 m3}; do
+  for r in 1 2; do
+    for v in ${AB_VARS:-off 550 2000}; do
+      unset GSPLAT_HIP_FWD_SPLIT GSPLAT_HIP_FWD_SPLIT_DIV GSPLAT_HIP_FWD_SPLIT_CHUNK GSPLAT_HIP_LIB
+      if [ $v = base ] || [ $v = w5 ] || [ $v = bw5 ]; then export GSPLAT_HIP_LIB=$PWD/ab_lib/$v.so;
+      elif [ $v = off ]; then export GSPLAT_HIP_FWD_SPLIT=0;
+      elif [ $v = forced ]; then export GSPLAT_HIP_FWD_SPLIT=100000000; else export GSPLAT_HIP_FWD_SPLIT_DIV=${v%%c*}; [ "$v" != "${v#*c}" ] && export GSPLAT_HIP_FWD_SPLIT_CHUNK=${v#*c}; fi
+      timeout -k 10 300 $B --config $cfg > $O/$cfg.$v.$r.json 2> $O/$cfg.$v.$r.err
+      rc=$?; echo "$cfg $v $r rc=$rc $(summ $O/$cfg.$v.$r.json)"; [ $rc -eq 0 ] || exit $rc
+    done
+  done
+done
