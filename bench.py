@@ -73,6 +73,11 @@ def parse():
                     help="with --dp-path: shard the optimizer rows as W ranks would and "
                          "update this rank's share (the per-rank compute of a W-GPU step; "
                          "the collectives of W ranks are not executed)")
+    ap.add_argument("--gshard-emulate", type=int, default=0, metavar="W",
+                    help="one GPU times rank 0 of a W-rank Gaussian-sharded step: its shard, "
+                         "its camera, the other ranks' exchanged rows from stand-ins "
+                         "recorded from their own renders (exchanges as device copies, no "
+                         "xGMI time; measurement only)")
     ap.add_argument("--probe", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
 
@@ -231,6 +236,11 @@ def main():
     # --dp-path asks for the replicated one
     dp_path = args.dp_path
     gshard = world > 1 and not dp_path
+    emu_world = args.gshard_emulate
+    if emu_world:
+        assert world == 1 and not dp_path and emu_world > 1, \
+            "--gshard-emulate W: a one-GPU measurement, W > 1"
+        gshard = True
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -262,7 +272,20 @@ def main():
         kw = dict(strategy=DefaultStrategyConfig(), sh_degree_interval=1000, max_steps=30_000,
                   init="sfm")
         start = max(0, REFINE_AT - args.warmup - args.steps // 2)
-    tr = Trainer(means, rgbs, vm_pool, K_pool, W, H, sh_degree=3, device=dev, world_size=world,
+    t_world = emu_world or world
+    if emu_world:
+        # the peers' rows for rank 0, from their own renders (distributed.Emulation)
+        from gsplat_hip import distributed as gdist
+        gdist.EMULATION = gdist.Emulation(emu_world)
+        for j in range(1, emu_world):
+            peer = Trainer(means, rgbs, vm_pool, K_pool, W, H, sh_degree=3, device=dev,
+                           world_size=emu_world, rank=j, model=model, gaussian_shard=True,
+                           graph=False, **kw)
+            gdist.EMULATION.record(j, lambda: peer.render(peer.camera_index(start),
+                                                          peer.sh_degree_at(start)))
+            del peer
+        torch.cuda.empty_cache()
+    tr = Trainer(means, rgbs, vm_pool, K_pool, W, H, sh_degree=3, device=dev, world_size=t_world,
                  rank=rank, model=model, sharded_optimizer=dp_path, gaussian_shard=gshard,
                  dp_emulate_world=args.dp_emulate or None,
                  graph=not (args.eager or args.probe), **kw)
@@ -404,6 +427,12 @@ def main():
                    "first_timed_step": start + args.warmup, "width": W, "height": H,
                    "cameras_per_rank_per_step": 1,
                    "parallelism": (
+                       f"gshard{emu_world} emulated on one GPU: the per-rank step of rank 0 "
+                       f"(Gaussians [0::{emu_world}], its own camera, projection + SH into "
+                       f"{emu_world} cameras, rasterization with all Gaussians, per-shard Adam); "
+                       "the other ranks' exchanged rows are stand-ins recorded from their own "
+                       "renders and the exchanges are device copies of the same rows -- no "
+                       "xGMI time (measurement only)") if emu_world else (
                        f"gshard{world}: rank r holds Gaussians [r::{world}] and renders its own "
                        "camera; projected pairs exchanged peer to peer over RCCL/xGMI "
                        "(rasterization(distributed=True)), per-shard Adam, no gradient "

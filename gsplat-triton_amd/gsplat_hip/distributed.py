@@ -14,7 +14,7 @@ of an exchange is the exchange with input and output splits swapped.
 
 import math
 from contextlib import nullcontext as _nullcontext
-from typing import List, Optional, Union
+from typing import List, Optional, Tuple, Union
 
 import torch
 import torch.distributed as dist
@@ -99,12 +99,74 @@ def all_gather_tensor_list(world_size: int, tensor_list: List[Tensor]) -> List[T
             zip(torch.split(collected, sizes, dim=-1), tensor_list)]
 
 
-def _all_to_all_rows(data: Tensor, splits: List[int], out_splits: List[int]) -> Tensor:
+# ---- measurement only (bench.py --gshard-emulate W): one process stands in
+# for rank 0 of a W-rank Gaussian-sharded job, to time that rank's compute on
+# one GPU.  Its exchanges take their peers' rows from stand-ins instead of
+# RCCL: forward, the rows each peer's own render would send to rank 0
+# (recorded once by running that peer's render up to its exchange, `record`),
+# backward, rank 0's own gradient block in every peer's place (same sizes).
+# The stand-ins are concatenated on the device, so the rows are copied but
+# no link is crossed: the exchange's xGMI time is not part of the measurement.
+class _Recorded(Exception):
+    """Raised by a recording render once its rows for rank 0 are kept."""
+
+
+class Emulation:
+    def __init__(self, world: int):
+        self.world, self.rank = int(world), 0
+        self.recording = False
+        self.standins = {}  # dtype -> {peer rank: rows for rank 0}
+
+    def record(self, rank: int, render) -> None:
+        """Run peer `rank`'s render (a callable) up to its float exchange and
+        keep the rows it sends to rank 0."""
+        self.rank, self.recording = int(rank), True
+        try:
+            with torch.no_grad():
+                render()
+        except _Recorded:
+            pass
+        finally:
+            self.rank, self.recording = 0, False
+
+    def rows(self, data: Tensor, splits: List[int], out_splits: List[int], backward: bool):
+        own = data[:splits[0]]  # the block rank 0 sends to itself
+        if self.recording:
+            self.standins.setdefault(data.dtype, {})[self.rank] = own.clone()
+            if data.dtype == torch.float32:
+                raise _Recorded()
+            return data.new_zeros((sum(out_splits),) + data.shape[1:])
+        parts = [own]
+        for j in range(1, self.world):
+            if backward:
+                assert out_splits[j] == own.shape[0], (out_splits, own.shape)
+                parts.append(own)
+            else:
+                blk = self.standins[data.dtype][j]
+                assert blk.shape == (out_splits[j],) + data.shape[1:], (blk.shape, out_splits)
+                parts.append(blk)
+        return torch.cat(parts, dim=0)
+
+
+EMULATION: Optional[Emulation] = None
+
+
+def rank_world() -> Tuple[int, int]:
+    """(rank, world size) of the process group, or of the emulated job."""
+    if EMULATION is not None:
+        return EMULATION.rank, EMULATION.world
+    return dist.get_rank(), dist.get_world_size()
+
+
+def _all_to_all_rows(data: Tensor, splits: List[int], out_splits: List[int],
+                     backward: bool = False) -> Tensor:
     """Rows data[sum(splits[:j]) : ...] to rank j; rank j's rows for me, in
     rank order.  RCCL: one all_to_all_single over contiguous buffers (the
     collective xGMI is built for, no per-peer concat); other backends: the
     per-peer P2P exchange."""
     data = data.contiguous()
+    if EMULATION is not None:
+        return EMULATION.rows(data, splits, out_splits, backward)
     if data.is_cuda and dist.get_backend() == "nccl":
         out = data.new_empty((sum(out_splits),) + data.shape[1:])
         dist.all_to_all_single(out, data, output_split_sizes=out_splits,
@@ -124,7 +186,7 @@ class _AllToAll(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, grad):
-        return _all_to_all_rows(grad, ctx.out_splits, ctx.splits), None, None
+        return _all_to_all_rows(grad, ctx.out_splits, ctx.splits, backward=True), None, None
 
 
 def all_to_all_tensor_list(world_size: int, tensor_list: List[Tensor],

@@ -133,8 +133,7 @@ def rasterization(
         assert (sh_degree is None and colors.dim() == 2) or (
             sh_degree is not None and (sh_rest is not None or colors.dim() == 3)), \
             "Distributed mode only supports per-Gaussian colors."
-        world_rank = torch.distributed.get_rank()
-        world_size = torch.distributed.get_world_size()
+        world_rank, world_size = gdist.rank_world()
         if _world_counts is not None:
             N_world = [int(n) for n in _world_counts]
             assert len(N_world) == world_size and N_world[world_rank] == N, (N_world, N)

@@ -63,3 +63,42 @@ def test_world_camera_schedule_agrees_across_ranks():
     # evaluation: every rank renders the same camera
     vms, _ = trs[1].world_cameras(2, world_ci=[2] * world)
     assert torch.equal(vms, vm[[2, 2, 2]])
+
+
+def test_emulated_exchange_rows():
+    """bench.py --gshard-emulate: a recording render keeps the rows a peer
+    sends to rank 0 (its first block) and stops at its float exchange; rank
+    0's exchanges then take those rows in the peers' places (forward) and its
+    own gradient block in every peer's place (backward)."""
+    from gsplat_hip import distributed as gdist
+    emu = gdist.Emulation(3)
+    n = [4, 4, 3]  # Gaussians per rank; one camera per rank
+
+    def peer_render(j):
+        radii = torch.arange(3 * n[j], dtype=torch.int32).view(3 * n[j], 1) + 100 * j
+        rows = torch.arange(3 * n[j] * 2, dtype=torch.float32).view(3 * n[j], 2) + 1000 * j
+        splits = [n[j]] * 3  # camera-major blocks: camera r's rows go to rank r
+        outs = [n[r] for r in range(3)]
+        gdist._all_to_all_rows(radii, splits, outs)
+        gdist._all_to_all_rows(rows, splits, outs)
+        raise AssertionError("a recording render stops at its float exchange")
+
+    prev = gdist.EMULATION
+    gdist.EMULATION = emu
+    try:
+        for j in (1, 2):
+            emu.record(j, lambda: peer_render(j))
+        assert gdist.rank_world() == (0, 3)
+        rows0 = torch.arange(3 * n[0] * 2, dtype=torch.float32).view(3 * n[0], 2)
+        got = gdist._all_to_all_rows(rows0, [n[0]] * 3, n)
+        assert torch.equal(got[:4], rows0[:4])
+        for j in (1, 2):
+            want = torch.arange(3 * n[j] * 2, dtype=torch.float32).view(3 * n[j], 2)[:n[j]] + 1000 * j
+            assert torch.equal(got[sum(n[:j]):sum(n[:j + 1])], want)
+        r0 = gdist._all_to_all_rows(torch.zeros(3 * n[0], 1, dtype=torch.int32), [n[0]] * 3, n)
+        assert torch.equal(r0[4:8].flatten(), torch.arange(4, dtype=torch.int32) + 100)
+        grad = torch.randn(sum(n), 2)
+        back = gdist._all_to_all_rows(grad, n, [n[0]] * 3, backward=True)
+        assert torch.equal(back, grad[:4].repeat(3, 1))
+    finally:
+        gdist.EMULATION = prev
