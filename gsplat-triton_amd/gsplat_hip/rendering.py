@@ -34,7 +34,10 @@ from ._wrapper import (
 
 def _reshape_view(C: int, world_view: Tensor, N_world: list) -> Tensor:
     """[sum_i C*N_i, ...] blocks by source rank -> [C, sum_i N_i, ...]
-    (gsplat/rendering.py:260-267)."""
+    (gsplat/rendering.py:260-267).  One camera per rank: the blocks already
+    are the Gaussians in rank order, a view (no copy)."""
+    if C == 1:
+        return world_view.unsqueeze(0)
     view_list = [x.split(int(x.shape[0] / C), dim=0)
                  for x in world_view.split([C * N_i for N_i in N_world], dim=0)]
     return torch.stack([torch.cat(parts, dim=0) for parts in zip(*view_list)], dim=0)
@@ -249,6 +252,10 @@ def rasterization(
             camera_ids, gaussian_ids = gdist.all_to_all_tensor_list(
                 world_size, [camera_ids, gaussian_ids], cnts, output_splits=got)
             C = C_world[world_rank]
+        elif C_world[world_rank] == 1:  # one camera per rank: one field-major exchange
+            C = 1
+            radii, means2d, depths, conics, opacities, colors = gdist.exchange_pairs(
+                N_world, radii, means2d, depths, conics, opacities, colors)
         else:
             C = C_world[world_rank]
             splits = [C_i * N for C_i in C_world]

@@ -460,3 +460,62 @@ def test_refine_under_dp_keeps_replicas_identical_gloo(world, scale2d):
         mm = ref.moments()[k]
         np.testing.assert_allclose(mm[0].numpy(), a["m"][k][0], rtol=1e-6, atol=1e-9)
         np.testing.assert_allclose(mm[1].numpy(), a["m"][k][1], rtol=1e-6, atol=1e-12)
+
+
+def _pairs_worker(rank, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+        from gsplat_hip import distributed as gd
+        from gsplat_hip.rendering import _reshape_view
+        n_world = [3, 2]  # uneven shards
+        Nr = n_world[rank]
+        g = torch.Generator().manual_seed(rank)
+        radii = torch.randint(0, 50, (WORLD, Nr, 2), generator=g, dtype=torch.int32)
+        fields = [torch.randn(WORLD, Nr, *sh, generator=g).requires_grad_(True)
+                  for sh in ((2,), (), (3,), (), (3,))]
+        wts = [torch.randn(1, sum(n_world), *f.shape[2:], generator=torch.Generator()
+                           .manual_seed(10 + rank)) for f in fields]
+        # the one field-major exchange
+        out = gd.exchange_pairs(n_world, radii, *fields)
+        sum((o * w).sum() for o, w in zip(out[1:], wts)).backward()
+        fast = [out[0]] + [o.detach() for o in out[1:]]
+        gfast = [f.grad.clone() for f in fields]
+        for f in fields:
+            f.grad = None
+        # the generic path (rendering.py's C > 1 branch)
+        splits, outs = [Nr] * WORLD, n_world
+        (r2,) = gd.all_to_all_tensor_list(WORLD, [radii.flatten(0, 1)], splits=splits,
+                                          output_splits=outs)
+        parts = gd.all_to_all_tensor_list(WORLD, [f.flatten(0, 1) for f in fields],
+                                          splits=splits, output_splits=outs)
+        ref = [_reshape_view(1, r2, n_world)] + [_reshape_view(1, t, n_world) for t in parts]
+        sum((o * w).sum() for o, w in zip(ref[1:], wts)).backward()
+        ok = all(torch.equal(a, b.detach()) and a.is_contiguous() for a, b in zip(fast, ref))
+        okg = all(torch.allclose(a, f.grad) for a, f in zip(gfast, fields))
+        q.put((rank, (ok, okg, [tuple(t.shape) for t in fast])))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:  # surface worker failures to the test
+        q.put((rank, repr(e)))
+
+
+def test_exchange_pairs_matches_generic_exchange_gloo():
+    """distributed.exchange_pairs (one field-major exchange, one camera per
+    rank) gives the generic all_to_all_tensor_list + _reshape_view results,
+    contiguous, and the same gradients, on two gloo ranks with uneven shards."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pairs_worker, args=(r, port, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(WORLD))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(WORLD):
+        assert isinstance(res[r], tuple), res[r]
+        ok, okg, shapes = res[r]
+        assert ok and okg, (r, ok, okg)
+        assert shapes == [(1, 5, 2), (1, 5, 2), (1, 5), (1, 5, 3), (1, 5), (1, 5, 3)]
