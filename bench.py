@@ -442,6 +442,12 @@ def main():
                        "collectives executed (measurement only)" if args.dp_emulate else
                        " (the N>1 code path on a 1-rank RCCL group: sharded Adam, "
                        "early SH reduce-scatter)" if dp_path and world == 1 else ""),
+                   # bytes this rank sends to its peers per step (distributed.exchange_pairs:
+                   # 48 B per (Gaussian, peer camera) forward, 40 B of gradients back)
+                   "exchange_bytes_out_per_rank": (
+                       {"forward": 48 * tr.params["means"].shape[0] * (len(tr._n_world) - 1),
+                        "backward": 40 * tr.params["means"].shape[0] * (len(tr._n_world) - 1)}
+                       if gshard else None),
                    "n_isects_mean": float(np.mean(isects)), "n_eff_mean": float(np.mean(n_effs)),
                    "visible_per_camera": per_cam_visible,
                    "visible_union_8_cameras": union_visible,
