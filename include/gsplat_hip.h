@@ -285,9 +285,10 @@ int gsplat_hip_debug_set_lane_histogram(unsigned long long *device_buffer);
  * rasterization must run with the same setting. */
 int gsplat_hip_debug_set_chunk(int isects);
 /* Split mode of the 16x16 forward: tiles with more isects than the
- * threshold are rendered as parallel chunks (ABI 25: a launch of their own on
- * a second stream, concurrent with the other tiles' and joined back into the
- * caller's stream; which tiles split is decided per render on the device).
+ * threshold are rendered as parallel chunks (ABI 25: workgroups of the same
+ * forward launch, dispatched before the whole tiles; the chunks hand their
+ * transmittance products to later chunks; which tiles split is decided per
+ * render on the device).
  * isects > 0: that threshold; 0: off; < 0: adaptive, max(2048, n_isects /
  * GSPLAT_HIP_FWD_SPLIT_DIV) (the default, or GSPLAT_HIP_FWD_SPLIT).  Returns
  * the previous mode.  Results do not depend on it beyond the float rounding
