@@ -1,24 +1,23 @@
-// Wave-per-tile rasterizer for 16x16 tiles (the gsplat default), gfx950.
+// Rasterizer for 16x16 tiles (the gsplat default), gfx950.
 //
 // Same semantics as rasterize.hip (reference: rasterize_to_pixels_fwd.py:13-196,
 // rasterize_to_pixels_bwd.py:13-337), different mapping, built for CDNA4:
 //
-//  * one wave64 owns one 16x16 tile, every lane owns a 2x2 pixel quad, so the
-//    per-Gaussian LDS broadcast reads, culling and (backward) cross-lane
-//    reductions are amortised over 4 pixels and no workgroup barrier is
-//    needed (a workgroup is 4 independent waves = 4 tiles);
-//  * each batch of 64 isects is gathered one record per lane, culled against
-//    the tile with the exact rectangle minimum of the Gaussian's quadratic
-//    form (a record that cannot reach alpha >= 1/255 on any pixel centre of
-//    the tile is dropped -- the per-pixel test would skip it anyway), and
-//    compacted into LDS with ballot/mbcnt;
-//  * backward: the per-lane partial gradients (up to 16 fields) are combined
-//    across the 64 lanes with a reduce-scatter (permlane32/16 swaps, then DPP
-//    mirrors and quad permutes: 35 VALU ops for 16 sums instead of 16
-//    butterflies), after which 16 lanes issue ONE coalesced 64-B fp32 atomic
-//    into a packed [G][S] gradient row.  MI355X float atomics execute at the
-//    memory side (MI355X_MICROARCH.md "Global float atomics"), so one 64-B
-//    request per (Gaussian, tile) replaces 4 waves x 9 single-lane requests.
+//  * forward: a 256-thread workgroup per tile, each wave64 owns a 16x4 strip
+//    (one pixel per lane) and walks the tile's isects alone -- no workgroup
+//    barriers; heavy tiles may be split into chunks rendered by several
+//    workgroups of the same launch ("Split heavy tiles");
+//  * each batch of 64 isects is gathered one 64-B render record per lane,
+//    culled against the strip with the exact rectangle minimum of the
+//    Gaussian's quadratic form (a record that cannot reach alpha >= 1/255 on
+//    any pixel centre of the strip is dropped -- the per-pixel test would skip
+//    it anyway), and compacted into a per-wave LDS queue with ballot/mbcnt;
+//  * backward: work items of at most L isects of one tile (chunked at the
+//    forward's saved state), two waves of 16x8 pixels (two per lane); the
+//    per-lane partial gradients are combined across the 64 lanes with a
+//    reduce-scatter (permlane32/16 swaps, then DPP mirrors and quad permutes),
+//    the item's rows summed in LDS, and one float atomic per non-zero field of
+//    a (Gaussian, item) row goes into a packed [G][S] gradient row.
 #include "common.h"
 #include "wave_ops.h"
 #include "../../include/gsplat_hip.h"
@@ -120,6 +119,7 @@ struct Args {
   const int64_t *n_dev;  // the isect count on the device (capacity mode) or null
   const float *means2d, *conics, *colors, *opacities, *backgrounds;
   const float *records;  // [G][kRecFloats] render records, or null (gather the arrays)
+  uint32_t rec_bytes;    // bytes of the record table (< 2^31: buffer-load offsets)
   const uint8_t *masks;
   const int32_t *offsets, *flatten_ids;
   float *render_colors, *render_alphas;
@@ -238,18 +238,27 @@ struct Attr {
 
 // Unconditional (the caller clamps the isect index into the tile's range and
 // masks the lanes past it), so the loads stay in flight across the batch.
+// The record is read with buffer_load_dwordx4 (a raw buffer over the table,
+// a.rec_bytes long): as plain global loads the compiler merged them with the
+// four-array path's loads into one set of instructions with selected
+// addresses -- a dwordx2 and seven dword gathers per lane, each touching 64
+// lines (TCP_TOTAL_CACHE_ACCESSES 89 M per forward launch at M2).  Three
+// 16-B loads per lane do the same in a third of the L1 tag lookups.
 template <int D, class A>
 GS_INLINE void load_attr(const A &a, int32_t g, Attr<D> &at) {
   at.g = g;
   if constexpr (D <= kRecMaxD) {
     if (a.records) {  // wave-uniform
       constexpr int N4 = (6 + D + 3) / 4;
-      const float4 *r = reinterpret_cast<const float4 *>(a.records + (int64_t)g * kRecFloats);
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<float *>(a.records), (short)0, (int)a.rec_bytes, 0x00020000);
+      const uint32_t base = (uint32_t)g * (uint32_t)(kRecFloats * 4);
       float v[4 * N4];
 #pragma unroll
       for (int q = 0; q < N4; ++q) {
-        const float4 x = r[q];
-        v[4 * q] = x.x; v[4 * q + 1] = x.y; v[4 * q + 2] = x.z; v[4 * q + 3] = x.w;
+        const auto x = __builtin_amdgcn_raw_buffer_load_b128(rs, base + 16u * q, 0, 0);
+        v[4 * q] = __uint_as_float(x[0]); v[4 * q + 1] = __uint_as_float(x[1]);
+        v[4 * q + 2] = __uint_as_float(x[2]); v[4 * q + 3] = __uint_as_float(x[3]);
       }
       at.xy = make_float2(v[0], v[1]);
       at.con = make_float3(v[2], v[3], v[4]);
@@ -432,22 +441,24 @@ GS_INLINE void stage_bwd_pad(float4 *st, int slot) {
 // ahead, two more waves) measured 0.198 / 0.686 ms at M2 / M3 against 0.184 /
 // 0.590, depth 2 (three buffers) no better than 1.
 // ---- Split heavy tiles.  A tile with more isects than the threshold is
-// rendered as chunks of SL isects by separate workgroups of a launch of its
-// own (fwd_kernel<SPLIT>, on a second, high-priority stream concurrent with
-// the whole tiles' launch; a tile's chunks at increasing block indices).
-// Chunk k needs the transmittance entering it, the product of the earlier
-// chunks' (1 - alpha) products: every chunk but the last first computes its
-// own product (chunk_product) and publishes it per wave, then takes the
-// earlier chunks' products, composites from their product and publishes its
-// end T, last id and colour; the tile's last chunk to finish combines them
-// into the pixels.  Hand-offs (MI355X_MICROARCH.md "inter-workgroup
-// visibility"): every published word is stored sc1 (relaxed agent-scope
-// atomic store) and drained (s_waitcnt vmcnt(0)) before the flag store /
-// counter add, and every load of it is an sc1 load behind the matched poll or
-// the returned add.  A chunk waits only for chunks at lower block indices,
-// dispatched before it; the wait is bounded anyway -- on timeout the chunk
-// computes the missing product itself (same code, same value), so no
-// schedule can hang it.
+// rendered as chunks of SL isects by separate workgroups of the SAME forward
+// launch (fwd_kernel<SPLIT>): the chunks are workgroups 0 .. n_chunks - 1,
+// dispatched before the whole tiles that follow them, a tile's chunks at
+// increasing block indices.  Chunk k needs the transmittance entering it, the
+// product of the earlier chunks' (1 - alpha) products: every chunk but the
+// last first computes its own product (chunk_product) and publishes it per
+// wave, then takes the earlier chunks' products, composites from their product
+// and publishes its end T, last id and colour; the tile's last chunk to finish
+// combines them into the pixels.  Hand-offs (MI355X_MICROARCH.md
+// "inter-workgroup visibility", producer / consumer forms): every published
+// word is stored sc1 and drained (s_waitcnt vmcnt(0)); the producer then runs
+// an agent-scope release fence (drained again: the compiler may drop the wait
+// after buffer_wbl2) before its relaxed flag store or counter add; the
+// consumer polls relaxed, runs ONE agent-scope acquire fence after the match
+// (or after the counter add that made it last), and reads the words with sc1
+// loads.  A chunk waits only for chunks at lower block indices, dispatched
+// before it; the wait is bounded anyway -- on timeout the chunk computes the
+// missing product itself (same code, same value), so no schedule can hang it.
 GS_INLINE void store_sc1(float *p, float v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -455,11 +466,26 @@ GS_INLINE float load_sc1(const float *p) {
   return __hip_atomic_load(const_cast<float *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 GS_INLINE void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-constexpr int kSpinPolls = 2048;  // >= ~1 ms of polling before the fallback
+// producer side, after the published stores: drain, release, drain
+GS_INLINE void release_published() {
+  drain_stores();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  drain_stores();
+}
+// consumer side, after the poll matched / the counter add returned
+GS_INLINE void acquire_published() {
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  drain_stores();
+}
+// 2048 polls of s_sleep 8 (~0.2 us each) plus the load round trips: about
+// 0.4-1 ms of waiting before the fallback computes the product itself
+constexpr int kSpinPolls = 2048;
 GS_INLINE bool wait_flag(const int32_t *f) {
   for (int i = 0; i < kSpinPolls; ++i) {
-    if (__hip_atomic_load(const_cast<int32_t *>(f), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+    if (__hip_atomic_load(const_cast<int32_t *>(f), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+      acquire_published();
       return true;
+    }
     __builtin_amdgcn_s_sleep(8);
   }
   return false;
@@ -583,7 +609,7 @@ GS_INLINE void fwd_item(const Args &a, float4 *st, int item) {
       if (own) {
         const int64_t sl = end / a.L;
         store_sc1(a.prod + sl * (kTS * kTS) + pix_in_tile, Pp);
-        drain_stores();
+        release_published();
         if (lane == 0)
           __hip_atomic_store(a.pflag + 4 * sl + wv, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         own = false;
@@ -758,9 +784,12 @@ GS_INLINE void fwd_item(const Args &a, float4 *st, int item) {
     drain_stores();
     __syncthreads();
     __shared__ int s_last;
-    if (threadIdx.x == 0)
+    if (threadIdx.x == 0) {
+      release_published();
       s_last = __hip_atomic_fetch_add(a.ctr + (cid - kc), 1, __ATOMIC_RELAXED,
                                       __HIP_MEMORY_SCOPE_AGENT) == nch - 1;
+      if (s_last) acquire_published();
+    }
     __syncthreads();
     if (s_last && inside) {
       // the tile's last chunk to finish: per pixel the sum of the chunks'
@@ -1555,6 +1584,8 @@ int rasterize16_pack_records(int64_t G, int D, const float *means2d, const float
                              float *records, hipStream_t st) {
   GS_REQUIRE(rasterize16_record_floats(D) > 0, "rasterize_pack_records: %d channels > %d", D,
              r16::kRecMaxD);
+  GS_REQUIRE(G < ((int64_t)1 << 31) / (r16::kRecFloats * 4),
+             "rasterize_pack_records: %lld rows exceed the 2 GiB buffer-load range", (long long)G);
   if (G <= 0) return 0;
   const dim3 grid((unsigned)((G + 255) / 256));
   switch (D) {
@@ -1887,6 +1918,7 @@ int rasterize16_fwd(int C, int D, int W, int H, int tw, int th, const float *mea
   r16::Args a{};
   a.n_dev = n_isects_dev;
   a.records = rasterize16_record_floats(D) ? records : nullptr;
+  a.rec_bytes = 0x7fffffffu;  // rows < 2^31 / 64 (rasterize16_pack_records)
   a.C = C; a.W = W; a.H = H; a.tw = tw; a.th = th; a.n_tiles = C * tw * th;
   a.n_isects = n_isects;
   a.timeline = (g_timeline && g_timeline_waves >= 4 * (int64_t)a.n_tiles) ? g_timeline : nullptr;
@@ -1968,6 +2000,7 @@ int rasterize16_bwd(int C, int64_t G, int D, int W, int H, int tw, int th,
   r16::Args a{};
   a.n_dev = n_isects_dev;
   a.records = rasterize16_record_floats(D) ? records : nullptr;
+  a.rec_bytes = 0x7fffffffu;  // rows < 2^31 / 64 (rasterize16_pack_records)
   a.C = C; a.W = W; a.H = H; a.tw = tw; a.th = th; a.n_tiles = C * tw * th;
   a.n_isects = n_isects;
   a.timeline = (g_timeline && g_timeline_waves >= 4 * n_items_bound(a.n_tiles, n_isects))

@@ -891,6 +891,8 @@ def pack_render_records(means2d, conics, colors, opacities, tile_size, visible=N
     D = colors.shape[-1]
     rf = int(_lib.query("gsplat_hip_rasterize_record_floats", D, tile_size)) if RECORDS else 0
     G = opacities.numel()
+    if G * rf * 4 >= 2 ** 31:  # buffer-load offsets are 32-bit: gather the arrays instead
+        rf = 0
     records = torch.empty(G * rf if rf else 0, dtype=torch.float32, device=means2d.device)
     if rf:
         means2d, conics, colors, opacities = (_f32c(x) for x in (means2d, conics, colors,

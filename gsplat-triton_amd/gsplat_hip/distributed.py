@@ -224,6 +224,7 @@ class _ExchangePairs(torch.autograd.Function):
         r_out = outs[0].view(torch.int32).view(1, ntot, *radii.shape[2:])
         f_out = [o.view(1, ntot, *sh) for o, sh in zip(outs[1:], shapes)]
         ctx.n_world, ctx.Nr, ctx.shapes, ctx.widths = list(n_world), Nr, shapes, widths
+        ctx.dtype, ctx.device = fields[0].dtype, fields[0].device
         ctx.mark_non_differentiable(r_out)
         return (r_out, *f_out)
 
@@ -231,7 +232,11 @@ class _ExchangePairs(torch.autograd.Function):
     def backward(ctx, _g_radii, *grads):
         n_world, Nr, shapes, widths = ctx.n_world, ctx.Nr, ctx.shapes, ctx.widths
         W, ntot, tot = len(n_world), sum(n_world), sum(widths)
-        ref = next(g for g in grads if g is not None)
+        # a field without a gradient sends zeros; so does a loss that reaches
+        # none of them -- every rank must still join the reverse all_to_all
+        ref = next((g for g in grads if g is not None), None)
+        if ref is None:
+            ref = torch.zeros(0, dtype=ctx.dtype, device=ctx.device)
         # [field][source rank] runs of each gradient field, flat
         runs = [(g if g is not None else ref.new_zeros((1, ntot) + sh)).reshape(-1)
                 .split([n * w for n in n_world]) for g, sh, w in zip(grads, shapes, widths)]

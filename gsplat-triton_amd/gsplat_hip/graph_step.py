@@ -58,6 +58,36 @@ def graphable(tr) -> bool:
             and isinstance(tr.opt, FusedAdam) and torch.device(tr.device).type == "cuda")
 
 
+NODE_TYPES = ("kernel", "memcpy", "memset", "host", "graph", "empty", "wait_event",
+              "event_record")
+
+
+def graph_node_census(g):
+    """{node type: count} of a captured torch.cuda.CUDAGraph(keep_graph=True),
+    and the memset nodes as (address, bytes per row, rows, element size)."""
+    counts = (ctypes.c_int64 * 16)()
+    ms = (ctypes.c_int64 * (4 * 64))()
+    _lib.call("gsplat_hip_graph_node_census", ctypes.c_void_p(g.raw_cuda_graph()),
+              ctypes.addressof(counts), ctypes.addressof(ms), 64)
+    names = {(NODE_TYPES[t] if t < len(NODE_TYPES) else f"type{t}"): int(c)
+             for t, c in enumerate(counts) if c}
+    n_ms = min(names.get("memset", 0), 64)
+    return names, [tuple(int(x) for x in ms[4 * k:4 * k + 4]) for k in range(n_ms)]
+
+
+def check_kernel_nodes_only(g):
+    """The captured step must hold kernel (and empty) nodes only: its replays
+    faulted with the backward's hipMemsetAsync nodes in the graph (DESIGN
+    §3.12), so a memset / copy that slips into the captured region (a
+    torch.zeros, a .copy_) fails here, at capture time."""
+    names, memsets = graph_node_census(g)
+    other = {k: v for k, v in names.items() if k not in ("kernel", "empty")}
+    if other:
+        raise RuntimeError(f"captured training step holds non-kernel nodes {other}; memset "
+                           f"nodes (address, row bytes, rows, element size): {memsets}")
+    return names
+
+
 class _Mapped:
     """Host-mapped, coherent memory (gsplat_hip_host_mapped_alloc): `np` for
     the host, `dev` (a pointer) for kernels.  Never freed: a captured graph
@@ -187,7 +217,7 @@ class GraphStep:
                 self._body(deg)
             torch.cuda.current_stream(self.dev).wait_stream(s)
             self.graph = None
-            g = torch.cuda.CUDAGraph()
+            g = torch.cuda.CUDAGraph(keep_graph=True)
             # no garbage collection while capturing: a collected object that
             # owns a HIP resource (an earlier trainer's graph or event) would
             # free it with a call that is illegal during a capture -- a test
@@ -200,6 +230,8 @@ class GraphStep:
             finally:
                 if gc_on:
                     gc.enable()
+            self.census = check_kernel_nodes_only(g)
+            g.instantiate()
             self.graph = g
             self.status.zero_()
             self.seq.fill_(self.issued)  # the next replay fetches slot issued % RING
@@ -253,7 +285,9 @@ class GraphStep:
             self._capture(deg)
         self._check(block=len(self.pending) >= self.lag)
         self._issue(it)
-        return self.loss
+        # a copy: the graph's static output is overwritten by the next replay
+        # (eager Trainer.step returns a fresh tensor per step as well)
+        return self.loss.clone()
 
     def _issue(self, it):
         slot = self.issued % self.RING

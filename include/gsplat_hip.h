@@ -369,6 +369,13 @@ int gsplat_hip_activate_fwd_fetch(int64_t n_scales, int64_t n_opacities,
                                   float *opacities, const void *ring_device, int64_t slot_bytes,
                                   int n_ring, int64_t *seq_device, void *block_device,
                                   void *stream);
+/* Node census of a captured graph (ABI 26; host-side check of
+ * gsplat_hip/graph_step.py, not a reference function): `graph` is a
+ * hipGraph_t; counts[t] += the number of nodes of hipGraphNodeType t (t < 16,
+ * larger types in counts[15]); for the first max_memsets memset nodes,
+ * memsets[4k .. 4k+3] = (destination, bytes per row, rows, element size). */
+int gsplat_hip_graph_node_census(void *graph, int64_t *counts, int64_t *memsets,
+                                 int max_memsets);
 
 /* DefaultStrategy._update_state for packed=False (gsplat/strategy/default.py:
  * 213-262): for every (c, g) with radii[c,g] > 0, in camera order,

@@ -217,6 +217,22 @@ def test_graph_trainer_tracks_eager(capacity):
     torch.testing.assert_close(b[3], a[3], rtol=1e-3, atol=1e-7)
 
 
+def test_captured_step_holds_kernel_nodes_only():
+    """Every capture is checked (graph_step.check_kernel_nodes_only): the
+    replayed step holds kernel nodes, no memset / memcpy nodes (DESIGN
+    §3.12); the returned loss is a copy that later replays do not touch."""
+    from gsplat_hip.train_step import Trainer
+    means, rgbs, vm, K, W, H = _trainer_scene()
+    tr = Trainer(means, rgbs, vm, K, W, H, device=DEV, graph=True, max_steps=100)
+    l0 = tr.step(0)
+    v0 = float(l0)
+    tr.step(1)
+    tr.sync()
+    census = tr._graph.census
+    assert set(census) <= {"kernel", "empty"} and census["kernel"] > 20, census
+    assert float(l0) == v0
+
+
 def test_loss_target_index_is_exact():
     """l1_ssim_loss(gt_index=...): the target picked on the device from a
     stack gives the loss and gradient of that target passed directly."""
