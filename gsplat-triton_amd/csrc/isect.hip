@@ -25,6 +25,7 @@
 #include <rocprim/block/block_radix_sort.hpp>
 #include <rocprim/device/device_radix_sort.hpp>
 
+#include "isect_st.h"
 #include "lsd_sort.h"
 #include "wave_ops.h"
 
@@ -538,6 +539,9 @@ namespace {
 struct SortedLayout {
   size_t V, dkey, Vs, dkeys, blk, big, nbig, tkey, val, tkeys, vals, tmp, total;
   size_t tmp_bytes;
+  // supertile expansion (isect_st.h)
+  size_t rect, st_start, seg_start, seg_st, segcnt, tile_tot, offs;
+  int64_t segcap;
 };
 
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -561,8 +565,26 @@ SortedLayout sorted_layout(int64_t nV, int64_t n, int key_bits) {
   L.tmp = o;
   L.tmp_bytes = t1 > t2 ? t1 : t2;
   o = align256(o + L.tmp_bytes + 1);
+  L.segcap = n / st::kSeg + st::kMaxKeys + 1;
+  L.rect = o; o = align256(o + 8 * (size_t)nV);
+  L.st_start = o; o = align256(o + 4 * (size_t)(st::kMaxKeys + 1));
+  L.seg_start = o; o = align256(o + 4 * (size_t)(st::kMaxKeys + 1));
+  L.seg_st = o; o = align256(o + 4 * (size_t)L.segcap);
+  L.segcnt = o; o = align256(o + 4 * st::S * st::S * (size_t)L.segcap);
+  L.tile_tot = o; o = align256(o + 4 * (size_t)(st::kMaxTiles + 1));
+  L.offs = o; o = align256(o + 4 * (size_t)st::kMaxTiles);
   L.total = o;
   return L;
+}
+
+// The supertile expansion runs for at most kMaxKeys supertiles (with the
+// negative-depth one); GSPLAT_HIP_ISECT_ST=0 keeps the emission + tile sort.
+bool st_enabled(const st::Geo &g) {
+  static const bool on = [] {
+    const char *e = getenv("GSPLAT_HIP_ISECT_ST");
+    return !(e && atoi(e) == 0);
+  }();
+  return on && g.nst <= st::kMaxKeys;
 }
 }  // namespace
 
@@ -575,17 +597,27 @@ extern "C" int64_t gsplat_hip_isect_sorted_workspace_bytes(int64_t n_visible, in
 // count_workspace is the gsplat_hip_isect_count workspace (scanned block sums).
 // cnt_dev (capacity mode): the {n_isects, n_visible, overflow} state on the
 // device; n_visible / n_isects are then the capacities the grids are sized for.
+// offsets (may be null): the tile offsets too (gsplat_hip_isect_offsets'
+// output, C * tile_width * tile_height int32).
 static int isect_write_sorted_impl(
     int64_t n_gaussians, int N, const float *means2d, const int32_t *radii, const float *depths,
     const int32_t *camera_ids, const int32_t *tiles_per_gauss, int tile_size, int tile_width,
     int tile_height, int tile_bits, int cam_bits, const void *count_workspace, int64_t n_visible,
     int64_t n_isects, const int64_t *cnt_dev, void *workspace, int64_t workspace_bytes,
-    int64_t *isect_ids, int32_t *flatten_ids, hipStream_t st, CapCheck cc = CapCheck{}) {
+    int64_t *isect_ids, int32_t *flatten_ids, int32_t *offsets, int n_cameras, hipStream_t st,
+    CapCheck cc = CapCheck{}) {
   GS_REQUIRE(n_gaussians >= 0 && (camera_ids || N > 0 || n_gaussians == 0),
              "isect_write_sorted: N must be > 0 when camera_ids is null");
   GS_REQUIRE(tile_bits + cam_bits <= 32, "isect_write_sorted: tile_bits + cam_bits > 32");
   GS_REQUIRE(n_isects < ((int64_t)1 << 30), "isect_write_sorted: more than 2^30 isects");
-  if (n_isects <= 0 || n_visible <= 0) return 0;
+  GS_REQUIRE(!offsets || n_cameras > 0, "isect_write_sorted: offsets need n_cameras");
+  const int n_tiles = tile_width * tile_height;
+  auto plain_offsets = [&]() -> int {  // offsets from the written ids (or all zero)
+    if (!offsets) return 0;
+    return gsplat_hip_isect_offsets(cnt_dev ? n_isects : (n_visible > 0 ? n_isects : 0), cnt_dev,
+                                    isect_ids, n_cameras, tile_width, tile_height, offsets, st);
+  };
+  if (n_isects <= 0 || n_visible <= 0) return plain_offsets();
   const int key_bits = tile_bits + cam_bits;
   const SortedLayout L = sorted_layout(n_visible, n_isects, key_bits);
   GS_REQUIRE(workspace_bytes >= (int64_t)L.total, "isect_write_sorted: workspace %lld < %lld",
@@ -605,10 +637,49 @@ static int isect_write_sorted_impl(
   hipLaunchKernelGGL(isect_compact_kernel, dim3((unsigned)nbG), dim3(kIsectBlock), 0, st,
                      n_gaussians, tiles_per_gauss, depths, vis_prefix, V, dkey, cc);
   // stable depth sort of the visible Gaussians (32 key bits)
+  const uint32_t *dks = dkeys;
   if (lsd_sort_pairs(dkey, V, dkeys, Vs, n_visible, 0, 32, tmp, st, nullptr,
-                     cnt_dev ? cnt_dev + 1 : nullptr) == 0)
+                     cnt_dev ? cnt_dev + 1 : nullptr) == 0) {
     Vs = V;
+    dks = dkey;
+  }
   const int64_t nbV = (n_visible + kIsectBlock - 1) / kIsectBlock;
+  const st::Geo geo = st::make_geo(n_cameras > 0 ? n_cameras : 1, N, tile_width, tile_height,
+                                   tile_bits);
+  if (n_cameras > 0 && (int64_t)n_cameras * n_tiles <= st::kMaxTiles && st_enabled(geo)) {
+    // supertile expansion (isect_st.h): isects written once, offsets included
+    ushort4 *rect = reinterpret_cast<ushort4 *>(ws + L.rect);
+    int32_t *st_start = reinterpret_cast<int32_t *>(ws + L.st_start);
+    int32_t *seg_start = reinterpret_cast<int32_t *>(ws + L.seg_start);
+    int32_t *seg_st = reinterpret_cast<int32_t *>(ws + L.seg_st);
+    int32_t *segcnt = reinterpret_cast<int32_t *>(ws + L.segcnt);
+    int32_t *tile_tot = reinterpret_cast<int32_t *>(ws + L.tile_tot);
+    int32_t *offs = offsets ? offsets : reinterpret_cast<int32_t *>(ws + L.offs);
+    hipLaunchKernelGGL(st::rect_kernel, dim3((unsigned)nbV), dim3(256), 0, st, n_visible, cnt_dev,
+                       Vs, dks, means2d, radii, tile_size, geo, rect, blk);
+    hipLaunchKernelGGL(isect_scan_blocks_kernel, dim3(1), dim3(1024), 0, st, nbV, blk, nullptr,
+                       nullptr);
+    hipLaunchKernelGGL(st::emit_kernel, dim3((unsigned)nbV), dim3(256), 0, st, n_visible, cnt_dev,
+                       Vs, dks, rect, camera_ids, geo, blk, tkey, val);
+    int kb = 0;
+    while ((1 << kb) < geo.nst) ++kb;
+    // the pair count (<= n_isects) is the scan's total, blk[nbV]
+    const uint32_t *totals = lsd_one_pass(tkey, val, tkeys, vals, n_isects, kb < 1 ? 1 : kb, tmp,
+                                          st, blk + nbV);
+    const int n_tt = geo.C * geo.n_tiles + 1;
+    hipLaunchKernelGGL(st::plan_kernel, dim3(1), dim3(1024), 0, st, geo.nst, totals, st_start,
+                       seg_start, seg_st, n_tt, tile_tot);
+    const unsigned nseg = (unsigned)(n_isects / st::kSeg + geo.nst + 1);
+    hipLaunchKernelGGL(st::seg_count_kernel, dim3(nseg), dim3(256), 0, st, geo, st_start,
+                       seg_start, seg_st, vals, rect, Vs, tiles_per_gauss, segcnt, tile_tot);
+    hipLaunchKernelGGL(st::tile_scan_kernel, dim3(1), dim3(1024), 0, st, geo, cnt_dev, tile_tot,
+                       offs);
+    hipLaunchKernelGGL(st::seg_write_kernel, dim3(nseg), dim3(256), 0, st, geo, cnt_dev, st_start,
+                       seg_start, seg_st, vals, rect, Vs, dks, tiles_per_gauss, segcnt, tile_tot,
+                       isect_ids, flatten_ids);
+    GS_CHECK_LAUNCH("isect_write_sorted (supertiles)");
+    return 0;
+  }
   BigEmit *big_list = reinterpret_cast<BigEmit *>(ws + L.big);
   int32_t *n_big = reinterpret_cast<int32_t *>(ws + L.nbig);
   hipLaunchKernelGGL(isect_sorted_count_kernel, dim3((unsigned)nbV), dim3(kIsectBlock), 0, st,
@@ -632,7 +703,7 @@ static int isect_write_sorted_impl(
                        flatten_ids);
   }
   GS_CHECK_LAUNCH("isect_write_sorted");
-  return 0;
+  return plain_offsets();
 }
 
 extern "C" int gsplat_hip_isect_write_sorted(
@@ -640,12 +711,12 @@ extern "C" int gsplat_hip_isect_write_sorted(
     const int32_t *camera_ids, const int32_t *tiles_per_gauss, int tile_size, int tile_width,
     int tile_height, int tile_bits, int cam_bits, const void *count_workspace, int64_t n_visible,
     int64_t n_isects, void *workspace, int64_t workspace_bytes, int64_t *isect_ids,
-    int32_t *flatten_ids, void *stream) {
+    int32_t *flatten_ids, int n_cameras, int32_t *offsets, void *stream) {
   return isect_write_sorted_impl(n_gaussians, N, means2d, radii, depths, camera_ids,
                                  tiles_per_gauss, tile_size, tile_width, tile_height, tile_bits,
                                  cam_bits, count_workspace, n_visible, n_isects, nullptr,
-                                 workspace, workspace_bytes, isect_ids, flatten_ids,
-                                 (hipStream_t)stream);
+                                 workspace, workspace_bytes, isect_ids, flatten_ids, offsets,
+                                 n_cameras, (hipStream_t)stream);
 }
 
 extern "C" int64_t gsplat_hip_isect_sorted_capped_workspace_bytes(int64_t n_gaussians,
@@ -667,7 +738,7 @@ extern "C" int gsplat_hip_isect_write_sorted_capped(
     const int64_t *totals_device, int64_t capacity, int64_t *counts_device,
     int32_t *status_device, int64_t *counts_host_ring, const int64_t *slot_device,
     void *workspace, int64_t workspace_bytes, int64_t *isect_ids, int32_t *flatten_ids,
-    void *stream) {
+    int n_cameras, int32_t *offsets, void *stream) {
   GS_REQUIRE(capacity >= 0 && capacity < ((int64_t)1 << 30),
              "isect_write_sorted_capped: capacity %lld out of range", (long long)capacity);
   GS_REQUIRE(counts_device && totals_device, "isect_write_sorted_capped: null count buffers");
@@ -689,7 +760,8 @@ extern "C" int gsplat_hip_isect_write_sorted_capped(
   return isect_write_sorted_impl(n_gaussians, N, means2d, radii, depths, camera_ids,
                                  tiles_per_gauss, tile_size, tile_width, tile_height, tile_bits,
                                  cam_bits, count_workspace, n_gaussians, capacity, counts_device,
-                                 workspace, workspace_bytes - 256, isect_ids, flatten_ids, st, cc);
+                                 workspace, workspace_bytes - 256, isect_ids, flatten_ids, offsets,
+                                 n_cameras, st, cc);
 }
 
 // -------------------------------------------------------- tile-first path --

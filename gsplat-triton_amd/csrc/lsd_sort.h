@@ -328,4 +328,43 @@ inline int lsd_sort_pairs(uint32_t *k0, int32_t *v0, uint32_t *k1, int32_t *v1, 
   return cur;
 }
 
+// One stable pass over keys < 2^nbits (nbits <= 11) with a digit as wide as
+// the key (RX = 256 .. 2048 bins), (k0, v0) -> (k1, v1).  Returns the digit
+// totals (the scan's row sums, inside `scratch`).  Device count as above.
+inline const uint32_t *lsd_one_pass(const uint32_t *k0, const int32_t *v0, uint32_t *k1,
+                                    int32_t *v1, int64_t n, int nbits, void *scratch,
+                                    hipStream_t st, const int64_t *n_dev) {
+  const int ipt = lsd::pick_ipt(n);
+  const int64_t nt = lsd::n_tiles(n, ipt);
+  const int rx = nbits <= 8 ? 256 : nbits <= 9 ? 512 : nbits <= 10 ? 1024 : 2048;
+  uint32_t *hist = reinterpret_cast<uint32_t *>(scratch);
+  uint32_t *totals = hist + (int64_t)rx * nt;
+  if (n <= 0) return totals;
+  const uint32_t mask = (1u << nbits) - 1u;
+  const lsd::FinalOut none{nullptr, nullptr, nullptr};
+#define GS_LSD1(I, RX)                                                                            \
+  do {                                                                                            \
+    hipLaunchKernelGGL((lsd::hist_kernel<I, RX>), dim3((unsigned)nt), dim3(lsd::NT), 0, st, k0,   \
+                       n, n_dev, 0, mask, hist, nt);                                              \
+    hipLaunchKernelGGL(lsd::scan_kernel, dim3((unsigned)RX), dim3(lsd::NT), 0, st, hist, nt,      \
+                       totals, n_dev, n, (int64_t)lsd::NT * I);                                   \
+    hipLaunchKernelGGL((lsd::scatter_kernel<I, false, RX>), dim3((unsigned)nt), dim3(lsd::NT), 0, \
+                       st, k0, v0, k1, v1, n, n_dev, 0, nbits, hist, totals, nt, none);           \
+  } while (0)
+#define GS_LSD1_RX(RX) \
+  do {                 \
+    if (ipt == 4)      \
+      GS_LSD1(4, RX);  \
+    else               \
+      GS_LSD1(16, RX); \
+  } while (0)
+  if (rx == 256) GS_LSD1_RX(256);
+  else if (rx == 512) GS_LSD1_RX(512);
+  else if (rx == 1024) GS_LSD1_RX(1024);
+  else GS_LSD1_RX(2048);
+#undef GS_LSD1_RX
+#undef GS_LSD1
+  return totals;
+}
+
 }  // namespace gs

@@ -318,7 +318,7 @@ int rasterize16_bwd(int C, int64_t G, int D, int W, int H, int tw, int th,
                     const float *v_render_alphas, float *v_means2d, float *v_conics,
                     float *v_colors, float *v_opacities, float *v_abs, const float *render_colors,
                     const float *records, const void *state, int64_t state_bytes,
-                    void *workspace, hipStream_t st);
+                    void *workspace, const int32_t *visible, hipStream_t st);
 }  // namespace gs
 
 using namespace gs;
@@ -426,7 +426,7 @@ extern "C" int gsplat_hip_rasterize_bwd(
     const float *v_render_alphas, float *v_means2d, float *v_conics, float *v_colors,
     float *v_opacities, float *v_means2d_abs, const float *render_colors, const float *records,
     const void *state, int64_t state_bytes, void *workspace, int64_t workspace_bytes,
-    void *stream) {
+    const int32_t *visible, void *stream) {
   if (int e = check_common(C, D, width, height, tile_size, tile_width, tile_height)) return e;
   GS_REQUIRE(tile_size == 16 || !n_isects_device,
              "rasterize_bwd: a device isect count needs 16x16 tiles");
@@ -444,7 +444,7 @@ extern "C" int gsplat_hip_rasterize_bwd(
                            v_render_colors,
                            v_render_alphas, v_means2d, v_conics, v_colors, v_opacities,
                            v_means2d_abs, render_colors, records, state, state_bytes, workspace,
-                           st);
+                           visible, st);
   }
   GS_HIP(gs::zero_async(v_means2d, sizeof(float) * 2 * G, st));
   GS_HIP(gs::zero_async(v_conics, sizeof(float) * 3 * G, st));

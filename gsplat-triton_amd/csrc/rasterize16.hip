@@ -1298,14 +1298,28 @@ __attribute__((amdgpu_waves_per_eu(BwdOcc<PX>::W))) bwd2_kernel(Args a) {
   tl_store(a, t_start, lane);
 }
 
-// packed [G][S] -> the autograd tensors
+// packed [G][S] -> the autograd tensors.  visible (or null: every row):
+// rows of Gaussians without an isect received no atomic and were not zeroed
+// (zero_rows_kernel): their gradients are written as zeros, nothing read.
 template <int D, bool ABS>
 __global__ void __launch_bounds__(256)
 unpack_kernel(int64_t G, int S, const float *__restrict__ packed, float *__restrict__ v_means2d,
               float *__restrict__ v_conics, float *__restrict__ v_colors,
-              float *__restrict__ v_opacities, float *__restrict__ v_abs) {
+              float *__restrict__ v_opacities, float *__restrict__ v_abs,
+              const int32_t *__restrict__ visible) {
   const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= G) return;
+  if (visible && visible[g] <= 0) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) v_colors[g * D + d] = 0.f;
+    v_opacities[g] = 0.f;
+    *reinterpret_cast<float2 *>(v_means2d + 2 * g) = make_float2(0.f, 0.f);
+    v_conics[3 * g] = 0.f;
+    v_conics[3 * g + 1] = 0.f;
+    v_conics[3 * g + 2] = 0.f;
+    if (ABS) *reinterpret_cast<float2 *>(v_abs + 2 * g) = make_float2(0.f, 0.f);
+    return;
+  }
   const float *r = packed + g * S;
 #pragma unroll
   for (int d = 0; d < D; ++d) v_colors[g * D + d] = r[d];
@@ -1861,15 +1875,41 @@ static size_t packed_bytes(int D, bool absgrad, int64_t G) {
   return (((size_t)sizeof(float) * ((F + 15) / 16) * 16 * G + 255) / 256) * 256;
 }
 
+// Zero the gradient rows of the visible Gaussians only (visible[g] > 0: the
+// rows the backward's atomics can reach) -- a quarter of the [G][S] table at
+// M2 -- and the 256 bytes of item counters after the table.  One 16-B store
+// per thread, S / 4 threads per row.
+__global__ void __launch_bounds__(256)
+zero_rows_kernel(int64_t G, int S, const int32_t *__restrict__ visible, float *__restrict__ packed,
+                 int64_t tail_floats) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int q = S / 4;
+  const int64_t row = i / q;
+  if (row < G && visible[row] > 0)
+    reinterpret_cast<float4 *>(packed)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (blockIdx.x == 0 && threadIdx.x < tail_floats) packed[G * S + threadIdx.x] = 0.f;
+}
+
 template <int D, bool ABS>
 int r16_bwd(r16::Args a, int64_t G, float *v_means2d, float *v_conics, float *v_colors,
-            float *v_opacities, float *v_abs, void *workspace, hipStream_t st) {
+            float *v_opacities, float *v_abs, void *workspace, const int32_t *visible,
+            hipStream_t st) {
   constexpr int F = D + 6 + (ABS ? 2 : 0);
   a.S = ((F + 15) / 16) * 16;
   a.packed = reinterpret_cast<float *>(workspace);
   const bool chunked = a.n_isects > 0 && a.state && a.L > 0 && a.render_colors_in;
-  // one memset: the gradient rows and, right after them, the item counters
-  GS_HIP(gs::zero_async(a.packed, packed_bytes(D, ABS, G) + (chunked ? 256 : 0), st));
+  // the gradient rows and, right after them, the item counters
+  const size_t pb = packed_bytes(D, ABS, G);
+  if (visible && G > 0) {
+    const int64_t n4 = G * (a.S / 4);
+    // the counters start at byte pb (the table padded to 256 B): zero from
+    // the table's end through them
+    const int64_t tail = (int64_t)(pb / 4) - G * a.S + (chunked ? 64 : 0);
+    hipLaunchKernelGGL(zero_rows_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0,
+                       st, G, a.S, visible, a.packed, tail);
+  } else {
+    GS_HIP(gs::zero_async(a.packed, pb + (chunked ? 256 : 0), st));
+  }
   if (a.n_isects > 0) {
     int64_t grid = a.n_tiles;
     if (chunked) {
@@ -1903,7 +1943,8 @@ int r16_bwd(r16::Args a, int64_t G, float *v_means2d, float *v_conics, float *v_
   }
   if (G > 0) {
     hipLaunchKernelGGL((r16::unpack_kernel<D, ABS>), dim3((unsigned)((G + 255) / 256)), dim3(256),
-                       0, st, G, a.S, a.packed, v_means2d, v_conics, v_colors, v_opacities, v_abs);
+                       0, st, G, a.S, a.packed, v_means2d, v_conics, v_colors, v_opacities, v_abs,
+                       visible);
     GS_CHECK_LAUNCH("rasterize_bwd16_unpack");
   }
   return 0;
@@ -1996,7 +2037,7 @@ int rasterize16_bwd(int C, int64_t G, int D, int W, int H, int tw, int th,
                     const float *v_render_alphas, float *v_means2d, float *v_conics,
                     float *v_colors, float *v_opacities, float *v_abs, const float *render_colors,
                     const float *records, const void *state, int64_t state_bytes,
-                    void *workspace, hipStream_t st) {
+                    void *workspace, const int32_t *visible, hipStream_t st) {
   r16::Args a{};
   a.n_dev = n_isects_dev;
   a.records = rasterize16_record_floats(D) ? records : nullptr;
@@ -2021,9 +2062,9 @@ int rasterize16_bwd(int C, int64_t G, int D, int W, int H, int tw, int th,
 #define GS_R16B(DD)                                                                            \
   case DD:                                                                                     \
     return ab ? r16_bwd<DD, true>(a, G, v_means2d, v_conics, v_colors, v_opacities, v_abs,     \
-                                  workspace, st)                                               \
+                                  workspace, visible, st)                                      \
               : r16_bwd<DD, false>(a, G, v_means2d, v_conics, v_colors, v_opacities, v_abs,    \
-                                   workspace, st);
+                                   workspace, visible, st);
   switch (D) { GS_R16B(1) GS_R16B(2) GS_R16B(3) GS_R16B(4) GS_R16B(8) GS_R16B(16) GS_R16B(32) }
 #undef GS_R16B
   GS_REQUIRE(false, "rasterize16_bwd: unsupported channels %d", D);

@@ -12,7 +12,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GSPLAT_HIP_LIB", os.path.join(_HERE, "libgsplat_hip.so"))
-ABI_VERSION = 26
+ABI_VERSION = 27
 
 _p = ctypes.c_void_p
 _i32 = ctypes.c_int
@@ -38,12 +38,13 @@ _SIGS = {
                                       _p, _p, _p]),
     "gsplat_hip_isect_sorted_workspace_bytes": (_i64, [_i64, _i64, _i32]),
     "gsplat_hip_isect_write_sorted": (_i32, [_i64, _i32, _p, _p, _p, _p, _p, _i32, _i32, _i32,
-                                             _i32, _i32, _p, _i64, _i64, _p, _i64, _p, _p, _p]),
+                                             _i32, _i32, _p, _i64, _i64, _p, _i64, _p, _p, _i32,
+                                             _p, _p]),
     "gsplat_hip_isect_tilefirst_workspace_bytes": (_i64, [_i64, _i32, _i32]),
     "gsplat_hip_isect_sorted_capped_workspace_bytes": (_i64, [_i64, _i64, _i32]),
     "gsplat_hip_isect_write_sorted_capped": (_i32, [_i64, _i32, _p, _p, _p, _p, _p, _i32, _i32,
                                                     _i32, _i32, _i32, _p, _p, _i64, _p, _p, _p,
-                                                    _p, _p, _i64, _p, _p, _p]),
+                                                    _p, _p, _i64, _p, _p, _i32, _p, _p]),
     "gsplat_hip_host_mapped_alloc": (_i32, [_i64, _p, _p]),
     "gsplat_hip_host_mapped_free": (_i32, [_p]),
     "gsplat_hip_step_fetch": (_i32, [_p, _i64, _i32, _p, _p, _p]),
@@ -68,7 +69,7 @@ _SIGS = {
                                                         _i64]),
     "gsplat_hip_rasterize_bwd": (_i32, [_i32, _i64, _i32, _i32, _i32, _i32, _i32, _i32, _p, _p,
                                         _p, _p, _p, _p, _p, _i64, _p, _p, _p, _p, _p, _p, _p, _p,
-                                        _p, _p, _p, _p, _p, _p, _i64, _p, _i64, _p]),
+                                        _p, _p, _p, _p, _p, _p, _i64, _p, _i64, _p, _p]),
     "gsplat_hip_debug_set_timeline": (_i32, [_p, _i64]),
     "gsplat_hip_debug_set_lane_histogram": (_i32, [_p]),
     "gsplat_hip_debug_set_chunk": (_i32, [_i32]),

@@ -379,6 +379,7 @@ class _IsectCount:
         self.args = (means2d, radii, depths, camera_ids, C, N, G, tile_size, tile_width,
                      tile_height, n_bit_tile, n_bit_cam, packed)
         self.tpg = torch.empty(G, dtype=torch.int32, device=dev)
+        self.offsets = None  # the tile offsets, when the emission produced them
         self.ws = torch.empty(max(int(_lib.query("gsplat_hip_isect_workspace_bytes", G)), 8),
                               dtype=torch.uint8, device=dev)
         totals = torch.empty(2, dtype=torch.int64, device=dev)
@@ -432,10 +433,14 @@ class _IsectCount:
             sws = torch.empty(max(int(_lib.query("gsplat_hip_isect_sorted_workspace_bytes", n_visible,
                                                  n_isects, key_bits)), 8),
                               dtype=torch.uint8, device=dev)
+            # the tile offsets come with the isects (supertile expansion,
+            # csrc/isect_st.h): rasterization() reads them from `.offsets`
+            self.offsets = torch.empty((C, tile_height, tile_width), dtype=torch.int32,
+                                       device=dev)
             _lib.call("gsplat_hip_isect_write_sorted", G, N, _ptr(means2d), _ptr(radii),
                       _ptr(depths), _ptr(camera_ids), _ptr(tpg), tile_size, tile_width, tile_height,
                       n_bit_tile, n_bit_cam, _ptr(ws), n_visible, n_isects, _ptr(sws), sws.numel(),
-                      _ptr(isect_ids), _ptr(flatten_ids), st)
+                      _ptr(isect_ids), _ptr(flatten_ids), C, _ptr(self.offsets), st)
         else:
             _lib.call("gsplat_hip_isect_write", G, N, _ptr(means2d), _ptr(radii), _ptr(depths),
                       _ptr(camera_ids), tile_size, tile_width, tile_height, n_bit_tile, _ptr(ws),
@@ -476,6 +481,8 @@ class _IsectCount:
         isect_ids = torch.empty(capacity, dtype=torch.int64, device=dev)
         flatten_ids = torch.empty(capacity, dtype=torch.int32, device=dev)
         counts = torch.empty(4, dtype=torch.int64, device=dev)  # written by the emission
+        # the tile offsets too (as isect_offset_encode with _n_isects_device=counts)
+        self.offsets = torch.empty((C, tile_height, tile_width), dtype=torch.int32, device=dev)
         if status is not None:
             assert status.dtype == torch.int32 and status.is_cuda
         ring, slot = (None, None) if report is None else report
@@ -485,7 +492,7 @@ class _IsectCount:
                   _ptr(depths), _ptr(camera_ids), _ptr(self.tpg), tile_size, tile_width,
                   tile_height, n_bit_tile, n_bit_cam, _ptr(self.ws), _ptr(self.totals), capacity,
                   _ptr(counts), _ptr(status), ring, _ptr(slot), _ptr(ws), ws.numel(),
-                  _ptr(isect_ids), _ptr(flatten_ids), _stream())
+                  _ptr(isect_ids), _ptr(flatten_ids), C, _ptr(self.offsets), _stream())
         tpg = self.tpg if packed else self.tpg.view(C, N)
         return tpg, isect_ids, flatten_ids, counts
 
@@ -816,6 +823,10 @@ class _RasterizeToPixels(torch.autograd.Function):
                               flatten_ids, render_alphas, last_ids, render_colors, state, records)
         ctx.width, ctx.height, ctx.tile_size, ctx.absgrad = width, height, tile_size, absgrad
         ctx.n_dev = n_dev
+        # tiles_per_gauss: the backward zeroes / reads only those rows
+        ctx.visible = None if visible is None else visible.to(torch.int32).contiguous()
+        if ctx.visible is not None and ctx.visible.numel() != opacities.numel():
+            ctx.visible = None
         return render_colors, render_alphas
 
     @staticmethod
@@ -846,7 +857,7 @@ class _RasterizeToPixels(torch.autograd.Function):
                       _ptr(v_conics), _ptr(v_colors), _ptr(v_opacities), _ptr(v_abs),
                       _ptr(render_colors), _ptr(records) if records.numel() else 0,
                       _ptr(state) if state.numel() else 0, state.numel() * 4, _ptr(ws), wsb,
-                      _stream())
+                      _ptr(ctx.visible), _stream())
         if ctx.absgrad:
             ctx.means2d_in.absgrad = v_abs
         v_backgrounds = None

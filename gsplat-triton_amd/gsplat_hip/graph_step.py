@@ -31,8 +31,12 @@ What makes the step capturable:
   GPU, grows the capacity, re-captures and re-runs the void steps in order
   -- so the result is the eager step sequence's.
 
-Scope: the fused one-rank 3DGS trainer without a densification schedule
-(the bench's M2 configuration); anything else runs eagerly (Trainer.step).
+Scope: the fused one-rank 3DGS trainer (the bench's M2 and, with its
+DefaultStrategy schedule, M3 configurations): the steps between two refines
+are replays of one capture; a refine (eager, after its step's replay has
+been checked) replaces the parameter tensors, and the next step re-captures
+with an isect capacity grown in proportion to the Gaussians.  Anything else
+runs eagerly (Trainer.step).
 """
 
 import collections
@@ -51,10 +55,15 @@ from .strategy import activate, update_state_
 
 
 def graphable(tr) -> bool:
-    """Whether Trainer `tr` can run its steps as graph replays."""
+    """Whether Trainer `tr` can run its steps as graph replays.  With a
+    DefaultStrategy schedule the steps between refines are replays; the
+    refine / opacity reset run eagerly after their step (Trainer.step), and a
+    refine (new parameter tensors, Trainer._param_gen) re-captures."""
+    st = tr.strategy
     return (tr.fused and not tr.sharded and tr.world_size == 1 and tr.model == "3dgs"
             and not getattr(tr, "gshard", False)
-            and not getattr(tr, "defer_sh", False) and tr.strategy is None
+            and not getattr(tr, "defer_sh", False)
+            and (st is None or (not st.absgrad and tr.radii2d is None))
             and isinstance(tr.opt, FusedAdam) and torch.device(tr.device).type == "cuda")
 
 
@@ -111,7 +120,7 @@ class GraphStep:
     SLOT = 512  # bytes per input block
 
     def __init__(self, tr, capacity=None, headroom=1.25, lag=2):
-        assert graphable(tr), "GraphStep: a fused one-rank 3DGS trainer without densification"
+        assert graphable(tr), "GraphStep: a fused one-rank 3DGS trainer"
         self.tr = tr
         dev = torch.device(tr.device)
         self.dev = dev
@@ -157,7 +166,7 @@ class GraphStep:
         idx = [i for i in range(self.n_groups) if not (self.tr.sh_adam_in_bwd and i in sh)]
         return idx, 2 * len(idx)
 
-    def _body(self, deg):
+    def _body(self, deg, stats=True):
         tr = self.tr
         p = tr.params
         names = list(p)
@@ -186,7 +195,7 @@ class GraphStep:
         loss = tr._regularise(l1_ssim_loss(colors, tr.targets, tr.ssim_lambda, gt_index=self.cam))
         from . import losses as _losses
         torch.autograd.backward(loss, _losses.ONE_GRAD)
-        if "g" in grad_box:
+        if stats and "g" in grad_box:  # DefaultStrategy statistics (until refine_stop_iter)
             update_state_(tr.grad2d, tr.count, grad_box["g"], meta["radii"], meta["width"],
                           meta["height"], meta["n_cameras"], skip=self.status)
         skip = tr._sh_skip(fusion)
@@ -197,7 +206,7 @@ class GraphStep:
         tr.opt.zero_grad(set_to_none=True)
         return loss, meta["isect_counts"]
 
-    def _capture(self, deg):
+    def _capture(self, deg, stats=True):
         tr = self.tr
         from . import losses as _losses
         if _losses.ONE_GRAD is None or _losses.ONE_GRAD.device != self.dev:
@@ -214,7 +223,7 @@ class GraphStep:
             s = torch.cuda.Stream(device=self.dev)
             s.wait_stream(torch.cuda.current_stream(self.dev))
             with torch.cuda.stream(s):
-                self._body(deg)
+                self._body(deg, stats)
             torch.cuda.current_stream(self.dev).wait_stream(s)
             self.graph = None
             g = torch.cuda.CUDAGraph(keep_graph=True)
@@ -226,7 +235,7 @@ class GraphStep:
             gc.disable()
             try:
                 with torch.cuda.graph(g):
-                    self.loss, self.counts = self._body(deg)
+                    self.loss, self.counts = self._body(deg, stats)
             finally:
                 if gc_on:
                     gc.enable()
@@ -238,7 +247,7 @@ class GraphStep:
             torch.cuda.synchronize(self.dev)
         finally:
             _wrapper._timers = timers
-        self.key = (deg, tr.params["means"].shape[0], self.capacity)
+        self.key = self._key_of(deg, stats)
         self.recaptures += 1
 
     def _probe_capacity(self, deg):
@@ -276,13 +285,31 @@ class GraphStep:
         if tr.max_steps:
             tr._set_means_lr(lrs[0])
 
+    def _key_of(self, deg, stats):
+        """What a capture is valid for: SH degree, the parameter tensors
+        (their generation: a refine replaces them) and whether the step
+        accumulates the strategy statistics."""
+        tr = self.tr
+        return (deg, tr.params["means"].shape[0], getattr(tr, "_param_gen", 0), stats)
+
+    def _stats_at(self, it):
+        st = self.tr.strategy
+        return st is None or it < st.refine_stop_iter
+
     def step(self, it):
         tr = self.tr
         deg = tr.sh_degree_at(it)
-        key = (deg, tr.params["means"].shape[0], self.capacity)
-        if self.graph is None or key[:2] != self.key[:2]:
+        stats = self._stats_at(it)
+        key = self._key_of(deg, stats)
+        if self.graph is None or key != self.key:
             self._drain()
-            self._capture(deg)
+            if self.key is not None and key[1] != self.key[1] and self.capacity is not None:
+                # a refine changed the Gaussian count: grow the isect capacity
+                # in proportion (an overflow would void and re-run the step)
+                self.capacity = max(self.capacity,
+                                    int(math.ceil(self.capacity * key[1] / self.key[1])))
+            self.graph = None  # the old capture's pool holds the old tensors
+            self._capture(deg, stats)
         self._check(block=len(self.pending) >= self.lag)
         self._issue(it)
         # a copy: the graph's static output is overwritten by the next replay
@@ -334,7 +361,7 @@ class GraphStep:
         tr.opt.step_count -= len(redo)  # their Adam steps did not happen
         self.capacity = int(math.ceil(self.max_isects * self.headroom)) + 1
         self.status.zero_()
-        self._capture(tr.sh_degree_at(redo[0]))
+        self._capture(tr.sh_degree_at(redo[0]), self._stats_at(redo[0]))
         for it in redo:
             self._issue(it)
             self._check(block=True)

@@ -301,8 +301,10 @@ def rasterization(
         meta["isect_counts"] = counts
     else:
         tiles_per_gauss, isect_ids, flatten_ids = pending_isects.finish(sort=True)
-    isect_offsets = isect_offset_encode(isect_ids, C, tile_width, tile_height,
-                                        _n_isects_device=counts)
+    isect_offsets = pending_isects.offsets  # written with the sorted isects
+    if isect_offsets is None:
+        isect_offsets = isect_offset_encode(isect_ids, C, tile_width, tile_height,
+                                            _n_isects_device=counts)
     if late:
         _colors_ready()
         colors, backgrounds = add_depth(eval_colors(colors), backgrounds)
@@ -534,7 +536,9 @@ def rasterization_2dgs(
         colors = depths[..., None]
 
     tiles_per_gauss, isect_ids, flatten_ids = pending_isects.finish(sort=True)
-    isect_offsets = isect_offset_encode(isect_ids, C, tile_width, tile_height)
+    isect_offsets = pending_isects.offsets  # written with the sorted isects
+    if isect_offsets is None:
+        isect_offsets = isect_offset_encode(isect_ids, C, tile_width, tile_height)
 
     render_colors, render_alphas, render_normals, render_distort, render_median = \
         rasterize_to_pixels_2dgs(means2d, ray_transforms, colors, opacities, normals, densify,

@@ -271,9 +271,10 @@ class Trainer:
         self.last_meta = None
         self.refine_log = []  # (step, n_dupli, n_split, n_prune, N after)
         # graph=True: the step as HIP graph replays where the configuration
-        # allows (graph_step.graphable: fused one-rank 3DGS, no densification
-        # schedule); isect_capacity: its isect arrays' initial size (default:
-        # 1.25 x the first camera's count)
+        # allows (graph_step.graphable: fused one-rank 3DGS; with a
+        # DefaultStrategy schedule the refines run eagerly between replays);
+        # isect_capacity: its isect arrays' initial size (default: 1.25 x the
+        # first camera's count)
         self._graph = None
         if graph:
             from .graph_step import GraphStep, graphable
@@ -450,7 +451,10 @@ class Trainer:
 
     def step(self, it: int):
         if getattr(self, "_graph", None) is not None:
-            return self._graph.step(it)
+            loss = self._graph.step(it)
+            if self.strategy is not None:
+                self.post_step(it)  # eager refine / reset: drains the replays first
+            return loss
         ci = self.camera_index(it)
         self._sh_ready = 0
         fusion = self._make_fusion()
@@ -639,6 +643,7 @@ class Trainer:
         if self.radii2d is not None:
             self.radii2d = torch.zeros(n, device=self.device)
         self.refine_log.append((it,) + tuple(counts) + (n,))
+        self._param_gen = getattr(self, "_param_gen", 0) + 1  # a captured step re-captures
         if getattr(self, "gshard", False) and self.world_size > 1:  # each shard refined alone
             from .distributed import all_gather_int32
             self._n_world = all_gather_int32(self.world_size, n, device=self.device)

@@ -138,7 +138,15 @@ int gsplat_hip_isect_write_sorted(int64_t n_gaussians, int N, const float *means
                                   int tile_size, int tile_width, int tile_height, int tile_bits,
                                   int cam_bits, const void *count_workspace, int64_t n_visible,
                                   int64_t n_isects, void *workspace, int64_t workspace_bytes,
-                                  int64_t *isect_ids, int32_t *flatten_ids, void *stream);
+                                  int64_t *isect_ids, int32_t *flatten_ids, int n_cameras,
+                                  int32_t *offsets, void *stream);
+/* n_cameras / offsets (ABI 27): offsets (may be NULL) receives the tile
+ * offsets i32[n_cameras, tile_height, tile_width] as gsplat_hip_isect_offsets
+ * computes them from the written ids (isect_offset.py:8-33).  With them the
+ * isects are produced by the supertile expansion (csrc/isect_st.h: pairs of
+ * (4x4-tile supertile, Gaussian) in depth order, one stable pass over those,
+ * then every isect written once at its final slot; up to 2047 supertiles,
+ * GSPLAT_HIP_ISECT_ST=0 for the emission + tile sort) -- the same ids. */
 /* The same sorted emission with NO host sync (ABI 20; the reference reads
  * n_isects with .item(), isect_tiles.py:101-102): the totals stay on the
  * device (step 1's totals_device), isect_ids / flatten_ids have `capacity`
@@ -161,7 +169,7 @@ int gsplat_hip_isect_write_sorted_capped(
     const int64_t *totals_device, int64_t capacity, int64_t *counts_device,
     int32_t *status_device, int64_t *counts_host_ring, const int64_t *slot_device,
     void *workspace, int64_t workspace_bytes, int64_t *isect_ids, int32_t *flatten_ids,
-    void *stream);
+    int n_cameras, int32_t *offsets, void *stream);
 /* Sorted emission, tile-first (the default of isect_tiles(sort=True)): the
  * SAME isect_ids / flatten_ids again, from Gaussian-major emission with
  * 32-bit (camera, tile) keys, a stable sort by those keys, and a segmented
@@ -268,7 +276,11 @@ int gsplat_hip_rasterize_bwd(int C, int64_t n_gaussians, int D, int width, int h
                              float *v_opacities, float *v_means2d_abs,
                              const float *render_colors, const float *records,
                              const void *state, int64_t state_bytes, void *workspace,
-                             int64_t workspace_bytes, void *stream);
+                             int64_t workspace_bytes, const int32_t *visible, void *stream);
+/* visible (ABI 27, may be NULL): i32[G] with visible[g] > 0 for every
+ * Gaussian that has an isect (tiles_per_gauss); the 16x16 path then zeroes
+ * and reads back only those Gaussians' gradient rows (the others' gradients
+ * are written as zeros without reading anything). */
 
 /* Debug/profiling: when device_buffer (u64[2*capacity_waves]) is non-NULL, the
  * 16x16 rasterizer kernels store each wave's (start, end) s_memrealtime stamps

@@ -217,6 +217,38 @@ def test_graph_trainer_tracks_eager(capacity):
     torch.testing.assert_close(b[3], a[3], rtol=1e-3, atol=1e-7)
 
 
+def test_graph_trainer_refine_tracks_eager():
+    """A DefaultStrategy schedule (refines at steps 3 and 6, opacity resets at
+    0 and 7): the graph-replayed trainer re-captures after every refine (new
+    parameter tensors) and its sequence of updates -- the refines' counts
+    included -- follows the eager trainer's."""
+    from gsplat_hip.densify import DefaultStrategyConfig
+    from gsplat_hip.train_step import Trainer
+    means, rgbs, vm, K, W, H = _trainer_scene()
+    cfg = DefaultStrategyConfig(refine_start_iter=1, refine_every=3, reset_every=7)
+    out = {}
+    for graph in (False, True):
+        tr = Trainer(means, rgbs, vm, K, W, H, device=DEV, graph=graph, max_steps=100,
+                     strategy=cfg)
+        assert (tr._graph is not None) == graph
+        for it in range(9):
+            tr.step(it)
+        tr.sync()
+        out[graph] = ({k: p.detach().clone() for k, p in tr.params.items()},
+                      list(tr.refine_log), tr.opt.step_count, tr.grad2d.clone(),
+                      tr.count.clone())
+        if graph:
+            g = tr._graph
+            assert g.replays >= 9 and g.recaptures >= 3  # first capture + one per refine
+    a, b = out[False], out[True]
+    assert [r[0] for r in a[1]] == [3, 6] and a[1] == b[1], (a[1], b[1])
+    assert a[2] == b[2] == 9
+    for k in a[0]:
+        torch.testing.assert_close(b[0][k], a[0][k], rtol=1e-3, atol=1e-5)
+    torch.testing.assert_close(b[4], a[4], rtol=0, atol=0)
+    torch.testing.assert_close(b[3], a[3], rtol=1e-3, atol=1e-7)
+
+
 def test_captured_step_holds_kernel_nodes_only():
     """Every capture is checked (graph_step.check_kernel_nodes_only): the
     replayed step holds kernel nodes, no memset / memcpy nodes (DESIGN

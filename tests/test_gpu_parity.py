@@ -140,18 +140,35 @@ def isect_mode(request, monkeypatch):
     return request.param
 
 
+def _isect(m2, r, d, ts, tw, th):
+    """isect_tiles plus the tile offsets the sorted emission writes with the
+    isects (None for the strategies that do not)."""
+    from gsplat_hip import _wrapper
+    p = _wrapper.isect_tiles_begin(m2, r, d, ts, tw, th)
+    tpg, ids, fids = p.finish(sort=True)
+    return tpg, ids, fids, p.offsets
+
+
+def _check_offsets(off, ids, C, tw, th):
+    """Offsets written with the isects == isect_offset_encode of the ids."""
+    import gsplat_hip
+    if off is not None:
+        assert torch.equal(off, gsplat_hip.isect_offset_encode(ids, C, tw, th))
+
+
 @pytest.mark.parametrize("name", ["isect_garden_t16", "isect_garden_t4", "isect_pow2_c2"])
 def test_isect_bit_exact_vs_reference(name, isect_mode):
     import gsplat_hip
     g = load_golden(name)
     ts, tw, th, C = (int(g[k]) for k in ("tile_size", "tile_width", "tile_height", "C"))
-    tpg, ids, fids = gsplat_hip.isect_tiles(T(g["means2d"]), T(g["radii"]), T(g["depths"]),
-                                            ts, tw, th)
+    tpg, ids, fids, off_w = _isect(T(g["means2d"]), T(g["radii"]), T(g["depths"]), ts, tw, th)
     assert np.array_equal(tpg.cpu().numpy(), g["tiles_per_gauss"])
     assert np.array_equal(ids.cpu().numpy(), g["isect_ids"])
     assert np.array_equal(fids.cpu().numpy(), g["flatten_ids"])
     off = gsplat_hip.isect_offset_encode(ids, C, tw, th)
     assert np.array_equal(off.cpu().numpy(), g["isect_offsets"])
+    if off_w is not None:
+        assert np.array_equal(off_w.cpu().numpy(), g["isect_offsets"])
 
 
 def test_isect_edge_cases(isect_mode):
@@ -162,8 +179,9 @@ def test_isect_edge_cases(isect_mode):
         m2 = torch.zeros(C, N, 2, device=DEV)
         r = torch.zeros(C, N, dtype=torch.int32, device=DEV)
         d = torch.ones(C, N, device=DEV)
-        tpg, ids, fids = gsplat_hip.isect_tiles(m2, r, d, 16, 4, 3)
+        tpg, ids, fids, off_w = _isect(m2, r, d, 16, 4, 3)
         assert ids.numel() == 0 and fids.numel() == 0 and not tpg.any()
+        assert off_w is None or (off_w.shape == (C, 3, 4) and not off_w.any())
         off = gsplat_hip.isect_offset_encode(ids, C, 4, 3)
         assert off.shape == (C, 3, 4) and not off.any()
     ids = torch.tensor([(2 << 32) | 7], dtype=torch.int64, device=DEV)
@@ -182,11 +200,12 @@ def test_isect_random_vs_oracle_large_radii(isect_mode):
     r = rng.choice([0, 1, 2, 5, 17, 90, 300], (C, N)).astype(np.int32)
     d = rng.uniform(0.05, 50, (C, N)).astype(np.float32)
     d[0, :50] = d[0, 50:100]  # depth ties -> stability matters
-    tpg, ids, fids = gsplat_hip.isect_tiles(T(m2), T(r), T(d), ts, tw, th)
+    tpg, ids, fids, off_w = _isect(T(m2), T(r), T(d), ts, tw, th)
     otpg, oids, ofids = O.isect_tiles(m2, r, d, ts, tw, th)
     assert np.array_equal(tpg.cpu().numpy(), otpg)
     assert np.array_equal(ids.cpu().numpy(), oids)
     assert np.array_equal(fids.cpu().numpy(), ofids)
+    _check_offsets(off_w, ids, C, tw, th)
     off = gsplat_hip.isect_offset_encode(ids, C, tw, th)
     assert np.array_equal(off.cpu().numpy(), O.isect_offset_encode(oids, C, tw, th))
 
@@ -207,8 +226,9 @@ def test_isect_huge_gaussians_vs_oracle(isect_mode):
     r[:, huge] = rng.integers(300, 5000, (C, 150))
     d[:, huge] = rng.uniform(0.01, 0.02, (C, 150))  # nearest: adjacent after the depth sort
     d[0, huge[:10]] = -1.0
-    tpg, ids, fids = gsplat_hip.isect_tiles(T(m2), T(r), T(d), ts, tw, th)
+    tpg, ids, fids, off_w = _isect(T(m2), T(r), T(d), ts, tw, th)
     otpg, oids, ofids = O.isect_tiles(m2, r, d, ts, tw, th)
+    _check_offsets(off_w, ids, C, tw, th)
     assert int((otpg > 1024).sum()) >= 100
     assert np.array_equal(tpg.cpu().numpy(), otpg)
     assert np.array_equal(ids.cpu().numpy(), oids)
@@ -227,8 +247,9 @@ def test_isect_negative_and_tied_depths(isect_mode, C, tw, th):
     r = rng.choice([0, 3, 9, 30, 70], (C, N)).astype(np.int32)
     d = rng.choice(np.array([-2.5, -1e-3, -0.0, 0.0, 0.5, 0.5, 1.0, 3.0, 1e6], np.float32), (C, N))
     d = np.where(rng.random((C, N)) < 0.3, rng.uniform(-5, 5, (C, N)), d).astype(np.float32)
-    tpg, ids, fids = gsplat_hip.isect_tiles(T(m2), T(r), T(d), ts, tw, th)
+    tpg, ids, fids, off_w = _isect(T(m2), T(r), T(d), ts, tw, th)
     otpg, oids, ofids = O.isect_tiles(m2, r, d, ts, tw, th)
+    _check_offsets(off_w, ids, C, tw, th)
     assert np.array_equal(tpg.cpu().numpy(), otpg)
     assert np.array_equal(ids.cpu().numpy(), oids)
     assert np.array_equal(fids.cpu().numpy(), ofids)
