@@ -593,6 +593,8 @@ extern "C" int64_t gsplat_hip_isect_sorted_workspace_bytes(int64_t n_visible, in
   return (int64_t)sorted_layout(n_visible, n_isects, key_bits).total;
 }
 
+extern "C" int gsplat_hip_isect_ranked(int n_cameras, int tile_width, int tile_height);
+
 // Sorted isects without sorting 64-bit keys: see "Depth-first sorted emission".
 // count_workspace is the gsplat_hip_isect_count workspace (scanned block sums).
 // cnt_dev (capacity mode): the {n_isects, n_visible, overflow} state on the
@@ -605,12 +607,15 @@ static int isect_write_sorted_impl(
     int tile_height, int tile_bits, int cam_bits, const void *count_workspace, int64_t n_visible,
     int64_t n_isects, const int64_t *cnt_dev, void *workspace, int64_t workspace_bytes,
     int64_t *isect_ids, int32_t *flatten_ids, int32_t *offsets, int n_cameras, hipStream_t st,
-    CapCheck cc = CapCheck{}) {
+    CapCheck cc = CapCheck{}, int32_t *rank_ids = nullptr, int32_t *vis_rank = nullptr) {
   GS_REQUIRE(n_gaussians >= 0 && (camera_ids || N > 0 || n_gaussians == 0),
              "isect_write_sorted: N must be > 0 when camera_ids is null");
   GS_REQUIRE(tile_bits + cam_bits <= 32, "isect_write_sorted: tile_bits + cam_bits > 32");
   GS_REQUIRE(n_isects < ((int64_t)1 << 30), "isect_write_sorted: more than 2^30 isects");
   GS_REQUIRE(!offsets || n_cameras > 0, "isect_write_sorted: offsets need n_cameras");
+  GS_REQUIRE(!rank_ids == !vis_rank, "isect_write_sorted: rank_ids and vis_rank go together");
+  GS_REQUIRE(!rank_ids || gsplat_hip_isect_ranked(n_cameras, tile_width, tile_height),
+             "isect_write_sorted: rank ids need the supertile expansion");
   const int n_tiles = tile_width * tile_height;
   auto plain_offsets = [&]() -> int {  // offsets from the written ids (or all zero)
     if (!offsets) return 0;
@@ -646,7 +651,7 @@ static int isect_write_sorted_impl(
   const int64_t nbV = (n_visible + kIsectBlock - 1) / kIsectBlock;
   const st::Geo geo = st::make_geo(n_cameras > 0 ? n_cameras : 1, N, tile_width, tile_height,
                                    tile_bits);
-  if (n_cameras > 0 && (int64_t)n_cameras * n_tiles <= st::kMaxTiles && st_enabled(geo)) {
+  if (gsplat_hip_isect_ranked(n_cameras, tile_width, tile_height)) {
     // supertile expansion (isect_st.h): isects written once, offsets included
     ushort4 *rect = reinterpret_cast<ushort4 *>(ws + L.rect);
     int32_t *st_start = reinterpret_cast<int32_t *>(ws + L.st_start);
@@ -656,7 +661,7 @@ static int isect_write_sorted_impl(
     int32_t *tile_tot = reinterpret_cast<int32_t *>(ws + L.tile_tot);
     int32_t *offs = offsets ? offsets : reinterpret_cast<int32_t *>(ws + L.offs);
     hipLaunchKernelGGL(st::rect_kernel, dim3((unsigned)nbV), dim3(256), 0, st, n_visible, cnt_dev,
-                       Vs, dks, means2d, radii, tile_size, geo, rect, blk);
+                       Vs, dks, means2d, radii, tile_size, geo, rect, blk, vis_rank);
     hipLaunchKernelGGL(isect_scan_blocks_kernel, dim3(1), dim3(1024), 0, st, nbV, blk, nullptr,
                        nullptr);
     hipLaunchKernelGGL(st::emit_kernel, dim3((unsigned)nbV), dim3(256), 0, st, n_visible, cnt_dev,
@@ -676,7 +681,7 @@ static int isect_write_sorted_impl(
                        offs);
     hipLaunchKernelGGL(st::seg_write_kernel, dim3(nseg), dim3(256), 0, st, geo, cnt_dev, st_start,
                        seg_start, seg_st, vals, rect, Vs, dks, tiles_per_gauss, segcnt, tile_tot,
-                       isect_ids, flatten_ids);
+                       isect_ids, flatten_ids, rank_ids);
     GS_CHECK_LAUNCH("isect_write_sorted (supertiles)");
     return 0;
   }
@@ -711,12 +716,22 @@ extern "C" int gsplat_hip_isect_write_sorted(
     const int32_t *camera_ids, const int32_t *tiles_per_gauss, int tile_size, int tile_width,
     int tile_height, int tile_bits, int cam_bits, const void *count_workspace, int64_t n_visible,
     int64_t n_isects, void *workspace, int64_t workspace_bytes, int64_t *isect_ids,
-    int32_t *flatten_ids, int n_cameras, int32_t *offsets, void *stream) {
+    int32_t *flatten_ids, int n_cameras, int32_t *offsets, int32_t *rank_ids, int32_t *vis_rank,
+    void *stream) {
   return isect_write_sorted_impl(n_gaussians, N, means2d, radii, depths, camera_ids,
                                  tiles_per_gauss, tile_size, tile_width, tile_height, tile_bits,
                                  cam_bits, count_workspace, n_visible, n_isects, nullptr,
                                  workspace, workspace_bytes, isect_ids, flatten_ids, offsets,
-                                 n_cameras, (hipStream_t)stream);
+                                 n_cameras, (hipStream_t)stream, CapCheck{}, rank_ids, vis_rank);
+}
+
+// Whether gsplat_hip_isect_write_sorted(_capped) with these dimensions (and
+// offsets) runs the supertile expansion -- the path that can write rank ids.
+extern "C" int gsplat_hip_isect_ranked(int n_cameras, int tile_width, int tile_height) {
+  if (n_cameras <= 0 || tile_width <= 0 || tile_height <= 0) return 0;
+  const st::Geo geo = st::make_geo(n_cameras, 1, tile_width, tile_height, 0);
+  return ((int64_t)n_cameras * tile_width * tile_height <= st::kMaxTiles && st_enabled(geo)) ? 1
+                                                                                              : 0;
 }
 
 extern "C" int64_t gsplat_hip_isect_sorted_capped_workspace_bytes(int64_t n_gaussians,
@@ -738,7 +753,7 @@ extern "C" int gsplat_hip_isect_write_sorted_capped(
     const int64_t *totals_device, int64_t capacity, int64_t *counts_device,
     int32_t *status_device, int64_t *counts_host_ring, const int64_t *slot_device,
     void *workspace, int64_t workspace_bytes, int64_t *isect_ids, int32_t *flatten_ids,
-    int n_cameras, int32_t *offsets, void *stream) {
+    int n_cameras, int32_t *offsets, int32_t *rank_ids, int32_t *vis_rank, void *stream) {
   GS_REQUIRE(capacity >= 0 && capacity < ((int64_t)1 << 30),
              "isect_write_sorted_capped: capacity %lld out of range", (long long)capacity);
   GS_REQUIRE(counts_device && totals_device, "isect_write_sorted_capped: null count buffers");
@@ -761,7 +776,7 @@ extern "C" int gsplat_hip_isect_write_sorted_capped(
                                  tiles_per_gauss, tile_size, tile_width, tile_height, tile_bits,
                                  cam_bits, count_workspace, n_gaussians, capacity, counts_device,
                                  workspace, workspace_bytes - 256, isect_ids, flatten_ids, offsets,
-                                 n_cameras, st, cc);
+                                 n_cameras, st, cc, rank_ids, vis_rank);
 }
 
 // -------------------------------------------------------- tile-first path --

@@ -107,12 +107,17 @@ __global__ void __launch_bounds__(256)
 rect_kernel(int64_t nV, const int64_t *__restrict__ cap, const int32_t *__restrict__ Vs,
             const uint32_t *__restrict__ dkeys, const float *__restrict__ means2d,
             const int32_t *__restrict__ radii, int ts, Geo geo, ushort4 *__restrict__ rect,
-            int64_t *__restrict__ blk) {
+            int64_t *__restrict__ blk, int32_t *__restrict__ vis_rank) {
   __shared__ int64_t lds[5];
-  if (cap) nV = void_call(cap) ? 0 : min(nV, cap[1]);
+  // the ranks are written even when the call is void (an overflow): the
+  // rasterizer's record packing and gradient rows read them for every
+  // Gaussian with a tile
+  if (cap) nV = min(nV, cap[1]);
+  const bool vd = void_call(cap);
   const int64_t s = (int64_t)blockIdx.x * 256 + threadIdx.x;
   int np = 0;
-  if (s < nV) {
+  if (s < nV && vis_rank) vis_rank[Vs[s]] = (int32_t)s;
+  if (s < nV && !vd) {
     const int32_t g = Vs[s];
     const float2 p = *reinterpret_cast<const float2 *>(means2d + 2 * (int64_t)g);
     const float r = (float)radii[g], t = (float)ts;
@@ -349,44 +354,64 @@ seg_count_kernel(Geo geo, const int32_t *__restrict__ st_start, const int32_t *_
 }
 
 // (6) one workgroup: exclusive scan of the tile totals [0, T] in place (tile
-// T the virtual one); offsets[t] = tile_tot[t] for t < T (0 on a void call)
+// T the virtual one); offsets[t] = tile_tot[t] for t < T (0 on a void call).
+// Rounds of 8192 tiles staged through LDS: coalesced loads and stores, then
+// 8 contiguous tiles per thread.
 __global__ void __launch_bounds__(1024)
 tile_scan_kernel(Geo geo, const int64_t *__restrict__ cap, int32_t *__restrict__ tile_tot,
                  int32_t *__restrict__ offsets) {
+  constexpr int R = 8192, PT = R / 1024;
+  __shared__ int32_t buf[R];
   __shared__ int32_t wsum[16];
   const int T = geo.C * geo.n_tiles;
   const int nt = T + 1;
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
   const bool vd = void_call(cap);
-  constexpr int kPer = kMaxTiles / 1024 + 1;  // tiles per thread, at most
-  const int per = (nt + 1023) / 1024;
-  const int c0 = min(nt, t * per), c1 = min(nt, c0 + per);
-  int v[kPer];
-  int sum = 0;
+  int carry = 0;
+  for (int base = 0; base < nt; base += R) {
 #pragma unroll
-  for (int k = 0; k < kPer; ++k) {
-    v[k] = (k < per && c0 + k < c1) ? tile_tot[c0 + k] : 0;
-    sum += v[k];
-  }
-  int x = sum;
+    for (int k = 0; k < PT; ++k) {
+      const int i = base + k * 1024 + t;
+      buf[k * 1024 + t] = i < nt ? tile_tot[i] : 0;
+    }
+    __syncthreads();
+    int v[PT], sum = 0;
 #pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int y = __shfl_up(x, o, 64);
-    if (lane >= o) x += y;
-  }
-  if (lane == 63) wsum[wid] = x;
-  __syncthreads();
-  int run = x - sum;
+    for (int k = 0; k < PT; ++k) {
+      v[k] = buf[t * PT + k];
+      sum += v[k];
+    }
+    int x = sum;
 #pragma unroll
-  for (int w = 0; w < 16; ++w) run += w < wid ? wsum[w] : 0;
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(x, o, 64);
+      if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[wid] = x;
+    __syncthreads();
+    int run = carry + x - sum, all = carry;
 #pragma unroll
-  for (int k = 0; k < kPer; ++k) {
-    const int tile = c0 + k;
-    if (k < per && tile < c1) {
-      tile_tot[tile] = run;
-      if (tile < T) offsets[tile] = vd ? 0 : run;
+    for (int w = 0; w < 16; ++w) {
+      run += w < wid ? wsum[w] : 0;
+      all += wsum[w];
+    }
+#pragma unroll
+    for (int k = 0; k < PT; ++k) {
+      buf[t * PT + k] = run;
       run += v[k];
     }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < PT; ++k) {
+      const int i = base + k * 1024 + t;
+      if (i < nt) {
+        const int o = buf[k * 1024 + t];
+        tile_tot[i] = o;
+        if (i < T) offsets[i] = vd ? 0 : o;
+      }
+    }
+    carry = all;
+    __syncthreads();
   }
 }
 
@@ -399,7 +424,7 @@ seg_write_kernel(Geo geo, const int64_t *__restrict__ cap, const int32_t *__rest
                  const int32_t *__restrict__ Vs, const uint32_t *__restrict__ dkeys,
                  const int32_t *__restrict__ tpg, const int32_t *__restrict__ segcnt,
                  const int32_t *__restrict__ tile_off, int64_t *__restrict__ isect_ids,
-                 int32_t *__restrict__ flatten_ids) {
+                 int32_t *__restrict__ flatten_ids, int32_t *__restrict__ rank_ids) {
   __shared__ int32_t wc[4][S * S];
   __shared__ int32_t sbase[S * S];
   if (void_call(cap)) return;
@@ -450,6 +475,7 @@ seg_write_kernel(Geo geo, const int64_t *__restrict__ cap, const int32_t *__rest
       for (int k = 0; k < c; ++k) {
         isect_ids[pos + k] = id;
         flatten_ids[pos + k] = g[e];
+        if (rank_ids) rank_ids[pos + k] = wp.s[e];
       }
       cur[0] += __shfl(x, 63, 64);
     }
@@ -468,6 +494,7 @@ seg_write_kernel(Geo geo, const int64_t *__restrict__ cap, const int32_t *__rest
         const int tile = (sg.ty0 + t / S) * geo.tw + sg.tx0 + t % S;
         isect_ids[pos] = ((tkey0 | (int64_t)tile) << 32) | (int64_t)db[e];
         flatten_ids[pos] = g[e];
+        if (rank_ids) rank_ids[pos] = wp.s[e];
       }
       cur[t] += __popcll(bal);
     }

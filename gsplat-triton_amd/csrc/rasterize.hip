@@ -303,7 +303,7 @@ int rasterize16_fwd(int C, int D, int W, int H, int tw, int th, const float *mea
 int rasterize16_record_floats(int D);
 int rasterize16_pack_records(int64_t G, int D, const float *means2d, const float *conics,
                              const float *colors, const float *opacities, const int32_t *visible,
-                             float *records, hipStream_t st);
+                             const int32_t *vis_rank, float *records, hipStream_t st);
 int64_t rasterize16_fwd_state_bytes(int D, int n_tiles, int64_t n_isects);
 int rasterize16_prepare(int D, int n_tiles, const int32_t *offsets, int64_t n_isects,
                         const int64_t *n_isects_dev, void *state, int64_t state_bytes,
@@ -318,7 +318,8 @@ int rasterize16_bwd(int C, int64_t G, int D, int W, int H, int tw, int th,
                     const float *v_render_alphas, float *v_means2d, float *v_conics,
                     float *v_colors, float *v_opacities, float *v_abs, const float *render_colors,
                     const float *records, const void *state, int64_t state_bytes,
-                    void *workspace, const int32_t *visible, hipStream_t st);
+                    void *workspace, const int32_t *visible, const int32_t *vis_rank,
+                    hipStream_t st);
 }  // namespace gs
 
 using namespace gs;
@@ -359,9 +360,11 @@ extern "C" int gsplat_hip_rasterize_record_floats(int D, int tile_size) {
 extern "C" int gsplat_hip_rasterize_pack_records(int64_t n_gaussians, int D, const float *means2d,
                                                  const float *conics, const float *colors,
                                                  const float *opacities, const int32_t *visible,
-                                                 float *records, void *stream) {
+                                                 const int32_t *vis_rank, float *records,
+                                                 void *stream) {
+  GS_REQUIRE(!vis_rank || visible, "rasterize_pack_records: vis_rank needs visible");
   return rasterize16_pack_records(n_gaussians, D, means2d, conics, colors, opacities, visible,
-                                  records, (hipStream_t)stream);
+                                  vis_rank, records, (hipStream_t)stream);
 }
 
 static int check_common(int C, int D, int W, int H, int ts, int tw, int th) {
@@ -426,7 +429,7 @@ extern "C" int gsplat_hip_rasterize_bwd(
     const float *v_render_alphas, float *v_means2d, float *v_conics, float *v_colors,
     float *v_opacities, float *v_means2d_abs, const float *render_colors, const float *records,
     const void *state, int64_t state_bytes, void *workspace, int64_t workspace_bytes,
-    const int32_t *visible, void *stream) {
+    const int32_t *visible, const int32_t *vis_rank, void *stream) {
   if (int e = check_common(C, D, width, height, tile_size, tile_width, tile_height)) return e;
   GS_REQUIRE(tile_size == 16 || !n_isects_device,
              "rasterize_bwd: a device isect count needs 16x16 tiles");
@@ -444,7 +447,7 @@ extern "C" int gsplat_hip_rasterize_bwd(
                            v_render_colors,
                            v_render_alphas, v_means2d, v_conics, v_colors, v_opacities,
                            v_means2d_abs, render_colors, records, state, state_bytes, workspace,
-                           visible, st);
+                           visible, vis_rank, st);
   }
   GS_HIP(gs::zero_async(v_means2d, sizeof(float) * 2 * G, st));
   GS_HIP(gs::zero_async(v_conics, sizeof(float) * 3 * G, st));

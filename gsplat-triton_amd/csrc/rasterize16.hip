@@ -1306,7 +1306,7 @@ __global__ void __launch_bounds__(256)
 unpack_kernel(int64_t G, int S, const float *__restrict__ packed, float *__restrict__ v_means2d,
               float *__restrict__ v_conics, float *__restrict__ v_colors,
               float *__restrict__ v_opacities, float *__restrict__ v_abs,
-              const int32_t *__restrict__ visible) {
+              const int32_t *__restrict__ visible, const int32_t *__restrict__ vis_rank) {
   const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= G) return;
   if (visible && visible[g] <= 0) {
@@ -1320,7 +1320,7 @@ unpack_kernel(int64_t G, int S, const float *__restrict__ packed, float *__restr
     if (ABS) *reinterpret_cast<float2 *>(v_abs + 2 * g) = make_float2(0.f, 0.f);
     return;
   }
-  const float *r = packed + g * S;
+  const float *r = packed + (vis_rank ? min<int64_t>((uint32_t)vis_rank[g], G - 1) : g) * S;
 #pragma unroll
   for (int d = 0; d < D; ++d) v_colors[g * D + d] = r[d];
   v_opacities[g] = r[D];
@@ -1566,9 +1566,12 @@ template <int D>
 __global__ void __launch_bounds__(256)
 pack_records_kernel(int64_t G, const float *__restrict__ means2d, const float *__restrict__ conics,
                     const float *__restrict__ colors, const float *__restrict__ opacities,
-                    const int32_t *__restrict__ visible, float *__restrict__ records) {
+                    const int32_t *__restrict__ visible, const int32_t *__restrict__ vis_rank,
+                    float *__restrict__ records) {
   const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= G || (visible && visible[g] <= 0)) return;
+  // rank-indexed table: row = the Gaussian's depth rank among the visible
+  const int64_t row = vis_rank ? min<int64_t>((uint32_t)vis_rank[g], G - 1) : g;
   constexpr int N4 = (6 + D + 3) / 4;
   float r[4 * N4];
   const float2 xy = *reinterpret_cast<const float2 *>(means2d + 2 * g);
@@ -1582,7 +1585,7 @@ pack_records_kernel(int64_t G, const float *__restrict__ means2d, const float *_
   for (int d = 0; d < D; ++d) r[6 + d] = colors[g * D + d];
 #pragma unroll
   for (int d = 6 + D; d < 4 * N4; ++d) r[d] = 0.f;
-  float4 *o = reinterpret_cast<float4 *>(records + g * kRecFloats);
+  float4 *o = reinterpret_cast<float4 *>(records + row * kRecFloats);
 #pragma unroll
   for (int q = 0; q < N4; ++q) o[q] = make_float4(r[4 * q], r[4 * q + 1], r[4 * q + 2], r[4 * q + 3]);
 }
@@ -1595,7 +1598,7 @@ int rasterize16_record_floats(int D) {
 
 int rasterize16_pack_records(int64_t G, int D, const float *means2d, const float *conics,
                              const float *colors, const float *opacities, const int32_t *visible,
-                             float *records, hipStream_t st) {
+                             const int32_t *vis_rank, float *records, hipStream_t st) {
   GS_REQUIRE(rasterize16_record_floats(D) > 0, "rasterize_pack_records: %d channels > %d", D,
              r16::kRecMaxD);
   GS_REQUIRE(G < ((int64_t)1 << 31) / (r16::kRecFloats * 4),
@@ -1606,7 +1609,7 @@ int rasterize16_pack_records(int64_t G, int D, const float *means2d, const float
 #define GS_PACK(DD)                                                                              \
   case DD:                                                                                       \
     hipLaunchKernelGGL(r16::pack_records_kernel<DD>, grid, dim3(256), 0, st, G, means2d, conics, \
-                       colors, opacities, visible, records);                                    \
+                       colors, opacities, visible, vis_rank, records);                          \
     break;
     GS_PACK(1) GS_PACK(2) GS_PACK(3) GS_PACK(4) GS_PACK(5) GS_PACK(6) GS_PACK(7) GS_PACK(8)
     GS_PACK(9) GS_PACK(10)
@@ -1877,23 +1880,25 @@ static size_t packed_bytes(int D, bool absgrad, int64_t G) {
 
 // Zero the gradient rows of the visible Gaussians only (visible[g] > 0: the
 // rows the backward's atomics can reach) -- a quarter of the [G][S] table at
-// M2 -- and the 256 bytes of item counters after the table.  One 16-B store
-// per thread, S / 4 threads per row.
+// M2 -- and the 256 bytes of item counters after the table.  One lane per
+// row: one visibility load, S / 4 16-B stores.
 __global__ void __launch_bounds__(256)
-zero_rows_kernel(int64_t G, int S, const int32_t *__restrict__ visible, float *__restrict__ packed,
+zero_rows_kernel(int64_t G, int S, const int32_t *__restrict__ visible,
+                 const int32_t *__restrict__ vis_rank, float *__restrict__ packed,
                  int64_t tail_floats) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int q = S / 4;
-  const int64_t row = i / q;
-  if (row < G && visible[row] > 0)
-    reinterpret_cast<float4 *>(packed)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (g < G && visible[g] > 0) {
+    const int64_t row = vis_rank ? min<int64_t>((uint32_t)vis_rank[g], G - 1) : g;
+    float4 *r = reinterpret_cast<float4 *>(packed + row * S);
+    for (int q = 0; q < S / 4; ++q) r[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
   if (blockIdx.x == 0 && threadIdx.x < tail_floats) packed[G * S + threadIdx.x] = 0.f;
 }
 
 template <int D, bool ABS>
 int r16_bwd(r16::Args a, int64_t G, float *v_means2d, float *v_conics, float *v_colors,
             float *v_opacities, float *v_abs, void *workspace, const int32_t *visible,
-            hipStream_t st) {
+            const int32_t *vis_rank, hipStream_t st) {
   constexpr int F = D + 6 + (ABS ? 2 : 0);
   a.S = ((F + 15) / 16) * 16;
   a.packed = reinterpret_cast<float *>(workspace);
@@ -1901,12 +1906,11 @@ int r16_bwd(r16::Args a, int64_t G, float *v_means2d, float *v_conics, float *v_
   // the gradient rows and, right after them, the item counters
   const size_t pb = packed_bytes(D, ABS, G);
   if (visible && G > 0) {
-    const int64_t n4 = G * (a.S / 4);
     // the counters start at byte pb (the table padded to 256 B): zero from
     // the table's end through them
     const int64_t tail = (int64_t)(pb / 4) - G * a.S + (chunked ? 64 : 0);
-    hipLaunchKernelGGL(zero_rows_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0,
-                       st, G, a.S, visible, a.packed, tail);
+    hipLaunchKernelGGL(zero_rows_kernel, dim3((unsigned)((G + 255) / 256)), dim3(256), 0, st, G,
+                       a.S, visible, vis_rank, a.packed, tail);
   } else {
     GS_HIP(gs::zero_async(a.packed, pb + (chunked ? 256 : 0), st));
   }
@@ -1944,7 +1948,7 @@ int r16_bwd(r16::Args a, int64_t G, float *v_means2d, float *v_conics, float *v_
   if (G > 0) {
     hipLaunchKernelGGL((r16::unpack_kernel<D, ABS>), dim3((unsigned)((G + 255) / 256)), dim3(256),
                        0, st, G, a.S, a.packed, v_means2d, v_conics, v_colors, v_opacities, v_abs,
-                       visible);
+                       visible, vis_rank);
     GS_CHECK_LAUNCH("rasterize_bwd16_unpack");
   }
   return 0;
@@ -2037,7 +2041,9 @@ int rasterize16_bwd(int C, int64_t G, int D, int W, int H, int tw, int th,
                     const float *v_render_alphas, float *v_means2d, float *v_conics,
                     float *v_colors, float *v_opacities, float *v_abs, const float *render_colors,
                     const float *records, const void *state, int64_t state_bytes,
-                    void *workspace, const int32_t *visible, hipStream_t st) {
+                    void *workspace, const int32_t *visible, const int32_t *vis_rank,
+                    hipStream_t st) {
+  GS_REQUIRE(!vis_rank || visible, "rasterize_bwd: vis_rank needs visible");
   r16::Args a{};
   a.n_dev = n_isects_dev;
   a.records = rasterize16_record_floats(D) ? records : nullptr;
@@ -2062,9 +2068,9 @@ int rasterize16_bwd(int C, int64_t G, int D, int W, int H, int tw, int th,
 #define GS_R16B(DD)                                                                            \
   case DD:                                                                                     \
     return ab ? r16_bwd<DD, true>(a, G, v_means2d, v_conics, v_colors, v_opacities, v_abs,     \
-                                  workspace, visible, st)                                      \
+                                  workspace, visible, vis_rank, st)                            \
               : r16_bwd<DD, false>(a, G, v_means2d, v_conics, v_colors, v_opacities, v_abs,    \
-                                   workspace, visible, st);
+                                   workspace, visible, vis_rank, st);
   switch (D) { GS_R16B(1) GS_R16B(2) GS_R16B(3) GS_R16B(4) GS_R16B(8) GS_R16B(16) GS_R16B(32) }
 #undef GS_R16B
   GS_REQUIRE(false, "rasterize16_bwd: unsupported channels %d", D);

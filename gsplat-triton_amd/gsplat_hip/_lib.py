@@ -39,12 +39,13 @@ _SIGS = {
     "gsplat_hip_isect_sorted_workspace_bytes": (_i64, [_i64, _i64, _i32]),
     "gsplat_hip_isect_write_sorted": (_i32, [_i64, _i32, _p, _p, _p, _p, _p, _i32, _i32, _i32,
                                              _i32, _i32, _p, _i64, _i64, _p, _i64, _p, _p, _i32,
-                                             _p, _p]),
+                                             _p, _p, _p, _p]),
+    "gsplat_hip_isect_ranked": (_i32, [_i32, _i32, _i32]),
     "gsplat_hip_isect_tilefirst_workspace_bytes": (_i64, [_i64, _i32, _i32]),
     "gsplat_hip_isect_sorted_capped_workspace_bytes": (_i64, [_i64, _i64, _i32]),
     "gsplat_hip_isect_write_sorted_capped": (_i32, [_i64, _i32, _p, _p, _p, _p, _p, _i32, _i32,
                                                     _i32, _i32, _i32, _p, _p, _i64, _p, _p, _p,
-                                                    _p, _p, _i64, _p, _p, _i32, _p, _p]),
+                                                    _p, _p, _i64, _p, _p, _i32, _p, _p, _p, _p]),
     "gsplat_hip_host_mapped_alloc": (_i32, [_i64, _p, _p]),
     "gsplat_hip_host_mapped_free": (_i32, [_p]),
     "gsplat_hip_step_fetch": (_i32, [_p, _i64, _i32, _p, _p, _p]),
@@ -62,14 +63,14 @@ _SIGS = {
     "gsplat_hip_rasterize_prepare": (_i32, [_i32, _i32, _i32, _i32, _i32, _p, _i64, _p, _p, _i64,
                                             _p]),
     "gsplat_hip_rasterize_record_floats": (_i32, [_i32, _i32]),
-    "gsplat_hip_rasterize_pack_records": (_i32, [_i64, _i32, _p, _p, _p, _p, _p, _p, _p]),
+    "gsplat_hip_rasterize_pack_records": (_i32, [_i64, _i32, _p, _p, _p, _p, _p, _p, _p, _p]),
     "gsplat_hip_rasterize_fwd": (_i32, [_i32, _i32, _i32, _i32, _i32, _i32, _i32, _p, _p, _p, _p,
                                         _p, _p, _p, _i64, _p, _p, _p, _p, _p, _p, _p, _i64, _p]),
     "gsplat_hip_rasterize_bwd_workspace_bytes": (_i64, [_i64, _i32, _i32, _i32, _i32, _i32, _i32,
                                                         _i64]),
     "gsplat_hip_rasterize_bwd": (_i32, [_i32, _i64, _i32, _i32, _i32, _i32, _i32, _i32, _p, _p,
                                         _p, _p, _p, _p, _p, _i64, _p, _p, _p, _p, _p, _p, _p, _p,
-                                        _p, _p, _p, _p, _p, _p, _i64, _p, _i64, _p, _p]),
+                                        _p, _p, _p, _p, _p, _p, _i64, _p, _i64, _p, _p, _p]),
     "gsplat_hip_debug_set_timeline": (_i32, [_p, _i64]),
     "gsplat_hip_debug_set_lane_histogram": (_i32, [_p]),
     "gsplat_hip_debug_set_chunk": (_i32, [_i32]),

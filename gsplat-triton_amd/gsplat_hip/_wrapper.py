@@ -301,6 +301,10 @@ ISECT_SORT = os.environ.get("GSPLAT_HIP_ISECT_SORT", "depth_first")
 # 16x16 rasterizer gathers from packed 64-B render records (GSPLAT_HIP_RECORDS=0:
 # from the four attribute arrays, as before ABI 15)
 RECORDS = os.environ.get("GSPLAT_HIP_RECORDS", "1") != "0"
+# render records and gradient rows indexed by the Gaussians' depth rank among
+# the visible ones (isect supertile expansion's rank ids): the live rows are
+# the first n_visible, in depth order (GSPLAT_HIP_RANKS=0: indexed by Gaussian)
+RANKS = os.environ.get("GSPLAT_HIP_RANKS", "1") != "0"
 # longest busy-poll of the n_isects copy before a blocking event wait (s)
 SPIN_S = float(os.environ.get("GSPLAT_HIP_SYNC_SPIN_US", "2000")) * 1e-6
 
@@ -380,6 +384,8 @@ class _IsectCount:
                      tile_height, n_bit_tile, n_bit_cam, packed)
         self.tpg = torch.empty(G, dtype=torch.int32, device=dev)
         self.offsets = None  # the tile offsets, when the emission produced them
+        # (rank_ids [n_isects], vis_rank [G]) when the emission produced them
+        self.ranks = None
         self.ws = torch.empty(max(int(_lib.query("gsplat_hip_isect_workspace_bytes", G)), 8),
                               dtype=torch.uint8, device=dev)
         totals = torch.empty(2, dtype=torch.int64, device=dev)
@@ -400,7 +406,7 @@ class _IsectCount:
         self.event.record()
 
     @torch.no_grad()
-    def finish(self, sort: bool = True) -> Tuple[Tensor, Tensor, Tensor]:
+    def finish(self, sort: bool = True, ranks: bool = True) -> Tuple[Tensor, Tensor, Tensor]:
         (means2d, radii, depths, camera_ids, C, N, G, tile_size, tile_width, tile_height,
          n_bit_tile, n_bit_cam, packed) = self.args
         dev, st = means2d.device, _stream()
@@ -437,10 +443,13 @@ class _IsectCount:
             # csrc/isect_st.h): rasterization() reads them from `.offsets`
             self.offsets = torch.empty((C, tile_height, tile_width), dtype=torch.int32,
                                        device=dev)
+            rk = self._rank_buffers(n_isects) if ranks else None
             _lib.call("gsplat_hip_isect_write_sorted", G, N, _ptr(means2d), _ptr(radii),
                       _ptr(depths), _ptr(camera_ids), _ptr(tpg), tile_size, tile_width, tile_height,
                       n_bit_tile, n_bit_cam, _ptr(ws), n_visible, n_isects, _ptr(sws), sws.numel(),
-                      _ptr(isect_ids), _ptr(flatten_ids), C, _ptr(self.offsets), st)
+                      _ptr(isect_ids), _ptr(flatten_ids), C, _ptr(self.offsets),
+                      *(_ptr(t) for t in (rk or (None, None))), st)
+            self.ranks = rk
         else:
             _lib.call("gsplat_hip_isect_write", G, N, _ptr(means2d), _ptr(radii), _ptr(depths),
                       _ptr(camera_ids), tile_size, tile_width, tile_height, n_bit_tile, _ptr(ws),
@@ -457,6 +466,24 @@ class _IsectCount:
         if not packed:
             tpg = tpg.view(C, N)
         return tpg, isect_ids, flatten_ids
+
+    def will_rank(self, capped: bool = False) -> bool:
+        """Whether finish(sort=True) / finish_capped will also return the depth
+        ranks (`.ranks`): render records packed before then would be indexed
+        by Gaussian, not by rank."""
+        (_, _, _, _, C, _, _, _, tile_width, tile_height, _, _, packed) = self.args
+        return (RANKS and not packed and (capped or ISECT_SORT == "depth_first")
+                and bool(_lib.query("gsplat_hip_isect_ranked", C, tile_width, tile_height)))
+
+    def _rank_buffers(self, n_slots, capped=False):
+        """(rank_ids [n_slots], vis_rank [G]) when the sorted emission can write
+        the depth ranks (supertile expansion), else None."""
+        means2d, G = self.args[0], self.args[6]
+        if G == 0 or not self.will_rank(capped):
+            return None
+        dev = means2d.device
+        return (torch.empty(max(int(n_slots), 1), dtype=torch.int32, device=dev),
+                torch.empty(G, dtype=torch.int32, device=dev))
 
     @torch.no_grad()
     def finish_capped(self, capacity: int, status: Optional[Tensor] = None, report=None):
@@ -483,6 +510,7 @@ class _IsectCount:
         counts = torch.empty(4, dtype=torch.int64, device=dev)  # written by the emission
         # the tile offsets too (as isect_offset_encode with _n_isects_device=counts)
         self.offsets = torch.empty((C, tile_height, tile_width), dtype=torch.int32, device=dev)
+        rk = self._rank_buffers(capacity, capped=True)
         if status is not None:
             assert status.dtype == torch.int32 and status.is_cuda
         ring, slot = (None, None) if report is None else report
@@ -492,7 +520,9 @@ class _IsectCount:
                   _ptr(depths), _ptr(camera_ids), _ptr(self.tpg), tile_size, tile_width,
                   tile_height, n_bit_tile, n_bit_cam, _ptr(self.ws), _ptr(self.totals), capacity,
                   _ptr(counts), _ptr(status), ring, _ptr(slot), _ptr(ws), ws.numel(),
-                  _ptr(isect_ids), _ptr(flatten_ids), C, _ptr(self.offsets), _stream())
+                  _ptr(isect_ids), _ptr(flatten_ids), C, _ptr(self.offsets),
+                  *(_ptr(t) for t in (rk or (None, None))), _stream())
+        self.ranks = rk
         tpg = self.tpg if packed else self.tpg.view(C, N)
         return tpg, isect_ids, flatten_ids, counts
 
@@ -784,7 +814,7 @@ class _RasterizeToPixels(torch.autograd.Function):
     @staticmethod
     def forward(ctx, means2d, conics, colors, opacities, backgrounds, masks, width, height,
                 tile_size, isect_offsets, flatten_ids, absgrad, block_size=8, visible=None,
-                records=None, n_dev=None):
+                records=None, n_dev=None, ranks=None):
         ctx.means2d_in = means2d if absgrad else None  # receives .absgrad (_wrapper.py:156)
         ctx.set_materialize_grads(False)  # alphas without a loss: None, not zeros
         means2d, conics, colors, opacities, backgrounds = (
@@ -807,8 +837,15 @@ class _RasterizeToPixels(torch.autograd.Function):
         # one 64-B render record per Gaussian for the 16x16 kernels' gathers
         # (rasterization() may have packed them already, before its isect sync)
         if records is None:
-            records = pack_render_records(means2d, conics, colors, opacities, tile_size, visible)
+            records = pack_render_records(means2d, conics, colors, opacities, tile_size, visible,
+                                          ranks)
         rf = 1 if records.numel() else 0
+        # rank-indexed records (ranks = (rank_ids, vis_rank), packed by rank):
+        # the kernels walk the isects' ranks instead of their Gaussians
+        vis_rank = None
+        kernel_ids = flatten_ids
+        if ranks is not None and rf and visible is not None:
+            kernel_ids, vis_rank = ranks
         if sb:  # dispatch order into the state, outside the timed rasterizer launch
             _lib.call("gsplat_hip_rasterize_prepare", C, D, tile_size, tw, th, _ptr(isect_offsets),
                       flatten_ids.numel(), _ptr(n_dev), _ptr(state), sb, _stream())
@@ -816,11 +853,12 @@ class _RasterizeToPixels(torch.autograd.Function):
             _lib.call("gsplat_hip_rasterize_fwd", C, D, width, height, tile_size, tw, th,
                       _ptr(means2d), _ptr(conics), _ptr(colors), _ptr(opacities),
                       _ptr(backgrounds), _ptr(m), _ptr(isect_offsets), flatten_ids.numel(),
-                      _ptr(n_dev), _ptr(flatten_ids), _ptr(render_colors), _ptr(render_alphas),
+                      _ptr(n_dev), _ptr(kernel_ids), _ptr(render_colors), _ptr(render_alphas),
                       _ptr(last_ids), _ptr(records) if rf else 0, _ptr(state) if sb else 0, sb,
                       _stream())
         ctx.save_for_backward(means2d, conics, colors, opacities, backgrounds, m, isect_offsets,
-                              flatten_ids, render_alphas, last_ids, render_colors, state, records)
+                              kernel_ids, render_alphas, last_ids, render_colors, state, records,
+                              vis_rank)
         ctx.width, ctx.height, ctx.tile_size, ctx.absgrad = width, height, tile_size, absgrad
         ctx.n_dev = n_dev
         # tiles_per_gauss: the backward zeroes / reads only those rows
@@ -832,7 +870,7 @@ class _RasterizeToPixels(torch.autograd.Function):
     @staticmethod
     def backward(ctx, v_render_colors, v_render_alphas):
         (means2d, conics, colors, opacities, backgrounds, m, isect_offsets, flatten_ids,
-         render_alphas, last_ids, render_colors, state, records) = ctx.saved_tensors
+         render_alphas, last_ids, render_colors, state, records, vis_rank) = ctx.saved_tensors
         C, th, tw = isect_offsets.shape
         D = colors.shape[-1]
         G = opacities.numel()
@@ -857,14 +895,15 @@ class _RasterizeToPixels(torch.autograd.Function):
                       _ptr(v_conics), _ptr(v_colors), _ptr(v_opacities), _ptr(v_abs),
                       _ptr(render_colors), _ptr(records) if records.numel() else 0,
                       _ptr(state) if state.numel() else 0, state.numel() * 4, _ptr(ws), wsb,
-                      _ptr(ctx.visible), _stream())
+                      _ptr(ctx.visible), _ptr(vis_rank if ctx.visible is not None else None),
+                      _stream())
         if ctx.absgrad:
             ctx.means2d_in.absgrad = v_abs
         v_backgrounds = None
         if ctx.needs_input_grad[4]:
             v_backgrounds = (v_render_colors * (1.0 - render_alphas)).sum(dim=(1, 2))
         return (v_means2d, v_conics, v_colors, v_opacities, v_backgrounds,
-                None, None, None, None, None, None, None, None, None, None, None)
+                None, None, None, None, None, None, None, None, None, None, None, None)
 
 
 def rasterize_to_pixels(
@@ -894,11 +933,14 @@ def rasterize_to_pixels(
 
 
 @torch.no_grad()
-def pack_render_records(means2d, conics, colors, opacities, tile_size, visible=None) -> Tensor:
+def pack_render_records(means2d, conics, colors, opacities, tile_size, visible=None,
+                        ranks=None) -> Tensor:
     """The 16x16 rasterizer's render records (gsplat_hip_rasterize_pack_records):
     one 64-B row [x, y, conic, opacity, colour] per Gaussian, only the rows
     whose `visible` count (tiles_per_gauss) is > 0 written.  Empty when the
-    configuration has no record path (then the kernels gather the arrays)."""
+    configuration has no record path (then the kernels gather the arrays).
+    `ranks` = (rank_ids, vis_rank) of the sorted emission (with `visible`):
+    the row of Gaussian g is vis_rank[g]."""
     D = colors.shape[-1]
     rf = int(_lib.query("gsplat_hip_rasterize_record_floats", D, tile_size)) if RECORDS else 0
     G = opacities.numel()
@@ -910,15 +952,16 @@ def pack_render_records(means2d, conics, colors, opacities, tile_size, visible=N
                                                                  opacities))
         vis = None if visible is None else visible.to(torch.int32).contiguous()
         assert vis is None or vis.numel() == G, (vis.shape, G)
+        vr = ranks[1] if (ranks is not None and vis is not None) else None
         _lib.call("gsplat_hip_rasterize_pack_records", G, D, _ptr(means2d), _ptr(conics),
-                  _ptr(colors), _ptr(opacities), _ptr(vis), _ptr(records), _stream())
+                  _ptr(colors), _ptr(opacities), _ptr(vis), _ptr(vr), _ptr(records), _stream())
     return records
 
 
 def _rasterize_to_pixels(means2d, conics, colors, opacities, image_width, image_height, tile_size,
                          isect_offsets, flatten_ids, backgrounds=None, masks=None, packed=False,
                          absgrad=False, block_size=8, visible=None, records=None,
-                         n_isects_device=None):
+                         n_isects_device=None, ranks=None):
     """rasterize_to_pixels with rasterization()'s private hints: `visible`
     ([C,N] tiles_per_gauss: only those Gaussians' render records are packed)
     and `records` (already packed by pack_render_records for these exact
@@ -965,7 +1008,7 @@ def _rasterize_to_pixels(means2d, conics, colors, opacities, image_width, image_
                                           image_width, image_height, tile_size, isect_offsets,
                                           flatten_ids, absgrad, block_size, visible,
                                           records if Dp == D and cols is colors else None,
-                                          n_isects_device)
+                                          n_isects_device, ranks)
         return (rc[..., :D] if Dp != D else rc), ra
 
     if channels <= 32:

@@ -286,11 +286,12 @@ def rasterization(
         return colors, backgrounds
 
     records = None
+    ranked = pending_isects.will_rank(capped)
     if not late:
         colors, backgrounds = add_depth(colors, backgrounds)
-        if colors.shape[-1] <= channel_chunk:
+        if colors.shape[-1] <= channel_chunk and not ranked:
             # queued before the isect sync, so the GPU has it to run while the
-            # host waits for n_isects
+            # host waits for n_isects (rank-indexed records wait for the ranks)
             records = pack_render_records(means2d, conics, colors, opacities, tile_size,
                                           None if packed else pending_isects.tpg)
 
@@ -305,12 +306,13 @@ def rasterization(
     if isect_offsets is None:
         isect_offsets = isect_offset_encode(isect_ids, C, tile_width, tile_height,
                                             _n_isects_device=counts)
+    ranks = pending_isects.ranks
     if late:
         _colors_ready()
         colors, backgrounds = add_depth(eval_colors(colors), backgrounds)
-        if colors.shape[-1] <= channel_chunk:
-            records = pack_render_records(means2d, conics, colors, opacities, tile_size,
-                                          tiles_per_gauss)
+    if (late or ranks is not None) and colors.shape[-1] <= channel_chunk:
+        records = pack_render_records(means2d, conics, colors, opacities, tile_size,
+                                      tiles_per_gauss, ranks)
     meta.update({"tile_width": tile_width, "tile_height": tile_height,
                  "tiles_per_gauss": tiles_per_gauss, "isect_ids": isect_ids,
                  "flatten_ids": flatten_ids, "isect_offsets": isect_offsets, "width": width,
@@ -327,7 +329,8 @@ def rasterization(
                 means2d, conics, colors[..., sl], opacities, width, height, tile_size,
                 isect_offsets, flatten_ids,
                 backgrounds=None if backgrounds is None else backgrounds[..., sl],
-                packed=packed, absgrad=absgrad, visible=visible, n_isects_device=counts)
+                packed=packed, absgrad=absgrad, visible=visible, n_isects_device=counts,
+                ranks=ranks)
             render_colors.append(rc)
             render_alphas.append(ra)
         render_colors = torch.cat(render_colors, dim=-1)
@@ -336,7 +339,7 @@ def rasterization(
         render_colors, render_alphas = _rasterize_to_pixels(
             means2d, conics, colors, opacities, width, height, tile_size, isect_offsets,
             flatten_ids, backgrounds=backgrounds, packed=packed, absgrad=absgrad, visible=visible,
-            records=records, n_isects_device=counts)
+            records=records, n_isects_device=counts, ranks=ranks)
     if render_mode in ["ED", "RGB+ED"]:
         render_colors = torch.cat(
             [render_colors[..., :-1],
@@ -535,7 +538,8 @@ def rasterization_2dgs(
     elif render_mode in ["D", "ED"]:
         colors = depths[..., None]
 
-    tiles_per_gauss, isect_ids, flatten_ids = pending_isects.finish(sort=True)
+    # (the 2DGS rasterizer gathers its own arrays: no rank ids)
+    tiles_per_gauss, isect_ids, flatten_ids = pending_isects.finish(sort=True, ranks=False)
     isect_offsets = pending_isects.offsets  # written with the sorted isects
     if isect_offsets is None:
         isect_offsets = isect_offset_encode(isect_ids, C, tile_width, tile_height)

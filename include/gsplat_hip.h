@@ -139,7 +139,8 @@ int gsplat_hip_isect_write_sorted(int64_t n_gaussians, int N, const float *means
                                   int cam_bits, const void *count_workspace, int64_t n_visible,
                                   int64_t n_isects, void *workspace, int64_t workspace_bytes,
                                   int64_t *isect_ids, int32_t *flatten_ids, int n_cameras,
-                                  int32_t *offsets, void *stream);
+                                  int32_t *offsets, int32_t *rank_ids, int32_t *vis_rank,
+                                  void *stream);
 /* n_cameras / offsets (ABI 27): offsets (may be NULL) receives the tile
  * offsets i32[n_cameras, tile_height, tile_width] as gsplat_hip_isect_offsets
  * computes them from the written ids (isect_offset.py:8-33).  With them the
@@ -169,7 +170,14 @@ int gsplat_hip_isect_write_sorted_capped(
     const int64_t *totals_device, int64_t capacity, int64_t *counts_device,
     int32_t *status_device, int64_t *counts_host_ring, const int64_t *slot_device,
     void *workspace, int64_t workspace_bytes, int64_t *isect_ids, int32_t *flatten_ids,
-    int n_cameras, int32_t *offsets, void *stream);
+    int n_cameras, int32_t *offsets, int32_t *rank_ids, int32_t *vis_rank, void *stream);
+/* rank_ids / vis_rank (ABI 27, both NULL or both set; only when
+ * gsplat_hip_isect_ranked says the supertile expansion runs): rank_ids
+ * i32[n_isects] = the depth rank of each isect's Gaussian among the visible
+ * Gaussians (flatten_ids[i] is the Gaussian itself), vis_rank i32[G] = that
+ * rank for every Gaussian with tiles_per_gauss > 0 (other entries untouched):
+ * the render records and gradient rows can then be indexed by rank. */
+int gsplat_hip_isect_ranked(int n_cameras, int tile_width, int tile_height);
 /* Sorted emission, tile-first (the default of isect_tiles(sort=True)): the
  * SAME isect_ids / flatten_ids again, from Gaussian-major emission with
  * 32-bit (camera, tile) keys, a stable sort by those keys, and a segmented
@@ -240,7 +248,13 @@ int gsplat_hip_rasterize_record_floats(int D, int tile_size);
 int gsplat_hip_rasterize_pack_records(int64_t n_gaussians, int D, const float *means2d,
                                       const float *conics, const float *colors,
                                       const float *opacities, const int32_t *visible,
-                                      float *records, void *stream);
+                                      const int32_t *vis_rank, float *records, void *stream);
+/* vis_rank (ABI 27, may be NULL; needs visible): rank-indexed records -- the
+ * row of Gaussian g is vis_rank[g] (its depth rank among the visible ones,
+ * gsplat_hip_isect_write_sorted's vis_rank), so the live rows are the first
+ * n_visible, in depth order.  The rasterizer then takes the isects' ranks
+ * (rank_ids) in place of flatten_ids, and the backward (same vis_rank) sums
+ * its gradient rows by rank and unpacks them to the Gaussians. */
 int gsplat_hip_rasterize_fwd(int C, int D, int width, int height, int tile_size, int tile_width,
                              int tile_height, const float *means2d, const float *conics,
                              const float *colors, const float *opacities,
@@ -276,7 +290,8 @@ int gsplat_hip_rasterize_bwd(int C, int64_t n_gaussians, int D, int width, int h
                              float *v_opacities, float *v_means2d_abs,
                              const float *render_colors, const float *records,
                              const void *state, int64_t state_bytes, void *workspace,
-                             int64_t workspace_bytes, const int32_t *visible, void *stream);
+                             int64_t workspace_bytes, const int32_t *visible,
+                             const int32_t *vis_rank, void *stream);
 /* visible (ABI 27, may be NULL): i32[G] with visible[g] > 0 for every
  * Gaussian that has an isect (tiles_per_gauss); the 16x16 path then zeroes
  * and reads back only those Gaussians' gradient rows (the others' gradients

@@ -4,7 +4,8 @@ only, never results.
 * render records (gsplat_hip_rasterize_pack_records, ABI 15): the forward
   through the packed 64-B records is bit-identical to the forward gathering
   the four attribute arrays (the same floats reach the same arithmetic), and
-  the backward agrees up to the order of its float atomics;
+  the backward agrees up to the order of its float atomics; the same for
+  records and gradient rows indexed by depth rank (ABI 27);
 * the forward's dispatch order (tile_order_kernel): a permutation of the
   tiles, heaviest bucket first;
 * split heavy tiles (GSPLAT_HIP_FWD_SPLIT): the images of the unsplit
@@ -63,6 +64,48 @@ def test_records_match_plain_gathers(mode):
         scale = b.abs().max().item()
         err = (a - b).abs().max().item()
         assert err <= 1e-5 * scale + 1e-9, (name, err, scale)
+
+
+def _render_ranks(ins, W, H, ranks, **kw):
+    import gsplat_hip
+    from gsplat_hip import _wrapper
+    saved = _wrapper.RANKS
+    _wrapper.RANKS = ranks
+    try:
+        leaves = [x.clone().requires_grad_(True) for x in ins[:5]]
+        rc, ra, meta = gsplat_hip.rasterization(*leaves, ins[5], ins[6], W, H, packed=False, **kw)
+        g = torch.Generator(device=DEV).manual_seed(1)
+        w = torch.rand(rc.shape, generator=g, device=DEV)
+        (rc * w).sum().backward()
+        torch.cuda.synchronize()
+        return rc.detach(), ra.detach(), meta, [x.grad for x in leaves]
+    finally:
+        _wrapper.RANKS = saved
+
+
+@pytest.mark.parametrize("capped", [False, True])
+def test_rank_indexed_rows_match_gaussian_rows(capped):
+    """Render records and gradient rows indexed by the visible Gaussians'
+    depth rank (GSPLAT_HIP_RANKS, ABI 27): the same records reach the same
+    arithmetic, so the forward is bit-identical and the backward agrees up to
+    its float atomics' order; meta["flatten_ids"] keeps the Gaussian ids."""
+    ins, W, H = _scene()
+    kw = {}
+    if capped:
+        kw = dict(_isect_capacity=400000,
+                  _isect_status=torch.zeros(1, dtype=torch.int32, device=DEV))
+    rc0, ra0, m0, g0 = _render_ranks(ins, W, H, False, **kw)
+    rc1, ra1, m1, g1 = _render_ranks(ins, W, H, True, **kw)
+    # (capacity-sized arrays: the first counts[0] entries are the isects)
+    n = int(m0["isect_counts"][0]) if capped else m0["flatten_ids"].numel()
+    assert torch.equal(m0["flatten_ids"][:n], m1["flatten_ids"][:n])
+    assert torch.equal(m0["isect_ids"][:n], m1["isect_ids"][:n])
+    assert torch.equal(rc0, rc1) and torch.equal(ra0, ra1)
+    for a, b, name in zip(g0, g1, ["means", "quats", "scales", "opacities", "colors"]):
+        scale = b.abs().max().item()
+        err = (a - b).abs().max().item()
+        assert err <= 1e-5 * scale + 1e-9, (name, err, scale)
+    assert n > 50000
 
 
 def test_dispatch_order_is_heaviest_first_permutation():
