@@ -137,10 +137,44 @@ GS_INLINE void fused_dir(const Fused &fz, int64_t i, float &x, float &y, float &
   z = m[2] - pz;
 }
 
+// Lazy SH Adam (one rank, the trainer's fused SH step): a Gaussian outside
+// the view has a zero SH gradient, and torch.optim.Adam's update with a zero
+// gradient depends only on the row's own (p, m, v) and the step's factors.
+// So those updates are deferred: last[g] counts the Adam steps applied to
+// row g, and the row is brought up to date -- the same adam_update calls,
+// in the same order, with each skipped step's factors from the ring fac --
+// only when it is next visible (in registers in the colour forward; for
+// good in the backward, before the step's own update) or at a flush.  The
+// parameters and moments equal the eager ones bit for bit at every flush;
+// rows outside the view cost no HBM traffic per step.
+struct LazySH {
+  int32_t *last;         // [N] Adam steps applied to the row
+  float4 *fac;           // ring [R]: step s -> fac[s % R] = (ss0, ss_rest, ib, 0)
+  int R;
+  int step;              // this step's Adam step t (1-based) ...
+  const int64_t *step_dev;  // ... or read here (a captured step)
+  const float *m0, *v0, *mr, *vr;  // moments (the forward reads them)
+  float b1, b2, eps;
+};
+
+GS_INLINE int lazy_step(const LazySH &lz) {
+  return lz.step_dev ? (int)*lz.step_dev : lz.step;
+}
+
+// zero-gradient Adam steps (from, to] of one element (DC: ss = fac.x, rest: fac.y)
+GS_INLINE void lazy_catch_up(float &p, float &m, float &v, int from, int to, bool dc,
+                             const LazySH &lz) {
+  for (int s = from + 1; s <= to; ++s) {
+    const float4 f = lz.fac[s % lz.R];
+    adam_update(p, 0.f, m, v, lz.b1, lz.b2, lz.eps, dc ? f.x : f.y, f.z);
+  }
+}
+
 template <int DEG, bool FUSED>
 __global__ void __launch_bounds__(256)
 sh_fwd_kernel(int64_t n, int64_t n_coeff_rows, Coeffs cf, const float *__restrict__ dirs,
-              const uint8_t *__restrict__ masks, float *__restrict__ colors, Fused fz) {
+              const uint8_t *__restrict__ masks, float *__restrict__ colors, Fused fz,
+              LazySH lz = LazySH{}) {
   constexpr int NB = (DEG + 1) * (DEG + 1);
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -167,12 +201,38 @@ sh_fwd_kernel(int64_t n, int64_t n_coeff_rows, Coeffs cf, const float *__restric
   const int64_t row = i % n_coeff_rows;
   const float *p0 = cf.c0 + row * cf.s0;
   const float *pr = cf.cr + row * cf.sr;
-  float r = B[0] * p0[0], g = B[0] * p0[1], b = B[0] * p0[2];
+  float r, g, b;
+  if (FUSED && lz.last) {
+    // lazy SH Adam: the coefficients after step t - 1, in registers (the
+    // moments are read, nothing is written; C == 1, rows = Gaussians)
+    const int t = lazy_step(lz), from = lz.last[row];
+    float c[NB][3];
 #pragma unroll
-  for (int k = 1; k < NB; ++k) {
-    r += B[k] * pr[3 * (k - 1)];
-    g += B[k] * pr[3 * (k - 1) + 1];
-    b += B[k] * pr[3 * (k - 1) + 2];
+    for (int k = 0; k < NB; ++k)
+#pragma unroll
+      for (int ch = 0; ch < 3; ++ch) {
+        const int64_t e = k == 0 ? row * 3 + ch : row * 45 + 3 * (k - 1) + ch;
+        float pp = k == 0 ? p0[ch] : pr[3 * (k - 1) + ch];
+        float mm = k == 0 ? lz.m0[e] : lz.mr[e];
+        float vv = k == 0 ? lz.v0[e] : lz.vr[e];
+        lazy_catch_up(pp, mm, vv, from, t - 1, k == 0, lz);
+        c[k][ch] = pp;
+      }
+    r = B[0] * c[0][0], g = B[0] * c[0][1], b = B[0] * c[0][2];
+#pragma unroll
+    for (int k = 1; k < NB; ++k) {
+      r += B[k] * c[k][0];
+      g += B[k] * c[k][1];
+      b += B[k] * c[k][2];
+    }
+  } else {
+    r = B[0] * p0[0], g = B[0] * p0[1], b = B[0] * p0[2];
+#pragma unroll
+    for (int k = 1; k < NB; ++k) {
+      r += B[k] * pr[3 * (k - 1)];
+      g += B[k] * pr[3 * (k - 1) + 1];
+      b += B[k] * pr[3 * (k - 1) + 2];
+    }
   }
   if (FUSED) {
     r = fmaxf(r + 0.5f, 0.f);
@@ -334,6 +394,46 @@ GS_INLINE void adam_rows(float *P, float *M, float *V, const float *g, int rows,
   }
 }
 
+// adam_rows for the lazy SH Adam (LazySH): only the rows with from[r] >= 0
+// (visible: their gradient is in g) are touched -- each element first
+// catches up the zero-gradient steps (from[r], t - 1], then takes step t.
+template <int WID, int GS>
+GS_INLINE void adam_rows_lazy(float *P, float *M, float *V, const float *g, const int *from,
+                              int rows, int lane, float ss, const AdamSH &ad, int t, bool dc,
+                              const LazySH &lz) {
+  const int count = rows * WID, n4 = count >> 2;
+  float4 *P4 = reinterpret_cast<float4 *>(P);
+  float4 *M4 = reinterpret_cast<float4 *>(M);
+  float4 *V4 = reinterpret_cast<float4 *>(V);
+  auto one = [&](float &p, float &m, float &v, int e) {
+    const int r = e / WID;
+    const int f = from[r];
+    if (f < 0) return;
+    lazy_catch_up(p, m, v, f, t - 1, dc, lz);
+    adam_update(p, g[r * GS + (e - r * WID)], m, v, ad.b1, ad.b2, ad.eps, ss, ad.ib);
+  };
+  for (int q = lane; q < n4; q += 64) {
+    const int e = 4 * q;
+    if (from[e / WID] < 0 && from[(e + 3) / WID] < 0) continue;  // WID >= 3: rows of e..e+3
+    float4 p = P4[q], m = M4[q], v = V4[q];
+    one(p.x, m.x, v.x, e);
+    one(p.y, m.y, v.y, e + 1);
+    one(p.z, m.z, v.z, e + 2);
+    one(p.w, m.w, v.w, e + 3);
+    P4[q] = p;
+    M4[q] = m;
+    V4[q] = v;
+  }
+  for (int e = 4 * n4 + lane; e < count; e += 64) {
+    if (from[e / WID] < 0) continue;
+    float pp = P[e], mm = M[e], vv = V[e];
+    one(pp, mm, vv, e);
+    P[e] = pp;
+    M[e] = mm;
+    V[e] = vv;
+  }
+}
+
 // CAMS (FUSED): the row of lane i is Gaussian i seen from all C cameras of
 // fz (C = fz's camera count, rows c * N + i of radii / v_colors): the
 // coefficients are read once, the gradient rows and the means gradient
@@ -346,13 +446,14 @@ __global__ void __launch_bounds__(256)
 sh_bwd_staged_kernel(int64_t n, Coeffs cf, const float *__restrict__ dirs,
                      const uint8_t *__restrict__ masks, const float *__restrict__ v_colors,
                      VCoeffs vc, float *__restrict__ v_dirs, Fused fz, AdamSH ad = AdamSH{},
-                     int C = 1) {
+                     int C = 1, LazySH lz = LazySH{}) {
   static_assert(!CAMS || FUSED, "the camera loop is the fused colour path's");
   if (!CAMS) C = 1;
   constexpr int NB = (DEG + 1) * (DEG + 1), WR = 3 * KR, RSR = WR | 1;
   static_assert(KR >= NB - 1, "KR covers the active coefficients");
   __shared__ float l_dc[4][64 * 3];               // row stride 3 (odd)
   __shared__ float l_rest[4][64 * (RSR > 1 ? RSR : 1)];  // odd row stride
+  __shared__ int l_from[4][ADAM ? 64 : 1];        // lazy SH Adam: a row's last step, -1 = skip
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t i0 = (int64_t)blockIdx.x * 256 + wid * 64;
   if (i0 >= n) return;
@@ -376,6 +477,20 @@ sh_bwd_staged_kernel(int64_t n, Coeffs cf, const float *__restrict__ dirs,
       for (int k = 0; k < NB; ++k)
 #pragma unroll
         for (int ch = 0; ch < 3; ++ch) cr[k][ch] = k == 0 ? p0[ch] : pr[3 * (k - 1) + ch];
+    }
+    if (ADAM && !CAMS && lz.last) {
+      // lazy SH Adam: the coefficients after step t - 1 (as the forward saw
+      // them); the Adam phase below redoes this catch-up and stores it
+      const int t = lazy_step(lz), from = lz.last[i];
+#pragma unroll
+      for (int k = 0; k < NB; ++k)
+#pragma unroll
+        for (int ch = 0; ch < 3; ++ch) {
+          const int64_t e = k == 0 ? i * 3 + ch : i * WR + 3 * (k - 1) + ch;
+          float mm = k == 0 ? ad.m0[e] : ad.mr[e];
+          float vv = k == 0 ? ad.v0[e] : ad.vr[e];
+          lazy_catch_up(cr[k][ch], mm, vv, from, t - 1, k == 0, lz);
+        }
     }
     auto coef = [&](int k, int ch) { return cr[k][ch]; };
     const bool want_dirs = (v_dirs != nullptr) && DEG > 0;
@@ -460,6 +575,22 @@ sh_bwd_staged_kernel(int64_t n, Coeffs cf, const float *__restrict__ dirs,
       a.ssr = ad.hyper[1];
       a.ib = ad.hyper[2];
     }
+    if (!CAMS && lz.last) {  // lazy: visible rows only, after their catch-up
+      const int t = lazy_step(lz);
+      if (blockIdx.x == 0 && threadIdx.x == 0) lz.fac[t % lz.R] = make_float4(a.ss0, a.ssr, a.ib, 0.f);
+      int *fr = l_from[wid];
+      if (lane < rows) fr[lane] = on ? lz.last[i] : -1;
+      __builtin_amdgcn_wave_barrier();
+      adam_rows_lazy<3, 3>(const_cast<float *>(cf.c0) + i0 * 3, a.m0 + i0 * 3, a.v0 + i0 * 3, sd,
+                           fr, rows, lane, a.ss0, a, t, true, lz);
+      if (WR > 0)
+        adam_rows_lazy<(WR > 0 ? WR : 1), RSR>(const_cast<float *>(cf.cr) + i0 * WR,
+                                               a.mr + i0 * WR, a.vr + i0 * WR, sr, fr, rows,
+                                               lane, a.ssr, a, t, false, lz);
+      __builtin_amdgcn_wave_barrier();
+      if (on) lz.last[i] = t;
+      return;
+    }
     adam_rows<3, 3>(const_cast<float *>(cf.c0) + i0 * 3, a.m0 + i0 * 3, a.v0 + i0 * 3, sd,
                     rows, lane, a.ss0, a);
     if (WR > 0)
@@ -479,6 +610,27 @@ sh_bwd_staged_kernel(int64_t n, Coeffs cf, const float *__restrict__ dirs,
         gr[(int64_t)wr.rr * vc.sr + wr.c] = sr[wr.rr * RSR + wr.c];
     }
   }
+}
+
+// Lazy SH Adam flush: every row brought up to Adam step T (the zero-gradient
+// steps it skipped), last[] = T.  One lane per row.
+__global__ void __launch_bounds__(256)
+sh_lazy_flush_kernel(int64_t N, float *__restrict__ p0, float *__restrict__ pr, LazySH lz,
+                     float *__restrict__ m0, float *__restrict__ v0, float *__restrict__ mr,
+                     float *__restrict__ vr, int T) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= N) return;
+  const int from = lz.last[i];
+  if (from >= T) return;
+  for (int ch = 0; ch < 3; ++ch) {
+    const int64_t e = i * 3 + ch;
+    lazy_catch_up(p0[e], m0[e], v0[e], from, T, true, lz);
+  }
+  for (int k = 0; k < 45; ++k) {
+    const int64_t e = i * 45 + k;
+    lazy_catch_up(pr[e], mr[e], vr[e], from, T, false, lz);
+  }
+  lz.last[i] = T;
 }
 
 }  // namespace gs
@@ -574,6 +726,57 @@ extern "C" int gsplat_hip_sh_colors_fwd(int degree, int C, int64_t N, int64_t n_
   return 0;
 }
 
+// The colour forward of the lazy SH Adam (ABI 28; C == 1, sh0 [N,1,3] +
+// shN [N,15,3] with their moments): each visible row's coefficients brought
+// to Adam step t - 1 in registers (t = step, or *step_device when non-null)
+// from its last[] and the factor ring fac [R] x (ss0, ss_rest, ib, 0); the
+// colours equal those of the eagerly updated coefficients bit for bit.
+extern "C" int gsplat_hip_sh_colors_fwd_lazy(int degree, int64_t N, const float *means,
+                                             const float *viewmats, const float *coeffs,
+                                             const float *coeffs_rest, const int32_t *radii,
+                                             float *colors, const float *m0, const float *v0,
+                                             const float *m_rest, const float *v_rest,
+                                             int32_t *last, float *fac, int R, int step,
+                                             const int64_t *step_device, float beta1, float beta2,
+                                             float eps, void *stream) {
+  if (N <= 0) return 0;
+  GS_REQUIRE(degree >= 0 && degree <= 3, "sh_colors_fwd_lazy: degree %d not in [0, 3]", degree);
+  GS_REQUIRE(coeffs && coeffs_rest && m0 && v0 && m_rest && v_rest && last && fac && R > 0,
+             "sh_colors_fwd_lazy: null buffer");
+  GS_REQUIRE(step_device || step >= 1, "sh_colors_fwd_lazy: step must be >= 1");
+  const Coeffs cf{coeffs, coeffs_rest, 3, 45};
+  const Fused fz{means, viewmats, radii, N};
+  const LazySH lz{last, reinterpret_cast<float4 *>(fac), R, step, step_device, m0, v0, m_rest,
+                  v_rest, beta1, beta2, eps};
+  dim3 grid((unsigned)((N + 255) / 256));
+  hipStream_t st = (hipStream_t)stream;
+#define GS_SH_FWDL(D)                                                                       \
+  case D:                                                                                   \
+    hipLaunchKernelGGL((sh_fwd_kernel<D, true>), grid, dim3(256), 0, st, N, N, cf, nullptr,  \
+                       nullptr, colors, fz, lz);                                            \
+    break;
+  switch (degree) { GS_SH_FWDL(0) GS_SH_FWDL(1) GS_SH_FWDL(2) GS_SH_FWDL(3) }
+#undef GS_SH_FWDL
+  GS_CHECK_LAUNCH("sh_colors_fwd_lazy");
+  return 0;
+}
+
+// Flush of the lazy SH Adam: rows brought to Adam step T (see LazySH).
+extern "C" int gsplat_hip_sh_lazy_flush(int64_t N, float *coeffs, float *coeffs_rest, float *m0,
+                                        float *v0, float *m_rest, float *v_rest, int32_t *last,
+                                        float *fac, int R, int T, float beta1, float beta2,
+                                        float eps, void *stream) {
+  if (N <= 0 || T <= 0) return 0;
+  GS_REQUIRE(coeffs && coeffs_rest && m0 && v0 && m_rest && v_rest && last && fac && R > 0,
+             "sh_lazy_flush: null buffer");
+  const LazySH lz{last, reinterpret_cast<float4 *>(fac), R, T, nullptr, m0, v0, m_rest, v_rest,
+                  beta1, beta2, eps};
+  hipLaunchKernelGGL(sh_lazy_flush_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, N, coeffs, coeffs_rest, lz, m0, v0, m_rest, v_rest, T);
+  GS_CHECK_LAUNCH("sh_lazy_flush");
+  return 0;
+}
+
 extern "C" int gsplat_hip_sh_colors_bwd(int degree, int C, int64_t N, int64_t n_coeff_rows, int K,
                                         const float *means, const float *viewmats,
                                         const float *coeffs, const float *coeffs_rest,
@@ -616,7 +819,8 @@ extern "C" int gsplat_hip_sh_colors_bwd(int degree, int C, int64_t N, int64_t n_
 static int sh_colors_bwd_adam_launch(int degree, int C, int64_t N, const float *means,
                                      const float *viewmats, float *coeffs, float *coeffs_rest,
                                      const int32_t *radii, const float *v_colors, float *v_dirs,
-                                     const AdamSH &ad, hipStream_t st);
+                                     const AdamSH &ad, hipStream_t st,
+                                     const LazySH &lz = LazySH{});
 
 extern "C" int gsplat_hip_sh_colors_bwd_adam(int degree, int C, int64_t N, const float *means,
                                              const float *viewmats, float *coeffs,
@@ -624,7 +828,8 @@ extern "C" int gsplat_hip_sh_colors_bwd_adam(int degree, int C, int64_t N, const
                                              const float *v_colors, float *v_dirs, float *m0,
                                              float *v0, float *m_rest, float *v_rest, float lr0,
                                              float lr_rest, float beta1, float beta2, float eps,
-                                             int step, void *stream) {
+                                             int step, int32_t *last, float *fac, int R,
+                                             void *stream) {
   if (N <= 0) return 0;
   GS_REQUIRE(degree >= 0 && degree <= 3, "sh_colors_bwd_adam: degree %d not in [0, 3]", degree);
   GS_REQUIRE(coeffs && coeffs_rest && m0 && v0 && m_rest && v_rest,
@@ -636,8 +841,11 @@ extern "C" int gsplat_hip_sh_colors_bwd_adam(int degree, int C, int64_t N, const
   const double bc1 = 1.0 - pow((double)beta1, step), bc2 = 1.0 - pow((double)beta2, step);
   AdamSH ad{m0, v0, m_rest, v_rest, (float)(lr0 / bc1), (float)(lr_rest / bc1),
             (float)(1.0 / sqrt(bc2)), beta1, beta2, eps, nullptr, nullptr};
+  GS_REQUIRE(!last || (fac && R > 0 && C == 1), "sh_colors_bwd_adam: lazy SH Adam needs C == 1");
+  const LazySH lz{last, reinterpret_cast<float4 *>(fac), R, step, nullptr, m0, v0, m_rest,
+                  v_rest, beta1, beta2, eps};
   return sh_colors_bwd_adam_launch(degree, C, N, means, viewmats, coeffs, coeffs_rest, radii,
-                                   v_colors, v_dirs, ad, (hipStream_t)stream);
+                                   v_colors, v_dirs, ad, (hipStream_t)stream, lz);
 }
 
 // The same with the step-dependent factors read on the device (ABI 20, a
@@ -652,7 +860,9 @@ extern "C" int gsplat_hip_sh_colors_bwd_adam_dev(int degree, int C, int64_t N,
                                                  float *v0, float *m_rest, float *v_rest,
                                                  const float *hyper_device, float beta1,
                                                  float beta2, float eps,
-                                                 const int32_t *skip_device, void *stream) {
+                                                 const int32_t *skip_device, int32_t *last,
+                                                 float *fac, int R, const int64_t *step_device,
+                                                 void *stream) {
   if (N <= 0) return 0;
   GS_REQUIRE(degree >= 0 && degree <= 3, "sh_colors_bwd_adam: degree %d not in [0, 3]", degree);
   GS_REQUIRE(coeffs && coeffs_rest && m0 && v0 && m_rest && v_rest && hyper_device,
@@ -661,14 +871,18 @@ extern "C" int gsplat_hip_sh_colors_bwd_adam_dev(int degree, int C, int64_t N,
                (uintptr_t)m_rest | (uintptr_t)v_rest) & 15) == 0,
              "sh_colors_bwd_adam: coefficient and moment buffers must be 16-B aligned");
   AdamSH ad{m0, v0, m_rest, v_rest, 0.f, 0.f, 0.f, beta1, beta2, eps, hyper_device, skip_device};
+  GS_REQUIRE(!last || (fac && R > 0 && C == 1 && step_device),
+             "sh_colors_bwd_adam_dev: lazy SH Adam needs C == 1 and step_device");
+  const LazySH lz{last, reinterpret_cast<float4 *>(fac), R, 0, step_device, m0, v0, m_rest,
+                  v_rest, beta1, beta2, eps};
   return sh_colors_bwd_adam_launch(degree, C, N, means, viewmats, coeffs, coeffs_rest, radii,
-                                   v_colors, v_dirs, ad, (hipStream_t)stream);
+                                   v_colors, v_dirs, ad, (hipStream_t)stream, lz);
 }
 
 static int sh_colors_bwd_adam_launch(int degree, int C, int64_t N, const float *means,
                                      const float *viewmats, float *coeffs, float *coeffs_rest,
                                      const int32_t *radii, const float *v_colors, float *v_dirs,
-                                     const AdamSH &ad, hipStream_t st) {
+                                     const AdamSH &ad, hipStream_t st, const LazySH &lz) {
   GS_REQUIRE(C >= 1, "sh_colors_bwd_adam: C=%d cameras", C);
   Coeffs cf{coeffs, coeffs_rest, 3, 45};
   VCoeffs vc{nullptr, nullptr, 3, 45};
@@ -678,7 +892,7 @@ static int sh_colors_bwd_adam_launch(int degree, int C, int64_t N, const float *
   case D:                                                                                        \
     if (C == 1)                                                                                  \
       hipLaunchKernelGGL((sh_bwd_staged_kernel<D, true, 15, true>), grid, dim3(256), 0, st, N,   \
-                         cf, nullptr, nullptr, v_colors, vc, v_dirs, fz, ad, 1);                 \
+                         cf, nullptr, nullptr, v_colors, vc, v_dirs, fz, ad, 1, lz);             \
     else                                                                                         \
       hipLaunchKernelGGL((sh_bwd_staged_kernel<D, true, 15, true, true>), grid, dim3(256), 0, st, \
                          N, cf, nullptr, nullptr, v_colors, vc, v_dirs, fz, ad, C);              \

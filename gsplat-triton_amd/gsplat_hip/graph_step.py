@@ -138,6 +138,7 @@ class GraphStep:
         self.vm = f[64:80].view(1, 4, 4)
         self.K = f[80:89].view(1, 3, 3)
         self.cam = self.blk[384:392].view(torch.int64)
+        self.adam_step = self.blk[392:400].view(torch.int64)  # this step's Adam step t
         self.slot = self.blk[self.SLOT - 8:].view(torch.int64)
         self.seq = torch.zeros(1, dtype=torch.int64, device=dev)  # steps fetched
         self.status = torch.zeros(1, dtype=torch.int32, device=dev)  # sticky overflow flag
@@ -175,10 +176,12 @@ class GraphStep:
         if tr.sh_adam_in_bwd:
             o = tr.opt
             i0, i1 = names.index("sh0"), names.index("shN")
+            lazy = tr.sh_lazy if (getattr(tr, "sh_lazy", None) is not None and deg == 3) else None
             fa = _wrapper.ShAdamInBackward(
                 p["sh0"].data, p["shN"].data, o.exp_avg[i0], o.exp_avg_sq[i0], o.exp_avg[i1],
                 o.exp_avg_sq[i1], o.lrs[i0], o.lrs[i1], o.betas, o.eps, 1,
-                hyper=self.scal[sh_off:sh_off + 3], skip=self.status)
+                hyper=self.scal[sh_off:sh_off + 3], skip=self.status, lazy=lazy,
+                step_dev=self.adam_step if lazy is not None else None)
         fusion = _wrapper.StepFusion(sh_adam=fa, geom=tr.geom_fuse) \
             if (fa is not None or tr.geom_fuse) else None
         # the first launch also fetches this step's input block (the ring slot)
@@ -218,13 +221,17 @@ class GraphStep:
         torch.cuda.synchronize(self.dev)
         try:
             # warm-up on a side stream (torch's capture recipe) as a VOID
-            # step: the flag makes every state update a no-op
+            # step: the flag makes every state update a no-op.  Only before
+            # the first capture: a re-capture (a refine's new tensors, the SH
+            # degree) runs code that has run before, and the warm-up would
+            # cost a whole extra step per refine
             self.status.fill_(1)
-            s = torch.cuda.Stream(device=self.dev)
-            s.wait_stream(torch.cuda.current_stream(self.dev))
-            with torch.cuda.stream(s):
-                self._body(deg, stats)
-            torch.cuda.current_stream(self.dev).wait_stream(s)
+            if self.recaptures == 0:
+                s = torch.cuda.Stream(device=self.dev)
+                s.wait_stream(torch.cuda.current_stream(self.dev))
+                with torch.cuda.stream(s):
+                    self._body(deg, stats)
+                torch.cuda.current_stream(self.dev).wait_stream(s)
             self.graph = None
             g = torch.cuda.CUDAGraph(keep_graph=True)
             # no garbage collection while capturing: a collected object that
@@ -282,6 +289,7 @@ class GraphStep:
         f[64:80] = self._vm_host[ci].reshape(-1)
         f[80:89] = self._K_host[ci].reshape(-1)
         b[384:392].view(np.int64)[0] = ci
+        b[392:400].view(np.int64)[0] = step  # the lazy SH Adam's step count
         if tr.max_steps:
             tr._set_means_lr(lrs[0])
 
