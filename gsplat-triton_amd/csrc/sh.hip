@@ -153,8 +153,9 @@ struct LazySH {
   int R;
   int step;              // this step's Adam step t (1-based) ...
   const int64_t *step_dev;  // ... or read here (a captured step)
-  const float *m0, *v0, *mr, *vr;  // moments (the forward reads them)
+  float *m0, *v0, *mr, *vr;  // moments (the forward brings the visible rows up to date)
   float b1, b2, eps;
+  const int32_t *skip;     // a void captured step (the forward then writes nothing)
 };
 
 GS_INLINE int lazy_step(const LazySH &lz) {
@@ -170,11 +171,31 @@ GS_INLINE void lazy_catch_up(float &p, float &m, float &v, int from, int to, boo
   }
 }
 
+// The same for E elements of a lane at once, with the step loop uniform over
+// the wave (s from the wave's smallest `from` + 1 to `to`; a lane takes step
+// s only if s > its from): the factors are one scalar load per step, and the
+// E independent updates per step hide each other's latency.
+template <int E>
+GS_INLINE void lazy_catch_up_wave(float (&p)[E], float (&m)[E], float (&v)[E], int from, int to,
+                                  const bool (&dc)[E], const LazySH &lz) {
+  int lo = from;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) lo = min(lo, __shfl_xor(lo, o, 64));
+  lo = __builtin_amdgcn_readfirstlane(lo);
+  for (int s = lo + 1; s <= to; ++s) {
+    const float4 f = lz.fac[s % lz.R];
+    if (s > from) {
+#pragma unroll
+      for (int j = 0; j < E; ++j)
+        adam_update(p[j], 0.f, m[j], v[j], lz.b1, lz.b2, lz.eps, dc[j] ? f.x : f.y, f.z);
+    }
+  }
+}
+
 template <int DEG, bool FUSED>
 __global__ void __launch_bounds__(256)
 sh_fwd_kernel(int64_t n, int64_t n_coeff_rows, Coeffs cf, const float *__restrict__ dirs,
-              const uint8_t *__restrict__ masks, float *__restrict__ colors, Fused fz,
-              LazySH lz = LazySH{}) {
+              const uint8_t *__restrict__ masks, float *__restrict__ colors, Fused fz) {
   constexpr int NB = (DEG + 1) * (DEG + 1);
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -201,38 +222,12 @@ sh_fwd_kernel(int64_t n, int64_t n_coeff_rows, Coeffs cf, const float *__restric
   const int64_t row = i % n_coeff_rows;
   const float *p0 = cf.c0 + row * cf.s0;
   const float *pr = cf.cr + row * cf.sr;
-  float r, g, b;
-  if (FUSED && lz.last) {
-    // lazy SH Adam: the coefficients after step t - 1, in registers (the
-    // moments are read, nothing is written; C == 1, rows = Gaussians)
-    const int t = lazy_step(lz), from = lz.last[row];
-    float c[NB][3];
+  float r = B[0] * p0[0], g = B[0] * p0[1], b = B[0] * p0[2];
 #pragma unroll
-    for (int k = 0; k < NB; ++k)
-#pragma unroll
-      for (int ch = 0; ch < 3; ++ch) {
-        const int64_t e = k == 0 ? row * 3 + ch : row * 45 + 3 * (k - 1) + ch;
-        float pp = k == 0 ? p0[ch] : pr[3 * (k - 1) + ch];
-        float mm = k == 0 ? lz.m0[e] : lz.mr[e];
-        float vv = k == 0 ? lz.v0[e] : lz.vr[e];
-        lazy_catch_up(pp, mm, vv, from, t - 1, k == 0, lz);
-        c[k][ch] = pp;
-      }
-    r = B[0] * c[0][0], g = B[0] * c[0][1], b = B[0] * c[0][2];
-#pragma unroll
-    for (int k = 1; k < NB; ++k) {
-      r += B[k] * c[k][0];
-      g += B[k] * c[k][1];
-      b += B[k] * c[k][2];
-    }
-  } else {
-    r = B[0] * p0[0], g = B[0] * p0[1], b = B[0] * p0[2];
-#pragma unroll
-    for (int k = 1; k < NB; ++k) {
-      r += B[k] * pr[3 * (k - 1)];
-      g += B[k] * pr[3 * (k - 1) + 1];
-      b += B[k] * pr[3 * (k - 1) + 2];
-    }
+  for (int k = 1; k < NB; ++k) {
+    r += B[k] * pr[3 * (k - 1)];
+    g += B[k] * pr[3 * (k - 1) + 1];
+    b += B[k] * pr[3 * (k - 1) + 2];
   }
   if (FUSED) {
     r = fmaxf(r + 0.5f, 0.f);
@@ -240,6 +235,84 @@ sh_fwd_kernel(int64_t n, int64_t n_coeff_rows, Coeffs cf, const float *__restric
     b = fmaxf(b + 0.5f, 0.f);
   }
   o[0] = r; o[1] = g; o[2] = b;
+}
+
+// The colour forward of the lazy SH Adam (C == 1, rows = Gaussians, the
+// trainer's sh0 [N,1,3] / shN [N,15,3] layout): a visible row is brought to
+// step t - 1 -- all 16 coefficients, written back with their moments and
+// last = t - 1 unless the step is void -- and its colour computed from it,
+// as sh_fwd_kernel<DEG, true> computes it from eagerly updated
+// coefficients.  Every lane of a wave takes part in the wave-uniform step
+// loop (masked rows with nothing to catch up).
+template <int DEG>
+__global__ void __launch_bounds__(256)
+sh_fwd_lazy_kernel(int64_t N, Coeffs cf, float *__restrict__ colors, Fused fz, LazySH lz) {
+  constexpr int NB = (DEG + 1) * (DEG + 1);
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool on = i < N && fz.radii[i] > 0;
+  const int t = lazy_step(lz);
+  const int from = on ? lz.last[i] : 0x7fffffff;
+  const bool wb = on && from < t - 1 && !(lz.skip && *lz.skip);
+  float *P0 = const_cast<float *>(cf.c0) + i * 3, *PR = const_cast<float *>(cf.cr) + i * 45;
+  float c[NB][3];
+#pragma unroll
+  for (int k0 = 0; k0 < 16; k0 += 2) {
+    float pp[6], mm[6], vv[6];
+    bool dc[6];
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      const int k = k0 + j / 3, ch = j % 3;
+      const int64_t e = k == 0 ? i * 3 + ch : i * 45 + 3 * (k - 1) + ch;
+      dc[j] = k == 0;
+      pp[j] = mm[j] = vv[j] = 0.f;
+      if (on && (k < NB || from < t - 1)) {
+        pp[j] = k == 0 ? P0[ch] : PR[3 * (k - 1) + ch];
+        if (from < t - 1) {
+          mm[j] = k == 0 ? lz.m0[e] : lz.mr[e];
+          vv[j] = k == 0 ? lz.v0[e] : lz.vr[e];
+        }
+      }
+    }
+    lazy_catch_up_wave<6>(pp, mm, vv, from, t - 1, dc, lz);
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      const int k = k0 + j / 3, ch = j % 3;
+      if (k < NB) c[k][ch] = pp[j];
+      if (wb) {
+        const int64_t e = k == 0 ? i * 3 + ch : i * 45 + 3 * (k - 1) + ch;
+        if (k == 0) {
+          P0[ch] = pp[j]; lz.m0[e] = mm[j]; lz.v0[e] = vv[j];
+        } else {
+          PR[3 * (k - 1) + ch] = pp[j]; lz.mr[e] = mm[j]; lz.vr[e] = vv[j];
+        }
+      }
+    }
+  }
+  if (wb) lz.last[i] = t - 1;
+  if (i >= N) return;
+  float *o = colors + 3 * i;
+  if (!on) {
+    o[0] = 0.5f; o[1] = 0.5f; o[2] = 0.5f;
+    return;
+  }
+  float x = 0.f, y = 0.f, z = 0.f;
+  if (DEG > 0) {
+    fused_dir(fz, i, x, y, z);
+    const float inorm = rsqrtf(x * x + y * y + z * z);
+    x *= inorm; y *= inorm; z *= inorm;
+  }
+  float B[NB];
+  sh_basis<DEG, false>(x, y, z, B, nullptr);
+  float r = B[0] * c[0][0], g = B[0] * c[0][1], b = B[0] * c[0][2];
+#pragma unroll
+  for (int k = 1; k < NB; ++k) {
+    r += B[k] * c[k][0];
+    g += B[k] * c[k][1];
+    b += B[k] * c[k][2];
+  }
+  o[0] = fmaxf(r + 0.5f, 0.f);
+  o[1] = fmaxf(g + 0.5f, 0.f);
+  o[2] = fmaxf(b + 0.5f, 0.f);
 }
 
 template <int DEG, bool FUSED>
@@ -440,20 +513,23 @@ GS_INLINE void adam_rows_lazy(float *P, float *M, float *V, const float *g, cons
 // (v_dirs [N, 3]) are summed over the cameras in registers -- the shared
 // coefficients of a Gaussian-sharded render's N-camera colours, whose sum
 // is also what the fused Adam needs.  C == 1 is the one-camera kernel.
+// LAZY (ADAM, C == 1): the lazy SH Adam (LazySH); a template of its own so
+// that the eager kernels' code -- and their bits -- stay as they were.
 template <int DEG, bool FUSED, int KR = (DEG + 1) * (DEG + 1) - 1, bool ADAM = false,
-          bool CAMS = false>
+          bool CAMS = false, bool LAZY = false>
 __global__ void __launch_bounds__(256)
 sh_bwd_staged_kernel(int64_t n, Coeffs cf, const float *__restrict__ dirs,
                      const uint8_t *__restrict__ masks, const float *__restrict__ v_colors,
                      VCoeffs vc, float *__restrict__ v_dirs, Fused fz, AdamSH ad = AdamSH{},
                      int C = 1, LazySH lz = LazySH{}) {
   static_assert(!CAMS || FUSED, "the camera loop is the fused colour path's");
+  static_assert(!LAZY || (ADAM && !CAMS), "the lazy SH Adam: one camera, Adam fused");
   if (!CAMS) C = 1;
   constexpr int NB = (DEG + 1) * (DEG + 1), WR = 3 * KR, RSR = WR | 1;
   static_assert(KR >= NB - 1, "KR covers the active coefficients");
   __shared__ float l_dc[4][64 * 3];               // row stride 3 (odd)
   __shared__ float l_rest[4][64 * (RSR > 1 ? RSR : 1)];  // odd row stride
-  __shared__ int l_from[4][ADAM ? 64 : 1];        // lazy SH Adam: a row's last step, -1 = skip
+  __shared__ int l_from[4][LAZY ? 64 : 1];        // lazy SH Adam: a row's last step, -1 = skip
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t i0 = (int64_t)blockIdx.x * 256 + wid * 64;
   if (i0 >= n) return;
@@ -477,20 +553,6 @@ sh_bwd_staged_kernel(int64_t n, Coeffs cf, const float *__restrict__ dirs,
       for (int k = 0; k < NB; ++k)
 #pragma unroll
         for (int ch = 0; ch < 3; ++ch) cr[k][ch] = k == 0 ? p0[ch] : pr[3 * (k - 1) + ch];
-    }
-    if (ADAM && !CAMS && lz.last) {
-      // lazy SH Adam: the coefficients after step t - 1 (as the forward saw
-      // them); the Adam phase below redoes this catch-up and stores it
-      const int t = lazy_step(lz), from = lz.last[i];
-#pragma unroll
-      for (int k = 0; k < NB; ++k)
-#pragma unroll
-        for (int ch = 0; ch < 3; ++ch) {
-          const int64_t e = k == 0 ? i * 3 + ch : i * WR + 3 * (k - 1) + ch;
-          float mm = k == 0 ? ad.m0[e] : ad.mr[e];
-          float vv = k == 0 ? ad.v0[e] : ad.vr[e];
-          lazy_catch_up(cr[k][ch], mm, vv, from, t - 1, k == 0, lz);
-        }
     }
     auto coef = [&](int k, int ch) { return cr[k][ch]; };
     const bool want_dirs = (v_dirs != nullptr) && DEG > 0;
@@ -575,7 +637,7 @@ sh_bwd_staged_kernel(int64_t n, Coeffs cf, const float *__restrict__ dirs,
       a.ssr = ad.hyper[1];
       a.ib = ad.hyper[2];
     }
-    if (!CAMS && lz.last) {  // lazy: visible rows only, after their catch-up
+    if (LAZY) {  // lazy: visible rows only, after their catch-up
       const int t = lazy_step(lz);
       if (blockIdx.x == 0 && threadIdx.x == 0) lz.fac[t % lz.R] = make_float4(a.ss0, a.ssr, a.ib, 0.f);
       int *fr = l_from[wid];
@@ -612,25 +674,40 @@ sh_bwd_staged_kernel(int64_t n, Coeffs cf, const float *__restrict__ dirs,
   }
 }
 
-// Lazy SH Adam flush: every row brought up to Adam step T (the zero-gradient
-// steps it skipped), last[] = T.  One lane per row.
+// Lazy SH Adam flush: every element brought up to Adam step T (the
+// zero-gradient steps its row skipped); one lane per element of the DC
+// ([N,3]) and rest ([N,45]) arrays, wave-uniform step loop.  last[] = T is
+// written by a second launch (every element reads its row's last here).
 __global__ void __launch_bounds__(256)
 sh_lazy_flush_kernel(int64_t N, float *__restrict__ p0, float *__restrict__ pr, LazySH lz,
-                     float *__restrict__ m0, float *__restrict__ v0, float *__restrict__ mr,
-                     float *__restrict__ vr, int T) {
+                     int T) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t n0 = N * 3, n1 = N * 45;
+  const bool dc = e < n0;
+  const bool ok = e < n0 + n1;
+  const int64_t q = dc ? e : e - n0;
+  const int64_t row = ok ? (dc ? q / 3 : q / 45) : 0;
+  const int from = ok ? lz.last[row] : T;
+  float pp[1] = {0.f}, mm[1] = {0.f}, vv[1] = {0.f};
+  const bool d1[1] = {dc};
+  if (ok && from < T) {
+    pp[0] = dc ? p0[q] : pr[q];
+    mm[0] = dc ? lz.m0[q] : lz.mr[q];
+    vv[0] = dc ? lz.v0[q] : lz.vr[q];
+  }
+  lazy_catch_up_wave<1>(pp, mm, vv, from, T, d1, lz);
+  if (ok && from < T) {
+    if (dc) {
+      p0[q] = pp[0]; lz.m0[q] = mm[0]; lz.v0[q] = vv[0];
+    } else {
+      pr[q] = pp[0]; lz.mr[q] = mm[0]; lz.vr[q] = vv[0];
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) sh_lazy_set_kernel(int64_t N, int32_t *last, int T) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= N) return;
-  const int from = lz.last[i];
-  if (from >= T) return;
-  for (int ch = 0; ch < 3; ++ch) {
-    const int64_t e = i * 3 + ch;
-    lazy_catch_up(p0[e], m0[e], v0[e], from, T, true, lz);
-  }
-  for (int k = 0; k < 45; ++k) {
-    const int64_t e = i * 45 + k;
-    lazy_catch_up(pr[e], mr[e], vr[e], from, T, false, lz);
-  }
-  lz.last[i] = T;
+  if (i < N) last[i] = T;
 }
 
 }  // namespace gs
@@ -732,13 +809,13 @@ extern "C" int gsplat_hip_sh_colors_fwd(int degree, int C, int64_t N, int64_t n_
 // from its last[] and the factor ring fac [R] x (ss0, ss_rest, ib, 0); the
 // colours equal those of the eagerly updated coefficients bit for bit.
 extern "C" int gsplat_hip_sh_colors_fwd_lazy(int degree, int64_t N, const float *means,
-                                             const float *viewmats, const float *coeffs,
-                                             const float *coeffs_rest, const int32_t *radii,
-                                             float *colors, const float *m0, const float *v0,
-                                             const float *m_rest, const float *v_rest,
-                                             int32_t *last, float *fac, int R, int step,
-                                             const int64_t *step_device, float beta1, float beta2,
-                                             float eps, void *stream) {
+                                             const float *viewmats, float *coeffs,
+                                             float *coeffs_rest, const int32_t *radii,
+                                             float *colors, float *m0, float *v0, float *m_rest,
+                                             float *v_rest, int32_t *last, float *fac, int R,
+                                             int step, const int64_t *step_device, float beta1,
+                                             float beta2, float eps, const int32_t *skip_device,
+                                             void *stream) {
   if (N <= 0) return 0;
   GS_REQUIRE(degree >= 0 && degree <= 3, "sh_colors_fwd_lazy: degree %d not in [0, 3]", degree);
   GS_REQUIRE(coeffs && coeffs_rest && m0 && v0 && m_rest && v_rest && last && fac && R > 0,
@@ -747,13 +824,13 @@ extern "C" int gsplat_hip_sh_colors_fwd_lazy(int degree, int64_t N, const float 
   const Coeffs cf{coeffs, coeffs_rest, 3, 45};
   const Fused fz{means, viewmats, radii, N};
   const LazySH lz{last, reinterpret_cast<float4 *>(fac), R, step, step_device, m0, v0, m_rest,
-                  v_rest, beta1, beta2, eps};
+                  v_rest, beta1, beta2, eps, skip_device};
   dim3 grid((unsigned)((N + 255) / 256));
   hipStream_t st = (hipStream_t)stream;
 #define GS_SH_FWDL(D)                                                                       \
   case D:                                                                                   \
-    hipLaunchKernelGGL((sh_fwd_kernel<D, true>), grid, dim3(256), 0, st, N, N, cf, nullptr,  \
-                       nullptr, colors, fz, lz);                                            \
+    hipLaunchKernelGGL((sh_fwd_lazy_kernel<D>), grid, dim3(256), 0, st, N, cf, colors, fz,   \
+                       lz);                                                                 \
     break;
   switch (degree) { GS_SH_FWDL(0) GS_SH_FWDL(1) GS_SH_FWDL(2) GS_SH_FWDL(3) }
 #undef GS_SH_FWDL
@@ -770,9 +847,12 @@ extern "C" int gsplat_hip_sh_lazy_flush(int64_t N, float *coeffs, float *coeffs_
   GS_REQUIRE(coeffs && coeffs_rest && m0 && v0 && m_rest && v_rest && last && fac && R > 0,
              "sh_lazy_flush: null buffer");
   const LazySH lz{last, reinterpret_cast<float4 *>(fac), R, T, nullptr, m0, v0, m_rest, v_rest,
-                  beta1, beta2, eps};
-  hipLaunchKernelGGL(sh_lazy_flush_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0,
-                     (hipStream_t)stream, N, coeffs, coeffs_rest, lz, m0, v0, m_rest, v_rest, T);
+                  beta1, beta2, eps, nullptr};
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(sh_lazy_flush_kernel, dim3((unsigned)((N * 48 + 255) / 256)), dim3(256), 0,
+                     st, N, coeffs, coeffs_rest, lz, T);
+  hipLaunchKernelGGL(sh_lazy_set_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, st, N,
+                     last, T);
   GS_CHECK_LAUNCH("sh_lazy_flush");
   return 0;
 }
@@ -843,7 +923,7 @@ extern "C" int gsplat_hip_sh_colors_bwd_adam(int degree, int C, int64_t N, const
             (float)(1.0 / sqrt(bc2)), beta1, beta2, eps, nullptr, nullptr};
   GS_REQUIRE(!last || (fac && R > 0 && C == 1), "sh_colors_bwd_adam: lazy SH Adam needs C == 1");
   const LazySH lz{last, reinterpret_cast<float4 *>(fac), R, step, nullptr, m0, v0, m_rest,
-                  v_rest, beta1, beta2, eps};
+                  v_rest, beta1, beta2, eps, nullptr};
   return sh_colors_bwd_adam_launch(degree, C, N, means, viewmats, coeffs, coeffs_rest, radii,
                                    v_colors, v_dirs, ad, (hipStream_t)stream, lz);
 }
@@ -874,7 +954,7 @@ extern "C" int gsplat_hip_sh_colors_bwd_adam_dev(int degree, int C, int64_t N,
   GS_REQUIRE(!last || (fac && R > 0 && C == 1 && step_device),
              "sh_colors_bwd_adam_dev: lazy SH Adam needs C == 1 and step_device");
   const LazySH lz{last, reinterpret_cast<float4 *>(fac), R, 0, step_device, m0, v0, m_rest,
-                  v_rest, beta1, beta2, eps};
+                  v_rest, beta1, beta2, eps, skip_device};
   return sh_colors_bwd_adam_launch(degree, C, N, means, viewmats, coeffs, coeffs_rest, radii,
                                    v_colors, v_dirs, ad, (hipStream_t)stream, lz);
 }
@@ -890,9 +970,12 @@ static int sh_colors_bwd_adam_launch(int degree, int C, int64_t N, const float *
   dim3 grid((unsigned)((N + 255) / 256));
 #define GS_SH_BWD_ADAM(D)                                                                        \
   case D:                                                                                        \
-    if (C == 1)                                                                                  \
+    if (C == 1 && lz.last)                                                                       \
+      hipLaunchKernelGGL((sh_bwd_staged_kernel<D, true, 15, true, false, true>), grid, dim3(256),  \
+                         0, st, N, cf, nullptr, nullptr, v_colors, vc, v_dirs, fz, ad, 1, lz);   \
+    else if (C == 1)                                                                             \
       hipLaunchKernelGGL((sh_bwd_staged_kernel<D, true, 15, true>), grid, dim3(256), 0, st, N,   \
-                         cf, nullptr, nullptr, v_colors, vc, v_dirs, fz, ad, 1, lz);             \
+                         cf, nullptr, nullptr, v_colors, vc, v_dirs, fz, ad, 1);                 \
     else                                                                                         \
       hipLaunchKernelGGL((sh_bwd_staged_kernel<D, true, 15, true, true>), grid, dim3(256), 0, st, \
                          N, cf, nullptr, nullptr, v_colors, vc, v_dirs, fz, ad, C);              \

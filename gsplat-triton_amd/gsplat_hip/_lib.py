@@ -96,7 +96,7 @@ _SIGS = {
                                                  _p, _p, _p, _p, _p, _f, _f, _f, _p, _p, _p, _i32,
                                                  _p, _p]),
     "gsplat_hip_sh_colors_fwd_lazy": (_i32, [_i32, _i64, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p,
-                                             _p, _p, _i32, _i32, _p, _f, _f, _f, _p]),
+                                             _p, _p, _i32, _i32, _p, _f, _f, _f, _p, _p]),
     "gsplat_hip_sh_lazy_flush": (_i32, [_i64, _p, _p, _p, _p, _p, _p, _p, _p, _i32, _i32, _f, _f,
                                         _f, _p]),
     "gsplat_hip_sh_colors_bwd_sum": (_i32, [_i32, _i32, _i64, _p, _p, _p, _p, _p, _p, _p, _p, _p,

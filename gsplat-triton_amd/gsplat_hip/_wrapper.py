@@ -763,7 +763,7 @@ class _SHColors(torch.autograd.Function):
                       _ptr(v0), _ptr(mr), _ptr(vr), _ptr(lz.last), _ptr(lz.fac), lz.R,
                       int(fa.step) if fa.step_dev is None else 0, _ptr(fa.step_dev),
                       ctypes.c_float(fa.betas[0]), ctypes.c_float(fa.betas[1]),
-                      ctypes.c_float(fa.eps), _stream())
+                      ctypes.c_float(fa.eps), _ptr(fa.skip), _stream())
         else:
             _lib.call("gsplat_hip_sh_colors_fwd", int(sh_degree), C, N, n_rows, K, _ptr(means),
                       _ptr(viewmats), _ptr(base), _ptr(rest), _ptr(radii), _ptr(colors), _stream())

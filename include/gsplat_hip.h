@@ -499,25 +499,25 @@ int gsplat_hip_sh_colors_bwd_adam_dev(int degree, int C, int64_t N, const float 
  * depends only on the row's own (p, m, v) and the step's factors -- so it is
  * deferred.  last i32[N] counts the Adam steps applied to each row; fac
  * f32[R][4] is a ring of the steps' factors (ss0, ss_rest, ib, 0) at s % R.
- * With last non-NULL the backward above updates only the visible rows: each
- * first takes its skipped zero-gradient steps (last[g], t - 1] (the same
- * adam_update calls in the same order as the eager step), then step t with
- * its gradient, and last[g] = t; it also stores step t's factors at
- * fac[t % R] (t = step, or *step_device for the _dev form).
- * sh_colors_fwd_lazy: the colours from the visible rows' coefficients
- * brought to step t - 1 in registers (nothing written).
+ * With last non-NULL the backward above updates only the visible rows (the
+ * colour forward has brought them to step t - 1; any step it left out is
+ * taken first, the same adam_update calls in the same order as the eager
+ * steps): step t with its gradient, last[g] = t; it also stores step t's
+ * factors at fac[t % R] (t = step, or *step_device for the _dev form).
+ * sh_colors_fwd_lazy: each visible row brought to step t - 1 (written back
+ * with its moments, last = t - 1; nothing written when *skip_device != 0, a
+ * void captured step) and the colours from it.
  * sh_lazy_flush: every row brought to step T (last[] = T) -- before anything
  * else reads the coefficients or moments; at most R - 1 steps may pass
  * between a row's updates (the caller flushes at least every R - 1 steps).
  * Parameters and moments equal the eager sequence's bit for bit after a
  * flush. */
 int gsplat_hip_sh_colors_fwd_lazy(int degree, int64_t N, const float *means,
-                                  const float *viewmats, const float *coeffs,
-                                  const float *coeffs_rest, const int32_t *radii, float *colors,
-                                  const float *m0, const float *v0, const float *m_rest,
-                                  const float *v_rest, int32_t *last, float *fac, int R,
+                                  const float *viewmats, float *coeffs, float *coeffs_rest,
+                                  const int32_t *radii, float *colors, float *m0, float *v0,
+                                  float *m_rest, float *v_rest, int32_t *last, float *fac, int R,
                                   int step, const int64_t *step_device, float beta1, float beta2,
-                                  float eps, void *stream);
+                                  float eps, const int32_t *skip_device, void *stream);
 int gsplat_hip_sh_lazy_flush(int64_t N, float *coeffs, float *coeffs_rest, float *m0, float *v0,
                              float *m_rest, float *v_rest, int32_t *last, float *fac, int R,
                              int T, float beta1, float beta2, float eps, void *stream);

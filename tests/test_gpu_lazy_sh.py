@@ -80,7 +80,7 @@ def test_lazy_sh_adam_is_exact(R, steps):
                 _lib.call("gsplat_hip_sh_colors_fwd_lazy", 3, N, _ptr(means), _ptr(vm), _ptr(p0),
                           _ptr(pr), _ptr(radii), _ptr(colors), _ptr(m0), _ptr(v0), _ptr(mr),
                           _ptr(vr), _ptr(last), _ptr(fac), R, 0 if use_dev else t,
-                          _ptr(stepd) if use_dev else None, 0.9, 0.999, eps, _stream())
+                          _ptr(stepd) if use_dev else None, 0.9, 0.999, eps, None, _stream())
                 if use_dev:
                     (s0, ib), (sr, _) = adam_factors([lr0, lrr], betas, t)
                     hyper.copy_(torch.tensor([s0, sr, ib]))
