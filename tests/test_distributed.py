@@ -462,13 +462,17 @@ def test_refine_under_dp_keeps_replicas_identical_gloo(world, scale2d):
         np.testing.assert_allclose(mm[1].numpy(), a["m"][k][1], rtol=1e-6, atol=1e-12)
 
 
-def _pairs_worker(rank, port, q):
+PAIR_SHARDS = {2: [3, 2], 3: [4, 3, 3], 8: [3, 2, 3, 1, 2, 2, 3, 2]}  # uneven shards
+
+
+def _pairs_worker(rank, port, q, world=WORLD):
+    WORLD = world  # noqa: N806 (the module constant's role, per test)
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         dist.init_process_group("gloo", rank=rank, world_size=WORLD)
         from gsplat_hip import distributed as gd
         from gsplat_hip.rendering import _reshape_view
-        n_world = [3, 2]  # uneven shards
+        n_world = PAIR_SHARDS[WORLD]
         Nr = n_world[rank]
         g = torch.Generator().manual_seed(rank)
         radii = torch.randint(0, 50, (WORLD, Nr, 2), generator=g, dtype=torch.int32)
@@ -500,22 +504,25 @@ def _pairs_worker(rank, port, q):
         q.put((rank, repr(e)))
 
 
-def test_exchange_pairs_matches_generic_exchange_gloo():
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_exchange_pairs_matches_generic_exchange_gloo(world):
     """distributed.exchange_pairs (one field-major exchange, one camera per
     rank) gives the generic all_to_all_tensor_list + _reshape_view results,
-    contiguous, and the same gradients, on two gloo ranks with uneven shards."""
+    contiguous, and the same gradients, on 2 / 3 / 8 gloo ranks with uneven
+    shards (every rank exchanging with several peers at 3 and 8)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_pairs_worker, args=(r, port, q)) for r in range(WORLD)]
+    procs = [ctx.Process(target=_pairs_worker, args=(r, port, q, world)) for r in range(world)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=120) for _ in range(WORLD))
+    res = dict(q.get(timeout=180) for _ in range(world))
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for r in range(WORLD):
+    n = sum(PAIR_SHARDS[world])
+    for r in range(world):
         assert isinstance(res[r], tuple), res[r]
         ok, okg, shapes = res[r]
         assert ok and okg, (r, ok, okg)
-        assert shapes == [(1, 5, 2), (1, 5, 2), (1, 5), (1, 5, 3), (1, 5), (1, 5, 3)]
+        assert shapes == [(1, n, 2), (1, n, 2), (1, n), (1, n, 3), (1, n), (1, n, 3)]

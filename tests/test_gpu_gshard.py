@@ -128,11 +128,13 @@ def _trainer_rank(rank, world, port, out_dir):
         dist.destroy_process_group()
 
 
-def _trainer_scene(W=320, H=240):
+def _trainer_scene(W=320, H=240, trim=0):
     from gsplat_hip.train_step import camera_pool, load_garden_scene
     means, rgbs, vms, Ks, sw, sh_ = load_garden_scene(
         os.path.join(ROOT, "tests", "golden", "garden_scene.npz"), scene_grid=1)
     means, rgbs = means[::8].contiguous(), rgbs[::8].contiguous()
+    if trim:  # 13974 points split evenly three ways; 13973 do not
+        means, rgbs = means[:-trim].contiguous(), rgbs[:-trim].contiguous()
     vm, K = camera_pool(vms, Ks, sw, sh_, W, H, n=4)
     return means, rgbs, vm, K, W, H
 
@@ -185,6 +187,86 @@ def test_gshard_trainer_step_matches_whole_scene_step(tmp_path):
             # within rounding of zero may take either sign (a few entries)
             close_most(a, b, 1e-5, 1e-6, f"{k} rank {r}", max_frac=2e-3,
                        out_bound=2.5 * lrs[list(params).index(k)])
+
+
+def _trainer_rank_refine(rank, world, port, out_dir):
+    """World-`world` Gaussian-sharded trainer, uneven shards, a refine at step
+    1 (each shard refined alone, then the shard sizes all-gathered), then a
+    step with the new shard sizes."""
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    try:
+        from gsplat_hip import densify, train_step
+        from gsplat_hip.densify import DefaultStrategyConfig
+        from gsplat_hip.train_step import Trainer
+        means, rgbs, vm, K, W, H = _trainer_scene(trim=1)
+        cfg = DefaultStrategyConfig(refine_start_iter=0, refine_every=1, reset_every=10 ** 6,
+                                    grow_grad2d=2e-5)
+        tr = Trainer(means, rgbs, vm, K, W, H, device=DEV, world_size=world, rank=rank,
+                     gaussian_shard=True, strategy=cfg)
+        n0 = tr.params["means"].shape[0]
+        saved = {}
+        orig = densify.refine
+
+        def spy(params, moments, grad2d, count, step, *a, **kw):
+            saved.update(params={k: v.detach().cpu().clone() for k, v in params.items()},
+                         grad2d=grad2d.cpu().clone(), count=count.cpu().clone(), step=step)
+            return orig(params, moments, grad2d, count, step, *a, **kw)
+        train_step.densify.refine = spy
+        try:
+            tr.step(0)
+            tr.step(1)  # refine
+        finally:
+            train_step.densify.refine = orig
+        loss = float(tr.step(2))
+        tr.sync()
+        torch.save({"n0": n0, "n1": tr.params["means"].shape[0], "n_world": tr._n_world,
+                    "log": tr.refine_log, "pre": saved, "loss": loss},
+                   os.path.join(out_dir, f"refine{rank}.pt"))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gshard_trainer_refine_world3(tmp_path):
+    """Three ranks on the one GPU (gloo), shards [r::3] of uneven sizes: the
+    per-shard refines make the whole scene's decisions (the refine on the
+    re-interleaved shards' statistics gives the same duplicate / split /
+    prune counts), every rank all-gathers the same new shard sizes, and the
+    next step runs with them."""
+    import torch.multiprocessing as mp
+    from gsplat_hip import densify
+    from gsplat_hip.densify import DefaultStrategyConfig
+    world = 3
+    mp.spawn(_trainer_rank_refine, args=(world, _port(), str(tmp_path)), nprocs=world,
+             join=True)
+    got = [torch.load(os.path.join(tmp_path, f"refine{r}.pt"), weights_only=True)
+           for r in range(world)]
+    N = sum(g["n0"] for g in got)
+    assert N % world != 0 and len({g["n0"] for g in got}) == 2  # uneven shards
+    sizes = [g["n1"] for g in got]
+    for g in got:
+        assert g["n_world"] == sizes
+        assert [e[0] for e in g["log"]] == [1] and np.isfinite(g["loss"])
+    # the whole scene's refine decisions from the shards' inputs, re-interleaved
+    def whole(key, sub=None):
+        parts = [g["pre"][key] if sub is None else g["pre"][key][sub] for g in got]
+        out = torch.empty((N,) + tuple(parts[0].shape[1:]), dtype=parts[0].dtype)
+        for r, p in enumerate(parts):
+            out[r::world] = p
+        return out.to(DEV)
+    params = {k: whole("params", k).contiguous() for k in got[0]["pre"]["params"]}
+    moments = {k: [torch.zeros_like(v), torch.zeros_like(v)] for k, v in params.items()}
+    cfg = DefaultStrategyConfig(refine_start_iter=0, refine_every=1, reset_every=10 ** 6,
+                                grow_grad2d=2e-5)
+    _, _, counts = densify.refine(params, moments, whole("grad2d").contiguous(),
+                                  whole("count").contiguous(), 1, cfg, 1.0,
+                                  generator=torch.Generator(device=DEV).manual_seed(0))
+    per_rank = [g["log"][0][1:4] for g in got]
+    assert tuple(counts) == tuple(sum(c[i] for c in per_rank) for i in range(3)), \
+        (counts, per_rank)
+    assert sum(counts) > 0
 
 
 def _sh_case(C=5, N=3001, seed=3):
