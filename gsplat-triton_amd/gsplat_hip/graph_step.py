@@ -43,6 +43,7 @@ import collections
 import ctypes
 import gc
 import math
+import os
 import time
 
 import numpy as np
@@ -60,8 +61,16 @@ def graphable(tr) -> bool:
     refine / opacity reset run eagerly after their step (Trainer.step), and a
     refine (new parameter tensors, Trainer._param_gen) re-captures."""
     st = tr.strategy
-    return (tr.fused and not tr.sharded and tr.world_size == 1 and tr.model == "3dgs"
-            and not getattr(tr, "gshard", False)
+    # Gaussian-sharded (one camera per rank): its two pair exchanges inside
+    # the graph -- the device copies of the one-GPU emulation
+    # (distributed.EMULATION, bench --gshard-emulate), or RCCL's
+    # all_to_all_single when GSPLAT_HIP_GRAPH_RCCL=1 (not run on more than one
+    # GPU here)
+    from . import distributed as gdist
+    gshard_ok = getattr(tr, "gshard", False) and tr.world_size <= GraphStep.MAX_WORLD and (
+        gdist.EMULATION is not None or os.environ.get("GSPLAT_HIP_GRAPH_RCCL", "0") == "1")
+    return (tr.fused and not tr.sharded and tr.model == "3dgs"
+            and (gshard_ok or (tr.world_size == 1 and not getattr(tr, "gshard", False)))
             and not getattr(tr, "defer_sh", False)
             and (st is None or (not st.absgrad and tr.radii2d is None))
             and isinstance(tr.opt, FusedAdam) and torch.device(tr.device).type == "cuda")
@@ -117,7 +126,8 @@ class GraphStep:
     """Trainer.step as HIP graph replays (see the module docstring)."""
 
     RING = 8  # host-mapped slots for the per-step input block and counts
-    SLOT = 512  # bytes per input block
+    SLOT = 2048  # bytes per input block
+    MAX_WORLD = 8  # cameras of a Gaussian-sharded step in the block
 
     def __init__(self, tr, capacity=None, headroom=1.25, lag=2):
         assert graphable(tr), "GraphStep: a fused one-rank 3DGS trainer"
@@ -127,18 +137,23 @@ class GraphStep:
         self.headroom = float(headroom)
         self.lag = int(lag)  # steps the host may run ahead of its overflow check
         self.capacity = None if capacity is None else int(capacity)
-        # device input of the graph: one 512-B block per step -- f32 [0, 64) the
-        # Adam factors, f32 [64, 80) the camera's viewmat, [80, 89) its K,
-        # i64 at byte 384 the camera index, i64 at byte 504 the ring slot
-        # (written by gsplat_hip_step_fetch)
+        # device input of the graph: one 2-KB block per step -- f32 [0, 64)
+        # the Adam factors, i64 at byte 256 the rank's camera index, i64 at 264
+        # the Adam step t, f32 viewmats [W][16] at byte 512 and Ks [W][9] at
+        # byte 1024 (W = the world's cameras: 1, or the Gaussian-sharded job's
+        # ranks), i64 at SLOT - 8 the ring slot (written by
+        # gsplat_hip_step_fetch)
         self.n_groups = len(tr.params)
+        self.gshard = bool(getattr(tr, "gshard", False))
+        self.W = tr.world_size if self.gshard else 1
         self.blk = torch.zeros(self.SLOT, dtype=torch.uint8, device=dev)
-        f = self.blk[:384].view(torch.float32)
-        self.scal = f[:64]
-        self.vm = f[64:80].view(1, 4, 4)
-        self.K = f[80:89].view(1, 3, 3)
-        self.cam = self.blk[384:392].view(torch.int64)
-        self.adam_step = self.blk[392:400].view(torch.int64)  # this step's Adam step t
+        self.scal = self.blk[:256].view(torch.float32)
+        self.cam = self.blk[256:264].view(torch.int64)
+        self.adam_step = self.blk[264:272].view(torch.int64)  # this step's Adam step t
+        self.vm_w = self.blk[512:512 + 64 * self.W].view(torch.float32).view(self.W, 4, 4)
+        self.K_w = self.blk[1024:1024 + 36 * self.W].view(torch.float32).view(self.W, 3, 3)
+        r = tr.rank if self.gshard else 0
+        self.vm, self.K = self.vm_w[r:r + 1], self.K_w[r:r + 1]  # this rank's camera
         self.slot = self.blk[self.SLOT - 8:].view(torch.int64)
         self.seq = torch.zeros(1, dtype=torch.int64, device=dev)  # steps fetched
         self.status = torch.zeros(1, dtype=torch.int32, device=dev)  # sticky overflow flag
@@ -187,12 +202,16 @@ class GraphStep:
         # the first launch also fetches this step's input block (the ring slot)
         scales, opac = activate(p["scales"], p["opacities"], fusion,
                                 fetch=(self.ring_in.dev, self.SLOT, self.RING, self.seq, self.blk))
+        dkw = {}
+        if self.gshard:  # the world's cameras from the block, shard sizes fixed per capture
+            dkw = dict(distributed=True, _world_cameras=(self.vm_w, self.K_w),
+                       _world_counts=tr._n_world)
         colors, _, meta = rasterization(
             p["means"], p["quats"], scales, opac, (p["sh0"], p["shN"]), self.vm, self.K, tr.width,
             tr.height, sh_degree=deg, packed=False, near_plane=0.01, far_plane=1e10,
             radius_clip=0.0, rasterize_mode="classic", _fusion=fusion,
             _isect_capacity=self.capacity, _isect_status=self.status,
-            _isect_report=(self.ring_out.dev, self.slot))
+            _isect_report=(self.ring_out.dev, self.slot), **dkw)
         grad_box = {}
         meta["means2d"].register_hook(lambda g: grad_box.__setitem__("g", g))
         loss = tr._regularise(l1_ssim_loss(colors, tr.targets, tr.ssim_lambda, gt_index=self.cam))
@@ -276,7 +295,7 @@ class GraphStep:
             lrs[0] = tr.lrs[0] * (0.01 ** (1.0 / tr.max_steps)) ** it
         idx, sh_off = self._layout()
         b = self.ring_in.np[slot * self.SLOT:(slot + 1) * self.SLOT]
-        f = b[:384].view(np.float32)
+        f = b[:256].view(np.float32)
         fac = adam_factors([lrs[i] for i in idx], o.betas, step)
         for k, (ss, ib) in enumerate(fac):
             f[2 * k], f[2 * k + 1] = ss, ib
@@ -286,10 +305,12 @@ class GraphStep:
                                              o.betas, step)
             f[sh_off:sh_off + 3] = (s0, sr, ib)
         ci = tr.camera_index(it)
-        f[64:80] = self._vm_host[ci].reshape(-1)
-        f[80:89] = self._K_host[ci].reshape(-1)
-        b[384:392].view(np.int64)[0] = ci
-        b[392:400].view(np.int64)[0] = step  # the lazy SH Adam's step count
+        n = len(self._vm_host)
+        world_ci = [(ci - tr.rank + r) % n for r in range(self.W)] if self.gshard else [ci]
+        b[512:512 + 64 * self.W].view(np.float32)[:] = self._vm_host[world_ci].reshape(-1)
+        b[1024:1024 + 36 * self.W].view(np.float32)[:] = self._K_host[world_ci].reshape(-1)
+        b[256:264].view(np.int64)[0] = ci
+        b[264:272].view(np.int64)[0] = step  # the lazy SH Adam's step count
         if tr.max_steps:
             tr._set_means_lr(lrs[0])
 

@@ -382,3 +382,42 @@ def test_emulated_rank0_render_matches_whole_scene():
     close_most(rc[0].detach(), rf[0], 1e-5, 1e-5, "colors")
     close_most(ra[0].detach(), af[0], 1e-5, 1e-5, "alphas")
     assert all(t.grad is not None and torch.isfinite(t.grad).all() for t in local)
+
+
+def test_graph_gshard_emulated_step_tracks_eager():
+    """The Gaussian-sharded step replayed as a HIP graph (the pair exchanges
+    inside it: the one-GPU emulation's device copies; graph_step.graphable):
+    rank 0 of an emulated 3-rank job, four steps, the world's cameras from
+    the step block, against the same steps issued eagerly."""
+    from gsplat_hip import distributed as gdist
+    from gsplat_hip.train_step import Trainer
+    means, rgbs, vm, K, W, H = _trainer_scene(trim=1)
+    world = 3
+    saved = gdist.EMULATION
+    try:
+        gdist.EMULATION = gdist.Emulation(world)
+        for j in range(1, world):
+            peer = Trainer(means, rgbs, vm, K, W, H, device=DEV, world_size=world, rank=j,
+                           gaussian_shard=True, graph=False)
+            gdist.EMULATION.record(j, lambda: peer.render(peer.camera_index(0),
+                                                          peer.sh_degree_at(0)))
+            del peer
+        out = {}
+        for graph in (False, True):
+            tr = Trainer(means, rgbs, vm, K, W, H, device=DEV, world_size=world, rank=0,
+                         gaussian_shard=True, graph=graph, max_steps=100)
+            assert (tr._graph is not None) == graph
+            for it in range(4):
+                tr.step(it)
+            tr.sync()
+            out[graph] = ({k: p.detach().clone() for k, p in tr.params.items()},
+                          tr.count.clone(), tr.grad2d.clone())
+            if graph:
+                assert tr._graph.replays >= 4 and set(tr._graph.census) <= {"kernel", "empty"}
+    finally:
+        gdist.EMULATION = saved
+    a, b = out[False], out[True]
+    for k in a[0]:
+        torch.testing.assert_close(b[0][k], a[0][k], rtol=1e-3, atol=1e-5)
+    torch.testing.assert_close(b[1], a[1], rtol=0, atol=0)
+    torch.testing.assert_close(b[2], a[2], rtol=1e-3, atol=1e-7)
