@@ -1,0 +1,36 @@
+#!/bin/bash
+# Round-4 batch: GPU suite, lazy SH Adam A/B (M2), emulated 8-rank gshard
+# step graph vs eager, M3 graph vs eager, a kernel trace of the default M2
+# line, and last the memset diagnosis (it may fault: nothing runs after it).
+cd "$GRAFT_REPO_ROOT" || exit 1
+export TMPDIR=/tmp
+O=gpurun_out/${1:-r4_batch}; mkdir -p $O
+v() { python3 -c "import json;d=json.loads(open('$1').read().strip().splitlines()[-1]);r=d['roofline'];print(round(d['value'],1), round(d['ms_per_step'],3), 'fwd', round(r['launch_ms'],4), 'bwd', round(r['bwd']['launch_ms'],4))"; }
+if [ -z "$SKIP_TESTS" ]; then
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 180 --timeout-method thread > $O/tests.log 2>&1
+  rc=$?; echo "tests rc=$rc"; tail -2 $O/tests.log; [ $rc -eq 0 ] || exit $rc
+fi
+for r in 1 2; do
+  for l in 0 1; do
+    GSPLAT_HIP_SH_LAZY=$l timeout -k 10 300 python -u bench.py --no-traffic --no-cpu-baseline > $O/m2_lazy$l.$r.json 2> $O/m2_lazy$l.$r.err || exit 2
+    echo "m2 lazy=$l run $r $(v $O/m2_lazy$l.$r.json)"
+  done
+done
+for r in 1 2; do
+  timeout -k 10 400 python -u bench.py --gshard-emulate 8 --no-traffic --no-cpu-baseline > $O/gs8_graph.$r.json 2> $O/gs8_graph.$r.err || exit 3
+  echo "gshard-emulate 8 graph run $r $(v $O/gs8_graph.$r.json)"
+done
+timeout -k 10 400 python -u bench.py --gshard-emulate 8 --eager --no-traffic --no-cpu-baseline > $O/gs8_eager.json 2> $O/gs8_eager.err || exit 4
+echo "gshard-emulate 8 eager $(v $O/gs8_eager.json)"
+for m in graph eager; do
+  a=""; [ $m = eager ] && a="--eager"
+  timeout -k 10 400 python -u bench.py --config m3 --no-traffic --no-cpu-baseline $a > $O/m3_$m.json 2> $O/m3_$m.err || exit 5
+  echo "m3 $m $(v $O/m3_$m.json)"
+done
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $O/trace -o run -- /usr/bin/python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-traffic > $O/trace.log 2>&1 || exit 6
+echo "trace ok"
+if [ -n "$MEMSET_DIAG" ]; then
+  GSPLAT_HIP_MEMSET_NODES=1 GSPLAT_HIP_GRAPH_ALLOW_MEMSET=1 AMD_SERIALIZE_KERNEL=3 timeout -k 10 180 python -u tools/graph_diag.py memset > $O/memset_diag.log 2>&1
+  echo "memset diag rc=$?"; tail -5 $O/memset_diag.log
+fi
+exit 0
