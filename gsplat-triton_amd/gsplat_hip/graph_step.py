@@ -168,6 +168,11 @@ class GraphStep:
         self._slot_ev = [None] * self.RING
         self._vm_host = tr.viewmats.detach().float().cpu().numpy()
         self._K_host = tr.Ks.detach().float().cpu().numpy()
+        # SH colours (and their backward) on a second captured stream,
+        # concurrent with the tile intersection (GSPLAT_HIP_SIDE_SH)
+        self.side = None
+        if not self.gshard and os.environ.get("GSPLAT_HIP_SIDE_SH", "0") == "1":
+            self.side = torch.cuda.Stream(device=dev)
         self.graph = None
         self.key = None
         self.counts = None  # the graph's isect counts (device i64[4])
@@ -216,7 +221,7 @@ class GraphStep:
             tr.height, sh_degree=deg, packed=False, near_plane=0.01, far_plane=1e10,
             radius_clip=0.0, rasterize_mode="classic", _fusion=fusion,
             _isect_capacity=self.capacity, _isect_status=self.status,
-            _isect_report=(self.ring_out.dev, self.slot), **dkw)
+            _isect_report=(self.ring_out.dev, self.slot), _colors_stream=self.side, **dkw)
         grad_box = {}
         meta["means2d"].register_hook(lambda g: grad_box.__setitem__("g", g))
         loss = tr._regularise(l1_ssim_loss(colors, tr.targets, tr.ssim_lambda, gt_index=self.cam))
@@ -225,6 +230,11 @@ class GraphStep:
         if stats and "g" in grad_box:  # DefaultStrategy statistics (until refine_stop_iter)
             update_state_(tr.grad2d, tr.count, grad_box["g"], meta["radii"], meta["width"],
                           meta["height"], meta["n_cameras"], skip=self.status)
+        if self.side is not None:  # the SH backward ran on the side stream
+            cur = torch.cuda.current_stream(self.dev)
+            cur.wait_stream(self.side)
+            if fusion is not None and fusion.v_dirs is not None:
+                fusion.v_dirs.record_stream(cur)
         skip = tr._sh_skip(fusion)
         assert tuple(i for i in range(self.n_groups) if i not in skip) == tuple(idx), \
             (skip, idx)
