@@ -202,8 +202,9 @@ def _trainer_rank_refine(rank, world, port, out_dir):
         from gsplat_hip.densify import DefaultStrategyConfig
         from gsplat_hip.train_step import Trainer
         means, rgbs, vm, K, W, H = _trainer_scene(trim=1)
-        cfg = DefaultStrategyConfig(refine_start_iter=0, refine_every=1, reset_every=10 ** 6,
-                                    grow_grad2d=2e-5)
+        # one refine, at step 1 (steps below refine_stop_iter = 2)
+        cfg = DefaultStrategyConfig(refine_start_iter=0, refine_every=1, refine_stop_iter=2,
+                                    reset_every=10 ** 6, grow_grad2d=2e-5)
         tr = Trainer(means, rgbs, vm, K, W, H, device=DEV, world_size=world, rank=rank,
                      gaussian_shard=True, strategy=cfg)
         n0 = tr.params["means"].shape[0]
@@ -258,8 +259,8 @@ def test_gshard_trainer_refine_world3(tmp_path):
         return out.to(DEV)
     params = {k: whole("params", k).contiguous() for k in got[0]["pre"]["params"]}
     moments = {k: [torch.zeros_like(v), torch.zeros_like(v)] for k, v in params.items()}
-    cfg = DefaultStrategyConfig(refine_start_iter=0, refine_every=1, reset_every=10 ** 6,
-                                grow_grad2d=2e-5)
+    cfg = DefaultStrategyConfig(refine_start_iter=0, refine_every=1, refine_stop_iter=2,
+                                reset_every=10 ** 6, grow_grad2d=2e-5)
     _, _, counts = densify.refine(params, moments, whole("grad2d").contiguous(),
                                   whole("count").contiguous(), 1, cfg, 1.0,
                                   generator=torch.Generator(device=DEV).manual_seed(0))
