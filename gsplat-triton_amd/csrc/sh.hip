@@ -435,8 +435,12 @@ struct AdamSH {
 
 // Adam over `rows` consecutive rows of WID floats (16-B aligned start): the
 // gradient of element (r, c) is g[r * GS + c] (LDS); 4 elements per lane and
-// iteration as float4, a scalar tail.
-template <int WID, int GS>
+// iteration as float4, a scalar tail.  U float4 slots per lane per iteration,
+// all U slots' loads issued before any update: the stores of one iteration
+// may alias the next one's loads as far as the compiler knows, so without
+// the unrolling a wave has only 3 x 16 B per lane in flight (the update is
+// HBM-latency bound at the 3 workgroups per CU the LDS staging allows).
+template <int WID, int GS, int U = 1>
 GS_INLINE void adam_rows(float *P, float *M, float *V, const float *g, int rows, int lane,
                          float ss, const AdamSH &ad) {
   const int count = rows * WID, n4 = count >> 2;
@@ -447,16 +451,31 @@ GS_INLINE void adam_rows(float *P, float *M, float *V, const float *g, int rows,
     const int r = e / WID;
     return g[r * GS + (e - r * WID)];
   };
-  for (int q = lane; q < n4; q += 64) {
-    float4 p = P4[q], m = M4[q], v = V4[q];
-    const int e = 4 * q;
-    adam_update(p.x, gr(e), m.x, v.x, ad.b1, ad.b2, ad.eps, ss, ad.ib);
-    adam_update(p.y, gr(e + 1), m.y, v.y, ad.b1, ad.b2, ad.eps, ss, ad.ib);
-    adam_update(p.z, gr(e + 2), m.z, v.z, ad.b1, ad.b2, ad.eps, ss, ad.ib);
-    adam_update(p.w, gr(e + 3), m.w, v.w, ad.b1, ad.b2, ad.eps, ss, ad.ib);
-    P4[q] = p;
-    M4[q] = m;
-    V4[q] = v;
+  for (int q0 = lane; q0 < n4; q0 += 64 * U) {
+    float4 p[U], m[U], v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int q = q0 + 64 * u;
+      if (q < n4) {
+        p[u] = P4[q];
+        m[u] = M4[q];
+        v[u] = V4[q];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int q = q0 + 64 * u;
+      if (q < n4) {
+        const int e = 4 * q;
+        adam_update(p[u].x, gr(e), m[u].x, v[u].x, ad.b1, ad.b2, ad.eps, ss, ad.ib);
+        adam_update(p[u].y, gr(e + 1), m[u].y, v[u].y, ad.b1, ad.b2, ad.eps, ss, ad.ib);
+        adam_update(p[u].z, gr(e + 2), m[u].z, v[u].z, ad.b1, ad.b2, ad.eps, ss, ad.ib);
+        adam_update(p[u].w, gr(e + 3), m[u].w, v[u].w, ad.b1, ad.b2, ad.eps, ss, ad.ib);
+        P4[q] = p[u];
+        M4[q] = m[u];
+        V4[q] = v[u];
+      }
+    }
   }
   for (int e = 4 * n4 + lane; e < count; e += 64) {
     float pp = P[e], mm = M[e], vv = V[e];
@@ -516,7 +535,7 @@ GS_INLINE void adam_rows_lazy(float *P, float *M, float *V, const float *g, cons
 // LAZY (ADAM, C == 1): the lazy SH Adam (LazySH); a template of its own so
 // that the eager kernels' code -- and their bits -- stay as they were.
 template <int DEG, bool FUSED, int KR = (DEG + 1) * (DEG + 1) - 1, bool ADAM = false,
-          bool CAMS = false, bool LAZY = false>
+          bool CAMS = false, bool LAZY = false, int AU = 1>
 __global__ void __launch_bounds__(256)
 sh_bwd_staged_kernel(int64_t n, Coeffs cf, const float *__restrict__ dirs,
                      const uint8_t *__restrict__ masks, const float *__restrict__ v_colors,
@@ -653,11 +672,12 @@ sh_bwd_staged_kernel(int64_t n, Coeffs cf, const float *__restrict__ dirs,
       if (on) lz.last[i] = t;
       return;
     }
-    adam_rows<3, 3>(const_cast<float *>(cf.c0) + i0 * 3, a.m0 + i0 * 3, a.v0 + i0 * 3, sd,
-                    rows, lane, a.ss0, a);
+    adam_rows<3, 3, AU>(const_cast<float *>(cf.c0) + i0 * 3, a.m0 + i0 * 3, a.v0 + i0 * 3, sd,
+                        rows, lane, a.ss0, a);
     if (WR > 0)
-      adam_rows<(WR > 0 ? WR : 1), RSR>(const_cast<float *>(cf.cr) + i0 * WR, a.mr + i0 * WR,
-                                         a.vr + i0 * WR, sr, rows, lane, a.ssr, a);
+      adam_rows<(WR > 0 ? WR : 1), RSR, AU>(const_cast<float *>(cf.cr) + i0 * WR,
+                                             a.mr + i0 * WR, a.vr + i0 * WR, sr, rows, lane,
+                                             a.ssr, a);
     return;
   }
   {  // gradient rows out, lane-contiguous
@@ -968,14 +988,27 @@ static int sh_colors_bwd_adam_launch(int degree, int C, int64_t N, const float *
   VCoeffs vc{nullptr, nullptr, 3, 45};
   const Fused fz{means, viewmats, radii, N};
   dim3 grid((unsigned)((N + 255) / 256));
+  // the Adam phase's loads, unrolled 4 slots per lane (GSPLAT_HIP_SH_ADAM_U=1: one)
+  static const int au = [] {
+    const char *e = getenv("GSPLAT_HIP_SH_ADAM_U");
+    return e && atoi(e) == 1 ? 1 : 4;
+  }();
 #define GS_SH_BWD_ADAM(D)                                                                        \
   case D:                                                                                        \
     if (C == 1 && lz.last)                                                                       \
       hipLaunchKernelGGL((sh_bwd_staged_kernel<D, true, 15, true, false, true>), grid, dim3(256),  \
                          0, st, N, cf, nullptr, nullptr, v_colors, vc, v_dirs, fz, ad, 1, lz);   \
+    else if (C == 1 && au == 4)                                                                  \
+      hipLaunchKernelGGL((sh_bwd_staged_kernel<D, true, 15, true, false, false, 4>), grid,       \
+                         dim3(256), 0, st, N, cf, nullptr, nullptr, v_colors, vc, v_dirs, fz, ad, \
+                         1);                                                                     \
     else if (C == 1)                                                                             \
       hipLaunchKernelGGL((sh_bwd_staged_kernel<D, true, 15, true>), grid, dim3(256), 0, st, N,   \
                          cf, nullptr, nullptr, v_colors, vc, v_dirs, fz, ad, 1);                 \
+    else if (au == 4)                                                                            \
+      hipLaunchKernelGGL((sh_bwd_staged_kernel<D, true, 15, true, true, false, 4>), grid,        \
+                         dim3(256), 0, st, N, cf, nullptr, nullptr, v_colors, vc, v_dirs, fz, ad, \
+                         C);                                                                     \
     else                                                                                         \
       hipLaunchKernelGGL((sh_bwd_staged_kernel<D, true, 15, true, true>), grid, dim3(256), 0, st, \
                          N, cf, nullptr, nullptr, v_colors, vc, v_dirs, fz, ad, C);              \

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-4 batch: GPU suite, lazy SH Adam / side-stream SH A/B (M2), emulated 8-rank gshard
+# Round-4 batch: GPU suite, lazy SH Adam / side-stream SH / SH-Adam unroll A/B (M2), emulated 8-rank gshard
 # step graph vs eager, M3 graph vs eager, a kernel trace of the default M2
 # line, and last the memset diagnosis (it may fault: nothing runs after it).
 cd "$GRAFT_REPO_ROOT" || exit 1
@@ -11,13 +11,14 @@ if [ -z "$SKIP_TESTS" ]; then
   rc=$?; echo "tests rc=$rc"; tail -2 $O/tests.log; [ $rc -eq 0 ] || exit $rc
 fi
 for r in 1 2; do
-  for c in "0 0" "1 0" "0 1"; do
+  for c in "0 0 4" "0 0 1" "1 0 4" "0 1 4"; do
     set -- $c
-    GSPLAT_HIP_SH_LAZY=$1 GSPLAT_HIP_SIDE_SH=$2 timeout -k 10 300 python -u bench.py --no-traffic --no-cpu-baseline > $O/m2_lazy$1_side$2.$r.json 2> $O/m2_lazy$1_side$2.$r.err || exit 2
-    echo "m2 lazy=$1 side=$2 run $r $(v $O/m2_lazy$1_side$2.$r.json)"
+    n=m2_lazy$1_side$2_u$3.$r
+    GSPLAT_HIP_SH_LAZY=$1 GSPLAT_HIP_SIDE_SH=$2 GSPLAT_HIP_SH_ADAM_U=$3 timeout -k 10 300 python -u bench.py --no-traffic --no-cpu-baseline > $O/$n.json 2> $O/$n.err || exit 2
+    echo "m2 lazy=$1 side=$2 adam_u=$3 run $r $(v $O/$n.json)"
   done
 done
-for r in 1 2; do
+for r in 1; do
   timeout -k 10 400 python -u bench.py --gshard-emulate 8 --no-traffic --no-cpu-baseline > $O/gs8_graph.$r.json 2> $O/gs8_graph.$r.err || exit 3
   echo "gshard-emulate 8 graph run $r $(v $O/gs8_graph.$r.json)"
 done
