@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-4 batch: GPU suite, lazy SH Adam / side-stream SH / SH-Adam unroll A/B (M2), emulated 8-rank gshard
+# Round-4 batch: GPU suite, lazy SH Adam / side-stream SH / SH-Adam unroll / one-launch depth sort A/B (M2), emulated 8-rank gshard
 # step graph vs eager, M3 graph vs eager, a kernel trace of the default M2
 # line, and last the memset diagnosis (it may fault: nothing runs after it).
 cd "$GRAFT_REPO_ROOT" || exit 1
@@ -10,12 +10,17 @@ if [ -z "$SKIP_TESTS" ]; then
   timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 180 --timeout-method thread > $O/tests.log 2>&1
   rc=$?; echo "tests rc=$rc"; tail -2 $O/tests.log; [ $rc -eq 0 ] || exit $rc
 fi
+# the one-launch depth sort (GSPLAT_HIP_DSORT=1): the isect / graph tests with it
+GSPLAT_HIP_DSORT=1 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_graph.py -x -q --timeout 180 --timeout-method thread > $O/tests_dsort.log 2>&1
+drc=$?; echo "dsort tests rc=$drc"; tail -2 $O/tests_dsort.log
+[ $drc -eq 124 ] || [ $drc -eq 137 ] || [ $drc -eq 134 ] || [ $drc -eq 139 ] && exit 7
 for r in 1 2; do
-  for c in "0 0 4" "0 0 1" "1 0 4" "0 1 4"; do
+  for c in "0 0 4 0" "0 0 1 0" "1 0 4 0" "0 1 4 0" "0 0 4 1"; do
     set -- $c
-    n=m2_lazy$1_side$2_u$3.$r
-    GSPLAT_HIP_SH_LAZY=$1 GSPLAT_HIP_SIDE_SH=$2 GSPLAT_HIP_SH_ADAM_U=$3 timeout -k 10 300 python -u bench.py --no-traffic --no-cpu-baseline > $O/$n.json 2> $O/$n.err || exit 2
-    echo "m2 lazy=$1 side=$2 adam_u=$3 run $r $(v $O/$n.json)"
+    [ $4 = 1 ] && [ $drc -ne 0 ] && continue
+    n=m2_lazy$1_side$2_u$3_ds$4.$r
+    GSPLAT_HIP_SH_LAZY=$1 GSPLAT_HIP_SIDE_SH=$2 GSPLAT_HIP_SH_ADAM_U=$3 GSPLAT_HIP_DSORT=$4 timeout -k 10 300 python -u bench.py --no-traffic --no-cpu-baseline > $O/$n.json 2> $O/$n.err || exit 2
+    echo "m2 lazy=$1 side=$2 adam_u=$3 dsort=$4 run $r $(v $O/$n.json)"
   done
 done
 for r in 1; do
