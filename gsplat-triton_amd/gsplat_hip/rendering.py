@@ -182,8 +182,8 @@ def rasterization(
     tile_height = math.ceil(height / float(tile_size))
     pending_isects = None
     capped = _isect_capacity is not None
-    if capped:
-        assert not distributed and tile_size == 16, "the sync-free isect: local 16x16 renders"
+    if capped:  # Gaussian-sharded too: the isect of the exchanged pairs
+        assert tile_size == 16 and not packed, "the sync-free isect: 16x16, packed=False"
     if not distributed:
         pending_isects = isect_tiles_begin(means2d, radii, depths, tile_size, tile_width,
                                            tile_height, packed=packed, n_cameras=C,
@@ -286,7 +286,8 @@ def rasterization(
                                                           for t in parts)
         pending_isects = isect_tiles_begin(means2d, radii, depths, tile_size, tile_width,
                                            tile_height, packed=packed, n_cameras=C,
-                                           camera_ids=camera_ids, gaussian_ids=gaussian_ids)
+                                           camera_ids=camera_ids, gaussian_ids=gaussian_ids,
+                                           sync=not capped)
 
     def add_depth(colors, backgrounds):
         if render_mode in ["RGB+D", "RGB+ED"]:
