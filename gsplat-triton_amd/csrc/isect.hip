@@ -25,7 +25,6 @@
 #include <rocprim/block/block_radix_sort.hpp>
 #include <rocprim/device/device_radix_sort.hpp>
 
-#include "dsort.h"
 #include "isect_st.h"
 #include "lsd_sort.h"
 #include "wave_ops.h"
@@ -260,12 +259,9 @@ GS_INLINE void cap_check(const CapCheck &cc) {
 __global__ void __launch_bounds__(kIsectBlock)
 isect_compact_kernel(int64_t G, const int32_t *__restrict__ tiles_per_gauss,
                      const float *__restrict__ depths, const int64_t *__restrict__ vis_prefix,
-                     int32_t *__restrict__ V, uint32_t *__restrict__ dkey, CapCheck cc,
-                     unsigned *__restrict__ dbar = nullptr) {
+                     int32_t *__restrict__ V, uint32_t *__restrict__ dkey, CapCheck cc) {
   __shared__ int64_t lds[kIsectBlock / 64 + 1];
   if (cc.cap_state && blockIdx.x == 0 && threadIdx.x == 0) cap_check(cc);
-  // the one-launch depth sort's barrier counters (dsort.h), zeroed here
-  if (dbar && blockIdx.x == 0 && threadIdx.x < dsort::kBars) dbar[threadIdx.x] = 0u;
   const int64_t i = (int64_t)blockIdx.x * kIsectBlock + threadIdx.x;
   const int on = (i < G) && tiles_per_gauss[i] > 0;
   int64_t tot;
@@ -542,7 +538,6 @@ extern "C" int gsplat_hip_isect_offsets(int64_t n_isects, const int64_t *n_isect
 namespace {
 struct SortedLayout {
   size_t V, dkey, Vs, dkeys, blk, big, nbig, tkey, val, tkeys, vals, tmp, total;
-  size_t dhist, dbar;  // the one-launch depth sort (dsort.h)
   size_t tmp_bytes;
   // supertile expansion (isect_st.h)
   size_t rect, st_start, seg_start, seg_st, segcnt, tile_tot, offs;
@@ -578,8 +573,6 @@ SortedLayout sorted_layout(int64_t nV, int64_t n, int key_bits) {
   L.segcnt = o; o = align256(o + 4 * st::S * st::S * (size_t)L.segcap);
   L.tile_tot = o; o = align256(o + 4 * (size_t)(st::kMaxTiles + 1));
   L.offs = o; o = align256(o + 4 * (size_t)st::kMaxTiles);
-  L.dhist = o; o = align256(o + 4 * (size_t)dsort::kWG * dsort::kRX);
-  L.dbar = o; o = align256(o + 4 * (size_t)dsort::kBars);
   L.total = o;
   return L;
 }
@@ -592,17 +585,6 @@ bool st_enabled(const st::Geo &g) {
     return !(e && atoi(e) == 0);
   }();
   return on && g.nst <= st::kMaxKeys;
-}
-
-// The one-launch depth sort (dsort.h) for up to dsort::kMaxItems visible
-// Gaussians, GSPLAT_HIP_DSORT=1 (until measured; 0 keeps lsd_sort_pairs'
-// 12 launches).
-bool dsort_enabled(int64_t n_visible) {
-  static const bool on = [] {
-    const char *e = getenv("GSPLAT_HIP_DSORT");
-    return e && atoi(e) == 1;
-  }();
-  return on && n_visible <= dsort::kMaxItems;
 }
 }  // namespace
 
@@ -657,20 +639,12 @@ static int isect_write_sorted_impl(
 
   const int64_t nbG = (n_gaussians + kIsectBlock - 1) / kIsectBlock;
   const int64_t *vis_prefix = reinterpret_cast<const int64_t *>(count_workspace) + nbG + 1;
-  const bool one_launch = dsort_enabled(n_visible);
-  unsigned *dbar = one_launch ? reinterpret_cast<unsigned *>(ws + L.dbar) : nullptr;
   hipLaunchKernelGGL(isect_compact_kernel, dim3((unsigned)nbG), dim3(kIsectBlock), 0, st,
-                     n_gaussians, tiles_per_gauss, depths, vis_prefix, V, dkey, cc, dbar);
+                     n_gaussians, tiles_per_gauss, depths, vis_prefix, V, dkey, cc);
   // stable depth sort of the visible Gaussians (32 key bits)
   const uint32_t *dks = dkeys;
-  if (one_launch) {  // result back in (dkey, V)
-    hipLaunchKernelGGL(dsort::sort_kernel, dim3(dsort::kWG), dim3(dsort::kNT), 0, st, dkey, V,
-                       dkeys, Vs, n_visible, cnt_dev ? cnt_dev + 1 : nullptr,
-                       reinterpret_cast<uint32_t *>(ws + L.dhist), dbar);
-    Vs = V;
-    dks = dkey;
-  } else if (lsd_sort_pairs(dkey, V, dkeys, Vs, n_visible, 0, 32, tmp, st, nullptr,
-                            cnt_dev ? cnt_dev + 1 : nullptr) == 0) {
+  if (lsd_sort_pairs(dkey, V, dkeys, Vs, n_visible, 0, 32, tmp, st, nullptr,
+                     cnt_dev ? cnt_dev + 1 : nullptr) == 0) {
     Vs = V;
     dks = dkey;
   }

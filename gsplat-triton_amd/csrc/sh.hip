@@ -137,61 +137,6 @@ GS_INLINE void fused_dir(const Fused &fz, int64_t i, float &x, float &y, float &
   z = m[2] - pz;
 }
 
-// Lazy SH Adam (one rank, the trainer's fused SH step): a Gaussian outside
-// the view has a zero SH gradient, and torch.optim.Adam's update with a zero
-// gradient depends only on the row's own (p, m, v) and the step's factors.
-// So those updates are deferred: last[g] counts the Adam steps applied to
-// row g, and the row is brought up to date -- the same adam_update calls,
-// in the same order, with each skipped step's factors from the ring fac --
-// only when it is next visible (in registers in the colour forward; for
-// good in the backward, before the step's own update) or at a flush.  The
-// parameters and moments equal the eager ones bit for bit at every flush;
-// rows outside the view cost no HBM traffic per step.
-struct LazySH {
-  int32_t *last;         // [N] Adam steps applied to the row
-  float4 *fac;           // ring [R]: step s -> fac[s % R] = (ss0, ss_rest, ib, 0)
-  int R;
-  int step;              // this step's Adam step t (1-based) ...
-  const int64_t *step_dev;  // ... or read here (a captured step)
-  float *m0, *v0, *mr, *vr;  // moments (the forward brings the visible rows up to date)
-  float b1, b2, eps;
-  const int32_t *skip;     // a void captured step (the forward then writes nothing)
-};
-
-GS_INLINE int lazy_step(const LazySH &lz) {
-  return lz.step_dev ? (int)*lz.step_dev : lz.step;
-}
-
-// zero-gradient Adam steps (from, to] of one element (DC: ss = fac.x, rest: fac.y)
-GS_INLINE void lazy_catch_up(float &p, float &m, float &v, int from, int to, bool dc,
-                             const LazySH &lz) {
-  for (int s = from + 1; s <= to; ++s) {
-    const float4 f = lz.fac[s % lz.R];
-    adam_update(p, 0.f, m, v, lz.b1, lz.b2, lz.eps, dc ? f.x : f.y, f.z);
-  }
-}
-
-// The same for E elements of a lane at once, with the step loop uniform over
-// the wave (s from the wave's smallest `from` + 1 to `to`; a lane takes step
-// s only if s > its from): the factors are one scalar load per step, and the
-// E independent updates per step hide each other's latency.
-template <int E>
-GS_INLINE void lazy_catch_up_wave(float (&p)[E], float (&m)[E], float (&v)[E], int from, int to,
-                                  const bool (&dc)[E], const LazySH &lz) {
-  int lo = from;
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) lo = min(lo, __shfl_xor(lo, o, 64));
-  lo = __builtin_amdgcn_readfirstlane(lo);
-  for (int s = lo + 1; s <= to; ++s) {
-    const float4 f = lz.fac[s % lz.R];
-    if (s > from) {
-#pragma unroll
-      for (int j = 0; j < E; ++j)
-        adam_update(p[j], 0.f, m[j], v[j], lz.b1, lz.b2, lz.eps, dc[j] ? f.x : f.y, f.z);
-    }
-  }
-}
-
 template <int DEG, bool FUSED>
 __global__ void __launch_bounds__(256)
 sh_fwd_kernel(int64_t n, int64_t n_coeff_rows, Coeffs cf, const float *__restrict__ dirs,
@@ -235,84 +180,6 @@ sh_fwd_kernel(int64_t n, int64_t n_coeff_rows, Coeffs cf, const float *__restric
     b = fmaxf(b + 0.5f, 0.f);
   }
   o[0] = r; o[1] = g; o[2] = b;
-}
-
-// The colour forward of the lazy SH Adam (C == 1, rows = Gaussians, the
-// trainer's sh0 [N,1,3] / shN [N,15,3] layout): a visible row is brought to
-// step t - 1 -- all 16 coefficients, written back with their moments and
-// last = t - 1 unless the step is void -- and its colour computed from it,
-// as sh_fwd_kernel<DEG, true> computes it from eagerly updated
-// coefficients.  Every lane of a wave takes part in the wave-uniform step
-// loop (masked rows with nothing to catch up).
-template <int DEG>
-__global__ void __launch_bounds__(256)
-sh_fwd_lazy_kernel(int64_t N, Coeffs cf, float *__restrict__ colors, Fused fz, LazySH lz) {
-  constexpr int NB = (DEG + 1) * (DEG + 1);
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const bool on = i < N && fz.radii[i] > 0;
-  const int t = lazy_step(lz);
-  const int from = on ? lz.last[i] : 0x7fffffff;
-  const bool wb = on && from < t - 1 && !(lz.skip && *lz.skip);
-  float *P0 = const_cast<float *>(cf.c0) + i * 3, *PR = const_cast<float *>(cf.cr) + i * 45;
-  float c[NB][3];
-#pragma unroll
-  for (int k0 = 0; k0 < 16; k0 += 2) {
-    float pp[6], mm[6], vv[6];
-    bool dc[6];
-#pragma unroll
-    for (int j = 0; j < 6; ++j) {
-      const int k = k0 + j / 3, ch = j % 3;
-      const int64_t e = k == 0 ? i * 3 + ch : i * 45 + 3 * (k - 1) + ch;
-      dc[j] = k == 0;
-      pp[j] = mm[j] = vv[j] = 0.f;
-      if (on && (k < NB || from < t - 1)) {
-        pp[j] = k == 0 ? P0[ch] : PR[3 * (k - 1) + ch];
-        if (from < t - 1) {
-          mm[j] = k == 0 ? lz.m0[e] : lz.mr[e];
-          vv[j] = k == 0 ? lz.v0[e] : lz.vr[e];
-        }
-      }
-    }
-    lazy_catch_up_wave<6>(pp, mm, vv, from, t - 1, dc, lz);
-#pragma unroll
-    for (int j = 0; j < 6; ++j) {
-      const int k = k0 + j / 3, ch = j % 3;
-      if (k < NB) c[k][ch] = pp[j];
-      if (wb) {
-        const int64_t e = k == 0 ? i * 3 + ch : i * 45 + 3 * (k - 1) + ch;
-        if (k == 0) {
-          P0[ch] = pp[j]; lz.m0[e] = mm[j]; lz.v0[e] = vv[j];
-        } else {
-          PR[3 * (k - 1) + ch] = pp[j]; lz.mr[e] = mm[j]; lz.vr[e] = vv[j];
-        }
-      }
-    }
-  }
-  if (wb) lz.last[i] = t - 1;
-  if (i >= N) return;
-  float *o = colors + 3 * i;
-  if (!on) {
-    o[0] = 0.5f; o[1] = 0.5f; o[2] = 0.5f;
-    return;
-  }
-  float x = 0.f, y = 0.f, z = 0.f;
-  if (DEG > 0) {
-    fused_dir(fz, i, x, y, z);
-    const float inorm = rsqrtf(x * x + y * y + z * z);
-    x *= inorm; y *= inorm; z *= inorm;
-  }
-  float B[NB];
-  sh_basis<DEG, false>(x, y, z, B, nullptr);
-  float r = B[0] * c[0][0], g = B[0] * c[0][1], b = B[0] * c[0][2];
-#pragma unroll
-  for (int k = 1; k < NB; ++k) {
-    r += B[k] * c[k][0];
-    g += B[k] * c[k][1];
-    b += B[k] * c[k][2];
-  }
-  o[0] = fmaxf(r + 0.5f, 0.f);
-  o[1] = fmaxf(g + 0.5f, 0.f);
-  o[2] = fmaxf(b + 0.5f, 0.f);
 }
 
 template <int DEG, bool FUSED>
@@ -435,12 +302,13 @@ struct AdamSH {
 
 // Adam over `rows` consecutive rows of WID floats (16-B aligned start): the
 // gradient of element (r, c) is g[r * GS + c] (LDS); 4 elements per lane and
-// iteration as float4, a scalar tail.  U float4 slots per lane per iteration,
-// all U slots' loads issued before any update: the stores of one iteration
-// may alias the next one's loads as far as the compiler knows, so without
-// the unrolling a wave has only 3 x 16 B per lane in flight (the update is
-// HBM-latency bound at the 3 workgroups per CU the LDS staging allows).
-template <int WID, int GS, int U = 1>
+// iteration as float4, a scalar tail.  kU float4 slots per lane and
+// iteration, all their loads issued before any update (the stores may alias
+// the next slot's loads as far as the compiler knows): at the 3 workgroups
+// per CU the LDS staging allows, one slot left 3 x 16 B per lane in flight
+// (M2 776.2 / 774.1 vs 773.8 / 765.5 images/s, profiles/r4_batch/).
+constexpr int kU = 4;
+template <int WID, int GS>
 GS_INLINE void adam_rows(float *P, float *M, float *V, const float *g, int rows, int lane,
                          float ss, const AdamSH &ad) {
   const int count = rows * WID, n4 = count >> 2;
@@ -451,10 +319,10 @@ GS_INLINE void adam_rows(float *P, float *M, float *V, const float *g, int rows,
     const int r = e / WID;
     return g[r * GS + (e - r * WID)];
   };
-  for (int q0 = lane; q0 < n4; q0 += 64 * U) {
-    float4 p[U], m[U], v[U];
+  for (int q0 = lane; q0 < n4; q0 += 64 * kU) {
+    float4 p[kU], m[kU], v[kU];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
+    for (int u = 0; u < kU; ++u) {
       const int q = q0 + 64 * u;
       if (q < n4) {
         p[u] = P4[q];
@@ -463,7 +331,7 @@ GS_INLINE void adam_rows(float *P, float *M, float *V, const float *g, int rows,
       }
     }
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
+    for (int u = 0; u < kU; ++u) {
       const int q = q0 + 64 * u;
       if (q < n4) {
         const int e = 4 * q;
@@ -486,69 +354,25 @@ GS_INLINE void adam_rows(float *P, float *M, float *V, const float *g, int rows,
   }
 }
 
-// adam_rows for the lazy SH Adam (LazySH): only the rows with from[r] >= 0
-// (visible: their gradient is in g) are touched -- each element first
-// catches up the zero-gradient steps (from[r], t - 1], then takes step t.
-template <int WID, int GS>
-GS_INLINE void adam_rows_lazy(float *P, float *M, float *V, const float *g, const int *from,
-                              int rows, int lane, float ss, const AdamSH &ad, int t, bool dc,
-                              const LazySH &lz) {
-  const int count = rows * WID, n4 = count >> 2;
-  float4 *P4 = reinterpret_cast<float4 *>(P);
-  float4 *M4 = reinterpret_cast<float4 *>(M);
-  float4 *V4 = reinterpret_cast<float4 *>(V);
-  auto one = [&](float &p, float &m, float &v, int e) {
-    const int r = e / WID;
-    const int f = from[r];
-    if (f < 0) return;
-    lazy_catch_up(p, m, v, f, t - 1, dc, lz);
-    adam_update(p, g[r * GS + (e - r * WID)], m, v, ad.b1, ad.b2, ad.eps, ss, ad.ib);
-  };
-  for (int q = lane; q < n4; q += 64) {
-    const int e = 4 * q;
-    if (from[e / WID] < 0 && from[(e + 3) / WID] < 0) continue;  // WID >= 3: rows of e..e+3
-    float4 p = P4[q], m = M4[q], v = V4[q];
-    one(p.x, m.x, v.x, e);
-    one(p.y, m.y, v.y, e + 1);
-    one(p.z, m.z, v.z, e + 2);
-    one(p.w, m.w, v.w, e + 3);
-    P4[q] = p;
-    M4[q] = m;
-    V4[q] = v;
-  }
-  for (int e = 4 * n4 + lane; e < count; e += 64) {
-    if (from[e / WID] < 0) continue;
-    float pp = P[e], mm = M[e], vv = V[e];
-    one(pp, mm, vv, e);
-    P[e] = pp;
-    M[e] = mm;
-    V[e] = vv;
-  }
-}
-
 // CAMS (FUSED): the row of lane i is Gaussian i seen from all C cameras of
 // fz (C = fz's camera count, rows c * N + i of radii / v_colors): the
 // coefficients are read once, the gradient rows and the means gradient
 // (v_dirs [N, 3]) are summed over the cameras in registers -- the shared
 // coefficients of a Gaussian-sharded render's N-camera colours, whose sum
 // is also what the fused Adam needs.  C == 1 is the one-camera kernel.
-// LAZY (ADAM, C == 1): the lazy SH Adam (LazySH); a template of its own so
-// that the eager kernels' code -- and their bits -- stay as they were.
 template <int DEG, bool FUSED, int KR = (DEG + 1) * (DEG + 1) - 1, bool ADAM = false,
-          bool CAMS = false, bool LAZY = false, int AU = 1>
+          bool CAMS = false>
 __global__ void __launch_bounds__(256)
 sh_bwd_staged_kernel(int64_t n, Coeffs cf, const float *__restrict__ dirs,
                      const uint8_t *__restrict__ masks, const float *__restrict__ v_colors,
                      VCoeffs vc, float *__restrict__ v_dirs, Fused fz, AdamSH ad = AdamSH{},
-                     int C = 1, LazySH lz = LazySH{}) {
+                     int C = 1) {
   static_assert(!CAMS || FUSED, "the camera loop is the fused colour path's");
-  static_assert(!LAZY || (ADAM && !CAMS), "the lazy SH Adam: one camera, Adam fused");
   if (!CAMS) C = 1;
   constexpr int NB = (DEG + 1) * (DEG + 1), WR = 3 * KR, RSR = WR | 1;
   static_assert(KR >= NB - 1, "KR covers the active coefficients");
   __shared__ float l_dc[4][64 * 3];               // row stride 3 (odd)
   __shared__ float l_rest[4][64 * (RSR > 1 ? RSR : 1)];  // odd row stride
-  __shared__ int l_from[4][LAZY ? 64 : 1];        // lazy SH Adam: a row's last step, -1 = skip
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t i0 = (int64_t)blockIdx.x * 256 + wid * 64;
   if (i0 >= n) return;
@@ -656,28 +480,11 @@ sh_bwd_staged_kernel(int64_t n, Coeffs cf, const float *__restrict__ dirs,
       a.ssr = ad.hyper[1];
       a.ib = ad.hyper[2];
     }
-    if (LAZY) {  // lazy: visible rows only, after their catch-up
-      const int t = lazy_step(lz);
-      if (blockIdx.x == 0 && threadIdx.x == 0) lz.fac[t % lz.R] = make_float4(a.ss0, a.ssr, a.ib, 0.f);
-      int *fr = l_from[wid];
-      if (lane < rows) fr[lane] = on ? lz.last[i] : -1;
-      __builtin_amdgcn_wave_barrier();
-      adam_rows_lazy<3, 3>(const_cast<float *>(cf.c0) + i0 * 3, a.m0 + i0 * 3, a.v0 + i0 * 3, sd,
-                           fr, rows, lane, a.ss0, a, t, true, lz);
-      if (WR > 0)
-        adam_rows_lazy<(WR > 0 ? WR : 1), RSR>(const_cast<float *>(cf.cr) + i0 * WR,
-                                               a.mr + i0 * WR, a.vr + i0 * WR, sr, fr, rows,
-                                               lane, a.ssr, a, t, false, lz);
-      __builtin_amdgcn_wave_barrier();
-      if (on) lz.last[i] = t;
-      return;
-    }
-    adam_rows<3, 3, AU>(const_cast<float *>(cf.c0) + i0 * 3, a.m0 + i0 * 3, a.v0 + i0 * 3, sd,
-                        rows, lane, a.ss0, a);
+    adam_rows<3, 3>(const_cast<float *>(cf.c0) + i0 * 3, a.m0 + i0 * 3, a.v0 + i0 * 3, sd,
+                    rows, lane, a.ss0, a);
     if (WR > 0)
-      adam_rows<(WR > 0 ? WR : 1), RSR, AU>(const_cast<float *>(cf.cr) + i0 * WR,
-                                             a.mr + i0 * WR, a.vr + i0 * WR, sr, rows, lane,
-                                             a.ssr, a);
+      adam_rows<(WR > 0 ? WR : 1), RSR>(const_cast<float *>(cf.cr) + i0 * WR, a.mr + i0 * WR,
+                                         a.vr + i0 * WR, sr, rows, lane, a.ssr, a);
     return;
   }
   {  // gradient rows out, lane-contiguous
@@ -692,42 +499,6 @@ sh_bwd_staged_kernel(int64_t n, Coeffs cf, const float *__restrict__ dirs,
         gr[(int64_t)wr.rr * vc.sr + wr.c] = sr[wr.rr * RSR + wr.c];
     }
   }
-}
-
-// Lazy SH Adam flush: every element brought up to Adam step T (the
-// zero-gradient steps its row skipped); one lane per element of the DC
-// ([N,3]) and rest ([N,45]) arrays, wave-uniform step loop.  last[] = T is
-// written by a second launch (every element reads its row's last here).
-__global__ void __launch_bounds__(256)
-sh_lazy_flush_kernel(int64_t N, float *__restrict__ p0, float *__restrict__ pr, LazySH lz,
-                     int T) {
-  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int64_t n0 = N * 3, n1 = N * 45;
-  const bool dc = e < n0;
-  const bool ok = e < n0 + n1;
-  const int64_t q = dc ? e : e - n0;
-  const int64_t row = ok ? (dc ? q / 3 : q / 45) : 0;
-  const int from = ok ? lz.last[row] : T;
-  float pp[1] = {0.f}, mm[1] = {0.f}, vv[1] = {0.f};
-  const bool d1[1] = {dc};
-  if (ok && from < T) {
-    pp[0] = dc ? p0[q] : pr[q];
-    mm[0] = dc ? lz.m0[q] : lz.mr[q];
-    vv[0] = dc ? lz.v0[q] : lz.vr[q];
-  }
-  lazy_catch_up_wave<1>(pp, mm, vv, from, T, d1, lz);
-  if (ok && from < T) {
-    if (dc) {
-      p0[q] = pp[0]; lz.m0[q] = mm[0]; lz.v0[q] = vv[0];
-    } else {
-      pr[q] = pp[0]; lz.mr[q] = mm[0]; lz.vr[q] = vv[0];
-    }
-  }
-}
-
-__global__ void __launch_bounds__(256) sh_lazy_set_kernel(int64_t N, int32_t *last, int T) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i < N) last[i] = T;
 }
 
 }  // namespace gs
@@ -823,60 +594,6 @@ extern "C" int gsplat_hip_sh_colors_fwd(int degree, int C, int64_t N, int64_t n_
   return 0;
 }
 
-// The colour forward of the lazy SH Adam (ABI 28; C == 1, sh0 [N,1,3] +
-// shN [N,15,3] with their moments): each visible row's coefficients brought
-// to Adam step t - 1 in registers (t = step, or *step_device when non-null)
-// from its last[] and the factor ring fac [R] x (ss0, ss_rest, ib, 0); the
-// colours equal those of the eagerly updated coefficients bit for bit.
-extern "C" int gsplat_hip_sh_colors_fwd_lazy(int degree, int64_t N, const float *means,
-                                             const float *viewmats, float *coeffs,
-                                             float *coeffs_rest, const int32_t *radii,
-                                             float *colors, float *m0, float *v0, float *m_rest,
-                                             float *v_rest, int32_t *last, float *fac, int R,
-                                             int step, const int64_t *step_device, float beta1,
-                                             float beta2, float eps, const int32_t *skip_device,
-                                             void *stream) {
-  if (N <= 0) return 0;
-  GS_REQUIRE(degree >= 0 && degree <= 3, "sh_colors_fwd_lazy: degree %d not in [0, 3]", degree);
-  GS_REQUIRE(coeffs && coeffs_rest && m0 && v0 && m_rest && v_rest && last && fac && R > 0,
-             "sh_colors_fwd_lazy: null buffer");
-  GS_REQUIRE(step_device || step >= 1, "sh_colors_fwd_lazy: step must be >= 1");
-  const Coeffs cf{coeffs, coeffs_rest, 3, 45};
-  const Fused fz{means, viewmats, radii, N};
-  const LazySH lz{last, reinterpret_cast<float4 *>(fac), R, step, step_device, m0, v0, m_rest,
-                  v_rest, beta1, beta2, eps, skip_device};
-  dim3 grid((unsigned)((N + 255) / 256));
-  hipStream_t st = (hipStream_t)stream;
-#define GS_SH_FWDL(D)                                                                       \
-  case D:                                                                                   \
-    hipLaunchKernelGGL((sh_fwd_lazy_kernel<D>), grid, dim3(256), 0, st, N, cf, colors, fz,   \
-                       lz);                                                                 \
-    break;
-  switch (degree) { GS_SH_FWDL(0) GS_SH_FWDL(1) GS_SH_FWDL(2) GS_SH_FWDL(3) }
-#undef GS_SH_FWDL
-  GS_CHECK_LAUNCH("sh_colors_fwd_lazy");
-  return 0;
-}
-
-// Flush of the lazy SH Adam: rows brought to Adam step T (see LazySH).
-extern "C" int gsplat_hip_sh_lazy_flush(int64_t N, float *coeffs, float *coeffs_rest, float *m0,
-                                        float *v0, float *m_rest, float *v_rest, int32_t *last,
-                                        float *fac, int R, int T, float beta1, float beta2,
-                                        float eps, void *stream) {
-  if (N <= 0 || T <= 0) return 0;
-  GS_REQUIRE(coeffs && coeffs_rest && m0 && v0 && m_rest && v_rest && last && fac && R > 0,
-             "sh_lazy_flush: null buffer");
-  const LazySH lz{last, reinterpret_cast<float4 *>(fac), R, T, nullptr, m0, v0, m_rest, v_rest,
-                  beta1, beta2, eps, nullptr};
-  hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(sh_lazy_flush_kernel, dim3((unsigned)((N * 48 + 255) / 256)), dim3(256), 0,
-                     st, N, coeffs, coeffs_rest, lz, T);
-  hipLaunchKernelGGL(sh_lazy_set_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, st, N,
-                     last, T);
-  GS_CHECK_LAUNCH("sh_lazy_flush");
-  return 0;
-}
-
 extern "C" int gsplat_hip_sh_colors_bwd(int degree, int C, int64_t N, int64_t n_coeff_rows, int K,
                                         const float *means, const float *viewmats,
                                         const float *coeffs, const float *coeffs_rest,
@@ -919,8 +636,7 @@ extern "C" int gsplat_hip_sh_colors_bwd(int degree, int C, int64_t N, int64_t n_
 static int sh_colors_bwd_adam_launch(int degree, int C, int64_t N, const float *means,
                                      const float *viewmats, float *coeffs, float *coeffs_rest,
                                      const int32_t *radii, const float *v_colors, float *v_dirs,
-                                     const AdamSH &ad, hipStream_t st,
-                                     const LazySH &lz = LazySH{});
+                                     const AdamSH &ad, hipStream_t st);
 
 extern "C" int gsplat_hip_sh_colors_bwd_adam(int degree, int C, int64_t N, const float *means,
                                              const float *viewmats, float *coeffs,
@@ -928,8 +644,7 @@ extern "C" int gsplat_hip_sh_colors_bwd_adam(int degree, int C, int64_t N, const
                                              const float *v_colors, float *v_dirs, float *m0,
                                              float *v0, float *m_rest, float *v_rest, float lr0,
                                              float lr_rest, float beta1, float beta2, float eps,
-                                             int step, int32_t *last, float *fac, int R,
-                                             void *stream) {
+                                             int step, void *stream) {
   if (N <= 0) return 0;
   GS_REQUIRE(degree >= 0 && degree <= 3, "sh_colors_bwd_adam: degree %d not in [0, 3]", degree);
   GS_REQUIRE(coeffs && coeffs_rest && m0 && v0 && m_rest && v_rest,
@@ -941,11 +656,8 @@ extern "C" int gsplat_hip_sh_colors_bwd_adam(int degree, int C, int64_t N, const
   const double bc1 = 1.0 - pow((double)beta1, step), bc2 = 1.0 - pow((double)beta2, step);
   AdamSH ad{m0, v0, m_rest, v_rest, (float)(lr0 / bc1), (float)(lr_rest / bc1),
             (float)(1.0 / sqrt(bc2)), beta1, beta2, eps, nullptr, nullptr};
-  GS_REQUIRE(!last || (fac && R > 0 && C == 1), "sh_colors_bwd_adam: lazy SH Adam needs C == 1");
-  const LazySH lz{last, reinterpret_cast<float4 *>(fac), R, step, nullptr, m0, v0, m_rest,
-                  v_rest, beta1, beta2, eps, nullptr};
   return sh_colors_bwd_adam_launch(degree, C, N, means, viewmats, coeffs, coeffs_rest, radii,
-                                   v_colors, v_dirs, ad, (hipStream_t)stream, lz);
+                                   v_colors, v_dirs, ad, (hipStream_t)stream);
 }
 
 // The same with the step-dependent factors read on the device (ABI 20, a
@@ -960,9 +672,7 @@ extern "C" int gsplat_hip_sh_colors_bwd_adam_dev(int degree, int C, int64_t N,
                                                  float *v0, float *m_rest, float *v_rest,
                                                  const float *hyper_device, float beta1,
                                                  float beta2, float eps,
-                                                 const int32_t *skip_device, int32_t *last,
-                                                 float *fac, int R, const int64_t *step_device,
-                                                 void *stream) {
+                                                 const int32_t *skip_device, void *stream) {
   if (N <= 0) return 0;
   GS_REQUIRE(degree >= 0 && degree <= 3, "sh_colors_bwd_adam: degree %d not in [0, 3]", degree);
   GS_REQUIRE(coeffs && coeffs_rest && m0 && v0 && m_rest && v_rest && hyper_device,
@@ -971,44 +681,24 @@ extern "C" int gsplat_hip_sh_colors_bwd_adam_dev(int degree, int C, int64_t N,
                (uintptr_t)m_rest | (uintptr_t)v_rest) & 15) == 0,
              "sh_colors_bwd_adam: coefficient and moment buffers must be 16-B aligned");
   AdamSH ad{m0, v0, m_rest, v_rest, 0.f, 0.f, 0.f, beta1, beta2, eps, hyper_device, skip_device};
-  GS_REQUIRE(!last || (fac && R > 0 && C == 1 && step_device),
-             "sh_colors_bwd_adam_dev: lazy SH Adam needs C == 1 and step_device");
-  const LazySH lz{last, reinterpret_cast<float4 *>(fac), R, 0, step_device, m0, v0, m_rest,
-                  v_rest, beta1, beta2, eps, skip_device};
   return sh_colors_bwd_adam_launch(degree, C, N, means, viewmats, coeffs, coeffs_rest, radii,
-                                   v_colors, v_dirs, ad, (hipStream_t)stream, lz);
+                                   v_colors, v_dirs, ad, (hipStream_t)stream);
 }
 
 static int sh_colors_bwd_adam_launch(int degree, int C, int64_t N, const float *means,
                                      const float *viewmats, float *coeffs, float *coeffs_rest,
                                      const int32_t *radii, const float *v_colors, float *v_dirs,
-                                     const AdamSH &ad, hipStream_t st, const LazySH &lz) {
+                                     const AdamSH &ad, hipStream_t st) {
   GS_REQUIRE(C >= 1, "sh_colors_bwd_adam: C=%d cameras", C);
   Coeffs cf{coeffs, coeffs_rest, 3, 45};
   VCoeffs vc{nullptr, nullptr, 3, 45};
   const Fused fz{means, viewmats, radii, N};
   dim3 grid((unsigned)((N + 255) / 256));
-  // the Adam phase's loads, unrolled 4 slots per lane (GSPLAT_HIP_SH_ADAM_U=1: one)
-  static const int au = [] {
-    const char *e = getenv("GSPLAT_HIP_SH_ADAM_U");
-    return e && atoi(e) == 1 ? 1 : 4;
-  }();
 #define GS_SH_BWD_ADAM(D)                                                                        \
   case D:                                                                                        \
-    if (C == 1 && lz.last)                                                                       \
-      hipLaunchKernelGGL((sh_bwd_staged_kernel<D, true, 15, true, false, true>), grid, dim3(256),  \
-                         0, st, N, cf, nullptr, nullptr, v_colors, vc, v_dirs, fz, ad, 1, lz);   \
-    else if (C == 1 && au == 4)                                                                  \
-      hipLaunchKernelGGL((sh_bwd_staged_kernel<D, true, 15, true, false, false, 4>), grid,       \
-                         dim3(256), 0, st, N, cf, nullptr, nullptr, v_colors, vc, v_dirs, fz, ad, \
-                         1);                                                                     \
-    else if (C == 1)                                                                             \
+    if (C == 1)                                                                                  \
       hipLaunchKernelGGL((sh_bwd_staged_kernel<D, true, 15, true>), grid, dim3(256), 0, st, N,   \
                          cf, nullptr, nullptr, v_colors, vc, v_dirs, fz, ad, 1);                 \
-    else if (au == 4)                                                                            \
-      hipLaunchKernelGGL((sh_bwd_staged_kernel<D, true, 15, true, true, false, 4>), grid,        \
-                         dim3(256), 0, st, N, cf, nullptr, nullptr, v_colors, vc, v_dirs, fz, ad, \
-                         C);                                                                     \
     else                                                                                         \
       hipLaunchKernelGGL((sh_bwd_staged_kernel<D, true, 15, true, true>), grid, dim3(256), 0, st, \
                          N, cf, nullptr, nullptr, v_colors, vc, v_dirs, fz, ad, C);              \

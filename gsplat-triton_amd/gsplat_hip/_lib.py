@@ -12,7 +12,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GSPLAT_HIP_LIB", os.path.join(_HERE, "libgsplat_hip.so"))
-ABI_VERSION = 28
+ABI_VERSION = 29
 
 _p = ctypes.c_void_p
 _i32 = ctypes.c_int
@@ -90,15 +90,9 @@ _SIGS = {
     "gsplat_hip_activate_bwd": (_i32, [_i64, _i64, _p, _p, _p, _p, _p, _p, _p]),
     "gsplat_hip_adam_step": (_i32, [_i32, _p, _p, _p, _p, _p, _p, _f, _f, _f, _i32, _p]),
     "gsplat_hip_sh_colors_bwd_adam": (_i32, [_i32, _i32, _i64, _p, _p, _p, _p, _p, _p, _p, _p,
-                                             _p, _p, _p, _f, _f, _f, _f, _f, _i32, _p, _p, _i32,
-                                             _p]),
+                                             _p, _p, _p, _f, _f, _f, _f, _f, _i32, _p]),
     "gsplat_hip_sh_colors_bwd_adam_dev": (_i32, [_i32, _i32, _i64, _p, _p, _p, _p, _p, _p, _p,
-                                                 _p, _p, _p, _p, _p, _f, _f, _f, _p, _p, _p, _i32,
-                                                 _p, _p]),
-    "gsplat_hip_sh_colors_fwd_lazy": (_i32, [_i32, _i64, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p,
-                                             _p, _p, _i32, _i32, _p, _f, _f, _f, _p, _p]),
-    "gsplat_hip_sh_lazy_flush": (_i32, [_i64, _p, _p, _p, _p, _p, _p, _p, _p, _i32, _i32, _f, _f,
-                                        _f, _p]),
+                                                 _p, _p, _p, _p, _p, _f, _f, _f, _p, _p]),
     "gsplat_hip_sh_colors_bwd_sum": (_i32, [_i32, _i32, _i64, _p, _p, _p, _p, _p, _p, _p, _p, _p,
                                             _p]),
     "gsplat_hip_adam_step_dev": (_i32, [_i32, _p, _p, _p, _p, _p, _p, _p, _p, _f, _f, _f, _p, _p]),

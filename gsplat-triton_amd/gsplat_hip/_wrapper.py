@@ -674,7 +674,7 @@ class ShAdamInBackward:
     `applied` tells the caller whether it ran (else: take the normal step)."""
 
     def __init__(self, coeffs, coeffs_rest, m0, v0, m_rest, v_rest, lr0, lr_rest, betas, eps,
-                 step, hyper=None, skip=None, lazy=None, step_dev=None):
+                 step, hyper=None, skip=None):
         self.coeffs, self.coeffs_rest = coeffs, coeffs_rest
         self.moments = (m0, v0, m_rest, v_rest)
         self.lr0, self.lr_rest, self.betas, self.eps, self.step = lr0, lr_rest, betas, eps, step
@@ -682,10 +682,6 @@ class ShAdamInBackward:
         # 1 / sqrt(bc2)} in a device f32[3] view, and a device i32 void-step
         # flag (gsplat_hip_sh_colors_bwd_adam_dev)
         self.hyper, self.skip = hyper, skip
-        # lazy SH Adam (LazyShAdam, one camera): rows outside the view skip
-        # their zero-gradient steps until they are next visible or flushed;
-        # step_dev: the step count on the device (the captured step)
-        self.lazy, self.step_dev = lazy, step_dev
         self.applied = False
 
     def matches(self, base, rest, C, N, K, n_rows, degree):
@@ -697,37 +693,6 @@ class ShAdamInBackward:
                 and degree == 3 and base.data_ptr() == self.coeffs.data_ptr()
                 and rest.data_ptr() == self.coeffs_rest.data_ptr()
                 and self.coeffs.is_contiguous() and self.coeffs_rest.is_contiguous())
-
-
-class LazyShAdam:
-    """State of the lazy SH Adam (gsplat_hip_sh_colors_fwd_lazy / the lazy
-    form of gsplat_hip_sh_colors_bwd_adam / gsplat_hip_sh_lazy_flush, ABI 28):
-    last i32[N] = the Adam steps applied to each Gaussian's SH row, fac =
-    a ring of R steps' factors.  Rows outside the view take their
-    zero-gradient steps when next visible (or at a flush) -- bit-identical to
-    the eager update sequence, without touching those rows every step."""
-
-    R = 4096
-
-    def __init__(self, n, device, steps_done=0):
-        self.last = torch.full((n,), int(steps_done), dtype=torch.int32, device=device)
-        self.fac = torch.zeros(self.R, 4, dtype=torch.float32, device=device)
-        self.flushed_at = int(steps_done)  # every row current at this step
-
-    def flush(self, coeffs, coeffs_rest, moments, T, betas, eps):
-        """Every row brought to Adam step T (rows must have been current at
-        most R - 1 steps ago)."""
-        m0, v0, mr, vr = moments
-        _lib.call("gsplat_hip_sh_lazy_flush", coeffs.shape[0], _ptr(coeffs), _ptr(coeffs_rest),
-                  _ptr(m0), _ptr(v0), _ptr(mr), _ptr(vr), _ptr(self.last), _ptr(self.fac),
-                  self.R, int(T), ctypes.c_float(betas[0]), ctypes.c_float(betas[1]),
-                  ctypes.c_float(eps), _stream())
-        self.flushed_at = int(T)
-
-    def resize(self, n, T):
-        """After a refine (new rows, every row current at step T)."""
-        self.last = torch.full((n,), int(T), dtype=torch.int32, device=self.last.device)
-        self.flushed_at = int(T)
 
 
 class _SHColors(torch.autograd.Function):
@@ -751,22 +716,8 @@ class _SHColors(torch.autograd.Function):
         C, N = radii.shape
         K = coeffs.shape[-2] + (0 if rest is None else coeffs_rest.shape[-2])
         colors = torch.empty(C, N, 3, device=means.device, dtype=torch.float32)
-        fa = None if fusion is None else fusion.sh_adam
-        if (fa is not None and fa.lazy is not None and C == 1
-                and fa.matches(base, rest, C, N, K, n_rows, int(sh_degree))):
-            # lazy SH Adam: the visible rows' coefficients brought to the
-            # previous step in registers
-            m0, v0, mr, vr = fa.moments
-            lz = fa.lazy
-            _lib.call("gsplat_hip_sh_colors_fwd_lazy", int(sh_degree), N, _ptr(means),
-                      _ptr(viewmats), _ptr(base), _ptr(rest), _ptr(radii), _ptr(colors), _ptr(m0),
-                      _ptr(v0), _ptr(mr), _ptr(vr), _ptr(lz.last), _ptr(lz.fac), lz.R,
-                      int(fa.step) if fa.step_dev is None else 0, _ptr(fa.step_dev),
-                      ctypes.c_float(fa.betas[0]), ctypes.c_float(fa.betas[1]),
-                      ctypes.c_float(fa.eps), _ptr(fa.skip), _stream())
-        else:
-            _lib.call("gsplat_hip_sh_colors_fwd", int(sh_degree), C, N, n_rows, K, _ptr(means),
-                      _ptr(viewmats), _ptr(base), _ptr(rest), _ptr(radii), _ptr(colors), _stream())
+        _lib.call("gsplat_hip_sh_colors_fwd", int(sh_degree), C, N, n_rows, K, _ptr(means),
+                  _ptr(viewmats), _ptr(base), _ptr(rest), _ptr(radii), _ptr(colors), _stream())
         ctx.save_for_backward(means, viewmats, base, rest, radii)
         ctx.sh_degree, ctx.n_rows, ctx.K = int(sh_degree), n_rows, K
         ctx.coeff_shape = coeffs.shape
@@ -794,22 +745,19 @@ class _SHColors(torch.autograd.Function):
                   torch.empty(C, N, 3, device=dev)) if want_means else None
         if fused_adam:
             m0, v0, mr, vr = fa.moments
-            lz = fa.lazy if C == 1 else None
-            lzp = (_ptr(lz.last), _ptr(lz.fac), lz.R) if lz is not None else (None, None, 0)
             if fa.hyper is not None:
                 _lib.call("gsplat_hip_sh_colors_bwd_adam_dev", ctx.sh_degree, C, N, _ptr(means),
                           _ptr(viewmats), _ptr(base), _ptr(rest), _ptr(radii), _ptr(v_colors),
                           _ptr(v_dirs), _ptr(m0), _ptr(v0), _ptr(mr), _ptr(vr), _ptr(fa.hyper),
                           ctypes.c_float(fa.betas[0]), ctypes.c_float(fa.betas[1]),
-                          ctypes.c_float(fa.eps), _ptr(fa.skip), *lzp,
-                          _ptr(fa.step_dev if lz is not None else None), _stream())
+                          ctypes.c_float(fa.eps), _ptr(fa.skip), _stream())
             else:
                 _lib.call("gsplat_hip_sh_colors_bwd_adam", ctx.sh_degree, C, N, _ptr(means),
                           _ptr(viewmats), _ptr(base), _ptr(rest), _ptr(radii), _ptr(v_colors),
                           _ptr(v_dirs), _ptr(m0), _ptr(v0), _ptr(mr), _ptr(vr),
                           ctypes.c_float(fa.lr0), ctypes.c_float(fa.lr_rest),
                           ctypes.c_float(fa.betas[0]), ctypes.c_float(fa.betas[1]),
-                          ctypes.c_float(fa.eps), int(fa.step), *lzp, _stream())
+                          ctypes.c_float(fa.eps), int(fa.step), _stream())
             fa.applied = True
             return (None, fusion.take_means_grad(v_dirs), None, None, None, None, None)
         if shared:

@@ -143,8 +143,8 @@ class GraphStep:
         self.lag = int(lag)  # steps the host may run ahead of its overflow check
         self.capacity = None if capacity is None else int(capacity)
         # device input of the graph: one 2-KB block per step -- f32 [0, 64)
-        # the Adam factors, i64 at byte 256 the rank's camera index, i64 at 264
-        # the Adam step t, f32 viewmats [W][16] at byte 512 and Ks [W][9] at
+        # the Adam factors, i64 at byte 256 the rank's camera index, f32
+        # viewmats [W][16] at byte 512 and Ks [W][9] at
         # byte 1024 (W = the world's cameras: 1, or the Gaussian-sharded job's
         # ranks), i64 at SLOT - 8 the ring slot (written by
         # gsplat_hip_step_fetch)
@@ -154,7 +154,6 @@ class GraphStep:
         self.blk = torch.zeros(self.SLOT, dtype=torch.uint8, device=dev)
         self.scal = self.blk[:256].view(torch.float32)
         self.cam = self.blk[256:264].view(torch.int64)
-        self.adam_step = self.blk[264:272].view(torch.int64)  # this step's Adam step t
         self.vm_w = self.blk[512:512 + 64 * self.W].view(torch.float32).view(self.W, 4, 4)
         self.K_w = self.blk[1024:1024 + 36 * self.W].view(torch.float32).view(self.W, 3, 3)
         r = tr.rank if self.gshard else 0
@@ -168,11 +167,6 @@ class GraphStep:
         self._slot_ev = [None] * self.RING
         self._vm_host = tr.viewmats.detach().float().cpu().numpy()
         self._K_host = tr.Ks.detach().float().cpu().numpy()
-        # SH colours (and their backward) on a second captured stream,
-        # concurrent with the tile intersection (GSPLAT_HIP_SIDE_SH)
-        self.side = None
-        if not self.gshard and os.environ.get("GSPLAT_HIP_SIDE_SH", "0") == "1":
-            self.side = torch.cuda.Stream(device=dev)
         self.graph = None
         self.key = None
         self.counts = None  # the graph's isect counts (device i64[4])
@@ -201,12 +195,10 @@ class GraphStep:
         if tr.sh_adam_in_bwd:
             o = tr.opt
             i0, i1 = names.index("sh0"), names.index("shN")
-            lazy = tr.sh_lazy if (getattr(tr, "sh_lazy", None) is not None and deg == 3) else None
             fa = _wrapper.ShAdamInBackward(
                 p["sh0"].data, p["shN"].data, o.exp_avg[i0], o.exp_avg_sq[i0], o.exp_avg[i1],
                 o.exp_avg_sq[i1], o.lrs[i0], o.lrs[i1], o.betas, o.eps, 1,
-                hyper=self.scal[sh_off:sh_off + 3], skip=self.status, lazy=lazy,
-                step_dev=self.adam_step if lazy is not None else None)
+                hyper=self.scal[sh_off:sh_off + 3], skip=self.status)
         fusion = _wrapper.StepFusion(sh_adam=fa, geom=tr.geom_fuse) \
             if (fa is not None or tr.geom_fuse) else None
         # the first launch also fetches this step's input block (the ring slot)
@@ -221,7 +213,7 @@ class GraphStep:
             tr.height, sh_degree=deg, packed=False, near_plane=0.01, far_plane=1e10,
             radius_clip=0.0, rasterize_mode="classic", _fusion=fusion,
             _isect_capacity=self.capacity, _isect_status=self.status,
-            _isect_report=(self.ring_out.dev, self.slot), _colors_stream=self.side, **dkw)
+            _isect_report=(self.ring_out.dev, self.slot), **dkw)
         grad_box = {}
         meta["means2d"].register_hook(lambda g: grad_box.__setitem__("g", g))
         loss = tr._regularise(l1_ssim_loss(colors, tr.targets, tr.ssim_lambda, gt_index=self.cam))
@@ -230,11 +222,6 @@ class GraphStep:
         if stats and "g" in grad_box:  # DefaultStrategy statistics (until refine_stop_iter)
             update_state_(tr.grad2d, tr.count, grad_box["g"], meta["radii"], meta["width"],
                           meta["height"], meta["n_cameras"], skip=self.status)
-        if self.side is not None:  # the SH backward ran on the side stream
-            cur = torch.cuda.current_stream(self.dev)
-            cur.wait_stream(self.side)
-            if fusion is not None and fusion.v_dirs is not None:
-                fusion.v_dirs.record_stream(cur)
         skip = tr._sh_skip(fusion)
         assert tuple(i for i in range(self.n_groups) if i not in skip) == tuple(idx), \
             (skip, idx)
@@ -325,7 +312,6 @@ class GraphStep:
         b[512:512 + 64 * self.W].view(np.float32)[:] = self._vm_host[world_ci].reshape(-1)
         b[1024:1024 + 36 * self.W].view(np.float32)[:] = self._K_host[world_ci].reshape(-1)
         b[256:264].view(np.int64)[0] = ci
-        b[264:272].view(np.int64)[0] = step  # the lazy SH Adam's step count
         if tr.max_steps:
             tr._set_means_lr(lrs[0])
 

@@ -76,7 +76,6 @@ def rasterization(
     _isect_report=None,
     _world_cameras=None,
     _world_counts=None,
-    _colors_stream=None,
 ) -> Tuple[Tensor, Tensor, Dict]:
     """Rasterize N 3D Gaussians to C images (gsplat/rendering.py:44-598).
 
@@ -94,12 +93,7 @@ def rasterization(
     cameras in rank order and `_world_counts` = every rank's Gaussian count,
     when the caller knows them (a trainer's camera schedule and shard sizes):
     the all-gathers of gsplat/rendering.py:303-308 -- one of them a host
-    read -- are then skipped.
-    `_colors_stream` (a torch.cuda.Stream, the captured training step): the
-    SH colours are evaluated on that stream, concurrently with the tile
-    intersection (latency-bound launches that leave most CUs idle), and
-    joined before their first use; their backward then also runs there
-    (autograd's stream rule), so the CALLER joins it after backward."""
+    read -- are then skipped."""
     meta = {}
     N = means.shape[0]
     C = viewmats.shape[0]
@@ -234,19 +228,10 @@ def rasterization(
     # intersection -- lets a sharded optimizer's all-gather of the SH
     # coefficients overlap projection and isect (train_step.Trainer)
     late = _colors_ready is not None and not packed and not distributed
-    side = _colors_stream
-    if late or packed or distributed or sh_degree is None or render_mode != "RGB":
-        side = None
     if not late:
         if _colors_ready is not None:  # packed / distributed: wait before, not after
             _colors_ready()
-        if side is not None:
-            main = torch.cuda.current_stream(device)
-            side.wait_stream(main)
-            with torch.cuda.stream(side):
-                colors = eval_colors(colors)
-        else:
-            colors = eval_colors(colors)
+        colors = eval_colors(colors)
 
     if distributed:  # gsplat/rendering.py:413-494
         if packed:
@@ -305,7 +290,7 @@ def rasterization(
     ranked = pending_isects.will_rank(capped)
     if not late:
         colors, backgrounds = add_depth(colors, backgrounds)
-        if colors.shape[-1] <= channel_chunk and not ranked and side is None:
+        if colors.shape[-1] <= channel_chunk and not ranked:
             # queued before the isect sync, so the GPU has it to run while the
             # host waits for n_isects (rank-indexed records wait for the ranks)
             records = pack_render_records(means2d, conics, colors, opacities, tile_size,
@@ -323,13 +308,10 @@ def rasterization(
         isect_offsets = isect_offset_encode(isect_ids, C, tile_width, tile_height,
                                             _n_isects_device=counts)
     ranks = pending_isects.ranks
-    if side is not None:  # join the colours (allocated on the side stream)
-        main.wait_stream(side)
-        colors.record_stream(main)
     if late:
         _colors_ready()
         colors, backgrounds = add_depth(eval_colors(colors), backgrounds)
-    if (late or ranks is not None or side is not None) and colors.shape[-1] <= channel_chunk:
+    if (late or ranks is not None) and colors.shape[-1] <= channel_chunk:
         records = pack_render_records(means2d, conics, colors, opacities, tile_size,
                                       tiles_per_gauss, ranks)
     meta.update({"tile_width": tile_width, "tile_height": tile_height,

@@ -235,17 +235,6 @@ class Trainer:
         self.sh_adam_in_bwd = (fused and not self.sharded and not self.defer_sh
                                and (world_size == 1 or self.gshard)
                                and os.environ.get("GSPLAT_HIP_SH_ADAM_IN_BWD", "1") != "0")
-        # lazy SH Adam (one camera per step, the fused SH Adam at degree 3):
-        # rows outside the view take their zero-gradient Adam steps only when
-        # next visible or at a flush (Trainer.sync) -- bit-identical to the
-        # eager sequence, without their HBM traffic every step
-        # (_wrapper.LazyShAdam; GSPLAT_HIP_SH_LAZY=0 turns it off)
-        self.sh_lazy = None
-        self._lazy_on = False  # rows may be behind: lazy steps since the last flush
-        if (self.sh_adam_in_bwd and world_size == 1 and not self.gshard
-                and torch.device(device).type == "cuda"
-                and os.environ.get("GSPLAT_HIP_SH_LAZY", "1") != "0"):
-            self.sh_lazy = _wrapper.LazyShAdam(N, device)
         # the exp / sigmoid VJPs and the means-gradient sum formed inside the
         # geometry groups' Adam (gsplat_hip_adam_step_ex): at one rank, and
         # under the sharded optimizer on the reduced shard (ShardedAdam.step)
@@ -380,49 +369,12 @@ class Trainer:
 
     def sync(self):
         """Order the current stream after any optimizer communication still in
-        flight (the sharded optimizer's deferred all-gathers) and bring every
-        lazily updated SH row up to date: call before reading the parameters
-        outside the training step (checkpoint, eval, refine)."""
+        flight (the sharded optimizer's deferred all-gathers): call before
+        reading the parameters outside the training step (checkpoint, eval)."""
         if getattr(self, "_graph", None) is not None:
             self._graph.sync()
         if self.sharded or getattr(self, "defer_sh", False):
             self.opt.wait()
-        self._lazy_flush()
-
-    def _lazy_flush(self):
-        lz = getattr(self, "sh_lazy", None)
-        if lz is None or not self._lazy_on:
-            return
-        T = self.opt.step_count
-        if lz.flushed_at < T:
-            names = list(self.params)
-            i0, i1 = names.index("sh0"), names.index("shN")
-            o = self.opt
-            lz.flush(self.params["sh0"].data, self.params["shN"].data,
-                     (o.exp_avg[i0], o.exp_avg_sq[i0], o.exp_avg[i1], o.exp_avg_sq[i1]), T,
-                     o.betas, o.eps)
-
-    def _lazy_prepare(self, it: int):
-        """Before step `it`: the lazy SH Adam (if any) for this step, or None.
-        It runs where the SH step is fused (degree 3); every row is brought up
-        to date before a step that updates them eagerly, and before the ring
-        of step factors could wrap."""
-        lz = getattr(self, "sh_lazy", None)
-        if lz is None:
-            return None
-        t = self.opt.step_count + 1
-        if self.sh_degree_at(it) != 3:
-            if self._lazy_on:
-                self.sync()
-                self._lazy_on = False
-            return None
-        if not self._lazy_on:
-            lz.last.fill_(t - 1)  # every row current: the steps so far were eager
-            lz.flushed_at = t - 1
-            self._lazy_on = True
-        elif t - 1 - lz.flushed_at >= lz.R - 1:
-            self.sync()
-        return lz
 
     def synced_params(self):
         self.sync()
@@ -498,7 +450,6 @@ class Trainer:
             **dkw)
 
     def step(self, it: int):
-        self._step_lazy = self._lazy_prepare(it)
         if getattr(self, "_graph", None) is not None:
             loss = self._graph.step(it)
             if self.strategy is not None:
@@ -569,7 +520,7 @@ class Trainer:
             fa = _wrapper.ShAdamInBackward(
                 self.params["sh0"].data, self.params["shN"].data, o.exp_avg[i0],
                 o.exp_avg_sq[i0], o.exp_avg[i1], o.exp_avg_sq[i1], o.lrs[i0], o.lrs[i1],
-                o.betas, o.eps, o.step_count + 1, lazy=getattr(self, "_step_lazy", None))
+                o.betas, o.eps, o.step_count + 1)
         geom = getattr(self, "geom_fuse", False) and (isinstance(self.opt, FusedAdam) or
                                                       self.sharded)
         if fa is None and not geom:
@@ -687,8 +638,6 @@ class Trainer:
         self._load_moments(new_m)
         self._register_hooks()
         n = self.params["means"].shape[0]
-        if getattr(self, "sh_lazy", None) is not None:  # every row current (flushed above)
-            self.sh_lazy.resize(n, self.opt.step_count)
         self.grad2d = torch.zeros(n, device=self.device)
         self.count = torch.zeros(n, device=self.device)
         if self.radii2d is not None:

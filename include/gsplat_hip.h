@@ -27,6 +27,9 @@ extern "C" {
 #endif
 
 const char *gsplat_hip_last_error(void);
+/* 29: the lazy SH-Adam entries of 28 (gsplat_hip_sh_colors_fwd_lazy,
+ * gsplat_hip_sh_lazy_flush and the lazy arguments of the fused SH backward)
+ * removed -- measured slower. */
 int gsplat_hip_abi_version(void);
 
 /* ---------------------------------------------------------------------------
@@ -480,7 +483,7 @@ int gsplat_hip_sh_colors_bwd_adam(int degree, int C, int64_t N, const float *mea
                                   const int32_t *radii, const float *v_colors, float *v_dirs,
                                   float *m0, float *v0, float *m_rest, float *v_rest, float lr0,
                                   float lr_rest, float beta1, float beta2, float eps, int step,
-                                  int32_t *last, float *fac, int R, void *stream);
+                                  void *stream);
 /* The same with the step's factors on the device (ABI 20; a captured
  * training step replays with a new step count): hyper_device = {lr0 /
  * (1 - beta1^t), lr_rest / (1 - beta1^t), 1 / sqrt(1 - beta2^t)}, computed
@@ -491,36 +494,7 @@ int gsplat_hip_sh_colors_bwd_adam_dev(int degree, int C, int64_t N, const float 
                                       const int32_t *radii, const float *v_colors, float *v_dirs,
                                       float *m0, float *v0, float *m_rest, float *v_rest,
                                       const float *hyper_device, float beta1, float beta2,
-                                      float eps, const int32_t *skip_device, int32_t *last,
-                                      float *fac, int R, const int64_t *step_device,
-                                      void *stream);
-/* Lazy SH Adam (ABI 28; C == 1, the one-rank trainer): a Gaussian outside
- * the view has a zero SH gradient, and Adam's update with a zero gradient
- * depends only on the row's own (p, m, v) and the step's factors -- so it is
- * deferred.  last i32[N] counts the Adam steps applied to each row; fac
- * f32[R][4] is a ring of the steps' factors (ss0, ss_rest, ib, 0) at s % R.
- * With last non-NULL the backward above updates only the visible rows (the
- * colour forward has brought them to step t - 1; any step it left out is
- * taken first, the same adam_update calls in the same order as the eager
- * steps): step t with its gradient, last[g] = t; it also stores step t's
- * factors at fac[t % R] (t = step, or *step_device for the _dev form).
- * sh_colors_fwd_lazy: each visible row brought to step t - 1 (written back
- * with its moments, last = t - 1; nothing written when *skip_device != 0, a
- * void captured step) and the colours from it.
- * sh_lazy_flush: every row brought to step T (last[] = T) -- before anything
- * else reads the coefficients or moments; at most R - 1 steps may pass
- * between a row's updates (the caller flushes at least every R - 1 steps).
- * Parameters and moments equal the eager sequence's bit for bit after a
- * flush. */
-int gsplat_hip_sh_colors_fwd_lazy(int degree, int64_t N, const float *means,
-                                  const float *viewmats, float *coeffs, float *coeffs_rest,
-                                  const int32_t *radii, float *colors, float *m0, float *v0,
-                                  float *m_rest, float *v_rest, int32_t *last, float *fac, int R,
-                                  int step, const int64_t *step_device, float beta1, float beta2,
-                                  float eps, const int32_t *skip_device, void *stream);
-int gsplat_hip_sh_lazy_flush(int64_t N, float *coeffs, float *coeffs_rest, float *m0, float *v0,
-                             float *m_rest, float *v_rest, int32_t *last, float *fac, int R,
-                             int T, float beta1, float beta2, float eps, void *stream);
+                                      float eps, const int32_t *skip_device, void *stream);
 /* gsplat_hip_sh_colors_bwd for C cameras sharing one set of coefficient rows
  * in the trainer's layout (coeffs [N,1,3], coeffs_rest [N,15,3], degree
  * 0..3; ABI 23): v_coeffs [N,1,3], v_coeffs_rest [N,15,3] and v_dirs [N,3]

@@ -217,35 +217,6 @@ def test_graph_trainer_tracks_eager(capacity):
     torch.testing.assert_close(b[3], a[3], rtol=1e-3, atol=1e-7)
 
 
-def test_graph_trainer_side_stream_tracks_eager(monkeypatch):
-    """GSPLAT_HIP_SIDE_SH=1: the SH colours and their fused backward run on a
-    second captured stream (concurrent with the tile intersection); the
-    graph still holds kernel nodes only and the updates follow the eager
-    trainer's (same tolerance as above: the rasterizer's float atomics)."""
-    from gsplat_hip.train_step import Trainer
-    means, rgbs, vm, K, W, H = _trainer_scene()
-    out = {}
-    for graph in (False, True):
-        if graph:
-            monkeypatch.setenv("GSPLAT_HIP_SIDE_SH", "1")
-        tr = Trainer(means, rgbs, vm, K, W, H, device=DEV, graph=graph, max_steps=100)
-        if graph:
-            assert tr._graph.side is not None
-        for it in range(6):
-            tr.step(it)
-        tr.sync()
-        out[graph] = ({k: p.detach().clone() for k, p in tr.params.items()},
-                      tr.opt.step_count, tr.count.clone())
-        if graph:
-            census = tr._graph.census
-            assert set(census) <= {"kernel", "empty"} and census["kernel"] > 20, census
-    a, b = out[False], out[True]
-    assert a[1] == b[1] == 6
-    for k in a[0]:
-        torch.testing.assert_close(b[0][k], a[0][k], rtol=1e-3, atol=1e-5)
-    torch.testing.assert_close(b[2], a[2], rtol=0, atol=0)
-
-
 def test_graph_trainer_refine_tracks_eager():
     """A DefaultStrategy schedule (refines at steps 3 and 6, opacity resets at
     0 and 7): the graph-replayed trainer re-captures after every refine (new

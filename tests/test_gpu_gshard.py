@@ -330,7 +330,7 @@ def test_sh_adam_in_backward_over_cameras_is_exact():
                 _lib.call("gsplat_hip_sh_colors_bwd_adam", 3, C, N, _ptr(means), _ptr(vm),
                           _ptr(p0), _ptr(pr), _ptr(radii), _ptr(vcol), _ptr(vd), _ptr(m0),
                           _ptr(v0), _ptr(mr), _ptr(vr), 2.5e-3, 1.25e-4, 0.9, 0.999, 1e-15,
-                          step, None, None, 0, _stream())
+                          step, _stream())
             else:
                 g0 = torch.empty_like(p0)
                 gr = torch.empty_like(pr)
