@@ -1905,7 +1905,9 @@ int r16_bwd(r16::Args a, int64_t G, float *v_means2d, float *v_conics, float *v_
   const bool chunked = a.n_isects > 0 && a.state && a.L > 0 && a.render_colors_in;
   // the gradient rows and, right after them, the item counters
   const size_t pb = packed_bytes(D, ABS, G);
-  if (visible && G > 0) {
+  // (GSPLAT_HIP_MEMSET_NODES=1, diagnosis only: the whole table and the
+  // counters by hipMemsetAsync, as the round-3 step captured them)
+  if (visible && G > 0 && !gs::memset_nodes()) {
     // the counters start at byte pb (the table padded to 256 B): zero from
     // the table's end through them
     const int64_t tail = (int64_t)(pb / 4) - G * a.S + (chunked ? 64 : 0);
