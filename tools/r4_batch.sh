@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-4 batch: GPU suite, M2 default twice, emulated 8-rank gshard step
 # graph-replayed (twice) and eager, M3 graph vs eager, a kernel trace of the
-# default M2 line.  Test failures are reported; crashes / time limits end it.
+# default M2 line, the memset diagnosis.  Test failures are reported; crashes / time limits end it.
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 O=gpurun_out/${1:-r4_batch}; mkdir -p $O
@@ -29,4 +29,8 @@ for m in graph eager; do
 done
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $O/trace -o run -- /usr/bin/python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-traffic > $O/trace.log 2>&1 || exit 6
 echo "trace ok"
+# last (it may fault, nothing runs after it): the round-3 memset nodes
+# restored in the captured step, replays serialized
+GSPLAT_HIP_MEMSET_NODES=1 GSPLAT_HIP_GRAPH_ALLOW_MEMSET=1 AMD_SERIALIZE_KERNEL=3 timeout -k 10 180 python -u tools/graph_diag.py memset > $O/memset_diag.log 2>&1
+echo "memset diag rc=$?"; tail -12 $O/memset_diag.log
 exit 0
