@@ -152,7 +152,8 @@ struct Args {
   int SL;  // split tiles: isects per chunk (a multiple of L)
   const float *render_colors_in;  // backward: forward colours (for suffix sums)
   int dbg;  // debug flags (gsplat_hip_debug_set_flags): bit 0 = backward skips its
-            // atomics, bit 1 = split chunks never wait for a published product
+            // atomics, bit 1 = split chunks never wait for a published product,
+            // bit 2 = the split hand-off without its agent-scope fences
   uint64_t *timeline;  // debug: per-wave (start, end) s_memrealtime stamps or null
   unsigned long long *lanehist;  // debug: histogram of contributing lanes per (record, wave)
 };
@@ -480,10 +481,12 @@ GS_INLINE void acquire_published() {
 // 2048 polls of s_sleep 8 (~0.2 us each) plus the load round trips: about
 // 0.4-1 ms of waiting before the fallback computes the product itself
 constexpr int kSpinPolls = 2048;
-GS_INLINE bool wait_flag(const int32_t *f) {
+// nofence (debug bit 2, measurement only): round 3's hand-off, drains without
+// the agent-scope fences
+GS_INLINE bool wait_flag(const int32_t *f, bool nofence = false) {
   for (int i = 0; i < kSpinPolls; ++i) {
     if (__hip_atomic_load(const_cast<int32_t *>(f), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-      acquire_published();
+      if (nofence) drain_stores(); else acquire_published();
       return true;
     }
     __builtin_amdgcn_s_sleep(8);
@@ -599,7 +602,7 @@ GS_INLINE void fwd_item(const Args &a, float4 *st, int item) {
       if (!own) {
         for (; jn < kc; ++jn) {
           const int64_t sl = (tstart + (jn + 1) * a.SL) / a.L;
-          if ((a.dbg & 2) || !wait_flag(a.pflag + 4 * sl + wv)) break;
+          if ((a.dbg & 2) || !wait_flag(a.pflag + 4 * sl + wv, a.dbg & 4)) break;
           Tin *= load_sc1(a.prod + sl * (kTS * kTS) + pix_in_tile);
         }
         if (jn == kc) break;
@@ -609,7 +612,7 @@ GS_INLINE void fwd_item(const Args &a, float4 *st, int item) {
       if (own) {
         const int64_t sl = end / a.L;
         store_sc1(a.prod + sl * (kTS * kTS) + pix_in_tile, Pp);
-        release_published();
+        if (a.dbg & 4) drain_stores(); else release_published();
         if (lane == 0)
           __hip_atomic_store(a.pflag + 4 * sl + wv, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         own = false;
@@ -785,10 +788,10 @@ GS_INLINE void fwd_item(const Args &a, float4 *st, int item) {
     __syncthreads();
     __shared__ int s_last;
     if (threadIdx.x == 0) {
-      release_published();
+      if (!(a.dbg & 4)) release_published();
       s_last = __hip_atomic_fetch_add(a.ctr + (cid - kc), 1, __ATOMIC_RELAXED,
                                       __HIP_MEMORY_SCOPE_AGENT) == nch - 1;
-      if (s_last) acquire_published();
+      if (s_last && !(a.dbg & 4)) acquire_published();
     }
     __syncthreads();
     if (s_last && inside) {
