@@ -29,7 +29,7 @@ for m in graph eager nofence; do
   echo "m3 $m $(v $O/m3_$m.json)"
 done
 GSPLAT_HIP_DBG=4 timeout -k 10 300 python -u bench.py --no-traffic --no-cpu-baseline > $O/m2_nofence.json 2> $O/m2_nofence.err || exit 5
-echo "m2 nofence $(v $O/m2_nofence.json)
+echo "m2 nofence $(v $O/m2_nofence.json)"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $O/trace -o run -- /usr/bin/python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-traffic > $O/trace.log 2>&1 || exit 6
 echo "trace ok"
 # last (it may fault, nothing runs after it): the round-3 memset nodes
