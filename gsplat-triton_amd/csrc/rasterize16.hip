@@ -152,8 +152,7 @@ struct Args {
   int SL;  // split tiles: isects per chunk (a multiple of L)
   const float *render_colors_in;  // backward: forward colours (for suffix sums)
   int dbg;  // debug flags (gsplat_hip_debug_set_flags): bit 0 = backward skips its
-            // atomics, bit 1 = split chunks never wait for a published product,
-            // bit 2 = the split hand-off without its agent-scope fences
+            // atomics, bit 1 = split chunks never wait for a published product
   uint64_t *timeline;  // debug: per-wave (start, end) s_memrealtime stamps or null
   unsigned long long *lanehist;  // debug: histogram of contributing lanes per (record, wave)
 };
@@ -450,16 +449,19 @@ GS_INLINE void stage_bwd_pad(float4 *st, int slot) {
 // last first computes its own product (chunk_product) and publishes it per
 // wave, then takes the earlier chunks' products, composites from their product
 // and publishes its end T, last id and colour; the tile's last chunk to finish
-// combines them into the pixels.  Hand-offs (MI355X_MICROARCH.md
-// "inter-workgroup visibility", producer / consumer forms): every published
-// word is stored sc1 and drained (s_waitcnt vmcnt(0)); the producer then runs
-// an agent-scope release fence (drained again: the compiler may drop the wait
-// after buffer_wbl2) before its relaxed flag store or counter add; the
-// consumer polls relaxed, runs ONE agent-scope acquire fence after the match
-// (or after the counter add that made it last), and reads the words with sc1
-// loads.  A chunk waits only for chunks at lower block indices, dispatched
-// before it; the wait is bounded anyway -- on timeout the chunk computes the
-// missing product itself (same code, same value), so no schedule can hang it.
+// combines them into the pixels.  Hand-offs (cdna_hip_programming.md
+// Guideline 16, form R1): every published word is stored write-through (sc1,
+// a relaxed agent-scope atomic store) and drained (s_waitcnt vmcnt(0)) by the
+// storing wave before its relaxed agent-scope flag store or counter add, so
+// no release fence -- an agent release is a buffer_wbl2, a write-back of the
+// XCD's whole L2, and the forward keeps much of its output dirty there (one
+// per published product and per chunk cost M3's forward 0.494 -> 0.615 ms);
+// the consumer polls relaxed, runs ONE agent-scope acquire (this CU's L1)
+// after ALL its polls have matched (or after the counter add that made it
+// last), and reads the words with sc1 loads.  A chunk waits only for chunks
+// at lower block indices, dispatched before it; the wait is bounded anyway --
+// on timeout the chunk computes the missing products itself (same code, same
+// value), so no schedule can hang it.
 GS_INLINE void store_sc1(float *p, float v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -467,12 +469,8 @@ GS_INLINE float load_sc1(const float *p) {
   return __hip_atomic_load(const_cast<float *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 GS_INLINE void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-// producer side, after the published stores: drain, release, drain
-GS_INLINE void release_published() {
-  drain_stores();
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-  drain_stores();
-}
+// producer side, after the published (sc1) stores, before the flag / counter
+GS_INLINE void release_published() { drain_stores(); }
 // consumer side, after the poll matched / the counter add returned
 GS_INLINE void acquire_published() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -481,14 +479,11 @@ GS_INLINE void acquire_published() {
 // 2048 polls of s_sleep 8 (~0.2 us each) plus the load round trips: about
 // 0.4-1 ms of waiting before the fallback computes the product itself
 constexpr int kSpinPolls = 2048;
-// nofence (debug bit 2, measurement only): round 3's hand-off, drains without
-// the agent-scope fences
-GS_INLINE bool wait_flag(const int32_t *f, bool nofence = false) {
+// the poll only; the caller runs ONE acquire after all its polls matched
+GS_INLINE bool wait_flag(const int32_t *f) {
   for (int i = 0; i < kSpinPolls; ++i) {
-    if (__hip_atomic_load(const_cast<int32_t *>(f), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-      if (nofence) drain_stores(); else acquire_published();
+    if (__hip_atomic_load(const_cast<int32_t *>(f), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
       return true;
-    }
     __builtin_amdgcn_s_sleep(8);
   }
   return false;
@@ -594,32 +589,29 @@ GS_INLINE void fwd_item(const Args &a, float4 *st, int item) {
   // transmittance entering the chunk
   const int nch = SPLIT ? (int)((tend - tstart + a.SL - 1) / a.SL) : 0;
   if (SPLIT && nch > 1 && !skip_tile) {
-    bool own = kc < nch - 1;  // this chunk's product still to publish
-    int jn = 0;               // next earlier chunk whose product to take
     float Tin = 1.f;
-    for (;;) {
-      int ps = start;
-      if (!own) {
-        for (; jn < kc; ++jn) {
-          const int64_t sl = (tstart + (jn + 1) * a.SL) / a.L;
-          if ((a.dbg & 2) || !wait_flag(a.pflag + 4 * sl + wv, a.dbg & 4)) break;
-          Tin *= load_sc1(a.prod + sl * (kTS * kTS) + pix_in_tile);
-        }
-        if (jn == kc) break;
-        ps = tstart + jn * a.SL;
-      }
-      const float Pp = chunk_product<D>(a, geo, ps, ps + a.SL, st, lane, fx, fy);
-      if (own) {
-        const int64_t sl = end / a.L;
-        store_sc1(a.prod + sl * (kTS * kTS) + pix_in_tile, Pp);
-        if (a.dbg & 4) drain_stores(); else release_published();
-        if (lane == 0)
-          __hip_atomic_store(a.pflag + 4 * sl + wv, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        own = false;
-      } else {
-        Tin *= Pp;
-        ++jn;
-      }
+    if (kc < nch - 1) {  // this chunk's own product, published first
+      const float Pp = chunk_product<D>(a, geo, start, end, st, lane, fx, fy);
+      const int64_t sl = end / a.L;
+      store_sc1(a.prod + sl * (kTS * kTS) + pix_in_tile, Pp);
+      release_published();
+      if (lane == 0)
+        __hip_atomic_store(a.pflag + 4 * sl + wv, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // the earlier chunks' products: poll their flags in order, ONE acquire for
+    // the run that matched, their products; the rest (timed out) computed here
+    int jm = 0;
+    if (!(a.dbg & 2))
+      for (; jm < kc; ++jm)
+        if (!wait_flag(a.pflag + 4 * ((tstart + (jm + 1) * a.SL) / a.L) + wv)) break;
+    if (jm > 0) {
+      acquire_published();
+      for (int j = 0; j < jm; ++j)
+        Tin *= load_sc1(a.prod + ((tstart + (j + 1) * a.SL) / a.L) * (kTS * kTS) + pix_in_tile);
+    }
+    for (int j = jm; j < kc; ++j) {
+      const int ps = tstart + j * a.SL;
+      Tin *= chunk_product<D>(a, geo, ps, ps + a.SL, st, lane, fx, fy);
     }
     // at or below 1e-4 the pixel terminated in an earlier chunk (every
     // blended factor kept it above): -Tin marks it finished with about that
@@ -788,10 +780,9 @@ GS_INLINE void fwd_item(const Args &a, float4 *st, int item) {
     __syncthreads();
     __shared__ int s_last;
     if (threadIdx.x == 0) {
-      if (!(a.dbg & 4)) release_published();
       s_last = __hip_atomic_fetch_add(a.ctr + (cid - kc), 1, __ATOMIC_RELAXED,
                                       __HIP_MEMORY_SCOPE_AGENT) == nch - 1;
-      if (s_last && !(a.dbg & 4)) acquire_published();
+      if (s_last) acquire_published();
     }
     __syncthreads();
     if (s_last && inside) {

@@ -328,9 +328,7 @@ int gsplat_hip_debug_set_fwd_split(int isects);
  * bit 0 = the backward skips its gradient atomics (timing experiments);
  * bit 1 = a chunk of a split tile never waits for an earlier chunk's
  * published product and computes it itself (the timeout path; results are
- * identical); bit 2 = the split hand-off's stores drained but without its
- * agent-scope release / acquire fences (round 3's protocol; measurement
- * only).  Returns the previous flags. */
+ * identical).  Returns the previous flags. */
 int gsplat_hip_debug_set_flags(int flags);
 
 /* ---------------------------------------------------------------------------
