@@ -616,7 +616,6 @@ static int isect_write_sorted_impl(
   GS_REQUIRE(!rank_ids == !vis_rank, "isect_write_sorted: rank_ids and vis_rank go together");
   GS_REQUIRE(!rank_ids || gsplat_hip_isect_ranked(n_cameras, tile_width, tile_height),
              "isect_write_sorted: rank ids need the supertile expansion");
-  const int n_tiles = tile_width * tile_height;
   auto plain_offsets = [&]() -> int {  // offsets from the written ids (or all zero)
     if (!offsets) return 0;
     return gsplat_hip_isect_offsets(cnt_dev ? n_isects : (n_visible > 0 ? n_isects : 0), cnt_dev,

@@ -22,14 +22,11 @@ for r in 1 2; do
 done
 timeout -k 10 400 python -u bench.py --gshard-emulate 8 --eager --no-traffic --no-cpu-baseline > $O/gs8_eager.json 2> $O/gs8_eager.err || exit 4
 echo "gshard-emulate 8 eager $(v $O/gs8_eager.json)"
-for m in graph eager nofence; do
+for m in graph eager; do
   a=""; [ $m = eager ] && a="--eager"
-  dbg=0; [ $m = nofence ] && dbg=4
-  GSPLAT_HIP_DBG=$dbg timeout -k 10 400 python -u bench.py --config m3 --no-traffic --no-cpu-baseline $a > $O/m3_$m.json 2> $O/m3_$m.err || exit 5
+  timeout -k 10 400 python -u bench.py --config m3 --no-traffic --no-cpu-baseline $a > $O/m3_$m.json 2> $O/m3_$m.err || exit 5
   echo "m3 $m $(v $O/m3_$m.json)"
 done
-GSPLAT_HIP_DBG=4 timeout -k 10 300 python -u bench.py --no-traffic --no-cpu-baseline > $O/m2_nofence.json 2> $O/m2_nofence.err || exit 5
-echo "m2 nofence $(v $O/m2_nofence.json)"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $O/trace -o run -- /usr/bin/python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-traffic > $O/trace.log 2>&1 || exit 6
 echo "trace ok"
 # last (it may fault, nothing runs after it): the round-3 memset nodes
