@@ -1341,6 +1341,63 @@ GS_INLINE void block_max_out(int64_t v, int32_t *out) {
   if (threadIdx.x == 0 && out) *out = smax;
 }
 
+// The backward's work items of this render (see chunk_items_kernel), made by
+// the forward's one-workgroup order / plan kernel, which reads the tile
+// counts anyway: full-length chunks to `full`, tails to `tail`, the two
+// counts to n_items[0..1] (written, not accumulated).  1024 lanes, tiles tid
+// + 1024 i (n_tiles <= 16384).  `full` null: nothing.
+GS_INLINE void emit_bwd_items(int n_tiles, const int32_t *offsets, const int64_t *n_dev,
+                              int64_t n_isects, int L, int2 *full, int2 *tail,
+                              int32_t *n_items) {
+  if (!full) return;
+  __shared__ int ws[16][2];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  auto count = [&](int t) -> int64_t {
+    return tile_end(offsets, t, n_tiles, n_dev, n_isects) - offsets[t];
+  };
+  int nf = 0, nt = 0;
+  for (int i = 0; i < 16; ++i) {
+    const int t = tid + 1024 * i;
+    if (t >= n_tiles) break;
+    const int64_t n = count(t);
+    nf += (int)(n / L);
+    nt += (n % L) != 0;
+  }
+  int xf = nf, xt = nt;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int yf = __shfl_up(xf, o, 64), yt = __shfl_up(xt, o, 64);
+    if (lane >= o) {
+      xf += yf;
+      xt += yt;
+    }
+  }
+  if (lane == 63) {
+    ws[w][0] = xf;
+    ws[w][1] = xt;
+  }
+  __syncthreads();
+  int bf = xf - nf, bt = xt - nt, tf = 0, tt = 0;
+  for (int ww = 0; ww < 16; ++ww) {
+    bf += ww < w ? ws[ww][0] : 0;
+    bt += ww < w ? ws[ww][1] : 0;
+    tf += ws[ww][0];
+    tt += ws[ww][1];
+  }
+  for (int i = 0; i < 16; ++i) {
+    const int t = tid + 1024 * i;
+    if (t >= n_tiles) break;
+    const int64_t n = count(t);
+    const int f = (int)(n / L);
+    for (int k = 0; k < f; ++k) full[bf++] = make_int2(t, k);
+    if (n % L) tail[bt++] = make_int2(t, f);
+  }
+  if (tid == 0) {
+    n_items[0] = tf;
+    n_items[1] = tt;
+  }
+}
+
 // Forward dispatch order: tiles bucketed by isect count (>= 2048, >= 1024,
 // >= 512, the rest), heaviest bucket first, so the longest tiles start in the
 // first wave of workgroups instead of finishing last.  Inside a bucket: lane
@@ -1350,7 +1407,8 @@ GS_INLINE void block_max_out(int64_t v, int32_t *out) {
 __global__ void __launch_bounds__(1024)
 tile_order_kernel(int n_tiles, const int32_t *__restrict__ offsets, int64_t n_isects,
                   const int64_t *__restrict__ n_dev, int32_t *__restrict__ order,
-                  int32_t *__restrict__ max_out) {
+                  int32_t *__restrict__ max_out, int L, int2 *__restrict__ items_full,
+                  int2 *__restrict__ items_tail, int32_t *__restrict__ n_items) {
   constexpr int MAXPER = 16;  // tiles per thread (n_tiles <= 16384)
   __shared__ uint64_t wsum[16];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -1406,6 +1464,7 @@ tile_order_kernel(int n_tiles, const int32_t *__restrict__ offsets, int64_t n_is
       pos[3] += bk == 3;
     }
   }
+  emit_bwd_items(n_tiles, offsets, n_dev, n_isects, L, items_full, items_tail, n_items);
 }
 
 // Forward plan with split heavy tiles, decided on this render's tiles.  A
@@ -1422,7 +1481,9 @@ fwd_plan_kernel(int n_tiles, const int32_t *__restrict__ offsets, int64_t n_isec
                 const int64_t *__restrict__ n_dev, const uint8_t *__restrict__ masks, int SL,
                 int L, int split, int32_t *__restrict__ hdr, int32_t *__restrict__ order,
                 int2 *__restrict__ chunks, int32_t *__restrict__ pflag,
-                int32_t *__restrict__ ctr, int32_t *__restrict__ max_out) {
+                int32_t *__restrict__ ctr, int32_t *__restrict__ max_out,
+                int2 *__restrict__ items_full, int2 *__restrict__ items_tail,
+                int32_t *__restrict__ n_items) {
   // quantities: [0..3] whole tiles per bucket, [4] chunks
   constexpr int PER = 16, NQ = 5;
   __shared__ int wsum[16][NQ];
@@ -1513,6 +1574,7 @@ fwd_plan_kernel(int n_tiles, const int32_t *__restrict__ offsets, int64_t n_isec
     hdr[0] = base;
     hdr[1] = total[4];
   }
+  emit_bwd_items(n_tiles, offsets, n_dev, n_isects, L, items_full, items_tail, n_items);
 }
 
 // Backward work items.  A tile with n isects becomes ceil(n / L) items
@@ -1754,14 +1816,37 @@ static int64_t order_bytes(int n_tiles, int64_t n_isects) {
   return use_order(n_tiles, n_isects) ? align256(4 * (int64_t)n_tiles) : 0;
 }
 
-int64_t rasterize16_fwd_state_bytes(int D, int n_tiles, int64_t n_isects) {
-  return chunk_slot_bytes(D, n_isects) + order_bytes(n_tiles, n_isects) +
-         split_layout(D, n_tiles, n_isects).bytes;
-}
-
 static int64_t n_items_bound(int n_tiles, int64_t n_isects) {
   const int L = chunk_len();
   return L ? (int64_t)n_tiles + n_isects / L + 1 : (int64_t)n_tiles;
+}
+
+// After the split area: the backward's work items, written by the order /
+// plan kernel ([n_items i32 x 2, 256 B][full int2 x (n_isects / L + 1)][tail
+// int2 x n_tiles], bwd workspace layout), when the forward has chunk slots
+// and a tile order.
+static int64_t items_bytes(int D, int n_tiles, int64_t n_isects) {
+  return (chunk_slot_bytes(D, n_isects) > 0 && use_order(n_tiles, n_isects))
+             ? align256(256 + (int64_t)sizeof(int2) * n_items_bound(n_tiles, n_isects)) : 0;
+}
+
+int64_t rasterize16_fwd_state_bytes(int D, int n_tiles, int64_t n_isects) {
+  return chunk_slot_bytes(D, n_isects) + order_bytes(n_tiles, n_isects) +
+         split_layout(D, n_tiles, n_isects).bytes + items_bytes(D, n_tiles, n_isects);
+}
+
+struct ItemLists {
+  int32_t *n_items;
+  int2 *full, *tail;
+};
+
+static ItemLists item_lists(const void *state, int D, int n_tiles, int64_t n_isects) {
+  if (!state || items_bytes(D, n_tiles, n_isects) == 0) return ItemLists{nullptr, nullptr, nullptr};
+  char *b = const_cast<char *>(reinterpret_cast<const char *>(state)) +
+            chunk_slot_bytes(D, n_isects) + order_bytes(n_tiles, n_isects) +
+            split_layout(D, n_tiles, n_isects).bytes;
+  int2 *full = reinterpret_cast<int2 *>(b + 256);
+  return ItemLists{reinterpret_cast<int32_t *>(b), full, full + (n_isects / chunk_len() + 1)};
 }
 
 // Pixels per lane in the backward (1: bwd_kernel, 16x4 per wave; 2 or 4:
@@ -1821,7 +1906,7 @@ static thread_local bool g_prepared_split = false;  // the split decision of tha
 
 static void launch_order(int n_tiles, const int32_t *offsets, int64_t n_isects,
                          const int64_t *n_dev, int32_t *order, hipStream_t st,
-                         char *split_base = nullptr, int D = 0) {
+                         char *split_base, int D, const ItemLists &it) {
   if (split_base) {
     const SplitLayout l = split_layout(D, n_tiles, n_isects);
     hipLaunchKernelGGL(r16::fwd_plan_kernel, dim3(1), dim3(1024), 0, st, n_tiles, offsets,
@@ -1830,18 +1915,20 @@ static void launch_order(int n_tiles, const int32_t *offsets, int64_t n_isects,
                        reinterpret_cast<int32_t *>(split_base + l.hdr), order,
                        reinterpret_cast<int2 *>(split_base + l.fitems),
                        reinterpret_cast<int32_t *>(split_base + l.pflag),
-                       reinterpret_cast<int32_t *>(split_base + l.ctr), stat_dev());
+                       reinterpret_cast<int32_t *>(split_base + l.ctr), stat_dev(), it.full,
+                       it.tail, it.n_items);
   } else
     hipLaunchKernelGGL(r16::tile_order_kernel, dim3(1), dim3(1024), 0, st, n_tiles, offsets,
                        n_isects, n_dev, order,
-                       split_capable(n_tiles, n_isects) ? stat_dev() : nullptr);
+                       split_capable(n_tiles, n_isects) ? stat_dev() : nullptr, chunk_len(),
+                       it.full, it.tail, it.n_items);
 }
 
 template <int D>
 int r16_fwd(r16::Args a, const void *state, char *split_base, hipStream_t st) {
   if (a.order && state != g_prepared_state)
     launch_order(a.n_tiles, a.offsets, a.n_isects, a.n_dev, const_cast<int32_t *>(a.order), st,
-                 split_base, D);
+                 split_base, D, item_lists(state, D, a.n_tiles, a.n_isects));
   g_prepared_state = nullptr;
   if (split_base) {
     // the split tiles' chunks and the other tiles in one launch; the grid is
@@ -1892,7 +1979,7 @@ zero_rows_kernel(int64_t G, int S, const int32_t *__restrict__ visible,
 template <int D, bool ABS>
 int r16_bwd(r16::Args a, int64_t G, float *v_means2d, float *v_conics, float *v_colors,
             float *v_opacities, float *v_abs, void *workspace, const int32_t *visible,
-            const int32_t *vis_rank, hipStream_t st) {
+            const int32_t *vis_rank, const ItemLists &fwd_items, hipStream_t st) {
   constexpr int F = D + 6 + (ABS ? 2 : 0);
   a.S = ((F + 15) / 16) * 16;
   a.packed = reinterpret_cast<float *>(workspace);
@@ -1912,7 +1999,12 @@ int r16_bwd(r16::Args a, int64_t G, float *v_means2d, float *v_conics, float *v_
   }
   if (a.n_isects > 0) {
     int64_t grid = a.n_tiles;
-    if (chunked) {
+    if (chunked && fwd_items.full) {  // made by the forward's order / plan kernel
+      a.n_items = fwd_items.n_items;
+      a.items = fwd_items.full;
+      a.items_tail = fwd_items.tail;
+      grid = n_items_bound(a.n_tiles, a.n_isects);
+    } else if (chunked) {
       char *w = reinterpret_cast<char *>(workspace) + packed_bytes(D, ABS, G);
       a.n_items = reinterpret_cast<int32_t *>(w);
       a.items = reinterpret_cast<int2 *>(w + 256);
@@ -2015,7 +2107,8 @@ int rasterize16_prepare(int D, int n_tiles, const int32_t *offsets, int64_t n_is
   int32_t *order = reinterpret_cast<int32_t *>(base);
   const bool split = chunk_slot_bytes(D, n_isects) > 0 && use_split_now(n_tiles, n_isects);
   launch_order(n_tiles, offsets, n_isects, n_isects_dev, order, st,
-               split ? base + order_bytes(n_tiles, n_isects) : nullptr, D);
+               split ? base + order_bytes(n_tiles, n_isects) : nullptr, D,
+               item_lists(state, D, n_tiles, n_isects));
   GS_CHECK_LAUNCH("rasterize_prepare");
   g_prepared_state = state;
   g_prepared_split = split;
@@ -2060,13 +2153,14 @@ int rasterize16_bwd(int C, int64_t G, int D, int W, int H, int tw, int th,
                 ? const_cast<float *>(reinterpret_cast<const float *>(state)) : nullptr;
   a.render_colors_in = render_colors;
   a.dbg = dbg_flags();
+  const ItemLists fi = a.state ? item_lists(state, D, a.n_tiles, n_isects) : ItemLists{};
   const bool ab = v_abs != nullptr;
 #define GS_R16B(DD)                                                                            \
   case DD:                                                                                     \
     return ab ? r16_bwd<DD, true>(a, G, v_means2d, v_conics, v_colors, v_opacities, v_abs,     \
-                                  workspace, visible, vis_rank, st)                            \
+                                  workspace, visible, vis_rank, fi, st)                        \
               : r16_bwd<DD, false>(a, G, v_means2d, v_conics, v_colors, v_opacities, v_abs,    \
-                                   workspace, visible, vis_rank, st);
+                                   workspace, visible, vis_rank, fi, st);
   switch (D) { GS_R16B(1) GS_R16B(2) GS_R16B(3) GS_R16B(4) GS_R16B(8) GS_R16B(16) GS_R16B(32) }
 #undef GS_R16B
   GS_REQUIRE(false, "rasterize16_bwd: unsupported channels %d", D);
