@@ -107,38 +107,45 @@ isect_count_kernel(int64_t G, const float *__restrict__ means2d, const int32_t *
 // Exclusive scan of the per-block sums in place; total -> block_sums[nb] (and
 // -> totals[blockIdx.x] when totals is non-null).  One 1024-lane workgroup per
 // array walks its (at most a few thousand) block sums: workgroup 0 scans
-// `first`, workgroup 1 (if launched) `second`.
+// `first`, workgroup 1 (if launched) `second`.  Each lane takes kScanK
+// consecutive sums per round with all its loads in flight (a round of 8192
+// covers M2's 3930 blocks: one load latency instead of one per 1024).
+constexpr int kScanK = 8;
 __global__ void __launch_bounds__(1024) isect_scan_blocks_kernel(int64_t nb, int64_t *first,
                                                                  int64_t *second,
                                                                  int64_t *totals) {
   int64_t *block_sums = blockIdx.x == 0 ? first : second;
   __shared__ int64_t wave_tot[16];
-  __shared__ int64_t chunk_tot;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   int64_t carry = 0;  // identical in every lane
-  for (int64_t base = 0; base < nb; base += 1024) {
-    const int64_t i = base + threadIdx.x;
-    const int64_t v = (i < nb) ? block_sums[i] : 0;
-    int64_t x = v;
+  for (int64_t base = 0; base < nb; base += 1024 * kScanK) {
+    const int64_t i0 = base + (int64_t)threadIdx.x * kScanK;
+    int64_t v[kScanK], s = 0;
+#pragma unroll
+    for (int k = 0; k < kScanK; ++k) v[k] = (i0 + k < nb) ? block_sums[i0 + k] : 0;
+#pragma unroll
+    for (int k = 0; k < kScanK; ++k) s += v[k];
+    int64_t x = s;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
-      int64_t y = __shfl_up(x, o, 64);
+      const int64_t y = __shfl_up(x, o, 64);
       if (lane >= o) x += y;
     }
     if (lane == 63) wave_tot[wid] = x;
     __syncthreads();
-    if (threadIdx.x == 0) {
-      int64_t run = 0;
-      for (int w = 0; w < 16; ++w) {
-        const int64_t s = wave_tot[w];
-        wave_tot[w] = run;
-        run += s;
-      }
-      chunk_tot = run;
+    int64_t before = 0, all = 0;
+#pragma unroll
+    for (int w = 0; w < 16; ++w) {
+      before += w < wid ? wave_tot[w] : 0;
+      all += wave_tot[w];
     }
-    __syncthreads();
-    if (i < nb) block_sums[i] = carry + wave_tot[wid] + x - v;
-    carry += chunk_tot;
+    int64_t run = carry + before + x - s;
+#pragma unroll
+    for (int k = 0; k < kScanK; ++k) {
+      if (i0 + k < nb) block_sums[i0 + k] = run;
+      run += v[k];
+    }
+    carry += all;
     __syncthreads();
   }
   if (threadIdx.x == 0) {
