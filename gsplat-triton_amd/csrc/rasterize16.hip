@@ -1345,22 +1345,18 @@ GS_INLINE void block_max_out(int64_t v, int32_t *out) {
 // the forward's one-workgroup order / plan kernel, which reads the tile
 // counts anyway: full-length chunks to `full`, tails to `tail`, the two
 // counts to n_items[0..1] (written, not accumulated).  1024 lanes, tiles tid
-// + 1024 i (n_tiles <= 16384).  `full` null: nothing.
-GS_INLINE void emit_bwd_items(int n_tiles, const int32_t *offsets, const int64_t *n_dev,
-                              int64_t n_isects, int L, int2 *full, int2 *tail,
+// + 1024 i (n_tiles <= 16384), their isect counts cnt[i] (< 0: no tile) from
+// the caller's registers.  `full` null: nothing.
+GS_INLINE void emit_bwd_items(const int (&cnt)[16], int L, int2 *full, int2 *tail,
                               int32_t *n_items) {
   if (!full) return;
   __shared__ int ws[16][2];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  auto count = [&](int t) -> int64_t {
-    return tile_end(offsets, t, n_tiles, n_dev, n_isects) - offsets[t];
-  };
   int nf = 0, nt = 0;
-  for (int i = 0; i < 16; ++i) {
-    const int t = tid + 1024 * i;
-    if (t >= n_tiles) break;
-    const int64_t n = count(t);
-    nf += (int)(n / L);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {  // cnt < 0: no tile
+    const int n = cnt[i] > 0 ? cnt[i] : 0;
+    nf += n / L;
     nt += (n % L) != 0;
   }
   int xf = nf, xt = nt;
@@ -1384,11 +1380,11 @@ GS_INLINE void emit_bwd_items(int n_tiles, const int32_t *offsets, const int64_t
     tf += ws[ww][0];
     tt += ws[ww][1];
   }
+#pragma unroll
   for (int i = 0; i < 16; ++i) {
     const int t = tid + 1024 * i;
-    if (t >= n_tiles) break;
-    const int64_t n = count(t);
-    const int f = (int)(n / L);
+    const int n = cnt[i] > 0 ? cnt[i] : 0;
+    const int f = n / L;
     for (int k = 0; k < f; ++k) full[bf++] = make_int2(t, k);
     if (n % L) tail[bt++] = make_int2(t, f);
   }
@@ -1413,15 +1409,18 @@ tile_order_kernel(int n_tiles, const int32_t *__restrict__ offsets, int64_t n_is
   __shared__ uint64_t wsum[16];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   int bucket[MAXPER];
+  int cnt[MAXPER];  // isect counts fit 32 bits (the offsets are int32)
   uint64_t mine = 0;
   int64_t nmax = 0;
 #pragma unroll
   for (int i = 0; i < MAXPER; ++i) {
     const int t = tid + 1024 * i;
     bucket[i] = -1;
+    cnt[i] = -1;
     if (t < n_tiles) {
       const int64_t e = tile_end(offsets, t, n_tiles, n_dev, n_isects);
       const int64_t n = e - offsets[t];
+      cnt[i] = (int)n;
       nmax = max(nmax, n);
       bucket[i] = n >= 2048 ? 0 : n >= 1024 ? 1 : n >= 512 ? 2 : 3;
       mine += (uint64_t)1 << (16 * bucket[i]);
@@ -1464,7 +1463,7 @@ tile_order_kernel(int n_tiles, const int32_t *__restrict__ offsets, int64_t n_is
       pos[3] += bk == 3;
     }
   }
-  emit_bwd_items(n_tiles, offsets, n_dev, n_isects, L, items_full, items_tail, n_items);
+  emit_bwd_items(cnt, L, items_full, items_tail, n_items);
 }
 
 // Forward plan with split heavy tiles, decided on this render's tiles.  A
@@ -1488,12 +1487,19 @@ fwd_plan_kernel(int n_tiles, const int32_t *__restrict__ offsets, int64_t n_isec
   constexpr int PER = 16, NQ = 5;
   __shared__ int wsum[16][NQ];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  // bucket (or -1: split) and chunk count of tile t (recomputed in the write
-  // pass: keeps the 16 tiles' state out of registers)
-  auto classify = [&](int t, int &nch) -> int {
-    const int64_t n = tile_end(offsets, t, n_tiles, n_dev, n_isects) - offsets[t];
+  // the 16 tiles' isect counts, loaded once with every load in flight (< 0:
+  // no tile)
+  int cnt[PER];  // isect counts fit 32 bits (the offsets are int32)
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int t = tid + 1024 * i;
+    cnt[i] = t < n_tiles ? (int)(tile_end(offsets, t, n_tiles, n_dev, n_isects) - offsets[t]) : -1;
+  }
+  // bucket (or -1: split) and chunk count of tile i of this lane
+  auto classify = [&](int i, int &nch) -> int {
+    const int n = cnt[i];
     nch = 0;
-    if (n > split && !(masks && masks[t])) {
+    if (n > split && !(masks && masks[tid + 1024 * i])) {
       nch = (int)((n + SL - 1) / SL);
       return -1;
     }
@@ -1501,15 +1507,15 @@ fwd_plan_kernel(int n_tiles, const int32_t *__restrict__ offsets, int64_t n_isec
   };
   int mine[NQ] = {0, 0, 0, 0, 0};
   int64_t nmax = 0;
+#pragma unroll
   for (int i = 0; i < PER; ++i) {
-    const int t = tid + 1024 * i;
-    if (t >= n_tiles) break;
+    if (cnt[i] < 0) continue;
     int nch;
-    const int kd = classify(t, nch);
+    const int kd = classify(i, nch);
 #pragma unroll
     for (int q = 0; q < 4; ++q) mine[q] += q == kd;
     mine[4] += nch;
-    nmax = max(nmax, tile_end(offsets, t, n_tiles, n_dev, n_isects) - offsets[t]);
+    nmax = max(nmax, (int64_t)cnt[i]);
   }
   block_max_out(nmax, max_out);
   int x[NQ];
@@ -1544,11 +1550,12 @@ fwd_plan_kernel(int n_tiles, const int32_t *__restrict__ offsets, int64_t n_isec
     pos[q] += base;
     base += total[q];
   }
+#pragma unroll
   for (int i = 0; i < PER; ++i) {
     const int t = tid + 1024 * i;
-    if (t >= n_tiles) break;
+    if (cnt[i] < 0) continue;
     int nch;
-    const int kd = classify(t, nch);
+    const int kd = classify(i, nch);
     if (kd < 0) {
       ctr[pos[4]] = 0;  // index of chunk 0
       for (int k = 0; k < nch; ++k) {
@@ -1574,7 +1581,7 @@ fwd_plan_kernel(int n_tiles, const int32_t *__restrict__ offsets, int64_t n_isec
     hdr[0] = base;
     hdr[1] = total[4];
   }
-  emit_bwd_items(n_tiles, offsets, n_dev, n_isects, L, items_full, items_tail, n_items);
+  emit_bwd_items(cnt, L, items_full, items_tail, n_items);
 }
 
 // Backward work items.  A tile with n isects becomes ceil(n / L) items
