@@ -1303,7 +1303,10 @@ unpack_kernel(int64_t G, int S, const float *__restrict__ packed, float *__restr
               const int32_t *__restrict__ visible, const int32_t *__restrict__ vis_rank) {
   const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= G) return;
-  if (visible && visible[g] <= 0) {
+  // both loads issued together (the rank does not wait for the visibility)
+  const int32_t vg = visible ? visible[g] : 1;
+  const int32_t rk = vis_rank ? vis_rank[g] : 0;
+  if (vg <= 0) {
 #pragma unroll
     for (int d = 0; d < D; ++d) v_colors[g * D + d] = 0.f;
     v_opacities[g] = 0.f;
@@ -1314,7 +1317,7 @@ unpack_kernel(int64_t G, int S, const float *__restrict__ packed, float *__restr
     if (ABS) *reinterpret_cast<float2 *>(v_abs + 2 * g) = make_float2(0.f, 0.f);
     return;
   }
-  const float *r = packed + (vis_rank ? min<int64_t>((uint32_t)vis_rank[g], G - 1) : g) * S;
+  const float *r = packed + (vis_rank ? min<int64_t>((uint32_t)rk, G - 1) : g) * S;
 #pragma unroll
   for (int d = 0; d < D; ++d) v_colors[g * D + d] = r[d];
   v_opacities[g] = r[D];
@@ -1983,6 +1986,20 @@ zero_rows_kernel(int64_t G, int S, const int32_t *__restrict__ visible,
   if (blockIdx.x == 0 && threadIdx.x < tail_floats) packed[G * S + threadIdx.x] = 0.f;
 }
 
+// Rank-indexed rows with the visible count on the device (the sync-free
+// isect's counts, {written, n_visible, ...}): the live rows are exactly rows
+// 0 .. n_visible - 1, zeroed as one contiguous range -- consecutive lanes,
+// consecutive rows, no per-Gaussian reads (zero_rows_kernel's scattered
+// rows cost 9.5 us at M2).
+__global__ void __launch_bounds__(256)
+zero_ranked_rows_kernel(int64_t G, int S, const int64_t *__restrict__ counts,
+                        float *__restrict__ packed, int64_t tail_floats) {
+  const int64_t nv = min(G, counts[1]);
+  const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;  // float4 slot
+  if (q < nv * (S / 4)) reinterpret_cast<float4 *>(packed)[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (blockIdx.x == 0 && threadIdx.x < tail_floats) packed[G * S + threadIdx.x] = 0.f;
+}
+
 template <int D, bool ABS>
 int r16_bwd(r16::Args a, int64_t G, float *v_means2d, float *v_conics, float *v_colors,
             float *v_opacities, float *v_abs, void *workspace, const int32_t *visible,
@@ -1999,8 +2016,13 @@ int r16_bwd(r16::Args a, int64_t G, float *v_means2d, float *v_conics, float *v_
     // the counters start at byte pb (the table padded to 256 B): zero from
     // the table's end through them
     const int64_t tail = (int64_t)(pb / 4) - G * a.S + (chunked ? 64 : 0);
-    hipLaunchKernelGGL(zero_rows_kernel, dim3((unsigned)((G + 255) / 256)), dim3(256), 0, st, G,
-                       a.S, visible, vis_rank, a.packed, tail);
+    if (vis_rank && a.n_dev)  // the counts of the sync-free isect: rows 0 .. n_visible - 1
+      hipLaunchKernelGGL(zero_ranked_rows_kernel,
+                         dim3((unsigned)((G * (a.S / 4) + 255) / 256)), dim3(256), 0, st, G, a.S,
+                         a.n_dev, a.packed, tail);
+    else
+      hipLaunchKernelGGL(zero_rows_kernel, dim3((unsigned)((G + 255) / 256)), dim3(256), 0, st,
+                         G, a.S, visible, vis_rank, a.packed, tail);
   } else {
     GS_HIP(gs::zero_async(a.packed, pb + (chunked ? 256 : 0), st));
   }

@@ -298,7 +298,10 @@ int gsplat_hip_rasterize_bwd(int C, int64_t n_gaussians, int D, int width, int h
 /* visible (ABI 27, may be NULL): i32[G] with visible[g] > 0 for every
  * Gaussian that has an isect (tiles_per_gauss); the 16x16 path then zeroes
  * and reads back only those Gaussians' gradient rows (the others' gradients
- * are written as zeros without reading anything). */
+ * are written as zeros without reading anything).  With vis_rank and
+ * n_isects_device both set, n_isects_device is the counts_device of
+ * gsplat_hip_isect_write_sorted_capped and its n_visible (element 1) bounds
+ * the rank-indexed rows, zeroed as one range. */
 
 /* Debug/profiling: when device_buffer (u64[2*capacity_waves]) is non-NULL, the
  * 16x16 rasterizer kernels store each wave's (start, end) s_memrealtime stamps
