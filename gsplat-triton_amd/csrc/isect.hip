@@ -623,8 +623,16 @@ static int isect_write_sorted_impl(
   GS_REQUIRE(!rank_ids == !vis_rank, "isect_write_sorted: rank_ids and vis_rank go together");
   GS_REQUIRE(!rank_ids || gsplat_hip_isect_ranked(n_cameras, tile_width, tile_height),
              "isect_write_sorted: rank ids need the supertile expansion");
+  // isect_ids / flatten_ids may both be null when rank_ids and offsets are
+  // written (a caller that walks the ranks and never reads the ids: the
+  // training step) -- 12 of the 16 bytes per isect not written
+  GS_REQUIRE((isect_ids && flatten_ids) || (!isect_ids && !flatten_ids && rank_ids && offsets),
+             "isect_write_sorted: null isect_ids / flatten_ids need rank_ids and offsets");
   auto plain_offsets = [&]() -> int {  // offsets from the written ids (or all zero)
     if (!offsets) return 0;
+    if (!isect_ids)  // nothing written (no isect or no visible Gaussian): all zero
+      return gs::zero_async(offsets, sizeof(int32_t) * (size_t)n_cameras * tile_width *
+                                         tile_height, st) == hipSuccess ? 0 : 2;
     return gsplat_hip_isect_offsets(cnt_dev ? n_isects : (n_visible > 0 ? n_isects : 0), cnt_dev,
                                     isect_ids, n_cameras, tile_width, tile_height, offsets, st);
   };

@@ -433,13 +433,16 @@ seg_write_kernel(Geo geo, const int64_t *__restrict__ cap, const int32_t *__rest
   WavePairs wp;
   load_pairs(sg, pval, rect, Vs, tpg, wp);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  int32_t g[4];
-  uint32_t db[4];
+  int32_t g[4] = {0, 0, 0, 0};
+  uint32_t db[4] = {0u, 0u, 0u, 0u};
+  const bool ids = isect_ids != nullptr;  // else rank ids only (see isect_write_sorted)
+  if (ids) {
 #pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const int s = max(wp.s[e], 0);
-    g[e] = Vs[s];
-    db[e] = dkeys[s];
+    for (int e = 0; e < 4; ++e) {
+      const int s = max(wp.s[e], 0);
+      g[e] = Vs[s];
+      db[e] = dkeys[s];
+    }
   }
   if (threadIdx.x < S * S) {  // the earlier segments of this supertile
     const int t = threadIdx.x;
@@ -473,8 +476,10 @@ seg_write_kernel(Geo geo, const int64_t *__restrict__ cap, const int32_t *__rest
       const int pos = cur[0] + x - c;
       const int64_t id = (int64_t)(int32_t)db[e];
       for (int k = 0; k < c; ++k) {
-        isect_ids[pos + k] = id;
-        flatten_ids[pos + k] = g[e];
+        if (ids) {
+          isect_ids[pos + k] = id;
+          flatten_ids[pos + k] = g[e];
+        }
         if (rank_ids) rank_ids[pos + k] = wp.s[e];
       }
       cur[0] += __shfl(x, 63, 64);
@@ -491,9 +496,11 @@ seg_write_kernel(Geo geo, const int64_t *__restrict__ cap, const int32_t *__rest
       if (bal == 0) continue;
       if (bit) {
         const int pos = cur[t] + __popcll(bal & lt);
-        const int tile = (sg.ty0 + t / S) * geo.tw + sg.tx0 + t % S;
-        isect_ids[pos] = ((tkey0 | (int64_t)tile) << 32) | (int64_t)db[e];
-        flatten_ids[pos] = g[e];
+        if (ids) {
+          const int tile = (sg.ty0 + t / S) * geo.tw + sg.tx0 + t % S;
+          isect_ids[pos] = ((tkey0 | (int64_t)tile) << 32) | (int64_t)db[e];
+          flatten_ids[pos] = g[e];
+        }
         if (rank_ids) rank_ids[pos] = wp.s[e];
       }
       cur[t] += __popcll(bal);

@@ -486,7 +486,8 @@ class _IsectCount:
                 torch.empty(G, dtype=torch.int32, device=dev))
 
     @torch.no_grad()
-    def finish_capped(self, capacity: int, status: Optional[Tensor] = None, report=None):
+    def finish_capped(self, capacity: int, status: Optional[Tensor] = None, report=None,
+                      ids: bool = True):
         """The sorted isects with NO host synchronisation (the one sync of
         isect_tiles, isect_tiles.py:101-102, removed so that a training step
         can be captured into a HIP graph): isect_ids / flatten_ids have
@@ -495,7 +496,10 @@ class _IsectCount:
         (counts[2] = 1; status[0] |= 1, sticky, when given); counts[1] = the
         visible Gaussians, counts[3] = n_isects whether it fit or not.
         `report` = (device pointer of a host-mapped i64[ring][4], device i64
-        slot tensor): the counts also go to that ring row.  Returns
+        slot tensor): the counts also go to that ring row.  ids=False (a
+        caller that only walks the depth ranks, the training step; needs
+        will_rank(capped=True)): isect_ids / flatten_ids are not written and
+        come back None -- the rank ids and offsets are.  Returns
         (tiles_per_gauss, isect_ids, flatten_ids, counts)."""
         (means2d, radii, depths, camera_ids, C, N, G, tile_size, tile_width, tile_height,
          n_bit_tile, n_bit_cam, packed) = self.args
@@ -505,12 +509,13 @@ class _IsectCount:
         ws = torch.empty(max(int(_lib.query("gsplat_hip_isect_sorted_capped_workspace_bytes", G,
                                             capacity, key_bits)), 8),
                          dtype=torch.uint8, device=dev)
-        isect_ids = torch.empty(capacity, dtype=torch.int64, device=dev)
-        flatten_ids = torch.empty(capacity, dtype=torch.int32, device=dev)
+        rk = self._rank_buffers(capacity, capped=True)
+        ids = ids or rk is None
+        isect_ids = torch.empty(capacity, dtype=torch.int64, device=dev) if ids else None
+        flatten_ids = torch.empty(capacity, dtype=torch.int32, device=dev) if ids else None
         counts = torch.empty(4, dtype=torch.int64, device=dev)  # written by the emission
         # the tile offsets too (as isect_offset_encode with _n_isects_device=counts)
         self.offsets = torch.empty((C, tile_height, tile_width), dtype=torch.int32, device=dev)
-        rk = self._rank_buffers(capacity, capped=True)
         if status is not None:
             assert status.dtype == torch.int32 and status.is_cuda
         ring, slot = (None, None) if report is None else report

@@ -213,7 +213,7 @@ class GraphStep:
             tr.height, sh_degree=deg, packed=False, near_plane=0.01, far_plane=1e10,
             radius_clip=0.0, rasterize_mode="classic", _fusion=fusion,
             _isect_capacity=self.capacity, _isect_status=self.status,
-            _isect_report=(self.ring_out.dev, self.slot), **dkw)
+            _isect_report=(self.ring_out.dev, self.slot), _isect_ids=False, **dkw)
         grad_box = {}
         meta["means2d"].register_hook(lambda g: grad_box.__setitem__("g", g))
         loss = tr._regularise(l1_ssim_loss(colors, tr.targets, tr.ssim_lambda, gt_index=self.cam))

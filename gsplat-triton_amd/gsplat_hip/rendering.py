@@ -15,7 +15,7 @@ from typing import Callable, Dict, Optional, Tuple
 import torch
 from torch import Tensor
 
-from . import _lib
+from . import _lib, _wrapper
 from ._wrapper import (
     _dev_check,
     _f32c,
@@ -76,6 +76,7 @@ def rasterization(
     _isect_report=None,
     _world_cameras=None,
     _world_counts=None,
+    _isect_ids: bool = True,
 ) -> Tuple[Tensor, Tensor, Dict]:
     """Rasterize N 3D Gaussians to C images (gsplat/rendering.py:44-598).
 
@@ -93,7 +94,10 @@ def rasterization(
     cameras in rank order and `_world_counts` = every rank's Gaussian count,
     when the caller knows them (a trainer's camera schedule and shard sizes):
     the all-gathers of gsplat/rendering.py:303-308 -- one of them a host
-    read -- are then skipped."""
+    read -- are then skipped.  `_isect_ids=False` (with `_isect_capacity`,
+    the training step): the sorted isects are emitted as depth ranks only
+    when the rasterizer walks ranks -- meta["isect_ids"] / ["flatten_ids"]
+    are then None (12 of 16 bytes per isect not written)."""
     meta = {}
     N = means.shape[0]
     C = viewmats.shape[0]
@@ -298,8 +302,11 @@ def rasterization(
 
     counts = None
     if capped:
+        # rank ids only: the rasterizer walks ranks through the render records
+        ids = (_isect_ids or late or not _wrapper.RECORDS
+               or opacities.numel() * 64 >= 2 ** 31)
         tiles_per_gauss, isect_ids, flatten_ids, counts = pending_isects.finish_capped(
-            _isect_capacity, _isect_status, _isect_report)
+            _isect_capacity, _isect_status, _isect_report, ids=ids)
         meta["isect_counts"] = counts
     else:
         tiles_per_gauss, isect_ids, flatten_ids = pending_isects.finish(sort=True)
@@ -308,6 +315,8 @@ def rasterization(
         isect_offsets = isect_offset_encode(isect_ids, C, tile_width, tile_height,
                                             _n_isects_device=counts)
     ranks = pending_isects.ranks
+    # the rasterizer's isect array: the flatten ids, or the rank ids it walks
+    raster_ids = flatten_ids if flatten_ids is not None else ranks[0]
     if late:
         _colors_ready()
         colors, backgrounds = add_depth(eval_colors(colors), backgrounds)
@@ -328,7 +337,7 @@ def rasterization(
             sl = slice(i * channel_chunk, (i + 1) * channel_chunk)
             rc, ra = _rasterize_to_pixels(
                 means2d, conics, colors[..., sl], opacities, width, height, tile_size,
-                isect_offsets, flatten_ids,
+                isect_offsets, raster_ids,
                 backgrounds=None if backgrounds is None else backgrounds[..., sl],
                 packed=packed, absgrad=absgrad, visible=visible, n_isects_device=counts,
                 ranks=ranks)
@@ -339,7 +348,7 @@ def rasterization(
     else:
         render_colors, render_alphas = _rasterize_to_pixels(
             means2d, conics, colors, opacities, width, height, tile_size, isect_offsets,
-            flatten_ids, backgrounds=backgrounds, packed=packed, absgrad=absgrad, visible=visible,
+            raster_ids, backgrounds=backgrounds, packed=packed, absgrad=absgrad, visible=visible,
             records=records, n_isects_device=counts, ranks=ranks)
     if render_mode in ["ED", "RGB+ED"]:
         render_colors = torch.cat(
