@@ -319,6 +319,7 @@ def main():
         # rasterizer launches over eager steps right after the timed region
         g = tr._graph
         graph_info = {"replays": g.replays, "captures": g.recaptures,
+                      "capture_ms": [round(1e3 * x, 1) for x in g.capture_s],
                       "isect_capacity": g.capacity, "max_isects": g.max_isects,
                       "host_issue_ms_per_step": 1e3 * g.host_s / max(g.replays, 1)}
         tr._graph = None

@@ -174,6 +174,7 @@ class GraphStep:
         self.pending = collections.deque()  # (it, slot, event) awaiting the overflow check
         self.issued = 0
         self.recaptures = 0
+        self.capture_s = []  # host seconds per capture (warm-up, capture, instantiate)
         self.replays = 0
         self.max_isects = 0
         self.host_s = 0.0
@@ -231,6 +232,13 @@ class GraphStep:
         return loss, meta["isect_counts"]
 
     def _capture(self, deg, stats=True):
+        t0 = time.perf_counter()
+        try:
+            self._capture_impl(deg, stats)
+        finally:
+            self.capture_s.append(time.perf_counter() - t0)
+
+    def _capture_impl(self, deg, stats=True):
         tr = self.tr
         from . import losses as _losses
         if _losses.ONE_GRAD is None or _losses.ONE_GRAD.device != self.dev:
