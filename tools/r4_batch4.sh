@@ -1,0 +1,28 @@
+#!/bin/bash
+# Round-4 batch 4: GPU suite, M2 twice with / without the chained LSD histograms, M3 eager + graph, kernel trace of
+# the default M2 line, and last the memset-node probe (it may fault: nothing
+# runs after it).  Test failures are reported; crashes / time limits end it.
+cd "$GRAFT_REPO_ROOT" || exit 1
+export TMPDIR=/tmp
+O=gpurun_out/${1:-r4_batch4}; mkdir -p $O
+v() { python3 -c "import json;d=json.loads(open('$1').read().strip().splitlines()[-1]);r=d['roofline'];print(round(d['value'],1), round(d['ms_per_step'],3), 'fwd', round(r['launch_ms'],4), 'bwd', round(r['bwd']['launch_ms'],4))"; }
+dead() { [ $1 -eq 124 ] || [ $1 -eq 137 ] || [ $1 -eq 134 ] || [ $1 -eq 139 ]; }
+timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 180 --timeout-method thread > $O/tests.log 2>&1
+rc=$?; echo "tests rc=$rc"; grep FAILED $O/tests.log; tail -1 $O/tests.log
+dead $rc && exit $rc
+for r in 1 2; do
+  for c in 1 0; do
+    GSPLAT_HIP_LSD_CHAIN=$c timeout -k 10 300 python -u bench.py --no-traffic --no-cpu-baseline > $O/m2_chain$c.$r.json 2> $O/m2_chain$c.$r.err || exit 2
+    echo "m2 lsd_chain=$c run $r $(v $O/m2_chain$c.$r.json)"
+  done
+done
+for m in eager graph; do
+  a=""; [ $m = eager ] && a="--eager"
+  timeout -k 10 400 python -u bench.py --config m3 --no-traffic --no-cpu-baseline $a > $O/m3_$m.json 2> $O/m3_$m.err || exit 5
+  echo "m3 $m $(v $O/m3_$m.json)"
+done
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $O/trace -o run -- /usr/bin/python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-traffic > $O/trace.log 2>&1 || exit 6
+echo "trace ok"
+timeout -k 10 400 python -u tools/memset_node_probe.py > $O/memset_probe.log 2>&1
+echo "memset probe rc=$?"; cat $O/memset_probe.log | tail -30
+exit 0
