@@ -23,6 +23,11 @@ for m in eager graph; do
 done
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $O/trace -o run -- /usr/bin/python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-traffic > $O/trace.log 2>&1 || exit 6
 echo "trace ok"
+# the default bench line (PMC traffic + CPU baseline), as the driver runs it
+timeout -k 10 600 python -u bench.py > $O/bench_m2.json 2> $O/bench_m2.err || exit 7
+echo "bench default $(v $O/bench_m2.json)"
+timeout -k 10 300 python -u bench.py --config m5 --no-traffic --no-cpu-baseline > $O/bench_m5.json 2> $O/bench_m5.err || exit 8
+echo "m5 $(v $O/bench_m5.json)"
 timeout -k 10 400 python -u tools/memset_node_probe.py > $O/memset_probe.log 2>&1
 echo "memset probe rc=$?"; cat $O/memset_probe.log | tail -30
 exit 0
