@@ -626,7 +626,8 @@ static int isect_write_sorted_impl(
   // isect_ids / flatten_ids may both be null when rank_ids and offsets are
   // written (a caller that walks the ranks and never reads the ids: the
   // training step) -- 12 of the 16 bytes per isect not written
-  GS_REQUIRE((isect_ids && flatten_ids) || (!isect_ids && !flatten_ids && rank_ids && offsets),
+  GS_REQUIRE(n_isects <= 0 || (isect_ids && flatten_ids) ||
+                 (!isect_ids && !flatten_ids && rank_ids && offsets),
              "isect_write_sorted: null isect_ids / flatten_ids need rank_ids and offsets");
   auto plain_offsets = [&]() -> int {  // offsets from the written ids (or all zero)
     if (!offsets) return 0;

@@ -95,14 +95,9 @@ hist_kernel(const uint32_t *__restrict__ keys, int64_t n, const int64_t *__restr
 // Device count: only the tiles holding items (tile = tile_items items).
 __global__ void __launch_bounds__(NT)
 scan_kernel(uint32_t *__restrict__ hist, int64_t nt, uint32_t *__restrict__ totals,
-            const int64_t *__restrict__ n_dev, int64_t n, int64_t tile_items,
-            uint32_t *__restrict__ hzero = nullptr) {
+            const int64_t *__restrict__ n_dev, int64_t n, int64_t tile_items) {
   __shared__ uint32_t wsum[NT / 64];
   uint32_t *row = hist + (int64_t)blockIdx.x * nt;
-  if (hzero) {  // the next pass's row of this digit, which the scatter fills by atomics
-    uint32_t *z = hzero + (int64_t)blockIdx.x * nt;
-    for (int64_t i = threadIdx.x; i < nt; i += NT) z[i] = 0u;
-  }
   if (n_dev) nt = min(nt, (min(n, *n_dev) + tile_items - 1) / tile_items);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   uint32_t carry = 0;
@@ -137,17 +132,13 @@ scan_kernel(uint32_t *__restrict__ hist, int64_t nt, uint32_t *__restrict__ tota
 // number of such lanes below.  Cross-wave offsets and the tile's digit starts
 // come from the 4 x 256 wave counts; items are then reordered through LDS so
 // the global stores are digit-contiguous.
-// hnext (may be null): the next pass's per-tile digit histogram (digit bits
-// [next_shift, next_shift + 8)), built here by one atomic add per item into
-// the row its key lands in (the scan kernel zeroed it) -- the next pass's
-// histogram launch is then not needed.
 template <int IPT, bool FINAL, int RX>
 __global__ void __launch_bounds__(NT)
 scatter_kernel(const uint32_t *__restrict__ kin, const int32_t *__restrict__ vin,
                uint32_t *__restrict__ kout, int32_t *__restrict__ vout, int64_t n,
                const int64_t *__restrict__ n_dev, int shift, int nbits,
                const uint32_t *__restrict__ hist, const uint32_t *__restrict__ totals, int64_t nt,
-               FinalOut fo, uint32_t *__restrict__ hnext = nullptr, int next_shift = 0) {
+               FinalOut fo) {
   constexpr int NW = NT / 64, TILE = NT * IPT, DPT = RX / NT;  // digits per thread
   __shared__ uint32_t cnt[NW][RX];
   __shared__ uint32_t gbase[RX];  // global position of tile slot 0 of digit d's range
@@ -265,8 +256,6 @@ scatter_kernel(const uint32_t *__restrict__ kin, const int32_t *__restrict__ vin
       } else {
         kout[dst] = k;
         vout[dst] = v;
-        if (hnext)
-          atomicAdd(&hnext[(int64_t)((k >> next_shift) & 255u) * nt + dst / (uint32_t)TILE], 1u);
       }
     }
   }
@@ -277,9 +266,7 @@ scatter_kernel(const uint32_t *__restrict__ kin, const int32_t *__restrict__ vin
 // Scratch for lsd_sort_pairs: hist rows + totals (sized for 11-bit digits).
 inline size_t lsd_sort_scratch_bytes(int64_t n) {
   const int64_t nt = lsd::n_tiles(n, lsd::pick_ipt(n));
-  // hist rows (11-bit digits at most) + totals + a second set of 8-bit rows
-  // (the next pass's histogram, filled by the scatter)
-  return 4 * (size_t)(lsd::RADIX_WIDE * nt + lsd::RADIX_WIDE + lsd::RADIX * nt);
+  return 4 * (size_t)(lsd::RADIX_WIDE * nt + lsd::RADIX_WIDE);
 }
 
 // Stable sort of n pairs by key bits [begin_bit, end_bit), ping-ponging
@@ -303,46 +290,30 @@ inline int lsd_sort_pairs(uint32_t *k0, int32_t *v0, uint32_t *k1, int32_t *v1, 
   }();
   const bool wide = wide_ok && end_bit - begin_bit > 24 && fo == nullptr;
   const int dbits = wide ? 11 : 8, radix = wide ? lsd::RADIX_WIDE : lsd::RADIX;
-  uint32_t *hbuf[2] = {reinterpret_cast<uint32_t *>(scratch), nullptr};
-  uint32_t *totals = hbuf[0] + (int64_t)radix * nt;
-  hbuf[1] = totals + lsd::RADIX_WIDE;
-  // 8-bit passes: each scatter builds the next pass's histogram (atomics into
-  // rows the scan zeroed), so only the first pass launches hist_kernel
-  // (GSPLAT_HIP_LSD_CHAIN=0: every pass its own histogram launch)
-  static const bool chain_ok = [] {
-    const char *e = getenv("GSPLAT_HIP_LSD_CHAIN");
-    return !(e && atoi(e) == 0);
-  }();
-  const bool chain = chain_ok && !wide;
-  int cur = 0, hb = 0;
-  bool have_hist = false;  // this pass's histogram built by the previous scatter
+  uint32_t *hist = reinterpret_cast<uint32_t *>(scratch);
+  uint32_t *totals = hist + (int64_t)radix * nt;
+  int cur = 0;
   for (int shift = begin_bit; shift < end_bit; shift += dbits) {
     const int nbits = end_bit - shift < dbits ? end_bit - shift : dbits;
     const uint32_t mask = (1u << nbits) - 1u;
     uint32_t *ki = cur ? k1 : k0, *ko = cur ? k0 : k1;
     int32_t *vi = cur ? v1 : v0, *vo = cur ? v0 : v1;
-    uint32_t *hist = hbuf[hb];
-    const bool next = chain && shift + dbits < end_bit && end_bit - (shift + dbits) >= dbits;
-    uint32_t *hnext = next ? hbuf[hb ^ 1] : nullptr;
 #define GS_LSD_HIST(I, RX)                                                                     \
   hipLaunchKernelGGL((lsd::hist_kernel<I, RX>), dim3((unsigned)nt), dim3(lsd::NT), 0, st, ki, n, \
                      n_dev, shift, mask, hist, nt)
-    if (!have_hist) {
-      if (wide) {
-        if (ipt == 4) GS_LSD_HIST(4, lsd::RADIX_WIDE); else GS_LSD_HIST(16, lsd::RADIX_WIDE);
-      } else {
-        if (ipt == 4) GS_LSD_HIST(4, lsd::RADIX); else GS_LSD_HIST(16, lsd::RADIX);
-      }
+    if (wide) {
+      if (ipt == 4) GS_LSD_HIST(4, lsd::RADIX_WIDE); else GS_LSD_HIST(16, lsd::RADIX_WIDE);
+    } else {
+      if (ipt == 4) GS_LSD_HIST(4, lsd::RADIX); else GS_LSD_HIST(16, lsd::RADIX);
     }
 #undef GS_LSD_HIST
     hipLaunchKernelGGL(lsd::scan_kernel, dim3((unsigned)radix), dim3(lsd::NT), 0, st, hist, nt,
-                       totals, n_dev, n, (int64_t)lsd::NT * ipt, hnext);
+                       totals, n_dev, n, (int64_t)lsd::NT * ipt);
     const bool fin = fo && shift + dbits >= end_bit;
     const lsd::FinalOut f = fin ? *fo : lsd::FinalOut{nullptr, nullptr, nullptr};
 #define GS_LSD_SCATTER(I, F, RX)                                                              \
   hipLaunchKernelGGL((lsd::scatter_kernel<I, F, RX>), dim3((unsigned)nt), dim3(lsd::NT), 0, st, \
-                     ki, vi, ko, vo, n, n_dev, shift, nbits, hist, totals, nt, f, hnext,      \
-                     shift + dbits)
+                     ki, vi, ko, vo, n, n_dev, shift, nbits, hist, totals, nt, f)
     if (wide) {
       if (ipt == 4) GS_LSD_SCATTER(4, false, lsd::RADIX_WIDE);
       else GS_LSD_SCATTER(16, false, lsd::RADIX_WIDE);
@@ -353,8 +324,6 @@ inline int lsd_sort_pairs(uint32_t *k0, int32_t *v0, uint32_t *k1, int32_t *v1, 
     }
 #undef GS_LSD_SCATTER
     cur ^= 1;
-    hb ^= next ? 1 : 0;
-    have_hist = next;
   }
   return cur;
 }

@@ -1134,11 +1134,25 @@ __attribute__((amdgpu_waves_per_eu(BwdOcc<PX>::W))) bwd2_kernel(Args a) {
         const int p = 64 * PX * w + 64 * q + lane;  // row-major pixel of the tile
         const int64_t per = (int64_t)(kTS * kTS * (1 + D));
         T[q] = fabsf(a.state[(cend / a.L) * per + p]);
+        // the later chunks' colours, four boundaries' loads in flight at a
+        // time (one round trip per four chunks of a long tile, not per
+        // chunk); summed in the same order as one at a time
         float s = 0.f;
-        for (int bi = cend; bi <= mylast[q]; bi += a.L) {
-          const float *sl = a.state + (bi / a.L) * per;
+        for (int b0 = cend; b0 <= mylast[q]; b0 += 4 * a.L) {
+          float v[4][D];
 #pragma unroll
-          for (int d = 0; d < D; ++d) s += sl[(1 + d) * kTS * kTS + p] * Drc[q][d];
+          for (int u = 0; u < 4; ++u) {
+            const int bi = b0 + u * a.L;
+            const float *sl = a.state + (min(bi, mylast[q]) / a.L) * per;
+#pragma unroll
+            for (int d = 0; d < D; ++d) v[u][d] = sl[(1 + d) * kTS * kTS + p];
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            if (b0 + u * a.L > mylast[q]) break;
+#pragma unroll
+            for (int d = 0; d < D; ++d) s += v[u][d] * Drc[q][d];
+          }
         }
         rD[q] = s;
       }

@@ -132,8 +132,12 @@ def test_dispatch_order_is_heaviest_first_permutation():
         torch.cuda.synchronize()
     finally:
         _lib.query("gsplat_hip_debug_set_fwd_split", old)
-    order_ints = (4 * nt + 255) // 256 * 64  # the order area, 256-B aligned, at the end
-    order = state[-order_ints:][:nt].cpu().numpy()
+    # the order area (256-B aligned) is followed by the backward's work-item
+    # lists (round 4: [2 counts, 256 B][full int2 x (n / L + 1)][tail int2 x
+    # nt], 256-B aligned; chunk length L = 256, the default)
+    order_ints = (4 * nt + 255) // 256 * 64
+    items_ints = (256 + 8 * (nt + n // 256 + 1) + 255) // 256 * 64
+    order = state[-(order_ints + items_ints):-items_ints][:nt].cpu().numpy()
     assert np.array_equal(np.sort(order), np.arange(nt)), "not a permutation"
     o = offs.flatten().cpu().numpy().astype(np.int64)
     cnt = np.diff(np.concatenate([o, [n]]))
