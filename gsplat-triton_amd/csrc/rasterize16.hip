@@ -1364,50 +1364,82 @@ GS_INLINE void block_max_out(int64_t v, int32_t *out) {
 // counts to n_items[0..1] (written, not accumulated).  1024 lanes, tiles tid
 // + 1024 i (n_tiles <= 16384), their isect counts cnt[i] (< 0: no tile) from
 // the caller's registers.  `full` null: nothing.
+// Both lists are in tile order (slot i = tiles 1024 i .. 1024 i + 1023, then
+// wave, then lane).  A wave writes its full chunks of one slot as one
+// contiguous run, 64 consecutive entries per store (each lane finds the tile
+// of its entry by a binary search over the wave's prefix of chunk counts):
+// one lane looping over its own tile's chunks scattered its stores over a
+// kilobyte per instruction, and a lone workgroup's request rate made that
+// the kernel's cost (20.6 us with the lists against 9.4 without).
+GS_INLINE int wave_incl_scan(int x) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  return x;
+}
+
 GS_INLINE void emit_bwd_items(const int (&cnt)[16], int L, int2 *full, int2 *tail,
                               int32_t *n_items) {
   if (!full) return;
-  __shared__ int ws[16][2];
+  __shared__ int ws[2][16][16];  // [list][slot][wave] wave totals -> bases
+  __shared__ int wtot[2];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  int nf = 0, nt = 0;
 #pragma unroll
   for (int i = 0; i < 16; ++i) {  // cnt < 0: no tile
     const int n = cnt[i] > 0 ? cnt[i] : 0;
-    nf += n / L;
-    nt += (n % L) != 0;
-  }
-  int xf = nf, xt = nt;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int yf = __shfl_up(xf, o, 64), yt = __shfl_up(xt, o, 64);
-    if (lane >= o) {
-      xf += yf;
-      xt += yt;
+    const int f = wave_incl_scan(n / L), e = wave_incl_scan((n % L) != 0);
+    if (lane == 63) {
+      ws[0][i][w] = f;
+      ws[1][i][w] = e;
     }
   }
-  if (lane == 63) {
-    ws[w][0] = xf;
-    ws[w][1] = xt;
+  __syncthreads();
+  if (w == 0) {  // exclusive scan of the 256 (slot, wave) totals per list, slot-major
+#pragma unroll
+    for (int l = 0; l < 2; ++l) {
+      int v[4], s = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        v[j] = (&ws[l][0][0])[4 * lane + j];
+        s += v[j];
+      }
+      const int incl = wave_incl_scan(s);
+      int b = incl - s;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        (&ws[l][0][0])[4 * lane + j] = b;
+        b += v[j];
+      }
+      if (lane == 63) wtot[l] = incl;
+    }
   }
   __syncthreads();
-  int bf = xf - nf, bt = xt - nt, tf = 0, tt = 0;
-  for (int ww = 0; ww < 16; ++ww) {
-    bf += ww < w ? ws[ww][0] : 0;
-    bt += ww < w ? ws[ww][1] : 0;
-    tf += ws[ww][0];
-    tt += ws[ww][1];
-  }
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     const int t = tid + 1024 * i;
     const int n = cnt[i] > 0 ? cnt[i] : 0;
-    const int f = n / L;
-    for (int k = 0; k < f; ++k) full[bf++] = make_int2(t, k);
-    if (n % L) tail[bt++] = make_int2(t, f);
+    const int f = n / L, e = (n % L) != 0;
+    const int incl = wave_incl_scan(f), incl_t = wave_incl_scan(e);
+    const int F = __builtin_amdgcn_readfirstlane(__shfl(incl, 63, 64));
+    int2 *run = full + ws[0][i][w];
+    for (int j0 = 0; j0 < F; j0 += 64) {  // every lane runs the search (shuffles)
+      const int j = j0 + lane;
+      int o = 0;  // the first lane whose inclusive prefix exceeds j (63 past F)
+#pragma unroll
+      for (int s = 32; s >= 1; s >>= 1)
+        if (__shfl(incl, o + s - 1, 64) <= j) o += s;
+      o = min(o, 63);
+      const int before = __shfl(incl - f, o, 64);
+      if (j < F) run[j] = make_int2(w * 64 + o + 1024 * i, j - before);
+    }
+    if (e) tail[ws[1][i][w] + incl_t - 1] = make_int2(t, f);
   }
   if (tid == 0) {
-    n_items[0] = tf;
-    n_items[1] = tt;
+    n_items[0] = wtot[0];
+    n_items[1] = wtot[1];
   }
 }
 

@@ -32,5 +32,10 @@ for _ in range(50):
     run()
 b.record()
 torch.cuda.synchronize()
+loss = l1_ssim_loss(img, gt, 0.2, fused=fused)
+loss.backward()
+torch.cuda.synchronize()
+# bit-level fingerprint: variants that only re-block the passes must agree
+fp = (float(loss), float(img.grad.double().sum()), float(img.grad.abs().double().sum()))
 print(f"fused={int(fused)} FV={os.environ.get('GSPLAT_HIP_SSIM_FV', '0')}: "
-      f"{a.elapsed_time(b) / 50 * 1e3:.1f} us per loss fwd+bwd")
+      f"{a.elapsed_time(b) / 50 * 1e3:.1f} us per loss fwd+bwd; fingerprint {fp!r}")
