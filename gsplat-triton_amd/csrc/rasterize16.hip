@@ -1358,91 +1358,6 @@ GS_INLINE void block_max_out(int64_t v, int32_t *out) {
   if (threadIdx.x == 0 && out) *out = smax;
 }
 
-// The backward's work items of this render (see chunk_items_kernel), made by
-// the forward's one-workgroup order / plan kernel, which reads the tile
-// counts anyway: full-length chunks to `full`, tails to `tail`, the two
-// counts to n_items[0..1] (written, not accumulated).  1024 lanes, tiles tid
-// + 1024 i (n_tiles <= 16384), their isect counts cnt[i] (< 0: no tile) from
-// the caller's registers.  `full` null: nothing.
-// Both lists are in tile order (slot i = tiles 1024 i .. 1024 i + 1023, then
-// wave, then lane).  A wave writes its full chunks of one slot as one
-// contiguous run, 64 consecutive entries per store (each lane finds the tile
-// of its entry by a binary search over the wave's prefix of chunk counts):
-// one lane looping over its own tile's chunks scattered its stores over a
-// kilobyte per instruction, and a lone workgroup's request rate made that
-// the kernel's cost (20.6 us with the lists against 9.4 without).
-GS_INLINE int wave_incl_scan(int x) {
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int y = __shfl_up(x, o, 64);
-    if (lane >= o) x += y;
-  }
-  return x;
-}
-
-GS_INLINE void emit_bwd_items(const int (&cnt)[16], int L, int2 *full, int2 *tail,
-                              int32_t *n_items) {
-  if (!full) return;
-  __shared__ int ws[2][16][16];  // [list][slot][wave] wave totals -> bases
-  __shared__ int wtot[2];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {  // cnt < 0: no tile
-    const int n = cnt[i] > 0 ? cnt[i] : 0;
-    const int f = wave_incl_scan(n / L), e = wave_incl_scan((n % L) != 0);
-    if (lane == 63) {
-      ws[0][i][w] = f;
-      ws[1][i][w] = e;
-    }
-  }
-  __syncthreads();
-  if (w == 0) {  // exclusive scan of the 256 (slot, wave) totals per list, slot-major
-#pragma unroll
-    for (int l = 0; l < 2; ++l) {
-      int v[4], s = 0;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        v[j] = (&ws[l][0][0])[4 * lane + j];
-        s += v[j];
-      }
-      const int incl = wave_incl_scan(s);
-      int b = incl - s;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        (&ws[l][0][0])[4 * lane + j] = b;
-        b += v[j];
-      }
-      if (lane == 63) wtot[l] = incl;
-    }
-  }
-  __syncthreads();
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int t = tid + 1024 * i;
-    const int n = cnt[i] > 0 ? cnt[i] : 0;
-    const int f = n / L, e = (n % L) != 0;
-    const int incl = wave_incl_scan(f), incl_t = wave_incl_scan(e);
-    const int F = __builtin_amdgcn_readfirstlane(__shfl(incl, 63, 64));
-    int2 *run = full + ws[0][i][w];
-    for (int j0 = 0; j0 < F; j0 += 64) {  // every lane runs the search (shuffles)
-      const int j = j0 + lane;
-      int o = 0;  // the first lane whose inclusive prefix exceeds j (63 past F)
-#pragma unroll
-      for (int s = 32; s >= 1; s >>= 1)
-        if (__shfl(incl, o + s - 1, 64) <= j) o += s;
-      o = min(o, 63);
-      const int before = __shfl(incl - f, o, 64);
-      if (j < F) run[j] = make_int2(w * 64 + o + 1024 * i, j - before);
-    }
-    if (e) tail[ws[1][i][w] + incl_t - 1] = make_int2(t, f);
-  }
-  if (tid == 0) {
-    n_items[0] = wtot[0];
-    n_items[1] = wtot[1];
-  }
-}
-
 // Forward dispatch order: tiles bucketed by isect count (>= 2048, >= 1024,
 // >= 512, the rest), heaviest bucket first, so the longest tiles start in the
 // first wave of workgroups instead of finishing last.  Inside a bucket: lane
@@ -1452,24 +1367,20 @@ GS_INLINE void emit_bwd_items(const int (&cnt)[16], int L, int2 *full, int2 *tai
 __global__ void __launch_bounds__(1024)
 tile_order_kernel(int n_tiles, const int32_t *__restrict__ offsets, int64_t n_isects,
                   const int64_t *__restrict__ n_dev, int32_t *__restrict__ order,
-                  int32_t *__restrict__ max_out, int L, int2 *__restrict__ items_full,
-                  int2 *__restrict__ items_tail, int32_t *__restrict__ n_items) {
+                  int32_t *__restrict__ max_out) {
   constexpr int MAXPER = 16;  // tiles per thread (n_tiles <= 16384)
   __shared__ uint64_t wsum[16];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   int bucket[MAXPER];
-  int cnt[MAXPER];  // isect counts fit 32 bits (the offsets are int32)
   uint64_t mine = 0;
   int64_t nmax = 0;
 #pragma unroll
   for (int i = 0; i < MAXPER; ++i) {
     const int t = tid + 1024 * i;
     bucket[i] = -1;
-    cnt[i] = -1;
     if (t < n_tiles) {
       const int64_t e = tile_end(offsets, t, n_tiles, n_dev, n_isects);
       const int64_t n = e - offsets[t];
-      cnt[i] = (int)n;
       nmax = max(nmax, n);
       bucket[i] = n >= 2048 ? 0 : n >= 1024 ? 1 : n >= 512 ? 2 : 3;
       mine += (uint64_t)1 << (16 * bucket[i]);
@@ -1512,7 +1423,6 @@ tile_order_kernel(int n_tiles, const int32_t *__restrict__ offsets, int64_t n_is
       pos[3] += bk == 3;
     }
   }
-  emit_bwd_items(cnt, L, items_full, items_tail, n_items);
 }
 
 // Forward plan with split heavy tiles, decided on this render's tiles.  A
@@ -1529,26 +1439,17 @@ fwd_plan_kernel(int n_tiles, const int32_t *__restrict__ offsets, int64_t n_isec
                 const int64_t *__restrict__ n_dev, const uint8_t *__restrict__ masks, int SL,
                 int L, int split, int32_t *__restrict__ hdr, int32_t *__restrict__ order,
                 int2 *__restrict__ chunks, int32_t *__restrict__ pflag,
-                int32_t *__restrict__ ctr, int32_t *__restrict__ max_out,
-                int2 *__restrict__ items_full, int2 *__restrict__ items_tail,
-                int32_t *__restrict__ n_items) {
+                int32_t *__restrict__ ctr, int32_t *__restrict__ max_out) {
   // quantities: [0..3] whole tiles per bucket, [4] chunks
   constexpr int PER = 16, NQ = 5;
   __shared__ int wsum[16][NQ];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  // the 16 tiles' isect counts, loaded once with every load in flight (< 0:
-  // no tile)
-  int cnt[PER];  // isect counts fit 32 bits (the offsets are int32)
-#pragma unroll
-  for (int i = 0; i < PER; ++i) {
-    const int t = tid + 1024 * i;
-    cnt[i] = t < n_tiles ? (int)(tile_end(offsets, t, n_tiles, n_dev, n_isects) - offsets[t]) : -1;
-  }
-  // bucket (or -1: split) and chunk count of tile i of this lane
-  auto classify = [&](int i, int &nch) -> int {
-    const int n = cnt[i];
+  // bucket (or -1: split) and chunk count of tile t (recomputed in the write
+  // pass: keeps the 16 tiles' state out of registers)
+  auto classify = [&](int t, int &nch) -> int {
+    const int64_t n = tile_end(offsets, t, n_tiles, n_dev, n_isects) - offsets[t];
     nch = 0;
-    if (n > split && !(masks && masks[tid + 1024 * i])) {
+    if (n > split && !(masks && masks[t])) {
       nch = (int)((n + SL - 1) / SL);
       return -1;
     }
@@ -1556,15 +1457,15 @@ fwd_plan_kernel(int n_tiles, const int32_t *__restrict__ offsets, int64_t n_isec
   };
   int mine[NQ] = {0, 0, 0, 0, 0};
   int64_t nmax = 0;
-#pragma unroll
   for (int i = 0; i < PER; ++i) {
-    if (cnt[i] < 0) continue;
+    const int t = tid + 1024 * i;
+    if (t >= n_tiles) break;
     int nch;
-    const int kd = classify(i, nch);
+    const int kd = classify(t, nch);
 #pragma unroll
     for (int q = 0; q < 4; ++q) mine[q] += q == kd;
     mine[4] += nch;
-    nmax = max(nmax, (int64_t)cnt[i]);
+    nmax = max(nmax, tile_end(offsets, t, n_tiles, n_dev, n_isects) - offsets[t]);
   }
   block_max_out(nmax, max_out);
   int x[NQ];
@@ -1599,12 +1500,11 @@ fwd_plan_kernel(int n_tiles, const int32_t *__restrict__ offsets, int64_t n_isec
     pos[q] += base;
     base += total[q];
   }
-#pragma unroll
   for (int i = 0; i < PER; ++i) {
     const int t = tid + 1024 * i;
-    if (cnt[i] < 0) continue;
+    if (t >= n_tiles) break;
     int nch;
-    const int kd = classify(i, nch);
+    const int kd = classify(t, nch);
     if (kd < 0) {
       ctr[pos[4]] = 0;  // index of chunk 0
       for (int k = 0; k < nch; ++k) {
@@ -1630,7 +1530,6 @@ fwd_plan_kernel(int n_tiles, const int32_t *__restrict__ offsets, int64_t n_isec
     hdr[0] = base;
     hdr[1] = total[4];
   }
-  emit_bwd_items(cnt, L, items_full, items_tail, n_items);
 }
 
 // Backward work items.  A tile with n isects becomes ceil(n / L) items
@@ -1877,32 +1776,9 @@ static int64_t n_items_bound(int n_tiles, int64_t n_isects) {
   return L ? (int64_t)n_tiles + n_isects / L + 1 : (int64_t)n_tiles;
 }
 
-// After the split area: the backward's work items, written by the order /
-// plan kernel ([n_items i32 x 2, 256 B][full int2 x (n_isects / L + 1)][tail
-// int2 x n_tiles], bwd workspace layout), when the forward has chunk slots
-// and a tile order.
-static int64_t items_bytes(int D, int n_tiles, int64_t n_isects) {
-  return (chunk_slot_bytes(D, n_isects) > 0 && use_order(n_tiles, n_isects))
-             ? align256(256 + (int64_t)sizeof(int2) * n_items_bound(n_tiles, n_isects)) : 0;
-}
-
 int64_t rasterize16_fwd_state_bytes(int D, int n_tiles, int64_t n_isects) {
   return chunk_slot_bytes(D, n_isects) + order_bytes(n_tiles, n_isects) +
-         split_layout(D, n_tiles, n_isects).bytes + items_bytes(D, n_tiles, n_isects);
-}
-
-struct ItemLists {
-  int32_t *n_items;
-  int2 *full, *tail;
-};
-
-static ItemLists item_lists(const void *state, int D, int n_tiles, int64_t n_isects) {
-  if (!state || items_bytes(D, n_tiles, n_isects) == 0) return ItemLists{nullptr, nullptr, nullptr};
-  char *b = const_cast<char *>(reinterpret_cast<const char *>(state)) +
-            chunk_slot_bytes(D, n_isects) + order_bytes(n_tiles, n_isects) +
-            split_layout(D, n_tiles, n_isects).bytes;
-  int2 *full = reinterpret_cast<int2 *>(b + 256);
-  return ItemLists{reinterpret_cast<int32_t *>(b), full, full + (n_isects / chunk_len() + 1)};
+         split_layout(D, n_tiles, n_isects).bytes;
 }
 
 // Pixels per lane in the backward (1: bwd_kernel, 16x4 per wave; 2 or 4:
@@ -1962,7 +1838,7 @@ static thread_local bool g_prepared_split = false;  // the split decision of tha
 
 static void launch_order(int n_tiles, const int32_t *offsets, int64_t n_isects,
                          const int64_t *n_dev, int32_t *order, hipStream_t st,
-                         char *split_base, int D, const ItemLists &it) {
+                         char *split_base, int D) {
   if (split_base) {
     const SplitLayout l = split_layout(D, n_tiles, n_isects);
     hipLaunchKernelGGL(r16::fwd_plan_kernel, dim3(1), dim3(1024), 0, st, n_tiles, offsets,
@@ -1971,20 +1847,18 @@ static void launch_order(int n_tiles, const int32_t *offsets, int64_t n_isects,
                        reinterpret_cast<int32_t *>(split_base + l.hdr), order,
                        reinterpret_cast<int2 *>(split_base + l.fitems),
                        reinterpret_cast<int32_t *>(split_base + l.pflag),
-                       reinterpret_cast<int32_t *>(split_base + l.ctr), stat_dev(), it.full,
-                       it.tail, it.n_items);
+                       reinterpret_cast<int32_t *>(split_base + l.ctr), stat_dev());
   } else
     hipLaunchKernelGGL(r16::tile_order_kernel, dim3(1), dim3(1024), 0, st, n_tiles, offsets,
                        n_isects, n_dev, order,
-                       split_capable(n_tiles, n_isects) ? stat_dev() : nullptr, chunk_len(),
-                       it.full, it.tail, it.n_items);
+                       split_capable(n_tiles, n_isects) ? stat_dev() : nullptr);
 }
 
 template <int D>
 int r16_fwd(r16::Args a, const void *state, char *split_base, hipStream_t st) {
   if (a.order && state != g_prepared_state)
     launch_order(a.n_tiles, a.offsets, a.n_isects, a.n_dev, const_cast<int32_t *>(a.order), st,
-                 split_base, D, item_lists(state, D, a.n_tiles, a.n_isects));
+                 split_base, D);
   g_prepared_state = nullptr;
   if (split_base) {
     // the split tiles' chunks and the other tiles in one launch; the grid is
@@ -2049,7 +1923,7 @@ zero_ranked_rows_kernel(int64_t G, int S, const int64_t *__restrict__ counts,
 template <int D, bool ABS>
 int r16_bwd(r16::Args a, int64_t G, float *v_means2d, float *v_conics, float *v_colors,
             float *v_opacities, float *v_abs, void *workspace, const int32_t *visible,
-            const int32_t *vis_rank, const ItemLists &fwd_items, hipStream_t st) {
+            const int32_t *vis_rank, hipStream_t st) {
   constexpr int F = D + 6 + (ABS ? 2 : 0);
   a.S = ((F + 15) / 16) * 16;
   a.packed = reinterpret_cast<float *>(workspace);
@@ -2074,12 +1948,7 @@ int r16_bwd(r16::Args a, int64_t G, float *v_means2d, float *v_conics, float *v_
   }
   if (a.n_isects > 0) {
     int64_t grid = a.n_tiles;
-    if (chunked && fwd_items.full) {  // made by the forward's order / plan kernel
-      a.n_items = fwd_items.n_items;
-      a.items = fwd_items.full;
-      a.items_tail = fwd_items.tail;
-      grid = n_items_bound(a.n_tiles, a.n_isects);
-    } else if (chunked) {
+    if (chunked) {
       char *w = reinterpret_cast<char *>(workspace) + packed_bytes(D, ABS, G);
       a.n_items = reinterpret_cast<int32_t *>(w);
       a.items = reinterpret_cast<int2 *>(w + 256);
@@ -2182,8 +2051,7 @@ int rasterize16_prepare(int D, int n_tiles, const int32_t *offsets, int64_t n_is
   int32_t *order = reinterpret_cast<int32_t *>(base);
   const bool split = chunk_slot_bytes(D, n_isects) > 0 && use_split_now(n_tiles, n_isects);
   launch_order(n_tiles, offsets, n_isects, n_isects_dev, order, st,
-               split ? base + order_bytes(n_tiles, n_isects) : nullptr, D,
-               item_lists(state, D, n_tiles, n_isects));
+               split ? base + order_bytes(n_tiles, n_isects) : nullptr, D);
   GS_CHECK_LAUNCH("rasterize_prepare");
   g_prepared_state = state;
   g_prepared_split = split;
@@ -2228,14 +2096,13 @@ int rasterize16_bwd(int C, int64_t G, int D, int W, int H, int tw, int th,
                 ? const_cast<float *>(reinterpret_cast<const float *>(state)) : nullptr;
   a.render_colors_in = render_colors;
   a.dbg = dbg_flags();
-  const ItemLists fi = a.state ? item_lists(state, D, a.n_tiles, n_isects) : ItemLists{};
   const bool ab = v_abs != nullptr;
 #define GS_R16B(DD)                                                                            \
   case DD:                                                                                     \
     return ab ? r16_bwd<DD, true>(a, G, v_means2d, v_conics, v_colors, v_opacities, v_abs,     \
-                                  workspace, visible, vis_rank, fi, st)                        \
+                                  workspace, visible, vis_rank, st)                            \
               : r16_bwd<DD, false>(a, G, v_means2d, v_conics, v_colors, v_opacities, v_abs,    \
-                                   workspace, visible, vis_rank, fi, st);
+                                   workspace, visible, vis_rank, st);
   switch (D) { GS_R16B(1) GS_R16B(2) GS_R16B(3) GS_R16B(4) GS_R16B(8) GS_R16B(16) GS_R16B(32) }
 #undef GS_R16B
   GS_REQUIRE(false, "rasterize16_bwd: unsupported channels %d", D);

@@ -475,14 +475,12 @@ constexpr int kOffA = FI * SX * 8, kOffB = kOffA + FI * SH * 8, kOffC = kOffB + 
 constexpr int kFusedLds = kOffC + FI * SH * 4;
 static_assert(FM * SH * 12 <= FI * SX * 8, "maps fit in s_xy");
 static_assert(FM * SG * 12 <= FI * SH * 8, "backward h-pass fits in hA");
-constexpr int kHC = 4;  // adjacent outputs per work item in pass C1
+constexpr int kHA = 6, kHC = 4;  // adjacent outputs per work item in passes A, C1
 
-// BR: map rows per work item of pass B (sliding window of K + BR - 1 rows);
-// CR: image rows per thread in pass C2 (2: all 512 threads, 4: 256);
-// KA: adjacent outputs per work item of pass A.  Passes A and C1 are
-// register-blocked: KA / kHC adjacent outputs of one row from one run of
-// K + KA - 1 / K + kHC - 1 LDS values.
-template <int C, int BR, int CR, int KA>
+// BR: map rows per work item of pass B (sliding window of K + BR - 1 rows).
+// Passes A and C1 are register-blocked: kHA / kHC adjacent outputs of one
+// row from one run of K + kHA - 1 / K + kHC - 1 LDS values.
+template <int C, int BR>
 __global__ void __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(4)))
 fused_kernel(int B, int H, int W, const float *__restrict__ x, const float *__restrict__ y,
              const int64_t *__restrict__ y_index, float cs, float cl, float *__restrict__ grad,
@@ -528,10 +526,8 @@ fused_kernel(int B, int H, int W, const float *__restrict__ x, const float *__re
     }
   };
   float lsum = 0.f, ssum = 0.f;
-  // backward vertical pass mapping: column gc, image rows CR gr .. CR gr + CR - 1
-  static_assert(FT * FT / CR <= kFThreads, "pass C2 mapping");
+  // backward vertical pass mapping: column gc, image rows 2 gr, 2 gr + 1
   const int gc = tid & 31, gr = tid >> 5;
-  const bool c2 = tid < FT * FT / CR;
 #pragma nounroll
   for (int c = 0; c < C; ++c) {
     // ---- stage channel c (+ its L1 over the tile's own pixels, window
@@ -547,45 +543,33 @@ fused_kernel(int B, int H, int W, const float *__restrict__ x, const float *__re
         lsum += fabsf(a - bb);
     }
     __syncthreads();
-    f2v px[CR];  // (x, y) of this thread's pass-C2 pixels
-#pragma unroll
-    for (int j = 0; j < CR; ++j)
-      px[j] = c2 ? s_xy[2 * R + CR * gr + j][2 * R + gc] : f2v{0.f, 0.f};
+    const f2v px0 = s_xy[2 * R + 2 * gr][2 * R + gc], px1 = s_xy[2 * R + 2 * gr + 1][2 * R + gc];
     // ---- A: horizontal blur of the statistics, FI rows x FM columns
-    static_assert(FM % KA == 0 && FT % kHC == 0, "pass A / C1 blocking");
-    for (int idx = tid; idx < FI * (FM / KA); idx += kFThreads) {
-      const int jg = idx / FI, r = idx - jg * FI, j0 = jg * KA;
-      // input-outer: one window value live at a time, KA accumulators (each
-      // output still sums its taps k = 0 .. K-1 in order)
-      f2v a[KA], bb[KA];
-      float cc[KA];
+    static_assert(FM % kHA == 0 && FT % kHC == 0, "pass A / C1 blocking");
+    for (int idx = tid; idx < FI * (FM / kHA); idx += kFThreads) {
+      const int jg = idx / FI, r = idx - jg * FI, j0 = jg * kHA;
+      f2v v[K + kHA - 1], sq[K + kHA - 1];
+      float xy[K + kHA - 1];
 #pragma unroll
-      for (int o = 0; o < KA; ++o) {
-        a[o] = f2v{0.f, 0.f};
-        bb[o] = f2v{0.f, 0.f};
-        cc[o] = 0.f;
+      for (int i = 0; i < K + kHA - 1; ++i) {
+        v[i] = s_xy[r][j0 + i];
+        sq[i] = v[i] * v[i];
+        xy[i] = v[i].x * v[i].y;
       }
 #pragma unroll
-      for (int i = 0; i < K + KA - 1; ++i) {
-        const f2v v = s_xy[r][j0 + i];
-        const f2v sq = v * v;
-        const float xy = v.x * v.y;
+      for (int o = 0; o < kHA; ++o) {
+        f2v a = {0.f, 0.f}, bb = {0.f, 0.f};
+        float cc = 0.f;
 #pragma unroll
-        for (int o = 0; o < KA; ++o) {
-          const int k = i - o;
-          if (k >= 0 && k < K) {
-            const float g = kG[k];
-            a[o] = __builtin_elementwise_fma(f2v{g, g}, v, a[o]);
-            bb[o] = __builtin_elementwise_fma(f2v{g, g}, sq, bb[o]);
-            cc[o] = __builtin_fmaf(g, xy, cc[o]);
-          }
+        for (int k = 0; k < K; ++k) {
+          const float g = kG[k];
+          a = __builtin_elementwise_fma(f2v{g, g}, v[o + k], a);
+          bb = __builtin_elementwise_fma(f2v{g, g}, sq[o + k], bb);
+          cc = __builtin_fmaf(g, xy[o + k], cc);
         }
-      }
-#pragma unroll
-      for (int o = 0; o < KA; ++o) {
-        hA[r][j0 + o] = a[o];
-        hB[r][j0 + o] = bb[o];
-        hC[r][j0 + o] = cc[o];
+        hA[r][j0 + o] = a;
+        hB[r][j0 + o] = bb;
+        hC[r][j0 + o] = cc;
       }
     }
     __syncthreads();
@@ -647,31 +631,25 @@ fused_kernel(int B, int H, int W, const float *__restrict__ x, const float *__re
     // kernel, see bwd_kernel), into hA
     for (int idx = tid; idx < FM * (FT / kHC); idx += kFThreads) {
       const int jg = idx / FM, r = idx - jg * FM, j0 = jg * kHC;
-      f2v a[kHC];
-      float cc[kHC];
-#pragma unroll
-      for (int o = 0; o < kHC; ++o) {
-        a[o] = f2v{0.f, 0.f};
-        cc[o] = 0.f;
-      }
+      f2v v[K + kHC - 1];
+      float w[K + kHC - 1];
 #pragma unroll
       for (int i = 0; i < K + kHC - 1; ++i) {
-        const f2v v = m01[r][j0 + i];
-        const float w = m2[r][j0 + i];
-#pragma unroll
-        for (int o = 0; o < kHC; ++o) {
-          const int k = i - o;
-          if (k >= 0 && k < K) {
-            const float g = kG[k];
-            a[o] = __builtin_elementwise_fma(f2v{g, g}, v, a[o]);
-            cc[o] = __builtin_fmaf(g, w, cc[o]);
-          }
-        }
+        v[i] = m01[r][j0 + i];
+        w[i] = m2[r][j0 + i];
       }
 #pragma unroll
       for (int o = 0; o < kHC; ++o) {
-        g01[r][j0 + o] = a[o];
-        g2[r][j0 + o] = cc[o];
+        f2v a = {0.f, 0.f};
+        float cc = 0.f;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          const float g = kG[k];
+          a = __builtin_elementwise_fma(f2v{g, g}, v[o + k], a);
+          cc = __builtin_fmaf(g, w[o + k], cc);
+        }
+        g01[r][j0 + o] = a;
+        g2[r][j0 + o] = cc;
       }
     }
     __syncthreads();
@@ -679,21 +657,16 @@ fused_kernel(int B, int H, int W, const float *__restrict__ x, const float *__re
     // channel's staging writes only s_xy, whose last readers, pass C1, are
     // behind the barrier above; its pass A rewrites hA only after the
     // staging barrier, which every thread reaches after its C2.)
-    if (c2) {
-      f2v oa[CR];
-      float oc[CR];
+    {
+      f2v oa[2] = {f2v{0.f, 0.f}, f2v{0.f, 0.f}};
+      float oc[2] = {0.f, 0.f};
 #pragma unroll
-      for (int j = 0; j < CR; ++j) {
-        oa[j] = f2v{0.f, 0.f};
-        oc[j] = 0.f;
-      }
-#pragma unroll
-      for (int i = 0; i < K + CR - 1; ++i) {
-        const int r = CR * gr + i;
+      for (int i = 0; i < K + 1; ++i) {
+        const int r = 2 * gr + i;
         const f2v a = g01[r][gc];
         const float cc = g2[r][gc];
 #pragma unroll
-        for (int j = 0; j < CR; ++j) {
+        for (int j = 0; j < 2; ++j) {
           const int k = i - j;
           if (k >= 0 && k < K) {
             const float g = kG[k];
@@ -703,9 +676,9 @@ fused_kernel(int B, int H, int W, const float *__restrict__ x, const float *__re
         }
       }
 #pragma unroll
-      for (int j = 0; j < CR; ++j) {
-        const int qi = qi0 + CR * gr + j, qj = qj0 + gc;
-        const f2v v = px[j];
+      for (int j = 0; j < 2; ++j) {
+        const int qi = qi0 + 2 * gr + j, qj = qj0 + gc;
+        const f2v v = j ? px1 : px0;
         const float d = v.x - v.y;
         const float sgn = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
         if (qi < H && qj < W)
@@ -878,22 +851,13 @@ extern "C" int gsplat_hip_l1_ssim_loss_fused_fwd(int B, int H, int W, int C, con
     const char *e = getenv("GSPLAT_HIP_SSIM_FV");
     return e ? atoi(e) : 0;
   }();
-#define GS_FUSED(CC, BR, CR, KA)                                                            \
-  hipLaunchKernelGGL((ssim::fused_kernel<CC, BR, CR, KA>), grid, dim3(ssim::kFThreads), 0, st, B, \
-                     H, W, img1, img2, img2_index, cs, cl, grad_unit, partials)
+#define GS_FUSED(CC, BR)                                                                   \
+  hipLaunchKernelGGL((ssim::fused_kernel<CC, BR>), grid, dim3(ssim::kFThreads), 0, st, B, H, W, \
+                     img1, img2, img2_index, cs, cl, grad_unit, partials)
   if (C == 3) {
-    switch (fv) {  // A/B variants (tools/ab_ssim3.sh)
-      case 1: GS_FUSED(3, 2, 2, 6); break;
-      case 2: GS_FUSED(3, 6, 2, 6); break;
-      case 3: GS_FUSED(3, 7, 2, 6); break;
-      case 4: GS_FUSED(3, 4, 4, 6); break;
-      case 5: GS_FUSED(3, 6, 4, 6); break;
-      case 6: GS_FUSED(3, 6, 4, 7); break;
-      case 7: GS_FUSED(3, 7, 4, 7); break;
-      default: GS_FUSED(3, 4, 2, 6);
-    }
+    if (fv == 1) GS_FUSED(3, 2); else GS_FUSED(3, 4);
   } else {
-    GS_FUSED(1, 2, 2, 6);
+    GS_FUSED(1, 2);
   }
 #undef GS_FUSED
   hipLaunchKernelGGL(ssim::reduce_partials_kernel, dim3(1), dim3(1024), 0, st, (int)(B * nt),

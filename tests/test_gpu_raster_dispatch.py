@@ -132,12 +132,9 @@ def test_dispatch_order_is_heaviest_first_permutation():
         torch.cuda.synchronize()
     finally:
         _lib.query("gsplat_hip_debug_set_fwd_split", old)
-    # the order area (256-B aligned) is followed by the backward's work-item
-    # lists (round 4: [2 counts, 256 B][full int2 x (n / L + 1)][tail int2 x
-    # nt], 256-B aligned; chunk length L = 256, the default)
+    # the order area (256-B aligned) is the last part of the state
     order_ints = (4 * nt + 255) // 256 * 64
-    items_ints = (256 + 8 * (nt + n // 256 + 1) + 255) // 256 * 64
-    order = state[-(order_ints + items_ints):-items_ints][:nt].cpu().numpy()
+    order = state[-order_ints:][:nt].cpu().numpy()
     assert np.array_equal(np.sort(order), np.arange(nt)), "not a permutation"
     o = offs.flatten().cpu().numpy().astype(np.int64)
     cnt = np.diff(np.concatenate([o, [n]]))
@@ -148,19 +145,6 @@ def test_dispatch_order_is_heaviest_first_permutation():
     for bk in range(4):  # lane t % 1024 holds tiles t, t + 1024, ...: lane-major
         t = order[b == bk].astype(np.int64)
         assert np.all(np.diff((t % 1024) * 16 + t // 1024) > 0), f"bucket {bk}: not lane order"
-    # the backward's work items, in tile order: every full-length chunk (t, k),
-    # then one tail (t, n // L) per tile whose count is not a multiple of L
-    items = state[-items_ints:].cpu().numpy()
-    nf, ntl = int(items[0]), int(items[1])
-    L = 256
-    full = items[64:64 + 2 * (n // L + 1)].reshape(-1, 2)
-    tail = items[64 + 2 * (n // L + 1):64 + 2 * (n // L + 1) + 2 * nt].reshape(-1, 2)
-    want_full = np.array([(t, k) for t in range(nt) for k in range(cnt[t] // L)]).reshape(-1, 2)
-    want_tail = np.array([(t, cnt[t] // L) for t in range(nt) if cnt[t] % L]).reshape(-1, 2)
-    assert nf == len(want_full) and ntl == len(want_tail), (nf, len(want_full), ntl, len(want_tail))
-    assert nf > 0, "scene has no full-length chunks"
-    assert np.array_equal(full[:nf], want_full)
-    assert np.array_equal(tail[:ntl], want_tail)
 
 
 def _heavy_scene(N=60000, W=320, H=240, seed=5):
