@@ -1915,8 +1915,11 @@ __global__ void __launch_bounds__(256)
 zero_ranked_rows_kernel(int64_t G, int S, const int64_t *__restrict__ counts,
                         float *__restrict__ packed, int64_t tail_floats) {
   const int64_t nv = min(G, counts[1]);
-  const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;  // float4 slot
-  if (q < nv * (S / 4)) reinterpret_cast<float4 *>(packed)[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+  // grid-stride over the live float4 slots (the grid is sized for the
+  // expected live rows, not for all G: no workgroups that only exit)
+  const int64_t n4 = nv * (S / 4);
+  for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < n4; q += (int64_t)gridDim.x * 256)
+    reinterpret_cast<float4 *>(packed)[q] = make_float4(0.f, 0.f, 0.f, 0.f);
   if (blockIdx.x == 0 && threadIdx.x < tail_floats) packed[G * S + threadIdx.x] = 0.f;
 }
 
@@ -1938,8 +1941,8 @@ int r16_bwd(r16::Args a, int64_t G, float *v_means2d, float *v_conics, float *v_
     const int64_t tail = (int64_t)(pb / 4) - G * a.S + (chunked ? 64 : 0);
     if (vis_rank && a.n_dev)  // the counts of the sync-free isect: rows 0 .. n_visible - 1
       hipLaunchKernelGGL(zero_ranked_rows_kernel,
-                         dim3((unsigned)((G * (a.S / 4) + 255) / 256)), dim3(256), 0, st, G, a.S,
-                         a.n_dev, a.packed, tail);
+                         dim3((unsigned)std::min<int64_t>((G * (a.S / 4) + 255) / 256, 2048)),
+                         dim3(256), 0, st, G, a.S, a.n_dev, a.packed, tail);
     else
       hipLaunchKernelGGL(zero_rows_kernel, dim3((unsigned)((G + 255) / 256)), dim3(256), 0, st,
                          G, a.S, visible, vis_rank, a.packed, tail);

@@ -26,28 +26,59 @@
 namespace gs {
 namespace strat {
 
+GS_INLINE void update_one(float r, float vx, float vy, float sx, float sy, float &acc,
+                          float &cnt) {
+  if (r > 0.f) {
+    const float x = vx * sx, y = vy * sy;
+    acc += sqrtf(x * x + y * y);  // .norm(dim=-1) of a 2-vector
+    cnt += 1.f;
+  }
+}
+
+// Four Gaussians per lane.  VEC (16-B aligned arrays, and C == 1 or N a
+// multiple of 4): 16-B loads, every load of the lane issued before the
+// arithmetic (the gradient rows unconditionally), the four accumulators
+// stored back whole (an untouched one rewrites its own bits).
+template <bool VEC>
 __global__ void __launch_bounds__(256)
 update_state_kernel(int C, int64_t N, const float *__restrict__ g2d,
                     const int32_t *__restrict__ radii, float sx, float sy,
                     float *__restrict__ grad2d, float *__restrict__ count,
                     const int32_t *__restrict__ skip) {
-  const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (g >= N || (skip && *skip)) return;
-  float acc = grad2d[g], cnt = count[g];
-  bool any = false;
-  for (int c = 0; c < C; ++c) {
-    const int64_t i = (int64_t)c * N + g;
-    if (radii[i] > 0) {
-      const float2 v = *reinterpret_cast<const float2 *>(g2d + 2 * i);
-      const float x = v.x * sx, y = v.y * sy;
-      acc += sqrtf(x * x + y * y);  // .norm(dim=-1) of a 2-vector
-      cnt += 1.f;
-      any = true;
+  const int64_t g0 = 4 * ((int64_t)blockIdx.x * 256 + threadIdx.x);
+  if (g0 >= N || (skip && *skip)) return;
+  if (VEC && g0 + 4 <= N) {
+    float4 acc = *reinterpret_cast<const float4 *>(grad2d + g0);
+    float4 cnt = *reinterpret_cast<const float4 *>(count + g0);
+    for (int c = 0; c < C; ++c) {
+      const int64_t i = (int64_t)c * N + g0;
+      const int4 r = *reinterpret_cast<const int4 *>(radii + i);
+      const float4 a = *reinterpret_cast<const float4 *>(g2d + 2 * i);
+      const float4 b = *reinterpret_cast<const float4 *>(g2d + 2 * i + 4);
+      update_one(r.x > 0 ? 1.f : 0.f, a.x, a.y, sx, sy, acc.x, cnt.x);
+      update_one(r.y > 0 ? 1.f : 0.f, a.z, a.w, sx, sy, acc.y, cnt.y);
+      update_one(r.z > 0 ? 1.f : 0.f, b.x, b.y, sx, sy, acc.z, cnt.z);
+      update_one(r.w > 0 ? 1.f : 0.f, b.z, b.w, sx, sy, acc.w, cnt.w);
     }
+    *reinterpret_cast<float4 *>(grad2d + g0) = acc;
+    *reinterpret_cast<float4 *>(count + g0) = cnt;
+    return;
   }
-  if (any) {
-    grad2d[g] = acc;
-    count[g] = cnt;
+  for (int64_t g = g0; g < min(g0 + 4, N); ++g) {
+    float acc = grad2d[g], cnt = count[g];
+    bool any = false;
+    for (int c = 0; c < C; ++c) {
+      const int64_t i = (int64_t)c * N + g;
+      if (radii[i] > 0) {
+        const float2 v = *reinterpret_cast<const float2 *>(g2d + 2 * i);
+        update_one(1.f, v.x, v.y, sx, sy, acc, cnt);
+        any = true;
+      }
+    }
+    if (any) {
+      grad2d[g] = acc;
+      count[g] = cnt;
+    }
   }
 }
 
@@ -66,7 +97,24 @@ GS_INLINE void step_fetch_wave(const StepFetch &f, int lane) {
   const int64_t q = *f.seq;
   const int64_t slot = q % f.n_ring;
   const uint32_t *src = f.ring + slot * f.slot_words;
-  for (int64_t w = lane; w < f.slot_words - 2; w += 64) f.blk[w] = src[w];
+  // the slot crosses PCIe: every load of a round is issued before any store
+  // (a load / store loop pays one host round trip per 64 words -- the
+  // compiler cannot move a load above a store that may alias it)
+  constexpr int kU = 8;
+  const int64_t nw = f.slot_words - 2;
+  for (int64_t w0 = 0; w0 < nw; w0 += 64 * kU) {
+    uint32_t v[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int64_t w = w0 + lane + 64 * u;
+      v[u] = w < nw ? src[w] : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int64_t w = w0 + lane + 64 * u;
+      if (w < nw) f.blk[w] = v[u];
+    }
+  }
   if (lane == 0) {
     reinterpret_cast<int64_t *>(f.blk)[f.slot_words / 2 - 1] = slot;
     *f.seq = q + 1;
@@ -75,15 +123,33 @@ GS_INLINE void step_fetch_wave(const StepFetch &f, int lane) {
 
 // fetch (the first kernel of a captured step): its first wave also fetches
 // the step's input block
+template <bool VEC>
 __global__ void __launch_bounds__(256)
 activate_fwd_kernel(int64_t n_s, int64_t n_o, const float *__restrict__ log_scales,
                     const float *__restrict__ logits, float *__restrict__ scales,
                     float *__restrict__ opacities, StepFetch fetch) {
   if (fetch.ring && blockIdx.x == 0 && threadIdx.x < 64) step_fetch_wave(fetch, threadIdx.x);
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i < n_s) scales[i] = expf(log_scales[i]);
-  if (i < n_o) opacities[i] = 1.f / (1.f + expf(-logits[i]));
+  // four elements per lane (16-B loads and stores where the arrays are
+  // 16-B aligned; the same expf per element)
+  const int64_t i4 = 4 * ((int64_t)blockIdx.x * 256 + threadIdx.x);
+  if (i4 + 4 <= n_s && VEC) {
+    const float4 v = *reinterpret_cast<const float4 *>(log_scales + i4);
+    *reinterpret_cast<float4 *>(scales + i4) = make_float4(expf(v.x), expf(v.y), expf(v.z), expf(v.w));
+  } else {
+    for (int64_t i = i4; i < min(i4 + 4, n_s); ++i) scales[i] = expf(log_scales[i]);
+  }
+  if (i4 + 4 <= n_o && VEC) {
+    const float4 v = *reinterpret_cast<const float4 *>(logits + i4);
+    *reinterpret_cast<float4 *>(opacities + i4) =
+        make_float4(1.f / (1.f + expf(-v.x)), 1.f / (1.f + expf(-v.y)), 1.f / (1.f + expf(-v.z)),
+                    1.f / (1.f + expf(-v.w)));
+  } else {
+    for (int64_t i = i4; i < min(i4 + 4, n_o); ++i) opacities[i] = 1.f / (1.f + expf(-logits[i]));
+  }
 }
+
+inline bool aligned16(const void *p) { return ((uintptr_t)p & 15) == 0; }
+inline unsigned activate_blocks(int64_t n) { return (unsigned)std::max<int64_t>((n + 1023) / 1024, 1); }
 
 __global__ void __launch_bounds__(256)
 activate_bwd_kernel(int64_t n_s, int64_t n_o, const float *__restrict__ scales,
@@ -367,9 +433,15 @@ extern "C" int gsplat_hip_update_state(int C, int64_t N, const float *means2d_gr
                                        void *stream) {
   GS_REQUIRE(C >= 0 && N >= 0, "update_state: bad sizes C=%d N=%lld", C, (long long)N);
   if (N == 0 || C == 0) return 0;
-  hipLaunchKernelGGL(strat::update_state_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0,
-                     (hipStream_t)stream, C, N, means2d_grad, radii, scale_x, scale_y, grad2d,
-                     count, skip_device);
+  const bool vec = (C == 1 || N % 4 == 0) && strat::aligned16(means2d_grad) &&
+                   strat::aligned16(radii) && strat::aligned16(grad2d) && strat::aligned16(count);
+  const dim3 grid((unsigned)((N + 1023) / 1024));
+  if (vec)
+    hipLaunchKernelGGL(strat::update_state_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream,
+                       C, N, means2d_grad, radii, scale_x, scale_y, grad2d, count, skip_device);
+  else
+    hipLaunchKernelGGL(strat::update_state_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream,
+                       C, N, means2d_grad, radii, scale_x, scale_y, grad2d, count, skip_device);
   GS_CHECK_LAUNCH("update_state");
   return 0;
 }
@@ -379,9 +451,16 @@ extern "C" int gsplat_hip_activate_fwd(int64_t n_scales, int64_t n_opacities,
                                        float *scales, float *opacities, void *stream) {
   const int64_t n = n_scales > n_opacities ? n_scales : n_opacities;
   if (n <= 0) return 0;
-  hipLaunchKernelGGL(strat::activate_fwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
-                     (hipStream_t)stream, n_scales, n_opacities, log_scales, logits, scales,
-                     opacities, strat::StepFetch{});
+  const bool vec = strat::aligned16(log_scales) && strat::aligned16(logits) &&
+                   strat::aligned16(scales) && strat::aligned16(opacities);
+  if (vec)
+    hipLaunchKernelGGL(strat::activate_fwd_kernel<true>, dim3(strat::activate_blocks(n)), dim3(256),
+                       0, (hipStream_t)stream, n_scales, n_opacities, log_scales, logits, scales,
+                       opacities, strat::StepFetch{});
+  else
+    hipLaunchKernelGGL(strat::activate_fwd_kernel<false>, dim3(strat::activate_blocks(n)), dim3(256),
+                       0, (hipStream_t)stream, n_scales, n_opacities, log_scales, logits, scales,
+                       opacities, strat::StepFetch{});
   GS_CHECK_LAUNCH("activate_fwd");
   return 0;
 }
@@ -400,9 +479,16 @@ extern "C" int gsplat_hip_activate_fwd_fetch(int64_t n_scales, int64_t n_opaciti
   const strat::StepFetch f{reinterpret_cast<const uint32_t *>(ring_device), slot_bytes / 4, n_ring,
                            seq_device, reinterpret_cast<uint32_t *>(block_device)};
   const int64_t n = n_scales > n_opacities ? n_scales : n_opacities;
-  hipLaunchKernelGGL(strat::activate_fwd_kernel, dim3((unsigned)std::max<int64_t>((n + 255) / 256, 1)),
-                     dim3(256), 0, (hipStream_t)stream, n_scales, n_opacities, log_scales, logits,
-                     scales, opacities, f);
+  const bool vec = strat::aligned16(log_scales) && strat::aligned16(logits) &&
+                   strat::aligned16(scales) && strat::aligned16(opacities);
+  if (vec)
+    hipLaunchKernelGGL(strat::activate_fwd_kernel<true>, dim3(strat::activate_blocks(n)), dim3(256),
+                       0, (hipStream_t)stream, n_scales, n_opacities, log_scales, logits, scales,
+                       opacities, f);
+  else
+    hipLaunchKernelGGL(strat::activate_fwd_kernel<false>, dim3(strat::activate_blocks(n)), dim3(256),
+                       0, (hipStream_t)stream, n_scales, n_opacities, log_scales, logits, scales,
+                       opacities, f);
   GS_CHECK_LAUNCH("activate_fwd_fetch");
   return 0;
 }

@@ -124,12 +124,13 @@ def test_activate_matches_torch_exactly():
     assert torch.equal(ls.grad, ls_r.grad) and torch.equal(lg.grad, lg_r.grad)
 
 
-@pytest.mark.parametrize("C", [1, 3])
-def test_update_state_matches_torch(C):
+@pytest.mark.parametrize("C,N", [(1, 5003), (3, 5003), (3, 5004)])
+def test_update_state_matches_torch(C, N):
     """DefaultStrategy._update_state (default.py:213-262) with torch ops vs the
-    one-launch HIP version, over two steps (accumulation)."""
+    one-launch HIP version, over two steps (accumulation); N % 4 != 0 with
+    C > 1 takes the scalar kernel, the others the 16-B one with a tail."""
     from gsplat_hip.strategy import update_state_
-    N, W, H = 5003, 640, 480
+    W, H = 640, 480
     g = torch.Generator(device="cuda").manual_seed(C)
     grad2d = torch.zeros(N, device="cuda")
     count = torch.zeros(N, device="cuda")
