@@ -1614,9 +1614,13 @@ pack_records_kernel(int64_t G, const float *__restrict__ means2d, const float *_
                     const int32_t *__restrict__ visible, const int32_t *__restrict__ vis_rank,
                     float *__restrict__ records) {
   const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= G || (visible && visible[g] <= 0)) return;
+  if (g >= G) return;
+  // both loads issued together (the rank does not wait for the visibility)
+  const int32_t vg = visible ? visible[g] : 1;
+  const int32_t rk = vis_rank ? vis_rank[g] : 0;
+  if (vg <= 0) return;
   // rank-indexed table: row = the Gaussian's depth rank among the visible
-  const int64_t row = vis_rank ? min<int64_t>((uint32_t)vis_rank[g], G - 1) : g;
+  const int64_t row = vis_rank ? min<int64_t>((uint32_t)rk, G - 1) : g;
   constexpr int N4 = (6 + D + 3) / 4;
   float r[4 * N4];
   const float2 xy = *reinterpret_cast<const float2 *>(means2d + 2 * g);
