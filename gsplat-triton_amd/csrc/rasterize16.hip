@@ -1309,47 +1309,13 @@ __attribute__((amdgpu_waves_per_eu(BwdOcc<PX>::W))) bwd2_kernel(Args a) {
 // packed [G][S] -> the autograd tensors.  visible (or null: every row):
 // rows of Gaussians without an isect received no atomic and were not zeroed
 // (zero_rows_kernel): their gradients are written as zeros, nothing read.
-// VEC (16-B aligned outputs): the [G, D] colours and [G, 3] conics of the
-// block's 256 Gaussians go through LDS and leave as consecutive float4s (a
-// lane's own D / 3 floats are a 12-B-strided scatter per store otherwise);
-// means2d, opacities (and abs) are written per lane as before.
-template <int D, bool ABS, bool VEC>
+template <int D, bool ABS>
 __global__ void __launch_bounds__(256)
 unpack_kernel(int64_t G, int S, const float *__restrict__ packed, float *__restrict__ v_means2d,
               float *__restrict__ v_conics, float *__restrict__ v_colors,
               float *__restrict__ v_opacities, float *__restrict__ v_abs,
               const int32_t *__restrict__ visible, const int32_t *__restrict__ vis_rank) {
-  const int64_t g0 = (int64_t)blockIdx.x * 256;
-  if (VEC && g0 + 256 <= G) {
-    __shared__ float s_col[256 * D], s_con[256 * 3];
-    const int t = threadIdx.x;
-    const int64_t g = g0 + t;
-    const int32_t vg = visible ? visible[g] : 1;
-    const int32_t rk = vis_rank ? vis_rank[g] : 0;
-    float r[D + 8];
-    if (vg > 0) {
-      const float *row = packed + (vis_rank ? min<int64_t>((uint32_t)rk, G - 1) : g) * S;
-#pragma unroll
-      for (int k = 0; k < D + (ABS ? 8 : 6); ++k) r[k] = row[k];
-    } else {
-#pragma unroll
-      for (int k = 0; k < D + 8; ++k) r[k] = 0.f;
-    }
-#pragma unroll
-    for (int d = 0; d < D; ++d) s_col[t * D + d] = r[d];
-    v_opacities[g] = r[D];
-    *reinterpret_cast<float2 *>(v_means2d + 2 * g) = make_float2(r[D + 1], r[D + 2]);
-#pragma unroll
-    for (int k = 0; k < 3; ++k) s_con[t * 3 + k] = r[D + 3 + k];
-    if (ABS) *reinterpret_cast<float2 *>(v_abs + 2 * g) = make_float2(r[D + 6], r[D + 7]);
-    __syncthreads();
-    float4 *oc = reinterpret_cast<float4 *>(v_colors + g0 * D);
-    for (int q = t; q < 64 * D; q += 256) oc[q] = reinterpret_cast<const float4 *>(s_col)[q];
-    float4 *on = reinterpret_cast<float4 *>(v_conics + g0 * 3);
-    if (t < 192) on[t] = reinterpret_cast<const float4 *>(s_con)[t];
-    return;
-  }
-  const int64_t g = g0 + threadIdx.x;
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= G) return;
   // both loads issued together (the rank does not wait for the visibility)
   const int32_t vg = visible ? visible[g] : 1;
@@ -1614,9 +1580,13 @@ pack_records_kernel(int64_t G, const float *__restrict__ means2d, const float *_
                     const int32_t *__restrict__ visible, const int32_t *__restrict__ vis_rank,
                     float *__restrict__ records) {
   const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= G || (visible && visible[g] <= 0)) return;
+  if (g >= G) return;
+  // both loads issued together (the rank does not wait for the visibility)
+  const int32_t vg = visible ? visible[g] : 1;
+  const int32_t rk = vis_rank ? vis_rank[g] : 0;
+  if (vg <= 0) return;
   // rank-indexed table: row = the Gaussian's depth rank among the visible
-  const int64_t row = vis_rank ? min<int64_t>((uint32_t)vis_rank[g], G - 1) : g;
+  const int64_t row = vis_rank ? min<int64_t>((uint32_t)rk, G - 1) : g;
   constexpr int N4 = (6 + D + 3) / 4;
   float r[4 * N4];
   const float2 xy = *reinterpret_cast<const float2 *>(means2d + 2 * g);
@@ -2015,15 +1985,9 @@ int r16_bwd(r16::Args a, int64_t G, float *v_means2d, float *v_conics, float *v_
     GS_CHECK_LAUNCH("rasterize_bwd16");
   }
   if (G > 0) {
-    const bool vec = (((uintptr_t)v_colors | (uintptr_t)v_conics) & 15) == 0;
-    if (vec)
-      hipLaunchKernelGGL((r16::unpack_kernel<D, ABS, true>), dim3((unsigned)((G + 255) / 256)),
-                         dim3(256), 0, st, G, a.S, a.packed, v_means2d, v_conics, v_colors,
-                         v_opacities, v_abs, visible, vis_rank);
-    else
-      hipLaunchKernelGGL((r16::unpack_kernel<D, ABS, false>), dim3((unsigned)((G + 255) / 256)),
-                         dim3(256), 0, st, G, a.S, a.packed, v_means2d, v_conics, v_colors,
-                         v_opacities, v_abs, visible, vis_rank);
+    hipLaunchKernelGGL((r16::unpack_kernel<D, ABS>), dim3((unsigned)((G + 255) / 256)), dim3(256),
+                       0, st, G, a.S, a.packed, v_means2d, v_conics, v_colors, v_opacities, v_abs,
+                       visible, vis_rank);
     GS_CHECK_LAUNCH("rasterize_bwd16_unpack");
   }
   return 0;

@@ -26,59 +26,28 @@
 namespace gs {
 namespace strat {
 
-GS_INLINE void update_one(float r, float vx, float vy, float sx, float sy, float &acc,
-                          float &cnt) {
-  if (r > 0.f) {
-    const float x = vx * sx, y = vy * sy;
-    acc += sqrtf(x * x + y * y);  // .norm(dim=-1) of a 2-vector
-    cnt += 1.f;
-  }
-}
-
-// Four Gaussians per lane.  VEC (16-B aligned arrays, and C == 1 or N a
-// multiple of 4): 16-B loads, every load of the lane issued before the
-// arithmetic (the gradient rows unconditionally), the four accumulators
-// stored back whole (an untouched one rewrites its own bits).
-template <bool VEC>
 __global__ void __launch_bounds__(256)
 update_state_kernel(int C, int64_t N, const float *__restrict__ g2d,
                     const int32_t *__restrict__ radii, float sx, float sy,
                     float *__restrict__ grad2d, float *__restrict__ count,
                     const int32_t *__restrict__ skip) {
-  const int64_t g0 = 4 * ((int64_t)blockIdx.x * 256 + threadIdx.x);
-  if (g0 >= N || (skip && *skip)) return;
-  if (VEC && g0 + 4 <= N) {
-    float4 acc = *reinterpret_cast<const float4 *>(grad2d + g0);
-    float4 cnt = *reinterpret_cast<const float4 *>(count + g0);
-    for (int c = 0; c < C; ++c) {
-      const int64_t i = (int64_t)c * N + g0;
-      const int4 r = *reinterpret_cast<const int4 *>(radii + i);
-      const float4 a = *reinterpret_cast<const float4 *>(g2d + 2 * i);
-      const float4 b = *reinterpret_cast<const float4 *>(g2d + 2 * i + 4);
-      update_one(r.x > 0 ? 1.f : 0.f, a.x, a.y, sx, sy, acc.x, cnt.x);
-      update_one(r.y > 0 ? 1.f : 0.f, a.z, a.w, sx, sy, acc.y, cnt.y);
-      update_one(r.z > 0 ? 1.f : 0.f, b.x, b.y, sx, sy, acc.z, cnt.z);
-      update_one(r.w > 0 ? 1.f : 0.f, b.z, b.w, sx, sy, acc.w, cnt.w);
+  const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (g >= N || (skip && *skip)) return;
+  float acc = grad2d[g], cnt = count[g];
+  bool any = false;
+  for (int c = 0; c < C; ++c) {
+    const int64_t i = (int64_t)c * N + g;
+    if (radii[i] > 0) {
+      const float2 v = *reinterpret_cast<const float2 *>(g2d + 2 * i);
+      const float x = v.x * sx, y = v.y * sy;
+      acc += sqrtf(x * x + y * y);  // .norm(dim=-1) of a 2-vector
+      cnt += 1.f;
+      any = true;
     }
-    *reinterpret_cast<float4 *>(grad2d + g0) = acc;
-    *reinterpret_cast<float4 *>(count + g0) = cnt;
-    return;
   }
-  for (int64_t g = g0; g < min(g0 + 4, N); ++g) {
-    float acc = grad2d[g], cnt = count[g];
-    bool any = false;
-    for (int c = 0; c < C; ++c) {
-      const int64_t i = (int64_t)c * N + g;
-      if (radii[i] > 0) {
-        const float2 v = *reinterpret_cast<const float2 *>(g2d + 2 * i);
-        update_one(1.f, v.x, v.y, sx, sy, acc, cnt);
-        any = true;
-      }
-    }
-    if (any) {
-      grad2d[g] = acc;
-      count[g] = cnt;
-    }
+  if (any) {
+    grad2d[g] = acc;
+    count[g] = cnt;
   }
 }
 
@@ -433,15 +402,9 @@ extern "C" int gsplat_hip_update_state(int C, int64_t N, const float *means2d_gr
                                        void *stream) {
   GS_REQUIRE(C >= 0 && N >= 0, "update_state: bad sizes C=%d N=%lld", C, (long long)N);
   if (N == 0 || C == 0) return 0;
-  const bool vec = (C == 1 || N % 4 == 0) && strat::aligned16(means2d_grad) &&
-                   strat::aligned16(radii) && strat::aligned16(grad2d) && strat::aligned16(count);
-  const dim3 grid((unsigned)((N + 1023) / 1024));
-  if (vec)
-    hipLaunchKernelGGL(strat::update_state_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream,
-                       C, N, means2d_grad, radii, scale_x, scale_y, grad2d, count, skip_device);
-  else
-    hipLaunchKernelGGL(strat::update_state_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream,
-                       C, N, means2d_grad, radii, scale_x, scale_y, grad2d, count, skip_device);
+  hipLaunchKernelGGL(strat::update_state_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, C, N, means2d_grad, radii, scale_x, scale_y, grad2d,
+                     count, skip_device);
   GS_CHECK_LAUNCH("update_state");
   return 0;
 }

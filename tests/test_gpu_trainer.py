@@ -127,8 +127,7 @@ def test_activate_matches_torch_exactly():
 @pytest.mark.parametrize("C,N", [(1, 5003), (3, 5003), (3, 5004)])
 def test_update_state_matches_torch(C, N):
     """DefaultStrategy._update_state (default.py:213-262) with torch ops vs the
-    one-launch HIP version, over two steps (accumulation); N % 4 != 0 with
-    C > 1 takes the scalar kernel, the others the 16-B one with a tail."""
+    one-launch HIP version, over two steps (accumulation)."""
     from gsplat_hip.strategy import update_state_
     W, H = 640, 480
     g = torch.Generator(device="cuda").manual_seed(C)
