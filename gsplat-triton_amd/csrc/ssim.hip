@@ -339,7 +339,10 @@ fwd_c_kernel(int B, int H, int W, const float *__restrict__ x, const float *__re
 __global__ void __launch_bounds__(1024) reduce_partials_kernel(int n, const float *partials,
                                                                float *sums, float *loss,
                                                                float lam, float n_map,
-                                                               float n_img) {
+                                                               float n_img,
+                                                               float *ring = nullptr,
+                                                               int64_t ring_len = 0,
+                                                               const int64_t *seq = nullptr) {
   __shared__ float red[2][16];
   float a = 0.f, b = 0.f;
   for (int i = threadIdx.x; i < n; i += 1024) {
@@ -368,6 +371,10 @@ __global__ void __launch_bounds__(1024) reduce_partials_kernel(int n, const floa
       loss[0] = l1 * (1.f - lam) + (1.f - s) * lam;
       loss[1] = s;
       loss[2] = l1;
+      if (ring) {
+        int64_t k = (seq[0] - 1) % ring_len;
+        ring[k < 0 ? k + ring_len : k] = loss[0];
+      }
     }
   }
 }
@@ -833,10 +840,10 @@ extern "C" int64_t gsplat_hip_l1_ssim_loss_fused_workspace_bytes(int B, int H, i
   return (int64_t)sizeof(float) * 2 * B * fused_tiles(H, W);
 }
 
-extern "C" int gsplat_hip_l1_ssim_loss_fused_fwd(int B, int H, int W, int C, const float *img1,
-                                                 const float *img2, const int64_t *img2_index,
-                                                 float lam, float *out, float *grad_unit,
-                                                 void *workspace, void *stream) {
+static int fused_fwd(int B, int H, int W, int C, const float *img1, const float *img2,
+                     const int64_t *img2_index, float lam, float *out, float *grad_unit,
+                     void *workspace, float *ring, int64_t ring_len, const int64_t *seq,
+                     void *stream) {
   GS_REQUIRE(B > 0 && H > 10 && W > 10,
              "l1_ssim_loss_fused_fwd: images must be larger than the 11x11 window (got %dx%d)", H,
              W);
@@ -861,9 +868,31 @@ extern "C" int gsplat_hip_l1_ssim_loss_fused_fwd(int B, int H, int W, int C, con
   }
 #undef GS_FUSED
   hipLaunchKernelGGL(ssim::reduce_partials_kernel, dim3(1), dim3(1024), 0, st, (int)(B * nt),
-                     partials, nullptr, out, lam, n_map(B, H, W, C), n_img(B, H, W, C));
+                     partials, nullptr, out, lam, n_map(B, H, W, C), n_img(B, H, W, C), ring,
+                     ring_len, seq);
   GS_CHECK_LAUNCH("l1_ssim_loss_fused_fwd");
   return 0;
+}
+
+extern "C" int gsplat_hip_l1_ssim_loss_fused_fwd(int B, int H, int W, int C, const float *img1,
+                                                 const float *img2, const int64_t *img2_index,
+                                                 float lam, float *out, float *grad_unit,
+                                                 void *workspace, void *stream) {
+  return fused_fwd(B, H, W, C, img1, img2, img2_index, lam, out, grad_unit, workspace, nullptr, 0,
+                   nullptr, stream);
+}
+
+extern "C" int gsplat_hip_l1_ssim_loss_fused_fwd_ring(int B, int H, int W, int C,
+                                                      const float *img1, const float *img2,
+                                                      const int64_t *img2_index, float lam,
+                                                      float *out, float *grad_unit,
+                                                      void *workspace, float *loss_ring,
+                                                      int64_t ring_len, const int64_t *seq_device,
+                                                      void *stream) {
+  GS_REQUIRE(loss_ring && seq_device && ring_len > 0,
+             "l1_ssim_loss_fused_fwd_ring: null ring / step counter or empty ring");
+  return fused_fwd(B, H, W, C, img1, img2, img2_index, lam, out, grad_unit, workspace, loss_ring,
+                   ring_len, seq_device, stream);
 }
 
 extern "C" int gsplat_hip_l1_ssim_loss_fused_bwd(int64_t n, const float *grad_unit,

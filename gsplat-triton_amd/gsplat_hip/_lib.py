@@ -12,7 +12,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GSPLAT_HIP_LIB", os.path.join(_HERE, "libgsplat_hip.so"))
-ABI_VERSION = 29
+ABI_VERSION = 30
 
 _p = ctypes.c_void_p
 _i32 = ctypes.c_int
@@ -85,6 +85,8 @@ _SIGS = {
     "gsplat_hip_l1_ssim_loss_fused_fwd": (_i32, [_i32, _i32, _i32, _i32, _p, _p, _p, _f, _p, _p, _p,
                                                   _p]),
     "gsplat_hip_l1_ssim_loss_fused_bwd": (_i32, [_i64, _p, _p, _p, _p]),
+    "gsplat_hip_l1_ssim_loss_fused_fwd_ring": (_i32, [_i32, _i32, _i32, _i32, _p, _p, _p, _f, _p,
+                                                       _p, _p, _p, _i64, _p, _p]),
     "gsplat_hip_update_state": (_i32, [_i32, _i64, _p, _p, _f, _f, _p, _p, _p, _p]),
     "gsplat_hip_activate_fwd": (_i32, [_i64, _i64, _p, _p, _p, _p, _p]),
     "gsplat_hip_activate_bwd": (_i32, [_i64, _i64, _p, _p, _p, _p, _p, _p, _p]),

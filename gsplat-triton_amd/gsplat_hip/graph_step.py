@@ -132,6 +132,7 @@ class GraphStep:
 
     RING = 8  # host-mapped slots for the per-step input block and counts
     SLOT = 2048  # bytes per input block
+    LOSS_RING = 4096  # device slots of the returned per-step losses
     MAX_WORLD = 8  # cameras of a Gaussian-sharded step in the block
 
     def __init__(self, tr, capacity=None, headroom=1.25, lag=2):
@@ -160,6 +161,13 @@ class GraphStep:
         self.vm, self.K = self.vm_w[r:r + 1], self.K_w[r:r + 1]  # this rank's camera
         self.slot = self.blk[self.SLOT - 8:].view(torch.int64)
         self.seq = torch.zeros(1, dtype=torch.int64, device=dev)  # steps fetched
+        # the step's loss, written by the loss's own reduction launch into
+        # slot (seq - 1) % LOSS_RING: step() returns that slot, no copy launch
+        # after the replay (a 4-B device copy cost ~4 us of GPU time a step);
+        # a returned loss stays valid for LOSS_RING later steps
+        self.loss_ring = torch.zeros(self.LOSS_RING, dtype=torch.float32, device=dev)
+        self.ring_loss = not (getattr(tr, "opacity_reg", 0.0) > 0.0 or
+                              getattr(tr, "scale_reg", 0.0) > 0.0)
         self.status = torch.zeros(1, dtype=torch.int32, device=dev)  # sticky overflow flag
         self.ring_in = _Mapped(self.RING * self.SLOT)
         self.ring_out = _Mapped(self.RING * 4 * 8)
@@ -217,7 +225,9 @@ class GraphStep:
             _isect_report=(self.ring_out.dev, self.slot), _isect_ids=False, **dkw)
         grad_box = {}
         meta["means2d"].register_hook(lambda g: grad_box.__setitem__("g", g))
-        loss = tr._regularise(l1_ssim_loss(colors, tr.targets, tr.ssim_lambda, gt_index=self.cam))
+        loss = tr._regularise(l1_ssim_loss(
+            colors, tr.targets, tr.ssim_lambda, gt_index=self.cam,
+            _out_ring=(self.loss_ring, self.seq) if self.ring_loss else None))
         from . import losses as _losses
         torch.autograd.backward(loss, _losses.ONE_GRAD)
         if stats and "g" in grad_box:  # DefaultStrategy statistics (until refine_stop_iter)
@@ -349,7 +359,10 @@ class GraphStep:
             self.graph = None  # the old capture's pool holds the old tensors
             self._capture(deg, stats)
         self._check(block=len(self.pending) >= self.lag)
+        k = self.issued  # this replay's fetch sees seq == k
         self._issue(it)
+        if self.ring_loss:  # the loss launch wrote it to its own slot
+            return self.loss_ring[k % self.LOSS_RING]
         # a copy: the graph's static output is overwritten by the next replay
         # (eager Trainer.step returns a fresh tensor per step as well)
         return self.loss.clone()

@@ -86,9 +86,11 @@ class _L1SSIMLossFused(torch.autograd.Function):
     gradient.  The training path: no per-pixel SSIM partials through HBM."""
 
     @staticmethod
-    def forward(ctx, img, gt, lam, gt_index=None):
+    def forward(ctx, img, gt, lam, gt_index=None, out_ring=None):
         # gt_index: device int64 [1]; gt is then a stack [n, H, W, C] of
-        # single-image targets and gt[gt_index] is this image's target
+        # single-image targets and gt[gt_index] is this image's target.
+        # out_ring: (ring float32 [R], seq int64 [1], both on the device): the
+        # loss also goes to ring[(seq - 1) % R] (gsplat_hip_l1_ssim_loss_fused_fwd_ring)
         if gt_index is None:
             assert img.dim() == 4 and img.shape == gt.shape, (img.shape, gt.shape)
         else:
@@ -103,8 +105,16 @@ class _L1SSIMLossFused(torch.autograd.Function):
                          dtype=torch.uint8, device=img.device)
         out = torch.empty(3, device=img.device)
         unit = torch.empty_like(img)
-        _lib.call("gsplat_hip_l1_ssim_loss_fused_fwd", B, H, W, C, _ptr(img), _ptr(gt),
-                  _ptr(gt_index), ctypes.c_float(lam), _ptr(out), _ptr(unit), _ptr(ws), _stream())
+        if out_ring is None:
+            _lib.call("gsplat_hip_l1_ssim_loss_fused_fwd", B, H, W, C, _ptr(img), _ptr(gt),
+                      _ptr(gt_index), ctypes.c_float(lam), _ptr(out), _ptr(unit), _ptr(ws),
+                      _stream())
+        else:
+            ring, seq = out_ring
+            assert ring.dtype == torch.float32 and ring.is_cuda and seq.dtype == torch.int64
+            _lib.call("gsplat_hip_l1_ssim_loss_fused_fwd_ring", B, H, W, C, _ptr(img), _ptr(gt),
+                      _ptr(gt_index), ctypes.c_float(lam), _ptr(out), _ptr(unit), _ptr(ws),
+                      _ptr(ring), ring.numel(), _ptr(seq), _stream())
         ctx.save_for_backward(unit)
         return out[0]
 
@@ -112,12 +122,12 @@ class _L1SSIMLossFused(torch.autograd.Function):
     def backward(ctx, g_loss):
         (unit,) = ctx.saved_tensors
         if g_loss is ONE_GRAD:  # the trainer's constant 1.0 seed: the unit gradient as is
-            return unit, None, None, None
+            return unit, None, None, None, None
         g_loss = g_loss.float().contiguous()
         grad = torch.empty_like(unit)
         _lib.call("gsplat_hip_l1_ssim_loss_fused_bwd", unit.numel(), _ptr(unit), _ptr(g_loss),
                   _ptr(grad), _stream())
-        return grad, None, None, None
+        return grad, None, None, None, None
 
 
 # A constant scalar 1.0 the trainer seeds loss.backward() with (never written):
@@ -129,19 +139,21 @@ ONE_GRAD = None
 SSIM_FUSED = os.environ.get("GSPLAT_HIP_SSIM_FUSED", "1") != "0"
 
 
-def l1_ssim_loss(img, gt, ssim_lambda=0.2, fused=None, gt_index=None):
+def l1_ssim_loss(img, gt, ssim_lambda=0.2, fused=None, gt_index=None, _out_ring=None):
     """(1 - ssim_lambda) * mean L1 + ssim_lambda * (1 - mean SSIM_valid).
     With a gradient to compute (and C in {1, 3}) the one-pass fused kernel
     runs, unless `fused=False` (or GSPLAT_HIP_SSIM_FUSED=0).  `gt_index`
     (device int64 [1], fused kernel only): `gt` is a stack of targets and
     gt[gt_index] the one of this [1, H, W, C] image -- chosen on the device,
-    no copy (the captured training step)."""
+    no copy (the captured training step).  `_out_ring` (internal, with
+    gt_index): (ring, seq) device tensors; the loss value is also written to
+    ring[(seq - 1) % len(ring)] by the reduction launch (graph_step.py)."""
     if fused is None:
         fused = SSIM_FUSED and torch.is_grad_enabled() and img.requires_grad
     if gt_index is not None:
         if not (fused and img.dim() == 4 and img.shape[-1] in (1, 3)):
             raise ValueError("l1_ssim_loss: gt_index needs the fused kernel (grad, C in {1, 3})")
-        return _L1SSIMLossFused.apply(img, gt, float(ssim_lambda), gt_index)
+        return _L1SSIMLossFused.apply(img, gt, float(ssim_lambda), gt_index, _out_ring)
     if fused and img.dim() == 4 and img.shape[-1] in (1, 3):
         return _L1SSIMLossFused.apply(img, gt, float(ssim_lambda))
     return _L1SSIMLoss.apply(img, gt, float(ssim_lambda))

@@ -29,7 +29,9 @@ extern "C" {
 const char *gsplat_hip_last_error(void);
 /* 29: the lazy SH-Adam entries of 28 (gsplat_hip_sh_colors_fwd_lazy,
  * gsplat_hip_sh_lazy_flush and the lazy arguments of the fused SH backward)
- * removed -- measured slower. */
+ * removed -- measured slower.
+ * 30: gsplat_hip_l1_ssim_loss_fused_fwd_ring (the loss also into a device
+ * ring slot chosen by a device step counter). */
 int gsplat_hip_abi_version(void);
 
 /* ---------------------------------------------------------------------------
@@ -378,6 +380,16 @@ int gsplat_hip_l1_ssim_loss_fused_fwd(int B, int H, int W, int C, const float *i
                                       void *stream);
 int gsplat_hip_l1_ssim_loss_fused_bwd(int64_t n, const float *grad_unit, const float *g_loss,
                                       float *grad_img1, void *stream);
+/* fused_fwd_ring (ABI 30): fused_fwd, and the loss out[0] also written to
+ * loss_ring[(seq_device[0] - 1) % ring_len] by the same reduction launch --
+ * a captured training step returns that slot instead of copying its static
+ * output after every replay (seq_device: the step counter the step's fetch
+ * launch has already incremented; gsplat_hip/graph_step.py). */
+int gsplat_hip_l1_ssim_loss_fused_fwd_ring(int B, int H, int W, int C, const float *img1,
+                                           const float *img2, const int64_t *img2_index,
+                                           float lam, float *out, float *grad_unit,
+                                           void *workspace, float *loss_ring, int64_t ring_len,
+                                           const int64_t *seq_device, void *stream);
 
 /* The captured training step's per-step input without copy engines (ABI 22;
  * gsplat_hip/graph_step.py, not a reference function):

@@ -196,12 +196,11 @@ def test_graph_trainer_tracks_eager(capacity):
         tr = Trainer(means, rgbs, vm, K, W, H, device=DEV, graph=graph, isect_capacity=capacity,
                      max_steps=100)
         assert (tr._graph is not None) == graph
-        for it in range(6):
-            tr.step(it)
+        losses = [tr.step(it) for it in range(6)]
         tr.sync()
         out[graph] = ({k: p.detach().clone() for k, p in tr.params.items()},
                       [m.clone() for m in tr.opt.exp_avg], tr.opt.step_count,
-                      tr.grad2d.clone(), tr.count.clone())
+                      tr.grad2d.clone(), tr.count.clone(), [float(x) for x in losses])
         if graph:
             g = tr._graph
             assert g.replays >= 6
@@ -215,6 +214,9 @@ def test_graph_trainer_tracks_eager(capacity):
         torch.testing.assert_close(y, x, rtol=1e-2, atol=1e-6)
     torch.testing.assert_close(b[4], a[4], rtol=0, atol=0)  # visibility counts: exact
     torch.testing.assert_close(b[3], a[3], rtol=1e-3, atol=1e-7)
+    if capacity is None:  # the returned per-step losses (the graph's loss ring slots)
+        torch.testing.assert_close(torch.tensor(b[5]), torch.tensor(a[5]), rtol=1e-4, atol=1e-6)
+        assert len(set(b[5])) == 6, b[5]
 
 
 def test_graph_trainer_refine_tracks_eager():
