@@ -137,8 +137,6 @@ GS_INLINE void fused_dir(const Fused &fz, int64_t i, float &x, float &y, float &
   z = m[2] - pz;
 }
 
-typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));  // 4-B aligned float4
-
 template <int DEG, bool FUSED>
 __global__ void __launch_bounds__(256)
 sh_fwd_kernel(int64_t n, int64_t n_coeff_rows, Coeffs cf, const float *__restrict__ dirs,
@@ -169,26 +167,12 @@ sh_fwd_kernel(int64_t n, int64_t n_coeff_rows, Coeffs cf, const float *__restric
   const int64_t row = i % n_coeff_rows;
   const float *p0 = cf.c0 + row * cf.s0;
   const float *pr = cf.cr + row * cf.sr;
-  // the lane's 3 (NB - 1) rest coefficients as 16-B loads (rows are only
-  // 4-B aligned: 45 floats at degree 3; unaligned vector loads are legal on
-  // global memory), a quarter of the load instructions of one per float --
-  // lanes gather rows of scattered visible Gaussians, so the load count is
-  // the cost
-  constexpr int NR = 3 * (NB - 1), NV = NR / 4;
-  float c[NR > 0 ? NR : 1];
-#pragma unroll
-  for (int v = 0; v < NV; ++v) {
-    const f4u q = *reinterpret_cast<const f4u *>(pr + 4 * v);
-    c[4 * v] = q.x; c[4 * v + 1] = q.y; c[4 * v + 2] = q.z; c[4 * v + 3] = q.w;
-  }
-#pragma unroll
-  for (int k = 4 * NV; k < NR; ++k) c[k] = pr[k];
   float r = B[0] * p0[0], g = B[0] * p0[1], b = B[0] * p0[2];
 #pragma unroll
   for (int k = 1; k < NB; ++k) {
-    r += B[k] * c[3 * (k - 1)];
-    g += B[k] * c[3 * (k - 1) + 1];
-    b += B[k] * c[3 * (k - 1) + 2];
+    r += B[k] * pr[3 * (k - 1)];
+    g += B[k] * pr[3 * (k - 1) + 1];
+    b += B[k] * pr[3 * (k - 1) + 2];
   }
   if (FUSED) {
     r = fmaxf(r + 0.5f, 0.f);
