@@ -298,7 +298,32 @@ struct AdamSH {
   // read on the device, and a void step (*skip != 0) leaves the state alone
   const float *hyper;
   const int32_t *skip;
+  int nt;  // non-temporal row loads / stores (GSPLAT_HIP_SH_ADAM_NT, A/B)
 };
+
+// The rows are touched once per step: non-temporal accesses keep them from
+// displacing what the caches hold for the rest of the step (A/B switch).
+static int sh_adam_nt() {
+  static const int v = [] {
+    const char *e = getenv("GSPLAT_HIP_SH_ADAM_NT");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+typedef float f4v __attribute__((ext_vector_type(4)));
+GS_INLINE float4 ld4(const float4 *p, bool nt) {
+  if (nt) {
+    const f4v v = __builtin_nontemporal_load(reinterpret_cast<const f4v *>(p));
+    return make_float4(v.x, v.y, v.z, v.w);
+  }
+  return *p;
+}
+GS_INLINE void st4(float4 *p, const float4 &v, bool nt) {
+  if (nt)
+    __builtin_nontemporal_store(f4v{v.x, v.y, v.z, v.w}, reinterpret_cast<f4v *>(p));
+  else
+    *p = v;
+}
 
 // Adam over `rows` consecutive rows of WID floats (16-B aligned start): the
 // gradient of element (r, c) is g[r * GS + c] (LDS); 4 elements per lane and
@@ -325,9 +350,9 @@ GS_INLINE void adam_rows(float *P, float *M, float *V, const float *g, int rows,
     for (int u = 0; u < kU; ++u) {
       const int q = q0 + 64 * u;
       if (q < n4) {
-        p[u] = P4[q];
-        m[u] = M4[q];
-        v[u] = V4[q];
+        p[u] = ld4(P4 + q, ad.nt);
+        m[u] = ld4(M4 + q, ad.nt);
+        v[u] = ld4(V4 + q, ad.nt);
       }
     }
 #pragma unroll
@@ -339,9 +364,9 @@ GS_INLINE void adam_rows(float *P, float *M, float *V, const float *g, int rows,
         adam_update(p[u].y, gr(e + 1), m[u].y, v[u].y, ad.b1, ad.b2, ad.eps, ss, ad.ib);
         adam_update(p[u].z, gr(e + 2), m[u].z, v[u].z, ad.b1, ad.b2, ad.eps, ss, ad.ib);
         adam_update(p[u].w, gr(e + 3), m[u].w, v[u].w, ad.b1, ad.b2, ad.eps, ss, ad.ib);
-        P4[q] = p[u];
-        M4[q] = m[u];
-        V4[q] = v[u];
+        st4(P4 + q, p[u], ad.nt);
+        st4(M4 + q, m[u], ad.nt);
+        st4(V4 + q, v[u], ad.nt);
       }
     }
   }
@@ -655,7 +680,7 @@ extern "C" int gsplat_hip_sh_colors_bwd_adam(int degree, int C, int64_t N, const
              "sh_colors_bwd_adam: coefficient and moment buffers must be 16-B aligned");
   const double bc1 = 1.0 - pow((double)beta1, step), bc2 = 1.0 - pow((double)beta2, step);
   AdamSH ad{m0, v0, m_rest, v_rest, (float)(lr0 / bc1), (float)(lr_rest / bc1),
-            (float)(1.0 / sqrt(bc2)), beta1, beta2, eps, nullptr, nullptr};
+            (float)(1.0 / sqrt(bc2)), beta1, beta2, eps, nullptr, nullptr, sh_adam_nt()};
   return sh_colors_bwd_adam_launch(degree, C, N, means, viewmats, coeffs, coeffs_rest, radii,
                                    v_colors, v_dirs, ad, (hipStream_t)stream);
 }
@@ -680,7 +705,8 @@ extern "C" int gsplat_hip_sh_colors_bwd_adam_dev(int degree, int C, int64_t N,
   GS_REQUIRE((((uintptr_t)coeffs | (uintptr_t)coeffs_rest | (uintptr_t)m0 | (uintptr_t)v0 |
                (uintptr_t)m_rest | (uintptr_t)v_rest) & 15) == 0,
              "sh_colors_bwd_adam: coefficient and moment buffers must be 16-B aligned");
-  AdamSH ad{m0, v0, m_rest, v_rest, 0.f, 0.f, 0.f, beta1, beta2, eps, hyper_device, skip_device};
+  AdamSH ad{m0, v0, m_rest, v_rest, 0.f, 0.f, 0.f, beta1, beta2, eps, hyper_device, skip_device,
+            sh_adam_nt()};
   return sh_colors_bwd_adam_launch(degree, C, N, means, viewmats, coeffs, coeffs_rest, radii,
                                    v_colors, v_dirs, ad, (hipStream_t)stream);
 }
