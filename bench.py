@@ -450,6 +450,8 @@ def main():
                         "backward": 40 * tr.params["means"].shape[0] * (len(tr._n_world) - 1)}
                        if gshard else None),
                    "n_isects_mean": float(np.mean(isects)), "n_eff_mean": float(np.mean(n_effs)),
+                   "fwd_split_div": getattr(tr, "split_div", None),
+                   "termination_ratio_first_render": getattr(tr, "term_ratio", None),
                    "visible_per_camera": per_cam_visible,
                    "visible_union_8_cameras": union_visible,
                    "packed": False, "loss": "0.8*L1+0.2*(1-SSIM valid)",

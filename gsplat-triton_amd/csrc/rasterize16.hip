@@ -1683,15 +1683,21 @@ static int fwd_split_mode() {
   return g_fwd_split;
 }
 
+static int split_div_default() {
+  static const int div = [] {
+    const char *e = getenv("GSPLAT_HIP_FWD_SPLIT_DIV");
+    const int x = e ? atoi(e) : 550;
+    return x > 0 ? x : 550;
+  }();
+  return div;
+}
+static int g_split_div = 0;  // gsplat_hip_set_fwd_split_div; 0: the default
+static int split_div() { return g_split_div > 0 ? g_split_div : split_div_default(); }
+
 static int64_t split_threshold(int64_t n_isects) {
   const int m = fwd_split_mode();
   if (m > 0) return m;
-  static const int64_t div = [] {
-    const char *e = getenv("GSPLAT_HIP_FWD_SPLIT_DIV");
-    const int x = e ? atoi(e) : 550;
-    return (int64_t)(x > 0 ? x : 550);
-  }();
-  return std::max<int64_t>(2048, n_isects / div);
+  return std::max<int64_t>(2048, n_isects / split_div());
 }
 
 static int chunk_len();
@@ -2116,6 +2122,12 @@ int rasterize16_bwd(int C, int64_t G, int D, int W, int H, int tw, int th,
 }
 
 }  // namespace gs
+
+extern "C" int gsplat_hip_set_fwd_split_div(int div) {
+  const int old = gs::split_div();
+  gs::g_split_div = div > 0 ? div : 0;
+  return old;
+}
 
 extern "C" int gsplat_hip_debug_set_fwd_split(int isects) {
   const int old = gs::fwd_split_mode();

@@ -76,6 +76,7 @@ _SIGS = {
     "gsplat_hip_debug_set_chunk": (_i32, [_i32]),
     "gsplat_hip_debug_set_flags": (_i32, [_i32]),
     "gsplat_hip_debug_set_fwd_split": (_i32, [_i32]),
+    "gsplat_hip_set_fwd_split_div": (_i32, [_i32]),
     "gsplat_hip_ssim_workspace_bytes": (_i64, [_i32, _i32, _i32, _i32]),
     "gsplat_hip_ssim_l1_fwd": (_i32, [_i32, _i32, _i32, _i32, _p, _p, _p, _p, _p]),
     "gsplat_hip_ssim_l1_bwd": (_i32, [_i32, _i32, _i32, _i32, _p, _p, _p, _p, _p, _p]),

@@ -938,6 +938,29 @@ def rasterize_to_pixels(
 
 
 @torch.no_grad()
+def forward_termination_ratio(colors: Tensor, meta: dict, width: int, height: int) -> float:
+    """n_eff / n_isects of a 3DGS render (colors from rasterization() with a
+    gradient to compute): n_eff = sum over tiles of min(range end, the tile's
+    largest last id + 1) - range start, from the forward's own last ids (the
+    autograd node's saved tensors).  1.0 when the node is not found."""
+    offs = meta["isect_offsets"].flatten().long()
+    n = int(meta["isect_counts"][0]) if "isect_counts" in meta else meta["flatten_ids"].numel()
+    if n <= 0:
+        return 1.0
+    node = colors.grad_fn
+    while node is not None and type(node).__name__ != "_RasterizeToPixelsBackward":
+        node = node.next_functions[0][0] if node.next_functions else None
+    if node is None:
+        return 1.0
+    last = node.saved_tensors[9]  # (..., render_alphas, last_ids, ...): see _RasterizeToPixels
+    ts, tw, th = meta["tile_size"], meta["tile_width"], meta["tile_height"]
+    lp = torch.nn.functional.pad(last[0], (0, tw * ts - width, 0, th * ts - height))
+    tmax = lp.view(th, ts, tw, ts).amax(dim=(1, 3)).flatten().long()
+    ends = torch.cat([offs[1:], torch.tensor([n], device=offs.device)])
+    n_eff = int(torch.clamp(torch.minimum(ends, tmax + 1) - offs, min=0).sum())
+    return n_eff / n
+
+
 def pack_render_records(means2d, conics, colors, opacities, tile_size, visible=None,
                         ranks=None) -> Tensor:
     """The 16x16 rasterizer's render records (gsplat_hip_rasterize_pack_records):

@@ -57,7 +57,7 @@ import torch.nn.functional as F
 from . import densify
 from .densify import DefaultStrategyConfig
 from .losses import FusedAdam, l1_ssim_loss, ssim_and_l1
-from . import _wrapper
+from . import _lib, _wrapper
 from .rendering import rasterization, rasterization_2dgs
 from .strategy import activate, update_state_
 
@@ -449,7 +449,28 @@ class Trainer:
             rasterize_mode="classic", absgrad=absgrad, _colors_ready=hook, _fusion=fusion,
             **dkw)
 
+    def _tune_split(self, it: int):
+        """Once, before the first step (and so before a graph capture freezes
+        the forward's variant): the split-forward threshold's divisor from the
+        scene's termination.  Pixels that rarely stop early (n_eff / n_isects
+        > 0.75, M3: 0.89) make the heaviest tiles the forward's tail: split
+        more of them (divisor 1100); scenes that terminate early (M2: 0.56)
+        keep 550, whose split-capable variant would only cost occupancy
+        (DESIGN 3.4).  One-GPU 3DGS on the HIP path; GSPLAT_HIP_FWD_SPLIT_DIV
+        set by the user wins."""
+        self._split_tuned = True
+        if (self.model != "3dgs" or not self.fused or self.world_size != 1
+                or os.environ.get("GSPLAT_HIP_FWD_SPLIT_DIV")):
+            return
+        colors, _, meta = self.render(self.camera_index(it), self.sh_degree_at(it))
+        self.term_ratio = _wrapper.forward_termination_ratio(colors, meta, self.width, self.height)
+        self.split_div = 1100 if self.term_ratio > 0.75 else 550
+        _lib.query("gsplat_hip_set_fwd_split_div", self.split_div)
+        del colors, meta
+
     def step(self, it: int):
+        if not getattr(self, "_split_tuned", False):
+            self._tune_split(it)
         if getattr(self, "_graph", None) is not None:
             loss = self._graph.step(it)
             if self.strategy is not None:

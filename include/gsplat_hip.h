@@ -31,7 +31,7 @@ const char *gsplat_hip_last_error(void);
  * gsplat_hip_sh_lazy_flush and the lazy arguments of the fused SH backward)
  * removed -- measured slower.
  * 30: gsplat_hip_l1_ssim_loss_fused_fwd_ring (the loss also into a device
- * ring slot chosen by a device step counter). */
+ * ring slot chosen by a device step counter), gsplat_hip_set_fwd_split_div. */
 int gsplat_hip_abi_version(void);
 
 /* ---------------------------------------------------------------------------
@@ -329,6 +329,11 @@ int gsplat_hip_debug_set_chunk(int isects);
  * the previous mode.  Results do not depend on it beyond the float rounding
  * of the chunks' transmittance products. */
 int gsplat_hip_debug_set_fwd_split(int isects);
+/* The adaptive threshold's divisor (ABI 30): div > 0 sets it, div <= 0
+ * restores the default (GSPLAT_HIP_FWD_SPLIT_DIV, else 550).  Returns the
+ * divisor in effect before the call.  The trainer picks 1100 for scenes
+ * whose pixels rarely terminate early (train_step.Trainer._tune_split). */
+int gsplat_hip_set_fwd_split_div(int div);
 /* Debug flags of the 16x16 rasterizer (ABI 25; default 0, or GSPLAT_HIP_DBG):
  * bit 0 = the backward skips its gradient atomics (timing experiments);
  * bit 1 = a chunk of a split tile never waits for an earlier chunk's

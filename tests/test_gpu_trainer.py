@@ -4,6 +4,7 @@ and the one-launch Adam (vs torch.optim.Adam)."""
 
 import math
 
+import numpy as np
 import pytest
 import torch
 
@@ -158,6 +159,43 @@ def _small_scene(n_cams=4, W=320, H=240):
     means, rgbs = means[::8].contiguous(), rgbs[::8].contiguous()
     vm, K = camera_pool(vms, Ks, sw, sh_, W, H, n=n_cams)
     return means, rgbs, vm, K, W, H
+
+
+def test_trainer_tunes_split_divisor_from_termination():
+    """Trainer._tune_split: before the first step, the forward's n_eff /
+    n_isects (forward_termination_ratio, the bench's formula) picks the split
+    threshold's divisor: 1100 above 0.75, else 550; the library reports it
+    back.  The ratio is checked against a direct per-tile evaluation."""
+    from gsplat_hip import _lib, _wrapper
+    from gsplat_hip.train_step import Trainer
+    means, rgbs, vm, K, W, H = _small_scene()
+    try:
+        tr = Trainer(means, rgbs, vm, K, W, H, device="cuda", max_steps=100)
+        tr.step(0)
+        r = tr.term_ratio
+        assert 0.0 < r <= 1.0
+        assert tr.split_div == (1100 if r > 0.75 else 550)
+        assert _lib.query("gsplat_hip_set_fwd_split_div", 0) == tr.split_div
+        # direct: per tile, isects up to the tile's largest last id + 1
+        colors, _, meta = tr.render(tr.camera_index(0), tr.sh_degree_at(0))
+        r2 = _wrapper.forward_termination_ratio(colors, meta, W, H)
+        node = colors.grad_fn
+        while type(node).__name__ != "_RasterizeToPixelsBackward":
+            node = node.next_functions[0][0]
+        last = node.saved_tensors[9][0].cpu().numpy()
+        offs = meta["isect_offsets"].flatten().cpu().numpy().astype(np.int64)
+        n = meta["flatten_ids"].numel()
+        ts, tw, th = meta["tile_size"], meta["tile_width"], meta["tile_height"]
+        n_eff = 0
+        for t in range(tw * th):
+            y, x = divmod(t, tw)
+            end = offs[t + 1] if t + 1 < len(offs) else n
+            blk = last[y * ts:(y + 1) * ts, x * ts:(x + 1) * ts]
+            if end > offs[t]:
+                n_eff += max(0, min(end, int(blk.max()) + 1) - offs[t])
+        assert abs(r2 - n_eff / n) < 1e-9, (r2, n_eff / n)
+    finally:
+        _lib.query("gsplat_hip_set_fwd_split_div", 0)
 
 
 @pytest.mark.parametrize("sharded", [False, True])
