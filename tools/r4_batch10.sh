@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round-4 batch 10: SH Adam rows non-temporal (GSPLAT_HIP_SH_ADAM_NT) A/B at
-# M2, alternating, with a kernel trace of each; SH tests under NT=1.
+# M2, alternating, with a kernel trace of each; SH tests under NT=1; then
+# batch 11 (the trainer-chosen split divisor) in the same call.
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 O=gpurun_out/${1:-r4_batch10}; mkdir -p $O
@@ -25,3 +26,4 @@ for nt in (0, 1):
             if any(k in r["Name"] for k in ("sh_bwd", "adam::step", "bwd2_kernel", "fwd_kernel<3, 0, false>", "fused_kernel")):
                 print(f"nt={nt}", r["Name"][:50], r["Calls"], round(float(r["AverageNs"]) / 1000, 1), "us")
 PY
+tools/r4_batch11.sh ${1:-r4_batch10}/b11 || exit 7
