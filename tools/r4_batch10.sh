@@ -1,29 +1,27 @@
 #!/bin/bash
-# Round-4 batch 10: SH Adam rows non-temporal (GSPLAT_HIP_SH_ADAM_NT) A/B at
-# M2, alternating, with a kernel trace of each; SH tests under NT=1; then
-# batch 11 (the trainer-chosen split divisor) in the same call.
+# Round-4 batch 10: the whole GPU suite (incl. the split-divisor test), the
+# SH Adam rows non-temporal A/B at M2 (GSPLAT_HIP_SH_ADAM_NT, alternating),
+# M3 eager with the trainer-chosen divisor against a forced 550, a kernel
+# trace of the default M2 workload.
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 O=gpurun_out/${1:-r4_batch10}; mkdir -p $O
-v() { python3 -c "import json;d=json.loads(open('$1').read().strip().splitlines()[-1]);r=d['roofline'];print(round(d['value'],1), round(d['ms_per_step'],3), 'fwd', round(r['launch_ms'],4), 'bwd', round(r['bwd']['launch_ms'],4))"; }
-GSPLAT_HIP_SH_ADAM_NT=1 timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_graph.py tests/test_gpu_trainer.py -q -k "sh or graph or adam" --timeout 180 --timeout-method thread > $O/tests_nt.log 2>&1
-rc=$?; echo "tests (NT=1) rc=$rc"; grep FAILED $O/tests_nt.log; tail -1 $O/tests_nt.log
-[ $rc -eq 0 ] || exit $rc
+v() { python3 -c "import json;d=json.loads(open('$1').read().strip().splitlines()[-1]);r=d['roofline'];c=d['config'];print(round(d['value'],1), round(d['ms_per_step'],3), 'fwd', round(r['launch_ms'],4), 'bwd', round(r['bwd']['launch_ms'],4), 'div', c.get('fwd_split_div'), 'ratio', c.get('termination_ratio_first_render'))"; }
+dead() { [ $1 -eq 124 ] || [ $1 -eq 137 ] || [ $1 -eq 134 ] || [ $1 -eq 139 ]; }
+timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 180 --timeout-method thread > $O/tests.log 2>&1
+rc=$?; echo "tests rc=$rc"; grep FAILED $O/tests.log; tail -1 $O/tests.log
+dead $rc && exit $rc
 for r in 1 2; do
   for nt in 0 1; do
     GSPLAT_HIP_SH_ADAM_NT=$nt timeout -k 10 300 python -u bench.py --no-traffic --no-cpu-baseline > $O/m2_nt$nt.$r.json 2> $O/m2_nt$nt.$r.err || exit 2
     echo "m2 nt=$nt run $r $(v $O/m2_nt$nt.$r.json)"
   done
 done
-for nt in 0 1; do
-  GSPLAT_HIP_SH_ADAM_NT=$nt timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $O/trace_nt$nt -o run -- /usr/bin/python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-traffic > $O/trace_nt$nt.log 2>&1 || exit 6
+for r in 1 2; do
+  timeout -k 10 400 python -u bench.py --config m3 --eager --no-traffic --no-cpu-baseline > $O/m3_auto.$r.json 2> $O/m3_auto.$r.err || exit 3
+  echo "m3 eager auto run $r $(v $O/m3_auto.$r.json)"
+  GSPLAT_HIP_FWD_SPLIT_DIV=550 timeout -k 10 400 python -u bench.py --config m3 --eager --no-traffic --no-cpu-baseline > $O/m3_550.$r.json 2> $O/m3_550.$r.err || exit 4
+  echo "m3 eager div550 run $r $(v $O/m3_550.$r.json)"
 done
-python3 - $O <<'PY'
-import csv, glob, sys
-for nt in (0, 1):
-    for f in glob.glob(sys.argv[1] + f"/trace_nt{nt}/**/*kernel_stats.csv", recursive=True):
-        for r in csv.DictReader(open(f)):
-            if any(k in r["Name"] for k in ("sh_bwd", "adam::step", "bwd2_kernel", "fwd_kernel<3, 0, false>", "fused_kernel")):
-                print(f"nt={nt}", r["Name"][:50], r["Calls"], round(float(r["AverageNs"]) / 1000, 1), "us")
-PY
-tools/r4_batch11.sh ${1:-r4_batch10}/b11 || exit 7
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $O/trace -o run -- /usr/bin/python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-traffic > $O/trace.log 2>&1 || exit 6
+echo "trace ok"
