@@ -298,15 +298,17 @@ struct AdamSH {
   // read on the device, and a void step (*skip != 0) leaves the state alone
   const float *hyper;
   const int32_t *skip;
-  int nt;  // non-temporal row loads / stores (GSPLAT_HIP_SH_ADAM_NT, A/B)
+  int nt;  // non-temporal row loads / stores (GSPLAT_HIP_SH_ADAM_NT, default on)
 };
 
-// The rows are touched once per step: non-temporal accesses keep them from
-// displacing what the caches hold for the rest of the step (A/B switch).
+// The rows are touched once per step: non-temporal loads / stores stream
+// them past the caches (M2 804.8 / 805.4 against 795.3 / 797.2 images/s,
+// alternating in one call, profiles/r4_batch10/).  GSPLAT_HIP_SH_ADAM_NT=0
+// turns them off.
 static int sh_adam_nt() {
   static const int v = [] {
     const char *e = getenv("GSPLAT_HIP_SH_ADAM_NT");
-    return e ? atoi(e) : 0;
+    return e ? atoi(e) : 1;
   }();
   return v;
 }
