@@ -185,20 +185,12 @@ static int adam_launch(int n_groups, float *const *params, const float *const *g
                        (hipStream_t)stream, g, beta1, beta2, eps);
   } else {
     // one 16-B slot per lane per iteration; deeper unrolling and non-temporal
-    // accesses measured no faster alone (tools/adam_bench.py: ~5.8 TB/s);
-    // GSPLAT_HIP_ADAM_NT=1: non-temporal inside the training step (A/B: the
-    // SH Adam's rows gained from it there)
-    static const bool nt = [] {
-      const char *e = getenv("GSPLAT_HIP_ADAM_NT");
-      return e && atoi(e) == 1;
-    }();
+    // accesses measured no faster (tools/adam_bench.py: ~5.8 TB/s; inside the
+    // M2 step non-temporal ran 776.4 / 785.0 / 804.3 against 803.8 x 3
+    // images/s, profiles/r4_batch12/ -- unlike the SH Adam's rows)
     const int blocks = (int)std::min<int64_t>((total + 255) / 256, 256 * 64);
-    if (nt)
-      hipLaunchKernelGGL((adam::step_kernel<1, true>), dim3(blocks), dim3(256), 0,
-                         (hipStream_t)stream, g, beta1, beta2, eps);
-    else
-      hipLaunchKernelGGL((adam::step_kernel<1, false>), dim3(blocks), dim3(256), 0,
-                         (hipStream_t)stream, g, beta1, beta2, eps);
+    hipLaunchKernelGGL((adam::step_kernel<1, false>), dim3(blocks), dim3(256), 0,
+                       (hipStream_t)stream, g, beta1, beta2, eps);
   }
   GS_CHECK_LAUNCH("adam_step");
   return 0;
