@@ -124,8 +124,9 @@ struct Fused {
   int64_t N;
 };
 
-GS_INLINE void fused_dir(const Fused &fz, int64_t i, float &x, float &y, float &z) {
-  const int64_t c = i / fz.N, g = i - c * fz.N;
+GS_INLINE void fused_dir(const Fused &fz, int64_t i, float &x, float &y, float &z, bool one_cam) {
+  // one camera (n == N, the training step): no 64-bit division per lane
+  const int64_t c = one_cam ? 0 : i / fz.N, g = i - c * fz.N;
   const float *vm = fz.viewmats + 16 * c;
   const float t0 = vm[3], t1 = vm[7], t2 = vm[11];
   const float px = -(vm[0] * t0 + vm[4] * t1 + vm[8] * t2);
@@ -154,7 +155,7 @@ sh_fwd_kernel(int64_t n, int64_t n_coeff_rows, Coeffs cf, const float *__restric
   float x = 0.f, y = 0.f, z = 0.f;
   if (DEG > 0) {
     if (FUSED) {
-      fused_dir(fz, i, x, y, z);
+      fused_dir(fz, i, x, y, z, n == fz.N);
     } else {
       const float *d = dirs + 3 * i;
       x = d[0]; y = d[1]; z = d[2];
@@ -164,7 +165,7 @@ sh_fwd_kernel(int64_t n, int64_t n_coeff_rows, Coeffs cf, const float *__restric
   }
   float B[NB];
   sh_basis<DEG, false>(x, y, z, B, nullptr);
-  const int64_t row = i % n_coeff_rows;
+  const int64_t row = n_coeff_rows == n ? i : i % n_coeff_rows;
   const float *p0 = cf.c0 + row * cf.s0;
   const float *pr = cf.cr + row * cf.sr;
   float r = B[0] * p0[0], g = B[0] * p0[1], b = B[0] * p0[2];
@@ -203,7 +204,7 @@ sh_bwd_kernel(int64_t n, int K, int64_t n_coeff_rows, Coeffs cf, const float *__
   float x = 0.f, y = 0.f, z = 0.f, inorm = 0.f;
   if (DEG > 0) {
     if (FUSED) {
-      fused_dir(fz, i, x, y, z);
+      fused_dir(fz, i, x, y, z, false);
     } else {
       const float *d = dirs + 3 * i;
       x = d[0]; y = d[1]; z = d[2];
@@ -437,7 +438,7 @@ sh_bwd_staged_kernel(int64_t n, Coeffs cf, const float *__restrict__ dirs,
       float x = 0.f, y = 0.f, z = 0.f, inorm = 0.f;
       if (DEG > 0) {
         if (FUSED) {
-          fused_dir(fz, ri, x, y, z);
+          fused_dir(fz, ri, x, y, z, false);
         } else {
           x = dirs[3 * i]; y = dirs[3 * i + 1]; z = dirs[3 * i + 2];
         }
