@@ -124,9 +124,7 @@ struct Fused {
   int64_t N;
 };
 
-GS_INLINE void fused_dir(const Fused &fz, int64_t i, float &x, float &y, float &z, bool one_cam) {
-  // one camera (n == N, the training step): no 64-bit division per lane
-  const int64_t c = one_cam ? 0 : i / fz.N, g = i - c * fz.N;
+GS_INLINE void fused_dir_cg(const Fused &fz, int64_t c, int64_t g, float &x, float &y, float &z) {
   const float *vm = fz.viewmats + 16 * c;
   const float t0 = vm[3], t1 = vm[7], t2 = vm[11];
   const float px = -(vm[0] * t0 + vm[4] * t1 + vm[8] * t2);
@@ -136,6 +134,13 @@ GS_INLINE void fused_dir(const Fused &fz, int64_t i, float &x, float &y, float &
   x = m[0] - px;
   y = m[1] - py;
   z = m[2] - pz;
+}
+
+// row i of [C, N]; one camera (n == N, the training step): no 64-bit
+// division per lane
+GS_INLINE void fused_dir(const Fused &fz, int64_t i, float &x, float &y, float &z, bool one_cam) {
+  const int64_t c = one_cam ? 0 : i / fz.N;
+  fused_dir_cg(fz, c, i - c * fz.N, x, y, z);
 }
 
 template <int DEG, bool FUSED>
@@ -204,7 +209,7 @@ sh_bwd_kernel(int64_t n, int K, int64_t n_coeff_rows, Coeffs cf, const float *__
   float x = 0.f, y = 0.f, z = 0.f, inorm = 0.f;
   if (DEG > 0) {
     if (FUSED) {
-      fused_dir(fz, i, x, y, z, false);
+      fused_dir(fz, i, x, y, z, n == fz.N);
     } else {
       const float *d = dirs + 3 * i;
       x = d[0]; y = d[1]; z = d[2];
@@ -438,7 +443,7 @@ sh_bwd_staged_kernel(int64_t n, Coeffs cf, const float *__restrict__ dirs,
       float x = 0.f, y = 0.f, z = 0.f, inorm = 0.f;
       if (DEG > 0) {
         if (FUSED) {
-          fused_dir(fz, ri, x, y, z, false);
+          fused_dir_cg(fz, CAMS ? c : 0, i, x, y, z);  // ri = c N + i
         } else {
           x = dirs[3 * i]; y = dirs[3 * i + 1]; z = dirs[3 * i + 2];
         }
