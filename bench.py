@@ -289,7 +289,6 @@ def main():
                  rank=rank, model=model, sharded_optimizer=dp_path, gaussian_shard=gshard,
                  dp_emulate_world=args.dp_emulate or None,
                  graph=not (args.eager or args.probe), **kw)
-    graphed = getattr(tr, "_graph", None) is not None
     N = means.shape[0]
 
     for it in range(start, start + args.warmup):
@@ -313,6 +312,8 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = max_over_ranks(time.perf_counter() - t0, world, dev)
+    # (after the timed region: a failed capture falls back to eager steps)
+    graphed = getattr(tr, "_graph", None) is not None
     if graphed:
         # kernel durations: a graph replay runs the same kernels as an eager
         # step, but HIP events cannot be recorded per replay -- time the
@@ -456,7 +457,9 @@ def main():
                    "visible_union_8_cameras": union_visible,
                    "packed": False, "loss": "0.8*L1+0.2*(1-SSIM valid)",
                    "step_issue": ("HIP graph replay of the captured step (sync-free isect, "
-                                  f"{graph_info})" if graphed else "eager launches"),
+                                  f"{graph_info})" if graphed else "eager launches" + (
+                                      f" (graph capture failed: {tr.graph_fallback})"
+                                      if getattr(tr, "graph_fallback", None) else "")),
                    "optimizer": "Adam (6 groups)" + (
                        ", each rank on its own Gaussians" if gshard else
                        ", sharded over ranks" if dp_path else

@@ -542,7 +542,7 @@ GS_INLINE float chunk_product(const Args &a, const WaveGeom &geo, int64_t start,
 // One work item of the forward: SPLIT = chunk `item` of the split tiles'
 // list, else the whole tile `item` of the dispatch order (past the plan's
 // count of whole tiles: nothing).
-template <int D, int BLEND, bool SPLIT>
+template <int D, bool SPLIT>
 GS_INLINE void fwd_item(const Args &a, float4 *st, int item) {
   using P = FwdPair<D>;
   constexpr int N4 = P::N4;
@@ -629,21 +629,6 @@ GS_INLINE void fwd_item(const Args &a, float4 *st, int item) {
     // one record of a pair: sequential in T
     auto blend = [&](float s2, float smax, float al, float idx) -> float {
       const bool hit = __float_as_uint(s2) <= __float_as_uint(smax);  // 0 <= s2 <= smax
-      if (BLEND == 1) {
-        // every select takes its compare's mask directly (no SALU mask
-        // arithmetic between the compare and the select): a miss blends
-        // alpha 0; a live pixel keeps T > 1e-4 through a miss, a dead one
-        // (T < 0) stays below it, so `gt` alone decides
-        const float a = hit ? al : 0.f;
-        const float nT = __builtin_fmaf(-T, a, T);
-        const bool gt = nT > kTMin;
-        const float Tsel = gt ? nT : T;
-        const float vis = T - Tsel;  // alpha * T when blended, else 0
-        const int32_t li = hit ? __float_as_int(idx) : last;
-        last = gt ? li : last;
-        T = gt ? nT : -fabsf(T);
-        return vis;
-      }
       const float nT = __builtin_fmaf(-T, al, T);  // T (1 - alpha)
       const bool gt = nT > kTMin;
       const bool ok = hit & gt;
@@ -835,7 +820,7 @@ GS_INLINE void fwd_item(const Args &a, float4 *st, int item) {
 // first: they are the longest work) and the other tiles in one launch, so the
 // chunks overlap the whole tiles; else the whole tiles only (the split path's
 // code costs registers: 80 -> 95 VGPRs, 6 -> 5 waves per SIMD at D = 3).
-template <int D, int BLEND = 0, bool SPLIT = false>
+template <int D, bool SPLIT = false>
 __global__ void __launch_bounds__(256)
 __attribute__((amdgpu_waves_per_eu(!SPLIT && D <= 3 ? 6 : 5))) fwd_kernel(Args a) {
   __shared__ float4 stage_all[4][32 * FwdPair<D>::N4];
@@ -843,11 +828,11 @@ __attribute__((amdgpu_waves_per_eu(!SPLIT && D <= 3 ? 6 : 5))) fwd_kernel(Args a
   if constexpr (SPLIT) {
     const int nc = a.n_chunks[0];
     if ((int)blockIdx.x < nc)
-      fwd_item<D, BLEND, true>(a, st, (int)blockIdx.x);
+      fwd_item<D, true>(a, st, (int)blockIdx.x);
     else
-      fwd_item<D, BLEND, false>(a, st, (int)blockIdx.x - nc);
+      fwd_item<D, false>(a, st, (int)blockIdx.x - nc);
   } else {
-    fwd_item<D, BLEND, false>(a, st, (int)blockIdx.x);
+    fwd_item<D, false>(a, st, (int)blockIdx.x);
   }
 }
 
@@ -1822,16 +1807,6 @@ static bool bwd_pf() {
 // work per wave doubles) -- unlike the 2DGS forward, where two pixels per
 // lane won 32 % -- and was removed.
 
-// Forward blend form (GSPLAT_HIP_FWD_BLEND, A/B): 0 = masks combined on the
-// SALU, 1 = every select on its own compare's mask.
-static int fwd_blend() {
-  static const int v = [] {
-    const char *e = getenv("GSPLAT_HIP_FWD_BLEND");
-    return (e && atoi(e) == 1) ? 1 : 0;
-  }();
-  return v;
-}
-
 static int g_dbg = INT32_MIN;  // not yet read from the environment
 static int dbg_flags() {
   if (g_dbg == INT32_MIN) {
@@ -1877,19 +1852,12 @@ int r16_fwd(r16::Args a, const void *state, char *split_base, hipStream_t st) {
     const int64_t nc = std::min<int64_t>(
         (int64_t)a.n_tiles + a.n_isects / a.SL + 1,
         a.n_isects / a.SL + a.n_isects / std::max<int64_t>(1, split_threshold(a.n_isects)) + 1);
-    if (fwd_blend() == 1)
-      hipLaunchKernelGGL((r16::fwd_kernel<D, 1, true>), dim3((unsigned)(a.n_tiles + nc)), dim3(256),
-                         0, st, a);
-    else
-      hipLaunchKernelGGL((r16::fwd_kernel<D, 0, true>), dim3((unsigned)(a.n_tiles + nc)), dim3(256),
-                         0, st, a);
+    hipLaunchKernelGGL((r16::fwd_kernel<D, true>), dim3((unsigned)(a.n_tiles + nc)), dim3(256),
+                       0, st, a);
     GS_CHECK_LAUNCH("rasterize_fwd16_split");
     return 0;
   }
-  if (fwd_blend() == 1)
-    hipLaunchKernelGGL((r16::fwd_kernel<D, 1>), dim3(a.n_tiles), dim3(256), 0, st, a);
-  else
-    hipLaunchKernelGGL((r16::fwd_kernel<D>), dim3(a.n_tiles), dim3(256), 0, st, a);
+  hipLaunchKernelGGL((r16::fwd_kernel<D>), dim3(a.n_tiles), dim3(256), 0, st, a);
   GS_CHECK_LAUNCH("rasterize_fwd16");
   return 0;
 }

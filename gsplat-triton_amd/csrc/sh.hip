@@ -443,7 +443,11 @@ sh_bwd_staged_kernel(int64_t n, Coeffs cf, const float *__restrict__ dirs,
       float x = 0.f, y = 0.f, z = 0.f, inorm = 0.f;
       if (DEG > 0) {
         if (FUSED) {
-          fused_dir_cg(fz, CAMS ? c : 0, i, x, y, z);  // ri = c N + i
+          // CAMS: ri = c N + i.  Otherwise row i of [C, N] (per-camera
+          // coefficients [C, N, K, 3]): camera and Gaussian from i, with no
+          // division when there is one camera (n == N)
+          if (CAMS) fused_dir_cg(fz, c, i, x, y, z);
+          else fused_dir(fz, i, x, y, z, n == fz.N);
         } else {
           x = dirs[3 * i]; y = dirs[3 * i + 1]; z = dirs[3 * i + 2];
         }

@@ -15,6 +15,7 @@ Same signatures, defaults, assertions, error types and autograd contract
 stream; there is no CPU or Triton fallback.
 """
 
+import contextlib
 import ctypes
 import math
 import os
@@ -935,6 +936,22 @@ def rasterize_to_pixels(
     return _rasterize_to_pixels(means2d, conics, colors, opacities, image_width, image_height,
                                 tile_size, isect_offsets, flatten_ids, backgrounds, masks, packed,
                                 absgrad, block_size)
+
+
+@contextlib.contextmanager
+def fwd_split_div(div: Optional[int]):
+    """The split forward's threshold divisor (gsplat_hip_set_fwd_split_div)
+    for the renders queued inside the block only; the previous value is
+    restored after it, so a trainer's choice does not leak into other
+    rasterization() calls of the process.  None / 0: leave it alone."""
+    if not div:
+        yield
+        return
+    old = int(_lib.query("gsplat_hip_set_fwd_split_div", int(div)))
+    try:
+        yield
+    finally:
+        _lib.query("gsplat_hip_set_fwd_split_div", old)
 
 
 @torch.no_grad()

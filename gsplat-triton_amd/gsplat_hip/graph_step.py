@@ -55,6 +55,13 @@ from .rendering import rasterization
 from .strategy import activate, update_state_
 
 
+class GraphCaptureError(RuntimeError):
+    """A capture of the training step failed (on this rank or, for a
+    Gaussian-sharded job, on any rank: the ranks agree before replaying).
+    Trainer.step catches it and runs the steps eagerly from then on, in the
+    same process."""
+
+
 def graphable(tr) -> bool:
     """Whether Trainer `tr` can run its steps as graph replays.  With a
     DefaultStrategy schedule the steps between refines are replays; the
@@ -62,13 +69,14 @@ def graphable(tr) -> bool:
     refine (new parameter tensors, Trainer._param_gen) re-captures."""
     st = tr.strategy
     # Gaussian-sharded (one camera per rank): its two pair exchanges inside
-    # the graph -- the device copies of the one-GPU emulation
-    # (distributed.EMULATION, bench --gshard-emulate), or RCCL's
-    # all_to_all_single when GSPLAT_HIP_GRAPH_RCCL=1 (not run on more than one
-    # GPU here)
+    # the graph -- RCCL's all_to_all_single (the default at N > 1; the
+    # capture is checked on a one-rank RCCL group by
+    # tests/test_gpu_distributed.py; GSPLAT_HIP_GRAPH_RCCL=0 issues those
+    # steps eagerly) or the device copies of the one-GPU emulation
+    # (distributed.EMULATION, bench --gshard-emulate)
     from . import distributed as gdist
     gshard_ok = getattr(tr, "gshard", False) and tr.world_size <= GraphStep.MAX_WORLD and (
-        gdist.EMULATION is not None or os.environ.get("GSPLAT_HIP_GRAPH_RCCL", "0") == "1")
+        gdist.EMULATION is not None or os.environ.get("GSPLAT_HIP_GRAPH_RCCL", "1") != "0")
     return (tr.fused and not tr.sharded and tr.model == "3dgs"
             and (gshard_ok or (tr.world_size == 1 and not getattr(tr, "gshard", False)))
             and not getattr(tr, "defer_sh", False)
@@ -179,7 +187,8 @@ class GraphStep:
         self.key = None
         self.counts = None  # the graph's isect counts (device i64[4])
         self.loss = None
-        self.pending = collections.deque()  # (it, slot, event) awaiting the overflow check
+        # (it, slot, event, seq, returned loss) awaiting the overflow check
+        self.pending = collections.deque()
         self.issued = 0
         self.recaptures = 0
         self.capture_s = []  # host seconds per capture (warm-up, capture, instantiate)
@@ -217,12 +226,13 @@ class GraphStep:
         if self.gshard:  # the world's cameras from the block, shard sizes fixed per capture
             dkw = dict(distributed=True, _world_cameras=(self.vm_w, self.K_w),
                        _world_counts=tr._n_world)
-        colors, _, meta = rasterization(
-            p["means"], p["quats"], scales, opac, (p["sh0"], p["shN"]), self.vm, self.K, tr.width,
-            tr.height, sh_degree=deg, packed=False, near_plane=0.01, far_plane=1e10,
-            radius_clip=0.0, rasterize_mode="classic", _fusion=fusion,
-            _isect_capacity=self.capacity, _isect_status=self.status,
-            _isect_report=(self.ring_out.dev, self.slot), _isect_ids=False, **dkw)
+        with _wrapper.fwd_split_div(getattr(tr, "split_div", None)):
+            colors, _, meta = rasterization(
+                p["means"], p["quats"], scales, opac, (p["sh0"], p["shN"]), self.vm, self.K,
+                tr.width, tr.height, sh_degree=deg, packed=False, near_plane=0.01,
+                far_plane=1e10, radius_clip=0.0, rasterize_mode="classic", _fusion=fusion,
+                _isect_capacity=self.capacity, _isect_status=self.status,
+                _isect_report=(self.ring_out.dev, self.slot), _isect_ids=False, **dkw)
         grad_box = {}
         meta["means2d"].register_hook(lambda g: grad_box.__setitem__("g", g))
         loss = tr._regularise(l1_ssim_loss(
@@ -243,10 +253,33 @@ class GraphStep:
 
     def _capture(self, deg, stats=True):
         t0 = time.perf_counter()
+        err = None
         try:
             self._capture_impl(deg, stats)
+        except Exception as e:  # noqa: BLE001 -- any capture failure: eager fallback
+            err = e
+            self.graph, self.key = None, None
         finally:
             self.capture_s.append(time.perf_counter() - t0)
+        ok = self._agree(err is None)
+        if err is not None:
+            raise GraphCaptureError(f"capture failed on this rank: {err!r}") from err
+        if not ok:
+            self.graph, self.key = None, None
+            raise GraphCaptureError("capture failed on another rank")
+
+    def _agree(self, ok: bool) -> bool:
+        """A Gaussian-sharded job replays only if every rank captured: one
+        MIN all-reduce of the ranks' outcomes, outside the capture (the
+        ranks' replays hold matching RCCL exchanges, so all replay or none)."""
+        import torch.distributed as dist
+        from . import distributed as gdist
+        if not (self.gshard and self.tr.world_size > 1 and gdist.EMULATION is None
+                and dist.is_initialized()):
+            return ok
+        t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=self.dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        return bool(int(t.item()))
 
     def _capture_impl(self, deg, stats=True):
         tr = self.tr
@@ -359,16 +392,17 @@ class GraphStep:
             self.graph = None  # the old capture's pool holds the old tensors
             self._capture(deg, stats)
         self._check(block=len(self.pending) >= self.lag)
-        k = self.issued  # this replay's fetch sees seq == k
-        self._issue(it)
-        if self.ring_loss:  # the loss launch wrote it to its own slot
-            return self.loss_ring[k % self.LOSS_RING]
-        # a copy: the graph's static output is overwritten by the next replay
-        # (eager Trainer.step returns a fresh tensor per step as well)
-        return self.loss.clone()
+        return self._issue(it)
 
-    def _issue(self, it):
-        slot = self.issued % self.RING
+    def _issue(self, it, ret=None):
+        """Replay step `it` as the `issued`-th step; returns its loss: the
+        loss-ring slot `issued % LOSS_RING` (written by the loss launch), or,
+        without the ring, a copy of the graph's static loss (overwritten by
+        the next replay; eager Trainer.step returns a fresh tensor per step as
+        well).  `ret`: a redo of a voided step writes into the tensor already
+        returned for it (_recover)."""
+        k = self.issued  # this replay's fetch sees seq == k
+        slot = k % self.RING
         ev = self._slot_ev[slot]
         if ev is not None:
             ev.synchronize()  # the step that used this slot RING steps ago is done
@@ -376,18 +410,25 @@ class GraphStep:
         self._fill(it, slot)
         self.graph.replay()
         self.tr.opt.step_count += 1
+        if self.ring_loss:
+            ret = self.loss_ring[k % self.LOSS_RING]
+        elif ret is None:
+            ret = self.loss.clone()
+        else:
+            ret.copy_(self.loss)
         ev = torch.cuda.Event()
         ev.record(torch.cuda.current_stream(self.dev))
         self._slot_ev[slot] = ev
-        self.pending.append((it, slot, ev))
+        self.pending.append((it, slot, ev, k, ret))
         self.issued += 1
         self.replays += 1
         self.host_s += time.perf_counter() - t0  # host work of the step, waits excluded
+        return ret
 
     def _check(self, block=False):
         """Read the counts of finished steps; on an overflow, redo from there."""
         while self.pending:
-            it, slot, ev = self.pending[0]
+            it, slot, ev = self.pending[0][:3]
             if not ev.query():
                 if not block:
                     return
@@ -405,16 +446,20 @@ class GraphStep:
         flag): grow, re-capture, re-run them in order."""
         tr = self.tr
         torch.cuda.synchronize(self.dev)
-        redo = [it for it, _, _ in self.pending]
-        for _, slot, _ in self.pending:
+        redo = [(it, k, ret) for it, _, _, k, ret in self.pending]
+        for _, slot, _, _, _ in self.pending:
             self.max_isects = max(self.max_isects, int(self._out[slot][3]))
         self.pending.clear()
         tr.opt.step_count -= len(redo)  # their Adam steps did not happen
         self.capacity = int(math.ceil(self.max_isects * self.headroom)) + 1
         self.status.zero_()
-        self._capture(tr.sh_degree_at(redo[0]), self._stats_at(redo[0]))
-        for it in redo:
-            self._issue(it)
+        # the redo steps take the voided steps' sequence numbers, so each
+        # step's loss lands in the slot (or tensor) already returned for it
+        self.issued = redo[0][1]
+        self._capture(tr.sh_degree_at(redo[0][0]), self._stats_at(redo[0][0]))
+        for it, k, ret in redo:
+            assert self.issued == k
+            self._issue(it, ret)
             self._check(block=True)
 
     def _drain(self):

@@ -57,7 +57,7 @@ import torch.nn.functional as F
 from . import densify
 from .densify import DefaultStrategyConfig
 from .losses import FusedAdam, l1_ssim_loss, ssim_and_l1
-from . import _lib, _wrapper
+from . import _wrapper
 from .rendering import rasterization, rasterization_2dgs
 from .strategy import activate, update_state_
 
@@ -276,6 +276,7 @@ class Trainer:
         # isect_capacity: its isect arrays' initial size (default: 1.25 x the
         # first camera's count)
         self._graph = None
+        self.graph_fallback = None  # why the captured step fell back to eager, if it did
         if graph:
             from .graph_step import GraphStep, graphable
             if graphable(self):
@@ -441,13 +442,14 @@ class Trainer:
         if getattr(self, "gshard", False):
             dkw = dict(distributed=True, _world_cameras=self.world_cameras(ci, world_ci),
                        _world_counts=self._n_world)
-        return rasterization(
-            p["means"], p["quats"], scales, opac,
-            (p["sh0"], p["shN"]) if self.fused else torch.cat([p["sh0"], p["shN"]], 1),
-            self.viewmats[ci:ci + 1], self.Ks[ci:ci + 1], self.width, self.height,
-            sh_degree=deg, packed=False, near_plane=0.01, far_plane=1e10, radius_clip=0.0,
-            rasterize_mode="classic", absgrad=absgrad, _colors_ready=hook, _fusion=fusion,
-            **dkw)
+        with _wrapper.fwd_split_div(getattr(self, "split_div", None)):
+            return rasterization(
+                p["means"], p["quats"], scales, opac,
+                (p["sh0"], p["shN"]) if self.fused else torch.cat([p["sh0"], p["shN"]], 1),
+                self.viewmats[ci:ci + 1], self.Ks[ci:ci + 1], self.width, self.height,
+                sh_degree=deg, packed=False, near_plane=0.01, far_plane=1e10, radius_clip=0.0,
+                rasterize_mode="classic", absgrad=absgrad, _colors_ready=hook, _fusion=fusion,
+                **dkw)
 
     def _tune_split(self, it: int):
         """Once, before the first step (and so before a graph capture freezes
@@ -457,7 +459,10 @@ class Trainer:
         more of them (divisor 1100); scenes that terminate early (M2: 0.56)
         keep 550, whose split-capable variant would only cost occupancy
         (DESIGN 3.4).  One-GPU 3DGS on the HIP path; GSPLAT_HIP_FWD_SPLIT_DIV
-        set by the user wins."""
+        set by the user wins.  The divisor is this trainer's: its renders (and
+        its graph capture) set it around their launches and restore the
+        previous value (_wrapper.fwd_split_div), nothing else in the process
+        sees it.  Costs one eager render (no backward) before the first step."""
         self._split_tuned = True
         if (self.model != "3dgs" or not self.fused or self.world_size != 1
                 or os.environ.get("GSPLAT_HIP_FWD_SPLIT_DIV")):
@@ -465,17 +470,26 @@ class Trainer:
         colors, _, meta = self.render(self.camera_index(it), self.sh_degree_at(it))
         self.term_ratio = _wrapper.forward_termination_ratio(colors, meta, self.width, self.height)
         self.split_div = 1100 if self.term_ratio > 0.75 else 550
-        _lib.query("gsplat_hip_set_fwd_split_div", self.split_div)
         del colors, meta
 
     def step(self, it: int):
         if not getattr(self, "_split_tuned", False):
             self._tune_split(it)
         if getattr(self, "_graph", None) is not None:
-            loss = self._graph.step(it)
-            if self.strategy is not None:
-                self.post_step(it)  # eager refine / reset: drains the replays first
-            return loss
+            from .graph_step import GraphCaptureError
+            try:
+                loss = self._graph.step(it)
+            except GraphCaptureError as e:
+                # the capture failed (on any rank of a sharded job): eager
+                # steps from here on, in this process (no re-exec)
+                import warnings
+                self.graph_fallback = str(e)
+                warnings.warn(f"gsplat_hip: {e}; issuing the training steps eagerly")
+                self._graph = None
+            else:
+                if self.strategy is not None:
+                    self.post_step(it)  # eager refine / reset: drains the replays first
+                return loss
         ci = self.camera_index(it)
         self._sh_ready = 0
         fusion = self._make_fusion()

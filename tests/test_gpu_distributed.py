@@ -122,3 +122,61 @@ def test_trainer_sharded_optimizer_single_rank_matches(model):
     for k in out[0]:
         d = float((out[1][k] - out[0][k]).abs().max())
         assert d <= 6 * Trainer.LRS[k], (k, d)
+
+
+def test_graph_gshard_rccl_step_tracks_eager():
+    """The Gaussian-sharded step captured with its two pair exchanges as
+    RCCL all_to_all_single inside the graph (the N > 1 default,
+    graph_step.graphable) on a one-rank RCCL group: every replayed step's
+    loss equals the eager step's, and after five steps the parameters, the
+    strategy statistics and the step counts agree.  No fallback was taken."""
+    from gsplat_hip.train_step import Trainer
+    from test_gpu_graph import _trainer_scene
+    means, rgbs, vm, K, W, H = _trainer_scene()
+    out = {}
+    for graph in (False, True):
+        tr = Trainer(means, rgbs, vm, K, W, H, device=DEV, world_size=1, rank=0,
+                     gaussian_shard=True, graph=graph, max_steps=100)
+        assert (tr._graph is not None) == graph
+        losses = [tr.step(it) for it in range(5)]
+        tr.sync()
+        assert tr.graph_fallback is None, tr.graph_fallback
+        if graph:
+            g = tr._graph
+            assert g is not None and g.replays >= 5
+            census = dict(g.census)
+            print("census", census)
+            assert census.get("kernel", 0) > 20 and "memset" not in census, census
+        out[graph] = ({k: p.detach().clone() for k, p in tr.params.items()},
+                      tr.count.clone(), tr.grad2d.clone(), tr.opt.step_count,
+                      [float(x) for x in losses])
+    a, b = out[False], out[True]
+    assert a[3] == b[3] == 5
+    torch.testing.assert_close(torch.tensor(b[4]), torch.tensor(a[4]), rtol=1e-4, atol=1e-6)
+    for k in a[0]:
+        torch.testing.assert_close(b[0][k], a[0][k], rtol=1e-3, atol=1e-5)
+    torch.testing.assert_close(b[1], a[1], rtol=0, atol=0)
+    torch.testing.assert_close(b[2], a[2], rtol=1e-3, atol=1e-7)
+
+
+def test_graph_capture_failure_falls_back_to_eager(monkeypatch):
+    """A capture that raises leaves the trainer on eager steps in the same
+    process (Trainer.graph_fallback says why), with the eager results."""
+    from gsplat_hip import graph_step
+    from gsplat_hip.train_step import Trainer
+    from test_gpu_graph import _trainer_scene
+    means, rgbs, vm, K, W, H = _trainer_scene()
+    ref = Trainer(means, rgbs, vm, K, W, H, device=DEV, graph=False, max_steps=100)
+    la = [float(ref.step(it)) for it in range(3)]
+
+    def boom(self, deg, stats=True):
+        raise RuntimeError("injected capture failure")
+    monkeypatch.setattr(graph_step.GraphStep, "_capture_impl", boom)
+    tr = Trainer(means, rgbs, vm, K, W, H, device=DEV, graph=True, max_steps=100)
+    assert tr._graph is not None
+    with pytest.warns(UserWarning, match="eagerly"):
+        lb = [float(tr.step(it)) for it in range(3)]
+    assert tr._graph is None and "injected" in tr.graph_fallback
+    assert tr.opt.step_count == 3
+    for x, y in zip(la, lb):
+        assert abs(x - y) <= 1e-4 * abs(x), (la, lb)

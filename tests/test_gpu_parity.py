@@ -705,6 +705,47 @@ def test_sh_colors_fused_vs_unfused(degree, C, split):
         close(b, a, 1e-4, 5e-5)
 
 
+@pytest.mark.parametrize("degree,C", [(3, 2), (3, 3), (2, 4), (1, 2)])
+def test_sh_colors_per_camera_coeffs(degree, C):
+    """Per-camera coefficients [C,N,K,3] with K == (degree+1)^2 (the staged
+    backward over C*N rows): row i must take camera i // N's centre and
+    Gaussian i % N's mean -- against the torch glue of rendering.py:396-406."""
+    import gsplat_hip
+    from gsplat_hip._wrapper import sh_colors
+    g = torch.Generator().manual_seed(100 + degree * 10 + C)
+    N, K = 2500, (degree + 1) ** 2
+    means = (torch.randn(N, 3, generator=g) * 2).to(DEV)
+    sh = (torch.randn(C, N, K, 3, generator=g) * 0.5).to(DEV)
+    vm = torch.eye(4).repeat(C, 1, 1)
+    for c in range(C):
+        q = torch.nn.functional.normalize(torch.randn(4, generator=g), dim=0)
+        w, x, y, z = q.tolist()
+        vm[c, :3, :3] = torch.tensor([[1 - 2 * (y * y + z * z), 2 * (x * y - w * z), 2 * (x * z + w * y)],
+                                      [2 * (x * y + w * z), 1 - 2 * (x * x + z * z), 2 * (y * z - w * x)],
+                                      [2 * (x * z - w * y), 2 * (y * z + w * x), 1 - 2 * (x * x + y * y)]])
+        vm[c, :3, 3] = torch.randn(3, generator=g) * 3
+    vm = vm.to(DEV)
+    radii = (torch.rand(C, N, generator=g) > 0.3).int().to(DEV) * 5
+    vc = torch.randn(C, N, 3, generator=g).to(DEV)
+
+    def unfused(m, s):
+        dirs = m[None] - torch.inverse(vm)[:, None, :3, 3]
+        col = gsplat_hip.spherical_harmonics(degree, dirs, s, masks=radii > 0)
+        return torch.clamp_min(col + 0.5, 0.0)
+
+    def fused(m, s):
+        return sh_colors(degree, m, vm, s, radii)
+
+    outs = []
+    for fn in (unfused, fused):
+        m = means.clone().requires_grad_(True)
+        s = sh.clone().requires_grad_(True)
+        col = fn(m, s)
+        outs.append((col,) + tuple(torch.autograd.grad((col * vc).sum(), [m, s])))
+    for a, b in zip(outs[0], outs[1]):
+        close(b, a, 1e-4, 5e-5)
+
+
 @pytest.mark.parametrize("n_pile", [300, 5000, 20000])
 def test_isect_tile_first_long_runs(n_pile):
     """Tiles with very long isect runs: the per-run depth sort switches from
