@@ -56,3 +56,48 @@ extern "C" int gsplat_hip_graph_node_census(void *graph, int64_t *counts, int64_
   }
   return 0;
 }
+
+// The memcpy nodes of a captured graph (ABI 31): for the first max_nodes,
+// out[4 k .. 4 k + 3] = (destination, source, bytes, hipMemcpyKind), -1 where
+// the node's parameters cannot be read.  RCCL's one-rank exchange inside a
+// captured Gaussian-sharded step is such a node (a device-to-device copy of
+// the rank's own block); graph_step allows device-to-device copies there.
+// Returns 0, or 2 when a HIP graph query fails.
+extern "C" int gsplat_hip_graph_memcpy_census(void *graph, int64_t *out, int max_nodes,
+                                              int *n_out) {
+  hipGraph_t g = reinterpret_cast<hipGraph_t>(graph);
+  size_t n = 0;
+  *n_out = 0;
+  if (hipGraphGetNodes(g, nullptr, &n) != hipSuccess) {
+    gs::set_error("graph_memcpy_census: hipGraphGetNodes failed");
+    return 2;
+  }
+  std::vector<hipGraphNode_t> nodes(n);
+  if (n && hipGraphGetNodes(g, nodes.data(), &n) != hipSuccess) {
+    gs::set_error("graph_memcpy_census: hipGraphGetNodes failed");
+    return 2;
+  }
+  int k = 0;
+  for (size_t i = 0; i < n; ++i) {
+    hipGraphNodeType t;
+    if (hipGraphNodeGetType(nodes[i], &t) != hipSuccess) {
+      gs::set_error("graph_memcpy_census: hipGraphNodeGetType failed");
+      return 2;
+    }
+    if (t != hipGraphNodeTypeMemcpy) continue;
+    if (k < max_nodes) {
+      hipMemcpy3DParms p{};
+      int64_t *o = out + 4 * k;
+      o[0] = o[1] = o[2] = o[3] = -1;
+      if (hipGraphMemcpyNodeGetParams(nodes[i], &p) == hipSuccess) {
+        o[0] = (int64_t)reinterpret_cast<uintptr_t>(p.dstPtr.ptr);
+        o[1] = (int64_t)reinterpret_cast<uintptr_t>(p.srcPtr.ptr);
+        o[2] = (int64_t)p.extent.width * (int64_t)p.extent.height * (int64_t)p.extent.depth;
+        o[3] = (int64_t)p.kind;
+      }
+    }
+    ++k;
+  }
+  *n_out = k;
+  return 0;
+}

@@ -211,6 +211,53 @@ __global__ void __launch_bounds__(1024) packed_scan_kernel(int64_t nb, int64_t *
   if (threadIdx.x == 0) total[0] = carry;
 }
 
+// The geometry groups' Adam step fused into the backward (ABI 31,
+// gsplat_hip_projection_bwd_adam; C == 1, non-packed): instead of storing
+// v_means / v_quats / v_scales, every lane applies torch.optim.Adam to its
+// Gaussian's rows of the four geometry parameters in place, with the
+// gradients the trainer's FusedAdam would have formed (adam_step_ex modes):
+// means  g = v_means + v_dirs          (the SH backward's part; autograd's sum)
+// quats  g = v_quats
+// log-scales  g = v_scales * exp(log_scales)   (exp's VJP, the activated scale)
+// logits      g = v_opac * (1 - o) * o         (sigmoid's VJP, o = sigmoid(logits))
+// -- the same arithmetic as activate_bwd_kernel / adam::xform, the same
+// element update (common.h adam_update), so the result is bit-identical to
+// projection backward + activation backward + FusedAdam (the gradient
+// algebra above is the unfused kernel's own code: the fusion is a runtime
+// branch of the epilogue).  88 B per Gaussian of gradients never reach HBM.
+struct GeomAdam {
+  float *p[4];  // means [N,3], log-scales [N,3], quats [N,4], logits [N] (the trainer's order)
+  float *m[4], *v[4];
+  const float *v_dirs;  // [N,3] or null
+  const float *v_opac;  // [N] dL/d sigmoid(logits), or null
+  const float *opac;    // [N] sigmoid(logits) of the forward
+  float ss[4], ib;      // lr_i / (1 - beta1^t), 1 / sqrt(1 - beta2^t)
+  const float *hyper;   // device [8]: (ss_i, ib) per group (captured step), or null
+  const int32_t *skip;  // device flag: non-zero = void step (nothing updated), or null
+  float b1, b2, eps;
+  int on;
+};
+
+template <int K>
+GS_INLINE void adam_row(float *P, float *M, float *V, const float *g, float ss, float ib,
+                        const GeomAdam &ga) {
+  float pp[K], mm[K], vv[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    pp[k] = P[k];
+    mm[k] = M[k];
+    vv[k] = V[k];
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) adam_update(pp[k], g[k], mm[k], vv[k], ga.b1, ga.b2, ga.eps, ss, ib);
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    P[k] = pp[k];
+    M[k] = mm[k];
+    V[k] = vv[k];
+  }
+}
+
 struct ProjBwdArgs {
   int C, N, W, H;
   float eps2d;
@@ -225,6 +272,7 @@ struct ProjBwdArgs {
   const int64_t *camera_ids, *gaussian_ids;
   int64_t nnz;
   int sparse;
+  GeomAdam ga;  // ga.on: the geometry Adam instead of the gradient stores (store_mode)
 };
 
 __global__ void __launch_bounds__(256) projection_bwd_kernel(ProjBwdArgs a) {
@@ -362,6 +410,41 @@ __global__ void __launch_bounds__(256) projection_bwd_kernel(ProjBwdArgs a) {
       o = a.v_scales + 3 * idx;
       o[0] = vs[0]; o[1] = vs[1]; o[2] = vs[2];
     }
+  } else if (a.store_mode && a.ga.on) {
+    const GeomAdam &ga = a.ga;
+    if (n < a.N && !(ga.skip && *ga.skip)) {
+      const size_t i = (size_t)n;
+      float ss[4], ib;
+      if (ga.hyper) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) ss[k] = ga.hyper[2 * k];
+        ib = ga.hyper[1];
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) ss[k] = ga.ss[k];
+        ib = ga.ib;
+      }
+      float g[4];
+      // means: v_means + v_dirs
+#pragma unroll
+      for (int j = 0; j < 3; ++j) g[j] = ga.v_dirs ? vm[j] + ga.v_dirs[3 * i + j] : vm[j];
+      adam_row<3>(ga.p[0] + 3 * i, ga.m[0] + 3 * i, ga.v[0] + 3 * i, g, ss[0], ib, ga);
+      // log-scales: exp's VJP with the activated scale (the input `scales`)
+      const float *sp = a.scales + 3 * i;
+#pragma unroll
+      for (int j = 0; j < 3; ++j) g[j] = vs[j] * sp[j];
+      adam_row<3>(ga.p[1] + 3 * i, ga.m[1] + 3 * i, ga.v[1] + 3 * i, g, ss[1], ib, ga);
+      // quats
+      adam_row<4>(ga.p[2] + 4 * i, ga.m[2] + 4 * i, ga.v[2] + 4 * i, vq, ss[2], ib, ga);
+      // logits: sigmoid's VJP
+      if (ga.v_opac) {
+        const float o = ga.opac[i];
+        g[0] = ga.v_opac[i] * (1.f - o) * o;
+      } else {
+        g[0] = 0.f;
+      }
+      adam_row<1>(ga.p[3] + i, ga.m[3] + i, ga.v[3] + i, g, ss[3], ib, ga);
+    }
   } else if (a.store_mode) {
     if (n < a.N) {
       float *o = a.v_means + 3 * (size_t)n;
@@ -484,6 +567,57 @@ extern "C" int gsplat_hip_projection_bwd(
   dim3 grid((N + 255) / 256, C);
   hipLaunchKernelGGL(projection_bwd_kernel, grid, dim3(256), 0, st, a);
   GS_CHECK_LAUNCH("projection_bwd");
+  return 0;
+}
+
+// gsplat_hip_projection_bwd with the geometry groups' Adam step fused in
+// (ABI 31, see struct GeomAdam): C == 1; params / exp_avgs / exp_avg_sqs are
+// [means, log_scales, quats, logits]; lrs[4] with the 1-based step, or
+// hyper_device f32[8] = (lr_i / (1 - beta1^t), 1 / sqrt(1 - beta2^t)) per
+// group in that order (then lrs / step are unused); skip_device may be NULL.
+extern "C" int gsplat_hip_projection_bwd_adam(
+    int N, const float *means, const float *quats, const float *scales, const float *viewmats,
+    const float *Ks, int width, int height, float eps2d, const int32_t *radii,
+    const float *conics, const float *v_means2d, const float *v_depths, const float *v_conics,
+    const float *v_dirs, const float *v_opac, const float *opac, float *const *params,
+    float *const *exp_avgs, float *const *exp_avg_sqs, const float *lrs, float beta1,
+    float beta2, float eps, int step, const float *hyper_device, const int32_t *skip_device,
+    void *stream) {
+  GS_REQUIRE(N >= 0, "projection_bwd_adam: negative N=%d", N);
+  if (N == 0) return 0;
+  GS_REQUIRE(params && exp_avgs && exp_avg_sqs, "projection_bwd_adam: null group arrays");
+  GS_REQUIRE(hyper_device || (lrs && step >= 1), "projection_bwd_adam: lrs and step >= 1, or hyper");
+  GS_REQUIRE(!v_opac || opac, "projection_bwd_adam: v_opac needs opac");
+  GS_REQUIRE(((uintptr_t)quats & 15) == 0, "projection_bwd_adam: quats must be 16-B aligned");
+  GeomAdam ga{};
+  for (int k = 0; k < 4; ++k) {
+    GS_REQUIRE(params[k] && exp_avgs[k] && exp_avg_sqs[k],
+               "projection_bwd_adam: null parameter / moment of group %d", k);
+    ga.p[k] = params[k];
+    ga.m[k] = exp_avgs[k];
+    ga.v[k] = exp_avg_sqs[k];
+  }
+  ga.v_dirs = v_dirs;
+  ga.v_opac = v_opac;
+  ga.opac = opac;
+  ga.hyper = hyper_device;
+  ga.skip = skip_device;
+  ga.b1 = beta1;
+  ga.b2 = beta2;
+  ga.eps = eps;
+  ga.on = 1;
+  if (!hyper_device) {  // gsplat_hip_adam_step's host arithmetic
+    const double bc1 = 1.0 - pow((double)beta1, step), bc2 = 1.0 - pow((double)beta2, step);
+    for (int k = 0; k < 4; ++k) ga.ss[k] = (float)(lrs[k] / bc1);
+    ga.ib = (float)(1.0 / sqrt(bc2));
+  }
+  ProjBwdArgs a{1, N, width, height, eps2d, means, quats, scales, viewmats, Ks, radii, conics,
+                nullptr, v_means2d, v_depths, v_conics, nullptr, nullptr, nullptr, nullptr,
+                nullptr, 1};
+  a.ga = ga;
+  hipLaunchKernelGGL(projection_bwd_kernel, dim3((N + 255) / 256, 1), dim3(256), 0,
+                     (hipStream_t)stream, a);
+  GS_CHECK_LAUNCH("projection_bwd_adam");
   return 0;
 }
 

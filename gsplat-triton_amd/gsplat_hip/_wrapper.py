@@ -107,10 +107,11 @@ class _FullyFusedProjection(torch.autograd.Function):
     @staticmethod
     def forward(ctx, means, covars, quats, scales, viewmats, Ks, width, height, eps2d,
                 near_plane, far_plane, radius_clip, calc_compensations,
-                camera_model="pinhole", block_size=256):
+                camera_model="pinhole", block_size=256, fusion=None):
         if camera_model != "pinhole":
             raise NotImplementedError(f"Unsupported camera model: {camera_model}")
         ctx.set_materialize_grads(False)  # unused outputs: None, no zero-filled buffers
+        ctx.fusion = fusion  # a training step's StepFusion (geometry Adam in this backward)
         assert (covars is None) and (quats is not None) and (scales is not None)
         means, quats, scales, viewmats, Ks = (_f32c(x) for x in (means, quats, scales, viewmats, Ks))
         quats = _aligned16(quats)
@@ -148,6 +149,14 @@ class _FullyFusedProjection(torch.autograd.Function):
         else:
             v_compensations = None
         want_vm = ctx.needs_input_grad[4]
+        fusion = ctx.fusion
+        if (fusion is not None and C == 1 and comps is None and not want_vm
+                and fusion.geom_adam_ready()):
+            # the trainer's geometry Adam step in this backward: no gradients
+            # stored (gsplat_hip_projection_bwd_adam)
+            fusion.geom_adam.run(means, quats, scales, viewmats, Ks, ctx.width, ctx.height,
+                                 ctx.eps2d, radii, conics, v_means2d, v_depths, v_conics, fusion)
+            return (None,) * 16
         v_means = torch.empty((N, 3), device=dev)
         v_quats = torch.empty((N, 4), device=dev)
         v_scales = torch.empty((N, 3), device=dev)
@@ -160,7 +169,7 @@ class _FullyFusedProjection(torch.autograd.Function):
         return (v_means if ctx.needs_input_grad[0] else None, None,
                 v_quats if ctx.needs_input_grad[2] else None,
                 v_scales if ctx.needs_input_grad[3] else None,
-                v_viewmats, None, None, None, None, None, None, None, None, None, None)
+                v_viewmats, None, None, None, None, None, None, None, None, None, None, None)
 
 
 class _FullyFusedProjectionPacked(torch.autograd.Function):
@@ -648,12 +657,31 @@ class StepFusion:
     nodes (retain_graph) returns ordinary gradients, which the trainer then
     adds as extra terms."""
 
-    def __init__(self, sh_adam: Optional["ShAdamInBackward"] = None, geom: bool = False):
+    def __init__(self, sh_adam: Optional["ShAdamInBackward"] = None, geom: bool = False,
+                 geom_adam: Optional["GeomAdamInBackward"] = None):
         self.sh_adam = sh_adam
-        self.geom = bool(geom)
+        self.geom = bool(geom) or geom_adam is not None
+        self.geom_adam = geom_adam
         self.v_dirs = None
         self.v_scales = self.v_opac = self.scales = self.opac = None
         self.act_taken = False
+        # geom_adam: set in the forward by the nodes whose gradients the
+        # projection backward needs (the SH colours' means gradient, the
+        # opacities' gradient through _OpacityTap, the activation's output)
+        self.expect_v_dirs = False
+        self.opac_act = None
+        self.opac_tapped = False
+        self.v_opac_in = None
+
+    def geom_adam_ready(self) -> bool:
+        """The projection backward may run the geometry Adam: armed, not run
+        yet, and every gradient it consumes has arrived (autograd runs the SH
+        colours' and the opacity tap's backward before the projection's: they
+        were created after it; otherwise the step takes the unfused path)."""
+        ga = self.geom_adam
+        return (ga is not None and not ga.applied and self.opac_act is not None
+                and (self.v_dirs is not None or not self.expect_v_dirs)
+                and (self.v_opac_in is not None or not self.opac_tapped))
 
     def take_means_grad(self, v_means: Optional[Tensor]) -> Optional[Tensor]:
         """The SH backward's means gradient: kept here (returns None) when the
@@ -670,6 +698,65 @@ class StepFusion:
         self.act_taken = True
         self.v_scales, self.v_opac, self.scales, self.opac = v_scales, v_opac, scales, opac
         return True
+
+
+class GeomAdamInBackward:
+    """Arms the next projection backward (C == 1) to apply torch.optim.Adam to
+    the four geometry parameters [means, log-scales, quats, logits] (the
+    trainer's order and learning rates) in place, from the gradients the
+    trainer's FusedAdam would have formed (gsplat_hip_projection_bwd_adam):
+    the optimizer step fused into its producer, as ShAdamInBackward does for
+    the SH rows.  `applied` tells the caller whether it ran; the activation
+    backward then returns nothing (its gradients were consumed)."""
+
+    def __init__(self, params, exp_avgs, exp_avg_sqs, lrs, betas, eps, step, hyper=None,
+                 skip=None):
+        assert len(params) == len(exp_avgs) == len(exp_avg_sqs) == len(lrs) == 4
+        self.params, self.exp_avgs, self.exp_avg_sqs = list(params), list(exp_avgs), \
+            list(exp_avg_sqs)
+        self.lrs, self.betas, self.eps, self.step = [float(x) for x in lrs], betas, eps, step
+        self.hyper, self.skip = hyper, skip  # captured step: device factors f32[8], void flag
+        self.applied = False
+
+    def run(self, means, quats, scales, viewmats, Ks, width, height, eps2d, radii, conics,
+            v_means2d, v_depths, v_conics, fusion):
+        N = means.shape[0]
+        for t in self.params + self.exp_avgs + self.exp_avg_sqs:
+            assert t.is_contiguous() and t.dtype == torch.float32
+        assert [t.shape[0] for t in self.params] == [N] * 4
+        P = ctypes.c_void_p * 4
+        v_opac = fusion.v_opac_in
+        _lib.call("gsplat_hip_projection_bwd_adam", N, _ptr(means), _ptr(quats), _ptr(scales),
+                  _ptr(viewmats), _ptr(Ks), int(width), int(height), float(eps2d), _ptr(radii),
+                  _ptr(conics), _ptr(v_means2d), _ptr(v_depths), _ptr(v_conics),
+                  _ptr(fusion.v_dirs), _ptr(v_opac), _ptr(fusion.opac_act),
+                  P(*[t.data_ptr() for t in self.params]),
+                  P(*[t.data_ptr() for t in self.exp_avgs]),
+                  P(*[t.data_ptr() for t in self.exp_avg_sqs]),
+                  (ctypes.c_float * 4)(*self.lrs), float(self.betas[0]), float(self.betas[1]),
+                  float(self.eps), int(self.step), _ptr(self.hyper), _ptr(self.skip), _stream())
+        self.applied = True
+
+
+class _OpacityTap(torch.autograd.Function):
+    """opacities[None] for one camera, whose backward also hands the incoming
+    dL/dopacities to the step's StepFusion (the geometry Adam in the
+    projection backward reads it; autograd runs this node's backward first:
+    it is created after the projection)."""
+
+    @staticmethod
+    def forward(ctx, opacities, fusion):
+        ctx.fusion = fusion
+        fusion.opac_tapped = True
+        return opacities.view(1, -1)
+
+    @staticmethod
+    def backward(ctx, g):
+        if g is not None:
+            g = _f32c(g)
+            ctx.fusion.v_opac_in = g
+            return g.view(-1), None
+        return None, None
 
 
 class ShAdamInBackward:
@@ -711,6 +798,8 @@ class _SHColors(torch.autograd.Function):
     @staticmethod
     def forward(ctx, sh_degree, means, viewmats, coeffs, coeffs_rest, radii, fusion=None):
         ctx.fusion = fusion
+        if fusion is not None and fusion.geom and ctx.needs_input_grad[1]:
+            fusion.expect_v_dirs = True  # this backward hands dL/dmeans to the fusion
         means, viewmats = _f32c(means), _f32c(viewmats)
         base, n_rows = _coeff_rows(coeffs)
         rest = None

@@ -101,13 +101,36 @@ def graph_node_census(g):
     return names, [tuple(int(x) for x in ms[4 * k:4 * k + 4]) for k in range(n_ms)]
 
 
-def check_kernel_nodes_only(g):
+def graph_memcpy_census(g):
+    """(destination, source, bytes, hipMemcpyKind) of every memcpy node of a
+    captured graph (-1 where unreadable)."""
+    out = (ctypes.c_int64 * (4 * 64))()
+    n = ctypes.c_int(0)
+    _lib.call("gsplat_hip_graph_memcpy_census", ctypes.c_void_p(g.raw_cuda_graph()),
+              ctypes.addressof(out), 64, ctypes.addressof(n))
+    return [tuple(int(x) for x in out[4 * k:4 * k + 4]) for k in range(min(n.value, 64))]
+
+
+HIP_MEMCPY_D2D = 3  # hipMemcpyDeviceToDevice
+
+
+def check_kernel_nodes_only(g, allow_d2d=False):
     """The captured step must hold kernel (and empty) nodes only: its replays
     faulted with the backward's hipMemsetAsync nodes in the graph (DESIGN
     §3.12), so a memset / copy that slips into the captured region (a
-    torch.zeros, a .copy_) fails here, at capture time."""
+    torch.zeros, a .copy_) fails here, at capture time.  `allow_d2d`: the
+    Gaussian-sharded step's RCCL exchanges may add device-to-device memcpy
+    nodes (RCCL copies a one-rank group's own block with them); any other
+    memcpy kind still fails."""
     names, memsets = graph_node_census(g)
-    other = {k: v for k, v in names.items() if k not in ("kernel", "empty")}
+    allowed = ("kernel", "empty")
+    if allow_d2d and names.get("memcpy"):
+        cps = graph_memcpy_census(g)
+        if cps and all(k == HIP_MEMCPY_D2D or k == 4 for _, _, _, k in cps):
+            # 4 = hipMemcpyDefault between device pointers (unified addressing)
+            allowed = allowed + ("memcpy",)
+        names = dict(names, memcpy_nodes=[(hex(d), hex(s_), b, k) for d, s_, b, k in cps])
+    other = {k: v for k, v in names.items() if k not in allowed and k != "memcpy_nodes"}
     if other and os.environ.get("GSPLAT_HIP_GRAPH_ALLOW_MEMSET", "0") == "1":
         # diagnosis only (tools/graph_diag.py memset): report and go on
         print(f"graph census {names}; memset nodes (address, row bytes, rows, element "
@@ -217,7 +240,13 @@ class GraphStep:
                 p["sh0"].data, p["shN"].data, o.exp_avg[i0], o.exp_avg_sq[i0], o.exp_avg[i1],
                 o.exp_avg_sq[i1], o.lrs[i0], o.lrs[i1], o.betas, o.eps, 1,
                 hyper=self.scal[sh_off:sh_off + 3], skip=self.status)
-        fusion = _wrapper.StepFusion(sh_adam=fa, geom=tr.geom_fuse) \
+        ga = None
+        if getattr(tr, "geom_in_proj", False):
+            # the geometry groups' factors are the launch groups' (_fill):
+            # (ss, ib) of means, scales, quats, opacities at [0, 8)
+            assert [names[i] for i in idx] == list(tr.GEOM), (idx, names)
+            ga = tr.geom_adam_in_backward(1, hyper=self.scal[:2 * len(idx)], skip=self.status)
+        fusion = _wrapper.StepFusion(sh_adam=fa, geom=tr.geom_fuse, geom_adam=ga) \
             if (fa is not None or tr.geom_fuse) else None
         # the first launch also fetches this step's input block (the ring slot)
         scales, opac = activate(p["scales"], p["opacities"], fusion,
@@ -244,7 +273,8 @@ class GraphStep:
             update_state_(tr.grad2d, tr.count, grad_box["g"], meta["radii"], meta["width"],
                           meta["height"], meta["n_cameras"], skip=self.status)
         skip = tr._sh_skip(fusion)
-        assert tuple(i for i in range(self.n_groups) if i not in skip) == tuple(idx), \
+        launched = tuple(i for i in range(self.n_groups) if i not in skip)
+        assert launched == tuple(idx) or (ga is not None and ga.applied and launched == ()), \
             (skip, idx)
         tr.opt.step(skip=skip, xform=tr._geom_xform(fusion), hyper=self.scal[:sh_off],
                     void=self.status)
@@ -318,7 +348,11 @@ class GraphStep:
             finally:
                 if gc_on:
                     gc.enable()
-            self.census = check_kernel_nodes_only(g)
+            # RCCL's exchanges (a Gaussian-sharded step on a real process
+            # group) may hold device-to-device copies
+            from . import distributed as gdist
+            self.census = check_kernel_nodes_only(
+                g, allow_d2d=self.gshard and gdist.EMULATION is None)
             g.instantiate()
             self.graph = g
             self.status.zero_()

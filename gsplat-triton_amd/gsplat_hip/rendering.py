@@ -156,18 +156,31 @@ def rasterization(
             viewmats, Ks = gdist.all_gather_tensor_list(world_size, [viewmats, Ks])
         C = len(viewmats)
 
-    proj = fully_fused_projection(
-        means, None, quats, scales, viewmats, Ks, width, height, eps2d=eps2d, packed=packed,
-        near_plane=near_plane, far_plane=far_plane, radius_clip=radius_clip,
-        sparse_grad=sparse_grad, calc_compensations=(rasterize_mode == "antialiased"),
-        camera_model=camera_model)
+    # a training step's geometry Adam inside the projection backward
+    # (StepFusion.geom_adam): one camera, dense, no pose gradient
+    geom_adam = (_fusion is not None and _fusion.geom_adam is not None and not packed
+                 and not distributed and C == 1 and rasterize_mode == "classic"
+                 and not viewmats.requires_grad)
+    if geom_adam:
+        proj = _wrapper._FullyFusedProjection.apply(
+            means, None, quats, scales, viewmats, Ks, width, height, eps2d, near_plane,
+            far_plane, radius_clip, False, camera_model, 256, _fusion)
+    else:
+        proj = fully_fused_projection(
+            means, None, quats, scales, viewmats, Ks, width, height, eps2d=eps2d, packed=packed,
+            near_plane=near_plane, far_plane=far_plane, radius_clip=radius_clip,
+            sparse_grad=sparse_grad, calc_compensations=(rasterize_mode == "antialiased"),
+            camera_model=camera_model)
     if packed:  # [nnz] pairs, all valid (gsplat/rendering.py:332-343)
         camera_ids, gaussian_ids, radii, means2d, depths, conics, compensations = proj
         opacities = opacities[gaussian_ids]
     else:
         radii, means2d, depths, conics, compensations = proj
         # [C, N]; for C == 1 a view, so backward is not a (copying) reduction
-        opacities = opacities[None] if C == 1 else opacities.repeat(C, 1)
+        if geom_adam:  # the same view, its gradient also handed to the fusion
+            opacities = _wrapper._OpacityTap.apply(opacities, _fusion)
+        else:
+            opacities = opacities[None] if C == 1 else opacities.repeat(C, 1)
         camera_ids, gaussian_ids = None, None
     if compensations is not None:
         opacities = opacities * compensations

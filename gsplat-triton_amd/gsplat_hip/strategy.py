@@ -37,11 +37,19 @@ class _Activate(torch.autograd.Function):
                       _ptr(log_scales), _ptr(logits), _ptr(scales), _ptr(opac), _stream())
         ctx.save_for_backward(scales, opac)
         ctx.fusion = fusion
+        if fusion is not None and fusion.geom_adam is not None:
+            fusion.opac_act = opac  # sigmoid(logits), for the geometry Adam's VJP
         return scales, opac
 
     @staticmethod
     def backward(ctx, v_scales, v_opac):
         scales, opac = ctx.saved_tensors
+        if ctx.fusion is not None and ctx.fusion.geom_adam is not None \
+                and ctx.fusion.geom_adam.applied and not ctx.fusion.act_taken:
+            # the projection backward already ran the geometry Adam with these
+            # gradients (v_scales never left it; v_opac came through the tap)
+            ctx.fusion.act_taken = True
+            return None, None, None, None
         # the trainer's geometry update applies the VJPs in-register
         # (adam_step_ex modes 2 / 3): hand over the incoming gradients
         if ctx.fusion is not None and ctx.fusion.take_activation_grads(

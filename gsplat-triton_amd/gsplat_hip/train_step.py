@@ -241,6 +241,14 @@ class Trainer:
         self.geom_fuse = (fused and not self.defer_sh
                           and (world_size == 1 or self.sharded or self.gshard)
                           and os.environ.get("GSPLAT_HIP_GEOM_FUSE", "1") != "0")
+        # one rank, 3DGS: the geometry groups' whole Adam step inside the
+        # projection backward (gsplat_hip_projection_bwd_adam), so their
+        # gradients never go through HBM; GSPLAT_HIP_GEOM_IN_PROJ=0 turns it
+        # off.  Not with the regularisers (extra terms on the raw parameters)
+        self.geom_in_proj = (self.geom_fuse and world_size == 1 and not self.gshard
+                             and not self.sharded and model == "3dgs"
+                             and self.opacity_reg == 0.0 and self.scale_reg == 0.0
+                             and os.environ.get("GSPLAT_HIP_GEOM_IN_PROJ", "1") != "0")
         # sharded optimizer: the SH group's collectives on a communicator of
         # their own (issued from a gradient hook during the backward), the
         # geometry's on the default group
@@ -492,6 +500,9 @@ class Trainer:
                 return loss
         ci = self.camera_index(it)
         self._sh_ready = 0
+        if self.max_steps:  # means ExponentialLR: this step's lr, before the
+            # backward that may run the geometry update (geom_in_proj)
+            self._set_means_lr(self.lrs[0] * (0.01 ** (1.0 / self.max_steps)) ** it)
         fusion = self._make_fusion()
         colors, alphas, meta = self.render(ci, self.sh_degree_at(it), fusion)
         if self.model == "3dgs":
@@ -520,8 +531,9 @@ class Trainer:
             self.allreduce_grads()
         if self.strategy is None or it < self.strategy.refine_stop_iter:
             self.update_state(meta)
-        if self.max_steps:  # means ExponentialLR, stepped after every optimizer step
-            self._set_means_lr(self.lrs[0] * (0.01 ** (1.0 / self.max_steps)) ** it)
+        # whether this step's geometry update ran inside the projection backward
+        self.geom_applied = bool(fusion is not None and fusion.geom_adam is not None
+                                 and fusion.geom_adam.applied)
         if self.sharded:
             self.opt.step(defer_gather=True, xform=self._geom_xform(fusion))
         else:
@@ -558,24 +570,50 @@ class Trainer:
                 o.betas, o.eps, o.step_count + 1)
         geom = getattr(self, "geom_fuse", False) and (isinstance(self.opt, FusedAdam) or
                                                       self.sharded)
+        ga = None
+        if getattr(self, "geom_in_proj", False) and isinstance(self.opt, FusedAdam):
+            ga = self.geom_adam_in_backward(self.opt.step_count + 1)
         if fa is None and not geom:
             return None
-        return _wrapper.StepFusion(sh_adam=fa, geom=geom)
+        return _wrapper.StepFusion(sh_adam=fa, geom=geom, geom_adam=ga)
+
+    GEOM = ("means", "scales", "quats", "opacities")
+
+    def geom_adam_in_backward(self, step, hyper=None, skip=None):
+        """The geometry groups' Adam step for the projection backward
+        (_wrapper.GeomAdamInBackward), in the trainer's group order."""
+        names = list(self.params)
+        o = self.opt
+        ix = [names.index(k) for k in self.GEOM]
+        return _wrapper.GeomAdamInBackward(
+            [self.params[k].data for k in self.GEOM], [o.exp_avg[i] for i in ix],
+            [o.exp_avg_sq[i] for i in ix], [o.lrs[i] for i in ix], o.betas, o.eps, step,
+            hyper=hyper, skip=skip)
 
     def _sh_skip(self, fusion):
-        """Indices of the SH groups when the SH backward already applied their
-        update.  Their .grad must then be empty: a loss term reaching sh0 /
-        shN by another path would have been left out of that update."""
-        if fusion is None or fusion.sh_adam is None or not fusion.sh_adam.applied:
+        """Indices of the groups whose update a backward already applied: the
+        SH groups (SH-colour backward) and the geometry groups (projection
+        backward).  Their .grad must then be empty: a loss term reaching them
+        by another path would have been left out of that update."""
+        if fusion is None:
             return ()
         names = list(self.params)
-        for k in ("sh0", "shN"):
-            if self.params[k].grad is not None:
-                raise RuntimeError(
-                    f"{k} received a gradient outside the SH-colour backward while its Adam "
-                    "step was fused into that backward; set GSPLAT_HIP_SH_ADAM_IN_BWD=0 for "
-                    "losses with extra terms on the SH coefficients")
-        return (names.index("sh0"), names.index("shN"))
+        done = []
+        if fusion.sh_adam is not None and fusion.sh_adam.applied:
+            done += [("sh0", "shN"), "GSPLAT_HIP_SH_ADAM_IN_BWD=0", "SH-colour"]
+        if fusion.geom_adam is not None and fusion.geom_adam.applied:
+            done += [self.GEOM, "GSPLAT_HIP_GEOM_IN_PROJ=0", "projection"]
+        out = []
+        for j in range(0, len(done), 3):
+            keys, env, who = done[j:j + 3]
+            for k in keys:
+                if self.params[k].grad is not None:
+                    raise RuntimeError(
+                        f"{k} received a gradient outside the {who} backward while its Adam "
+                        f"step was fused into that backward; set {env} for losses with extra "
+                        "terms on those parameters")
+            out += [names.index(k) for k in keys]
+        return tuple(sorted(out))
 
     def _geom_xform(self, fusion):
         """FusedAdam xform of the gradients the fusion took: means = its .grad +
@@ -587,6 +625,8 @@ class Trainer:
         and summed with it, which is autograd's accumulation exactly."""
         if fusion is None or not fusion.geom:
             return None
+        if fusion.geom_adam is not None and fusion.geom_adam.applied:
+            return None  # the projection backward ran the geometry update
         names = list(self.params)
         xf = {}
         if fusion.v_dirs is not None:

@@ -66,6 +66,25 @@ int gsplat_hip_projection_bwd(int C, int N, const float *means, const float *qua
                               float *v_means, float *v_quats, float *v_scales,
                               float *v_viewmats, void *stream);
 
+/* gsplat_hip_projection_bwd (C == 1) with the trainer's geometry Adam step
+ * fused in (ABI 31): no gradient is stored; params / exp_avgs / exp_avg_sqs
+ * [4] = means [N,3], log-scales [N,3], quats [N,4], logits [N] (the trainer's
+ * parameters, in its order; `scales` is exp(log-scales)) are updated in place with
+ * torch.optim.Adam from g_means = v_means + v_dirs, g_quats = v_quats,
+ * g_logscales = v_scales * scales, g_logits = v_opac * (1 - opac) * opac
+ * (v_dirs / v_opac may be NULL: zero).  lrs[4] and the 1-based step, or
+ * hyper_device f32[8] (lr_i / (1 - beta1^t), 1 / sqrt(1 - beta2^t) per group;
+ * a captured step); skip_device (may be NULL) non-zero updates nothing.
+ * Bit-identical to projection_bwd + activate_bwd + adam_step. */
+int gsplat_hip_projection_bwd_adam(
+    int N, const float *means, const float *quats, const float *scales, const float *viewmats,
+    const float *Ks, int width, int height, float eps2d, const int32_t *radii,
+    const float *conics, const float *v_means2d, const float *v_depths, const float *v_conics,
+    const float *v_dirs, const float *v_opac, const float *opac, float *const *params,
+    float *const *exp_avgs, float *const *exp_avg_sqs, const float *lrs, float beta1,
+    float beta2, float eps, int step, const float *hyper_device, const int32_t *skip_device,
+    void *stream);
+
 /* ---------------------------------------------------------------------------
  * Spherical harmonics, degree 0..4, RGB.
  * Replaces sh_to_color_fwd() (gsplat/triton_impl/sh_fwd.py:194-233) and the
@@ -426,6 +445,13 @@ int gsplat_hip_activate_fwd_fetch(int64_t n_scales, int64_t n_opacities,
  * memsets[4k .. 4k+3] = (destination, bytes per row, rows, element size). */
 int gsplat_hip_graph_node_census(void *graph, int64_t *counts, int64_t *memsets,
                                  int max_memsets);
+
+/* The memcpy nodes of a captured graph (ABI 31): for the first max_nodes,
+ * out[4k .. 4k+3] = (destination, source, bytes, hipMemcpyKind), -1 where
+ * unreadable; *n_out = the number of memcpy nodes.  (RCCL's one-rank
+ * all_to_all inside a captured Gaussian-sharded step copies the rank's own
+ * block with such nodes.) */
+int gsplat_hip_graph_memcpy_census(void *graph, int64_t *out, int max_nodes, int *n_out);
 
 /* DefaultStrategy._update_state for packed=False (gsplat/strategy/default.py:
  * 213-262): for every (c, g) with radii[c,g] > 0, in camera order,
