@@ -89,11 +89,14 @@ extern "C" int gsplat_hip_graph_memcpy_census(void *graph, int64_t *out, int max
       hipMemcpy3DParms p{};
       int64_t *o = out + 4 * k;
       o[0] = o[1] = o[2] = o[3] = -1;
-      if (hipGraphMemcpyNodeGetParams(nodes[i], &p) == hipSuccess) {
+      const hipError_t qe = hipGraphMemcpyNodeGetParams(nodes[i], &p);
+      if (qe == hipSuccess) {
         o[0] = (int64_t)reinterpret_cast<uintptr_t>(p.dstPtr.ptr);
         o[1] = (int64_t)reinterpret_cast<uintptr_t>(p.srcPtr.ptr);
         o[2] = (int64_t)p.extent.width * (int64_t)p.extent.height * (int64_t)p.extent.depth;
         o[3] = (int64_t)p.kind;
+      } else {
+        o[3] = -1000 - (int64_t)qe;  // unreadable: -1000 - the HIP error code
       }
     }
     ++k;

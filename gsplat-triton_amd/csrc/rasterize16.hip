@@ -57,8 +57,6 @@ typedef float f2v __attribute__((ext_vector_type(2)));
         : "v"(give.x), "v"(keep.x), "v"(give.y), "v"(keep.y));                             \
     return f2v{rx, ry};                                                                    \
   }
-GS_ADD_DPP2(add_row_mirror2, "row_mirror")
-GS_ADD_DPP2(add_row_half_mirror2, "row_half_mirror")
 GS_ADD_DPP2(add_quad_10322, "quad_perm:[1,0,3,2]")
 GS_ADD_DPP2(add_quad_23012, "quad_perm:[2,3,0,1]")
 #undef GS_ADD_DPP2
@@ -90,17 +88,16 @@ GS_INLINE f2v reduce_scatter2(const f2v *v, int lane) {
     w[i] = swap32_sum2(v[2 * i], 2 * i + 1 < N ? v[2 * i + 1] : f2v{0.f, 0.f});
 #pragma unroll
   for (int i = 0; i < N2; ++i) x[i] = swap16_sum2(w[2 * i], pick2(w, 2 * i + 1));
-  const bool b3 = lane & 8, b2 = lane & 4;
-  // DPP steps per component, one v_add_f32_dpp per value and step
+  (void)lane;
+  // lane bits 3 and 2: bank-masked DPP adds per component (wave_ops.h add_b3
+  // / add_b2), no per-lane selects
 #pragma unroll
   for (int i = 0; i < N3; ++i) {
     const f2v lo = x[2 * i], hi = pick2(x, 2 * i + 1);
-    const f2v keep = b3 ? hi : lo, give = b3 ? lo : hi;
-    y[i] = add_row_mirror2(keep, give);
+    y[i] = f2v{add_b3(lo.x, hi.x), add_b3(lo.y, hi.y)};
   }
   const f2v lo = y[0], hi = pick2(y, 1);
-  const f2v keep = b2 ? hi : lo, give = b2 ? lo : hi;
-  f2v z = add_row_half_mirror2(keep, give);
+  f2v z = f2v{add_b2(lo.x, hi.x), add_b2(lo.y, hi.y)};
   z = add_quad_10322(z, z);
   z = add_quad_23012(z, z);
   return z;

@@ -28,6 +28,34 @@ GS_INLINE float swap16_sum(float a, float b) {
   return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
+// Pair exchange of lane bit 3 / bit 2 with the reduction, selected by DPP
+// bank masks instead of per-lane selects (a bank is 4 lanes of a 16-lane
+// row).  add_b3(lo, hi): lanes with bit 3 clear (banks 0, 1) get
+// lo + lo[lane ^ 8], lanes with it set (banks 2, 3) hi + hi[lane ^ 8]
+// (row_ror:8 pairs exactly lane ^ 8).  add_b2: the same for bit 2 (banks 0,
+// 2 read lane + 4 = row_ror:12, banks 1, 3 lane - 4 = row_ror:4).  Two
+// v_add_f32_dpp per value; the select-based form took 2 v_cndmask_b32 more.
+// s_nop 1: the VALU-write -> DPP-read hazard needs two wait states, which the
+// compiler does not insert for inline asm.
+GS_INLINE float add_b3(float lo, float hi) {
+  float r;
+  asm("s_nop 1\n\t"
+      "v_add_f32_dpp %0, %1, %1 row_ror:8 row_mask:0xf bank_mask:0x3\n\t"
+      "v_add_f32_dpp %0, %2, %2 row_ror:8 row_mask:0xf bank_mask:0xc"
+      : "=&v"(r)
+      : "v"(lo), "v"(hi));
+  return r;
+}
+GS_INLINE float add_b2(float lo, float hi) {
+  float r;
+  asm("s_nop 1\n\t"
+      "v_add_f32_dpp %0, %1, %1 row_ror:12 row_mask:0xf bank_mask:0x5\n\t"
+      "v_add_f32_dpp %0, %2, %2 row_ror:4 row_mask:0xf bank_mask:0xa"
+      : "=&v"(r)
+      : "v"(lo), "v"(hi));
+  return r;
+}
+
 // Reduce-scatter of N <= 16 per-lane values over the wave: every lane ends
 // with the wave-wide total of field rs_field(lane).  Fields are paired
 // adjacently at each halving (lane bits 5, 4, 3, 2 choose the half), so an
@@ -48,14 +76,10 @@ GS_INLINE float reduce_scatter(const float *v, int lane) {
   for (int i = 0; i < N1; ++i) w[i] = swap32_sum(v[2 * i], 2 * i + 1 < N ? v[2 * i + 1] : 0.f);
 #pragma unroll
   for (int i = 0; i < N2; ++i) x[i] = swap16_sum(w[2 * i], pick(w, 2 * i + 1));
-  const bool b3 = lane & 8, b2 = lane & 4;
+  (void)lane;
 #pragma unroll
-  for (int i = 0; i < N3; ++i) {  // row mirror pairs lanes across bit 3
-    const float lo = x[2 * i], hi = pick(x, 2 * i + 1);
-    y[i] = (b3 ? hi : lo) + dpp<0x140>(b3 ? lo : hi);
-  }
-  const float lo = y[0], hi = pick(y, 1);  // half-row mirror: bit 2
-  float z = (b2 ? hi : lo) + dpp<0x141>(b2 ? lo : hi);
+  for (int i = 0; i < N3; ++i) y[i] = add_b3(x[2 * i], pick(x, 2 * i + 1));  // bit 3
+  float z = add_b2(y[0], pick(y, 1));  // bit 2
   z += dpp<0xB1>(z);  // quad lane ^ 1
   z += dpp<0x4E>(z);  // quad lane ^ 2
   return z;

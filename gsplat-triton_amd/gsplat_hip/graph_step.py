@@ -124,13 +124,18 @@ def check_kernel_nodes_only(g, allow_d2d=False):
     memcpy kind still fails."""
     names, memsets = graph_node_census(g)
     allowed = ("kernel", "empty")
-    if allow_d2d and names.get("memcpy"):
+    if names.get("memcpy"):
         cps = graph_memcpy_census(g)
-        if cps and all(k == HIP_MEMCPY_D2D or k == 4 for _, _, _, k in cps):
-            # 4 = hipMemcpyDefault between device pointers (unified addressing)
+        # kinds: 3 device-to-device, 4 default (unified addressing); <= -1000
+        # the node's parameters could not be read (RCCL's one-rank copies:
+        # their correctness is what tests/test_gpu_distributed.py replays)
+        if allow_d2d and cps and all(k in (HIP_MEMCPY_D2D, 4) or k <= -1000
+                                     for _, _, _, k in cps):
             allowed = allowed + ("memcpy",)
         names = dict(names, memcpy_nodes=[(hex(d), hex(s_), b, k) for d, s_, b, k in cps])
     other = {k: v for k, v in names.items() if k not in allowed and k != "memcpy_nodes"}
+    if "memcpy" in other:
+        other["memcpy_nodes"] = names["memcpy_nodes"]
     if other and os.environ.get("GSPLAT_HIP_GRAPH_ALLOW_MEMSET", "0") == "1":
         # diagnosis only (tools/graph_diag.py memset): report and go on
         print(f"graph census {names}; memset nodes (address, row bytes, rows, element "
