@@ -111,26 +111,23 @@ def graph_memcpy_census(g):
     return [tuple(int(x) for x in out[4 * k:4 * k + 4]) for k in range(min(n.value, 64))]
 
 
-HIP_MEMCPY_D2D = 3  # hipMemcpyDeviceToDevice
-
-
 def check_kernel_nodes_only(g, allow_d2d=False):
     """The captured step must hold kernel (and empty) nodes only: its replays
     faulted with the backward's hipMemsetAsync nodes in the graph (DESIGN
     §3.12), so a memset / copy that slips into the captured region (a
     torch.zeros, a .copy_) fails here, at capture time.  `allow_d2d`: the
-    Gaussian-sharded step's RCCL exchanges may add device-to-device memcpy
-    nodes (RCCL copies a one-rank group's own block with them); any other
-    memcpy kind still fails."""
+    Gaussian-sharded step's RCCL exchanges may add memcpy nodes (RCCL
+    copies a one-rank group's own block with them); memset nodes still fail."""
     names, memsets = graph_node_census(g)
     allowed = ("kernel", "empty")
     if names.get("memcpy"):
         cps = graph_memcpy_census(g)
-        # kinds: 3 device-to-device, 4 default (unified addressing); <= -1000
-        # the node's parameters could not be read (RCCL's one-rank copies:
-        # their correctness is what tests/test_gpu_distributed.py replays)
-        if allow_d2d and cps and all(k in (HIP_MEMCPY_D2D, 4) or k <= -1000
-                                     for _, _, _, k in cps):
+        # RCCL's copies: torch's bundled HIP runtime returns garbage from
+        # hipGraphMemcpyNodeGetParams for the 1-D memcpy nodes a captured
+        # hipMemcpyAsync makes (profiles/r5/rccl_capture.txt), so their kind
+        # cannot be checked here; their replay is checked against eager steps
+        # by tests/test_gpu_distributed.py (one-rank RCCL group)
+        if allow_d2d:
             allowed = allowed + ("memcpy",)
         names = dict(names, memcpy_nodes=[(hex(d), hex(s_), b, k) for d, s_, b, k in cps])
     other = {k: v for k, v in names.items() if k not in allowed and k != "memcpy_nodes"}
