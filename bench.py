@@ -323,7 +323,8 @@ def main():
                       "capture_ms": [round(1e3 * x, 1) for x in g.capture_s],
                       "isect_capacity": g.capacity, "max_isects": g.max_isects,
                       "host_issue_ms_per_step": 1e3 * g.host_s / max(g.replays, 1)}
-        tr._graph = None
+        g = None
+        tr.release_graph()  # (RCCL: before destroy_process_group, GraphStep.release)
         timers = _wrapper.enable_kernel_timers(True)
         n_t = min(args.steps, 10)
         for it in range(start + args.warmup + args.steps,
@@ -503,6 +504,10 @@ def main():
     if world > 1:
         dist.barrier()
     if dist.is_initialized():
+        tr.release_graph()
+        import gc
+        gc.collect()  # graphs that captured RCCL collectives, before the group goes
+        torch.cuda.synchronize()
         dist.destroy_process_group()
 
 

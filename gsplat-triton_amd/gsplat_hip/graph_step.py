@@ -508,3 +508,15 @@ class GraphStep:
         """Wait for every issued step and settle its overflow check."""
         self._drain()
         torch.cuda.synchronize(self.dev)
+
+    def release(self):
+        """Settle the issued steps and destroy the captured graph.  A graph
+        that captured RCCL collectives keeps their communicator's resources
+        referenced until it is destroyed, and destroy_process_group waits for
+        them (a test process hung there with the graph still alive): free the
+        graph before the process group goes."""
+        if self.graph is not None:
+            self.sync()
+            self.graph.reset()
+            self.graph = None
+        self.key = None

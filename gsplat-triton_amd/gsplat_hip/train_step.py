@@ -385,6 +385,14 @@ class Trainer:
         if self.sharded or getattr(self, "defer_sh", False):
             self.opt.wait()
 
+    def release_graph(self):
+        """Stop replaying: settle the captured step's replays, destroy its
+        graph (before destroy_process_group, see GraphStep.release) and issue
+        later steps eagerly."""
+        if getattr(self, "_graph", None) is not None:
+            self._graph.release()
+            self._graph = None
+
     def synced_params(self):
         self.sync()
         return self.params

@@ -27,6 +27,9 @@ def _pg():
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
     yield
+    import gc
+    gc.collect()  # graphs that captured RCCL collectives go before the group
+    torch.cuda.synchronize()
     dist.destroy_process_group()
 
 
@@ -150,6 +153,8 @@ def test_graph_gshard_rccl_step_tracks_eager():
         out[graph] = ({k: p.detach().clone() for k, p in tr.params.items()},
                       tr.count.clone(), tr.grad2d.clone(), tr.opt.step_count,
                       [float(x) for x in losses])
+        tr.release_graph()  # the captured RCCL exchanges, before the group goes
+        del tr
     a, b = out[False], out[True]
     assert a[3] == b[3] == 5
     torch.testing.assert_close(torch.tensor(b[4]), torch.tensor(a[4]), rtol=1e-4, atol=1e-6)

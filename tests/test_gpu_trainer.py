@@ -164,18 +164,24 @@ def _small_scene(n_cams=4, W=320, H=240):
 def test_trainer_tunes_split_divisor_from_termination():
     """Trainer._tune_split: before the first step, the forward's n_eff /
     n_isects (forward_termination_ratio, the bench's formula) picks the split
-    threshold's divisor: 1100 above 0.75, else 550; the library reports it
-    back.  The ratio is checked against a direct per-tile evaluation."""
+    threshold's divisor: 1100 above 0.75, else 550.  The divisor is the
+    trainer's own: inside its renders the library reports it, outside the
+    process-wide value is left as it was.  The ratio is checked against a
+    direct per-tile evaluation."""
     from gsplat_hip import _lib, _wrapper
     from gsplat_hip.train_step import Trainer
     means, rgbs, vm, K, W, H = _small_scene()
     try:
+        before = _lib.query("gsplat_hip_set_fwd_split_div", 777)  # a sentinel
         tr = Trainer(means, rgbs, vm, K, W, H, device="cuda", max_steps=100)
         tr.step(0)
         r = tr.term_ratio
         assert 0.0 < r <= 1.0
         assert tr.split_div == (1100 if r > 0.75 else 550)
-        assert _lib.query("gsplat_hip_set_fwd_split_div", 0) == tr.split_div
+        assert _lib.query("gsplat_hip_set_fwd_split_div", 777) == 777  # not leaked
+        with _wrapper.fwd_split_div(tr.split_div):
+            assert _lib.query("gsplat_hip_set_fwd_split_div", tr.split_div) == tr.split_div
+        assert _lib.query("gsplat_hip_set_fwd_split_div", before) == 777
         # direct: per tile, isects up to the tile's largest last id + 1
         colors, _, meta = tr.render(tr.camera_index(0), tr.sh_degree_at(0))
         r2 = _wrapper.forward_termination_ratio(colors, meta, W, H)
