@@ -239,8 +239,17 @@ struct GeomAdam {
 };
 
 template <int K>
-GS_INLINE void adam_row(float *P, float *M, float *V, const float *g, float ss, float ib,
+GS_INLINE void adam_row(float *P, float *M, float *V, const float *g_in, float ss, float ib,
                         const GeomAdam &ga) {
+  // the gradient as its own rounded value: no multiply of its VJP may be
+  // contracted into adam_update's subtraction (adam::step_kernel forms it
+  // through a runtime select, which keeps them apart there)
+  float g[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    g[k] = g_in[k];
+    asm volatile("" : "+v"(g[k]));
+  }
   float pp[K], mm[K], vv[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) {
@@ -401,6 +410,12 @@ __global__ void __launch_bounds__(256) projection_bwd_kernel(ProjBwdArgs a) {
     for (int j = 0; j < 3; ++j)
       vs[j] = Rq.m[0][j] * dRS.m[0][j] + Rq.m[1][j] * dRS.m[1][j] + Rq.m[2][j] * dRS.m[2][j];
   }
+  // the gradients are formed once, here, for every epilogue below: without
+  // this the compiler may duplicate their algebra into the branches and
+  // contract the multiply-adds differently per branch (the geometry-Adam
+  // epilogue then differs from the stored gradients in the last bit)
+  asm volatile("" : "+v"(vm[0]), "+v"(vm[1]), "+v"(vm[2]), "+v"(vq[0]), "+v"(vq[1]),
+               "+v"(vq[2]), "+v"(vq[3]), "+v"(vs[0]), "+v"(vs[1]), "+v"(vs[2]));
 
   if (a.sparse) {
     if (valid) {  // COO values, one row per packed entry
