@@ -189,31 +189,40 @@ def _trainer_scene(n_cams=3, W=320, H=240):
 
 @pytest.mark.parametrize("capacity", [None, 1000])
 def test_graph_trainer_tracks_eager(capacity):
+    """Six replayed steps against six eager ones.  The rasterizer backward's
+    float atomics make two eager runs differ in the last bits, and the
+    strategy statistic grad2d sums gradient norms that can cancel: its bar is
+    twice the spread of two eager runs (measured here), not a fixed rtol."""
     from gsplat_hip.train_step import Trainer
     means, rgbs, vm, K, W, H = _trainer_scene()
     out = {}
-    for graph in (False, True):
+    for run in ("eager", "eager2", "graph"):
+        graph = run == "graph"
         tr = Trainer(means, rgbs, vm, K, W, H, device=DEV, graph=graph, isect_capacity=capacity,
                      max_steps=100)
         assert (tr._graph is not None) == graph
         losses = [tr.step(it) for it in range(6)]
         tr.sync()
-        out[graph] = ({k: p.detach().clone() for k, p in tr.params.items()},
-                      [m.clone() for m in tr.opt.exp_avg], tr.opt.step_count,
-                      tr.grad2d.clone(), tr.count.clone(), [float(x) for x in losses])
+        out[run] = ({k: p.detach().clone() for k, p in tr.params.items()},
+                    [m.clone() for m in tr.opt.exp_avg], tr.opt.step_count,
+                    tr.grad2d.clone(), tr.count.clone(), [float(x) for x in losses])
         if graph:
             g = tr._graph
             assert g.replays >= 6
             if capacity is not None:  # started too small: grown and re-captured
                 assert g.recaptures >= 2 and g.capacity > g.max_isects > capacity
-    a, b = out[False], out[True]
+    a, a2, b = out["eager"], out["eager2"], out["graph"]
     assert a[2] == b[2] == 6
     for k in a[0]:
         torch.testing.assert_close(b[0][k], a[0][k], rtol=1e-3, atol=1e-5)
     for x, y in zip(a[1], b[1]):
         torch.testing.assert_close(y, x, rtol=1e-2, atol=1e-6)
     torch.testing.assert_close(b[4], a[4], rtol=0, atol=0)  # visibility counts: exact
-    torch.testing.assert_close(b[3], a[3], rtol=1e-3, atol=1e-7)
+    spread = float((a2[3] - a[3]).abs().max())
+    err = float((b[3] - a[3]).abs().max())
+    print(f"grad2d: graph-vs-eager {err:.3e}, eager run-to-run {spread:.3e}, "
+          f"max {float(a[3].abs().max()):.3e}")
+    assert err <= 2.0 * spread + 1e-7, (err, spread)
     # the returned per-step losses (the graph's loss ring slots): with a tiny
     # capacity too, where the voided steps' redo writes the returned slots
     torch.testing.assert_close(torch.tensor(b[5]), torch.tensor(a[5]), rtol=1e-4, atol=1e-6)

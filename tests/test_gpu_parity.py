@@ -772,3 +772,79 @@ def test_isect_tile_first_long_runs(n_pile):
         _wrapper.ISECT_SORT = old
     for a, b in zip(out["tile_first"], out["full"]):
         assert torch.equal(a, b)
+
+
+def test_full_size_invariants_m3():
+    """BASELINE configs[2] scale (M3: the garden crop tiled 7x7, 5,477,465
+    Gaussians, 1920x1080, SH degree 3, the record table above 64 MB):
+    size-independent properties -- isect keys sorted, offsets = lower_bound
+    of the tile keys, tiles_per_gauss summing to the isect count, the split
+    forward at the trainer's M3 divisor (1100) and at a forced 2048-isect
+    threshold equal to the unsplit forward up to chunk-product rounding, and
+    finite gradients through the split forward's chunk state."""
+    import os
+    import gsplat_hip
+    from gsplat_hip import _lib, _wrapper
+    from gsplat_hip.train_step import camera_pool, load_garden_scene
+    from test_gpu_parity import close_most
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    means, rgbs, vms, Ks, sw, sh_ = load_garden_scene(
+        os.path.join(root, "tests", "golden", "garden_scene.npz"), scene_grid=7)
+    N, W, H = means.shape[0], 1920, 1080
+    assert N == 5_477_465
+    vm, K = camera_pool(vms, Ks, sw, sh_, W, H, n=1)
+    g = torch.Generator().manual_seed(11)
+    quats = torch.nn.functional.normalize(torch.randn(N, 4, generator=g), dim=-1)
+    scales = torch.rand(N, 3, generator=g) * 0.02
+    opac = torch.rand(N, generator=g)
+    sh = torch.randn(N, 16, 3, generator=g) * 0.2
+    sh[:, 0] = (rgbs - 0.5) / 0.28209479177387814
+    ins = [t.to(DEV) for t in (means, quats, scales, opac, sh)]
+    vm, K = vm.to(DEV), K.to(DEV)
+
+    # isect invariants at this size
+    radii, m2, d, cn, _ = gsplat_hip.fully_fused_projection(ins[0], None, ins[1], ins[2], vm, K,
+                                                            W, H)
+    tw, th = math.ceil(W / 16), math.ceil(H / 16)
+    tpg, ids, fids = gsplat_hip.isect_tiles(m2, radii, d, 16, tw, th)
+    assert ids.numel() == int(tpg.sum()) > 3_000_000
+    assert torch.all(ids[1:] >= ids[:-1])
+    off = gsplat_hip.isect_offset_encode(ids, 1, tw, th)
+    tiles = torch.arange(tw * th, device=DEV, dtype=torch.int64)
+    tile_key = (ids >> 32) & ((1 << (tw * th - 1).bit_length()) - 1)
+    assert torch.equal(off.flatten().long(), torch.searchsorted(tile_key.contiguous(), tiles))
+    del ids, fids, tile_key
+
+    def render(split, div=None):
+        old = _lib.query("gsplat_hip_debug_set_fwd_split", split)
+        try:
+            leaves = [x.clone().requires_grad_(True) for x in ins]
+            with _wrapper.fwd_split_div(div):
+                rc, ra, meta = gsplat_hip.rasterization(*leaves[:4], leaves[4], vm, K, W, H,
+                                                        sh_degree=3, packed=False)
+            w = torch.rand(rc.shape, generator=torch.Generator(device=DEV).manual_seed(2),
+                           device=DEV)
+            (rc * w).sum().backward()
+            torch.cuda.synchronize()
+            return rc.detach(), ra.detach(), meta, [x.grad for x in leaves]
+        finally:
+            _lib.query("gsplat_hip_debug_set_fwd_split", old)
+
+    rc0, ra0, m0, g0 = render(0)            # unsplit
+    offs = m0["isect_offsets"].flatten().long()
+    n = int(m0["flatten_ids"].numel())
+    cnt = torch.diff(torch.cat([offs, torch.tensor([n], device=DEV)]))
+    thr = max(2048, n // 1100)
+    assert int((cnt > 2048).sum()) >= 4, "M3 has heavy tiles"
+    for split, div in ((-1, 1100), (2048, None)):  # adaptive at M3's divisor; forced
+        if split < 0 and int((cnt > thr).sum()) == 0:
+            continue
+        rc1, ra1, _, g1 = render(split, div)
+        close_most(rc1, rc0, 1e-5, 1e-5, "colors", max_frac=1e-3)
+        close_most(ra1, ra0, 1e-5, 1e-5, "alphas", max_frac=1e-3)
+        for gg in g1:
+            assert torch.isfinite(gg).all()
+        for a, b, name in zip(g1, g0, ["means", "quats", "scales", "opacities", "sh"]):
+            scale = max(1e-12, float(b.abs().max()))
+            close_most(a, b, 1e-3, 1e-4 * scale, name, max_frac=2e-3, rows=True,
+                       out_bound=0.05 * scale)

@@ -53,17 +53,32 @@ def _render(ins, W, H, records, mode="RGB"):
         _wrapper.RECORDS = saved
 
 
+NAMES = ["means", "quats", "scales", "opacities", "colors"]
+
+
+def _check_within_spread(g_ref, g_ref2, g_alt, what):
+    """The alternative layout's gradients differ from the reference layout's
+    by at most twice the reference's own run-to-run spread (two runs of the
+    same configuration: the backward's float atomics land in a different
+    order each time), per input, plus one ulp-scale floor (1e-7 of the
+    largest value) for a spread that happens to be zero."""
+    for a, a2, b, name in zip(g_ref, g_ref2, g_alt, NAMES):
+        scale = a.abs().max().item()
+        spread = (a2 - a).abs().max().item()
+        err = (b - a).abs().max().item()
+        print(f"{what} {name}: err {err:.3e} spread {spread:.3e} max {scale:.3e}")
+        assert err <= 2.0 * spread + 1e-7 * scale + 1e-12, (what, name, err, spread, scale)
+
+
 @pytest.mark.parametrize("mode", ["RGB", "RGB+D"])
 def test_records_match_plain_gathers(mode):
     ins, W, H = _scene()
     rc0, ra0, m0, g0 = _render(ins, W, H, False, mode)
+    _, _, _, g0b = _render(ins, W, H, False, mode)
     rc1, ra1, m1, g1 = _render(ins, W, H, True, mode)
     assert m0["flatten_ids"].numel() > 50000
     assert torch.equal(rc0, rc1) and torch.equal(ra0, ra1)
-    for a, b, name in zip(g0, g1, ["means", "quats", "scales", "opacities", "colors"]):
-        scale = b.abs().max().item()
-        err = (a - b).abs().max().item()
-        assert err <= 1e-4 * scale + 1e-9, (name, err, scale)
+    _check_within_spread(g0, g0b, g1, f"records {mode}")
 
 
 def _render_ranks(ins, W, H, ranks, **kw):
@@ -88,25 +103,22 @@ def test_rank_indexed_rows_match_gaussian_rows(capped):
     """Render records and gradient rows indexed by the visible Gaussians'
     depth rank (GSPLAT_HIP_RANKS, ABI 27): the same records reach the same
     arithmetic, so the forward is bit-identical and the backward agrees up to
-    its float atomics' order (the work items' order differs from run to run:
-    1.3e-5 of the largest scale gradient seen); meta["flatten_ids"] keeps the
-    Gaussian ids."""
+    its float atomics' order -- within twice the spread of two runs of the
+    Gaussian-indexed layout; meta["flatten_ids"] keeps the Gaussian ids."""
     ins, W, H = _scene()
     kw = {}
     if capped:
         kw = dict(_isect_capacity=400000,
                   _isect_status=torch.zeros(1, dtype=torch.int32, device=DEV))
     rc0, ra0, m0, g0 = _render_ranks(ins, W, H, False, **kw)
+    _, _, _, g0b = _render_ranks(ins, W, H, False, **kw)
     rc1, ra1, m1, g1 = _render_ranks(ins, W, H, True, **kw)
     # (capacity-sized arrays: the first counts[0] entries are the isects)
     n = int(m0["isect_counts"][0]) if capped else m0["flatten_ids"].numel()
     assert torch.equal(m0["flatten_ids"][:n], m1["flatten_ids"][:n])
     assert torch.equal(m0["isect_ids"][:n], m1["isect_ids"][:n])
     assert torch.equal(rc0, rc1) and torch.equal(ra0, ra1)
-    for a, b, name in zip(g0, g1, ["means", "quats", "scales", "opacities", "colors"]):
-        scale = b.abs().max().item()
-        err = (a - b).abs().max().item()
-        assert err <= 1e-4 * scale + 1e-9, (name, err, scale)
+    _check_within_spread(g0, g0b, g1, f"ranks capped={capped}")
     assert n > 50000
 
 
