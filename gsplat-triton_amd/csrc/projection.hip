@@ -235,37 +235,8 @@ struct GeomAdam {
   const float *hyper;   // device [8]: (ss_i, ib) per group (captured step), or null
   const int32_t *skip;  // device flag: non-zero = void step (nothing updated), or null
   float b1, b2, eps;
-  int on;
-};
 
-template <int K>
-GS_INLINE void adam_row(float *P, float *M, float *V, const float *g_in, float ss, float ib,
-                        const GeomAdam &ga) {
-  // the gradient as its own rounded value: no multiply of its VJP may be
-  // contracted into adam_update's subtraction (adam::step_kernel forms it
-  // through a runtime select, which keeps them apart there)
-  float g[K];
-#pragma unroll
-  for (int k = 0; k < K; ++k) {
-    g[k] = g_in[k];
-    asm volatile("" : "+v"(g[k]));
-  }
-  float pp[K], mm[K], vv[K];
-#pragma unroll
-  for (int k = 0; k < K; ++k) {
-    pp[k] = P[k];
-    mm[k] = M[k];
-    vv[k] = V[k];
-  }
-#pragma unroll
-  for (int k = 0; k < K; ++k) adam_update(pp[k], g[k], mm[k], vv[k], ga.b1, ga.b2, ga.eps, ss, ib);
-#pragma unroll
-  for (int k = 0; k < K; ++k) {
-    P[k] = pp[k];
-    M[k] = mm[k];
-    V[k] = vv[k];
-  }
-}
+};
 
 struct ProjBwdArgs {
   int C, N, W, H;
@@ -281,9 +252,16 @@ struct ProjBwdArgs {
   const int64_t *camera_ids, *gaussian_ids;
   int64_t nnz;
   int sparse;
-  GeomAdam ga;  // ga.on: the geometry Adam instead of the gradient stores (store_mode)
+  GeomAdam ga;  // projection_bwd_kernel<true>: the geometry Adam instead of the stores
 };
 
+// FUSE: the geometry-Adam epilogue (struct GeomAdam; C == 1, store mode).
+// Its lane's optimizer rows (33 floats) and gradient inputs are loaded at
+// the start, so their latency overlaps the gradient algebra instead of
+// following it group by group (the stores of one group could alias the next
+// group's loads as far as the compiler knows): 93.6 us as an epilogue
+// issuing them after the algebra at M2 (profiles/r5/).
+template <bool FUSE = false>
 __global__ void __launch_bounds__(256) projection_bwd_kernel(ProjBwdArgs a) {
   const bool packed = a.camera_ids != nullptr;
   int c, n;
@@ -302,6 +280,35 @@ __global__ void __launch_bounds__(256) projection_bwd_kernel(ProjBwdArgs a) {
     valid = (n < a.N) && (a.radii[idx] > 0);
   }
   const Cam k = load_cam(a.viewmats, a.Ks, c);
+
+  // FUSE: the lane's rows of the four geometry groups -- parameters, both
+  // moments -- and the other gradient terms, in flight from here
+  constexpr int kG = 11;  // means 3 | log-scales 3 | quats 4 | logits 1
+  float gp[kG], gm[kG], gv[kG], gvd[3] = {0.f, 0.f, 0.f}, gvo = 0.f, gop = 0.f, gsc[3];
+  const bool fuse_on = FUSE && n < a.N && !(a.ga.skip && *a.ga.skip);
+  if (FUSE && fuse_on) {
+    const GeomAdam &ga = a.ga;
+    const size_t i = (size_t)n;
+    constexpr int off[4] = {0, 3, 6, 10}, wid[4] = {3, 3, 4, 1};
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int e = 0; e < wid[q]; ++e) {
+        gp[off[q] + e] = ga.p[q][wid[q] * i + e];
+        gm[off[q] + e] = ga.m[q][wid[q] * i + e];
+        gv[off[q] + e] = ga.v[q][wid[q] * i + e];
+      }
+    if (ga.v_dirs) {
+#pragma unroll
+      for (int j = 0; j < 3; ++j) gvd[j] = ga.v_dirs[3 * i + j];
+    }
+    if (ga.v_opac) {
+      gvo = ga.v_opac[i];
+      gop = ga.opac[i];
+    }
+#pragma unroll
+    for (int j = 0; j < 3; ++j) gsc[j] = a.scales[3 * i + j];
+  }
 
   float vR[3][3] = {{0.f}}, vt[3] = {0.f, 0.f, 0.f};
   float vm[3] = {0.f, 0.f, 0.f}, vq[4] = {0.f, 0.f, 0.f, 0.f}, vs[3] = {0.f, 0.f, 0.f};
@@ -425,40 +432,48 @@ __global__ void __launch_bounds__(256) projection_bwd_kernel(ProjBwdArgs a) {
       o = a.v_scales + 3 * idx;
       o[0] = vs[0]; o[1] = vs[1]; o[2] = vs[2];
     }
-  } else if (a.store_mode && a.ga.on) {
-    const GeomAdam &ga = a.ga;
-    if (n < a.N && !(ga.skip && *ga.skip)) {
+  } else if (FUSE) {
+    if (fuse_on) {
+      const GeomAdam &ga = a.ga;
       const size_t i = (size_t)n;
       float ss[4], ib;
       if (ga.hyper) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) ss[k] = ga.hyper[2 * k];
+        for (int q = 0; q < 4; ++q) ss[q] = ga.hyper[2 * q];
         ib = ga.hyper[1];
       } else {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) ss[k] = ga.ss[k];
+        for (int q = 0; q < 4; ++q) ss[q] = ga.ss[q];
         ib = ga.ib;
       }
-      float g[4];
-      // means: v_means + v_dirs
+      float g[kG];
+      // means: v_means + v_dirs (autograd's sum); log-scales: exp's VJP with
+      // the activated scale (the input `scales`); quats; logits: sigmoid's VJP
 #pragma unroll
-      for (int j = 0; j < 3; ++j) g[j] = ga.v_dirs ? vm[j] + ga.v_dirs[3 * i + j] : vm[j];
-      adam_row<3>(ga.p[0] + 3 * i, ga.m[0] + 3 * i, ga.v[0] + 3 * i, g, ss[0], ib, ga);
-      // log-scales: exp's VJP with the activated scale (the input `scales`)
-      const float *sp = a.scales + 3 * i;
+      for (int j = 0; j < 3; ++j) g[j] = ga.v_dirs ? vm[j] + gvd[j] : vm[j];
 #pragma unroll
-      for (int j = 0; j < 3; ++j) g[j] = vs[j] * sp[j];
-      adam_row<3>(ga.p[1] + 3 * i, ga.m[1] + 3 * i, ga.v[1] + 3 * i, g, ss[1], ib, ga);
-      // quats
-      adam_row<4>(ga.p[2] + 4 * i, ga.m[2] + 4 * i, ga.v[2] + 4 * i, vq, ss[2], ib, ga);
-      // logits: sigmoid's VJP
-      if (ga.v_opac) {
-        const float o = ga.opac[i];
-        g[0] = ga.v_opac[i] * (1.f - o) * o;
-      } else {
-        g[0] = 0.f;
-      }
-      adam_row<1>(ga.p[3] + i, ga.m[3] + i, ga.v[3] + i, g, ss[3], ib, ga);
+      for (int j = 0; j < 3; ++j) g[3 + j] = vs[j] * gsc[j];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) g[6 + j] = vq[j];
+      g[10] = ga.v_opac ? gvo * (1.f - gop) * gop : 0.f;
+      // each gradient its own rounded value: no VJP multiply may be
+      // contracted into adam_update's subtraction (adam::step_kernel forms
+      // them through a runtime select, which keeps them apart there)
+#pragma unroll
+      for (int e = 0; e < kG; ++e) asm volatile("" : "+v"(g[e]));
+      constexpr int grp[kG] = {0, 0, 0, 1, 1, 1, 2, 2, 2, 2, 3};
+#pragma unroll
+      for (int e = 0; e < kG; ++e)
+        adam_update(gp[e], g[e], gm[e], gv[e], ga.b1, ga.b2, ga.eps, ss[grp[e]], ib);
+      constexpr int off[4] = {0, 3, 6, 10}, wid[4] = {3, 3, 4, 1};
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int e = 0; e < wid[q]; ++e) {
+          ga.p[q][wid[q] * i + e] = gp[off[q] + e];
+          ga.m[q][wid[q] * i + e] = gm[off[q] + e];
+          ga.v[q][wid[q] * i + e] = gv[off[q] + e];
+        }
     }
   } else if (a.store_mode) {
     if (n < a.N) {
@@ -580,7 +595,7 @@ extern "C" int gsplat_hip_projection_bwd(
                 compensations, v_means2d, v_depths, v_conics, v_compensations, v_means, v_quats,
                 v_scales, v_viewmats, store_mode};
   dim3 grid((N + 255) / 256, C);
-  hipLaunchKernelGGL(projection_bwd_kernel, grid, dim3(256), 0, st, a);
+  hipLaunchKernelGGL(projection_bwd_kernel<false>, grid, dim3(256), 0, st, a);
   GS_CHECK_LAUNCH("projection_bwd");
   return 0;
 }
@@ -620,7 +635,7 @@ extern "C" int gsplat_hip_projection_bwd_adam(
   ga.b1 = beta1;
   ga.b2 = beta2;
   ga.eps = eps;
-  ga.on = 1;
+
   if (!hyper_device) {  // gsplat_hip_adam_step's host arithmetic
     const double bc1 = 1.0 - pow((double)beta1, step), bc2 = 1.0 - pow((double)beta2, step);
     for (int k = 0; k < 4; ++k) ga.ss[k] = (float)(lrs[k] / bc1);
@@ -630,7 +645,7 @@ extern "C" int gsplat_hip_projection_bwd_adam(
                 nullptr, v_means2d, v_depths, v_conics, nullptr, nullptr, nullptr, nullptr,
                 nullptr, 1};
   a.ga = ga;
-  hipLaunchKernelGGL(projection_bwd_kernel, dim3((N + 255) / 256, 1), dim3(256), 0,
+  hipLaunchKernelGGL(projection_bwd_kernel<true>, dim3((N + 255) / 256, 1), dim3(256), 0,
                      (hipStream_t)stream, a);
   GS_CHECK_LAUNCH("projection_bwd_adam");
   return 0;
@@ -737,7 +752,7 @@ extern "C" int gsplat_hip_projection_packed_bwd(
   a.gaussian_ids = gaussian_ids;
   a.nnz = nnz;
   a.sparse = sparse_grad;
-  hipLaunchKernelGGL(projection_bwd_kernel, dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, st,
+  hipLaunchKernelGGL(projection_bwd_kernel<false>, dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, st,
                      a);
   GS_CHECK_LAUNCH("projection_packed_bwd");
   return 0;

@@ -58,16 +58,21 @@ NAMES = ["means", "quats", "scales", "opacities", "colors"]
 
 def _check_within_spread(g_ref, g_ref2, g_alt, what):
     """The alternative layout's gradients differ from the reference layout's
-    by at most twice the reference's own run-to-run spread (two runs of the
-    same configuration: the backward's float atomics land in a different
-    order each time), per input, plus one ulp-scale floor (1e-7 of the
-    largest value) for a spread that happens to be zero."""
+    by no more than the reference's own run-to-run noise: two runs of the same
+    configuration differ because the backward's float atomics land in a
+    different order each time.  Measured (profiles/r5/spread.txt): the
+    per-input maxima of that noise are a few ulps of the sums and heavy-tailed
+    -- layout-vs-layout over run-to-run ratios up to 5 in one run, every
+    difference below 2.1e-6 of the input's largest gradient -- so the bar is
+    4x the measured spread or 1e-5 of the largest value, whichever is larger
+    (10x tighter than round 4's fixed 1e-4; an indexing error moves whole
+    rows by O(1))."""
     for a, a2, b, name in zip(g_ref, g_ref2, g_alt, NAMES):
         scale = a.abs().max().item()
         spread = (a2 - a).abs().max().item()
         err = (b - a).abs().max().item()
         print(f"{what} {name}: err {err:.3e} spread {spread:.3e} max {scale:.3e}")
-        assert err <= 2.0 * spread + 1e-7 * scale + 1e-12, (what, name, err, spread, scale)
+        assert err <= max(4.0 * spread, 1e-5 * scale) + 1e-12, (what, name, err, spread, scale)
 
 
 @pytest.mark.parametrize("mode", ["RGB", "RGB+D"])
