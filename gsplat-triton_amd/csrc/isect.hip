@@ -555,8 +555,7 @@ size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 SortedLayout sorted_layout(int64_t nV, int64_t n, int key_bits) {
   (void)key_bits;
-  const size_t t1 = std::max(lsd_sort_scratch_bytes(nV), lsd_chain_scratch_bytes(nV)),
-               t2 = lsd_sort_scratch_bytes(n);
+  const size_t t1 = lsd_sort_scratch_bytes(nV), t2 = lsd_sort_scratch_bytes(n);
   SortedLayout L{};
   size_t o = 0;
   L.V = o; o = align256(o + 4 * (size_t)nV);
@@ -583,14 +582,6 @@ SortedLayout sorted_layout(int64_t nV, int64_t n, int key_bits) {
   L.offs = o; o = align256(o + 4 * (size_t)st::kMaxTiles);
   L.total = o;
   return L;
-}
-
-bool depth_chain() {
-  static const bool on = [] {
-    const char *e = getenv("GSPLAT_HIP_DEPTH_CHAIN");
-    return !(e && atoi(e) == 0);
-  }();
-  return on;
 }
 
 // The supertile expansion runs for at most kMaxKeys supertiles (with the
@@ -665,16 +656,10 @@ static int isect_write_sorted_impl(
   const int64_t *vis_prefix = reinterpret_cast<const int64_t *>(count_workspace) + nbG + 1;
   hipLaunchKernelGGL(isect_compact_kernel, dim3((unsigned)nbG), dim3(kIsectBlock), 0, st,
                      n_gaussians, tiles_per_gauss, depths, vis_prefix, V, dkey, cc);
-  // stable depth sort of the visible Gaussians (32 key bits): the chained
-  // 5-launch sort (lsd_sort_chain32; GSPLAT_HIP_DEPTH_CHAIN=0: the 12-launch
-  // hist / scan / scatter passes)
+  // stable depth sort of the visible Gaussians (32 key bits)
   const uint32_t *dks = dkeys;
-  if (depth_chain()) {
-    lsd_sort_chain32(dkey, V, dkeys, Vs, n_visible, tmp, st, cnt_dev ? cnt_dev + 1 : nullptr);
-    Vs = V;
-    dks = dkey;
-  } else if (lsd_sort_pairs(dkey, V, dkeys, Vs, n_visible, 0, 32, tmp, st, nullptr,
-                            cnt_dev ? cnt_dev + 1 : nullptr) == 0) {
+  if (lsd_sort_pairs(dkey, V, dkeys, Vs, n_visible, 0, 32, tmp, st, nullptr,
+                     cnt_dev ? cnt_dev + 1 : nullptr) == 0) {
     Vs = V;
     dks = dkey;
   }

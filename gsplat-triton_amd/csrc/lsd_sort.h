@@ -261,207 +261,7 @@ scatter_kernel(const uint32_t *__restrict__ kin, const int32_t *__restrict__ vin
   }
 }
 
-// ---- Chained 4-pass sort of 32-bit keys (the depth sort of the visible
-// Gaussians, ~0.3 M keys): 5 launches instead of 12.  Tiles of 4096 items;
-// per pass p a [256][ntp] histogram H[p] of the tiles' digits.
-//   chain_hist0  per tile: H[0] column of the first digit; zeroes its columns
-//                of H[1..3] (read only by later launches)
-//   chain_scatter<P>  per tile: the digit's global base = the sum of every
-//                tile's count of smaller digits + the earlier tiles' count of
-//                this digit, summed from H[P] itself (no scan launch: at most
-//                ntl / 4 16-B loads per digit thread, ntl = the tiles holding
-//                items); stable in-tile ranks and the LDS reorder of
-//                scatter_kernel; every item adds itself to H[P+1] at (its
-//                next digit, its output tile) -- the next pass's histogram
-//                without a histogram launch (about 16 adds per counter: the
-//                items of one digit run carry random higher digits)
-constexpr int CH_IPT = 16, CH_TILE = NT * CH_IPT;
-
-inline int64_t chain_tiles(int64_t n) { return (n + CH_TILE - 1) / CH_TILE; }
-inline int64_t chain_stride(int64_t n) { return (chain_tiles(n) + 3) / 4 * 4; }
-
-__global__ void __launch_bounds__(NT)
-chain_hist0_kernel(const uint32_t *__restrict__ keys, int64_t n, const int64_t *__restrict__ n_dev,
-                   uint32_t *__restrict__ H, int64_t ntp) {
-  __shared__ uint32_t h[RADIX];
-  if (n_dev) n = min(n, *n_dev);
-  const int64_t base = (int64_t)blockIdx.x * CH_TILE;
-  if (base >= n) return;
-  h[threadIdx.x] = 0;
-  __syncthreads();
-#pragma unroll
-  for (int e = 0; e < CH_IPT; ++e) {
-    const int64_t i = base + e * NT + threadIdx.x;
-    if (i < n) atomicAdd(&h[keys[i] & 255u], 1u);
-  }
-  __syncthreads();
-  const int64_t plane = (int64_t)RADIX * ntp;
-  const int64_t at = (int64_t)threadIdx.x * ntp + blockIdx.x;
-  H[at] = h[threadIdx.x];
-  H[plane + at] = 0u;
-  H[2 * plane + at] = 0u;
-  H[3 * plane + at] = 0u;
-}
-
-template <int P>
-__global__ void __launch_bounds__(NT)
-chain_scatter_kernel(const uint32_t *__restrict__ kin, const int32_t *__restrict__ vin,
-                     uint32_t *__restrict__ kout, int32_t *__restrict__ vout, int64_t n,
-                     const int64_t *__restrict__ n_dev, uint32_t *__restrict__ H, int64_t ntp) {
-  constexpr int NW = NT / 64, TILE = CH_TILE, SHIFT = 8 * P;
-  __shared__ uint32_t cnt[NW][RADIX];
-  __shared__ uint32_t gbase[RADIX];
-  __shared__ uint32_t wsum[NW];
-  __shared__ uint32_t kbuf[TILE];
-  __shared__ int32_t vbuf[TILE];
-  if (n_dev) n = min(n, *n_dev);
-  const int64_t base = (int64_t)blockIdx.x * TILE;
-  if (base >= n) return;
-  const int nvalid = (int)min<int64_t>((int64_t)TILE, n - base);
-  const int ntl = (int)((n + TILE - 1) / TILE);  // tiles holding items
-  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
-  const uint32_t *hp = H + (int64_t)P * RADIX * ntp;
-  // digit t: this tile's prefix (earlier tiles) and the whole pass's total,
-  // from its row of H[P] (16-B loads, ntp a multiple of 4)
-  uint32_t pre = 0, tot = 0;
-  {
-    const uint4 *row = reinterpret_cast<const uint4 *>(hp + (int64_t)t * ntp);
-    const int nq = (ntl + 3) >> 2, b = (int)blockIdx.x;
-    for (int q0 = 0; q0 < nq; q0 += 8) {
-      uint4 v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u)
-        v[u] = q0 + u < nq ? row[q0 + u] : make_uint4(0u, 0u, 0u, 0u);
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int c0 = 4 * (q0 + u);
-        const uint32_t x[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const uint32_t y = c0 + j < ntl ? x[j] : 0u;
-          tot += y;
-          pre += c0 + j < b ? y : 0u;
-        }
-      }
-    }
-  }
-#pragma unroll
-  for (int w = 0; w < NW; ++w) cnt[w][t] = 0;
-  uint32_t key[CH_IPT];
-  int32_t val[CH_IPT];
-#pragma unroll
-  for (int e = 0; e < CH_IPT; ++e) {
-    const int j = wid * 64 * CH_IPT + e * 64 + lane;
-    key[e] = j < nvalid ? kin[base + j] : 0u;
-    val[e] = j < nvalid ? vin[base + j] : 0;
-  }
-  __syncthreads();
-  uint32_t rank[CH_IPT];
-  const uint64_t lt = (1ull << lane) - 1ull;
-#pragma unroll
-  for (int e = 0; e < CH_IPT; ++e) {
-    const int j = wid * 64 * CH_IPT + e * 64 + lane;
-    const bool ok = j < nvalid;
-    const uint32_t dg = (key[e] >> SHIFT) & 255u;
-    uint64_t peers = __ballot(ok);
-#pragma unroll
-    for (int bt = 0; bt < 8; ++bt) {
-      const bool bit = (dg >> bt) & 1u;
-      const uint64_t bal = __ballot(bit);
-      peers &= bit ? bal : ~bal;
-    }
-    const uint32_t below = (uint32_t)__popcll(peers & lt);
-    const uint32_t old = ok ? cnt[wid][dg] : 0u;
-    // LDS ops of one wave complete in order: every peer read `old` above.
-    if (ok && below == 0) cnt[wid][dg] = old + (uint32_t)__popcll(peers);
-    rank[e] = old + below;
-  }
-  __syncthreads();
-  // digit t: wave offsets, tile-local start (exclusive scan of the tile's
-  // digit counts) and global start (exclusive scan of the totals)
-  uint32_t woff[NW], ttot = 0;
-#pragma unroll
-  for (int w = 0; w < NW; ++w) {
-    woff[w] = ttot;
-    ttot += cnt[w][t];
-  }
-  uint32_t x = ttot, g = tot;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t y = __shfl_up(x, o, 64), z = __shfl_up(g, o, 64);
-    if (lane >= o) {
-      x += y;
-      g += z;
-    }
-  }
-  if (lane == 63) wsum[wid] = x;
-  __syncthreads();
-  uint32_t lbefore = 0;
-#pragma unroll
-  for (int w = 0; w < NW; ++w) lbefore += w < wid ? wsum[w] : 0u;
-  const uint32_t lrun = lbefore + x - ttot;  // tile slot of digit t's first item
-  __syncthreads();
-  if (lane == 63) wsum[wid] = g;
-  __syncthreads();
-  uint32_t gbefore = 0;
-#pragma unroll
-  for (int w = 0; w < NW; ++w) gbefore += w < wid ? wsum[w] : 0u;
-  const uint32_t grun = gbefore + g - tot;  // global start of digit t
-  gbase[t] = grun + pre - lrun;
-#pragma unroll
-  for (int w = 0; w < NW; ++w) cnt[w][t] = lrun + woff[w];
-  __syncthreads();
-#pragma unroll
-  for (int e = 0; e < CH_IPT; ++e) {
-    const int j = wid * 64 * CH_IPT + e * 64 + lane;
-    if (j < nvalid) {
-      const uint32_t slot = cnt[wid][(key[e] >> SHIFT) & 255u] + rank[e];
-      kbuf[slot] = key[e];
-      vbuf[slot] = val[e];
-    }
-  }
-  __syncthreads();
-  uint32_t *hn = H + (int64_t)(P + 1) * RADIX * ntp;
-#pragma unroll
-  for (int e = 0; e < CH_IPT; ++e) {
-    const int s = e * NT + t;
-    if (s < nvalid) {
-      const uint32_t k = kbuf[s];
-      const uint32_t dst = gbase[(k >> SHIFT) & 255u] + (uint32_t)s;
-      kout[dst] = k;
-      vout[dst] = vbuf[s];
-      if (P < 3)  // the next pass's histogram: (next digit, output tile)
-        atomicAdd(&hn[(int64_t)((k >> (SHIFT + 8)) & 255u) * ntp + dst / TILE], 1u);
-    }
-  }
-}
-
 }  // namespace lsd
-
-// Scratch of lsd_sort_chain32: four [256][ntp] histograms.
-inline size_t lsd_chain_scratch_bytes(int64_t n) {
-  return 4 * (size_t)lsd::RADIX * (size_t)lsd::chain_stride(n) * 4;
-}
-
-// Stable sort of n (uint32 key, int32 value) pairs by all 32 key bits in 5
-// launches (see chain_scatter_kernel); (k0, v0) -> (k1, v1) -> ... four
-// passes, the result in (k0, v0).  Device count as lsd_sort_pairs.
-inline void lsd_sort_chain32(uint32_t *k0, int32_t *v0, uint32_t *k1, int32_t *v1, int64_t n,
-                             void *scratch, hipStream_t st, const int64_t *n_dev = nullptr) {
-  if (n <= 0) return;
-  const int64_t nt = lsd::chain_tiles(n), ntp = lsd::chain_stride(n);
-  uint32_t *H = reinterpret_cast<uint32_t *>(scratch);
-  hipLaunchKernelGGL(lsd::chain_hist0_kernel, dim3((unsigned)nt), dim3(lsd::NT), 0, st, k0, n,
-                     n_dev, H, ntp);
-  hipLaunchKernelGGL(lsd::chain_scatter_kernel<0>, dim3((unsigned)nt), dim3(lsd::NT), 0, st, k0,
-                     v0, k1, v1, n, n_dev, H, ntp);
-  hipLaunchKernelGGL(lsd::chain_scatter_kernel<1>, dim3((unsigned)nt), dim3(lsd::NT), 0, st, k1,
-                     v1, k0, v0, n, n_dev, H, ntp);
-  hipLaunchKernelGGL(lsd::chain_scatter_kernel<2>, dim3((unsigned)nt), dim3(lsd::NT), 0, st, k0,
-                     v0, k1, v1, n, n_dev, H, ntp);
-  hipLaunchKernelGGL(lsd::chain_scatter_kernel<3>, dim3((unsigned)nt), dim3(lsd::NT), 0, st, k1,
-                     v1, k0, v0, n, n_dev, H, ntp);
-}
 
 // Scratch for lsd_sort_pairs: hist rows + totals (sized for 11-bit digits).
 inline size_t lsd_sort_scratch_bytes(int64_t n) {
