@@ -64,6 +64,11 @@ def parse():
     ap.add_argument("--eager", action="store_true",
                     help="issue every launch from the host each step instead of replaying "
                          "the step captured as a HIP graph")
+    ap.add_argument("--graph", action="store_true",
+                    help="replay the captured step also for the densifying config (m3), whose "
+                         "default is eager: each refine re-captures, and the timed window "
+                         "centred on a refine ran 213.6 graph-replayed against 228.8 images/s "
+                         "eager (profiles/r4_final)")
     ap.add_argument("--dp-path", action="store_true",
                     help="replicated data parallelism instead of the default Gaussian "
                          "sharding at N>1 (every rank holds all Gaussians; sharded Adam, "
@@ -288,7 +293,8 @@ def main():
     tr = Trainer(means, rgbs, vm_pool, K_pool, W, H, sh_degree=3, device=dev, world_size=t_world,
                  rank=rank, model=model, sharded_optimizer=dp_path, gaussian_shard=gshard,
                  dp_emulate_world=args.dp_emulate or None,
-                 graph=not (args.eager or args.probe), **kw)
+                 graph=not (args.eager or args.probe
+                            or (args.config in DENSIFY and not args.graph)), **kw)
     N = means.shape[0]
 
     for it in range(start, start + args.warmup):
