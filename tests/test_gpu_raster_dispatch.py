@@ -272,13 +272,17 @@ def test_shared_gather_forward_matches(mode):
     noise)."""
     from gsplat_hip import _lib
     ins, W, H = _scene(N=60000, W=1280, H=720)
-    rc0, ra0, m0, g0 = _render(ins, W, H, True, mode)
-    _, _, _, g0b = _render(ins, W, H, True, mode)
-    old = _lib.query("gsplat_hip_debug_set_flags", 4)
+    split = _lib.query("gsplat_hip_debug_set_fwd_split", 0)  # whole tiles only
     try:
-        rc1, ra1, m1, g1 = _render(ins, W, H, True, mode)
+        rc0, ra0, m0, g0 = _render(ins, W, H, True, mode)
+        _, _, _, g0b = _render(ins, W, H, True, mode)
+        old = _lib.query("gsplat_hip_debug_set_flags", 4)
+        try:
+            rc1, ra1, m1, g1 = _render(ins, W, H, True, mode)
+        finally:
+            _lib.query("gsplat_hip_debug_set_flags", old)
     finally:
-        _lib.query("gsplat_hip_debug_set_flags", old)
+        _lib.query("gsplat_hip_debug_set_fwd_split", split)
     offs = m0["isect_offsets"].flatten().long()
     n = m0["flatten_ids"].numel()
     cnt = torch.diff(torch.cat([offs, torch.tensor([n], device=DEV)]))
