@@ -89,7 +89,8 @@ def parse():
 
 PMC_PASSES = (("FETCH_SIZE",), ("WRITE_SIZE",),
               ("SQ_INSTS_VALU", "SQ_WAIT_INST_ANY", "SQ_WAVE_CYCLES", "SQ_INSTS_LDS",
-               "SQ_LDS_BANK_CONFLICT", "SQ_INSTS_VMEM_WR"))
+               "SQ_LDS_BANK_CONFLICT", "SQ_INSTS_VMEM_WR", "SQ_INSTS_SALU"),
+              ("TCC_HIT_sum", "TCC_MISS_sum"))
 
 
 def pmc_traffic(config: str):
@@ -128,7 +129,7 @@ def pmc_traffic(config: str):
                            stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
         except (subprocess.SubprocessError, OSError):
             shutil.rmtree(d, ignore_errors=True)
-            if ctrs[0].startswith("SQ_"):
+            if ctrs[0].startswith(("SQ_", "TCC_HIT")):
                 continue  # optional pass
             return None
         vals = {}
@@ -172,6 +173,11 @@ def _valu_frac(pmc, launch_ms):
            "unit": "wave-instr/s", "frac": achieved / peak}
     if ctr.get("SQ_WAVE_CYCLES"):
         res["wait_inst_any_frac"] = ctr.get("SQ_WAIT_INST_ANY", 0.0) / ctr["SQ_WAVE_CYCLES"]
+    if ctr.get("SQ_INSTS_SALU"):
+        res["salu_per_valu"] = ctr["SQ_INSTS_SALU"] / insts
+    if ctr.get("TCC_HIT_sum") is not None and ctr.get("TCC_MISS_sum") is not None:
+        tot = ctr["TCC_HIT_sum"] + ctr["TCC_MISS_sum"]
+        res["l2_hit_rate"] = ctr["TCC_HIT_sum"] / tot if tot else None
     return res
 
 

@@ -539,17 +539,8 @@ GS_INLINE float chunk_product(const Args &a, const WaveGeom &geo, int64_t start,
 // One work item of the forward: SPLIT = chunk `item` of the split tiles'
 // list, else the whole tile `item` of the dispatch order (past the plan's
 // count of whole tiles: nothing).
-// SHG ("shared gather", whole tiles with render records only; debug flag
-// bit 2 / GSPLAT_HIP_FWD_SHARED=1): the workgroup gathers each batch of 64
-// records ONCE -- thread t loads 16 B (float4 t & 3 of record t >> 2) into a
-// double-buffered LDS batch, one barrier per batch -- instead of every wave
-// gathering the whole batch itself; each wave then reads its records from
-// LDS, culls and composites as usual.  The waves of a tile stay in lockstep
-// by batch (a finished wave keeps loading for the others until all four are
-// done or the range ends).  shg: [2][64][4] float4, sh_alive: [2][4].
-template <int D, bool SPLIT, bool SHG = false>
-GS_INLINE void fwd_item(const Args &a, float4 *st, int item, float4 *shg = nullptr,
-                        int *sh_alive = nullptr) {
+template <int D, bool SPLIT>
+GS_INLINE void fwd_item(const Args &a, float4 *st, int item) {
   using P = FwdPair<D>;
   constexpr int N4 = P::N4;
   const int lane = threadIdx.x & 63;
@@ -725,58 +716,6 @@ GS_INLINE void fwd_item(const Args &a, float4 *st, int item, float4 *shg = nullp
     // a chunk of a split tile writes the state of the boundaries inside it
     // and the colour it adds at its own start boundary
     const bool chunked = a.state && L > 0 && (end - start > L || kc > 0);
-    if constexpr (SHG && !SPLIT && D <= kRecMaxD) {
-      constexpr int NR4 = (6 + D + 3) / 4;  // float4s of a record that carry data
-      const int t = threadIdx.x, rec = t >> 2, q = t & 3;
-      const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-          const_cast<float *>(a.records), (short)0, (int)a.rec_bytes, 0x00020000);
-      auto gid = [&](int bb) -> int32_t { return a.flatten_ids[min(bb + rec, re - 1)]; };
-      auto ld = [&](int32_t g) -> float4 {
-        if (q >= NR4) return make_float4(0.f, 0.f, 0.f, 0.f);
-        const auto x = __builtin_amdgcn_raw_buffer_load_b128(
-            rsrc, (uint32_t)g * (uint32_t)(kRecFloats * 4) + 16u * (uint32_t)q, 0, 0);
-        return make_float4(__uint_as_float(x[0]), __uint_as_float(x[1]), __uint_as_float(x[2]),
-                           __uint_as_float(x[3]));
-      };
-      float4 cur = ld(gid(rs));
-      int32_t g_n = gid(rs + 64);
-      bool alive = __ballot(T > 0.f) != 0;
-      int par = 0;
-      for (int b0 = rs; b0 < re; b0 += 64, par ^= 1) {
-        // publish this batch (its slot's last readers finished before the
-        // previous barrier), put the next batch's loads in flight
-        float4 *sb = shg + par * 256;
-        if (q < NR4) sb[4 * rec + q] = cur;
-        const float4 nxt = ld(g_n);
-        g_n = gid(b0 + 128);
-        if (lane == 0) sh_alive[4 * par + wv] = alive ? 1 : 0;
-        __syncthreads();
-        if ((sh_alive[4 * par] | sh_alive[4 * par + 1] | sh_alive[4 * par + 2] |
-             sh_alive[4 * par + 3]) == 0)
-          break;  // every strip of the tile finished (the same decision in all waves)
-        if (alive) {
-          if (chunked && b0 > start && (b0 - start) % L == 0) save_state(b0);
-          Attr<D> A;
-          float v[4 * NR4];
-#pragma unroll
-          for (int i = 0; i < NR4; ++i) {
-            const float4 x = sb[4 * lane + i];
-            v[4 * i] = x.x; v[4 * i + 1] = x.y; v[4 * i + 2] = x.z; v[4 * i + 3] = x.w;
-          }
-          A.g = 0;
-          A.xy = make_float2(v[0], v[1]);
-          A.con = make_float3(v[2], v[3], v[4]);
-          A.op = v[5];
-#pragma unroll
-          for (int d = 0; d < D; ++d) A.col[d] = v[6 + d];
-          composite(stage(A, b0));
-          wave_sync_lds();
-          alive = !done;
-        }
-        cur = nxt;
-      }
-      if (chunked) close_chunk();
-    } else {
     int b0 = rs;
     // two attribute buffers in alternation: while batch b is composited from
     // one, the other receives batch b+1, and the ids of batch b+2 load
@@ -801,7 +740,6 @@ GS_INLINE void fwd_item(const Args &a, float4 *st, int item, float4 *shg = nullp
       if (done) break;
     }
     if (chunked) close_chunk();
-    }
   }
 
 #pragma unroll
@@ -879,17 +817,11 @@ GS_INLINE void fwd_item(const Args &a, float4 *st, int item, float4 *shg = nullp
 // first: they are the longest work) and the other tiles in one launch, so the
 // chunks overlap the whole tiles; else the whole tiles only (the split path's
 // code costs registers: 80 -> 95 VGPRs, 6 -> 5 waves per SIMD at D = 3).
-template <int D, bool SPLIT = false, bool SHG = false>
+template <int D, bool SPLIT = false>
 __global__ void __launch_bounds__(256)
 __attribute__((amdgpu_waves_per_eu(!SPLIT && D <= 3 ? 6 : 5))) fwd_kernel(Args a) {
   __shared__ float4 stage_all[4][32 * FwdPair<D>::N4];
   float4 *st = stage_all[threadIdx.x >> 6];
-  if constexpr (SHG && !SPLIT) {
-    __shared__ float4 shg[2 * 64 * 4];
-    __shared__ int sh_alive[2 * 4];
-    fwd_item<D, false, true>(a, st, (int)blockIdx.x, shg, sh_alive);
-    return;
-  }
   if constexpr (SPLIT) {
     const int nc = a.n_chunks[0];
     if ((int)blockIdx.x < nc)
@@ -1880,16 +1812,6 @@ static int dbg_flags() {
   }
   return g_dbg;
 }
-// Shared per-tile gather forward (fwd_item SHG): GSPLAT_HIP_FWD_SHARED=1, or
-// debug flag bit 2 (A/B and tests).
-static bool fwd_shared() {
-  static const bool env = [] {
-    const char *e = getenv("GSPLAT_HIP_FWD_SHARED");
-    return e && atoi(e) == 1;
-  }();
-  return env || (dbg_flags() & 4);
-}
-
 // State whose tile order gsplat_hip_rasterize_prepare already queued (so the
 // forward call does not launch the order kernel again); cleared by the
 // forward that consumes it.  Same host thread, same stream.
@@ -1932,10 +1854,7 @@ int r16_fwd(r16::Args a, const void *state, char *split_base, hipStream_t st) {
     GS_CHECK_LAUNCH("rasterize_fwd16_split");
     return 0;
   }
-  if (fwd_shared() && a.records && D <= r16::kRecMaxD)
-    hipLaunchKernelGGL((r16::fwd_kernel<D, false, true>), dim3(a.n_tiles), dim3(256), 0, st, a);
-  else
-    hipLaunchKernelGGL((r16::fwd_kernel<D>), dim3(a.n_tiles), dim3(256), 0, st, a);
+  hipLaunchKernelGGL((r16::fwd_kernel<D>), dim3(a.n_tiles), dim3(256), 0, st, a);
   GS_CHECK_LAUNCH("rasterize_fwd16");
   return 0;
 }

@@ -262,30 +262,3 @@ def test_split_forward_vs_oracle():
     close_most(ra, oa, 1e-4, 1e-4, "alphas", max_frac=1e-3)
     close_most(rc, oc, 1e-4, 1e-4, "colors", max_frac=1e-3)
 
-
-@pytest.mark.parametrize("mode", ["RGB", "RGB+D"])
-def test_shared_gather_forward_matches(mode):
-    """The forward whose workgroup gathers each batch of render records once
-    into LDS (debug flag bit 2, GSPLAT_HIP_FWD_SHARED=1) gives the per-wave
-    gather forward's images bit for bit, and the chunk state it leaves for
-    the backward gives the same gradients (up to the atomics' run-to-run
-    noise)."""
-    from gsplat_hip import _lib
-    ins, W, H = _scene(N=60000, W=1280, H=720)
-    split = _lib.query("gsplat_hip_debug_set_fwd_split", 0)  # whole tiles only
-    try:
-        rc0, ra0, m0, g0 = _render(ins, W, H, True, mode)
-        _, _, _, g0b = _render(ins, W, H, True, mode)
-        old = _lib.query("gsplat_hip_debug_set_flags", 4)
-        try:
-            rc1, ra1, m1, g1 = _render(ins, W, H, True, mode)
-        finally:
-            _lib.query("gsplat_hip_debug_set_flags", old)
-    finally:
-        _lib.query("gsplat_hip_debug_set_fwd_split", split)
-    offs = m0["isect_offsets"].flatten().long()
-    n = m0["flatten_ids"].numel()
-    cnt = torch.diff(torch.cat([offs, torch.tensor([n], device=DEV)]))
-    assert int((cnt > 256).sum()) > 0, "no chunked tile"
-    assert torch.equal(rc0, rc1) and torch.equal(ra0, ra1)
-    _check_within_spread(g0, g0b, g1, f"shared gather {mode}")
