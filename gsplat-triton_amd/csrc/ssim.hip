@@ -487,11 +487,15 @@ constexpr int kHA = 6, kHC = 4;  // adjacent outputs per work item in passes A, 
 // BR: map rows per work item of pass B (sliding window of K + BR - 1 rows).
 // Passes A and C1 are register-blocked: kHA / kHC adjacent outputs of one
 // row from one run of K + kHA - 1 / K + kHC - 1 LDS values.
-template <int C, int BR>
+// CPW: channels per workgroup (C / CPW workgroups per tile, channel groups of
+// a tile adjacent in the XCD-aware order so they share that XCD's L2).
+template <int C, int BR, int CPW = C>
 __global__ void __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(4)))
 fused_kernel(int B, int H, int W, const float *__restrict__ x, const float *__restrict__ y,
              const int64_t *__restrict__ y_index, float cs, float cl, float *__restrict__ grad,
              float *__restrict__ partials) {
+  static_assert(C % CPW == 0, "channel groups");
+  constexpr int CG = C / CPW;
   __shared__ __attribute__((aligned(16))) char lds[kFusedLds];
   __shared__ float red[2][kFThreads / 64];
   f2v(*s_xy)[SX] = reinterpret_cast<f2v(*)[SX]>(lds);
@@ -504,13 +508,15 @@ fused_kernel(int B, int H, int W, const float *__restrict__ x, const float *__re
   float(*g2)[SG] = reinterpret_cast<float(*)[SG]>(lds + kOffA + FM * SG * 8);
 
   const int Hm = H - 2 * R, Wm = W - 2 * R;
-  const int tx = (W + FT - 1) / FT, ty = (H + FT - 1) / FT, nt = tx * ty;
+  const int tx = (W + FT - 1) / FT, ty = (H + FT - 1) / FT, nt = tx * ty, ntc = nt * CG;
   // XCD-aware: workgroup L runs on XCD L % 8; each XCD takes a contiguous
-  // run of tiles so neighbouring windows' shared apron rows hit its L2
-  const int per = (nt + 7) / 8, L = blockIdx.x;
+  // run of (tile, channel group)s so neighbouring windows' shared apron rows
+  // (and a tile's other channel groups) hit its L2
+  const int per = (ntc + 7) / 8, L = blockIdx.x;
   const int b = L / (8 * per), q = L - b * 8 * per;
-  const int t = (q & 7) * per + (q >> 3);
-  if (b >= B || t >= nt) return;
+  const int tc = (q & 7) * per + (q >> 3);
+  if (b >= B || tc >= ntc) return;
+  const int t = tc / CG, cg = tc - t * CG;
   if (y_index) y += y_index[0] * ((int64_t)B * H * W * C);  // image y_index of a stack
   const int qi0 = (t / tx) * FT, qj0 = (t % tx) * FT;  // image tile origin
   const int ri0 = qi0 - 2 * R, rj0 = qj0 - 2 * R;       // window origin (image coords)
@@ -536,7 +542,7 @@ fused_kernel(int B, int H, int W, const float *__restrict__ x, const float *__re
   // backward vertical pass mapping: column gc, image rows 2 gr, 2 gr + 1
   const int gc = tid & 31, gr = tid >> 5;
 #pragma nounroll
-  for (int c = 0; c < C; ++c) {
+  for (int c = cg * CPW; c < cg * CPW + CPW; ++c) {
     // ---- stage channel c (+ its L1 over the tile's own pixels, window
     // rows / cols 2R .. 2R+31)
     load(c);
@@ -707,8 +713,8 @@ fused_kernel(int B, int H, int W, const float *__restrict__ x, const float *__re
       s += red[0][w];
       l += red[1][w];
     }
-    partials[2 * (b * nt + t)] = s;
-    partials[2 * (b * nt + t) + 1] = l;
+    partials[2 * ((int64_t)b * ntc + tc)] = s;
+    partials[2 * ((int64_t)b * ntc + tc) + 1] = l;
   }
 }
 
@@ -835,9 +841,17 @@ static int64_t fused_tiles(int H, int W) {
 }
 
 extern "C" int64_t gsplat_hip_l1_ssim_loss_fused_workspace_bytes(int B, int H, int W, int C) {
-  (void)C;
   if (H <= 10 || W <= 10) return 0;
-  return (int64_t)sizeof(float) * 2 * B * fused_tiles(H, W);
+  return (int64_t)sizeof(float) * 2 * B * fused_tiles(H, W) * (C == 3 ? 3 : 1);
+}
+
+// Channels per workgroup of the fused loss (GSPLAT_HIP_SSIM_CPW: 3 or 1)
+static int ssim_cpw() {
+  static const int v = [] {
+    const char *e = getenv("GSPLAT_HIP_SSIM_CPW");
+    return (e && atoi(e) == 1) ? 1 : 3;
+  }();
+  return v;
 }
 
 static int fused_fwd(int B, int H, int W, int C, const float *img1, const float *img2,
@@ -851,20 +865,23 @@ static int fused_fwd(int B, int H, int W, int C, const float *img1, const float 
   GS_REQUIRE(out != nullptr && grad_unit != nullptr, "l1_ssim_loss_fused_fwd: null output");
   hipStream_t st = (hipStream_t)stream;
   float *partials = reinterpret_cast<float *>(workspace);
-  const int64_t nt = fused_tiles(H, W), per = (nt + 7) / 8;
+  const int cg = C == 3 ? 3 / ssim_cpw() : 1;  // workgroups per tile
+  const int64_t nt = fused_tiles(H, W) * cg, per = (nt + 7) / 8;
   const dim3 grid((unsigned)(B * 8 * per));
   const float cs = -lam / n_map(B, H, W, C), cl = (1.f - lam) / n_img(B, H, W, C);
   static const int fv = [] {
     const char *e = getenv("GSPLAT_HIP_SSIM_FV");
     return e ? atoi(e) : 0;
   }();
-#define GS_FUSED(CC, BR)                                                                   \
-  hipLaunchKernelGGL((ssim::fused_kernel<CC, BR>), grid, dim3(ssim::kFThreads), 0, st, B, H, W, \
-                     img1, img2, img2_index, cs, cl, grad_unit, partials)
+#define GS_FUSED(CC, BR, CPW)                                                                \
+  hipLaunchKernelGGL((ssim::fused_kernel<CC, BR, CPW>), grid, dim3(ssim::kFThreads), 0, st, B, H, \
+                     W, img1, img2, img2_index, cs, cl, grad_unit, partials)
   if (C == 3) {
-    if (fv == 1) GS_FUSED(3, 2); else GS_FUSED(3, 4);
+    if (cg == 3) GS_FUSED(3, 4, 1);
+    else if (fv == 1) GS_FUSED(3, 2, 3);
+    else GS_FUSED(3, 4, 3);
   } else {
-    GS_FUSED(1, 2);
+    GS_FUSED(1, 2, 1);
   }
 #undef GS_FUSED
   hipLaunchKernelGGL(ssim::reduce_partials_kernel, dim3(1), dim3(1024), 0, st, (int)(B * nt),

@@ -36,6 +36,10 @@ class _Activate(torch.autograd.Function):
             _lib.call("gsplat_hip_activate_fwd", log_scales.numel(), logits.numel(),
                       _ptr(log_scales), _ptr(logits), _ptr(scales), _ptr(opac), _stream())
         ctx.save_for_backward(scales, opac)
+        # an output without a gradient arrives as None, not as a zero-filled
+        # tensor (the geometry Adam in the projection backward leaves scales'
+        # gradient None: a [N, 3] fill launch per step otherwise)
+        ctx.set_materialize_grads(False)
         ctx.fusion = fusion
         if fusion is not None and fusion.geom_adam is not None:
             fusion.opac_act = opac  # sigmoid(logits), for the geometry Adam's VJP
