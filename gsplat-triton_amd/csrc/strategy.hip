@@ -354,6 +354,13 @@ __global__ void __launch_bounds__(64) step_fetch_kernel(StepFetch f) {
   step_fetch_wave(f, threadIdx.x);
 }
 
+// The ranks' agreed overflow flag into the overflow field of the step's row
+// of the host-mapped count ring (gsplat_hip_status_to_ring).
+__global__ void __launch_bounds__(64) status_to_ring_kernel(const int32_t *status,
+                                                            int64_t *ring, const int64_t *slot) {
+  if (threadIdx.x == 0 && status[0] != 0) ring[4 * slot[0] + 2] = 1;
+}
+
 }  // namespace strat
 }  // namespace gs
 
@@ -393,6 +400,15 @@ extern "C" int gsplat_hip_step_fetch(const void *ring_device, int64_t slot_bytes
                            seq_device, reinterpret_cast<uint32_t *>(block_device)};
   hipLaunchKernelGGL(strat::step_fetch_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, f);
   GS_CHECK_LAUNCH("step_fetch");
+  return 0;
+}
+
+extern "C" int gsplat_hip_status_to_ring(const int32_t *status_device, void *ring_device,
+                                         const int64_t *slot_device, void *stream) {
+  GS_REQUIRE(status_device && ring_device && slot_device, "status_to_ring: null buffer");
+  hipLaunchKernelGGL(strat::status_to_ring_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream,
+                     status_device, reinterpret_cast<int64_t *>(ring_device), slot_device);
+  GS_CHECK_LAUNCH("status_to_ring");
   return 0;
 }
 

@@ -12,7 +12,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GSPLAT_HIP_LIB", os.path.join(_HERE, "libgsplat_hip.so"))
-ABI_VERSION = 31
+ABI_VERSION = 32
 
 _p = ctypes.c_void_p
 _i32 = ctypes.c_int
@@ -53,6 +53,7 @@ _SIGS = {
                                              _p]),
     "gsplat_hip_graph_node_census": (_i32, [_p, _p, _p, _i32]),
     "gsplat_hip_graph_memcpy_census": (_i32, [_p, _p, _i32, _p]),
+    "gsplat_hip_status_to_ring": (_i32, [_p, _p, _p, _p]),
     "gsplat_hip_projection_bwd_adam": (_i32, [_i32, _p, _p, _p, _p, _p, _i32, _i32, _f, _p, _p,
                                               _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _f, _f,
                                               _f, _i32, _p, _p, _p]),

@@ -13,6 +13,7 @@ of an exchange is the exchange with input and output splits swapped.
 """
 
 import math
+import os
 from contextlib import nullcontext as _nullcontext
 from typing import List, Optional, Tuple, Union
 
@@ -353,7 +354,9 @@ class ShardedAdam:
         self.world, self.rank = dist.get_world_size(), dist.get_rank()
         # a group of one rank exchanges nothing: the collectives are skipped
         # (the shard is the gradient itself, the rows are updated in place)
-        self.solo = self.world == 1
+        # (GSPLAT_HIP_DP_SOLO=0: the collectives on a one-rank group as well --
+        # the RCCL path of an N > 1 job, checked on one GPU by the tests)
+        self.solo = self.world == 1 and os.environ.get("GSPLAT_HIP_DP_SOLO", "1") != "0"
         if emulate_world:
             # measurement only (bench.py --dp-emulate): on ONE rank, shard the
             # rows as `emulate_world` ranks would and update rank 0's share --
@@ -450,14 +453,31 @@ class ShardedAdam:
         if gi not in self._early:
             self._early[gi] = self._issue_reduce(gi, self._grads(self.groups[gi], xform))
 
+    def launch_plan(self):
+        """The parameter indices of each Adam launch of step(), in launch
+        order: per group its shard rows, then its remainder rows.  A captured
+        step's device-side factors (`hyper`) are laid out in this order."""
+        plan = []
+        for grp in self.groups:
+            for sel in ([i for i in grp if self.layout[i][2]],
+                        [i for i in grp if self.layout[i][3] > self.layout[i][2]]):
+                if sel:
+                    plan.append(sel)
+        return plan
+
     @torch.no_grad()
-    def step(self, defer_gather=False, xform=None):
+    def step(self, defer_gather=False, xform=None, hyper=None, void=None):
         """defer_gather: leave the all-gathers in flight; the caller orders
         each parameter's next use after `wait([i])` (stream order only).
         xform: {index: (grad, aux, mode)} as FusedAdam.step (see the class
-        docstring for where each mode is applied)."""
+        docstring for where each mode is applied).  hyper / void: the
+        captured step's device-side Adam factors (adam_factors of every
+        launch of launch_plan(), in its order) and void-step flag; step_count
+        is then the caller's business (graph_step.GraphStep)."""
         self.wait()
-        self.step_count += 1
+        if hyper is None:
+            self.step_count += 1
+        self._hyper = None if hyper is None else [hyper, 0, void]
         side = self.side
         for gi, grp in enumerate(self.groups):
             if gi in self._early:
@@ -489,6 +509,15 @@ class ShardedAdam:
         if not defer_gather:
             self.wait()
 
+    def _dev(self, n):
+        """kwargs of the next launch's device-side factors (captured step)."""
+        h = getattr(self, "_hyper", None)
+        if h is None:
+            return {}
+        hyper, off, void = h
+        h[1] = off + 2 * n
+        return dict(hyper=hyper[off:off + 2 * n], skip=void)
+
     def _update_group(self, grp, flats, xform=None):
         def tx(i):  # (aux, mode) of a post-reduction transform, else (None, 0)
             if xform and i in xform and xform[i][2] in (2, 3):
@@ -504,7 +533,7 @@ class ShardedAdam:
                         [self.v[i] for i in idx], [self.lrs[i] for i in idx], self.betas,
                         self.eps, self.step_count,
                         aux=[None if a is None else self._shard(i, a) for i, a in zip(idx, aux)],
-                        modes=[tx(i)[1] for i in idx])
+                        modes=[tx(i)[1] for i in idx], **self._dev(len(idx)))
         tails = [i for i in grp if self.layout[i][3] > self.layout[i][2]]
         if tails:
             aux = [tx(i)[0] for i in tails]
@@ -514,7 +543,7 @@ class ShardedAdam:
                         [self.lrs[i] for i in tails], self.betas, self.eps, self.step_count,
                         aux=[None if a is None else a[self.layout[i][2]:]
                              for i, a in zip(tails, aux)],
-                        modes=[tx(i)[1] for i in tails])
+                        modes=[tx(i)[1] for i in tails], **self._dev(len(tails)))
 
     def zero_grad(self, set_to_none=True):
         for p in self.params:

@@ -31,12 +31,23 @@ What makes the step capturable:
   GPU, grows the capacity, re-captures and re-runs the void steps in order
   -- so the result is the eager step sequence's.
 
-Scope: the fused one-rank 3DGS trainer (the bench's M2 and, with its
-DefaultStrategy schedule, M3 configurations): the steps between two refines
-are replays of one capture; a refine (eager, after its step's replay has
-been checked) replaces the parameter tensors, and the next step re-captures
-with an isect capacity grown in proportion to the Gaussians.  Anything else
-runs eagerly (Trainer.step).
+Scope: the fused 3DGS trainer -- one rank (the bench's M2 and, with its
+DefaultStrategy schedule, M3 configurations), Gaussian-sharded (its pair
+exchanges inside the graph) and per-camera data parallel with the sharded
+optimizer (its reduce-scatters, Adam and all-gathers inside the graph): the
+steps between two refines are replays of one capture; a refine (eager,
+after its step's replay has been checked) replaces the parameter tensors,
+and the next step re-captures with an isect capacity grown in proportion to
+the Gaussians.  Anything else runs eagerly (Trainer.step).
+
+Several ranks: a rank whose isects overflow voids its step, and its
+gradients reach the other ranks' updates (the exchanges, the reductions),
+so the ranks agree on the flag inside the graph (a MAX all-reduce of it,
+issued after the forward and waited for before the backward, beside the
+loss kernels) and write the agreed flag into their count rings
+(gsplat_hip_status_to_ring); each rank checks its steps in issue order at
+fixed points (no opportunistic early check), so all ranks recover from the
+same step and re-capture together.
 """
 
 import collections
@@ -75,13 +86,20 @@ def graphable(tr) -> bool:
     # steps eagerly) or the device copies of the one-GPU emulation
     # (distributed.EMULATION, bench --gshard-emulate)
     from . import distributed as gdist
-    gshard_ok = getattr(tr, "gshard", False) and tr.world_size <= GraphStep.MAX_WORLD and (
-        gdist.EMULATION is not None or os.environ.get("GSPLAT_HIP_GRAPH_RCCL", "1") != "0")
-    return (tr.fused and not tr.sharded and tr.model == "3dgs"
-            and (gshard_ok or (tr.world_size == 1 and not getattr(tr, "gshard", False)))
+    rccl_ok = os.environ.get("GSPLAT_HIP_GRAPH_RCCL", "1") != "0"
+    gshard_ok = (getattr(tr, "gshard", False) and tr.world_size <= GraphStep.MAX_WORLD
+                 and isinstance(tr.opt, FusedAdam) and (gdist.EMULATION is not None or rccl_ok))
+    # per-camera data parallelism with the sharded optimizer (bench --dp-path):
+    # its reduce-scatters / all-gathers inside the graph (none on a one-rank
+    # group, distributed.ShardedAdam.solo)
+    dp_ok = (tr.sharded and isinstance(tr.opt, gdist.ShardedAdam)
+             and (tr.opt.solo or rccl_ok))
+    one = tr.world_size == 1 and not getattr(tr, "gshard", False) and not tr.sharded
+    return (tr.fused and tr.model == "3dgs"
+            and (gshard_ok or dp_ok or (one and isinstance(tr.opt, FusedAdam)))
             and not getattr(tr, "defer_sh", False)
             and (st is None or (not st.absgrad and tr.radii2d is None))
-            and isinstance(tr.opt, FusedAdam) and torch.device(tr.device).type == "cuda")
+            and torch.device(tr.device).type == "cuda")
 
 
 NODE_TYPES = ("kernel", "memcpy", "memset", "host", "graph", "empty", "wait_event",
@@ -169,7 +187,7 @@ class GraphStep:
     MAX_WORLD = 8  # cameras of a Gaussian-sharded step in the block
 
     def __init__(self, tr, capacity=None, headroom=1.25, lag=2):
-        assert graphable(tr), "GraphStep: a fused one-rank 3DGS trainer"
+        assert graphable(tr), "GraphStep: a fused 3DGS trainer (graph_step.graphable)"
         self.tr = tr
         dev = torch.device(tr.device)
         self.dev = dev
@@ -184,7 +202,13 @@ class GraphStep:
         # gsplat_hip_step_fetch)
         self.n_groups = len(tr.params)
         self.gshard = bool(getattr(tr, "gshard", False))
+        self.dp = bool(tr.sharded)  # per-camera data parallel, distributed.ShardedAdam
         self.W = tr.world_size if self.gshard else 1
+        # the ranks agree on the overflow flag inside the graph (module docstring)
+        import torch.distributed as dist
+        from . import distributed as gdist
+        self.vote = ((self.gshard or self.dp) and gdist.EMULATION is None
+                     and dist.is_available() and dist.is_initialized())
         self.blk = torch.zeros(self.SLOT, dtype=torch.uint8, device=dev)
         self.scal = self.blk[:256].view(torch.float32)
         self.cam = self.blk[256:264].view(torch.int64)
@@ -223,7 +247,11 @@ class GraphStep:
 
     # ------------------------------------------------------------------ body
     def _layout(self):
-        """(groups of the Adam launch, offset of the SH-Adam factors)."""
+        """(groups of the Adam launches in launch order, offset of the SH-Adam
+        factors): the device-side factors are laid out in that order."""
+        if self.dp:
+            idx = [i for sel in self.tr.opt.launch_plan() for i in sel]
+            return idx, 2 * len(idx)
         names = list(self.tr.params)
         sh = {names.index("sh0"), names.index("shN")}
         idx = [i for i in range(self.n_groups) if not (self.tr.sh_adam_in_bwd and i in sh)]
@@ -266,20 +294,34 @@ class GraphStep:
                 _isect_report=(self.ring_out.dev, self.slot), _isect_ids=False, **dkw)
         grad_box = {}
         meta["means2d"].register_hook(lambda g: grad_box.__setitem__("g", g))
+        vote = None
+        if self.vote:  # the ranks' overflow flags, agreed beside the loss kernels
+            import torch.distributed as dist
+            vote = dist.all_reduce(self.status, op=dist.ReduceOp.MAX, async_op=True)
         loss = tr._regularise(l1_ssim_loss(
             colors, tr.targets, tr.ssim_lambda, gt_index=self.cam,
             _out_ring=(self.loss_ring, self.seq) if self.ring_loss else None))
+        if vote is not None:
+            vote.wait()
+            _lib.call("gsplat_hip_status_to_ring", self.status.data_ptr(), self.ring_out.dev,
+                      self.slot.data_ptr(), _wrapper._stream())
         from . import losses as _losses
+        tr._sh_ready = 0  # the sharded optimizer's SH reduce-scatter hook
         torch.autograd.backward(loss, _losses.ONE_GRAD)
         if stats and "g" in grad_box:  # DefaultStrategy statistics (until refine_stop_iter)
             update_state_(tr.grad2d, tr.count, grad_box["g"], meta["radii"], meta["width"],
                           meta["height"], meta["n_cameras"], skip=self.status)
-        skip = tr._sh_skip(fusion)
-        launched = tuple(i for i in range(self.n_groups) if i not in skip)
-        assert launched == tuple(idx) or (ga is not None and ga.applied and launched == ()), \
-            (skip, idx)
-        tr.opt.step(skip=skip, xform=tr._geom_xform(fusion), hyper=self.scal[:sh_off],
-                    void=self.status)
+        if self.dp:  # reduce-scatter, Adam on this rank's rows, all-gather: all inside
+            assert not tr._sh_skip(fusion)
+            tr.opt.step(defer_gather=False, xform=tr._geom_xform(fusion),
+                        hyper=self.scal[:sh_off], void=self.status)
+        else:
+            skip = tr._sh_skip(fusion)
+            launched = tuple(i for i in range(self.n_groups) if i not in skip)
+            assert launched == tuple(idx) or (ga is not None and ga.applied and launched == ()), \
+                (skip, idx)
+            tr.opt.step(skip=skip, xform=tr._geom_xform(fusion), hyper=self.scal[:sh_off],
+                        void=self.status)
         tr.opt.zero_grad(set_to_none=True)
         return loss, meta["isect_counts"]
 
@@ -306,7 +348,7 @@ class GraphStep:
         ranks' replays hold matching RCCL exchanges, so all replay or none)."""
         import torch.distributed as dist
         from . import distributed as gdist
-        if not (self.gshard and self.tr.world_size > 1 and gdist.EMULATION is None
+        if not (self.vote and self.tr.world_size > 1 and gdist.EMULATION is None
                 and dist.is_initialized()):
             return ok
         t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=self.dev)
@@ -322,6 +364,8 @@ class GraphStep:
             self.capacity = self._probe_capacity(deg)
         timers = _wrapper._timers
         _wrapper._timers = None  # no timing events inside the graph
+        if self.dp:
+            tr.opt.wait()  # an eager step's deferred all-gathers
         torch.cuda.synchronize(self.dev)
         try:
             # warm-up on a side stream (torch's capture recipe) as a VOID
@@ -350,11 +394,9 @@ class GraphStep:
             finally:
                 if gc_on:
                     gc.enable()
-            # RCCL's exchanges (a Gaussian-sharded step on a real process
-            # group) may hold device-to-device copies
-            from . import distributed as gdist
-            self.census = check_kernel_nodes_only(
-                g, allow_d2d=self.gshard and gdist.EMULATION is None)
+            # RCCL's collectives (a Gaussian-sharded or data-parallel step on
+            # a real process group) may hold device-to-device copies
+            self.census = check_kernel_nodes_only(g, allow_d2d=self.vote)
             g.instantiate()
             self.graph = g
             self.status.zero_()
@@ -427,7 +469,12 @@ class GraphStep:
                                     int(math.ceil(self.capacity * key[1] / self.key[1])))
             self.graph = None  # the old capture's pool holds the old tensors
             self._capture(deg, stats)
-        self._check(block=len(self.pending) >= self.lag)
+        if not self.vote:
+            self._check(block=len(self.pending) >= self.lag)
+        elif len(self.pending) >= self.lag:
+            # several ranks: the oldest step exactly when `lag` are pending,
+            # on every rank alike (a recovery is collective)
+            self._check(block=True, one=True)
         return self._issue(it)
 
     def _issue(self, it, ret=None):
@@ -461,8 +508,9 @@ class GraphStep:
         self.host_s += time.perf_counter() - t0  # host work of the step, waits excluded
         return ret
 
-    def _check(self, block=False):
-        """Read the counts of finished steps; on an overflow, redo from there."""
+    def _check(self, block=False, one=False):
+        """Read the counts of finished steps; on an overflow, redo from there.
+        `one`: the oldest pending step only."""
         while self.pending:
             it, slot, ev = self.pending[0][:3]
             if not ev.query():
@@ -476,6 +524,8 @@ class GraphStep:
                 self._recover()
                 return
             self.pending.popleft()
+            if one:
+                return
 
     def _recover(self):
         """Every pending step from the first overflowed one was void (sticky
@@ -487,7 +537,9 @@ class GraphStep:
             self.max_isects = max(self.max_isects, int(self._out[slot][3]))
         self.pending.clear()
         tr.opt.step_count -= len(redo)  # their Adam steps did not happen
-        self.capacity = int(math.ceil(self.max_isects * self.headroom)) + 1
+        # (a rank voided by another's overflow keeps at least its capacity)
+        self.capacity = max(self.capacity or 0,
+                            int(math.ceil(self.max_isects * self.headroom)) + 1)
         self.status.zero_()
         # the redo steps take the voided steps' sequence numbers, so each
         # step's loss lands in the slot (or tensor) already returned for it

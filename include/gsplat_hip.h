@@ -31,7 +31,9 @@ const char *gsplat_hip_last_error(void);
  * gsplat_hip_sh_lazy_flush and the lazy arguments of the fused SH backward)
  * removed -- measured slower.
  * 30: gsplat_hip_l1_ssim_loss_fused_fwd_ring (the loss also into a device
- * ring slot chosen by a device step counter), gsplat_hip_set_fwd_split_div. */
+ * ring slot chosen by a device step counter), gsplat_hip_set_fwd_split_div.
+ * 31: gsplat_hip_projection_bwd_adam, gsplat_hip_graph_memcpy_census.
+ * 32: gsplat_hip_status_to_ring. */
 int gsplat_hip_abi_version(void);
 
 /* ---------------------------------------------------------------------------
@@ -452,6 +454,14 @@ int gsplat_hip_graph_node_census(void *graph, int64_t *counts, int64_t *memsets,
  * all_to_all inside a captured Gaussian-sharded step copies the rank's own
  * block with such nodes.) */
 int gsplat_hip_graph_memcpy_census(void *graph, int64_t *out, int max_nodes, int *n_out);
+
+/* The ranks' agreed overflow flag of a captured multi-rank step (ABI 32;
+ * gsplat_hip/graph_step.py, not a reference function): one-wave launch; when
+ * status_device[0] != 0, sets the overflow field (index 2) of row
+ * slot_device[0] of the host-mapped count ring ring_device (i64[4] rows, as
+ * gsplat_hip_isect_write_sorted_capped's counts_host_ring). */
+int gsplat_hip_status_to_ring(const int32_t *status_device, void *ring_device,
+                              const int64_t *slot_device, void *stream);
 
 /* DefaultStrategy._update_state for packed=False (gsplat/strategy/default.py:
  * 213-262): for every (c, g) with radii[c,g] > 0, in camera order,

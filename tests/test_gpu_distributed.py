@@ -185,3 +185,61 @@ def test_graph_capture_failure_falls_back_to_eager(monkeypatch):
     assert tr.opt.step_count == 3
     for x, y in zip(la, lb):
         assert abs(x - y) <= 1e-4 * abs(x), (la, lb)
+
+
+@pytest.mark.parametrize("solo,capacity", [("1", None), ("0", None), ("0", 1000)])
+def test_graph_dp_step_tracks_eager(monkeypatch, solo, capacity):
+    """Per-camera data parallelism with the sharded optimizer (bench
+    --dp-path) captured and replayed: on a one-rank group with
+    GSPLAT_HIP_DP_SOLO=0 the graph holds RCCL's reduce-scatters, all-gathers
+    and the ranks' overflow vote (the N > 1 path); with a tiny isect capacity
+    the voted overflow is read back from the count ring, the steps re-run and
+    the returned losses are the eager ones.  Six replayed steps against six
+    eager steps: losses, parameters, moments and strategy statistics, with
+    the split forward pinned off (test_graph_trainer_tracks_eager's reason)
+    and grad2d at the run-to-run spread of two eager runs."""
+    from gsplat_hip import _lib
+    from gsplat_hip.train_step import Trainer
+    from test_gpu_graph import _trainer_scene
+    monkeypatch.setenv("GSPLAT_HIP_DP_SOLO", solo)
+    means, rgbs, vm, K, W, H = _trainer_scene()
+    out = {}
+    old = _lib.query("gsplat_hip_debug_set_fwd_split", 0)
+    try:
+        for run in ("eager", "eager2", "graph"):
+            graph = run == "graph"
+            tr = Trainer(means, rgbs, vm, K, W, H, device=DEV, world_size=1, rank=0,
+                         sharded_optimizer=True, graph=graph, isect_capacity=capacity,
+                         max_steps=100)
+            assert tr.sharded and tr.opt.solo == (solo == "1")
+            assert (tr._graph is not None) == graph
+            losses = [tr.step(it) for it in range(6)]
+            tr.sync()
+            assert tr.graph_fallback is None, tr.graph_fallback
+            if graph:
+                g = tr._graph
+                assert g.replays >= 6 and g.vote
+                print("census", dict(g.census))
+                assert "memset" not in g.census, g.census
+                if capacity is not None:
+                    assert g.recaptures >= 2 and g.capacity > g.max_isects > capacity
+            st = tr.opt.full_state()
+            out[run] = ({k: p.detach().clone() for k, p in tr.params.items()},
+                        [m.clone() for m, _ in st], tr.opt.step_count, tr.grad2d.clone(),
+                        tr.count.clone(), [float(x) for x in losses])
+            tr.release_graph()
+            del tr
+    finally:
+        _lib.query("gsplat_hip_debug_set_fwd_split", old)
+    a, a2, b = out["eager"], out["eager2"], out["graph"]
+    assert a[2] == b[2] == 6
+    torch.testing.assert_close(torch.tensor(b[5]), torch.tensor(a[5]), rtol=1e-4, atol=1e-6)
+    assert len(set(b[5])) == 6, b[5]
+    for k in a[0]:
+        torch.testing.assert_close(b[0][k], a[0][k], rtol=1e-3, atol=1e-5)
+    for x, y in zip(a[1], b[1]):
+        torch.testing.assert_close(y, x, rtol=1e-2, atol=1e-6)
+    torch.testing.assert_close(b[4], a[4], rtol=0, atol=0)
+    spread = float((a2[3] - a[3]).abs().max())
+    err = float((b[3] - a[3]).abs().max())
+    assert err <= max(4.0 * spread, 1e-5 * float(a[3].abs().max())), (err, spread)
