@@ -322,7 +322,8 @@ struct Rec {
 
 struct RasterArgs {
   int C, W, H, ts, tw, th, n_tiles;
-  int64_t n_isects;
+  int64_t n_isects;       // isect count, or with n_dev the capacity of flatten_ids
+  const int64_t *n_dev;   // the isect count on the device (sync-free isect) or null
   const float *means2d, *ray_transforms, *colors, *opacities, *normals, *backgrounds;
   const uint8_t *masks;
   const int32_t *offsets, *flatten_ids;
@@ -357,7 +358,8 @@ struct Pix {
     const int64_t off = (int64_t)c * a.H * a.W;
     pid = off + (inside ? (int64_t)py * a.W + px : 0);
     start = a.offsets[tile];
-    end = (tile == a.n_tiles - 1) ? a.n_isects : (int64_t)a.offsets[tile + 1];
+    end = (tile == a.n_tiles - 1) ? (a.n_dev ? a.n_dev[0] : a.n_isects)
+                                  : (int64_t)a.offsets[tile + 1];
     // pixel-centre rectangle of the wave's rows (whole tile width)
     const int r0 = (64 * w) / a.ts, r1 = min(a.ts - 1, (64 * w + 63) / a.ts);
     x0 = tx * a.ts + 0.5f;
@@ -708,7 +710,8 @@ __global__ void __launch_bounds__(128) fwd2_kernel(RasterArgs a) {
   const int rem = tile - c * ntile;
   const int ty = rem / a.tw, tx = rem - ty * a.tw;
   const int64_t start = a.offsets[tile];
-  const int64_t end = (tile == a.n_tiles - 1) ? a.n_isects : (int64_t)a.offsets[tile + 1];
+  const int64_t end = (tile == a.n_tiles - 1) ? (a.n_dev ? a.n_dev[0] : a.n_isects)
+                                              : (int64_t)a.offsets[tile + 1];
   const float rx0 = tx * 16 + 0.5f, rx1 = rx0 + 15.f;
   const float ry0 = ty * 16 + 8 * w + 0.5f, ry1 = ry0 + 7.f;
   const float *bg = a.backgrounds ? a.backgrounds + (int64_t)c * D : nullptr;
@@ -1004,7 +1007,8 @@ __global__ void __launch_bounds__(128) bwd2_kernel(RasterArgs a) {
   const int rem = tile - c * ntile;
   const int ty = rem / a.tw, tx = rem - ty * a.tw;
   const int64_t start = a.offsets[tile];
-  const int64_t tend = (tile == a.n_tiles - 1) ? a.n_isects : (int64_t)a.offsets[tile + 1];
+  const int64_t tend = (tile == a.n_tiles - 1) ? (a.n_dev ? a.n_dev[0] : a.n_isects)
+                                               : (int64_t)a.offsets[tile + 1];
   const float rx0 = tx * 16 + 0.5f, rx1 = rx0 + 15.f;
   const float ry0 = ty * 16 + 8 * w + 0.5f, ry1 = ry0 + 7.f;
   PixState<D> ps[2];
@@ -1401,9 +1405,9 @@ extern "C" int gsplat_hip_rasterize_2dgs_fwd(
     const float *means2d, const float *ray_transforms, const float *colors,
     const float *opacities, const float *normals, const float *backgrounds,
     const uint8_t *masks, const int32_t *isect_offsets, int64_t n_isects,
-    const int32_t *flatten_ids, float *render_colors, float *render_alphas,
-    float *render_normals, float *render_distort, float *render_median, int32_t *last_ids,
-    int32_t *median_ids, void *stream) {
+    const int64_t *n_isects_device, const int32_t *flatten_ids, float *render_colors,
+    float *render_alphas, float *render_normals, float *render_distort, float *render_median,
+    int32_t *last_ids, int32_t *median_ids, void *stream) {
   if (int e = check_tiles(C, width, height, tile_size, tile_width, tile_height)) return e;
   GS_REQUIRE(channels_supported(D), "rasterize_2dgs_fwd: unsupported channel count %d", D);
   const int n_tiles = C * tile_width * tile_height;
@@ -1417,7 +1421,7 @@ extern "C" int gsplat_hip_rasterize_2dgs_fwd(
   GS_REQUIRE(((uintptr_t)means2d & 7) == 0, "rasterize_2dgs_fwd: means2d must be 8-B aligned");
   RasterArgs a{};
   a.C = C; a.W = width; a.H = height; a.ts = tile_size; a.tw = tile_width; a.th = tile_height;
-  a.n_tiles = n_tiles; a.n_isects = n_isects;
+  a.n_tiles = n_tiles; a.n_isects = n_isects; a.n_dev = n_isects_device;
   a.means2d = means2d; a.ray_transforms = ray_transforms; a.colors = colors;
   a.opacities = opacities; a.normals = normals; a.backgrounds = backgrounds; a.masks = masks;
   a.offsets = isect_offsets; a.flatten_ids = flatten_ids;
@@ -1452,7 +1456,8 @@ extern "C" int gsplat_hip_rasterize_2dgs_bwd(
     int64_t n_gaussians, const float *means2d, const float *ray_transforms, const float *colors,
     const float *opacities, const float *normals, const float *backgrounds,
     const uint8_t *masks, const int32_t *isect_offsets, int64_t n_isects,
-    const int32_t *flatten_ids, const float *render_colors, const float *render_alphas,
+    const int64_t *n_isects_device, const int32_t *flatten_ids, const float *render_colors,
+    const float *render_alphas,
     const int32_t *last_ids, const int32_t *median_ids, const float *v_render_colors,
     const float *v_render_alphas, const float *v_render_normals, const float *v_render_distort,
     const float *v_render_median, float *v_means2d, float *v_ray_transforms, float *v_colors,
@@ -1479,7 +1484,7 @@ extern "C" int gsplat_hip_rasterize_2dgs_bwd(
                "rasterize_2dgs_bwd: null pointer argument");
     RasterArgs a{};
     a.C = C; a.W = width; a.H = height; a.ts = tile_size; a.tw = tile_width;
-    a.th = tile_height; a.n_tiles = n_tiles; a.n_isects = n_isects;
+    a.th = tile_height; a.n_tiles = n_tiles; a.n_isects = n_isects; a.n_dev = n_isects_device;
     a.means2d = means2d; a.ray_transforms = ray_transforms; a.colors = colors;
     a.opacities = opacities; a.normals = normals; a.backgrounds = backgrounds; a.masks = masks;
     a.offsets = isect_offsets; a.flatten_ids = flatten_ids;

@@ -497,7 +497,7 @@ class _IsectCount:
 
     @torch.no_grad()
     def finish_capped(self, capacity: int, status: Optional[Tensor] = None, report=None,
-                      ids: bool = True):
+                      ids: bool = True, ranks: bool = True):
         """The sorted isects with NO host synchronisation (the one sync of
         isect_tiles, isect_tiles.py:101-102, removed so that a training step
         can be captured into a HIP graph): isect_ids / flatten_ids have
@@ -509,7 +509,8 @@ class _IsectCount:
         slot tensor): the counts also go to that ring row.  ids=False (a
         caller that only walks the depth ranks, the training step; needs
         will_rank(capped=True)): isect_ids / flatten_ids are not written and
-        come back None -- the rank ids and offsets are.  Returns
+        come back None -- the rank ids and offsets are.  ranks=False: no depth
+        ranks (a rasterizer that gathers by Gaussian id, the 2DGS one).  Returns
         (tiles_per_gauss, isect_ids, flatten_ids, counts)."""
         (means2d, radii, depths, camera_ids, C, N, G, tile_size, tile_width, tile_height,
          n_bit_tile, n_bit_cam, packed) = self.args
@@ -519,7 +520,7 @@ class _IsectCount:
         ws = torch.empty(max(int(_lib.query("gsplat_hip_isect_sorted_capped_workspace_bytes", G,
                                             capacity, key_bits)), 8),
                          dtype=torch.uint8, device=dev)
-        rk = self._rank_buffers(capacity, capped=True)
+        rk = self._rank_buffers(capacity, capped=True) if ranks else None
         ids = ids or rk is None
         isect_ids = torch.empty(capacity, dtype=torch.int64, device=dev) if ids else None
         flatten_ids = torch.empty(capacity, dtype=torch.int32, device=dev) if ids else None

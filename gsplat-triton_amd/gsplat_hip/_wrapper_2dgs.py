@@ -208,7 +208,8 @@ class _RasterizeToPixels2DGS(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, means2d, ray_transforms, colors, opacities, normals, densify, backgrounds,
-                masks, width, height, tile_size, isect_offsets, flatten_ids, absgrad, distloss):
+                masks, width, height, tile_size, isect_offsets, flatten_ids, absgrad, distloss,
+                n_dev=None):
         means2d, ray_transforms, colors, opacities, normals, backgrounds = (
             _f32c(x) for x in (means2d, ray_transforms, colors, opacities, normals, backgrounds))
         _dev_check(means2d, ray_transforms, colors, opacities, normals, isect_offsets, flatten_ids)
@@ -229,7 +230,7 @@ class _RasterizeToPixels2DGS(torch.autograd.Function):
             _lib.call("gsplat_hip_rasterize_2dgs_fwd", C, D, int(width), int(height),
                       int(tile_size), tw, th, _ptr(means2d), _ptr(ray_transforms), _ptr(colors),
                       _ptr(opacities), _ptr(normals), _ptr(backgrounds), _ptr(masks_u8),
-                      _ptr(isect_offsets), flatten_ids.numel(), _ptr(flatten_ids),
+                      _ptr(isect_offsets), flatten_ids.numel(), _ptr(n_dev), _ptr(flatten_ids),
                       _ptr(render_colors), _ptr(render_alphas), _ptr(render_normals),
                       _ptr(render_distort), _ptr(render_median), _ptr(last_ids),
                       _ptr(median_ids), _stream())
@@ -238,6 +239,7 @@ class _RasterizeToPixels2DGS(torch.autograd.Function):
                               render_alphas, last_ids, median_ids)
         ctx.width, ctx.height, ctx.tile_size = int(width), int(height), int(tile_size)
         ctx.absgrad, ctx.distloss = absgrad, distloss
+        ctx.n_dev = n_dev
         return render_colors, render_alphas, render_normals, render_distort, render_median
 
     @staticmethod
@@ -273,7 +275,7 @@ class _RasterizeToPixels2DGS(torch.autograd.Function):
             _lib.call("gsplat_hip_rasterize_2dgs_bwd", C, D, W, H, ctx.tile_size, tw, th, G,
                       _ptr(means2d), _ptr(ray_transforms), _ptr(colors), _ptr(opacities),
                       _ptr(normals), _ptr(backgrounds), _ptr(masks_u8), _ptr(isect_offsets),
-                      flatten_ids.numel(), _ptr(flatten_ids), _ptr(render_colors),
+                      flatten_ids.numel(), _ptr(ctx.n_dev), _ptr(flatten_ids), _ptr(render_colors),
                       _ptr(render_alphas), _ptr(last_ids), _ptr(median_ids),
                       _ptr(v_render_colors), _ptr(v_render_alphas), _ptr(v_render_normals),
                       _ptr(v_render_distort), _ptr(v_render_median), _ptr(v_means2d),
@@ -285,7 +287,7 @@ class _RasterizeToPixels2DGS(torch.autograd.Function):
         if ctx.needs_input_grad[6]:  # _wrapper.py:1953-1958
             v_backgrounds = (v_render_colors * (1.0 - render_alphas).float()).sum(dim=(1, 2))
         return (v_means2d, v_ray_transforms, v_colors, v_opacities, v_normals, v_densify,
-                v_backgrounds, None, None, None, None, None, None, None, None)
+                v_backgrounds, None, None, None, None, None, None, None, None, None)
 
 
 def rasterize_to_pixels_2dgs(
@@ -305,13 +307,16 @@ def rasterize_to_pixels_2dgs(
     packed: bool = False,
     absgrad: bool = False,
     distloss: bool = False,
+    _n_isects_device: Optional[Tensor] = None,
 ) -> Tuple[Tensor, Tensor, Tensor, Tensor, Tensor]:
     """Rasterizes surfels to pixels (gsplat/cuda/_wrapper.py:1595-1726).
 
     Returns render_colors [C,H,W,channels], render_alphas [C,H,W,1],
     render_normals [C,H,W,3], render_distort [C,H,W,1], render_median
     [C,H,W,1].  The depth used by the distortion and median terms is the last
-    colour channel, as in the reference."""
+    colour channel, as in the reference.  `_n_isects_device` (private): the
+    isect count on the device when flatten_ids is a capacity-sized array
+    (the sync-free isect of a captured training step)."""
     C = isect_offsets.size(0)
     device = means2d.device
     if packed:  # flatten_ids index the [nnz] rows directly (_wrapper.py:1628-1636)
@@ -362,7 +367,7 @@ def rasterize_to_pixels_2dgs(
             means2d.contiguous(), ray_transforms.contiguous(), colors.contiguous(),
             opacities.contiguous(), normals.contiguous(), densify.contiguous(), backgrounds,
             masks, image_width, image_height, tile_size, isect_offsets.contiguous(),
-            flatten_ids.contiguous(), absgrad, distloss)
+            flatten_ids.contiguous(), absgrad, distloss, _n_isects_device)
     if padded_channels > 0:
         render_colors = torch.cat([render_colors[..., : -padded_channels - 1],
                                    render_colors[..., -1:]], dim=-1)

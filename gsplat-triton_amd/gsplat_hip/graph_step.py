@@ -62,7 +62,7 @@ import torch
 
 from . import _lib, _wrapper
 from .losses import FusedAdam, adam_factors, l1_ssim_loss
-from .rendering import rasterization
+from .rendering import rasterization, rasterization_2dgs
 from .strategy import activate, update_state_
 
 
@@ -95,7 +95,8 @@ def graphable(tr) -> bool:
     dp_ok = (tr.sharded and isinstance(tr.opt, gdist.ShardedAdam)
              and (tr.opt.solo or rccl_ok))
     one = tr.world_size == 1 and not getattr(tr, "gshard", False) and not tr.sharded
-    return (tr.fused and tr.model == "3dgs"
+    # one rank: 3DGS or 2DGS (surfels, rasterization_2dgs with the sync-free isect)
+    return (tr.fused and (tr.model == "3dgs" or (one and tr.model == "2dgs"))
             and (gshard_ok or dp_ok or (one and isinstance(tr.opt, FusedAdam)))
             and not getattr(tr, "defer_sh", False)
             and (st is None or (not st.absgrad and tr.radii2d is None))
@@ -198,7 +199,8 @@ class GraphStep:
         # the Adam factors, i64 at byte 256 the rank's camera index, f32
         # viewmats [W][16] at byte 512 and Ks [W][9] at
         # byte 1024 (W = the world's cameras: 1, or the Gaussian-sharded job's
-        # ranks), i64 at SLOT - 8 the ring slot (written by
+        # ranks), the camera-to-world matrix f32 [16] at byte 1536 (2DGS: its
+        # normals), i64 at SLOT - 8 the ring slot (written by
         # gsplat_hip_step_fetch)
         self.n_groups = len(tr.params)
         self.gshard = bool(getattr(tr, "gshard", False))
@@ -216,6 +218,7 @@ class GraphStep:
         self.K_w = self.blk[1024:1024 + 36 * self.W].view(torch.float32).view(self.W, 3, 3)
         r = tr.rank if self.gshard else 0
         self.vm, self.K = self.vm_w[r:r + 1], self.K_w[r:r + 1]  # this rank's camera
+        self.c2w = self.blk[1536:1536 + 64].view(torch.float32).view(1, 4, 4)
         self.slot = self.blk[self.SLOT - 8:].view(torch.int64)
         self.seq = torch.zeros(1, dtype=torch.int64, device=dev)  # steps fetched
         # the step's loss, written by the loss's own reduction launch into
@@ -285,15 +288,26 @@ class GraphStep:
         if self.gshard:  # the world's cameras from the block, shard sizes fixed per capture
             dkw = dict(distributed=True, _world_cameras=(self.vm_w, self.K_w),
                        _world_counts=tr._n_world)
-        with _wrapper.fwd_split_div(getattr(tr, "split_div", None)):
-            colors, _, meta = rasterization(
+        grad_box = {}
+        if tr.model == "2dgs":  # Trainer.render's call, with the sync-free isect
+            rc, _, _, _, _, _, meta = rasterization_2dgs(
                 p["means"], p["quats"], scales, opac, (p["sh0"], p["shN"]), self.vm, self.K,
                 tr.width, tr.height, sh_degree=deg, packed=False, near_plane=0.01,
-                far_plane=1e10, radius_clip=0.0, rasterize_mode="classic", _fusion=fusion,
+                far_plane=1e10, render_mode="RGB+D", _fusion=fusion,
                 _isect_capacity=self.capacity, _isect_status=self.status,
-                _isect_report=(self.ring_out.dev, self.slot), _isect_ids=False, **dkw)
-        grad_box = {}
-        meta["means2d"].register_hook(lambda g: grad_box.__setitem__("g", g))
+                _isect_report=(self.ring_out.dev, self.slot), _camtoworlds=self.c2w)
+            colors = rc[..., :3]
+            # the densification input (a leaf): its gradient, as .grad would hold it
+            meta["gradient_2dgs"].register_hook(lambda g: grad_box.__setitem__("g", g))
+        else:
+            with _wrapper.fwd_split_div(getattr(tr, "split_div", None)):
+                colors, _, meta = rasterization(
+                    p["means"], p["quats"], scales, opac, (p["sh0"], p["shN"]), self.vm, self.K,
+                    tr.width, tr.height, sh_degree=deg, packed=False, near_plane=0.01,
+                    far_plane=1e10, radius_clip=0.0, rasterize_mode="classic", _fusion=fusion,
+                    _isect_capacity=self.capacity, _isect_status=self.status,
+                    _isect_report=(self.ring_out.dev, self.slot), _isect_ids=False, **dkw)
+            meta["means2d"].register_hook(lambda g: grad_box.__setitem__("g", g))
         vote = None
         if self.vote:  # the ranks' overflow flags, agreed beside the loss kernels
             import torch.distributed as dist
@@ -441,6 +455,9 @@ class GraphStep:
         b[512:512 + 64 * self.W].view(np.float32)[:] = self._vm_host[world_ci].reshape(-1)
         b[1024:1024 + 36 * self.W].view(np.float32)[:] = self._K_host[world_ci].reshape(-1)
         b[256:264].view(np.int64)[0] = ci
+        if tr.model == "2dgs":  # rasterization_2dgs's torch.linalg.inv(viewmats), on the host
+            b[1536:1536 + 64].view(np.float32)[:] = np.linalg.inv(
+                self._vm_host[ci].astype(np.float64)).astype(np.float32).reshape(-1)
         if tr.max_steps:
             tr._set_means_lr(lrs[0])
 

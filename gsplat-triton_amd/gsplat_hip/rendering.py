@@ -475,13 +475,20 @@ def rasterization_2dgs(
     distloss: bool = False,
     depth_mode: str = "expected",
     _fusion=None,
+    _isect_capacity: Optional[int] = None,
+    _isect_status: Optional[Tensor] = None,
+    _isect_report=None,
+    _camtoworlds: Optional[Tensor] = None,
 ):
     """Rasterize N surfels (2DGS) to C images (gsplat/rendering.py:1018-1339).
 
     Returns (render_colors, render_alphas, render_normals,
     render_normals_from_depth, render_distort, render_median, meta), with
     meta["gradient_2dgs"] the densification input whose .grad the 2DGS
-    strategy reads."""
+    strategy reads.  Private (the captured training step, graph_step): the
+    sync-free isect as rasterization()'s `_isect_capacity` / `_isect_status`
+    / `_isect_report` (meta["isect_counts"]); `_camtoworlds` [C,4,4] the
+    inverse viewmats (torch.linalg.inv reads its error flag on the host)."""
     from ._wrapper_2dgs import fully_fused_projection_2dgs, rasterize_to_pixels_2dgs
 
     N = means.shape[0]
@@ -525,9 +532,11 @@ def rasterization_2dgs(
 
     tile_width = math.ceil(width / float(tile_size))
     tile_height = math.ceil(height / float(tile_size))
+    capped = _isect_capacity is not None
+    assert not (capped and packed), "the sync-free isect: packed=False"
     pending_isects = isect_tiles_begin(means2d, radii, depths, tile_size, tile_width, tile_height,
                                        packed=packed, n_cameras=C, camera_ids=camera_ids,
-                                       gaussian_ids=gaussian_ids)
+                                       gaussian_ids=gaussian_ids, sync=not capped)
 
     if packed:  # gsplat/rendering.py:1216-1236
         if sh_degree is None:
@@ -562,7 +571,12 @@ def rasterization_2dgs(
         colors = depths[..., None]
 
     # (the 2DGS rasterizer gathers its own arrays: no rank ids)
-    tiles_per_gauss, isect_ids, flatten_ids = pending_isects.finish(sort=True, ranks=False)
+    counts = None
+    if capped:
+        tiles_per_gauss, isect_ids, flatten_ids, counts = pending_isects.finish_capped(
+            _isect_capacity, _isect_status, _isect_report, ranks=False)
+    else:
+        tiles_per_gauss, isect_ids, flatten_ids = pending_isects.finish(sort=True, ranks=False)
     isect_offsets = pending_isects.offsets  # written with the sorted isects
     if isect_offsets is None:
         isect_offsets = isect_offset_encode(isect_ids, C, tile_width, tile_height)
@@ -571,7 +585,8 @@ def rasterization_2dgs(
         rasterize_to_pixels_2dgs(means2d, ray_transforms, colors, opacities, normals, densify,
                                  width, height, tile_size, isect_offsets, flatten_ids,
                                  backgrounds=backgrounds, packed=packed, absgrad=absgrad,
-                                 distloss=distloss)
+                                 distloss=distloss, _n_isects_device=counts)
+    camtoworlds = torch.linalg.inv(viewmats) if _camtoworlds is None else _camtoworlds
     render_normals_from_depth = None
     if render_mode in ["ED", "RGB+ED"]:
         render_colors = torch.cat(
@@ -583,7 +598,7 @@ def rasterization_2dgs(
         elif depth_mode == "median":
             depth_for_normal = render_median
         render_normals_from_depth = depth_to_normal(
-            depth_for_normal, torch.linalg.inv(viewmats), Ks).squeeze(0)
+            depth_for_normal, camtoworlds, Ks).squeeze(0)
 
     meta = {"camera_ids": camera_ids, "gaussian_ids": gaussian_ids, "radii": radii,
             "means2d": means2d, "depths": depths, "ray_transforms": ray_transforms,
@@ -592,6 +607,8 @@ def rasterization_2dgs(
             "isect_ids": isect_ids, "flatten_ids": flatten_ids, "isect_offsets": isect_offsets,
             "width": width, "height": height, "tile_size": tile_size, "n_cameras": C,
             "render_distort": render_distort, "gradient_2dgs": densify}
-    render_normals = _rotate(torch.linalg.inv(viewmats)[..., :3, :3], render_normals)
+    if counts is not None:
+        meta["isect_counts"] = counts
+    render_normals = _rotate(camtoworlds[..., :3, :3], render_normals)
     return (render_colors, render_alphas, render_normals, render_normals_from_depth,
             render_distort, render_median, meta)

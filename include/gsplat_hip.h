@@ -33,7 +33,7 @@ const char *gsplat_hip_last_error(void);
  * 30: gsplat_hip_l1_ssim_loss_fused_fwd_ring (the loss also into a device
  * ring slot chosen by a device step counter), gsplat_hip_set_fwd_split_div.
  * 31: gsplat_hip_projection_bwd_adam, gsplat_hip_graph_memcpy_census.
- * 32: gsplat_hip_status_to_ring. */
+ * 32: gsplat_hip_status_to_ring; n_isects_device of the 2DGS rasterizer. */
 int gsplat_hip_abi_version(void);
 
 /* ---------------------------------------------------------------------------
@@ -682,7 +682,10 @@ int gsplat_hip_projection_2dgs_packed_bwd(int C, int N, int64_t nnz, const float
  * backgrounds[C,D] or NULL, masks u8[C,th,tw] or NULL ->
  * render_colors[C,H,W,D], render_alphas[C,H,W,1], render_normals[C,H,W,3],
  * render_distort[C,H,W,1], render_median[C,H,W,1], last_ids i32[C,H,W],
- * median_ids i32[C,H,W]. */
+ * median_ids i32[C,H,W].
+ * n_isects_device (ABI 32, here and in _bwd, may be NULL): the isect count on
+ * the device, n_isects then being the capacity of flatten_ids (the sync-free
+ * isect, gsplat_hip_isect_write_sorted_capped: a captured 2DGS step). */
 int gsplat_hip_rasterize_2dgs_supported_channels(int D);
 int gsplat_hip_rasterize_2dgs_fwd(int C, int D, int width, int height, int tile_size,
                                   int tile_width, int tile_height, const float *means2d,
@@ -690,7 +693,8 @@ int gsplat_hip_rasterize_2dgs_fwd(int C, int D, int width, int height, int tile_
                                   const float *opacities, const float *normals,
                                   const float *backgrounds, const uint8_t *masks,
                                   const int32_t *isect_offsets, int64_t n_isects,
-                                  const int32_t *flatten_ids, float *render_colors,
+                                  const int64_t *n_isects_device, const int32_t *flatten_ids,
+                                  float *render_colors,
                                   float *render_alphas, float *render_normals,
                                   float *render_distort, float *render_median,
                                   int32_t *last_ids, int32_t *median_ids, void *stream);
@@ -710,8 +714,8 @@ int gsplat_hip_rasterize_2dgs_bwd(
     int64_t n_gaussians, const float *means2d, const float *ray_transforms, const float *colors,
     const float *opacities, const float *normals, const float *backgrounds,
     const uint8_t *masks, const int32_t *isect_offsets, int64_t n_isects,
-    const int32_t *flatten_ids, const float *render_colors, const float *render_alphas,
-    const int32_t *last_ids, const int32_t *median_ids, const float *v_render_colors,
+    const int64_t *n_isects_device, const int32_t *flatten_ids, const float *render_colors,
+    const float *render_alphas, const int32_t *last_ids, const int32_t *median_ids, const float *v_render_colors,
     const float *v_render_alphas, const float *v_render_normals, const float *v_render_distort,
     const float *v_render_median, float *v_means2d, float *v_ray_transforms, float *v_colors,
     float *v_opacities, float *v_normals, float *v_densify, float *v_means2d_abs,

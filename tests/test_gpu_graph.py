@@ -237,6 +237,48 @@ def test_graph_trainer_tracks_eager(capacity):
     assert len(set(b[5])) == 6, b[5]
 
 
+@pytest.mark.parametrize("capacity", [None, 1000])
+def test_graph_2dgs_trainer_tracks_eager(capacity):
+    """The 2DGS (surfel) trainer's step captured and replayed (configs[4]):
+    rasterization_2dgs with the sync-free isect and the surfel rasterizer
+    reading the isect count on the device; with a tiny capacity the voided
+    steps re-run.  Six replayed steps against six eager ones, grad2d at the
+    run-to-run spread of two eager runs (float atomics of the backward)."""
+    from gsplat_hip.train_step import Trainer
+    means, rgbs, vm, K, W, H = _trainer_scene()
+    out = {}
+    for run in ("eager", "eager2", "graph"):
+        graph = run == "graph"
+        tr = Trainer(means, rgbs, vm, K, W, H, device=DEV, model="2dgs", graph=graph,
+                     isect_capacity=capacity, max_steps=100)
+        assert (tr._graph is not None) == graph
+        losses = [tr.step(it) for it in range(6)]
+        tr.sync()
+        assert tr.graph_fallback is None, tr.graph_fallback
+        out[run] = ({k: p.detach().clone() for k, p in tr.params.items()},
+                    [m.clone() for m in tr.opt.exp_avg], tr.opt.step_count,
+                    tr.grad2d.clone(), tr.count.clone(), [float(x) for x in losses])
+        if graph:
+            g = tr._graph
+            assert g.replays >= 6
+            assert set(g.census) <= {"kernel", "empty"}, g.census
+            if capacity is not None:
+                assert g.recaptures >= 2 and g.capacity > g.max_isects > capacity
+    a, a2, b = out["eager"], out["eager2"], out["graph"]
+    assert a[2] == b[2] == 6
+    torch.testing.assert_close(torch.tensor(b[5]), torch.tensor(a[5]), rtol=1e-4, atol=1e-6)
+    assert len(set(b[5])) == 6, b[5]
+    for k in a[0]:
+        torch.testing.assert_close(b[0][k], a[0][k], rtol=1e-3, atol=1e-5)
+    for x, y in zip(a[1], b[1]):
+        torch.testing.assert_close(y, x, rtol=1e-2, atol=1e-6)
+    torch.testing.assert_close(b[4], a[4], rtol=0, atol=0)
+    spread = float((a2[3] - a[3]).abs().max())
+    err = float((b[3] - a[3]).abs().max())
+    print(f"grad2d: graph-vs-eager {err:.3e}, eager run-to-run {spread:.3e}")
+    assert err <= max(4.0 * spread, 1e-5 * float(a[3].abs().max())), (err, spread)
+
+
 def test_graph_trainer_refine_tracks_eager():
     """A DefaultStrategy schedule (refines at steps 3 and 6, opacity resets at
     0 and 7): the graph-replayed trainer re-captures after every refine (new
