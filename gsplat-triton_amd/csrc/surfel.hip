@@ -823,6 +823,309 @@ __global__ void __launch_bounds__(128) fwd2_kernel(RasterArgs a) {
   }
 }
 
+// ---- Scalar-operand records (GSPLAT_HIP_SURFEL_SREC=1; D <= 4, 16x16
+// tiles).  fwd2_kernel spends, per (record, wave), six ds_read_b128 on the
+// staged record (every lane reads the same 96 B: 48 of the CU's 128 B/clk LDS
+// cycles) besides the staging writes.  Here pack_srec_kernel writes one 128-B
+// record per surfel with everything the culling test and the compositing
+// read, precomputed; the lanes cull their candidates from vector loads of the
+// first 80 B, and the kept records are composited in ascending isect order
+// from scalar loads (constant address space, wave-uniform address from
+// v_readlane of the candidate's id): the fields reach the VALU as SGPR
+// operands, with no LDS traffic at all.  Same per-pixel arithmetic and order
+// as fwd2_kernel (bit-identical outputs).
+constexpr int kSRecMaxD = 4;
+namespace srec {
+// floats of a record
+constexpr int NF = 32;
+constexpr int X = 0, Y = 1, OP = 2, SMAX = 3,   // chunk 0
+    AZ = 4, BZ = 5, CZ = 6,                      // chunk 1 (z parts: unscaled)
+    BOX = 8,                                     // chunk 2: xlo, xhi, ylo, yhi
+    U0X = 12, U0Y = 13, U1X = 14, U1Y = 15,      // chunk 3: v x w, w x u (unscaled)
+    U2X = 16, U2Y = 17, NRM0 = 18, NRM1 = 19,    // chunk 4: u x v
+    AX = 20, AY = 21, BX = 22, BY = 23,          // chunk 5 (scaled)
+    CX = 24, CY = 25, NRM2 = 26,                 // chunk 6
+    COL = 28;                                    // chunk 7: colour[D <= 4]
+}  // namespace srec
+
+template <int D>
+__global__ void __launch_bounds__(256)
+pack_srec_kernel(int64_t G, const float *__restrict__ means2d, const float *__restrict__ rt,
+                 const float *__restrict__ opac, const float *__restrict__ nrm,
+                 const float *__restrict__ col, float *__restrict__ rec) {
+  using namespace srec;
+  const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (g >= G) return;
+  float m[9];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) m[i] = rt[9 * g + i];
+  const float *u = m, *v = m + 3, *w = m + 6;
+  const float op = opac[g];
+  float r[NF];
+#pragma unroll
+  for (int i = 0; i < NF; ++i) r[i] = 0.f;
+  r[X] = means2d[2 * g];
+  r[Y] = means2d[2 * g + 1];
+  r[OP] = op;
+  r[SMAX] = __builtin_amdgcn_logf(255.f * op);  // log2, as stage_fwd
+  // surfel_keep's quantities, in its expressions
+  const float lnv = 0.69314718f * r[SMAX] + 0.05f;
+  const float r2 = 2.f * lnv;
+  const float c22 = r2 * (m[6] * m[6] + m[7] * m[7]) - m[8] * m[8];
+  float xlo = -INFINITY, xhi = INFINITY, ylo = -INFINITY, yhi = INFINITY;
+  if (c22 < 0.f) {
+    const float ic = 1.f / c22;
+    const float c00 = r2 * (m[0] * m[0] + m[1] * m[1]) - m[2] * m[2];
+    const float c11 = r2 * (m[3] * m[3] + m[4] * m[4]) - m[5] * m[5];
+    const float c02 = r2 * (m[0] * m[6] + m[1] * m[7]) - m[2] * m[8];
+    const float c12 = r2 * (m[3] * m[6] + m[4] * m[7]) - m[5] * m[8];
+    const float cx = c02 * ic, cy = c12 * ic;
+    const float hx = sqrtf(fmaxf(cx * cx - c00 * ic, 0.f)) + 1.f;
+    const float hy = sqrtf(fmaxf(cy * cy - c11 * ic, 0.f)) + 1.f;
+    xlo = cx - hx; xhi = cx + hx; ylo = cy - hy; yhi = cy + hy;
+  }
+  r[BOX] = xlo; r[BOX + 1] = xhi; r[BOX + 2] = ylo; r[BOX + 3] = yhi;
+  r[U0X] = v[1] * w[2] - v[2] * w[1];
+  r[U0Y] = v[2] * w[0] - v[0] * w[2];
+  r[AZ] = v[0] * w[1] - v[1] * w[0];
+  r[U1X] = w[1] * u[2] - w[2] * u[1];
+  r[U1Y] = w[2] * u[0] - w[0] * u[2];
+  r[BZ] = w[0] * u[1] - w[1] * u[0];
+  r[U2X] = u[1] * v[2] - u[2] * v[1];
+  r[U2Y] = u[2] * v[0] - u[0] * v[2];
+  r[CZ] = u[0] * v[1] - u[1] * v[0];
+  const float k = kSqrtHalfLog2e;  // stage_fwd's scaling
+  r[AX] = k * (v[1] * w[2] - v[2] * w[1]);
+  r[AY] = k * (v[2] * w[0] - v[0] * w[2]);
+  r[BX] = k * (w[1] * u[2] - w[2] * u[1]);
+  r[BY] = k * (w[2] * u[0] - w[0] * u[2]);
+  r[CX] = k * (u[1] * v[2] - u[2] * v[1]);
+  r[CY] = k * (u[2] * v[0] - u[0] * v[2]);
+  r[NRM0] = nrm[3 * g];
+  r[NRM1] = nrm[3 * g + 1];
+  r[NRM2] = nrm[3 * g + 2];
+#pragma unroll
+  for (int d = 0; d < D; ++d) r[COL + d] = col[D * g + d];
+  float4 *o = reinterpret_cast<float4 *>(rec + NF * g);
+#pragma unroll
+  for (int q = 0; q < NF / 4; ++q) o[q] = make_float4(r[4 * q], r[4 * q + 1], r[4 * q + 2], r[4 * q + 3]);
+}
+
+// The culling fields of a candidate (the record's first five float4s).
+struct SCull {
+  float4 c[5];
+};
+
+GS_INLINE void srec_load_cull(const float *rec, int32_t g, SCull &k) {
+  const float4 *p = reinterpret_cast<const float4 *>(rec + (int64_t)srec::NF * g);
+#pragma unroll
+  for (int q = 0; q < 5; ++q) k.c[q] = p[q];
+}
+
+// surfel_keep from the record's precomputed fields (same tests, same values).
+GS_INLINE bool srec_keep(const SCull &k, float x0, float x1, float y0, float y1) {
+  const float x = k.c[0].x, y = k.c[0].y, op = k.c[0].z, smax = k.c[0].w;
+  if (!(op >= kAlphaMin)) return false;
+  const float lnv = 0.69314718f * smax + 0.05f;
+  const float ddx = fmaxf(fmaxf(x0 - x, x - x1), 0.f), ddy = fmaxf(fmaxf(y0 - y, y - y1), 0.f);
+  if (ddx * ddx + ddy * ddy <= lnv) return true;
+  const float r2 = 2.f * lnv;
+  if (k.c[2].y < x0 || k.c[2].x > x1 || k.c[2].w < y0 || k.c[2].z > y1) return false;
+  const float a0x = k.c[3].x, a0y = k.c[3].y, a0z = k.c[1].x;
+  const float a1x = k.c[3].z, a1y = k.c[3].w, a1z = k.c[1].y;
+  const float a2x = k.c[4].x, a2y = k.c[4].y, a2z = k.c[1].z;
+  float sx[4], sy[4], zmin = 3.4e38f, zmax = -3.4e38f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float X = (i == 1 || i == 2) ? x1 : x0, Y = i >= 2 ? y1 : y0;
+    const float zx = X * a0x + Y * a1x + a2x, zy = X * a0y + Y * a1y + a2y,
+                zz = X * a0z + Y * a1z + a2z;
+    zmin = fminf(zmin, zz);
+    zmax = fmaxf(zmax, zz);
+    const float iz = 1.f / zz;
+    sx[i] = zx * iz;
+    sy[i] = zy * iz;
+  }
+  if (!(zmin > 0.f || zmax < 0.f)) return true;
+  float best = 3.4e38f;
+  bool pos = true, neg = true;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int j = (i + 1) & 3;
+    const float ex = sx[j] - sx[i], ey = sy[j] - sy[i];
+    const float cr = ey * sx[i] - ex * sy[i];
+    pos &= cr >= 0.f;
+    neg &= cr <= 0.f;
+    const float L = ex * ex + ey * ey;
+    const float t = L > 0.f ? fminf(fmaxf(-(sx[i] * ex + sy[i] * ey) / L, 0.f), 1.f) : 0.f;
+    const float dx = sx[i] + t * ex, dy = sy[i] + t * ey;
+    best = fminf(best, dx * dx + dy * dy);
+  }
+  return pos || neg || best <= r2;
+}
+
+typedef __attribute__((address_space(4))) const float cfloat_t;
+
+// The compositing fields of one kept record, read with scalar loads.
+template <int D>
+struct SBlend {
+  float x, y, op, smax, az, bz, cz, ax, ay, bx, by, cx, cy, n0, n1, n2, col[D];
+};
+
+template <int D>
+GS_INLINE void srec_load_blend(const float *rec, int32_t g, SBlend<D> &r) {
+  cfloat_t *p = (cfloat_t *)(rec) + (int64_t)srec::NF * g;
+  using namespace srec;
+  r.x = p[X]; r.y = p[Y]; r.op = p[OP]; r.smax = p[SMAX];
+  r.az = p[AZ]; r.bz = p[BZ]; r.cz = p[CZ];
+  r.n0 = p[NRM0]; r.n1 = p[NRM1];
+  r.ax = p[AX]; r.ay = p[AY]; r.bx = p[BX]; r.by = p[BY];
+  r.cx = p[CX]; r.cy = p[CY]; r.n2 = p[NRM2];
+#pragma unroll
+  for (int d = 0; d < D; ++d) r.col[d] = p[COL + d];
+}
+
+template <int D>
+__global__ void __launch_bounds__(128) fwd2s_kernel(RasterArgs a, const float *__restrict__ rec) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int tile = blockIdx.x;
+  const int ntile = a.tw * a.th;
+  const int c = tile / ntile;
+  const int rem = tile - c * ntile;
+  const int ty = rem / a.tw, tx = rem - ty * a.tw;
+  const int64_t start = a.offsets[tile];
+  const int64_t end = (tile == a.n_tiles - 1) ? (a.n_dev ? a.n_dev[0] : a.n_isects)
+                                              : (int64_t)a.offsets[tile + 1];
+  const float rx0 = tx * 16 + 0.5f, rx1 = rx0 + 15.f;
+  const float ry0 = ty * 16 + 8 * w + 0.5f, ry1 = ry0 + 7.f;
+  const float *bg = a.backgrounds ? a.backgrounds + (int64_t)c * D : nullptr;
+  const bool masked = a.masks && !a.masks[tile];
+  const float fx = (float)(tx * 16 + (lane & 15)) + 0.5f;
+  float fy[2], T[2], col[2][D], nrm[2][3], distort[2], acc_vd[2], median[2];
+  int32_t cur[2], med[2];
+  bool done[2], inside[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int py = ty * 16 + 8 * w + 4 * k + (lane >> 4);
+    fy[k] = (float)py + 0.5f;
+    inside[k] = (tx * 16 + (lane & 15)) < a.W && py < a.H;
+    T[k] = 1.f;
+#pragma unroll
+    for (int d = 0; d < D; ++d) col[k][d] = 0.f;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) nrm[k][i] = 0.f;
+    distort[k] = acc_vd[k] = median[k] = 0.f;
+    cur[k] = med[k] = 0;
+    done[k] = !inside[k] || masked;
+  }
+  // one record into both pixels of the lane (fwd2_kernel's arithmetic)
+  auto blend = [&](const SBlend<D> &r, int32_t idx) {
+    const float rxb = fx * r.ax + r.cx, ryb = fx * r.ay + r.cy, rzb = fx * r.az + r.cz;
+    const float dx = r.x - fx, dx2 = dx * dx;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      if (done[k]) continue;
+      const float rx = fy[k] * r.bx + rxb;
+      const float ry = fy[k] * r.by + ryb;
+      const float rz = fy[k] * r.bz + rzb;
+      const float iz = __builtin_amdgcn_rcpf(rz);
+      const float g3 = (rx * rx + ry * ry) * (iz * iz);
+      const float dy = r.y - fy[k];
+      const float g2 = kLog2e * (dx2 + dy * dy);
+      const float m = fminf(g3, g2);
+      if (rz != 0.f && m <= r.smax) {
+        const float alpha = fminf(kAlphaMax, r.op * __builtin_amdgcn_exp2f(-m));
+        const float nT = T[k] * (1.f - alpha);
+        if (nT <= kTMin) {
+          done[k] = true;
+        } else {
+          const float vis = alpha * T[k];
+#pragma unroll
+          for (int d = 0; d < D; ++d) col[k][d] += r.col[d] * vis;
+          nrm[k][0] += r.n0 * vis;
+          nrm[k][1] += r.n1 * vis;
+          nrm[k][2] += r.n2 * vis;
+          const float depth = r.col[D - 1];
+          distort[k] += 2.f * (vis * depth * (1.f - T[k]) - vis * acc_vd[k]);
+          acc_vd[k] += vis * depth;
+          if (T[k] > 0.5f) {
+            median[k] = depth;
+            med[k] = idx;
+          }
+          cur[k] = idx;
+          T[k] = nT;
+        }
+      }
+    }
+  };
+
+  int64_t b = start;
+  const bool run = !masked && b < end;
+  int32_t gn = 0;
+  SCull kn;
+  if (run) {
+    gn = b + lane < end ? a.flatten_ids[b + lane] : 0;
+    srec_load_cull(rec, gn, kn);
+  }
+  for (; run && b < end; b += 64) {
+    if (__ballot(!(done[0] & done[1])) == 0) break;
+    const bool keep = (b + lane < end) && srec_keep(kn, rx0, rx1, ry0, ry1);
+    uint64_t km = __ballot(keep);
+    const int32_t gc = gn;
+    if (b + 64 < end) {  // the next batch's candidates, in flight while this one composites
+      gn = b + 64 + lane < end ? a.flatten_ids[b + 64 + lane] : 0;
+      srec_load_cull(rec, gn, kn);
+    }
+    // kept records in ascending isect order, two per round: both records'
+    // scalar loads are issued before the first is blended (no record value
+    // is carried across rounds, so the compiler keeps them in SGPRs)
+    int n = 0;
+    while (km) {
+      const int t0 = __builtin_ctzll(km);
+      km &= km - 1;
+      const bool two = km != 0;
+      const int t1 = two ? __builtin_ctzll(km) : t0;
+      km &= km - 1;
+      SBlend<D> r0, r1;
+      srec_load_blend<D>(rec, __builtin_amdgcn_readlane(gc, t0), r0);
+      srec_load_blend<D>(rec, __builtin_amdgcn_readlane(gc, t1), r1);
+      blend(r0, (int32_t)(b + t0));
+      if ((++n & 7) == 0 && __ballot(!(done[0] & done[1])) == 0) break;
+      if (!two) break;
+      blend(r1, (int32_t)(b + t1));
+      if ((++n & 7) == 0 && __ballot(!(done[0] & done[1])) == 0) break;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    if (!inside[k]) continue;
+    const int64_t pid = ((int64_t)c * a.H + (ty * 16 + 8 * w + 4 * k + (lane >> 4))) * a.W +
+                        tx * 16 + (lane & 15);
+    if (masked) {  // as fwd_kernel
+#pragma unroll
+      for (int d = 0; d < D; ++d) a.render_colors[pid * D + d] = bg ? bg[d] : 0.f;
+      a.render_alphas[pid] = 0.f;
+#pragma unroll
+      for (int i = 0; i < 3; ++i) a.render_normals[pid * 3 + i] = 0.f;
+      a.render_distort[pid] = 0.f;
+      a.render_median[pid] = 0.f;
+      a.last_ids[pid] = 0;
+      a.median_ids[pid] = 0;
+      continue;
+    }
+    a.render_alphas[pid] = 1.f - T[k];
+#pragma unroll
+    for (int d = 0; d < D; ++d)
+      a.render_colors[pid * D + d] = bg ? col[k][d] + T[k] * bg[d] : col[k][d];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) a.render_normals[pid * 3 + i] = nrm[k][i];
+    a.render_distort[pid] = distort[k];
+    a.render_median[pid] = median[k];
+    a.last_ids[pid] = cur[k];
+    a.median_ids[pid] = med[k];
+  }
+}
+
 // Gradient fields of a packed row: colour[D], normal[3], ray transform[9],
 // means2d[2], opacity, |means2d|[2] (absgrad only).
 template <int D, bool ABS>
@@ -1405,9 +1708,9 @@ extern "C" int gsplat_hip_rasterize_2dgs_fwd(
     const float *means2d, const float *ray_transforms, const float *colors,
     const float *opacities, const float *normals, const float *backgrounds,
     const uint8_t *masks, const int32_t *isect_offsets, int64_t n_isects,
-    const int64_t *n_isects_device, const int32_t *flatten_ids, float *render_colors,
-    float *render_alphas, float *render_normals, float *render_distort, float *render_median,
-    int32_t *last_ids, int32_t *median_ids, void *stream) {
+    const int64_t *n_isects_device, const int32_t *flatten_ids, const float *records,
+    float *render_colors, float *render_alphas, float *render_normals, float *render_distort,
+    float *render_median, int32_t *last_ids, int32_t *median_ids, void *stream) {
   if (int e = check_tiles(C, width, height, tile_size, tile_width, tile_height)) return e;
   GS_REQUIRE(channels_supported(D), "rasterize_2dgs_fwd: unsupported channel count %d", D);
   const int n_tiles = C * tile_width * tile_height;
@@ -1432,6 +1735,16 @@ extern "C" int gsplat_hip_rasterize_2dgs_fwd(
   hipStream_t st = (hipStream_t)stream;
   // 16x16 tiles: two pixels per lane (fwd2_kernel) unless GSPLAT_HIP_FWD_PX=1
   const bool px2 = tile_size == 16 && fwd2_enabled();
+  if (records) {  // scalar-operand records (gsplat_hip_rasterize_2dgs_pack_records)
+    GS_REQUIRE(px2 && D <= kSRecMaxD, "rasterize_2dgs_fwd: records need 16x16 tiles, D <= %d",
+               kSRecMaxD);
+#define GS_CASE(n)                                                                            \
+  if (D == n) hipLaunchKernelGGL(fwd2s_kernel<n>, dim3(n_tiles), dim3(128), 0, st, a, records);
+    GS_CASE(1) GS_CASE(2) GS_CASE(3) GS_CASE(4)
+#undef GS_CASE
+    GS_CHECK_LAUNCH("rasterize_2dgs_fwd");
+    return 0;
+  }
 #define GS_CASE(n)                                                                            \
   if (D == n) {                                                                               \
     const size_t lds = (size_t)waves * 64 * Rec<n>::NF * sizeof(float);                       \
@@ -1443,6 +1756,35 @@ extern "C" int gsplat_hip_rasterize_2dgs_fwd(
   GS_SURFEL_CHANNELS(GS_CASE)
 #undef GS_CASE
   GS_CHECK_LAUNCH("rasterize_2dgs_fwd");
+  return 0;
+}
+
+extern "C" int gsplat_hip_rasterize_2dgs_record_floats(int D, int tile_size) {
+  return (tile_size == 16 && D >= 1 && D <= kSRecMaxD && fwd2_enabled()) ? srec::NF : 0;
+}
+
+extern "C" int gsplat_hip_rasterize_2dgs_pack_records(int64_t n_gaussians, int D,
+                                                      const float *means2d,
+                                                      const float *ray_transforms,
+                                                      const float *opacities, const float *normals,
+                                                      const float *colors, float *records,
+                                                      void *stream) {
+  GS_REQUIRE(D >= 1 && D <= kSRecMaxD, "rasterize_2dgs_pack_records: D %d not in [1, %d]", D,
+             kSRecMaxD);
+  GS_REQUIRE(n_gaussians >= 0, "rasterize_2dgs_pack_records: negative count");
+  if (n_gaussians == 0) return 0;
+  GS_REQUIRE(means2d && ray_transforms && opacities && normals && colors && records,
+             "rasterize_2dgs_pack_records: null pointer argument");
+  GS_REQUIRE(((uintptr_t)records & 15) == 0, "rasterize_2dgs_pack_records: records not 16-B aligned");
+  const dim3 grid((unsigned)((n_gaussians + 255) / 256));
+  hipStream_t st = (hipStream_t)stream;
+#define GS_CASE(n)                                                                            \
+  if (D == n)                                                                                 \
+    hipLaunchKernelGGL(pack_srec_kernel<n>, grid, dim3(256), 0, st, n_gaussians, means2d,     \
+                       ray_transforms, opacities, normals, colors, records);
+  GS_CASE(1) GS_CASE(2) GS_CASE(3) GS_CASE(4)
+#undef GS_CASE
+  GS_CHECK_LAUNCH("rasterize_2dgs_pack_records");
   return 0;
 }
 

@@ -201,6 +201,9 @@ def fully_fused_projection_2dgs(
 
 # ============================================================ rasterization ==
 _SUPPORTED_D = (1, 2, 3, 4, 5, 6, 7, 8, 9, 16, 17, 32, 33)
+# the forward composites from scalar-operand records (csrc/surfel.hip
+# fwd2s_kernel) where the configuration has them
+SREC = os.environ.get("GSPLAT_HIP_SURFEL_SREC", "0") == "1"
 
 
 class _RasterizeToPixels2DGS(torch.autograd.Function):
@@ -226,12 +229,21 @@ class _RasterizeToPixels2DGS(torch.autograd.Function):
         render_median = torch.empty((C, height, width, 1), device=dev)
         last_ids = torch.empty((C, height, width), dtype=torch.int32, device=dev)
         median_ids = torch.empty((C, height, width), dtype=torch.int32, device=dev)
+        records = None
+        nf = int(_lib.query("gsplat_hip_rasterize_2dgs_record_floats", D, int(tile_size))) \
+            if SREC else 0
+        if nf:  # scalar-operand records (GSPLAT_HIP_SURFEL_SREC=1)
+            G = opacities.numel()
+            records = torch.empty(max(G, 1) * nf, device=dev)
+            _lib.call("gsplat_hip_rasterize_2dgs_pack_records", G, D, _ptr(means2d),
+                      _ptr(ray_transforms), _ptr(opacities), _ptr(normals), _ptr(colors),
+                      _ptr(records), _stream())
         with _Timed("rasterize_2dgs_fwd"):
             _lib.call("gsplat_hip_rasterize_2dgs_fwd", C, D, int(width), int(height),
                       int(tile_size), tw, th, _ptr(means2d), _ptr(ray_transforms), _ptr(colors),
                       _ptr(opacities), _ptr(normals), _ptr(backgrounds), _ptr(masks_u8),
                       _ptr(isect_offsets), flatten_ids.numel(), _ptr(n_dev), _ptr(flatten_ids),
-                      _ptr(render_colors), _ptr(render_alphas), _ptr(render_normals),
+                      _ptr(records), _ptr(render_colors), _ptr(render_alphas), _ptr(render_normals),
                       _ptr(render_distort), _ptr(render_median), _ptr(last_ids),
                       _ptr(median_ids), _stream())
         ctx.save_for_backward(means2d, ray_transforms, colors, opacities, normals, densify,

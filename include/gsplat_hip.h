@@ -685,7 +685,18 @@ int gsplat_hip_projection_2dgs_packed_bwd(int C, int N, int64_t nnz, const float
  * median_ids i32[C,H,W].
  * n_isects_device (ABI 32, here and in _bwd, may be NULL): the isect count on
  * the device, n_isects then being the capacity of flatten_ids (the sync-free
- * isect, gsplat_hip_isect_write_sorted_capped: a captured 2DGS step). */
+ * isect, gsplat_hip_isect_write_sorted_capped: a captured 2DGS step).
+ * records (ABI 32, may be NULL): the surfels' compositing records
+ * (gsplat_hip_rasterize_2dgs_pack_records): the forward then culls from them
+ * and composites with scalar loads instead of its LDS queue; same outputs.
+ * record_floats: floats per record (32), 0 when the configuration (D,
+ * tile_size) has no record path; pack_records writes records f32[G][32]
+ * from the rasterizer's inputs (G rows of means2d ...). */
+int gsplat_hip_rasterize_2dgs_record_floats(int D, int tile_size);
+int gsplat_hip_rasterize_2dgs_pack_records(int64_t n_gaussians, int D, const float *means2d,
+                                           const float *ray_transforms, const float *opacities,
+                                           const float *normals, const float *colors,
+                                           float *records, void *stream);
 int gsplat_hip_rasterize_2dgs_supported_channels(int D);
 int gsplat_hip_rasterize_2dgs_fwd(int C, int D, int width, int height, int tile_size,
                                   int tile_width, int tile_height, const float *means2d,
@@ -694,7 +705,7 @@ int gsplat_hip_rasterize_2dgs_fwd(int C, int D, int width, int height, int tile_
                                   const float *backgrounds, const uint8_t *masks,
                                   const int32_t *isect_offsets, int64_t n_isects,
                                   const int64_t *n_isects_device, const int32_t *flatten_ids,
-                                  float *render_colors,
+                                  const float *records, float *render_colors,
                                   float *render_alphas, float *render_normals,
                                   float *render_distort, float *render_median,
                                   int32_t *last_ids, int32_t *median_ids, void *stream);

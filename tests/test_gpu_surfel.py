@@ -121,6 +121,33 @@ def test_raster2dgs_fwd(seed, D, bg, C, thin):
     close_most(rm, om, 1e-4, 1e-4, "median", max_frac=5e-3)
 
 
+@pytest.mark.parametrize("seed,D,bg,C,thin,masked", [(0, 4, True, 1, False, False),
+                                                     (5, 4, True, 1, True, False),
+                                                     (6, 3, False, 2, True, False),
+                                                     (2, 1, True, 2, False, True),
+                                                     (7, 2, False, 1, False, False)])
+def test_raster2dgs_fwd_records_bit_identical(monkeypatch, seed, D, bg, C, thin, masked):
+    """The scalar-operand record forward (csrc/surfel.hip fwd2s_kernel,
+    GSPLAT_HIP_SURFEL_SREC=1) renders exactly what the LDS-queue forward
+    renders -- all five outputs bit for bit, and so the backward's gradients
+    (which read the forward's outputs and last / median ids)."""
+    from gsplat_hip import _lib, _wrapper_2dgs
+    assert _lib.query("gsplat_hip_rasterize_2dgs_record_floats", D, 16) == 32
+    sc = surfel_scene(seed, N=600, W=150, H=100, D=D, bg=bg, C=C, thin=thin)
+    masks = (np.random.default_rng(seed).random(sc["off"].shape) > 0.3) if masked else None
+    res = []
+    for srec in (False, True):
+        monkeypatch.setattr(_wrapper_2dgs, "SREC", srec)
+        leaves, bgt, densify, out = _raster_gpu(sc, masks=masks)
+        w = [torch.linspace(-1, 1, o.numel(), device=DEV).view_as(o) for o in out]
+        sum((o * ww).sum() for o, ww in zip(out, w)).backward()
+        res.append(([o.detach() for o in out], [leaves[k].grad for k in sorted(leaves)]))
+    for a, b in zip(res[0][0], res[1][0]):
+        assert torch.equal(a, b), float((a - b).abs().max())
+    for a, b in zip(res[0][1], res[1][1]):
+        torch.testing.assert_close(b, a, rtol=1e-5, atol=1e-6)  # float atomics' order only
+
+
 def test_raster2dgs_fwd_masks():
     sc = surfel_scene(5, N=300, W=70, H=52, D=4, bg=True)
     rng = np.random.default_rng(0)

@@ -14,6 +14,11 @@ for r in 1 2; do
     > $O/bench_m5.$r.json 2> $O/bench_m5.$r.err || exit 7
   python -c "import json; d=json.load(open('$O/bench_m5.$r.json')); print('m5', d['value'], d['ms_per_step'], d.get('step_issue'), d['roofline'].get('launch_ms'), d['roofline'].get('bwd',{}).get('launch_ms'))"
 done
+for r in 1 2; do
+  GSPLAT_HIP_SURFEL_SREC=1 timeout -k 10 300 python bench.py --config m5 --no-cpu-baseline --no-traffic \
+    > $O/bench_m5_srec.$r.json 2> $O/bench_m5_srec.$r.err || exit 9
+  python -c "import json; d=json.load(open('$O/bench_m5_srec.$r.json')); print('m5 srec', d['value'], d['ms_per_step'], d['roofline'].get('launch_ms'))"
+done
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $O/trace_m5 -o run -- /usr/bin/python3 bench.py --config m5 --steps 10 --warmup 3 --no-cpu-baseline --no-traffic > $O/trace_m5.log 2>&1 || exit 8
 python tools/kstats.py $(find $O/trace_m5 -name "*kernel_stats.csv" | head -1) 13 > $O/kstats_m5.txt 2>&1; head -25 $O/kstats_m5.txt
 for m in "" "--eager"; do
