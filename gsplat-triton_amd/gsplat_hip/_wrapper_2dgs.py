@@ -13,6 +13,7 @@ signal).  Every op runs through the HIP C ABI on torch's current stream; there
 is no CPU fallback.
 """
 
+import os
 from typing import Optional, Tuple
 
 import torch
