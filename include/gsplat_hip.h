@@ -359,7 +359,9 @@ int gsplat_hip_set_fwd_split_div(int div);
  * bit 0 = the backward skips its gradient atomics (timing experiments);
  * bit 1 = a chunk of a split tile never waits for an earlier chunk's
  * published product and computes it itself (the timeout path; results are
- * identical).  Returns the previous flags. */
+ * identical); bit 3 = the forward composites from scalar-operand records
+ * (as GSPLAT_HIP_FWD_SREC=1; records packed by later renders carry its
+ * fields; results are identical).  Returns the previous flags. */
 int gsplat_hip_debug_set_flags(int flags);
 
 /* ---------------------------------------------------------------------------

@@ -262,3 +262,26 @@ def test_split_forward_vs_oracle():
     close_most(ra, oa, 1e-4, 1e-4, "alphas", max_frac=1e-3)
     close_most(rc, oc, 1e-4, 1e-4, "colors", max_frac=1e-3)
 
+
+
+@pytest.mark.parametrize("split,mode", [(0, "RGB"), (300, "RGB"), (0, "RGB+D")])
+def test_scalar_record_forward_is_bit_identical(split, mode):
+    """The scalar-operand forward (debug flag bit 3 / GSPLAT_HIP_FWD_SREC=1:
+    kept records read with s_load and composited from SGPR operands, no LDS
+    staging) renders exactly what the LDS-pair forward renders: colours and
+    alphas bit for bit, with and without split heavy tiles; the backward,
+    which reads the forward's chunk state, to the order of its atomics."""
+    from gsplat_hip import _lib
+    ins, W, H = _heavy_scene()
+    outs = []
+    for flag in (0, 8):
+        old = _lib.query("gsplat_hip_debug_set_flags", flag)
+        try:
+            outs.append(_render_split(ins, W, H, split, mode))
+        finally:
+            _lib.query("gsplat_hip_debug_set_flags", old)
+    (rc0, ra0, _, g0), (rc1, ra1, _, g1) = outs
+    assert torch.equal(rc0, rc1), float((rc0 - rc1).abs().max())
+    assert torch.equal(ra0, ra1), float((ra0 - ra1).abs().max())
+    for a, b in zip(g1, g0):
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-6 * float(b.abs().max()))

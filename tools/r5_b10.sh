@@ -6,8 +6,8 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 O=gpurun_out/r5_b10; mkdir -p $O
 timeout -k 10 500 python -u -m pytest tests/test_gpu_distributed.py tests/test_gpu_graph.py \
-  tests/test_gpu_surfel.py -x -v --timeout 200 --timeout-method thread \
-  -k "dp_step or gshard_rccl or 2dgs or surfel or Surfel" > $O/dp_tests.log 2>&1
+  tests/test_gpu_surfel.py tests/test_gpu_raster_dispatch.py -x -v --timeout 200 --timeout-method thread \
+  -k "dp_step or gshard_rccl or 2dgs or surfel or Surfel or scalar_record" > $O/dp_tests.log 2>&1
 rc=$?; echo "dp/2dgs tests rc=$rc"; tail -4 $O/dp_tests.log; [ $rc -eq 0 ] || exit $rc
 for r in 1 2; do
   timeout -k 10 300 python bench.py --config m5 --no-cpu-baseline $([ $r = 2 ] && echo --no-traffic) \
@@ -27,10 +27,13 @@ for m in "" "--eager"; do
   python -c "import json; d=json.load(open('$O/bench_dp$m.json')); print('dp$m', d['value'], d['ms_per_step'], d.get('step_issue'))"
 done
 for r in 1 2; do
+  GSPLAT_HIP_FWD_SREC=1 timeout -k 10 300 python bench.py --no-cpu-baseline --no-traffic \
+    > $O/bench_fsrec.$r.json 2> $O/bench_fsrec.$r.err || exit 10
+  python -c "import json; d=json.load(open('$O/bench_fsrec.$r.json')); print('fwd srec', d['value'], d['ms_per_step'], d['roofline'].get('launch_ms'))"
   for cpw in 3 1; do
     GSPLAT_HIP_SSIM_CPW=$cpw timeout -k 10 300 python bench.py --no-cpu-baseline --no-traffic \
       > $O/bench_cpw$cpw.$r.json 2> $O/bench_cpw$cpw.$r.err || exit 5
-    python -c "import json; d=json.load(open('$O/bench_cpw$cpw.$r.json')); print('cpw$cpw', d['value'], d['ms_per_step'])"
+    python -c "import json; d=json.load(open('$O/bench_cpw$cpw.$r.json')); print('cpw$cpw', d['value'], d['ms_per_step'], d['roofline'].get('launch_ms'))"
   done
 done
 exit 0
