@@ -398,6 +398,13 @@ class ShardedAdam:
         self._updated = {}
         # Adam + all-gather issue stream (CUDA only; gloo runs them inline)
         self.side = torch.cuda.Stream(device=dev) if dev.type == "cuda" else None
+        # set while a HIP graph captures the step (graph_step.GraphStep): every
+        # collective on the default group, issued and waited for in order on
+        # the capturing stream -- no side stream, no second communicator, no
+        # early SH reduce-scatter (a capture with them crashed in
+        # hipStreamEndCapture on a one-rank RCCL group); the graph's replay
+        # has no host gaps to hide anyway
+        self.capturing = False
 
     def wait(self, indices=None):
         """Order the current stream after the deferred all-gathers of these
@@ -417,13 +424,13 @@ class ShardedAdam:
     def _issue_reduce(self, gi, grads):
         """Reduce-scatter (main rows) and all-reduce (remainder rows) of group
         gi's gradients on its process group, issued from the current stream."""
-        pg = self.group_pgs[gi]
+        pg = None if self.capturing else self.group_pgs[gi]
         flats, works = {}, []
         for i in sorted(self.groups[gi], key=lambda i: -self.params[i].numel()):
             g = grads.get(i)
             gf = (torch.zeros_like(self.params[i]) if g is None else g).contiguous().view(-1)
             flats[i] = gf
-            if self.side is not None:  # its tail rows are read on the side stream
+            if self.side is not None and not self.capturing:  # tail rows read on the side stream
                 gf.record_stream(self.side)
             _, _, main, tot = self.layout[i]
             if self.solo:
@@ -450,6 +457,8 @@ class ShardedAdam:
         """Issue group gi's reductions now (from a gradient hook, while the
         rest of the backward is still being queued); the next step() only
         waits for them.  Stream order only, no host synchronisation."""
+        if self.capturing:
+            return  # step() issues it, in order
         if gi not in self._early:
             self._early[gi] = self._issue_reduce(gi, self._grads(self.groups[gi], xform))
 
@@ -478,7 +487,7 @@ class ShardedAdam:
         if hyper is None:
             self.step_count += 1
         self._hyper = None if hyper is None else [hyper, 0, void]
-        side = self.side
+        side = None if self.capturing else self.side
         for gi, grp in enumerate(self.groups):
             if gi in self._early:
                 flats, works = self._early.pop(gi)
@@ -505,7 +514,8 @@ class ShardedAdam:
                         mine = self._shard(i, full)
                         self._pending[i] = dist.all_gather_into_tensor(
                             full, mine if full.is_cuda else mine.clone(),
-                            group=self.group_pgs[gi], async_op=True)
+                            group=None if self.capturing else self.group_pgs[gi],
+                            async_op=True)
         if not defer_gather:
             self.wait()
 

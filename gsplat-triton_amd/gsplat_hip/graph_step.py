@@ -321,6 +321,8 @@ class GraphStep:
                       self.slot.data_ptr(), _wrapper._stream())
         from . import losses as _losses
         tr._sh_ready = 0  # the sharded optimizer's SH reduce-scatter hook
+        if self.dp:  # its collectives in order on this stream (ShardedAdam.capturing)
+            tr.opt.capturing = True
         torch.autograd.backward(loss, _losses.ONE_GRAD)
         if stats and "g" in grad_box:  # DefaultStrategy statistics (until refine_stop_iter)
             update_state_(tr.grad2d, tr.count, grad_box["g"], meta["radii"], meta["width"],
@@ -329,6 +331,7 @@ class GraphStep:
             assert not tr._sh_skip(fusion)
             tr.opt.step(defer_gather=False, xform=tr._geom_xform(fusion),
                         hyper=self.scal[:sh_off], void=self.status)
+            tr.opt.capturing = False
         else:
             skip = tr._sh_skip(fusion)
             launched = tuple(i for i in range(self.n_groups) if i not in skip)
