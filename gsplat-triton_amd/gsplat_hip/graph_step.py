@@ -399,6 +399,9 @@ class GraphStep:
                 torch.cuda.current_stream(self.dev).wait_stream(s)
             self.graph = None
             g = torch.cuda.CUDAGraph(keep_graph=True)
+            dump = os.environ.get("GSPLAT_HIP_GRAPH_DUMP")  # diagnosis: the graph as DOT
+            if dump:
+                g.enable_debug_mode()
             # no garbage collection while capturing: a collected object that
             # owns a HIP resource (an earlier trainer's graph or event) would
             # free it with a call that is illegal during a capture -- a test
@@ -411,6 +414,8 @@ class GraphStep:
             finally:
                 if gc_on:
                     gc.enable()
+            if dump:
+                g.debug_dump(f"{dump}.{self.recaptures}.dot")
             # RCCL's collectives (a Gaussian-sharded or data-parallel step on
             # a real process group) may hold device-to-device copies
             self.census = check_kernel_nodes_only(g, allow_d2d=self.vote)
