@@ -297,8 +297,9 @@ class GraphStep:
                 _isect_capacity=self.capacity, _isect_status=self.status,
                 _isect_report=(self.ring_out.dev, self.slot), _camtoworlds=self.c2w)
             colors = rc[..., :3]
-            # the densification input (a leaf): its gradient, as .grad would hold it
-            meta["gradient_2dgs"].register_hook(lambda g: grad_box.__setitem__("g", g))
+            # the densification input is a leaf: its .grad after the backward
+            # (a hook keeping a reference would make AccumulateGrad clone the
+            # gradient -- a memcpy node in the graph)
         else:
             with _wrapper.fwd_split_div(getattr(tr, "split_div", None)):
                 colors, _, meta = rasterization(
@@ -324,6 +325,8 @@ class GraphStep:
         if self.dp:  # its collectives in order on this stream (ShardedAdam.capturing)
             tr.opt.capturing = True
         torch.autograd.backward(loss, _losses.ONE_GRAD)
+        if tr.model == "2dgs" and meta["gradient_2dgs"].grad is not None:
+            grad_box["g"] = meta["gradient_2dgs"].grad
         if stats and "g" in grad_box:  # DefaultStrategy statistics (until refine_stop_iter)
             update_state_(tr.grad2d, tr.count, grad_box["g"], meta["radii"], meta["width"],
                           meta["height"], meta["n_cameras"], skip=self.status)
