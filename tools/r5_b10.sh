@@ -7,13 +7,9 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 O=gpurun_out/r5_b10; mkdir -p $O
-# the 2DGS capture's one memcpy node: dump the captured graph (DOT) to find it
-GSPLAT_HIP_GRAPH_DUMP=$O/g2dgs timeout -k 10 200 python -u -m pytest tests/test_gpu_graph.py -x -q \
-  --timeout 150 --timeout-method thread -k "2dgs and None" > $O/dump.log 2>&1
-echo "dump rc=$?"; ls $O; grep -il memcpy $O/*.dot | head; grep -i -B2 -A6 "memcpy" $O/g2dgs.0.dot | head -60
 timeout -k 10 500 python -u -m pytest tests/test_gpu_distributed.py tests/test_gpu_graph.py \
   tests/test_gpu_surfel.py tests/test_gpu_raster_dispatch.py -x -v --timeout 200 --timeout-method thread \
-  -k "(dp_step and 1-None) or gshard_rccl or surfel or Surfel or scalar_record" > $O/tests.log 2>&1
+  -k "(dp_step and 1-None) or 2dgs or scalar_record or records_bit" > $O/tests.log 2>&1
 rc=$?; echo "tests rc=$rc"; tail -4 $O/tests.log; [ $rc -eq 0 ] || exit $rc
 for r in 1 2; do
   timeout -k 10 300 python bench.py --config m5 --no-cpu-baseline $([ $r = 2 ] && echo --no-traffic) \
