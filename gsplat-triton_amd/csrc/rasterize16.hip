@@ -109,12 +109,6 @@ GS_INLINE f2v reduce_scatter2(const f2v *v, int lane) {
 // (rasterize_to_pixels_fwd.py:93-145 loads the four arrays separately).
 constexpr int kRecFloats = 16;
 constexpr int kRecMaxD = kRecFloats - 6;
-// Scalar-operand forward (GSPLAT_HIP_FWD_SREC=1, D <= kSRecMaxD): the pad
-// floats 12..15 of a record also hold the forward's pre-scaled conic and
-// smax, (0.5 a, 0.5 c, b) * log2(e) and log2(255 opacity), so a wave reads a
-// kept record as one s_load_dwordx16 and composites from SGPR operands.
-constexpr int kSRecMaxD = 6;
-constexpr int kSA = 12, kSC = 13, kSB = 14, kSMAX = 15;
 
 struct Args {
   int C, W, H, tw, th, n_tiles;
@@ -155,8 +149,7 @@ struct Args {
   int SL;  // split tiles: isects per chunk (a multiple of L)
   const float *render_colors_in;  // backward: forward colours (for suffix sums)
   int dbg;  // debug flags (gsplat_hip_debug_set_flags): bit 0 = backward skips its
-            // atomics, bit 1 = split chunks never wait for a published product,
-            // bit 3 = scalar-operand forward (host side, fwd_srec)
+            // atomics, bit 1 = split chunks never wait for a published product
   uint64_t *timeline;  // debug: per-wave (start, end) s_memrealtime stamps or null
   unsigned long long *lanehist;  // debug: histogram of contributing lanes per (record, wave)
 };
@@ -546,9 +539,7 @@ GS_INLINE float chunk_product(const Args &a, const WaveGeom &geo, int64_t start,
 // One work item of the forward: SPLIT = chunk `item` of the split tiles'
 // list, else the whole tile `item` of the dispatch order (past the plan's
 // count of whole tiles: nothing).
-typedef __attribute__((address_space(4))) const float cfloat_t;
-
-template <int D, bool SPLIT, bool SREC = false>
+template <int D, bool SPLIT>
 GS_INLINE void fwd_item(const Args &a, float4 *st, int item) {
   using P = FwdPair<D>;
   constexpr int N4 = P::N4;
@@ -649,46 +640,12 @@ GS_INLINE void fwd_item(const Args &a, float4 *st, int item) {
     };
     // composite one staged batch pair by pair, checking every 8 pairs
     // whether the strip is alive
-    // SREC: the staged batch's kept mask and the lanes' record rows
-    uint64_t km_s = 0;
-    int32_t gc_s = 0;
-    int b_s = 0;
     auto composite = [&](int cnt) {
       const int np = (cnt + 1) >> 1;
       for (int pb = 0; pb < np; pb += 8) {
         const int pe = min(np, pb + 8);
         for (int p = pb; p < pe; ++p) {
           f2v f[2 * N4];
-          if constexpr (SREC) {
-            // the pair's two records from scalar loads (the second a pad --
-            // x = NaN, the rest 0, as stage_fwd_pad -- when cnt is odd)
-            const int t0 = __builtin_ctzll(km_s);
-            km_s &= km_s - 1;
-            const bool two = km_s != 0;
-            const int t1 = two ? __builtin_ctzll(km_s) : t0;
-            km_s &= km_s - 1;
-            cfloat_t *r0 = (cfloat_t *)a.records +
-                           (int64_t)kRecFloats * __builtin_amdgcn_readlane(gc_s, t0);
-            cfloat_t *r1 = (cfloat_t *)a.records +
-                           (int64_t)kRecFloats * __builtin_amdgcn_readlane(gc_s, t1);
-            float q0[kRecFloats], q1[kRecFloats];
-#pragma unroll
-            for (int i = 0; i < kRecFloats; ++i) {
-              q0[i] = r0[i];
-              q1[i] = r1[i];
-            }
-            const float nan = __int_as_float(0x7fc00000);
-            f[0] = f2v{q0[0], two ? q1[0] : nan};
-            f[1] = f2v{q0[1], q1[1]};
-            f[2] = f2v{q0[kSA], q1[kSA]};
-            f[3] = f2v{q0[kSB], q1[kSB]};
-            f[4] = f2v{q0[kSC], q1[kSC]};
-            f[5] = f2v{q0[5], two ? q1[5] : 0.f};
-            f[6] = f2v{q0[kSMAX], two ? q1[kSMAX] : 0.f};
-            f[7] = f2v{__int_as_float(b_s + t0), two ? __int_as_float(b_s + t1) : 0.f};
-#pragma unroll
-            for (int d = 0; d < D; ++d) f[8 + d] = f2v{q0[6 + d], two ? q1[6 + d] : 0.f};
-          } else {
           float4 v[N4];
 #pragma unroll
           for (int i = 0; i < N4; ++i) v[i] = st[p * N4 + i];
@@ -698,7 +655,6 @@ GS_INLINE void fwd_item(const Args &a, float4 *st, int item) {
             asm volatile("" ::"v"(v[i].x), "v"(v[i].y), "v"(v[i].z), "v"(v[i].w));
             f[2 * i] = f2v{v[i].x, v[i].y};
             f[2 * i + 1] = f2v{v[i].z, v[i].w};
-          }
           }
           const f2v dx = f[0] - fx, dy = f[1] - fy;
           const f2v s2 = dx * (f[2] * dx + f[3] * dy) + f[4] * dy * dy;  // sigma * log2(e)
@@ -721,12 +677,6 @@ GS_INLINE void fwd_item(const Args &a, float4 *st, int item) {
       const bool keep = (b0 + lane < re) && keep_attr<D>(at, geo.x0, geo.x1, geo.y0, geo.y1);
       const uint64_t m = __ballot(keep);
       const int cnt = __popcll(m);
-      if constexpr (SREC) {  // nothing staged: composite reads the kept rows itself
-        km_s = m;
-        gc_s = at.g;
-        b_s = b0;
-        return cnt;
-      }
       if (keep) stage_fwd_pair<D>(st, ballot_slot(m), at, (int32_t)(b0 + lane));
       // the odd slot of a final half-filled pair
       if ((cnt & 1) && lane == 0) stage_fwd_pad<D>(st, cnt);
@@ -867,7 +817,7 @@ GS_INLINE void fwd_item(const Args &a, float4 *st, int item) {
 // first: they are the longest work) and the other tiles in one launch, so the
 // chunks overlap the whole tiles; else the whole tiles only (the split path's
 // code costs registers: 80 -> 95 VGPRs, 6 -> 5 waves per SIMD at D = 3).
-template <int D, bool SPLIT = false, bool SREC = false>
+template <int D, bool SPLIT = false>
 __global__ void __launch_bounds__(256)
 __attribute__((amdgpu_waves_per_eu(!SPLIT && D <= 3 ? 6 : 5))) fwd_kernel(Args a) {
   __shared__ float4 stage_all[4][32 * FwdPair<D>::N4];
@@ -875,11 +825,11 @@ __attribute__((amdgpu_waves_per_eu(!SPLIT && D <= 3 ? 6 : 5))) fwd_kernel(Args a
   if constexpr (SPLIT) {
     const int nc = a.n_chunks[0];
     if ((int)blockIdx.x < nc)
-      fwd_item<D, true, SREC>(a, st, (int)blockIdx.x);
+      fwd_item<D, true>(a, st, (int)blockIdx.x);
     else
-      fwd_item<D, false, SREC>(a, st, (int)blockIdx.x - nc);
+      fwd_item<D, false>(a, st, (int)blockIdx.x - nc);
   } else {
-    fwd_item<D, false, SREC>(a, st, (int)blockIdx.x);
+    fwd_item<D, false>(a, st, (int)blockIdx.x);
   }
 }
 
@@ -1610,7 +1560,7 @@ __global__ void __launch_bounds__(256)
 pack_records_kernel(int64_t G, const float *__restrict__ means2d, const float *__restrict__ conics,
                     const float *__restrict__ colors, const float *__restrict__ opacities,
                     const int32_t *__restrict__ visible, const int32_t *__restrict__ vis_rank,
-                    float *__restrict__ records, int srec) {
+                    float *__restrict__ records) {
   const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= G) return;
   // both loads issued together (the rank does not wait for the visibility)
@@ -1635,24 +1585,9 @@ pack_records_kernel(int64_t G, const float *__restrict__ means2d, const float *_
   float4 *o = reinterpret_cast<float4 *>(records + row * kRecFloats);
 #pragma unroll
   for (int q = 0; q < N4; ++q) o[q] = make_float4(r[4 * q], r[4 * q + 1], r[4 * q + 2], r[4 * q + 3]);
-  if (D <= kSRecMaxD && srec)  // stage_fwd_pair's expressions
-    o[3] = make_float4(0.5f * kLog2e * r[2], 0.5f * kLog2e * r[4], kLog2e * r[3],
-                       __builtin_amdgcn_logf(255.f * r[5]));
 }
 
 }  // namespace r16
-
-// GSPLAT_HIP_FWD_SREC=1 (or debug flag bit 3, gsplat_hip_debug_set_flags):
-// the scalar-operand forward (fwd_kernel<D, SPLIT, true>) where the records
-// allow it
-static int dbg_flags();
-static bool fwd_srec() {
-  static const bool v = [] {
-    const char *e = getenv("GSPLAT_HIP_FWD_SREC");
-    return e && atoi(e) == 1;
-  }();
-  return v || (dbg_flags() & 8);
-}
 
 int rasterize16_record_floats(int D) {
   return (D >= 1 && D <= r16::kRecMaxD) ? r16::kRecFloats : 0;
@@ -1671,7 +1606,7 @@ int rasterize16_pack_records(int64_t G, int D, const float *means2d, const float
 #define GS_PACK(DD)                                                                              \
   case DD:                                                                                       \
     hipLaunchKernelGGL(r16::pack_records_kernel<DD>, grid, dim3(256), 0, st, G, means2d, conics, \
-                       colors, opacities, visible, vis_rank, records, fwd_srec() ? 1 : 0);     \
+                       colors, opacities, visible, vis_rank, records);                          \
     break;
     GS_PACK(1) GS_PACK(2) GS_PACK(3) GS_PACK(4) GS_PACK(5) GS_PACK(6) GS_PACK(7) GS_PACK(8)
     GS_PACK(9) GS_PACK(10)
@@ -1907,8 +1842,6 @@ int r16_fwd(r16::Args a, const void *state, char *split_base, hipStream_t st) {
     launch_order(a.n_tiles, a.offsets, a.n_isects, a.n_dev, const_cast<int32_t *>(a.order), st,
                  split_base, D);
   g_prepared_state = nullptr;
-  constexpr bool srec_ok = D <= r16::kSRecMaxD;
-  const bool srec = srec_ok && a.records && fwd_srec();
   if (split_base) {
     // the split tiles' chunks and the other tiles in one launch; the grid is
     // an upper bound (the plan's counts are on the device; surplus
@@ -1916,19 +1849,12 @@ int r16_fwd(r16::Args a, const void *state, char *split_base, hipStream_t st) {
     const int64_t nc = std::min<int64_t>(
         (int64_t)a.n_tiles + a.n_isects / a.SL + 1,
         a.n_isects / a.SL + a.n_isects / std::max<int64_t>(1, split_threshold(a.n_isects)) + 1);
-    if (srec)
-      hipLaunchKernelGGL((r16::fwd_kernel<D, true, srec_ok>), dim3((unsigned)(a.n_tiles + nc)),
-                         dim3(256), 0, st, a);
-    else
-      hipLaunchKernelGGL((r16::fwd_kernel<D, true>), dim3((unsigned)(a.n_tiles + nc)), dim3(256),
-                         0, st, a);
+    hipLaunchKernelGGL((r16::fwd_kernel<D, true>), dim3((unsigned)(a.n_tiles + nc)), dim3(256),
+                       0, st, a);
     GS_CHECK_LAUNCH("rasterize_fwd16_split");
     return 0;
   }
-  if (srec)
-    hipLaunchKernelGGL((r16::fwd_kernel<D, false, srec_ok>), dim3(a.n_tiles), dim3(256), 0, st, a);
-  else
-    hipLaunchKernelGGL((r16::fwd_kernel<D>), dim3(a.n_tiles), dim3(256), 0, st, a);
+  hipLaunchKernelGGL((r16::fwd_kernel<D>), dim3(a.n_tiles), dim3(256), 0, st, a);
   GS_CHECK_LAUNCH("rasterize_fwd16");
   return 0;
 }

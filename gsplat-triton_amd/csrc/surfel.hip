@@ -1158,10 +1158,10 @@ __global__ void __launch_bounds__(256) bwd_kernel(RasterArgs a) {
     vc[d] = a.v_render_colors[pid * D + d];
     buf[d] = 0.f;
   }
-  const float va = a.v_render_alphas[pid];
+  const float va = a.v_render_alphas ? a.v_render_alphas[pid] : 0.f;
   float vn[3], bufn[3] = {0.f, 0.f, 0.f};
 #pragma unroll
-  for (int i = 0; i < 3; ++i) vn[i] = a.v_render_normals[pid * 3 + i];
+  for (int i = 0; i < 3; ++i) vn[i] = a.v_render_normals ? a.v_render_normals[pid * 3 + i] : 0.f;
   const float vdist = a.v_render_distort ? a.v_render_distort[pid] : 0.f;
   const float accum_d = a.render_colors[pid * D + D - 1], accum_w = 1.f - Tf;
   float accd_buf = accum_d, accw_buf = accum_w, dist_buf = 0.f;
@@ -1335,10 +1335,10 @@ __global__ void __launch_bounds__(128) bwd2_kernel(RasterArgs a) {
       s.buf[d] = 0.f;
       if (a.backgrounds) bg_dot += a.backgrounds[(int64_t)c * D + d] * s.vc[d];
     }
-    s.tfvb = Tf * (a.v_render_alphas[pid] - bg_dot);
+    s.tfvb = Tf * ((a.v_render_alphas ? a.v_render_alphas[pid] : 0.f) - bg_dot);
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
-      s.vn[i] = a.v_render_normals[pid * 3 + i];
+      s.vn[i] = a.v_render_normals ? a.v_render_normals[pid * 3 + i] : 0.f;
       s.bufn[i] = 0.f;
     }
     s.vdist = a.v_render_distort ? a.v_render_distort[pid] : 0.f;
@@ -1822,7 +1822,7 @@ extern "C" int gsplat_hip_rasterize_2dgs_bwd(
   const int n_tiles = C * tile_width * tile_height;
   if (n_tiles > 0 && n_isects > 0 && width > 0 && height > 0) {
     GS_REQUIRE(isect_offsets && flatten_ids && render_colors && render_alphas && last_ids &&
-                   median_ids && v_render_colors && v_render_alphas && v_render_normals,
+                   median_ids && v_render_colors,
                "rasterize_2dgs_bwd: null pointer argument");
     RasterArgs a{};
     a.C = C; a.W = width; a.H = height; a.ts = tile_size; a.tw = tile_width;

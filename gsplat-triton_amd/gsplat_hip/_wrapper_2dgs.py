@@ -204,7 +204,8 @@ def fully_fused_projection_2dgs(
 _SUPPORTED_D = (1, 2, 3, 4, 5, 6, 7, 8, 9, 16, 17, 32, 33)
 # the forward composites from scalar-operand records (csrc/surfel.hip
 # fwd2s_kernel) where the configuration has them
-SREC = os.environ.get("GSPLAT_HIP_SURFEL_SREC", "0") == "1"
+# (GSPLAT_HIP_SURFEL_SREC=0: the LDS-queue forward, fwd2_kernel)
+SREC = os.environ.get("GSPLAT_HIP_SURFEL_SREC", "1") != "0"
 
 
 class _RasterizeToPixels2DGS(torch.autograd.Function):
@@ -253,6 +254,9 @@ class _RasterizeToPixels2DGS(torch.autograd.Function):
         ctx.width, ctx.height, ctx.tile_size = int(width), int(height), int(tile_size)
         ctx.absgrad, ctx.distloss = absgrad, distloss
         ctx.n_dev = n_dev
+        # outputs without a loss term (alphas, normals, distortion, median in
+        # the trainer's RGB loss): None in the backward, not zero-filled images
+        ctx.set_materialize_grads(False)
         return render_colors, render_alphas, render_normals, render_distort, render_median
 
     @staticmethod
@@ -270,8 +274,8 @@ class _RasterizeToPixels2DGS(torch.autograd.Function):
             return torch.zeros(shape, device=dev) if t is None else _f32c(t)
 
         v_render_colors = grad(v_render_colors, (C, H, W, D))
-        v_render_alphas = grad(v_render_alphas, (C, H, W, 1))
-        v_render_normals = grad(v_render_normals, (C, H, W, 3))
+        v_render_alphas = None if v_render_alphas is None else _f32c(v_render_alphas)
+        v_render_normals = None if v_render_normals is None else _f32c(v_render_normals)
         v_render_distort = None if v_render_distort is None else _f32c(v_render_distort)
         v_render_median = None if v_render_median is None else _f32c(v_render_median)
         G = opacities.numel()

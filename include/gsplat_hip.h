@@ -359,9 +359,7 @@ int gsplat_hip_set_fwd_split_div(int div);
  * bit 0 = the backward skips its gradient atomics (timing experiments);
  * bit 1 = a chunk of a split tile never waits for an earlier chunk's
  * published product and computes it itself (the timeout path; results are
- * identical); bit 3 = the forward composites from scalar-operand records
- * (as GSPLAT_HIP_FWD_SREC=1; records packed by later renders carry its
- * fields; results are identical).  Returns the previous flags. */
+ * identical).  Returns the previous flags. */
 int gsplat_hip_debug_set_flags(int flags);
 
 /* ---------------------------------------------------------------------------
@@ -720,7 +718,8 @@ int gsplat_hip_rasterize_2dgs_fwd(int C, int D, int width, int height, int tile_
  *    v_normals[G,3], v_densify[G,2] = (v_rt[0][2], v_rt[1][2]) * rt[2][2]
  *    (formed from the final sums; the reference writes it racily from partial
  *    sums), v_means2d_abs[G,2] or NULL (absgrad off).
- * v_render_distort / v_render_median may be NULL (no gradient). */
+ * v_render_alphas / v_render_normals (ABI 32) / v_render_distort /
+ * v_render_median may be NULL (no gradient). */
 int64_t gsplat_hip_rasterize_2dgs_bwd_workspace_bytes(int64_t n_gaussians, int D, int absgrad);
 int gsplat_hip_rasterize_2dgs_bwd(
     int C, int D, int width, int height, int tile_size, int tile_width, int tile_height,

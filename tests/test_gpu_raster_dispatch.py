@@ -261,33 +261,3 @@ def test_split_forward_vs_oracle():
     from test_gpu_parity import close_most
     close_most(ra, oa, 1e-4, 1e-4, "alphas", max_frac=1e-3)
     close_most(rc, oc, 1e-4, 1e-4, "colors", max_frac=1e-3)
-
-
-
-@pytest.mark.parametrize("split,mode", [(0, "RGB"), (300, "RGB"), (0, "RGB+D")])
-def test_scalar_record_forward_is_bit_identical(split, mode):
-    """The scalar-operand forward (debug flag bit 3 / GSPLAT_HIP_FWD_SREC=1:
-    kept records read with s_load and composited from SGPR operands, no LDS
-    staging) renders what the LDS-pair forward renders -- the same pairs, the
-    same per-record arithmetic on the same record values, up to the
-    compiler's FMA contraction (7.7e-7 seen in the colours) -- with and
-    without split heavy tiles; the backward, which reads the forward's chunk
-    state and last ids, to the order of its atomics."""
-    from gsplat_hip import _lib
-    ins, W, H = _heavy_scene()
-    outs = []
-    for flag in (0, 8):
-        old = _lib.query("gsplat_hip_debug_set_flags", flag)
-        try:
-            outs.append(_render_split(ins, W, H, split, mode))
-        finally:
-            _lib.query("gsplat_hip_debug_set_flags", old)
-    (rc0, ra0, _, g0), (rc1, ra1, _, g1) = outs
-    print(f"colors {float((rc0 - rc1).abs().max()):.3e} alphas {float((ra0 - ra1).abs().max()):.3e}")
-    torch.testing.assert_close(rc1, rc0, rtol=1e-5, atol=1e-5)
-    torch.testing.assert_close(ra1, ra0, rtol=1e-5, atol=1e-5)
-    from test_gpu_parity import close_most
-    for a, b, name in zip(g1, g0, NAMES):
-        scale = max(1e-12, float(b.abs().max()))
-        close_most(a, b, 1e-3, 1e-4 * scale, name, max_frac=2e-3, rows=True,
-                   out_bound=0.05 * scale)
