@@ -1468,195 +1468,6 @@ __global__ void __launch_bounds__(128) bwd2_kernel(RasterArgs a) {
   }
 }
 
-// Backward from the scalar-operand records (fwd2s_kernel's table, GSPLAT_HIP_SURFEL_SREC):
-// culling from the record fields, the kept records read with scalar loads
-// instead of the LDS queue.  Same per-pixel arithmetic as bwd2_kernel.
-template <int D, bool ABS, int WPE = 3>
-__global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE)))
-bwd2s_kernel(RasterArgs a, const float *__restrict__ rec) {
-  using R = Rec<D>;
-  using F = Fields<D, ABS>;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int tile = blockIdx.x;
-  if (a.masks && !a.masks[tile]) return;
-  const int ntile = a.tw * a.th;
-  const int c = tile / ntile;
-  const int rem = tile - c * ntile;
-  const int ty = rem / a.tw, tx = rem - ty * a.tw;
-  const int64_t start = a.offsets[tile];
-  const int64_t tend = (tile == a.n_tiles - 1) ? (a.n_dev ? a.n_dev[0] : a.n_isects)
-                                               : (int64_t)a.offsets[tile + 1];
-  const float rx0 = tx * 16 + 0.5f, rx1 = rx0 + 15.f;
-  const float ry0 = ty * 16 + 8 * w + 0.5f, ry1 = ry0 + 7.f;
-  PixState<D> ps[2];
-  int32_t wmax = 0;
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    PixState<D> &s = ps[k];
-    const int px = tx * 16 + (lane & 15), py = ty * 16 + 8 * w + 4 * k + (lane >> 4);
-    s.inside = px < a.W && py < a.H;
-    const int64_t pid = (int64_t)c * a.H * a.W + (s.inside ? (int64_t)py * a.W + px : 0);
-    s.fx = (float)px + 0.5f;
-    s.fy = (float)py + 0.5f;
-    const float Tf = 1.f - a.render_alphas[pid];
-    s.T = Tf;
-    s.bin_final = s.inside ? a.last_ids[pid] : 0;
-    s.med_idx = s.inside ? a.median_ids[pid] : 0;
-    float bg_dot = 0.f;
-#pragma unroll
-    for (int d = 0; d < D; ++d) {
-      s.vc[d] = a.v_render_colors[pid * D + d];
-      s.buf[d] = 0.f;
-      if (a.backgrounds) bg_dot += a.backgrounds[(int64_t)c * D + d] * s.vc[d];
-    }
-    s.tfvb = Tf * ((a.v_render_alphas ? a.v_render_alphas[pid] : 0.f) - bg_dot);
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      s.vn[i] = a.v_render_normals ? a.v_render_normals[pid * 3 + i] : 0.f;
-      s.bufn[i] = 0.f;
-    }
-    s.vdist = a.v_render_distort ? a.v_render_distort[pid] : 0.f;
-    s.accum_d = a.render_colors[pid * D + D - 1];
-    s.accum_w = 1.f - Tf;
-    s.accd_buf = s.accum_d;
-    s.accw_buf = s.accum_w;
-    s.dist_buf = 0.f;
-    s.vmed = a.v_render_median ? a.v_render_median[pid] : 0.f;
-    wmax = max(wmax, s.bin_final);
-  }
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) wmax = max(wmax, __shfl_xor(wmax, m, 64));
-  const int64_t end = min(tend, (int64_t)wmax + 1);
-  const int lf = rs_field(lane);
-
-  for (int64_t b1 = end; b1 > start; b1 -= 64) {
-    const int64_t b0 = max(start, b1 - 64);
-    uint64_t km;
-    int32_t gc;
-    {
-      const int64_t j = b0 + lane;
-      gc = j < b1 ? a.flatten_ids[j] : 0;
-      SCull kc;
-      srec_load_cull(rec, gc, kc);
-      const bool keep = (j < b1) && srec_keep(kc, rx0, rx1, ry0, ry1);
-      km = __ballot(keep);
-    }
-    // the kept records back to front, each read with scalar loads: the
-    // record's position, opacity, normal and colour, and the ray transform
-    while (km) {
-      const int t = 63 - __builtin_clzll(km);
-      km &= ~(1ull << t);
-      const int32_t gi = __builtin_amdgcn_readlane(gc, t);
-      const int32_t idx = (int32_t)(b0 + t);
-      cfloat_t *p = (cfloat_t *)rec + (int64_t)srec::NF * gi;
-      cfloat_t *pm = (cfloat_t *)a.ray_transforms + 9 * (int64_t)gi;
-      float r[R::NF];
-      r[R::X] = p[srec::X];
-      r[R::Y] = p[srec::Y];
-      r[R::OP] = p[srec::OP];
-#pragma unroll
-      for (int i = 0; i < 9; ++i) r[R::M + i] = pm[i];
-      r[R::G] = __int_as_float(gi);
-      r[R::NRM] = p[srec::NRM0];
-      r[R::NRM + 1] = p[srec::NRM1];
-      r[R::NRM + 2] = p[srec::NRM2];
-#pragma unroll
-      for (int d = 0; d < D; ++d) r[R::COL + d] = p[srec::COL + d];
-      const float *m = r + R::M;
-      Hit h[2];
-      bool valid[2];
-#pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        h[k] = eval_hit(m, r[R::X], r[R::Y], r[R::OP], ps[k].fx, ps[k].fy);
-        valid[k] = ps[k].inside && idx <= ps[k].bin_final && h[k].ok;
-      }
-      if (__ballot(valid[0] | valid[1]) == 0) continue;
-      float v[16 * F::NV];
-#pragma unroll
-      for (int kk = 0; kk < 16 * F::NV; ++kk) v[kk] = 0.f;
-#pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        PixState<D> &s = ps[k];
-        const Hit &hk = h[k];
-        if (!valid[k]) continue;
-        if (idx == s.med_idx) v[F::COL + D - 1] += s.vmed;
-        const float ra = __builtin_amdgcn_rcpf(1.f - hk.alpha);
-        s.T *= ra;
-        const float T = s.T;
-        const float fac = hk.alpha * T;
-        float v_alpha = 0.f;
-#pragma unroll
-        for (int d = 0; d < D; ++d) {
-          v[F::COL + d] += fac * s.vc[d];
-          v_alpha += (r[R::COL + d] * T - s.buf[d] * ra) * s.vc[d];
-        }
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-          v[F::NRM + i] += fac * s.vn[i];
-          v_alpha += (r[R::NRM + i] * T - s.bufn[i] * ra) * s.vn[i];
-        }
-        v_alpha += ra * s.tfvb;
-        {  // distortion (RasterizeToPixels2DGSBwd.cu:483-503)
-          const float depth = r[R::COL + D - 1];
-          const float dl_dw =
-              2.f * (2.f * (depth * s.accw_buf - s.accd_buf) + (s.accum_d - depth * s.accum_w));
-          v_alpha += (dl_dw * T - s.dist_buf * ra) * s.vdist;
-          s.accd_buf -= fac * depth;
-          s.accw_buf -= fac;
-          s.dist_buf += dl_dw * fac;
-          v[F::COL + D - 1] += 2.f * fac * (2.f - 2.f * T - s.accum_w + fac) * s.vdist;
-        }
-        if (r[R::OP] * hk.vis <= kAlphaMax) {
-          const float vG = r[R::OP] * v_alpha;
-          if (hk.g3 <= hk.g2) {
-            const float vsx = vG * -hk.vis * hk.s[0], vsy = vG * -hk.vis * hk.s[1];
-            const float iz = __builtin_amdgcn_rcpf(hk.rc[2]);
-            const float ax = vsx * iz, ay = vsy * iz;
-            const float vrc[3] = {ax, ay, -(ax * hk.s[0] + ay * hk.s[1])};
-            const float vhu[3] = {hk.hv[1] * vrc[2] - hk.hv[2] * vrc[1],
-                                  hk.hv[2] * vrc[0] - hk.hv[0] * vrc[2],
-                                  hk.hv[0] * vrc[1] - hk.hv[1] * vrc[0]};
-            const float vhv[3] = {vrc[1] * hk.hu[2] - vrc[2] * hk.hu[1],
-                                  vrc[2] * hk.hu[0] - vrc[0] * hk.hu[2],
-                                  vrc[0] * hk.hu[1] - vrc[1] * hk.hu[0]};
-#pragma unroll
-            for (int i = 0; i < 3; ++i) {
-              v[F::M + i] -= vhu[i];
-              v[F::M + 3 + i] -= vhv[i];
-              v[F::M + 6 + i] += s.fx * vhu[i] + s.fy * vhv[i];
-            }
-          } else {
-            const float dx = r[R::X] - s.fx, dy = r[R::Y] - s.fy;
-            const float gx = vG * (-hk.vis * kFilterInvSquare * dx);
-            const float gy = vG * (-hk.vis * kFilterInvSquare * dy);
-            v[F::XY] += gx;
-            v[F::XY + 1] += gy;
-            if (ABS) {
-              v[F::AB] += fabsf(gx);
-              v[F::AB + 1] += fabsf(gy);
-            }
-          }
-          v[F::OP] += hk.vis * v_alpha;
-        }
-#pragma unroll
-        for (int d = 0; d < D; ++d) s.buf[d] += r[R::COL + d] * fac;
-#pragma unroll
-        for (int i = 0; i < 3; ++i) s.bufn[i] += r[R::NRM + i] * fac;
-      }
-      const int32_t g = __float_as_int(r[R::G]);
-      float *row = a.packed + (int64_t)g * F::S;
-#pragma unroll
-      for (int kq = 0; kq < F::NV; ++kq) {
-        constexpr int NQ = F::NF - 16 * (F::NV - 1);
-        const float tot = kq < F::NV - 1 ? reduce_scatter<16>(v + 16 * kq, lane)
-                                         : reduce_scatter<NQ>(v + 16 * kq, lane);
-        if ((lane & 3) == 0 && lf < (kq < F::NV - 1 ? 16 : NQ) && tot != 0.f)
-          atomic_add_f32(row + 16 * kq + lf, tot);
-      }
-    }
-  }
-}
-
 // packed [G][S] -> autograd tensors; densify = (v_M[0][2], v_M[1][2]) * depth
 // with depth = M[2][2] (the reference writes this racily from partial sums,
 // RasterizeToPixels2DGSBwd.cu:689-697; here it is formed from the final sums).
@@ -1706,16 +1517,6 @@ bool fwd2_enabled() {
   static const bool v = [] {
     const char *e = getenv("GSPLAT_HIP_FWD_PX");
     return !(e && atoi(e) == 1);
-  }();
-  return v;
-}
-
-// GSPLAT_HIP_SURFEL_BWD_W4=1: the scalar-record backward limited to 128 VGPRs
-// (4 waves per SIMD, a few spills) instead of 145 (3 waves)
-bool bwd_w4() {
-  static const bool v = [] {
-    const char *e = getenv("GSPLAT_HIP_SURFEL_BWD_W4");
-    return e && atoi(e) == 1;
   }();
   return v;
 }
@@ -1997,9 +1798,9 @@ extern "C" int gsplat_hip_rasterize_2dgs_bwd(
     int64_t n_gaussians, const float *means2d, const float *ray_transforms, const float *colors,
     const float *opacities, const float *normals, const float *backgrounds,
     const uint8_t *masks, const int32_t *isect_offsets, int64_t n_isects,
-    const int64_t *n_isects_device, const int32_t *flatten_ids, const float *records,
-    const float *render_colors, const float *render_alphas,
-    const int32_t *last_ids, const int32_t *median_ids, const float *v_render_colors,
+    const int64_t *n_isects_device, const int32_t *flatten_ids, const float *render_colors,
+    const float *render_alphas, const int32_t *last_ids, const int32_t *median_ids,
+    const float *v_render_colors,
     const float *v_render_alphas, const float *v_render_normals, const float *v_render_distort,
     const float *v_render_median, float *v_means2d, float *v_ray_transforms, float *v_colors,
     float *v_opacities, float *v_normals, float *v_densify, float *v_means2d_abs,
@@ -2040,22 +1841,10 @@ extern "C" int gsplat_hip_rasterize_2dgs_bwd(
     const int waves = (tile_size * tile_size + 63) / 64;
     // 16x16 tiles: two pixels per lane (bwd2_kernel) unless GSPLAT_HIP_BWD_PX=1
     const bool px2 = tile_size == 16 && bwd2_enabled();
-    const bool srec = records != nullptr;
-    GS_REQUIRE(!srec || (px2 && D <= kSRecMaxD),
-               "rasterize_2dgs_bwd: records need 16x16 tiles, D <= %d", kSRecMaxD);
 #define GS_CASE(n)                                                                            \
   if (D == n) {                                                                               \
     const size_t lds = (size_t)waves * 64 * Rec<n>::NF * sizeof(float);                       \
-    if (srec && absgrad)                                                                      \
-      hipLaunchKernelGGL((bwd2s_kernel<(n <= kSRecMaxD ? n : 1), true>), dim3(n_tiles),       \
-                         dim3(128), 0, st, a, records);                                       \
-    else if (srec && bwd_w4())                                                                \
-      hipLaunchKernelGGL((bwd2s_kernel<(n <= kSRecMaxD ? n : 1), false, 4>), dim3(n_tiles),   \
-                         dim3(128), 0, st, a, records);                                       \
-    else if (srec)                                                                            \
-      hipLaunchKernelGGL((bwd2s_kernel<(n <= kSRecMaxD ? n : 1), false>), dim3(n_tiles),      \
-                         dim3(128), 0, st, a, records);                                       \
-    else if (px2 && absgrad)                                                                  \
+    if (px2 && absgrad)                                                                       \
       hipLaunchKernelGGL((bwd2_kernel<n, true>), dim3(n_tiles), dim3(128), lds / 2, st, a);    \
     else if (px2)                                                                             \
       hipLaunchKernelGGL((bwd2_kernel<n, false>), dim3(n_tiles), dim3(128), lds / 2, st, a);   \

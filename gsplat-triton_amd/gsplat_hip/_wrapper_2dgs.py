@@ -206,8 +206,6 @@ _SUPPORTED_D = (1, 2, 3, 4, 5, 6, 7, 8, 9, 16, 17, 32, 33)
 # fwd2s_kernel) where the configuration has them
 # (GSPLAT_HIP_SURFEL_SREC=0: the LDS-queue forward, fwd2_kernel)
 SREC = os.environ.get("GSPLAT_HIP_SURFEL_SREC", "1") != "0"
-# the backward reads the forward's records too (GSPLAT_HIP_SURFEL_SREC_BWD)
-SREC_BWD = os.environ.get("GSPLAT_HIP_SURFEL_SREC_BWD", "0") == "1"
 
 
 class _RasterizeToPixels2DGS(torch.autograd.Function):
@@ -252,7 +250,7 @@ class _RasterizeToPixels2DGS(torch.autograd.Function):
                       _ptr(median_ids), _stream())
         ctx.save_for_backward(means2d, ray_transforms, colors, opacities, normals, densify,
                               backgrounds, masks_u8, isect_offsets, flatten_ids, render_colors,
-                              render_alphas, last_ids, median_ids, records)
+                              render_alphas, last_ids, median_ids)
         ctx.width, ctx.height, ctx.tile_size = int(width), int(height), int(tile_size)
         ctx.absgrad, ctx.distloss = absgrad, distloss
         ctx.n_dev = n_dev
@@ -266,7 +264,7 @@ class _RasterizeToPixels2DGS(torch.autograd.Function):
                  v_render_median):
         (means2d, ray_transforms, colors, opacities, normals, densify, backgrounds, masks_u8,
          isect_offsets, flatten_ids, render_colors, render_alphas, last_ids,
-         median_ids, records) = ctx.saved_tensors
+         median_ids) = ctx.saved_tensors
         C, th, tw = isect_offsets.shape
         D = colors.shape[-1]
         H, W = ctx.height, ctx.width
@@ -294,8 +292,7 @@ class _RasterizeToPixels2DGS(torch.autograd.Function):
             _lib.call("gsplat_hip_rasterize_2dgs_bwd", C, D, W, H, ctx.tile_size, tw, th, G,
                       _ptr(means2d), _ptr(ray_transforms), _ptr(colors), _ptr(opacities),
                       _ptr(normals), _ptr(backgrounds), _ptr(masks_u8), _ptr(isect_offsets),
-                      flatten_ids.numel(), _ptr(ctx.n_dev), _ptr(flatten_ids),
-                      _ptr(records if SREC_BWD else None), _ptr(render_colors),
+                      flatten_ids.numel(), _ptr(ctx.n_dev), _ptr(flatten_ids), _ptr(render_colors),
                       _ptr(render_alphas), _ptr(last_ids), _ptr(median_ids),
                       _ptr(v_render_colors), _ptr(v_render_alphas), _ptr(v_render_normals),
                       _ptr(v_render_distort), _ptr(v_render_median), _ptr(v_means2d),

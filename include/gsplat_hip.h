@@ -719,18 +719,15 @@ int gsplat_hip_rasterize_2dgs_fwd(int C, int D, int width, int height, int tile_
  *    (formed from the final sums; the reference writes it racily from partial
  *    sums), v_means2d_abs[G,2] or NULL (absgrad off).
  * v_render_alphas / v_render_normals (ABI 32) / v_render_distort /
- * v_render_median may be NULL (no gradient).  records (ABI 32, may be NULL):
- * the forward's records (gsplat_hip_rasterize_2dgs_pack_records): the
- * backward then culls from them and reads the kept records with scalar
- * loads instead of its LDS queue. */
+ * v_render_median may be NULL (no gradient). */
 int64_t gsplat_hip_rasterize_2dgs_bwd_workspace_bytes(int64_t n_gaussians, int D, int absgrad);
 int gsplat_hip_rasterize_2dgs_bwd(
     int C, int D, int width, int height, int tile_size, int tile_width, int tile_height,
     int64_t n_gaussians, const float *means2d, const float *ray_transforms, const float *colors,
     const float *opacities, const float *normals, const float *backgrounds,
     const uint8_t *masks, const int32_t *isect_offsets, int64_t n_isects,
-    const int64_t *n_isects_device, const int32_t *flatten_ids, const float *records,
-    const float *render_colors, const float *render_alphas, const int32_t *last_ids, const int32_t *median_ids, const float *v_render_colors,
+    const int64_t *n_isects_device, const int32_t *flatten_ids, const float *render_colors,
+    const float *render_alphas, const int32_t *last_ids, const int32_t *median_ids, const float *v_render_colors,
     const float *v_render_alphas, const float *v_render_normals, const float *v_render_distort,
     const float *v_render_median, float *v_means2d, float *v_ray_transforms, float *v_colors,
     float *v_opacities, float *v_normals, float *v_densify, float *v_means2d_abs,

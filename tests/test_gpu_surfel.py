@@ -131,9 +131,8 @@ def test_raster2dgs_fwd_records_bit_identical(monkeypatch, seed, D, bg, C, thin,
     GSPLAT_HIP_SURFEL_SREC=1) renders what the LDS-queue forward renders: the
     same per-pixel arithmetic on the same record values, up to the
     compiler's FMA contraction of a few expressions (3.6e-7 seen in one of
-    the five outputs); the backward from the same records (bwd2s_kernel:
-    culling from the record fields, kept records read with scalar loads)
-    agrees with the LDS-queue backward to the order of its float atomics."""
+    the five outputs); the backward, which reads the forward's outputs and
+    last / median ids, agrees to the order of its float atomics."""
     from gsplat_hip import _lib, _wrapper_2dgs
     assert _lib.query("gsplat_hip_rasterize_2dgs_record_floats", D, 16) == 32
     sc = surfel_scene(seed, N=600, W=150, H=100, D=D, bg=bg, C=C, thin=thin)
@@ -141,7 +140,6 @@ def test_raster2dgs_fwd_records_bit_identical(monkeypatch, seed, D, bg, C, thin,
     res = []
     for srec in (False, True):
         monkeypatch.setattr(_wrapper_2dgs, "SREC", srec)
-        monkeypatch.setattr(_wrapper_2dgs, "SREC_BWD", srec)
         leaves, bgt, densify, out = _raster_gpu(sc, masks=masks)
         w = [torch.linspace(-1, 1, o.numel(), device=DEV).view_as(o) for o in out]
         sum((o * ww).sum() for o, ww in zip(out, w)).backward()
