@@ -324,6 +324,7 @@ struct RasterArgs {
   int C, W, H, ts, tw, th, n_tiles;
   int64_t n_isects;       // isect count, or with n_dev the capacity of flatten_ids
   const int64_t *n_dev;   // the isect count on the device (sync-free isect) or null
+  const int32_t *order;   // dispatch order of the tiles (heaviest first) or null
   const float *means2d, *ray_transforms, *colors, *opacities, *normals, *backgrounds;
   const uint8_t *masks;
   const int32_t *offsets, *flatten_ids;
@@ -601,7 +602,7 @@ __global__ void __launch_bounds__(1024) fwd_kernel(RasterArgs a) {
   extern __shared__ float4 lds4[];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   float *q = reinterpret_cast<float *>(lds4) + (size_t)w * 64 * R::NF;
-  const Pix p(a, blockIdx.x, w, lane);
+  const Pix p(a, a.order ? a.order[blockIdx.x] : (int)blockIdx.x, w, lane);
   const float fx = (float)p.px + 0.5f, fy = (float)p.py + 0.5f;
   const float *bg = a.backgrounds ? a.backgrounds + (int64_t)p.c * D : nullptr;
 
@@ -704,7 +705,7 @@ __global__ void __launch_bounds__(128) fwd2_kernel(RasterArgs a) {
   extern __shared__ float4 lds4[];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   float *q = reinterpret_cast<float *>(lds4) + (size_t)w * 64 * R::NF;
-  const int tile = blockIdx.x;
+  const int tile = a.order ? a.order[blockIdx.x] : (int)blockIdx.x;
   const int ntile = a.tw * a.th;
   const int c = tile / ntile;
   const int rem = tile - c * ntile;
@@ -834,6 +835,37 @@ __global__ void __launch_bounds__(128) fwd2_kernel(RasterArgs a) {
 // v_readlane of the candidate's id): the fields reach the VALU as SGPR
 // operands, with no LDS traffic at all.  Same per-pixel arithmetic and order
 // as fwd2_kernel (bit-identical outputs).
+// Dispatch order (GSPLAT_HIP_SURFEL_ORDER=1): the tiles bucketed by
+// floor(log2(isects)), heaviest bucket first, so the longest tiles start in
+// the first wave of workgroups instead of finishing last (order inside a
+// bucket: arrival at an LDS counter).  One workgroup.
+__global__ void __launch_bounds__(1024)
+tile_order_kernel(int n_tiles, const int32_t *__restrict__ offsets, int64_t n_isects,
+                  const int64_t *__restrict__ n_dev, int32_t *__restrict__ order) {
+  __shared__ int hist[34];
+  const int tid = threadIdx.x;
+  if (tid < 34) hist[tid] = 0;
+  __syncthreads();
+  const int64_t total = n_dev ? n_dev[0] : n_isects;
+  auto key = [&](int t) {
+    const int64_t e = t == n_tiles - 1 ? total : (int64_t)offsets[t + 1];
+    const int64_t n = e - offsets[t];
+    return n > 0 ? 32 - (63 - __builtin_clzll((uint64_t)n)) : 33;  // 2^31.. -> 1, 1 -> 32
+  };
+  for (int t = tid; t < n_tiles; t += 1024) atomicAdd(&hist[key(t)], 1);
+  __syncthreads();
+  if (tid == 0) {
+    int run = 0;
+    for (int k = 0; k < 34; ++k) {
+      const int h = hist[k];
+      hist[k] = run;
+      run += h;
+    }
+  }
+  __syncthreads();
+  for (int t = tid; t < n_tiles; t += 1024) order[atomicAdd(&hist[key(t)], 1)] = t;
+}
+
 constexpr int kSRecMaxD = 4;
 namespace srec {
 // floats of a record
@@ -988,7 +1020,7 @@ GS_INLINE void srec_load_blend(const float *rec, int32_t g, SBlend<D> &r) {
 template <int D>
 __global__ void __launch_bounds__(128) fwd2s_kernel(RasterArgs a, const float *__restrict__ rec) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int tile = blockIdx.x;
+  const int tile = a.order ? a.order[blockIdx.x] : (int)blockIdx.x;
   const int ntile = a.tw * a.th;
   const int c = tile / ntile;
   const int rem = tile - c * ntile;
@@ -1143,7 +1175,7 @@ __global__ void __launch_bounds__(256) bwd_kernel(RasterArgs a) {
   extern __shared__ float4 lds4[];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   float *q = reinterpret_cast<float *>(lds4) + (size_t)w * 64 * R::NF;
-  const Pix p(a, blockIdx.x, w, lane);
+  const Pix p(a, a.order ? a.order[blockIdx.x] : (int)blockIdx.x, w, lane);
   if (a.masks && !a.masks[p.tile]) return;
   const float fx = (float)p.px + 0.5f, fy = (float)p.py + 0.5f;
   const int64_t pid = p.pid;
@@ -1303,7 +1335,7 @@ __global__ void __launch_bounds__(128) bwd2_kernel(RasterArgs a) {
   extern __shared__ float4 lds4[];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   float *q = reinterpret_cast<float *>(lds4) + (size_t)w * 64 * R::NF;
-  const int tile = blockIdx.x;
+  const int tile = a.order ? a.order[blockIdx.x] : (int)blockIdx.x;
   if (a.masks && !a.masks[tile]) return;
   const int ntile = a.tw * a.th;
   const int c = tile / ntile;
@@ -1709,8 +1741,9 @@ extern "C" int gsplat_hip_rasterize_2dgs_fwd(
     const float *opacities, const float *normals, const float *backgrounds,
     const uint8_t *masks, const int32_t *isect_offsets, int64_t n_isects,
     const int64_t *n_isects_device, const int32_t *flatten_ids, const float *records,
-    float *render_colors, float *render_alphas, float *render_normals, float *render_distort,
-    float *render_median, int32_t *last_ids, int32_t *median_ids, void *stream) {
+    int32_t *tile_order, float *render_colors, float *render_alphas, float *render_normals,
+    float *render_distort, float *render_median, int32_t *last_ids, int32_t *median_ids,
+    void *stream) {
   if (int e = check_tiles(C, width, height, tile_size, tile_width, tile_height)) return e;
   GS_REQUIRE(channels_supported(D), "rasterize_2dgs_fwd: unsupported channel count %d", D);
   const int n_tiles = C * tile_width * tile_height;
@@ -1733,6 +1766,11 @@ extern "C" int gsplat_hip_rasterize_2dgs_fwd(
   a.render_median = render_median; a.last_ids = last_ids; a.median_ids = median_ids;
   const int waves = (tile_size * tile_size + 63) / 64;
   hipStream_t st = (hipStream_t)stream;
+  if (tile_order && n_tiles > 0) {  // written here, read by this launch and the backward
+    hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(1024), 0, st, n_tiles, isect_offsets,
+                       n_isects, n_isects_device, tile_order);
+    a.order = tile_order;
+  }
   // 16x16 tiles: two pixels per lane (fwd2_kernel) unless GSPLAT_HIP_FWD_PX=1
   const bool px2 = tile_size == 16 && fwd2_enabled();
   if (records) {  // scalar-operand records (gsplat_hip_rasterize_2dgs_pack_records)
@@ -1798,9 +1836,9 @@ extern "C" int gsplat_hip_rasterize_2dgs_bwd(
     int64_t n_gaussians, const float *means2d, const float *ray_transforms, const float *colors,
     const float *opacities, const float *normals, const float *backgrounds,
     const uint8_t *masks, const int32_t *isect_offsets, int64_t n_isects,
-    const int64_t *n_isects_device, const int32_t *flatten_ids, const float *render_colors,
-    const float *render_alphas, const int32_t *last_ids, const int32_t *median_ids,
-    const float *v_render_colors,
+    const int64_t *n_isects_device, const int32_t *flatten_ids, const int32_t *tile_order,
+    const float *render_colors, const float *render_alphas, const int32_t *last_ids,
+    const int32_t *median_ids, const float *v_render_colors,
     const float *v_render_alphas, const float *v_render_normals, const float *v_render_distort,
     const float *v_render_median, float *v_means2d, float *v_ray_transforms, float *v_colors,
     float *v_opacities, float *v_normals, float *v_densify, float *v_means2d_abs,
@@ -1827,6 +1865,7 @@ extern "C" int gsplat_hip_rasterize_2dgs_bwd(
     RasterArgs a{};
     a.C = C; a.W = width; a.H = height; a.ts = tile_size; a.tw = tile_width;
     a.th = tile_height; a.n_tiles = n_tiles; a.n_isects = n_isects; a.n_dev = n_isects_device;
+    a.order = tile_order;
     a.means2d = means2d; a.ray_transforms = ray_transforms; a.colors = colors;
     a.opacities = opacities; a.normals = normals; a.backgrounds = backgrounds; a.masks = masks;
     a.offsets = isect_offsets; a.flatten_ids = flatten_ids;

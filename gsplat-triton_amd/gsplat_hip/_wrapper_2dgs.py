@@ -206,6 +206,8 @@ _SUPPORTED_D = (1, 2, 3, 4, 5, 6, 7, 8, 9, 16, 17, 32, 33)
 # fwd2s_kernel) where the configuration has them
 # (GSPLAT_HIP_SURFEL_SREC=0: the LDS-queue forward, fwd2_kernel)
 SREC = os.environ.get("GSPLAT_HIP_SURFEL_SREC", "1") != "0"
+# heaviest-first dispatch order of the tiles, forward and backward
+ORDER = os.environ.get("GSPLAT_HIP_SURFEL_ORDER", "0") == "1"
 
 
 class _RasterizeToPixels2DGS(torch.autograd.Function):
@@ -240,12 +242,14 @@ class _RasterizeToPixels2DGS(torch.autograd.Function):
             _lib.call("gsplat_hip_rasterize_2dgs_pack_records", G, D, _ptr(means2d),
                       _ptr(ray_transforms), _ptr(opacities), _ptr(normals), _ptr(colors),
                       _ptr(records), _stream())
+        order = torch.empty(C * th * tw, dtype=torch.int32, device=dev) \
+            if ORDER and int(tile_size) == 16 else None
         with _Timed("rasterize_2dgs_fwd"):
             _lib.call("gsplat_hip_rasterize_2dgs_fwd", C, D, int(width), int(height),
                       int(tile_size), tw, th, _ptr(means2d), _ptr(ray_transforms), _ptr(colors),
                       _ptr(opacities), _ptr(normals), _ptr(backgrounds), _ptr(masks_u8),
                       _ptr(isect_offsets), flatten_ids.numel(), _ptr(n_dev), _ptr(flatten_ids),
-                      _ptr(records), _ptr(render_colors), _ptr(render_alphas), _ptr(render_normals),
+                      _ptr(records), _ptr(order), _ptr(render_colors), _ptr(render_alphas), _ptr(render_normals),
                       _ptr(render_distort), _ptr(render_median), _ptr(last_ids),
                       _ptr(median_ids), _stream())
         ctx.save_for_backward(means2d, ray_transforms, colors, opacities, normals, densify,
@@ -254,6 +258,7 @@ class _RasterizeToPixels2DGS(torch.autograd.Function):
         ctx.width, ctx.height, ctx.tile_size = int(width), int(height), int(tile_size)
         ctx.absgrad, ctx.distloss = absgrad, distloss
         ctx.n_dev = n_dev
+        ctx.order = order
         # outputs without a loss term (alphas, normals, distortion, median in
         # the trainer's RGB loss): None in the backward, not zero-filled images
         ctx.set_materialize_grads(False)
@@ -292,7 +297,8 @@ class _RasterizeToPixels2DGS(torch.autograd.Function):
             _lib.call("gsplat_hip_rasterize_2dgs_bwd", C, D, W, H, ctx.tile_size, tw, th, G,
                       _ptr(means2d), _ptr(ray_transforms), _ptr(colors), _ptr(opacities),
                       _ptr(normals), _ptr(backgrounds), _ptr(masks_u8), _ptr(isect_offsets),
-                      flatten_ids.numel(), _ptr(ctx.n_dev), _ptr(flatten_ids), _ptr(render_colors),
+                      flatten_ids.numel(), _ptr(ctx.n_dev), _ptr(flatten_ids), _ptr(ctx.order),
+                      _ptr(render_colors),
                       _ptr(render_alphas), _ptr(last_ids), _ptr(median_ids),
                       _ptr(v_render_colors), _ptr(v_render_alphas), _ptr(v_render_normals),
                       _ptr(v_render_distort), _ptr(v_render_median), _ptr(v_means2d),

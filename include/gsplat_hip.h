@@ -691,7 +691,10 @@ int gsplat_hip_projection_2dgs_packed_bwd(int C, int N, int64_t nnz, const float
  * and composites with scalar loads instead of its LDS queue; same outputs.
  * record_floats: floats per record (32), 0 when the configuration (D,
  * tile_size) has no record path; pack_records writes records f32[G][32]
- * from the rasterizer's inputs (G rows of means2d ...). */
+ * from the rasterizer's inputs (G rows of means2d ...).
+ * tile_order (ABI 32, may be NULL; i32[C*th*tw]): the forward writes the
+ * tiles' dispatch order there (heaviest first, by floor(log2(isects))) and
+ * runs in it; pass it to the backward, which then runs in it too. */
 int gsplat_hip_rasterize_2dgs_record_floats(int D, int tile_size);
 int gsplat_hip_rasterize_2dgs_pack_records(int64_t n_gaussians, int D, const float *means2d,
                                            const float *ray_transforms, const float *opacities,
@@ -705,7 +708,7 @@ int gsplat_hip_rasterize_2dgs_fwd(int C, int D, int width, int height, int tile_
                                   const float *backgrounds, const uint8_t *masks,
                                   const int32_t *isect_offsets, int64_t n_isects,
                                   const int64_t *n_isects_device, const int32_t *flatten_ids,
-                                  const float *records, float *render_colors,
+                                  const float *records, int32_t *tile_order, float *render_colors,
                                   float *render_alphas, float *render_normals,
                                   float *render_distort, float *render_median,
                                   int32_t *last_ids, int32_t *median_ids, void *stream);
@@ -726,8 +729,8 @@ int gsplat_hip_rasterize_2dgs_bwd(
     int64_t n_gaussians, const float *means2d, const float *ray_transforms, const float *colors,
     const float *opacities, const float *normals, const float *backgrounds,
     const uint8_t *masks, const int32_t *isect_offsets, int64_t n_isects,
-    const int64_t *n_isects_device, const int32_t *flatten_ids, const float *render_colors,
-    const float *render_alphas, const int32_t *last_ids, const int32_t *median_ids, const float *v_render_colors,
+    const int64_t *n_isects_device, const int32_t *flatten_ids, const int32_t *tile_order,
+    const float *render_colors, const float *render_alphas, const int32_t *last_ids, const int32_t *median_ids, const float *v_render_colors,
     const float *v_render_alphas, const float *v_render_normals, const float *v_render_distort,
     const float *v_render_median, float *v_means2d, float *v_ray_transforms, float *v_colors,
     float *v_opacities, float *v_normals, float *v_densify, float *v_means2d_abs,

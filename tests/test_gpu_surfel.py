@@ -153,6 +153,27 @@ def test_raster2dgs_fwd_records_bit_identical(monkeypatch, seed, D, bg, C, thin,
         torch.testing.assert_close(b, a, rtol=1e-4, atol=1e-5 * float(a.abs().max()))
 
 
+@pytest.mark.parametrize("masked", [False, True])
+def test_raster2dgs_tile_order_changes_nothing(monkeypatch, masked):
+    """Heaviest-first dispatch of the tiles (GSPLAT_HIP_SURFEL_ORDER=1): the
+    forward's images bit for bit, the backward to the order of its float
+    atomics."""
+    from gsplat_hip import _wrapper_2dgs
+    sc = surfel_scene(3, N=800, W=150, H=100, D=4, bg=True, C=2, thin=True)
+    masks = (np.random.default_rng(3).random(sc["off"].shape) > 0.3) if masked else None
+    res = []
+    for order in (False, True):
+        monkeypatch.setattr(_wrapper_2dgs, "ORDER", order)
+        leaves, bgt, densify, out = _raster_gpu(sc, masks=masks)
+        w = [torch.linspace(-1, 1, o.numel(), device=DEV).view_as(o) for o in out]
+        sum((o * ww).sum() for o, ww in zip(out, w)).backward()
+        res.append(([o.detach() for o in out], [leaves[k].grad for k in sorted(leaves)]))
+    for a, b in zip(res[0][0], res[1][0]):
+        assert torch.equal(a, b), float((a - b).abs().max())
+    for a, b in zip(res[0][1], res[1][1]):
+        torch.testing.assert_close(b, a, rtol=1e-4, atol=1e-5 * float(a.abs().max()))
+
+
 def test_raster2dgs_fwd_masks():
     sc = surfel_scene(5, N=300, W=70, H=52, D=4, bg=True)
     rng = np.random.default_rng(0)
