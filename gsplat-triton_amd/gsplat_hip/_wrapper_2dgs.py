@@ -207,7 +207,8 @@ _SUPPORTED_D = (1, 2, 3, 4, 5, 6, 7, 8, 9, 16, 17, 32, 33)
 # (GSPLAT_HIP_SURFEL_SREC=0: the LDS-queue forward, fwd2_kernel)
 SREC = os.environ.get("GSPLAT_HIP_SURFEL_SREC", "1") != "0"
 # heaviest-first dispatch order of the tiles, forward and backward
-ORDER = os.environ.get("GSPLAT_HIP_SURFEL_ORDER", "0") == "1"
+# (M5: 293 -> 309 images/s, backward 1.68 -> 1.48 ms; GSPLAT_HIP_SURFEL_ORDER=0 turns it off)
+ORDER = os.environ.get("GSPLAT_HIP_SURFEL_ORDER", "1") != "0"
 
 
 class _RasterizeToPixels2DGS(torch.autograd.Function):

@@ -411,8 +411,19 @@ class GraphStep:
             # process aborted there.  torch.cuda.graph collects right before.
             gc_on = gc.isenabled()
             gc.disable()
+            import torch.distributed as dist
+            if dist.is_available() and dist.is_initialized():
+                # RCCL's watchdog threads query the end events of earlier
+                # collectives; an event query against a stream that a capture
+                # has pulled in (the communicator's own stream, when a
+                # captured collective runs on it) aborted a test process.  Let
+                # them retire every finished collective first (their poll
+                # interval is 100 ms), and capture in thread-local mode so
+                # their calls on other streams stay legal meanwhile.
+                torch.cuda.synchronize(self.dev)
+                time.sleep(0.3)
             try:
-                with torch.cuda.graph(g):
+                with torch.cuda.graph(g, capture_error_mode="thread_local"):
                     self.loss, self.counts = self._body(deg, stats)
             finally:
                 if gc_on:
