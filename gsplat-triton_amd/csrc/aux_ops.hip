@@ -179,8 +179,9 @@ selective_adam_kernel(int64_t n_rows, int64_t row, float *__restrict__ param,
 // n = normalize((p[y+1,x] - p[y-1,x]) x (p[y,x+1] - p[y,x-1])), zero on the
 // one-pixel border.  One lane per pixel; the torch formula is a dozen
 // full-image passes.
-__device__ __forceinline__ void d2n_point(const float *dep, const float *c2w, const float *K,
-                                          int W, int x, int y, int z_depth, float p[3]) {
+__device__ __forceinline__ void d2n_point(const float *dep, int64_t ps, const float *c2w,
+                                          const float *K, int W, int x, int y, int z_depth,
+                                          float p[3]) {
   const float dx = ((float)x - K[2] + 0.5f) / K[0], dy = ((float)y - K[5] + 0.5f) / K[4];
   float d[3];
 #pragma unroll
@@ -190,13 +191,13 @@ __device__ __forceinline__ void d2n_point(const float *dep, const float *c2w, co
 #pragma unroll
     for (int i = 0; i < 3; ++i) d[i] /= n;
   }
-  const float z = dep[(int64_t)y * W + x];
+  const float z = dep[((int64_t)y * W + x) * ps];
 #pragma unroll
   for (int i = 0; i < 3; ++i) p[i] = c2w[4 * i + 3] + z * d[i];
 }
 
 __global__ void __launch_bounds__(256)
-depth_to_normal_kernel(int C, int H, int W, const float *__restrict__ depths,
+depth_to_normal_kernel(int C, int H, int W, const float *__restrict__ depths, int64_t ps,
                        const float *__restrict__ camtoworlds, const float *__restrict__ Ks,
                        int z_depth, float *__restrict__ normals) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -210,12 +211,12 @@ depth_to_normal_kernel(int C, int H, int W, const float *__restrict__ depths,
     out[0] = out[1] = out[2] = 0.f;
     return;
   }
-  const float *dep = depths + c * HW, *c2w = camtoworlds + 16 * c, *K = Ks + 9 * c;
+  const float *dep = depths + c * HW * ps, *c2w = camtoworlds + 16 * c, *K = Ks + 9 * c;
   float pu[3], pd[3], pl[3], pr[3];
-  d2n_point(dep, c2w, K, W, x, y + 1, z_depth, pd);
-  d2n_point(dep, c2w, K, W, x, y - 1, z_depth, pu);
-  d2n_point(dep, c2w, K, W, x + 1, y, z_depth, pr);
-  d2n_point(dep, c2w, K, W, x - 1, y, z_depth, pl);
+  d2n_point(dep, ps, c2w, K, W, x, y + 1, z_depth, pd);
+  d2n_point(dep, ps, c2w, K, W, x, y - 1, z_depth, pu);
+  d2n_point(dep, ps, c2w, K, W, x + 1, y, z_depth, pr);
+  d2n_point(dep, ps, c2w, K, W, x - 1, y, z_depth, pl);
   const float a[3] = {pd[0] - pu[0], pd[1] - pu[1], pd[2] - pu[2]};
   const float b[3] = {pr[0] - pl[0], pr[1] - pl[1], pr[2] - pl[2]};
   const float n[3] = {a[1] * b[2] - a[2] * b[1], a[2] * b[0] - a[0] * b[2],
@@ -224,6 +225,19 @@ depth_to_normal_kernel(int C, int H, int W, const float *__restrict__ depths,
   out[0] = n[0] / l;
   out[1] = n[1] / l;
   out[2] = n[2] / l;
+}
+
+// out[c, p, i] = sum_j c2w[c][i][j] v[c, p, j] (the rotation of the
+// camera-to-world matrices), one lane per pixel.
+__global__ void __launch_bounds__(256)
+rotate3_kernel(int C, int64_t HW, const float *__restrict__ c2w, const float *__restrict__ v,
+               float *__restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= C * HW) return;
+  const float *R = c2w + 16 * (i / HW);
+  const float x = v[3 * i], y = v[3 * i + 1], z = v[3 * i + 2];
+#pragma unroll
+  for (int r = 0; r < 3; ++r) out[3 * i + r] = R[4 * r] * x + R[4 * r + 1] * y + R[4 * r + 2] * z;
 }
 
 }  // namespace auxk
@@ -293,14 +307,29 @@ extern "C" int gsplat_hip_selective_adam(int64_t n_rows, int64_t row, float *par
 }
 
 extern "C" int gsplat_hip_depth_to_normal(int C, int H, int W, const float *depths,
-                                          const float *camtoworlds, const float *Ks, int z_depth,
-                                          float *normals, void *stream) {
+                                          int64_t depth_stride, const float *camtoworlds,
+                                          const float *Ks, int z_depth, float *normals,
+                                          void *stream) {
   GS_REQUIRE(C >= 0 && H >= 0 && W >= 0, "depth_to_normal: negative sizes");
   const int64_t n = (int64_t)C * H * W;
   if (n == 0) return 0;
   GS_REQUIRE(depths && camtoworlds && Ks && normals, "depth_to_normal: null pointer");
+  GS_REQUIRE(depth_stride >= 1, "depth_to_normal: depth_stride %lld < 1", (long long)depth_stride);
   hipLaunchKernelGGL(auxk::depth_to_normal_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256),
-                     0, (hipStream_t)stream, C, H, W, depths, camtoworlds, Ks, z_depth, normals);
+                     0, (hipStream_t)stream, C, H, W, depths, depth_stride, camtoworlds, Ks,
+                     z_depth, normals);
   GS_CHECK_LAUNCH("depth_to_normal");
+  return 0;
+}
+
+extern "C" int gsplat_hip_rotate3(int C, int64_t HW, const float *camtoworlds, const float *v,
+                                  float *out, void *stream) {
+  GS_REQUIRE(C >= 0 && HW >= 0, "rotate3: negative sizes");
+  const int64_t n = (int64_t)C * HW;
+  if (n == 0) return 0;
+  GS_REQUIRE(camtoworlds && v && out, "rotate3: null pointer");
+  hipLaunchKernelGGL(auxk::rotate3_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, C, HW, camtoworlds, v, out);
+  GS_CHECK_LAUNCH("rotate3");
   return 0;
 }

@@ -153,7 +153,8 @@ _SIGS = {
     "gsplat_hip_rasterize_to_indices_write": (_i32, [_i32, _i32, _i32, _i32, _i32, _i32, _i32,
                                                      _i32, _i64, _i64, _i64, _p, _p, _p, _p, _p,
                                                      _p, _p, _p, _p, _p]),
-    "gsplat_hip_depth_to_normal": (_i32, [_i32, _i32, _i32, _p, _p, _p, _i32, _p, _p]),
+    "gsplat_hip_depth_to_normal": (_i32, [_i32, _i32, _i32, _p, _i64, _p, _p, _i32, _p, _p]),
+    "gsplat_hip_rotate3": (_i32, [_i32, _i64, _p, _p, _p, _p]),
 }
 
 EXPORTED = tuple(_SIGS)

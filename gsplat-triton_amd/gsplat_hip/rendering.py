@@ -370,6 +370,32 @@ def rasterization(
     return render_colors, render_alphas, meta
 
 
+class _Rotate3(torch.autograd.Function):
+    """_rotate's output for R = camtoworlds[C, :3, :3] and v [C, H, W, 3] in
+    one HIP launch (gsplat_hip_rotate3); backward: autograd of the torch
+    formula (only under a loss on the rendered normals)."""
+
+    @staticmethod
+    def forward(ctx, c2w, v):
+        C = c2w.shape[0]
+        vc = _f32c(v)
+        out = torch.empty_like(vc)
+        _lib.call("gsplat_hip_rotate3", C, vc.numel() // (3 * C), _ptr(_f32c(c2w)), _ptr(vc),
+                  _ptr(out), _stream())
+        ctx.save_for_backward(c2w, v)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        c2w, v = ctx.saved_tensors
+        with torch.enable_grad():
+            ins = [t.detach().requires_grad_(t.requires_grad) for t in (c2w, v)]
+            out = _rotate(ins[0][..., :3, :3], ins[1])
+            want = [t for t in ins if t.requires_grad]
+            grads = iter(torch.autograd.grad(out, want, g, allow_unused=True)) if want else iter(())
+        return tuple(next(grads) if t.requires_grad else None for t in ins)
+
+
 def _rotate(R: Tensor, v: Tensor) -> Tensor:
     """out[..., i] = sum_j R[..., i, j] v[..., h, w, j] for R [..., 3, 3] and
     v [..., H, W, 3] -- the einsum "...ij,...hwj->...hwi" of the reference as
@@ -420,13 +446,20 @@ class _DepthToNormal(torch.autograd.Function):
         _dev_check(depths, camtoworlds, Ks)
         H, W = depths.shape[-3:-1]
         lead = depths.shape[:-3]
-        d = _f32c(depths).reshape(-1, H, W)
-        C = d.shape[0]
+        # the last channel of an RGB+D render is read in place (pixel stride)
+        ps = depths.stride(-2)
+        strided = (depths.dtype == torch.float32 and depths.shape[-1] == 1 and ps >= 1
+                   and all(depths.stride(i) == depths.shape[i + 1] * depths.stride(i + 1)
+                           for i in range(depths.dim() - 3)) and depths.stride(-3) == W * ps)
+        d = depths if strided else _f32c(depths).reshape(-1, H, W)
+        if not strided:
+            ps = 1
+        C = math.prod(lead) if lead else 1
         c2w = _f32c(camtoworlds).reshape(-1, 4, 4)
         k = _f32c(Ks).reshape(-1, 3, 3)
         assert c2w.shape[0] == C and k.shape[0] == C, (depths.shape, camtoworlds.shape, Ks.shape)
         out = torch.empty((C, H, W, 3), device=depths.device)
-        _lib.call("gsplat_hip_depth_to_normal", C, H, W, _ptr(d), _ptr(c2w), _ptr(k),
+        _lib.call("gsplat_hip_depth_to_normal", C, H, W, _ptr(d), int(ps), _ptr(c2w), _ptr(k),
                   int(bool(z_depth)), _ptr(out), _stream())
         ctx.save_for_backward(depths, camtoworlds, Ks)
         ctx.z_depth = z_depth
@@ -609,6 +642,10 @@ def rasterization_2dgs(
             "render_distort": render_distort, "gradient_2dgs": densify}
     if counts is not None:
         meta["isect_counts"] = counts
-    render_normals = _rotate(camtoworlds[..., :3, :3], render_normals)
+    if camtoworlds.dim() == 3 and render_normals.dim() == 4 and render_normals.is_cuda \
+            and camtoworlds.shape[0] == render_normals.shape[0]:
+        render_normals = _Rotate3.apply(camtoworlds, render_normals)
+    else:
+        render_normals = _rotate(camtoworlds[..., :3, :3], render_normals)
     return (render_colors, render_alphas, render_normals, render_normals_from_depth,
             render_distort, render_median, meta)

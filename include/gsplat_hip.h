@@ -845,10 +845,19 @@ int gsplat_hip_rasterize_to_indices_write(int kind, int C, int N, int W, int H, 
 
 /* Normals from depth maps (gsplat/utils.py:201-224, depth_to_normal, called by
  * rasterization_2dgs for render_normals_from_depth): depths[C,H,W] (the [..,1]
- * channel), camtoworlds[C,4,4], Ks[C,3,3] -> normals[C,H,W,3], zero border.
+ * channel; depth_stride (ABI 32): floats from one pixel's depth to the next,
+ * e.g. 4 for the last channel of an RGB+D render read in place),
+ * camtoworlds[C,4,4], Ks[C,3,3] -> normals[C,H,W,3], zero border.
  * Forward only; the Python binding differentiates the torch formula. */
-int gsplat_hip_depth_to_normal(int C, int H, int W, const float *depths, const float *camtoworlds,
-                               const float *Ks, int z_depth, float *normals, void *stream);
+int gsplat_hip_depth_to_normal(int C, int H, int W, const float *depths, int64_t depth_stride,
+                               const float *camtoworlds, const float *Ks, int z_depth,
+                               float *normals, void *stream);
+/* rasterization_2dgs's rotation of the rendered normals into world space
+ * (gsplat/rendering.py, the einsum of camtoworlds[..., :3, :3] with
+ * render_normals; ABI 32): out[c,p,i] = sum_j camtoworlds[c][i][j] v[c,p,j]
+ * for v, out f32[C,HW,3]; one launch.  Forward only. */
+int gsplat_hip_rotate3(int C, int64_t HW, const float *camtoworlds, const float *v, float *out,
+                       void *stream);
 
 #ifdef __cplusplus
 }
