@@ -4,6 +4,9 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 O=gpurun_out/r5_b14; mkdir -p $O
+timeout -k 10 300 python -u -m pytest tests/test_gpu_surfel.py tests/test_gpu_graph.py -x -q --timeout 200 \
+  --timeout-method thread -k "e2e or depth_to_normal or 2dgs or packed" > $O/sel.log 2>&1
+rc=$?; echo "selected tests rc=$rc"; tail -2 $O/sel.log; [ $rc -eq 0 ] || exit $rc
 for r in 1 2; do
   for v in base f5 b4 f5b4; do
     case $v in
