@@ -1017,9 +1017,8 @@ GS_INLINE void srec_load_blend(const float *rec, int32_t g, SBlend<D> &r) {
   for (int d = 0; d < D; ++d) r.col[d] = p[COL + d];
 }
 
-template <int D, int WPE = 4>
-__global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE)))
-fwd2s_kernel(RasterArgs a, const float *__restrict__ rec) {
+template <int D>
+__global__ void __launch_bounds__(128) fwd2s_kernel(RasterArgs a, const float *__restrict__ rec) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int tile = a.order ? a.order[blockIdx.x] : (int)blockIdx.x;
   const int ntile = a.tw * a.th;
@@ -1329,9 +1328,8 @@ struct PixState {
   bool inside;
 };
 
-template <int D, bool ABS, int WPE = 3>
-__global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE)))
-bwd2_kernel(RasterArgs a) {
+template <int D, bool ABS>
+__global__ void __launch_bounds__(128) bwd2_kernel(RasterArgs a) {
   using R = Rec<D>;
   using F = Fields<D, ABS>;
   extern __shared__ float4 lds4[];
@@ -1553,13 +1551,6 @@ bool fwd2_enabled() {
     return !(e && atoi(e) == 1);
   }();
   return v;
-}
-
-// waves-per-SIMD targets of experiments (GSPLAT_HIP_SURFEL_FWD_WPE=5,
-// GSPLAT_HIP_SURFEL_BWD_WPE=4: fewer VGPRs, a few spills); 0 = the default
-int wpe_env(const char *name) {
-  const char *e = getenv(name);
-  return e ? atoi(e) : 0;
 }
 
 bool bwd2_enabled() {
@@ -1786,12 +1777,7 @@ extern "C" int gsplat_hip_rasterize_2dgs_fwd(
     GS_REQUIRE(px2 && D <= kSRecMaxD, "rasterize_2dgs_fwd: records need 16x16 tiles, D <= %d",
                kSRecMaxD);
 #define GS_CASE(n)                                                                            \
-  if (D == n) {                                                                               \
-    if (wpe_env("GSPLAT_HIP_SURFEL_FWD_WPE") == 5)                                            \
-      hipLaunchKernelGGL((fwd2s_kernel<n, 5>), dim3(n_tiles), dim3(128), 0, st, a, records);  \
-    else                                                                                      \
-      hipLaunchKernelGGL((fwd2s_kernel<n>), dim3(n_tiles), dim3(128), 0, st, a, records);     \
-  }
+  if (D == n) hipLaunchKernelGGL(fwd2s_kernel<n>, dim3(n_tiles), dim3(128), 0, st, a, records);
     GS_CASE(1) GS_CASE(2) GS_CASE(3) GS_CASE(4)
 #undef GS_CASE
     GS_CHECK_LAUNCH("rasterize_2dgs_fwd");
@@ -1899,8 +1885,6 @@ extern "C" int gsplat_hip_rasterize_2dgs_bwd(
     const size_t lds = (size_t)waves * 64 * Rec<n>::NF * sizeof(float);                       \
     if (px2 && absgrad)                                                                       \
       hipLaunchKernelGGL((bwd2_kernel<n, true>), dim3(n_tiles), dim3(128), lds / 2, st, a);    \
-    else if (px2 && wpe_env("GSPLAT_HIP_SURFEL_BWD_WPE") == 4)                                \
-      hipLaunchKernelGGL((bwd2_kernel<n, false, 4>), dim3(n_tiles), dim3(128), lds / 2, st, a); \
     else if (px2)                                                                             \
       hipLaunchKernelGGL((bwd2_kernel<n, false>), dim3(n_tiles), dim3(128), lds / 2, st, a);   \
     else if (absgrad)                                                                         \
