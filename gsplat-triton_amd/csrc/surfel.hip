@@ -852,7 +852,21 @@ tile_order_kernel(int n_tiles, const int32_t *__restrict__ offsets, int64_t n_is
     const int64_t n = e - offsets[t];
     return n > 0 ? 32 - (63 - __builtin_clzll((uint64_t)n)) : 33;  // 2^31.. -> 1, 1 -> 32
   };
-  for (int t = tid; t < n_tiles; t += 1024) atomicAdd(&hist[key(t)], 1);
+  // per wave and distinct key one LDS atomic (a few keys per wave: M5's
+  // tiles fall into 2-3 buckets, and 64 lanes on one counter serialised)
+  const int lane = tid & 63;
+  const int n_rounds = (n_tiles + 1023) / 1024;
+  for (int rd = 0; rd < n_rounds; ++rd) {
+    const int t = tid + 1024 * rd;
+    const int k = t < n_tiles ? key(t) : -1;
+    uint64_t todo = __ballot(k >= 0);
+    while (todo) {
+      const int kk = __builtin_amdgcn_readlane(k, __builtin_ctzll(todo));
+      const uint64_t m = __ballot(k == kk) & todo;
+      if (lane == __builtin_ctzll(m)) atomicAdd(&hist[kk], __popcll(m));
+      todo &= ~m;
+    }
+  }
   __syncthreads();
   if (tid == 0) {
     int run = 0;
@@ -863,7 +877,21 @@ tile_order_kernel(int n_tiles, const int32_t *__restrict__ offsets, int64_t n_is
     }
   }
   __syncthreads();
-  for (int t = tid; t < n_tiles; t += 1024) order[atomicAdd(&hist[key(t)], 1)] = t;
+  for (int rd = 0; rd < n_rounds; ++rd) {
+    const int t = tid + 1024 * rd;
+    const int k = t < n_tiles ? key(t) : -1;
+    uint64_t todo = __ballot(k >= 0);
+    while (todo) {
+      const int kk = __builtin_amdgcn_readlane(k, __builtin_ctzll(todo));
+      const uint64_t m = __ballot(k == kk) & todo;
+      const int leader = __builtin_ctzll(m);
+      int base = 0;
+      if (lane == leader) base = atomicAdd(&hist[kk], __popcll(m));
+      base = __shfl(base, leader, 64);
+      if (k == kk) order[base + __popcll(m & ((1ull << lane) - 1))] = t;
+      todo &= ~m;
+    }
+  }
 }
 
 constexpr int kSRecMaxD = 4;
@@ -884,10 +912,12 @@ template <int D>
 __global__ void __launch_bounds__(256)
 pack_srec_kernel(int64_t G, const float *__restrict__ means2d, const float *__restrict__ rt,
                  const float *__restrict__ opac, const float *__restrict__ nrm,
-                 const float *__restrict__ col, float *__restrict__ rec) {
+                 const float *__restrict__ col, const int32_t *__restrict__ visible,
+                 float *__restrict__ rec) {
   using namespace srec;
   const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (g >= G) return;
+  if (visible && visible[g] <= 0) return;  // never gathered: no record
   float m[9];
 #pragma unroll
   for (int i = 0; i < 9; ++i) m[i] = rt[9 * g + i];
@@ -1500,18 +1530,42 @@ __global__ void __launch_bounds__(128) bwd2_kernel(RasterArgs a) {
   }
 }
 
+// Zero the packed gradient rows of the visible surfels (the rows the
+// backward's atomics can reach); one lane per row, S / 4 16-B stores.
+__global__ void __launch_bounds__(256)
+zero_rows_kernel(int64_t G, int S, const int32_t *__restrict__ visible, float *__restrict__ packed) {
+  const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (g >= G || visible[g] <= 0) return;
+  float4 *r = reinterpret_cast<float4 *>(packed + g * S);
+  for (int q = 0; q < S / 4; ++q) r[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
 // packed [G][S] -> autograd tensors; densify = (v_M[0][2], v_M[1][2]) * depth
 // with depth = M[2][2] (the reference writes this racily from partial sums,
 // RasterizeToPixels2DGSBwd.cu:689-697; here it is formed from the final sums).
 template <int D, bool ABS>
 __global__ void __launch_bounds__(256)
-unpack_kernel(int64_t G, const float *__restrict__ packed, const float *__restrict__ rt,
+unpack_kernel(int64_t G, const int32_t *__restrict__ visible, const float *__restrict__ packed,
+              const float *__restrict__ rt,
               float *__restrict__ v_means2d, float *__restrict__ v_rt, float *__restrict__ v_colors,
               float *__restrict__ v_opacities, float *__restrict__ v_normals,
               float *__restrict__ v_densify, float *__restrict__ v_abs) {
   using F = Fields<D, ABS>;
   const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= G) return;
+  if (visible && visible[g] <= 0) {  // no isect: every gradient is zero (row never zeroed)
+#pragma unroll
+    for (int d = 0; d < D; ++d) v_colors[g * D + d] = 0.f;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) v_normals[g * 3 + i] = 0.f;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) v_rt[g * 9 + i] = 0.f;
+    *reinterpret_cast<float2 *>(v_means2d + 2 * g) = make_float2(0.f, 0.f);
+    v_opacities[g] = 0.f;
+    *reinterpret_cast<float2 *>(v_densify + 2 * g) = make_float2(0.f, 0.f);
+    if (ABS) *reinterpret_cast<float2 *>(v_abs + 2 * g) = make_float2(0.f, 0.f);
+    return;
+  }
   const float *r = packed + g * F::S;
 #pragma unroll
   for (int d = 0; d < D; ++d) v_colors[g * D + d] = r[F::COL + d];
@@ -1805,8 +1859,8 @@ extern "C" int gsplat_hip_rasterize_2dgs_pack_records(int64_t n_gaussians, int D
                                                       const float *means2d,
                                                       const float *ray_transforms,
                                                       const float *opacities, const float *normals,
-                                                      const float *colors, float *records,
-                                                      void *stream) {
+                                                      const float *colors, const int32_t *visible,
+                                                      float *records, void *stream) {
   GS_REQUIRE(D >= 1 && D <= kSRecMaxD, "rasterize_2dgs_pack_records: D %d not in [1, %d]", D,
              kSRecMaxD);
   GS_REQUIRE(n_gaussians >= 0, "rasterize_2dgs_pack_records: negative count");
@@ -1819,7 +1873,7 @@ extern "C" int gsplat_hip_rasterize_2dgs_pack_records(int64_t n_gaussians, int D
 #define GS_CASE(n)                                                                            \
   if (D == n)                                                                                 \
     hipLaunchKernelGGL(pack_srec_kernel<n>, grid, dim3(256), 0, st, n_gaussians, means2d,     \
-                       ray_transforms, opacities, normals, colors, records);
+                       ray_transforms, opacities, normals, colors, visible, records);
   GS_CASE(1) GS_CASE(2) GS_CASE(3) GS_CASE(4)
 #undef GS_CASE
   GS_CHECK_LAUNCH("rasterize_2dgs_pack_records");
@@ -1837,7 +1891,8 @@ extern "C" int gsplat_hip_rasterize_2dgs_bwd(
     const float *opacities, const float *normals, const float *backgrounds,
     const uint8_t *masks, const int32_t *isect_offsets, int64_t n_isects,
     const int64_t *n_isects_device, const int32_t *flatten_ids, const int32_t *tile_order,
-    const float *render_colors, const float *render_alphas, const int32_t *last_ids,
+    const int32_t *visible, const float *render_colors, const float *render_alphas,
+    const int32_t *last_ids,
     const int32_t *median_ids, const float *v_render_colors,
     const float *v_render_alphas, const float *v_render_normals, const float *v_render_distort,
     const float *v_render_median, float *v_means2d, float *v_ray_transforms, float *v_colors,
@@ -1856,7 +1911,11 @@ extern "C" int gsplat_hip_rasterize_2dgs_bwd(
   GS_REQUIRE(workspace && v_means2d && v_ray_transforms && v_colors && v_opacities && v_normals &&
                  v_densify && ray_transforms,
              "rasterize_2dgs_bwd: null pointer argument");
-  GS_HIP(gs::zero_async(workspace, (size_t)G * S * sizeof(float), st));
+  if (visible)
+    hipLaunchKernelGGL(zero_rows_kernel, dim3((unsigned)((G + 255) / 256)), dim3(256), 0, st, G, S,
+                       visible, (float *)workspace);
+  else
+    GS_HIP(gs::zero_async(workspace, (size_t)G * S * sizeof(float), st));
   const int n_tiles = C * tile_width * tile_height;
   if (n_tiles > 0 && n_isects > 0 && width > 0 && height > 0) {
     GS_REQUIRE(isect_offsets && flatten_ids && render_colors && render_alphas && last_ids &&
@@ -1900,11 +1959,11 @@ extern "C" int gsplat_hip_rasterize_2dgs_bwd(
 #define GS_CASE(n)                                                                             \
   if (D == n) {                                                                                \
     if (absgrad)                                                                               \
-      hipLaunchKernelGGL((unpack_kernel<n, true>), grid, dim3(256), 0, st, G, (const float *)workspace, \
+      hipLaunchKernelGGL((unpack_kernel<n, true>), grid, dim3(256), 0, st, G, visible, (const float *)workspace, \
                          ray_transforms, v_means2d, v_ray_transforms, v_colors, v_opacities,   \
                          v_normals, v_densify, v_means2d_abs);                                 \
     else                                                                                       \
-      hipLaunchKernelGGL((unpack_kernel<n, false>), grid, dim3(256), 0, st, G, (const float *)workspace, \
+      hipLaunchKernelGGL((unpack_kernel<n, false>), grid, dim3(256), 0, st, G, visible, (const float *)workspace, \
                          ray_transforms, v_means2d, v_ray_transforms, v_colors, v_opacities,   \
                          v_normals, v_densify, v_means2d_abs);                                 \
   }

@@ -129,10 +129,11 @@ _SIGS = {
                                              _p, _p, _p, _p, _p, _i64, _p, _p, _p, _p, _p, _p,
                                              _p, _p, _p, _p, _p, _p]),
     "gsplat_hip_rasterize_2dgs_record_floats": (_i32, [_i32, _i32]),
-    "gsplat_hip_rasterize_2dgs_pack_records": (_i32, [_i64, _i32, _p, _p, _p, _p, _p, _p, _p]),
+    "gsplat_hip_rasterize_2dgs_pack_records": (_i32, [_i64, _i32, _p, _p, _p, _p, _p, _p, _p, _p]),
     "gsplat_hip_rasterize_2dgs_bwd_workspace_bytes": (_i64, [_i64, _i32, _i32]),
     "gsplat_hip_rasterize_2dgs_bwd": (_i32, [_i32, _i32, _i32, _i32, _i32, _i32, _i32, _i64, _p,
                                              _p, _p, _p, _p, _p, _p, _p, _i64, _p, _p, _p, _p, _p, _p,
+                                             _p,
                                              _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p,
                                              _p, _i64, _p]),
     "gsplat_hip_quat_scale_to_covar_preci_fwd": (_i32, [_i64, _p, _p, _i32, _p, _p, _p]),

@@ -217,7 +217,7 @@ class _RasterizeToPixels2DGS(torch.autograd.Function):
     @staticmethod
     def forward(ctx, means2d, ray_transforms, colors, opacities, normals, densify, backgrounds,
                 masks, width, height, tile_size, isect_offsets, flatten_ids, absgrad, distloss,
-                n_dev=None):
+                n_dev=None, visible=None):
         means2d, ray_transforms, colors, opacities, normals, backgrounds = (
             _f32c(x) for x in (means2d, ray_transforms, colors, opacities, normals, backgrounds))
         _dev_check(means2d, ray_transforms, colors, opacities, normals, isect_offsets, flatten_ids)
@@ -242,7 +242,7 @@ class _RasterizeToPixels2DGS(torch.autograd.Function):
             records = torch.empty(max(G, 1) * nf, device=dev)
             _lib.call("gsplat_hip_rasterize_2dgs_pack_records", G, D, _ptr(means2d),
                       _ptr(ray_transforms), _ptr(opacities), _ptr(normals), _ptr(colors),
-                      _ptr(records), _stream())
+                      _ptr(visible), _ptr(records), _stream())
         order = torch.empty(C * th * tw, dtype=torch.int32, device=dev) \
             if ORDER and int(tile_size) == 16 else None
         with _Timed("rasterize_2dgs_fwd"):
@@ -260,6 +260,7 @@ class _RasterizeToPixels2DGS(torch.autograd.Function):
         ctx.absgrad, ctx.distloss = absgrad, distloss
         ctx.n_dev = n_dev
         ctx.order = order
+        ctx.visible = visible
         # outputs without a loss term (alphas, normals, distortion, median in
         # the trainer's RGB loss): None in the backward, not zero-filled images
         ctx.set_materialize_grads(False)
@@ -299,7 +300,7 @@ class _RasterizeToPixels2DGS(torch.autograd.Function):
                       _ptr(means2d), _ptr(ray_transforms), _ptr(colors), _ptr(opacities),
                       _ptr(normals), _ptr(backgrounds), _ptr(masks_u8), _ptr(isect_offsets),
                       flatten_ids.numel(), _ptr(ctx.n_dev), _ptr(flatten_ids), _ptr(ctx.order),
-                      _ptr(render_colors),
+                      _ptr(ctx.visible), _ptr(render_colors),
                       _ptr(render_alphas), _ptr(last_ids), _ptr(median_ids),
                       _ptr(v_render_colors), _ptr(v_render_alphas), _ptr(v_render_normals),
                       _ptr(v_render_distort), _ptr(v_render_median), _ptr(v_means2d),
@@ -311,7 +312,7 @@ class _RasterizeToPixels2DGS(torch.autograd.Function):
         if ctx.needs_input_grad[6]:  # _wrapper.py:1953-1958
             v_backgrounds = (v_render_colors * (1.0 - render_alphas).float()).sum(dim=(1, 2))
         return (v_means2d, v_ray_transforms, v_colors, v_opacities, v_normals, v_densify,
-                v_backgrounds, None, None, None, None, None, None, None, None, None)
+                v_backgrounds, None, None, None, None, None, None, None, None, None, None)
 
 
 def rasterize_to_pixels_2dgs(
@@ -332,6 +333,7 @@ def rasterize_to_pixels_2dgs(
     absgrad: bool = False,
     distloss: bool = False,
     _n_isects_device: Optional[Tensor] = None,
+    _visible: Optional[Tensor] = None,
 ) -> Tuple[Tensor, Tensor, Tensor, Tensor, Tensor]:
     """Rasterizes surfels to pixels (gsplat/cuda/_wrapper.py:1595-1726).
 
@@ -340,7 +342,10 @@ def rasterize_to_pixels_2dgs(
     [C,H,W,1].  The depth used by the distortion and median terms is the last
     colour channel, as in the reference.  `_n_isects_device` (private): the
     isect count on the device when flatten_ids is a capacity-sized array
-    (the sync-free isect of a captured training step)."""
+    (the sync-free isect of a captured training step).  `_visible`
+    (private): i32 per row of means2d, > 0 for the rows an isect references
+    (the isect's tiles_per_gauss): only those get a record and a zeroed
+    gradient row."""
     C = isect_offsets.size(0)
     device = means2d.device
     if packed:  # flatten_ids index the [nnz] rows directly (_wrapper.py:1628-1636)
@@ -391,7 +396,8 @@ def rasterize_to_pixels_2dgs(
             means2d.contiguous(), ray_transforms.contiguous(), colors.contiguous(),
             opacities.contiguous(), normals.contiguous(), densify.contiguous(), backgrounds,
             masks, image_width, image_height, tile_size, isect_offsets.contiguous(),
-            flatten_ids.contiguous(), absgrad, distloss, _n_isects_device)
+            flatten_ids.contiguous(), absgrad, distloss, _n_isects_device,
+            None if _visible is None else _visible.to(torch.int32).contiguous().view(-1))
     if padded_channels > 0:
         render_colors = torch.cat([render_colors[..., : -padded_channels - 1],
                                    render_colors[..., -1:]], dim=-1)

@@ -618,7 +618,8 @@ def rasterization_2dgs(
         rasterize_to_pixels_2dgs(means2d, ray_transforms, colors, opacities, normals, densify,
                                  width, height, tile_size, isect_offsets, flatten_ids,
                                  backgrounds=backgrounds, packed=packed, absgrad=absgrad,
-                                 distloss=distloss, _n_isects_device=counts)
+                                 distloss=distloss, _n_isects_device=counts,
+                                 _visible=tiles_per_gauss)
     camtoworlds = torch.linalg.inv(viewmats) if _camtoworlds is None else _camtoworlds
     render_normals_from_depth = None
     if render_mode in ["ED", "RGB+ED"]:

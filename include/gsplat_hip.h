@@ -691,7 +691,9 @@ int gsplat_hip_projection_2dgs_packed_bwd(int C, int N, int64_t nnz, const float
  * and composites with scalar loads instead of its LDS queue; same outputs.
  * record_floats: floats per record (32), 0 when the configuration (D,
  * tile_size) has no record path; pack_records writes records f32[G][32]
- * from the rasterizer's inputs (G rows of means2d ...).
+ * from the rasterizer's inputs (G rows of means2d ...); rows with
+ * visible[g] <= 0 (e.g. tiles_per_gauss; NULL = all) are never gathered and
+ * are left unwritten.
  * tile_order (ABI 32, may be NULL; i32[C*th*tw]): the forward writes the
  * tiles' dispatch order there (heaviest first, by floor(log2(isects))) and
  * runs in it; pass it to the backward, which then runs in it too. */
@@ -699,7 +701,7 @@ int gsplat_hip_rasterize_2dgs_record_floats(int D, int tile_size);
 int gsplat_hip_rasterize_2dgs_pack_records(int64_t n_gaussians, int D, const float *means2d,
                                            const float *ray_transforms, const float *opacities,
                                            const float *normals, const float *colors,
-                                           float *records, void *stream);
+                                           const int32_t *visible, float *records, void *stream);
 int gsplat_hip_rasterize_2dgs_supported_channels(int D);
 int gsplat_hip_rasterize_2dgs_fwd(int C, int D, int width, int height, int tile_size,
                                   int tile_width, int tile_height, const float *means2d,
@@ -722,7 +724,9 @@ int gsplat_hip_rasterize_2dgs_fwd(int C, int D, int width, int height, int tile_
  *    (formed from the final sums; the reference writes it racily from partial
  *    sums), v_means2d_abs[G,2] or NULL (absgrad off).
  * v_render_alphas / v_render_normals (ABI 32) / v_render_distort /
- * v_render_median may be NULL (no gradient). */
+ * v_render_median may be NULL (no gradient).  visible (ABI 32, may be NULL;
+ * i32[G], e.g. tiles_per_gauss): only the rows with visible[g] > 0 can
+ * receive gradient -- the others are written as zeros without a read. */
 int64_t gsplat_hip_rasterize_2dgs_bwd_workspace_bytes(int64_t n_gaussians, int D, int absgrad);
 int gsplat_hip_rasterize_2dgs_bwd(
     int C, int D, int width, int height, int tile_size, int tile_width, int tile_height,
@@ -730,7 +734,8 @@ int gsplat_hip_rasterize_2dgs_bwd(
     const float *opacities, const float *normals, const float *backgrounds,
     const uint8_t *masks, const int32_t *isect_offsets, int64_t n_isects,
     const int64_t *n_isects_device, const int32_t *flatten_ids, const int32_t *tile_order,
-    const float *render_colors, const float *render_alphas, const int32_t *last_ids, const int32_t *median_ids, const float *v_render_colors,
+    const int32_t *visible, const float *render_colors, const float *render_alphas,
+    const int32_t *last_ids, const int32_t *median_ids, const float *v_render_colors,
     const float *v_render_alphas, const float *v_render_normals, const float *v_render_distort,
     const float *v_render_median, float *v_means2d, float *v_ray_transforms, float *v_colors,
     float *v_opacities, float *v_normals, float *v_densify, float *v_means2d_abs,
