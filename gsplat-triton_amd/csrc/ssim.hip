@@ -491,9 +491,9 @@ constexpr int kHA = 6, kHC = 4;  // adjacent outputs per work item in passes A, 
 // a tile adjacent in the XCD-aware order so they share that XCD's L2).
 template <int C, int BR, int CPW = C>
 __global__ void __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(4)))
-fused_kernel(int B, int H, int W, const float *__restrict__ x, const float *__restrict__ y,
-             const int64_t *__restrict__ y_index, float cs, float cl, float *__restrict__ grad,
-             float *__restrict__ partials) {
+fused_kernel(int B, int H, int W, int XS, const float *__restrict__ x,
+             const float *__restrict__ y, const int64_t *__restrict__ y_index, float cs, float cl,
+             float *__restrict__ grad, float *__restrict__ partials) {
   static_assert(C % CPW == 0, "channel groups");
   constexpr int CG = C / CPW;
   __shared__ __attribute__((aligned(16))) char lds[kFusedLds];
@@ -526,16 +526,19 @@ fused_kernel(int B, int H, int W, const float *__restrict__ x, const float *__re
   // window loads of one channel: lane = window column, wave w = rows w, w+8,
   // ...; clamped addresses (unconditional loads), zeroed outside the image
   // (row pointers are wave-uniform: saddr + one 32-bit lane offset per load)
-  const uint32_t lo = (uint32_t)(min(max(rj0 + lane, 0), W - 1) * C);
+  // x (the render, and its gradient) has XS >= C floats per pixel (an RGB+D
+  // render read in place: XS = 4, C = 3); y has C
+  const int colc = min(max(rj0 + lane, 0), W - 1);
+  const uint32_t lox = (uint32_t)(colc * XS), loy = (uint32_t)(colc * C);
   const bool col_ok = lane < FI && rj0 + lane >= 0 && rj0 + lane < W;
-  const float *xb = x + (int64_t)b * H * W * C, *yb = y + (int64_t)b * H * W * C;
+  const float *xb = x + (int64_t)b * H * W * XS, *yb = y + (int64_t)b * H * W * C;
   float vx[kFRows], vy[kFRows];
   auto load = [&](int c) {
 #pragma unroll
     for (int k = 0; k < kFRows; ++k) {
-      const int64_t row = (int64_t)min(max(ri0 + w8 + 8 * k, 0), H - 1) * W * C;
-      vx[k] = (xb + row)[lo + c];
-      vy[k] = (yb + row)[lo + c];
+      const int64_t row = (int64_t)min(max(ri0 + w8 + 8 * k, 0), H - 1) * W;
+      vx[k] = (xb + row * XS)[lox + c];
+      vy[k] = (yb + row * C)[loy + c];
     }
   };
   float lsum = 0.f, ssum = 0.f;
@@ -695,9 +698,17 @@ fused_kernel(int B, int H, int W, const float *__restrict__ x, const float *__re
         const float d = v.x - v.y;
         const float sgn = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
         if (qi < H && qj < W)
-          grad[(((int64_t)b * H + qi) * W + qj) * C + c] =
+          grad[(((int64_t)b * H + qi) * W + qj) * XS + c] =
               cs * (oa[j].x + 2.f * v.x * oa[j].y + v.y * oc[j]) + cl * sgn;
       }
+    }
+  }
+  if (XS > C && cg == CG - 1) {  // the render's other channels: no loss term, zero gradient
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int qi = qi0 + 2 * gr + j, qj = qj0 + gc;
+      if (qi < H && qj < W)
+        for (int e = C; e < XS; ++e) grad[(((int64_t)b * H + qi) * W + qj) * XS + e] = 0.f;
     }
   }
   ssum = wave_sum(ssum);
@@ -854,7 +865,7 @@ static int ssim_cpw() {
   return v;
 }
 
-static int fused_fwd(int B, int H, int W, int C, const float *img1, const float *img2,
+static int fused_fwd(int B, int H, int W, int C, int XS, const float *img1, const float *img2,
                      const int64_t *img2_index, float lam, float *out, float *grad_unit,
                      void *workspace, float *ring, int64_t ring_len, const int64_t *seq,
                      void *stream) {
@@ -863,6 +874,7 @@ static int fused_fwd(int B, int H, int W, int C, const float *img1, const float 
              W);
   GS_REQUIRE(C == 1 || C == 3, "l1_ssim_loss_fused_fwd: C must be 1 or 3 (got %d)", C);
   GS_REQUIRE(out != nullptr && grad_unit != nullptr, "l1_ssim_loss_fused_fwd: null output");
+  GS_REQUIRE(XS >= C, "l1_ssim_loss_fused_fwd: pixel stride %d < C = %d", XS, C);
   hipStream_t st = (hipStream_t)stream;
   float *partials = reinterpret_cast<float *>(workspace);
   const int cg = C == 3 ? 3 / ssim_cpw() : 1;  // workgroups per tile
@@ -875,7 +887,7 @@ static int fused_fwd(int B, int H, int W, int C, const float *img1, const float 
   }();
 #define GS_FUSED(CC, BR, CPW)                                                                \
   hipLaunchKernelGGL((ssim::fused_kernel<CC, BR, CPW>), grid, dim3(ssim::kFThreads), 0, st, B, H, \
-                     W, img1, img2, img2_index, cs, cl, grad_unit, partials)
+                     W, XS, img1, img2, img2_index, cs, cl, grad_unit, partials)
   if (C == 3) {
     if (cg == 3) GS_FUSED(3, 4, 1);
     else if (fv == 1) GS_FUSED(3, 2, 3);
@@ -891,15 +903,15 @@ static int fused_fwd(int B, int H, int W, int C, const float *img1, const float 
   return 0;
 }
 
-extern "C" int gsplat_hip_l1_ssim_loss_fused_fwd(int B, int H, int W, int C, const float *img1,
-                                                 const float *img2, const int64_t *img2_index,
-                                                 float lam, float *out, float *grad_unit,
-                                                 void *workspace, void *stream) {
-  return fused_fwd(B, H, W, C, img1, img2, img2_index, lam, out, grad_unit, workspace, nullptr, 0,
-                   nullptr, stream);
+extern "C" int gsplat_hip_l1_ssim_loss_fused_fwd(int B, int H, int W, int C, int x_stride,
+                                                 const float *img1, const float *img2,
+                                                 const int64_t *img2_index, float lam, float *out,
+                                                 float *grad_unit, void *workspace, void *stream) {
+  return fused_fwd(B, H, W, C, x_stride, img1, img2, img2_index, lam, out, grad_unit, workspace,
+                   nullptr, 0, nullptr, stream);
 }
 
-extern "C" int gsplat_hip_l1_ssim_loss_fused_fwd_ring(int B, int H, int W, int C,
+extern "C" int gsplat_hip_l1_ssim_loss_fused_fwd_ring(int B, int H, int W, int C, int x_stride,
                                                       const float *img1, const float *img2,
                                                       const int64_t *img2_index, float lam,
                                                       float *out, float *grad_unit,
@@ -908,8 +920,8 @@ extern "C" int gsplat_hip_l1_ssim_loss_fused_fwd_ring(int B, int H, int W, int C
                                                       void *stream) {
   GS_REQUIRE(loss_ring && seq_device && ring_len > 0,
              "l1_ssim_loss_fused_fwd_ring: null ring / step counter or empty ring");
-  return fused_fwd(B, H, W, C, img1, img2, img2_index, lam, out, grad_unit, workspace, loss_ring,
-                   ring_len, seq_device, stream);
+  return fused_fwd(B, H, W, C, x_stride, img1, img2, img2_index, lam, out, grad_unit, workspace,
+                   loss_ring, ring_len, seq_device, stream);
 }
 
 extern "C" int gsplat_hip_l1_ssim_loss_fused_bwd(int64_t n, const float *grad_unit,

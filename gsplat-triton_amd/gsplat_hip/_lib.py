@@ -88,11 +88,11 @@ _SIGS = {
     "gsplat_hip_l1_ssim_loss_fwd": (_i32, [_i32, _i32, _i32, _i32, _p, _p, _f, _p, _p, _p]),
     "gsplat_hip_l1_ssim_loss_bwd": (_i32, [_i32, _i32, _i32, _i32, _p, _p, _p, _f, _p, _p, _p]),
     "gsplat_hip_l1_ssim_loss_fused_workspace_bytes": (_i64, [_i32, _i32, _i32, _i32]),
-    "gsplat_hip_l1_ssim_loss_fused_fwd": (_i32, [_i32, _i32, _i32, _i32, _p, _p, _p, _f, _p, _p, _p,
-                                                  _p]),
+    "gsplat_hip_l1_ssim_loss_fused_fwd": (_i32, [_i32, _i32, _i32, _i32, _i32, _p, _p, _p, _f, _p,
+                                                  _p, _p, _p]),
     "gsplat_hip_l1_ssim_loss_fused_bwd": (_i32, [_i64, _p, _p, _p, _p]),
-    "gsplat_hip_l1_ssim_loss_fused_fwd_ring": (_i32, [_i32, _i32, _i32, _i32, _p, _p, _p, _f, _p,
-                                                       _p, _p, _p, _i64, _p, _p]),
+    "gsplat_hip_l1_ssim_loss_fused_fwd_ring": (_i32, [_i32, _i32, _i32, _i32, _i32, _p, _p, _p, _f,
+                                                       _p, _p, _p, _p, _i64, _p, _p]),
     "gsplat_hip_update_state": (_i32, [_i32, _i64, _p, _p, _f, _f, _p, _p, _p, _p]),
     "gsplat_hip_activate_fwd": (_i32, [_i64, _i64, _p, _p, _p, _p, _p]),
     "gsplat_hip_activate_bwd": (_i32, [_i64, _i64, _p, _p, _p, _p, _p, _p, _p]),

@@ -296,7 +296,7 @@ class GraphStep:
                 far_plane=1e10, render_mode="RGB+D", _fusion=fusion,
                 _isect_capacity=self.capacity, _isect_status=self.status,
                 _isect_report=(self.ring_out.dev, self.slot), _camtoworlds=self.c2w)
-            colors = rc[..., :3]
+            colors = rc  # the loss reads the colour channels in place (_channels=3)
             # the densification input is a leaf: its .grad after the backward
             # (a hook keeping a reference would make AccumulateGrad clone the
             # gradient -- a memcpy node in the graph)
@@ -315,7 +315,8 @@ class GraphStep:
             vote = dist.all_reduce(self.status, op=dist.ReduceOp.MAX, async_op=True)
         loss = tr._regularise(l1_ssim_loss(
             colors, tr.targets, tr.ssim_lambda, gt_index=self.cam,
-            _out_ring=(self.loss_ring, self.seq) if self.ring_loss else None))
+            _out_ring=(self.loss_ring, self.seq) if self.ring_loss else None,
+            _channels=3 if tr.model == "2dgs" else None))
         if vote is not None:
             vote.wait()
             _lib.call("gsplat_hip_status_to_ring", self.status.data_ptr(), self.ring_out.dev,

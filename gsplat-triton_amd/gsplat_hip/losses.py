@@ -86,33 +86,38 @@ class _L1SSIMLossFused(torch.autograd.Function):
     gradient.  The training path: no per-pixel SSIM partials through HBM."""
 
     @staticmethod
-    def forward(ctx, img, gt, lam, gt_index=None, out_ring=None):
+    def forward(ctx, img, gt, lam, gt_index=None, out_ring=None, channels=None):
         # gt_index: device int64 [1]; gt is then a stack [n, H, W, C] of
         # single-image targets and gt[gt_index] is this image's target.
         # out_ring: (ring float32 [R], seq int64 [1], both on the device): the
         # loss also goes to ring[(seq - 1) % R] (gsplat_hip_l1_ssim_loss_fused_fwd_ring)
+        # channels: the loss reads the first `channels` of img's XS channels
+        # (an RGB+D render in place); its gradient is img-shaped, zero in the rest
+        XS = img.shape[-1]
+        C = XS if channels is None else int(channels)
         if gt_index is None:
-            assert img.dim() == 4 and img.shape == gt.shape, (img.shape, gt.shape)
-        else:
-            assert img.dim() == 4 and img.shape[0] == 1 and gt.shape[1:] == img.shape[1:], \
+            assert img.dim() == 4 and img.shape[:3] == gt.shape[:3] and gt.shape[3] == C, \
                 (img.shape, gt.shape)
+        else:
+            assert img.dim() == 4 and img.shape[0] == 1 and gt.shape[1:3] == img.shape[1:3] \
+                and gt.shape[3] == C, (img.shape, gt.shape)
             assert gt_index.dtype == torch.int64 and gt_index.is_cuda and gt.is_contiguous()
         img = img.contiguous().float()
         gt = gt.contiguous().float()
-        B, H, W, C = img.shape
+        B, H, W, _ = img.shape
         ws = torch.empty(max(int(_lib.query("gsplat_hip_l1_ssim_loss_fused_workspace_bytes",
                                             B, H, W, C)), 4),
                          dtype=torch.uint8, device=img.device)
         out = torch.empty(3, device=img.device)
         unit = torch.empty_like(img)
         if out_ring is None:
-            _lib.call("gsplat_hip_l1_ssim_loss_fused_fwd", B, H, W, C, _ptr(img), _ptr(gt),
+            _lib.call("gsplat_hip_l1_ssim_loss_fused_fwd", B, H, W, C, XS, _ptr(img), _ptr(gt),
                       _ptr(gt_index), ctypes.c_float(lam), _ptr(out), _ptr(unit), _ptr(ws),
                       _stream())
         else:
             ring, seq = out_ring
             assert ring.dtype == torch.float32 and ring.is_cuda and seq.dtype == torch.int64
-            _lib.call("gsplat_hip_l1_ssim_loss_fused_fwd_ring", B, H, W, C, _ptr(img), _ptr(gt),
+            _lib.call("gsplat_hip_l1_ssim_loss_fused_fwd_ring", B, H, W, C, XS, _ptr(img), _ptr(gt),
                       _ptr(gt_index), ctypes.c_float(lam), _ptr(out), _ptr(unit), _ptr(ws),
                       _ptr(ring), ring.numel(), _ptr(seq), _stream())
         ctx.save_for_backward(unit)
@@ -122,12 +127,12 @@ class _L1SSIMLossFused(torch.autograd.Function):
     def backward(ctx, g_loss):
         (unit,) = ctx.saved_tensors
         if g_loss is ONE_GRAD:  # the trainer's constant 1.0 seed: the unit gradient as is
-            return unit, None, None, None, None
+            return unit, None, None, None, None, None
         g_loss = g_loss.float().contiguous()
         grad = torch.empty_like(unit)
         _lib.call("gsplat_hip_l1_ssim_loss_fused_bwd", unit.numel(), _ptr(unit), _ptr(g_loss),
                   _ptr(grad), _stream())
-        return grad, None, None, None, None
+        return grad, None, None, None, None, None
 
 
 # A constant scalar 1.0 the trainer seeds loss.backward() with (never written):
@@ -139,7 +144,8 @@ ONE_GRAD = None
 SSIM_FUSED = os.environ.get("GSPLAT_HIP_SSIM_FUSED", "1") != "0"
 
 
-def l1_ssim_loss(img, gt, ssim_lambda=0.2, fused=None, gt_index=None, _out_ring=None):
+def l1_ssim_loss(img, gt, ssim_lambda=0.2, fused=None, gt_index=None, _out_ring=None,
+                 _channels=None):
     """(1 - ssim_lambda) * mean L1 + ssim_lambda * (1 - mean SSIM_valid).
     With a gradient to compute (and C in {1, 3}) the one-pass fused kernel
     runs, unless `fused=False` (or GSPLAT_HIP_SSIM_FUSED=0).  `gt_index`
@@ -147,7 +153,17 @@ def l1_ssim_loss(img, gt, ssim_lambda=0.2, fused=None, gt_index=None, _out_ring=
     gt[gt_index] the one of this [1, H, W, C] image -- chosen on the device,
     no copy (the captured training step).  `_out_ring` (internal, with
     gt_index): (ring, seq) device tensors; the loss value is also written to
-    ring[(seq - 1) % len(ring)] by the reduction launch (graph_step.py)."""
+    ring[(seq - 1) % len(ring)] by the reduction launch (graph_step.py).
+    `_channels` (internal): the loss is over img[..., :_channels] (an RGB+D
+    render read in place by the fused kernel; its gradient is img-shaped)."""
+    if _channels is not None and _channels != img.shape[-1]:
+        if fused is None:
+            fused = SSIM_FUSED and torch.is_grad_enabled() and img.requires_grad
+        if not (fused and img.dim() == 4 and _channels in (1, 3)):
+            img = img[..., :_channels]  # the generic path on the slice
+        else:
+            return _L1SSIMLossFused.apply(img, gt, float(ssim_lambda), gt_index, _out_ring,
+                                          int(_channels))
     if fused is None:
         fused = SSIM_FUSED and torch.is_grad_enabled() and img.requires_grad
     if gt_index is not None:

@@ -453,6 +453,7 @@ class Trainer:
                 self.viewmats[ci:ci + 1], self.Ks[ci:ci + 1], self.width, self.height,
                 sh_degree=deg, packed=False, near_plane=0.01, far_plane=1e10,
                 render_mode="RGB+D", absgrad=absgrad, _fusion=fusion)
+            meta["_rgbd"] = rc  # the loss reads its colour channels in place
             return rc[..., :3], ra, meta
         dkw = {}
         if getattr(self, "gshard", False):
@@ -518,7 +519,9 @@ class Trainer:
             # captured by a hook (retain_grad would clone it into .grad)
             meta["means2d"].register_hook(lambda g: meta.__setitem__("means2d_grad", g))
         gt = self.targets[ci:ci + 1]
-        if self.fused:
+        if self.fused and "_rgbd" in meta:  # 2DGS: the RGB+D render in place
+            loss = l1_ssim_loss(meta["_rgbd"], gt, self.ssim_lambda, _channels=3)
+        elif self.fused:
             loss = l1_ssim_loss(colors, gt, self.ssim_lambda)
         else:
             l1 = F.l1_loss(colors, gt)

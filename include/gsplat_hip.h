@@ -398,12 +398,16 @@ int gsplat_hip_l1_ssim_loss_bwd(int B, int H, int W, int C, const float *img1,
  *            img2_index (ABI 21, may be NULL): device int64; img2 is then a
  *            stack of [B,H,W,C] images and image img2_index[0] is the target
  *            (a captured training step picks its camera's target on the device).
+ *            x_stride (ABI 32, >= C): floats per pixel of img1 and grad_unit
+ *            (img2 has C): an RGB+D render's colour channels read in place
+ *            (x_stride 4, C 3); grad_unit's channels C .. x_stride-1 are
+ *            written as zeros (the loss does not read them).
  * fused_bwd: grad_img1[i] = g_loss[0] * grad_unit[i] (16-B aligned buffers). */
 int64_t gsplat_hip_l1_ssim_loss_fused_workspace_bytes(int B, int H, int W, int C);
-int gsplat_hip_l1_ssim_loss_fused_fwd(int B, int H, int W, int C, const float *img1,
-                                      const float *img2, const int64_t *img2_index, float lam,
-                                      float *out, float *grad_unit, void *workspace,
-                                      void *stream);
+int gsplat_hip_l1_ssim_loss_fused_fwd(int B, int H, int W, int C, int x_stride,
+                                      const float *img1, const float *img2,
+                                      const int64_t *img2_index, float lam, float *out,
+                                      float *grad_unit, void *workspace, void *stream);
 int gsplat_hip_l1_ssim_loss_fused_bwd(int64_t n, const float *grad_unit, const float *g_loss,
                                       float *grad_img1, void *stream);
 /* fused_fwd_ring (ABI 30): fused_fwd, and the loss out[0] also written to
@@ -411,8 +415,9 @@ int gsplat_hip_l1_ssim_loss_fused_bwd(int64_t n, const float *grad_unit, const f
  * a captured training step returns that slot instead of copying its static
  * output after every replay (seq_device: the step counter the step's fetch
  * launch has already incremented; gsplat_hip/graph_step.py). */
-int gsplat_hip_l1_ssim_loss_fused_fwd_ring(int B, int H, int W, int C, const float *img1,
-                                           const float *img2, const int64_t *img2_index,
+int gsplat_hip_l1_ssim_loss_fused_fwd_ring(int B, int H, int W, int C, int x_stride,
+                                           const float *img1, const float *img2,
+                                           const int64_t *img2_index,
                                            float lam, float *out, float *grad_unit,
                                            void *workspace, float *loss_ring, int64_t ring_len,
                                            const int64_t *seq_device, void *stream);

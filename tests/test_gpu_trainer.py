@@ -59,6 +59,36 @@ def test_l1_ssim_loss_matches_torch(B, H, W, C, lam, fused):
     torch.testing.assert_close(img.grad, img_r.grad, rtol=1e-3, atol=1e-9)
 
 
+@pytest.mark.parametrize("H,W,ring", [(64, 80, False), (1080, 1920, False), (37, 131, True)])
+def test_fused_loss_reads_rgbd_render_in_place(H, W, ring):
+    """The fused loss over the colour channels of an RGB+D render read in
+    place (x_stride 4, the 2DGS trainer's loss) equals the loss of the
+    contiguous colour copy bit for bit, value and gradient; the depth
+    channel's gradient is exactly zero (no slice copy, no zero-filled
+    gradient image)."""
+    from gsplat_hip.losses import ONE_GRAD, l1_ssim_loss
+    import gsplat_hip.losses as L
+    g = torch.Generator(device="cuda").manual_seed(H + W)
+    rgbd = torch.rand(1, H, W, 4, device="cuda", generator=g)
+    gt = torch.rand(3, H, W, 3, device="cuda", generator=g)
+    idx = torch.tensor([1], device="cuda")
+    kw = {}
+    if ring:
+        kw = dict(gt_index=idx, _out_ring=(torch.zeros(8, device="cuda"),
+                                          torch.ones(1, dtype=torch.int64, device="cuda")))
+    target = gt if ring else gt[1:2].contiguous()
+    a = rgbd.clone().requires_grad_(True)
+    b = rgbd[..., :3].contiguous().requires_grad_(True)
+    la = l1_ssim_loss(a, target, 0.2, fused=True, _channels=3, **kw)
+    lb = l1_ssim_loss(b, target, 0.2, fused=True, **kw)
+    assert torch.equal(la, lb), (float(la), float(lb))
+    la.backward()
+    lb.backward()
+    assert a.grad.shape == (1, H, W, 4)
+    assert torch.equal(a.grad[..., :3], b.grad)
+    assert torch.equal(a.grad[..., 3], torch.zeros_like(a.grad[..., 3]))
+
+
 def test_fused_loss_matches_two_pass_on_renders():
     """Fused vs two-pass loss on a smooth, correlated image pair (a render
     and a shifted copy, as in training): same loss, same gradient up to the
