@@ -489,9 +489,11 @@ constexpr int kHA = 6, kHC = 4;  // adjacent outputs per work item in passes A, 
 // row from one run of K + kHA - 1 / K + kHC - 1 LDS values.
 // CPW: channels per workgroup (C / CPW workgroups per tile, channel groups of
 // a tile adjacent in the XCD-aware order so they share that XCD's L2).
-template <int C, int BR, int CPW = C>
+// XS: floats per pixel of x and grad (a compile-time constant: a runtime
+// stride cost the C = 3 kernel 114 -> 148 us at 1080p).
+template <int C, int BR, int CPW = C, int XS = C>
 __global__ void __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(4)))
-fused_kernel(int B, int H, int W, int XS, const float *__restrict__ x,
+fused_kernel(int B, int H, int W, const float *__restrict__ x,
              const float *__restrict__ y, const int64_t *__restrict__ y_index, float cs, float cl,
              float *__restrict__ grad, float *__restrict__ partials) {
   static_assert(C % CPW == 0, "channel groups");
@@ -885,15 +887,21 @@ static int fused_fwd(int B, int H, int W, int C, int XS, const float *img1, cons
     const char *e = getenv("GSPLAT_HIP_SSIM_FV");
     return e ? atoi(e) : 0;
   }();
-#define GS_FUSED(CC, BR, CPW)                                                                \
-  hipLaunchKernelGGL((ssim::fused_kernel<CC, BR, CPW>), grid, dim3(ssim::kFThreads), 0, st, B, H, \
-                     W, XS, img1, img2, img2_index, cs, cl, grad_unit, partials)
-  if (C == 3) {
-    if (cg == 3) GS_FUSED(3, 4, 1);
-    else if (fv == 1) GS_FUSED(3, 2, 3);
-    else GS_FUSED(3, 4, 3);
+#define GS_FUSED(CC, BR, CPW, XS_)                                                           \
+  hipLaunchKernelGGL((ssim::fused_kernel<CC, BR, CPW, XS_>), grid, dim3(ssim::kFThreads), 0, st, \
+                     B, H, W, img1, img2, img2_index, cs, cl, grad_unit, partials)
+  GS_REQUIRE(XS == C || (C == 3 && XS == 4),
+             "l1_ssim_loss_fused_fwd: pixel stride %d with C = %d (supported: C, or 4 with C = 3)",
+             XS, C);
+  if (C == 3 && XS == 4) {
+    if (cg == 3) GS_FUSED(3, 4, 1, 4);
+    else GS_FUSED(3, 4, 3, 4);
+  } else if (C == 3) {
+    if (cg == 3) GS_FUSED(3, 4, 1, 3);
+    else if (fv == 1) GS_FUSED(3, 2, 3, 3);
+    else GS_FUSED(3, 4, 3, 3);
   } else {
-    GS_FUSED(1, 2, 1);
+    GS_FUSED(1, 2, 1, 1);
   }
 #undef GS_FUSED
   hipLaunchKernelGGL(ssim::reduce_partials_kernel, dim3(1), dim3(1024), 0, st, (int)(B * nt),

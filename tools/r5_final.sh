@@ -5,6 +5,9 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 O=gpurun_out/r5_final; mkdir -p $O
+timeout -k 10 300 python -u -m pytest tests/test_gpu_trainer.py -x -q --timeout 200 --timeout-method thread \
+  -k "loss or ssim" > $O/loss_tests.log 2>&1
+rc=$?; echo "loss tests rc=$rc"; tail -1 $O/loss_tests.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 600 python bench.py > $O/bench_m2.json 2> $O/bench_m2.err || exit 3
 python -c "import json; d=json.load(open('$O/bench_m2.json')); print('m2', round(d['value'],1), round(d['ms_per_step'],4), 'fwd', d['roofline']['launch_ms'], d['roofline']['frac'], d['roofline']['traffic'], 'cpu', d['cpu_baseline'])"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $O/trace_m2 -o run -- /usr/bin/python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-traffic > $O/trace_m2.log 2>&1 || exit 4
