@@ -842,27 +842,31 @@ __global__ void __launch_bounds__(128) fwd2_kernel(RasterArgs a) {
 __global__ void __launch_bounds__(1024)
 tile_order_kernel(int n_tiles, const int32_t *__restrict__ offsets, int64_t n_isects,
                   const int64_t *__restrict__ n_dev, int32_t *__restrict__ order) {
+  constexpr int MAXR = 16;  // tiles per thread (n_tiles <= 16384)
   __shared__ int hist[34];
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63;
   if (tid < 34) hist[tid] = 0;
-  __syncthreads();
   const int64_t total = n_dev ? n_dev[0] : n_isects;
-  auto key = [&](int t) {
-    const int64_t e = t == n_tiles - 1 ? total : (int64_t)offsets[t + 1];
-    const int64_t n = e - offsets[t];
-    return n > 0 ? 32 - (63 - __builtin_clzll((uint64_t)n)) : 33;  // 2^31.. -> 1, 1 -> 32
-  };
+  // every tile's two offsets loaded up front (one load latency, not one per
+  // round), the keys kept in registers for both passes
+  int k[MAXR];
+#pragma unroll
+  for (int rd = 0; rd < MAXR; ++rd) {
+    const int t = tid + 1024 * rd;
+    int64_t n = -1;
+    if (t < n_tiles) n = (t == n_tiles - 1 ? total : (int64_t)offsets[t + 1]) - offsets[t];
+    // 2^31.. -> 1, 1 -> 32, empty -> 33, no tile -> -1
+    k[rd] = n < 0 ? -1 : (n > 0 ? 32 - (63 - __builtin_clzll((uint64_t)n)) : 33);
+  }
+  __syncthreads();
   // per wave and distinct key one LDS atomic (a few keys per wave: M5's
   // tiles fall into 2-3 buckets, and 64 lanes on one counter serialised)
-  const int lane = tid & 63;
-  const int n_rounds = (n_tiles + 1023) / 1024;
-  for (int rd = 0; rd < n_rounds; ++rd) {
-    const int t = tid + 1024 * rd;
-    const int k = t < n_tiles ? key(t) : -1;
-    uint64_t todo = __ballot(k >= 0);
+#pragma unroll
+  for (int rd = 0; rd < MAXR; ++rd) {
+    uint64_t todo = __ballot(k[rd] >= 0);
     while (todo) {
-      const int kk = __builtin_amdgcn_readlane(k, __builtin_ctzll(todo));
-      const uint64_t m = __ballot(k == kk) & todo;
+      const int kk = __builtin_amdgcn_readlane(k[rd], __builtin_ctzll(todo));
+      const uint64_t m = __ballot(k[rd] == kk) & todo;
       if (lane == __builtin_ctzll(m)) atomicAdd(&hist[kk], __popcll(m));
       todo &= ~m;
     }
@@ -870,25 +874,25 @@ tile_order_kernel(int n_tiles, const int32_t *__restrict__ offsets, int64_t n_is
   __syncthreads();
   if (tid == 0) {
     int run = 0;
-    for (int k = 0; k < 34; ++k) {
-      const int h = hist[k];
-      hist[k] = run;
+    for (int q = 0; q < 34; ++q) {
+      const int h = hist[q];
+      hist[q] = run;
       run += h;
     }
   }
   __syncthreads();
-  for (int rd = 0; rd < n_rounds; ++rd) {
+#pragma unroll
+  for (int rd = 0; rd < MAXR; ++rd) {
     const int t = tid + 1024 * rd;
-    const int k = t < n_tiles ? key(t) : -1;
-    uint64_t todo = __ballot(k >= 0);
+    uint64_t todo = __ballot(k[rd] >= 0);
     while (todo) {
-      const int kk = __builtin_amdgcn_readlane(k, __builtin_ctzll(todo));
-      const uint64_t m = __ballot(k == kk) & todo;
+      const int kk = __builtin_amdgcn_readlane(k[rd], __builtin_ctzll(todo));
+      const uint64_t m = __ballot(k[rd] == kk) & todo;
       const int leader = __builtin_ctzll(m);
       int base = 0;
       if (lane == leader) base = atomicAdd(&hist[kk], __popcll(m));
       base = __shfl(base, leader, 64);
-      if (k == kk) order[base + __popcll(m & ((1ull << lane) - 1))] = t;
+      if (k[rd] == kk) order[base + __popcll(m & ((1ull << lane) - 1))] = t;
       todo &= ~m;
     }
   }
@@ -1190,10 +1194,15 @@ __global__ void __launch_bounds__(128) fwd2s_kernel(RasterArgs a, const float *_
 
 // Gradient fields of a packed row: colour[D], normal[3], ray transform[9],
 // means2d[2], opacity, |means2d|[2] (absgrad only).
-template <int D, bool ABS>
+// LEAN (the backward of a render whose normals, distortion and median carry
+// no gradient -- the training step's RGB(+D) loss): no normal fields, so
+// D + 12 fields (one reduce-scatter group for RGB+D instead of two).
+template <int D, bool ABS, bool LEAN = false>
 struct Fields {
-  static constexpr int COL = 0, NRM = D, M = D + 3, XY = D + 12, OP = D + 14, AB = D + 15;
-  static constexpr int NF = D + 15 + (ABS ? 2 : 0);
+  static constexpr int NN = LEAN ? 0 : 3;  // normal fields
+  static constexpr int COL = 0, NRM = D, M = D + NN, XY = D + NN + 9, OP = D + NN + 11,
+                       AB = D + NN + 12;
+  static constexpr int NF = D + NN + 12 + (ABS ? 2 : 0);
   static constexpr int NV = (NF + 15) / 16;  // reduce_scatter groups
   static constexpr int S = 16 * NV;          // packed row stride (floats)
 };
@@ -1358,10 +1367,13 @@ struct PixState {
   bool inside;
 };
 
-template <int D, bool ABS>
+// LEAN: v_render_normals, v_render_distort and v_render_median are null (the
+// terms they feed are exact zeros, skipped): 26 fewer VGPRs of per-pixel state
+// and no normal fields in the reduce-scatter.
+template <int D, bool ABS, bool LEAN = false>
 __global__ void __launch_bounds__(128) bwd2_kernel(RasterArgs a) {
   using R = Rec<D>;
-  using F = Fields<D, ABS>;
+  using F = Fields<D, ABS, LEAN>;
   extern __shared__ float4 lds4[];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   float *q = reinterpret_cast<float *>(lds4) + (size_t)w * 64 * R::NF;
@@ -1398,18 +1410,20 @@ __global__ void __launch_bounds__(128) bwd2_kernel(RasterArgs a) {
       if (a.backgrounds) bg_dot += a.backgrounds[(int64_t)c * D + d] * s.vc[d];
     }
     s.tfvb = Tf * ((a.v_render_alphas ? a.v_render_alphas[pid] : 0.f) - bg_dot);
+    if (!LEAN) {
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      s.vn[i] = a.v_render_normals ? a.v_render_normals[pid * 3 + i] : 0.f;
-      s.bufn[i] = 0.f;
+      for (int i = 0; i < 3; ++i) {
+        s.vn[i] = a.v_render_normals ? a.v_render_normals[pid * 3 + i] : 0.f;
+        s.bufn[i] = 0.f;
+      }
+      s.vdist = a.v_render_distort ? a.v_render_distort[pid] : 0.f;
+      s.accum_d = a.render_colors[pid * D + D - 1];
+      s.accum_w = 1.f - Tf;
+      s.accd_buf = s.accum_d;
+      s.accw_buf = s.accum_w;
+      s.dist_buf = 0.f;
+      s.vmed = a.v_render_median ? a.v_render_median[pid] : 0.f;
     }
-    s.vdist = a.v_render_distort ? a.v_render_distort[pid] : 0.f;
-    s.accum_d = a.render_colors[pid * D + D - 1];
-    s.accum_w = 1.f - Tf;
-    s.accd_buf = s.accum_d;
-    s.accw_buf = s.accum_w;
-    s.dist_buf = 0.f;
-    s.vmed = a.v_render_median ? a.v_render_median[pid] : 0.f;
     wmax = max(wmax, s.bin_final);
   }
 #pragma unroll
@@ -1451,7 +1465,7 @@ __global__ void __launch_bounds__(128) bwd2_kernel(RasterArgs a) {
         PixState<D> &s = ps[k];
         const Hit &hk = h[k];
         if (!valid[k]) continue;
-        if (idx == s.med_idx) v[F::COL + D - 1] += s.vmed;
+        if (!LEAN && idx == s.med_idx) v[F::COL + D - 1] += s.vmed;
         const float ra = __builtin_amdgcn_rcpf(1.f - hk.alpha);
         s.T *= ra;
         const float T = s.T;
@@ -1462,13 +1476,15 @@ __global__ void __launch_bounds__(128) bwd2_kernel(RasterArgs a) {
           v[F::COL + d] += fac * s.vc[d];
           v_alpha += (r[R::COL + d] * T - s.buf[d] * ra) * s.vc[d];
         }
+        if (!LEAN) {
 #pragma unroll
-        for (int i = 0; i < 3; ++i) {
-          v[F::NRM + i] += fac * s.vn[i];
-          v_alpha += (r[R::NRM + i] * T - s.bufn[i] * ra) * s.vn[i];
+          for (int i = 0; i < 3; ++i) {
+            v[F::NRM + i] += fac * s.vn[i];
+            v_alpha += (r[R::NRM + i] * T - s.bufn[i] * ra) * s.vn[i];
+          }
         }
         v_alpha += ra * s.tfvb;
-        {  // distortion (RasterizeToPixels2DGSBwd.cu:483-503)
+        if (!LEAN) {  // distortion (RasterizeToPixels2DGSBwd.cu:483-503)
           const float depth = r[R::COL + D - 1];
           const float dl_dw =
               2.f * (2.f * (depth * s.accw_buf - s.accd_buf) + (s.accum_d - depth * s.accum_w));
@@ -1512,8 +1528,10 @@ __global__ void __launch_bounds__(128) bwd2_kernel(RasterArgs a) {
         }
 #pragma unroll
         for (int d = 0; d < D; ++d) s.buf[d] += r[R::COL + d] * fac;
+        if (!LEAN) {
 #pragma unroll
-        for (int i = 0; i < 3; ++i) s.bufn[i] += r[R::NRM + i] * fac;
+          for (int i = 0; i < 3; ++i) s.bufn[i] += r[R::NRM + i] * fac;
+        }
       }
       const int32_t g = __float_as_int(r[R::G]);
       float *row = a.packed + (int64_t)g * F::S;
@@ -1543,14 +1561,14 @@ zero_rows_kernel(int64_t G, int S, const int32_t *__restrict__ visible, float *_
 // packed [G][S] -> autograd tensors; densify = (v_M[0][2], v_M[1][2]) * depth
 // with depth = M[2][2] (the reference writes this racily from partial sums,
 // RasterizeToPixels2DGSBwd.cu:689-697; here it is formed from the final sums).
-template <int D, bool ABS>
+template <int D, bool ABS, bool LEAN = false>
 __global__ void __launch_bounds__(256)
 unpack_kernel(int64_t G, const int32_t *__restrict__ visible, const float *__restrict__ packed,
               const float *__restrict__ rt,
               float *__restrict__ v_means2d, float *__restrict__ v_rt, float *__restrict__ v_colors,
               float *__restrict__ v_opacities, float *__restrict__ v_normals,
               float *__restrict__ v_densify, float *__restrict__ v_abs) {
-  using F = Fields<D, ABS>;
+  using F = Fields<D, ABS, LEAN>;
   const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= G) return;
   if (visible && visible[g] <= 0) {  // no isect: every gradient is zero (row never zeroed)
@@ -1570,7 +1588,7 @@ unpack_kernel(int64_t G, const int32_t *__restrict__ visible, const float *__res
 #pragma unroll
   for (int d = 0; d < D; ++d) v_colors[g * D + d] = r[F::COL + d];
 #pragma unroll
-  for (int i = 0; i < 3; ++i) v_normals[g * 3 + i] = r[F::NRM + i];
+  for (int i = 0; i < 3; ++i) v_normals[g * 3 + i] = LEAN ? 0.f : r[F::NRM + i];
 #pragma unroll
   for (int i = 0; i < 9; ++i) v_rt[g * 9 + i] = r[F::M + i];
   *reinterpret_cast<float2 *>(v_means2d + 2 * g) = make_float2(r[F::XY], r[F::XY + 1]);
@@ -1618,6 +1636,19 @@ bool bwd2_enabled() {
 int fields_stride(int D, int absgrad) {
   const int nf = D + 15 + (absgrad ? 2 : 0);
   return 16 * ((nf + 15) / 16);
+}
+
+int lean_stride(int D, int absgrad) {  // Fields<D, ABS, true>::S
+  const int nf = D + 12 + (absgrad ? 2 : 0);
+  return 16 * ((nf + 15) / 16);
+}
+
+bool lean_enabled() {
+  static const bool v = [] {
+    const char *e = getenv("GSPLAT_HIP_SURFEL_LEAN");
+    return !(e && atoi(e) == 0);
+  }();
+  return v;
 }
 
 int check_tiles(int C, int W, int H, int ts, int tw, int th) {
@@ -1820,7 +1851,7 @@ extern "C" int gsplat_hip_rasterize_2dgs_fwd(
   a.render_median = render_median; a.last_ids = last_ids; a.median_ids = median_ids;
   const int waves = (tile_size * tile_size + 63) / 64;
   hipStream_t st = (hipStream_t)stream;
-  if (tile_order && n_tiles > 0) {  // written here, read by this launch and the backward
+  if (tile_order && n_tiles > 0 && n_tiles <= 16384) {  // written here, read by this launch and the backward
     hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(1024), 0, st, n_tiles, isect_offsets,
                        n_isects, n_isects_device, tile_order);
     a.order = tile_order;
@@ -1902,7 +1933,12 @@ extern "C" int gsplat_hip_rasterize_2dgs_bwd(
   GS_REQUIRE(channels_supported(D), "rasterize_2dgs_bwd: unsupported channel count %d", D);
   GS_REQUIRE(tile_size * tile_size <= 256, "rasterize_2dgs_bwd: tile_size %d > 16", tile_size);
   const int absgrad = v_means2d_abs != nullptr;
-  const int S = fields_stride(D, absgrad);
+  // LEAN kernels (bwd2_kernel): 16x16 tiles, D <= 4, no normal / distortion /
+  // median gradient (GSPLAT_HIP_SURFEL_LEAN=0: the general kernel)
+  const bool px2 = tile_size == 16 && bwd2_enabled();
+  const bool lean = px2 && D <= 4 && lean_enabled() && !v_render_normals && !v_render_distort &&
+                    !v_render_median;
+  const int S = lean ? lean_stride(D, absgrad) : fields_stride(D, absgrad);
   const int64_t G = n_gaussians;
   GS_REQUIRE(workspace_bytes >= G * S * (int64_t)sizeof(float),
              "rasterize_2dgs_bwd: workspace too small");
@@ -1938,11 +1974,16 @@ extern "C" int gsplat_hip_rasterize_2dgs_bwd(
     a.packed = (float *)workspace; a.S = S;
     const int waves = (tile_size * tile_size + 63) / 64;
     // 16x16 tiles: two pixels per lane (bwd2_kernel) unless GSPLAT_HIP_BWD_PX=1
-    const bool px2 = tile_size == 16 && bwd2_enabled();
 #define GS_CASE(n)                                                                            \
   if (D == n) {                                                                               \
     const size_t lds = (size_t)waves * 64 * Rec<n>::NF * sizeof(float);                       \
-    if (px2 && absgrad)                                                                       \
+    if (lean && absgrad)                                                                      \
+      hipLaunchKernelGGL((bwd2_kernel<n <= 4 ? n : 4, true, true>), dim3(n_tiles), dim3(128), \
+                         lds / 2, st, a);                                                     \
+    else if (lean)                                                                            \
+      hipLaunchKernelGGL((bwd2_kernel<n <= 4 ? n : 4, false, true>), dim3(n_tiles), dim3(128),\
+                         lds / 2, st, a);                                                     \
+    else if (px2 && absgrad)                                                                       \
       hipLaunchKernelGGL((bwd2_kernel<n, true>), dim3(n_tiles), dim3(128), lds / 2, st, a);    \
     else if (px2)                                                                             \
       hipLaunchKernelGGL((bwd2_kernel<n, false>), dim3(n_tiles), dim3(128), lds / 2, st, a);   \
@@ -1957,7 +1998,18 @@ extern "C" int gsplat_hip_rasterize_2dgs_bwd(
   }
   const dim3 grid((unsigned)((G + 255) / 256));
 #define GS_CASE(n)                                                                             \
-  if (D == n) {                                                                                \
+  if (D == n && lean) {                                                                        \
+    if (absgrad)                                                                               \
+      hipLaunchKernelGGL((unpack_kernel<n <= 4 ? n : 4, true, true>), grid, dim3(256), 0, st, G, \
+                         visible, (const float *)workspace, ray_transforms, v_means2d,         \
+                         v_ray_transforms, v_colors, v_opacities, v_normals, v_densify,        \
+                         v_means2d_abs);                                                       \
+    else                                                                                       \
+      hipLaunchKernelGGL((unpack_kernel<n <= 4 ? n : 4, false, true>), grid, dim3(256), 0, st, G,\
+                         visible, (const float *)workspace, ray_transforms, v_means2d,         \
+                         v_ray_transforms, v_colors, v_opacities, v_normals, v_densify,        \
+                         v_means2d_abs);                                                       \
+  } else if (D == n) {                                                                         \
     if (absgrad)                                                                               \
       hipLaunchKernelGGL((unpack_kernel<n, true>), grid, dim3(256), 0, st, G, visible, (const float *)workspace, \
                          ray_transforms, v_means2d, v_ray_transforms, v_colors, v_opacities,   \

@@ -47,6 +47,7 @@ class _FullyFusedProjection2DGS(torch.autograd.Function):
         ctx.save_for_backward(means, quats, scales, viewmats, Ks, radii, ray_transforms, normals)
         ctx.width, ctx.height, ctx.eps2d = int(width), int(height), eps2d
         ctx.mark_non_differentiable(radii)
+        ctx.set_materialize_grads(False)  # no zero-filled gradient of radii (or unused outputs)
         return radii, means2d, depths, ray_transforms, normals
 
     @staticmethod

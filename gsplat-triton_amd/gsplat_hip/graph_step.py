@@ -295,7 +295,8 @@ class GraphStep:
                 tr.width, tr.height, sh_degree=deg, packed=False, near_plane=0.01,
                 far_plane=1e10, render_mode="RGB+D", _fusion=fusion,
                 _isect_capacity=self.capacity, _isect_status=self.status,
-                _isect_report=(self.ring_out.dev, self.slot), _camtoworlds=self.c2w)
+                _isect_report=(self.ring_out.dev, self.slot), _camtoworlds=self.c2w,
+                _colors_only=True)
             colors = rc  # the loss reads the colour channels in place (_channels=3)
             # the densification input is a leaf: its .grad after the backward
             # (a hook keeping a reference would make AccumulateGrad clone the

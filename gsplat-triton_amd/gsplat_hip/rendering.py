@@ -512,6 +512,7 @@ def rasterization_2dgs(
     _isect_status: Optional[Tensor] = None,
     _isect_report=None,
     _camtoworlds: Optional[Tensor] = None,
+    _colors_only: bool = False,
 ):
     """Rasterize N surfels (2DGS) to C images (gsplat/rendering.py:1018-1339).
 
@@ -521,7 +522,10 @@ def rasterization_2dgs(
     strategy reads.  Private (the captured training step, graph_step): the
     sync-free isect as rasterization()'s `_isect_capacity` / `_isect_status`
     / `_isect_report` (meta["isect_counts"]); `_camtoworlds` [C,4,4] the
-    inverse viewmats (torch.linalg.inv reads its error flag on the host)."""
+    inverse viewmats (torch.linalg.inv reads its error flag on the host);
+    `_colors_only` (the training step, whose loss reads the colours alone):
+    render_normals and render_normals_from_depth are not formed (None) --
+    the world-space rotation and the depth-to-normal pass are skipped."""
     from ._wrapper_2dgs import fully_fused_projection_2dgs, rasterize_to_pixels_2dgs
 
     N = means.shape[0]
@@ -561,7 +565,10 @@ def rasterization_2dgs(
         radii, means2d, depths, ray_transforms, normals = proj
         opacities = opacities[None] if C == 1 else opacities.repeat(C, 1)
         camera_ids, gaussian_ids = None, None
-    densify = torch.zeros_like(means2d, dtype=means.dtype, requires_grad=True)
+    # the densification input only receives a gradient (its values are never
+    # read): the training step's (_colors_only) skips the reference's zero fill
+    densify = (torch.empty_like(means2d, dtype=means.dtype) if _colors_only else
+               torch.zeros_like(means2d, dtype=means.dtype)).requires_grad_(True)
 
     tile_width = math.ceil(width / float(tile_size))
     tile_height = math.ceil(height / float(tile_size))
@@ -620,6 +627,18 @@ def rasterization_2dgs(
                                  backgrounds=backgrounds, packed=packed, absgrad=absgrad,
                                  distloss=distloss, _n_isects_device=counts,
                                  _visible=tiles_per_gauss)
+    if _colors_only:
+        meta = {"camera_ids": camera_ids, "gaussian_ids": gaussian_ids, "radii": radii,
+                "means2d": means2d, "depths": depths, "ray_transforms": ray_transforms,
+                "opacities": opacities, "normals": normals, "tile_width": tile_width,
+                "tile_height": tile_height, "tiles_per_gauss": tiles_per_gauss,
+                "isect_ids": isect_ids, "flatten_ids": flatten_ids,
+                "isect_offsets": isect_offsets, "width": width, "height": height,
+                "tile_size": tile_size, "n_cameras": C, "render_distort": render_distort,
+                "gradient_2dgs": densify}
+        if counts is not None:
+            meta["isect_counts"] = counts
+        return render_colors, render_alphas, None, None, render_distort, render_median, meta
     camtoworlds = torch.linalg.inv(viewmats) if _camtoworlds is None else _camtoworlds
     render_normals_from_depth = None
     if render_mode in ["ED", "RGB+ED"]:

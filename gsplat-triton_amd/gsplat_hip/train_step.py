@@ -452,7 +452,7 @@ class Trainer:
                 p["means"], p["quats"], scales, opac, (p["sh0"], p["shN"]),
                 self.viewmats[ci:ci + 1], self.Ks[ci:ci + 1], self.width, self.height,
                 sh_degree=deg, packed=False, near_plane=0.01, far_plane=1e10,
-                render_mode="RGB+D", absgrad=absgrad, _fusion=fusion)
+                render_mode="RGB+D", absgrad=absgrad, _fusion=fusion, _colors_only=True)
             meta["_rgbd"] = rc  # the loss reads its colour channels in place
             return rc[..., :3], ra, meta
         dkw = {}

@@ -217,6 +217,61 @@ def test_raster2dgs_bwd(seed, D, bg, absgrad, thin):
                    max_frac=5e-3, rows=True)
 
 
+@pytest.mark.parametrize("seed,D,bg,absgrad,thin", [(0, 4, True, False, False),
+                                                    (1, 3, False, True, False),
+                                                    (2, 1, True, False, True)])
+def test_raster2dgs_bwd_lean_vs_oracle(seed, D, bg, absgrad, thin):
+    """The LEAN backward (csrc/surfel.hip bwd2_kernel<D, ABS, true>): a loss on
+    the colours and alphas only -- the normal, distortion and median outputs
+    get no gradient (None in the backward), the training step's case -- against
+    the oracle's backward with zero gradients for those outputs."""
+    sc = surfel_scene(seed, N=300, W=70, H=52, D=D, bg=bg, thin=thin)
+    leaves, bgt, densify, outs = _raster_gpu(sc, absgrad=absgrad)
+    rng = np.random.default_rng(seed + 200)
+    vs = [rng.standard_normal(o.shape).astype(np.float32) for o in outs]
+    for i in (2, 3, 4):  # normals, distortion, median: no loss term
+        vs[i] = np.zeros_like(vs[i])
+    loss = (outs[0] * T(vs[0])).sum() + (outs[1] * T(vs[1])).sum()
+    wrt = list(leaves.values()) + ([bgt] if bgt is not None else []) + [densify]
+    grads = torch.autograd.grad(loss, wrt)
+    oc, oa, on, od, om, ol, omi = _oracle_fwd(sc)
+    ref = S.raster2dgs_bwd(sc["m2"], sc["rt"], sc["colors"], sc["opac"], sc["nr"], sc["bg"], None,
+                           sc["W"], sc["H"], sc["ts"], sc["off"], sc["fids"], oc, oa, ol, omi,
+                           *vs, absgrad=absgrad)
+    vm, vrt, vcl, vop, vnr, vden, vbg, vab = ref
+    names = ["v_means2d", "v_ray_transforms", "v_colors", "v_opacities", "v_normals"]
+    for gpu, o, n in zip(grads[:5], (vm, vrt, vcl, vop, vnr), names):
+        scale = max(1.0, float(np.abs(o).max()))
+        close_most(gpu, o, 1e-3, 1e-3 * scale, n, max_frac=5e-3, rows=True)
+    assert float(grads[4].abs().max()) == 0.0  # v_normals: exactly zero
+    if bg:
+        close(grads[5], vbg, 1e-4, 1e-4, "v_backgrounds")
+    close_most(grads[-1], vden, 1e-3, 1e-3 * max(1.0, float(np.abs(vden).max())), "v_densify",
+               max_frac=5e-3, rows=True)
+    if absgrad:
+        close_most(leaves["m2"].absgrad, vab, 1e-3, 1e-3 * max(1.0, float(np.abs(vab).max())),
+                   "absgrad", max_frac=5e-3, rows=True)
+
+
+def test_raster2dgs_bwd_lean_matches_general():
+    """LEAN against the general backward on the same scene: the general one
+    runs when the normal / distortion / median outputs get explicit zero
+    gradients (the terms LEAN skips are exact zeros), so the two agree to the
+    order of their float atomics."""
+    sc = surfel_scene(4, N=800, W=150, H=100, D=4, bg=True, C=1, thin=True)
+    res = []
+    for general in (False, True):
+        leaves, bgt, densify, out = _raster_gpu(sc)
+        w0 = torch.linspace(-1, 1, out[0].numel(), device=DEV).view_as(out[0])
+        loss = (out[0] * w0).sum() + out[1].sum()
+        if general:
+            loss = loss + sum((o * 0.0).sum() for o in out[2:])
+        loss.backward()
+        res.append([leaves[k].grad for k in sorted(leaves)] + [densify.grad])
+    for a, b in zip(res[0], res[1]):
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-5 * max(float(b.abs().max()), 1e-30))
+
+
 def test_raster2dgs_channel_padding():
     """10 channels are padded to the next compiled count with the depth kept
     last (gsplat/cuda/_wrapper.py:1657-1683); results equal the oracle at 10."""
