@@ -895,7 +895,7 @@ static int fused_fwd(int B, int H, int W, int C, int XS, const float *img1, cons
              XS, C);
   if (C == 3 && XS == 4) {
     if (cg == 3) GS_FUSED(3, 4, 1, 4);
-    else GS_FUSED(3, 4, 3, 4);
+    else GS_FUSED(3, 2, 3, 4);
   } else if (C == 3) {
     if (cg == 3) GS_FUSED(3, 4, 1, 3);
     else if (fv == 1) GS_FUSED(3, 2, 3, 3);

@@ -326,6 +326,9 @@ struct RasterArgs {
   const int64_t *n_dev;   // the isect count on the device (sync-free isect) or null
   const int32_t *order;   // dispatch order of the tiles (heaviest first) or null
   const float *means2d, *ray_transforms, *colors, *opacities, *normals, *backgrounds;
+  // depths (ABI 33, or null): the last colour channel from this [G] array,
+  // `colors` then holding D - 1 channels per row (no concatenated copy)
+  const float *depths;
   const uint8_t *masks;
   const int32_t *offsets, *flatten_ids;
   // forward outputs / backward inputs
@@ -470,9 +473,16 @@ GS_INLINE void gather(const RasterArgs &a, int64_t j, bool ok, Gathered<D> &r) {
   const float *nr = a.normals + 3 * (int64_t)g;
 #pragma unroll
   for (int i = 0; i < 3; ++i) r.nrm[i] = nr[i];
-  const float *cl = a.colors + D * (int64_t)g;
+  if (a.depths) {
+    const float *cl = a.colors + (D - 1) * (int64_t)g;
 #pragma unroll
-  for (int i = 0; i < D; ++i) r.col[i] = cl[i];
+    for (int i = 0; i < D - 1; ++i) r.col[i] = cl[i];
+    r.col[D - 1] = a.depths[g];
+  } else {
+    const float *cl = a.colors + D * (int64_t)g;
+#pragma unroll
+    for (int i = 0; i < D; ++i) r.col[i] = cl[i];
+  }
 }
 
 template <int D>
@@ -699,7 +709,7 @@ __global__ void __launch_bounds__(1024) fwd_kernel(RasterArgs a) {
 // scheduler independent work between dependent steps, and the gather,
 // culling test and LDS reads of a record are shared by both pixels.  Same
 // per-pixel arithmetic as fwd_kernel.
-template <int D>
+template <int D, bool LEAN = false>  // LEAN: fwd2s_kernel's colours-only form (unused here)
 __global__ void __launch_bounds__(128) fwd2_kernel(RasterArgs a) {
   using R = FRec<D>;
   extern __shared__ float4 lds4[];
@@ -803,24 +813,28 @@ __global__ void __launch_bounds__(128) fwd2_kernel(RasterArgs a) {
 #pragma unroll
       for (int d = 0; d < D; ++d) a.render_colors[pid * D + d] = bg ? bg[d] : 0.f;
       a.render_alphas[pid] = 0.f;
-#pragma unroll
-      for (int i = 0; i < 3; ++i) a.render_normals[pid * 3 + i] = 0.f;
-      a.render_distort[pid] = 0.f;
-      a.render_median[pid] = 0.f;
       a.last_ids[pid] = 0;
-      a.median_ids[pid] = 0;
+      if (!LEAN) {
+#pragma unroll
+        for (int i = 0; i < 3; ++i) a.render_normals[pid * 3 + i] = 0.f;
+        a.render_distort[pid] = 0.f;
+        a.render_median[pid] = 0.f;
+        a.median_ids[pid] = 0;
+      }
       continue;
     }
     a.render_alphas[pid] = 1.f - T[k];
 #pragma unroll
     for (int d = 0; d < D; ++d)
       a.render_colors[pid * D + d] = bg ? col[k][d] + T[k] * bg[d] : col[k][d];
-#pragma unroll
-    for (int i = 0; i < 3; ++i) a.render_normals[pid * 3 + i] = nrm[k][i];
-    a.render_distort[pid] = distort[k];
-    a.render_median[pid] = median[k];
     a.last_ids[pid] = cur[k];
-    a.median_ids[pid] = med[k];
+    if (!LEAN) {
+#pragma unroll
+      for (int i = 0; i < 3; ++i) a.render_normals[pid * 3 + i] = nrm[k][i];
+      a.render_distort[pid] = distort[k];
+      a.render_median[pid] = median[k];
+      a.median_ids[pid] = med[k];
+    }
   }
 }
 
@@ -916,8 +930,8 @@ template <int D>
 __global__ void __launch_bounds__(256)
 pack_srec_kernel(int64_t G, const float *__restrict__ means2d, const float *__restrict__ rt,
                  const float *__restrict__ opac, const float *__restrict__ nrm,
-                 const float *__restrict__ col, const int32_t *__restrict__ visible,
-                 float *__restrict__ rec) {
+                 const float *__restrict__ col, const float *__restrict__ depths,
+                 const int32_t *__restrict__ visible, float *__restrict__ rec) {
   using namespace srec;
   const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (g >= G) return;
@@ -970,8 +984,14 @@ pack_srec_kernel(int64_t G, const float *__restrict__ means2d, const float *__re
   r[NRM0] = nrm[3 * g];
   r[NRM1] = nrm[3 * g + 1];
   r[NRM2] = nrm[3 * g + 2];
+  if (depths) {  // colors: D - 1 channels, the last one from depths (ABI 33)
 #pragma unroll
-  for (int d = 0; d < D; ++d) r[COL + d] = col[D * g + d];
+    for (int d = 0; d < D - 1; ++d) r[COL + d] = col[(D - 1) * g + d];
+    r[COL + D - 1] = depths[g];
+  } else {
+#pragma unroll
+    for (int d = 0; d < D; ++d) r[COL + d] = col[D * g + d];
+  }
   float4 *o = reinterpret_cast<float4 *>(rec + NF * g);
 #pragma unroll
   for (int q = 0; q < NF / 4; ++q) o[q] = make_float4(r[4 * q], r[4 * q + 1], r[4 * q + 2], r[4 * q + 3]);
@@ -1051,7 +1071,9 @@ GS_INLINE void srec_load_blend(const float *rec, int32_t g, SBlend<D> &r) {
   for (int d = 0; d < D; ++d) r.col[d] = p[COL + d];
 }
 
-template <int D>
+// LEAN (a colours-only render: render_normals / distort / median and
+// median_ids null): only the colours, alphas and last ids are formed.
+template <int D, bool LEAN = false>
 __global__ void __launch_bounds__(128) fwd2s_kernel(RasterArgs a, const float *__restrict__ rec) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int tile = a.order ? a.order[blockIdx.x] : (int)blockIdx.x;
@@ -1108,15 +1130,17 @@ __global__ void __launch_bounds__(128) fwd2s_kernel(RasterArgs a, const float *_
           const float vis = alpha * T[k];
 #pragma unroll
           for (int d = 0; d < D; ++d) col[k][d] += r.col[d] * vis;
-          nrm[k][0] += r.n0 * vis;
-          nrm[k][1] += r.n1 * vis;
-          nrm[k][2] += r.n2 * vis;
-          const float depth = r.col[D - 1];
-          distort[k] += 2.f * (vis * depth * (1.f - T[k]) - vis * acc_vd[k]);
-          acc_vd[k] += vis * depth;
-          if (T[k] > 0.5f) {
-            median[k] = depth;
-            med[k] = idx;
+          if (!LEAN) {
+            nrm[k][0] += r.n0 * vis;
+            nrm[k][1] += r.n1 * vis;
+            nrm[k][2] += r.n2 * vis;
+            const float depth = r.col[D - 1];
+            distort[k] += 2.f * (vis * depth * (1.f - T[k]) - vis * acc_vd[k]);
+            acc_vd[k] += vis * depth;
+            if (T[k] > 0.5f) {
+              median[k] = depth;
+              med[k] = idx;
+            }
           }
           cur[k] = idx;
           T[k] = nT;
@@ -1171,24 +1195,28 @@ __global__ void __launch_bounds__(128) fwd2s_kernel(RasterArgs a, const float *_
 #pragma unroll
       for (int d = 0; d < D; ++d) a.render_colors[pid * D + d] = bg ? bg[d] : 0.f;
       a.render_alphas[pid] = 0.f;
-#pragma unroll
-      for (int i = 0; i < 3; ++i) a.render_normals[pid * 3 + i] = 0.f;
-      a.render_distort[pid] = 0.f;
-      a.render_median[pid] = 0.f;
       a.last_ids[pid] = 0;
-      a.median_ids[pid] = 0;
+      if (!LEAN) {
+#pragma unroll
+        for (int i = 0; i < 3; ++i) a.render_normals[pid * 3 + i] = 0.f;
+        a.render_distort[pid] = 0.f;
+        a.render_median[pid] = 0.f;
+        a.median_ids[pid] = 0;
+      }
       continue;
     }
     a.render_alphas[pid] = 1.f - T[k];
 #pragma unroll
     for (int d = 0; d < D; ++d)
       a.render_colors[pid * D + d] = bg ? col[k][d] + T[k] * bg[d] : col[k][d];
-#pragma unroll
-    for (int i = 0; i < 3; ++i) a.render_normals[pid * 3 + i] = nrm[k][i];
-    a.render_distort[pid] = distort[k];
-    a.render_median[pid] = median[k];
     a.last_ids[pid] = cur[k];
-    a.median_ids[pid] = med[k];
+    if (!LEAN) {
+#pragma unroll
+      for (int i = 0; i < 3; ++i) a.render_normals[pid * 3 + i] = nrm[k][i];
+      a.render_distort[pid] = distort[k];
+      a.render_median[pid] = median[k];
+      a.median_ids[pid] = med[k];
+    }
   }
 }
 
@@ -1401,7 +1429,7 @@ __global__ void __launch_bounds__(128) bwd2_kernel(RasterArgs a) {
     const float Tf = 1.f - a.render_alphas[pid];
     s.T = Tf;
     s.bin_final = s.inside ? a.last_ids[pid] : 0;
-    s.med_idx = s.inside ? a.median_ids[pid] : 0;
+    s.med_idx = (!LEAN && s.inside) ? a.median_ids[pid] : 0;  // LEAN: may be null
     float bg_dot = 0.f;
 #pragma unroll
     for (int d = 0; d < D; ++d) {
@@ -1519,7 +1547,7 @@ __global__ void __launch_bounds__(128) bwd2_kernel(RasterArgs a) {
             const float gy = vG * (-hk.vis * kFilterInvSquare * dy);
             v[F::XY] += gx;
             v[F::XY + 1] += gy;
-            if (ABS) {
+            if constexpr (ABS) {
               v[F::AB] += fabsf(gx);
               v[F::AB + 1] += fabsf(gy);
             }
@@ -1566,14 +1594,20 @@ __global__ void __launch_bounds__(256)
 unpack_kernel(int64_t G, const int32_t *__restrict__ visible, const float *__restrict__ packed,
               const float *__restrict__ rt,
               float *__restrict__ v_means2d, float *__restrict__ v_rt, float *__restrict__ v_colors,
-              float *__restrict__ v_opacities, float *__restrict__ v_normals,
-              float *__restrict__ v_densify, float *__restrict__ v_abs) {
+              float *__restrict__ v_depths, float *__restrict__ v_opacities,
+              float *__restrict__ v_normals, float *__restrict__ v_densify,
+              float *__restrict__ v_abs) {
   using F = Fields<D, ABS, LEAN>;
+  // v_depths (ABI 33, or null): the last channel's gradient there, v_colors
+  // then [G, D - 1]
+  const int DC = v_depths ? D - 1 : D;
   const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= G) return;
   if (visible && visible[g] <= 0) {  // no isect: every gradient is zero (row never zeroed)
 #pragma unroll
-    for (int d = 0; d < D; ++d) v_colors[g * D + d] = 0.f;
+    for (int d = 0; d < D; ++d)
+      if (d < DC) v_colors[g * DC + d] = 0.f;
+    if (v_depths) v_depths[g] = 0.f;
 #pragma unroll
     for (int i = 0; i < 3; ++i) v_normals[g * 3 + i] = 0.f;
 #pragma unroll
@@ -1586,7 +1620,9 @@ unpack_kernel(int64_t G, const int32_t *__restrict__ visible, const float *__res
   }
   const float *r = packed + g * F::S;
 #pragma unroll
-  for (int d = 0; d < D; ++d) v_colors[g * D + d] = r[F::COL + d];
+  for (int d = 0; d < D; ++d)
+    if (d < DC) v_colors[g * DC + d] = r[F::COL + d];
+  if (v_depths) v_depths[g] = r[F::COL + D - 1];
 #pragma unroll
   for (int i = 0; i < 3; ++i) v_normals[g * 3 + i] = LEAN ? 0.f : r[F::NRM + i];
 #pragma unroll
@@ -1822,7 +1858,7 @@ extern "C" int gsplat_hip_rasterize_2dgs_supported_channels(int D) {
 
 extern "C" int gsplat_hip_rasterize_2dgs_fwd(
     int C, int D, int width, int height, int tile_size, int tile_width, int tile_height,
-    const float *means2d, const float *ray_transforms, const float *colors,
+    const float *means2d, const float *ray_transforms, const float *colors, const float *depths,
     const float *opacities, const float *normals, const float *backgrounds,
     const uint8_t *masks, const int32_t *isect_offsets, int64_t n_isects,
     const int64_t *n_isects_device, const int32_t *flatten_ids, const float *records,
@@ -1833,9 +1869,17 @@ extern "C" int gsplat_hip_rasterize_2dgs_fwd(
   GS_REQUIRE(channels_supported(D), "rasterize_2dgs_fwd: unsupported channel count %d", D);
   const int n_tiles = C * tile_width * tile_height;
   if (n_tiles == 0 || width == 0 || height == 0) return 0;
-  GS_REQUIRE(isect_offsets && render_colors && render_alphas && render_normals &&
-                 render_distort && render_median && last_ids && median_ids,
+  // a colours-only render (ABI 33): render_normals, render_distort,
+  // render_median and median_ids all null -- the record path forms the
+  // colours, alphas and last ids alone (its backward then takes no gradient
+  // of the other outputs)
+  const bool lean = !render_normals && !render_distort && !render_median && !median_ids;
+  GS_REQUIRE(isect_offsets && render_colors && render_alphas && last_ids &&
+                 (lean || (render_normals && render_distort && render_median && median_ids)),
              "rasterize_2dgs_fwd: null pointer argument");
+  GS_REQUIRE(!lean || (records && tile_size == 16 && fwd2_enabled()),
+             "rasterize_2dgs_fwd: a colours-only render needs the record path (16x16 tiles, D <= %d)",
+             kSRecMaxD);
   GS_REQUIRE(n_isects == 0 || (means2d && ray_transforms && colors && opacities && normals &&
                                flatten_ids),
              "rasterize_2dgs_fwd: null pointer argument");
@@ -1843,7 +1887,7 @@ extern "C" int gsplat_hip_rasterize_2dgs_fwd(
   RasterArgs a{};
   a.C = C; a.W = width; a.H = height; a.ts = tile_size; a.tw = tile_width; a.th = tile_height;
   a.n_tiles = n_tiles; a.n_isects = n_isects; a.n_dev = n_isects_device;
-  a.means2d = means2d; a.ray_transforms = ray_transforms; a.colors = colors;
+  a.means2d = means2d; a.ray_transforms = ray_transforms; a.colors = colors; a.depths = depths;
   a.opacities = opacities; a.normals = normals; a.backgrounds = backgrounds; a.masks = masks;
   a.offsets = isect_offsets; a.flatten_ids = flatten_ids;
   a.render_colors = render_colors; a.render_alphas = render_alphas;
@@ -1862,7 +1906,10 @@ extern "C" int gsplat_hip_rasterize_2dgs_fwd(
     GS_REQUIRE(px2 && D <= kSRecMaxD, "rasterize_2dgs_fwd: records need 16x16 tiles, D <= %d",
                kSRecMaxD);
 #define GS_CASE(n)                                                                            \
-  if (D == n) hipLaunchKernelGGL(fwd2s_kernel<n>, dim3(n_tiles), dim3(128), 0, st, a, records);
+  if (D == n && lean)                                                                         \
+    hipLaunchKernelGGL((fwd2s_kernel<n, true>), dim3(n_tiles), dim3(128), 0, st, a, records); \
+  else if (D == n)                                                                            \
+    hipLaunchKernelGGL((fwd2s_kernel<n, false>), dim3(n_tiles), dim3(128), 0, st, a, records);
     GS_CASE(1) GS_CASE(2) GS_CASE(3) GS_CASE(4)
 #undef GS_CASE
     GS_CHECK_LAUNCH("rasterize_2dgs_fwd");
@@ -1890,8 +1937,9 @@ extern "C" int gsplat_hip_rasterize_2dgs_pack_records(int64_t n_gaussians, int D
                                                       const float *means2d,
                                                       const float *ray_transforms,
                                                       const float *opacities, const float *normals,
-                                                      const float *colors, const int32_t *visible,
-                                                      float *records, void *stream) {
+                                                      const float *colors, const float *depths,
+                                                      const int32_t *visible, float *records,
+                                                      void *stream) {
   GS_REQUIRE(D >= 1 && D <= kSRecMaxD, "rasterize_2dgs_pack_records: D %d not in [1, %d]", D,
              kSRecMaxD);
   GS_REQUIRE(n_gaussians >= 0, "rasterize_2dgs_pack_records: negative count");
@@ -1904,7 +1952,7 @@ extern "C" int gsplat_hip_rasterize_2dgs_pack_records(int64_t n_gaussians, int D
 #define GS_CASE(n)                                                                            \
   if (D == n)                                                                                 \
     hipLaunchKernelGGL(pack_srec_kernel<n>, grid, dim3(256), 0, st, n_gaussians, means2d,     \
-                       ray_transforms, opacities, normals, colors, visible, records);
+                       ray_transforms, opacities, normals, colors, depths, visible, records);
   GS_CASE(1) GS_CASE(2) GS_CASE(3) GS_CASE(4)
 #undef GS_CASE
   GS_CHECK_LAUNCH("rasterize_2dgs_pack_records");
@@ -1919,7 +1967,7 @@ extern "C" int64_t gsplat_hip_rasterize_2dgs_bwd_workspace_bytes(int64_t n_gauss
 extern "C" int gsplat_hip_rasterize_2dgs_bwd(
     int C, int D, int width, int height, int tile_size, int tile_width, int tile_height,
     int64_t n_gaussians, const float *means2d, const float *ray_transforms, const float *colors,
-    const float *opacities, const float *normals, const float *backgrounds,
+    const float *depths, const float *opacities, const float *normals, const float *backgrounds,
     const uint8_t *masks, const int32_t *isect_offsets, int64_t n_isects,
     const int64_t *n_isects_device, const int32_t *flatten_ids, const int32_t *tile_order,
     const int32_t *visible, const float *render_colors, const float *render_alphas,
@@ -1927,9 +1975,10 @@ extern "C" int gsplat_hip_rasterize_2dgs_bwd(
     const int32_t *median_ids, const float *v_render_colors,
     const float *v_render_alphas, const float *v_render_normals, const float *v_render_distort,
     const float *v_render_median, float *v_means2d, float *v_ray_transforms, float *v_colors,
-    float *v_opacities, float *v_normals, float *v_densify, float *v_means2d_abs,
-    void *workspace, int64_t workspace_bytes, void *stream) {
+    float *v_depths, float *v_opacities, float *v_normals, float *v_densify,
+    float *v_means2d_abs, void *workspace, int64_t workspace_bytes, void *stream) {
   if (int e = check_tiles(C, width, height, tile_size, tile_width, tile_height)) return e;
+  GS_REQUIRE(!depths == !v_depths, "rasterize_2dgs_bwd: depths and v_depths: both or neither");
   GS_REQUIRE(channels_supported(D), "rasterize_2dgs_bwd: unsupported channel count %d", D);
   GS_REQUIRE(tile_size * tile_size <= 256, "rasterize_2dgs_bwd: tile_size %d > 16", tile_size);
   const int absgrad = v_means2d_abs != nullptr;
@@ -1955,13 +2004,14 @@ extern "C" int gsplat_hip_rasterize_2dgs_bwd(
   const int n_tiles = C * tile_width * tile_height;
   if (n_tiles > 0 && n_isects > 0 && width > 0 && height > 0) {
     GS_REQUIRE(isect_offsets && flatten_ids && render_colors && render_alphas && last_ids &&
-                   median_ids && v_render_colors,
-               "rasterize_2dgs_bwd: null pointer argument");
+                   (median_ids || lean) && v_render_colors,
+               "rasterize_2dgs_bwd: null pointer argument (median_ids: null only for a "
+               "colours-only render's backward)");
     RasterArgs a{};
     a.C = C; a.W = width; a.H = height; a.ts = tile_size; a.tw = tile_width;
     a.th = tile_height; a.n_tiles = n_tiles; a.n_isects = n_isects; a.n_dev = n_isects_device;
     a.order = tile_order;
-    a.means2d = means2d; a.ray_transforms = ray_transforms; a.colors = colors;
+    a.means2d = means2d; a.ray_transforms = ray_transforms; a.colors = colors; a.depths = depths;
     a.opacities = opacities; a.normals = normals; a.backgrounds = backgrounds; a.masks = masks;
     a.offsets = isect_offsets; a.flatten_ids = flatten_ids;
     a.render_colors = const_cast<float *>(render_colors);
@@ -2002,21 +2052,21 @@ extern "C" int gsplat_hip_rasterize_2dgs_bwd(
     if (absgrad)                                                                               \
       hipLaunchKernelGGL((unpack_kernel<n <= 4 ? n : 4, true, true>), grid, dim3(256), 0, st, G, \
                          visible, (const float *)workspace, ray_transforms, v_means2d,         \
-                         v_ray_transforms, v_colors, v_opacities, v_normals, v_densify,        \
+                         v_ray_transforms, v_colors, v_depths, v_opacities, v_normals, v_densify,\
                          v_means2d_abs);                                                       \
     else                                                                                       \
       hipLaunchKernelGGL((unpack_kernel<n <= 4 ? n : 4, false, true>), grid, dim3(256), 0, st, G,\
                          visible, (const float *)workspace, ray_transforms, v_means2d,         \
-                         v_ray_transforms, v_colors, v_opacities, v_normals, v_densify,        \
+                         v_ray_transforms, v_colors, v_depths, v_opacities, v_normals, v_densify,\
                          v_means2d_abs);                                                       \
   } else if (D == n) {                                                                         \
     if (absgrad)                                                                               \
       hipLaunchKernelGGL((unpack_kernel<n, true>), grid, dim3(256), 0, st, G, visible, (const float *)workspace, \
-                         ray_transforms, v_means2d, v_ray_transforms, v_colors, v_opacities,   \
+                         ray_transforms, v_means2d, v_ray_transforms, v_colors, v_depths, v_opacities,\
                          v_normals, v_densify, v_means2d_abs);                                 \
     else                                                                                       \
       hipLaunchKernelGGL((unpack_kernel<n, false>), grid, dim3(256), 0, st, G, visible, (const float *)workspace, \
-                         ray_transforms, v_means2d, v_ray_transforms, v_colors, v_opacities,   \
+                         ray_transforms, v_means2d, v_ray_transforms, v_colors, v_depths, v_opacities,\
                          v_normals, v_densify, v_means2d_abs);                                 \
   }
   GS_SURFEL_CHANNELS(GS_CASE)

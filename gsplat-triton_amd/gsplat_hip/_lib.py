@@ -12,7 +12,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GSPLAT_HIP_LIB", os.path.join(_HERE, "libgsplat_hip.so"))
-ABI_VERSION = 32
+ABI_VERSION = 33
 
 _p = ctypes.c_void_p
 _i32 = ctypes.c_int
@@ -126,16 +126,17 @@ _SIGS = {
                                                      _p, _p, _p, _p]),
     "gsplat_hip_rasterize_2dgs_supported_channels": (_i32, [_i32]),
     "gsplat_hip_rasterize_2dgs_fwd": (_i32, [_i32, _i32, _i32, _i32, _i32, _i32, _i32, _p, _p, _p,
-                                             _p, _p, _p, _p, _p, _i64, _p, _p, _p, _p, _p, _p,
+                                             _p, _p, _p, _p, _p, _p, _i64, _p, _p, _p, _p, _p, _p,
                                              _p, _p, _p, _p, _p, _p]),
     "gsplat_hip_rasterize_2dgs_record_floats": (_i32, [_i32, _i32]),
-    "gsplat_hip_rasterize_2dgs_pack_records": (_i32, [_i64, _i32, _p, _p, _p, _p, _p, _p, _p, _p]),
+    "gsplat_hip_rasterize_2dgs_pack_records": (_i32, [_i64, _i32, _p, _p, _p, _p, _p, _p, _p, _p,
+                                                      _p]),
     "gsplat_hip_rasterize_2dgs_bwd_workspace_bytes": (_i64, [_i64, _i32, _i32]),
-    "gsplat_hip_rasterize_2dgs_bwd": (_i32, [_i32, _i32, _i32, _i32, _i32, _i32, _i32, _i64, _p,
-                                             _p, _p, _p, _p, _p, _p, _p, _i64, _p, _p, _p, _p, _p, _p,
-                                             _p,
+    "gsplat_hip_rasterize_2dgs_bwd": (_i32, [_i32, _i32, _i32, _i32, _i32, _i32, _i32, _i64,
+                                             _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64,
+                                             _p, _p, _p, _p, _p, _p, _p,
                                              _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p,
-                                             _p, _i64, _p]),
+                                             _p, _p, _i64, _p]),
     "gsplat_hip_quat_scale_to_covar_preci_fwd": (_i32, [_i64, _p, _p, _i32, _p, _p, _p]),
     "gsplat_hip_quat_scale_to_covar_preci_bwd": (_i32, [_i64, _p, _p, _i32, _p, _p, _p, _p, _p]),
     "gsplat_hip_relocation": (_i32, [_i64, _p, _p, _p, _p, _i32, _p, _p, _p]),

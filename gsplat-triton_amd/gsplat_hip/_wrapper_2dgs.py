@@ -218,45 +218,54 @@ class _RasterizeToPixels2DGS(torch.autograd.Function):
     @staticmethod
     def forward(ctx, means2d, ray_transforms, colors, opacities, normals, densify, backgrounds,
                 masks, width, height, tile_size, isect_offsets, flatten_ids, absgrad, distloss,
-                n_dev=None, visible=None):
-        means2d, ray_transforms, colors, opacities, normals, backgrounds = (
-            _f32c(x) for x in (means2d, ray_transforms, colors, opacities, normals, backgrounds))
+                n_dev=None, visible=None, colors_only=False, depths=None):
+        # depths (ABI 33, [C, N] or [nnz], or None): the last colour channel,
+        # read in place -- colors then holds the other D - 1
+        means2d, ray_transforms, colors, opacities, normals, backgrounds, depths = (
+            _f32c(x) for x in (means2d, ray_transforms, colors, opacities, normals, backgrounds,
+                               depths))
         _dev_check(means2d, ray_transforms, colors, opacities, normals, isect_offsets, flatten_ids)
         C, th, tw = isect_offsets.shape
-        D = colors.shape[-1]
+        D = colors.shape[-1] + (1 if depths is not None else 0)
         dev = means2d.device
         isect_offsets = isect_offsets.to(torch.int32).contiguous()
         flatten_ids = flatten_ids.to(torch.int32).contiguous()
         masks_u8 = None if masks is None else masks.to(torch.uint8).contiguous()
-        render_colors = torch.empty((C, height, width, D), device=dev)
-        render_alphas = torch.empty((C, height, width, 1), device=dev)
-        render_normals = torch.empty((C, height, width, 3), device=dev)
-        render_distort = torch.empty((C, height, width, 1), device=dev)
-        render_median = torch.empty((C, height, width, 1), device=dev)
-        last_ids = torch.empty((C, height, width), dtype=torch.int32, device=dev)
-        median_ids = torch.empty((C, height, width), dtype=torch.int32, device=dev)
         records = None
         nf = int(_lib.query("gsplat_hip_rasterize_2dgs_record_floats", D, int(tile_size))) \
             if SREC else 0
+        # colours-only (ABI 33, the record path): no normals / distortion /
+        # median images (None) and no median ids
+        lean = bool(colors_only) and nf > 0
+        render_colors = torch.empty((C, height, width, D), device=dev)
+        render_alphas = torch.empty((C, height, width, 1), device=dev)
+        last_ids = torch.empty((C, height, width), dtype=torch.int32, device=dev)
+        render_normals = render_distort = render_median = median_ids = None
+        if not lean:
+            render_normals = torch.empty((C, height, width, 3), device=dev)
+            render_distort = torch.empty((C, height, width, 1), device=dev)
+            render_median = torch.empty((C, height, width, 1), device=dev)
+            median_ids = torch.empty((C, height, width), dtype=torch.int32, device=dev)
         if nf:  # scalar-operand records (GSPLAT_HIP_SURFEL_SREC=1)
             G = opacities.numel()
             records = torch.empty(max(G, 1) * nf, device=dev)
             _lib.call("gsplat_hip_rasterize_2dgs_pack_records", G, D, _ptr(means2d),
                       _ptr(ray_transforms), _ptr(opacities), _ptr(normals), _ptr(colors),
-                      _ptr(visible), _ptr(records), _stream())
+                      _ptr(depths), _ptr(visible), _ptr(records), _stream())
         order = torch.empty(C * th * tw, dtype=torch.int32, device=dev) \
             if ORDER and int(tile_size) == 16 else None
         with _Timed("rasterize_2dgs_fwd"):
             _lib.call("gsplat_hip_rasterize_2dgs_fwd", C, D, int(width), int(height),
                       int(tile_size), tw, th, _ptr(means2d), _ptr(ray_transforms), _ptr(colors),
-                      _ptr(opacities), _ptr(normals), _ptr(backgrounds), _ptr(masks_u8),
+                      _ptr(depths), _ptr(opacities), _ptr(normals), _ptr(backgrounds),
+                      _ptr(masks_u8),
                       _ptr(isect_offsets), flatten_ids.numel(), _ptr(n_dev), _ptr(flatten_ids),
                       _ptr(records), _ptr(order), _ptr(render_colors), _ptr(render_alphas), _ptr(render_normals),
                       _ptr(render_distort), _ptr(render_median), _ptr(last_ids),
                       _ptr(median_ids), _stream())
         ctx.save_for_backward(means2d, ray_transforms, colors, opacities, normals, densify,
                               backgrounds, masks_u8, isect_offsets, flatten_ids, render_colors,
-                              render_alphas, last_ids, median_ids)
+                              render_alphas, last_ids, median_ids, depths)
         ctx.width, ctx.height, ctx.tile_size = int(width), int(height), int(tile_size)
         ctx.absgrad, ctx.distloss = absgrad, distloss
         ctx.n_dev = n_dev
@@ -272,9 +281,9 @@ class _RasterizeToPixels2DGS(torch.autograd.Function):
                  v_render_median):
         (means2d, ray_transforms, colors, opacities, normals, densify, backgrounds, masks_u8,
          isect_offsets, flatten_ids, render_colors, render_alphas, last_ids,
-         median_ids) = ctx.saved_tensors
+         median_ids, depths) = ctx.saved_tensors
         C, th, tw = isect_offsets.shape
-        D = colors.shape[-1]
+        D = colors.shape[-1] + (1 if depths is not None else 0)
         H, W = ctx.height, ctx.width
         dev = means2d.device
 
@@ -290,6 +299,7 @@ class _RasterizeToPixels2DGS(torch.autograd.Function):
         v_means2d = torch.empty_like(means2d)
         v_ray_transforms = torch.empty_like(ray_transforms)
         v_colors = torch.empty_like(colors)
+        v_depths = None if depths is None else torch.empty_like(depths)
         v_opacities = torch.empty_like(opacities)
         v_normals = torch.empty_like(normals)
         v_densify = torch.empty(densify.shape, device=dev)
@@ -298,14 +308,16 @@ class _RasterizeToPixels2DGS(torch.autograd.Function):
                                             int(ctx.absgrad))), 4), dtype=torch.uint8, device=dev)
         with _Timed("rasterize_2dgs_bwd"):
             _lib.call("gsplat_hip_rasterize_2dgs_bwd", C, D, W, H, ctx.tile_size, tw, th, G,
-                      _ptr(means2d), _ptr(ray_transforms), _ptr(colors), _ptr(opacities),
-                      _ptr(normals), _ptr(backgrounds), _ptr(masks_u8), _ptr(isect_offsets),
+                      _ptr(means2d), _ptr(ray_transforms), _ptr(colors), _ptr(depths),
+                      _ptr(opacities), _ptr(normals), _ptr(backgrounds), _ptr(masks_u8),
+                      _ptr(isect_offsets),
                       flatten_ids.numel(), _ptr(ctx.n_dev), _ptr(flatten_ids), _ptr(ctx.order),
                       _ptr(ctx.visible), _ptr(render_colors),
                       _ptr(render_alphas), _ptr(last_ids), _ptr(median_ids),
                       _ptr(v_render_colors), _ptr(v_render_alphas), _ptr(v_render_normals),
                       _ptr(v_render_distort), _ptr(v_render_median), _ptr(v_means2d),
-                      _ptr(v_ray_transforms), _ptr(v_colors), _ptr(v_opacities), _ptr(v_normals),
+                      _ptr(v_ray_transforms), _ptr(v_colors), _ptr(v_depths), _ptr(v_opacities),
+                      _ptr(v_normals),
                       _ptr(v_densify), _ptr(v_abs), _ptr(ws), ws.numel(), _stream())
         if ctx.absgrad:
             means2d.absgrad = v_abs
@@ -313,7 +325,8 @@ class _RasterizeToPixels2DGS(torch.autograd.Function):
         if ctx.needs_input_grad[6]:  # _wrapper.py:1953-1958
             v_backgrounds = (v_render_colors * (1.0 - render_alphas).float()).sum(dim=(1, 2))
         return (v_means2d, v_ray_transforms, v_colors, v_opacities, v_normals, v_densify,
-                v_backgrounds, None, None, None, None, None, None, None, None, None, None)
+                v_backgrounds, None, None, None, None, None, None, None, None, None, None, None,
+                v_depths)
 
 
 def rasterize_to_pixels_2dgs(
@@ -335,6 +348,8 @@ def rasterize_to_pixels_2dgs(
     distloss: bool = False,
     _n_isects_device: Optional[Tensor] = None,
     _visible: Optional[Tensor] = None,
+    _colors_only: bool = False,
+    _depths: Optional[Tensor] = None,
 ) -> Tuple[Tensor, Tensor, Tensor, Tensor, Tensor]:
     """Rasterizes surfels to pixels (gsplat/cuda/_wrapper.py:1595-1726).
 
@@ -346,8 +361,16 @@ def rasterize_to_pixels_2dgs(
     (the sync-free isect of a captured training step).  `_visible`
     (private): i32 per row of means2d, > 0 for the rows an isect references
     (the isect's tiles_per_gauss): only those get a record and a zeroed
-    gradient row."""
+    gradient row.  `_colors_only` (private, the training step): where the
+    record path runs, render_normals / render_distort / render_median come
+    back None (not formed).  `_depths` (private, [C, N]): the last colour
+    channel read from it in place, `colors` holding the others (an RGB+D
+    render without the concatenated copy; its gradient flows to _depths)."""
     C = isect_offsets.size(0)
+    if _depths is not None:
+        assert not packed and colors.shape[-1] + 1 in _SUPPORTED_D and backgrounds is None, \
+            "_depths: dense, no backgrounds, a compiled channel count"
+        assert _depths.shape == colors.shape[:-1], (_depths.shape, colors.shape)
     device = means2d.device
     if packed:  # flatten_ids index the [nnz] rows directly (_wrapper.py:1628-1636)
         nnz = means2d.size(0)
@@ -365,7 +388,7 @@ def rasterize_to_pixels_2dgs(
         assert backgrounds.shape == (C, colors.shape[-1]), backgrounds.shape
         backgrounds = backgrounds.contiguous()
 
-    channels = colors.shape[-1]
+    channels = colors.shape[-1] + (1 if _depths is not None else 0)
     if channels > 512 or channels == 0:
         raise ValueError(f"Unsupported number of color channels: {channels}")
     if channels not in _SUPPORTED_D:
@@ -398,7 +421,8 @@ def rasterize_to_pixels_2dgs(
             opacities.contiguous(), normals.contiguous(), densify.contiguous(), backgrounds,
             masks, image_width, image_height, tile_size, isect_offsets.contiguous(),
             flatten_ids.contiguous(), absgrad, distloss, _n_isects_device,
-            None if _visible is None else _visible.to(torch.int32).contiguous().view(-1))
+            None if _visible is None else _visible.to(torch.int32).contiguous().view(-1),
+            _colors_only, None if _depths is None else _depths.contiguous())
     if padded_channels > 0:
         render_colors = torch.cat([render_colors[..., : -padded_channels - 1],
                                    render_colors[..., -1:]], dim=-1)

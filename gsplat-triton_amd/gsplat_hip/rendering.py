@@ -526,6 +526,7 @@ def rasterization_2dgs(
     `_colors_only` (the training step, whose loss reads the colours alone):
     render_normals and render_normals_from_depth are not formed (None) --
     the world-space rotation and the depth-to-normal pass are skipped."""
+    from ._wrapper_2dgs import _SUPPORTED_D as _SUPPORTED_D_2DGS
     from ._wrapper_2dgs import fully_fused_projection_2dgs, rasterize_to_pixels_2dgs
 
     N = means.shape[0]
@@ -603,7 +604,12 @@ def rasterization_2dgs(
             colors = spherical_harmonics(sh_degree, dirs, colors, masks=radii > 0)
             colors = torch.clamp_min(colors + 0.5, 0.0)
 
-    if render_mode in ["RGB+D", "RGB+ED"]:
+    depth_channel = None  # the rasterizer reads the depth channel in place (ABI 33)
+    if (render_mode in ["RGB+D", "RGB+ED"] and not packed and backgrounds is None
+            and colors.dim() == 3 and colors.shape[:2] == depths.shape
+            and colors.shape[-1] + 1 in _SUPPORTED_D_2DGS):
+        depth_channel = depths
+    elif render_mode in ["RGB+D", "RGB+ED"]:
         colors = torch.cat((colors, depths[..., None]), dim=-1)
         if backgrounds is not None:
             backgrounds = torch.cat((backgrounds, torch.zeros((C, 1), device=colors.device)), -1)
@@ -626,7 +632,8 @@ def rasterization_2dgs(
                                  width, height, tile_size, isect_offsets, flatten_ids,
                                  backgrounds=backgrounds, packed=packed, absgrad=absgrad,
                                  distloss=distloss, _n_isects_device=counts,
-                                 _visible=tiles_per_gauss)
+                                 _visible=tiles_per_gauss, _colors_only=_colors_only,
+                                 _depths=depth_channel)
     if _colors_only:
         meta = {"camera_ids": camera_ids, "gaussian_ids": gaussian_ids, "radii": radii,
                 "means2d": means2d, "depths": depths, "ray_transforms": ray_transforms,

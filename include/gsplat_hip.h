@@ -33,7 +33,11 @@ const char *gsplat_hip_last_error(void);
  * 30: gsplat_hip_l1_ssim_loss_fused_fwd_ring (the loss also into a device
  * ring slot chosen by a device step counter), gsplat_hip_set_fwd_split_div.
  * 31: gsplat_hip_projection_bwd_adam, gsplat_hip_graph_memcpy_census.
- * 32: gsplat_hip_status_to_ring; n_isects_device of the 2DGS rasterizer. */
+ * 32: gsplat_hip_status_to_ring; n_isects_device of the 2DGS rasterizer.
+ * 33: colours-only 2DGS renders (render_normals / distort / median and
+ *     median_ids NULL in gsplat_hip_rasterize_2dgs_fwd and _bwd); the 2DGS
+ *     rasterizer's last colour channel from a separate depths array
+ *     (depths / v_depths of _pack_records, _fwd, _bwd). */
 int gsplat_hip_abi_version(void);
 
 /* ---------------------------------------------------------------------------
@@ -701,17 +705,28 @@ int gsplat_hip_projection_2dgs_packed_bwd(int C, int N, int64_t nnz, const float
  * are left unwritten.
  * tile_order (ABI 32, may be NULL; i32[C*th*tw]): the forward writes the
  * tiles' dispatch order there (heaviest first, by floor(log2(isects))) and
- * runs in it; pass it to the backward, which then runs in it too. */
+ * runs in it; pass it to the backward, which then runs in it too.
+ * A colours-only render (ABI 33; the record path only): render_normals,
+ * render_distort, render_median and median_ids all NULL -- only
+ * render_colors, render_alphas and last_ids are formed; its backward gets
+ * median_ids = NULL and no gradient of those outputs.
+ * depths (ABI 33, may be NULL; f32[G]): the last of the D colour channels is
+ * read from depths[g], `colors` then holding D - 1 channels per row (the
+ * RGB+D render without a concatenated colour copy); the backward then takes
+ * the same depths and writes that channel's gradient to v_depths[G]
+ * (v_colors [G, D - 1]). */
 int gsplat_hip_rasterize_2dgs_record_floats(int D, int tile_size);
 int gsplat_hip_rasterize_2dgs_pack_records(int64_t n_gaussians, int D, const float *means2d,
                                            const float *ray_transforms, const float *opacities,
                                            const float *normals, const float *colors,
-                                           const int32_t *visible, float *records, void *stream);
+                                           const float *depths, const int32_t *visible,
+                                           float *records, void *stream);
 int gsplat_hip_rasterize_2dgs_supported_channels(int D);
 int gsplat_hip_rasterize_2dgs_fwd(int C, int D, int width, int height, int tile_size,
                                   int tile_width, int tile_height, const float *means2d,
                                   const float *ray_transforms, const float *colors,
-                                  const float *opacities, const float *normals,
+                                  const float *depths, const float *opacities,
+                                  const float *normals,
                                   const float *backgrounds, const uint8_t *masks,
                                   const int32_t *isect_offsets, int64_t n_isects,
                                   const int64_t *n_isects_device, const int32_t *flatten_ids,
@@ -729,22 +744,23 @@ int gsplat_hip_rasterize_2dgs_fwd(int C, int D, int width, int height, int tile_
  *    (formed from the final sums; the reference writes it racily from partial
  *    sums), v_means2d_abs[G,2] or NULL (absgrad off).
  * v_render_alphas / v_render_normals (ABI 32) / v_render_distort /
- * v_render_median may be NULL (no gradient).  visible (ABI 32, may be NULL;
+ * v_render_median may be NULL (no gradient).  depths / v_depths (ABI 33, both
+ * NULL or both set): the forward's separate last channel and its gradient.  visible (ABI 32, may be NULL;
  * i32[G], e.g. tiles_per_gauss): only the rows with visible[g] > 0 can
  * receive gradient -- the others are written as zeros without a read. */
 int64_t gsplat_hip_rasterize_2dgs_bwd_workspace_bytes(int64_t n_gaussians, int D, int absgrad);
 int gsplat_hip_rasterize_2dgs_bwd(
     int C, int D, int width, int height, int tile_size, int tile_width, int tile_height,
     int64_t n_gaussians, const float *means2d, const float *ray_transforms, const float *colors,
-    const float *opacities, const float *normals, const float *backgrounds,
+    const float *depths, const float *opacities, const float *normals, const float *backgrounds,
     const uint8_t *masks, const int32_t *isect_offsets, int64_t n_isects,
     const int64_t *n_isects_device, const int32_t *flatten_ids, const int32_t *tile_order,
     const int32_t *visible, const float *render_colors, const float *render_alphas,
     const int32_t *last_ids, const int32_t *median_ids, const float *v_render_colors,
     const float *v_render_alphas, const float *v_render_normals, const float *v_render_distort,
     const float *v_render_median, float *v_means2d, float *v_ray_transforms, float *v_colors,
-    float *v_opacities, float *v_normals, float *v_densify, float *v_means2d_abs,
-    void *workspace, int64_t workspace_bytes, void *stream);
+    float *v_depths, float *v_opacities, float *v_normals, float *v_densify,
+    float *v_means2d_abs, void *workspace, int64_t workspace_bytes, void *stream);
 
 /* ---------------------------------------------------------------------------
  * Auxiliary kernels reached by the reference's strategies / optimizers through

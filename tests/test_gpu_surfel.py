@@ -272,6 +272,70 @@ def test_raster2dgs_bwd_lean_matches_general():
         torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-5 * max(float(b.abs().max()), 1e-30))
 
 
+@pytest.mark.parametrize("D,masked", [(4, False), (3, True)])
+def test_raster2dgs_colors_only_matches_full(D, masked):
+    """A colours-only render (ABI 33, `_colors_only`: the training step's)
+    forms the full render's colours and alphas (the same arithmetic, up to
+    the compiler's FMA contraction in the smaller kernel: 6e-8 seen), returns
+    None for the normal / distortion / median images, and its backward (the
+    LEAN kernel, no median ids) gives the full render's gradients for a loss
+    on the colours and alphas, to the order of the float atomics."""
+    from gsplat_hip import rasterize_to_pixels_2dgs
+    sc = surfel_scene(8, N=800, W=150, H=100, D=D, bg=True, C=1, thin=True)
+    masks = (np.random.default_rng(8).random(sc["off"].shape) > 0.3) if masked else None
+    res = []
+    for only in (False, True):
+        leaves = {k: T(sc[k]).requires_grad_(True) for k in ("m2", "rt", "colors", "opac", "nr")}
+        densify = torch.zeros_like(leaves["m2"], requires_grad=True)
+        out = rasterize_to_pixels_2dgs(
+            leaves["m2"], leaves["rt"], leaves["colors"], leaves["opac"], leaves["nr"], densify,
+            sc["W"], sc["H"], sc["ts"], T(sc["off"]), T(sc["fids"]), backgrounds=T(sc["bg"]),
+            masks=None if masks is None else T(masks), _colors_only=only)
+        if only:
+            assert out[2] is None and out[3] is None and out[4] is None
+        w0 = torch.linspace(-1, 1, out[0].numel(), device=DEV).view_as(out[0])
+        ((out[0] * w0).sum() + out[1].sum()).backward()
+        res.append(([out[0].detach(), out[1].detach()],
+                    [leaves[k].grad for k in sorted(leaves)] + [densify.grad]))
+    for a, b in zip(res[0][0], res[1][0]):
+        torch.testing.assert_close(b, a, rtol=1e-6, atol=1e-6)
+    for a, b in zip(res[0][1], res[1][1]):
+        torch.testing.assert_close(b, a, rtol=1e-4, atol=1e-5 * max(float(a.abs().max()), 1e-30))
+
+
+@pytest.mark.parametrize("srec,only", [(True, False), (True, True), (False, False)])
+def test_raster2dgs_depth_channel_in_place(monkeypatch, srec, only):
+    """The last colour channel read from a separate depths array (ABI 33,
+    `_depths`: RGB+D without the concatenated copy) renders what the
+    concatenated colours render, bit for bit, and returns that channel's
+    gradient to the depths, the rest to the colours (to the atomics' order)."""
+    from gsplat_hip import _wrapper_2dgs, rasterize_to_pixels_2dgs
+    monkeypatch.setattr(_wrapper_2dgs, "SREC", srec)
+    sc = surfel_scene(9, N=800, W=150, H=100, D=4, bg=False, C=1, thin=True)
+    res = []
+    for split in (False, True):
+        leaves = {k: T(sc[k]).requires_grad_(True) for k in ("m2", "rt", "opac", "nr")}
+        rgb = T(sc["colors"][..., :3]).requires_grad_(True)
+        dep = T(sc["colors"][..., 3]).requires_grad_(True)
+        densify = torch.zeros_like(leaves["m2"], requires_grad=True)
+        cols = rgb if split else torch.cat([rgb, dep[..., None]], -1)
+        out = rasterize_to_pixels_2dgs(
+            leaves["m2"], leaves["rt"], cols, leaves["opac"], leaves["nr"], densify,
+            sc["W"], sc["H"], sc["ts"], T(sc["off"]), T(sc["fids"]),
+            _colors_only=only, _depths=dep if split else None)
+        w0 = torch.linspace(-1, 1, out[0].numel(), device=DEV).view_as(out[0])
+        loss = (out[0] * w0).sum() + out[1].sum()
+        if not only:
+            loss = loss + out[2].sum() + 0.5 * out[3].sum() + 0.25 * out[4].sum()
+        loss.backward()
+        res.append(([o.detach() for o in out if o is not None],
+                    [leaves[k].grad for k in sorted(leaves)] + [rgb.grad, dep.grad, densify.grad]))
+    for a, b in zip(res[0][0], res[1][0]):
+        assert torch.equal(a, b), float((a - b).abs().max())
+    for a, b in zip(res[0][1], res[1][1]):
+        torch.testing.assert_close(b, a, rtol=1e-4, atol=1e-5 * max(float(a.abs().max()), 1e-30))
+
+
 def test_raster2dgs_channel_padding():
     """10 channels are padded to the next compiled count with the depth kept
     last (gsplat/cuda/_wrapper.py:1657-1683); results equal the oracle at 10."""

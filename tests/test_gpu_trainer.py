@@ -63,7 +63,9 @@ def test_l1_ssim_loss_matches_torch(B, H, W, C, lam, fused):
 def test_fused_loss_reads_rgbd_render_in_place(H, W, ring):
     """The fused loss over the colour channels of an RGB+D render read in
     place (x_stride 4, the 2DGS trainer's loss) equals the loss of the
-    contiguous colour copy bit for bit, value and gradient; the depth
+    contiguous colour copy, value and gradient, to float rounding (the
+    in-place kernel blocks its vertical pass by 2 rows, not 4: at 128 VGPRs
+    the 4-row form spilled 25 of them with the strided reads); the depth
     channel's gradient is exactly zero (no slice copy, no zero-filled
     gradient image)."""
     from gsplat_hip.losses import ONE_GRAD, l1_ssim_loss
@@ -81,11 +83,12 @@ def test_fused_loss_reads_rgbd_render_in_place(H, W, ring):
     b = rgbd[..., :3].contiguous().requires_grad_(True)
     la = l1_ssim_loss(a, target, 0.2, fused=True, _channels=3, **kw)
     lb = l1_ssim_loss(b, target, 0.2, fused=True, **kw)
-    assert torch.equal(la, lb), (float(la), float(lb))
+    torch.testing.assert_close(la, lb, rtol=1e-6, atol=0)
     la.backward()
     lb.backward()
     assert a.grad.shape == (1, H, W, 4)
-    assert torch.equal(a.grad[..., :3], b.grad)
+    torch.testing.assert_close(a.grad[..., :3], b.grad, rtol=1e-5,
+                               atol=1e-6 * float(b.grad.abs().max()))
     assert torch.equal(a.grad[..., 3], torch.zeros_like(a.grad[..., 3]))
 
 
