@@ -10,6 +10,7 @@
 // camera parameters are wave-uniform scalar loads.  Inputs stay AoS as the
 // caller holds them ([N,3] means, [N,4] quats, [N,3] scales).
 #include "common.h"
+#include "geom_adam.h"
 #include "../../include/gsplat_hip.h"
 
 namespace gs {
@@ -210,33 +211,6 @@ __global__ void __launch_bounds__(1024) packed_scan_kernel(int64_t nb, int64_t *
   }
   if (threadIdx.x == 0) total[0] = carry;
 }
-
-// The geometry groups' Adam step fused into the backward (ABI 31,
-// gsplat_hip_projection_bwd_adam; C == 1, non-packed): instead of storing
-// v_means / v_quats / v_scales, every lane applies torch.optim.Adam to its
-// Gaussian's rows of the four geometry parameters in place, with the
-// gradients the trainer's FusedAdam would have formed (adam_step_ex modes):
-// means  g = v_means + v_dirs          (the SH backward's part; autograd's sum)
-// quats  g = v_quats
-// log-scales  g = v_scales * exp(log_scales)   (exp's VJP, the activated scale)
-// logits      g = v_opac * (1 - o) * o         (sigmoid's VJP, o = sigmoid(logits))
-// -- the same arithmetic as activate_bwd_kernel / adam::xform, the same
-// element update (common.h adam_update), so the result is bit-identical to
-// projection backward + activation backward + FusedAdam (the gradient
-// algebra above is the unfused kernel's own code: the fusion is a runtime
-// branch of the epilogue).  88 B per Gaussian of gradients never reach HBM.
-struct GeomAdam {
-  float *p[4];  // means [N,3], log-scales [N,3], quats [N,4], logits [N] (the trainer's order)
-  float *m[4], *v[4];
-  const float *v_dirs;  // [N,3] or null
-  const float *v_opac;  // [N] dL/d sigmoid(logits), or null
-  const float *opac;    // [N] sigmoid(logits) of the forward
-  float ss[4], ib;      // lr_i / (1 - beta1^t), 1 / sqrt(1 - beta2^t)
-  const float *hyper;   // device [8]: (ss_i, ib) per group (captured step), or null
-  const int32_t *skip;  // device flag: non-zero = void step (nothing updated), or null
-  float b1, b2, eps;
-
-};
 
 struct ProjBwdArgs {
   int C, N, W, H;

@@ -25,6 +25,7 @@
 //    unpack_kernel scatters the rows into the autograd tensors and forms the
 //    densification gradient.
 #include "common.h"
+#include "geom_adam.h"
 #include "wave_ops.h"
 #include "../../include/gsplat_hip.h"
 
@@ -198,8 +199,15 @@ struct ProjBwdArgs {
   const int64_t *camera_ids, *gaussian_ids;
   int64_t nnz;
   int sparse;
+  GeomAdam ga;  // proj_bwd_kernel: the geometry Adam instead of the stores
 };
 
+// a.ga.p[0] set (ABI 33, gsplat_hip_projection_2dgs_bwd_adam; C == 1,
+// dense): the geometry groups' Adam step on the lane's rows instead of
+// storing v_means / v_quats / v_scales (geom_adam.h).  A runtime branch of
+// the one kernel, so that the fused update consumes exactly the gradient
+// values the plain backward stores (two instantiations contracted the
+// algebra differently: 1 ulp in the log-scales).
 __global__ void __launch_bounds__(256) proj_bwd_kernel(ProjBwdArgs a) {
   int c, n;
   size_t idx;
@@ -219,6 +227,10 @@ __global__ void __launch_bounds__(256) proj_bwd_kernel(ProjBwdArgs a) {
     idx = (size_t)c * a.N + n;
     valid = a.radii[idx] > 0;
   }
+  GeomRows gr;
+  const bool fuse = a.ga.p[0] != nullptr;
+  const bool fuse_on = fuse && !(a.ga.skip && *a.ga.skip);
+  if (fuse_on) geom_rows_load(a.ga, (size_t)n, a.scales, gr);  // in flight from here
   const Cam k = load_cam(a.viewmats, a.Ks, c);
   float vm[3] = {0.f, 0.f, 0.f}, vq[4] = {0.f, 0.f, 0.f, 0.f}, vs[3] = {0.f, 0.f, 0.f};
   if (valid) {
@@ -284,6 +296,16 @@ __global__ void __launch_bounds__(256) proj_bwd_kernel(ProjBwdArgs a) {
     vs[1] = vRS[0][1] * f.Rq.m[0][1] + vRS[1][1] * f.Rq.m[1][1] + vRS[2][1] * f.Rq.m[2][1];
 #pragma unroll
     for (int i = 0; i < 3; ++i) vm[i] = vRS[i][2];
+  }
+  // the gradients are formed once, here, for every epilogue below, each
+  // rounded on its own: the fused Adam epilogue (FUSE) then consumes exactly
+  // the values the plain kernel stores (without the barrier the compiler may
+  // contract the algebra differently in the two instantiations)
+  asm volatile("" : "+v"(vm[0]), "+v"(vm[1]), "+v"(vm[2]), "+v"(vq[0]), "+v"(vq[1]),
+               "+v"(vq[2]), "+v"(vq[3]), "+v"(vs[0]), "+v"(vs[1]), "+v"(vs[2]));
+  if (fuse) {
+    if (fuse_on) geom_rows_update(a.ga, (size_t)n, gr, vm, vs, vq);
+    return;
   }
   if (packed && a.sparse) {  // COO values, one row per packed entry
     float *o = a.v_means + 3 * idx;
@@ -1749,6 +1771,39 @@ extern "C" int gsplat_hip_projection_2dgs_bwd(
                 v_depths, v_normals, v_ray_transforms, v_means, v_quats, v_scales, store_mode};
   hipLaunchKernelGGL(proj_bwd_kernel, dim3((N + 255) / 256, C), dim3(256), 0, st, a);
   GS_CHECK_LAUNCH("projection_2dgs_bwd");
+  return 0;
+}
+
+// gsplat_hip_projection_2dgs_bwd with the geometry groups' Adam step fused in
+// (ABI 33; geom_adam.h, as gsplat_hip_projection_bwd_adam for 3DGS): one
+// camera; params / exp_avgs / exp_avg_sqs are [means, log_scales, quats,
+// logits]; lrs[4] with the 1-based step, or hyper_device f32[8]; skip_device
+// may be NULL.  No gradient is stored.
+extern "C" int gsplat_hip_projection_2dgs_bwd_adam(
+    int N, const float *means, const float *quats, const float *scales, const float *viewmats,
+    const float *Ks, const int32_t *radii, const float *ray_transforms, const float *v_means2d,
+    const float *v_depths, const float *v_normals, const float *v_ray_transforms,
+    const float *v_dirs, const float *v_opac, const float *opac, float *const *params,
+    float *const *exp_avgs, float *const *exp_avg_sqs, const float *lrs, float beta1,
+    float beta2, float eps, int step, const float *hyper_device, const int32_t *skip_device,
+    void *stream) {
+  GS_REQUIRE(N >= 0, "projection_2dgs_bwd_adam: negative N=%d", N);
+  if (N == 0) return 0;
+  GS_REQUIRE(means && quats && scales && viewmats && Ks && radii && ray_transforms &&
+                 v_means2d && v_normals && v_ray_transforms,
+             "projection_2dgs_bwd_adam: null pointer argument");
+  GS_REQUIRE(((uintptr_t)quats & 15) == 0, "projection_2dgs_bwd_adam: quats must be 16-B aligned");
+  GeomAdam ga;
+  if (int e = geom_adam_setup(ga, params, exp_avgs, exp_avg_sqs, lrs, beta1, beta2, eps, step,
+                              hyper_device, skip_device, v_dirs, v_opac, opac,
+                              "projection_2dgs_bwd_adam"))
+    return e;
+  ProjBwdArgs a{1, N, means, quats, scales, viewmats, Ks, radii, ray_transforms, v_means2d,
+                v_depths, v_normals, v_ray_transforms, nullptr, nullptr, nullptr, 1};
+  a.ga = ga;
+  hipLaunchKernelGGL(proj_bwd_kernel, dim3((N + 255) / 256, 1), dim3(256), 0,
+                     (hipStream_t)stream, a);
+  GS_CHECK_LAUNCH("projection_2dgs_bwd_adam");
   return 0;
 }
 

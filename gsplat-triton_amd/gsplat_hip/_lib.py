@@ -54,6 +54,8 @@ _SIGS = {
     "gsplat_hip_graph_node_census": (_i32, [_p, _p, _p, _i32]),
     "gsplat_hip_graph_memcpy_census": (_i32, [_p, _p, _i32, _p]),
     "gsplat_hip_status_to_ring": (_i32, [_p, _p, _p, _p]),
+    "gsplat_hip_projection_2dgs_bwd_adam": (_i32, [_i32] + [_p] * 18 + [_f] * 3 + [_i32]
+                                            + [_p] * 3),
     "gsplat_hip_projection_bwd_adam": (_i32, [_i32, _p, _p, _p, _p, _p, _i32, _i32, _f, _p, _p,
                                               _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _f, _f,
                                               _f, _i32, _p, _p, _p]),

@@ -739,6 +739,26 @@ class GeomAdamInBackward:
         self.applied = True
 
 
+    def run_2dgs(self, means, quats, scales, viewmats, Ks, radii, ray_transforms, v_means2d,
+                 v_depths, v_normals, v_ray_transforms, fusion):
+        """The 2DGS projection backward's form (gsplat_hip_projection_2dgs_bwd_adam)."""
+        N = means.shape[0]
+        for t in self.params + self.exp_avgs + self.exp_avg_sqs:
+            assert t.is_contiguous() and t.dtype == torch.float32
+        assert [t.shape[0] for t in self.params] == [N] * 4
+        P = ctypes.c_void_p * 4
+        _lib.call("gsplat_hip_projection_2dgs_bwd_adam", N, _ptr(means), _ptr(quats),
+                  _ptr(scales), _ptr(viewmats), _ptr(Ks), _ptr(radii), _ptr(ray_transforms),
+                  _ptr(v_means2d), _ptr(v_depths), _ptr(v_normals), _ptr(v_ray_transforms),
+                  _ptr(fusion.v_dirs), _ptr(fusion.v_opac_in), _ptr(fusion.opac_act),
+                  P(*[t.data_ptr() for t in self.params]),
+                  P(*[t.data_ptr() for t in self.exp_avgs]),
+                  P(*[t.data_ptr() for t in self.exp_avg_sqs]),
+                  (ctypes.c_float * 4)(*self.lrs), float(self.betas[0]), float(self.betas[1]),
+                  float(self.eps), int(self.step), _ptr(self.hyper), _ptr(self.skip), _stream())
+        self.applied = True
+
+
 class _OpacityTap(torch.autograd.Function):
     """opacities[None] for one camera, whose backward also hands the incoming
     dL/dopacities to the step's StepFusion (the geometry Adam in the

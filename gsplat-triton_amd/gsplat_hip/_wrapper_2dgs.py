@@ -29,7 +29,10 @@ class _FullyFusedProjection2DGS(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, means, quats, scales, viewmats, Ks, width, height, eps2d, near_plane,
-                far_plane, radius_clip):
+                far_plane, radius_clip, fusion=None):
+        # fusion: a training step's StepFusion whose geometry Adam this
+        # backward runs (gsplat_hip_projection_2dgs_bwd_adam, one camera)
+        ctx.fusion = fusion
         means, quats, scales, viewmats, Ks = (_f32c(x) for x in (means, quats, scales, viewmats, Ks))
         quats = _aligned16(quats)
         _dev_check(means, quats, scales, viewmats, Ks)
@@ -63,6 +66,13 @@ class _FullyFusedProjection2DGS(torch.autograd.Function):
         v_ray_transforms = grad(v_ray_transforms, (C, N, 3, 3))
         v_normals = grad(v_normals, (C, N, 3))
         v_depths = None if v_depths is None else _f32c(v_depths)
+        fusion = ctx.fusion
+        if (fusion is not None and C == 1 and not ctx.needs_input_grad[3]
+                and fusion.geom_adam_ready()):
+            # the trainer's geometry Adam step in this backward: no gradients stored
+            fusion.geom_adam.run_2dgs(means, quats, scales, viewmats, Ks, radii, ray_transforms,
+                                      v_means2d, v_depths, v_normals, v_ray_transforms, fusion)
+            return (None,) * 12
         v_means = torch.empty((N, 3), device=dev)
         v_quats = torch.empty((N, 4), device=dev)
         v_scales = torch.empty((N, 3), device=dev)
@@ -78,7 +88,8 @@ class _FullyFusedProjection2DGS(torch.autograd.Function):
             v_quats = None
         if not ctx.needs_input_grad[2]:
             v_scales = None
-        return (v_means, v_quats, v_scales, v_viewmats, None, None, None, None, None, None, None)
+        return (v_means, v_quats, v_scales, v_viewmats, None, None, None, None, None, None, None,
+                None)
 
 
 class _FullyFusedProjectionPacked2DGS(torch.autograd.Function):

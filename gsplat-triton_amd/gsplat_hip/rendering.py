@@ -556,15 +556,27 @@ def rasterization_2dgs(
     else:
         assert colors.dim() == 3 and colors.shape[0] == N and colors.shape[2] == 3, colors.shape
         assert (sh_degree + 1) ** 2 <= colors.shape[1], colors.shape
-    proj = fully_fused_projection_2dgs(
-        means, quats, scales, viewmats, Ks, width, height, eps2d, near_plane, far_plane,
-        radius_clip, packed, sparse_grad)
+    # a training step's geometry Adam inside the projection backward
+    # (StepFusion.geom_adam, ABI 33): one camera, dense, no pose gradient
+    geom_adam = (_fusion is not None and _fusion.geom_adam is not None and not packed
+                 and C == 1 and not viewmats.requires_grad)
+    if geom_adam:
+        from ._wrapper_2dgs import _FullyFusedProjection2DGS
+        proj = _FullyFusedProjection2DGS.apply(means, quats, scales, viewmats, Ks, width, height,
+                                               eps2d, near_plane, far_plane, radius_clip, _fusion)
+    else:
+        proj = fully_fused_projection_2dgs(
+            means, quats, scales, viewmats, Ks, width, height, eps2d, near_plane, far_plane,
+            radius_clip, packed, sparse_grad)
     if packed:  # gsplat/rendering.py:1188-1199
         camera_ids, gaussian_ids, radii, means2d, depths, ray_transforms, normals = proj
         opacities = opacities[gaussian_ids]
     else:
         radii, means2d, depths, ray_transforms, normals = proj
-        opacities = opacities[None] if C == 1 else opacities.repeat(C, 1)
+        if geom_adam:  # the same view, its gradient also handed to the fusion
+            opacities = _wrapper._OpacityTap.apply(opacities, _fusion)
+        else:
+            opacities = opacities[None] if C == 1 else opacities.repeat(C, 1)
         camera_ids, gaussian_ids = None, None
     # the densification input only receives a gradient (its values are never
     # read): the training step's (_colors_only) skips the reference's zero fill

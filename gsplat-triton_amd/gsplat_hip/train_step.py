@@ -241,12 +241,13 @@ class Trainer:
         self.geom_fuse = (fused and not self.defer_sh
                           and (world_size == 1 or self.sharded or self.gshard)
                           and os.environ.get("GSPLAT_HIP_GEOM_FUSE", "1") != "0")
-        # one rank, 3DGS: the geometry groups' whole Adam step inside the
-        # projection backward (gsplat_hip_projection_bwd_adam), so their
-        # gradients never go through HBM; GSPLAT_HIP_GEOM_IN_PROJ=0 turns it
-        # off.  Not with the regularisers (extra terms on the raw parameters)
+        # one rank: the geometry groups' whole Adam step inside the
+        # projection backward (gsplat_hip_projection_bwd_adam, 2DGS:
+        # gsplat_hip_projection_2dgs_bwd_adam), so their gradients never go
+        # through HBM; GSPLAT_HIP_GEOM_IN_PROJ=0 turns it off.  Not with the
+        # regularisers (extra terms on the raw parameters)
         self.geom_in_proj = (self.geom_fuse and world_size == 1 and not self.gshard
-                             and not self.sharded and model == "3dgs"
+                             and not self.sharded and model in ("3dgs", "2dgs")
                              and self.opacity_reg == 0.0 and self.scale_reg == 0.0
                              and os.environ.get("GSPLAT_HIP_GEOM_IN_PROJ", "1") != "0")
         # sharded optimizer: the SH group's collectives on a communicator of

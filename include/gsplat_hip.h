@@ -37,7 +37,8 @@ const char *gsplat_hip_last_error(void);
  * 33: colours-only 2DGS renders (render_normals / distort / median and
  *     median_ids NULL in gsplat_hip_rasterize_2dgs_fwd and _bwd); the 2DGS
  *     rasterizer's last colour channel from a separate depths array
- *     (depths / v_depths of _pack_records, _fwd, _bwd). */
+ *     (depths / v_depths of _pack_records, _fwd, _bwd);
+ *     gsplat_hip_projection_2dgs_bwd_adam. */
 int gsplat_hip_abi_version(void);
 
 /* ---------------------------------------------------------------------------
@@ -642,6 +643,20 @@ int gsplat_hip_projection_2dgs_bwd(int C, int N, const float *means, const float
                                    const float *v_ray_transforms, float *v_means,
                                    float *v_quats, float *v_scales, float *v_viewmats,
                                    void *stream);
+/* The same backward for one camera with the geometry groups' Adam step fused
+ * in (ABI 33; as gsplat_hip_projection_bwd_adam for 3DGS): no gradient is
+ * stored; params / exp_avgs / exp_avg_sqs are [means, log_scales, quats,
+ * logits]; v_dirs [N,3] (the SH backward's means gradient) and v_opac [N]
+ * (dL/d sigmoid(logits), with opac = sigmoid(logits)) may be NULL; lrs[4]
+ * with the 1-based step, or hyper_device f32[8]; skip_device may be NULL. */
+int gsplat_hip_projection_2dgs_bwd_adam(
+    int N, const float *means, const float *quats, const float *scales, const float *viewmats,
+    const float *Ks, const int32_t *radii, const float *ray_transforms, const float *v_means2d,
+    const float *v_depths, const float *v_normals, const float *v_ray_transforms,
+    const float *v_dirs, const float *v_opac, const float *opac, float *const *params,
+    float *const *exp_avgs, float *const *exp_avg_sqs, const float *lrs, float beta1,
+    float beta2, float eps, int step, const float *hyper_device, const int32_t *skip_device,
+    void *stream);
 /* Packed 2DGS projection.  Replaces projection_2dgs_packed_fwd / _bwd
  * (gsplat/cuda/csrc/Projection2DGSPacked.cu:17-270, 274-420) behind
  * _FullyFusedProjectionPacked2DGS (gsplat/cuda/_wrapper.py:1440-1592).

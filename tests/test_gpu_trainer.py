@@ -693,3 +693,108 @@ def test_trainer_geometry_adam_in_projection_close(monkeypatch):
         assert abs(a - b) <= 1e-4 * abs(a) + 1e-7, (out["0"][0], out["1"][0])
     for k in out["0"][1]:
         torch.testing.assert_close(out["1"][1][k], out["0"][1][k], rtol=1e-3, atol=1e-5)
+
+
+@pytest.mark.parametrize("dev_factors", [False, True])
+def test_projection_2dgs_bwd_adam_is_exact(dev_factors):
+    """The 2DGS projection backward with the geometry groups' Adam fused in
+    (gsplat_hip_projection_2dgs_bwd_adam, ABI 33) updates parameters and
+    moments bit for bit as projection_2dgs_bwd + FusedAdam with the trainer's
+    gradient transforms (means + v_dirs, exp and sigmoid VJPs), over three
+    steps, host and device factor forms, invisible surfels and a ragged N."""
+    import ctypes
+    from gsplat_hip import _lib
+    from gsplat_hip._wrapper import _ptr, _stream
+    from gsplat_hip.losses import FusedAdam, adam_factors
+    g = torch.Generator().manual_seed(4)
+    N, W, H = 3001, 320, 240
+    means = (torch.randn(N, 3, generator=g) * 0.8 + torch.tensor([0, 0, 4.0])).cuda()
+    logs = torch.log(torch.rand(N, 3, generator=g) * 0.05 + 0.005).cuda()
+    quats = torch.nn.functional.normalize(torch.randn(N, 4, generator=g), dim=-1).cuda()
+    logit = torch.randn(N, generator=g).cuda()
+    vm = torch.eye(4)[None].cuda()
+    K = torch.tensor([[[300.0, 0, 160], [0, 300.0, 120], [0, 0, 1]]]).cuda()
+    lrs = [1.6e-4, 5e-3, 1e-3, 5e-2]
+    res = []
+    for fused in (False, True):
+        ps = [t.clone() for t in (means, logs, quats, logit)]
+        opt = FusedAdam([torch.nn.Parameter(p) for p in ps], lrs, betas=(0.9, 0.999), eps=1e-15)
+        ps = [p.data for p in opt.params]
+        for it in range(3):
+            gg = torch.Generator(device="cuda").manual_seed(30 + it)
+            scales = torch.exp(ps[1])
+            opac = torch.sigmoid(ps[3])
+            radii = torch.empty(1, N, dtype=torch.int32, device="cuda")
+            m2 = torch.empty(1, N, 2, device="cuda")
+            dep = torch.empty(1, N, device="cuda")
+            rt = torch.empty(1, N, 3, 3, device="cuda")
+            nr = torch.empty(1, N, 3, device="cuda")
+            _lib.call("gsplat_hip_projection_2dgs_fwd", 1, N, _ptr(ps[0]), _ptr(ps[2]),
+                      _ptr(scales), _ptr(vm), _ptr(K), W, H, ctypes.c_float(0.01),
+                      ctypes.c_float(1e10), ctypes.c_float(0.0), _ptr(radii), _ptr(m2),
+                      _ptr(dep), _ptr(rt), _ptr(nr), _stream())
+            v2 = torch.randn(1, N, 2, device="cuda", generator=gg)
+            vrt = torch.randn(1, N, 3, 3, device="cuda", generator=gg) * 1e-3
+            vnr = torch.randn(1, N, 3, device="cuda", generator=gg) * 1e-2
+            vd = torch.randn(1, N, device="cuda", generator=gg)
+            vdirs = torch.randn(N, 3, device="cuda", generator=gg)
+            vop = torch.randn(N, device="cuda", generator=gg)
+            step = opt.step_count + 1
+            if fused:
+                P = ctypes.c_void_p * 4
+                hyper = None
+                if dev_factors:
+                    fac = adam_factors(lrs, opt.betas, step)
+                    hyper = torch.tensor([x for f in fac for x in f], device="cuda")
+                _lib.call("gsplat_hip_projection_2dgs_bwd_adam", N, _ptr(ps[0]), _ptr(ps[2]),
+                          _ptr(scales), _ptr(vm), _ptr(K), _ptr(radii), _ptr(rt), _ptr(v2),
+                          _ptr(vd), _ptr(vnr), _ptr(vrt), _ptr(vdirs), _ptr(vop), _ptr(opac),
+                          P(*[p.data_ptr() for p in ps]),
+                          P(*[m.data_ptr() for m in opt.exp_avg]),
+                          P(*[v.data_ptr() for v in opt.exp_avg_sq]),
+                          (ctypes.c_float * 4)(*lrs), ctypes.c_float(0.9),
+                          ctypes.c_float(0.999), ctypes.c_float(1e-15), step, _ptr(hyper), 0,
+                          _stream())
+                opt.step_count += 1
+            else:
+                v_means = torch.empty(N, 3, device="cuda")
+                v_quats = torch.empty(N, 4, device="cuda")
+                v_scales = torch.empty(N, 3, device="cuda")
+                _lib.call("gsplat_hip_projection_2dgs_bwd", 1, N, _ptr(ps[0]), _ptr(ps[2]),
+                          _ptr(scales), _ptr(vm), _ptr(K), W, H, _ptr(radii), _ptr(rt),
+                          _ptr(v2), _ptr(vd), _ptr(vnr), _ptr(vrt), _ptr(v_means),
+                          _ptr(v_quats), _ptr(v_scales), 0, _stream())
+                opt.params[0].grad, opt.params[2].grad = v_means, v_quats
+                opt.step(xform={0: (v_means, vdirs, 1), 1: (v_scales, scales, 2),
+                                3: (vop, opac, 3)})
+                opt.zero_grad()
+            assert (radii > 0).any() and (radii == 0).any()
+        torch.cuda.synchronize()
+        res.append([p.clone() for p in ps] + [m.clone() for m in opt.exp_avg] +
+                   [v.clone() for v in opt.exp_avg_sq])
+    for a, b in zip(res[0], res[1]):
+        assert torch.equal(a, b), float((a - b).abs().max())
+
+
+def test_trainer_2dgs_geometry_adam_in_projection_close(monkeypatch):
+    """The 2DGS trainer with the geometry Adam inside the surfel projection
+    backward (the one-rank default) applies it on every step and tracks the
+    trainer that steps FusedAdam after the backward (last-bit differences
+    from the rasterizer's atomics)."""
+    from gsplat_hip.train_step import Trainer
+    means, rgbs, vm, K, W, H = _small_scene()
+    out = {}
+    for f in ("0", "1"):
+        monkeypatch.setenv("GSPLAT_HIP_GEOM_IN_PROJ", f)
+        tr = Trainer(means, rgbs, vm, K, W, H, device="cuda", model="2dgs", max_steps=100)
+        assert tr.geom_in_proj == (f == "1")
+        losses = []
+        for it in range(5):
+            losses.append(float(tr.step(it)))
+            assert tr.geom_applied == (f == "1")
+        out[f] = (losses, {k: p.detach().clone() for k, p in tr.params.items()})
+    assert out["0"][0][0] == out["1"][0][0]
+    for a, b in zip(out["0"][0], out["1"][0]):
+        assert abs(a - b) <= 1e-4 * abs(a) + 1e-7, (out["0"][0], out["1"][0])
+    for k in out["0"][1]:
+        torch.testing.assert_close(out["1"][1][k], out["0"][1][k], rtol=1e-3, atol=1e-5)
