@@ -117,7 +117,7 @@ def pmc_traffic(config: str):
         return None  # already running under a profiler: no nested profiler runs
     env = dict(os.environ, TMPDIR="/tmp")
     ns = "surfel" if MODEL.get(config) == "2dgs" else "r16"
-    regex = f"{ns}::(fwd|bwd)2?_kernel"
+    regex = f"{ns}::(fwd|bwd)2?s?_kernel"
     per = {"fwd": {}, "bwd": {}}
     for ctrs in PMC_PASSES:
         d = tempfile.mkdtemp(prefix="gsplat_pmc_", dir="/tmp")
