@@ -277,7 +277,11 @@ __global__ void __launch_bounds__(256) proj_bwd_kernel(ProjBwdArgs a) {
 #pragma unroll
       for (int j = 0; j < 3; ++j)
         vRS[i][j] = k.R.m[0][i] * dW[0][j] + k.R.m[1][i] * dW[1][j] + k.R.m[2][i] * dW[2][j];
-    const float *gn = a.v_normals + 3 * idx;
+    // v_normals may be null (ABI 33: a render whose normals carry no
+    // gradient): zeros through the same arithmetic
+    float gn[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) gn[i] = a.v_normals ? a.v_normals[3 * idx + i] : 0.f;
     const float sgn =
         -(f.nz[0] * f.mc[0] + f.nz[1] * f.mc[1] + f.nz[2] * f.mc[2]) > 0.f ? 1.f : -1.f;
     float vtn[3];
@@ -1630,8 +1634,10 @@ unpack_kernel(int64_t G, const int32_t *__restrict__ visible, const float *__res
     for (int d = 0; d < D; ++d)
       if (d < DC) v_colors[g * DC + d] = 0.f;
     if (v_depths) v_depths[g] = 0.f;
+    if (v_normals) {
 #pragma unroll
-    for (int i = 0; i < 3; ++i) v_normals[g * 3 + i] = 0.f;
+      for (int i = 0; i < 3; ++i) v_normals[g * 3 + i] = 0.f;
+    }
 #pragma unroll
     for (int i = 0; i < 9; ++i) v_rt[g * 9 + i] = 0.f;
     *reinterpret_cast<float2 *>(v_means2d + 2 * g) = make_float2(0.f, 0.f);
@@ -1645,8 +1651,10 @@ unpack_kernel(int64_t G, const int32_t *__restrict__ visible, const float *__res
   for (int d = 0; d < D; ++d)
     if (d < DC) v_colors[g * DC + d] = r[F::COL + d];
   if (v_depths) v_depths[g] = r[F::COL + D - 1];
+  if (v_normals) {  // null: the render's normals had no gradient (all zero)
 #pragma unroll
-  for (int i = 0; i < 3; ++i) v_normals[g * 3 + i] = LEAN ? 0.f : r[F::NRM + i];
+    for (int i = 0; i < 3; ++i) v_normals[g * 3 + i] = LEAN ? 0.f : r[F::NRM + i];
+  }
 #pragma unroll
   for (int i = 0; i < 9; ++i) v_rt[g * 9 + i] = r[F::M + i];
   *reinterpret_cast<float2 *>(v_means2d + 2 * g) = make_float2(r[F::XY], r[F::XY + 1]);
@@ -1763,7 +1771,7 @@ extern "C" int gsplat_hip_projection_2dgs_bwd(
   }
   if (C == 0) return 0;
   GS_REQUIRE(means && quats && scales && viewmats && Ks && radii && ray_transforms &&
-                 v_means2d && v_normals && v_ray_transforms && v_means && v_quats && v_scales,
+                 v_means2d && v_ray_transforms && v_means && v_quats && v_scales,
              "projection_2dgs_bwd: null pointer argument");
   GS_REQUIRE(((uintptr_t)quats & 15) == 0 && ((uintptr_t)v_quats & 15) == 0,
              "projection_2dgs_bwd: quats / v_quats must be 16-B aligned");
@@ -1790,7 +1798,7 @@ extern "C" int gsplat_hip_projection_2dgs_bwd_adam(
   GS_REQUIRE(N >= 0, "projection_2dgs_bwd_adam: negative N=%d", N);
   if (N == 0) return 0;
   GS_REQUIRE(means && quats && scales && viewmats && Ks && radii && ray_transforms &&
-                 v_means2d && v_normals && v_ray_transforms,
+                 v_means2d && v_ray_transforms,
              "projection_2dgs_bwd_adam: null pointer argument");
   GS_REQUIRE(((uintptr_t)quats & 15) == 0, "projection_2dgs_bwd_adam: quats must be 16-B aligned");
   GeomAdam ga;
@@ -2048,7 +2056,7 @@ extern "C" int gsplat_hip_rasterize_2dgs_bwd(
              "rasterize_2dgs_bwd: workspace too small");
   hipStream_t st = (hipStream_t)stream;
   if (G == 0) return 0;
-  GS_REQUIRE(workspace && v_means2d && v_ray_transforms && v_colors && v_opacities && v_normals &&
+  GS_REQUIRE(workspace && v_means2d && v_ray_transforms && v_colors && v_opacities &&
                  v_densify && ray_transforms,
              "rasterize_2dgs_bwd: null pointer argument");
   if (visible)

@@ -64,7 +64,8 @@ class _FullyFusedProjection2DGS(torch.autograd.Function):
 
         v_means2d = grad(v_means2d, (C, N, 2))
         v_ray_transforms = grad(v_ray_transforms, (C, N, 3, 3))
-        v_normals = grad(v_normals, (C, N, 3))
+        # None (the rasterizer's normals had no gradient, ABI 33): null = zeros
+        v_normals = None if v_normals is None else _f32c(v_normals)
         v_depths = None if v_depths is None else _f32c(v_depths)
         fusion = ctx.fusion
         if (fusion is not None and C == 1 and not ctx.needs_input_grad[3]
@@ -312,7 +313,9 @@ class _RasterizeToPixels2DGS(torch.autograd.Function):
         v_colors = torch.empty_like(colors)
         v_depths = None if depths is None else torch.empty_like(depths)
         v_opacities = torch.empty_like(opacities)
-        v_normals = torch.empty_like(normals)
+        # without a gradient of the normal image the normals' gradient is
+        # exactly zero: None (the kernel skips it) instead of a zero-filled [G,3]
+        v_normals = None if v_render_normals is None else torch.empty_like(normals)
         v_densify = torch.empty(densify.shape, device=dev)
         v_abs = torch.empty_like(means2d) if ctx.absgrad else None
         ws = torch.empty(max(int(_lib.query("gsplat_hip_rasterize_2dgs_bwd_workspace_bytes", G, D,

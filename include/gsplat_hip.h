@@ -38,7 +38,8 @@ const char *gsplat_hip_last_error(void);
  *     median_ids NULL in gsplat_hip_rasterize_2dgs_fwd and _bwd); the 2DGS
  *     rasterizer's last colour channel from a separate depths array
  *     (depths / v_depths of _pack_records, _fwd, _bwd);
- *     gsplat_hip_projection_2dgs_bwd_adam. */
+ *     gsplat_hip_projection_2dgs_bwd_adam; v_normals may be NULL in the
+ *     2DGS rasterizer's backward (output) and projection backward (input). */
 int gsplat_hip_abi_version(void);
 
 /* ---------------------------------------------------------------------------
@@ -634,7 +635,7 @@ int gsplat_hip_projection_2dgs_fwd(int C, int N, const float *means, const float
  * Projection.cpp:569-633; _FullyFusedProjection2DGS.backward, _wrapper.py:1391-1437).
  * -> v_means[N,3], v_quats[N,4], v_scales[N,3] (v_scales[:,2] = 0).
  * v_viewmats[C,4,4] (or NULL) is written as zeros, as the reference's kernel
- * never writes it.  v_depths may be NULL. */
+ * never writes it.  v_depths may be NULL; v_normals too (ABI 33; zeros). */
 int gsplat_hip_projection_2dgs_bwd(int C, int N, const float *means, const float *quats,
                                    const float *scales, const float *viewmats, const float *Ks,
                                    int width, int height, const int32_t *radii,
@@ -760,7 +761,9 @@ int gsplat_hip_rasterize_2dgs_fwd(int C, int D, int width, int height, int tile_
  *    sums), v_means2d_abs[G,2] or NULL (absgrad off).
  * v_render_alphas / v_render_normals (ABI 32) / v_render_distort /
  * v_render_median may be NULL (no gradient).  depths / v_depths (ABI 33, both
- * NULL or both set): the forward's separate last channel and its gradient.  visible (ABI 32, may be NULL;
+ * NULL or both set): the forward's separate last channel and its gradient.
+ * v_normals (ABI 33) may be NULL when v_render_normals is: that gradient is
+ * then exactly zero and not written.  visible (ABI 32, may be NULL;
  * i32[G], e.g. tiles_per_gauss): only the rows with visible[g] > 0 can
  * receive gradient -- the others are written as zeros without a read. */
 int64_t gsplat_hip_rasterize_2dgs_bwd_workspace_bytes(int64_t n_gaussians, int D, int absgrad);

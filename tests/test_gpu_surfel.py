@@ -98,6 +98,15 @@ def _raster_gpu(sc, masks=None, absgrad=False, D=None):
     return leaves, bg, densify, out
 
 
+def _grads(leaves, extra=()):
+    """Leaf gradients in sorted-key order; an absent one (the backward returned
+    None: exactly zero, e.g. the normals' without a normal-image gradient)
+    as zeros."""
+    return [leaves[k].grad if leaves[k].grad is not None else torch.zeros_like(leaves[k])
+            for k in sorted(leaves)] + [t.grad if t.grad is not None else torch.zeros_like(t)
+                                        for t in extra]
+
+
 def _oracle_fwd(sc, masks=None):
     return S.raster2dgs_fwd(sc["m2"], sc["rt"], sc["colors"], sc["opac"], sc["nr"], sc["bg"],
                             masks, sc["W"], sc["H"], sc["ts"], sc["off"], sc["fids"])
@@ -233,7 +242,8 @@ def test_raster2dgs_bwd_lean_vs_oracle(seed, D, bg, absgrad, thin):
         vs[i] = np.zeros_like(vs[i])
     loss = (outs[0] * T(vs[0])).sum() + (outs[1] * T(vs[1])).sum()
     wrt = list(leaves.values()) + ([bgt] if bgt is not None else []) + [densify]
-    grads = torch.autograd.grad(loss, wrt)
+    grads = [torch.zeros_like(t) if g is None else g
+             for g, t in zip(torch.autograd.grad(loss, wrt, allow_unused=True), wrt)]
     oc, oa, on, od, om, ol, omi = _oracle_fwd(sc)
     ref = S.raster2dgs_bwd(sc["m2"], sc["rt"], sc["colors"], sc["opac"], sc["nr"], sc["bg"], None,
                            sc["W"], sc["H"], sc["ts"], sc["off"], sc["fids"], oc, oa, ol, omi,
@@ -267,7 +277,7 @@ def test_raster2dgs_bwd_lean_matches_general():
         if general:
             loss = loss + sum((o * 0.0).sum() for o in out[2:])
         loss.backward()
-        res.append([leaves[k].grad for k in sorted(leaves)] + [densify.grad])
+        res.append(_grads(leaves, (densify,)))
     for a, b in zip(res[0], res[1]):
         torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-5 * max(float(b.abs().max()), 1e-30))
 
@@ -295,8 +305,7 @@ def test_raster2dgs_colors_only_matches_full(D, masked):
             assert out[2] is None and out[3] is None and out[4] is None
         w0 = torch.linspace(-1, 1, out[0].numel(), device=DEV).view_as(out[0])
         ((out[0] * w0).sum() + out[1].sum()).backward()
-        res.append(([out[0].detach(), out[1].detach()],
-                    [leaves[k].grad for k in sorted(leaves)] + [densify.grad]))
+        res.append(([out[0].detach(), out[1].detach()], _grads(leaves, (densify,))))
     for a, b in zip(res[0][0], res[1][0]):
         torch.testing.assert_close(b, a, rtol=1e-6, atol=1e-6)
     for a, b in zip(res[0][1], res[1][1]):
@@ -329,7 +338,7 @@ def test_raster2dgs_depth_channel_in_place(monkeypatch, srec, only):
             loss = loss + out[2].sum() + 0.5 * out[3].sum() + 0.25 * out[4].sum()
         loss.backward()
         res.append(([o.detach() for o in out if o is not None],
-                    [leaves[k].grad for k in sorted(leaves)] + [rgb.grad, dep.grad, densify.grad]))
+                    _grads(leaves, (rgb, dep, densify))))
     for a, b in zip(res[0][0], res[1][0]):
         assert torch.equal(a, b), float((a - b).abs().max())
     for a, b in zip(res[0][1], res[1][1]):
