@@ -487,18 +487,23 @@ struct Gathered {
   float col[D];
 };
 
-template <int D>
-GS_INLINE void gather(const RasterArgs &a, int64_t j, bool ok, Gathered<D> &r) {
-  const int32_t g = ok ? a.flatten_ids[j] : 0;
+// The attributes of surfel g (NRM: its normal too).
+template <int D, bool NRM = true>
+GS_INLINE void gather_at(const RasterArgs &a, int32_t g, Gathered<D> &r) {
   r.g = g;
   r.xy = *reinterpret_cast<const float2 *>(a.means2d + 2 * (int64_t)g);
   r.op = a.opacities[g];
   const float *m = a.ray_transforms + 9 * (int64_t)g;
 #pragma unroll
   for (int i = 0; i < 9; ++i) r.m[i] = m[i];
-  const float *nr = a.normals + 3 * (int64_t)g;
+  if (NRM) {
+    const float *nr = a.normals + 3 * (int64_t)g;
 #pragma unroll
-  for (int i = 0; i < 3; ++i) r.nrm[i] = nr[i];
+    for (int i = 0; i < 3; ++i) r.nrm[i] = nr[i];
+  } else {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) r.nrm[i] = 0.f;
+  }
   if (a.depths) {
     const float *cl = a.colors + (D - 1) * (int64_t)g;
 #pragma unroll
@@ -509,6 +514,11 @@ GS_INLINE void gather(const RasterArgs &a, int64_t j, bool ok, Gathered<D> &r) {
 #pragma unroll
     for (int i = 0; i < D; ++i) r.col[i] = cl[i];
   }
+}
+
+template <int D>
+GS_INLINE void gather(const RasterArgs &a, int64_t j, bool ok, Gathered<D> &r) {
+  gather_at<D>(a, ok ? a.flatten_ids[j] : 0, r);
 }
 
 template <int D>
@@ -1485,13 +1495,30 @@ __global__ void __launch_bounds__(128) bwd2_kernel(RasterArgs a) {
   const int64_t end = min(tend, (int64_t)wmax + 1);
   const int lf = rs_field(lane);
 
+  // LEAN: the next batch's surfel ids loaded while this one composites (the
+  // batch's gathers then wait one global load, not two), and no normals
+  // gathered (their record fields are never read)
+  int32_t gid_next = 0;
+  if (LEAN && end > start) {
+    const int64_t j = max(start, end - 64) + lane;
+    gid_next = j < end ? a.flatten_ids[j] : 0;
+  }
   for (int64_t b1 = end; b1 > start; b1 -= 64) {
     const int64_t b0 = max(start, b1 - 64);
     int n;
     {
       Gathered<D> g;
       const int64_t j = b0 + lane;
-      gather<D>(a, j, j < b1, g);
+      if constexpr (LEAN) {
+        gather_at<D, false>(a, gid_next, g);
+        const int64_t b1n = b1 - 64;
+        if (b1n > start) {
+          const int64_t jn = max(start, b1n - 64) + lane;
+          gid_next = jn < b1n ? a.flatten_ids[jn] : 0;
+        }
+      } else {
+        gather<D>(a, j, j < b1, g);
+      }
       const bool keep = (j < b1) && surfel_keep(g.m, g.xy.x, g.xy.y, g.op, rx0, rx1, ry0, ry1);
       const uint64_t km = __ballot(keep);
       n = __popcll(km);
