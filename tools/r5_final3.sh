@@ -1,5 +1,6 @@
 #!/bin/bash
-# Round-5 final evidence (3): the whole GPU suite, the default bench line (PMC traffic + CPU baseline),
+# Round-5 final evidence (profiles/r5/final, final2, final3 were made by its
+# earlier forms): the whole GPU suite, the default bench line (PMC traffic + CPU baseline),
 # its rocprofv3 kernel stats, the other configurations' lines.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
