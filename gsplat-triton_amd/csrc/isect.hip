@@ -625,10 +625,15 @@ static int isect_write_sorted_impl(
              "isect_write_sorted: rank ids need the supertile expansion");
   // isect_ids / flatten_ids may both be null when rank_ids and offsets are
   // written (a caller that walks the ranks and never reads the ids: the
-  // training step) -- 12 of the 16 bytes per isect not written
+  // training step) -- 12 of the 16 bytes per isect not written; isect_ids
+  // alone may be null when flatten_ids and offsets are (ABI 33: the 2DGS
+  // training step, whose rasterizer gathers by Gaussian id) -- 8 of 12.
+  // Both forms need the supertile expansion.
   GS_REQUIRE(n_isects <= 0 || (isect_ids && flatten_ids) ||
-                 (!isect_ids && !flatten_ids && rank_ids && offsets),
-             "isect_write_sorted: null isect_ids / flatten_ids need rank_ids and offsets");
+                 (!isect_ids && !flatten_ids && rank_ids && offsets) ||
+                 (!isect_ids && flatten_ids && offsets &&
+                  gsplat_hip_isect_ranked(n_cameras, tile_width, tile_height)),
+             "isect_write_sorted: null isect_ids need rank_ids or flatten_ids, and offsets");
   auto plain_offsets = [&]() -> int {  // offsets from the written ids (or all zero)
     if (!offsets) return 0;
     if (!isect_ids)  // nothing written (no isect or no visible Gaussian): all zero

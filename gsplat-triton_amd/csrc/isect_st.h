@@ -435,13 +435,15 @@ seg_write_kernel(Geo geo, const int64_t *__restrict__ cap, const int32_t *__rest
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   int32_t g[4] = {0, 0, 0, 0};
   uint32_t db[4] = {0u, 0u, 0u, 0u};
-  const bool ids = isect_ids != nullptr;  // else rank ids only (see isect_write_sorted)
-  if (ids) {
+  // isect_ids null: rank ids only, or flatten ids only (a rasterizer that
+  // gathers by Gaussian id and reads the offsets, not the 64-bit keys)
+  const bool ids = isect_ids != nullptr, fl = flatten_ids != nullptr;
+  if (fl) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int s = max(wp.s[e], 0);
       g[e] = Vs[s];
-      db[e] = dkeys[s];
+      if (ids || sg.virt) db[e] = dkeys[s];
     }
   }
   if (threadIdx.x < S * S) {  // the earlier segments of this supertile
@@ -476,10 +478,8 @@ seg_write_kernel(Geo geo, const int64_t *__restrict__ cap, const int32_t *__rest
       const int pos = cur[0] + x - c;
       const int64_t id = (int64_t)(int32_t)db[e];
       for (int k = 0; k < c; ++k) {
-        if (ids) {
-          isect_ids[pos + k] = id;
-          flatten_ids[pos + k] = g[e];
-        }
+        if (ids) isect_ids[pos + k] = id;
+        if (fl) flatten_ids[pos + k] = g[e];
         if (rank_ids) rank_ids[pos + k] = wp.s[e];
       }
       cur[0] += __shfl(x, 63, 64);
@@ -499,8 +499,8 @@ seg_write_kernel(Geo geo, const int64_t *__restrict__ cap, const int32_t *__rest
         if (ids) {
           const int tile = (sg.ty0 + t / S) * geo.tw + sg.tx0 + t % S;
           isect_ids[pos] = ((tkey0 | (int64_t)tile) << 32) | (int64_t)db[e];
-          flatten_ids[pos] = g[e];
         }
+        if (fl) flatten_ids[pos] = g[e];
         if (rank_ids) rank_ids[pos] = wp.s[e];
       }
       cur[t] += __popcll(bal);

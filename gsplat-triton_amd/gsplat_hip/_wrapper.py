@@ -510,7 +510,10 @@ class _IsectCount:
         caller that only walks the depth ranks, the training step; needs
         will_rank(capped=True)): isect_ids / flatten_ids are not written and
         come back None -- the rank ids and offsets are.  ranks=False: no depth
-        ranks (a rasterizer that gathers by Gaussian id, the 2DGS one).  Returns
+        ranks (a rasterizer that gathers by Gaussian id, the 2DGS one); with
+        ids=False too (the 2DGS training step, ABI 33) only flatten_ids and
+        the offsets are written, isect_ids comes back None (where the
+        supertile expansion runs; else both are written).  Returns
         (tiles_per_gauss, isect_ids, flatten_ids, counts)."""
         (means2d, radii, depths, camera_ids, C, N, G, tile_size, tile_width, tile_height,
          n_bit_tile, n_bit_cam, packed) = self.args
@@ -521,9 +524,11 @@ class _IsectCount:
                                             capacity, key_bits)), 8),
                          dtype=torch.uint8, device=dev)
         rk = self._rank_buffers(capacity, capped=True) if ranks else None
-        ids = ids or rk is None
+        flat_only = not ids and not ranks and G > 0 and self.will_rank(capped=True)
+        ids = ids or (rk is None and not flat_only)
         isect_ids = torch.empty(capacity, dtype=torch.int64, device=dev) if ids else None
-        flatten_ids = torch.empty(capacity, dtype=torch.int32, device=dev) if ids else None
+        flatten_ids = torch.empty(capacity, dtype=torch.int32, device=dev) \
+            if (ids or flat_only) else None
         counts = torch.empty(4, dtype=torch.int64, device=dev)  # written by the emission
         # the tile offsets too (as isect_offset_encode with _n_isects_device=counts)
         self.offsets = torch.empty((C, tile_height, tile_width), dtype=torch.int32, device=dev)

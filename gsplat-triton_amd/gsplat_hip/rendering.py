@@ -631,8 +631,10 @@ def rasterization_2dgs(
     # (the 2DGS rasterizer gathers its own arrays: no rank ids)
     counts = None
     if capped:
+        # the training step (_colors_only) reads the offsets and flatten ids
+        # only: no 64-bit isect ids (8 of 12 bytes per isect not written)
         tiles_per_gauss, isect_ids, flatten_ids, counts = pending_isects.finish_capped(
-            _isect_capacity, _isect_status, _isect_report, ranks=False)
+            _isect_capacity, _isect_status, _isect_report, ids=not _colors_only, ranks=False)
     else:
         tiles_per_gauss, isect_ids, flatten_ids = pending_isects.finish(sort=True, ranks=False)
     isect_offsets = pending_isects.offsets  # written with the sorted isects

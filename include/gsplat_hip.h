@@ -39,7 +39,9 @@ const char *gsplat_hip_last_error(void);
  *     rasterizer's last colour channel from a separate depths array
  *     (depths / v_depths of _pack_records, _fwd, _bwd);
  *     gsplat_hip_projection_2dgs_bwd_adam; v_normals may be NULL in the
- *     2DGS rasterizer's backward (output) and projection backward (input). */
+ *     2DGS rasterizer's backward (output) and projection backward (input);
+ *     isect_ids alone may be NULL in the sorted emission (flatten_ids and
+ *     offsets written: a rasterizer that gathers by id). */
 int gsplat_hip_abi_version(void);
 
 /* ---------------------------------------------------------------------------

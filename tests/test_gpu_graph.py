@@ -77,6 +77,33 @@ def test_capped_isect_matches_synchronous():
     assert torch.equal(m2["isect_ids"], m0["isect_ids"])
 
 
+def test_capped_isect_flatten_only_2dgs():
+    """The 2DGS training step's capped isect (ABI 33: `_colors_only`, no
+    64-bit isect ids): the flatten ids and offsets written equal the
+    synchronous emission's, isect_ids comes back None, and the render is the
+    same (the colours-only render of the same per-tile lists)."""
+    import gsplat_hip
+    ins, W, H = _scene(N=20000)
+    vm, K = ins[5], ins[6]
+    out0 = gsplat_hip.rasterization_2dgs(*ins[:5], vm, K, W, H, sh_degree=3,
+                                         render_mode="RGB+D", _colors_only=True)
+    m0 = out0[-1]
+    n = m0["flatten_ids"].numel()
+    status = torch.zeros(1, dtype=torch.int32, device=DEV)
+    out1 = gsplat_hip.rasterization_2dgs(*ins[:5], vm, K, W, H, sh_degree=3,
+                                         render_mode="RGB+D", _colors_only=True,
+                                         _isect_capacity=n + 777, _isect_status=status)
+    m1 = out1[-1]
+    counts = m1["isect_counts"].tolist()
+    assert counts[0] == n and counts[2] == 0 and int(status) == 0
+    from gsplat_hip import _lib
+    if _lib.query("gsplat_hip_isect_ranked", 1, m0["tile_width"], m0["tile_height"]):
+        assert m1["isect_ids"] is None
+    assert torch.equal(m1["flatten_ids"][:n], m0["flatten_ids"])
+    assert torch.equal(m1["isect_offsets"], m0["isect_offsets"])
+    assert torch.equal(out1[0], out0[0]) and torch.equal(out1[1], out0[1])
+
+
 def test_capped_isect_overflow_writes_nothing():
     ins, W, H = _scene(N=8000)
     _, _, m0, _ = _render(ins, W, H)
