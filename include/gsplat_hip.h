@@ -210,7 +210,11 @@ int gsplat_hip_isect_write_sorted_capped(
  * i32[n_isects] = the depth rank of each isect's Gaussian among the visible
  * Gaussians (flatten_ids[i] is the Gaussian itself), vis_rank i32[G] = that
  * rank for every Gaussian with tiles_per_gauss > 0 (other entries untouched):
- * the render records and gradient rows can then be indexed by rank. */
+ * the render records and gradient rows can then be indexed by rank.
+ * When the supertile expansion runs, isect_ids and flatten_ids may both be
+ * NULL (rank_ids and offsets set: a rasterizer that walks ranks), or
+ * isect_ids alone (ABI 33; flatten_ids and offsets set: one that gathers by
+ * Gaussian id and reads the offsets, not the 64-bit keys). */
 int gsplat_hip_isect_ranked(int n_cameras, int tile_width, int tile_height);
 /* Sorted emission, tile-first (the default of isect_tiles(sort=True)): the
  * SAME isect_ids / flatten_ids again, from Gaussian-major emission with
