@@ -83,6 +83,19 @@ def parse():
                          "its camera, the other ranks' exchanged rows from stand-ins "
                          "recorded from their own renders (exchanges as device copies, no "
                          "xGMI time; measurement only)")
+    ap.add_argument("--no-dp-phase", action="store_true",
+                    help="at N>1: skip the second timed region that runs the replicated "
+                         "per-camera data-parallel scheme (north_star's) after the default "
+                         "Gaussian-sharded one (config.dp)")
+    ap.add_argument("--dp-phase", action="store_true",
+                    help="run that data-parallel phase at N=1 too (a 1-rank RCCL group with "
+                         "the collectives issued: the N>1 code path on one GPU)")
+    ap.add_argument("--watchdog-s", type=float,
+                    default=float(os.environ.get("GSPLAT_HIP_WATCHDOG_S", "120")),
+                    help="end the job (status 3, rank / step / phase on stderr) when a rank "
+                         "makes no progress for this long; also the process group's "
+                         "collective timeout (0: off)")
+    ap.add_argument("--debug-hang", default="", metavar="RANK:STEP", help=argparse.SUPPRESS)
     ap.add_argument("--probe", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
 
@@ -252,15 +265,23 @@ def main():
         assert world == 1 and not dp_path and emu_world > 1, \
             "--gshard-emulate W: a one-GPU measurement, W > 1"
         gshard = True
+    # every eager collective bounded (RCCL's watchdog ends the process on a
+    # timeout); captured ones are covered by the progress watchdog below
+    import datetime
+    pg_kw = {}
+    if args.watchdog_s > 0:
+        pg_kw["timeout"] = datetime.timedelta(seconds=args.watchdog_s)
+    dp_phase = (world > 1 and not dp_path and not args.no_dp_phase) or (
+        args.dp_phase and world == 1 and not dp_path and not emu_world and not args.probe)
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    elif args.dp_path:  # a 1-rank RCCL group: the N>1 code path on one GPU
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local), **pg_kw)
+    elif args.dp_path or dp_phase:  # a 1-rank RCCL group: the N>1 code path on one GPU
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", str(_free_port()))
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", rank=0, world_size=1,
-                                device_id=torch.device("cuda", local))
+                                device_id=torch.device("cuda", local), **pg_kw)
     traffic = None
     if rank == 0 and world == 1 and not args.no_traffic and not args.probe:
         traffic = pmc_traffic(args.config)  # child processes, before this one uses the GPU
@@ -302,8 +323,29 @@ def main():
                  graph=not (args.eager or args.probe
                             or (args.config in DENSIFY and not args.graph)), **kw)
     N = means.shape[0]
+    # progress watchdog: a rank that stops making progress (a collective a
+    # peer never joins, captured or eager) ends the job with its rank, step
+    # and phase on stderr and status 3 -- never a silent hang
+    from gsplat_hip.distributed import Watchdog
+    wd = Watchdog(args.watchdog_s, f"bench.py rank {rank}/{world}") \
+        if args.watchdog_s > 0 and not args.probe else None
+    hang = tuple(int(x) for x in args.debug_hang.split(":")) if args.debug_hang else None
 
+    def beat(phase, it, trainer):
+        if wd is not None:
+            g = getattr(trainer, "_graph", None)
+            mode = ("eager" if g is None else "capture pending" if g.graph is None
+                    else f"replay (captures {g.recaptures}, replays {g.replays})")
+            wd.beat(f"rank {rank} {phase} step {it}: {mode}")
+        if hang is not None and hang == (rank, it):  # debug: this rank never joins step it
+            print(f"bench.py: rank {rank} skips step {it} (--debug-hang)", file=sys.stderr,
+                  flush=True)
+            time.sleep(1e6)
+
+    if wd is not None:
+        wd.arm(f"rank {rank} trainer built")
     for it in range(start, start + args.warmup):
+        beat("warmup", it, tr)
         tr.step(it)
     torch.cuda.synchronize()
     if args.probe:  # PMC child run: a few steps, no output
@@ -318,7 +360,9 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for it in range(start + args.warmup, start + args.warmup + args.steps):
+        beat("timed", it, tr)
         tr.step(it)
+    beat("timed sync", start + args.warmup + args.steps, tr)
     tr.sync()  # graph replays: every step's overflow check settled inside the timed region
     torch.cuda.synchronize()
     if world > 1:
@@ -326,21 +370,18 @@ def main():
     elapsed = max_over_ranks(time.perf_counter() - t0, world, dev)
     # (after the timed region: a failed capture falls back to eager steps)
     graphed = getattr(tr, "_graph", None) is not None
+    graph_info = None
     if graphed:
         # kernel durations: a graph replay runs the same kernels as an eager
         # step, but HIP events cannot be recorded per replay -- time the
         # rasterizer launches over eager steps right after the timed region
-        g = tr._graph
-        graph_info = {"replays": g.replays, "captures": g.recaptures,
-                      "capture_ms": [round(1e3 * x, 1) for x in g.capture_s],
-                      "isect_capacity": g.capacity, "max_isects": g.max_isects,
-                      "host_issue_ms_per_step": 1e3 * g.host_s / max(g.replays, 1)}
-        g = None
+        graph_info = _graph_info(tr._graph)
         tr.release_graph()  # (RCCL: before destroy_process_group, GraphStep.release)
         timers = _wrapper.enable_kernel_timers(True)
         n_t = min(args.steps, 10)
         for it in range(start + args.warmup + args.steps,
                         start + args.warmup + args.steps + n_t):
+            beat("kernel timing", it, tr)
             tr.step(it)
         torch.cuda.synchronize()
     _wrapper.enable_kernel_timers(False)
@@ -376,6 +417,7 @@ def main():
     last_slot = 12 if two else 9
     byts, byts_bwd, isects, n_effs = [], [], [], []
     for it in range(start + args.warmup, start + args.warmup + min(args.steps, len(vm_pool))):
+        beat("roofline bytes", it, tr)
         ci = tr.camera_index(it)
         colors, alphas, meta = tr.render(ci)
         # last_ids are internal to the autograd node (the forward's saved
@@ -505,22 +547,107 @@ def main():
                                  "(per-GPU workload is the same at every N)"},
         "model": model,
     }
+    if dp_path:  # the main region IS the replicated data-parallel scheme
+        result["config"]["dp"] = {"phase": "main", "value": result["value"],
+                                  "ms_per_step": result["ms_per_step"],
+                                  "step_issue": result["config"]["step_issue"]}
     if rank == 0 and not args.no_cpu_baseline:
         # after the timed region; the other ranks wait at the barrier below
+        if wd is not None:
+            wd.disarm()  # host-only work of bounded length (tens of seconds)
         try:
             result["cpu_baseline"] = cpu_baseline(tr, args.cpu_tile_stride, cpu_pool)
         finally:
             cpu_pool.close()
+        if wd is not None:
+            wd.arm(f"rank {rank} cpu baseline done")
+    if dp_phase:
+        # north_star's own multi-GPU scheme, timed in the same job after the
+        # main (Gaussian-sharded) region: replicated Gaussians, per-camera
+        # data parallelism, gradients reduce-scattered and rows all-gathered
+        # over RCCL (distributed.ShardedAdam).  A failure is recorded here
+        # without losing the main value; a hang ends the job through the
+        # watchdog, which then still delivers the main line (dp: "hung")
+        if wd is not None:
+            hung = dict(result, config=dict(result["config"], dp={
+                "error": f"hung: no progress for {args.watchdog_s:.0f} s (watchdog)"}))
+            wd.fallback(json_fd if rank == 0 else 2,
+                        json.dumps(hung) + "\n" if rank == 0 else "", 0)
+        tr.release_graph()
+        del tr
+        import gc
+        gc.collect()
+        torch.cuda.empty_cache()
+        try:
+            result["config"]["dp"] = dp_region(args, means, rgbs, vm_pool, K_pool, W, H, dev, world,
+                                               rank, start, kw, beat)
+        except Exception as e:  # noqa: BLE001 -- recorded, the main value stands
+            import traceback
+            traceback.print_exc()
+            result["config"]["dp"] = {"error": repr(e)[:400]}
+        if wd is not None:
+            wd.fallback(-1, None)
+        tr = None
     if rank == 0:
         os.write(json_fd, (json.dumps(result) + "\n").encode())
     if world > 1:
         dist.barrier()
+    if wd is not None:
+        wd.disarm()
     if dist.is_initialized():
-        tr.release_graph()
+        if tr is not None:
+            tr.release_graph()
         import gc
         gc.collect()  # graphs that captured RCCL collectives, before the group goes
         torch.cuda.synchronize()
         dist.destroy_process_group()
+
+
+def _graph_info(g):
+    return {"replays": g.replays, "captures": g.recaptures,
+            "capture_ms": [round(1e3 * x, 1) for x in g.capture_s],
+            "isect_capacity": g.capacity, "max_isects": g.max_isects,
+            "host_issue_ms_per_step": 1e3 * g.host_s / max(g.replays, 1)}
+
+
+def dp_region(args, means, rgbs, vm_pool, K_pool, W, H, dev, world, rank, start, kw, beat):
+    """The replicated per-camera data-parallel step (Trainer(sharded_optimizer=
+    True), graph-replayed with its RCCL collectives inside), timed like the
+    main region: barrier + synchronize on both sides, max over ranks."""
+    from gsplat_hip.train_step import Trainer
+    if world == 1:
+        os.environ["GSPLAT_HIP_DP_SOLO"] = "0"  # the collectives on the 1-rank group
+    tr = Trainer(means, rgbs, vm_pool, K_pool, W, H, sh_degree=3, device=dev, world_size=world,
+                 rank=rank, sharded_optimizer=True, gaussian_shard=False,
+                 graph=not args.eager, **kw)
+    try:
+        for it in range(start, start + args.warmup):
+            beat("dp warmup", it, tr)
+            tr.step(it)
+        torch.cuda.synchronize()
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for it in range(start + args.warmup, start + args.warmup + args.steps):
+            beat("dp timed", it, tr)
+            tr.step(it)
+        beat("dp timed sync", start + args.warmup + args.steps, tr)
+        tr.sync()
+        torch.cuda.synchronize()
+        dist.barrier()
+        elapsed = max_over_ranks(time.perf_counter() - t0, world, dev)
+        g = getattr(tr, "_graph", None)
+        issue = (f"HIP graph replay with the RCCL reduce-scatters / all-gathers inside "
+                 f"({_graph_info(g)})" if g is not None else "eager launches" + (
+                     f" (graph capture failed: {tr.graph_fallback})" if tr.graph_fallback else ""))
+        return {"phase": "second timed region (after the main one)", "value": world * args.steps / elapsed,
+                "unit": "images/s", "ms_per_step": 1e3 * elapsed / args.steps,
+                "steps": args.steps, "warmup": args.warmup, "step_issue": issue,
+                "parallelism": f"dp{world}: every rank holds all Gaussians and renders its own "
+                               "camera; gradients reduce-scattered, Adam on the rank's rows, rows "
+                               "all-gathered over RCCL (sharded optimizer)"}
+    finally:
+        tr.release_graph()
 
 
 def host_threads() -> int:

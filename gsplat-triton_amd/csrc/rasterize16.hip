@@ -1229,6 +1229,10 @@ __attribute__((amdgpu_waves_per_eu(BwdOcc<PX>::W))) bwd2_kernel(Args a) {
           grad_seq(q, v1[q], ar[q].y <= kAlphaMax, al.y, ra.y, gD.y, w1, Da1);
           grad_seq(q, v0[q], ar[q].x <= kAlphaMax, al.x, ra.x, gD.x, w0, Da0);
           const f2v wt = f2v{w0, w1}, Da = f2v{Da0, Da1};
+          if (a.dbg & 8) {  // timing attribution only: no gradient algebra
+            v[0] += wt + Da;
+            continue;
+          }
           const f2v aD = al * Da;
 #pragma unroll
           for (int d = 0; d < D; ++d)
@@ -1250,8 +1254,18 @@ __attribute__((amdgpu_waves_per_eu(BwdOcc<PX>::W))) bwd2_kernel(Args a) {
 #pragma unroll
         for (int qq = 0; qq < NV; ++qq) {
           constexpr int NQ = F - 16 * (NV - 1);
-          const f2v tot = qq < NV - 1 ? reduce_scatter2<16>(v + 16 * qq, lane)
-                                      : reduce_scatter2<NQ>(v + 16 * qq, lane);
+          // (GSPLAT_HIP_DBG bit 2, timing attribution only: no cross-lane
+          // reduction, each lane's own partial of its field)
+          f2v tot;
+          if (a.dbg & 4) {
+            tot = v[16 * qq];
+#pragma unroll
+            for (int i = 1; i < 16; ++i)
+              if (16 * qq + i < NV * 16 && lf == i) tot = v[16 * qq + i];
+          } else {
+            tot = qq < NV - 1 ? reduce_scatter2<16>(v + 16 * qq, lane)
+                              : reduce_scatter2<NQ>(v + 16 * qq, lane);
+          }
           const int field = 16 * qq + lf;
           if ((lane & 3) == 0 && lf < (qq < NV - 1 ? 16 : NQ) && !(a.dbg & 1)) {
             const float sc = field_scale(field);
@@ -1736,6 +1750,11 @@ static int32_t *stat_dev() {
 // wrong guess costs speed only: an unsplit heavy tile, or the split-capable
 // kernel's lower occupancy with nothing to split.  A captured step keeps the
 // choice of its capture.
+// The trainer takes the decision out of this heuristic: from its first
+// render it sets a fixed threshold (always the split-capable forward) or 0
+// (never) with gsplat_hip_set_fwd_split_threshold (Trainer._tune_split), so
+// every render of a run -- eager or captured -- takes the same variant with
+// the same threshold.
 static bool use_split_now(int n_tiles, int64_t n_isects) {
   if (!split_capable(n_tiles, n_isects)) return false;
   if (fwd_split_mode() > 0) return true;
@@ -2068,9 +2087,14 @@ int rasterize16_bwd(int C, int64_t G, int D, int W, int H, int tw, int th,
   a.render_alphas = const_cast<float *>(render_alphas);
   a.last_ids = const_cast<int32_t *>(last_ids);
   a.v_render_colors = v_render_colors; a.v_render_alphas = v_render_alphas;
-  const int64_t need = rasterize16_fwd_state_bytes(D, a.n_tiles, n_isects);
+  // the backward reads the chunk slots only (the head of the state): the
+  // tile-order and split areas after them depend on the forward's split
+  // settings (a caller's gsplat_hip_set_fwd_split_threshold around the
+  // forward alone, Trainer._tune_split), which must not turn the chunked
+  // backward off
+  const int64_t need = chunk_slot_bytes(D, n_isects);
   a.L = chunk_len();
-  a.state = (state && chunk_slot_bytes(D, n_isects) > 0 && state_bytes >= need)
+  a.state = (state && need > 0 && state_bytes >= need)
                 ? const_cast<float *>(reinterpret_cast<const float *>(state)) : nullptr;
   a.render_colors_in = render_colors;
   a.dbg = dbg_flags();
@@ -2092,6 +2116,16 @@ extern "C" int gsplat_hip_set_fwd_split_div(int div) {
   const int old = gs::split_div();
   gs::g_split_div = div > 0 ? div : 0;
   return old;
+}
+
+extern "C" int gsplat_hip_set_fwd_split_threshold(int isects) {
+  const int old = gs::fwd_split_mode();
+  gs::g_fwd_split = isects < 0 ? -1 : isects;
+  return old;
+}
+
+extern "C" int64_t gsplat_hip_fwd_split_threshold(int64_t n_isects) {
+  return gs::fwd_split_mode() == 0 ? -1 : gs::split_threshold(n_isects);
 }
 
 extern "C" int gsplat_hip_debug_set_fwd_split(int isects) {

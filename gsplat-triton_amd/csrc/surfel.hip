@@ -888,37 +888,46 @@ __global__ void __launch_bounds__(128) fwd2_kernel(RasterArgs a) {
 // Dispatch order (GSPLAT_HIP_SURFEL_ORDER=1): the tiles bucketed by
 // floor(log2(isects)), heaviest bucket first, so the longest tiles start in
 // the first wave of workgroups instead of finishing last (order inside a
-// bucket: arrival at an LDS counter).  One workgroup.
+// bucket: arrival at an LDS counter).  One workgroup; any tile count: the
+// tiles are taken in blocks of 16384 (16 per thread), and with more than one
+// block each pass reloads its block's keys.
 __global__ void __launch_bounds__(1024)
 tile_order_kernel(int n_tiles, const int32_t *__restrict__ offsets, int64_t n_isects,
                   const int64_t *__restrict__ n_dev, int32_t *__restrict__ order) {
-  constexpr int MAXR = 16;  // tiles per thread (n_tiles <= 16384)
+  constexpr int MAXR = 16;  // tiles per thread and block
+  constexpr int BLK = 1024 * MAXR;
   __shared__ int hist[34];
   const int tid = threadIdx.x, lane = tid & 63;
   if (tid < 34) hist[tid] = 0;
   const int64_t total = n_dev ? n_dev[0] : n_isects;
-  // every tile's two offsets loaded up front (one load latency, not one per
-  // round), the keys kept in registers for both passes
+  const int n_blk = (n_tiles + BLK - 1) / BLK;
+  // a block's offsets loaded up front (one load latency, not one per round),
+  // its keys kept in registers (for both passes when there is one block)
   int k[MAXR];
+  auto load_keys = [&](int b0) {
 #pragma unroll
-  for (int rd = 0; rd < MAXR; ++rd) {
-    const int t = tid + 1024 * rd;
-    int64_t n = -1;
-    if (t < n_tiles) n = (t == n_tiles - 1 ? total : (int64_t)offsets[t + 1]) - offsets[t];
-    // 2^31.. -> 1, 1 -> 32, empty -> 33, no tile -> -1
-    k[rd] = n < 0 ? -1 : (n > 0 ? 32 - (63 - __builtin_clzll((uint64_t)n)) : 33);
-  }
+    for (int rd = 0; rd < MAXR; ++rd) {
+      const int t = b0 + tid + 1024 * rd;
+      int64_t n = -1;
+      if (t < n_tiles) n = (t == n_tiles - 1 ? total : (int64_t)offsets[t + 1]) - offsets[t];
+      // 2^31.. -> 1, 1 -> 32, empty -> 33, no tile -> -1
+      k[rd] = n < 0 ? -1 : (n > 0 ? 32 - (63 - __builtin_clzll((uint64_t)n)) : 33);
+    }
+  };
   __syncthreads();
   // per wave and distinct key one LDS atomic (a few keys per wave: M5's
   // tiles fall into 2-3 buckets, and 64 lanes on one counter serialised)
+  for (int b = 0; b < n_blk; ++b) {
+    load_keys(b * BLK);
 #pragma unroll
-  for (int rd = 0; rd < MAXR; ++rd) {
-    uint64_t todo = __ballot(k[rd] >= 0);
-    while (todo) {
-      const int kk = __builtin_amdgcn_readlane(k[rd], __builtin_ctzll(todo));
-      const uint64_t m = __ballot(k[rd] == kk) & todo;
-      if (lane == __builtin_ctzll(m)) atomicAdd(&hist[kk], __popcll(m));
-      todo &= ~m;
+    for (int rd = 0; rd < MAXR; ++rd) {
+      uint64_t todo = __ballot(k[rd] >= 0);
+      while (todo) {
+        const int kk = __builtin_amdgcn_readlane(k[rd], __builtin_ctzll(todo));
+        const uint64_t m = __ballot(k[rd] == kk) & todo;
+        if (lane == __builtin_ctzll(m)) atomicAdd(&hist[kk], __popcll(m));
+        todo &= ~m;
+      }
     }
   }
   __syncthreads();
@@ -931,19 +940,22 @@ tile_order_kernel(int n_tiles, const int32_t *__restrict__ offsets, int64_t n_is
     }
   }
   __syncthreads();
+  for (int b = 0; b < n_blk; ++b) {
+    if (n_blk > 1) load_keys(b * BLK);
 #pragma unroll
-  for (int rd = 0; rd < MAXR; ++rd) {
-    const int t = tid + 1024 * rd;
-    uint64_t todo = __ballot(k[rd] >= 0);
-    while (todo) {
-      const int kk = __builtin_amdgcn_readlane(k[rd], __builtin_ctzll(todo));
-      const uint64_t m = __ballot(k[rd] == kk) & todo;
-      const int leader = __builtin_ctzll(m);
-      int base = 0;
-      if (lane == leader) base = atomicAdd(&hist[kk], __popcll(m));
-      base = __shfl(base, leader, 64);
-      if (k[rd] == kk) order[base + __popcll(m & ((1ull << lane) - 1))] = t;
-      todo &= ~m;
+    for (int rd = 0; rd < MAXR; ++rd) {
+      const int t = b * BLK + tid + 1024 * rd;
+      uint64_t todo = __ballot(k[rd] >= 0);
+      while (todo) {
+        const int kk = __builtin_amdgcn_readlane(k[rd], __builtin_ctzll(todo));
+        const uint64_t m = __ballot(k[rd] == kk) & todo;
+        const int leader = __builtin_ctzll(m);
+        int base = 0;
+        if (lane == leader) base = atomicAdd(&hist[kk], __popcll(m));
+        base = __shfl(base, leader, 64);
+        if (k[rd] == kk) order[base + __popcll(m & ((1ull << lane) - 1))] = t;
+        todo &= ~m;
+      }
     }
   }
 }
@@ -1985,7 +1997,7 @@ extern "C" int gsplat_hip_rasterize_2dgs_fwd(
   a.render_median = render_median; a.last_ids = last_ids; a.median_ids = median_ids;
   const int waves = (tile_size * tile_size + 63) / 64;
   hipStream_t st = (hipStream_t)stream;
-  if (tile_order && n_tiles > 0 && n_tiles <= 16384) {  // written here, read by this launch and the backward
+  if (tile_order && n_tiles > 0) {  // written here, read by this launch and the backward
     hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(1024), 0, st, n_tiles, isect_offsets,
                        n_isects, n_isects_device, tile_order);
     a.order = tile_order;
@@ -2074,9 +2086,12 @@ extern "C" int gsplat_hip_rasterize_2dgs_bwd(
   const int absgrad = v_means2d_abs != nullptr;
   // LEAN kernels (bwd2_kernel): 16x16 tiles, D <= 4, no normal / distortion /
   // median gradient (GSPLAT_HIP_SURFEL_LEAN=0: the general kernel)
-  const bool px2 = tile_size == 16 && bwd2_enabled();
-  const bool lean = px2 && D <= 4 && lean_enabled() && !v_render_normals && !v_render_distort &&
-                    !v_render_median;
+  // a colours-only forward (no median ids) has only the LEAN backward: it
+  // is taken whatever GSPLAT_HIP_SURFEL_LEAN / GSPLAT_HIP_BWD_PX say
+  const bool colors_only = !median_ids;
+  const bool px2 = tile_size == 16 && (bwd2_enabled() || colors_only);
+  const bool lean = px2 && D <= 4 && (lean_enabled() || colors_only) && !v_render_normals &&
+                    !v_render_distort && !v_render_median;
   const int S = lean ? lean_stride(D, absgrad) : fields_stride(D, absgrad);
   const int64_t G = n_gaussians;
   GS_REQUIRE(workspace_bytes >= G * S * (int64_t)sizeof(float),

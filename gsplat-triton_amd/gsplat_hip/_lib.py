@@ -12,7 +12,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GSPLAT_HIP_LIB", os.path.join(_HERE, "libgsplat_hip.so"))
-ABI_VERSION = 33
+ABI_VERSION = 34
 
 _p = ctypes.c_void_p
 _i32 = ctypes.c_int
@@ -84,6 +84,8 @@ _SIGS = {
     "gsplat_hip_debug_set_flags": (_i32, [_i32]),
     "gsplat_hip_debug_set_fwd_split": (_i32, [_i32]),
     "gsplat_hip_set_fwd_split_div": (_i32, [_i32]),
+    "gsplat_hip_set_fwd_split_threshold": (_i32, [_i32]),
+    "gsplat_hip_fwd_split_threshold": (_i64, [_i64]),
     "gsplat_hip_ssim_workspace_bytes": (_i64, [_i32, _i32, _i32, _i32]),
     "gsplat_hip_ssim_l1_fwd": (_i32, [_i32, _i32, _i32, _i32, _p, _p, _p, _p, _p]),
     "gsplat_hip_ssim_l1_bwd": (_i32, [_i32, _i32, _i32, _i32, _p, _p, _p, _p, _p, _p]),
@@ -159,6 +161,10 @@ _SIGS = {
                                                      _p, _p, _p, _p, _p]),
     "gsplat_hip_depth_to_normal": (_i32, [_i32, _i32, _i32, _p, _i64, _p, _p, _i32, _p, _p]),
     "gsplat_hip_rotate3": (_i32, [_i32, _i64, _p, _p, _p, _p]),
+    "gsplat_hip_watchdog_arm": (_i32, [ctypes.c_double, ctypes.c_char_p, _i32]),
+    "gsplat_hip_watchdog_beat": (_i32, [ctypes.c_char_p]),
+    "gsplat_hip_watchdog_set_fallback": (_i32, [_i32, ctypes.c_char_p, _i32]),
+    "gsplat_hip_watchdog_disarm": (_i32, []),
 }
 
 EXPORTED = tuple(_SIGS)

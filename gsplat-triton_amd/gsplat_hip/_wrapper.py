@@ -1054,19 +1054,39 @@ def rasterize_to_pixels(
 
 
 @contextlib.contextmanager
-def fwd_split_div(div: Optional[int]):
+def fwd_split(div: Optional[int], threshold: Optional[int] = None):
     """The split forward's threshold divisor (gsplat_hip_set_fwd_split_div)
-    for the renders queued inside the block only; the previous value is
-    restored after it, so a trainer's choice does not leak into other
-    rasterization() calls of the process.  None / 0: leave it alone."""
-    if not div:
-        yield
-        return
-    old = int(_lib.query("gsplat_hip_set_fwd_split_div", int(div)))
+    and fixed threshold (gsplat_hip_set_fwd_split_threshold: > 0 always the
+    split-capable variant with that threshold, 0 never split) for the renders
+    queued inside the block only; the previous values are restored after it,
+    so a trainer's choice does not leak into other rasterization() calls of
+    the process.  None: leave that one alone (div 0 as well)."""
+    old_div = int(_lib.query("gsplat_hip_set_fwd_split_div", int(div))) if div else None
+    old_thr = (int(_lib.query("gsplat_hip_set_fwd_split_threshold", int(threshold)))
+               if threshold is not None else None)
     try:
         yield
     finally:
-        _lib.query("gsplat_hip_set_fwd_split_div", old)
+        if old_thr is not None:
+            _lib.query("gsplat_hip_set_fwd_split_threshold", old_thr)
+        if old_div is not None:
+            _lib.query("gsplat_hip_set_fwd_split_div", old_div)
+
+
+def max_tile_isects(meta: dict) -> int:
+    """The largest tile's isect count of a render (its meta's offsets and ids)."""
+    offs = meta["isect_offsets"].flatten().long()
+    n = int(meta["isect_counts"][0]) if "isect_counts" in meta else meta["flatten_ids"].numel()
+    if n <= 0 or offs.numel() == 0:
+        return 0
+    ends = torch.cat([offs[1:], torch.tensor([n], device=offs.device)])
+    return int((ends - offs).max())
+
+
+def fwd_split_threshold(n_isects: int) -> int:
+    """gsplat_hip_fwd_split_threshold: isects above which a tile splits with
+    the divisor in effect (-1: splitting off)."""
+    return int(_lib.query("gsplat_hip_fwd_split_threshold", int(n_isects)))
 
 
 @torch.no_grad()

@@ -12,6 +12,7 @@ one GPU) explicit per-peer P2P transfers (`batch_isend_irecv`).  The backward
 of an exchange is the exchange with input and output splits swapped.
 """
 
+import contextlib
 import math
 import os
 from contextlib import nullcontext as _nullcontext
@@ -21,6 +22,86 @@ import torch
 import torch.distributed as dist
 import torch.distributed.nn.functional as distF
 from torch import Tensor
+
+
+# ---- the process group of captured collectives ----------------------------
+# While a HIP graph captures a training step (graph_step.GraphStep), its
+# collectives run on a communicator that never issues eager work: RCCL's
+# watchdog thread queries the end events of the eager collectives it still
+# tracks, and a query of an event recorded on a stream that a capture has
+# pulled in (the communicator's own stream, once a captured collective runs
+# on it) is illegal -- a test process aborted that way.  Collectives issued
+# during a capture are never tracked (torch does not enqueue them), so a
+# group used ONLY inside captures gives the watchdog nothing to query there,
+# by construction.  None: the default group.
+_CAPTURE_PG = None
+
+
+@contextlib.contextmanager
+def capture_group(pg):
+    """Route this module's collectives (the pair exchange, ShardedAdam while
+    capturing) to `pg` inside the block."""
+    global _CAPTURE_PG
+    old, _CAPTURE_PG = _CAPTURE_PG, pg
+    try:
+        yield
+    finally:
+        _CAPTURE_PG = old
+
+
+def current_capture_group():
+    return _CAPTURE_PG
+
+
+def new_capture_group():
+    """A process group over every rank for captured collectives only (see
+    _CAPTURE_PG).  Its communicator must exist before the capture without an
+    eager collective on it: that needs the default group bound to a device
+    (init_process_group(device_id=...)), which makes new_group connect
+    eagerly.  Collective over the ranks (every rank creates its trainer's
+    GraphStep in the same order)."""
+    if dist.get_backend() == "nccl" and getattr(dist.distributed_c10d._get_default_group(),
+                                                "bound_device_id", None) is None:
+        raise RuntimeError("captured RCCL collectives need init_process_group(device_id=...) "
+                           "(an eagerly connected communicator for the capture group)")
+    return dist.new_group(list(range(dist.get_world_size())))
+
+
+# ---- progress watchdog -------------------------------------------------------
+class Watchdog:
+    """gsplat_hip_watchdog_* (csrc/watchdog.cpp): a native thread that ends
+    the process when no progress is reported within `timeout_s` -- printing
+    the last reported state (rank, step, phase, capture / replay) to stderr
+    and exiting with `exit_code` -- so that a collective one rank never joins
+    ends a multi-GPU job with a diagnosis, not a silent hang (a collective
+    replayed inside a HIP graph is invisible to RCCL's own timeout, and a
+    host thread blocked in a HIP wait never returns to Python)."""
+
+    def __init__(self, timeout_s: float, tag: str, exit_code: int = 3):
+        from . import _lib
+        self._lib = _lib
+        self.timeout_s, self.tag, self.exit_code = float(timeout_s), tag, int(exit_code)
+        self.armed = False
+
+    def arm(self, state: str = "armed"):
+        self._lib.call("gsplat_hip_watchdog_arm", self.timeout_s, self.tag.encode(),
+                       self.exit_code)
+        self.armed = True
+        self.beat(state)
+
+    def beat(self, state: str):
+        if self.armed:
+            self._lib.call("gsplat_hip_watchdog_beat", state.encode(errors="replace"))
+
+    def fallback(self, fd: int, text: Optional[str], exit_code: int = 0):
+        """On expiry also write `text` to `fd` and exit with `exit_code`."""
+        self._lib.call("gsplat_hip_watchdog_set_fallback", int(fd) if text is not None else -1,
+                       (text or "").encode(), int(exit_code))
+
+    def disarm(self):
+        if self.armed:
+            self._lib.call("gsplat_hip_watchdog_disarm")
+            self.armed = False
 
 
 def all_gather_int32(world_size: int, value: Union[int, Tensor],
@@ -171,7 +252,7 @@ def _all_to_all_rows(data: Tensor, splits: List[int], out_splits: List[int],
     if data.is_cuda and dist.get_backend() == "nccl":
         out = data.new_empty((sum(out_splits),) + data.shape[1:])
         dist.all_to_all_single(out, data, output_split_sizes=out_splits,
-                               input_split_sizes=splits)
+                               input_split_sizes=splits, group=_CAPTURE_PG)
         return out
     send = list(data.split(splits, dim=0))
     recv = [data.new_empty((n,) + data.shape[1:]) for n in out_splits]
@@ -424,7 +505,9 @@ class ShardedAdam:
     def _issue_reduce(self, gi, grads):
         """Reduce-scatter (main rows) and all-reduce (remainder rows) of group
         gi's gradients on its process group, issued from the current stream."""
-        pg = None if self.capturing else self.group_pgs[gi]
+        # capturing: in order on the capturing stream, on the capture-only
+        # group (graph_step; the default group during the capture's warm-up)
+        pg = _CAPTURE_PG if self.capturing else self.group_pgs[gi]
         flats, works = {}, []
         for i in sorted(self.groups[gi], key=lambda i: -self.params[i].numel()):
             g = grads.get(i)
@@ -514,7 +597,7 @@ class ShardedAdam:
                         mine = self._shard(i, full)
                         self._pending[i] = dist.all_gather_into_tensor(
                             full, mine if full.is_cuda else mine.clone(),
-                            group=None if self.capturing else self.group_pgs[gi],
+                            group=_CAPTURE_PG if self.capturing else self.group_pgs[gi],
                             async_op=True)
         if not defer_gather:
             self.wait()

@@ -211,6 +211,13 @@ class GraphStep:
         from . import distributed as gdist
         self.vote = ((self.gshard or self.dp) and gdist.EMULATION is None
                      and dist.is_available() and dist.is_initialized())
+        # the captured collectives' own communicator: never any eager work on
+        # it (distributed._CAPTURE_PG); None where the step has no collective
+        # (a one-rank data-parallel step with the collectives skipped still
+        # votes, on a one-rank group)
+        self.cap_pg = None
+        if self.vote and dist.get_backend() == "nccl":
+            self.cap_pg = gdist.new_capture_group()
         self.blk = torch.zeros(self.SLOT, dtype=torch.uint8, device=dev)
         self.scal = self.blk[:256].view(torch.float32)
         self.cam = self.blk[256:264].view(torch.int64)
@@ -247,6 +254,9 @@ class GraphStep:
         self.replays = 0
         self.max_isects = 0
         self.host_s = 0.0
+        # set when a recovery's re-capture failed (its voided steps were then
+        # re-run eagerly): Trainer.step issues every later step eagerly
+        self.failed = None
 
     # ------------------------------------------------------------------ body
     def _layout(self):
@@ -275,9 +285,10 @@ class GraphStep:
                 hyper=self.scal[sh_off:sh_off + 3], skip=self.status)
         ga = None
         if getattr(tr, "geom_in_proj", False):
-            # the geometry groups' factors are the launch groups' (_fill):
-            # (ss, ib) of means, scales, quats, opacities at [0, 8)
-            assert [names[i] for i in idx] == list(tr.GEOM), (idx, names)
+            # the geometry groups' factors are the first launch groups' (_fill):
+            # (ss, ib) of means, scales, quats, opacities at [0, 8); the SH
+            # groups follow when their update is not fused into the SH backward
+            assert [names[i] for i in idx][:len(tr.GEOM)] == list(tr.GEOM), (idx, names)
             ga = tr.geom_adam_in_backward(1, hyper=self.scal[:2 * len(idx)], skip=self.status)
         fusion = _wrapper.StepFusion(sh_adam=fa, geom=tr.geom_fuse, geom_adam=ga) \
             if (fa is not None or tr.geom_fuse) else None
@@ -302,7 +313,8 @@ class GraphStep:
             # (a hook keeping a reference would make AccumulateGrad clone the
             # gradient -- a memcpy node in the graph)
         else:
-            with _wrapper.fwd_split_div(getattr(tr, "split_div", None)):
+            with _wrapper.fwd_split(getattr(tr, "split_div", None),
+                                    getattr(tr, "split_threshold", None)):
                 colors, _, meta = rasterization(
                     p["means"], p["quats"], scales, opac, (p["sh0"], p["shN"]), self.vm, self.K,
                     tr.width, tr.height, sh_degree=deg, packed=False, near_plane=0.01,
@@ -313,7 +325,9 @@ class GraphStep:
         vote = None
         if self.vote:  # the ranks' overflow flags, agreed beside the loss kernels
             import torch.distributed as dist
-            vote = dist.all_reduce(self.status, op=dist.ReduceOp.MAX, async_op=True)
+            from . import distributed as gdist
+            vote = dist.all_reduce(self.status, op=dist.ReduceOp.MAX, async_op=True,
+                                   group=gdist.current_capture_group())
         loss = tr._regularise(l1_ssim_loss(
             colors, tr.targets, tr.ssim_lambda, gt_index=self.cam,
             _out_ring=(self.loss_ring, self.seq) if self.ring_loss else None,
@@ -326,24 +340,32 @@ class GraphStep:
         tr._sh_ready = 0  # the sharded optimizer's SH reduce-scatter hook
         if self.dp:  # its collectives in order on this stream (ShardedAdam.capturing)
             tr.opt.capturing = True
-        torch.autograd.backward(loss, _losses.ONE_GRAD)
-        if tr.model == "2dgs" and meta["gradient_2dgs"].grad is not None:
-            grad_box["g"] = meta["gradient_2dgs"].grad
-        if stats and "g" in grad_box:  # DefaultStrategy statistics (until refine_stop_iter)
-            update_state_(tr.grad2d, tr.count, grad_box["g"], meta["radii"], meta["width"],
-                          meta["height"], meta["n_cameras"], skip=self.status)
-        if self.dp:  # reduce-scatter, Adam on this rank's rows, all-gather: all inside
-            assert not tr._sh_skip(fusion)
-            tr.opt.step(defer_gather=False, xform=tr._geom_xform(fusion),
-                        hyper=self.scal[:sh_off], void=self.status)
-            tr.opt.capturing = False
-        else:
-            skip = tr._sh_skip(fusion)
-            launched = tuple(i for i in range(self.n_groups) if i not in skip)
-            assert launched == tuple(idx) or (ga is not None and ga.applied and launched == ()), \
-                (skip, idx)
-            tr.opt.step(skip=skip, xform=tr._geom_xform(fusion), hyper=self.scal[:sh_off],
-                        void=self.status)
+        try:
+            torch.autograd.backward(loss, _losses.ONE_GRAD)
+            if tr.model == "2dgs" and meta["gradient_2dgs"].grad is not None:
+                grad_box["g"] = meta["gradient_2dgs"].grad
+            if stats and "g" in grad_box:  # DefaultStrategy statistics (until refine_stop_iter)
+                update_state_(tr.grad2d, tr.count, grad_box["g"], meta["radii"], meta["width"],
+                              meta["height"], meta["n_cameras"], skip=self.status)
+            if self.dp:  # reduce-scatter, Adam on this rank's rows, all-gather: all inside
+                assert not tr._sh_skip(fusion)
+                tr.opt.step(defer_gather=False, xform=tr._geom_xform(fusion),
+                            hyper=self.scal[:sh_off], void=self.status)
+            else:
+                skip = tr._sh_skip(fusion)
+                launched = tuple(i for i in range(self.n_groups) if i not in skip)
+                # the launched groups are the launch plan's tail (the geometry
+                # groups, its head, may have been updated by the projection
+                # backward): their factors start at that offset
+                assert launched == tuple(idx[len(idx) - len(launched):]), (skip, idx)
+                off = 2 * (len(idx) - len(launched))
+                tr.opt.step(skip=skip, xform=tr._geom_xform(fusion),
+                            hyper=self.scal[off:sh_off], void=self.status)
+        finally:
+            # (also when the body raises: later eager steps use the optimizer's
+            # own streams and communicators again)
+            if self.dp:
+                tr.opt.capturing = False
         tr.opt.zero_grad(set_to_none=True)
         return loss, meta["isect_counts"]
 
@@ -352,7 +374,9 @@ class GraphStep:
         err = None
         try:
             self._capture_impl(deg, stats)
-        except Exception as e:  # noqa: BLE001 -- any capture failure: eager fallback
+        except RuntimeError as e:  # a HIP / RCCL / torch failure of the capture:
+            # eager fallback (programming errors -- assertions, type errors --
+            # propagate)
             err = e
             self.graph, self.key = None, None
         finally:
@@ -413,19 +437,19 @@ class GraphStep:
             # process aborted there.  torch.cuda.graph collects right before.
             gc_on = gc.isenabled()
             gc.disable()
-            import torch.distributed as dist
-            if dist.is_available() and dist.is_initialized():
-                # RCCL's watchdog threads query the end events of earlier
-                # collectives; an event query against a stream that a capture
-                # has pulled in (the communicator's own stream, when a
-                # captured collective runs on it) aborted a test process.  Let
-                # them retire every finished collective first (their poll
-                # interval is 100 ms), and capture in thread-local mode so
-                # their calls on other streams stay legal meanwhile.
-                torch.cuda.synchronize(self.dev)
-                time.sleep(0.3)
+            # RCCL's watchdog threads query the end events of the eager
+            # collectives they track; a query of an event recorded on a stream
+            # the capture has pulled in aborted a test process (round 5).  The
+            # captured collectives therefore run on a communicator of their
+            # own that never issues eager work (self.cap_pg,
+            # distributed._CAPTURE_PG; torch does not track collectives issued
+            # during a capture), so every event the watchdogs query lives on a
+            # stream outside the capture -- by construction, not by timing --
+            # and thread-local capture mode keeps their queries legal.
+            from . import distributed as gdist
             try:
-                with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                with gdist.capture_group(self.cap_pg), \
+                        torch.cuda.graph(g, capture_error_mode="thread_local"):
                     self.loss, self.counts = self._body(deg, stats)
             finally:
                 if gc_on:
@@ -501,8 +525,12 @@ class GraphStep:
         deg = tr.sh_degree_at(it)
         stats = self._stats_at(it)
         key = self._key_of(deg, stats)
+        if self.failed is not None:
+            raise GraphCaptureError(self.failed)
         if self.graph is None or key != self.key:
             self._drain()
+            if self.failed is not None:
+                raise GraphCaptureError(self.failed)
             if self.key is not None and key[1] != self.key[1] and self.capacity is not None:
                 # a refine changed the Gaussian count: grow the isect capacity
                 # in proportion (an overflow would void and re-run the step)
@@ -516,6 +544,8 @@ class GraphStep:
             # several ranks: the oldest step exactly when `lag` are pending,
             # on every rank alike (a recovery is collective)
             self._check(block=True, one=True)
+        if self.failed is not None:  # a recovery's re-capture failed: eager from here
+            raise GraphCaptureError(self.failed)
         return self._issue(it)
 
     def _issue(self, it, ret=None):
@@ -585,17 +615,27 @@ class GraphStep:
         # the redo steps take the voided steps' sequence numbers, so each
         # step's loss lands in the slot (or tensor) already returned for it
         self.issued = redo[0][1]
-        self._capture(tr.sh_degree_at(redo[0][0]), self._stats_at(redo[0][0]))
+        try:
+            self._capture(tr.sh_degree_at(redo[0][0]), self._stats_at(redo[0][0]))
+        except GraphCaptureError as e:
+            # no graph any more: the voided steps run eagerly, in order, before
+            # anything else (their losses into the tensors already returned),
+            # and the trainer issues every later step eagerly (self.failed)
+            self.failed = str(e)
+            self.graph, self.key = None, None
+            for it, _, ret in redo:
+                loss = tr._eager_step(it)
+                if ret is not None:
+                    ret.copy_(loss.detach().reshape(ret.shape))
+            return
         for it, k, ret in redo:
             assert self.issued == k
             self._issue(it, ret)
             self._check(block=True)
 
     def _drain(self):
-        if self.pending:
+        while self.pending and self.failed is None:
             self._check(block=True)
-            while self.pending:
-                self._check(block=True)
 
     def sync(self):
         """Wait for every issued step and settle its overflow check."""

@@ -383,6 +383,9 @@ class Trainer:
         reading the parameters outside the training step (checkpoint, eval)."""
         if getattr(self, "_graph", None) is not None:
             self._graph.sync()
+            if self._graph.failed is not None:  # a recovery's re-capture failed
+                self.graph_fallback = self._graph.failed
+                self._graph = None
         if self.sharded or getattr(self, "defer_sh", False):
             self.opt.wait()
 
@@ -460,7 +463,8 @@ class Trainer:
         if getattr(self, "gshard", False):
             dkw = dict(distributed=True, _world_cameras=self.world_cameras(ci, world_ci),
                        _world_counts=self._n_world)
-        with _wrapper.fwd_split_div(getattr(self, "split_div", None)):
+        with _wrapper.fwd_split(getattr(self, "split_div", None),
+                                getattr(self, "split_threshold", None)):
             return rasterization(
                 p["means"], p["quats"], scales, opac,
                 (p["sh0"], p["shN"]) if self.fused else torch.cat([p["sh0"], p["shN"]], 1),
@@ -471,23 +475,41 @@ class Trainer:
 
     def _tune_split(self, it: int):
         """Once, before the first step (and so before a graph capture freezes
-        the forward's variant): the split-forward threshold's divisor from the
-        scene's termination.  Pixels that rarely stop early (n_eff / n_isects
-        > 0.75, M3: 0.89) make the heaviest tiles the forward's tail: split
-        more of them (divisor 1100); scenes that terminate early (M2: 0.56)
-        keep 550, whose split-capable variant would only cost occupancy
-        (DESIGN 3.4).  One-GPU 3DGS on the HIP path; GSPLAT_HIP_FWD_SPLIT_DIV
-        set by the user wins.  The divisor is this trainer's: its renders (and
-        its graph capture) set it around their launches and restore the
-        previous value (_wrapper.fwd_split_div), nothing else in the process
-        sees it.  Costs one eager render (no backward) before the first step."""
+        the forward's variant):
+        * the split-forward threshold's divisor from the scene's termination.
+          Pixels that rarely stop early (n_eff / n_isects > 0.75, M3: 0.89)
+          make the heaviest tiles the forward's tail: split more of them
+          (divisor 1100); scenes that terminate early (M2: 0.56) keep 550,
+          whose split-capable variant would only cost occupancy.
+          One-GPU 3DGS on the HIP path; GSPLAT_HIP_FWD_SPLIT_DIV set by the
+          user wins;
+        * which forward variant every render of this trainer launches: the
+          split-capable one with this first render's threshold fixed if the
+          render has a tile above it, else the plain one.  Decided once, so
+          eager and captured steps run the same kernel with the same
+          threshold (a captured step's isect count is its capacity) (the library's default heuristic reads an
+          earlier render's largest tile from host-mapped memory with no sync:
+          eager renders would pick a variant by timing).
+        Both are this trainer's: its renders (and its graph capture) set them
+        around their launches and restore the previous values
+        (_wrapper.fwd_split), nothing else in the process sees them.  Costs
+        one eager render (no backward) before the first step; a
+        Gaussian-sharded render is a collective, and every rank's first step
+        runs it."""
         self._split_tuned = True
-        if (self.model != "3dgs" or not self.fused or self.world_size != 1
-                or os.environ.get("GSPLAT_HIP_FWD_SPLIT_DIV")):
+        if self.model != "3dgs" or not self.fused:
             return
         colors, _, meta = self.render(self.camera_index(it), self.sh_degree_at(it))
         self.term_ratio = _wrapper.forward_termination_ratio(colors, meta, self.width, self.height)
-        self.split_div = 1100 if self.term_ratio > 0.75 else 550
+        if self.world_size == 1 and not os.environ.get("GSPLAT_HIP_FWD_SPLIT_DIV"):
+            self.split_div = 1100 if self.term_ratio > 0.75 else 550
+        n = int(meta["isect_counts"][0]) if "isect_counts" in meta else meta["flatten_ids"].numel()
+        with _wrapper.fwd_split(getattr(self, "split_div", None)):
+            thr = _wrapper.fwd_split_threshold(n)
+        self.max_tile_first = _wrapper.max_tile_isects(meta)
+        self.split_launch = 1 if 0 <= thr < self.max_tile_first else 0
+        # > 0: the split-capable forward at this fixed threshold; 0: never
+        self.split_threshold = max(int(thr), 1) if self.split_launch else 0
         del colors, meta
 
     def step(self, it: int):
@@ -499,7 +521,8 @@ class Trainer:
                 loss = self._graph.step(it)
             except GraphCaptureError as e:
                 # the capture failed (on any rank of a sharded job): eager
-                # steps from here on, in this process (no re-exec)
+                # steps from here on, in this process (no re-exec); steps a
+                # failed recovery voided have been re-run eagerly already
                 import warnings
                 self.graph_fallback = str(e)
                 warnings.warn(f"gsplat_hip: {e}; issuing the training steps eagerly")
@@ -507,7 +530,17 @@ class Trainer:
             else:
                 if self.strategy is not None:
                     self.post_step(it)  # eager refine / reset: drains the replays first
+                if self._graph is not None and self._graph.failed is not None:
+                    self.graph_fallback = self._graph.failed  # (failed in that drain)
+                    self._graph = None
                 return loss
+        loss = self._eager_step(it)
+        if self.strategy is not None:
+            self.post_step(it)
+        return loss
+
+    def _eager_step(self, it: int):
+        """Training step `it` issued from the host (no refine / reset: post_step)."""
         ci = self.camera_index(it)
         self._sh_ready = 0
         if self.max_steps:  # means ExponentialLR: this step's lr, before the
@@ -552,8 +585,6 @@ class Trainer:
             self.opt.step(skip=self._sh_skip(fusion), xform=self._geom_xform(fusion))
         self.opt.zero_grad(set_to_none=True)
         self.last_meta = meta
-        if self.strategy is not None:
-            self.post_step(it)
         return loss
 
     def _regularise(self, loss):

@@ -41,7 +41,11 @@ const char *gsplat_hip_last_error(void);
  *     gsplat_hip_projection_2dgs_bwd_adam; v_normals may be NULL in the
  *     2DGS rasterizer's backward (output) and projection backward (input);
  *     isect_ids alone may be NULL in the sorted emission (flatten_ids and
- *     offsets written: a rasterizer that gathers by id). */
+ *     offsets written: a rasterizer that gathers by id).
+ * 34: gsplat_hip_set_fwd_split_threshold, gsplat_hip_fwd_split_threshold
+ *     (the split-forward variant chosen once by the caller: deterministic
+ *     renders); gsplat_hip_watchdog_arm / _beat / _disarm (bounded waits of
+ *     a multi-GPU job). */
 int gsplat_hip_abi_version(void);
 
 /* ---------------------------------------------------------------------------
@@ -367,8 +371,24 @@ int gsplat_hip_debug_set_fwd_split(int isects);
  * divisor in effect before the call.  The trainer picks 1100 for scenes
  * whose pixels rarely terminate early (train_step.Trainer._tune_split). */
 int gsplat_hip_set_fwd_split_div(int div);
+/* The split forward's threshold (ABI 34): > 0 = always the split-capable
+ * forward, tiles above that many isects split (which ones is decided per
+ * render on the device); 0 = never split; -1 = the library default
+ * (GSPLAT_HIP_FWD_SPLIT, else adaptive: max(2048, n_isects / divisor), the
+ * split-capable variant launched when an earlier render's largest tile
+ * exceeded it -- a heuristic read of host-mapped memory, speed only; the two
+ * variants' renders differ by the chunk products' rounding).  The trainer
+ * sets it once from its first render, so every later render -- eager or
+ * captured -- runs the same variant with the same threshold.  Returns the
+ * previous value (-1 for the adaptive default). */
+int gsplat_hip_set_fwd_split_threshold(int isects);
+/* The split threshold (isects per tile) for a render of n_isects with the
+ * divisor in effect; -1 when splitting is off (ABI 34). */
+int64_t gsplat_hip_fwd_split_threshold(int64_t n_isects);
 /* Debug flags of the 16x16 rasterizer (ABI 25; default 0, or GSPLAT_HIP_DBG):
  * bit 0 = the backward skips its gradient atomics (timing experiments);
+ * bit 2 = the backward skips its cross-lane reduction, bit 3 its gradient
+ * algebra (timing attribution only: wrong gradients);
  * bit 1 = a chunk of a split tile never waits for an earlier chunk's
  * published product and computes it itself (the timeout path; results are
  * identical).  Returns the previous flags. */
@@ -908,6 +928,28 @@ int gsplat_hip_depth_to_normal(int C, int H, int W, const float *depths, int64_t
  * for v, out f32[C,HW,3]; one launch.  Forward only. */
 int gsplat_hip_rotate3(int C, int64_t HW, const float *camtoworlds, const float *v, float *out,
                        void *stream);
+
+/* ---------------------------------------------------------------------------
+ * Progress watchdog (ABI 34; csrc/watchdog.cpp).  A native thread that ends
+ * the process when no progress is reported within a timeout: a collective one
+ * rank never joins -- also one replayed inside a HIP graph, which RCCL's own
+ * watchdog does not track -- must end a multi-GPU job with a diagnosis and a
+ * non-zero status, not hang it.  No interpreter lock is needed, so a host
+ * thread blocked in a HIP wait is no obstacle.  All return 0 (arm: 1 for a
+ * non-positive timeout).
+ *   _arm:           (re)start with `timeout_s`; `tag` names the process
+ *                   ("rank 3"); `exit_code` (non-zero) is the status on expiry.
+ *   _beat:          progress; `state` (one line) is printed on expiry.
+ *   _set_fallback:  on expiry also write `text` to `fd` and end with
+ *                   `exit_code` (fd < 0 clears it): a later phase's hang still
+ *                   delivers the result of a phase that completed.
+ *   _disarm:        stop watching (the thread stays, idle).
+ * No reference counterpart: gsplat/distributed.py relies on NCCL's timeout,
+ * which sees eager collectives only. */
+int gsplat_hip_watchdog_arm(double timeout_s, const char *tag, int exit_code);
+int gsplat_hip_watchdog_beat(const char *state);
+int gsplat_hip_watchdog_set_fallback(int fd, const char *text, int exit_code);
+int gsplat_hip_watchdog_disarm(void);
 
 #ifdef __cplusplus
 }

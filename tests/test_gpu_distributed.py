@@ -187,50 +187,48 @@ def test_graph_capture_failure_falls_back_to_eager(monkeypatch):
         assert abs(x - y) <= 1e-4 * abs(x), (la, lb)
 
 
-@pytest.mark.parametrize("solo,capacity", [("1", None), ("0", None), ("0", 1000)])
-def test_graph_dp_step_tracks_eager(monkeypatch, solo, capacity):
+@pytest.mark.parametrize("solo,capacity,stride",
+                         [("1", None, 8), ("0", None, 8), ("0", 1000, 8), ("0", None, 1)])
+def test_graph_dp_step_tracks_eager(monkeypatch, solo, capacity, stride):
     """Per-camera data parallelism with the sharded optimizer (bench
     --dp-path) captured and replayed: on a one-rank group with
     GSPLAT_HIP_DP_SOLO=0 the graph holds RCCL's reduce-scatters, all-gathers
     and the ranks' overflow vote (the N > 1 path); with a tiny isect capacity
     the voted overflow is read back from the count ring, the steps re-run and
     the returned losses are the eager ones.  Six replayed steps against six
-    eager steps: losses, parameters, moments and strategy statistics, with
-    the split forward pinned off (test_graph_trainer_tracks_eager's reason)
-    and grad2d at the run-to-run spread of two eager runs."""
-    from gsplat_hip import _lib
+    eager steps: losses, parameters, moments and strategy statistics, the
+    adaptive split forward on (the trainer's one variant choice), grad2d at
+    the run-to-run spread of two eager runs; stride 1 runs heavy tiles
+    through the split forward."""
     from gsplat_hip.train_step import Trainer
     from test_gpu_graph import _trainer_scene
     monkeypatch.setenv("GSPLAT_HIP_DP_SOLO", solo)
-    means, rgbs, vm, K, W, H = _trainer_scene()
+    means, rgbs, vm, K, W, H = _trainer_scene(stride=stride)
     out = {}
-    old = _lib.query("gsplat_hip_debug_set_fwd_split", 0)
-    try:
-        for run in ("eager", "eager2", "graph"):
-            graph = run == "graph"
-            tr = Trainer(means, rgbs, vm, K, W, H, device=DEV, world_size=1, rank=0,
-                         sharded_optimizer=True, graph=graph, isect_capacity=capacity,
-                         max_steps=100)
-            assert tr.sharded and tr.opt.solo == (solo == "1")
-            assert (tr._graph is not None) == graph
-            losses = [tr.step(it) for it in range(6)]
-            tr.sync()
-            assert tr.graph_fallback is None, tr.graph_fallback
-            if graph:
-                g = tr._graph
-                assert g.replays >= 6 and g.vote
-                print("census", dict(g.census))
-                assert "memset" not in g.census, g.census
-                if capacity is not None:
-                    assert g.recaptures >= 2 and g.capacity > g.max_isects > capacity
-            st = tr.opt.full_state()
-            out[run] = ({k: p.detach().clone() for k, p in tr.params.items()},
-                        [m.clone() for m, _ in st], tr.opt.step_count, tr.grad2d.clone(),
-                        tr.count.clone(), [float(x) for x in losses])
-            tr.release_graph()
-            del tr
-    finally:
-        _lib.query("gsplat_hip_debug_set_fwd_split", old)
+    for run in ("eager", "eager2", "graph"):
+        graph = run == "graph"
+        tr = Trainer(means, rgbs, vm, K, W, H, device=DEV, world_size=1, rank=0,
+                     sharded_optimizer=True, graph=graph, isect_capacity=capacity,
+                     max_steps=100)
+        assert tr.sharded and tr.opt.solo == (solo == "1")
+        assert (tr._graph is not None) == graph
+        losses = [tr.step(it) for it in range(6)]
+        tr.sync()
+        assert tr.graph_fallback is None, tr.graph_fallback
+        assert tr.split_launch == (1 if stride == 1 else 0), (tr.split_launch, tr.max_tile_first)
+        if graph:
+            g = tr._graph
+            assert g.replays >= 6 and g.vote
+            print("census", dict(g.census))
+            assert "memset" not in g.census, g.census
+            if capacity is not None:
+                assert g.recaptures >= 2 and g.capacity > g.max_isects > capacity
+        st = tr.opt.full_state()
+        out[run] = ({k: p.detach().clone() for k, p in tr.params.items()},
+                    [m.clone() for m, _ in st], tr.opt.step_count, tr.grad2d.clone(),
+                    tr.count.clone(), [float(x) for x in losses])
+        tr.release_graph()
+        del tr
     a, a2, b = out["eager"], out["eager2"], out["graph"]
     assert a[2] == b[2] == 6
     torch.testing.assert_close(torch.tensor(b[5]), torch.tensor(a[5]), rtol=1e-4, atol=1e-6)
@@ -256,3 +254,50 @@ def test_graph_dp_step_tracks_eager(monkeypatch, solo, capacity):
           f"{int((err > bar).sum())} of {err.numel()} above {bar:.3e}")
     assert int((err > bar).sum()) <= max(2, err.numel() // 2000), (float(err.max()), spread)
     assert float(err.max()) <= 1e-3 * gmax, (float(err.max()), gmax)
+
+
+@pytest.mark.parametrize("scheme", ["dp", "gshard"])
+def test_capture_right_after_eager_collectives(monkeypatch, scheme):
+    """Round 5's abort: RCCL's watchdog thread queried the end event of an
+    eager collective while a capture had pulled that communicator's stream
+    in.  Here eager collectives are issued -- and not waited for -- on the
+    default group (and the sharded optimizer's SH group) right before every
+    capture, the tiny isect capacity forcing re-captures too: the captures
+    succeed (their collectives run on the capture-only group, GraphStep.cap_pg)
+    and the replayed steps return the eager losses."""
+    from gsplat_hip import graph_step
+    from gsplat_hip.train_step import Trainer
+    from test_gpu_graph import _trainer_scene
+    monkeypatch.setenv("GSPLAT_HIP_DP_SOLO", "0")
+    orig = graph_step.GraphStep._capture_impl
+    issued = []
+
+    def eager_then_capture(self, deg, stats=True):
+        t = torch.ones(1 << 16, device=DEV)
+        works = [dist.all_reduce(t, async_op=True)]
+        if getattr(self.tr, "_sh_pg", None) is not None:
+            works.append(dist.all_reduce(t, async_op=True, group=self.tr._sh_pg))
+        issued.append(works)  # kept alive, never waited for
+        return orig(self, deg, stats)
+
+    means, rgbs, vm, K, W, H = _trainer_scene()
+    kw = dict(sharded_optimizer=True) if scheme == "dp" else dict(gaussian_shard=True)
+    out = {}
+    for graph in (False, True):
+        if graph:
+            monkeypatch.setattr(graph_step.GraphStep, "_capture_impl", eager_then_capture)
+        tr = Trainer(means, rgbs, vm, K, W, H, device=DEV, world_size=1, rank=0, graph=graph,
+                     isect_capacity=1000 if graph else None, max_steps=100, **kw)
+        losses = [tr.step(it) for it in range(5)]
+        tr.sync()  # (a voided step's redo rewrites the loss returned for it)
+        losses = [float(x) for x in losses]
+        assert tr.graph_fallback is None, tr.graph_fallback
+        if graph:
+            g = tr._graph
+            assert g.cap_pg is not None and g.recaptures >= 2 and len(issued) >= 2
+            assert g.replays >= 5
+        out[graph] = losses
+        tr.release_graph()
+        del tr
+    torch.testing.assert_close(torch.tensor(out[True]), torch.tensor(out[False]),
+                               rtol=1e-4, atol=1e-6)

@@ -203,49 +203,51 @@ def test_sh_adam_device_factors_are_exact():
         assert torch.equal(a, b)
 
 
-def _trainer_scene(n_cams=3, W=320, H=240):
+def _trainer_scene(n_cams=3, W=320, H=240, stride=8):
+    """The garden crop's every `stride`-th point at W x H.  stride 8: 13,974
+    Gaussians, tiles of <= 554 isects; stride 1 (heavy tiles): 111,785
+    Gaussians, ~280 k isects, 32-38 tiles above 2048 isects per camera --
+    above the split threshold, so the trainer runs the split forward."""
     import os
     from gsplat_hip.train_step import camera_pool, load_garden_scene
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     means, rgbs, vms, Ks, sw, sh_ = load_garden_scene(
         os.path.join(root, "tests", "golden", "garden_scene.npz"), scene_grid=1)
-    means, rgbs = means[::8].contiguous(), rgbs[::8].contiguous()
+    means, rgbs = means[::stride].contiguous(), rgbs[::stride].contiguous()
     vm, K = camera_pool(vms, Ks, sw, sh_, W, H, n=n_cams)
     return means, rgbs, vm, K, W, H
 
 
-@pytest.mark.parametrize("capacity", [None, 1000])
-def test_graph_trainer_tracks_eager(capacity):
-    """Six replayed steps against six eager ones.  The split forward is
-    pinned off: adaptively, an eager render decides to split from the
-    previous render's largest tile while a capture freezes its decision, and
-    split and unsplit images differ by chunk-product rounding (3e-6 of grad2d
-    seen).  The rasterizer backward's float atomics still make two eager runs
-    differ in the last bits and grad2d sums gradient norms that can cancel:
-    its bar comes from the spread of two eager runs (measured here)."""
-    from gsplat_hip import _lib
+@pytest.mark.parametrize("capacity,stride", [(None, 8), (1000, 8), (None, 1), (20000, 1)])
+def test_graph_trainer_tracks_eager(capacity, stride):
+    """Six replayed steps against six eager ones, with the library's adaptive
+    split forward on: the trainer picks the forward variant once, from its
+    first render (Trainer.split_launch), so eager and captured renders run
+    the same kernel.  stride 1: heavy tiles, the split forward runs (its
+    chunks' products are exercised in both).  The rasterizer backward's float
+    atomics still make two eager runs differ in the last bits and grad2d sums
+    gradient norms that can cancel: its bar comes from the spread of two
+    eager runs (measured here)."""
     from gsplat_hip.train_step import Trainer
-    means, rgbs, vm, K, W, H = _trainer_scene()
+    means, rgbs, vm, K, W, H = _trainer_scene(stride=stride)
     out = {}
-    old = _lib.query("gsplat_hip_debug_set_fwd_split", 0)
-    try:
-        for run in ("eager", "eager2", "graph"):
-            graph = run == "graph"
-            tr = Trainer(means, rgbs, vm, K, W, H, device=DEV, graph=graph,
-                         isect_capacity=capacity, max_steps=100)
-            assert (tr._graph is not None) == graph
-            losses = [tr.step(it) for it in range(6)]
-            tr.sync()
-            out[run] = ({k: p.detach().clone() for k, p in tr.params.items()},
-                        [m.clone() for m in tr.opt.exp_avg], tr.opt.step_count,
-                        tr.grad2d.clone(), tr.count.clone(), [float(x) for x in losses])
-            if graph:
-                g = tr._graph
-                assert g.replays >= 6
-                if capacity is not None:  # started too small: grown and re-captured
-                    assert g.recaptures >= 2 and g.capacity > g.max_isects > capacity
-    finally:
-        _lib.query("gsplat_hip_debug_set_fwd_split", old)
+    for run in ("eager", "eager2", "graph"):
+        graph = run == "graph"
+        tr = Trainer(means, rgbs, vm, K, W, H, device=DEV, graph=graph,
+                     isect_capacity=capacity, max_steps=100)
+        assert (tr._graph is not None) == graph
+        losses = [tr.step(it) for it in range(6)]
+        tr.sync()
+        assert tr.graph_fallback is None, tr.graph_fallback
+        assert tr.split_launch == (1 if stride == 1 else 0), (tr.split_launch, tr.max_tile_first)
+        out[run] = ({k: p.detach().clone() for k, p in tr.params.items()},
+                    [m.clone() for m in tr.opt.exp_avg], tr.opt.step_count,
+                    tr.grad2d.clone(), tr.count.clone(), [float(x) for x in losses])
+        if graph:
+            g = tr._graph
+            assert g.replays >= 6
+            if capacity is not None:  # started too small: grown and re-captured
+                assert g.recaptures >= 2 and g.capacity > g.max_isects > capacity
     a, a2, b = out["eager"], out["eager2"], out["graph"]
     assert a[2] == b[2] == 6
     for k in a[0]:
@@ -377,3 +379,64 @@ def test_loss_target_index_is_exact():
         la.backward()
         lb.backward()
         assert torch.equal(la.detach(), lb.detach()) and torch.equal(a.grad, b.grad)
+
+
+def test_graph_recapture_failure_reruns_voided_steps(monkeypatch):
+    """A recovery (isect overflow: grow, re-capture, redo) whose re-capture
+    fails: the voided steps run eagerly, in order, before the current one,
+    their losses land in the tensors already returned for them, and the
+    trainer continues eagerly -- the same update sequence as an eager run
+    (no step lost)."""
+    from gsplat_hip import graph_step
+    from gsplat_hip.train_step import Trainer
+    means, rgbs, vm, K, W, H = _trainer_scene()
+    ref = Trainer(means, rgbs, vm, K, W, H, device=DEV, graph=False, max_steps=100)
+    la = [float(ref.step(it)) for it in range(6)]
+    ref.sync()
+    orig = graph_step.GraphStep._capture_impl
+    calls = []
+
+    def second_fails(self, deg, stats=True):
+        calls.append(1)
+        if len(calls) >= 2:
+            raise RuntimeError("injected re-capture failure")
+        return orig(self, deg, stats)
+
+    monkeypatch.setattr(graph_step.GraphStep, "_capture_impl", second_fails)
+    tr = Trainer(means, rgbs, vm, K, W, H, device=DEV, graph=True, isect_capacity=1000,
+                 max_steps=100)
+    with pytest.warns(UserWarning, match="eagerly"):
+        ret = [tr.step(it) for it in range(6)]
+    tr.sync()
+    assert tr._graph is None and "injected" in tr.graph_fallback
+    assert tr.opt.step_count == 6 and len(calls) == 2
+    lb = [float(x) for x in ret]
+    for x, y in zip(la, lb):
+        assert abs(x - y) <= 1e-4 * abs(x), (la, lb)
+    for k in ref.params:
+        torch.testing.assert_close(tr.params[k].detach(), ref.params[k].detach(), rtol=1e-3,
+                                   atol=1e-5)
+    torch.testing.assert_close(tr.count, ref.count, rtol=0, atol=0)
+
+
+def test_graph_trainer_sh_adam_unfused_tracks_eager(monkeypatch):
+    """GSPLAT_HIP_SH_ADAM_IN_BWD=0 with the geometry update in the projection
+    backward: the launched groups (sh0, shN) take their device-side factors
+    from the launch plan's tail (not the geometry's) -- replays equal eager
+    steps."""
+    from gsplat_hip.train_step import Trainer
+    monkeypatch.setenv("GSPLAT_HIP_SH_ADAM_IN_BWD", "0")
+    means, rgbs, vm, K, W, H = _trainer_scene()
+    out = {}
+    for graph in (False, True):
+        tr = Trainer(means, rgbs, vm, K, W, H, device=DEV, graph=graph, max_steps=100)
+        assert not tr.sh_adam_in_bwd and tr.geom_in_proj
+        losses = [float(tr.step(it)) for it in range(5)]
+        tr.sync()
+        assert tr.graph_fallback is None, tr.graph_fallback
+        assert (tr._graph is not None) == graph
+        out[graph] = (losses, {k: p.detach().clone() for k, p in tr.params.items()})
+    torch.testing.assert_close(torch.tensor(out[True][0]), torch.tensor(out[False][0]),
+                               rtol=1e-4, atol=1e-6)
+    for k in out[False][1]:
+        torch.testing.assert_close(out[True][1][k], out[False][1][k], rtol=1e-3, atol=1e-5)

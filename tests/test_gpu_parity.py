@@ -819,7 +819,7 @@ def test_full_size_invariants_m3():
         old = _lib.query("gsplat_hip_debug_set_fwd_split", split)
         try:
             leaves = [x.clone().requires_grad_(True) for x in ins]
-            with _wrapper.fwd_split_div(div):
+            with _wrapper.fwd_split(div):
                 rc, ra, meta = gsplat_hip.rasterization(*leaves[:4], leaves[4], vm, K, W, H,
                                                         sh_degree=3, packed=False)
             w = torch.rand(rc.shape, generator=torch.Generator(device=DEV).manual_seed(2),

@@ -183,6 +183,29 @@ def test_raster2dgs_tile_order_changes_nothing(monkeypatch, masked):
         torch.testing.assert_close(b, a, rtol=1e-4, atol=1e-5 * float(a.abs().max()))
 
 
+def test_raster2dgs_tile_order_above_16384_tiles(monkeypatch):
+    """More tiles than one block of the order kernel (2200 x 2100 at 16 px:
+    18,216 tiles): the forward writes the dispatch order for every tile (the
+    kernel walks 16,384-tile blocks), and the backward, which reuses it,
+    sees a complete order -- images bit for bit and gradients as without the
+    order (before: no order past 16,384 tiles, and the backward read an
+    unwritten one)."""
+    from gsplat_hip import _wrapper_2dgs
+    sc = surfel_scene(7, N=800, W=2200, H=2100, D=4, bg=True, C=1)
+    assert sc["off"].size > 16384
+    res = []
+    for order in (False, True):
+        monkeypatch.setattr(_wrapper_2dgs, "ORDER", order)
+        leaves, bgt, densify, out = _raster_gpu(sc)
+        w = [torch.linspace(-1, 1, o.numel(), device=DEV).view_as(o) for o in out]
+        sum((o * ww).sum() for o, ww in zip(out, w)).backward()
+        res.append(([o.detach() for o in out], [leaves[k].grad for k in sorted(leaves)]))
+    for a, b in zip(res[0][0], res[1][0]):
+        assert torch.equal(a, b), float((a - b).abs().max())
+    for a, b in zip(res[0][1], res[1][1]):
+        torch.testing.assert_close(b, a, rtol=1e-4, atol=1e-5 * float(a.abs().max()))
+
+
 def test_raster2dgs_fwd_masks():
     sc = surfel_scene(5, N=300, W=70, H=52, D=4, bg=True)
     rng = np.random.default_rng(0)

@@ -194,6 +194,13 @@ def _small_scene(n_cams=4, W=320, H=240):
     return means, rgbs, vm, K, W, H
 
 
+def thr_first(tr):
+    from gsplat_hip import _wrapper
+    with _wrapper.fwd_split(tr.split_div):
+        colors, _, meta = tr.render(tr.camera_index(0), tr.sh_degree_at(0))
+        return _wrapper.fwd_split_threshold(meta["flatten_ids"].numel())
+
+
 def test_trainer_tunes_split_divisor_from_termination():
     """Trainer._tune_split: before the first step, the forward's n_eff /
     n_isects (forward_termination_ratio, the bench's formula) picks the split
@@ -211,8 +218,15 @@ def test_trainer_tunes_split_divisor_from_termination():
         r = tr.term_ratio
         assert 0.0 < r <= 1.0
         assert tr.split_div == (1100 if r > 0.75 else 550)
+        # the forward variant: decided once from the first render's largest tile
+        with _wrapper.fwd_split(tr.split_div):
+            thr = _wrapper.fwd_split_threshold(1)
+        assert tr.split_launch in (0, 1) and thr >= 2048
+        old_thr = _lib.query("gsplat_hip_set_fwd_split_threshold", -1)
+        assert old_thr == -1, old_thr  # not leaked
+        assert tr.split_threshold == (thr_first(tr) if tr.split_launch else 0)
         assert _lib.query("gsplat_hip_set_fwd_split_div", 777) == 777  # not leaked
-        with _wrapper.fwd_split_div(tr.split_div):
+        with _wrapper.fwd_split(tr.split_div):
             assert _lib.query("gsplat_hip_set_fwd_split_div", tr.split_div) == tr.split_div
         assert _lib.query("gsplat_hip_set_fwd_split_div", before) == 777
         # direct: per tile, isects up to the tile's largest last id + 1
