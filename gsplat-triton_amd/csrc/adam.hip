@@ -141,8 +141,7 @@ using namespace gs;
 static int adam_launch(int n_groups, float *const *params, const float *const *grads,
                        const float *const *aux, const int32_t *modes, float *const *exp_avgs,
                        float *const *exp_avg_sqs, const int64_t *numels, const float *lrs,
-                       float beta1, float beta2, float eps, int step, int max_blocks,
-                       void *stream, const float *hyper = nullptr,
+                       float beta1, float beta2, float eps, int step, void *stream, const float *hyper = nullptr,
                        const int32_t *skip = nullptr) {
   GS_REQUIRE(n_groups > 0 && n_groups <= adam::kMaxGroups, "adam: 1..%d groups supported",
              adam::kMaxGroups);
@@ -177,21 +176,13 @@ static int adam_launch(int n_groups, float *const *params, const float *const *g
   for (int i = n_groups; i < adam::kMaxGroups; ++i) g.begin[i + 1] = g.begin[n_groups];
   const int64_t total = g.begin[n_groups];
   if (total == 0) return 0;
-  if (max_blocks > 0) {
-    // a bounded grid (an update overlapping other streams' kernels leaves
-    // them CU slots): four 16-B slots per lane in flight per iteration
-    const int blocks = (int)std::min<int64_t>((total + 1023) / 1024, max_blocks);
-    hipLaunchKernelGGL((adam::step_kernel<4, false>), dim3(blocks), dim3(256), 0,
-                       (hipStream_t)stream, g, beta1, beta2, eps);
-  } else {
-    // one 16-B slot per lane per iteration; deeper unrolling and non-temporal
-    // accesses measured no faster (tools/adam_bench.py: ~5.8 TB/s; inside the
-    // M2 step non-temporal ran 776.4 / 785.0 / 804.3 against 803.8 x 3
-    // images/s, profiles/r4_batch12/ -- unlike the SH Adam's rows)
-    const int blocks = (int)std::min<int64_t>((total + 255) / 256, 256 * 64);
-    hipLaunchKernelGGL((adam::step_kernel<1, false>), dim3(blocks), dim3(256), 0,
-                       (hipStream_t)stream, g, beta1, beta2, eps);
-  }
+  // one 16-B slot per lane per iteration; deeper unrolling and non-temporal
+  // accesses measured no faster (tools/adam_bench.py: ~5.8 TB/s; inside the
+  // M2 step non-temporal ran 776.4 / 785.0 / 804.3 against 803.8 x 3
+  // images/s, profiles/r4_batch12/ -- unlike the SH Adam's rows)
+  const int blocks = (int)std::min<int64_t>((total + 255) / 256, 256 * 64);
+  hipLaunchKernelGGL((adam::step_kernel<1, false>), dim3(blocks), dim3(256), 0,
+                     (hipStream_t)stream, g, beta1, beta2, eps);
   GS_CHECK_LAUNCH("adam_step");
   return 0;
 }
@@ -201,17 +192,7 @@ extern "C" int gsplat_hip_adam_step(int n_groups, float *const *params, const fl
                                     const int64_t *numels, const float *lrs, float beta1,
                                     float beta2, float eps, int step, void *stream) {
   return adam_launch(n_groups, params, grads, nullptr, nullptr, exp_avgs, exp_avg_sqs, numels, lrs,
-                     beta1, beta2, eps, step, 0, stream);
-}
-
-extern "C" int gsplat_hip_adam_step_bounded(int n_groups, float *const *params,
-                                            const float *const *grads, float *const *exp_avgs,
-                                            float *const *exp_avg_sqs, const int64_t *numels,
-                                            const float *lrs, float beta1, float beta2, float eps,
-                                            int step, int max_blocks, void *stream) {
-  GS_REQUIRE(max_blocks > 0, "adam_step_bounded: max_blocks must be > 0");
-  return adam_launch(n_groups, params, grads, nullptr, nullptr, exp_avgs, exp_avg_sqs, numels, lrs,
-                     beta1, beta2, eps, step, max_blocks, stream);
+                     beta1, beta2, eps, step, stream);
 }
 
 extern "C" int gsplat_hip_adam_step_ex(int n_groups, float *const *params,
@@ -221,7 +202,7 @@ extern "C" int gsplat_hip_adam_step_ex(int n_groups, float *const *params,
                                        const float *lrs, float beta1, float beta2, float eps,
                                        int step, void *stream) {
   return adam_launch(n_groups, params, grads, aux, modes, exp_avgs, exp_avg_sqs, numels, lrs,
-                     beta1, beta2, eps, step, 0, stream);
+                     beta1, beta2, eps, step, stream);
 }
 
 // The gsplat_hip_adam_step_ex update with the step-dependent factors read on
@@ -237,5 +218,5 @@ extern "C" int gsplat_hip_adam_step_dev(int n_groups, float *const *params,
                                         float eps, const int32_t *skip_device, void *stream) {
   GS_REQUIRE(hyper_device != nullptr, "adam_step_dev: null hyper_device");
   return adam_launch(n_groups, params, grads, aux, modes, exp_avgs, exp_avg_sqs, numels, nullptr,
-                     beta1, beta2, eps, 0, 0, stream, hyper_device, skip_device);
+                     beta1, beta2, eps, 0, stream, hyper_device, skip_device);
 }

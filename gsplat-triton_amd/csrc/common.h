@@ -66,20 +66,11 @@ __global__ void __launch_bounds__(256) zero_fill_kernel(void *p, int64_t n_vec, 
   if (t < bytes && i < V) reinterpret_cast<uint8_t *>(p)[t] = 0;
 }
 
-// GSPLAT_HIP_MEMSET_NODES=1 (diagnosis only, tools/graph_diag.py): zero with
-// hipMemsetAsync as before round 3, to reproduce the captured step's memset
-// nodes.
-inline bool memset_nodes() {
-  static const bool v = [] {
-    const char *e = getenv("GSPLAT_HIP_MEMSET_NODES");
-    return e && atoi(e) == 1;
-  }();
-  return v;
-}
-
+// Zero fill by kernel, never hipMemsetAsync: a captured memset node of the
+// bundled HIP runtime replays with a wrong fill value, and the
+// captured training step must hold kernel nodes only.
 inline hipError_t zero_async(void *p, size_t bytes, hipStream_t st) {
   if (bytes == 0) return hipSuccess;
-  if (memset_nodes()) return hipMemsetAsync(p, 0, bytes, st);
   const bool v16 = (reinterpret_cast<uintptr_t>(p) & 15) == 0;
   const int V = v16 ? 16 : 4;
   if (!v16 && (reinterpret_cast<uintptr_t>(p) & 3)) return hipErrorInvalidValue;

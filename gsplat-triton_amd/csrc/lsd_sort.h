@@ -2,8 +2,8 @@
 // the isect paths in place of rocPRIM's device sort (whose per-pass fixed cost,
 // ~25 us for a 0.3 M-item onesweep pass, dominated the depth sort).
 //
-// One pass = 8 key bits (optionally 11 for keys of more than 24 bits, see
-// lsd_sort_pairs), three launches:
+// One pass = 8 key bits (lsd_sort_pairs; lsd_one_pass: one digit as wide as
+// its key, up to 11 bits), three launches:
 //   lsd_hist     per tile of NT*IPT items: LDS digit histogram -> hist[d][tile]
 //   lsd_scan     one workgroup per digit: exclusive scan of its row in place,
 //                row total -> totals[d]
@@ -273,23 +273,17 @@ inline size_t lsd_sort_scratch_bytes(int64_t n) {
 // between (k0, v0) and (k1, v1).  Returns 0 if the result is in (k0, v0),
 // 1 if in (k1, v1).  With `fo` non-null the last pass writes the final isect
 // output instead (see FinalOut; the return value is then meaningless).
-// n < 2^32.  Ranges of more than 24 bits (without `fo`: the depth sort) use
-// 11-bit digits, 3 passes for 32 bits.
+// n < 2^32.
 inline int lsd_sort_pairs(uint32_t *k0, int32_t *v0, uint32_t *k1, int32_t *v1, int64_t n,
                           int begin_bit, int end_bit, void *scratch, hipStream_t st,
                           const lsd::FinalOut *fo = nullptr, const int64_t *n_dev = nullptr) {
   if (n <= 0 || end_bit <= begin_bit) return 0;
   const int ipt = lsd::pick_ipt(n);
   const int64_t nt = lsd::n_tiles(n, ipt);
-  // 11-bit digits for the 32-bit depth sort measured slower at M2 (3 passes
-  // 78 us vs 4 passes 68 us: the 2048-bin histograms and scans cost more
-  // than the pass they save); GSPLAT_HIP_LSD_WIDE=1 turns them on
-  static const bool wide_ok = [] {
-    const char *e = getenv("GSPLAT_HIP_LSD_WIDE");
-    return e && atoi(e) == 1;
-  }();
-  const bool wide = wide_ok && end_bit - begin_bit > 24 && fo == nullptr;
-  const int dbits = wide ? 11 : 8, radix = wide ? lsd::RADIX_WIDE : lsd::RADIX;
+  // 8-bit digits throughout: 11-bit digits for the 32-bit depth sort (3
+  // passes) measured slower at M2, 78 us against 68 us for 4 passes (the
+  // 2048-bin histograms and scans cost more than the pass they save); removed
+  constexpr int dbits = 8, radix = lsd::RADIX;
   uint32_t *hist = reinterpret_cast<uint32_t *>(scratch);
   uint32_t *totals = hist + (int64_t)radix * nt;
   int cur = 0;
@@ -298,15 +292,12 @@ inline int lsd_sort_pairs(uint32_t *k0, int32_t *v0, uint32_t *k1, int32_t *v1, 
     const uint32_t mask = (1u << nbits) - 1u;
     uint32_t *ki = cur ? k1 : k0, *ko = cur ? k0 : k1;
     int32_t *vi = cur ? v1 : v0, *vo = cur ? v0 : v1;
-#define GS_LSD_HIST(I, RX)                                                                     \
-  hipLaunchKernelGGL((lsd::hist_kernel<I, RX>), dim3((unsigned)nt), dim3(lsd::NT), 0, st, ki, n, \
-                     n_dev, shift, mask, hist, nt)
-    if (wide) {
-      if (ipt == 4) GS_LSD_HIST(4, lsd::RADIX_WIDE); else GS_LSD_HIST(16, lsd::RADIX_WIDE);
-    } else {
-      if (ipt == 4) GS_LSD_HIST(4, lsd::RADIX); else GS_LSD_HIST(16, lsd::RADIX);
-    }
-#undef GS_LSD_HIST
+    if (ipt == 4)
+      hipLaunchKernelGGL((lsd::hist_kernel<4, lsd::RADIX>), dim3((unsigned)nt), dim3(lsd::NT), 0,
+                         st, ki, n, n_dev, shift, mask, hist, nt);
+    else
+      hipLaunchKernelGGL((lsd::hist_kernel<16, lsd::RADIX>), dim3((unsigned)nt), dim3(lsd::NT), 0,
+                         st, ki, n, n_dev, shift, mask, hist, nt);
     hipLaunchKernelGGL(lsd::scan_kernel, dim3((unsigned)radix), dim3(lsd::NT), 0, st, hist, nt,
                        totals, n_dev, n, (int64_t)lsd::NT * ipt);
     const bool fin = fo && shift + dbits >= end_bit;
@@ -314,10 +305,7 @@ inline int lsd_sort_pairs(uint32_t *k0, int32_t *v0, uint32_t *k1, int32_t *v1, 
 #define GS_LSD_SCATTER(I, F, RX)                                                              \
   hipLaunchKernelGGL((lsd::scatter_kernel<I, F, RX>), dim3((unsigned)nt), dim3(lsd::NT), 0, st, \
                      ki, vi, ko, vo, n, n_dev, shift, nbits, hist, totals, nt, f)
-    if (wide) {
-      if (ipt == 4) GS_LSD_SCATTER(4, false, lsd::RADIX_WIDE);
-      else GS_LSD_SCATTER(16, false, lsd::RADIX_WIDE);
-    } else if (ipt == 4) {
+    if (ipt == 4) {
       if (fin) GS_LSD_SCATTER(4, true, lsd::RADIX); else GS_LSD_SCATTER(4, false, lsd::RADIX);
     } else {
       if (fin) GS_LSD_SCATTER(16, true, lsd::RADIX); else GS_LSD_SCATTER(16, false, lsd::RADIX);

@@ -305,7 +305,7 @@ int rasterize16_pack_records(int64_t G, int D, const float *means2d, const float
                              const float *colors, const float *opacities, const int32_t *visible,
                              const int32_t *vis_rank, float *records, hipStream_t st);
 int64_t rasterize16_fwd_state_bytes(int D, int n_tiles, int64_t n_isects);
-int rasterize16_prepare(int D, int n_tiles, const int32_t *offsets, int64_t n_isects,
+int rasterize16_prepare(int D, int C, int tw, int th, const int32_t *offsets, int64_t n_isects,
                         const int64_t *n_isects_dev, void *state, int64_t state_bytes,
                         hipStream_t st);
 int64_t rasterize16_bwd_workspace(int64_t G, int D, bool absgrad, int n_tiles, int64_t n_isects);
@@ -340,7 +340,7 @@ extern "C" int gsplat_hip_rasterize_prepare(int C, int D, int tile_size, int til
                                            int64_t n_isects, const int64_t *n_isects_device,
                                            void *state, int64_t state_bytes, void *stream) {
   if (tile_size != 16 || !supported_channels(D)) return 0;
-  return rasterize16_prepare(D, C * tile_width * tile_height, isect_offsets, n_isects,
+  return rasterize16_prepare(D, C, tile_width, tile_height, isect_offsets, n_isects,
                              n_isects_device, state, state_bytes, (hipStream_t)stream);
 }
 

@@ -29,7 +29,6 @@
 
 namespace gs {
 static uint64_t *g_timeline = nullptr;
-static unsigned long long *g_lanehist = nullptr;  // debug: [65] active-lane counts (backward)
 static int64_t g_timeline_waves = 0;
 
 namespace r16 {
@@ -151,7 +150,6 @@ struct Args {
   int dbg;  // debug flags (gsplat_hip_debug_set_flags): bit 0 = backward skips its
             // atomics, bit 1 = split chunks never wait for a published product
   uint64_t *timeline;  // debug: per-wave (start, end) s_memrealtime stamps or null
-  unsigned long long *lanehist;  // debug: histogram of contributing lanes per (record, wave)
 };
 
 // Isect count and the end of tile t's isect range.  Capacity mode (n_dev
@@ -553,6 +551,7 @@ GS_INLINE void fwd_item(const Args &a, float4 *st, int item) {
   } else {
     if (a.n_whole && item >= a.n_whole[0]) return;  // the split tiles' slots
     tile_ = a.order ? a.order[item] : item;
+    if (tile_ < 0) return;  // an empty slot of the XCD-grouped order
   }
   const WaveGeom geo(a, lane, tile_);
   const int tile = geo.tile, c = geo.c;
@@ -702,7 +701,7 @@ GS_INLINE void fwd_item(const Args &a, float4 *st, int item) {
 #pragma unroll
       for (int d = 0; d < D; ++d) {
         const float cs = acc[d].x + acc[d].y;
-        if (cur_b > tstart && live_b) sl[(1 + d) * kTS * kTS + pix_in_tile] = cs;
+        if (cur_b > tstart && live_b && !(a.dbg & 32)) sl[(1 + d) * kTS * kTS + pix_in_tile] = cs;
         tot[d] += cs;
         acc[d] = f2v{0.f, 0.f};
       }
@@ -711,7 +710,7 @@ GS_INLINE void fwd_item(const Args &a, float4 *st, int item) {
       close_chunk();
       cur_b = bidx;
       live_b = T > 0.f;
-      if (live_b) slot(bidx)[pix_in_tile] = T;
+      if (live_b && !(a.dbg & 32)) slot(bidx)[pix_in_tile] = T;
     };
     // a chunk of a split tile writes the state of the boundaries inside it
     // and the colour it adds at its own start boundary
@@ -833,209 +832,7 @@ __attribute__((amdgpu_waves_per_eu(!SPLIT && D <= 3 ? 6 : 5))) fwd_kernel(Args a
   }
 }
 
-// Backward: batches of 64 isects from the back, same two-deep gather pipeline.
-template <int D, bool ABS>
-// register budget: 72 VGPRs = 7 waves per SIMD without spills
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) bwd_kernel(Args a) {
-  using P = BwdPair<D>;
-  constexpr int N4 = P::N4;
-  constexpr int F = D + 6 + (ABS ? 2 : 0);
-  constexpr int NV = (F + 15) / 16;  // reduce-scatter groups of <= 16 fields
-  __shared__ float4 stage_all[4][32 * N4];
-  const int lane = threadIdx.x & 63;
-  float4 *st = stage_all[threadIdx.x >> 6];
-  const uint64_t t_start = tl_now(a);
-  // work item: a whole tile, or chunk k = isects [start + kL, start + (k+1)L)
-  // of a long tile (a.items, see "Chunked backward")
-  int tile = blockIdx.x, k = 0;
-  if (a.items) {
-    const int nf = a.n_items[0];
-    int b = blockIdx.x;
-    if (b >= nf && b - nf >= a.n_items[1]) return;
-    const int2 it = b < nf ? a.items[b] : a.items_tail[b - nf];
-    tile = it.x;
-    k = it.y;
-  }
-  const WaveGeom geo(a, lane, tile);
-  const int c = geo.c;
-  if (a.masks && a.masks[tile]) return;
-  const int64_t tstart = a.offsets[tile];
-  const int64_t tend = tile_end(a, tile);
-  const int64_t start = a.items ? tstart + (int64_t)k * a.L : tstart;
-  const int64_t cend = a.items ? min(tend, start + a.L) : tend;
-
-  const bool in = geo.px < a.W && geo.py < a.H;
-  const float fx = (float)geo.px + 0.5f, fy = (float)geo.py + 0.5f;
-  float T = 1.f, Tf = 1.f, Dra = 0.f, rD = 0.f, bgt = 0.f, Drc[D];
-  int32_t mylast = -1;
-#pragma unroll
-  for (int d = 0; d < D; ++d) Drc[d] = 0.f;
-  if (in) {
-    const int64_t pix = ((int64_t)c * a.H + geo.py) * a.W + geo.px;
-    Tf = 1.f - a.render_alphas[pix];
-    Dra = a.v_render_alphas ? a.v_render_alphas[pix] : 0.f;  // null: alphas unused
-    mylast = a.last_ids[pix];
-#pragma unroll
-    for (int d = 0; d < D; ++d) Drc[d] = a.v_render_colors[pix * D + d];
-    float bgv = 0.f;
-    if (a.backgrounds) {
-#pragma unroll
-      for (int d = 0; d < D; ++d) bgv += a.backgrounds[c * D + d] * Drc[d];
-      bgt = bgv * Tf;
-    }
-    T = Tf;
-    if (cend < tend && mylast >= cend) {
-      // a chunk followed by others in which the pixel still blends: start
-      // from the forward's state at the boundary cend (transmittance), and
-      // the suffix colour sum of the later chunks up to its last id (their
-      // chunk-local sums S), dotted with dL/dcolour.  (mylast < cend: the
-      // transmittance at cend is the final one, Tf, and nothing follows.)
-      const int p = (threadIdx.x >> 6) * 64 + lane;
-      const int64_t per = (int64_t)(kTS * kTS * (1 + D));
-      T = fabsf(a.state[(cend / a.L) * per + p]);
-      float s = 0.f;
-      for (int64_t bi = cend; bi <= mylast; bi += a.L) {
-        const float *sl = a.state + (bi / a.L) * per;
-#pragma unroll
-        for (int d = 0; d < D; ++d) s += sl[(1 + d) * kTS * kTS + p] * Drc[d];
-      }
-      rD = s;
-    }
-  }
-  const float TfDra = Tf * Dra;
-  int32_t lmax = mylast;
-#pragma unroll
-  for (int msk = 32; msk >= 1; msk >>= 1) lmax = max(lmax, __shfl_xor(lmax, msk, 64));
-  const int64_t end = min(cend, (int64_t)lmax + 1);
-
-  if (start < end) {
-    // the batch ending at b1 covers [max(start, b1 - 64), b1); lane l holds
-    // isect b1 - 64 + l (clamped into the range, masked when below start)
-    auto id_at = [&](int64_t b1) -> int32_t {
-      return a.flatten_ids[max(b1 - 64 + lane, start)];
-    };
-    auto stage = [&](const Attr<D> &at, int64_t b1) -> int {
-      const int64_t j = b1 - 64 + lane;
-      const bool keep = (j >= start) && keep_attr<D>(at, geo.x0, geo.x1, geo.y0, geo.y1);
-      const uint64_t m = __ballot(keep);
-      const int cnt = __popcll(m);
-      if (keep) stage_bwd_pair<D>(st, ballot_slot(m), at, (int32_t)j);
-      if ((cnt & 1) && lane == 0) stage_bwd_pad<D>(st, cnt);
-      wave_sync_lds();
-      return cnt;
-    };
-    // per-field scale applied once after the lane reduction: colours,
-    // opacity as accumulated; means2d from aD * (gx, gy): -2 / log2(e);
-    // conic from aD * (dx^2, dx dy, dy^2): (-1/2, -1, -1/2); |means2d|: 2 / log2(e)
-    const int lf = rs_field(lane);
-    auto field_scale = [&](int f) -> float {
-      constexpr float m2 = -2.f / kLog2e;
-      if (f < D + 1) return 1.f;
-      if (f < D + 3) return m2;
-      if (f == D + 3 || f == D + 5) return -0.5f;
-      if (f == D + 4) return -1.f;
-      return -m2;
-    };
-    // one record of a pair, back to front: sequential in T and rD
-    auto grad_seq = [&](bool valid, bool unclamped, float al, float ra, float gD, float &w,
-                        float &Da) {
-      T = valid ? T * ra : T;
-      w = valid ? al * T : 0.f;
-      rD += gD * w;
-      const float Da_raw = ra * (TfDra + T * gD - rD - bgt);
-      // clamped alpha (> 0.999) has no gradient (rasterize_to_pixels_bwd.py:184-187)
-      Da = (valid & unclamped) ? Da_raw : 0.f;
-    };
-    auto composite = [&](int cnt) {
-      for (int p = (cnt - 1) >> 1; p >= 0; --p) {
-        const float4 *q = st + p * N4;
-        float4 vv[N4];
-#pragma unroll
-        for (int i = 0; i < N4; ++i) vv[i] = q[i];
-        f2v f[2 * N4];
-#pragma unroll
-        for (int i = 0; i < N4; ++i) {
-          asm volatile("" ::"v"(vv[i].x), "v"(vv[i].y), "v"(vv[i].z), "v"(vv[i].w));
-          f[2 * i] = f2v{vv[i].x, vv[i].y};
-          f[2 * i + 1] = f2v{vv[i].z, vv[i].w};
-        }
-        const f2v dx = f[0] - fx, dy = f[1] - fy;
-        const f2v gx = f[2] * dx + f[3] * dy, gy = f[3] * dx + f[4] * dy;
-        const f2v s2 = dx * gx + dy * gy;  // sigma * log2(e)
-        const f2v ex = f2v{__builtin_amdgcn_exp2f(-s2.x), __builtin_amdgcn_exp2f(-s2.y)};
-        const f2v ar = f[5] * ex;  // alpha before the 0.999 clamp
-        const bool v0 = (__float_as_uint(s2.x) <= __float_as_uint(f[6].x)) &&
-                        (__float_as_int(f[7].x) <= mylast);
-        const bool v1 = (__float_as_uint(s2.y) <= __float_as_uint(f[6].y)) &&
-                        (__float_as_int(f[7].y) <= mylast);
-        if (__ballot(v0 | v1) == 0) continue;
-        if (a.lanehist) {
-          const int c0 = __popcll(__ballot(v0)), c1 = __popcll(__ballot(v1));
-          if (lane == 0) {
-            atomicAdd(&a.lanehist[c0], 1ull);
-            if (__float_as_int(f[8].y) >= 0) atomicAdd(&a.lanehist[c1], 1ull);
-          }
-        }
-        const f2v al = f2v{fminf(ar.x, kAlphaMax), fminf(ar.y, kAlphaMax)};
-        const f2v om = 1.f - al;
-        const f2v ra = f2v{__builtin_amdgcn_rcpf(om.x), __builtin_amdgcn_rcpf(om.y)};
-        f2v gD = f[9] * Drc[0];
-#pragma unroll
-        for (int d = 1; d < D; ++d) gD = __builtin_elementwise_fma(f[9 + d], f2v{Drc[d], Drc[d]}, gD);
-        float w1, Da1, w0, Da0;
-        grad_seq(v1, ar.y <= kAlphaMax, al.y, ra.y, gD.y, w1, Da1);  // later record first
-        grad_seq(v0, ar.x <= kAlphaMax, al.x, ra.x, gD.x, w0, Da0);
-        const f2v w = f2v{w0, w1}, Da = f2v{Da0, Da1};
-        const f2v aD = al * Da;
-        f2v v[NV * 16];
-#pragma unroll
-        for (int k = 0; k < NV * 16; ++k) v[k] = f2v{0.f, 0.f};
-#pragma unroll
-        for (int d = 0; d < D; ++d) v[d] = w * Drc[d];
-        v[D] = Da * ex;
-        v[D + 1] = aD * gx;
-        v[D + 2] = aD * gy;
-        const f2v P_ = aD * dx, Q_ = aD * dy;
-        v[D + 3] = P_ * dx;
-        v[D + 4] = P_ * dy;
-        v[D + 5] = Q_ * dy;
-        if (ABS) {
-          v[D + 6] = f2v{fabsf(v[D + 1].x), fabsf(v[D + 1].y)};
-          v[D + 7] = f2v{fabsf(v[D + 2].x), fabsf(v[D + 2].y)};
-        }
-        const int g0 = __float_as_int(f[8].x), g1 = __float_as_int(f[8].y);
-#pragma unroll
-        for (int qq = 0; qq < NV; ++qq) {
-          constexpr int NQ = F - 16 * (NV - 1);  // fields in the last group
-          const f2v tot = qq < NV - 1 ? reduce_scatter2<16>(v + 16 * qq, lane)
-                                      : reduce_scatter2<NQ>(v + 16 * qq, lane);
-          const int field = 16 * qq + lf;
-          if ((lane & 3) == 0 && lf < (qq < NV - 1 ? 16 : NQ) && !(a.dbg & 1)) {
-            const float sc = field_scale(field);
-            if (tot.x != 0.f) atomic_add_f32(a.packed + (int64_t)g0 * a.S + field, sc * tot.x);
-            if (g1 >= 0 && tot.y != 0.f)
-              atomic_add_f32(a.packed + (int64_t)g1 * a.S + field, sc * tot.y);
-          }
-        }
-      }
-    };
-    // The backward is throughput-bound (many waves per SIMD hide the gather
-    // latency; long tiles are split into chunk items), so it prefetches only
-    // the next batch's flatten ids and spends no registers on a second
-    // attribute buffer.
-    int32_t g_n = id_at(end);
-    for (int64_t b1 = end; b1 > start; b1 -= 64) {
-      Attr<D> A;
-      load_attr<D>(a, g_n, A);
-      g_n = id_at(b1 - 64);
-      composite(stage(A, b1));
-      wave_sync_lds();
-    }
-  }
-  tl_store(a, t_start, lane);
-}
-
-// Backward, PX pixels per lane (PX = 2 or 4): a wave owns a 16 x 4PX band
+// Backward, PX pixels per lane (the default PX = 2): a wave owns a 16 x 4PX band
 // of the tile, lane l the pixels (l & 15, 4PX w + 4q + (l >> 4)), q < PX, and
 // the 4/PX waves of a workgroup cover the tile.  Each record's gradient
 // terms of the PX pixels are summed in-lane before the one reduce-scatter and
@@ -1421,6 +1218,106 @@ tile_order_kernel(int n_tiles, const int32_t *__restrict__ offsets, int64_t n_is
   }
 }
 
+// XCD-grouped dispatch order: the same heaviest-first buckets, per 2x2 group
+// of neighbouring tiles instead of per tile (a group's bucket is its heaviest
+// tile's), and the four tiles of group q (q-th in that order) in slots
+// 32 (q / 8) + q % 8 + 8 k, k < 4.  Workgroup b runs on XCD b % 8, so a
+// group's tiles run on ONE XCD, dispatched together: the Gaussians they share
+// (at M3 a visible Gaussian covers ~5.5 tiles) are fetched into one L2 instead
+// of up to four.  Slots of missing tiles (image edges) hold -1 (the workgroup
+// exits); the grid covers order_slots() = 32 ceil(groups / 8) slots.  One
+// 1024-lane workgroup, up to 8 groups per lane (8192 groups).
+constexpr int kGS = 2;  // group side, tiles
+__host__ __device__ inline int order_groups(int C, int tw, int th) {
+  return C * ((tw + kGS - 1) / kGS) * ((th + kGS - 1) / kGS);
+}
+__global__ void __launch_bounds__(1024)
+tile_order_grouped_kernel(int C, int tw, int th, const int32_t *__restrict__ offsets,
+                          int64_t n_isects, const int64_t *__restrict__ n_dev,
+                          int32_t *__restrict__ order, int32_t *__restrict__ max_out) {
+  constexpr int MAXPER = 8;
+  __shared__ uint64_t wsum[16];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int gw = (tw + kGS - 1) / kGS, gh = (th + kGS - 1) / kGS, ng = C * gw * gh;
+  const int n_tiles = C * tw * th;
+  // the tiles of group g (-1: outside the grid)
+  auto tiles_of = [&](int g, int (&t)[kGS * kGS]) {
+    const int c = g / (gw * gh), r = g - c * (gw * gh);
+    const int gy = r / gw, gx = r - gy * gw;
+#pragma unroll
+    for (int k = 0; k < kGS * kGS; ++k) {
+      const int ty = gy * kGS + k / kGS, tx = gx * kGS + k % kGS;
+      t[k] = (tx < tw && ty < th) ? (c * th + ty) * tw + tx : -1;
+    }
+  };
+  int bucket[MAXPER];
+  uint64_t mine = 0;
+  int64_t nmax = 0;
+#pragma unroll
+  for (int i = 0; i < MAXPER; ++i) {
+    const int g = tid + 1024 * i;
+    bucket[i] = -1;
+    if (g < ng) {
+      int t[kGS * kGS];
+      tiles_of(g, t);
+      int64_t gm = 0;
+#pragma unroll
+      for (int k = 0; k < kGS * kGS; ++k)
+        if (t[k] >= 0)
+          gm = max(gm, tile_end(offsets, t[k], n_tiles, n_dev, n_isects) - offsets[t[k]]);
+      nmax = max(nmax, gm);
+      bucket[i] = gm >= 2048 ? 0 : gm >= 1024 ? 1 : gm >= 512 ? 2 : 3;
+      mine += (uint64_t)1 << (16 * bucket[i]);
+    }
+  }
+  block_max_out(nmax, max_out);
+  uint64_t x = mine;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint64_t y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) wsum[w] = x;
+  __syncthreads();
+  uint64_t before = 0, total = 0;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    before += i < w ? wsum[i] : 0;
+    total += wsum[i];
+  }
+  before += x - mine;
+  int pos[4], base = 0;
+#pragma unroll
+  for (int bk = 0; bk < 4; ++bk) {
+    pos[bk] = base + (int)((before >> (16 * bk)) & 0xffff);
+    base += (int)((total >> (16 * bk)) & 0xffff);
+  }
+  auto slot = [](int q, int k) { return 32 * (q >> 3) + (q & 7) + 8 * k; };
+#pragma unroll
+  for (int i = 0; i < MAXPER; ++i) {
+    const int bk = bucket[i];
+    if (bk >= 0) {
+      int q = pos[0];
+      q = bk == 1 ? pos[1] : q;
+      q = bk == 2 ? pos[2] : q;
+      q = bk == 3 ? pos[3] : q;
+      int t[kGS * kGS];
+      tiles_of(tid + 1024 * i, t);
+#pragma unroll
+      for (int k = 0; k < kGS * kGS; ++k) order[slot(q, k)] = t[k];
+      pos[0] += bk == 0;
+      pos[1] += bk == 1;
+      pos[2] += bk == 2;
+      pos[3] += bk == 3;
+    }
+  }
+  // the slots of the group positions past the last group (up to a multiple of 8)
+  const int q_end = (ng + 7) & ~7;
+  for (int q = ng + tid; q < q_end; q += 1024)
+#pragma unroll
+    for (int k = 0; k < kGS * kGS; ++k) order[slot(q, k)] = -1;
+}
+
 // Forward plan with split heavy tiles, decided on this render's tiles.  A
 // tile with more than `split` isects is rendered as ceil(n / SL) chunks that
 // run in parallel in a launch of their own (see "Split heavy tiles"), so the
@@ -1673,7 +1570,7 @@ static int g_fwd_split = INT32_MIN;  // not yet read from the environment
 static int fwd_split_mode() {
   if (g_fwd_split == INT32_MIN) {
     const char *e = getenv("GSPLAT_HIP_FWD_SPLIT");
-    g_fwd_split = e ? atoi(e) : -1;
+    g_fwd_split = (e && *e) ? atoi(e) : -1;  // (set but empty: the default)
     if (g_fwd_split < 0) g_fwd_split = -1;
   }
   return g_fwd_split;
@@ -1778,8 +1675,22 @@ static SplitLayout split_layout(int D, int n_tiles, int64_t n_isects) {
   return l;
 }
 
+// XCD-grouped forward order (tile_order_grouped_kernel): GSPLAT_HIP_DBG bit 4
+// selects it (A/B experiment; the unsplit forward only)
+static int dbg_flags();
+static int order_slots(int C, int tw, int th) {
+  return 32 * ((r16::order_groups(C, tw, th) + 7) / 8);
+}
+static bool grouped_order(int C, int tw, int th) {
+  const int64_t n_tiles = (int64_t)C * tw * th;
+  return (dbg_flags() & 16) && r16::order_groups(C, tw, th) <= 8192 &&
+         order_slots(C, tw, th) <= 2 * n_tiles + 64;
+}
+
 static int64_t order_bytes(int n_tiles, int64_t n_isects) {
-  return use_order(n_tiles, n_isects) ? align256(4 * (int64_t)n_tiles) : 0;
+  // room for the grouped order's slots too (32 ceil(groups / 8) <= 2 n_tiles
+  // + 64 for any grid)
+  return use_order(n_tiles, n_isects) ? align256(4 * (2 * (int64_t)n_tiles + 64)) : 0;
 }
 
 static int64_t n_items_bound(int n_tiles, int64_t n_isects) {
@@ -1792,31 +1703,12 @@ int64_t rasterize16_fwd_state_bytes(int D, int n_tiles, int64_t n_isects) {
          split_layout(D, n_tiles, n_isects).bytes;
 }
 
-// Pixels per lane in the backward (1: bwd_kernel, 16x4 per wave; 2 or 4:
-// bwd2_kernel, 16x8 or 16x16 per wave).  GSPLAT_HIP_BWD_PX overrides it.
-// With render records and the batch prefetch, 2 measured 0.427-0.430 ms at
-// M2 against 0.465-0.473 for 4 (profiles/r2_s4_bwdpf; 4 was ahead before
-// the records: its 160 VGPRs leave 3 waves per SIMD, 2 keeps 4).
-static int bwd_px() {
-  static const int v = [] {
-    const char *e = getenv("GSPLAT_HIP_BWD_PX");
-    const int x = e ? atoi(e) : 2;
-    return (x == 1 || x == 4) ? x : 2;
-  }();
-  return v;
-}
-
-// Backward record prefetch one batch ahead (bwd2_kernel PFB), default on
-// (PX 2: 0.427 vs 0.430 ms; PX 4 spills and runs slower with it);
-// GSPLAT_HIP_BWD_PF=0 turns it off.
-static bool bwd_pf() {
-  static const bool v = [] {
-    const char *e = getenv("GSPLAT_HIP_BWD_PF");
-    return !(e && atoi(e) == 0) && bwd_px() == 2;
-  }();
-  return v;
-}
-
+// The backward: two pixels per lane (bwd2_kernel<PX = 2>, a 16x8 band per
+// wave) with the next batch's records gathered while the current one
+// composites (PFB).  Measured against the alternatives, which were removed:
+// one pixel per lane (16x4, 7 waves per SIMD) and four (16x16, 3 waves per
+// SIMD) ran 0.47 / 0.465-0.473 ms against 0.427-0.430 ms at M2
+// (profiles/r2_s4_bwdpf); without the prefetch 0.430 ms.
 // One pixel per lane in the forward (16x4 per wave).  A two-pixel kernel
 // (16x8 per wave, two transmittance chains per lane) measured 0.29 ms against
 // 0.216 at M2 (158 VGPRs, 3 waves per SIMD, and the heaviest tiles' serial
@@ -1837,9 +1729,10 @@ static int dbg_flags() {
 static thread_local const void *g_prepared_state = nullptr;
 static thread_local bool g_prepared_split = false;  // the split decision of that preparation
 
-static void launch_order(int n_tiles, const int32_t *offsets, int64_t n_isects,
+static void launch_order(int C, int tw, int th, const int32_t *offsets, int64_t n_isects,
                          const int64_t *n_dev, int32_t *order, hipStream_t st,
                          char *split_base, int D) {
+  const int n_tiles = C * tw * th;
   if (split_base) {
     const SplitLayout l = split_layout(D, n_tiles, n_isects);
     hipLaunchKernelGGL(r16::fwd_plan_kernel, dim3(1), dim3(1024), 0, st, n_tiles, offsets,
@@ -1849,17 +1742,22 @@ static void launch_order(int n_tiles, const int32_t *offsets, int64_t n_isects,
                        reinterpret_cast<int2 *>(split_base + l.fitems),
                        reinterpret_cast<int32_t *>(split_base + l.pflag),
                        reinterpret_cast<int32_t *>(split_base + l.ctr), stat_dev());
-  } else
+  } else if (grouped_order(C, tw, th)) {
+    hipLaunchKernelGGL(r16::tile_order_grouped_kernel, dim3(1), dim3(1024), 0, st, C, tw, th,
+                       offsets, n_isects, n_dev, order,
+                       split_capable(n_tiles, n_isects) ? stat_dev() : nullptr);
+  } else {
     hipLaunchKernelGGL(r16::tile_order_kernel, dim3(1), dim3(1024), 0, st, n_tiles, offsets,
                        n_isects, n_dev, order,
                        split_capable(n_tiles, n_isects) ? stat_dev() : nullptr);
+  }
 }
 
 template <int D>
 int r16_fwd(r16::Args a, const void *state, char *split_base, hipStream_t st) {
   if (a.order && state != g_prepared_state)
-    launch_order(a.n_tiles, a.offsets, a.n_isects, a.n_dev, const_cast<int32_t *>(a.order), st,
-                 split_base, D);
+    launch_order(a.C, a.tw, a.th, a.offsets, a.n_isects, a.n_dev, const_cast<int32_t *>(a.order),
+                 st, split_base, D);
   g_prepared_state = nullptr;
   if (split_base) {
     // the split tiles' chunks and the other tiles in one launch; the grid is
@@ -1873,7 +1771,9 @@ int r16_fwd(r16::Args a, const void *state, char *split_base, hipStream_t st) {
     GS_CHECK_LAUNCH("rasterize_fwd16_split");
     return 0;
   }
-  hipLaunchKernelGGL((r16::fwd_kernel<D>), dim3(a.n_tiles), dim3(256), 0, st, a);
+  const int grid = (a.order && grouped_order(a.C, a.tw, a.th)) ? order_slots(a.C, a.tw, a.th)
+                                                                 : a.n_tiles;
+  hipLaunchKernelGGL((r16::fwd_kernel<D>), dim3(grid), dim3(256), 0, st, a);
   GS_CHECK_LAUNCH("rasterize_fwd16");
   return 0;
 }
@@ -1927,9 +1827,7 @@ int r16_bwd(r16::Args a, int64_t G, float *v_means2d, float *v_conics, float *v_
   const bool chunked = a.n_isects > 0 && a.state && a.L > 0 && a.render_colors_in;
   // the gradient rows and, right after them, the item counters
   const size_t pb = packed_bytes(D, ABS, G);
-  // (GSPLAT_HIP_MEMSET_NODES=1, diagnosis only: the whole table and the
-  // counters by hipMemsetAsync, as the round-3 step captured them)
-  if (visible && G > 0 && !gs::memset_nodes()) {
+  if (visible && G > 0) {
     // the counters start at byte pb (the table padded to 256 B): zero from
     // the table's end through them
     const int64_t tail = (int64_t)(pb / 4) - G * a.S + (chunked ? 64 : 0);
@@ -1960,18 +1858,8 @@ int r16_bwd(r16::Args a, int64_t G, float *v_means2d, float *v_conics, float *v_
       a.items = nullptr;
       a.n_items = nullptr;
     }
-    if (bwd_px() == 2 && bwd_pf())
-      hipLaunchKernelGGL((r16::bwd2_kernel<D, ABS, 2, true>), dim3((unsigned)grid), dim3(128), 0,
-                         st, a);
-    else if (bwd_px() == 2)
-      hipLaunchKernelGGL((r16::bwd2_kernel<D, ABS, 2>), dim3((unsigned)grid), dim3(128), 0, st, a);
-    else if (bwd_px() == 4 && bwd_pf())
-      hipLaunchKernelGGL((r16::bwd2_kernel<D, ABS, 4, true>), dim3((unsigned)grid), dim3(64), 0,
-                         st, a);
-    else if (bwd_px() == 4)
-      hipLaunchKernelGGL((r16::bwd2_kernel<D, ABS, 4>), dim3((unsigned)grid), dim3(64), 0, st, a);
-    else
-      hipLaunchKernelGGL((r16::bwd_kernel<D, ABS>), dim3((unsigned)grid), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((r16::bwd2_kernel<D, ABS, 2, true>), dim3((unsigned)grid), dim3(128), 0,
+                       st, a);
     GS_CHECK_LAUNCH("rasterize_bwd16");
   }
   if (G > 0) {
@@ -2037,9 +1925,10 @@ int rasterize16_fwd(int C, int D, int W, int H, int tw, int th, const float *mea
   GS_REQUIRE(false, "rasterize16_fwd: unsupported channels %d", D);
 }
 
-int rasterize16_prepare(int D, int n_tiles, const int32_t *offsets, int64_t n_isects,
+int rasterize16_prepare(int D, int C, int tw, int th, const int32_t *offsets, int64_t n_isects,
                         const int64_t *n_isects_dev, void *state, int64_t state_bytes,
                         hipStream_t st) {
+  const int n_tiles = C * tw * th;
   g_prepared_state = nullptr;
   if (!state || !use_order(n_tiles, n_isects)) return 0;
   GS_REQUIRE(state_bytes >= rasterize16_fwd_state_bytes(D, n_tiles, n_isects),
@@ -2047,7 +1936,7 @@ int rasterize16_prepare(int D, int n_tiles, const int32_t *offsets, int64_t n_is
   char *base = reinterpret_cast<char *>(state) + chunk_slot_bytes(D, n_isects);
   int32_t *order = reinterpret_cast<int32_t *>(base);
   const bool split = chunk_slot_bytes(D, n_isects) > 0 && use_split_now(n_tiles, n_isects);
-  launch_order(n_tiles, offsets, n_isects, n_isects_dev, order, st,
+  launch_order(C, tw, th, offsets, n_isects, n_isects_dev, order, st,
                split ? base + order_bytes(n_tiles, n_isects) : nullptr, D);
   GS_CHECK_LAUNCH("rasterize_prepare");
   g_prepared_state = state;
@@ -2081,7 +1970,6 @@ int rasterize16_bwd(int C, int64_t G, int D, int W, int H, int tw, int th,
   a.n_isects = n_isects;
   a.timeline = (g_timeline && g_timeline_waves >= 4 * n_items_bound(a.n_tiles, n_isects))
                    ? g_timeline : nullptr;
-  a.lanehist = g_lanehist;
   a.means2d = means2d; a.conics = conics; a.colors = colors; a.opacities = opacities;
   a.backgrounds = backgrounds; a.masks = masks; a.offsets = offsets; a.flatten_ids = flatten_ids;
   a.render_alphas = const_cast<float *>(render_alphas);
@@ -2143,11 +2031,6 @@ extern "C" int gsplat_hip_debug_set_flags(int flags) {
 extern "C" int gsplat_hip_debug_set_chunk(int isects) {
   gs::g_chunk = isects <= 0 ? 0 : ((isects + 63) / 64) * 64;
   return gs::g_chunk;
-}
-
-extern "C" int gsplat_hip_debug_set_lane_histogram(unsigned long long *device_buffer) {
-  gs::g_lanehist = device_buffer;
-  return 0;
 }
 
 extern "C" int gsplat_hip_debug_set_timeline(uint64_t *device_buffer, int64_t capacity_waves) {

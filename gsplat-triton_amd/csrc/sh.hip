@@ -304,20 +304,13 @@ struct AdamSH {
   // read on the device, and a void step (*skip != 0) leaves the state alone
   const float *hyper;
   const int32_t *skip;
-  int nt;  // non-temporal row loads / stores (GSPLAT_HIP_SH_ADAM_NT, default on)
+  int nt;  // non-temporal row loads / stores (always on)
 };
 
 // The rows are touched once per step: non-temporal loads / stores stream
-// them past the caches (M2 804.8 / 805.4 against 795.3 / 797.2 images/s,
-// alternating in one call, profiles/r4_batch10/).  GSPLAT_HIP_SH_ADAM_NT=0
-// turns them off.
-static int sh_adam_nt() {
-  static const int v = [] {
-    const char *e = getenv("GSPLAT_HIP_SH_ADAM_NT");
-    return e ? atoi(e) : 1;
-  }();
-  return v;
-}
+// them past the caches (M2 804.8 / 805.4 against 795.3 / 797.2 images/s
+// with plain accesses, alternating in one call, profiles/r4_batch10/).
+static int sh_adam_nt() { return 1; }
 typedef float f4v __attribute__((ext_vector_type(4)));
 GS_INLINE float4 ld4(const float4 *p, bool nt) {
   if (nt) {

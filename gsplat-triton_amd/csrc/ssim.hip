@@ -774,18 +774,10 @@ static float n_map(int B, int H, int W, int C) { return (float)B * C * (H - 10) 
 static float n_img(int B, int H, int W, int C) { return (float)B * C * H * W; }
 
 // The forward with all channels of a tile in one workgroup (fwd_c_kernel,
-// C = 3; 66 -> 56 us at 1080p); GSPLAT_HIP_SSIM_PER_IMAGE=0 selects the
-// one-channel-per-workgroup kernel.  The same change in the backward (map
+// C = 3; 66 -> 56 us at 1080p against one channel per workgroup, fwd_kernel,
+// which other channel counts use).  The same change in the backward (map
 // windows of all channels in one round) measured slower, 81 vs 62 us: its
 // 99 map values per lane in flight cost occupancy the blur needs.
-static bool ssim_per_image() {
-  static const bool v = [] {
-    const char *e = getenv("GSPLAT_HIP_SSIM_PER_IMAGE");
-    return !(e && atoi(e) == 0);
-  }();
-  return v;
-}
-
 static int ssim_fwd(int B, int H, int W, int C, const float *img1, const float *img2,
                     float *sums, float *loss, float lam, void *workspace, void *stream) {
   GS_REQUIRE(B > 0 && C > 0 && H > 10 && W > 10,
@@ -794,7 +786,7 @@ static int ssim_fwd(int B, int H, int W, int C, const float *img1, const float *
   float *maps = reinterpret_cast<float *>(workspace);
   float *partials = maps + ssim_map_floats(B, H, W, C);
   const int n_tiles = ((W - 10 + 31) / 32) * ((H - 10 + 31) / 32);
-  if (C == 3 && ssim_per_image()) {
+  if (C == 3) {
     hipLaunchKernelGGL(ssim::fwd_c_kernel<3>, dim3((unsigned)(n_tiles * B)), dim3(256), 0, st, B,
                        H, W, img1, img2, maps, partials);
     hipLaunchKernelGGL(ssim::reduce_partials_kernel, dim3(1), dim3(1024), 0, st, n_tiles * B,
@@ -855,16 +847,7 @@ static int64_t fused_tiles(int H, int W) {
 
 extern "C" int64_t gsplat_hip_l1_ssim_loss_fused_workspace_bytes(int B, int H, int W, int C) {
   if (H <= 10 || W <= 10) return 0;
-  return (int64_t)sizeof(float) * 2 * B * fused_tiles(H, W) * (C == 3 ? 3 : 1);
-}
-
-// Channels per workgroup of the fused loss (GSPLAT_HIP_SSIM_CPW: 3 or 1)
-static int ssim_cpw() {
-  static const int v = [] {
-    const char *e = getenv("GSPLAT_HIP_SSIM_CPW");
-    return (e && atoi(e) == 1) ? 1 : 3;
-  }();
-  return v;
+  return (int64_t)sizeof(float) * 2 * B * fused_tiles(H, W);
 }
 
 static int fused_fwd(int B, int H, int W, int C, int XS, const float *img1, const float *img2,
@@ -879,27 +862,27 @@ static int fused_fwd(int B, int H, int W, int C, int XS, const float *img1, cons
   GS_REQUIRE(XS >= C, "l1_ssim_loss_fused_fwd: pixel stride %d < C = %d", XS, C);
   hipStream_t st = (hipStream_t)stream;
   float *partials = reinterpret_cast<float *>(workspace);
-  const int cg = C == 3 ? 3 / ssim_cpw() : 1;  // workgroups per tile
-  const int64_t nt = fused_tiles(H, W) * cg, per = (nt + 7) / 8;
+  // one workgroup per tile, all its channels (one channel per workgroup --
+  // three times the workgroups at a third of the LDS each -- measured 112-114
+  // us either way, M2 805.2 / 809.7 against 813.3 / 811.4 images/s,
+  // profiles/r5/b10; removed)
+  const int64_t nt = fused_tiles(H, W), per = (nt + 7) / 8;
   const dim3 grid((unsigned)(B * 8 * per));
   const float cs = -lam / n_map(B, H, W, C), cl = (1.f - lam) / n_img(B, H, W, C);
-  static const int fv = [] {
-    const char *e = getenv("GSPLAT_HIP_SSIM_FV");
-    return e ? atoi(e) : 0;
-  }();
 #define GS_FUSED(CC, BR, CPW, XS_)                                                           \
   hipLaunchKernelGGL((ssim::fused_kernel<CC, BR, CPW, XS_>), grid, dim3(ssim::kFThreads), 0, st, \
                      B, H, W, img1, img2, img2_index, cs, cl, grad_unit, partials)
   GS_REQUIRE(XS == C || (C == 3 && XS == 4),
              "l1_ssim_loss_fused_fwd: pixel stride %d with C = %d (supported: C, or 4 with C = 3)",
              XS, C);
+  // map rows per pass-B item: 4 for the contiguous RGB images; 2 for an
+  // RGB+D render read in place (x stride 4: the 4-row form spilled 25 VGPRs
+  // there, 171.5 against 125.3 us; the 2-row form for the contiguous loss
+  // measured M2 814.0 / 817.2 against 817.6 / 817.8 images/s, profiles/r5/b22)
   if (C == 3 && XS == 4) {
-    if (cg == 3) GS_FUSED(3, 4, 1, 4);
-    else GS_FUSED(3, 2, 3, 4);
+    GS_FUSED(3, 2, 3, 4);
   } else if (C == 3) {
-    if (cg == 3) GS_FUSED(3, 4, 1, 3);
-    else if (fv == 1) GS_FUSED(3, 2, 3, 3);
-    else GS_FUSED(3, 4, 3, 3);
+    GS_FUSED(3, 4, 3, 3);
   } else {
     GS_FUSED(1, 2, 1, 1);
   }

@@ -1722,21 +1722,11 @@ bool channels_supported(int D) {
   return false;
 }
 
-bool fwd2_enabled() {
-  static const bool v = [] {
-    const char *e = getenv("GSPLAT_HIP_FWD_PX");
-    return !(e && atoi(e) == 1);
-  }();
-  return v;
-}
-
-bool bwd2_enabled() {
-  static const bool v = [] {
-    const char *e = getenv("GSPLAT_HIP_BWD_PX");
-    return !(e && atoi(e) == 1);
-  }();
-  return v;
-}
+// 16x16 tiles: two pixels per lane in the forward and the backward (fwd2 /
+// bwd2 kernels; the one-pixel kernels, which measured 1.62 / 1.76 against
+// 1.10 / 1.63 ms at M5, serve the other tile sizes)
+bool fwd2_enabled() { return true; }
+bool bwd2_enabled() { return true; }
 
 int fields_stride(int D, int absgrad) {
   const int nf = D + 15 + (absgrad ? 2 : 0);
@@ -1746,14 +1736,6 @@ int fields_stride(int D, int absgrad) {
 int lean_stride(int D, int absgrad) {  // Fields<D, ABS, true>::S
   const int nf = D + 12 + (absgrad ? 2 : 0);
   return 16 * ((nf + 15) / 16);
-}
-
-bool lean_enabled() {
-  static const bool v = [] {
-    const char *e = getenv("GSPLAT_HIP_SURFEL_LEAN");
-    return !(e && atoi(e) == 0);
-  }();
-  return v;
 }
 
 int check_tiles(int C, int W, int H, int ts, int tw, int th) {
@@ -2002,7 +1984,7 @@ extern "C" int gsplat_hip_rasterize_2dgs_fwd(
                        n_isects, n_isects_device, tile_order);
     a.order = tile_order;
   }
-  // 16x16 tiles: two pixels per lane (fwd2_kernel) unless GSPLAT_HIP_FWD_PX=1
+  // 16x16 tiles: two pixels per lane (fwd2_kernel)
   const bool px2 = tile_size == 16 && fwd2_enabled();
   if (records) {  // scalar-operand records (gsplat_hip_rasterize_2dgs_pack_records)
     GS_REQUIRE(px2 && D <= kSRecMaxD, "rasterize_2dgs_fwd: records need 16x16 tiles, D <= %d",
@@ -2084,14 +2066,11 @@ extern "C" int gsplat_hip_rasterize_2dgs_bwd(
   GS_REQUIRE(channels_supported(D), "rasterize_2dgs_bwd: unsupported channel count %d", D);
   GS_REQUIRE(tile_size * tile_size <= 256, "rasterize_2dgs_bwd: tile_size %d > 16", tile_size);
   const int absgrad = v_means2d_abs != nullptr;
-  // LEAN kernels (bwd2_kernel): 16x16 tiles, D <= 4, no normal / distortion /
-  // median gradient (GSPLAT_HIP_SURFEL_LEAN=0: the general kernel)
-  // a colours-only forward (no median ids) has only the LEAN backward: it
-  // is taken whatever GSPLAT_HIP_SURFEL_LEAN / GSPLAT_HIP_BWD_PX say
-  const bool colors_only = !median_ids;
-  const bool px2 = tile_size == 16 && (bwd2_enabled() || colors_only);
-  const bool lean = px2 && D <= 4 && (lean_enabled() || colors_only) && !v_render_normals &&
-                    !v_render_distort && !v_render_median;
+  // LEAN kernels (bwd2_kernel, 16x16 tiles, D <= 4) whenever no normal / distortion / median gradient is
+  // asked for (a colours-only forward, which writes no median ids, has only
+  // that backward)
+  const bool px2 = tile_size == 16 && bwd2_enabled();
+  const bool lean = px2 && D <= 4 && !v_render_normals && !v_render_distort && !v_render_median;
   const int S = lean ? lean_stride(D, absgrad) : fields_stride(D, absgrad);
   const int64_t G = n_gaussians;
   GS_REQUIRE(workspace_bytes >= G * S * (int64_t)sizeof(float),
@@ -2128,7 +2107,7 @@ extern "C" int gsplat_hip_rasterize_2dgs_bwd(
     a.v_render_median = v_render_median;
     a.packed = (float *)workspace; a.S = S;
     const int waves = (tile_size * tile_size + 63) / 64;
-    // 16x16 tiles: two pixels per lane (bwd2_kernel) unless GSPLAT_HIP_BWD_PX=1
+    // 16x16 tiles: two pixels per lane (bwd2_kernel)
 #define GS_CASE(n)                                                                            \
   if (D == n) {                                                                               \
     const size_t lds = (size_t)waves * 64 * Rec<n>::NF * sizeof(float);                       \

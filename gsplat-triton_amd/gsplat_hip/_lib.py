@@ -79,7 +79,6 @@ _SIGS = {
                                         _p, _p, _p, _p, _p, _i64, _p, _p, _p, _p, _p, _p, _p, _p,
                                         _p, _p, _p, _p, _p, _p, _i64, _p, _i64, _p, _p, _p]),
     "gsplat_hip_debug_set_timeline": (_i32, [_p, _i64]),
-    "gsplat_hip_debug_set_lane_histogram": (_i32, [_p]),
     "gsplat_hip_debug_set_chunk": (_i32, [_i32]),
     "gsplat_hip_debug_set_flags": (_i32, [_i32]),
     "gsplat_hip_debug_set_fwd_split": (_i32, [_i32]),
@@ -109,8 +108,6 @@ _SIGS = {
                                             _p]),
     "gsplat_hip_adam_step_dev": (_i32, [_i32, _p, _p, _p, _p, _p, _p, _p, _p, _f, _f, _f, _p, _p]),
     "gsplat_hip_adam_step_ex": (_i32, [_i32, _p, _p, _p, _p, _p, _p, _p, _p, _f, _f, _f, _i32, _p]),
-    "gsplat_hip_adam_step_bounded": (_i32, [_i32, _p, _p, _p, _p, _p, _p, _f, _f, _f, _i32, _i32,
-                                            _p]),
     "gsplat_hip_densify_workspace_bytes": (_i64, [_i64]),
     "gsplat_hip_densify_plan": (_i32, [_i64, _p, _p, _p, _p, _p, _f, _f, _f, _i32, _f, _f, _f,
                                        _i32, _p, _p, _p]),

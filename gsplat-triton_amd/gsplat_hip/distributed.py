@@ -367,8 +367,8 @@ def all_to_all_tensor_list(world_size: int, tensor_list: List[Tensor],
 
 # ------------------------------------------- per-camera data parallelism --
 
-def _adam_torch(params, grads, exp_avgs, exp_avg_sqs, lrs, betas, eps, step, max_blocks=0,
-                aux=None, modes=None):
+def _adam_torch(params, grads, exp_avgs, exp_avg_sqs, lrs, betas, eps, step, aux=None,
+                modes=None):
     """torch restatement of csrc/adam.hip's update (same operation order, the
     gradient transforms of gsplat_hip_adam_step_ex included), for running
     ShardedAdam's collectives on the CPU (gloo tests)."""

@@ -98,7 +98,6 @@ def graphable(tr) -> bool:
     # one rank: 3DGS or 2DGS (surfels, rasterization_2dgs with the sync-free isect)
     return (tr.fused and (tr.model == "3dgs" or (one and tr.model == "2dgs"))
             and (gshard_ok or dp_ok or (one and isinstance(tr.opt, FusedAdam)))
-            and not getattr(tr, "defer_sh", False)
             and (st is None or (not st.absgrad and tr.radii2d is None))
             and torch.device(tr.device).type == "cuda")
 
@@ -152,11 +151,6 @@ def check_kernel_nodes_only(g, allow_d2d=False):
     other = {k: v for k, v in names.items() if k not in allowed and k != "memcpy_nodes"}
     if "memcpy" in other:
         other["memcpy_nodes"] = names["memcpy_nodes"]
-    if other and os.environ.get("GSPLAT_HIP_GRAPH_ALLOW_MEMSET", "0") == "1":
-        # diagnosis only (tools/graph_diag.py memset): report and go on
-        print(f"graph census {names}; memset nodes (address, row bytes, rows, element "
-              f"size): {[(hex(a), b, c, d) for a, b, c, d in memsets]}", flush=True)
-        return names
     if other:
         raise RuntimeError(f"captured training step holds non-kernel nodes {other}; memset "
                            f"nodes (address, row bytes, rows, element size): {memsets}")

@@ -187,12 +187,11 @@ def adam_factors(lrs, betas, step):
     return [(float(np.float32(float(np.float32(lr)) / bc1)), ib) for lr in lrs]
 
 
-def adam_groups(params, grads, exp_avgs, exp_avg_sqs, lrs, betas, eps, step, max_blocks=0,
-                aux=None, modes=None, hyper=None, skip=None):
+def adam_groups(params, grads, exp_avgs, exp_avg_sqs, lrs, betas, eps, step, aux=None,
+                modes=None, hyper=None, skip=None):
     """One fused Adam launch (csrc/adam.hip) over flat float32 tensors: group
     i updates params[i] in place from grads[i] (None = zero) with its lr.
-    max_blocks > 0 bounds the grid (gsplat_hip_adam_step_bounded); aux/modes
-    form the gradient in-register (gsplat_hip_adam_step_ex); hyper (device
+    aux/modes form the gradient in-register (gsplat_hip_adam_step_ex); hyper (device
     f32[2 n], adam_factors' values) / skip (device i32 flag): the captured
     step's form (gsplat_hip_adam_step_dev; lrs and step unused)."""
     n = len(params)
@@ -202,7 +201,7 @@ def adam_groups(params, grads, exp_avgs, exp_avg_sqs, lrs, betas, eps, step, max
     head = [n, P(*[p.data_ptr() for p in params]),
             P(*[0 if g is None else g.data_ptr() for g in grads])]
     if hyper is not None:
-        assert max_blocks == 0 and hyper.dtype == torch.float32 and hyper.numel() >= 2 * n
+        assert hyper.dtype == torch.float32 and hyper.numel() >= 2 * n
         ax = [None] * n if aux is None else aux
         for a in ax:
             assert a is None or (a.is_contiguous() and a.dtype == torch.float32)
@@ -219,37 +218,24 @@ def adam_groups(params, grads, exp_avgs, exp_avg_sqs, lrs, betas, eps, step, max
             (ctypes.c_float * n)(*[float(x) for x in lrs]), float(betas[0]), float(betas[1]),
             float(eps), int(step)]
     if modes is not None and any(modes):
-        assert max_blocks == 0
         for a in aux:
             assert a is None or (a.is_contiguous() and a.dtype == torch.float32)
         _lib.call("gsplat_hip_adam_step_ex", *head,
                   P(*[0 if a is None else a.data_ptr() for a in aux]),
                   (ctypes.c_int32 * n)(*[int(m) for m in modes]), *tail, _stream())
         return
-    args = head + tail
-    if max_blocks > 0:
-        _lib.call("gsplat_hip_adam_step_bounded", *args, int(max_blocks), _stream())
-    else:
-        _lib.call("gsplat_hip_adam_step", *args, _stream())
-
-
-# workgroups of the deferred (side-stream) update: few enough that the main
-# stream's projection / isect kernels still find CU slots
-DEFER_BLOCKS = int(os.environ.get("GSPLAT_HIP_DEFER_BLOCKS", "512"))
+    _lib.call("gsplat_hip_adam_step", *(head + tail), _stream())
 
 
 class FusedAdam:
     """torch.optim.Adam semantics (per-group lr, shared betas/eps) in one launch.
 
-    deferred: indices of parameters whose update may run on a side stream
-    (after everything queued so far on the current stream): `step()` then
-    launches the other groups on the current stream and these on the side
-    stream, and `wait()` orders the current stream after them.  The trainer
-    defers the SH coefficients (81 % of the optimizer bytes at SH degree 3):
-    the next step needs them only for its colours, after projection and tile
-    intersection, which run meanwhile."""
+    (A variant that deferred the SH groups' update to a side stream, to
+    overlap the next step's projection and isect, measured slower at M2 --
+    620-650 against 660 images/s, profiles/r2_s4_defer: the two split the HBM
+    bandwidth instead of filling each other's gaps -- and was removed.)"""
 
-    def __init__(self, params, lrs, betas=(0.9, 0.999), eps=1e-8, deferred=()):
+    def __init__(self, params, lrs, betas=(0.9, 0.999), eps=1e-8):
         self.params = list(params)
         self.lrs = [float(x) for x in lrs]
         self.betas, self.eps = betas, eps
@@ -258,13 +244,8 @@ class FusedAdam:
         self.step_count = 0
         for p in self.params:
             assert p.is_contiguous() and p.dtype == torch.float32
-        self.deferred = sorted(set(deferred))
-        self.side = None
-        if self.deferred and self.params and self.params[0].is_cuda:
-            self.side = torch.cuda.Stream(device=self.params[0].device)
-        self._event = None
 
-    def _launch(self, idx, grads, max_blocks=0, xform=None, hyper=None, void=None):
+    def _launch(self, idx, grads, xform=None, hyper=None, void=None):
         aux = modes = None
         if xform:
             aux = [xform[i][1] if i in xform else None for i in idx]
@@ -273,7 +254,7 @@ class FusedAdam:
         adam_groups([self.params[i].data for i in idx], [grads[i] for i in idx],
                     [self.exp_avg[i] for i in idx], [self.exp_avg_sq[i] for i in idx],
                     [self.lrs[i] for i in idx], self.betas, self.eps, self.step_count,
-                    max_blocks, aux, modes, hyper, void)
+                    aux, modes, hyper, void)
 
     @torch.no_grad()
     def step(self, skip=(), xform=None, hyper=None, void=None):
@@ -284,36 +265,14 @@ class FusedAdam:
         the captured step's device-side factors of the launched groups (in
         launch order, adam_factors) and void-step flag (step_count is then
         the caller's business)."""
-        self.wait()  # a previous deferred update is ordered before this one
         if hyper is None:
             self.step_count += 1
         grads = [p.grad for p in self.params]
         for gr in grads:
             assert gr is None or gr.is_contiguous()
-        if self.side is None:
-            idx = [i for i in range(len(self.params)) if i not in skip]
-            if idx:
-                self._launch(idx, grads, xform=xform, hyper=hyper, void=void)
-            return
-        assert hyper is None, "the captured step has no deferred groups"
-        assert not skip and not xform, "skip / xform and deferred groups are exclusive"
-        now = [i for i in range(len(self.params)) if i not in self.deferred]
-        if now:
-            self._launch(now, grads)
-        self.side.wait_stream(torch.cuda.current_stream(self.side.device))
-        for i in self.deferred:  # read on the side stream after zero_grad frees them
-            if grads[i] is not None:
-                grads[i].record_stream(self.side)
-        with torch.cuda.stream(self.side):
-            self._launch(self.deferred, grads, DEFER_BLOCKS)
-            self._event = torch.cuda.Event()
-            self._event.record(self.side)
-
-    def wait(self):
-        """Order the current stream after a deferred update still in flight."""
-        if self._event is not None:
-            torch.cuda.current_stream(self.side.device).wait_event(self._event)
-            self._event = None
+        idx = [i for i in range(len(self.params)) if i not in skip]
+        if idx:
+            self._launch(idx, grads, xform=xform, hyper=hyper, void=void)
 
     def zero_grad(self, set_to_none=True):
         for p in self.params:

@@ -220,26 +220,18 @@ class Trainer:
         # measurement only (bench.py --dp-emulate W): one rank shards its
         # optimizer rows as W ranks would (ShardedAdam emulate_world)
         self.dp_emulate_world = dp_emulate_world if self.sharded else None
-        # GSPLAT_HIP_DEFER_SH=1: the SH rows' Adam on a side stream beside the
-        # next step's projection and isect (colours evaluated after the isect).
-        # Measured slower at M2 (620-630 vs 660 images/s): the
-        # sort kernels and the update split the HBM bandwidth instead of
-        # filling each other's gaps, so it is off by default.
-        self.defer_sh = (fused and not self.sharded and torch.device(device).type == "cuda"
-                         and os.environ.get("GSPLAT_HIP_DEFER_SH", "0") == "1")
         # one rank, fused path: the SH coefficients' Adam step runs inside the
         # SH-colour backward (gsplat_hip_sh_colors_bwd_adam), so their
         # gradients never go through HBM; GSPLAT_HIP_SH_ADAM_IN_BWD=0 turns it off
         # (Gaussian-sharded too: the SH backward sums its shard's gradient over
         # every rank's camera in the kernel before the update)
-        self.sh_adam_in_bwd = (fused and not self.sharded and not self.defer_sh
+        self.sh_adam_in_bwd = (fused and not self.sharded
                                and (world_size == 1 or self.gshard)
                                and os.environ.get("GSPLAT_HIP_SH_ADAM_IN_BWD", "1") != "0")
         # the exp / sigmoid VJPs and the means-gradient sum formed inside the
         # geometry groups' Adam (gsplat_hip_adam_step_ex): at one rank, and
         # under the sharded optimizer on the reduced shard (ShardedAdam.step)
-        self.geom_fuse = (fused and not self.defer_sh
-                          and (world_size == 1 or self.sharded or self.gshard)
+        self.geom_fuse = (fused and (world_size == 1 or self.sharded or self.gshard)
                           and os.environ.get("GSPLAT_HIP_GEOM_FUSE", "1") != "0")
         # one rank: the geometry groups' whole Adam step inside the
         # projection backward (gsplat_hip_projection_bwd_adam, 2DGS:
@@ -305,11 +297,7 @@ class Trainer:
                                emulate_world=getattr(self, "dp_emulate_world", None),
                                **self.adam_kw)
         if self.fused:  # HIP loss + one-launch Adam (csrc/ssim.hip, csrc/adam.hip)
-            # the SH rows' update on a side stream, overlapping the next
-            # step's projection and isect (render() waits before the colours)
-            names = list(self.params)
-            deferred = [names.index(k) for k in ("sh0", "shN")] if self.defer_sh else []
-            return FusedAdam(params, self.lrs, deferred=deferred, **self.adam_kw)
+            return FusedAdam(params, self.lrs, **self.adam_kw)
         groups = [{"params": [p], "lr": lr, "name": k}
                   for (k, p), lr in zip(self.params.items(), self.lrs)]
         return torch.optim.Adam(groups, foreach=True, **self.adam_kw)
@@ -386,7 +374,7 @@ class Trainer:
             if self._graph.failed is not None:  # a recovery's re-capture failed
                 self.graph_fallback = self._graph.failed
                 self._graph = None
-        if self.sharded or getattr(self, "defer_sh", False):
+        if self.sharded:
             self.opt.wait()
 
     def release_graph(self):
@@ -442,8 +430,6 @@ class Trainer:
             self.opt.wait([names.index(k) for k in ("means", "scales", "quats", "opacities")])
             sh_idx = [names.index(k) for k in ("sh0", "shN")]
             hook = lambda: self.opt.wait(sh_idx)  # noqa: E731
-        elif getattr(self, "defer_sh", False):
-            hook = self.opt.wait  # the previous step's SH update (side stream)
         if self.fused:  # one HIP launch each way for both activations
             scales, opac = activate(p["scales"], p["opacities"], fusion)
         else:

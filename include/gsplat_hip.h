@@ -45,7 +45,9 @@ const char *gsplat_hip_last_error(void);
  * 34: gsplat_hip_set_fwd_split_threshold, gsplat_hip_fwd_split_threshold
  *     (the split-forward variant chosen once by the caller: deterministic
  *     renders); gsplat_hip_watchdog_arm / _beat / _disarm (bounded waits of
- *     a multi-GPU job). */
+ *     a multi-GPU job); gsplat_hip_debug_set_lane_histogram, the
+ *     deferred-SH gsplat_hip_adam_step_bounded and the compiled-in variants
+ *     measured slower removed. */
 int gsplat_hip_abi_version(void);
 
 /* ---------------------------------------------------------------------------
@@ -347,10 +349,6 @@ int gsplat_hip_rasterize_bwd(int C, int64_t n_gaussians, int D, int width, int h
  * (100 MHz) at [2w, 2w+1], w = global wave index (4 waves per tile).  Not part
  * of the reference surface; NULL disables (the default). */
 int gsplat_hip_debug_set_timeline(uint64_t *device_buffer, int64_t capacity_waves);
-/* Debug/profiling: when non-NULL, the 16x16 backward adds, for every record
- * it composites on a wave, 1 to device_buffer[k] (u64[65]), k = number of the
- * wave's lanes the record contributes to.  NULL disables (the default). */
-int gsplat_hip_debug_set_lane_histogram(unsigned long long *device_buffer);
 /* Chunk length (isects, rounded up to a multiple of 64; <= 0 disables) of the
  * chunked 16x16 backward; returns the value in effect.  Default 1024, or the
  * GSPLAT_HIP_CHUNK environment variable.  Forward and backward of one
@@ -388,7 +386,9 @@ int64_t gsplat_hip_fwd_split_threshold(int64_t n_isects);
 /* Debug flags of the 16x16 rasterizer (ABI 25; default 0, or GSPLAT_HIP_DBG):
  * bit 0 = the backward skips its gradient atomics (timing experiments);
  * bit 2 = the backward skips its cross-lane reduction, bit 3 its gradient
- * algebra (timing attribution only: wrong gradients);
+ * algebra, bit 5 = the forward stores no chunk state (timing / traffic
+ * attribution only: wrong gradients); bit 4 = the XCD-grouped dispatch order
+ * of the unsplit forward (same results);
  * bit 1 = a chunk of a split tile never waits for an earlier chunk's
  * published product and computes it itself (the timeout path; results are
  * identical).  Returns the previous flags. */
@@ -628,13 +628,6 @@ int gsplat_hip_adam_step_dev(int n_groups, float *const *params, const float *co
                              float *const *exp_avgs, float *const *exp_avg_sqs,
                              const int64_t *numels, const float *hyper_device, float beta1,
                              float beta2, float eps, const int32_t *skip_device, void *stream);
-/* The same update on a grid of at most max_blocks workgroups (ABI 17): an
- * update running on a side stream beside other kernels leaves them CU slots
- * (the trainer's deferred SH-coefficient update). */
-int gsplat_hip_adam_step_bounded(int n_groups, float *const *params, const float *const *grads,
-                                 float *const *exp_avgs, float *const *exp_avg_sqs,
-                                 const int64_t *numels, const float *lrs, float beta1,
-                                 float beta2, float eps, int step, int max_blocks, void *stream);
 
 /* ---------------------------------------------------------------------------
  * 2DGS (surfels).  Replaces the CUDA kernels that gsplat.rendering.rasterization_2dgs

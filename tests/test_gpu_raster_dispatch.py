@@ -151,8 +151,9 @@ def test_dispatch_order_is_heaviest_first_permutation():
         torch.cuda.synchronize()
     finally:
         _lib.query("gsplat_hip_debug_set_fwd_split", old)
-    # the order area (256-B aligned) is the last part of the state
-    order_ints = (4 * nt + 255) // 256 * 64
+    # the order area (256-B aligned, room for the XCD-grouped order's slots:
+    # 2 nt + 64 entries) is the last part of the state
+    order_ints = (4 * (2 * nt + 64) + 255) // 256 * 64
     order = state[-order_ints:][:nt].cpu().numpy()
     assert np.array_equal(np.sort(order), np.arange(nt)), "not a permutation"
     o = offs.flatten().cpu().numpy().astype(np.int64)
@@ -261,3 +262,27 @@ def test_split_forward_vs_oracle():
     from test_gpu_parity import close_most
     close_most(ra, oa, 1e-4, 1e-4, "alphas", max_frac=1e-3)
     close_most(rc, oc, 1e-4, 1e-4, "colors", max_frac=1e-3)
+
+
+@pytest.mark.parametrize("W,H", [(640, 480), (200, 150), (1000, 24)])
+def test_xcd_grouped_order_changes_nothing(W, H):
+    """The XCD-grouped dispatch order (tile_order_grouped_kernel, debug flag
+    bit 4): 2x2 groups of tiles, heaviest group first, a group's tiles in
+    slots of one XCD, empty slots at the image edges (odd tile counts) -- the
+    forward's images bit for bit, the backward at the run-to-run spread of
+    the float atomics."""
+    from gsplat_hip import _lib
+    ins, _, _ = _scene(W=W, H=H)
+    old_split = _lib.query("gsplat_hip_debug_set_fwd_split", 0)  # the unsplit forward
+    try:
+        rc0, ra0, _, g0 = _render(ins, W, H, True)
+        rc0b, _, _, g0b = _render(ins, W, H, True)
+        old = _lib.query("gsplat_hip_debug_set_flags", 16)
+        try:
+            rc1, ra1, _, g1 = _render(ins, W, H, True)
+        finally:
+            _lib.query("gsplat_hip_debug_set_flags", old)
+    finally:
+        _lib.query("gsplat_hip_debug_set_fwd_split", old_split)
+    assert torch.equal(rc0, rc1) and torch.equal(ra0, ra1) and torch.equal(rc0, rc0b)
+    _check_within_spread(g0, g0b, g1, f"grouped order {W}x{H}")

@@ -335,58 +335,6 @@ def test_trainer_evaluate_psnr_ssim():
     assert same["ssim"] > 0.999 and same["psnr"] > 60
 
 
-def test_deferred_adam_update_is_exact():
-    """FusedAdam with some groups deferred to a side stream (the trainer's SH
-    coefficients) gives bit-identical parameters and moments to the all-in-one
-    launch; the gradients freed by zero_grad stay valid for the side stream."""
-    from gsplat_hip.losses import FusedAdam
-    torch.manual_seed(0)
-    shapes = [(5001, 3), (5001, 4), (5001, 1, 3), (5001, 15, 3)]
-    lrs = [1.6e-4, 1e-3, 2.5e-3, 2.5e-3 / 20]
-    base = [torch.randn(s, device="cuda") for s in shapes]
-    grads = [[torch.randn(s, device="cuda") for s in shapes] for _ in range(5)]
-    res = []
-    for deferred in ((), (2, 3)):
-        ps = [b.clone().requires_grad_(True) for b in base]
-        opt = FusedAdam(ps, lrs, betas=(0.9, 0.999), eps=1e-15, deferred=deferred)
-        for it in range(5):
-            opt.wait()  # as the trainer's render does before reading the SH rows
-            for p, g in zip(ps, grads[it]):
-                p.grad = g.clone()
-            opt.step()
-            opt.zero_grad()
-            torch.empty(1 << 22, device="cuda").fill_(7.0)  # reuse freed blocks
-        opt.wait()
-        torch.cuda.synchronize()
-        res.append(([p.detach().clone() for p in ps], opt.exp_avg, opt.exp_avg_sq))
-    for a, b in zip(res[0], res[1]):
-        for x, y in zip(a, b):
-            assert torch.equal(x, y)
-
-
-def test_trainer_deferred_sh_runs_through_refines(monkeypatch):
-    """The trainer with the deferred SH update (GSPLAT_HIP_DEFER_SH=1) across refines
-    and an opacity reset: state consistent, losses finite; the rasterizer's
-    backward atomics make two runs differ in the last bits, so the check
-    against the non-deferred trainer is a close one."""
-    from gsplat_hip.densify import DefaultStrategyConfig
-    from gsplat_hip.train_step import Trainer
-    means, rgbs, vm, K, W, H = _small_scene()
-    out = {}
-    for defer in ("0", "1"):
-        monkeypatch.setenv("GSPLAT_HIP_DEFER_SH", defer)
-        cfg = DefaultStrategyConfig(refine_start_iter=1, refine_every=2, reset_every=5)
-        tr = Trainer(means, rgbs, vm, K, W, H, device="cuda", strategy=cfg,
-                     sh_degree_interval=2, max_steps=100, init="sfm")
-        assert tr.defer_sh == (defer == "1")
-        losses = [float(tr.step(it)) for it in range(6)]
-        assert all(math.isfinite(x) for x in losses), losses
-        out[defer] = (losses, [r[0] for r in tr.refine_log])
-    assert out["0"][1] == out["1"][1] == [2, 4]
-    for a, b in zip(out["0"][0], out["1"][0]):
-        assert abs(a - b) <= 1e-3 * abs(a) + 1e-6, (out["0"][0], out["1"][0])
-
-
 @pytest.mark.parametrize("degree", [3, 1])
 def test_sh_adam_in_backward_is_exact(degree):
     """The SH-colour backward with the coefficients' Adam step fused in

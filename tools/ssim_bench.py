@@ -1,6 +1,5 @@
 """Time the training loss (l1_ssim_loss forward + backward) at 1080p RGB:
-fused one-pass kernel vs the two-pass pair (GSPLAT_HIP_SSIM_FV picks the
-fused variant)."""
+fused one-pass kernel vs the two-pass pair."""
 import os
 import sys
 
@@ -37,5 +36,5 @@ loss.backward()
 torch.cuda.synchronize()
 # bit-level fingerprint: variants that only re-block the passes must agree
 fp = (float(loss), float(img.grad.double().sum()), float(img.grad.abs().double().sum()))
-print(f"fused={int(fused)} FV={os.environ.get('GSPLAT_HIP_SSIM_FV', '0')}: "
+print(f"fused={int(fused)}: "
       f"{a.elapsed_time(b) / 50 * 1e3:.1f} us per loss fwd+bwd; fingerprint {fp!r}")
