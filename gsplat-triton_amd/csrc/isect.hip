@@ -614,13 +614,16 @@ static int isect_write_sorted_impl(
     int tile_height, int tile_bits, int cam_bits, const void *count_workspace, int64_t n_visible,
     int64_t n_isects, const int64_t *cnt_dev, void *workspace, int64_t workspace_bytes,
     int64_t *isect_ids, int32_t *flatten_ids, int32_t *offsets, int n_cameras, hipStream_t st,
-    CapCheck cc = CapCheck{}, int32_t *rank_ids = nullptr, int32_t *vis_rank = nullptr) {
+    CapCheck cc = CapCheck{}, int32_t *rank_ids = nullptr, int32_t *vis_rank = nullptr,
+    const st::SurfelCull *sc = nullptr) {
   GS_REQUIRE(n_gaussians >= 0 && (camera_ids || N > 0 || n_gaussians == 0),
              "isect_write_sorted: N must be > 0 when camera_ids is null");
   GS_REQUIRE(tile_bits + cam_bits <= 32, "isect_write_sorted: tile_bits + cam_bits > 32");
   GS_REQUIRE(n_isects < ((int64_t)1 << 30), "isect_write_sorted: more than 2^30 isects");
   GS_REQUIRE(!offsets || n_cameras > 0, "isect_write_sorted: offsets need n_cameras");
   GS_REQUIRE(!rank_ids == !vis_rank, "isect_write_sorted: rank_ids and vis_rank go together");
+  GS_REQUIRE(!sc || (cnt_dev && gsplat_hip_isect_ranked(n_cameras, tile_width, tile_height)),
+             "isect_write_sorted: tile culling needs the capacity mode and the supertiles");
   GS_REQUIRE(!rank_ids || gsplat_hip_isect_ranked(n_cameras, tile_width, tile_height),
              "isect_write_sorted: rank ids need the supertile expansion");
   // isect_ids / flatten_ids may both be null when rank_ids and offsets are
@@ -686,6 +689,11 @@ static int isect_write_sorted_impl(
                        nullptr);
     hipLaunchKernelGGL(st::emit_kernel, dim3((unsigned)nbV), dim3(256), 0, st, n_visible, cnt_dev,
                        Vs, dks, rect, camera_ids, geo, blk, tkey, val);
+    if (sc)  // large surfels' pairs: the tiles of the supertile they can reach
+      hipLaunchKernelGGL(st::tight_kernel,
+                         dim3((unsigned)std::min<int64_t>((n_isects + 255) / 256, 2048)),
+                         dim3(256), 0, st, n_isects, blk + nbV, geo, Vs, rect, cnt_dev, tkey, val,
+                         *sc);
     int kb = 0;
     while ((1 << kb) < geo.nst) ++kb;
     // the pair count (<= n_isects) is the scan's total, blk[nbV]
@@ -695,13 +703,14 @@ static int isect_write_sorted_impl(
     hipLaunchKernelGGL(st::plan_kernel, dim3(1), dim3(1024), 0, st, geo.nst, totals, st_start,
                        seg_start, seg_st, n_tt, tile_tot);
     const unsigned nseg = (unsigned)(n_isects / st::kSeg + geo.nst + 1);
+    const uint32_t *pk = sc ? tkeys : nullptr;  // the culled pairs' kept tiles
     hipLaunchKernelGGL(st::seg_count_kernel, dim3(nseg), dim3(256), 0, st, geo, st_start,
-                       seg_start, seg_st, vals, rect, Vs, tiles_per_gauss, segcnt, tile_tot);
+                       seg_start, seg_st, vals, rect, Vs, tiles_per_gauss, segcnt, tile_tot, pk);
     hipLaunchKernelGGL(st::tile_scan_kernel, dim3(1), dim3(1024), 0, st, geo, cnt_dev, tile_tot,
-                       offs);
+                       offs, sc ? const_cast<int64_t *>(cnt_dev) : nullptr);
     hipLaunchKernelGGL(st::seg_write_kernel, dim3(nseg), dim3(256), 0, st, geo, cnt_dev, st_start,
                        seg_start, seg_st, vals, rect, Vs, dks, tiles_per_gauss, segcnt, tile_tot,
-                       isect_ids, flatten_ids, rank_ids);
+                       isect_ids, flatten_ids, rank_ids, pk);
     GS_CHECK_LAUNCH("isect_write_sorted (supertiles)");
     return 0;
   }
@@ -766,14 +775,15 @@ extern "C" int64_t gsplat_hip_isect_sorted_capped_workspace_bytes(int64_t n_gaus
 // the number of isects written (0 when they did not fit: status_device[0]
 // gets bit 0 set, sticky), counts_device[1] the visible Gaussians; pass
 // counts_device to offsets / rasterize as their n_isects_device.
-extern "C" int gsplat_hip_isect_write_sorted_capped(
+static int isect_write_sorted_capped_impl(
     int64_t n_gaussians, int N, const float *means2d, const int32_t *radii, const float *depths,
     const int32_t *camera_ids, const int32_t *tiles_per_gauss, int tile_size, int tile_width,
     int tile_height, int tile_bits, int cam_bits, const void *count_workspace,
     const int64_t *totals_device, int64_t capacity, int64_t *counts_device,
     int32_t *status_device, int64_t *counts_host_ring, const int64_t *slot_device,
     void *workspace, int64_t workspace_bytes, int64_t *isect_ids, int32_t *flatten_ids,
-    int n_cameras, int32_t *offsets, int32_t *rank_ids, int32_t *vis_rank, void *stream) {
+    int n_cameras, int32_t *offsets, int32_t *rank_ids, int32_t *vis_rank, void *stream,
+    const st::SurfelCull *sc) {
   GS_REQUIRE(capacity >= 0 && capacity < ((int64_t)1 << 30),
              "isect_write_sorted_capped: capacity %lld out of range", (long long)capacity);
   GS_REQUIRE(counts_device && totals_device, "isect_write_sorted_capped: null count buffers");
@@ -796,7 +806,40 @@ extern "C" int gsplat_hip_isect_write_sorted_capped(
                                  tiles_per_gauss, tile_size, tile_width, tile_height, tile_bits,
                                  cam_bits, count_workspace, n_gaussians, capacity, counts_device,
                                  workspace, workspace_bytes - 256, isect_ids, flatten_ids, offsets,
-                                 n_cameras, st, cc, rank_ids, vis_rank);
+                                 n_cameras, st, cc, rank_ids, vis_rank, sc);
+}
+
+extern "C" int gsplat_hip_isect_write_sorted_capped(
+    int64_t n_gaussians, int N, const float *means2d, const int32_t *radii, const float *depths,
+    const int32_t *camera_ids, const int32_t *tiles_per_gauss, int tile_size, int tile_width,
+    int tile_height, int tile_bits, int cam_bits, const void *count_workspace,
+    const int64_t *totals_device, int64_t capacity, int64_t *counts_device,
+    int32_t *status_device, int64_t *counts_host_ring, const int64_t *slot_device,
+    void *workspace, int64_t workspace_bytes, int64_t *isect_ids, int32_t *flatten_ids,
+    int n_cameras, int32_t *offsets, int32_t *rank_ids, int32_t *vis_rank, void *stream) {
+  return isect_write_sorted_capped_impl(
+      n_gaussians, N, means2d, radii, depths, camera_ids, tiles_per_gauss, tile_size, tile_width,
+      tile_height, tile_bits, cam_bits, count_workspace, totals_device, capacity, counts_device,
+      status_device, counts_host_ring, slot_device, workspace, workspace_bytes, isect_ids,
+      flatten_ids, n_cameras, offsets, rank_ids, vis_rank, stream, nullptr);
+}
+
+extern "C" int gsplat_hip_isect_write_sorted_capped_surfel(
+    int64_t n_gaussians, int N, const float *means2d, const int32_t *radii, const float *depths,
+    const int32_t *camera_ids, const int32_t *tiles_per_gauss, int tile_size, int tile_width,
+    int tile_height, int tile_bits, int cam_bits, const void *count_workspace,
+    const int64_t *totals_device, int64_t capacity, int64_t *counts_device,
+    int32_t *status_device, int64_t *counts_host_ring, const int64_t *slot_device,
+    void *workspace, int64_t workspace_bytes, int32_t *flatten_ids, int n_cameras,
+    int32_t *offsets, const float *ray_transforms, const float *opacities, void *stream) {
+  GS_REQUIRE(means2d && ray_transforms && opacities && flatten_ids && offsets && !camera_ids,
+             "isect_write_sorted_capped_surfel: null argument (or packed camera ids)");
+  const st::SurfelCull sc{means2d, ray_transforms, opacities, tile_size};
+  return isect_write_sorted_capped_impl(
+      n_gaussians, N, means2d, radii, depths, camera_ids, tiles_per_gauss, tile_size, tile_width,
+      tile_height, tile_bits, cam_bits, count_workspace, totals_device, capacity, counts_device,
+      status_device, counts_host_ring, slot_device, workspace, workspace_bytes, nullptr,
+      flatten_ids, n_cameras, offsets, nullptr, nullptr, stream, &sc);
 }
 
 // -------------------------------------------------------- tile-first path --

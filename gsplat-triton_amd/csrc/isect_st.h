@@ -30,9 +30,21 @@
 // where the reference's masked 64-bit sort puts them.
 // Capacity mode (the captured step): every count is read on the device; on an
 // overflow nothing is written and every offset is 0.
+// Tile culling of large surfels (the captured 2DGS training step,
+// SurfelCull): a (supertile, surfel) pair of a surfel with more than
+// kLanePairs pairs carries in its key's upper half the tiles of the supertile
+// that its UV-plane image can reach (surfel_keep, the rasterizer's own strip
+// test, on the whole tile); the other tiles of its rectangle get no isect.
+// Near-degenerate surfels (the reference AABB's 1e-4 floor) cover every tile
+// with their rectangle and light a few: at M5 ~1,000 of them held 41 % of
+// the isects.  The rasterizer culls exactly these pairs per strip anyway
+// (a strip is inside its tile), so images and gradients are unchanged; only
+// the isect list -- an internal of the captured step -- is shorter.  The
+// offsets and the isect count on the device (tile_scan) follow it.
 #pragma once
 #include "common.h"
 #include "lsd_sort.h"
+#include "surfel_cull.h"
 
 namespace gs {
 namespace st {
@@ -41,6 +53,14 @@ constexpr int S = 4;            // tiles per supertile side
 constexpr int kSeg = 1024;      // pairs per segment (a 256-lane workgroup)
 constexpr int kMaxKeys = 2048;  // supertiles (+ the virtual one) of the LSD pass
 constexpr int kMaxTiles = kMaxKeys * S * S;
+
+struct SurfelCull {  // all null: no tile culling
+  const float *means2d;  // [G][2]
+  const float *T;        // [G][3][3] ray transforms
+  const float *opac;     // [G]
+  int ts;                // tile size (pixels)
+};
+constexpr uint32_t kTightFlag = 1u << 15;  // key bits 16..31 hold the kept tiles
 
 struct Geo {
   int C, N, tw, th, tile_bits;
@@ -187,6 +207,54 @@ emit_kernel(int64_t nV, const int64_t *__restrict__ cap, const int32_t *__restri
   }
 }
 
+// (2b) tile culling of large surfels (SurfelCull), one lane per pair, before
+// the supertile pass: a pair of a surfel with more than kLanePairs pairs gets
+// kTightFlag and, in key bits 16..31, the tiles of its supertile that the
+// surfel's image can reach (surfel_keep on the tile's pixel centres).  The
+// emission writes a surfel's pairs consecutively, so the waves holding large
+// surfels' pairs run the tests on all lanes.
+__global__ void __launch_bounds__(256)
+tight_kernel(int64_t cap_pairs, const int64_t *__restrict__ n_pairs, Geo geo,
+             const int32_t *__restrict__ Vs, const ushort4 *__restrict__ rect,
+             const int64_t *__restrict__ cap, uint32_t *__restrict__ pkey,
+             const int32_t *__restrict__ pval, SurfelCull sc) {
+  if (void_call(cap)) return;
+  const int64_t n = min(cap_pairs, n_pairs[0]);
+  // grid-stride: the grid is sized for a few sweeps of the chip, not for the
+  // capacity (a capacity-sized grid of mostly empty workgroups cost 87 us per
+  // step at M5)
+  for (int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x; p < n;
+       p += (int64_t)gridDim.x * 256) {
+  const uint32_t key = pkey[p];
+  if ((int)key >= geo.nst - 1) continue;  // the negative-depth key: no tiles to cull
+  const int32_t s = pval[p];
+  const ushort4 r = rect[s];
+  const int sx0 = r.x / S, sy0 = r.z / S;
+  const int np = ((r.y - 1) / S - sx0 + 1) * ((r.w - 1) / S - sy0 + 1);
+  if (np <= kLanePairs) continue;
+  const int32_t g = Vs[s];
+  float m9[9];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) m9[i] = sc.T[9 * (int64_t)g + i];
+  const float mx = sc.means2d[2 * (int64_t)g], my = sc.means2d[2 * (int64_t)g + 1];
+  const float op = sc.opac[g];
+  const int rr = (int)key % geo.nst1;  // supertile within its camera
+  const int sy = rr / geo.stw, sx = rr - sy * geo.stw;
+  const int tx0 = sx * S, ty0 = sy * S;
+  uint32_t m = st_mask(r, tx0, ty0), keep = 0u;
+  while (m) {
+    const int t = __builtin_ctz(m);
+    m &= m - 1u;
+    const float x0 = (float)((tx0 + t % S) * sc.ts) + 0.5f;
+    const float y0 = (float)((ty0 + t / S) * sc.ts) + 0.5f;
+    if (surfel::surfel_keep(m9, mx, my, op, x0, x0 + (float)(sc.ts - 1), y0,
+                            y0 + (float)(sc.ts - 1)))
+      keep |= 1u << t;
+  }
+  pkey[p] = key | kTightFlag | (keep << 16);
+  }
+}
+
 // (4) one workgroup: supertile starts, segments (kSeg pairs) and their keys
 __global__ void __launch_bounds__(1024)
 plan_kernel(int nst, const uint32_t *__restrict__ totals, int32_t *__restrict__ st_start,
@@ -277,19 +345,24 @@ struct WavePairs {
 };
 
 GS_INLINE void load_pairs(const Seg &sg, const int32_t *pval, const ushort4 *rect,
-                          const int32_t *Vs, const int32_t *tpg, WavePairs &wp) {
+                          const int32_t *Vs, const int32_t *tpg, WavePairs &wp,
+                          const uint32_t *pkey) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t kk[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     const int p = sg.p0 + w * 256 + e * 64 + lane;
     wp.s[e] = p < sg.p1 ? pval[p] : -1;
+    if (pkey && p < sg.p1) kk[e] = pkey[p];  // tile-culled pairs: their kept tiles
   }
   if (!sg.virt) {
     ushort4 r[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) r[e] = rect[max(wp.s[e], 0)];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) wp.m[e] = wp.s[e] >= 0 ? st_mask(r[e], sg.tx0, sg.ty0) : 0u;
+    for (int e = 0; e < 4; ++e)
+      wp.m[e] = wp.s[e] < 0 ? 0u
+                : (kk[e] & kTightFlag) ? (kk[e] >> 16) : st_mask(r[e], sg.tx0, sg.ty0);
   } else {
     int32_t g[4];
 #pragma unroll
@@ -337,12 +410,12 @@ seg_count_kernel(Geo geo, const int32_t *__restrict__ st_start, const int32_t *_
                  const int32_t *__restrict__ seg_st, const int32_t *__restrict__ pval,
                  const ushort4 *__restrict__ rect, const int32_t *__restrict__ Vs,
                  const int32_t *__restrict__ tpg, int32_t *__restrict__ segcnt,
-                 int32_t *__restrict__ tile_tot) {
+                 int32_t *__restrict__ tile_tot, const uint32_t *__restrict__ pkey) {
   __shared__ int32_t wc[4][S * S];
   Seg sg;
   if (!seg_of(blockIdx.x, geo, seg_start, seg_st, st_start, sg)) return;
   WavePairs wp;
-  load_pairs(sg, pval, rect, Vs, tpg, wp);
+  load_pairs(sg, pval, rect, Vs, tpg, wp, pkey);
   wave_counts(sg, wp, wc);
   __syncthreads();
   if (threadIdx.x < S * S) {
@@ -359,7 +432,7 @@ seg_count_kernel(Geo geo, const int32_t *__restrict__ st_start, const int32_t *_
 // 8 contiguous tiles per thread.
 __global__ void __launch_bounds__(1024)
 tile_scan_kernel(Geo geo, const int64_t *__restrict__ cap, int32_t *__restrict__ tile_tot,
-                 int32_t *__restrict__ offsets) {
+                 int32_t *__restrict__ offsets, int64_t *__restrict__ n_out) {
   constexpr int R = 8192, PT = R / 1024;
   __shared__ int32_t buf[R];
   __shared__ int32_t wsum[16];
@@ -413,6 +486,9 @@ tile_scan_kernel(Geo geo, const int64_t *__restrict__ cap, int32_t *__restrict__
     carry = all;
     __syncthreads();
   }
+  // tile culling (SurfelCull): the isects written -- fewer than the count of
+  // the tile rectangles -- are the count the rasterizer reads on the device
+  if (n_out && t == 0 && !vd) n_out[0] = carry;
 }
 
 // (7) every segment's isects at their final slots: per tile, the tile's
@@ -424,14 +500,15 @@ seg_write_kernel(Geo geo, const int64_t *__restrict__ cap, const int32_t *__rest
                  const int32_t *__restrict__ Vs, const uint32_t *__restrict__ dkeys,
                  const int32_t *__restrict__ tpg, const int32_t *__restrict__ segcnt,
                  const int32_t *__restrict__ tile_off, int64_t *__restrict__ isect_ids,
-                 int32_t *__restrict__ flatten_ids, int32_t *__restrict__ rank_ids) {
+                 int32_t *__restrict__ flatten_ids, int32_t *__restrict__ rank_ids,
+                 const uint32_t *__restrict__ pkey) {
   __shared__ int32_t wc[4][S * S];
   __shared__ int32_t sbase[S * S];
   if (void_call(cap)) return;
   Seg sg;
   if (!seg_of(blockIdx.x, geo, seg_start, seg_st, st_start, sg)) return;
   WavePairs wp;
-  load_pairs(sg, pval, rect, Vs, tpg, wp);
+  load_pairs(sg, pval, rect, Vs, tpg, wp, pkey);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   int32_t g[4] = {0, 0, 0, 0};
   uint32_t db[4] = {0u, 0u, 0u, 0u};

@@ -1675,15 +1675,19 @@ static SplitLayout split_layout(int D, int n_tiles, int64_t n_isects) {
   return l;
 }
 
-// XCD-grouped forward order (tile_order_grouped_kernel): GSPLAT_HIP_DBG bit 4
-// selects it (A/B experiment; the unsplit forward only)
+// XCD-grouped forward order (tile_order_grouped_kernel), the default for the
+// unsplit forward; GSPLAT_HIP_DBG bit 4 restores the per-tile order.
+// Measured (profiles/r6/xcd/, alternating bench runs, rocprofv3 counters of
+// the forward): M2 forward 0.1622 / 0.1622 against 0.1655 / 0.1649 ms, L2 hit
+// rate 0.618 -> 0.713, fetched bytes -27 %; M3 with the split off 0.605 /
+// 0.603 against 0.608 / 0.608 ms, hit 0.451 -> 0.522, fetched -15 %.
 static int dbg_flags();
 static int order_slots(int C, int tw, int th) {
   return 32 * ((r16::order_groups(C, tw, th) + 7) / 8);
 }
 static bool grouped_order(int C, int tw, int th) {
   const int64_t n_tiles = (int64_t)C * tw * th;
-  return (dbg_flags() & 16) && r16::order_groups(C, tw, th) <= 8192 &&
+  return !(dbg_flags() & 16) && r16::order_groups(C, tw, th) <= 8192 &&
          order_slots(C, tw, th) <= 2 * n_tiles + 64;
 }
 

@@ -46,6 +46,10 @@ _SIGS = {
     "gsplat_hip_isect_write_sorted_capped": (_i32, [_i64, _i32, _p, _p, _p, _p, _p, _i32, _i32,
                                                     _i32, _i32, _i32, _p, _p, _i64, _p, _p, _p,
                                                     _p, _p, _i64, _p, _p, _i32, _p, _p, _p, _p]),
+    "gsplat_hip_isect_write_sorted_capped_surfel": (_i32, [_i64, _i32, _p, _p, _p, _p, _p, _i32,
+                                                           _i32, _i32, _i32, _i32, _p, _p, _i64,
+                                                           _p, _p, _p, _p, _p, _i64, _p, _i32, _p,
+                                                           _p, _p, _p]),
     "gsplat_hip_host_mapped_alloc": (_i32, [_i64, _p, _p]),
     "gsplat_hip_host_mapped_free": (_i32, [_p]),
     "gsplat_hip_step_fetch": (_i32, [_p, _i64, _i32, _p, _p, _p]),

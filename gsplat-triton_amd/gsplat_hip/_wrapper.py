@@ -497,7 +497,7 @@ class _IsectCount:
 
     @torch.no_grad()
     def finish_capped(self, capacity: int, status: Optional[Tensor] = None, report=None,
-                      ids: bool = True, ranks: bool = True):
+                      ids: bool = True, ranks: bool = True, surfel_cull=None):
         """The sorted isects with NO host synchronisation (the one sync of
         isect_tiles, isect_tiles.py:101-102, removed so that a training step
         can be captured into a HIP graph): isect_ids / flatten_ids have
@@ -513,7 +513,12 @@ class _IsectCount:
         ranks (a rasterizer that gathers by Gaussian id, the 2DGS one); with
         ids=False too (the 2DGS training step, ABI 33) only flatten_ids and
         the offsets are written, isect_ids comes back None (where the
-        supertile expansion runs; else both are written).  Returns
+        supertile expansion runs; else both are written).  surfel_cull =
+        (ray_transforms [C,N,3,3], opacities [C,N]) with ids=False,
+        ranks=False (the 2DGS training step, ABI 34): large surfels get isects
+        only in the tiles their image can reach
+        (gsplat_hip_isect_write_sorted_capped_surfel); counts[0] is then the
+        number written, counts[3] the tile-rectangle count.  Returns
         (tiles_per_gauss, isect_ids, flatten_ids, counts)."""
         (means2d, radii, depths, camera_ids, C, N, G, tile_size, tile_width, tile_height,
          n_bit_tile, n_bit_cam, packed) = self.args
@@ -537,6 +542,17 @@ class _IsectCount:
         ring, slot = (None, None) if report is None else report
         if slot is not None:
             assert slot.dtype == torch.int64 and slot.is_cuda and ring
+        if surfel_cull is not None and flat_only and not packed:
+            rt, op = (_f32c(t) for t in surfel_cull)
+            assert rt.shape == (C, N, 3, 3) and op.shape == (C, N), (rt.shape, op.shape)
+            _lib.call("gsplat_hip_isect_write_sorted_capped_surfel", G, N, _ptr(means2d),
+                      _ptr(radii), _ptr(depths), _ptr(camera_ids), _ptr(self.tpg), tile_size,
+                      tile_width, tile_height, n_bit_tile, n_bit_cam, _ptr(self.ws),
+                      _ptr(self.totals), capacity, _ptr(counts), _ptr(status), ring, _ptr(slot),
+                      _ptr(ws), ws.numel(), _ptr(flatten_ids), C, _ptr(self.offsets), _ptr(rt),
+                      _ptr(op), _stream())
+            self.ranks = None
+            return self.tpg.view(C, N), None, flatten_ids, counts
         _lib.call("gsplat_hip_isect_write_sorted_capped", G, N, _ptr(means2d), _ptr(radii),
                   _ptr(depths), _ptr(camera_ids), _ptr(self.tpg), tile_size, tile_width,
                   tile_height, n_bit_tile, n_bit_cam, _ptr(self.ws), _ptr(self.totals), capacity,

@@ -16,6 +16,10 @@ import torch
 from torch import Tensor
 
 from . import _lib, _wrapper
+
+# the captured 2DGS training step's tile culling of large surfels (ABI 34,
+# gsplat_hip_isect_write_sorted_capped_surfel); a module attribute for A/B
+TILE_CULL = True
 from ._wrapper import (
     _dev_check,
     _f32c,
@@ -633,8 +637,12 @@ def rasterization_2dgs(
     if capped:
         # the training step (_colors_only) reads the offsets and flatten ids
         # only: no 64-bit isect ids (8 of 12 bytes per isect not written)
+        # ... and, in the colours-only training step, large surfels' isects
+        # only in the tiles their image can reach (the rasterizer culls the
+        # others on every strip: same render, shorter isect list; ABI 34)
         tiles_per_gauss, isect_ids, flatten_ids, counts = pending_isects.finish_capped(
-            _isect_capacity, _isect_status, _isect_report, ids=not _colors_only, ranks=False)
+            _isect_capacity, _isect_status, _isect_report, ids=not _colors_only, ranks=False,
+            surfel_cull=(ray_transforms, opacities) if (_colors_only and TILE_CULL) else None)
     else:
         tiles_per_gauss, isect_ids, flatten_ids = pending_isects.finish(sort=True, ranks=False)
     isect_offsets = pending_isects.offsets  # written with the sorted isects

@@ -42,7 +42,9 @@ const char *gsplat_hip_last_error(void);
  *     2DGS rasterizer's backward (output) and projection backward (input);
  *     isect_ids alone may be NULL in the sorted emission (flatten_ids and
  *     offsets written: a rasterizer that gathers by id).
- * 34: gsplat_hip_set_fwd_split_threshold, gsplat_hip_fwd_split_threshold
+ * 34: gsplat_hip_isect_write_sorted_capped_surfel (tile culling of large
+ *     surfels in the captured 2DGS step); gsplat_hip_set_fwd_split_threshold,
+ *     gsplat_hip_fwd_split_threshold
  *     (the split-forward variant chosen once by the caller: deterministic
  *     renders); gsplat_hip_watchdog_arm / _beat / _disarm (bounded waits of
  *     a multi-GPU job); gsplat_hip_debug_set_lane_histogram, the
@@ -222,6 +224,28 @@ int gsplat_hip_isect_write_sorted_capped(
  * isect_ids alone (ABI 33; flatten_ids and offsets set: one that gathers by
  * Gaussian id and reads the offsets, not the 64-bit keys). */
 int gsplat_hip_isect_ranked(int n_cameras, int tile_width, int tile_height);
+/* The capped emission for the 2DGS rasterizer with tile culling of large
+ * surfels (ABI 34; the captured 2DGS training step): a surfel whose tile
+ * rectangle spans more than 16 supertiles gets isects only in the tiles its
+ * UV-plane image can reach (the rasterizer's own strip test,
+ * csrc/surfel_cull.h, on the whole tile); near-degenerate surfels (the
+ * reference AABB's 1e-4 floor) otherwise cover every tile (41 % of the isects
+ * at M5).  The rasterizer would cull exactly those isects on every strip, so
+ * renders and gradients are unchanged; the isect list, an internal of the
+ * training step, is not the reference's.  flatten_ids and offsets written
+ * (no isect ids, no ranks); counts_device[0] receives the number written
+ * (fewer than counts_device[3], the tile-rectangle count, which the capacity
+ * check uses).  means2d [G][2], ray_transforms [G][3][3], opacities [G] of
+ * the (camera, surfel) rows; non-packed (camera_ids NULL).  No reference
+ * counterpart (the reference's isect is bit-exact; this path is not). */
+int gsplat_hip_isect_write_sorted_capped_surfel(
+    int64_t n_gaussians, int N, const float *means2d, const int32_t *radii, const float *depths,
+    const int32_t *camera_ids, const int32_t *tiles_per_gauss, int tile_size, int tile_width,
+    int tile_height, int tile_bits, int cam_bits, const void *count_workspace,
+    const int64_t *totals_device, int64_t capacity, int64_t *counts_device,
+    int32_t *status_device, int64_t *counts_host_ring, const int64_t *slot_device,
+    void *workspace, int64_t workspace_bytes, int32_t *flatten_ids, int n_cameras,
+    int32_t *offsets, const float *ray_transforms, const float *opacities, void *stream);
 /* Sorted emission, tile-first (the default of isect_tiles(sort=True)): the
  * SAME isect_ids / flatten_ids again, from Gaussian-major emission with
  * 32-bit (camera, tile) keys, a stable sort by those keys, and a segmented
@@ -387,8 +411,8 @@ int64_t gsplat_hip_fwd_split_threshold(int64_t n_isects);
  * bit 0 = the backward skips its gradient atomics (timing experiments);
  * bit 2 = the backward skips its cross-lane reduction, bit 3 its gradient
  * algebra, bit 5 = the forward stores no chunk state (timing / traffic
- * attribution only: wrong gradients); bit 4 = the XCD-grouped dispatch order
- * of the unsplit forward (same results);
+ * attribution only: wrong gradients); bit 4 = the per-tile dispatch order
+ * of the unsplit forward instead of the XCD-grouped one (same results);
  * bit 1 = a chunk of a split tile never waits for an earlier chunk's
  * published product and computes it itself (the timeout path; results are
  * identical).  Returns the previous flags. */

@@ -143,6 +143,7 @@ def test_dispatch_order_is_heaviest_first_permutation():
     nt = C * th * tw
     D = 3
     old = _lib.query("gsplat_hip_debug_set_fwd_split", 0)  # no split area after the order
+    old_flags = _lib.query("gsplat_hip_debug_set_flags", 16)  # the per-tile order
     try:
         sb = int(_lib.query("gsplat_hip_rasterize_fwd_state_bytes", C, D, 16, tw, th, n))
         state = torch.full((sb // 4,), -7, dtype=torch.int32, device=DEV)
@@ -151,6 +152,7 @@ def test_dispatch_order_is_heaviest_first_permutation():
         torch.cuda.synchronize()
     finally:
         _lib.query("gsplat_hip_debug_set_fwd_split", old)
+        _lib.query("gsplat_hip_debug_set_flags", old_flags)
     # the order area (256-B aligned, room for the XCD-grouped order's slots:
     # 2 nt + 64 entries) is the last part of the state
     order_ints = (4 * (2 * nt + 64) + 255) // 256 * 64
@@ -266,11 +268,11 @@ def test_split_forward_vs_oracle():
 
 @pytest.mark.parametrize("W,H", [(640, 480), (200, 150), (1000, 24)])
 def test_xcd_grouped_order_changes_nothing(W, H):
-    """The XCD-grouped dispatch order (tile_order_grouped_kernel, debug flag
-    bit 4): 2x2 groups of tiles, heaviest group first, a group's tiles in
-    slots of one XCD, empty slots at the image edges (odd tile counts) -- the
-    forward's images bit for bit, the backward at the run-to-run spread of
-    the float atomics."""
+    """The XCD-grouped dispatch order (tile_order_grouped_kernel, the default;
+    debug flag bit 4 restores the per-tile order): 2x2 groups of tiles,
+    heaviest group first, a group's tiles in slots of one XCD, empty slots at
+    the image edges (odd tile counts) -- the forward's images bit for bit, the
+    backward at the run-to-run spread of the float atomics."""
     from gsplat_hip import _lib
     ins, _, _ = _scene(W=W, H=H)
     old_split = _lib.query("gsplat_hip_debug_set_fwd_split", 0)  # the unsplit forward

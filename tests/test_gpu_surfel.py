@@ -575,3 +575,54 @@ def test_rasterization_2dgs_packed_matches_dense(mode, sh):
         close(b, a, 1e-5, 1e-5, n)
     for a, b, n in zip(grads[0], grads[1], ("means", "quats", "scales", "opacities", "colors")):
         close(b, a, 1e-4, 1e-5 * max(1.0, float(a.abs().max())), n)
+
+
+@pytest.mark.parametrize("thin", [False, True])
+def test_capped_surfel_tile_culling_changes_no_render(thin):
+    """The captured 2DGS step's isect (gsplat_hip_isect_write_sorted_capped_surfel,
+    rasterization_2dgs(_isect_capacity=..., _colors_only=True)): surfels whose
+    tile rectangle spans more than 16 supertiles get isects only in the tiles
+    their image can reach.  The scene has large and edge-on (thin) surfels
+    whose rectangles cover most of the image; fewer isects are written than
+    the rectangles hold, and the render -- colours and alphas -- equals the
+    uncapped colours-only render bit for bit (the rasterizer culls exactly
+    those isects on every strip); the gradients agree at the float atomics'
+    run-to-run spread."""
+    from gsplat_hip import rasterization_2dgs, rendering
+    rng = np.random.default_rng(21)
+    N, W, H = 3000, 1280, 720
+    means = (rng.standard_normal((N, 3)) * [1.2, 0.8, 0.4] + [0, 0, 3]).astype(np.float32)
+    quats = rng.standard_normal((N, 4)).astype(np.float32)
+    scales = (rng.random((N, 3)) * 0.05 + 0.005).astype(np.float32)
+    big = rng.random(N) < 0.03  # large surfels: rectangles over many supertiles
+    scales[big, :2] *= 20.0
+    if thin:  # needles seen edge-on: long thin images across the frame
+        scales[:, 1] = rng.uniform(0.0005, 0.002, N)
+    opac = rng.random(N).astype(np.float32)
+    sh = (rng.standard_normal((N, 16, 3)) * 0.3).astype(np.float32)
+    vm = np.eye(4, dtype=np.float32)[None]
+    K = np.array([[900.0, 0, W / 2], [0, 900.0, H / 2], [0, 0, 1]], np.float32)[None]
+    res = []
+    for capped in (False, True, False):
+        leaves = [T(x).requires_grad_(True) for x in (means, quats, scales, opac, sh)]
+        kw = dict(_isect_capacity=4 << 20) if capped else {}
+        rc, ra, _, _, _, _, meta = rasterization_2dgs(
+            *leaves[:4], leaves[4], T(vm), T(K), W, H, sh_degree=3, render_mode="RGB+D",
+            _colors_only=True, **kw)
+        w = torch.linspace(-1, 1, rc.numel(), device=DEV).view_as(rc)
+        (rc * w).sum().backward()
+        torch.cuda.synchronize()
+        res.append((rc.detach(), ra.detach(), [x.grad for x in leaves], meta))
+    (rc0, ra0, g0, m0), (rc1, ra1, g1, m1), (_, _, g0b, _) = res
+    counts = m1["isect_counts"].cpu().numpy()
+    n_rect = int(m0["flatten_ids"].numel())
+    assert counts[2] == 0 and counts[3] == n_rect, (counts, n_rect)
+    assert counts[0] < n_rect, "no isect culled: the scene has no large surfel"
+    print(f"isects written {counts[0]} of {n_rect} ({counts[0] / n_rect:.3f})")
+    assert rendering.TILE_CULL
+    assert torch.equal(rc0, rc1) and torch.equal(ra0, ra1)
+    for a, a2, b, name in zip(g0, g0b, g1, ["means", "quats", "scales", "opac", "sh"]):
+        scale = float(a.abs().max())
+        spread = float((a2 - a).abs().max())
+        err = float((b - a).abs().max())
+        assert err <= max(4.0 * spread, 1e-5 * scale) + 1e-12, (name, err, spread, scale)
