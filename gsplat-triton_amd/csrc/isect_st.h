@@ -207,12 +207,23 @@ emit_kernel(int64_t nV, const int64_t *__restrict__ cap, const int32_t *__restri
   }
 }
 
-// (2b) tile culling of large surfels (SurfelCull), one lane per pair, before
-// the supertile pass: a pair of a surfel with more than kLanePairs pairs gets
-// kTightFlag and, in key bits 16..31, the tiles of its supertile that the
-// surfel's image can reach (surfel_keep on the tile's pixel centres).  The
-// emission writes a surfel's pairs consecutively, so the waves holding large
-// surfels' pairs run the tests on all lanes.
+// (2b) tile culling of large surfels (SurfelCull), before the supertile pass:
+// a pair of a surfel with more than kLanePairs pairs gets kTightFlag and, in
+// key bits 16..31, the tiles of its supertile that the surfel's image can
+// reach (surfel_keep on the tiles' pixel centres).  The emission writes a
+// surfel's pairs consecutively, so a wave mostly holds one surfel's pairs,
+// most of whose supertiles a thin surfel does not cross.  Two phases per wave:
+// every lane tests its whole supertile (one test); then the surviving pairs'
+// tiles are dealt out 16 lanes to a pair, 4 pairs per round (the pair's
+// surfel from its lane by bpermute, the kept tiles back by one ballot), so a
+// wave runs ceil(survivors / 4) tile tests instead of 16.  (Per-lane tile
+// loops made it 88 us per M5 step: every wave paid for its busiest lane.)
+GS_INLINE bool reach_tiles(const float *m9, float mx, float my, float op, int ts, int x0, int x1,
+                           int y0, int y1) {  // tiles [x0, x1) x [y0, y1)
+  return surfel::surfel_keep(m9, mx, my, op, (float)(x0 * ts) + 0.5f, (float)(x1 * ts) - 0.5f,
+                             (float)(y0 * ts) + 0.5f, (float)(y1 * ts) - 0.5f);
+}
+
 __global__ void __launch_bounds__(256)
 tight_kernel(int64_t cap_pairs, const int64_t *__restrict__ n_pairs, Geo geo,
              const int32_t *__restrict__ Vs, const ushort4 *__restrict__ rect,
@@ -220,38 +231,70 @@ tight_kernel(int64_t cap_pairs, const int64_t *__restrict__ n_pairs, Geo geo,
              const int32_t *__restrict__ pval, SurfelCull sc) {
   if (void_call(cap)) return;
   const int64_t n = min(cap_pairs, n_pairs[0]);
-  // grid-stride: the grid is sized for a few sweeps of the chip, not for the
-  // capacity (a capacity-sized grid of mostly empty workgroups cost 87 us per
-  // step at M5)
-  for (int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x; p < n;
-       p += (int64_t)gridDim.x * 256) {
-  const uint32_t key = pkey[p];
-  if ((int)key >= geo.nst - 1) continue;  // the negative-depth key: no tiles to cull
-  const int32_t s = pval[p];
-  const ushort4 r = rect[s];
-  const int sx0 = r.x / S, sy0 = r.z / S;
-  const int np = ((r.y - 1) / S - sx0 + 1) * ((r.w - 1) / S - sy0 + 1);
-  if (np <= kLanePairs) continue;
-  const int32_t g = Vs[s];
-  float m9[9];
+  const int lane = threadIdx.x & 63;
+  // grid-stride over wave-sized chunks (the ballots need whole waves)
+  for (int64_t base = (int64_t)blockIdx.x * 256 + (threadIdx.x & ~63); base < n;
+       base += (int64_t)gridDim.x * 256) {
+    const int64_t p = base + lane;
+    uint32_t key = 0u;
+    bool big = false;
+    ushort4 r = {0, 0, 0, 0};
+    int32_t g = 0;
+    if (p < n) {
+      key = pkey[p];
+      if ((int)key < geo.nst - 1) {  // not the negative-depth key: no tiles to cull
+        const int32_t s = pval[p];
+        r = rect[s];
+        const int sx0 = r.x / S, sy0 = r.z / S;
+        big = ((r.y - 1) / S - sx0 + 1) * ((r.w - 1) / S - sy0 + 1) > kLanePairs;
+        if (big) g = Vs[s];
+      }
+    }
+    if (__ballot(big) == 0ull) continue;
+    float m9[9], mx = 0.f, my = 0.f, op = 0.f;
 #pragma unroll
-  for (int i = 0; i < 9; ++i) m9[i] = sc.T[9 * (int64_t)g + i];
-  const float mx = sc.means2d[2 * (int64_t)g], my = sc.means2d[2 * (int64_t)g + 1];
-  const float op = sc.opac[g];
-  const int rr = (int)key % geo.nst1;  // supertile within its camera
-  const int sy = rr / geo.stw, sx = rr - sy * geo.stw;
-  const int tx0 = sx * S, ty0 = sy * S;
-  uint32_t m = st_mask(r, tx0, ty0), keep = 0u;
-  while (m) {
-    const int t = __builtin_ctz(m);
-    m &= m - 1u;
-    const float x0 = (float)((tx0 + t % S) * sc.ts) + 0.5f;
-    const float y0 = (float)((ty0 + t / S) * sc.ts) + 0.5f;
-    if (surfel::surfel_keep(m9, mx, my, op, x0, x0 + (float)(sc.ts - 1), y0,
-                            y0 + (float)(sc.ts - 1)))
-      keep |= 1u << t;
-  }
-  pkey[p] = key | kTightFlag | (keep << 16);
+    for (int i = 0; i < 9; ++i) m9[i] = big ? sc.T[9 * (int64_t)g + i] : 0.f;
+    if (big) {
+      mx = sc.means2d[2 * (int64_t)g];
+      my = sc.means2d[2 * (int64_t)g + 1];
+      op = sc.opac[g];
+    }
+    const int rr = (int)key % geo.nst1;  // supertile within its camera
+    const int sy = rr / geo.stw;
+    const int tx0 = (rr - sy * geo.stw) * S, ty0 = sy * S;
+    const int ix0 = max((int)r.x, tx0), ix1 = min((int)r.y, tx0 + S);
+    const int iy0 = max((int)r.z, ty0), iy1 = min((int)r.w, ty0 + S);
+    // phase 1: the pair's covered part of its supertile
+    const bool live = big && ix0 < ix1 && iy0 < iy1 &&
+                      reach_tiles(m9, mx, my, op, sc.ts, ix0, ix1, iy0, iy1);
+    uint32_t keep = 0u;
+    // phase 2: 4 surviving pairs per round, one tile per lane
+    uint64_t rem = __ballot(live);
+    const int q = lane >> 4, t = lane & 15;
+    while (rem) {
+      int own[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        own[j] = rem ? __builtin_ctzll(rem) : 64;
+        rem &= rem - 1ull;
+      }
+      const int o = q == 0 ? own[0] : q == 1 ? own[1] : q == 2 ? own[2] : own[3];
+      const int src = o & 63;
+      float n9[9];
+#pragma unroll
+      for (int i = 0; i < 9; ++i) n9[i] = __shfl(m9[i], src, 64);
+      const float nx = __shfl(mx, src, 64), ny = __shfl(my, src, 64), nop = __shfl(op, src, 64);
+      const int a0 = __shfl(ix0, src, 64), a1 = __shfl(ix1, src, 64);
+      const int b0 = __shfl(iy0, src, 64), b1 = __shfl(iy1, src, 64);
+      const int x = __shfl(tx0, src, 64) + (t & (S - 1)), y = __shfl(ty0, src, 64) + t / S;
+      const bool hit = o < 64 && x >= a0 && x < a1 && y >= b0 && y < b1 &&
+                       reach_tiles(n9, nx, ny, nop, sc.ts, x, x + 1, y, y + 1);
+      const uint64_t hb = __ballot(hit);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (lane == own[j]) keep = (uint32_t)(hb >> (16 * j)) & 0xffffu;
+    }
+    if (big) pkey[p] = key | kTightFlag | (keep << 16);
   }
 }
 
