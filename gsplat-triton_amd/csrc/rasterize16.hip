@@ -1681,7 +1681,7 @@ static SplitLayout split_layout(int D, int n_tiles, int64_t n_isects) {
 // the forward): M2 forward 0.1622 / 0.1622 against 0.1655 / 0.1649 ms, L2 hit
 // rate 0.618 -> 0.713, fetched bytes -27 %; M3 with the split off 0.605 /
 // 0.603 against 0.608 / 0.608 ms, hit 0.451 -> 0.522, fetched -15 %.
-static int dbg_flags();
+int dbg_flags();
 static int order_slots(int C, int tw, int th) {
   return 32 * ((r16::order_groups(C, tw, th) + 7) / 8);
 }
@@ -1720,7 +1720,7 @@ int64_t rasterize16_fwd_state_bytes(int D, int n_tiles, int64_t n_isects) {
 // lane won 32 % -- and was removed.
 
 static int g_dbg = INT32_MIN;  // not yet read from the environment
-static int dbg_flags() {
+int dbg_flags() {  // also the 2DGS backward's (surfel.hip)
   if (g_dbg == INT32_MIN) {
     const char *e = getenv("GSPLAT_HIP_DBG");
     g_dbg = e ? atoi(e) : 0;

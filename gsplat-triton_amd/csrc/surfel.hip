@@ -365,6 +365,7 @@ struct RasterArgs {
       *v_render_median;
   float *packed;  // [G][S] gradient rows
   int S;
+  int dbg;  // gsplat_hip_debug_set_flags: backward bits 0 / 2 / 3 as the 3DGS kernel's
 };
 
 // Pixel of lane `lane` in wave `w`: the 64w + lane-th pixel of the tile in
@@ -1371,8 +1372,13 @@ struct PixState {
 // LEAN: v_render_normals, v_render_distort and v_render_median are null (the
 // terms they feed are exact zeros, skipped): 26 fewer VGPRs of per-pixel state
 // and no normal fields in the reduce-scatter.
-template <int D, bool ABS, bool LEAN = false>
-__global__ void __launch_bounds__(128) bwd2_kernel(RasterArgs a) {
+// DBG (LEAN only, launched when gsplat_hip_debug_set_flags bits 0 / 2 / 3 or
+// 6 -- this instance with nothing skipped -- are set): the timing-attribution instance (its checks cost 19 VGPRs, so the
+// production instance does not carry them; held to the production's 4 waves
+// per SIMD)
+template <int D, bool ABS, bool LEAN = false, bool DBG = false>
+__global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(DBG ? 4 : 1)))
+bwd2_kernel(RasterArgs a) {
   using R = Rec<D>;
   using F = Fields<D, ABS, LEAN>;
   extern __shared__ float4 lds4[];
@@ -1488,6 +1494,10 @@ __global__ void __launch_bounds__(128) bwd2_kernel(RasterArgs a) {
         s.T *= ra;
         const float T = s.T;
         const float fac = hk.alpha * T;
+        if (DBG && (a.dbg & 8)) {  // timing attribution only: no gradient algebra
+          v[0] += fac;
+          continue;
+        }
         float v_alpha = 0.f;
 #pragma unroll
         for (int d = 0; d < D; ++d) {
@@ -1556,9 +1566,18 @@ __global__ void __launch_bounds__(128) bwd2_kernel(RasterArgs a) {
 #pragma unroll
       for (int kq = 0; kq < F::NV; ++kq) {
         constexpr int NQ = F::NF - 16 * (F::NV - 1);
-        const float tot = kq < F::NV - 1 ? reduce_scatter<16>(v + 16 * kq, lane)
-                                         : reduce_scatter<NQ>(v + 16 * kq, lane);
-        if ((lane & 3) == 0 && lf < (kq < F::NV - 1 ? 16 : NQ) && tot != 0.f)
+        float tot;
+        if (DBG && (a.dbg & 4)) {  // timing attribution only: the lane's own partial
+          tot = v[16 * kq];
+#pragma unroll
+          for (int i = 1; i < 16; ++i)
+            if (lf == i) tot = v[16 * kq + i];
+        } else {
+          tot = kq < F::NV - 1 ? reduce_scatter<16>(v + 16 * kq, lane)
+                               : reduce_scatter<NQ>(v + 16 * kq, lane);
+        }
+        if ((lane & 3) == 0 && lf < (kq < F::NV - 1 ? 16 : NQ) && tot != 0.f &&
+            !(DBG && (a.dbg & 1)))
           atomic_add_f32(row + 16 * kq + lf, tot);
       }
     }
@@ -1632,6 +1651,9 @@ unpack_kernel(int64_t G, const int32_t *__restrict__ visible, const float *__res
 }  // namespace surfel
 }  // namespace gs
 
+namespace gs {
+int dbg_flags();  // rasterize16.hip: GSPLAT_HIP_DBG / gsplat_hip_debug_set_flags
+}
 using namespace gs;
 using namespace gs::surfel;
 
@@ -2017,6 +2039,7 @@ extern "C" int gsplat_hip_rasterize_2dgs_bwd(
                "rasterize_2dgs_bwd: null pointer argument (median_ids: null only for a "
                "colours-only render's backward)");
     RasterArgs a{};
+    a.dbg = gs::dbg_flags();
     a.C = C; a.W = width; a.H = height; a.ts = tile_size; a.tw = tile_width;
     a.th = tile_height; a.n_tiles = n_tiles; a.n_isects = n_isects; a.n_dev = n_isects_device;
     a.order = tile_order;
@@ -2039,6 +2062,9 @@ extern "C" int gsplat_hip_rasterize_2dgs_bwd(
     if (lean && absgrad)                                                                      \
       hipLaunchKernelGGL((bwd2_kernel<n <= 4 ? n : 4, true, true>), dim3(n_tiles), dim3(128), \
                          lds / 2, st, a);                                                     \
+    else if (lean && (a.dbg & 77))                                                            \
+      hipLaunchKernelGGL((bwd2_kernel<n <= 4 ? n : 4, false, true, true>), dim3(n_tiles),     \
+                         dim3(128), lds / 2, st, a);                                          \
     else if (lean)                                                                            \
       hipLaunchKernelGGL((bwd2_kernel<n <= 4 ? n : 4, false, true>), dim3(n_tiles), dim3(128),\
                          lds / 2, st, a);                                                     \

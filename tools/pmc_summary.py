@@ -7,7 +7,7 @@ import sys
 
 root = sys.argv[1]
 vals = collections.defaultdict(lambda: collections.defaultdict(list))
-for f in glob.glob(f"{root}/*/p_counter_collection.csv"):
+for f in glob.glob(f"{root}/*/p_counter_collection.csv") + glob.glob(f"{root}/p_counter_collection.csv"):
     per = collections.defaultdict(float)
     names = {}
     for r in csv.DictReader(open(f)):
