@@ -415,7 +415,9 @@ int64_t gsplat_hip_fwd_split_threshold(int64_t n_isects);
  * of the unsplit forward instead of the XCD-grouped one (same results);
  * bit 1 = a chunk of a split tile never waits for an earlier chunk's
  * published product and computes it itself (the timeout path; results are
- * identical).  Returns the previous flags. */
+ * identical).  Bits 0, 2 and 3 also apply to the 2DGS colours-only (LEAN)
+ * backward, which then runs its attribution instance; bit 6 runs that
+ * instance with nothing skipped (its baseline).  Returns the previous flags. */
 int gsplat_hip_debug_set_flags(int flags);
 
 /* ---------------------------------------------------------------------------
