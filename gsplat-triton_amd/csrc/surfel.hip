@@ -346,6 +346,8 @@ struct Rec {
   static constexpr int N4 = NF / 4;
 };
 
+typedef float f2v __attribute__((ext_vector_type(2)));
+
 struct RasterArgs {
   int C, W, H, ts, tw, th, n_tiles;
   int64_t n_isects;       // isect count, or with n_dev the capacity of flatten_ids
@@ -1475,10 +1477,57 @@ bwd2_kernel(RasterArgs a) {
       const float *m = r + R::M;
       Hit h[2];
       bool valid[2];
+      if constexpr (LEAN) {
+        // both pixels as one packed pair: same column fx (h_u = fx w - u
+        // shared), rows fy0 / fy1; the reference's cross product h_u x h_v
+        const float fx = ps[0].fx;
+        const f2v fy = f2v{ps[0].fy, ps[1].fy};
+        float hu[3];
+        f2v hv[3];
 #pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        h[k] = eval_hit(m, r[R::X], r[R::Y], r[R::OP], ps[k].fx, ps[k].fy);
-        valid[k] = ps[k].inside && idx <= ps[k].bin_final && h[k].ok;
+        for (int i = 0; i < 3; ++i) {
+          hu[i] = fx * m[6 + i] - m[i];
+          hv[i] = __builtin_elementwise_fma(fy, f2v{m[6 + i], m[6 + i]}, f2v{-m[3 + i], -m[3 + i]});
+        }
+        f2v rc[3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+          const int i1 = (i + 1) % 3, i2 = (i + 2) % 3;
+          rc[i] = f2v{hu[i1], hu[i1]} * hv[i2] - f2v{hu[i2], hu[i2]} * hv[i1];
+        }
+        const f2v iz = f2v{__builtin_amdgcn_rcpf(rc[2].x), __builtin_amdgcn_rcpf(rc[2].y)};
+        const f2v sx = rc[0] * iz, sy = rc[1] * iz;
+        const f2v g3 = __builtin_elementwise_fma(sx, sx, sy * sy);
+        const float dx = r[R::X] - fx;
+        const f2v dy = f2v{r[R::Y], r[R::Y]} - fy;
+        const f2v g2 = kFilterInvSquare * __builtin_elementwise_fma(dy, dy, f2v{dx * dx, dx * dx});
+        const f2v sigma = 0.5f * f2v{fminf(g3.x, g2.x), fminf(g3.y, g2.y)};
+        const f2v ex = sigma * -kLog2e;
+        const f2v vis = f2v{__builtin_amdgcn_exp2f(ex.x), __builtin_amdgcn_exp2f(ex.y)};
+        const f2v al = r[R::OP] * vis;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          h[k].s[0] = sx[k];
+          h[k].s[1] = sy[k];
+          h[k].rc[2] = rc[2][k];
+          h[k].g3 = g3[k];
+          h[k].g2 = g2[k];
+          h[k].vis = vis[k];
+          h[k].alpha = fminf(kAlphaMax, al[k]);
+          h[k].ok = (rc[2][k] != 0.f) && !(sigma[k] < 0.f) && !(h[k].alpha < kAlphaMin);
+#pragma unroll
+          for (int i = 0; i < 3; ++i) {
+            h[k].hu[i] = hu[i];
+            h[k].hv[i] = hv[i][k];
+          }
+          valid[k] = ps[k].inside && idx <= ps[k].bin_final && h[k].ok;
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          h[k] = eval_hit(m, r[R::X], r[R::Y], r[R::OP], ps[k].fx, ps[k].fy);
+          valid[k] = ps[k].inside && idx <= ps[k].bin_final && h[k].ok;
+        }
       }
       if (__ballot(valid[0] | valid[1]) == 0) continue;
       float v[16 * F::NV];
