@@ -546,11 +546,9 @@ fused_kernel(int B, int H, int W, const float *__restrict__ x,
   float lsum = 0.f, ssum = 0.f;
   // backward vertical pass mapping: column gc, image rows 2 gr, 2 gr + 1
   const int gc = tid & 31, gr = tid >> 5;
-#pragma nounroll
-  for (int c = cg * CPW; c < cg * CPW + CPW; ++c) {
-    // ---- stage channel c (+ its L1 over the tile's own pixels, window
-    // rows / cols 2R .. 2R+31)
-    load(c);
+  // the loaded window into s_xy (+ its L1 over the tile's own pixels, window
+  // rows / cols 2R .. 2R+31)
+  auto stage = [&]() {
 #pragma unroll
     for (int k = 0; k < kFRows; ++k) {
       const int r = w8 + 8 * k, gi = ri0 + r;
@@ -560,7 +558,17 @@ fused_kernel(int B, int H, int W, const float *__restrict__ x,
       if (r >= 2 * R && r < 2 * R + FT && lane >= 2 * R && lane < 2 * R + FT)
         lsum += fabsf(a - bb);
     }
-    __syncthreads();
+  };
+  // The next channel's window is loaded while pass C1 runs (its latency
+  // hidden behind C1) and staged while C2 runs: s_xy's last readers of this
+  // channel (pass C1, through m01 / m2) are behind C1's barrier, and this
+  // channel's own pixels (px0 / px1) were read into registers before pass A.
+  const int c_end = cg * CPW + CPW;
+  load(cg * CPW);
+  stage();
+  __syncthreads();
+#pragma nounroll
+  for (int c = cg * CPW; c < c_end; ++c) {
     const f2v px0 = s_xy[2 * R + 2 * gr][2 * R + gc], px1 = s_xy[2 * R + 2 * gr + 1][2 * R + gc];
     // ---- A: horizontal blur of the statistics, FI rows x FM columns
     static_assert(FM % kHA == 0 && FT % kHC == 0, "pass A / C1 blocking");
@@ -644,6 +652,8 @@ fused_kernel(int B, int H, int W, const float *__restrict__ x,
       }
     }
     __syncthreads();
+    const bool more = c + 1 < c_end;
+    if (more) load(c + 1);
     // ---- C1: horizontal blur of the partials, FM rows x FT columns (the
     // adjoint of the valid correlation: full correlation with the symmetric
     // kernel, see bwd_kernel), into hA
@@ -671,10 +681,10 @@ fused_kernel(int B, int H, int W, const float *__restrict__ x,
       }
     }
     __syncthreads();
+    if (more) stage();  // the next channel's window (s_xy is free: see above)
     // ---- C2: vertical blur onto the tile pixels, gradient out.  (The next
-    // channel's staging writes only s_xy, whose last readers, pass C1, are
-    // behind the barrier above; its pass A rewrites hA only after the
-    // staging barrier, which every thread reaches after its C2.)
+    // channel's pass A rewrites hA, which C2 reads, only after the barrier
+    // below.)
     {
       f2v oa[2] = {f2v{0.f, 0.f}, f2v{0.f, 0.f}};
       float oc[2] = {0.f, 0.f};
@@ -704,6 +714,7 @@ fused_kernel(int B, int H, int W, const float *__restrict__ x,
               cs * (oa[j].x + 2.f * v.x * oa[j].y + v.y * oc[j]) + cl * sgn;
       }
     }
+    if (more) __syncthreads();  // the staged window, and C2's reads of hA done
   }
   if (XS > C && cg == CG - 1) {  // the render's other channels: no loss term, zero gradient
 #pragma unroll
