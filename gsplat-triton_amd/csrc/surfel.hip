@@ -1439,6 +1439,14 @@ bwd2_kernel(RasterArgs a) {
   for (int m = 32; m >= 1; m >>= 1) wmax = max(wmax, __shfl_xor(wmax, m, 64));
   const int64_t end = min(tend, (int64_t)wmax + 1);
   const int lf = rs_field(lane);
+  // LEAN: the two pixels' state as packed pairs (.x pixel 0, .y pixel 1)
+  f2v T2 = f2v{ps[0].T, ps[1].T}, tfvb2 = f2v{ps[0].tfvb, ps[1].tfvb};
+  f2v buf2[D], vc2[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    buf2[d] = f2v{0.f, 0.f};
+    vc2[d] = f2v{ps[0].vc[d], ps[1].vc[d]};
+  }
 
   // LEAN: the next batch's surfel ids loaded while this one composites (the
   // batch's gathers then wait one global load, not two), and no normals
@@ -1531,6 +1539,79 @@ bwd2_kernel(RasterArgs a) {
       }
       if (__ballot(valid[0] | valid[1]) == 0) continue;
       float v[16 * F::NV];
+      if constexpr (LEAN && !DBG) {
+        // both pixels' gradient terms as packed pairs, branch-free: an
+        // invalid pixel enters with alpha 0 (ra = 1, fac = 0: its T and
+        // colour sums unchanged) and weight 0; the inputs of the branch not
+        // taken are zeroed, so no inf / NaN of an unused branch reaches a sum
+        const f2v al = f2v{valid[0] ? h[0].alpha : 0.f, valid[1] ? h[1].alpha : 0.f};
+        const f2v vis = f2v{h[0].vis, h[1].vis};
+        const f2v ra = f2v{__builtin_amdgcn_rcpf(1.f - al.x), __builtin_amdgcn_rcpf(1.f - al.y)};
+        T2 = T2 * ra;
+        const f2v fac = al * T2;
+        f2v va = f2v{0.f, 0.f};
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+          const f2v cT = __builtin_elementwise_fma(f2v{r[R::COL + d], r[R::COL + d]}, T2,
+                                                   -(buf2[d] * ra));
+          va = __builtin_elementwise_fma(cT, vc2[d], va);
+        }
+        va = __builtin_elementwise_fma(ra, tfvb2, va);
+        // pixels past the clamp (op * vis > kAlphaMax) take no opacity /
+        // geometry gradient
+        const float op = r[R::OP];
+        const f2v wt = f2v{(valid[0] && op * h[0].vis <= kAlphaMax) ? va.x : 0.f,
+                           (valid[1] && op * h[1].vis <= kAlphaMax) ? va.y : 0.f};
+        const f2v vG = op * wt;
+        const bool s0 = h[0].g3 <= h[0].g2, s1 = h[1].g3 <= h[1].g2;
+        // the ray-splat branch (g3 <= g2): vrc from the UV-plane gradient
+        const bool b0 = s0 && valid[0], b1 = s1 && valid[1];
+        const f2v ssx = f2v{b0 ? h[0].s[0] : 0.f, b1 ? h[1].s[0] : 0.f};
+        const f2v ssy = f2v{b0 ? h[0].s[1] : 0.f, b1 ? h[1].s[1] : 0.f};
+        const f2v izs = f2v{b0 ? __builtin_amdgcn_rcpf(h[0].rc[2]) : 0.f,
+                            b1 ? __builtin_amdgcn_rcpf(h[1].rc[2]) : 0.f};
+        const f2v nvG = vG * -vis;
+        const f2v ax = nvG * ssx * izs, ay = nvG * ssy * izs;
+        const f2v vrc[3] = {ax, ay, -__builtin_elementwise_fma(ax, ssx, ay * ssy)};
+        const float fx = ps[0].fx;
+        const f2v fy = f2v{ps[0].fy, ps[1].fy};
+        f2v hv[3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) hv[i] = f2v{h[0].hv[i], h[1].hv[i]};
+        const float *hu = h[0].hu;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+          const int i1 = (i + 1) % 3, i2 = (i + 2) % 3;
+          const f2v vhu = hv[i1] * vrc[i2] - hv[i2] * vrc[i1];
+          const f2v vhv = vrc[i1] * hu[i2] - vrc[i2] * hu[i1];
+          const f2v t6 = __builtin_elementwise_fma(fy, vhv, fx * vhu);
+          v[F::M + i] = -vhu.x - vhu.y;
+          v[F::M + 3 + i] = -vhv.x - vhv.y;
+          v[F::M + 6 + i] = t6.x + t6.y;
+        }
+        // the screen-space branch (g3 > g2): means2d
+        const f2v vG2 = f2v{s0 ? 0.f : vG.x, s1 ? 0.f : vG.y};
+        const float dx = r[R::X] - fx;
+        const f2v dy = f2v{r[R::Y], r[R::Y]} - fy;
+        const f2v nk = -vis * kFilterInvSquare;
+        const f2v gx = vG2 * (nk * dx), gy = vG2 * (nk * dy);
+        v[F::XY] = gx.x + gx.y;
+        v[F::XY + 1] = gy.x + gy.y;
+        if constexpr (ABS) {
+          v[F::AB] = fabsf(gx.x) + fabsf(gx.y);
+          v[F::AB + 1] = fabsf(gy.x) + fabsf(gy.y);
+        }
+        const f2v vo = vis * wt;
+        v[F::OP] = vo.x + vo.y;
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+          const f2v vcol = fac * vc2[d];
+          v[F::COL + d] = vcol.x + vcol.y;
+          buf2[d] = __builtin_elementwise_fma(f2v{r[R::COL + d], r[R::COL + d]}, fac, buf2[d]);
+        }
+#pragma unroll
+        for (int kk = F::NF; kk < 16 * F::NV; ++kk) v[kk] = 0.f;
+      } else {
 #pragma unroll
       for (int kk = 0; kk < 16 * F::NV; ++kk) v[kk] = 0.f;
 #pragma unroll
@@ -1609,6 +1690,7 @@ bwd2_kernel(RasterArgs a) {
 #pragma unroll
           for (int i = 0; i < 3; ++i) s.bufn[i] += r[R::NRM + i] * fac;
         }
+      }
       }
       const int32_t g = __float_as_int(r[R::G]);
       float *row = a.packed + (int64_t)g * F::S;
