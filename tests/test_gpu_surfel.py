@@ -577,8 +577,8 @@ def test_rasterization_2dgs_packed_matches_dense(mode, sh):
         close(b, a, 1e-4, 1e-5 * max(1.0, float(a.abs().max())), n)
 
 
-@pytest.mark.parametrize("thin", [False, True])
-def test_capped_surfel_tile_culling_changes_no_render(thin):
+@pytest.mark.parametrize("thin,dense", [(False, False), (True, False), (False, True)])
+def test_capped_surfel_tile_culling_changes_no_render(thin, dense):
     """The captured 2DGS step's isect (gsplat_hip_isect_write_sorted_capped_surfel,
     rasterization_2dgs(_isect_capacity=..., _colors_only=True)): surfels whose
     tile rectangle spans more than 16 supertiles get isects only in the tiles
@@ -587,14 +587,16 @@ def test_capped_surfel_tile_culling_changes_no_render(thin):
     the rectangles hold, and the render -- colours and alphas -- equals the
     uncapped colours-only render bit for bit (the rasterizer culls exactly
     those isects on every strip); the gradients agree at the float atomics'
-    run-to-run spread."""
+    run-to-run spread.  `dense`: most surfels large at 1080p -- over a
+    million (supertile, surfel) pairs, more than one sweep of the culling
+    kernel's grid-stride loop (2048 x 256 lanes)."""
     from gsplat_hip import rasterization_2dgs, rendering
     rng = np.random.default_rng(21)
-    N, W, H = 3000, 1280, 720
+    N, W, H = (8000, 1920, 1080) if dense else (3000, 1280, 720)
     means = (rng.standard_normal((N, 3)) * [1.2, 0.8, 0.4] + [0, 0, 3]).astype(np.float32)
     quats = rng.standard_normal((N, 4)).astype(np.float32)
     scales = (rng.random((N, 3)) * 0.05 + 0.005).astype(np.float32)
-    big = rng.random(N) < 0.03  # large surfels: rectangles over many supertiles
+    big = rng.random(N) < (0.6 if dense else 0.03)  # large: rectangles over many supertiles
     scales[big, :2] *= 20.0
     if thin:  # needles seen edge-on: long thin images across the frame
         scales[:, 1] = rng.uniform(0.0005, 0.002, N)
@@ -605,7 +607,7 @@ def test_capped_surfel_tile_culling_changes_no_render(thin):
     res = []
     for capped in (False, True, False):
         leaves = [T(x).requires_grad_(True) for x in (means, quats, scales, opac, sh)]
-        kw = dict(_isect_capacity=4 << 20) if capped else {}
+        kw = dict(_isect_capacity=(48 << 20) if dense else (4 << 20)) if capped else {}
         rc, ra, _, _, _, _, meta = rasterization_2dgs(
             *leaves[:4], leaves[4], T(vm), T(K), W, H, sh_degree=3, render_mode="RGB+D",
             _colors_only=True, **kw)
