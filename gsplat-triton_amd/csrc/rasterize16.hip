@@ -106,6 +106,7 @@ GS_INLINE f2v reduce_scatter2(const f2v *v, int lane) {
 // colour[D], pad] (D <= kRecMaxD), so the per-isect gather of a batch touches
 // one 64-B sector per lane instead of four lines of four arrays
 // (rasterize_to_pixels_fwd.py:93-145 loads the four arrays separately).
+constexpr int kItemRun = 4;  // backward work items per XCD run (bwd2_kernel)
 constexpr int kRecFloats = 16;
 constexpr int kRecMaxD = kRecFloats - 6;
 
@@ -861,6 +862,14 @@ __attribute__((amdgpu_waves_per_eu(BwdOcc<PX>::W))) bwd2_kernel(Args a) {
   if (a.items) {
     const int nf = a.n_items[0];
     int b = blockIdx.x;
+    if (!(a.dbg & 16)) {
+      // XCD-aware: runs of kItemRun consecutive items (a tile's chunks, or
+      // neighbouring tiles of a row, which share Gaussians) on one XCD
+      // (workgroup b runs on XCD b % 8), the runs dealt round-robin so the
+      // list order -- full chunks first -- is kept across the chip
+      const int x = b & 7, kk = b >> 3;
+      b = ((kk / kItemRun) * 8 + x) * kItemRun + kk % kItemRun;
+    }
     if (b >= nf && b - nf >= a.n_items[1]) return;
     const int2 it = b < nf ? a.items[b] : a.items_tail[b - nf];
     tile = it.x;
@@ -1699,7 +1708,9 @@ static int64_t order_bytes(int n_tiles, int64_t n_isects) {
 
 static int64_t n_items_bound(int n_tiles, int64_t n_isects) {
   const int L = chunk_len();
-  return L ? (int64_t)n_tiles + n_isects / L + 1 : (int64_t)n_tiles;
+  const int64_t n = L ? (int64_t)n_tiles + n_isects / L + 1 : (int64_t)n_tiles;
+  const int64_t q = 8 * r16::kItemRun;  // whole rounds of the XCD-aware item order
+  return (n + q - 1) / q * q;
 }
 
 int64_t rasterize16_fwd_state_bytes(int D, int n_tiles, int64_t n_isects) {
