@@ -272,7 +272,9 @@ def test_xcd_grouped_order_changes_nothing(W, H):
     debug flag bit 4 restores the per-tile order): 2x2 groups of tiles,
     heaviest group first, a group's tiles in slots of one XCD, empty slots at
     the image edges (odd tile counts) -- the forward's images bit for bit, the
-    backward at the run-to-run spread of the float atomics."""
+    backward at the run-to-run spread of the float atomics.  The same flag
+    selects the backward's work-item order (runs of four items per XCD by
+    default, the list order with bit 4), which the gradients cover."""
     from gsplat_hip import _lib
     ins, _, _ = _scene(W=W, H=H)
     old_split = _lib.query("gsplat_hip_debug_set_fwd_split", 0)  # the unsplit forward
