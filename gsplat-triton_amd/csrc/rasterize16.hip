@@ -824,10 +824,19 @@ __attribute__((amdgpu_waves_per_eu(!SPLIT && D <= 3 ? 6 : 5))) fwd_kernel(Args a
   float4 *st = stage_all[threadIdx.x >> 6];
   if constexpr (SPLIT) {
     const int nc = a.n_chunks[0];
-    if ((int)blockIdx.x < nc)
+    if ((int)blockIdx.x < nc) {
       fwd_item<D, true>(a, st, (int)blockIdx.x);
-    else
-      fwd_item<D, false>(a, st, (int)blockIdx.x - nc);
+    } else {
+      // the whole tiles: runs of kItemRun consecutive order entries (same
+      // bucket, mostly neighbouring tiles) on one XCD, dealt round-robin
+      // (workgroup b runs on XCD b % 8; the runs keep their XCD whatever nc)
+      int j = (int)blockIdx.x - nc;
+      if (!(a.dbg & 16)) {
+        const int x = j & 7, kk = j >> 3;
+        j = ((kk / kItemRun) * 8 + x) * kItemRun + kk % kItemRun;
+      }
+      fwd_item<D, false>(a, st, j);
+    }
   } else {
     fwd_item<D, false>(a, st, (int)blockIdx.x);
   }
@@ -1781,8 +1790,10 @@ int r16_fwd(r16::Args a, const void *state, char *split_base, hipStream_t st) {
     const int64_t nc = std::min<int64_t>(
         (int64_t)a.n_tiles + a.n_isects / a.SL + 1,
         a.n_isects / a.SL + a.n_isects / std::max<int64_t>(1, split_threshold(a.n_isects)) + 1);
-    hipLaunchKernelGGL((r16::fwd_kernel<D, true>), dim3((unsigned)(a.n_tiles + nc)), dim3(256),
-                       0, st, a);
+    const int64_t nw = ((int64_t)a.n_tiles + 8 * r16::kItemRun - 1) / (8 * r16::kItemRun) *
+                       (8 * r16::kItemRun);  // whole rounds of the XCD runs
+    hipLaunchKernelGGL((r16::fwd_kernel<D, true>), dim3((unsigned)(nw + nc)), dim3(256), 0, st,
+                       a);
     GS_CHECK_LAUNCH("rasterize_fwd16_split");
     return 0;
   }
