@@ -412,8 +412,9 @@ int64_t gsplat_hip_fwd_split_threshold(int64_t n_isects);
  * bit 2 = the backward skips its cross-lane reduction, bit 3 its gradient
  * algebra, bit 5 = the forward stores no chunk state (timing / traffic
  * attribution only: wrong gradients); bit 4 = the per-tile dispatch order
- * of the unsplit forward and the list order of the backward's work items
- * instead of the XCD-grouped ones (same results);
+ * of the unsplit forward and the list order of the split forward's whole
+ * tiles and of the backward's work items instead of the XCD-grouped ones
+ * (same results);
  * bit 1 = a chunk of a split tile never waits for an earlier chunk's
  * published product and computes it itself (the timeout path; results are
  * identical).  Bits 0, 2 and 3 also apply to the 2DGS colours-only (LEAN)
