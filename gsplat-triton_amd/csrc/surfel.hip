@@ -368,7 +368,23 @@ struct RasterArgs {
   float *packed;  // [G][S] gradient rows
   int S;
   int dbg;  // gsplat_hip_debug_set_flags: backward bits 0 / 2 / 3 as the 3DGS kernel's
+  int xcd_runs;  // deal runs of 4 consecutive order entries to one XCD (order_tile)
 };
+
+// The tile of workgroup blockIdx.x, or -1 (a surplus workgroup of a grid
+// rounded up to whole rounds).  With xcd_runs, runs of four consecutive
+// entries of the heaviest-first order (same bucket, mostly neighbouring
+// tiles, which share surfels) go to one XCD (workgroup b runs on XCD b % 8),
+// dealt round-robin so the order is kept across the chip.
+GS_INLINE int order_tile(const RasterArgs &a) {
+  if (!a.order) return (int)blockIdx.x;
+  int b = (int)blockIdx.x;
+  if (a.xcd_runs) {
+    const int x = b & 7, kk = b >> 3;
+    b = ((kk >> 2) * 8 + x) * 4 + (kk & 3);
+  }
+  return b < a.n_tiles ? a.order[b] : -1;
+}
 
 // Pixel of lane `lane` in wave `w`: the 64w + lane-th pixel of the tile in
 // row-major order (a 16x4 strip for 16x16 tiles).
@@ -576,7 +592,9 @@ __global__ void __launch_bounds__(1024) fwd_kernel(RasterArgs a) {
   extern __shared__ float4 lds4[];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   float *q = reinterpret_cast<float *>(lds4) + (size_t)w * 64 * R::NF;
-  const Pix p(a, a.order ? a.order[blockIdx.x] : (int)blockIdx.x, w, lane);
+  const int otile = order_tile(a);
+  if (otile < 0) return;
+  const Pix p(a, otile, w, lane);
   const float fx = (float)p.px + 0.5f, fy = (float)p.py + 0.5f;
   const float *bg = a.backgrounds ? a.backgrounds + (int64_t)p.c * D : nullptr;
 
@@ -679,7 +697,8 @@ __global__ void __launch_bounds__(128) fwd2_kernel(RasterArgs a) {
   extern __shared__ float4 lds4[];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   float *q = reinterpret_cast<float *>(lds4) + (size_t)w * 64 * R::NF;
-  const int tile = a.order ? a.order[blockIdx.x] : (int)blockIdx.x;
+  const int tile = order_tile(a);
+  if (tile < 0) return;
   const int ntile = a.tw * a.th;
   const int c = tile / ntile;
   const int rem = tile - c * ntile;
@@ -1052,7 +1071,8 @@ GS_INLINE void srec_load_blend(const float *rec, int32_t g, SBlend<D> &r) {
 template <int D, bool LEAN = false>
 __global__ void __launch_bounds__(128) fwd2s_kernel(RasterArgs a, const float *__restrict__ rec) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int tile = a.order ? a.order[blockIdx.x] : (int)blockIdx.x;
+  const int tile = order_tile(a);
+  if (tile < 0) return;
   const int ntile = a.tw * a.th;
   const int c = tile / ntile;
   const int rem = tile - c * ntile;
@@ -1218,7 +1238,9 @@ __global__ void __launch_bounds__(256) bwd_kernel(RasterArgs a) {
   extern __shared__ float4 lds4[];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   float *q = reinterpret_cast<float *>(lds4) + (size_t)w * 64 * R::NF;
-  const Pix p(a, a.order ? a.order[blockIdx.x] : (int)blockIdx.x, w, lane);
+  const int otile = order_tile(a);
+  if (otile < 0) return;
+  const Pix p(a, otile, w, lane);
   if (a.masks && !a.masks[p.tile]) return;
   const float fx = (float)p.px + 0.5f, fy = (float)p.py + 0.5f;
   const int64_t pid = p.pid;
@@ -1386,7 +1408,8 @@ bwd2_kernel(RasterArgs a) {
   extern __shared__ float4 lds4[];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   float *q = reinterpret_cast<float *>(lds4) + (size_t)w * 64 * R::NF;
-  const int tile = a.order ? a.order[blockIdx.x] : (int)blockIdx.x;
+  const int tile = order_tile(a);
+  if (tile < 0) return;
   if (a.masks && !a.masks[tile]) return;
   const int ntile = a.tw * a.th;
   const int c = tile / ntile;
@@ -1804,6 +1827,9 @@ bool channels_supported(int D) {
 // bwd2 kernels; the one-pixel kernels, which measured 1.62 / 1.76 against
 // 1.10 / 1.63 ms at M5, serve the other tile sizes)
 bool fwd2_enabled() { return true; }
+// the XCD runs of the tile order (RasterArgs::xcd_runs; GSPLAT_HIP_DBG bit 4:
+// one tile after the other, as the 3DGS rasterizer's flag)
+int xcd_runs() { return !(gs::dbg_flags() & 16); }
 bool bwd2_enabled() { return true; }
 
 int fields_stride(int D, int absgrad) {
@@ -2057,10 +2083,13 @@ extern "C" int gsplat_hip_rasterize_2dgs_fwd(
   a.render_median = render_median; a.last_ids = last_ids; a.median_ids = median_ids;
   const int waves = (tile_size * tile_size + 63) / 64;
   hipStream_t st = (hipStream_t)stream;
+  unsigned grid_t = (unsigned)n_tiles;
   if (tile_order && n_tiles > 0) {  // written here, read by this launch and the backward
     hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(1024), 0, st, n_tiles, isect_offsets,
                        n_isects, n_isects_device, tile_order);
     a.order = tile_order;
+    a.xcd_runs = xcd_runs();
+    if (a.xcd_runs) grid_t = (unsigned)((n_tiles + 31) / 32 * 32);
   }
   // 16x16 tiles: two pixels per lane (fwd2_kernel)
   const bool px2 = tile_size == 16 && fwd2_enabled();
@@ -2069,9 +2098,9 @@ extern "C" int gsplat_hip_rasterize_2dgs_fwd(
                kSRecMaxD);
 #define GS_CASE(n)                                                                            \
   if (D == n && lean)                                                                         \
-    hipLaunchKernelGGL((fwd2s_kernel<n, true>), dim3(n_tiles), dim3(128), 0, st, a, records); \
+    hipLaunchKernelGGL((fwd2s_kernel<n, true>), dim3(grid_t), dim3(128), 0, st, a, records); \
   else if (D == n)                                                                            \
-    hipLaunchKernelGGL((fwd2s_kernel<n, false>), dim3(n_tiles), dim3(128), 0, st, a, records);
+    hipLaunchKernelGGL((fwd2s_kernel<n, false>), dim3(grid_t), dim3(128), 0, st, a, records);
     GS_CASE(1) GS_CASE(2) GS_CASE(3) GS_CASE(4)
 #undef GS_CASE
     GS_CHECK_LAUNCH("rasterize_2dgs_fwd");
@@ -2081,9 +2110,9 @@ extern "C" int gsplat_hip_rasterize_2dgs_fwd(
   if (D == n) {                                                                               \
     const size_t lds = (size_t)waves * 64 * Rec<n>::NF * sizeof(float);                       \
     if (px2)                                                                                  \
-      hipLaunchKernelGGL(fwd2_kernel<n>, dim3(n_tiles), dim3(128), lds / 2, st, a);           \
+      hipLaunchKernelGGL(fwd2_kernel<n>, dim3(grid_t), dim3(128), lds / 2, st, a);           \
     else                                                                                      \
-      hipLaunchKernelGGL(fwd_kernel<n>, dim3(n_tiles), dim3(64 * waves), lds, st, a);         \
+      hipLaunchKernelGGL(fwd_kernel<n>, dim3(grid_t), dim3(64 * waves), lds, st, a);         \
   }
   GS_SURFEL_CHANNELS(GS_CASE)
 #undef GS_CASE
@@ -2174,6 +2203,9 @@ extern "C" int gsplat_hip_rasterize_2dgs_bwd(
     a.C = C; a.W = width; a.H = height; a.ts = tile_size; a.tw = tile_width;
     a.th = tile_height; a.n_tiles = n_tiles; a.n_isects = n_isects; a.n_dev = n_isects_device;
     a.order = tile_order;
+    a.xcd_runs = tile_order ? xcd_runs() : 0;
+    const unsigned grid_t =
+        a.xcd_runs ? (unsigned)((n_tiles + 31) / 32 * 32) : (unsigned)n_tiles;
     a.means2d = means2d; a.ray_transforms = ray_transforms; a.colors = colors; a.depths = depths;
     a.opacities = opacities; a.normals = normals; a.backgrounds = backgrounds; a.masks = masks;
     a.offsets = isect_offsets; a.flatten_ids = flatten_ids;
@@ -2191,22 +2223,22 @@ extern "C" int gsplat_hip_rasterize_2dgs_bwd(
   if (D == n) {                                                                               \
     const size_t lds = (size_t)waves * 64 * Rec<n>::NF * sizeof(float);                       \
     if (lean && absgrad)                                                                      \
-      hipLaunchKernelGGL((bwd2_kernel<n <= 4 ? n : 4, true, true>), dim3(n_tiles), dim3(128), \
+      hipLaunchKernelGGL((bwd2_kernel<n <= 4 ? n : 4, true, true>), dim3(grid_t), dim3(128), \
                          lds / 2, st, a);                                                     \
     else if (lean && (a.dbg & 77))                                                            \
-      hipLaunchKernelGGL((bwd2_kernel<n <= 4 ? n : 4, false, true, true>), dim3(n_tiles),     \
+      hipLaunchKernelGGL((bwd2_kernel<n <= 4 ? n : 4, false, true, true>), dim3(grid_t),     \
                          dim3(128), lds / 2, st, a);                                          \
     else if (lean)                                                                            \
-      hipLaunchKernelGGL((bwd2_kernel<n <= 4 ? n : 4, false, true>), dim3(n_tiles), dim3(128),\
+      hipLaunchKernelGGL((bwd2_kernel<n <= 4 ? n : 4, false, true>), dim3(grid_t), dim3(128),\
                          lds / 2, st, a);                                                     \
     else if (px2 && absgrad)                                                                       \
-      hipLaunchKernelGGL((bwd2_kernel<n, true>), dim3(n_tiles), dim3(128), lds / 2, st, a);    \
+      hipLaunchKernelGGL((bwd2_kernel<n, true>), dim3(grid_t), dim3(128), lds / 2, st, a);    \
     else if (px2)                                                                             \
-      hipLaunchKernelGGL((bwd2_kernel<n, false>), dim3(n_tiles), dim3(128), lds / 2, st, a);   \
+      hipLaunchKernelGGL((bwd2_kernel<n, false>), dim3(grid_t), dim3(128), lds / 2, st, a);   \
     else if (absgrad)                                                                         \
-      hipLaunchKernelGGL((bwd_kernel<n, true>), dim3(n_tiles), dim3(64 * waves), lds, st, a);  \
+      hipLaunchKernelGGL((bwd_kernel<n, true>), dim3(grid_t), dim3(64 * waves), lds, st, a);  \
     else                                                                                      \
-      hipLaunchKernelGGL((bwd_kernel<n, false>), dim3(n_tiles), dim3(64 * waves), lds, st, a); \
+      hipLaunchKernelGGL((bwd_kernel<n, false>), dim3(grid_t), dim3(64 * waves), lds, st, a); \
   }
     GS_SURFEL_CHANNELS(GS_CASE)
 #undef GS_CASE
