@@ -413,7 +413,8 @@ int64_t gsplat_hip_fwd_split_threshold(int64_t n_isects);
  * algebra, bit 5 = the forward stores no chunk state (timing / traffic
  * attribution only: wrong gradients); bit 4 = the per-tile dispatch order
  * of the unsplit forward and the list order of the split forward's whole
- * tiles and of the backward's work items instead of the XCD-grouped ones
+ * tiles and of the backward's work items, and the 2DGS rasterizer's tile
+ * order taken one tile after the other, instead of the XCD-grouped ones
  * (same results);
  * bit 1 = a chunk of a split tile never waits for an earlier chunk's
  * published product and computes it itself (the timeout path; results are
