@@ -18,4 +18,4 @@ void set_error(const char *fmt, ...) {
 extern "C" const char *gsplat_hip_last_error(void) { return gs::g_err; }
 
 // Bumped whenever an entry point's signature changes.
-extern "C" int gsplat_hip_abi_version(void) { return 34; }
+extern "C" int gsplat_hip_abi_version(void) { return 35; }

@@ -152,6 +152,34 @@ relocation_kernel(int64_t N, const float *__restrict__ opacities, const float *_
   for (int k = 0; k < 3; ++k) new_scales[3 * n + k] = coeff * scales[3 * n + k];
 }
 
+// ------------------------------------------------------- MCMC position noise
+// inject_noise_to_position (gsplat/strategy/ops.py:343-369) in one pass:
+// the reference's covariance launch, its activation / op_sigmoid passes, the
+// einsum and the add become 68 B per Gaussian (means read + written, quats,
+// log-scales, logit and the normal draw read).  Sigma w = R (s^2 * (R^T w)).
+__global__ void __launch_bounds__(256)
+mcmc_noise_kernel(int64_t N, float *__restrict__ means, const float *__restrict__ quats,
+                  const float *__restrict__ log_scales, const float *__restrict__ logits,
+                  const float *__restrict__ z, float scaler) {
+  const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  const float4 q = *reinterpret_cast<const float4 *>(quats + 4 * n);
+  const M3 R = quat_to_rotmat(q.x, q.y, q.z, q.w);
+  const float o = 1.f / (1.f + expf(-logits[n]));
+  // op_sigmoid(1 - o), k = 100, x0 = 0.995 (ops.py:360-361)
+  const float f = scaler / (1.f + expf(-100.f * ((1.f - o) - 0.995f)));
+  const float w[3] = {z[3 * n] * f, z[3 * n + 1] * f, z[3 * n + 2] * f};
+  float u[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const float s = expf(log_scales[3 * n + k]);
+    u[k] = s * s * (R.m[0][k] * w[0] + R.m[1][k] * w[1] + R.m[2][k] * w[2]);
+  }
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+    means[3 * n + i] += R.m[i][0] * u[0] + R.m[i][1] * u[1] + R.m[i][2] * u[2];
+}
+
 // -------------------------------------------------------- selective adam
 // The reference's fused Adam (AdamCUDA.cu:12-46): no bias correction,
 // m = b1 m + (1-b1) g, v = b2 v + (1-b2) g^2, p -= lr m / (sqrt(v) + eps);
@@ -288,6 +316,19 @@ extern "C" int gsplat_hip_relocation(int64_t N, const float *opacities, const fl
                      (hipStream_t)stream, N, opacities, scales, ratios, binoms, n_max,
                      new_opacities, new_scales);
   GS_CHECK_LAUNCH("relocation");
+  return 0;
+}
+
+extern "C" int gsplat_hip_mcmc_inject_noise(int64_t N, float *means, const float *quats,
+                                            const float *log_scales, const float *logits,
+                                            const float *z, float scaler, void *stream) {
+  GS_REQUIRE(N >= 0, "mcmc_inject_noise: negative N");
+  if (N == 0) return 0;
+  GS_REQUIRE(means && quats && log_scales && logits && z, "mcmc_inject_noise: null pointer");
+  GS_REQUIRE(((uintptr_t)quats & 15) == 0, "mcmc_inject_noise: quats must be 16-B aligned");
+  hipLaunchKernelGGL(auxk::mcmc_noise_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, N, means, quats, log_scales, logits, z, scaler);
+  GS_CHECK_LAUNCH("mcmc_inject_noise");
   return 0;
 }
 

@@ -12,7 +12,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GSPLAT_HIP_LIB", os.path.join(_HERE, "libgsplat_hip.so"))
-ABI_VERSION = 34
+ABI_VERSION = 35
 
 _p = ctypes.c_void_p
 _i32 = ctypes.c_int
@@ -146,6 +146,7 @@ _SIGS = {
     "gsplat_hip_quat_scale_to_covar_preci_bwd": (_i32, [_i64, _p, _p, _i32, _p, _p, _p, _p, _p]),
     "gsplat_hip_relocation": (_i32, [_i64, _p, _p, _p, _p, _i32, _p, _p, _p]),
     "gsplat_hip_selective_adam": (_i32, [_i64, _i64, _p, _p, _p, _p, _p, _f, _f, _f, _f, _p]),
+    "gsplat_hip_mcmc_inject_noise": (_i32, [_i64, _p, _p, _p, _p, _p, _f, _p]),
     "gsplat_hip_projection_packed_workspace_bytes": (_i64, [_i32, _i32]),
     "gsplat_hip_projection_packed_count": (_i32, [_i32, _i32, _p, _p, _p, _p, _p, _i32, _i32, _f,
                                                   _f, _f, _f, _p, _p, _p]),

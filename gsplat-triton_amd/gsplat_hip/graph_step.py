@@ -98,7 +98,8 @@ def graphable(tr) -> bool:
     # one rank: 3DGS or 2DGS (surfels, rasterization_2dgs with the sync-free isect)
     return (tr.fused and (tr.model == "3dgs" or (one and tr.model == "2dgs"))
             and (gshard_ok or dp_ok or (one and isinstance(tr.opt, FusedAdam)))
-            and (st is None or (not st.absgrad and tr.radii2d is None))
+            and (st is None or (not getattr(tr, "mcmc", False) and not st.absgrad
+                                and tr.radii2d is None))
             and torch.device(tr.device).type == "cuda")
 
 

@@ -48,7 +48,7 @@ camera each step:
 import dataclasses
 import math
 import os
-from typing import Dict, Optional
+from typing import Dict, Optional, Union
 
 import numpy as np
 import torch
@@ -56,6 +56,8 @@ import torch.nn.functional as F
 
 from . import densify
 from .densify import DefaultStrategyConfig
+from . import mcmc as _mcmc
+from .mcmc import MCMCStrategyConfig
 from .losses import FusedAdam, l1_ssim_loss, ssim_and_l1
 from . import _wrapper
 from .rendering import rasterization, rasterization_2dgs
@@ -147,7 +149,7 @@ class Trainer:
     def __init__(self, points, rgbs, viewmats, Ks, width, height, sh_degree=3, device="cuda",
                  seed=42, world_size=1, rank=0, ssim_lambda=0.2, scene_scale=1.0,
                  fused=True, model="3dgs", sharded_optimizer=None,
-                 strategy: Optional[DefaultStrategyConfig] = None,
+                 strategy: Optional[Union[DefaultStrategyConfig, MCMCStrategyConfig]] = None,
                  sh_degree_interval: Optional[int] = None, max_steps: Optional[int] = None,
                  init: str = "random", init_opacity: float = 0.1, init_scale: float = 1.0,
                  targets: Optional[torch.Tensor] = None, opacity_reg: float = 0.0,
@@ -167,7 +169,12 @@ class Trainer:
         self.scene_scale = scene_scale
         # the caller's config object is not modified (a private copy)
         self.strategy = None if strategy is None else dataclasses.replace(strategy)
-        if self.strategy is not None and model == "2dgs":
+        # MCMCStrategy (mcmc.py): relocation / sample-add refines and the
+        # per-step position noise instead of DefaultStrategy's statistics
+        self.mcmc = isinstance(self.strategy, MCMCStrategyConfig)
+        if self.mcmc:
+            self._binoms = None  # initialize_state's table, on the device at first use
+        elif self.strategy is not None and model == "2dgs":
             self.strategy.key_for_gradient = "gradient_2dgs"  # simple_trainer_2dgs.py:307-311
         # simple_trainer.py:135-137, 671-681: |sigmoid(opacities)| / |exp(scales)|
         # mean terms on the raw parameters (0 = off, the default config)
@@ -263,7 +270,7 @@ class Trainer:
         # state["radii"] (default.py:235-262): the largest screen radius of each
         # Gaussian normalised by max(W, H), tracked only while it is used
         self.radii2d = (torch.zeros(N, device=device) if self.strategy is not None
-                        and self.strategy.refine_scale2d_stop_iter > 0 else None)
+                        and getattr(self.strategy, "refine_scale2d_stop_iter", 0) > 0 else None)
         # split noise: the same stream on every rank (replicas stay identical);
         # Gaussian-sharded: a stream per shard
         self.rng = torch.Generator(device=device).manual_seed(
@@ -434,7 +441,7 @@ class Trainer:
             scales, opac = activate(p["scales"], p["opacities"], fusion)
         else:
             scales, opac = torch.exp(p["scales"]), torch.sigmoid(p["opacities"])
-        absgrad = self.strategy is not None and self.strategy.absgrad
+        absgrad = getattr(self.strategy, "absgrad", False)
         if self.model == "2dgs":
             if hook is not None:
                 hook()
@@ -560,7 +567,7 @@ class Trainer:
             loss.backward()
         if self.world_size > 1 and not self.sharded and not getattr(self, "gshard", False):
             self.allreduce_grads()
-        if self.strategy is None or it < self.strategy.refine_stop_iter:
+        if self.strategy is None or (not self.mcmc and it < self.strategy.refine_stop_iter):
             self.update_state(meta)
         # whether this step's geometry update ran inside the projection backward
         self.geom_applied = bool(fusion is not None and fusion.geom_adam is not None
@@ -712,6 +719,9 @@ class Trainer:
         """DefaultStrategy.step_post_backward after the statistics
         (default.py:175-211): refine, then the opacity reset."""
         cfg = self.strategy
+        if self.mcmc:
+            self.mcmc_step(it)
+            return
         if it >= cfg.refine_stop_iter:
             return
         if cfg.is_refine_step(it):
@@ -753,6 +763,58 @@ class Trainer:
             self._n_world = all_gather_int32(self.world_size, n, device=self.device)
 
     @torch.no_grad()
+    def mcmc_step(self, it: int):
+        """MCMCStrategy.step_post_backward (mcmc.py:103-145) after step `it`'s
+        optimizer update: on its refine steps relocate the dead Gaussians and
+        sample in new ones (mcmc.refine), then the position noise with the
+        means learning rate the reference passes (its scheduler already
+        stepped: simple_trainer.py:808-829)."""
+        cfg = self.strategy
+        if cfg.is_refine_step(it):
+            self.mcmc_refine(it)
+        self.sync()
+        lr = self.lrs[0]
+        if self.max_steps:
+            lr = lr * (0.01 ** (1.0 / self.max_steps)) ** (it + 1)
+        _mcmc.inject_noise({k: p.data for k, p in self.params.items()}, lr * cfg.noise_lr,
+                           generator=self.rng)
+
+    @torch.no_grad()
+    def mcmc_refine(self, it: int):
+        """_relocate_gs + _add_new_gs (mcmc.py:147-187) over the parameters and
+        the Adam moments.  Gaussian-sharded: each shard alone, cap_max split
+        evenly over the ranks."""
+        cfg = self.strategy
+        self.sync()
+        self.last_meta = None
+        if self._binoms is None:
+            self._binoms = _mcmc.binoms(self.device)
+        params = {k: p.data for k, p in self.params.items()}
+        moms = self.moments()
+        dead = torch.sigmoid(params["opacities"].flatten()) <= cfg.min_opacity
+        n_reloc = _mcmc.relocate(params, moms, dead, self._binoms, cfg.min_opacity,
+                                 generator=self.rng)
+        gshard = getattr(self, "gshard", False) and self.world_size > 1
+        cap = -(-cfg.cap_max // self.world_size) if gshard else cfg.cap_max
+        n_add = _mcmc.n_to_add(params["means"].shape[0], cap)
+        if n_add > 0:
+            params, moms = _mcmc.sample_add(params, moms, n_add, self._binoms, cfg.min_opacity,
+                                            generator=self.rng)
+        self.params = {k: torch.nn.Parameter(v) for k, v in params.items()}
+        self._load_moments(moms)
+        self._register_hooks()
+        n = self.params["means"].shape[0]
+        self.grad2d = torch.zeros(n, device=self.device)
+        self.count = torch.zeros(n, device=self.device)
+        self.refine_log.append((it, n_reloc, n_add, n))
+        if cfg.verbose:
+            print(f"Step {it}: Relocated {n_reloc} GSs. Added {n_add} GSs. Now having {n} GSs.")
+        self._param_gen = getattr(self, "_param_gen", 0) + 1
+        if gshard:
+            from .distributed import all_gather_int32
+            self._n_world = all_gather_int32(self.world_size, n, device=self.device)
+
+    @torch.no_grad()
     def reset_opacity(self):
         self.sync()
         value = self.strategy.prune_opa * 2.0
@@ -769,6 +831,11 @@ class Trainer:
         if self.strategy is None:
             return "off (DefaultStrategy statistics only; fixed Gaussian count)"
         c = self.strategy
+        if self.mcmc:
+            return (f"MCMCStrategy relocate + add every {c.refine_every} steps in "
+                    f"({c.refine_start_iter}, {c.refine_stop_iter}), cap {c.cap_max}, position "
+                    f"noise every step (noise_lr {c.noise_lr:g}); refines so far "
+                    f"(step, relocated, added, N): {self.refine_log}")
         return (f"DefaultStrategy refine every {c.refine_every} steps in "
                 f"({c.refine_start_iter}, {c.refine_stop_iter}), opacity reset every "
                 f"{c.reset_every}; refines so far: {self.refine_log}")
@@ -801,7 +868,7 @@ class Trainer:
             # invisible entries have radius 0 and leave the maximum unchanged
             r = meta["radii"].float() / float(max(meta["width"], meta["height"]))
             self.radii2d = torch.maximum(self.radii2d, r.amax(0))
-        absgrad = self.strategy is not None and self.strategy.absgrad
+        absgrad = getattr(self.strategy, "absgrad", False)
         if absgrad:
             g = meta[key].absgrad
         else:

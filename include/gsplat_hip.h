@@ -853,6 +853,18 @@ int gsplat_hip_relocation(int64_t N, const float *opacities, const float *scales
                           const int32_t *ratios, const float *binoms, int n_max,
                           float *new_opacities, float *new_scales, void *stream);
 
+/* Replaces inject_noise_to_position (ABI 35; gsplat/strategy/ops.py:343-369: its
+ * quat_scale_to_covar_preci launch, the sigmoid / exp / op_sigmoid torch
+ * passes, the einsum and the add) with one launch, in place:
+ * means[n] += Sigma_n (z[n] * op_sigmoid(1 - sigmoid(logits[n])) * scaler),
+ * Sigma_n = R(quats[n]) diag(exp(log_scales[n]))^2 R^T, op_sigmoid(x) =
+ * 1 / (1 + exp(-100 (x - 0.995))).  means/log_scales/z [N,3], quats [N,4]
+ * (16-B aligned), logits [N]; z is the caller's standard normal draw
+ * (randn_like(means)). */
+int gsplat_hip_mcmc_inject_noise(int64_t N, float *means, const float *quats,
+                                 const float *log_scales, const float *logits, const float *z,
+                                 float scaler, void *stream);
+
 /* Replaces adam (gsplat/cuda/csrc/AdamCUDA.cu:12-46, used by SelectiveAdam,
  * gsplat/optimizers/selective_adam.py): the reference's update without bias
  * correction on the rows (`row` consecutive elements each) whose visible[] is
