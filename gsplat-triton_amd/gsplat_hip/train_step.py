@@ -23,6 +23,13 @@ schedule (simple_trainer.py:600), `max_steps` the means ExponentialLR
 (:523-528), `init="sfm"` the SfM initialisation with knn scales, uniform
 quaternions and init_opacity (:212-233).
 
+With `strategy=MCMCStrategyConfig()` (gsplat_hip.mcmc) it runs MCMCStrategy
+instead (simple_trainer.py:821-829 -> gsplat/strategy/mcmc.py:103-187): no
+statistics; after the optimizer step, on refine steps the dead Gaussians are
+relocated and 5 % are sampled in (up to cap_max), and every step the
+positions get covariance-shaped noise (one fused HIP launch) scaled by the
+means learning rate of the next step.  MCMC steps are issued eagerly.
+
 Multi-GPU, two schemes, one process per GPU, every rank rendering its own
 camera each step:
 * `gaussian_shard=True` (the reference's multi-GPU training,
