@@ -69,6 +69,12 @@ def parse():
                          "default is eager: each refine re-captures, and the timed window "
                          "centred on a refine ran 213.6 graph-replayed against 228.8 images/s "
                          "eager (profiles/r4_final)")
+    ap.add_argument("--mcmc", action="store_true",
+                    help="the densifying schedule of simple_trainer.py's mcmc preset instead "
+                         "(MCMCStrategy: relocate / add every 100 steps, per-step position "
+                         "noise; init opacity 0.5, init scale 0.1, opacity / scale "
+                         "regularisers 0.01), timed window centred on a refine step; the "
+                         "steps between refines are graph replays unless --eager")
     ap.add_argument("--dp-path", action="store_true",
                     help="replicated data parallelism instead of the default Gaussian "
                          "sharding at N>1 (every rank holds all Gaussians; sharded Adam, "
@@ -299,7 +305,14 @@ def main():
     model = MODEL.get(args.config, "3dgs")
     kw = {}
     start = 0
-    if args.config in DENSIFY:
+    if args.mcmc:  # simple_trainer.py:1098-1107 (the mcmc preset)
+        from gsplat_hip.mcmc import MCMCStrategyConfig
+        assert model == "3dgs", "--mcmc: the 3DGS trainer"
+        kw = dict(strategy=MCMCStrategyConfig(), sh_degree_interval=1000, max_steps=30_000,
+                  init="sfm", init_opacity=0.5, init_scale=0.1, opacity_reg=0.01,
+                  scale_reg=0.01)
+        start = max(0, REFINE_AT - args.warmup - args.steps // 2)
+    elif args.config in DENSIFY:
         from gsplat_hip.densify import DefaultStrategyConfig
         kw = dict(strategy=DefaultStrategyConfig(), sh_degree_interval=1000, max_steps=30_000,
                   init="sfm")
@@ -321,7 +334,8 @@ def main():
                  rank=rank, model=model, sharded_optimizer=dp_path, gaussian_shard=gshard,
                  dp_emulate_world=args.dp_emulate or None,
                  graph=not (args.eager or args.probe
-                            or (args.config in DENSIFY and not args.graph)), **kw)
+                            or (args.config in DENSIFY and not args.graph and not args.mcmc)),
+                 **kw)
     N = means.shape[0]
     # progress watchdog: a rank that stops making progress (a collective a
     # peer never joins, captured or eager) ends the job with its rank, step

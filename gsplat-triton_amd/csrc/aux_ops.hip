@@ -156,19 +156,70 @@ relocation_kernel(int64_t N, const float *__restrict__ opacities, const float *_
 // inject_noise_to_position (gsplat/strategy/ops.py:343-369) in one pass:
 // the reference's covariance launch, its activation / op_sigmoid passes, the
 // einsum and the add become 68 B per Gaussian (means read + written, quats,
-// log-scales, logit and the normal draw read).  Sigma w = R (s^2 * (R^T w)).
+// log-scales, logit and the normal draw read; 56 B with the draw made here).
+// Sigma w = R (s^2 * (R^T w)).
+//
+// The draw: z[n] when given (torch's randn_like, the reference's), else three
+// standard normals of Philox-4x32-10 keyed by the seed, counter (n, step):
+// a pure function of (seed, step, n), so a replayed or re-run step draws the
+// same numbers (the captured training step reads step and scaler from its
+// input block, and skips a void step).
+struct Philox {
+  static GS_INLINE void round(uint32_t (&c)[4], uint32_t k0, uint32_t k1) {
+    const uint32_t m0 = 0xD2511F53u, m1 = 0xCD9E8D57u;
+    const uint32_t h0 = __umulhi(m0, c[0]), l0 = m0 * c[0];
+    const uint32_t h1 = __umulhi(m1, c[2]), l1 = m1 * c[2];
+    const uint32_t r0 = h1 ^ c[1] ^ k0, r2 = h0 ^ c[3] ^ k1;
+    c[0] = r0, c[1] = l1, c[2] = r2, c[3] = l0;
+  }
+  static GS_INLINE void draw(uint32_t (&c)[4], uint64_t key) {
+    uint32_t k0 = (uint32_t)key, k1 = (uint32_t)(key >> 32);
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+      round(c, k0, k1);
+      k0 += 0x9E3779B9u, k1 += 0xBB67AE85u;
+    }
+  }
+};
+
+// uniform in (0, 1]: 24 random bits, never 0 (the Box-Muller log)
+GS_INLINE float u01(uint32_t x) { return ((float)(x >> 8) + 1.f) * (1.f / 16777216.f); }
+
 __global__ void __launch_bounds__(256)
 mcmc_noise_kernel(int64_t N, float *__restrict__ means, const float *__restrict__ quats,
                   const float *__restrict__ log_scales, const float *__restrict__ logits,
-                  const float *__restrict__ z, float scaler) {
+                  const float *__restrict__ z, uint64_t seed, int64_t step,
+                  const int64_t *__restrict__ step_dev, float scaler,
+                  const float *__restrict__ scaler_dev, const int32_t *__restrict__ skip) {
+  if (skip && *skip) return;  // a void step of the captured training step
+  if (scaler_dev) scaler = *scaler_dev;
+  if (scaler == 0.f) return;  // nothing moves (a refine step: noise after the refine)
+  if (step_dev) step = *step_dev;
   const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (n >= N) return;
+  float zn[3];
+  if (z) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) zn[k] = z[3 * n + k];
+  } else {
+    uint32_t c[4] = {(uint32_t)n, (uint32_t)((uint64_t)n >> 32), (uint32_t)step,
+                     (uint32_t)((uint64_t)step >> 32)};
+    Philox::draw(c, seed);
+    // Box-Muller: (c0, c1) -> two normals, (c2, c3) -> the third
+    const float r0 = sqrtf(-2.f * logf(u01(c[0]))), t0 = 6.2831853071795864f * u01(c[1]);
+    const float r1 = sqrtf(-2.f * logf(u01(c[2]))), t1 = 6.2831853071795864f * u01(c[3]);
+    float sn, cs;
+    sincosf(t0, &sn, &cs);
+    zn[0] = r0 * cs;
+    zn[1] = r0 * sn;
+    zn[2] = r1 * cosf(t1);
+  }
   const float4 q = *reinterpret_cast<const float4 *>(quats + 4 * n);
   const M3 R = quat_to_rotmat(q.x, q.y, q.z, q.w);
   const float o = 1.f / (1.f + expf(-logits[n]));
   // op_sigmoid(1 - o), k = 100, x0 = 0.995 (ops.py:360-361)
   const float f = scaler / (1.f + expf(-100.f * ((1.f - o) - 0.995f)));
-  const float w[3] = {z[3 * n] * f, z[3 * n + 1] * f, z[3 * n + 2] * f};
+  const float w[3] = {zn[0] * f, zn[1] * f, zn[2] * f};
   float u[3];
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
@@ -321,13 +372,17 @@ extern "C" int gsplat_hip_relocation(int64_t N, const float *opacities, const fl
 
 extern "C" int gsplat_hip_mcmc_inject_noise(int64_t N, float *means, const float *quats,
                                             const float *log_scales, const float *logits,
-                                            const float *z, float scaler, void *stream) {
+                                            const float *z, uint64_t seed, int64_t step,
+                                            const int64_t *step_device, float scaler,
+                                            const float *scaler_device, const int32_t *skip_device,
+                                            void *stream) {
   GS_REQUIRE(N >= 0, "mcmc_inject_noise: negative N");
   if (N == 0) return 0;
-  GS_REQUIRE(means && quats && log_scales && logits && z, "mcmc_inject_noise: null pointer");
+  GS_REQUIRE(means && quats && log_scales && logits, "mcmc_inject_noise: null pointer");
   GS_REQUIRE(((uintptr_t)quats & 15) == 0, "mcmc_inject_noise: quats must be 16-B aligned");
   hipLaunchKernelGGL(auxk::mcmc_noise_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0,
-                     (hipStream_t)stream, N, means, quats, log_scales, logits, z, scaler);
+                     (hipStream_t)stream, N, means, quats, log_scales, logits, z, seed, step,
+                     step_device, scaler, scaler_device, skip_device);
   GS_CHECK_LAUNCH("mcmc_inject_noise");
   return 0;
 }

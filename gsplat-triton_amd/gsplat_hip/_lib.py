@@ -146,7 +146,8 @@ _SIGS = {
     "gsplat_hip_quat_scale_to_covar_preci_bwd": (_i32, [_i64, _p, _p, _i32, _p, _p, _p, _p, _p]),
     "gsplat_hip_relocation": (_i32, [_i64, _p, _p, _p, _p, _i32, _p, _p, _p]),
     "gsplat_hip_selective_adam": (_i32, [_i64, _i64, _p, _p, _p, _p, _p, _f, _f, _f, _f, _p]),
-    "gsplat_hip_mcmc_inject_noise": (_i32, [_i64, _p, _p, _p, _p, _p, _f, _p]),
+    "gsplat_hip_mcmc_inject_noise": (_i32, [_i64, _p, _p, _p, _p, _p, ctypes.c_uint64, _i64, _p,
+                                            _f, _p, _p, _p]),
     "gsplat_hip_projection_packed_workspace_bytes": (_i64, [_i32, _i32]),
     "gsplat_hip_projection_packed_count": (_i32, [_i32, _i32, _p, _p, _p, _p, _p, _i32, _i32, _f,
                                                   _f, _f, _f, _p, _p, _p]),

@@ -63,6 +63,7 @@ import torch
 from . import _lib, _wrapper
 from .losses import FusedAdam, adam_factors, l1_ssim_loss
 from .rendering import rasterization, rasterization_2dgs
+from . import mcmc as _mcmc
 from .strategy import activate, update_state_
 
 
@@ -75,9 +76,10 @@ class GraphCaptureError(RuntimeError):
 
 def graphable(tr) -> bool:
     """Whether Trainer `tr` can run its steps as graph replays.  With a
-    DefaultStrategy schedule the steps between refines are replays; the
-    refine / opacity reset run eagerly after their step (Trainer.step), and a
-    refine (new parameter tensors, Trainer._param_gen) re-captures."""
+    DefaultStrategy or MCMCStrategy schedule the steps between refines are
+    replays (MCMC's position noise inside them); the refine / opacity reset
+    run eagerly after their step (Trainer.step), and a refine (new parameter
+    tensors, Trainer._param_gen) re-captures."""
     st = tr.strategy
     # Gaussian-sharded (one camera per rank): its two pair exchanges inside
     # the graph -- RCCL's all_to_all_single (the default at N > 1; the
@@ -98,8 +100,7 @@ def graphable(tr) -> bool:
     # one rank: 3DGS or 2DGS (surfels, rasterization_2dgs with the sync-free isect)
     return (tr.fused and (tr.model == "3dgs" or (one and tr.model == "2dgs"))
             and (gshard_ok or dp_ok or (one and isinstance(tr.opt, FusedAdam)))
-            and (st is None or (not getattr(tr, "mcmc", False) and not st.absgrad
-                                and tr.radii2d is None))
+            and (st is None or (not getattr(st, "absgrad", False) and tr.radii2d is None))
             and torch.device(tr.device).type == "cuda")
 
 
@@ -195,7 +196,8 @@ class GraphStep:
         # viewmats [W][16] at byte 512 and Ks [W][9] at
         # byte 1024 (W = the world's cameras: 1, or the Gaussian-sharded job's
         # ranks), the camera-to-world matrix f32 [16] at byte 1536 (2DGS: its
-        # normals), i64 at SLOT - 8 the ring slot (written by
+        # normals), MCMC's step i64 / noise scale f32 at bytes 264 / 272,
+        # i64 at SLOT - 8 the ring slot (written by
         # gsplat_hip_step_fetch)
         self.n_groups = len(tr.params)
         self.gshard = bool(getattr(tr, "gshard", False))
@@ -221,6 +223,9 @@ class GraphStep:
         r = tr.rank if self.gshard else 0
         self.vm, self.K = self.vm_w[r:r + 1], self.K_w[r:r + 1]  # this rank's camera
         self.c2w = self.blk[1536:1536 + 64].view(torch.float32).view(1, 4, 4)
+        # MCMC: the step index (i64 at byte 264) and its noise scale (f32 at 272)
+        self.mstep = self.blk[264:272].view(torch.int64)
+        self.mscale = self.blk[272:276].view(torch.float32)
         self.slot = self.blk[self.SLOT - 8:].view(torch.int64)
         self.seq = torch.zeros(1, dtype=torch.int64, device=dev)  # steps fetched
         # the step's loss, written by the loss's own reduction launch into
@@ -362,6 +367,13 @@ class GraphStep:
             if self.dp:
                 tr.opt.capturing = False
         tr.opt.zero_grad(set_to_none=True)
+        if getattr(tr, "mcmc", False):
+            # MCMCStrategy's position noise after the update (Trainer.mcmc_noise):
+            # the step and its scale from the block (scale 0 on refine steps,
+            # whose noise follows the eager refine), nothing on a void step
+            _mcmc.inject_noise({k: p[k].data for k in ("means", "quats", "scales", "opacities")},
+                               0.0, seed=tr._noise_seed, step_dev=self.mstep,
+                               scaler_dev=self.mscale, skip=self.status)
         return loss, meta["isect_counts"]
 
     def _capture(self, deg, stats=True):
@@ -498,6 +510,10 @@ class GraphStep:
         b[512:512 + 64 * self.W].view(np.float32)[:] = self._vm_host[world_ci].reshape(-1)
         b[1024:1024 + 36 * self.W].view(np.float32)[:] = self._K_host[world_ci].reshape(-1)
         b[256:264].view(np.int64)[0] = ci
+        if getattr(tr, "mcmc", False):
+            b[264:272].view(np.int64)[0] = it
+            b[272:276].view(np.float32)[0] = \
+                0.0 if tr.strategy.is_refine_step(it) else tr.mcmc_scaler(it)
         if tr.model == "2dgs":  # rasterization_2dgs's torch.linalg.inv(viewmats), on the host
             b[1536:1536 + 64].view(np.float32)[:] = np.linalg.inv(
                 self._vm_host[ci].astype(np.float64)).astype(np.float32).reshape(-1)
@@ -513,6 +529,8 @@ class GraphStep:
 
     def _stats_at(self, it):
         st = self.tr.strategy
+        if getattr(self.tr, "mcmc", False):
+            return False  # MCMCStrategy keeps no statistics
         return st is None or it < st.refine_stop_iter
 
     def step(self, it):
@@ -620,6 +638,8 @@ class GraphStep:
             self.graph, self.key = None, None
             for it, _, ret in redo:
                 loss = tr._eager_step(it)
+                if getattr(tr, "mcmc", False) and not tr.strategy.is_refine_step(it):
+                    tr.mcmc_noise(it)  # the replay's noise (a refine step's follows its refine)
                 if ret is not None:
                     ret.copy_(loss.detach().reshape(ret.shape))
             return

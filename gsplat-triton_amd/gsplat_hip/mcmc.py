@@ -141,10 +141,19 @@ def sample_add(params: Dict[str, Tensor], moments: Dict[str, List[Tensor]], n: i
 @torch.no_grad()
 def inject_noise(params: Dict[str, Tensor], scaler: float,
                  generator: Optional[torch.Generator] = None,
-                 z: Optional[Tensor] = None) -> None:
+                 z: Optional[Tensor] = None, seed: Optional[int] = None, step: int = 0,
+                 step_dev: Optional[Tensor] = None, scaler_dev: Optional[Tensor] = None,
+                 skip: Optional[Tensor] = None) -> None:
     """inject_noise_to_position (ops.py:343-369) in place: means +=
-    Sigma (z * op_sigmoid(1 - opacity) * scaler), z ~ N(0, 1) [N, 3] drawn
-    as randn_like(means) unless given, one fused HIP launch."""
+    Sigma (z * op_sigmoid(1 - opacity) * scaler), one fused HIP launch.
+    The draw z ~ N(0, 1) [N, 3]: `z` if given; else with a `seed`, made in
+    the kernel (Philox-4x32-10 keyed by the seed, counter (gaussian, step): a
+    pure function of (seed, step, gaussian) -- the trainer's draw, identical
+    when a captured step is replayed or re-run); else torch's
+    randn_like(means) from `generator` (the reference's draw).  step_dev /
+    scaler_dev (int64 [1] / float32 [1] on the device) override step /
+    scaler, skip (int32 [1]) voids the launch when non-zero: the captured
+    training step's inputs."""
     means = params["means"]
     if not means.is_cuda:
         raise ValueError("mcmc.inject_noise: tensors must be on the GPU")
@@ -155,14 +164,18 @@ def inject_noise(params: Dict[str, Tensor], scaler: float,
                 raise ValueError(f"mcmc.inject_noise: {k} must be contiguous float32")
     assert means.shape == (N, 3) and params["scales"].shape == (N, 3)
     assert params["quats"].shape == (N, 4) and params["opacities"].numel() == N
-    if z is None:
+    if z is None and seed is None:
         z = torch.randn(means.shape, device=means.device, generator=generator)
-    z = z.to(device=means.device, dtype=torch.float32).contiguous()
-    assert z.shape == (N, 3), z.shape
+    if z is not None:
+        z = z.to(device=means.device, dtype=torch.float32).contiguous()
+        assert z.shape == (N, 3), z.shape
+    for t, dt in ((step_dev, torch.int64), (scaler_dev, torch.float32), (skip, torch.int32)):
+        assert t is None or (t.is_cuda and t.dtype == dt and t.numel() >= 1), (t, dt)
     quats = _aligned16(params["quats"])
     _lib.call("gsplat_hip_mcmc_inject_noise", N, _ptr(means), _ptr(quats),
-              _ptr(params["scales"]), _ptr(params["opacities"]), _ptr(z), float(scaler),
-              _stream())
+              _ptr(params["scales"]), _ptr(params["opacities"]), _ptr(z),
+              int(seed or 0) & 0xFFFFFFFFFFFFFFFF, int(step), _ptr(step_dev), float(scaler),
+              _ptr(scaler_dev), _ptr(skip), _stream())
 
 
 def n_to_add(n: int, cap_max: int) -> int:

@@ -27,8 +27,10 @@ With `strategy=MCMCStrategyConfig()` (gsplat_hip.mcmc) it runs MCMCStrategy
 instead (simple_trainer.py:821-829 -> gsplat/strategy/mcmc.py:103-187): no
 statistics; after the optimizer step, on refine steps the dead Gaussians are
 relocated and 5 % are sampled in (up to cap_max), and every step the
-positions get covariance-shaped noise (one fused HIP launch) scaled by the
-means learning rate of the next step.  MCMC steps are issued eagerly.
+positions get covariance-shaped noise (one fused HIP launch, its normal
+draw made in the kernel from the trainer's key and the step) scaled by the
+means learning rate of the next step.  With graph=True the steps between
+refines are replays with the noise inside; the refines run eagerly.
 
 Multi-GPU, two schemes, one process per GPU, every rank rendering its own
 camera each step:
@@ -145,6 +147,24 @@ def ssim(img1, img2, window=None):
     C1, C2 = 0.01 ** 2, 0.03 ** 2
     m = ((2 * mu1 * mu2 + C1) * (2 * s12 + C2)) / ((mu1 * mu1 + mu2 * mu2 + C1) * (s11 + s22 + C2))
     return m.mean()
+
+
+def _mean(x: torch.Tensor) -> torch.Tensor:
+    """x.mean() as reductions that each give one output per workgroup: rows
+    of 1024, then the row sums (and the tail).  torch's one-output reduction
+    of a large tensor splits it over workgroups with a zero-filled semaphore
+    buffer -- a memset node, which a captured step must not hold
+    (graph_step.check_kernel_nodes_only) -- e.g. the regularisers of
+    simple_trainer's mcmc preset at a million Gaussians."""
+    x = x.reshape(-1)
+    n = x.numel()
+    q = n // 1024
+    if q == 0:
+        return x.sum() / n
+    s = x[:q * 1024].view(q, 1024).sum(1).sum()
+    if n > q * 1024:
+        s = s + x[q * 1024:].sum()
+    return s / n
 
 
 class Trainer:
@@ -282,6 +302,10 @@ class Trainer:
         # Gaussian-sharded: a stream per shard
         self.rng = torch.Generator(device=device).manual_seed(
             seed + (7919 * rank if self.gshard else 0))
+        # MCMC position noise: drawn in the noise kernel from this key and the
+        # step (mcmc.inject_noise), so a replayed or re-run step draws the same
+        self._noise_seed = ((seed + (7919 * rank if self.gshard else 0) + 1)
+                            * 0x9E3779B97F4A7C15) % (1 << 64)
         self.window = _gauss_window(device=device)
         self.last_meta = None
         self.refine_log = []  # (step, n_dupli, n_split, n_prune, N after)
@@ -529,7 +553,8 @@ class Trainer:
                 self._graph = None
             else:
                 if self.strategy is not None:
-                    self.post_step(it)  # eager refine / reset: drains the replays first
+                    # eager refine / reset: drains the replays first
+                    self.post_step(it, replayed=True)
                 if self._graph is not None and self._graph.failed is not None:
                     self.graph_fallback = self._graph.failed  # (failed in that drain)
                     self._graph = None
@@ -593,9 +618,9 @@ class Trainer:
         torch autograd; the fused optimizer adds them as extra terms)."""
         p = self.params
         if self.opacity_reg > 0.0:
-            loss = loss + self.opacity_reg * torch.abs(torch.sigmoid(p["opacities"])).mean()
+            loss = loss + self.opacity_reg * _mean(torch.abs(torch.sigmoid(p["opacities"])))
         if self.scale_reg > 0.0:
-            loss = loss + self.scale_reg * torch.abs(torch.exp(p["scales"])).mean()
+            loss = loss + self.scale_reg * _mean(torch.abs(torch.exp(p["scales"])))
         return loss
 
     def _make_fusion(self) -> Optional[_wrapper.StepFusion]:
@@ -722,12 +747,14 @@ class Trainer:
                 "num_images": len(psnrs)}
 
     # ------------------------------------------------------------ strategy
-    def post_step(self, it: int):
+    def post_step(self, it: int, replayed: bool = False):
         """DefaultStrategy.step_post_backward after the statistics
-        (default.py:175-211): refine, then the opacity reset."""
+        (default.py:175-211): refine, then the opacity reset.  MCMC: its
+        step_post_backward (mcmc_step); `replayed`: step `it` ran as a graph
+        replay, which applied the position noise itself unless `it` refines."""
         cfg = self.strategy
         if self.mcmc:
-            self.mcmc_step(it)
+            self.mcmc_step(it, noise=not (replayed and not cfg.is_refine_step(it)))
             return
         if it >= cfg.refine_stop_iter:
             return
@@ -770,21 +797,32 @@ class Trainer:
             self._n_world = all_gather_int32(self.world_size, n, device=self.device)
 
     @torch.no_grad()
-    def mcmc_step(self, it: int):
+    def mcmc_step(self, it: int, noise: bool = True):
         """MCMCStrategy.step_post_backward (mcmc.py:103-145) after step `it`'s
         optimizer update: on its refine steps relocate the dead Gaussians and
-        sample in new ones (mcmc.refine), then the position noise with the
-        means learning rate the reference passes (its scheduler already
-        stepped: simple_trainer.py:808-829)."""
-        cfg = self.strategy
-        if cfg.is_refine_step(it):
+        sample in new ones (mcmc_refine), then the position noise (unless a
+        graph replay of the step applied it)."""
+        if self.strategy.is_refine_step(it):
             self.mcmc_refine(it)
-        self.sync()
+        if noise:
+            self.mcmc_noise(it)
+
+    def mcmc_scaler(self, it: int) -> float:
+        """The noise scale of step `it`: the means learning rate the reference
+        passes (its scheduler already stepped, simple_trainer.py:808-829)
+        times noise_lr (mcmc.py:143-145)."""
         lr = self.lrs[0]
         if self.max_steps:
             lr = lr * (0.01 ** (1.0 / self.max_steps)) ** (it + 1)
-        _mcmc.inject_noise({k: p.data for k, p in self.params.items()}, lr * cfg.noise_lr,
-                           generator=self.rng)
+        return lr * self.strategy.noise_lr
+
+    @torch.no_grad()
+    def mcmc_noise(self, it: int):
+        """inject_noise_to_position for step `it`, drawn in the kernel from
+        (trainer key, it): the draw a graph replay of the step makes."""
+        self.sync()
+        _mcmc.inject_noise({k: p.data for k, p in self.params.items()}, self.mcmc_scaler(it),
+                           seed=self._noise_seed, step=it)
 
     @torch.no_grad()
     def mcmc_refine(self, it: int):

@@ -858,12 +858,20 @@ int gsplat_hip_relocation(int64_t N, const float *opacities, const float *scales
  * passes, the einsum and the add) with one launch, in place:
  * means[n] += Sigma_n (z[n] * op_sigmoid(1 - sigmoid(logits[n])) * scaler),
  * Sigma_n = R(quats[n]) diag(exp(log_scales[n]))^2 R^T, op_sigmoid(x) =
- * 1 / (1 + exp(-100 (x - 0.995))).  means/log_scales/z [N,3], quats [N,4]
- * (16-B aligned), logits [N]; z is the caller's standard normal draw
- * (randn_like(means)). */
+ * 1 / (1 + exp(-100 (x - 0.995))).  means/log_scales [N,3], quats [N,4]
+ * (16-B aligned), logits [N].
+ * z [N,3]: the caller's standard normal draw (the reference's
+ * randn_like(means)); NULL: three normals per Gaussian from Philox-4x32-10
+ * keyed by `seed` with counter (n, step) (Box-Muller), a pure function of
+ * (seed, step, n).  step_device / scaler_device (may be NULL): read step /
+ * scaler from device memory instead (a captured step's input block); a zero
+ * scaler moves nothing.  skip_device (may be NULL): non-zero = void step,
+ * nothing written. */
 int gsplat_hip_mcmc_inject_noise(int64_t N, float *means, const float *quats,
                                  const float *log_scales, const float *logits, const float *z,
-                                 float scaler, void *stream);
+                                 uint64_t seed, int64_t step, const int64_t *step_device,
+                                 float scaler, const float *scaler_device,
+                                 const int32_t *skip_device, void *stream);
 
 /* Replaces adam (gsplat/cuda/csrc/AdamCUDA.cu:12-46, used by SelectiveAdam,
  * gsplat/optimizers/selective_adam.py): the reference's update without bias

@@ -123,8 +123,8 @@ def test_trainer_mcmc_schedule(graph):
     """simple_trainer.py's mcmc preset (opacity / scale regularisers 0.01) on
     the HIP path, compressed in time: relocate + add on steps 2, 4, 6, capped;
     each refine leaves no dead Gaussian, rebuilds parameters and Adam state
-    consistently, and the noise runs every step (eagerly: graph=True steps
-    are issued from the host with MCMC)."""
+    consistently, and the noise runs every step (graph=True: inside the
+    replays between the eager refines)."""
     from gsplat_hip.mcmc import MCMCStrategyConfig
     from gsplat_hip.train_step import Trainer
     from test_gpu_trainer import _small_scene
@@ -134,7 +134,7 @@ def test_trainer_mcmc_schedule(graph):
     cfg = MCMCStrategyConfig(refine_start_iter=1, refine_every=2, cap_max=cap)
     tr = Trainer(means, rgbs, vm, K, W, H, device="cuda", strategy=cfg, max_steps=100,
                  opacity_reg=0.01, scale_reg=0.01, graph=graph)
-    assert tr._graph is None
+    assert (tr._graph is not None) == graph
     # a few certainly dead Gaussians to relocate at the first refine
     tr.params["opacities"].data[:7] = -9.0
     losses = []
@@ -159,3 +159,99 @@ def test_trainer_mcmc_schedule(graph):
     assert [r[2] for r in tr.refine_log] == [n1 - n0, n2 - n1, 0]
     assert all(math.isfinite(x) for x in losses), losses
     assert "MCMCStrategy" in tr.densify_desc()
+    tr.sync()
+    if graph:
+        assert tr.graph_fallback is None, tr.graph_fallback
+        assert tr._graph.replays >= 7 and tr._graph.recaptures >= 3  # + one after each refine
+
+
+def _unit_scene(N, logit=-12.0):
+    """Sigma = I (identity rotation, unit scales) and opacity ~ 0: the
+    displacement is z * op_sigmoid(1) * scaler."""
+    p = {"means": torch.zeros(N, 3, device=DEV),
+         "quats": torch.tensor([1.0, 0, 0, 0], device=DEV).repeat(N, 1),
+         "scales": torch.zeros(N, 3, device=DEV), "opacities": torch.full((N,), logit, device=DEV)}
+    o = torch.sigmoid(torch.tensor(logit))
+    f = float(1 / (1 + torch.exp(-100 * ((1 - o) - 0.995))))
+    return p, f
+
+
+def test_noise_draw_in_kernel():
+    """The trainer's draw (Philox-4x32-10 keyed by seed, counter (n, step),
+    Box-Muller): standard normal per component, components and steps
+    uncorrelated, a pure function of (seed, step, n); device step / scale /
+    void flag as the captured step passes them."""
+    from gsplat_hip import mcmc
+    N = 1 << 20
+    p, f = _unit_scene(N)
+    mcmc.inject_noise(p, 1.0 / f, seed=1234, step=7)
+    z = p["means"].clone()
+    assert bool(torch.isfinite(z).all())
+    m, sd = z.mean(0), z.std(0)
+    assert float(m.abs().max()) < 5e-3 and float((sd - 1).abs().max()) < 5e-3, (m, sd)
+    c = torch.corrcoef(z.T)
+    assert float((c - torch.eye(3, device=DEV)).abs().max()) < 5e-3, c
+    within = (z.abs() < 1).float().mean(0)
+    assert float((within - 0.6827).abs().max()) < 3e-3, within
+    assert float((z.abs() > 4).float().mean()) < 1e-4  # tails of a normal, no outliers
+    # the same (seed, step): the same numbers; another step / seed: independent
+    p2, _ = _unit_scene(N)
+    mcmc.inject_noise(p2, 1.0 / f, seed=1234, step=7)
+    assert torch.equal(p2["means"], z)
+    for kw in (dict(seed=1234, step=8), dict(seed=1235, step=7)):
+        p3, _ = _unit_scene(N)
+        mcmc.inject_noise(p3, 1.0 / f, **kw)
+        r = torch.corrcoef(torch.stack([p3["means"].reshape(-1), z.reshape(-1)]))[0, 1]
+        assert abs(float(r)) < 5e-3, (kw, r)
+    # device inputs: step and scale from memory, a zero scale or a void flag
+    # moves nothing
+    p4, _ = _unit_scene(N)
+    sd_ = torch.tensor([7], dtype=torch.int64, device=DEV)
+    sc = torch.tensor([1.0 / f], dtype=torch.float32, device=DEV)
+    void = torch.zeros(1, dtype=torch.int32, device=DEV)
+    mcmc.inject_noise(p4, 0.0, seed=1234, step=0, step_dev=sd_, scaler_dev=sc, skip=void)
+    assert torch.equal(p4["means"], z)
+    void.fill_(1)
+    mcmc.inject_noise(p4, 0.0, seed=1234, step_dev=sd_, scaler_dev=sc, skip=void)
+    void.zero_()
+    sc.zero_()
+    mcmc.inject_noise(p4, 0.0, seed=1234, step_dev=sd_, scaler_dev=sc, skip=void)
+    assert torch.equal(p4["means"], z)
+
+
+@pytest.mark.parametrize("capacity", [None, 1000])
+def test_graph_mcmc_trainer_tracks_eager(capacity):
+    """MCMC training as graph replays (the noise inside, step and scale from
+    the step's input block) against eager steps: refines on steps 3 and 6
+    (eager, re-captured after), the same Gaussian counts and parameters at
+    the eager run-to-run spread; with a tiny isect capacity the voided steps
+    re-run and draw the same noise."""
+    from gsplat_hip.mcmc import MCMCStrategyConfig
+    from gsplat_hip.train_step import Trainer
+    from test_gpu_trainer import _small_scene
+    means, rgbs, vm, K, W, H = _small_scene()
+    cfg = MCMCStrategyConfig(refine_start_iter=2, refine_every=3)
+    out = {}
+    for run in ("eager", "eager2", "graph"):
+        graph = run == "graph"
+        tr = Trainer(means, rgbs, vm, K, W, H, device=DEV, strategy=cfg, max_steps=100,
+                     graph=graph, isect_capacity=capacity)
+        assert (tr._graph is not None) == graph
+        tr.params["opacities"].data[:5] = -9.0  # certainly dead at the first refine
+        # (a returned loss of a voided step is rewritten by its re-run: read
+        # them after the sync)
+        losses = [tr.step(it) for it in range(8)]
+        tr.sync()
+        losses = [float(x) for x in losses]
+        assert tr.graph_fallback is None, tr.graph_fallback
+        out[run] = ({k: p.detach().clone() for k, p in tr.params.items()},
+                    [r[1:] for r in tr.refine_log], losses)
+        if graph:
+            assert tr._graph.replays >= 8
+    a, a2, b = out["eager"], out["eager2"], out["graph"]
+    assert b[1] == a[1] == a2[1], (a[1], b[1])  # (relocated, added, N) per refine
+    for k in a[0]:
+        spread = float((a2[0][k] - a[0][k]).abs().max())
+        err = float((b[0][k] - a[0][k]).abs().max())
+        assert err <= max(4.0 * spread, 1e-5 * float(a[0][k].abs().max()) + 1e-6), (k, err, spread)
+    torch.testing.assert_close(torch.tensor(b[2]), torch.tensor(a[2]), rtol=1e-4, atol=1e-6)
