@@ -178,10 +178,23 @@ def inject_noise(params: Dict[str, Tensor], scaler: float,
               _ptr(scaler_dev), _ptr(skip), _stream())
 
 
+@torch.no_grad()
+def inject_noise_to_position(params, optimizers, state, scaler: float) -> None:
+    """Drop-in for gsplat.strategy.ops.inject_noise_to_position (ops.py:343-369),
+    same signature and draw (torch.randn_like(params["means"]) from the
+    global generator), one fused launch instead of the covariance launch and
+    the torch passes around it (`ops.inject_noise_to_position =
+    gsplat_hip.mcmc.inject_noise_to_position` under the reference's
+    MCMCStrategy).  `optimizers` / `state` are unused, as in the reference."""
+    z = torch.randn_like(params["means"])
+    inject_noise({k: params[k].data for k in ("means", "quats", "scales", "opacities")},
+                 scaler, z=z)
+
+
 def n_to_add(n: int, cap_max: int) -> int:
     """_add_new_gs's count (mcmc.py:175-177)."""
     return max(0, min(cap_max, int(1.05 * n)) - n)
 
 
 __all__ = ["MCMCStrategyConfig", "binoms", "multinomial_sample", "relocate", "sample_add",
-           "inject_noise", "n_to_add"]
+           "inject_noise", "inject_noise_to_position", "n_to_add"]

@@ -102,6 +102,28 @@ def test_noise_kernel_1m_vs_torch():
     assert torch.equal(p["means"], after)
 
 
+def test_inject_noise_to_position_dropin():
+    """The reference signature (ops.py:343-369) and draw: torch.randn_like
+    from the global generator, so a seeded run moves the means as the
+    reference's torch formula does with the same seed."""
+    from gsplat_hip import mcmc
+    gen = torch.Generator(device=DEV).manual_seed(3)
+    N = 50_000
+    params = {"means": torch.nn.Parameter(torch.randn(N, 3, device=DEV, generator=gen)),
+              "quats": torch.nn.Parameter(torch.randn(N, 4, device=DEV, generator=gen)),
+              "scales": torch.nn.Parameter(torch.rand(N, 3, device=DEV, generator=gen) * 4 - 6),
+              "opacities": torch.nn.Parameter(torch.randn(N, device=DEV, generator=gen) * 3 - 3)}
+    before = params["means"].detach().clone()
+    torch.manual_seed(77)
+    z = torch.randn_like(params["means"])
+    ref = _noise_reference(before, params["quats"].detach(), params["scales"].detach(),
+                           params["opacities"].detach(), z, 80.0)
+    torch.manual_seed(77)
+    mcmc.inject_noise_to_position(params, optimizers={}, state={}, scaler=80.0)
+    d_ref, d = ref - before, params["means"].detach() - before
+    assert float((d - d_ref).abs().max()) <= 1e-4 * float(d_ref.abs().max()) + 1e-7
+
+
 def test_noise_kernel_empty_and_misaligned_quats():
     from gsplat_hip import mcmc
     e = {"means": torch.zeros(0, 3, device=DEV), "quats": torch.zeros(0, 4, device=DEV),
