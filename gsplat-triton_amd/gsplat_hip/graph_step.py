@@ -32,7 +32,9 @@ What makes the step capturable:
   -- so the result is the eager step sequence's.
 
 Scope: the fused 3DGS trainer -- one rank (the bench's M2 and, with its
-DefaultStrategy schedule, M3 configurations), Gaussian-sharded (its pair
+DefaultStrategy schedule, M3 configurations; with MCMCStrategy the position
+noise is a launch of the captured step, its step index and scale in the
+input block), Gaussian-sharded (its pair
 exchanges inside the graph) and per-camera data parallel with the sharded
 optimizer (its reduce-scatters, Adam and all-gathers inside the graph): the
 steps between two refines are replays of one capture; a refine (eager,
