@@ -582,7 +582,9 @@ class GraphStep:
         if self.ring_loss:
             ret = self.loss_ring[k % self.LOSS_RING]
         elif ret is None:
-            ret = self.loss.clone()
+            # (detached: a clone would keep the captured step's autograd
+            # graph alive into the next capture)
+            ret = self.loss.detach().clone()
         else:
             ret.copy_(self.loss)
         ev = torch.cuda.Event()

@@ -182,7 +182,7 @@ class Trainer:
                  targets: Optional[torch.Tensor] = None, opacity_reg: float = 0.0,
                  scale_reg: float = 0.0, dp_emulate_world: Optional[int] = None,
                  graph: bool = False, isect_capacity: Optional[int] = None,
-                 gaussian_shard: bool = False):
+                 gaussian_shard: bool = False, visible_adam: bool = False):
         assert model in ("3dgs", "2dgs"), model
         assert init in ("random", "sfm"), init
         self.model = model
@@ -244,6 +244,16 @@ class Trainer:
         self.adam_kw = dict(eps=1e-15 / math.sqrt(BS),
                             betas=(1 - BS * (1 - 0.9), 1 - BS * (1 - 0.999)))
         self.fused = fused
+        # simple_trainer.py:263-266,782-797 (cfg.visible_adam): SelectiveAdam --
+        # the reference's Adam kernel (no bias correction) on the rows of the
+        # Gaussians some camera of the step sees, (radii > 0).any(0); one
+        # launch per group (gsplat_hip_selective_adam), no update fused into
+        # a backward, steps issued eagerly
+        self.visible_adam = bool(visible_adam)
+        if self.visible_adam:
+            assert not gaussian_shard and not sharded_optimizer, \
+                "visible_adam: one rank or replicated ranks with all-reduced gradients"
+            sharded_optimizer = False
         # N > 1: gradients reduce-scattered, Adam on this rank's rows, rows
         # all-gathered (distributed.ShardedAdam) instead of all-reduce + full Adam
         # (None: when world_size > 1; True also at world_size 1, for tests)
@@ -259,13 +269,14 @@ class Trainer:
         # gradients never go through HBM; GSPLAT_HIP_SH_ADAM_IN_BWD=0 turns it off
         # (Gaussian-sharded too: the SH backward sums its shard's gradient over
         # every rank's camera in the kernel before the update)
-        self.sh_adam_in_bwd = (fused and not self.sharded
+        self.sh_adam_in_bwd = (fused and not self.sharded and not self.visible_adam
                                and (world_size == 1 or self.gshard)
                                and os.environ.get("GSPLAT_HIP_SH_ADAM_IN_BWD", "1") != "0")
         # the exp / sigmoid VJPs and the means-gradient sum formed inside the
         # geometry groups' Adam (gsplat_hip_adam_step_ex): at one rank, and
         # under the sharded optimizer on the reduced shard (ShardedAdam.step)
-        self.geom_fuse = (fused and (world_size == 1 or self.sharded or self.gshard)
+        self.geom_fuse = (fused and not self.visible_adam
+                          and (world_size == 1 or self.sharded or self.gshard)
                           and os.environ.get("GSPLAT_HIP_GEOM_FUSE", "1") != "0")
         # one rank: the geometry groups' whole Adam step inside the
         # projection backward (gsplat_hip_projection_bwd_adam, 2DGS:
@@ -334,10 +345,13 @@ class Trainer:
                                group_pgs=[None, getattr(self, "_sh_pg", None)],
                                emulate_world=getattr(self, "dp_emulate_world", None),
                                **self.adam_kw)
-        if self.fused:  # HIP loss + one-launch Adam (csrc/ssim.hip, csrc/adam.hip)
-            return FusedAdam(params, self.lrs, **self.adam_kw)
         groups = [{"params": [p], "lr": lr, "name": k}
                   for (k, p), lr in zip(self.params.items(), self.lrs)]
+        if getattr(self, "visible_adam", False):
+            from ._wrapper_aux import SelectiveAdam
+            return SelectiveAdam(groups, **self.adam_kw)
+        if self.fused:  # HIP loss + one-launch Adam (csrc/ssim.hip, csrc/adam.hip)
+            return FusedAdam(params, self.lrs, **self.adam_kw)
         return torch.optim.Adam(groups, foreach=True, **self.adam_kw)
 
     def _register_hooks(self):
@@ -606,6 +620,12 @@ class Trainer:
                                  and fusion.geom_adam.applied)
         if self.sharded:
             self.opt.step(defer_gather=True, xform=self._geom_xform(fusion))
+        elif self.visible_adam:  # simple_trainer.py:782-797: (radii > 0).any(0)
+            radii = meta["radii"]
+            vis = radii > 0
+            if vis.dim() > 2:  # per-axis radii [C, N, 2]
+                vis = vis.all(-1)
+            self.opt.step(vis.any(0))
         else:
             self.opt.step(skip=self._sh_skip(fusion), xform=self._geom_xform(fusion))
         self.opt.zero_grad(set_to_none=True)
