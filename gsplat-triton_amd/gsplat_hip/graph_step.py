@@ -102,6 +102,7 @@ def graphable(tr) -> bool:
     # one rank: 3DGS or 2DGS (surfels, rasterization_2dgs with the sync-free isect)
     return (tr.fused and (tr.model == "3dgs" or (one and tr.model == "2dgs"))
             and (gshard_ok or dp_ok or (one and isinstance(tr.opt, FusedAdam)))
+            and not getattr(tr, "packed", False)
             and (st is None or (not getattr(st, "absgrad", False) and tr.radii2d is None))
             and torch.device(tr.device).type == "cuda")
 

@@ -182,7 +182,8 @@ class Trainer:
                  targets: Optional[torch.Tensor] = None, opacity_reg: float = 0.0,
                  scale_reg: float = 0.0, dp_emulate_world: Optional[int] = None,
                  graph: bool = False, isect_capacity: Optional[int] = None,
-                 gaussian_shard: bool = False, visible_adam: bool = False):
+                 gaussian_shard: bool = False, visible_adam: bool = False,
+                 packed: bool = False):
         assert model in ("3dgs", "2dgs"), model
         assert init in ("random", "sfm"), init
         self.model = model
@@ -250,6 +251,13 @@ class Trainer:
         # launch per group (gsplat_hip_selective_adam), no update fused into
         # a backward, steps issued eagerly
         self.visible_adam = bool(visible_adam)
+        # simple_trainer.py:123,501 (cfg.packed): the render's [nnz] pairs
+        # instead of [C, N] (rasterization(packed=True)); the strategy
+        # statistics by index_add over meta["gaussian_ids"] (default.py:240-243);
+        # steps issued eagerly
+        self.packed = bool(packed)
+        assert not (self.packed and (model != "3dgs" or gaussian_shard)), \
+            "packed: the one-camera-per-rank 3DGS trainer"
         if self.visible_adam:
             assert not gaussian_shard and not sharded_optimizer, \
                 "visible_adam: one rank or replicated ranks with all-reduced gradients"
@@ -507,9 +515,9 @@ class Trainer:
                 p["means"], p["quats"], scales, opac,
                 (p["sh0"], p["shN"]) if self.fused else torch.cat([p["sh0"], p["shN"]], 1),
                 self.viewmats[ci:ci + 1], self.Ks[ci:ci + 1], self.width, self.height,
-                sh_degree=deg, packed=False, near_plane=0.01, far_plane=1e10, radius_clip=0.0,
-                rasterize_mode="classic", absgrad=absgrad, _colors_ready=hook, _fusion=fusion,
-                **dkw)
+                sh_degree=deg, packed=getattr(self, "packed", False), near_plane=0.01,
+                far_plane=1e10, radius_clip=0.0, rasterize_mode="classic", absgrad=absgrad,
+                _colors_ready=hook, _fusion=fusion, **dkw)
 
     def _tune_split(self, it: int):
         """Once, before the first step (and so before a graph capture freezes
@@ -940,6 +948,18 @@ class Trainer:
             g = meta.get("means2d_grad") if key == "means2d" else None
             g = meta[key].grad if g is None else g
         if g is None:
+            return
+        if meta.get("gaussian_ids") is not None:  # packed: [nnz] pairs (default.py:240-254)
+            ids = meta["gaussian_ids"]
+            g = g.clone()
+            g[..., 0] *= meta["width"] / 2.0 * meta["n_cameras"]
+            g[..., 1] *= meta["height"] / 2.0 * meta["n_cameras"]
+            self.grad2d.index_add_(0, ids, g.norm(dim=-1))
+            self.count.index_add_(0, ids, torch.ones_like(ids, dtype=torch.float32))
+            if self.radii2d is not None:
+                self.radii2d[ids] = torch.maximum(
+                    self.radii2d[ids],
+                    meta["radii"].float() / float(max(meta["width"], meta["height"])))
             return
         if self.fused:
             update_state_(self.grad2d, self.count, g, meta["radii"], meta["width"],
