@@ -183,7 +183,7 @@ class Trainer:
                  scale_reg: float = 0.0, dp_emulate_world: Optional[int] = None,
                  graph: bool = False, isect_capacity: Optional[int] = None,
                  gaussian_shard: bool = False, visible_adam: bool = False,
-                 packed: bool = False):
+                 packed: bool = False, sparse_grad: bool = False):
         assert model in ("3dgs", "2dgs"), model
         assert init in ("random", "sfm"), init
         self.model = model
@@ -258,7 +258,15 @@ class Trainer:
         self.packed = bool(packed)
         assert not (self.packed and (model != "3dgs" or gaussian_shard)), \
             "packed: the one-camera-per-rank 3DGS trainer"
-        if self.visible_adam:
+        # simple_trainer.py:125,263-264,767-780 (cfg.sparse_grad): the packed
+        # projection's COO gradients (rasterization(sparse_grad=True)), every
+        # other gradient made COO over gaussian_ids, torch.optim.SparseAdam
+        self.sparse_grad = bool(sparse_grad)
+        if self.sparse_grad:
+            assert self.packed, "sparse_grad: packed mode only (simple_trainer.py:769)"
+            assert world_size == 1, "sparse_grad: one rank"
+        if self.visible_adam or self.sparse_grad:
+            assert not (self.visible_adam and self.sparse_grad), "visible_adam or sparse_grad"
             assert not gaussian_shard and not sharded_optimizer, \
                 "visible_adam: one rank or replicated ranks with all-reduced gradients"
             sharded_optimizer = False
@@ -278,12 +286,13 @@ class Trainer:
         # (Gaussian-sharded too: the SH backward sums its shard's gradient over
         # every rank's camera in the kernel before the update)
         self.sh_adam_in_bwd = (fused and not self.sharded and not self.visible_adam
+                               and not self.sparse_grad
                                and (world_size == 1 or self.gshard)
                                and os.environ.get("GSPLAT_HIP_SH_ADAM_IN_BWD", "1") != "0")
         # the exp / sigmoid VJPs and the means-gradient sum formed inside the
         # geometry groups' Adam (gsplat_hip_adam_step_ex): at one rank, and
         # under the sharded optimizer on the reduced shard (ShardedAdam.step)
-        self.geom_fuse = (fused and not self.visible_adam
+        self.geom_fuse = (fused and not self.visible_adam and not self.sparse_grad
                           and (world_size == 1 or self.sharded or self.gshard)
                           and os.environ.get("GSPLAT_HIP_GEOM_FUSE", "1") != "0")
         # one rank: the geometry groups' whole Adam step inside the
@@ -358,6 +367,8 @@ class Trainer:
         if getattr(self, "visible_adam", False):
             from ._wrapper_aux import SelectiveAdam
             return SelectiveAdam(groups, **self.adam_kw)
+        if getattr(self, "sparse_grad", False):
+            return torch.optim.SparseAdam(groups, **self.adam_kw)
         if self.fused:  # HIP loss + one-launch Adam (csrc/ssim.hip, csrc/adam.hip)
             return FusedAdam(params, self.lrs, **self.adam_kw)
         return torch.optim.Adam(groups, foreach=True, **self.adam_kw)
@@ -389,7 +400,7 @@ class Trainer:
         names = list(self.params)
         if self.sharded:
             return {k: list(mv) for k, mv in zip(names, self.opt.full_state())}
-        if self.fused:
+        if isinstance(self.opt, FusedAdam):
             self.sync()
             return {k: [self.opt.exp_avg[i], self.opt.exp_avg_sq[i]]
                     for i, k in enumerate(names)}
@@ -409,7 +420,7 @@ class Trainer:
             step = self.opt.step_count
             self.opt = self._make_optimizer(params)
             self.opt.load_full_state([moments[k] for k in names], step)
-        elif self.fused:
+        elif isinstance(self.opt, FusedAdam):
             self.opt.params = params
             self.opt.exp_avg = [moments[k][0] for k in names]
             self.opt.exp_avg_sq = [moments[k][1] for k in names]
@@ -422,7 +433,8 @@ class Trainer:
                 g["lr"] = lr
             if step is not None:
                 for k, p in self.params.items():
-                    self.opt.state[p] = {"step": step.clone(), "exp_avg": moments[k][0],
+                    self.opt.state[p] = {"step": step.clone() if torch.is_tensor(step) else step,
+                                         "exp_avg": moments[k][0],
                                          "exp_avg_sq": moments[k][1]}
 
     def sync(self):
@@ -490,7 +502,9 @@ class Trainer:
             self.opt.wait([names.index(k) for k in ("means", "scales", "quats", "opacities")])
             sh_idx = [names.index(k) for k in ("sh0", "shN")]
             hook = lambda: self.opt.wait(sh_idx)  # noqa: E731
-        if self.fused:  # one HIP launch each way for both activations
+        if self.fused and not getattr(self, "sparse_grad", False):
+            # one HIP launch each way for both activations (sparse_grad: torch's,
+            # whose backward takes the projection's COO gradients)
             scales, opac = activate(p["scales"], p["opacities"], fusion)
         else:
             scales, opac = torch.exp(p["scales"]), torch.sigmoid(p["opacities"])
@@ -517,7 +531,8 @@ class Trainer:
                 self.viewmats[ci:ci + 1], self.Ks[ci:ci + 1], self.width, self.height,
                 sh_degree=deg, packed=getattr(self, "packed", False), near_plane=0.01,
                 far_plane=1e10, radius_clip=0.0, rasterize_mode="classic", absgrad=absgrad,
-                _colors_ready=hook, _fusion=fusion, **dkw)
+                sparse_grad=getattr(self, "sparse_grad", False), _colors_ready=hook,
+                _fusion=fusion, **dkw)
 
     def _tune_split(self, it: int):
         """Once, before the first step (and so before a graph capture freezes
@@ -628,12 +643,26 @@ class Trainer:
                                  and fusion.geom_adam.applied)
         if self.sharded:
             self.opt.step(defer_gather=True, xform=self._geom_xform(fusion))
-        elif self.visible_adam:  # simple_trainer.py:782-797: (radii > 0).any(0)
-            radii = meta["radii"]
-            vis = radii > 0
-            if vis.dim() > 2:  # per-axis radii [C, N, 2]
-                vis = vis.all(-1)
-            self.opt.step(vis.any(0))
+        elif self.visible_adam:  # simple_trainer.py:782-797
+            if meta.get("gaussian_ids") is not None:  # packed: the Gaussians of the pairs
+                vis = torch.zeros(self.params["opacities"].shape[0], dtype=torch.bool,
+                                  device=self.params["opacities"].device)
+                vis[meta["gaussian_ids"]] = True
+            else:  # (radii > 0).any(0)
+                vis = meta["radii"] > 0
+                if vis.dim() > 2:  # per-axis radii [C, N, 2]
+                    vis = vis.all(-1)
+                vis = vis.any(0)
+            self.opt.step(vis)
+        elif self.sparse_grad:  # simple_trainer.py:767-780, then SparseAdam
+            ids = meta["gaussian_ids"]
+            for k, p in self.params.items():
+                g = p.grad
+                if g is None or g.is_sparse:
+                    continue
+                p.grad = torch.sparse_coo_tensor(indices=ids[None], values=g[ids], size=p.size(),
+                                                 is_coalesced=meta["n_cameras"] == 1)
+            self.opt.step()
         else:
             self.opt.step(skip=self._sh_skip(fusion), xform=self._geom_xform(fusion))
         self.opt.zero_grad(set_to_none=True)

@@ -5,7 +5,9 @@
   gsplat_hip_selective_adam, one launch per parameter group;
 * packed (simple_trainer.py:123,501): the render's [nnz] pairs and the
   strategy statistics by index_add over gaussian_ids (default.py:240-254)
-  train as the dense [C, N] path does."""
+  train as the dense [C, N] path does;
+* sparse_grad (simple_trainer.py:125,263-264,767-780): COO gradients over
+  the pairs' Gaussians and torch.optim.SparseAdam."""
 
 import math
 
@@ -99,3 +101,40 @@ def test_trainer_packed_tracks_dense():
         d = (b[1][k] - x).abs()
         assert float(d.max()) <= 2 * lr * 4 * 1.001, (k, float(d.max()), lr)
         assert float((d > 1e-6).float().mean()) < 0.01, (k, float((d > 1e-6).float().mean()))
+
+
+def test_trainer_sparse_grad():
+    """sparse_grad with packed: every parameter's gradient is COO over the
+    step's gaussian_ids, SparseAdam leaves the other rows and their moments
+    alone, and a refine (DefaultStrategy) carries the SparseAdam state."""
+    from gsplat_hip.densify import DefaultStrategyConfig
+    from gsplat_hip.train_step import Trainer
+    from test_gpu_trainer import _small_scene
+    means, rgbs, vm, K, W, H = _small_scene()
+    # (no strategy for the first step's checks: DefaultStrategy resets every
+    # opacity at step 0, as the reference's, default.py:195)
+    tr = Trainer(means, rgbs, vm, K, W, H, device="cuda", packed=True, sparse_grad=True,
+                 max_steps=100)
+    assert isinstance(tr.opt, torch.optim.SparseAdam) and tr._graph is None
+    with torch.no_grad():
+        _, _, meta = tr.render(tr.camera_index(0), tr.sh_degree_at(0))
+    seen = torch.zeros(means.shape[0], dtype=torch.bool, device="cuda")
+    seen[meta["gaussian_ids"]] = True
+    assert 0 < int(seen.sum()) < seen.numel()
+    p0 = {k: p.detach().clone() for k, p in tr.params.items()}
+    assert math.isfinite(float(tr.step(0)))
+    for k, p in tr.params.items():
+        d = (p.detach() - p0[k]).reshape(p.shape[0], -1)
+        assert torch.equal(d[~seen], torch.zeros_like(d[~seen])), k  # rows no pair touched
+        assert float(d[seen].abs().max()) > 0, k
+        m = tr.opt.state[p]["exp_avg"].reshape(p.shape[0], -1)
+        assert float(m[~seen].abs().max()) == 0.0, k
+    cfg = DefaultStrategyConfig(refine_start_iter=1, refine_every=2, reset_every=100)
+    tr = Trainer(means, rgbs, vm, K, W, H, device="cuda", packed=True, sparse_grad=True,
+                 strategy=cfg, max_steps=100)
+    for it in range(0, 5):  # refines at 2 and 4
+        assert math.isfinite(float(tr.step(it)))
+        n = tr.params["means"].shape[0]
+        for k, (m, v) in tr.moments().items():
+            assert m.shape == tr.params[k].shape and v.shape[0] == n, k
+    assert [r[0] for r in tr.refine_log] == [2, 4], tr.refine_log
