@@ -321,7 +321,8 @@ class GraphStep:
                 colors, _, meta = rasterization(
                     p["means"], p["quats"], scales, opac, (p["sh0"], p["shN"]), self.vm, self.K,
                     tr.width, tr.height, sh_degree=deg, packed=False, near_plane=0.01,
-                    far_plane=1e10, radius_clip=0.0, rasterize_mode="classic", _fusion=fusion,
+                    far_plane=1e10, radius_clip=0.0,
+                    rasterize_mode=getattr(tr, "rasterize_mode", "classic"), _fusion=fusion,
                     _isect_capacity=self.capacity, _isect_status=self.status,
                     _isect_report=(self.ring_out.dev, self.slot), _isect_ids=False, **dkw)
             meta["means2d"].register_hook(lambda g: grad_box.__setitem__("g", g))

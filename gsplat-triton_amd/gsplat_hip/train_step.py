@@ -183,7 +183,7 @@ class Trainer:
                  scale_reg: float = 0.0, dp_emulate_world: Optional[int] = None,
                  graph: bool = False, isect_capacity: Optional[int] = None,
                  gaussian_shard: bool = False, visible_adam: bool = False,
-                 packed: bool = False, sparse_grad: bool = False):
+                 packed: bool = False, sparse_grad: bool = False, antialiased: bool = False):
         assert model in ("3dgs", "2dgs"), model
         assert init in ("random", "sfm"), init
         self.model = model
@@ -262,6 +262,9 @@ class Trainer:
         # projection's COO gradients (rasterization(sparse_grad=True)), every
         # other gradient made COO over gaussian_ids, torch.optim.SparseAdam
         self.sparse_grad = bool(sparse_grad)
+        # simple_trainer.py:129,482 (cfg.antialiased): rasterize_mode
+        # "antialiased", the opacities scaled by the projection's compensation
+        self.rasterize_mode = "antialiased" if antialiased else "classic"
         if self.sparse_grad:
             assert self.packed, "sparse_grad: packed mode only (simple_trainer.py:769)"
             assert world_size == 1, "sparse_grad: one rank"
@@ -530,7 +533,8 @@ class Trainer:
                 (p["sh0"], p["shN"]) if self.fused else torch.cat([p["sh0"], p["shN"]], 1),
                 self.viewmats[ci:ci + 1], self.Ks[ci:ci + 1], self.width, self.height,
                 sh_degree=deg, packed=getattr(self, "packed", False), near_plane=0.01,
-                far_plane=1e10, radius_clip=0.0, rasterize_mode="classic", absgrad=absgrad,
+                far_plane=1e10, radius_clip=0.0, rasterize_mode=self.rasterize_mode,
+                absgrad=absgrad,
                 sparse_grad=getattr(self, "sparse_grad", False), _colors_ready=hook,
                 _fusion=fusion, **dkw)
 

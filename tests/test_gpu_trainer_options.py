@@ -7,7 +7,9 @@
   strategy statistics by index_add over gaussian_ids (default.py:240-254)
   train as the dense [C, N] path does;
 * sparse_grad (simple_trainer.py:125,263-264,767-780): COO gradients over
-  the pairs' Gaussians and torch.optim.SparseAdam."""
+  the pairs' Gaussians and torch.optim.SparseAdam;
+* antialiased (simple_trainer.py:129,482): rasterize_mode "antialiased",
+  eager and graph-replayed."""
 
 import math
 
@@ -138,3 +140,41 @@ def test_trainer_sparse_grad():
         for k, (m, v) in tr.moments().items():
             assert m.shape == tr.params[k].shape and v.shape[0] == n, k
     assert [r[0] for r in tr.refine_log] == [2, 4], tr.refine_log
+
+
+def test_trainer_antialiased_graph_tracks_eager():
+    """rasterize_mode "antialiased" (the projection's compensations scale
+    the opacities): the trainer's render equals rasterization() called with
+    that mode, and four replayed steps track four eager ones (the geometry
+    Adam stays out of the projection backward, which fuses only classic)."""
+    from gsplat_hip import rasterization
+    from gsplat_hip.train_step import Trainer
+    from test_gpu_trainer import _small_scene
+    means, rgbs, vm, K, W, H = _small_scene()
+    tr = Trainer(means, rgbs, vm, K, W, H, device="cuda", antialiased=True)
+    with torch.no_grad():
+        c, _, meta = tr.render(0, 3)
+        p = tr.params
+        ref, _, _ = rasterization(p["means"], p["quats"], torch.exp(p["scales"]),
+                                  torch.sigmoid(p["opacities"]),
+                                  torch.cat([p["sh0"], p["shN"]], 1), tr.viewmats[:1],
+                                  tr.Ks[:1], W, H, sh_degree=3, packed=False,
+                                  rasterize_mode="antialiased")
+    assert meta["opacities"].shape == (1, means.shape[0])
+    torch.testing.assert_close(c, ref, rtol=1e-4, atol=1e-5)
+    out = {}
+    for run in ("eager", "eager2", "graph"):
+        tr = Trainer(means, rgbs, vm, K, W, H, device="cuda", antialiased=True,
+                     graph=run == "graph", max_steps=100)
+        assert (tr._graph is not None) == (run == "graph")
+        losses = [tr.step(it) for it in range(4)]
+        tr.sync()
+        assert tr.graph_fallback is None, tr.graph_fallback
+        out[run] = ({k: q.detach().clone() for k, q in tr.params.items()},
+                    [float(x) for x in losses])
+    a, a2, b = out["eager"], out["eager2"], out["graph"]
+    for k in a[0]:
+        spread = float((a2[0][k] - a[0][k]).abs().max())
+        err = float((b[0][k] - a[0][k]).abs().max())
+        assert err <= max(4.0 * spread, 1e-5 * float(a[0][k].abs().max()) + 1e-6), (k, err, spread)
+    torch.testing.assert_close(torch.tensor(b[1]), torch.tensor(a[1]), rtol=1e-4, atol=1e-6)
