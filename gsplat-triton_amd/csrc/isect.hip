@@ -683,12 +683,19 @@ static int isect_write_sorted_impl(
     int32_t *segcnt = reinterpret_cast<int32_t *>(ws + L.segcnt);
     int32_t *tile_tot = reinterpret_cast<int32_t *>(ws + L.tile_tot);
     int32_t *offs = offsets ? offsets : reinterpret_cast<int32_t *>(ws + L.offs);
+    // the captured 2DGS step (sc): huge surfels' pairs spread over the grid
+    static_assert(sizeof(st::HugeEmit) <= sizeof(BigEmit), "the huge list fits L.big");
+    st::HugeEmit *huge_list = sc ? reinterpret_cast<st::HugeEmit *>(ws + L.big) : nullptr;
+    int32_t *n_huge = sc ? reinterpret_cast<int32_t *>(ws + L.nbig) : nullptr;
     hipLaunchKernelGGL(st::rect_kernel, dim3((unsigned)nbV), dim3(256), 0, st, n_visible, cnt_dev,
-                       Vs, dks, means2d, radii, tile_size, geo, rect, blk, vis_rank);
+                       Vs, dks, means2d, radii, tile_size, geo, rect, blk, vis_rank, n_huge);
     hipLaunchKernelGGL(isect_scan_blocks_kernel, dim3(1), dim3(1024), 0, st, nbV, blk, nullptr,
                        nullptr);
     hipLaunchKernelGGL(st::emit_kernel, dim3((unsigned)nbV), dim3(256), 0, st, n_visible, cnt_dev,
-                       Vs, dks, rect, camera_ids, geo, blk, tkey, val);
+                       Vs, dks, rect, camera_ids, geo, blk, tkey, val, huge_list, n_huge);
+    if (sc)
+      hipLaunchKernelGGL(st::huge_emit_kernel, dim3(st::kHugeBlocks), dim3(256), 0, st, huge_list,
+                         n_huge, geo, tkey, val);
     if (sc)  // large surfels' pairs: the tiles of the supertile they can reach
       hipLaunchKernelGGL(st::tight_kernel,
                          dim3((unsigned)std::min<int64_t>((n_isects + 255) / 256, 2048)),

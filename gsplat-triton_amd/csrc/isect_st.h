@@ -127,7 +127,8 @@ __global__ void __launch_bounds__(256)
 rect_kernel(int64_t nV, const int64_t *__restrict__ cap, const int32_t *__restrict__ Vs,
             const uint32_t *__restrict__ dkeys, const float *__restrict__ means2d,
             const int32_t *__restrict__ radii, int ts, Geo geo, ushort4 *__restrict__ rect,
-            int64_t *__restrict__ blk, int32_t *__restrict__ vis_rank) {
+            int64_t *__restrict__ blk, int32_t *__restrict__ vis_rank,
+            int32_t *__restrict__ n_huge) {
   __shared__ int64_t lds[5];
   // the ranks are written even when the call is void (an overflow): the
   // rasterizer's record packing and gradient rows read them for every
@@ -135,6 +136,7 @@ rect_kernel(int64_t nV, const int64_t *__restrict__ cap, const int32_t *__restri
   if (cap) nV = min(nV, cap[1]);
   const bool vd = void_call(cap);
   const int64_t s = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (n_huge && s == 0) *n_huge = 0;  // the huge list of emit_kernel (this launch precedes it)
   int np = 0;
   if (s < nV && vis_rank) vis_rank[Vs[s]] = (int32_t)s;
   if (s < nV && !vd) {
@@ -157,12 +159,24 @@ rect_kernel(int64_t nV, const int64_t *__restrict__ cap, const int32_t *__restri
 
 // (2) (supertile key, s) pairs in depth order
 constexpr int kLanePairs = 16;
+// Huge (n_huge non-null: the captured 2DGS step, whose near-degenerate
+// surfels span the whole image -- ~2,000 with ~510 pairs each at M5, all
+// adjacent in depth order, so a few dozen waves each looped over 64 of them
+// in turn while the rest of the grid idled): more than kHugePairs pairs go
+// to a list that huge_emit_kernel spreads over the grid.
+constexpr int kHugePairs = 128;
+struct HugeEmit {
+  int64_t cur;  // first output slot
+  int32_t s, n, x0, y0, w;
+  uint32_t kb;
+};
 
 __global__ void __launch_bounds__(256)
 emit_kernel(int64_t nV, const int64_t *__restrict__ cap, const int32_t *__restrict__ Vs,
             const uint32_t *__restrict__ dkeys, const ushort4 *__restrict__ rect,
             const int32_t *__restrict__ camera_ids, Geo geo, const int64_t *__restrict__ blk_prefix,
-            uint32_t *__restrict__ pkey, int32_t *__restrict__ pval) {
+            uint32_t *__restrict__ pkey, int32_t *__restrict__ pval,
+            HugeEmit *__restrict__ huge_list, int32_t *__restrict__ n_huge) {
   __shared__ int64_t lds[5];
   if (cap) nV = void_call(cap) ? 0 : min(nV, cap[1]);
   const int64_t s = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -189,8 +203,19 @@ emit_kernel(int64_t nV, const int64_t *__restrict__ cap, const int32_t *__restri
       pval[cur0 + k] = (int32_t)s;
     }
   }
+  // huge (the list given): one slot per lane in the list, one atomic per wave
+  const int huge_at = n_huge ? kHugePairs : 0x7fffffff;
+  const uint64_t huge = __ballot(np > huge_at);
+  if (huge) {
+    int base = 0;
+    if (lane == 0) base = atomicAdd(n_huge, __popcll(huge));
+    base = __shfl(base, 0, 64);
+    if (np > huge_at)
+      huge_list[base + __popcll(huge & ((1ull << lane) - 1ull))] =
+          HugeEmit{cur0, (int32_t)s, np, sx0, sy0, w, kbase};
+  }
   // large Gaussians: the whole wave writes each one's pairs (coalesced)
-  uint64_t big = __ballot(np > kLanePairs);
+  uint64_t big = __ballot(np > kLanePairs && np <= huge_at);
   while (big) {
     const int src = __builtin_ctzll(big);
     big &= big - 1;
@@ -203,6 +228,28 @@ emit_kernel(int64_t nV, const int64_t *__restrict__ cap, const int32_t *__restri
       const int yy = k / bw, xx = k - yy * bw;
       pkey[c0 + k] = kb + (uint32_t)((by + yy) * geo.stw + bx + xx);
       pval[c0 + k] = bs;
+    }
+  }
+}
+
+// (2a) the huge list: kHugeParts workgroups per entry, each writing a
+// contiguous part of its pairs (coalesced); a grid-stride over the entries
+constexpr int kHugeParts = 4;
+constexpr int kHugeBlocks = 1024;
+
+__global__ void __launch_bounds__(256)
+huge_emit_kernel(const HugeEmit *__restrict__ huge_list, const int32_t *__restrict__ n_huge,
+                 Geo geo, uint32_t *__restrict__ pkey, int32_t *__restrict__ pval) {
+  const int nh = *n_huge;
+  const int part = blockIdx.x % kHugeParts;
+  for (int e = blockIdx.x / kHugeParts; e < nh; e += kHugeBlocks / kHugeParts) {
+    const HugeEmit g = huge_list[e];
+    const int k0 = (int)(((int64_t)g.n * part) / kHugeParts);
+    const int k1 = (int)(((int64_t)g.n * (part + 1)) / kHugeParts);
+    for (int k = k0 + (int)threadIdx.x; k < k1; k += 256) {
+      const int yy = k / g.w, xx = k - yy * g.w;
+      pkey[g.cur + k] = g.kb + (uint32_t)((g.y0 + yy) * geo.stw + g.x0 + xx);
+      pval[g.cur + k] = g.s;
     }
   }
 }
